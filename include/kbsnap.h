@@ -1,0 +1,225 @@
+/*
+ * kbsnap.h — the KBS1 cluster-snapshot file format (format definition + a
+ * header-only reader).
+ *
+ * A KBS1 file is what the host hands to the placement engine at session open:
+ * the same objects kube-batch's SchedulerCache.Snapshot() clones into a
+ * ClusterInfo (reference pkg/scheduler/cache/cache.go:515-583) — nodes, queues,
+ * pod groups (jobs) and pods — plus the scheduler tier configuration
+ * (pkg/scheduler/conf/scheduler_conf.go:20-54).  Every resource quantity is
+ * already converted the way the reference converts it
+ * (Quantity.MilliValue()/Value(), vendor/k8s.io/apimachinery/pkg/api/resource/
+ * quantity.go:684-703): cpu and nvidia.com/gpu in milli-units, memory in bytes.
+ *
+ * The format is columnar: a directory of named, typed, flat arrays.  Strings
+ * are int32 offsets into the "strtab" section (NUL-terminated); -1 means the
+ * field is absent/empty.  Variable-length children use CSR offset columns
+ * ("*_off", count+1 entries).  The file is laid out so that numpy can write
+ * every column directly and C/C++ can read it in place.
+ *
+ * Canonical order: the writer emits nodes sorted by
+ * name, jobs by UID ("ns/name"), pods by UID and queues by name; every map
+ * iteration of the reference is pinned to ascending index in these arrays.
+ *
+ * This header is format plumbing only; it contains no scheduling logic.  It is
+ * used by the product library (kube-batch-1_amd/csrc) and by the test oracle.
+ */
+#ifndef KBSNAP_H_
+#define KBSNAP_H_
+
+#include <stdint.h>
+#include <string.h>
+
+#define KBS_MAGIC "KBS1"
+#define KBS_VERSION 1u
+
+enum kbs_dtype { KBS_I8 = 1, KBS_U8 = 2, KBS_I32 = 3, KBS_I64 = 4, KBS_F64 = 5, KBS_BYTES = 6 };
+
+/* pod phase (v1.PodPhase) */
+enum kbs_phase { KBS_PENDING = 0, KBS_RUNNING = 1, KBS_SUCCEEDED = 2, KBS_FAILED = 3, KBS_UNKNOWN = 4 };
+
+/* container "has" bits: which keys are present in Resources.Requests.  The
+ * distinction between an absent key and an explicit 0 matters for
+ * GetNonzeroRequests (vendor/.../priorities/util/non_zero.go:37-52). */
+enum { KBS_HAS_CPU = 1, KBS_HAS_MEM = 2, KBS_HAS_GPU = 4 };
+
+/* node-selector operators (v1.NodeSelectorOperator), label-selector
+ * operators (metav1.LabelSelectorOperator) share one numbering. */
+enum kbs_op { KBS_OP_IN = 0, KBS_OP_NOTIN = 1, KBS_OP_EXISTS = 2, KBS_OP_DOESNOTEXIST = 3,
+              KBS_OP_GT = 4, KBS_OP_LT = 5, KBS_OP_INVALID = 15 };
+
+/* affinity presence flags: nil vs empty matters in the reference
+ * (predicates.go:826-833 required-NA nil check; interpod_affinity.go:121-122). */
+enum { KBS_AFF_NA = 1, KBS_AFF_NA_REQ = 2, KBS_AFF_PA = 4, KBS_AFF_PAA = 8 };
+
+/* conf plugin option flags (conf.PluginOption *Disabled fields) */
+enum { KBS_DIS_JOBORDER = 1, KBS_DIS_JOBREADY = 2, KBS_DIS_TASKORDER = 4, KBS_DIS_PREEMPTABLE = 8,
+       KBS_DIS_RECLAIMABLE = 16, KBS_DIS_QUEUEORDER = 32, KBS_DIS_PREDICATE = 64,
+       KBS_DIS_NODEORDER = 128 };
+
+#pragma pack(push, 1)
+typedef struct kbs_header {
+    char magic[4];
+    uint32_t version;
+    uint32_t n_sections;
+    uint32_t reserved;
+} kbs_header;
+
+typedef struct kbs_dirent {
+    char name[24];
+    uint32_t dtype;
+    uint32_t elem_size;
+    uint64_t count;
+    uint64_t offset;
+} kbs_dirent;
+#pragma pack(pop)
+
+/*
+ * Section names (all optional unless noted; missing = zero rows).
+ *
+ * strtab                      bytes   NUL-terminated strings
+ * conf_actions                i32[1]  str: e.g. "allocate, backfill"
+ * conf_plugin_name/tier/flags i32[P]
+ * conf_arg_plugin/key/val     i32[A]  plugin index, str, str
+ * q_name, q_weight, q_ts      i32,i32,i64 [Q]
+ * n_name                      i32[N]
+ * n_alloc_cpu/mem/gpu/pods    i64[N]  Status.Allocatable
+ * n_cap_cpu/mem/gpu/pods      i64[N]  Status.Capacity
+ * n_unsched                   u8[N]   Spec.Unschedulable
+ * n_label_off (N+1) nl_key nl_val           node labels
+ * n_taint_off (N+1) nt_key nt_val nt_effect node taints
+ * j_ns j_name j_queue         i32[J]  PodGroup namespace/name/Spec.Queue
+ * j_min j_pg_priority         i32[J]  Spec.MinMember, PriorityClass value
+ * j_ts                        i64[J]  CreationTimestamp (ns)
+ * p_uid p_name p_ns           i32[P]
+ * p_job                       i32[P]  job index (-1 = no pod group)
+ * p_node                      i32[P]  str Spec.NodeName (-1 = "")
+ * p_phase p_deleting p_backfill u8[P]
+ * p_priority                  i32[P]  *Spec.Priority
+ * p_ts                        i64[P]  CreationTimestamp (ns)
+ * p_label_off (P+1) pl_key pl_val
+ * p_nsel_off  (P+1) ps_key ps_val   Spec.NodeSelector
+ * p_ctr_off   (P+1) c_cpu c_mem c_gpu (i64) c_has (u8) c_port_off (C+1)
+ *                   pt_ip pt_proto (str) pt_port (i32)
+ * p_ictr_off  (P+1) ic_cpu ic_mem ic_gpu (i64) ic_has (u8)  InitContainers
+ * p_tol_off   (P+1) tl_key tl_op tl_val tl_effect (str)
+ * p_aff                       i32[P]  affinity row (-1 = nil Affinity)
+ * a_flags                     u8[A]   KBS_AFF_* presence bits
+ * a_<list>_start, a_<list>_cnt i32[A] contiguous row runs, <list> in
+ *     nareq  -> nst rows  (NodeAffinity.Required.NodeSelectorTerms)
+ *     napref -> pst rows  (NodeAffinity.Preferred)
+ *     pareq  -> pat rows  (PodAffinity.Required)     papref  -> wpat rows
+ *     paareq -> pat rows  (PodAntiAffinity.Required) paapref -> wpat rows
+ * nst_expr_start/cnt, nst_field_start/cnt  i32 -> nsr rows
+ * nsr_key (str) nsr_op (u8) nsr_val_off (+1) -> nsrv (str)
+ * pst_weight pst_term         i32 (term -> nst row)
+ * pat_sel (i32 lsel row, -1 nil) pat_topo (str) pat_ns_off (+1) -> patns (str)
+ * wpat_weight wpat_term       i32 (term -> pat row)
+ * ls_ml_off (+1) -> lkv_key lkv_val (str) ; ls_me_off (+1) -> lsr rows
+ * lsr_key (str) lsr_op (u8) lsr_val_off (+1) -> lsrv (str)
+ */
+
+#ifdef __cplusplus
+#include <string>
+#include <vector>
+#include <stdexcept>
+#include <cstdio>
+
+namespace kbs {
+
+/* A read-only view of a KBS1 file held in memory (owned buffer). */
+class Snapshot {
+  public:
+    Snapshot() {}
+    explicit Snapshot(const std::string& path) { load_file(path); }
+
+    void load_file(const std::string& path) {
+        FILE* f = std::fopen(path.c_str(), "rb");
+        if (!f) throw std::runtime_error("kbsnap: cannot open " + path);
+        std::fseek(f, 0, SEEK_END);
+        long sz = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        buf_.resize((size_t)sz);
+        size_t got = sz > 0 ? std::fread(buf_.data(), 1, (size_t)sz, f) : 0;
+        std::fclose(f);
+        if (got != (size_t)sz) throw std::runtime_error("kbsnap: short read " + path);
+        parse();
+    }
+
+    void load_bytes(const void* p, size_t n) {
+        buf_.assign((const char*)p, (const char*)p + n);
+        parse();
+    }
+
+    /* Typed column access.  Returns nullptr and n=0 for a missing section. */
+    template <typename T>
+    const T* col(const char* name, size_t* n) const {
+        const kbs_dirent* d = find(name);
+        if (!d) { *n = 0; return nullptr; }
+        if (d->elem_size != sizeof(T))
+            throw std::runtime_error(std::string("kbsnap: element size mismatch for ") + name);
+        *n = (size_t)d->count;
+        return reinterpret_cast<const T*>(buf_.data() + d->offset);
+    }
+    template <typename T>
+    std::vector<T> vec(const char* name) const {
+        size_t n = 0;
+        const T* p = col<T>(name, &n);
+        return p ? std::vector<T>(p, p + n) : std::vector<T>();
+    }
+    /* CSR offsets column; synthesises [0]*(rows+1) when absent. */
+    std::vector<int32_t> offs(const char* name, size_t rows) const {
+        std::vector<int32_t> v = vec<int32_t>(name);
+        if (v.empty()) v.assign(rows + 1, 0);
+        if (v.size() != rows + 1)
+            throw std::runtime_error(std::string("kbsnap: bad offsets length for ") + name);
+        return v;
+    }
+    const char* str(int32_t off) const {
+        if (off < 0) return "";
+        if ((size_t)off >= strtab_n_) throw std::runtime_error("kbsnap: string offset out of range");
+        return strtab_ + off;
+    }
+    std::string s(int32_t off) const { return std::string(str(off)); }
+    bool has(const char* name) const { return find(name) != nullptr; }
+    size_t rows(const char* name) const {
+        const kbs_dirent* d = find(name);
+        return d ? (size_t)d->count : 0;
+    }
+
+  private:
+    const kbs_dirent* find(const char* name) const {
+        for (uint32_t i = 0; i < ndir_; ++i)
+            if (std::strncmp(dir_[i].name, name, sizeof(dir_[i].name)) == 0) return &dir_[i];
+        return nullptr;
+    }
+    void parse() {
+        if (buf_.size() < sizeof(kbs_header)) throw std::runtime_error("kbsnap: file too small");
+        const kbs_header* h = reinterpret_cast<const kbs_header*>(buf_.data());
+        if (std::memcmp(h->magic, KBS_MAGIC, 4) != 0) throw std::runtime_error("kbsnap: bad magic");
+        if (h->version != KBS_VERSION) throw std::runtime_error("kbsnap: unsupported version");
+        ndir_ = h->n_sections;
+        if (sizeof(kbs_header) + (size_t)ndir_ * sizeof(kbs_dirent) > buf_.size())
+            throw std::runtime_error("kbsnap: truncated directory");
+        dir_ = reinterpret_cast<const kbs_dirent*>(buf_.data() + sizeof(kbs_header));
+        for (uint32_t i = 0; i < ndir_; ++i) {
+            if (dir_[i].offset + dir_[i].count * dir_[i].elem_size > buf_.size())
+                throw std::runtime_error("kbsnap: section out of range");
+        }
+        size_t n = 0;
+        strtab_ = col<char>("strtab", &n);
+        strtab_n_ = n;
+        if (strtab_n_ && strtab_[strtab_n_ - 1] != '\0') throw std::runtime_error("kbsnap: strtab not terminated");
+    }
+
+    std::vector<char> buf_;
+    const kbs_dirent* dir_ = nullptr;
+    uint32_t ndir_ = 0;
+    const char* strtab_ = nullptr;
+    size_t strtab_n_ = 0;
+};
+
+}  // namespace kbs
+#endif /* __cplusplus */
+
+#endif /* KBSNAP_H_ */

@@ -1,0 +1,1294 @@
+/*
+ * kbfast.cpp — TEST ORACLE / CPU BASELINE (hoisted restatement).  Test
+ * infrastructure only: loaded by tests/ and by bench.py's cpu_baseline leg;
+ * the product (kube-batch-1_amd/) never links or calls it.
+ *
+ * Same semantics as kbref.cpp (the faithful restatement of
+ * pkg/scheduler/actions/allocate/allocate.go:41-201 and everything it calls),
+ * restructured the way a competent CPU implementation would be: all resource
+ * quantities as exact int64, per-node aggregates kept
+ * incrementally instead of rebuilding the k8s NodeInfo per (task, node) pair,
+ * label/taint/port dictionaries, per-task precompute of selector, toleration
+ * and inter-pod-affinity tables, then one O(N) predicate+score+select sweep per
+ * task partitioned over T host threads (the reference's only parallelism is
+ * workqueue.ParallelizeUntil(ctx, 16, ...), interpod_affinity.go:214).
+ *
+ * Placements are identical to kbref (tests/test_oracle.py checks it on random
+ * snapshots that exercise every predicate and priority).
+ */
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../include/kbsnap.h"
+
+namespace fast {
+
+using std::string;
+using std::vector;
+
+static const int64_t kMinCPU = 10, kMinGPU = 10, kMinMem = 10LL * 1024 * 1024;  // resource_info.go:54-56
+
+struct Res {
+    int64_t cpu = 0, mem = 0, gpu = 0;
+    Res& operator+=(const Res& o) { cpu += o.cpu; mem += o.mem; gpu += o.gpu; return *this; }
+    Res& operator-=(const Res& o) { cpu -= o.cpu; mem -= o.mem; gpu -= o.gpu; return *this; }
+};
+// Resource.LessEqual on exact integers: r - rr < min per dimension (resource_info.go:164-168)
+static inline bool le(const Res& r, const Res& rr) {
+    return r.cpu - rr.cpu < kMinCPU && r.mem - rr.mem < kMinMem && r.gpu - rr.gpu < kMinGPU;
+}
+static inline bool le_sum(const Res& r, const Res& a, const Res& b) {
+    return r.cpu - (a.cpu + b.cpu) < kMinCPU && r.mem - (a.mem + b.mem) < kMinMem && r.gpu - (a.gpu + b.gpu) < kMinGPU;
+}
+static inline bool isEmpty(const Res& r) { return r.cpu < kMinCPU && r.mem < kMinMem && r.gpu < kMinGPU; }
+
+// float64 Resource for the ordering plugins (drf / proportion shares)
+struct FRes {
+    double c = 0, m = 0, g = 0;
+    void add(const FRes& o) { c += o.c; m += o.m; g += o.g; }
+    void sub(const FRes& o) { c -= o.c; m -= o.m; g -= o.g; }
+    double get(int k) const { return k == 0 ? c : k == 1 ? m : g; }
+    bool lessEqual(const FRes& rr) const {
+        return (c < rr.c || std::fabs(rr.c - c) < (double)kMinCPU) &&
+               (m < rr.m || std::fabs(rr.m - m) < (double)kMinMem) &&
+               (g < rr.g || std::fabs(rr.g - g) < (double)kMinGPU);
+    }
+    bool isEmpty() const { return c < (double)kMinCPU && m < (double)kMinMem && g < (double)kMinGPU; }
+};
+static FRes toF(const Res& r) { return FRes{(double)r.cpu, (double)r.mem, (double)r.gpu}; }
+static double share(double l, double r) { return r == 0 ? (l == 0 ? 0 : 1) : l / r; }
+
+enum St { Pending = 1, AOB = 2, Allocated = 4, Pipelined = 8, Binding = 16, Bound = 32, Running = 64,
+          Releasing = 128, Succeeded = 256, Failed = 512, Unknown = 1024 };
+static inline bool allocSt(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
+
+/* --------------------------- dictionaries ------------------------------- */
+struct Dict {
+    std::unordered_map<string, int> ids;
+    vector<string> strs;
+    int get(const string& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        int id = (int)strs.size();
+        ids.emplace(s, id);
+        strs.push_back(s);
+        return id;
+    }
+    int find(const string& s) const {
+        auto it = ids.find(s);
+        return it == ids.end() ? -1 : it->second;
+    }
+};
+
+static bool parseI64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+    if (s.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; if (s.size() == 1) return false; }
+    unsigned long long v = 0, lim = neg ? 9223372036854775808ULL : 9223372036854775807ULL;
+    for (; i < s.size(); ++i) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        unsigned d = (unsigned)(s[i] - '0');
+        if (v > (lim - d) / 10) return false;
+        v = v * 10 + d;
+    }
+    *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+    return true;
+}
+
+/* A label set as a sorted (key id -> value id) vector. */
+typedef vector<std::pair<int, int>> LSet;
+static inline int lget(const LSet& l, int key) {
+    auto it = std::lower_bound(l.begin(), l.end(), std::make_pair(key, INT32_MIN));
+    return (it != l.end() && it->first == key) ? it->second : -1;
+}
+
+enum { OIn = 0, ONotIn = 1, OExists = 2, ODNE = 3, OGt = 4, OLt = 5, OEq = 6 };
+struct Req {  // compiled labels.Requirement
+    int key;
+    int op;
+    vector<int> vals;  // value ids (-1 for values never seen: they match nothing)
+    int64_t rhs = 0;   // Gt/Lt
+};
+struct Sel {  // compiled selector: nothing / AND of reqs
+    bool nothing = false;
+    vector<Req> reqs;
+};
+
+struct World;
+static bool reqMatch(const World& w, const Req& r, const LSet& ls);
+
+/* --------------------------- model -------------------------------------- */
+struct PATerm {  // compiled PodAffinityTerm
+    Sel sel;
+    bool selErr = false;
+    vector<int> ns;  // namespace ids (empty => definer's namespace)
+    int key = -1;    // topology key id (-1 == "")
+};
+struct WTerm {
+    int32_t w;
+    PATerm t;
+};
+struct NSTerm {
+    vector<Req> expr;
+    bool exprErr = false;
+    vector<std::pair<int, string>> fields;  // (op, value) on metadata.name; key checked at compile
+    vector<string> fieldKeys;
+    bool fieldErr = false;
+};
+struct Aff {
+    bool na = false, naReq = false, pa = false, paa = false;
+    vector<NSTerm> naReqTerms;
+    vector<std::pair<int32_t, NSTerm>> naPref;
+    vector<PATerm> paReq, paaReq;
+    vector<WTerm> paPref, paaPref;
+};
+struct Port {
+    int ip, proto;  // sanitised ids
+    int32_t port;
+};
+struct PodRec {
+    string uid, name;
+    int ns = -1;
+    LSet labels;
+    int nodeRaw = -1;  // node index of raw Spec.NodeName (-1 "")
+    int status = Pending;
+    int32_t priority = 0;
+    int64_t ts = 0;
+    bool backfill = false;
+    Res req, initReq;
+    int64_t nzc = 0, nzm = 0;
+    vector<Port> ports;
+    vector<std::pair<int, int>> nsel;  // (key, value) required
+    vector<int> tolTaints;             // tolerated taint ids (computed later)
+    std::shared_ptr<Aff> aff;
+    int job = -1;  // session job slot
+    string jobUID;
+    int curNode = -1;  // task.NodeName (node index)
+    bool hasPodAff() const { return aff && (aff->pa || aff->paa); }
+};
+struct NodeRec {
+    string name;
+    LSet labels;
+    vector<int> taints;  // NoSchedule/NoExecute taint ids
+    bool unsched = false;
+    int maxTasks = 0;
+    Res alloc, idle, used, rel, bf;
+    int64_t acpu = 0, amem = 0;  // k8s allocatable
+    int64_t nzc = 0, nzm = 0;    // k8s nonzeroRequest over node.Pods()
+    int pods = 0;
+    vector<Port> used_ports;  // sanitised (ip, proto, port>0)
+    vector<int> podList;      // pods on node (all statuses), pinned order by insertion
+    bool hasEmptyNamePod = false;  // some pod on it has raw Spec.NodeName == ""
+};
+struct JobRec {
+    string uid;
+    int queue = -1;
+    int32_t minAvail = 0, priority = 0;
+    int64_t ts = 0;
+    vector<int> tasks;  // pod indices, pinned order
+    int cntAlloc = 0, cntAOB = 0;  // AllocatedStatuses count, AllocatedOverBackfill count
+    FRes drfAlloc;
+    double drfShare = 0;
+};
+struct QueueRec {
+    string name;
+    int32_t weight = 1;
+    int64_t ts = 0;
+    bool hasAttr = false;
+    FRes deserved, allocated, request;
+    double share = 0;
+};
+struct Plugin {
+    string name;
+    int flags = 0;
+    std::map<string, string> args;
+};
+
+struct World {
+    Dict keys, vals, nss, ips, protos;
+    vector<std::map<int, int64_t>> intVal;  // not used
+    vector<NodeRec> nodes;
+    vector<PodRec> pods;
+    vector<JobRec> jobs;
+    vector<QueueRec> queues;
+    vector<vector<Plugin>> tiers;
+    vector<std::tuple<int, int, string>> taintDefs;  // (key id, value, effect)
+    // value id -> parsed int64 (for Gt/Lt)
+    vector<int64_t> valInt;
+    vector<char> valIntOk;
+    // plugin presence
+    bool predOn = false, nodeorderOn = false, drfOn = false, propOn = false, gangOn = false, prioOn = false;
+    int wLR = 1, wBRA = 1, wNA = 1, wPA = 1, noMult = 0;
+    FRes total;
+    // pod-affinity bookkeeping
+    vector<int> affPods;  // pods (anywhere on nodes) with PodAffinity/PodAntiAffinity
+    bool anyBackfilled = false;
+    int fallbackNode = -1;  // lowest node index holding a pod with empty raw NodeName
+    vector<std::tuple<int, int, int>> log;
+};
+
+static bool reqMatch(const World& w, const Req& r, const LSet& ls) {  // selector.go:192-236
+    int v = lget(ls, r.key);
+    switch (r.op) {
+        case OIn:
+        case OEq:
+            if (v < 0) return false;
+            for (int x : r.vals) if (x == v) return true;
+            return false;
+        case ONotIn:
+            if (v < 0) return true;
+            for (int x : r.vals) if (x == v) return false;
+            return true;
+        case OExists: return v >= 0;
+        case ODNE: return v < 0;
+        case OGt:
+        case OLt: {
+            if (v < 0 || !w.valIntOk[v]) return false;
+            int64_t lv = w.valInt[v];
+            return r.op == OGt ? lv > r.rhs : lv < r.rhs;
+        }
+    }
+    return false;
+}
+static bool selMatch(const World& w, const Sel& s, const LSet& ls) {
+    if (s.nothing) return false;
+    for (auto& r : s.reqs) if (!reqMatch(w, r, ls)) return false;
+    return true;
+}
+
+/* ---------------------------- loading ----------------------------------- */
+static void ensureValInt(World& w) {
+    size_t n = w.vals.strs.size();
+    size_t o = w.valInt.size();
+    w.valInt.resize(n);
+    w.valIntOk.resize(n);
+    for (size_t i = o; i < n; ++i) w.valIntOk[i] = parseI64(w.vals.strs[i], &w.valInt[i]);
+}
+
+// compile a requirement; returns false when labels.NewRequirement would error
+static bool compileReq(World& w, const string& key, int op, const vector<string>& values, Req* out) {
+    out->key = w.keys.get(key);
+    out->op = op;
+    out->vals.clear();
+    switch (op) {
+        case OIn:
+        case ONotIn: if (values.empty()) return false; break;
+        case OEq: if (values.size() != 1) return false; break;
+        case OExists:
+        case ODNE: if (!values.empty()) return false; break;
+        case OGt:
+        case OLt:
+            if (values.size() != 1 || !parseI64(values[0], &out->rhs)) return false;
+            break;
+        default: return false;
+    }
+    for (auto& v : values) out->vals.push_back(w.vals.get(v));
+    return true;
+}
+
+struct Loader {
+    const kbs::Snapshot& s;
+    World& w;
+    vector<int32_t> nsr_key, lsr_key, nsr_voff, lsr_voff, nsrv, lsrv, ls_ml, ls_me, lkv_k, lkv_v, pat_sel, pat_topo,
+        pat_ns, patns, es, ec, fs, fc;
+    vector<uint8_t> nsr_op, lsr_op;
+    Loader(const kbs::Snapshot& s_, World& w_) : s(s_), w(w_) {}
+
+    vector<string> strs(const vector<int32_t>& off, const vector<int32_t>& tab, int row) {
+        vector<string> v;
+        for (int k = off[row]; k < off[row + 1]; ++k) v.push_back(s.s(tab[k]));
+        return v;
+    }
+    bool nsReq(int row, Req* r) { return compileReq(w, s.s(nsr_key[row]), nsr_op[row], strs(nsr_voff, nsrv, row), r); }
+    NSTerm nst(int row) {
+        NSTerm t;
+        for (int k = es[row]; k < es[row] + ec[row]; ++k) {
+            Req r;
+            if (!nsReq(k, &r)) t.exprErr = true;
+            t.expr.push_back(r);
+        }
+        for (int k = fs[row]; k < fs[row] + fc[row]; ++k) {
+            vector<string> vs = strs(nsr_voff, nsrv, k);
+            int op = nsr_op[k];
+            if ((op != OIn && op != ONotIn) || vs.size() != 1) t.fieldErr = true;
+            t.fields.push_back({op, vs.empty() ? string() : vs[0]});
+            t.fieldKeys.push_back(s.s(nsr_key[k]));
+        }
+        return t;
+    }
+    PATerm pat(int row) {
+        PATerm t;
+        int sr = pat_sel[row];
+        if (sr < 0) t.sel.nothing = true;
+        else {
+            for (int k = ls_ml[sr]; k < ls_ml[sr + 1]; ++k) {
+                Req r;
+                if (!compileReq(w, s.s(lkv_k[k]), OEq, {s.s(lkv_v[k])}, &r)) t.selErr = true;
+                t.sel.reqs.push_back(r);
+            }
+            for (int k = ls_me[sr]; k < ls_me[sr + 1]; ++k) {
+                Req r;
+                int op = lsr_op[k];
+                if (op > ODNE || !compileReq(w, s.s(lsr_key[k]), op, strs(lsr_voff, lsrv, k), &r)) t.selErr = true;
+                t.sel.reqs.push_back(r);
+            }
+        }
+        for (int k = pat_ns[row]; k < pat_ns[row + 1]; ++k) t.ns.push_back(w.nss.get(s.s(patns[k])));
+        string tk = s.s(pat_topo[row]);
+        t.key = tk.empty() ? -1 : w.keys.get(tk);
+        return t;
+    }
+
+    void load() {
+        auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
+        // conf
+        auto pn = V32("conf_plugin_name"), pt = V32("conf_plugin_tier"), pf = V32("conf_plugin_flags"),
+             ap = V32("conf_arg_plugin"), ak = V32("conf_arg_key"), av = V32("conf_arg_val");
+        vector<Plugin> opts(pn.size());
+        for (size_t i = 0; i < pn.size(); ++i) { opts[i].name = s.s(pn[i]); opts[i].flags = pf[i]; }
+        for (size_t i = 0; i < ap.size(); ++i) opts[ap[i]].args[s.s(ak[i])] = s.s(av[i]);
+        for (size_t i = 0; i < pn.size(); ++i) {
+            if ((size_t)pt[i] >= w.tiers.size()) w.tiers.resize(pt[i] + 1);
+            w.tiers[pt[i]].push_back(opts[i]);
+        }
+        // nodes
+        auto nname = V32("n_name");
+        size_t N = nname.size();
+        auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"),
+             agpu = s.vec<int64_t>("n_alloc_gpu"), apods = s.vec<int64_t>("n_alloc_pods");
+        auto unsched = s.vec<uint8_t>("n_unsched");
+        auto loff = s.offs("n_label_off", N);
+        auto lk = V32("nl_key"), lv = V32("nl_val");
+        auto toff = s.offs("n_taint_off", N);
+        auto tk = V32("nt_key"), tv = V32("nt_val"), te = V32("nt_effect");
+        w.nodes.resize(N);
+        std::map<string, int> taintIds;
+        for (size_t i = 0; i < N; ++i) {
+            NodeRec& n = w.nodes[i];
+            n.name = s.s(nname[i]);
+            for (int k = loff[i]; k < loff[i + 1]; ++k) n.labels.push_back({w.keys.get(s.s(lk[k])), w.vals.get(s.s(lv[k]))});
+            std::sort(n.labels.begin(), n.labels.end());
+            for (int k = toff[i]; k < toff[i + 1]; ++k) {
+                string eff = s.s(te[k]);
+                if (eff != "NoSchedule" && eff != "NoExecute") continue;  // predicates.go:1494-1497
+                string key = s.s(tk[k]) + '\x01' + s.s(tv[k]) + '\x01' + eff;
+                auto it = taintIds.find(key);
+                int id;
+                if (it == taintIds.end()) {
+                    id = (int)w.taintDefs.size();
+                    taintIds[key] = id;
+                    w.taintDefs.emplace_back(w.keys.get(s.s(tk[k])), w.vals.get(s.s(tv[k])), eff);
+                } else id = it->second;
+                n.taints.push_back(id);
+            }
+            n.unsched = !unsched.empty() && unsched[i];
+            n.maxTasks = (int)apods[i];
+            n.alloc = Res{acpu[i], amem[i], agpu[i]};
+            n.idle = n.alloc;
+            n.acpu = acpu[i];
+            n.amem = amem[i];
+        }
+        // affinity tables
+        nsr_key = V32("nsr_key"); nsr_op = s.vec<uint8_t>("nsr_op"); nsr_voff = s.offs("nsr_val_off", nsr_key.size());
+        nsrv = V32("nsrv");
+        lsr_key = V32("lsr_key"); lsr_op = s.vec<uint8_t>("lsr_op"); lsr_voff = s.offs("lsr_val_off", lsr_key.size());
+        lsrv = V32("lsrv");
+        ls_ml = V32("ls_ml_off"); ls_me = V32("ls_me_off"); lkv_k = V32("lkv_key"); lkv_v = V32("lkv_val");
+        pat_sel = V32("pat_sel"); pat_topo = V32("pat_topo"); pat_ns = s.offs("pat_ns_off", pat_sel.size());
+        patns = V32("patns");
+        es = V32("nst_expr_start"); ec = V32("nst_expr_cnt"); fs = V32("nst_field_start"); fc = V32("nst_field_cnt");
+        auto a_flags = s.vec<uint8_t>("a_flags");
+        auto pst_w = V32("pst_weight"), pst_t = V32("pst_term"), wpat_w = V32("wpat_weight"), wpat_t = V32("wpat_term");
+        auto S = [&](const char* n) { return V32(n); };
+        auto nareq_s = S("a_nareq_start"), nareq_c = S("a_nareq_cnt"), napref_s = S("a_napref_start"),
+             napref_c = S("a_napref_cnt"), pareq_s = S("a_pareq_start"), pareq_c = S("a_pareq_cnt"),
+             papref_s = S("a_papref_start"), papref_c = S("a_papref_cnt"), paareq_s = S("a_paareq_start"),
+             paareq_c = S("a_paareq_cnt"), paapref_s = S("a_paapref_start"), paapref_c = S("a_paapref_cnt");
+        vector<std::shared_ptr<Aff>> affs(a_flags.size());
+        for (size_t a = 0; a < a_flags.size(); ++a) {
+            auto af = std::make_shared<Aff>();
+            af->na = a_flags[a] & KBS_AFF_NA; af->naReq = a_flags[a] & KBS_AFF_NA_REQ;
+            af->pa = a_flags[a] & KBS_AFF_PA; af->paa = a_flags[a] & KBS_AFF_PAA;
+            for (int k = nareq_s[a]; k < nareq_s[a] + nareq_c[a]; ++k) af->naReqTerms.push_back(nst(k));
+            for (int k = napref_s[a]; k < napref_s[a] + napref_c[a]; ++k) af->naPref.push_back({pst_w[k], nst(pst_t[k])});
+            for (int k = pareq_s[a]; k < pareq_s[a] + pareq_c[a]; ++k) af->paReq.push_back(pat(k));
+            for (int k = paareq_s[a]; k < paareq_s[a] + paareq_c[a]; ++k) af->paaReq.push_back(pat(k));
+            for (int k = papref_s[a]; k < papref_s[a] + papref_c[a]; ++k) af->paPref.push_back({wpat_w[k], pat(wpat_t[k])});
+            for (int k = paapref_s[a]; k < paapref_s[a] + paapref_c[a]; ++k) af->paaPref.push_back({wpat_w[k], pat(wpat_t[k])});
+            affs[a] = af;
+        }
+        // pods
+        auto puid = V32("p_uid");
+        size_t P = puid.size();
+        auto pname = V32("p_name"), pns = V32("p_ns"), pjob = V32("p_job"), pnode = V32("p_node"),
+             ppri = V32("p_priority"), paff = V32("p_aff");
+        auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+        auto pts = s.vec<int64_t>("p_ts");
+        auto plo = s.offs("p_label_off", P);
+        auto plk = V32("pl_key"), plv = V32("pl_val");
+        auto pso = s.offs("p_nsel_off", P);
+        auto psk = V32("ps_key"), psv = V32("ps_val");
+        auto pco = s.offs("p_ctr_off", P);
+        auto ccpu = s.vec<int64_t>("c_cpu"), cmem = s.vec<int64_t>("c_mem"), cgpu = s.vec<int64_t>("c_gpu");
+        auto chas = s.vec<uint8_t>("c_has");
+        auto cpo = s.offs("c_port_off", ccpu.size());
+        auto ptip = V32("pt_ip"), ptpr = V32("pt_proto"), ptpo = V32("pt_port");
+        auto pio = s.offs("p_ictr_off", P);
+        auto iccpu = s.vec<int64_t>("ic_cpu"), icmem = s.vec<int64_t>("ic_mem"), icgpu = s.vec<int64_t>("ic_gpu");
+        auto pto = s.offs("p_tol_off", P);
+        auto tlk = V32("tl_key"), tlo = V32("tl_op"), tlv = V32("tl_val"), tle = V32("tl_effect");
+        std::unordered_map<string, int> nodeIdx;
+        for (size_t i = 0; i < N; ++i) nodeIdx[w.nodes[i].name] = (int)i;
+        w.pods.resize(P);
+        int defaultNs = -1;
+        (void)defaultNs;
+        for (size_t i = 0; i < P; ++i) {
+            PodRec& p = w.pods[i];
+            p.uid = s.s(puid[i]);
+            p.name = s.s(pname[i]);
+            p.ns = w.nss.get(s.s(pns[i]));
+            for (int k = plo[i]; k < plo[i + 1]; ++k) p.labels.push_back({w.keys.get(s.s(plk[k])), w.vals.get(s.s(plv[k]))});
+            std::sort(p.labels.begin(), p.labels.end());
+            string nn = s.s(pnode[i]);
+            if (!nn.empty()) {
+                auto it = nodeIdx.find(nn);
+                if (it == nodeIdx.end()) throw std::runtime_error("pod " + p.uid + " bound to unknown node " + nn);
+                p.nodeRaw = it->second;
+            }
+            // getTaskStatus (api/helpers.go:35-61)
+            int ph = pphase[i];
+            bool del = pdel[i];
+            if (ph == KBS_RUNNING) p.status = del ? Releasing : Running;
+            else if (ph == KBS_PENDING) p.status = del ? Releasing : (nn.empty() ? Pending : Bound);
+            else if (ph == KBS_SUCCEEDED) p.status = Succeeded;
+            else if (ph == KBS_FAILED) p.status = Failed;
+            else p.status = Unknown;
+            p.priority = ppri[i];
+            p.ts = pts[i];
+            p.backfill = pbf[i];
+            for (int k = pco[i]; k < pco[i + 1]; ++k) {
+                p.req += Res{ccpu[k], cmem[k], cgpu[k]};
+                p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;                 // non_zero.go:43-47
+                p.nzm += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;  // non_zero.go:48-52
+                for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
+                    string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
+                    if (ip.empty()) ip = "0.0.0.0";
+                    if (pr.empty()) pr = "TCP";
+                    p.ports.push_back({w.ips.get(ip), w.protos.get(pr), ptpo[q]});
+                }
+            }
+            p.initReq = p.req;
+            for (int k = pio[i]; k < pio[i + 1]; ++k) {  // SetMaxResource (resource_info.go:114-128)
+                p.initReq.cpu = std::max(p.initReq.cpu, iccpu[k]);
+                p.initReq.mem = std::max(p.initReq.mem, icmem[k]);
+                p.initReq.gpu = std::max(p.initReq.gpu, icgpu[k]);
+            }
+            for (int k = pso[i]; k < pso[i + 1]; ++k) p.nsel.push_back({w.keys.get(s.s(psk[k])), w.vals.get(s.s(psv[k]))});
+            // tolerations -> tolerated taint ids (toleration.go:37-56)
+            for (size_t t = 0; t < w.taintDefs.size(); ++t) {
+                const auto& td = w.taintDefs[t];
+                bool tol = false;
+                for (int k = pto[i]; k < pto[i + 1] && !tol; ++k) {
+                    string key = s.s(tlk[k]), op = s.s(tlo[k]), val = s.s(tlv[k]), eff = s.s(tle[k]);
+                    if (!eff.empty() && eff != std::get<2>(td)) continue;
+                    if (!key.empty() && key != w.keys.strs[std::get<0>(td)]) continue;
+                    if (op.empty() || op == "Equal") tol = val == w.vals.strs[std::get<1>(td)];
+                    else if (op == "Exists") tol = true;
+                }
+                if (tol) p.tolTaints.push_back((int)t);
+            }
+            if (!paff.empty() && paff[i] >= 0) p.aff = affs[paff[i]];
+        }
+        ensureValInt(w);
+        // queues
+        auto qn = V32("q_name"), qw = V32("q_weight");
+        auto qts = s.vec<int64_t>("q_ts");
+        w.queues.resize(qn.size());
+        std::map<string, int> qidx;
+        for (size_t i = 0; i < qn.size(); ++i) {
+            w.queues[i].name = s.s(qn[i]);
+            w.queues[i].weight = qw[i];
+            w.queues[i].ts = qts.empty() ? 0 : qts[i];
+            qidx[w.queues[i].name] = (int)i;
+        }
+        // jobs: pod-group jobs + shadow jobs, sorted by UID; only jobs whose queue exists
+        auto jns = V32("j_ns"), jname = V32("j_name"), jq = V32("j_queue"), jmin = V32("j_min"),
+             jpri = V32("j_pg_priority");
+        auto jts = s.vec<int64_t>("j_ts");
+        struct Src { string uid; int row, pod; };
+        vector<Src> srcs;
+        for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
+        for (size_t i = 0; i < P; ++i) if (pjob[i] < 0) srcs.push_back({w.pods[i].uid, -1, (int)i});
+        std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+        vector<int> rowSlot(jns.size(), -1);
+        vector<int> shadowSlot(P, -1);
+        for (auto& src : srcs) {
+            string qname = src.row >= 0 ? s.s(jq[src.row]) : string("default");
+            auto qit = qidx.find(qname);
+            JobRec jr;
+            jr.uid = src.uid;
+            if (src.row >= 0) {
+                jr.minAvail = jmin[src.row];
+                jr.ts = jts[src.row];
+                jr.priority = jpri[src.row];
+            } else {
+                jr.minAvail = 1;
+                jr.ts = 0;
+                jr.priority = 0;
+            }
+            int slot = -1;
+            if (qit != qidx.end()) {
+                jr.queue = qit->second;
+                slot = (int)w.jobs.size();
+                w.jobs.push_back(jr);
+            }
+            if (src.row >= 0) rowSlot[src.row] = slot;
+            else shadowSlot[src.pod] = slot;
+        }
+        for (size_t i = 0; i < P; ++i) {
+            int slot = pjob[i] >= 0 ? rowSlot[pjob[i]] : shadowSlot[i];
+            w.pods[i].job = slot;
+            if (slot >= 0) {
+                w.jobs[slot].tasks.push_back((int)i);
+                w.pods[i].jobUID = w.jobs[slot].uid;
+            }
+        }
+        for (auto& j : w.jobs) {
+            for (int t : j.tasks) {
+                j.priority = w.pods[t].priority;  // AddTaskInfo: last task wins (job_info.go:242)
+                if (allocSt(w.pods[t].status)) j.cntAlloc++;
+                if (w.pods[t].status == AOB) j.cntAOB++;
+            }
+        }
+        // place pods on nodes (cache addTask -> NodeInfo.AddTask; terminated pods skipped)
+        for (size_t i = 0; i < P; ++i) {
+            PodRec& p = w.pods[i];
+            p.curNode = p.nodeRaw;
+            if (p.nodeRaw < 0 || p.status == Succeeded || p.status == Failed) continue;
+            NodeRec& n = w.nodes[p.nodeRaw];
+            if (p.backfill) n.bf += p.req;
+            if (p.status == Releasing) { n.rel += p.req; n.idle -= p.req; }
+            else if (p.status == Pipelined) n.rel -= p.req;
+            else n.idle -= p.req;
+            n.used += p.req;
+            n.pods++;
+            n.nzc += p.nzc;
+            n.nzm += p.nzm;
+            for (auto& pt : p.ports) if (pt.port > 0) n.used_ports.push_back(pt);
+            n.podList.push_back((int)i);
+        }
+        for (auto& n : w.nodes) if (n.bf.cpu || n.bf.mem || n.bf.gpu) w.anyBackfilled = true;
+        for (size_t i = 0; i < P; ++i) if (w.pods[i].hasPodAff() && w.pods[i].curNode >= 0 &&
+                                             w.pods[i].status != Succeeded && w.pods[i].status != Failed)
+            w.affPods.push_back((int)i);
+        // plugins (framework.go:33-48: one object per name, last entry's arguments;
+        // dispatch loops over tier entries, so an enabled duplicate entry counts twice)
+        for (auto& tier : w.tiers)
+            for (auto& p : tier) {
+                if (p.name == "predicates" && !(p.flags & KBS_DIS_PREDICATE)) w.predOn = true;
+                if (p.name == "nodeorder" && !(p.flags & KBS_DIS_NODEORDER)) { w.nodeorderOn = true; w.noMult++; }
+                if (p.name == "nodeorder") {
+                    w.wLR = w.wBRA = w.wNA = w.wPA = 1;
+                    auto get = [&](const char* k, int* dst) {
+                        auto it = p.args.find(k);
+                        int64_t v;
+                        if (it != p.args.end() && !it->second.empty() && parseI64(it->second, &v)) *dst = (int)v;
+                    };
+                    get("nodeaffinity.weight", &w.wNA);
+                    get("podaffinity.weight", &w.wPA);
+                    get("leastrequested.weight", &w.wLR);
+                    get("balancedresource.weight", &w.wBRA);
+                }
+                if (p.name == "drf") w.drfOn = true;
+                if (p.name == "proportion") w.propOn = true;
+                if (p.name == "gang") w.gangOn = true;
+                if (p.name == "priority") w.prioOn = true;
+            }
+        for (auto& n : w.nodes) w.total.add(toF(n.alloc));
+    }
+};
+
+/* ------------------------- per-task compiled view ------------------------ */
+struct TaskPlan {
+    int pod;
+    bool predErrAll = false;  // predicate fails on every node (selector errors)
+    bool scoreErrAll = false; // NodeOrderFn errors on every node -> all dropped
+    // pod (anti-)affinity predicate precompute
+    std::set<std::pair<int, int>> forbidden;  // (key, value) pairs
+    bool hasAffTerms = false, hasAntiTerms = false;
+    vector<vector<int>> affTuples;   // topology value tuples of targets matching all affinity props
+    bool affSelfPass = false;        // no target matched props and pod matches its own terms
+    vector<vector<int>> antiTuples;  // tuples of targets matching all anti-affinity props
+    vector<int> affKeys, antiKeys;
+    // inter-pod affinity priority: per (key, value) weight
+    bool ipaOn = false;
+    std::map<std::pair<int, int>, double> ipaAcc;
+    vector<int> ipaKeys;
+    double ipaMin = 0, ipaMax = 0;
+    // tolerated taints bitmap
+    vector<char> tol;
+};
+
+static bool nsHas(const PATerm& t, int definerNs, int ns) {
+    if (t.ns.empty()) return ns == definerNs;
+    for (int x : t.ns) if (x == ns) return true;
+    return false;
+}
+static bool termMatches(const World& w, const PATerm& t, const PodRec& definer, const PodRec& cand) {
+    return nsHas(t, definer.ns, cand.ns) && selMatch(w, t.sel, cand.labels);
+}
+
+// Nodes of targets: predicates' lister copies NodeName = task.NodeName (predicates.go:82-84)
+static void buildPodAffinityPlan(const World& w, TaskPlan& tp) {
+    const PodRec& pod = w.pods[tp.pod];
+    // targets: AllocatedStatuses tasks of session jobs, at their task.NodeName
+    // (1) existing pods' required anti-affinity (satisfiesExistingPodsAntiAffinity)
+    for (int ei : w.affPods) {
+        const PodRec& e = w.pods[ei];
+        if (e.job < 0 || !allocSt(e.status) || !e.aff || !e.aff->paa) continue;
+        for (auto& term : e.aff->paaReq) {
+            if (term.selErr) { tp.predErrAll = true; return; }
+            if (termMatches(w, term, e, pod)) {
+                int v = term.key < 0 ? -1 : lget(w.nodes[e.curNode].labels, term.key);
+                if (v >= 0) tp.forbidden.insert({term.key, v});
+            }
+        }
+    }
+    if (!pod.aff || (!pod.aff->pa && !pod.aff->paa)) return;
+    const vector<PATerm> none;
+    const vector<PATerm>& aff = pod.aff->pa ? pod.aff->paReq : none;
+    const vector<PATerm>& anti = pod.aff->paa ? pod.aff->paaReq : none;
+    for (auto& t : aff) if (t.selErr) { tp.predErrAll = true; return; }
+    for (auto& t : anti) if (t.selErr) { tp.predErrAll = true; return; }
+    tp.hasAffTerms = !aff.empty();
+    tp.hasAntiTerms = !anti.empty();
+    for (auto& t : aff) tp.affKeys.push_back(t.key);
+    for (auto& t : anti) tp.antiKeys.push_back(t.key);
+    // Empty topology keys: podMatchesPodAffinityTerms errors when it reaches one
+    // (predicates.go:1205-1208).  kbgen never emits them; the encoder rejects them.
+    bool anySel = false;
+    for (size_t ti = 0; ti < w.pods.size(); ++ti) {
+        const PodRec& t = w.pods[ti];
+        if (t.job < 0 || !allocSt(t.status) || t.curNode < 0) continue;
+        if (tp.hasAffTerms) {
+            bool all = true;
+            for (auto& term : aff) if (!termMatches(w, term, pod, t)) { all = false; break; }
+            if (all) {
+                anySel = true;
+                vector<int> tup;
+                bool ok = true;
+                for (int k : tp.affKeys) {
+                    int v = k < 0 ? -1 : lget(w.nodes[t.curNode].labels, k);
+                    if (v < 0) { ok = false; break; }
+                    tup.push_back(v);
+                }
+                if (ok) tp.affTuples.push_back(tup);
+            }
+        }
+        if (tp.hasAntiTerms) {
+            bool all = true;
+            for (auto& term : anti) if (!termMatches(w, term, pod, t)) { all = false; break; }
+            if (all) {
+                vector<int> tup;
+                bool ok = true;
+                for (int k : tp.antiKeys) {
+                    int v = k < 0 ? -1 : lget(w.nodes[t.curNode].labels, k);
+                    if (v < 0) { ok = false; break; }
+                    tup.push_back(v);
+                }
+                if (ok) tp.antiTuples.push_back(tup);
+            }
+        }
+    }
+    if (tp.hasAffTerms && !anySel) {
+        // targetPodMatchesAffinityOfPod(pod, pod) (metadata.go:498-509)
+        bool self = true;
+        for (auto& term : aff) if (!termMatches(w, term, pod, pod)) { self = false; break; }
+        tp.affSelfPass = self;
+    }
+    std::sort(tp.affTuples.begin(), tp.affTuples.end());
+    tp.affTuples.erase(std::unique(tp.affTuples.begin(), tp.affTuples.end()), tp.affTuples.end());
+    std::sort(tp.antiTuples.begin(), tp.antiTuples.end());
+    tp.antiTuples.erase(std::unique(tp.antiTuples.begin(), tp.antiTuples.end()), tp.antiTuples.end());
+}
+
+// CalculateInterPodAffinityPriority (interpod_affinity.go:119-240) as per-(key, value) tables
+static void buildIPAPlan(const World& w, TaskPlan& tp) {
+    const PodRec& pod = w.pods[tp.pod];
+    bool hasAff = pod.aff && pod.aff->pa, hasAnti = pod.aff && pod.aff->paa;
+    auto add = [&](const PATerm& term, const PodRec& definer, const PodRec& toCheck, int fixedNode, double wgt) {
+        if (term.selErr) { tp.scoreErrAll = true; return; }
+        if (!termMatches(w, term, definer, toCheck)) return;
+        if (term.key < 0) return;  // NodesHaveSameTopologyKey("") is false
+        int v = lget(w.nodes[fixedNode].labels, term.key);
+        if (v < 0) return;
+        tp.ipaAcc[{term.key, v}] += wgt;
+    };
+    auto process = [&](int ei) {
+        const PodRec& e = w.pods[ei];
+        // nodeorder cachedNodeInfo.GetNodeInfo(existing.Spec.NodeName) with fallback (nodeorder.go:78-93)
+        int fixed = e.nodeRaw >= 0 ? e.nodeRaw : w.fallbackNode;
+        if (fixed < 0) { tp.scoreErrAll = true; return; }
+        if (hasAff) for (auto& t : pod.aff->paPref) add(t.t, pod, e, fixed, (double)(t.w * 1));
+        if (hasAnti) for (auto& t : pod.aff->paaPref) add(t.t, pod, e, fixed, (double)(t.w * -1));
+        if (e.aff && e.aff->pa) {
+            for (auto& t : e.aff->paReq) add(t, e, pod, fixed, 1.0);
+            for (auto& t : e.aff->paPref) add(t.t, e, pod, fixed, (double)(t.w * 1));
+        }
+        if (e.aff && e.aff->paa) for (auto& t : e.aff->paaPref) add(t.t, e, pod, fixed, (double)(t.w * -1));
+    };
+    if (hasAff || hasAnti) {
+        for (auto& n : w.nodes) for (int ei : n.podList) process(ei);
+    } else {
+        for (int ei : w.affPods) process(ei);
+    }
+    if (tp.scoreErrAll) return;
+    std::set<int> keys;
+    for (auto& kv : tp.ipaAcc) keys.insert(kv.first.first);
+    tp.ipaKeys.assign(keys.begin(), keys.end());
+    tp.ipaOn = !tp.ipaAcc.empty();
+    if (!tp.ipaOn) return;
+    double mx = 0, mn = 0;
+    for (auto& n : w.nodes) {
+        double c = 0;
+        for (int k : tp.ipaKeys) {
+            int v = lget(n.labels, k);
+            if (v < 0) continue;
+            auto it = tp.ipaAcc.find({k, v});
+            if (it != tp.ipaAcc.end()) c += it->second;
+        }
+        if (c > mx) mx = c;
+        if (c < mn) mn = c;
+    }
+    tp.ipaMax = mx;
+    tp.ipaMin = mn;
+}
+
+static void buildPlan(const World& w, TaskPlan& tp) {
+    const PodRec& pod = w.pods[tp.pod];
+    tp.tol.assign(w.taintDefs.size(), 0);
+    for (int t : pod.tolTaints) tp.tol[t] = 1;
+    if (w.predOn) buildPodAffinityPlan(w, tp);
+    if (w.nodeorderOn) {
+        if (pod.aff && pod.aff->na)
+            for (auto& pt : pod.aff->naPref)
+                if (pt.first != 0 && pt.second.exprErr) tp.scoreErrAll = true;  // NA map error (node_affinity.go:61-63)
+        if (!tp.scoreErrAll) buildIPAPlan(w, tp);
+    }
+}
+
+/* one node: predicate + score; returns false when the node is filtered out */
+static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* scoreOut) {
+    const NodeRec& n = w.nodes[ni];
+    const PodRec& pod = w.pods[tp.pod];
+    if (w.predOn) {
+        if (tp.predErrAll) return false;
+        if (n.maxTasks <= n.pods) return false;                              // predicates.go:127
+        for (auto& kv : pod.nsel) if (lget(n.labels, kv.first) != kv.second) return false;  // predicates.go:809-814
+        if (pod.aff && pod.aff->na && pod.aff->naReq) {                      // predicates.go:826-846
+            bool any = false;
+            for (auto& term : pod.aff->naReqTerms) {
+                if (term.expr.empty() && term.fieldKeys.empty()) continue;
+                if (!term.expr.empty()) {
+                    if (term.exprErr) continue;
+                    bool ok = true;
+                    for (auto& r : term.expr) if (!reqMatch(w, r, n.labels)) { ok = false; break; }
+                    if (!ok) continue;
+                }
+                if (!term.fieldKeys.empty()) {
+                    if (term.fieldErr) continue;
+                    bool ok = true;
+                    for (size_t f = 0; f < term.fields.size(); ++f) {
+                        string fv = term.fieldKeys[f] == "metadata.name" ? n.name : string();
+                        bool eq = fv == term.fields[f].second;
+                        if ((term.fields[f].first == OIn && !eq) || (term.fields[f].first == ONotIn && eq)) { ok = false; break; }
+                    }
+                    if (!ok) continue;
+                }
+                any = true;
+                break;
+            }
+            if (!any) return false;
+        }
+        for (auto& pt : pod.ports) {                                         // host_ports.go:96-125
+            if (pt.port <= 0) continue;
+            bool anyIp = w.ips.strs[pt.ip] == "0.0.0.0";
+            for (auto& u : n.used_ports) {
+                if (u.proto != pt.proto || u.port != pt.port) continue;
+                if (anyIp || u.ip == pt.ip || w.ips.strs[u.ip] == "0.0.0.0") return false;
+            }
+        }
+        if (n.unsched) return false;                                         // predicates.go:107-112
+        for (int t : n.taints) if (!tp.tol[t]) return false;                 // helper/helpers.go:425-440
+        for (auto& kv : n.labels) if (tp.forbidden.count(kv)) return false;  // predicates.go:1326-1331
+        if (tp.hasAffTerms) {                                                // predicates.go:1402-1458
+            bool match = false;
+            vector<int> tup;
+            bool ok = true;
+            for (int k : tp.affKeys) {
+                int v = k < 0 ? -1 : lget(n.labels, k);
+                if (v < 0) { ok = false; break; }
+                tup.push_back(v);
+            }
+            if (ok) match = std::binary_search(tp.affTuples.begin(), tp.affTuples.end(), tup);
+            if (!match && !tp.affSelfPass) return false;
+        }
+        if (tp.hasAntiTerms) {
+            vector<int> tup;
+            bool ok = true;
+            for (int k : tp.antiKeys) {
+                int v = k < 0 ? -1 : lget(n.labels, k);
+                if (v < 0) { ok = false; break; }
+                tup.push_back(v);
+            }
+            if (ok && std::binary_search(tp.antiTuples.begin(), tp.antiTuples.end(), tup)) return false;
+        }
+    }
+    int score = 0;
+    if (w.nodeorderOn) {
+        if (tp.scoreErrAll) return false;
+        int64_t rc = pod.nzc + n.nzc, rm = pod.nzm + n.nzm;
+        auto lrs = [](int64_t req, int64_t cap) -> int64_t {                // least_requested.go:44-53
+            if (cap == 0 || req > cap) return 0;
+            return ((cap - req) * 10) / cap;
+        };
+        int64_t lr = (lrs(rc, n.acpu) + lrs(rm, n.amem)) / 2;
+        double cf = n.acpu == 0 ? 1 : (double)rc / (double)n.acpu;          // balanced_resource_allocation.go:72-77
+        double mf = n.amem == 0 ? 1 : (double)rm / (double)n.amem;
+        int64_t bra = 0;
+        if (!(cf >= 1 || mf >= 1)) {
+            double d = std::fabs(cf - mf);
+            double t = 1 - d;
+            bra = (int64_t)(t * 10.0);
+        }
+        int na = 0;
+        if (pod.aff && pod.aff->na)
+            for (auto& pt : pod.aff->naPref) {
+                if (pt.first == 0) continue;
+                if (pt.second.expr.empty()) continue;  // labels.Nothing()
+                bool ok = true;
+                for (auto& r : pt.second.expr) if (!reqMatch(w, r, n.labels)) { ok = false; break; }
+                if (ok) na += pt.first;
+            }
+        int ipa = 0;
+        if (tp.ipaOn && tp.ipaMax - tp.ipaMin > 0) {
+            double c = 0;
+            for (int k : tp.ipaKeys) {
+                int v = lget(n.labels, k);
+                if (v < 0) continue;
+                auto it = tp.ipaAcc.find({k, v});
+                if (it != tp.ipaAcc.end()) c += it->second;
+            }
+            double f = 10.0 * ((c - tp.ipaMin) / (tp.ipaMax - tp.ipaMin));
+            ipa = (int)f;
+        }
+        score = ((int)lr * w.wLR + (int)bra * w.wBRA + na * w.wNA + ipa * w.wPA) * w.noMult;
+    }
+    *scoreOut = score;
+    return true;
+}
+
+/* ------------------------- thread pool sweep ----------------------------- */
+struct Best {
+    int score = 0;
+    int idx = -1;
+    int kind = 0;  // 1 alloc, 2 pipeline
+};
+static inline bool better(int s, int i, const Best& b) { return b.idx < 0 || s > b.score || (s == b.score && i < b.idx); }
+
+struct Pool {
+    int T;
+    vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv, done;
+    int gen = 0, remaining = 0;
+    bool stop = false;
+    std::function<void(int)> job;
+    explicit Pool(int t) : T(t) {
+        for (int i = 1; i < T; ++i) th.emplace_back([this, i] { loop(i); });
+    }
+    ~Pool() {
+        { std::lock_guard<std::mutex> g(mu); stop = true; ++gen; }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+    void loop(int id) {
+        int seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return gen != seen; });
+            seen = gen;
+            if (stop) return;
+            lk.unlock();
+            job(id);
+            lk.lock();
+            if (--remaining == 0) done.notify_one();
+        }
+    }
+    void run(std::function<void(int)> f) {
+        if (T == 1) { f(0); return; }
+        {
+            std::lock_guard<std::mutex> g(mu);
+            job = f;
+            remaining = T - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu);
+        done.wait(lk, [&] { return remaining == 0; });
+    }
+};
+
+/* ------------------------- ordering (Go heap) ---------------------------- */
+template <typename L>
+struct Heap {  // container/heap over util.PriorityQueue (util/priority_queue.go)
+    vector<int> items;
+    L less;
+    explicit Heap(L l) : less(l) {}
+    bool Less(int i, int j) { return less(items[i], items[j]); }
+    void up(int j) {
+        for (;;) {
+            int i = (j - 1) / 2;
+            if (i == j || !Less(j, i)) break;
+            std::swap(items[i], items[j]);
+            j = i;
+        }
+    }
+    void down(int i, int n) {
+        for (;;) {
+            int j1 = 2 * i + 1;
+            if (j1 >= n || j1 < 0) break;
+            int j = j1, j2 = j1 + 1;
+            if (j2 < n && Less(j2, j1)) j = j2;
+            if (!Less(j, i)) break;
+            std::swap(items[i], items[j]);
+            i = j;
+        }
+    }
+    void push(int x) { items.push_back(x); up((int)items.size() - 1); }
+    int pop() {
+        int n = (int)items.size() - 1;
+        std::swap(items[0], items[n]);
+        down(0, n);
+        int x = items.back();
+        items.pop_back();
+        return x;
+    }
+    bool empty() const { return items.empty(); }
+};
+
+struct Engine {
+    World& w;
+    Pool pool;
+    int pops = 0, tried = 0;
+    Engine(World& w_, int threads) : w(w_), pool(threads) {}
+
+    int readiness(const JobRec& j) const {  // job_info.go:374-388
+        if (j.cntAlloc >= j.minAvail) return 1;
+        if (j.cntAlloc + j.cntAOB >= j.minAvail) return 2;
+        return 4;
+    }
+    bool jobReady(const JobRec& j) const {  // session_plugins.go:167-186 (gang is the only JobReadyFn)
+        int status = 1;
+        for (auto& tier : w.tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_JOBREADY) continue;
+                if (p.name != "gang") continue;
+                status = readiness(j);
+                break;
+            }
+        return status == 1;
+    }
+    bool jobLess(int l, int r) const {  // session_plugins.go:244-268
+        const JobRec &L = w.jobs[l], &R = w.jobs[r];
+        for (auto& tier : w.tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_JOBORDER) continue;
+                int c = 0;
+                if (p.name == "priority") c = L.priority > R.priority ? -1 : L.priority < R.priority ? 1 : 0;
+                else if (p.name == "gang") {
+                    bool lr = readiness(L) == 1, rr = readiness(R) == 1;
+                    c = (lr && rr) ? 0 : lr ? 1 : rr ? -1 : 0;
+                } else if (p.name == "drf") {
+                    c = L.drfShare == R.drfShare ? 0 : L.drfShare < R.drfShare ? -1 : 1;
+                } else continue;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.uid < R.uid;
+        return L.ts < R.ts;
+    }
+    bool queueLess(int l, int r) const {  // :270-295
+        const QueueRec &L = w.queues[l], &R = w.queues[r];
+        for (auto& tier : w.tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_QUEUEORDER) continue;
+                if (p.name != "proportion") continue;
+                int c = L.share == R.share ? 0 : L.share < R.share ? -1 : 1;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.name < R.name;
+        return L.ts < R.ts;
+    }
+    bool taskLess(int l, int r) const {  // :297-329
+        const PodRec &L = w.pods[l], &R = w.pods[r];
+        for (auto& tier : w.tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_TASKORDER) continue;
+                if (p.name != "priority") continue;
+                int c = L.priority == R.priority ? 0 : L.priority > R.priority ? -1 : 1;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.uid < R.uid;
+        return L.ts < R.ts;
+    }
+    void drfUpdate(JobRec& j) {  // drf.go:156-170
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double s = share(j.drfAlloc.get(k), w.total.get(k)); if (s > res) res = s; }
+        j.drfShare = res;
+    }
+    void propUpdate(QueueRec& q) {  // proportion.go:229-241
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double s = share(q.allocated.get(k), q.deserved.get(k)); if (s > res) res = s; }
+        q.share = res;
+    }
+    void openPlugins() {
+        if (w.drfOn)
+            for (auto& j : w.jobs) {
+                for (int t : j.tasks) if (allocSt(w.pods[t].status)) j.drfAlloc.add(toF(w.pods[t].req));
+                drfUpdate(j);
+            }
+        if (w.propOn) {
+            vector<int> order;
+            for (auto& j : w.jobs) {
+                QueueRec& q = w.queues[j.queue];
+                q.hasAttr = true;
+                for (int t : j.tasks) {
+                    const PodRec& p = w.pods[t];
+                    if (allocSt(p.status)) { q.allocated.add(toF(p.req)); q.request.add(toF(p.req)); }
+                    else if (p.status == Pending) q.request.add(toF(p.req));
+                }
+            }
+            for (size_t i = 0; i < w.queues.size(); ++i) if (w.queues[i].hasAttr) order.push_back((int)i);
+            FRes remaining = w.total;
+            vector<char> meet(w.queues.size(), 0);
+            for (;;) {  // proportion.go:100-142
+                int32_t tw = 0;
+                for (int q : order) if (!meet[q]) tw += w.queues[q].weight;
+                if (tw == 0) break;
+                FRes deserved;
+                for (int qi : order) {
+                    if (meet[qi]) continue;
+                    QueueRec& q = w.queues[qi];
+                    double ratio = (double)q.weight / (double)tw;
+                    FRes r = remaining;
+                    r.c *= ratio; r.m *= ratio; r.g *= ratio;
+                    q.deserved.add(r);
+                    if (!q.deserved.lessEqual(q.request)) {
+                        q.deserved.c = std::fmin(q.deserved.c, q.request.c);
+                        q.deserved.g = std::fmin(q.deserved.g, q.request.g);
+                        q.deserved.m = std::fmin(q.deserved.m, q.request.m);
+                        meet[qi] = 1;
+                    }
+                    propUpdate(q);
+                    deserved.add(q.deserved);
+                }
+                remaining.sub(deserved);
+                if (remaining.isEmpty()) break;
+            }
+        }
+    }
+    bool overused(int qi) const {  // proportion.go:186-197
+        if (!w.propOn) return false;
+        const QueueRec& q = w.queues[qi];
+        return q.deserved.lessEqual(q.allocated);
+    }
+
+    // event handlers (drf.go:134-143, proportion.go:200-210)
+    void onAllocate(const PodRec& p) {
+        if (w.drfOn) { JobRec& j = w.jobs[p.job]; j.drfAlloc.add(toF(p.req)); drfUpdate(j); }
+        if (w.propOn) { QueueRec& q = w.queues[w.jobs[p.job].queue]; q.allocated.add(toF(p.req)); propUpdate(q); }
+    }
+    void nodeAddTask(int pi, int ni, int status) {  // node_info.go:113-145 + k8s NodeInfo.AddPod
+        PodRec& p = w.pods[pi];
+        NodeRec& n = w.nodes[ni];
+        if (p.backfill) { n.bf += p.req; w.anyBackfilled = true; }
+        if (status == Releasing) { n.rel += p.req; n.idle -= p.req; }
+        else if (status == Pipelined) n.rel -= p.req;
+        else n.idle -= p.req;
+        n.used += p.req;
+        n.pods++;
+        n.nzc += p.nzc;
+        n.nzm += p.nzm;
+        for (auto& pt : p.ports) if (pt.port > 0) n.used_ports.push_back(pt);
+        n.podList.push_back(pi);
+        // raw Spec.NodeName stays "" for session-placed pods: nodeorder fallback node
+        if (p.nodeRaw < 0 && (w.fallbackNode < 0 || ni < w.fallbackNode)) w.fallbackNode = ni;
+        if (p.hasPodAff()) w.affPods.push_back(pi);
+    }
+
+    // one task: predicate + score sweep, select, commit.  Returns assigned.
+    bool placeTask(int pi) {
+        tried++;
+        TaskPlan tp;
+        tp.pod = pi;
+        buildPlan(w, tp);
+        PodRec& p = w.pods[pi];
+        int N = (int)w.nodes.size();
+        int T = pool.T;
+        vector<Best> bests(T);
+        vector<int> scores;  // kept only when the backfill mutation may apply
+        vector<char> passed;
+        bool track = w.anyBackfilled;
+        if (track) { scores.assign(N, 0); passed.assign(N, 0); }
+        pool.run([&](int t) {
+            int lo = (int)((int64_t)N * t / T), hi = (int)((int64_t)N * (t + 1) / T);
+            Best b;
+            for (int ni = lo; ni < hi; ++ni) {
+                int s;
+                if (!evalNode(w, tp, ni, &s)) continue;
+                const NodeRec& n = w.nodes[ni];
+                if (track) { scores[ni] = s; passed[ni] = 1; }
+                int kind = le_sum(p.initReq, n.idle, n.bf) ? 1 : le(p.initReq, n.rel) ? 2 : 0;
+                if (!kind) continue;
+                if (better(s, ni, b)) { b.score = s; b.idx = ni; b.kind = kind; }
+            }
+            bests[t] = b;
+        });
+        Best best;
+        for (auto& b : bests) if (b.idx >= 0 && better(b.score, b.idx, best)) best = b;
+        if (track) {
+            // GetAccessibleResource mutates Idle of every node the walk visits (node_info.go:209-211)
+            for (int ni = 0; ni < N; ++ni) {
+                if (!passed[ni]) continue;
+                if (best.idx >= 0 && !(scores[ni] > best.score || (scores[ni] == best.score && ni <= best.idx))) continue;
+                w.nodes[ni].idle += w.nodes[ni].bf;
+            }
+        }
+        if (best.idx < 0) return false;
+        JobRec& j = w.jobs[p.job];
+        int status;
+        if (best.kind == 1) {
+            // Allocate (session.go:237-297); usingBackfillTaskRes is always false here (Appendix A.1)
+            status = Allocated;
+            j.cntAlloc++;
+        } else {
+            status = Pipelined;  // Pipeline (session.go:199-235)
+        }
+        p.status = status;
+        p.curNode = best.idx;
+        nodeAddTask(pi, best.idx, status);
+        onAllocate(p);
+        w.log.emplace_back(pi, best.idx, status);
+        if (status == Allocated && jobReady(j)) {
+            // dispatch: Allocated -> Binding (both AllocatedStatuses; counts unchanged)
+            for (int t : j.tasks) if (w.pods[t].status == Allocated) w.pods[t].status = Binding;
+        }
+        return true;
+    }
+
+    void allocate(int maxPops) {  // allocate.go:41-201
+        auto ql = [this](int a, int b) { return queueLess(a, b); };
+        auto jl = [this](int a, int b) { return jobLess(a, b); };
+        auto tl = [this](int a, int b) { return taskLess(a, b); };
+        Heap<decltype(ql)> queues(ql);
+        std::map<int, Heap<decltype(jl)>> jobsMap;
+        for (size_t j = 0; j < w.jobs.size(); ++j) {
+            int q = w.jobs[j].queue;
+            queues.push(q);
+            auto it = jobsMap.find(q);
+            if (it == jobsMap.end()) it = jobsMap.emplace(q, Heap<decltype(jl)>(jl)).first;
+            it->second.push((int)j);
+        }
+        std::map<int, Heap<decltype(tl)>> pending;
+        while (!queues.empty()) {
+            if (maxPops >= 0 && pops >= maxPops) break;
+            int q = queues.pop();
+            if (overused(q)) continue;
+            auto jit = jobsMap.find(q);
+            if (jit == jobsMap.end() || jit->second.empty()) continue;
+            int jb = jit->second.pop();
+            pops++;
+            auto pit = pending.find(jb);
+            if (pit == pending.end()) {
+                Heap<decltype(tl)> h(tl);
+                for (int t : w.jobs[jb].tasks) {
+                    const PodRec& p = w.pods[t];
+                    if (p.status != Pending) continue;
+                    if (isEmpty(p.req)) continue;  // BestEffort (allocate.go:95)
+                    h.push(t);
+                }
+                pit = pending.emplace(jb, std::move(h)).first;
+            }
+            auto& tasks = pit->second;
+            while (!tasks.empty()) {
+                int t = tasks.pop();
+                if (!placeTask(t)) break;
+                if (jobReady(w.jobs[jb])) {
+                    jit->second.push(jb);
+                    break;
+                }
+            }
+            queues.push(q);
+        }
+    }
+};
+
+}  // namespace fast
+
+static thread_local std::string g_ferr;
+
+extern "C" {
+const char* fast_last_error(void) { return g_ferr.c_str(); }
+
+/* Hoisted allocate.  timing[0]=open s, [1]=allocate s, [2]=pops, [3]=tasks tried, [4]=load s */
+int fast_allocate(const char* path, int threads, int max_pops, int32_t* out_pod, int32_t* out_node,
+                  int32_t* out_status, int cap, double* timing) {
+    try {
+        using clk = std::chrono::steady_clock;
+        auto t0 = clk::now();
+        kbs::Snapshot snap(path);
+        fast::World w;
+        fast::Loader L(snap, w);
+        L.load();
+        auto t1 = clk::now();
+        fast::Engine e(w, threads < 1 ? 1 : threads);
+        e.openPlugins();
+        auto t2 = clk::now();
+        e.allocate(max_pops);
+        auto t3 = clk::now();
+        int n = (int)w.log.size();
+        for (int i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(w.log[i]);
+            out_node[i] = std::get<1>(w.log[i]);
+            out_status[i] = std::get<2>(w.log[i]);
+        }
+        if (timing) {
+            timing[0] = std::chrono::duration<double>(t2 - t1).count();
+            timing[1] = std::chrono::duration<double>(t3 - t2).count();
+            timing[2] = e.pops;
+            timing[3] = e.tried;
+            timing[4] = std::chrono::duration<double>(t1 - t0).count();
+        }
+        return n;
+    } catch (std::exception& ex) {
+        g_ferr = ex.what();
+        return -1;
+    }
+}
+}

@@ -1,0 +1,1771 @@
+/*
+ * kbref.cpp — TEST ORACLE (faithful restatement).  Test infrastructure only:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this; the product (kube-batch-1_amd/) never links or calls it.
+ *
+ * A C++ restatement of kube-batch's allocate action as the Go code at
+ * /root/reference is written (commit v0, vendored k8s.io/kubernetes v1.13.2):
+ * per-(task,node) recomputation exactly as the reference does it — the k8s
+ * NodeInfo is rebuilt from node.Pods() on every predicate/priority call, the
+ * pod-affinity predicate lists and copies every allocated pod in the session,
+ * and inter-pod-affinity priority is recomputed over ALL nodes for every
+ * (task, node) pair.  Cost O(T*N*(N+P)): use it on small snapshots only.
+ *
+ * Map iteration (Go-randomised in the reference) is pinned to ascending index
+ * in the KBS1 arrays: nodes by name, jobs by UID, pods
+ * by UID.  Equal-score nodes therefore resolve to the lowest node index.
+ *
+ * Parity pinning: this restatement is checked against the reference's own
+ * known-answer tests (allocate_test.go:141-310, node_info_test.go,
+ * pod_info_test.go, gang_test.go; see tests/test_golden.py).  The vendored k8s
+ * predicate/priority arithmetic has no tests in the reference tree (pruned,
+ * Gopkg.toml:76-78), so those parts are pinned by source text only.
+ *
+ * Scope limits (inputs the encoder/oracle reject, documented in DESIGN.md):
+ * pods bound to nodes that are not in the snapshot (the reference's
+ * predicates plugin would dereference a nil node, predicates.go:124-125).
+ */
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../include/kbsnap.h"
+
+namespace ref {
+
+using std::map;
+using std::string;
+using std::vector;
+
+/* ------------------------------------------------------------------------ */
+/* k8s object model subset                                                   */
+/* ------------------------------------------------------------------------ */
+enum Op { OpIn = 0, OpNotIn = 1, OpExists = 2, OpDoesNotExist = 3, OpGt = 4, OpLt = 5, OpEquals = 6,
+          OpInvalid = 15 };
+
+struct Requirement {  // labels.Requirement (apimachinery/pkg/labels/selector.go)
+    string key;
+    int op;
+    vector<string> values;
+};
+
+struct LabelSelector {  // metav1.LabelSelector
+    map<string, string> ml;
+    vector<Requirement> me;
+};
+
+struct NodeSelectorTerm {
+    vector<Requirement> expr, fields;
+};
+
+struct PodAffinityTerm {
+    std::shared_ptr<LabelSelector> sel;  // nil-able
+    vector<string> namespaces;
+    string topologyKey;
+};
+
+struct WeightedPodAffinityTerm {
+    int32_t weight;
+    PodAffinityTerm term;
+};
+
+struct Affinity {
+    bool hasNA = false, hasNAReq = false, hasPA = false, hasPAA = false;
+    vector<NodeSelectorTerm> naReq;
+    vector<std::pair<int32_t, NodeSelectorTerm>> naPref;
+    vector<PodAffinityTerm> paReq, paaReq;
+    vector<WeightedPodAffinityTerm> paPref, paaPref;
+};
+
+struct ContainerPort {
+    string ip, proto;
+    int32_t port;
+};
+
+struct Container {
+    int64_t cpu = 0, mem = 0, gpu = 0;
+    int has = 0;  // KBS_HAS_* : key present in Requests
+    vector<ContainerPort> ports;
+};
+
+struct Toleration {
+    string key, op, value, effect;
+};
+
+struct Taint {
+    string key, value, effect;
+};
+
+struct Pod {
+    int index = 0;
+    string uid, name, ns;
+    map<string, string> labels;
+    string nodeName;  // Spec.NodeName
+    int phase = KBS_PENDING;
+    bool deleting = false;
+    int32_t priority = 0;
+    int64_t ts = 0;
+    bool backfill = false;
+    vector<Container> containers, initContainers;
+    map<string, string> nodeSelector;
+    vector<Toleration> tolerations;
+    std::shared_ptr<Affinity> affinity;
+    int job = -1;  // snapshot job row
+};
+
+struct KNode {  // v1.Node
+    int index = 0;
+    string name;
+    map<string, string> labels;
+    vector<Taint> taints;
+    bool unschedulable = false;
+    int64_t a_cpu, a_mem, a_gpu, a_pods, c_cpu, c_mem, c_gpu, c_pods;
+};
+
+/* ------------------------------------------------------------------------ */
+/* kube-batch api (pkg/scheduler/api)                                        */
+/* ------------------------------------------------------------------------ */
+static const double minMilliCPU = 10, minMilliGPU = 10, minMemory = 10 * 1024 * 1024;  // resource_info.go:54-56
+
+struct Resource {  // resource_info.go:26-33
+    double MilliCPU = 0, Memory = 0, MilliGPU = 0;
+    int MaxTaskNum = 0;
+    Resource& Add(const Resource& r) { MilliCPU += r.MilliCPU; Memory += r.Memory; MilliGPU += r.MilliGPU; return *this; }
+    Resource& Sub(const Resource& r) { MilliCPU -= r.MilliCPU; Memory -= r.Memory; MilliGPU -= r.MilliGPU; return *this; }
+    Resource& Multi(double ratio) { MilliCPU *= ratio; Memory *= ratio; MilliGPU *= ratio; return *this; }
+    bool IsEmpty() const { return MilliCPU < minMilliCPU && Memory < minMemory && MilliGPU < minMilliGPU; }  // :75-77
+    bool LessEqual(const Resource& rr) const {  // :164-168
+        return (MilliCPU < rr.MilliCPU || std::fabs(rr.MilliCPU - MilliCPU) < minMilliCPU) &&
+               (Memory < rr.Memory || std::fabs(rr.Memory - Memory) < minMemory) &&
+               (MilliGPU < rr.MilliGPU || std::fabs(rr.MilliGPU - MilliGPU) < minMilliGPU);
+    }
+    void SetMaxResource(const Resource& rr) {  // :114-128
+        if (rr.MilliCPU > MilliCPU) MilliCPU = rr.MilliCPU;
+        if (rr.Memory > Memory) Memory = rr.Memory;
+        if (rr.MilliGPU > MilliGPU) MilliGPU = rr.MilliGPU;
+    }
+    double Get(int rn) const { return rn == 0 ? MilliCPU : rn == 1 ? Memory : MilliGPU; }
+};
+
+static Resource MinRes(const Resource& l, const Resource& r) {  // api/helpers/helpers.go:25-33
+    Resource res;
+    res.MilliCPU = std::fmin(l.MilliCPU, r.MilliCPU);
+    res.MilliGPU = std::fmin(l.MilliGPU, r.MilliGPU);
+    res.Memory = std::fmin(l.Memory, r.Memory);
+    return res;
+}
+
+static double Share(double l, double r) {  // helpers.go:35-48
+    if (r == 0) return l == 0 ? 0 : 1;
+    return l / r;
+}
+
+enum TaskStatus {  // types.go:22-61
+    Pending = 1 << 0, AllocatedOverBackfill = 1 << 1, Allocated = 1 << 2, Pipelined = 1 << 3,
+    Binding = 1 << 4, Bound = 1 << 5, Running = 1 << 6, Releasing = 1 << 7, Succeeded = 1 << 8,
+    Failed = 1 << 9, Unknown = 1 << 10
+};
+static const int AllocatedStatusesList[] = {Bound, Binding, Running, Allocated};  // types.go:82-84
+static bool AllocatedStatus(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
+
+enum JobReadiness { Ready = 1, AlmostReady = 2, NotReady = 4 };
+
+static int getTaskStatus(const Pod& p) {  // helpers.go:35-61
+    switch (p.phase) {
+        case KBS_RUNNING: return p.deleting ? Releasing : Running;
+        case KBS_PENDING:
+            if (p.deleting) return Releasing;
+            if (p.nodeName.empty()) return Pending;
+            return Bound;
+        case KBS_UNKNOWN: return Unknown;
+        case KBS_SUCCEEDED: return Succeeded;
+        case KBS_FAILED: return Failed;
+    }
+    return Unknown;
+}
+
+static Resource ContainerRes(const Container& c) {  // NewResource(container.Resources.Requests)
+    Resource r;
+    r.MilliCPU = (double)c.cpu;
+    r.Memory = (double)c.mem;
+    r.MilliGPU = (double)c.gpu;
+    return r;
+}
+
+static Resource GetPodResourceWithoutInitContainers(const Pod& p) {  // pod_info.go:64-71
+    Resource r;
+    for (auto& c : p.containers) r.Add(ContainerRes(c));
+    return r;
+}
+static Resource GetPodResourceRequest(const Pod& p) {  // pod_info.go:51-60
+    Resource r = GetPodResourceWithoutInitContainers(p);
+    for (auto& c : p.initContainers) r.SetMaxResource(ContainerRes(c));
+    return r;
+}
+
+struct TaskInfo {  // job_info.go:36-58
+    int pod = -1;  // index of pod (also the pinned map-iteration key)
+    string uid;
+    int job = -1;  // session job slot (-1 = not in a session job)
+    string jobUID;
+    string name, ns;
+    Resource Resreq, InitResreq;
+    string NodeName;
+    int Status = Pending;
+    int32_t Priority = 1;
+    Pod* P = nullptr;
+    bool IsBackfill = false;
+};
+
+struct NodeInfo {  // node_info.go:27-45
+    string Name;
+    KNode* Node = nullptr;
+    Resource Releasing, Idle, Used, Backfilled, Allocatable, Capability;
+    map<int, TaskInfo> Tasks;  // keyed by pod index: pinned map order
+
+    void init(KNode* n) {  // NewNodeInfo(node) :62-75
+        Name = n->name;
+        Node = n;
+        Idle.MilliCPU = (double)n->a_cpu; Idle.Memory = (double)n->a_mem; Idle.MilliGPU = (double)n->a_gpu;
+        Idle.MaxTaskNum = (int)n->a_pods;
+        Allocatable = Idle;
+        Capability.MilliCPU = (double)n->c_cpu; Capability.Memory = (double)n->c_mem;
+        Capability.MilliGPU = (double)n->c_gpu; Capability.MaxTaskNum = (int)n->c_pods;
+    }
+    bool AddTask(const TaskInfo& task) {  // :113-145
+        if (Tasks.count(task.pod)) return false;
+        TaskInfo ti = task;  // task.Clone()
+        if (Node) {
+            if (task.IsBackfill) Backfilled.Add(task.Resreq);
+            switch (ti.Status) {
+                case ::ref::Releasing: Releasing.Add(ti.Resreq); Idle.Sub(ti.Resreq); break;
+                case ::ref::Pipelined: Releasing.Sub(ti.Resreq); break;
+                default: Idle.Sub(ti.Resreq);
+            }
+            Used.Add(ti.Resreq);
+        }
+        Tasks[task.pod] = ti;
+        return true;
+    }
+    vector<Pod*> Pods() const {  // :201-207
+        vector<Pod*> v;
+        for (auto& kv : Tasks) v.push_back(kv.second.P);
+        return v;
+    }
+    Resource GetAccessibleResource() {  // :209-211 — mutates Idle (Appendix A.1)
+        Idle.Add(Backfilled);
+        return Idle;
+    }
+};
+
+struct JobInfo {  // job_info.go:140-167
+    string UID, Name, Namespace, Queue;
+    int32_t Priority = 0;
+    int32_t MinAvailable = 0;
+    map<int, map<int, TaskInfo*>> TaskStatusIndex;  // status -> pod index -> task
+    map<int, TaskInfo*> Tasks;
+    Resource Allocated, TotalRequest;
+    int64_t CreationTimestamp = 0;
+    map<string, Resource> NodesFitDelta;
+    int slot = 0;
+
+    void addTaskIndex(TaskInfo* ti) { TaskStatusIndex[ti->Status][ti->pod] = ti; }
+    void AddTaskInfo(TaskInfo* ti) {  // :239-249
+        Tasks[ti->pod] = ti;
+        addTaskIndex(ti);
+        Priority = ti->P->priority;
+        TotalRequest.Add(ti->Resreq);
+        if (AllocatedStatus(ti->Status)) Allocated.Add(ti->Resreq);
+    }
+    void deleteTaskIndex(TaskInfo* ti) {
+        auto it = TaskStatusIndex.find(ti->Status);
+        if (it != TaskStatusIndex.end()) {
+            it->second.erase(ti->pod);
+            if (it->second.empty()) TaskStatusIndex.erase(it);
+        }
+    }
+    void DeleteTaskInfo(TaskInfo* ti) {  // :276-292
+        auto it = Tasks.find(ti->pod);
+        if (it == Tasks.end()) return;
+        TaskInfo* task = it->second;
+        TotalRequest.Sub(task->Resreq);
+        if (AllocatedStatus(task->Status)) Allocated.Sub(task->Resreq);
+        Tasks.erase(it);
+        deleteTaskIndex(task);
+    }
+    void UpdateTaskStatus(TaskInfo* task, int status) {  // :251-264
+        DeleteTaskInfo(task);
+        task->Status = status;
+        AddTaskInfo(task);
+    }
+    int count(int status) const {
+        auto it = TaskStatusIndex.find(status);
+        return it == TaskStatusIndex.end() ? 0 : (int)it->second.size();
+    }
+    int GetReadiness() const {  // :374-388
+        int allocated = 0;
+        for (int s : AllocatedStatusesList) allocated += count(s);
+        if (allocated >= MinAvailable) return Ready;
+        if (allocated + count(AllocatedOverBackfill) >= MinAvailable) return AlmostReady;
+        return NotReady;
+    }
+};
+
+struct QueueInfo {
+    string UID, Name;
+    int32_t Weight = 1;
+    int64_t ts = 0;
+    int slot = 0;
+};
+
+/* ------------------------------------------------------------------------ */
+/* Go container/heap + util.PriorityQueue (util/priority_queue.go)           */
+/* ------------------------------------------------------------------------ */
+template <typename T>
+struct PriorityQueue {
+    vector<T*> items;
+    std::function<bool(T*, T*)> lessFn;
+    bool Less(int i, int j) { return lessFn(items[i], items[j]); }
+    void Swap(int i, int j) { std::swap(items[i], items[j]); }
+    void up(int j) {
+        for (;;) {
+            int i = (j - 1) / 2;  // parent
+            if (i == j || !Less(j, i)) break;
+            Swap(i, j);
+            j = i;
+        }
+    }
+    bool down(int i0, int n) {
+        int i = i0;
+        for (;;) {
+            int j1 = 2 * i + 1;
+            if (j1 >= n || j1 < 0) break;
+            int j = j1;
+            int j2 = j1 + 1;
+            if (j2 < n && Less(j2, j1)) j = j2;
+            if (!Less(j, i)) break;
+            Swap(i, j);
+            i = j;
+        }
+        return i > i0;
+    }
+    void Push(T* x) {
+        items.push_back(x);
+        up((int)items.size() - 1);
+    }
+    T* Pop() {
+        if (items.empty()) return nullptr;
+        int n = (int)items.size() - 1;
+        Swap(0, n);
+        down(0, n);
+        T* it = items.back();
+        items.pop_back();
+        return it;
+    }
+    bool Empty() const { return items.empty(); }
+    int Len() const { return (int)items.size(); }
+};
+
+/* ------------------------------------------------------------------------ */
+/* labels / selectors (apimachinery/pkg/labels/selector.go)                  */
+/* ------------------------------------------------------------------------ */
+static bool parseInt64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+    if (s.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') {
+        neg = s[0] == '-';
+        i = 1;
+        if (s.size() == 1) return false;
+    }
+    unsigned long long v = 0;
+    const unsigned long long lim = neg ? 9223372036854775808ULL : 9223372036854775807ULL;
+    for (; i < s.size(); ++i) {
+        char ch = s[i];
+        if (ch < '0' || ch > '9') return false;
+        unsigned d = (unsigned)(ch - '0');
+        if (v > (lim - d) / 10) return false;
+        v = v * 10 + d;
+    }
+    *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+    return true;
+}
+
+typedef map<string, string> Labels;
+
+static bool hasValue(const Requirement& r, const string& v) {
+    for (auto& s : r.values) if (s == v) return true;
+    return false;
+}
+
+static bool RequirementMatches(const Requirement& r, const Labels& ls) {  // selector.go:192-236
+    auto it = ls.find(r.key);
+    bool has = it != ls.end();
+    switch (r.op) {
+        case OpIn:
+        case OpEquals:
+            if (!has) return false;
+            return hasValue(r, it->second);
+        case OpNotIn:
+            if (!has) return true;
+            return !hasValue(r, it->second);
+        case OpExists: return has;
+        case OpDoesNotExist: return !has;
+        case OpGt:
+        case OpLt: {
+            if (!has) return false;
+            int64_t lv, rv = 0;
+            if (!parseInt64(it->second, &lv)) return false;
+            if (r.values.size() != 1) return false;
+            for (auto& s : r.values) if (!parseInt64(s, &rv)) return false;
+            return (r.op == OpGt && lv > rv) || (r.op == OpLt && lv < rv);
+        }
+    }
+    return false;
+}
+
+/* labels.NewRequirement validation (selector.go:134-170), without the
+ * key/value syntax checks (documented limitation). */
+static bool ValidRequirement(const Requirement& r) {
+    switch (r.op) {
+        case OpIn:
+        case OpNotIn: return !r.values.empty();
+        case OpEquals: return r.values.size() == 1;
+        case OpExists:
+        case OpDoesNotExist: return r.values.empty();
+        case OpGt:
+        case OpLt: {
+            if (r.values.size() != 1) return false;
+            int64_t v;
+            return parseInt64(r.values[0], &v);
+        }
+    }
+    return false;
+}
+
+/* A compiled selector: kind 0 = internal (AND of reqs), 1 = Nothing. */
+struct Selector {
+    bool nothing = false;
+    vector<Requirement> reqs;
+    bool Matches(const Labels& ls) const {
+        if (nothing) return false;
+        for (auto& r : reqs) if (!RequirementMatches(r, ls)) return false;
+        return true;
+    }
+};
+
+/* metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:31-67) */
+static bool LabelSelectorAsSelector(const LabelSelector* ps, Selector* out) {
+    *out = Selector();
+    if (!ps) { out->nothing = true; return true; }
+    if (ps->ml.size() + ps->me.size() == 0) return true;  // Everything
+    for (auto& kv : ps->ml) {
+        Requirement r{kv.first, OpEquals, {kv.second}};
+        if (!ValidRequirement(r)) return false;
+        out->reqs.push_back(r);
+    }
+    for (auto& e : ps->me) {
+        if (e.op != OpIn && e.op != OpNotIn && e.op != OpExists && e.op != OpDoesNotExist) return false;
+        if (!ValidRequirement(e)) return false;
+        out->reqs.push_back(e);
+    }
+    // internalSelector.Add sorts by key; irrelevant for Matches (AND).
+    return true;
+}
+
+/* v1helper.NodeSelectorRequirementsAsSelector (helper/helpers.go:222-252) */
+static bool NodeSelectorRequirementsAsSelector(const vector<Requirement>& nsm, Selector* out) {
+    *out = Selector();
+    if (nsm.empty()) { out->nothing = true; return true; }
+    for (auto& e : nsm) {
+        if (e.op > OpLt) return false;
+        if (!ValidRequirement(e)) return false;
+        out->reqs.push_back(e);
+    }
+    return true;
+}
+
+/* NodeSelectorRequirementsAsFieldSelector (helper/helpers.go:255-283) + Matches
+ * against fields.Set{metadata.name: node.Name} (algorithm/types.go:30-32). */
+static bool FieldSelectorMatches(const vector<Requirement>& nsm, const string& nodeName, bool* err) {
+    *err = false;
+    if (nsm.empty()) return false;  // fields.Nothing()
+    for (auto& e : nsm) {
+        if ((e.op != OpIn && e.op != OpNotIn) || e.values.size() != 1) { *err = true; return false; }
+    }
+    for (auto& e : nsm) {
+        string fv = e.key == "metadata.name" ? nodeName : string();
+        bool eq = fv == e.values[0];
+        if (e.op == OpIn && !eq) return false;
+        if (e.op == OpNotIn && eq) return false;
+    }
+    return true;
+}
+
+/* v1helper.MatchNodeSelectorTerms (helper/helpers.go:302-333) */
+static bool MatchNodeSelectorTerms(const vector<NodeSelectorTerm>& terms, const KNode& node) {
+    for (auto& req : terms) {
+        if (req.expr.empty() && req.fields.empty()) continue;
+        if (!req.expr.empty()) {
+            Selector sel;
+            if (!NodeSelectorRequirementsAsSelector(req.expr, &sel) || !sel.Matches(node.labels)) continue;
+        }
+        if (!req.fields.empty()) {
+            bool err;
+            if (!FieldSelectorMatches(req.fields, node.name, &err) || err) continue;
+        }
+        return true;
+    }
+    return false;
+}
+
+/* predicates.podMatchesNodeSelectorAndAffinityTerms (predicates.go:807-850) */
+static bool podMatchesNodeSelectorAndAffinityTerms(const Pod& pod, const KNode& node) {
+    if (!pod.nodeSelector.empty()) {
+        // labels.SelectorFromSet (selector.go:849-862): Equals requirements
+        for (auto& kv : pod.nodeSelector) {
+            auto it = node.labels.find(kv.first);
+            if (it == node.labels.end() || it->second != kv.second) return false;
+        }
+    }
+    bool nodeAffinityMatches = true;
+    if (pod.affinity && pod.affinity->hasNA) {
+        if (!pod.affinity->hasNAReq) return true;
+        nodeAffinityMatches = nodeAffinityMatches && MatchNodeSelectorTerms(pod.affinity->naReq, node);
+    }
+    return nodeAffinityMatches;
+}
+
+/* Toleration.ToleratesTaint (vendor/k8s.io/api/core/v1/toleration.go:37-56) */
+static bool ToleratesTaint(const Toleration& t, const Taint& taint) {
+    if (!t.effect.empty() && t.effect != taint.effect) return false;
+    if (!t.key.empty() && t.key != taint.key) return false;
+    if (t.op.empty() || t.op == "Equal") return t.value == taint.value;
+    if (t.op == "Exists") return true;
+    return false;
+}
+
+/* ------------------------------------------------------------------------ */
+/* vendored k8s scheduler cache NodeInfo (pkg/scheduler/cache/node_info.go)  */
+/* ------------------------------------------------------------------------ */
+struct PP {
+    string proto;
+    int32_t port;
+    bool operator<(const PP& o) const { return proto != o.proto ? proto < o.proto : port < o.port; }
+};
+typedef map<string, std::set<PP>> HostPortInfo;  // host_ports.go:50-51
+
+static void sanitize(string* ip, string* proto) {
+    if (ip->empty()) *ip = "0.0.0.0";
+    if (proto->empty()) *proto = "TCP";
+}
+static void HPAdd(HostPortInfo& h, string ip, string proto, int32_t port) {  // :53-72
+    if (port <= 0) return;
+    sanitize(&ip, &proto);
+    h[ip].insert(PP{proto, port});
+}
+static bool HPCheckConflict(const HostPortInfo& h, string ip, string proto, int32_t port) {  // :96-125
+    if (port <= 0) return false;
+    sanitize(&ip, &proto);
+    PP pp{proto, port};
+    if (ip == "0.0.0.0") {
+        for (auto& kv : h) if (kv.second.count(pp)) return true;
+        return false;
+    }
+    for (const string& key : {string("0.0.0.0"), ip}) {
+        auto it = h.find(key);
+        if (it != h.end() && it->second.count(pp)) return true;
+    }
+    return false;
+}
+
+static void GetNonzeroRequests(const Container& c, int64_t* cpu, int64_t* mem) {  // util/non_zero.go:37-52
+    *cpu = (c.has & KBS_HAS_CPU) ? c.cpu : 100;
+    *mem = (c.has & KBS_HAS_MEM) ? c.mem : 200LL * 1024 * 1024;
+}
+
+struct K8sNodeInfo {
+    KNode* node = nullptr;
+    vector<Pod*> pods, podsWithAffinity;
+    int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
+    HostPortInfo usedPorts;
+    int64_t alloc_cpu = 0, alloc_mem = 0;
+
+    static bool hasPodAffinityConstraints(const Pod* p) {
+        return p->affinity && (p->affinity->hasPA || p->affinity->hasPAA);
+    }
+    void AddPod(Pod* p) {  // :498-521
+        for (auto& c : p->containers) {
+            req_cpu += c.cpu;
+            req_mem += c.mem;
+            int64_t a, b;
+            GetNonzeroRequests(c, &a, &b);
+            nz_cpu += a;
+            nz_mem += b;
+        }
+        pods.push_back(p);
+        if (hasPodAffinityConstraints(p)) podsWithAffinity.push_back(p);
+        for (auto& c : p->containers)
+            for (auto& pt : c.ports) HPAdd(usedPorts, pt.ip, pt.proto, pt.port);
+    }
+    void SetNode(KNode* n) {  // :608-631
+        node = n;
+        alloc_cpu = n->a_cpu;
+        alloc_mem = n->a_mem;
+    }
+    bool Filter(const Pod* p) const {  // :692-702
+        if (p->nodeName != node->name) return true;
+        for (auto* q : pods) if (q->name == p->name && q->ns == p->ns) return true;
+        return false;
+    }
+};
+
+static K8sNodeInfo BuildK8sNodeInfo(const NodeInfo& ni) {  // cache.NewNodeInfo(node.Pods()...) + SetNode
+    K8sNodeInfo k;
+    for (auto* p : ni.Pods()) k.AddPod(p);
+    k.SetNode(ni.Node);
+    return k;
+}
+
+/* ------------------------------------------------------------------------ */
+/* framework.Session + plugins                                               */
+/* ------------------------------------------------------------------------ */
+struct PluginOption {
+    string name;
+    int flags = 0;
+    map<string, string> args;
+};
+typedef vector<vector<PluginOption>> Tiers;
+
+struct Session;
+typedef std::function<int(void*, void*)> CompareFn;
+typedef std::function<bool(TaskInfo*, NodeInfo*, string*)> PredicateFn;  // returns ok
+typedef std::function<bool(TaskInfo*, NodeInfo*, int*)> NodeOrderFn;      // returns ok
+typedef std::function<int(JobInfo*)> JobReadyFn;
+typedef std::function<bool(QueueInfo*)> OverusedFn;
+
+struct EventHandler {
+    std::function<void(TaskInfo*)> AllocateFunc;
+};
+
+struct Session {
+    vector<JobInfo*> Jobs;          // pinned order (by job UID)
+    map<string, JobInfo*> JobByUID;
+    vector<NodeInfo*> Nodes;        // pinned order (by node name)
+    map<string, NodeInfo*> NodeByName;
+    vector<QueueInfo*> Queues;      // pinned order (by queue name)
+    map<string, QueueInfo*> QueueByUID;
+    Tiers tiers;
+    map<string, CompareFn> jobOrderFns, queueOrderFns, taskOrderFns;
+    map<string, PredicateFn> predicateFns;
+    map<string, NodeOrderFn> nodeOrderFns;
+    map<string, JobReadyFn> jobReadyFns;
+    map<string, OverusedFn> overusedFns;
+    vector<EventHandler> eventHandlers;
+    // observer: placement log
+    vector<std::tuple<int, int, int>> log;  // (pod, node index, status)
+    map<string, int> nodeIndex;
+
+    bool JobOrderFn(JobInfo* l, JobInfo* r) {  // session_plugins.go:244-268
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_JOBORDER) continue;
+                auto it = jobOrderFns.find(p.name);
+                if (it == jobOrderFns.end()) continue;
+                int j = it->second(l, r);
+                if (j != 0) return j < 0;
+            }
+        if (l->CreationTimestamp == r->CreationTimestamp) return l->UID < r->UID;
+        return l->CreationTimestamp < r->CreationTimestamp;
+    }
+    bool QueueOrderFn(QueueInfo* l, QueueInfo* r) {  // :270-295
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_QUEUEORDER) continue;
+                auto it = queueOrderFns.find(p.name);
+                if (it == queueOrderFns.end()) continue;
+                int j = it->second(l, r);
+                if (j != 0) return j < 0;
+            }
+        if (l->ts == r->ts) return l->UID < r->UID;
+        return l->ts < r->ts;
+    }
+    bool TaskOrderFn(TaskInfo* l, TaskInfo* r) {  // :297-329
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_TASKORDER) continue;
+                auto it = taskOrderFns.find(p.name);
+                if (it == taskOrderFns.end()) continue;
+                int j = it->second(l, r);
+                if (j != 0) return j < 0;
+            }
+        if (l->P->ts == r->P->ts) return l->uid < r->uid;
+        return l->P->ts < r->P->ts;
+    }
+    bool PredicateFn_(TaskInfo* t, NodeInfo* n) {  // :331-348
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_PREDICATE) continue;
+                auto it = predicateFns.find(p.name);
+                if (it == predicateFns.end()) continue;
+                string err;
+                if (!it->second(t, n, &err)) return false;
+            }
+        return true;
+    }
+    bool NodeOrderFn_(TaskInfo* t, NodeInfo* n, int* score) {  // :350-370
+        int priorityScore = 0;
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_NODEORDER) continue;
+                auto it = nodeOrderFns.find(p.name);
+                if (it == nodeOrderFns.end()) continue;
+                int s = 0;
+                if (!it->second(t, n, &s)) { *score = 0; return false; }
+                priorityScore += s;
+            }
+        *score = priorityScore;
+        return true;
+    }
+    bool JobReady(JobInfo* job) {  // :167-186 — `break` leaves the plugin loop only,
+        int status = Ready;          // so the last tier with an enabled JobReadyFn decides
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_JOBREADY) continue;
+                auto it = jobReadyFns.find(p.name);
+                if (it == jobReadyFns.end()) continue;
+                status = it->second(job);
+                break;
+            }
+        return status == Ready;
+    }
+    bool Overused(QueueInfo* q) {  // :150-164
+        for (auto& tier : tiers)
+            for (auto& p : tier) {
+                auto it = overusedFns.find(p.name);
+                if (it == overusedFns.end()) continue;
+                if (it->second(q)) return true;
+            }
+        return false;
+    }
+
+    void Pipeline(TaskInfo* task, NodeInfo* node) {  // session.go:199-235
+        auto jit = JobByUID.find(task->jobUID);
+        if (jit != JobByUID.end()) jit->second->UpdateTaskStatus(task, Pipelined);
+        task->NodeName = node->Name;
+        node->AddTask(*task);
+        for (auto& eh : eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(task);
+        log.emplace_back(task->pod, nodeIndex[node->Name], Pipelined);
+    }
+    bool Allocate(TaskInfo* task, NodeInfo* node, bool usingBackfillTaskRes) {  // :237-297
+        auto jit = JobByUID.find(task->jobUID);
+        if (jit == JobByUID.end()) return false;
+        JobInfo* job = jit->second;
+        job->UpdateTaskStatus(task, usingBackfillTaskRes ? AllocatedOverBackfill : Allocated);
+        task->NodeName = node->Name;
+        if (!node->AddTask(*task)) return false;
+        for (auto& eh : eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(task);
+        log.emplace_back(task->pod, nodeIndex[node->Name], task->Status);
+        if (JobReady(job)) {
+            // dispatch every Allocated task (session.go:299-321): status -> Binding
+            auto it = job->TaskStatusIndex.find(Allocated);
+            if (it != job->TaskStatusIndex.end()) {
+                vector<TaskInfo*> ts;
+                for (auto& kv : it->second) ts.push_back(kv.second);
+                for (auto* t : ts) job->UpdateTaskStatus(t, Binding);
+            }
+        }
+        return true;
+    }
+};
+
+/* ---- priority plugin (plugins/priority/priority.go:38-79) ---------------- */
+static void priorityOpen(Session& ssn, const PluginOption&) {
+    ssn.taskOrderFns["priority"] = [](void* l, void* r) {
+        auto* lv = (TaskInfo*)l;
+        auto* rv = (TaskInfo*)r;
+        if (lv->Priority == rv->Priority) return 0;
+        if (lv->Priority > rv->Priority) return -1;
+        return 1;
+    };
+    ssn.jobOrderFns["priority"] = [](void* l, void* r) {
+        auto* lv = (JobInfo*)l;
+        auto* rv = (JobInfo*)r;
+        if (lv->Priority > rv->Priority) return -1;
+        if (lv->Priority < rv->Priority) return 1;
+        return 0;
+    };
+}
+
+/* ---- gang plugin (plugins/gang/gang.go:82-164) --------------------------- */
+static void gangOpen(Session& ssn, const PluginOption&) {
+    ssn.jobOrderFns["gang"] = [](void* l, void* r) {
+        bool lReady = ((JobInfo*)l)->GetReadiness() == Ready;
+        bool rReady = ((JobInfo*)r)->GetReadiness() == Ready;
+        if (lReady && rReady) return 0;
+        if (lReady) return 1;
+        if (rReady) return -1;
+        return 0;
+    };
+    ssn.jobReadyFns["gang"] = [](JobInfo* j) { return j->GetReadiness(); };
+}
+
+/* ---- drf plugin (plugins/drf/drf.go:59-170) ------------------------------ */
+struct DrfState {
+    Resource total;
+    map<string, Resource> allocated;
+    map<string, double> share;
+};
+static double drfShare(const Resource& alloc, const Resource& total) {  // :160-170
+    double res = 0;
+    for (int rn = 0; rn < 3; ++rn) {
+        double s = Share(alloc.Get(rn), total.Get(rn));
+        if (s > res) res = s;
+    }
+    return res;
+}
+static void drfOpen(Session& ssn, const PluginOption&, std::shared_ptr<DrfState> st) {
+    for (auto* n : ssn.Nodes) st->total.Add(n->Allocatable);
+    for (auto* job : ssn.Jobs) {
+        Resource a;
+        for (auto& kv : job->TaskStatusIndex)
+            if (AllocatedStatus(kv.first))
+                for (auto& t : kv.second) a.Add(t.second->Resreq);
+        st->allocated[job->UID] = a;
+        st->share[job->UID] = drfShare(a, st->total);
+    }
+    ssn.jobOrderFns["drf"] = [st](void* l, void* r) {
+        double ls = st->share[((JobInfo*)l)->UID], rs = st->share[((JobInfo*)r)->UID];
+        if (ls == rs) return 0;
+        if (ls < rs) return -1;
+        return 1;
+    };
+    EventHandler eh;
+    eh.AllocateFunc = [st](TaskInfo* t) {
+        Resource& a = st->allocated[t->jobUID];
+        a.Add(t->Resreq);
+        st->share[t->jobUID] = drfShare(a, st->total);
+    };
+    ssn.eventHandlers.push_back(eh);
+}
+
+/* ---- proportion plugin (plugins/proportion/proportion.go:57-241) --------- */
+struct QueueAttr {
+    string queueID, name;
+    int32_t weight = 0;
+    double share = 0;
+    Resource deserved, allocated, request;
+};
+struct PropState {
+    Resource total;
+    map<string, QueueAttr> opts;
+    vector<string> order;  // pinned iteration order of queueOpts (by queue index)
+};
+static void propUpdateShare(QueueAttr& a) {  // :229-241
+    double res = 0;
+    for (int rn = 0; rn < 3; ++rn) {
+        double s = Share(a.allocated.Get(rn), a.deserved.Get(rn));
+        if (s > res) res = s;
+    }
+    a.share = res;
+}
+static void propOpen(Session& ssn, const PluginOption&, std::shared_ptr<PropState> st) {
+    for (auto* n : ssn.Nodes) st->total.Add(n->Allocatable);
+    for (auto* job : ssn.Jobs) {
+        if (!st->opts.count(job->Queue)) {
+            QueueInfo* q = ssn.QueueByUID[job->Queue];
+            QueueAttr a;
+            a.queueID = q->UID;
+            a.name = q->Name;
+            a.weight = q->Weight;
+            st->opts[job->Queue] = a;
+        }
+        QueueAttr& a = st->opts[job->Queue];
+        for (auto& kv : job->TaskStatusIndex) {
+            if (AllocatedStatus(kv.first)) {
+                for (auto& t : kv.second) { a.allocated.Add(t.second->Resreq); a.request.Add(t.second->Resreq); }
+            } else if (kv.first == Pending) {
+                for (auto& t : kv.second) a.request.Add(t.second->Resreq);
+            }
+        }
+    }
+    for (auto* q : ssn.Queues) if (st->opts.count(q->UID)) st->order.push_back(q->UID);
+    Resource remaining = st->total;
+    std::set<string> meet;
+    for (;;) {
+        int32_t totalWeight = 0;
+        for (auto& id : st->order) if (!meet.count(id)) totalWeight += st->opts[id].weight;
+        if (totalWeight == 0) break;
+        Resource deserved;
+        for (auto& id : st->order) {
+            QueueAttr& a = st->opts[id];
+            if (meet.count(id)) continue;
+            Resource r = remaining;
+            a.deserved.Add(r.Multi((double)a.weight / (double)totalWeight));
+            if (!a.deserved.LessEqual(a.request)) {
+                a.deserved = MinRes(a.deserved, a.request);
+                meet.insert(id);
+            }
+            propUpdateShare(a);
+            deserved.Add(a.deserved);
+        }
+        remaining.Sub(deserved);
+        if (remaining.IsEmpty()) break;
+    }
+    ssn.queueOrderFns["proportion"] = [st](void* l, void* r) {
+        double ls = st->opts[((QueueInfo*)l)->UID].share, rs = st->opts[((QueueInfo*)r)->UID].share;
+        if (ls == rs) return 0;
+        if (ls < rs) return -1;
+        return 1;
+    };
+    ssn.overusedFns["proportion"] = [st](QueueInfo* q) {
+        QueueAttr& a = st->opts[q->UID];
+        return a.deserved.LessEqual(a.allocated);
+    };
+    Session* sp = &ssn;
+    EventHandler eh;
+    eh.AllocateFunc = [st, sp](TaskInfo* t) {
+        JobInfo* job = sp->JobByUID[t->jobUID];
+        QueueAttr& a = st->opts[job->Queue];
+        a.allocated.Add(t->Resreq);
+        propUpdateShare(a);
+    };
+    ssn.eventHandlers.push_back(eh);
+}
+
+/* ---- predicates plugin (plugins/predicates/predicates.go:114-204) -------- */
+
+// podLister.FilteredList (predicates.go:72-91): allocated-status tasks of all
+// session jobs, copied with Spec.NodeName = task.NodeName.
+struct ListedPod {
+    Pod* pod;
+    string nodeName;  // overridden Spec.NodeName
+};
+static vector<ListedPod> predFilteredList(Session& ssn, const K8sNodeInfo& ni) {
+    vector<ListedPod> out;
+    for (auto* job : ssn.Jobs)
+        for (auto& kv : job->TaskStatusIndex) {
+            if (!AllocatedStatus(kv.first)) continue;
+            for (auto& t : kv.second) {
+                TaskInfo* task = t.second;
+                if (ni.Filter(task->P)) out.push_back({task->P, task->NodeName});
+            }
+        }
+    return out;
+}
+
+// priorityutil.GetNamespacesFromPodAffinityTerm / PodMatchesTermsNamespaceAndSelector
+static std::set<string> termNamespaces(const Pod& definer, const PodAffinityTerm& t) {
+    std::set<string> s;
+    if (t.namespaces.empty()) s.insert(definer.ns);
+    else s.insert(t.namespaces.begin(), t.namespaces.end());
+    return s;
+}
+static bool podMatchesTermsNamespaceAndSelector(const Pod& pod, const std::set<string>& nss, const Selector& sel) {
+    if (!nss.count(pod.ns)) return false;
+    return sel.Matches(pod.labels);
+}
+
+// priorityutil.NodesHaveSameTopologyKey (util/topologies.go:53-75)
+static bool NodesHaveSameTopologyKey(const KNode* a, const KNode* b, const string& key) {
+    if (key.empty()) return false;
+    auto ia = a->labels.find(key), ib = b->labels.find(key);
+    if (ia != a->labels.end() && ib != b->labels.end()) return ia->second == ib->second;
+    return false;
+}
+
+struct PredErr {};
+
+// predicates cachedNodeInfo.GetNodeInfo (predicates.go:97-104): no fallback
+static KNode* predGetNode(Session& ssn, const string& name) {
+    auto it = ssn.NodeByName.find(name);
+    if (it == ssn.NodeByName.end()) throw PredErr();
+    return it->second->Node;
+}
+
+// podMatchesPodAffinityTerms (predicates.go:1189-1215): returns {match, propsMatch}; throws on error
+static std::pair<bool, bool> podMatchesPodAffinityTerms(Session& ssn, const Pod& pod, const ListedPod& target,
+                                                        const K8sNodeInfo& ni,
+                                                        const vector<PodAffinityTerm>& terms) {
+    if (terms.empty()) throw PredErr();
+    // getAffinityTermProperties + podMatchesAllAffinityTermProperties
+    for (auto& term : terms) {
+        Selector sel;
+        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) throw PredErr();
+    }
+    for (auto& term : terms) {
+        Selector sel;
+        LabelSelectorAsSelector(term.sel.get(), &sel);
+        if (!podMatchesTermsNamespaceAndSelector(*target.pod, termNamespaces(pod, term), sel))
+            return {false, false};
+    }
+    KNode* targetNode = predGetNode(ssn, target.nodeName);
+    for (auto& term : terms) {
+        if (term.topologyKey.empty()) throw PredErr();
+        if (!NodesHaveSameTopologyKey(ni.node, targetNode, term.topologyKey)) return {false, true};
+    }
+    return {true, true};
+}
+
+static bool targetPodMatchesAffinityOfPod(const Pod& pod, const Pod& target) {  // metadata.go:498-509
+    if (!pod.affinity || !pod.affinity->hasPA) return false;
+    const auto& terms = pod.affinity->paReq;
+    if (terms.empty()) return false;  // podMatchesAllAffinityTermProperties: no properties -> false
+    for (auto& term : terms) {
+        Selector sel;
+        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) return false;
+        if (!podMatchesTermsNamespaceAndSelector(target, termNamespaces(pod, term), sel)) return false;
+    }
+    return true;
+}
+
+// InterPodAffinityMatches slow path (predicates.go:1155-1184, 1293-1334, 1402-1458)
+static bool InterPodAffinityMatches(Session& ssn, const Pod& pod, const K8sNodeInfo& ni) {
+    try {
+        // satisfiesExistingPodsAntiAffinity
+        vector<ListedPod> filtered = predFilteredList(ssn, ni);
+        std::set<std::pair<string, string>> forbidden;
+        for (auto& ep : filtered) {
+            KNode* epNode = predGetNode(ssn, ep.nodeName);
+            const Pod& existing = *ep.pod;
+            if (!existing.affinity || !existing.affinity->hasPAA) continue;
+            for (auto& term : existing.affinity->paaReq) {
+                Selector sel;
+                if (!LabelSelectorAsSelector(term.sel.get(), &sel)) throw PredErr();
+                if (podMatchesTermsNamespaceAndSelector(pod, termNamespaces(existing, term), sel)) {
+                    auto it = epNode->labels.find(term.topologyKey);
+                    if (it != epNode->labels.end()) forbidden.insert({term.topologyKey, it->second});
+                }
+            }
+        }
+        for (auto& kv : ni.node->labels)
+            if (forbidden.count({kv.first, kv.second})) return false;
+
+        if (!pod.affinity || (!pod.affinity->hasPA && !pod.affinity->hasPAA)) return true;
+        // satisfiesPodsAffinityAntiAffinity, meta == nil branch
+        const vector<PodAffinityTerm> empty;
+        const auto& affinityTerms = pod.affinity->hasPA ? pod.affinity->paReq : empty;
+        const auto& antiAffinityTerms = pod.affinity->hasPAA ? pod.affinity->paaReq : empty;
+        bool matchFound = false, termsSelectorMatchFound = false;
+        for (auto& target : filtered) {
+            if (!matchFound && !affinityTerms.empty()) {
+                auto r = podMatchesPodAffinityTerms(ssn, pod, target, ni, affinityTerms);
+                if (r.second) termsSelectorMatchFound = true;
+                if (r.first) matchFound = true;
+            }
+            if (!antiAffinityTerms.empty()) {
+                try {
+                    auto r = podMatchesPodAffinityTerms(ssn, pod, target, ni, antiAffinityTerms);
+                    if (r.first) return false;
+                } catch (PredErr&) {
+                    return false;
+                }
+            }
+        }
+        if (!matchFound && !affinityTerms.empty()) {
+            if (termsSelectorMatchFound) return false;
+            if (!targetPodMatchesAffinityOfPod(pod, pod)) return false;
+        }
+        return true;
+    } catch (PredErr&) {
+        return false;
+    }
+}
+
+static void predicatesOpen(Session& ssn, const PluginOption&) {
+    Session* sp = &ssn;
+    ssn.predicateFns["predicates"] = [sp](TaskInfo* task, NodeInfo* node, string* err) {
+        K8sNodeInfo ni = BuildK8sNodeInfo(*node);
+        if (node->Allocatable.MaxTaskNum <= (int)ni.pods.size()) { *err = "maxtasks"; return false; }
+        const Pod& pod = *task->P;
+        if (!podMatchesNodeSelectorAndAffinityTerms(pod, *node->Node)) { *err = "selector"; return false; }
+        // PodFitsHostPorts (predicates.go:1031-1052)
+        for (auto& c : pod.containers)
+            for (auto& pt : c.ports)
+                if (HPCheckConflict(ni.usedPorts, pt.ip, pt.proto, pt.port)) { *err = "ports"; return false; }
+        // CheckNodeUnschedulable (predicates.go:107-112)
+        if (node->Node->unschedulable) { *err = "unschedulable"; return false; }
+        // PodToleratesNodeTaints (predicates.go:1489-1499, helper/helpers.go:425-440)
+        for (auto& taint : node->Node->taints) {
+            if (taint.effect != "NoSchedule" && taint.effect != "NoExecute") continue;
+            bool tol = false;
+            for (auto& t : pod.tolerations) if (ToleratesTaint(t, taint)) { tol = true; break; }
+            if (!tol) { *err = "taints"; return false; }
+        }
+        if (!InterPodAffinityMatches(*sp, pod, ni)) { *err = "podaffinity"; return false; }
+        return true;
+    };
+}
+
+/* ---- nodeorder plugin (plugins/nodeorder/nodeorder.go:177-319) ----------- */
+struct Weights {
+    int leastReq = 1, nodeAffinity = 1, podAffinity = 1, balanced = 1;
+};
+static bool atoi_go(const string& s, int* out) {  // strconv.Atoi
+    int64_t v;
+    if (!parseInt64(s, &v)) return false;
+    if (v < INT32_MIN || v > INT32_MAX) { /* Go int is 64-bit; keep within int */ }
+    *out = (int)v;
+    return true;
+}
+static Weights calculateWeight(const map<string, string>& args) {  // :177-249
+    Weights w;
+    auto get = [&](const char* k, int* dst) {
+        auto it = args.find(k);
+        if (it != args.end() && !it->second.empty()) {
+            int v;
+            if (atoi_go(it->second, &v)) *dst = v;
+        }
+    };
+    get("nodeaffinity.weight", &w.nodeAffinity);
+    get("podaffinity.weight", &w.podAffinity);
+    get("leastrequested.weight", &w.leastReq);
+    get("balancedresource.weight", &w.balanced);
+    return w;
+}
+
+static int64_t leastRequestedScore(int64_t requested, int64_t capacity) {  // least_requested.go:44-53
+    if (capacity == 0) return 0;
+    if (requested > capacity) return 0;
+    return ((capacity - requested) * 10) / capacity;
+}
+static double fractionOfCapacity(int64_t requested, int64_t capacity) {  // balanced_resource_allocation.go:72-77
+    if (capacity == 0) return 1;
+    return (double)requested / (double)capacity;
+}
+
+static void podNonZero(const Pod& p, int64_t* cpu, int64_t* mem) {  // resource_allocation.go:94-103
+    *cpu = 0;
+    *mem = 0;
+    for (auto& c : p.containers) {
+        int64_t a, b;
+        GetNonzeroRequests(c, &a, &b);
+        *cpu += a;
+        *mem += b;
+    }
+}
+
+// nodeorder cachedNodeInfo.GetNodeInfo with the empty-NodeName fallback (:78-93)
+static KNode* noGetNode(Session& ssn, const string& name, bool* ok) {
+    *ok = true;
+    auto it = ssn.NodeByName.find(name);
+    if (it != ssn.NodeByName.end()) return it->second->Node;
+    for (auto* n : ssn.Nodes)
+        for (auto* p : n->Pods())
+            if (p->nodeName.empty()) return n->Node;
+    *ok = false;
+    return nullptr;
+}
+
+// CalculateInterPodAffinityPriority (interpod_affinity.go:119-240); returns false on error
+static bool interPodAffinityScores(Session& ssn, const Pod& pod, map<string, int>* out) {
+    const Affinity* aff = pod.affinity.get();
+    bool hasAff = aff && aff->hasPA;
+    bool hasAnti = aff && aff->hasPAA;
+    map<string, double> counts;
+    bool err = false;
+    auto processTerm = [&](const PodAffinityTerm& term, const Pod& definer, const Pod& toCheck,
+                           const KNode* fixed, double weight) {
+        Selector sel;
+        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) { err = true; return; }
+        if (podMatchesTermsNamespaceAndSelector(toCheck, termNamespaces(definer, term), sel)) {
+            for (auto* n : ssn.Nodes)
+                if (NodesHaveSameTopologyKey(n->Node, fixed, term.topologyKey)) counts[n->Name] += weight;
+        }
+    };
+    auto processTerms = [&](const vector<WeightedPodAffinityTerm>& terms, const Pod& definer, const Pod& toCheck,
+                            const KNode* fixed, int mult) {
+        for (auto& t : terms) processTerm(t.term, definer, toCheck, fixed, (double)(t.weight * mult));
+    };
+    auto processPod = [&](const Pod& existing) {
+        bool ok;
+        KNode* epNode = noGetNode(ssn, existing.nodeName, &ok);
+        if (!ok) { err = true; return; }
+        const Affinity* ea = existing.affinity.get();
+        bool eAff = ea && ea->hasPA, eAnti = ea && ea->hasPAA;
+        if (hasAff) processTerms(aff->paPref, pod, existing, epNode, 1);
+        if (hasAnti) processTerms(aff->paaPref, pod, existing, epNode, -1);
+        if (eAff) {
+            for (auto& term : ea->paReq) processTerm(term, existing, pod, epNode, 1.0);  // hardPodAffinityWeight
+            processTerms(ea->paPref, existing, pod, epNode, 1);
+        }
+        if (eAnti) processTerms(ea->paaPref, existing, pod, epNode, -1);
+    };
+    for (auto* n : ssn.Nodes) {  // processNode over all nodes (16-way in the reference; sums are exact)
+        K8sNodeInfo ni = BuildK8sNodeInfo(*n);
+        const vector<Pod*>& pods = (hasAff || hasAnti) ? ni.pods : ni.podsWithAffinity;
+        for (auto* p : pods) processPod(*p);
+    }
+    if (err) return false;
+    double maxCount = 0, minCount = 0;
+    for (auto* n : ssn.Nodes) {
+        double c = counts[n->Name];
+        if (c > maxCount) maxCount = c;
+        if (c < minCount) minCount = c;
+    }
+    for (auto* n : ssn.Nodes) {
+        double f = 0;
+        if (maxCount - minCount > 0) f = 10.0 * ((counts[n->Name] - minCount) / (maxCount - minCount));
+        (*out)[n->Name] = (int)f;
+    }
+    return true;
+}
+
+static void nodeorderOpen(Session& ssn, const PluginOption& opt) {
+    Session* sp = &ssn;
+    map<string, string> args = opt.args;
+    ssn.nodeOrderFns["nodeorder"] = [sp, args](TaskInfo* task, NodeInfo* node, int* out) {
+        Weights weight = calculateWeight(args);
+        Session& s = *sp;
+        // generateNodeMapAndSlice(ssn.Nodes) is rebuilt inside the IPA below
+        K8sNodeInfo ni = BuildK8sNodeInfo(*node);
+        const Pod& pod = *task->P;
+        int score = 0;
+        int64_t rc, rm;
+        podNonZero(pod, &rc, &rm);
+        rc += ni.nz_cpu;
+        rm += ni.nz_mem;
+        // LeastRequestedPriorityMap
+        int64_t lr = (leastRequestedScore(rc, ni.alloc_cpu) + leastRequestedScore(rm, ni.alloc_mem)) / 2;
+        score += (int)lr * weight.leastReq;
+        // BalancedResourceAllocationMap
+        double cpuF = fractionOfCapacity(rc, ni.alloc_cpu), memF = fractionOfCapacity(rm, ni.alloc_mem);
+        int64_t bra;
+        if (cpuF >= 1 || memF >= 1) bra = 0;
+        else {
+            double diff = std::fabs(cpuF - memF);
+            volatile double t = 1 - diff;  // no contraction: Go rounds each op
+            bra = (int64_t)(t * 10.0);
+        }
+        score += (int)bra * weight.balanced;
+        // CalculateNodeAffinityPriorityMap
+        int32_t count = 0;
+        if (pod.affinity && pod.affinity->hasNA) {
+            for (auto& pt : pod.affinity->naPref) {
+                if (pt.first == 0) continue;
+                Selector sel;
+                if (!NodeSelectorRequirementsAsSelector(pt.second.expr, &sel)) { *out = 0; return false; }
+                if (sel.Matches(node->Node->labels)) count += pt.first;
+            }
+        }
+        score += (int)count * weight.nodeAffinity;
+        // CalculateInterPodAffinityPriority over all nodes, then lookup
+        map<string, int> ipa;
+        if (!interPodAffinityScores(s, pod, &ipa)) { *out = 0; return false; }
+        auto it = ipa.find(node->Name);
+        int hostScore = it == ipa.end() ? 0 : it->second;
+        score += hostScore * weight.podAffinity;
+        *out = score;
+        return true;
+    };
+}
+
+/* ------------------------------------------------------------------------ */
+/* Cache + Snapshot (pkg/scheduler/cache) and allocate action                */
+/* ------------------------------------------------------------------------ */
+struct World {
+    kbs::Snapshot snap;
+    vector<KNode> knodes;
+    vector<Pod> pods;
+    // session objects
+    vector<NodeInfo> nodes;
+    vector<TaskInfo> tasks;  // one per pod (snapshot-level TaskInfo)
+    vector<JobInfo> jobs;
+    vector<QueueInfo> queues;
+    Tiers tiers;
+    Session ssn;
+    std::shared_ptr<DrfState> drf;
+    std::shared_ptr<PropState> prop;
+};
+
+static Requirement readReq(const kbs::Snapshot& s, const std::vector<int32_t>& keys, const std::vector<uint8_t>& ops,
+                           const std::vector<int32_t>& voff, const std::vector<int32_t>& vals, int row) {
+    Requirement r;
+    r.key = s.s(keys[row]);
+    r.op = ops[row];
+    for (int v = voff[row]; v < voff[row + 1]; ++v) r.values.push_back(s.s(vals[v]));
+    return r;
+}
+
+static void loadWorld(World& w) {
+    const kbs::Snapshot& s = w.snap;
+    // conf
+    auto pn = s.vec<int32_t>("conf_plugin_name");
+    auto pt = s.vec<int32_t>("conf_plugin_tier");
+    auto pf = s.vec<int32_t>("conf_plugin_flags");
+    auto ap = s.vec<int32_t>("conf_arg_plugin");
+    auto ak = s.vec<int32_t>("conf_arg_key");
+    auto av = s.vec<int32_t>("conf_arg_val");
+    vector<PluginOption> opts(pn.size());
+    for (size_t i = 0; i < pn.size(); ++i) { opts[i].name = s.s(pn[i]); opts[i].flags = pf[i]; }
+    for (size_t i = 0; i < ap.size(); ++i) opts[ap[i]].args[s.s(ak[i])] = s.s(av[i]);
+    for (size_t i = 0; i < pn.size(); ++i) {
+        if ((size_t)pt[i] >= w.tiers.size()) w.tiers.resize(pt[i] + 1);
+        w.tiers[pt[i]].push_back(opts[i]);
+    }
+    // nodes
+    auto nname = s.vec<int32_t>("n_name");
+    size_t N = nname.size();
+    auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"), agpu = s.vec<int64_t>("n_alloc_gpu"),
+         apods = s.vec<int64_t>("n_alloc_pods"), ccpu = s.vec<int64_t>("n_cap_cpu"), cmem = s.vec<int64_t>("n_cap_mem"),
+         cgpu = s.vec<int64_t>("n_cap_gpu"), cpods = s.vec<int64_t>("n_cap_pods");
+    auto unsched = s.vec<uint8_t>("n_unsched");
+    auto loff = s.offs("n_label_off", N);
+    auto lk = s.vec<int32_t>("nl_key"), lv = s.vec<int32_t>("nl_val");
+    auto toff = s.offs("n_taint_off", N);
+    auto tk = s.vec<int32_t>("nt_key"), tv = s.vec<int32_t>("nt_val"), te = s.vec<int32_t>("nt_effect");
+    w.knodes.resize(N);
+    for (size_t i = 0; i < N; ++i) {
+        KNode& n = w.knodes[i];
+        n.index = (int)i;
+        n.name = s.s(nname[i]);
+        n.a_cpu = acpu[i]; n.a_mem = amem[i]; n.a_gpu = agpu[i]; n.a_pods = apods[i];
+        n.c_cpu = ccpu[i]; n.c_mem = cmem[i]; n.c_gpu = cgpu[i]; n.c_pods = cpods[i];
+        n.unschedulable = !unsched.empty() && unsched[i];
+        for (int k = loff[i]; k < loff[i + 1]; ++k) n.labels[s.s(lk[k])] = s.s(lv[k]);
+        for (int k = toff[i]; k < toff[i + 1]; ++k) n.taints.push_back({s.s(tk[k]), s.s(tv[k]), s.s(te[k])});
+    }
+    // affinity tables
+    auto a_flags = s.vec<uint8_t>("a_flags");
+    size_t A = a_flags.size();
+    auto nsr_key = s.vec<int32_t>("nsr_key");
+    auto nsr_op = s.vec<uint8_t>("nsr_op");
+    auto nsr_voff = s.offs("nsr_val_off", nsr_key.size());
+    auto nsrv = s.vec<int32_t>("nsrv");
+    auto es = s.vec<int32_t>("nst_expr_start"), ec = s.vec<int32_t>("nst_expr_cnt"),
+         fs = s.vec<int32_t>("nst_field_start"), fc = s.vec<int32_t>("nst_field_cnt");
+    auto nst = [&](int row) {
+        NodeSelectorTerm t;
+        for (int k = es[row]; k < es[row] + ec[row]; ++k) t.expr.push_back(readReq(s, nsr_key, nsr_op, nsr_voff, nsrv, k));
+        for (int k = fs[row]; k < fs[row] + fc[row]; ++k) t.fields.push_back(readReq(s, nsr_key, nsr_op, nsr_voff, nsrv, k));
+        return t;
+    };
+    auto pst_w = s.vec<int32_t>("pst_weight"), pst_t = s.vec<int32_t>("pst_term");
+    auto ls_ml = s.offs("ls_ml_off", s.rows("ls_ml_off") ? s.rows("ls_ml_off") - 1 : 0);
+    auto lkv_k = s.vec<int32_t>("lkv_key"), lkv_v = s.vec<int32_t>("lkv_val");
+    auto ls_me = s.offs("ls_me_off", s.rows("ls_me_off") ? s.rows("ls_me_off") - 1 : 0);
+    auto lsr_key = s.vec<int32_t>("lsr_key");
+    auto lsr_op = s.vec<uint8_t>("lsr_op");
+    auto lsr_voff = s.offs("lsr_val_off", lsr_key.size());
+    auto lsrv = s.vec<int32_t>("lsrv");
+    auto pat_sel = s.vec<int32_t>("pat_sel"), pat_topo = s.vec<int32_t>("pat_topo");
+    auto pat_ns = s.offs("pat_ns_off", pat_sel.size());
+    auto patns = s.vec<int32_t>("patns");
+    auto wpat_w = s.vec<int32_t>("wpat_weight"), wpat_t = s.vec<int32_t>("wpat_term");
+    auto pat = [&](int row) {
+        PodAffinityTerm t;
+        int sr = pat_sel[row];
+        if (sr >= 0) {
+            auto ls = std::make_shared<LabelSelector>();
+            for (int k = ls_ml[sr]; k < ls_ml[sr + 1]; ++k) ls->ml[s.s(lkv_k[k])] = s.s(lkv_v[k]);
+            for (int k = ls_me[sr]; k < ls_me[sr + 1]; ++k) ls->me.push_back(readReq(s, lsr_key, lsr_op, lsr_voff, lsrv, k));
+            t.sel = ls;
+        }
+        for (int k = pat_ns[row]; k < pat_ns[row + 1]; ++k) t.namespaces.push_back(s.s(patns[k]));
+        t.topologyKey = s.s(pat_topo[row]);
+        return t;
+    };
+    auto L = [&](const char* name) { return s.vec<int32_t>(name); };
+    auto nareq_s = L("a_nareq_start"), nareq_c = L("a_nareq_cnt"), napref_s = L("a_napref_start"),
+         napref_c = L("a_napref_cnt"), pareq_s = L("a_pareq_start"), pareq_c = L("a_pareq_cnt"),
+         papref_s = L("a_papref_start"), papref_c = L("a_papref_cnt"), paareq_s = L("a_paareq_start"),
+         paareq_c = L("a_paareq_cnt"), paapref_s = L("a_paapref_start"), paapref_c = L("a_paapref_cnt");
+    vector<std::shared_ptr<Affinity>> affs(A);
+    for (size_t a = 0; a < A; ++a) {
+        auto af = std::make_shared<Affinity>();
+        af->hasNA = a_flags[a] & KBS_AFF_NA;
+        af->hasNAReq = a_flags[a] & KBS_AFF_NA_REQ;
+        af->hasPA = a_flags[a] & KBS_AFF_PA;
+        af->hasPAA = a_flags[a] & KBS_AFF_PAA;
+        for (int k = nareq_s[a]; k < nareq_s[a] + nareq_c[a]; ++k) af->naReq.push_back(nst(k));
+        for (int k = napref_s[a]; k < napref_s[a] + napref_c[a]; ++k) af->naPref.push_back({pst_w[k], nst(pst_t[k])});
+        for (int k = pareq_s[a]; k < pareq_s[a] + pareq_c[a]; ++k) af->paReq.push_back(pat(k));
+        for (int k = paareq_s[a]; k < paareq_s[a] + paareq_c[a]; ++k) af->paaReq.push_back(pat(k));
+        for (int k = papref_s[a]; k < papref_s[a] + papref_c[a]; ++k) af->paPref.push_back({wpat_w[k], pat(wpat_t[k])});
+        for (int k = paapref_s[a]; k < paapref_s[a] + paapref_c[a]; ++k) af->paaPref.push_back({wpat_w[k], pat(wpat_t[k])});
+        affs[a] = af;
+    }
+    // pods
+    auto puid = s.vec<int32_t>("p_uid");
+    size_t P = puid.size();
+    auto pname = s.vec<int32_t>("p_name"), pns = s.vec<int32_t>("p_ns"), pjob = s.vec<int32_t>("p_job"),
+         pnode = s.vec<int32_t>("p_node"), ppri = s.vec<int32_t>("p_priority"), paff = s.vec<int32_t>("p_aff");
+    auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+    auto pts = s.vec<int64_t>("p_ts");
+    auto plo = s.offs("p_label_off", P);
+    auto plk = L("pl_key"), plv = L("pl_val");
+    auto pso = s.offs("p_nsel_off", P);
+    auto psk = L("ps_key"), psv = L("ps_val");
+    auto pco = s.offs("p_ctr_off", P);
+    auto ccpu_ = s.vec<int64_t>("c_cpu"), cmem_ = s.vec<int64_t>("c_mem"), cgpu_ = s.vec<int64_t>("c_gpu");
+    auto chas = s.vec<uint8_t>("c_has");
+    auto cpo = s.offs("c_port_off", ccpu_.size());
+    auto ptip = L("pt_ip"), ptpr = L("pt_proto"), ptpo = L("pt_port");
+    auto pio = s.offs("p_ictr_off", P);
+    auto iccpu = s.vec<int64_t>("ic_cpu"), icmem = s.vec<int64_t>("ic_mem"), icgpu = s.vec<int64_t>("ic_gpu");
+    auto ichas = s.vec<uint8_t>("ic_has");
+    auto pto = s.offs("p_tol_off", P);
+    auto tlk = L("tl_key"), tlo = L("tl_op"), tlv = L("tl_val"), tle = L("tl_effect");
+    w.pods.resize(P);
+    for (size_t i = 0; i < P; ++i) {
+        Pod& p = w.pods[i];
+        p.index = (int)i;
+        p.uid = s.s(puid[i]);
+        p.name = s.s(pname[i]);
+        p.ns = s.s(pns[i]);
+        p.job = pjob[i];
+        p.nodeName = s.s(pnode[i]);
+        p.phase = pphase[i];
+        p.deleting = pdel[i];
+        p.backfill = pbf[i];
+        p.priority = ppri[i];
+        p.ts = pts[i];
+        for (int k = plo[i]; k < plo[i + 1]; ++k) p.labels[s.s(plk[k])] = s.s(plv[k]);
+        for (int k = pso[i]; k < pso[i + 1]; ++k) p.nodeSelector[s.s(psk[k])] = s.s(psv[k]);
+        for (int k = pco[i]; k < pco[i + 1]; ++k) {
+            Container c;
+            c.cpu = ccpu_[k]; c.mem = cmem_[k]; c.gpu = cgpu_[k]; c.has = chas[k];
+            for (int q = cpo[k]; q < cpo[k + 1]; ++q) c.ports.push_back({s.s(ptip[q]), s.s(ptpr[q]), ptpo[q]});
+            p.containers.push_back(c);
+        }
+        for (int k = pio[i]; k < pio[i + 1]; ++k) {
+            Container c;
+            c.cpu = iccpu[k]; c.mem = icmem[k]; c.gpu = icgpu[k]; c.has = ichas[k];
+            p.initContainers.push_back(c);
+        }
+        for (int k = pto[i]; k < pto[i + 1]; ++k) p.tolerations.push_back({s.s(tlk[k]), s.s(tlo[k]), s.s(tlv[k]), s.s(tle[k])});
+        if (!paff.empty() && paff[i] >= 0) p.affinity = affs[paff[i]];
+    }
+}
+
+/* Build the session the way SchedulerCache.Snapshot + OpenSession do. */
+static void openSession(World& w) {
+    const kbs::Snapshot& s = w.snap;
+    Session& ssn = w.ssn;
+    ssn.tiers = w.tiers;
+    size_t N = w.knodes.size();
+    // cache nodes: NewNodeInfo(node); Snapshot clones (AddTask re-applied in task order)
+    w.nodes.resize(N);
+    for (size_t i = 0; i < N; ++i) {
+        w.nodes[i].init(&w.knodes[i]);
+        ssn.nodeIndex[w.knodes[i].name] = (int)i;
+    }
+    map<string, int> nodeByName;
+    for (size_t i = 0; i < N; ++i) nodeByName[w.knodes[i].name] = (int)i;
+    // tasks
+    size_t P = w.pods.size();
+    w.tasks.resize(P);
+    for (size_t i = 0; i < P; ++i) {
+        Pod& p = w.pods[i];
+        TaskInfo& t = w.tasks[i];
+        t.pod = (int)i;
+        t.uid = p.uid;
+        t.name = p.name;
+        t.ns = p.ns;
+        t.Resreq = GetPodResourceWithoutInitContainers(p);
+        t.InitResreq = GetPodResourceRequest(p);
+        t.NodeName = p.nodeName;
+        t.Status = getTaskStatus(p);
+        t.Priority = p.priority;
+        t.P = &p;
+        t.IsBackfill = p.backfill;
+        if (!p.nodeName.empty()) {
+            if (!nodeByName.count(p.nodeName))
+                throw std::runtime_error("pod " + p.uid + " bound to unknown node " + p.nodeName);
+            if (t.Status != Succeeded && t.Status != Failed) w.nodes[nodeByName[p.nodeName]].AddTask(t);
+        }
+    }
+    // queues
+    auto qn = s.vec<int32_t>("q_name");
+    auto qw = s.vec<int32_t>("q_weight");
+    auto qts = s.vec<int64_t>("q_ts");
+    w.queues.resize(qn.size());
+    for (size_t i = 0; i < qn.size(); ++i) {
+        w.queues[i].UID = w.queues[i].Name = s.s(qn[i]);
+        w.queues[i].Weight = qw[i];
+        w.queues[i].ts = qts.empty() ? 0 : qts[i];
+        w.queues[i].slot = (int)i;
+    }
+    // jobs: pod-group jobs + shadow jobs (cache/event_handlers.go:41-61, cache/util.go:42-60)
+    auto jns = s.vec<int32_t>("j_ns"), jname = s.vec<int32_t>("j_name"), jq = s.vec<int32_t>("j_queue"),
+         jmin = s.vec<int32_t>("j_min"), jpri = s.vec<int32_t>("j_pg_priority");
+    auto jts = s.vec<int64_t>("j_ts");
+    struct JobSrc { string uid; int row; int shadowPod; };
+    vector<JobSrc> srcs;
+    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
+    for (size_t i = 0; i < P; ++i)
+        if (w.pods[i].job < 0) srcs.push_back({w.pods[i].uid, -1, (int)i});
+    std::stable_sort(srcs.begin(), srcs.end(), [](const JobSrc& a, const JobSrc& b) { return a.uid < b.uid; });
+    map<string, int> qidx;
+    for (size_t i = 0; i < w.queues.size(); ++i) qidx[w.queues[i].UID] = (int)i;
+    w.jobs.resize(srcs.size());
+    map<int, int> rowToJob;
+    for (size_t k = 0; k < srcs.size(); ++k) {
+        JobInfo& j = w.jobs[k];
+        j.UID = srcs[k].uid;
+        if (srcs[k].row >= 0) {
+            int r = srcs[k].row;
+            j.Name = s.s(jname[r]);
+            j.Namespace = s.s(jns[r]);
+            j.Queue = s.s(jq[r]);
+            j.MinAvailable = jmin[r];
+            j.CreationTimestamp = jts[r];
+            j.Priority = jpri[r];
+            rowToJob[r] = (int)k;
+        } else {
+            const Pod& p = w.pods[srcs[k].shadowPod];
+            j.Name = p.uid;
+            j.Namespace = p.ns;
+            j.Queue = "default";
+            j.MinAvailable = 1;
+            j.CreationTimestamp = 0;
+            j.Priority = 0;
+        }
+    }
+    for (size_t i = 0; i < P; ++i) {
+        TaskInfo& t = w.tasks[i];
+        int jk = -1;
+        if (w.pods[i].job >= 0) jk = rowToJob[w.pods[i].job];
+        else {
+            for (size_t k = 0; k < srcs.size(); ++k) if (srcs[k].shadowPod == (int)i) { jk = (int)k; break; }
+        }
+        t.job = jk;
+        t.jobUID = w.jobs[jk].UID;
+    }
+    // Snapshot(): only jobs whose queue exists; Clone re-adds tasks (job_info.go:294-326)
+    for (size_t k = 0; k < w.jobs.size(); ++k) {
+        JobInfo& j = w.jobs[k];
+        if (!qidx.count(j.Queue)) continue;
+        for (size_t i = 0; i < P; ++i)
+            if (w.tasks[i].job == (int)k) j.AddTaskInfo(&w.tasks[i]);
+        j.slot = (int)ssn.Jobs.size();
+        ssn.Jobs.push_back(&j);
+        ssn.JobByUID[j.UID] = &j;
+    }
+    for (auto& n : w.nodes) { ssn.Nodes.push_back(&n); ssn.NodeByName[n.Name] = &n; }
+    for (auto& q : w.queues) { ssn.Queues.push_back(&q); ssn.QueueByUID[q.UID] = &q; }
+    // plugins: one object per name, the last tier entry's arguments win
+    // (framework.go:33-42 stores them in map ssn.plugins); OnSessionOpen once each
+    map<string, PluginOption> plugins;
+    vector<string> porder;
+    for (auto& tier : w.tiers)
+        for (auto& opt : tier) {
+            if (!plugins.count(opt.name)) porder.push_back(opt.name);
+            plugins[opt.name] = opt;
+        }
+    for (auto& name : porder) {
+        const PluginOption& opt = plugins[name];
+        {
+            if (opt.name == "priority") priorityOpen(ssn, opt);
+            else if (opt.name == "gang") gangOpen(ssn, opt);
+            else if (opt.name == "drf") { w.drf = std::make_shared<DrfState>(); drfOpen(ssn, opt, w.drf); }
+            else if (opt.name == "proportion") { w.prop = std::make_shared<PropState>(); propOpen(ssn, opt, w.prop); }
+            else if (opt.name == "predicates") predicatesOpen(ssn, opt);
+            else if (opt.name == "nodeorder") nodeorderOpen(ssn, opt);
+            // conformance: only preemptable/reclaimable fns; nothing on the allocate path
+        }
+    }
+}
+
+/* allocateAction.Execute (actions/allocate/allocate.go:41-201) */
+static void allocateExecute(World& w) {
+    Session& ssn = w.ssn;
+    PriorityQueue<QueueInfo> queues;
+    queues.lessFn = [&ssn](QueueInfo* l, QueueInfo* r) { return ssn.QueueOrderFn(l, r); };
+    map<string, std::unique_ptr<PriorityQueue<JobInfo>>> jobsMap;
+    for (auto* job : ssn.Jobs) {
+        auto qit = ssn.QueueByUID.find(job->Queue);
+        if (qit == ssn.QueueByUID.end()) continue;
+        queues.Push(qit->second);
+        if (!jobsMap.count(job->Queue)) {
+            jobsMap[job->Queue].reset(new PriorityQueue<JobInfo>());
+            jobsMap[job->Queue]->lessFn = [&ssn](JobInfo* l, JobInfo* r) { return ssn.JobOrderFn(l, r); };
+        }
+        jobsMap[job->Queue]->Push(job);
+    }
+    map<string, std::unique_ptr<PriorityQueue<TaskInfo>>> pendingTasks;
+    for (;;) {
+        if (queues.Empty()) break;
+        QueueInfo* queue = queues.Pop();
+        if (ssn.Overused(queue)) continue;
+        auto jit = jobsMap.find(queue->UID);
+        if (jit == jobsMap.end() || jit->second->Empty()) continue;
+        PriorityQueue<JobInfo>& jobs = *jit->second;
+        JobInfo* job = jobs.Pop();
+        if (!pendingTasks.count(job->UID)) {
+            auto* tq = new PriorityQueue<TaskInfo>();
+            tq->lessFn = [&ssn](TaskInfo* l, TaskInfo* r) { return ssn.TaskOrderFn(l, r); };
+            auto it = job->TaskStatusIndex.find(Pending);
+            if (it != job->TaskStatusIndex.end())
+                for (auto& kv : it->second) {
+                    if (kv.second->Resreq.IsEmpty()) continue;  // BestEffort skipped (:95)
+                    tq->Push(kv.second);
+                }
+            pendingTasks[job->UID].reset(tq);
+        }
+        PriorityQueue<TaskInfo>& tasks = *pendingTasks[job->UID];
+        while (!tasks.Empty()) {
+            vector<NodeInfo*> predicateNodes;
+            map<int, vector<NodeInfo*>> nodeScores;
+            TaskInfo* task = tasks.Pop();
+            bool assigned = false;
+            if (!job->NodesFitDelta.empty()) job->NodesFitDelta.clear();
+            for (auto* node : ssn.Nodes)
+                if (ssn.PredicateFn_(task, node)) predicateNodes.push_back(node);
+            for (auto* node : predicateNodes) {
+                int score;
+                if (ssn.NodeOrderFn_(task, node, &score)) nodeScores[score].push_back(node);
+            }
+            // util.SelectBestNode (sort.go:25-37): keys descending, buckets in insertion order
+            vector<NodeInfo*> selectedNodes;
+            for (auto it = nodeScores.rbegin(); it != nodeScores.rend(); ++it)
+                for (auto* n : it->second) selectedNodes.push_back(n);
+            for (auto* node : selectedNodes) {
+                if (task->InitResreq.LessEqual(node->GetAccessibleResource())) {
+                    if (!ssn.Allocate(task, node, !task->InitResreq.LessEqual(node->Idle))) continue;
+                    assigned = true;
+                    break;
+                } else {
+                    Resource d = node->Idle;  // NodesFitDelta bookkeeping (:166-167)
+                    if (task->Resreq.MilliCPU > 0) d.MilliCPU -= task->Resreq.MilliCPU + minMilliCPU;
+                    if (task->Resreq.Memory > 0) d.Memory -= task->Resreq.Memory + minMemory;
+                    if (task->Resreq.MilliGPU > 0) d.MilliGPU -= task->Resreq.MilliGPU + minMilliGPU;
+                    job->NodesFitDelta[node->Name] = d;
+                }
+                if (task->InitResreq.LessEqual(node->Releasing)) {
+                    ssn.Pipeline(task, node);
+                    assigned = true;
+                    break;
+                }
+            }
+            if (!assigned) break;
+            if (ssn.JobReady(job)) {
+                jobs.Push(job);
+                break;
+            }
+        }
+        queues.Push(queue);
+    }
+}
+
+}  // namespace ref
+
+/* ------------------------------------------------------------------------ */
+/* C ABI for the tests (ctypes)                                              */
+/* ------------------------------------------------------------------------ */
+static thread_local std::string g_err;
+
+extern "C" {
+
+const char* ref_last_error(void) { return g_err.c_str(); }
+
+/* Run the allocate action on a KBS1 snapshot.  Outputs, in placement order:
+ * pod index, node index, status code (ref::TaskStatus).  Returns the number
+ * of placements, or -1 on error.  `cap` bounds the output arrays. */
+int ref_allocate(const char* path, int32_t* out_pod, int32_t* out_node, int32_t* out_status, int cap,
+                 double* out_node_state /* optional: N x 12 doubles: idle, used, releasing, backfilled */) {
+    try {
+        ref::World w;
+        w.snap.load_file(path);
+        ref::loadWorld(w);
+        ref::openSession(w);
+        ref::allocateExecute(w);
+        int n = (int)w.ssn.log.size();
+        for (int i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(w.ssn.log[i]);
+            out_node[i] = std::get<1>(w.ssn.log[i]);
+            out_status[i] = std::get<2>(w.ssn.log[i]);
+        }
+        if (out_node_state) {
+            for (size_t i = 0; i < w.nodes.size(); ++i) {
+                const ref::Resource* rs[4] = {&w.nodes[i].Idle, &w.nodes[i].Used, &w.nodes[i].Releasing,
+                                              &w.nodes[i].Backfilled};
+                for (int k = 0; k < 4; ++k) {
+                    out_node_state[i * 12 + k * 3 + 0] = rs[k]->MilliCPU;
+                    out_node_state[i * 12 + k * 3 + 1] = rs[k]->Memory;
+                    out_node_state[i * 12 + k * 3 + 2] = rs[k]->MilliGPU;
+                }
+            }
+        }
+        return n;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+/* Session-open node state (after Snapshot/Clone, before any action):
+ * N x 12 doubles (idle, used, releasing, backfilled) and, when `accessible`
+ * is non-null, GetAccessibleResource() of every node (N x 3). */
+int ref_open_nodes(const char* path, double* out_node_state, double* accessible) {
+    try {
+        ref::World w;
+        w.snap.load_file(path);
+        ref::loadWorld(w);
+        ref::openSession(w);
+        for (size_t i = 0; i < w.nodes.size(); ++i) {
+            const ref::Resource* rs[4] = {&w.nodes[i].Idle, &w.nodes[i].Used, &w.nodes[i].Releasing,
+                                          &w.nodes[i].Backfilled};
+            for (int k = 0; k < 4; ++k) {
+                out_node_state[i * 12 + k * 3 + 0] = rs[k]->MilliCPU;
+                out_node_state[i * 12 + k * 3 + 1] = rs[k]->Memory;
+                out_node_state[i * 12 + k * 3 + 2] = rs[k]->MilliGPU;
+            }
+            if (accessible) {
+                ref::Resource a = w.nodes[i].GetAccessibleResource();
+                accessible[i * 3 + 0] = a.MilliCPU;
+                accessible[i * 3 + 1] = a.Memory;
+                accessible[i * 3 + 2] = a.MilliGPU;
+            }
+        }
+        return (int)w.nodes.size();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+/* TaskInfo request vectors of every pod: P x 6 doubles (Resreq, InitResreq). */
+int ref_task_requests(const char* path, double* out) {
+    try {
+        ref::World w;
+        w.snap.load_file(path);
+        ref::loadWorld(w);
+        for (size_t i = 0; i < w.pods.size(); ++i) {
+            ref::Resource a = ref::GetPodResourceWithoutInitContainers(w.pods[i]);
+            ref::Resource b = ref::GetPodResourceRequest(w.pods[i]);
+            double v[6] = {a.MilliCPU, a.Memory, a.MilliGPU, b.MilliCPU, b.Memory, b.MilliGPU};
+            std::memcpy(out + i * 6, v, sizeof v);
+        }
+        return (int)w.pods.size();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+/* JobInfo.GetReadiness for a job with the given per-status task counts
+ * (gang_test.go:14-43 known answers). statuses: ref::TaskStatus codes. */
+int ref_job_readiness(int32_t min_available, const int32_t* statuses, int n) {
+    ref::JobInfo j;
+    j.MinAvailable = min_available;
+    std::vector<ref::TaskInfo> ts(n);
+    std::vector<ref::Pod> ps(n);
+    for (int i = 0; i < n; ++i) {
+        ts[i].pod = i;
+        ts[i].Status = statuses[i];
+        ts[i].P = &ps[i];
+        j.AddTaskInfo(&ts[i]);
+    }
+    return j.GetReadiness();
+}
+
+}  // extern "C"

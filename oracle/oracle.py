@@ -1,0 +1,148 @@
+"""TEST ORACLE bindings (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline — never as the measured or
+shipped path.  The product library (kube-batch-1_amd/) must not import it.
+
+Two restatements of kube-batch's allocate action live next to this file:
+
+* ``kbref`` (kbref.cpp) — faithful: structured like the Go code, per-pair
+  recomputation; small snapshots only.
+* ``kbfast`` (kbfast.cpp) — hoisted: identical placements, per-task precompute
+  and an O(N) multi-threaded sweep; the CPU baseline.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+# ref::TaskStatus codes (pkg/scheduler/api/types.go:22-61)
+PENDING, ALLOCATED_OVER_BACKFILL, ALLOCATED, PIPELINED = 1, 2, 4, 8
+BINDING, BOUND, RUNNING, RELEASING = 16, 32, 64, 128
+SUCCEEDED, FAILED, UNKNOWN = 256, 512, 1024
+READY, ALMOST_READY, NOT_READY = 1, 2, 4
+
+_libs: Dict[str, ctypes.CDLL] = {}
+
+
+def build() -> None:
+    """Compile the oracle libraries (gcc only; no GPU)."""
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+
+
+def _lib(name: str) -> ctypes.CDLL:
+    if name not in _libs:
+        path = os.path.join(BUILD, f"lib{name}.so")
+        if not os.path.exists(path):
+            build()
+        lib = ctypes.CDLL(path)
+        _libs[name] = lib
+    return _libs[name]
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Placement:
+    """Placements in decision order: (pod index, node index, status code)."""
+
+    def __init__(self, pod: np.ndarray, node: np.ndarray, status: np.ndarray):
+        self.pod, self.node, self.status = pod, node, status
+
+    def __len__(self):
+        return int(self.pod.size)
+
+    def as_list(self) -> List[Tuple[int, int, int]]:
+        return list(zip(self.pod.tolist(), self.node.tolist(), self.status.tolist()))
+
+    def kinds(self) -> np.ndarray:
+        """1 = allocated (any Allocated* status), 2 = pipelined."""
+        return np.where(self.status == PIPELINED, 2, 1).astype(np.int32)
+
+
+def ref_allocate(path: str, cap: Optional[int] = None, with_nodes: bool = False):
+    lib = _lib("kbref")
+    fn = lib.ref_allocate
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
+    cap = cap or 1 << 20
+    pod = np.zeros(cap, np.int32)
+    node = np.zeros(cap, np.int32)
+    st = np.zeros(cap, np.int32)
+    nstate = None
+    if with_nodes:
+        nstate = np.zeros((1 << 16, 12), np.float64)
+    n = fn(path.encode(), _p(pod), _p(node), _p(st), cap, _p(nstate) if nstate is not None else None)
+    if n < 0:
+        lib.ref_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    pl = Placement(pod[:n].copy(), node[:n].copy(), st[:n].copy())
+    return (pl, nstate) if with_nodes else pl
+
+
+def ref_open_nodes(path: str, n_nodes: int):
+    lib = _lib("kbref")
+    fn = lib.ref_open_nodes
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p]
+    st = np.zeros((n_nodes, 12), np.float64)
+    acc = np.zeros((n_nodes, 3), np.float64)
+    n = fn(path.encode(), _p(st), _p(acc))
+    if n < 0:
+        lib.ref_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    return st[:n], acc[:n]
+
+
+def ref_task_requests(path: str, n_pods: int) -> np.ndarray:
+    lib = _lib("kbref")
+    fn = lib.ref_task_requests
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    out = np.zeros((n_pods, 6), np.float64)
+    n = fn(path.encode(), _p(out))
+    if n < 0:
+        lib.ref_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    return out[:n]
+
+
+def ref_job_readiness(min_available: int, statuses: List[int]) -> int:
+    lib = _lib("kbref")
+    fn = lib.ref_job_readiness
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int32, ctypes.c_void_p, ctypes.c_int]
+    a = np.asarray(statuses, dtype=np.int32)
+    return fn(min_available, _p(a), len(statuses))
+
+
+def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
+                  max_pops: int = -1, stats: Optional[dict] = None) -> Placement:
+    """Hoisted restatement (CPU baseline).  ``max_pops`` bounds the number of
+    job pops (a bounded sample of the session for timing)."""
+    lib = _lib("kbfast")
+    fn = lib.fast_allocate
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int, ctypes.c_void_p]
+    cap = cap or (1 << 21)
+    pod = np.zeros(cap, np.int32)
+    node = np.zeros(cap, np.int32)
+    st = np.zeros(cap, np.int32)
+    tm = np.zeros(8, np.float64)
+    n = fn(path.encode(), threads, max_pops, _p(pod), _p(node), _p(st), cap, _p(tm))
+    if n < 0:
+        lib.fast_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.fast_last_error().decode())
+    if stats is not None:
+        stats.update(open_s=tm[0], allocate_s=tm[1], pops=int(tm[2]), tasks_tried=int(tm[3]),
+                     load_s=tm[4])
+    return Placement(pod[:n].copy(), node[:n].copy(), st[:n].copy())
