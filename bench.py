@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""bench.py — kube-batch allocate action on MI355X: pod placements/sec and p50
+session latency on the C4 workload (100k nodes x 1M pods, BASELINE.json).
+
+A step is one scheduling session over the same synthetic snapshot: open the
+session from the in-memory KBS1 buffer (decode + encode + upload to HBM),
+run the allocate action (host ordering plugins + HIP placement kernels),
+close.  ``value`` = placements of all timed sessions on all ranks / max-over-
+ranks wall time.  Inputs are resident in host memory when the timed region
+starts (the session upload is part of every step, as in the reference where
+every session re-snapshots the cache).
+
+N > 1: one process per GPU (torch.distributed over RCCL for the barrier and
+the max-over-ranks time).  This round every rank runs an independent replica
+session on its own GPU (node-array sharding is the next step).
+
+Also reported:
+* roofline of the sweep kernel (k_sweep_topk): algorithmic bytes = nodes x
+  113 B per launch / its mean duration measured with HIP
+  events on the engine's stream during the timed steps;
+* cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
+  cores, on a bounded sample (the first job pops of the same session).
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+
+import numpy as np  # noqa: E402
+
+import kbgen  # noqa: E402
+import kbhip  # noqa: E402
+
+METRIC = "pod placements/sec + p50 session latency, 100k nodes × 1M pods"
+B_NODE = 113  # algorithmic bytes per node per sweep
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--pending", type=int, default=800_000)
+    ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
+    ap.add_argument("--time-every", type=int, default=4, help="HIP-event time every k-th sweep launch")
+    return ap.parse_args()
+
+
+def dist_setup(n):
+    if n <= 1:
+        return 0, 1, 0, None
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl")
+    return rank, world, local, dist
+
+
+def barrier(dist, local):
+    if dist is None:
+        return
+    import torch
+    t = torch.zeros(1, device=f"cuda:{local}")
+    dist.all_reduce(t)
+    torch.cuda.synchronize(local)
+
+
+def allmax(dist, local, x):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allsum(dist, local, x):
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def snapshot_path(args):
+    os.makedirs(args.cache, exist_ok=True)
+    p = os.path.join(args.cache, f"c4_{args.nodes}_{args.pending}_{kbgen.BASE_SEED + 4}.kbs")
+    if not os.path.exists(p):
+        tmp = p + f".tmp{os.getpid()}"
+        kbgen.gen_c4(tmp, n_nodes=args.nodes, n_pending=args.pending)
+        os.replace(tmp, p)
+    return p
+
+
+def run_session(buf, device, time_every):
+    t0 = time.perf_counter()
+    s = kbhip.Session(buf, device=device)
+    s.set_option("time_every", time_every)
+    pod, node, kind = s.allocate(cap=1 << 21)
+    st = s.stats()
+    s.close()
+    return time.perf_counter() - t0, len(pod), st
+
+
+def cpu_baseline(path, target_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the checker / CPU baseline only (test infrastructure)
+    threads = min(16, os.cpu_count() or 1)
+    probe_pops = 50
+    st = {}
+    pl = oracle.fast_allocate(path, threads=threads, max_pops=probe_pops, stats=st)
+    per_pop = st["allocate_s"] / max(st["pops"], 1)
+    pops = int(max(probe_pops, min(20000, target_s / max(per_pop, 1e-6))))
+    st = {}
+    pl = oracle.fast_allocate(path, threads=threads, max_pops=pops, stats=st)
+    return {"value": len(pl) / st["allocate_s"], "unit": "placements/s", "cores": threads, "kind": "port",
+            "sample": f"first {st['pops']} job pops ({len(pl)} placements) of the same C4 session, "
+                      f"allocate action only, hoisted C++ restatement oracle/kbfast.cpp, "
+                      f"{threads} threads on {os.cpu_count()} host cpus"}
+
+
+def main():
+    args = parse()
+    rank, world, local, dist = dist_setup(args.gpus)
+    path = snapshot_path(args) if rank == 0 or dist is None else None
+    barrier(dist, local)
+    if path is None:
+        path = snapshot_path(args)
+    with open(path, "rb") as f:
+        buf = f.read()
+    device = local
+    for _ in range(args.warmup):
+        run_session(buf, device, 0)
+    barrier(dist, local)
+    t0 = time.perf_counter()
+    lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
+    for _ in range(args.steps):
+        dt, n, st = run_session(buf, device, args.time_every)
+        lat.append(dt)
+        placed += n
+        sweeps_ms += st["device_s"] * 1e3
+        sweeps_n += st["timed_launches"]
+        st_last = st
+    barrier(dist, local)
+    wall = time.perf_counter() - t0
+    wall = allmax(dist, local, wall)
+    total_placed = allsum(dist, local, placed)
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    nodes = st_last["nodes"]
+    sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
+    achieved = nodes * B_NODE / (sweep_us * 1e-6) / 1e9 if sweeps_n else 0.0
+    out = {
+        "metric": METRIC,
+        "value": total_placed / wall,
+        "unit": "placements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "p50_session_ms": statistics.median(lat) * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (kbgen seed 20261015+4, C4 SKU mix, gang jobs minMember 8-64)",
+        "config": {"workload": "C4: 100k nodes x 1M pods (200k running, 800k pending), 1 allocate session per "
+                               "step, default kube-batch-conf tiers", "nodes": nodes, "pending": args.pending,
+                   "placements_per_session": placed // args.steps, "pops_per_session": st_last["pops"],
+                   "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
+                   "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
+                   "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
+        "roofline": {"kernel": "k_sweep_topk", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "mean_launch_us": sweep_us, "timed_launches": sweeps_n,
+                     "bytes_per_launch": nodes * B_NODE},
+    }
+    if args.cpu_baseline and world == 1:
+        out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds)
+    print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

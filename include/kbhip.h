@@ -1,0 +1,127 @@
+/*
+ * kbhip.h — C ABI of libkbhip.so, the MI355X (gfx950) placement engine for
+ * kube-batch's allocate action.
+ *
+ * The reference has no FFI: its hot path is a set of Go function types that
+ * plugins register into a framework.Session.  A per-(task, node) callback
+ * across cgo would cost N*T crossings, so the boundary is a batched session
+ * engine called once per job pop.  Each entry point below
+ * names the reference interface it replaces:
+ *
+ *   kbhip_session_open   <- framework.OpenSession -> cache.Snapshot()
+ *                           (pkg/scheduler/framework/framework.go:29-51,
+ *                            pkg/scheduler/cache/cache.go:515-583): the session
+ *                           snapshot, serialised as a KBS1 buffer (kbsnap.h),
+ *                           is copied, dictionary-encoded and uploaded to HBM.
+ *   kbhip_place_job      <- the inner loop of allocateAction.Execute
+ *                           (pkg/scheduler/actions/allocate/allocate.go:110-196)
+ *                           for one job pop: per task, Session.PredicateFn
+ *                           (framework/session_plugins.go:331-348, the
+ *                           predicates plugin predicates.go:123-203), Session.
+ *                           NodeOrderFn (:350-370, nodeorder.go:252-317),
+ *                           util.SelectBestNode (util/sort.go:25-37), the
+ *                           fit walk (allocate.go:149-185), Session.Allocate /
+ *                           Pipeline node updates (framework/session.go:199-297)
+ *                           and the gang JobReadyFn stop (gang.go:63-66).
+ *   kbhip_allocate       <- allocateAction.Execute as a whole
+ *                           (allocate.go:41-201) with the host-side ordering
+ *                           plugins (priority, gang, drf, proportion) run by
+ *                           the library's C++ mirror of the Go framework — for
+ *                           callers without a Go host (bench, tests).
+ *   kbhip_session_close  <- framework.CloseSession (framework.go:53-61).
+ *
+ * Conventions: every function returns 0 (or a count) on success and a
+ * negative KBHIP_E* code on failure; nothing throws or aborts across the ABI.
+ * kbhip_last_error() describes the last failure on the calling thread.
+ * Inputs are caller-owned and copied; outputs are caller-allocated; the
+ * session handle is engine-owned.  One session per calling thread; the
+ * library starts no host threads of its own.
+ *
+ * The library has exactly one execution path: HIP on a gfx950 device.  With
+ * no usable device every call fails with KBHIP_ENODEV; there is no CPU
+ * fallback.
+ */
+#ifndef KBHIP_H_
+#define KBHIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KBHIP_OK 0
+#define KBHIP_EINVAL (-1)       /* malformed snapshot or arguments */
+#define KBHIP_ENODEV (-2)       /* no HIP device / HIP runtime failure */
+#define KBHIP_EUNSUPPORTED (-3) /* snapshot uses a feature the engine does not implement */
+#define KBHIP_EDEVICE (-4)      /* kernel or copy failed */
+
+/* placement kinds (TaskStatus after the decision) */
+#define KBHIP_ALLOCATED 1 /* Session.Allocate -> api.Allocated */
+#define KBHIP_PIPELINED 2 /* Session.Pipeline -> api.Pipelined */
+
+/* stop reasons of kbhip_place_job */
+#define KBHIP_STOP_ALL 0        /* every given task was placed, job not yet ready */
+#define KBHIP_STOP_UNASSIGNED 1 /* a task found no node: allocate.go:187-189 */
+#define KBHIP_STOP_READY 2      /* JobReady after a placement: allocate.go:191-195 */
+
+typedef struct kb_session kb_session;
+
+/* Engine statistics (cumulative per session). */
+typedef struct kbhip_stats {
+    double open_s;       /* decode + encode + upload */
+    double allocate_s;   /* wall time inside kbhip_allocate */
+    double device_s;     /* summed HIP-event duration of the timed sweep launches */
+    int64_t pops;        /* job pops */
+    int64_t tasks;       /* tasks tried */
+    int64_t placed;      /* Allocated + Pipelined */
+    int64_t sweeps;      /* full-node sweeps launched */
+    int64_t batched_pops;/* pops served by the class-batched path */
+    int64_t nodes;       /* nodes in the session */
+    int64_t timed_launches; /* sweep launches timed with HIP events (option "time_every") */
+} kbhip_stats;
+
+/* Library / device probe: returns the number of usable gfx950 devices (>= 0),
+ * or KBHIP_ENODEV when the HIP runtime is unusable. */
+int kbhip_device_count(void);
+
+/* Open a session from a KBS1 snapshot held in memory (or a file). */
+int kbhip_session_open(const void* kbs_bytes, size_t len, int device, kb_session** out);
+int kbhip_session_open_file(const char* path, int device, kb_session** out);
+
+/* Place one job pop: tasks (pod indices of the snapshot, already in
+ * TaskOrderFn order) are tried in sequence until one is unassigned, the job
+ * becomes ready, or the list is exhausted.
+ *   gang_mode      1 = the gang JobReadyFn decides, 0 = no JobReadyFn (always Ready)
+ *   min_available  JobInfo.MinAvailable
+ *   ready_count    tasks of the job currently in AllocatedStatuses
+ * Outputs per consumed task: out_node (node index, -1 unassigned), out_kind
+ * (KBHIP_ALLOCATED / KBHIP_PIPELINED / 0).  *out_n_done = tasks consumed
+ * (including an unassigned one), *out_stop_reason = KBHIP_STOP_*. */
+int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
+                    int32_t min_available, int32_t ready_count, int32_t* out_node, uint8_t* out_kind,
+                    int32_t* out_n_done, int32_t* out_stop_reason);
+
+/* Run the whole allocate action.  Outputs the placement log in decision
+ * order: pod index, node index, kind.  Returns the number of placements. */
+int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+
+/* Read the device node state: N x 12 int64 (idle, used, releasing,
+ * backfilled; cpu/mem/gpu each).  `used` is maintained on the host mirror. */
+int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes);
+
+int kbhip_get_stats(kb_session* s, kbhip_stats* out);
+
+/* Engine knobs: "batched" = 0 forces the per-task sweep path (tests);
+ * "time_every" = k times every k-th sweep launch with HIP events. */
+int kbhip_set_option(kb_session* s, const char* key, int64_t value);
+
+int kbhip_session_close(kb_session* s);
+
+const char* kbhip_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KBHIP_H_ */

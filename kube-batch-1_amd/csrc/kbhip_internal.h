@@ -1,0 +1,29 @@
+// kbhip_internal.h — declarations shared by the host encoder/driver and the
+// kernel translation unit (not part of the public ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kbhip_types.h"
+
+namespace kbhip {
+
+// Read-only per-session tables (device pointers).
+struct DevTables {
+    const TaskClass* classes;
+    const Term* terms;
+    const Req* reqs;
+    const int32_t* vals;
+    const int64_t* valint;  // per global value id: parsed int64 (Gt/Lt)
+    const uint8_t* valok;   // per global value id: strconv.ParseInt succeeded
+    const uint64_t* masks;  // tolerated-taint / port-conflict / own-port words
+};
+
+hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
+                               uint64_t* walk, hipStream_t st);
+hipError_t launch_sweep_topk(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, uint64_t* cand,
+                             hipStream_t st);
+hipError_t launch_place_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
+                              const uint64_t* cand, hipStream_t st);
+int topk_blocks(int n_nodes, int* R_out);
+
+}  // namespace kbhip

@@ -1,0 +1,440 @@
+// kbhip_kernels.hip — gfx950 kernels of the placement engine.
+//
+// One sweep evaluates, for one task class and every node, the predicates
+// plugin (pkg/scheduler/plugins/predicates/predicates.go:123-203), the
+// nodeorder score (plugins/nodeorder/nodeorder.go:252-317) and the fit test
+// of the allocate walk (actions/allocate/allocate.go:149-185), and reduces to
+// the packed key (score, -index): the argmax of that key over feasible nodes
+// IS the node util.SelectBestNode + the walk would pick.
+//
+// Two ways to use a sweep:
+//  * per-task (general): k_sweep_argmax — one launch per task, 64-lane
+//    wave reduction -> LDS block reduction -> one 64-bit atomicMax per block;
+//    the last block to arrive commits the winner (Session.Allocate/Pipeline
+//    node update) and decides whether the job pop stops.
+//  * batched: when every task of a pop chunk has the same class and nothing
+//    but the winner's row can change between tasks, ONE sweep serves the whole
+//    chunk: k_sweep_topk keeps the top-64 keys of each block (bitonic sort in
+//    LDS), k_place_batch merges them and places the chunk's tasks in sequence
+//    against the sorted candidate list, re-evaluating only rows it changed.
+//    Placements are identical to per-task sweeps (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+
+#include "kbhip_internal.h"
+
+namespace kbhip {
+
+// ---------------------------------------------------------------------------
+// node row + evaluation
+// ---------------------------------------------------------------------------
+struct Row {  // the dynamic part of a node's state
+    int64_t idle_cpu, idle_mem, idle_gpu, rel_cpu, rel_mem, rel_gpu, bf_cpu, bf_mem, bf_gpu;
+    int64_t acpu, amem, nzc, nzm;
+    int32_t pods, maxtasks;
+};
+
+__device__ __forceinline__ Row load_row(const NodeCols& nc, int n) {
+    Row r;
+    r.idle_cpu = nc.idle_cpu[n]; r.idle_mem = nc.idle_mem[n]; r.idle_gpu = nc.idle_gpu[n];
+    r.rel_cpu = nc.rel_cpu[n]; r.rel_mem = nc.rel_mem[n]; r.rel_gpu = nc.rel_gpu[n];
+    r.bf_cpu = nc.bf_cpu[n]; r.bf_mem = nc.bf_mem[n]; r.bf_gpu = nc.bf_gpu[n];
+    r.acpu = nc.acpu[n]; r.amem = nc.amem[n]; r.nzc = nc.nzc[n]; r.nzm = nc.nzm[n];
+    r.pods = nc.pods[n]; r.maxtasks = nc.maxtasks[n];
+    return r;
+}
+
+__device__ __forceinline__ bool req_match(const DevTables& t, const NodeCols& nc, const Req& r, int n) {
+    // labels.Requirement.Matches (apimachinery/pkg/labels/selector.go:192-236)
+    switch (r.op) {
+        case OP_NAME_IN: return n == r.val_off;      // field selector metadata.name
+        case OP_NAME_NOTIN: return n != r.val_off;
+        case OP_FALSE: return false;
+        default: break;
+    }
+    const int v = nc.labels[(int64_t)r.key * nc.npad + n];
+    switch (r.op) {
+        case OP_IN:
+        case OP_NOTIN: {
+            bool hit = false;
+            for (int i = 0; i < r.nvals; ++i) hit |= t.vals[r.val_off + i] == v;
+            if (r.op == OP_IN) return v >= 0 && hit;
+            return v < 0 || !hit;
+        }
+        case OP_EXISTS: return v >= 0;
+        case OP_DNE: return v < 0;
+        case OP_GT: return v >= 0 && t.valok[v] && t.valint[v] > r.rhs;
+        case OP_LT: return v >= 0 && t.valok[v] && t.valint[v] < r.rhs;
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool term_match(const DevTables& t, const NodeCols& nc, const Term& tm, int n) {
+    bool ok = true;
+    for (int i = 0; i < tm.req_n; ++i) ok = ok && req_match(t, nc, t.reqs[tm.req_off + i], n);
+    return ok;
+}
+
+// The static part of the predicates: selector / node affinity, unschedulable,
+// taints.  Does not change while a session runs.
+__device__ __forceinline__ bool static_pred(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                            const NodeCols& nc, int n) {
+    if (!cf.pred_on) return true;
+    if (c.pred_err) return false;
+    if (nc.flags[n] & 1) return false;                                   // predicates.go:107-112
+    for (int w = 0; w < nc.taint_words; ++w)                             // helper/helpers.go:425-440
+        if (nc.taints[(int64_t)w * nc.npad + n] & ~t.masks[c.tol_off + w]) return false;
+    if (c.nsel_term >= 0 && !term_match(t, nc, t.terms[c.nsel_term], n)) return false;  // predicates.go:809-814
+    if (c.req_term_n >= 0) {                                             // predicates.go:826-846
+        bool any = false;
+        for (int i = 0; i < c.req_term_n; ++i) any = any || term_match(t, nc, t.terms[c.req_term_off + i], n);
+        if (!any) return false;
+    }
+    return true;
+}
+
+// ((cap - req) * 10) / cap for 0 <= req <= cap, cap > 0: the quotient is in
+// [0, 10]; a double estimate plus one exact integer correction step.
+__device__ __forceinline__ int64_t lr_score(int64_t req, int64_t cap) {  // least_requested.go:44-53
+    if (cap == 0 || req > cap) return 0;
+    const int64_t num = (cap - req) * 10;
+    int64_t q = (int64_t)((double)num / (double)cap);
+    if (q * cap > num) --q;
+    if ((q + 1) * cap <= num) ++q;
+    return q;
+}
+
+// Score of a feasible node (nodeorder.go:281-313; the inter-pod term is 0
+// for the sessions the engine accepts).
+__device__ __forceinline__ int32_t node_score(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                              const NodeCols& nc, const Row& r, int n) {
+    if (!cf.score_mult) return 0;
+    const int64_t rc = c.nz_cpu + r.nzc, rm = c.nz_mem + r.nzm;
+    const int64_t lr = (lr_score(rc, r.acpu) + lr_score(rm, r.amem)) / 2;
+    // balanced_resource_allocation.go:41-77, IEEE double, no contraction
+    const double cpuF = r.acpu == 0 ? 1.0 : (double)rc / (double)r.acpu;
+    const double memF = r.amem == 0 ? 1.0 : (double)rm / (double)r.amem;
+    int64_t bra = 0;
+    if (!(cpuF >= 1.0 || memF >= 1.0)) {
+        const double d = fabs(cpuF - memF);
+        const double one_minus = 1.0 - d;
+        bra = (int64_t)(one_minus * 10.0);
+    }
+    int32_t na = 0;                                                      // node_affinity.go:34-74
+    for (int i = 0; i < c.pref_term_n; ++i) {
+        const Term& tm = t.terms[c.pref_term_off + i];
+        if (term_match(t, nc, tm, n)) na += tm.weight;
+    }
+    return ((int32_t)lr * cf.w_lr + (int32_t)bra * cf.w_bra + na * cf.w_na) * cf.score_mult;
+}
+
+// Dynamic predicates (pod count, host ports) + fit + key, given the row.
+// passed: predicate pass and score computed (the node is in the walk).
+__device__ __forceinline__ uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                            const NodeCols& nc, const Row& r, const uint64_t* portw,
+                                            int n, bool stat_ok, int32_t* score_out, bool* passed) {
+    bool ok = stat_ok;
+    if (cf.pred_on) {
+        if (r.maxtasks <= r.pods) ok = false;                            // predicates.go:127
+        if (c.has_ports)                                                 // host_ports.go:96-125
+            for (int w = 0; w < nc.port_words; ++w)
+                if (portw[w] & t.masks[c.pconf_off + w]) ok = false;
+    }
+    if (ok && c.score_err) ok = false;  // NodeOrderFn error drops the node (allocate.go:141-145)
+    *passed = ok;
+    if (!ok) return 0;
+    const int32_t s = node_score(cf, c, t, nc, r, n);
+    *score_out = s;
+    // allocate.go:153 (InitResreq <= Idle + Backfilled) and :173 (<= Releasing)
+    const bool fit_acc = c.ireq_cpu - (r.idle_cpu + r.bf_cpu) < kMinCPU &&
+                         c.ireq_mem - (r.idle_mem + r.bf_mem) < kMinMem &&
+                         c.ireq_gpu - (r.idle_gpu + r.bf_gpu) < kMinGPU;
+    const bool fit_rel = c.ireq_cpu - r.rel_cpu < kMinCPU && c.ireq_mem - r.rel_mem < kMinMem &&
+                         c.ireq_gpu - r.rel_gpu < kMinGPU;
+    if (!fit_acc && !fit_rel) return 0;
+    return pack_key(s, n, fit_acc ? 0 : 1);
+}
+
+__device__ __forceinline__ uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                              const NodeCols& nc, int n, int32_t* score_out, bool* passed) {
+    const bool st = static_pred(cf, c, t, nc, n);
+    const Row r = load_row(nc, n);
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+    return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed);
+}
+
+// NodeInfo.AddTask for the winner (node_info.go:113-145) + the k8s NodeInfo
+// aggregates the predicates/nodeorder read (k8s cache/node_info.go:498-521).
+__device__ void commit_node(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {
+    if (c.backfill) { nc.bf_cpu[n] += c.req_cpu; nc.bf_mem[n] += c.req_mem; nc.bf_gpu[n] += c.req_gpu; }
+    if (kind == 1) { nc.idle_cpu[n] -= c.req_cpu; nc.idle_mem[n] -= c.req_mem; nc.idle_gpu[n] -= c.req_gpu; }
+    else { nc.rel_cpu[n] -= c.req_cpu; nc.rel_mem[n] -= c.req_mem; nc.rel_gpu[n] -= c.req_gpu; }
+    nc.pods[n] += 1;
+    nc.nzc[n] += c.nz_cpu;
+    nc.nzm[n] += c.nz_mem;
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words; ++w) nc.ports[(int64_t)w * nc.npad + n] |= t.masks[c.pown_off + w];
+}
+
+// Gang bookkeeping after an assignment: allocate.go:191-195 + gang.go:63-66.
+__device__ __forceinline__ void after_assign(PopCtrl* ctrl, int i, int kind) {
+    if (kind == 1) ctrl->ready_count += 1;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+    ctrl->n_done = i + 1;
+    if (!ctrl->gang_mode || ctrl->ready_count >= ctrl->min_avail) ctrl->stop = 2;
+    else if (i + 1 == ctrl->n_tasks) ctrl->stop = 0;
+}
+
+// ---------------------------------------------------------------------------
+// wave / block reductions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t u = __shfl_xor(v, o, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// per-task path
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
+                                                         int task_i, uint64_t* walk) {
+    __shared__ uint64_t red[kBlock / 64];
+    __shared__ int last;
+    if (ctrl->stop >= 0) return;  // the pop already stopped (uniform)
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
+    const TaskClass c = t.classes[cls];
+    const bool track = ctrl->any_bf != 0;
+    uint64_t best = 0;
+    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+        int32_t s = 0;
+        bool passed = false;
+        const uint64_t k = eval_node(cf, c, t, nc, n, &s, &passed);
+        if (track) walk[n] = passed ? pack_key(s, n, 0) : 0;
+        best = k > best ? k : best;
+    }
+    best = wave_max_u64(best);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
+    if (track) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // walk[] stores drained before the release
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t b = red[0];
+        for (int w = 1; w < kBlock / 64; ++w) b = red[w] > b ? red[w] : b;
+        if (b) atomicMax((unsigned long long*)&ctrl->slot[task_i], (unsigned long long)b);
+        __threadfence();
+        const unsigned prev = atomicAdd(&ctrl->arrive[task_i], 1u);
+        last = prev == gridDim.x - 1;
+        __threadfence();
+    }
+    __syncthreads();
+    if (!last) return;
+    // Last block: commit.
+    __shared__ uint64_t win;
+    if (threadIdx.x == 0) {
+        const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        win = k;
+        if (k == 0) {
+            ctrl->res_node[task_i] = -1;
+            ctrl->res_kind[task_i] = 0;
+            ctrl->n_done = task_i + 1;
+            ctrl->stop = 1;
+        } else {
+            const int n = key_idx(k), kind = key_kind(k);
+            ctrl->res_node[task_i] = n;
+            ctrl->res_kind[task_i] = kind;
+            if (track) {  // the winner is visited too: Idle += Backfilled first (node_info.go:209-211)
+                nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+            }
+            commit_node(c, t, nc, n, kind);
+            if (c.backfill) ctrl->any_bf = 1;
+            after_assign(ctrl, task_i, kind);
+        }
+    }
+    __syncthreads();
+    if (!track) return;
+    // GetAccessibleResource mutation for every other node the walk visited.
+    const uint64_t k = win;
+    const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
+    const int wn = k ? key_idx(k) : -1;
+    for (int n = threadIdx.x; n < nc.n; n += kBlock) {
+        const uint64_t v = walk[n];
+        if (!v || n == wn) continue;
+        if (k && v < wk) continue;
+        nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// batched path
+// ---------------------------------------------------------------------------
+// In-LDS bitonic sort, descending, of S (power of two) keys by all threads.
+template <int S, int NT>
+__device__ __forceinline__ void bitonic_desc(uint64_t* a) {
+    for (int k = 2; k <= S; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < S / 2; i += NT) {
+                // i-th compare-exchange pair of this stage
+                const int lo = (i / j) * 2 * j + (i % j);
+                const int hi = lo + j;
+                const bool desc = (lo & k) == 0;
+                const uint64_t x = a[lo], y = a[hi];
+                if ((x < y) == desc) { a[lo] = y; a[hi] = x; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+template <int R>
+__global__ __launch_bounds__(kBlock) void k_sweep_topk(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
+                                                       uint64_t* cand) {
+    __shared__ uint64_t keys[kBlock * R];
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
+    const TaskClass c = t.classes[cls];
+    const int base = blockIdx.x * kBlock * R;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int n = base + r * kBlock + threadIdx.x;
+        uint64_t k = 0;
+        if (n < nc.n) {
+            int32_t s;
+            bool passed;
+            k = eval_node(cf, c, t, nc, n, &s, &passed);
+        }
+        keys[r * kBlock + threadIdx.x] = k;
+    }
+    __syncthreads();
+    bitonic_desc<kBlock * R, kBlock>(keys);
+    if (threadIdx.x < kTopK) cand[(int64_t)blockIdx.x * kTopK + threadIdx.x] = keys[threadIdx.x];
+}
+
+// Single block: merge the per-block candidates, then place the chunk.
+constexpr int kPlaceThreads = 1024;
+constexpr int kMergeMax = 8192;  // keys sortable in LDS (64 KB)
+
+__global__ __launch_bounds__(kPlaceThreads) void k_place_batch(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
+                                                               const uint64_t* cand, int n_cand) {
+    __shared__ uint64_t keys[kMergeMax];
+    __shared__ Row rows[kTopK];
+    __shared__ uint64_t rport[kTopK][4];
+    __shared__ uint64_t cur[kTopK];      // current key of each list entry's node (after changes)
+    __shared__ int changed[kTopK];
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
+    const TaskClass c = t.classes[cls];
+    for (int i = threadIdx.x; i < kMergeMax; i += kPlaceThreads) keys[i] = i < n_cand ? cand[i] : 0;
+    __syncthreads();
+    bitonic_desc<kMergeMax, kPlaceThreads>(keys);
+    // keys[0..kTopK) = global top-64 (key order).  Prefetch their rows.
+    if (threadIdx.x < kTopK) {
+        const uint64_t k = keys[threadIdx.x];
+        changed[threadIdx.x] = 0;
+        cur[threadIdx.x] = k;
+        if (k) {
+            const int n = key_idx(k);
+            rows[threadIdx.x] = load_row(nc, n);
+            for (int w = 0; w < 4; ++w)
+                rport[threadIdx.x][w] = (c.has_ports && w < nc.port_words) ? nc.ports[(int64_t)w * nc.npad + n] : 0;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // Sequential placement.  Entry j of the list is either unchanged (its
+        // key is still keys[j]) or changed (cur[j] re-evaluated after a commit).
+        // The best node is the max over unchanged entries (the first one in
+        // list order) and changed entries; with <= kTopK tasks the list cannot
+        // run out before the chunk does.
+        const int T = ctrl->n_tasks;
+        int first = 0;
+        for (int i = 0; i < T; ++i) {
+            while (first < kTopK && keys[first] && changed[first]) ++first;
+            uint64_t best = (first < kTopK) ? keys[first] : 0;
+            int bj = best ? first : -1;
+            for (int j = 0; j < first; ++j)
+                if (changed[j] && cur[j] > best) { best = cur[j]; bj = j; }
+            if (!best) {
+                ctrl->res_node[i] = -1;
+                ctrl->res_kind[i] = 0;
+                ctrl->n_done = i + 1;
+                ctrl->stop = 1;
+                break;
+            }
+            const int n = key_idx(best), kind = key_kind(best);
+            ctrl->res_node[i] = n;
+            ctrl->res_kind[i] = kind;
+            Row& r = rows[bj];
+            if (kind == 1) { r.idle_cpu -= c.req_cpu; r.idle_mem -= c.req_mem; r.idle_gpu -= c.req_gpu; }
+            else { r.rel_cpu -= c.req_cpu; r.rel_mem -= c.req_mem; r.rel_gpu -= c.req_gpu; }
+            r.pods += 1;
+            r.nzc += c.nz_cpu;
+            r.nzm += c.nz_mem;
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) rport[bj][w] |= t.masks[c.pown_off + w];
+            changed[bj] = 1;
+            int32_t s = 0;
+            bool passed;
+            cur[bj] = dyn_key(cf, c, t, nc, r, rport[bj], n, true, &s, &passed);
+            after_assign(ctrl, i, kind);
+            if (ctrl->stop >= 0) break;
+        }
+    }
+    __syncthreads();
+    // write back changed rows
+    if (threadIdx.x < kTopK && changed[threadIdx.x]) {
+        const int n = key_idx(keys[threadIdx.x]);
+        const Row& r = rows[threadIdx.x];
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = rport[threadIdx.x][w];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers (host)
+// ---------------------------------------------------------------------------
+hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
+                               uint64_t* walk, hipStream_t st) {
+    int grid = (nc.n + kBlock - 1) / kBlock;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk);
+    return hipGetLastError();
+}
+
+int topk_blocks(int n_nodes, int* R_out) {
+    int R = 1;
+    while ((int64_t)kBlock * R * 128 < n_nodes && R < 32) R <<= 1;
+    *R_out = R;
+    return (n_nodes + kBlock * R - 1) / (kBlock * R);
+}
+
+hipError_t launch_sweep_topk(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, uint64_t* cand,
+                             hipStream_t st) {
+    int R;
+    const int nb = topk_blocks(nc.n, &R);
+    if ((int64_t)nb * kTopK > kMergeMax) return hipErrorInvalidValue;
+    switch (R) {
+        case 1: hipLaunchKernelGGL(k_sweep_topk<1>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+        case 2: hipLaunchKernelGGL(k_sweep_topk<2>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+        case 4: hipLaunchKernelGGL(k_sweep_topk<4>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+        case 8: hipLaunchKernelGGL(k_sweep_topk<8>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+        case 16: hipLaunchKernelGGL(k_sweep_topk<16>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+        default: hipLaunchKernelGGL(k_sweep_topk<32>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_place_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
+                              const uint64_t* cand, hipStream_t st) {
+    int R;
+    const int nb = topk_blocks(nc.n, &R);
+    hipLaunchKernelGGL(k_place_batch, dim3(1), dim3(kPlaceThreads), 0, st, cf, nc, t, ctrl, cand, nb * kTopK);
+    return hipGetLastError();
+}
+
+}  // namespace kbhip

@@ -1,0 +1,1177 @@
+// kbhip_session.cpp — host side of libkbhip.so: session open (KBS1 decode,
+// dictionary encoding, upload of the node SoA to HBM), the per-pop device
+// driver (kbhip_place_job) and a C++ mirror of the Go framework's ordering
+// plugins that runs the whole allocate action (kbhip_allocate).
+//
+// Reference map (pkg/scheduler unless noted):
+//   session open      cache/cache.go:515-583 (Snapshot), framework/session.go:66-122,
+//                     api/node_info.go:62-145 (NodeInfo.AddTask), api/job_info.go:239-326
+//   ordering          util/priority_queue.go + Go container/heap, framework/session_plugins.go:
+//                     244-329 (Job/Queue/TaskOrderFn), plugins/{priority,gang,drf,proportion}
+//   allocate loop     actions/allocate/allocate.go:41-201
+//   placement         the HIP kernels (kbhip_kernels.hip)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/kbhip.h"
+#include "../../include/kbsnap.h"
+#include "kbhip_internal.h"
+
+using std::string;
+using std::vector;
+
+namespace kbhip {
+
+static thread_local string g_err;
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(x)                                                                            \
+    do {                                                                                     \
+        hipError_t e_ = (x);                                                                 \
+        if (e_ != hipSuccess) throw Error(KBHIP_EDEVICE, string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+enum St { Pending = 1, AOB = 2, Allocated = 4, Pipelined = 8, Binding = 16, Bound = 32, Running = 64,
+          Releasing = 128, Succeeded = 256, Failed = 512, Unknown = 1024 };
+static inline bool allocated_status(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
+
+struct Dict {
+    std::unordered_map<string, int> ids;
+    vector<string> strs;
+    int get(const string& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        ids.emplace(s, (int)strs.size());
+        strs.push_back(s);
+        return (int)strs.size() - 1;
+    }
+};
+
+static bool parse_int64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+    if (s.empty()) return false;
+    size_t i = 0;
+    bool neg = false;
+    if (s[0] == '+' || s[0] == '-') { neg = s[0] == '-'; i = 1; if (s.size() == 1) return false; }
+    unsigned long long v = 0, lim = neg ? 9223372036854775808ULL : 9223372036854775807ULL;
+    for (; i < s.size(); ++i) {
+        if (s[i] < '0' || s[i] > '9') return false;
+        unsigned d = (unsigned)(s[i] - '0');
+        if (v > (lim - d) / 10) return false;
+        v = v * 10 + d;
+    }
+    *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+    return true;
+}
+
+struct R3 { int64_t c = 0, m = 0, g = 0; };
+struct F3 {  // float64 Resource of the ordering plugins
+    double c = 0, m = 0, g = 0;
+    void add(const R3& r) { c += (double)r.c; m += (double)r.m; g += (double)r.g; }
+    void addf(const F3& r) { c += r.c; m += r.m; g += r.g; }
+    void subf(const F3& r) { c -= r.c; m -= r.m; g -= r.g; }
+    double get(int k) const { return k == 0 ? c : k == 1 ? m : g; }
+    bool less_equal(const F3& rr) const {  // resource_info.go:164-168
+        return (c < rr.c || std::fabs(rr.c - c) < (double)kMinCPU) &&
+               (m < rr.m || std::fabs(rr.m - m) < (double)kMinMem) &&
+               (g < rr.g || std::fabs(rr.g - g) < (double)kMinGPU);
+    }
+    bool empty() const { return c < (double)kMinCPU && m < (double)kMinMem && g < (double)kMinGPU; }
+};
+static double share(double l, double r) { return r == 0 ? (l == 0 ? 0 : 1) : l / r; }  // helpers.go:35-48
+
+struct HPod {
+    string uid;
+    int ns = -1;
+    int status = Pending;
+    int32_t priority = 0;
+    int64_t ts = 0;
+    bool backfill = false;
+    R3 req, ireq;
+    int job = -1;   // session job slot
+    int cls = -1;   // device task class (pending tasks)
+    int node = -1;  // current node
+};
+struct HJob {
+    string uid;
+    int queue = -1;
+    int32_t min_avail = 0, priority = 0;
+    int64_t ts = 0;
+    vector<int> tasks;
+    vector<int> pending;  // pending non-BestEffort tasks in TaskOrderFn order (built at first pop)
+    size_t cursor = 0;
+    bool pending_built = false;
+    int cnt_alloc = 0, cnt_aob = 0;
+    F3 drf_alloc;
+    double drf_share = 0;
+};
+struct HQueue {
+    string name;
+    int32_t weight = 1;
+    int64_t ts = 0;
+    bool has_attr = false;
+    F3 deserved, allocated, request;
+    double share = 0;
+};
+struct Plugin {
+    string name;
+    int flags = 0;
+    std::map<string, string> args;
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    template <typename T>
+    T* alloc(size_t n) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size_t bytes = std::max<size_t>(n * sizeof(T), 16);
+        if (hipMalloc(&p, bytes) != hipSuccess) throw Error(KBHIP_EDEVICE, "hipMalloc failed");
+        return (T*)p;
+    }
+};
+
+template <typename T>
+static T* upload(DevBuf& b, const vector<T>& v, hipStream_t st) {
+    T* d = b.alloc<T>(v.size());
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    return d;
+}
+
+struct Session {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    // host model
+    vector<string> node_names;
+    vector<HPod> pods;
+    vector<HJob> jobs;
+    vector<HQueue> queues;
+    vector<vector<Plugin>> tiers;
+    bool drf_on = false, prop_on = false, gang_ready = false;
+    F3 total;
+    vector<R3> used;  // NodeInfo.Used mirror (for kbhip_read_nodes)
+    int any_bf = 0;
+    // device
+    Conf conf{};
+    NodeCols nc{};
+    DevTables tab{};
+    vector<TaskClass> classes;
+    DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
+        b_ctrl, b_cand, b_walk;
+    PopCtrl* d_ctrl = nullptr;
+    PopCtrl* h_ctrl = nullptr;  // pinned
+    uint64_t* d_cand = nullptr;
+    uint64_t* d_walk = nullptr;
+    bool batched = true;
+    int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
+    int64_t sweep_launches = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double timed_ms = 0;          // summed duration of the timed sweep launches
+    int64_t timed_n = 0;
+    kbhip_stats stats{};
+    vector<std::tuple<int, int, int>> log;
+
+    ~Session() {
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (h_ctrl) (void)hipHostFree(h_ctrl);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+// ---------------------------------------------------------------------------
+// encoder
+// ---------------------------------------------------------------------------
+struct Encoder {
+    const kbs::Snapshot& s;
+    Session& S;
+    Dict keys_all, vals, nss, taint_keys, port_keys, ip_dict, proto_dict;
+    std::map<string, int> sel_keys;  // label key -> label column
+    vector<Req> reqs;
+    vector<Term> terms;
+    vector<int32_t> vals_list;
+    vector<uint64_t> masks;
+    vector<vector<std::pair<int, int>>> node_labels;  // per node: (key id in keys_all, value id)
+    vector<std::tuple<string, string, string>> taint_defs;
+    vector<std::tuple<int, int, int32_t>> port_defs;  // (ip id, proto id, port)
+    std::map<std::tuple<int, int, int32_t>, int> port_ids;
+    int tw = 0, pw = 0;
+
+    Encoder(const kbs::Snapshot& s_, Session& S_) : s(s_), S(S_) {}
+
+    vector<int32_t> V32(const char* n) { return s.vec<int32_t>(n); }
+
+    int sel_key(const string& k) {
+        auto it = sel_keys.find(k);
+        if (it != sel_keys.end()) return it->second;
+        int id = (int)sel_keys.size();
+        sel_keys[k] = id;
+        return id;
+    }
+
+};
+
+static void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
+
+static void open_session(Session& S, const kbs::Snapshot& s, int device) {
+    auto t0 = std::chrono::steady_clock::now();
+    Encoder E(s, S);
+    auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
+    // ---------------- conf (framework.go:29-51) ----------------
+    {
+        auto pn = V32("conf_plugin_name"), pt = V32("conf_plugin_tier"), pf = V32("conf_plugin_flags"),
+             ap = V32("conf_arg_plugin"), ak = V32("conf_arg_key"), av = V32("conf_arg_val");
+        vector<Plugin> opts(pn.size());
+        for (size_t i = 0; i < pn.size(); ++i) { opts[i].name = s.s(pn[i]); opts[i].flags = pf[i]; }
+        for (size_t i = 0; i < ap.size(); ++i) {
+            if (ap[i] < 0 || (size_t)ap[i] >= opts.size()) throw Error(KBHIP_EINVAL, "bad conf_arg_plugin");
+            opts[ap[i]].args[s.s(ak[i])] = s.s(av[i]);
+        }
+        for (size_t i = 0; i < pn.size(); ++i) {
+            if (pt[i] < 0 || pt[i] > 64) throw Error(KBHIP_EINVAL, "bad conf_plugin_tier");
+            if ((size_t)pt[i] >= S.tiers.size()) S.tiers.resize(pt[i] + 1);
+            S.tiers[pt[i]].push_back(opts[i]);
+        }
+        S.conf.w_lr = S.conf.w_bra = S.conf.w_na = S.conf.w_pa = 1;
+        for (auto& tier : S.tiers)
+            for (auto& p : tier) {
+                if (p.name == "predicates" && !(p.flags & KBS_DIS_PREDICATE)) S.conf.pred_on = 1;
+                if (p.name == "nodeorder" && !(p.flags & KBS_DIS_NODEORDER)) S.conf.score_mult++;
+                if (p.name == "nodeorder") {  // the last entry's arguments win (framework.go:38-39)
+                    int w[4] = {1, 1, 1, 1};
+                    const char* names[4] = {"leastrequested.weight", "balancedresource.weight",
+                                            "nodeaffinity.weight", "podaffinity.weight"};
+                    for (int k = 0; k < 4; ++k) {  // nodeorder.go:177-249
+                        auto it = p.args.find(names[k]);
+                        int64_t v;
+                        if (it != p.args.end() && !it->second.empty() && parse_int64(it->second, &v)) w[k] = (int)v;
+                    }
+                    S.conf.w_lr = w[0]; S.conf.w_bra = w[1]; S.conf.w_na = w[2]; S.conf.w_pa = w[3];
+                }
+                if (p.name == "drf") S.drf_on = true;
+                if (p.name == "proportion") S.prop_on = true;
+                if (p.name == "gang" && !(p.flags & KBS_DIS_JOBREADY)) S.gang_ready = true;
+            }
+    }
+    // ---------------- nodes ----------------
+    auto nname = V32("n_name");
+    const int N = (int)nname.size();
+    const int npad = ((N + kBlock - 1) / kBlock) * kBlock;
+    auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"), agpu = s.vec<int64_t>("n_alloc_gpu"),
+         apods = s.vec<int64_t>("n_alloc_pods");
+    if ((int)acpu.size() != N || (int)amem.size() != N || (int)agpu.size() != N || (int)apods.size() != N)
+        throw Error(KBHIP_EINVAL, "node columns length mismatch");
+    auto unsched = s.vec<uint8_t>("n_unsched");
+    auto loff = s.offs("n_label_off", N);
+    auto lk = V32("nl_key"), lv = V32("nl_val");
+    auto toff = s.offs("n_taint_off", N);
+    auto tk = V32("nt_key"), tv = V32("nt_val"), te = V32("nt_effect");
+    S.node_names.resize(N);
+    std::unordered_map<string, int> node_idx;
+    E.node_labels.resize(N);
+    vector<vector<int>> node_taints(N);
+    std::map<std::tuple<string, string, string>, int> taint_ids;
+    for (int i = 0; i < N; ++i) {
+        S.node_names[i] = s.s(nname[i]);
+        node_idx[S.node_names[i]] = i;
+        for (int k = loff[i]; k < loff[i + 1]; ++k)
+            E.node_labels[i].push_back({E.keys_all.get(s.s(lk[k])), E.vals.get(s.s(lv[k]))});
+        for (int k = toff[i]; k < toff[i + 1]; ++k) {
+            string eff = s.s(te[k]);
+            if (eff != "NoSchedule" && eff != "NoExecute") continue;  // predicates.go:1494-1497
+            auto key = std::make_tuple(s.s(tk[k]), s.s(tv[k]), eff);
+            auto it = taint_ids.find(key);
+            int id;
+            if (it == taint_ids.end()) { id = (int)E.taint_defs.size(); taint_ids[key] = id; E.taint_defs.push_back(key); }
+            else id = it->second;
+            node_taints[i].push_back(id);
+        }
+    }
+    if ((int)node_idx.size() != N) throw Error(KBHIP_EINVAL, "duplicate node names");
+    // host-side node state (NewNodeInfo + AddTask replay, node_info.go:62-145)
+    vector<R3> idle(N), rel(N), bf(N);
+    vector<int64_t> nzc(N, 0), nzm(N, 0);
+    vector<int32_t> podcnt(N, 0);
+    vector<vector<int>> node_ports(N);
+    S.used.assign(N, R3{});
+    for (int i = 0; i < N; ++i) idle[i] = R3{acpu[i], amem[i], agpu[i]};
+
+    // ---------------- pods ----------------
+    auto puid = V32("p_uid");
+    const int P = (int)puid.size();
+    auto pns = V32("p_ns"), pjob = V32("p_job"), pnode = V32("p_node"), ppri = V32("p_priority"), paff = V32("p_aff");
+    auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+    auto pts = s.vec<int64_t>("p_ts");
+    if ((int)pns.size() != P || (int)pjob.size() != P || (int)pnode.size() != P || (int)ppri.size() != P ||
+        (int)pphase.size() != P || (int)pts.size() != P)
+        throw Error(KBHIP_EINVAL, "pod columns length mismatch");
+    auto pco = s.offs("p_ctr_off", P);
+    auto ccpu = s.vec<int64_t>("c_cpu"), cmem = s.vec<int64_t>("c_mem"), cgpu = s.vec<int64_t>("c_gpu");
+    auto chas = s.vec<uint8_t>("c_has");
+    auto cpo = s.offs("c_port_off", ccpu.size());
+    auto ptip = V32("pt_ip"), ptpr = V32("pt_proto"), ptpo = V32("pt_port");
+    auto pio = s.offs("p_ictr_off", P);
+    auto iccpu = s.vec<int64_t>("ic_cpu"), icmem = s.vec<int64_t>("ic_mem"), icgpu = s.vec<int64_t>("ic_gpu");
+    auto pso = s.offs("p_nsel_off", P);
+    auto psk = V32("ps_key"), psv = V32("ps_val");
+    auto pto = s.offs("p_tol_off", P);
+    auto tlk = V32("tl_key"), tlo = V32("tl_op"), tlv = V32("tl_val"), tle = V32("tl_effect");
+    auto a_flags = s.vec<uint8_t>("a_flags");
+    auto acnt = [&](const char* n) { return V32(n); };
+    auto pareq_c = acnt("a_pareq_cnt"), papref_c = acnt("a_papref_cnt"), paareq_c = acnt("a_paareq_cnt"),
+         paapref_c = acnt("a_paapref_cnt");
+    // inter-pod affinity is not implemented on the device yet: reject sessions
+    // in which any pod carries pod (anti-)affinity terms (scope).
+    for (size_t a = 0; a < a_flags.size(); ++a)
+        if (pareq_c[a] + papref_c[a] + paareq_c[a] + paapref_c[a] > 0)
+            fail_unsupported("pod (anti-)affinity terms are not supported by this engine build");
+
+    S.pods.resize(P);
+    vector<vector<int>> pod_ports(P);
+    vector<int64_t> pod_nzc(P, 0), pod_nzm(P, 0);
+    for (int i = 0; i < P; ++i) {
+        HPod& p = S.pods[i];
+        p.uid = s.s(puid[i]);
+        p.ns = E.nss.get(s.s(pns[i]));
+        string nn = s.s(pnode[i]);
+        int ph = pphase[i];
+        bool del = !pdel.empty() && pdel[i];
+        if (ph == KBS_RUNNING) p.status = del ? Releasing : Running;            // api/helpers.go:35-61
+        else if (ph == KBS_PENDING) p.status = del ? Releasing : (nn.empty() ? Pending : Bound);
+        else if (ph == KBS_SUCCEEDED) p.status = Succeeded;
+        else if (ph == KBS_FAILED) p.status = Failed;
+        else p.status = Unknown;
+        p.priority = ppri[i];
+        p.ts = pts[i];
+        p.backfill = !pbf.empty() && pbf[i];
+        for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
+            p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
+            pod_nzc[i] += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
+            pod_nzm[i] += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
+            for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
+                if (ptpo[q] <= 0) continue;  // HostPortInfo.Add ignores port <= 0
+                string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
+                if (ip.empty()) ip = "0.0.0.0";
+                if (pr.empty()) pr = "TCP";
+                auto key = std::make_tuple(E.ip_dict.get(ip), E.proto_dict.get(pr), (int32_t)ptpo[q]);
+                auto it = E.port_ids.find(key);
+                int id;
+                if (it == E.port_ids.end()) { id = (int)E.port_defs.size(); E.port_ids[key] = id; E.port_defs.push_back(key); }
+                else id = it->second;
+                pod_ports[i].push_back(id);
+            }
+        }
+        p.ireq = p.req;
+        for (int k = pio[i]; k < pio[i + 1]; ++k) {
+            p.ireq.c = std::max(p.ireq.c, iccpu[k]);
+            p.ireq.m = std::max(p.ireq.m, icmem[k]);
+            p.ireq.g = std::max(p.ireq.g, icgpu[k]);
+        }
+        if (!nn.empty()) {
+            auto it = node_idx.find(nn);
+            if (it == node_idx.end())
+                throw Error(KBHIP_EINVAL, "pod " + p.uid + " is bound to node " + nn + " which is not in the snapshot");
+            p.node = it->second;
+        }
+        if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
+            int n = p.node;
+            if (p.backfill) { bf[n].c += p.req.c; bf[n].m += p.req.m; bf[n].g += p.req.g; }
+            if (p.status == Releasing) {
+                rel[n].c += p.req.c; rel[n].m += p.req.m; rel[n].g += p.req.g;
+                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
+            } else {
+                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
+            }
+            S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+            podcnt[n]++;
+            nzc[n] += pod_nzc[i];
+            nzm[n] += pod_nzm[i];
+            for (int id : pod_ports[i]) node_ports[n].push_back(id);
+        }
+    }
+    for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
+
+    // ---------------- queues & jobs ----------------
+    auto qn = V32("q_name"), qw = V32("q_weight");
+    auto qts = s.vec<int64_t>("q_ts");
+    std::map<string, int> qidx;
+    S.queues.resize(qn.size());
+    for (size_t i = 0; i < qn.size(); ++i) {
+        S.queues[i].name = s.s(qn[i]);
+        S.queues[i].weight = qw[i];
+        S.queues[i].ts = qts.empty() ? 0 : qts[i];
+        qidx[S.queues[i].name] = (int)i;
+    }
+    auto jns = V32("j_ns"), jname = V32("j_name"), jq = V32("j_queue"), jmin = V32("j_min"), jpri = V32("j_pg_priority");
+    auto jts = s.vec<int64_t>("j_ts");
+    struct Src { string uid; int row, pod; };
+    vector<Src> srcs;
+    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
+    for (int i = 0; i < P; ++i) {
+        if (pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
+        if (pjob[i] < 0) srcs.push_back({S.pods[i].uid, -1, i});  // shadow PodGroup (cache/util.go:42-60)
+    }
+    std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+    vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
+    for (auto& src : srcs) {
+        string qname = src.row >= 0 ? s.s(jq[src.row]) : string("default");
+        auto qit = qidx.find(qname);
+        int slot = -1;
+        if (qit != qidx.end()) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
+            HJob j;
+            j.uid = src.uid;
+            j.queue = qit->second;
+            j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
+            j.ts = src.row >= 0 ? jts[src.row] : 0;
+            j.priority = src.row >= 0 ? jpri[src.row] : 0;
+            slot = (int)S.jobs.size();
+            S.jobs.push_back(j);
+        }
+        if (src.row >= 0) row_slot[src.row] = slot;
+        else shadow_slot[src.pod] = slot;
+    }
+    for (int i = 0; i < P; ++i) {
+        int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
+        S.pods[i].job = slot;
+        if (slot >= 0) S.jobs[slot].tasks.push_back(i);
+    }
+    for (auto& j : S.jobs)
+        for (int t : j.tasks) {
+            j.priority = S.pods[t].priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
+            if (allocated_status(S.pods[t].status)) j.cnt_alloc++;
+            if (S.pods[t].status == AOB) j.cnt_aob++;
+        }
+
+    // ---------------- task classes for pending tasks ----------------
+    // label columns: keys referenced by selectors / node affinity of pending tasks
+    auto es = V32("nst_expr_start"), ec = V32("nst_expr_cnt"), fs = V32("nst_field_start"), fc = V32("nst_field_cnt");
+    auto nsr_key = V32("nsr_key");
+    auto nsr_op = s.vec<uint8_t>("nsr_op");
+    auto nsr_voff = s.offs("nsr_val_off", nsr_key.size());
+    auto nsrv = V32("nsrv");
+    auto pst_w = V32("pst_weight"), pst_t = V32("pst_term");
+    auto nareq_s = acnt("a_nareq_start"), nareq_c = acnt("a_nareq_cnt"), napref_s = acnt("a_napref_start"),
+         napref_c = acnt("a_napref_cnt");
+    auto nsr_vals = [&](int row) {
+        vector<string> v;
+        for (int k = nsr_voff[row]; k < nsr_voff[row + 1]; ++k) v.push_back(s.s(nsrv[k]));
+        return v;
+    };
+    // A task is compiled into local tables (offsets relative to the task),
+    // hashed, and appended to the session tables only when its class is new.
+    struct Local {
+        vector<Req> reqs;
+        vector<Term> terms;
+        vector<int32_t> vals;
+    };
+    auto local_req = [&](Local& L, const string& key, int op, const vector<string>& values, Req* r) -> bool {
+        r->key = E.sel_key(key);
+        r->op = op;
+        r->nvals = 0;
+        r->val_off = (int32_t)L.vals.size();
+        r->rhs = 0;
+        switch (op) {  // labels.NewRequirement validation (selector.go:134-170)
+            case OP_IN:
+            case OP_NOTIN: if (values.empty()) return false; break;
+            case OP_EXISTS:
+            case OP_DNE: if (!values.empty()) return false; break;
+            case OP_GT:
+            case OP_LT: return values.size() == 1 && parse_int64(values[0], &r->rhs);
+            default: return false;
+        }
+        for (auto& v : values) L.vals.push_back(E.vals.get(v));
+        r->nvals = (int32_t)values.size();
+        return true;
+    };
+    auto local_false = [&](Local& L, int weight) {
+        Term t{(int32_t)L.reqs.size(), 1, weight, 0};
+        L.reqs.push_back(Req{0, OP_FALSE, 0, 0, 0});
+        L.terms.push_back(t);
+    };
+    // One NodeSelectorTerm.  required: MatchExpressions AND MatchFields
+    // (helper/helpers.go:302-333); preferred: MatchExpressions only
+    // (node_affinity.go:58-66).  *err: a preferred term's selector errors.
+    auto local_nst = [&](Local& L, int row, bool required, int weight, bool* err) {
+        if (required && ec[row] == 0 && fc[row] == 0) { local_false(L, weight); return; }  // empty term: nothing
+        if (!required && ec[row] == 0) { local_false(L, weight); return; }                // labels.Nothing()
+        vector<Req> rs;
+        bool bad = false;
+        for (int k = es[row]; k < es[row] + ec[row]; ++k) {
+            Req r;
+            int op = nsr_op[k];
+            if (op > OP_LT || !local_req(L, s.s(nsr_key[k]), op, nsr_vals(k), &r)) bad = true;
+            rs.push_back(r);
+        }
+        if (required) {
+            for (int k = fs[row]; k < fs[row] + fc[row]; ++k) {
+                vector<string> vs = nsr_vals(k);
+                int op = nsr_op[k];
+                if ((op != OP_IN && op != OP_NOTIN) || vs.size() != 1) { bad = true; continue; }
+                if (s.s(nsr_key[k]) == "metadata.name") {
+                    auto it = node_idx.find(vs[0]);
+                    rs.push_back(Req{0, op == OP_IN ? OP_NAME_IN : OP_NAME_NOTIN, 0,
+                                     it == node_idx.end() ? -1 : it->second, 0});
+                } else if ((op == OP_IN) != vs[0].empty()) {  // any other field reads ""
+                    rs.push_back(Req{0, OP_FALSE, 0, 0, 0});
+                }
+            }
+        }
+        if (bad) {
+            if (!required) { *err = true; return; }
+            local_false(L, weight);  // NodeSelectorRequirementsAsSelector error: the term `continue`s
+            return;
+        }
+        Term t{(int32_t)L.reqs.size(), (int32_t)rs.size(), weight, 0};
+        for (auto& r : rs) L.reqs.push_back(r);
+        L.terms.push_back(t);
+    };
+
+    std::unordered_map<string, int> class_ids;
+    for (int i = 0; i < P; ++i) {
+        HPod& p = S.pods[i];
+        if (p.status != Pending || p.job < 0) continue;
+        TaskClass c{};
+        c.ireq_cpu = p.ireq.c; c.ireq_mem = p.ireq.m; c.ireq_gpu = p.ireq.g;
+        c.req_cpu = p.req.c; c.req_mem = p.req.m; c.req_gpu = p.req.g;
+        c.nz_cpu = pod_nzc[i]; c.nz_mem = pod_nzm[i];
+        c.backfill = p.backfill;
+        c.nsel_term = -1;
+        c.req_term_n = -1;
+        Local L;
+        if (pso[i + 1] > pso[i]) {  // nodeSelector: labels.SelectorFromSet -> Equals requirements
+            Term t{(int32_t)L.reqs.size(), 0, 0, 0};
+            for (int k = pso[i]; k < pso[i + 1]; ++k) {
+                Req r;
+                local_req(L, s.s(psk[k]), OP_IN, {s.s(psv[k])}, &r);
+                L.reqs.push_back(r);
+                t.req_n++;
+            }
+            c.nsel_term = (int32_t)L.terms.size();
+            L.terms.push_back(t);
+        }
+        int a = paff.empty() ? -1 : paff[i];
+        if (a >= 0 && (a_flags[a] & KBS_AFF_NA)) {
+            if (a_flags[a] & KBS_AFF_NA_REQ) {
+                c.req_term_off = (int32_t)L.terms.size();
+                for (int k = nareq_s[a]; k < nareq_s[a] + nareq_c[a]; ++k) local_nst(L, k, true, 0, nullptr);
+                c.req_term_n = (int32_t)L.terms.size() - c.req_term_off;
+            }
+            c.pref_term_off = (int32_t)L.terms.size();
+            bool err = false;
+            for (int k = napref_s[a]; k < napref_s[a] + napref_c[a] && !err; ++k) {
+                if (pst_w[k] == 0) continue;  // node_affinity.go:54-56
+                local_nst(L, pst_t[k], false, pst_w[k], &err);
+            }
+            c.pref_term_n = (int32_t)L.terms.size() - c.pref_term_off;
+            if (err) { c.score_err = 1; c.pref_term_n = 0; }
+        }
+        // tolerations -> tolerated taint ids (toleration.go:37-56)
+        E.tw = ((int)E.taint_defs.size() + 63) / 64;
+        vector<uint64_t> tol(E.tw, 0);
+        for (size_t t = 0; t < E.taint_defs.size(); ++t) {
+            bool ok = false;
+            for (int k = pto[i]; k < pto[i + 1] && !ok; ++k) {
+                string key = s.s(tlk[k]), op = s.s(tlo[k]), val = s.s(tlv[k]), eff = s.s(tle[k]);
+                if (!eff.empty() && eff != std::get<2>(E.taint_defs[t])) continue;
+                if (!key.empty() && key != std::get<0>(E.taint_defs[t])) continue;
+                if (op.empty() || op == "Equal") ok = val == std::get<1>(E.taint_defs[t]);
+                else if (op == "Exists") ok = true;
+            }
+            if (ok) tol[t / 64] |= 1ULL << (t % 64);
+        }
+        c.has_ports = pod_ports[i].empty() ? 0 : 1;
+        // class signature: the task-relative tables + the class fields (offsets are local)
+        string sig((const char*)&c, sizeof(TaskClass));
+        sig.append((const char*)L.reqs.data(), L.reqs.size() * sizeof(Req));
+        sig.append((const char*)L.terms.data(), L.terms.size() * sizeof(Term));
+        sig.append((const char*)L.vals.data(), L.vals.size() * sizeof(int32_t));
+        sig.append((const char*)tol.data(), tol.size() * sizeof(uint64_t));
+        for (int id : pod_ports[i]) sig.append((const char*)&id, sizeof id);
+        auto it = class_ids.find(sig);
+        if (it != class_ids.end()) { p.cls = it->second; continue; }
+        // relocate into the session tables
+        const int32_t req0 = (int32_t)E.reqs.size(), term0 = (int32_t)E.terms.size(), val0 = (int32_t)E.vals_list.size();
+        for (Req r : L.reqs) {
+            if (r.op <= OP_LT) r.val_off += val0;
+            E.reqs.push_back(r);
+        }
+        for (Term t : L.terms) { t.req_off += req0; E.terms.push_back(t); }
+        for (int32_t v : L.vals) E.vals_list.push_back(v);
+        if (c.nsel_term >= 0) c.nsel_term += term0;
+        c.req_term_off += term0;
+        c.pref_term_off += term0;
+        c.tol_off = (int32_t)E.masks.size();
+        for (auto x : tol) E.masks.push_back(x);
+        p.cls = (int)S.classes.size();
+        class_ids.emplace(std::move(sig), p.cls);
+        S.classes.push_back(c);
+    }
+    // port masks per class (conflict = CheckConflict, own = HostPortInfo.Add)
+    if (E.port_defs.size() > 256) fail_unsupported("more than 256 distinct host ports");
+    E.pw = ((int)E.port_defs.size() + 63) / 64;
+    {
+        vector<int> cls_pod(S.classes.size(), -1);
+        for (int i = 0; i < P; ++i) if (S.pods[i].cls >= 0 && cls_pod[S.pods[i].cls] < 0) cls_pod[S.pods[i].cls] = i;
+        int zero_ip = E.ip_dict.get("0.0.0.0");
+        for (size_t ci = 0; ci < S.classes.size(); ++ci) {
+            TaskClass& c = S.classes[ci];
+            vector<uint64_t> conf(E.pw, 0), own(E.pw, 0);
+            for (int id : pod_ports[cls_pod[ci]]) {
+                auto [ip, pr, port] = E.port_defs[id];
+                own[id / 64] |= 1ULL << (id % 64);
+                for (size_t u = 0; u < E.port_defs.size(); ++u) {
+                    auto [uip, upr, uport] = E.port_defs[u];
+                    if (upr != pr || uport != port) continue;
+                    if (ip == zero_ip || uip == zero_ip || uip == ip) conf[u / 64] |= 1ULL << (u % 64);
+                }
+            }
+            c.pconf_off = (int32_t)E.masks.size();
+            for (auto x : conf) E.masks.push_back(x);
+            c.pown_off = (int32_t)E.masks.size();
+            for (auto x : own) E.masks.push_back(x);
+        }
+    }
+    // ---------------- upload ----------------
+    HIPCHK(hipSetDevice(device));
+    S.device = device;
+    HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+    hipStream_t st = S.stream;
+    auto pad64 = [&](const vector<int64_t>& v) { vector<int64_t> o(npad, 0); std::copy(v.begin(), v.end(), o.begin()); return o; };
+    vector<int64_t> col[13];
+    for (int i = 0; i < 13; ++i) col[i].assign(npad, 0);
+    for (int i = 0; i < N; ++i) {
+        col[0][i] = idle[i].c; col[1][i] = idle[i].m; col[2][i] = idle[i].g;
+        col[3][i] = rel[i].c; col[4][i] = rel[i].m; col[5][i] = rel[i].g;
+        col[6][i] = bf[i].c; col[7][i] = bf[i].m; col[8][i] = bf[i].g;
+        col[9][i] = acpu[i]; col[10][i] = amem[i]; col[11][i] = nzc[i]; col[12][i] = nzm[i];
+    }
+    (void)pad64;
+    int64_t** dst[13] = {&S.nc.idle_cpu, &S.nc.idle_mem, &S.nc.idle_gpu, &S.nc.rel_cpu, &S.nc.rel_mem, &S.nc.rel_gpu,
+                         &S.nc.bf_cpu, &S.nc.bf_mem, &S.nc.bf_gpu, &S.nc.acpu, &S.nc.amem, &S.nc.nzc, &S.nc.nzm};
+    for (int i = 0; i < 13; ++i) *dst[i] = upload(S.b_cols[i], col[i], st);
+    vector<int32_t> pods_col(npad, 0), max_col(npad, 0);
+    vector<uint8_t> flags_col(npad, 0);
+    for (int i = 0; i < N; ++i) {
+        pods_col[i] = podcnt[i];
+        max_col[i] = (int32_t)apods[i];
+        flags_col[i] = (!unsched.empty() && unsched[i]) ? 1 : 0;
+    }
+    S.nc.pods = upload(S.b_cols[13], pods_col, st);
+    S.nc.maxtasks = upload(S.b_cols[14], max_col, st);
+    S.nc.flags = upload(S.b_cols[15], flags_col, st);
+    const int K = (int)E.sel_keys.size();
+    vector<int32_t> lab((size_t)std::max(K, 1) * npad, -1);
+    for (auto& kv : E.sel_keys) {
+        auto kit = E.keys_all.ids.find(kv.first);
+        if (kit == E.keys_all.ids.end()) continue;  // no node has the key
+        int kid = kit->second;
+        for (int i = 0; i < N; ++i)
+            for (auto& lv2 : E.node_labels[i])
+                if (lv2.first == kid) lab[(size_t)kv.second * npad + i] = lv2.second;
+    }
+    S.nc.labels = upload(S.b_labels, lab, st);
+    vector<uint64_t> tcol((size_t)std::max(E.tw, 1) * npad, 0);
+    for (int i = 0; i < N; ++i)
+        for (int id : node_taints[i]) tcol[(size_t)(id / 64) * npad + i] |= 1ULL << (id % 64);
+    S.nc.taints = upload(S.b_taints, tcol, st);
+    vector<uint64_t> pcol((size_t)std::max(E.pw, 1) * npad, 0);
+    for (int i = 0; i < N; ++i)
+        for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npad + i] |= 1ULL << (id % 64);
+    S.nc.ports = upload(S.b_ports, pcol, st);
+    S.nc.n = N;
+    S.nc.npad = npad;
+    S.nc.n_keys = K;
+    S.nc.taint_words = E.tw;
+    S.nc.port_words = E.pw;
+    // value tables (Gt/Lt parse per value id)
+    vector<int64_t> valint(E.vals.strs.size() + 1, 0);
+    vector<uint8_t> valok(E.vals.strs.size() + 1, 0);
+    for (size_t v = 0; v < E.vals.strs.size(); ++v) valok[v] = parse_int64(E.vals.strs[v], &valint[v]);
+    S.tab.classes = upload(S.b_classes, S.classes, st);
+    S.tab.terms = upload(S.b_terms, E.terms, st);
+    S.tab.reqs = upload(S.b_reqs, E.reqs, st);
+    S.tab.vals = upload(S.b_vals, E.vals_list, st);
+    S.tab.valint = upload(S.b_valint, valint, st);
+    S.tab.valok = upload(S.b_valok, valok, st);
+    S.tab.masks = upload(S.b_masks, E.masks, st);
+    S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
+    HIPCHK(hipHostMalloc((void**)&S.h_ctrl, sizeof(PopCtrl), hipHostMallocDefault));
+    int R;
+    int nb = topk_blocks(N, &R);
+    S.d_cand = S.b_cand.alloc<uint64_t>((size_t)nb * kTopK);
+    S.d_walk = S.b_walk.alloc<uint64_t>(npad);
+    HIPCHK(hipStreamSynchronize(st));
+    // ---------------- ordering plugins OnSessionOpen ----------------
+    for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
+    S.stats.nodes = N;
+    S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ---------------------------------------------------------------------------
+// device driver for one job pop
+// ---------------------------------------------------------------------------
+static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
+                     int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop) {
+    int done = 0, stop = KBHIP_STOP_ALL;
+    for (int i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= (int)S.pods.size() || S.pods[ids[i]].cls < 0)
+            throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
+    while (done < n) {
+        const int cls0 = S.pods[ids[done]].cls;
+        int m = 1;
+        while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
+        const TaskClass& c = S.classes[cls0];
+        const bool batch = S.batched && !S.any_bf && !c.backfill && S.nc.port_words <= 4;
+        if (!batch) {  // general path: take up to a chunk of mixed classes
+            m = std::min(n - done, kMaxChunk);
+        }
+        PopCtrl& h = *S.h_ctrl;
+        h.stop = -1;
+        h.n_done = 0;
+        h.ready_count = ready_count;
+        h.min_avail = min_avail;
+        h.gang_mode = gang_mode;
+        h.n_tasks = m;
+        h.any_bf = S.any_bf;
+        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
+        std::memset(h.arrive, 0, sizeof h.arrive);
+        std::memset(h.slot, 0, sizeof h.slot);
+        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+        // sampled HIP-event timing of the sweep launch (kbhip_set_option "time_every")
+        const bool timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
+        if (timed) {
+            if (!S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
+            HIPCHK(hipEventRecord(S.ev0, S.stream));
+        }
+        if (batch) {
+            HIPCHK(launch_sweep_topk(S.conf, S.nc, S.tab, S.d_ctrl, S.d_cand, S.stream));
+            if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
+            HIPCHK(launch_place_batch(S.conf, S.nc, S.tab, S.d_ctrl, S.d_cand, S.stream));
+            S.stats.sweeps += 1;
+            S.stats.batched_pops += 1;
+        } else {
+            for (int i = 0; i < m; ++i) {
+                HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
+                if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
+            }
+            S.stats.sweeps += m;
+        }
+        S.sweep_launches++;
+        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+        if (timed) {
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, S.ev0, S.ev1));
+            S.timed_ms += ms;
+            S.timed_n++;
+        }
+        if (h.stop < 0 || h.n_done < 1 || h.n_done > m) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+        for (int i = 0; i < h.n_done; ++i) {
+            out_node[done + i] = h.res_node[i];
+            out_kind[done + i] = (uint8_t)h.res_kind[i];
+            const int node = h.res_node[i];
+            if (node >= 0) {
+                HPod& p = S.pods[ids[done + i]];
+                S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+            }
+        }
+        S.any_bf = h.any_bf;
+        ready_count = h.ready_count;
+        done += h.n_done;
+        stop = h.stop;
+        if (stop != KBHIP_STOP_ALL) break;
+    }
+    *out_n_done = done;
+    *out_stop = stop;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// allocate action with the Go framework's ordering (host mirror)
+// ---------------------------------------------------------------------------
+template <typename L>
+struct GoHeap {  // container/heap over util.PriorityQueue (util/priority_queue.go:25-88)
+    vector<int> items;
+    L less;
+    explicit GoHeap(L l) : less(l) {}
+    bool Less(int i, int j) { return less(items[i], items[j]); }
+    void up(int j) {
+        for (;;) {
+            int i = (j - 1) / 2;
+            if (i == j || !Less(j, i)) break;
+            std::swap(items[i], items[j]);
+            j = i;
+        }
+    }
+    void down(int i, int n) {
+        for (;;) {
+            int j1 = 2 * i + 1;
+            if (j1 >= n || j1 < 0) break;
+            int j = j1, j2 = j1 + 1;
+            if (j2 < n && Less(j2, j1)) j = j2;
+            if (!Less(j, i)) break;
+            std::swap(items[i], items[j]);
+            i = j;
+        }
+    }
+    void push(int x) { items.push_back(x); up((int)items.size() - 1); }
+    int pop() {
+        int n = (int)items.size() - 1;
+        std::swap(items[0], items[n]);
+        down(0, n);
+        int x = items.back();
+        items.pop_back();
+        return x;
+    }
+    bool empty() const { return items.empty(); }
+};
+
+struct Allocator {
+    Session& S;
+    explicit Allocator(Session& s) : S(s) {}
+
+    int readiness(const HJob& j) const {  // job_info.go:374-388
+        if (j.cnt_alloc >= j.min_avail) return 1;
+        if (j.cnt_alloc + j.cnt_aob >= j.min_avail) return 2;
+        return 4;
+    }
+    bool job_ready(const HJob& j) const { return !S.gang_ready || readiness(j) == 1; }  // session_plugins.go:167-186
+    bool job_less(int l, int r) const {  // session_plugins.go:244-268
+        const HJob &L = S.jobs[l], &R = S.jobs[r];
+        for (auto& tier : S.tiers)
+            for (auto& p : tier) {
+                if (p.flags & KBS_DIS_JOBORDER) continue;
+                int c;
+                if (p.name == "priority") c = L.priority > R.priority ? -1 : L.priority < R.priority ? 1 : 0;  // priority.go:60-76
+                else if (p.name == "gang") {  // gang.go:136-160
+                    bool lr = readiness(L) == 1, rr = readiness(R) == 1;
+                    c = (lr && rr) ? 0 : lr ? 1 : rr ? -1 : 0;
+                } else if (p.name == "drf") c = L.drf_share == R.drf_share ? 0 : L.drf_share < R.drf_share ? -1 : 1;  // drf.go:113-129
+                else continue;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.uid < R.uid;
+        return L.ts < R.ts;
+    }
+    bool queue_less(int l, int r) const {  // session_plugins.go:270-295, proportion.go:144-157
+        const HQueue &L = S.queues[l], &R = S.queues[r];
+        for (auto& tier : S.tiers)
+            for (auto& p : tier) {
+                if ((p.flags & KBS_DIS_QUEUEORDER) || p.name != "proportion") continue;
+                int c = L.share == R.share ? 0 : L.share < R.share ? -1 : 1;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.name < R.name;
+        return L.ts < R.ts;
+    }
+    bool task_less(int l, int r) const {  // session_plugins.go:297-329, priority.go:39-55
+        const HPod &L = S.pods[l], &R = S.pods[r];
+        for (auto& tier : S.tiers)
+            for (auto& p : tier) {
+                if ((p.flags & KBS_DIS_TASKORDER) || p.name != "priority") continue;
+                int c = L.priority == R.priority ? 0 : L.priority > R.priority ? -1 : 1;
+                if (c != 0) return c < 0;
+            }
+        if (L.ts == R.ts) return L.uid < R.uid;
+        return L.ts < R.ts;
+    }
+    void drf_update(HJob& j) {  // drf.go:156-170
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double x = share(j.drf_alloc.get(k), S.total.get(k)); if (x > res) res = x; }
+        j.drf_share = res;
+    }
+    void prop_update(HQueue& q) {  // proportion.go:229-241
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double x = share(q.allocated.get(k), q.deserved.get(k)); if (x > res) res = x; }
+        q.share = res;
+    }
+    void open_plugins() {
+        if (S.drf_on)
+            for (auto& j : S.jobs) {  // drf.go:65-82
+                for (int t : j.tasks) if (allocated_status(S.pods[t].status)) j.drf_alloc.add(S.pods[t].req);
+                drf_update(j);
+            }
+        if (S.prop_on) {  // proportion.go:65-142
+            for (auto& j : S.jobs) {
+                HQueue& q = S.queues[j.queue];
+                q.has_attr = true;
+                for (int t : j.tasks) {
+                    const HPod& p = S.pods[t];
+                    if (allocated_status(p.status)) { q.allocated.add(p.req); q.request.add(p.req); }
+                    else if (p.status == Pending) q.request.add(p.req);
+                }
+            }
+            vector<int> order;
+            for (size_t i = 0; i < S.queues.size(); ++i) if (S.queues[i].has_attr) order.push_back((int)i);
+            F3 remaining = S.total;
+            vector<char> meet(S.queues.size(), 0);
+            for (;;) {
+                int32_t tw = 0;
+                for (int q : order) if (!meet[q]) tw += S.queues[q].weight;
+                if (tw == 0) break;
+                F3 deserved;
+                for (int qi : order) {
+                    if (meet[qi]) continue;
+                    HQueue& q = S.queues[qi];
+                    const double ratio = (double)q.weight / (double)tw;
+                    F3 r = remaining;
+                    r.c *= ratio; r.m *= ratio; r.g *= ratio;
+                    q.deserved.addf(r);
+                    if (!q.deserved.less_equal(q.request)) {  // helpers.Min
+                        q.deserved.c = std::fmin(q.deserved.c, q.request.c);
+                        q.deserved.g = std::fmin(q.deserved.g, q.request.g);
+                        q.deserved.m = std::fmin(q.deserved.m, q.request.m);
+                        meet[qi] = 1;
+                    }
+                    prop_update(q);
+                    deserved.addf(q.deserved);
+                }
+                remaining.subf(deserved);
+                if (remaining.empty()) break;
+            }
+        }
+    }
+    bool overused(int qi) const {  // proportion.go:186-197
+        if (!S.prop_on) return false;
+        return S.queues[qi].deserved.less_equal(S.queues[qi].allocated);
+    }
+    void on_allocate(int pi) {  // event handlers drf.go:134-143, proportion.go:200-210
+        const HPod& p = S.pods[pi];
+        HJob& j = S.jobs[p.job];
+        if (S.drf_on) { j.drf_alloc.add(p.req); drf_update(j); }
+        if (S.prop_on) { HQueue& q = S.queues[j.queue]; q.allocated.add(p.req); prop_update(q); }
+    }
+
+    void run() {  // allocate.go:41-201
+        auto t0 = std::chrono::steady_clock::now();
+        open_plugins();
+        auto ql = [this](int a, int b) { return queue_less(a, b); };
+        auto jl = [this](int a, int b) { return job_less(a, b); };
+        GoHeap<decltype(ql)> queues(ql);
+        std::map<int, GoHeap<decltype(jl)>> jobs_map;
+        for (size_t j = 0; j < S.jobs.size(); ++j) {
+            int q = S.jobs[j].queue;
+            queues.push(q);
+            auto it = jobs_map.find(q);
+            if (it == jobs_map.end()) it = jobs_map.emplace(q, GoHeap<decltype(jl)>(jl)).first;
+            it->second.push((int)j);
+        }
+        vector<int32_t> ids, onode;
+        vector<uint8_t> okind;
+        while (!queues.empty()) {
+            int q = queues.pop();
+            if (overused(q)) continue;
+            auto jit = jobs_map.find(q);
+            if (jit == jobs_map.end() || jit->second.empty()) continue;
+            int jb = jit->second.pop();
+            HJob& job = S.jobs[jb];
+            S.stats.pops++;
+            if (!job.pending_built) {  // allocate.go:91-104; TaskOrderFn is a strict total order
+                for (int t : job.tasks) {
+                    const HPod& p = S.pods[t];
+                    if (p.status != Pending) continue;
+                    if (p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU) continue;  // BestEffort
+                    job.pending.push_back(t);
+                }
+                std::sort(job.pending.begin(), job.pending.end(), [this](int a, int b) { return task_less(a, b); });
+                job.pending_built = true;
+            }
+            if (job.cursor < job.pending.size()) {
+                int n = (int)(job.pending.size() - job.cursor);
+                ids.assign(job.pending.begin() + job.cursor, job.pending.end());
+                onode.assign(n, -1);
+                okind.assign(n, 0);
+                int32_t n_done = 0, stop = 0;
+                place_job(S, ids.data(), n, S.gang_ready ? 1 : 0, job.min_avail, job.cnt_alloc, onode.data(),
+                          okind.data(), &n_done, &stop);
+                S.stats.tasks += n_done;
+                for (int i = 0; i < n_done; ++i) {
+                    const int pi = ids[i];
+                    if (onode[i] < 0) continue;
+                    HPod& p = S.pods[pi];
+                    p.node = onode[i];
+                    if (okind[i] == KBHIP_ALLOCATED) { p.status = Allocated; job.cnt_alloc++; }
+                    else p.status = Pipelined;
+                    on_allocate(pi);
+                    S.log.emplace_back(pi, onode[i], okind[i]);
+                    S.stats.placed++;
+                    if (p.status == Allocated && job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-294)
+                        for (int t : job.tasks) if (S.pods[t].status == Allocated) S.pods[t].status = Binding;
+                }
+                job.cursor += n_done;
+                if (stop == KBHIP_STOP_READY) jit->second.push(jb);
+            }
+            queues.push(q);
+        }
+        S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+};
+
+static int device_count() {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        g_err = string("hipGetDeviceCount: ") + hipGetErrorString(e);
+        return KBHIP_ENODEV;
+    }
+    int ok = 0;
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, i) != hipSuccess) continue;
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ok++;
+    }
+    return ok;
+}
+
+}  // namespace kbhip
+
+using namespace kbhip;
+
+#define ABI_GUARD(...)                                       \
+    try {                                                    \
+        __VA_ARGS__                                          \
+    } catch (kbhip::Error & e) {                             \
+        kbhip::g_err = e.what();                             \
+        return e.code;                                       \
+    } catch (std::exception & e) {                           \
+        kbhip::g_err = e.what();                             \
+        return KBHIP_EINVAL;                                 \
+    } catch (...) {                                          \
+        kbhip::g_err = "unknown error";                      \
+        return KBHIP_EINVAL;                                 \
+    }
+
+extern "C" {
+
+struct kb_session {
+    kbhip::Session s;
+};
+
+const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
+
+int kbhip_device_count(void) { ABI_GUARD(return kbhip::device_count();) }
+
+static int open_common(const kbs::Snapshot& snap, int device, kb_session** out) {
+    int nd = kbhip::device_count();
+    if (nd <= 0) throw kbhip::Error(KBHIP_ENODEV, "no gfx950 HIP device available");
+    if (device < 0 || device >= nd) throw kbhip::Error(KBHIP_EINVAL, "device index out of range");
+    std::unique_ptr<kb_session> s(new kb_session());
+    kbhip::open_session(s->s, snap, device);
+    *out = s.release();
+    return KBHIP_OK;
+}
+
+int kbhip_session_open(const void* bytes, size_t len, int device, kb_session** out) {
+    ABI_GUARD({
+        if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbs::Snapshot snap;
+        snap.load_bytes(bytes, len);
+        return open_common(snap, device, out);
+    })
+}
+
+int kbhip_session_open_file(const char* path, int device, kb_session** out) {
+    ABI_GUARD({
+        if (!path || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbs::Snapshot snap(path);
+        return open_common(snap, device, out);
+    })
+}
+
+int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode, int32_t min_available,
+                    int32_t ready_count, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                    int32_t* out_stop_reason) {
+    ABI_GUARD({
+        if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
+            throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
+                                out_n_done, out_stop_reason);
+    })
+}
+
+int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        HIPCHK(hipSetDevice(s->s.device));
+        s->s.log.clear();
+        kbhip::Allocator a(s->s);
+        a.run();
+        const int64_t n = (int64_t)s->s.log.size();
+        for (int64_t i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(s->s.log[i]);
+            out_node[i] = std::get<1>(s->s.log[i]);
+            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
+        }
+        return (int)n;
+    })
+}
+
+int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
+    ABI_GUARD({
+        if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::Session& S = s->s;
+        const int N = S.nc.n;
+        if (n_nodes < N) throw kbhip::Error(KBHIP_EINVAL, "output too small");
+        HIPCHK(hipSetDevice(S.device));
+        vector<int64_t> buf[9];
+        int64_t* src[9] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem,
+                           S.nc.rel_gpu, S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu};
+        for (int k = 0; k < 9; ++k) {
+            buf[k].resize(N);
+            if (N) HIPCHK(hipMemcpy(buf[k].data(), src[k], N * sizeof(int64_t), hipMemcpyDeviceToHost));
+        }
+        for (int i = 0; i < N; ++i) {
+            int64_t* o = out + (int64_t)i * 12;
+            o[0] = buf[0][i]; o[1] = buf[1][i]; o[2] = buf[2][i];
+            o[3] = S.used[i].c; o[4] = S.used[i].m; o[5] = S.used[i].g;
+            o[6] = buf[3][i]; o[7] = buf[4][i]; o[8] = buf[5][i];
+            o[9] = buf[6][i]; o[10] = buf[7][i]; o[11] = buf[8][i];
+        }
+        return N;
+    })
+}
+
+int kbhip_get_stats(kb_session* s, kbhip_stats* out) {
+    ABI_GUARD({
+        if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        *out = s->s.stats;
+        out->device_s = s->s.timed_ms * 1e-3;
+        out->timed_launches = s->s.timed_n;
+        return KBHIP_OK;
+    })
+}
+
+int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
+    ABI_GUARD({
+        if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
+        else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);
+        return KBHIP_OK;
+    })
+}
+
+int kbhip_session_close(kb_session* s) {
+    ABI_GUARD({
+        delete s;
+        return KBHIP_OK;
+    })
+}
+
+}  // extern "C"

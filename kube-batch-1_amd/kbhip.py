@@ -1,0 +1,148 @@
+"""kbhip — Python binding of libkbhip.so (the MI355X placement engine).
+
+This is the host-side mirror of the reference's plugin boundary for callers
+that are not Go (tests, bench): it loads the in-tree ``_build/libkbhip.so`` and
+exposes the C ABI of include/kbhip.h.  There is no fallback: if the library or
+a gfx950 device is missing, calls raise ``KbhipError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libkbhip.so")
+
+ALLOCATED, PIPELINED = 1, 2
+STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
+
+# int kbhip_* entry points declared by include/kbhip.h
+EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file", "kbhip_place_job",
+           "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
+           "kbhip_session_close", "kbhip_last_error")
+
+
+class KbhipError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("open_s", ctypes.c_double), ("allocate_s", ctypes.c_double), ("device_s", ctypes.c_double),
+                ("pops", ctypes.c_int64), ("tasks", ctypes.c_int64), ("placed", ctypes.c_int64),
+                ("sweeps", ctypes.c_int64), ("batched_pops", ctypes.c_int64), ("nodes", ctypes.c_int64),
+                ("timed_launches", ctypes.c_int64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def build() -> str:
+    """Compile libkbhip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise KbhipError(f"{LIB_PATH} is missing: run kbhip.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+        L.kbhip_last_error.restype = ctypes.c_char_p
+        L.kbhip_device_count.restype = ctypes.c_int
+        L.kbhip_session_open.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(vp)]
+        L.kbhip_session_open_file.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
+        L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
+        L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_read_nodes.argtypes = [vp, vp, i64]
+        L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+        L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
+        L.kbhip_session_close.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc: int) -> int:
+    if rc < 0:
+        raise KbhipError(f"kbhip error {rc}: {lib().kbhip_last_error().decode()}")
+    return rc
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count() -> int:
+    return _check(lib().kbhip_device_count())
+
+
+class Session:
+    """One scheduling session on one GPU (framework.Session equivalent)."""
+
+    def __init__(self, snapshot, device: int = 0):
+        self._h = ctypes.c_void_p()
+        if isinstance(snapshot, (bytes, bytearray, memoryview)):
+            buf = bytes(snapshot)
+            _check(lib().kbhip_session_open(ctypes.c_char_p(buf), len(buf), device, ctypes.byref(self._h)))
+        else:
+            _check(lib().kbhip_session_open_file(str(snapshot).encode(), device, ctypes.byref(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            _check(lib().kbhip_session_close(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, key: str, value: int) -> None:
+        _check(lib().kbhip_set_option(self._h, key.encode(), int(value)))
+
+    def allocate(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Run allocateAction.Execute; returns (pod, node, kind) in decision order."""
+        pod = np.zeros(cap, np.int32)
+        node = np.zeros(cap, np.int32)
+        kind = np.zeros(cap, np.uint8)
+        n = _check(lib().kbhip_allocate(self._h, _p(pod), _p(node), _p(kind), cap))
+        if n > cap:
+            raise KbhipError("placement log larger than cap")
+        return pod[:n].copy(), node[:n].copy(), kind[:n].copy()
+
+    def place_job(self, task_ids, gang_mode: int, min_available: int, ready_count: int):
+        ids = np.ascontiguousarray(task_ids, dtype=np.int32)
+        n = ids.size
+        node = np.full(max(n, 1), -1, np.int32)
+        kind = np.zeros(max(n, 1), np.uint8)
+        done = np.zeros(1, np.int32)
+        stop = np.zeros(1, np.int32)
+        _check(lib().kbhip_place_job(self._h, _p(ids), n, gang_mode, min_available, ready_count, _p(node),
+                                     _p(kind), _p(done), _p(stop)))
+        d = int(done[0])
+        return node[:d].copy(), kind[:d].copy(), int(stop[0])
+
+    def read_nodes(self, n_nodes: int) -> np.ndarray:
+        out = np.zeros((n_nodes, 12), np.int64)
+        _check(lib().kbhip_read_nodes(self._h, _p(out), n_nodes))
+        return out
+
+    def stats(self) -> dict:
+        st = Stats()
+        _check(lib().kbhip_get_stats(self._h, ctypes.byref(st)))
+        return st.as_dict()

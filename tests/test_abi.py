@@ -1,0 +1,41 @@
+"""The C ABI library builds for gfx950, loads, and exports exactly what
+include/kbhip.h declares (no compute calls here: this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "kbhip.h")).read()
+    return sorted(set(re.findall(r"\b(kbhip_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_abi():
+    import kbhip
+    assert set(_declared()) == set(kbhip.EXPORTS)
+
+
+def test_library_exports_every_symbol(engine_lib):
+    for name in _declared():
+        assert hasattr(engine_lib, name), name
+
+
+def test_library_contains_gfx950_code_object():
+    import kbhip
+    data = open(kbhip.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_device_is_an_error_not_a_fallback(engine_lib):
+    """Without a usable gfx950 device every session open fails loudly."""
+    import kbhip
+    n = engine_lib.kbhip_device_count()
+    if n >= 1:
+        return  # on the GPU box this is covered by the gpu tests
+    h = ctypes.c_void_p()
+    rc = engine_lib.kbhip_session_open_file(os.path.join(HERE, "golden", "c1_default.kbs").encode(), 0,
+                                            ctypes.byref(h))
+    assert rc == -2  # KBHIP_ENODEV
