@@ -15,7 +15,7 @@ the max-over-ranks time).  This round every rank runs an independent replica
 session on its own GPU (node-array sharding is the next step).
 
 Also reported:
-* roofline of the sweep kernel (k_sweep_topk): algorithmic bytes = nodes x
+* roofline of the fused pop kernel (k_pop_batch: sweep + top-64 + placement): algorithmic bytes = nodes x
   113 B per launch / its mean duration measured with HIP
   events on the engine's stream during the timed steps;
 * cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
@@ -185,7 +185,7 @@ def main():
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
-        "roofline": {"kernel": "k_sweep_topk", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": "k_pop_batch", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "mean_launch_us": sweep_us, "timed_launches": sweeps_n,
                      "bytes_per_launch": nodes * B_NODE},

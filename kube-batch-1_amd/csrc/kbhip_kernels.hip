@@ -395,6 +395,198 @@ __global__ __launch_bounds__(kPlaceThreads) void k_place_batch(Conf cf, NodeCols
 }
 
 // ---------------------------------------------------------------------------
+// batched path v2: one launch per pop chunk
+// ---------------------------------------------------------------------------
+// Wave-level sorting on registers: lane i holds one u64; descending order.
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint64_t o = __shfl_xor(v, j, 64);
+            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
+            v = keep_max ? (o > v ? o : v) : (o < v ? o : v);
+        }
+    }
+    return v;
+}
+// Top-64 of two descending lists (lane i holds a[i], b[i]); result descending.
+__device__ __forceinline__ uint64_t wave_merge_desc(uint64_t a, uint64_t b) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t br = __shfl(b, 63 - lane, 64);
+    uint64_t v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) {
+        const uint64_t o = __shfl_xor(v, j, 64);
+        v = ((lane & j) == 0) ? (o > v ? o : v) : (o < v ? o : v);
+    }
+    return v;
+}
+
+struct PopOut {  // written by the device into pinned host memory
+    int32_t stop, n_done, ready_count, pad;
+    int32_t res_node[kMaxChunk];
+    int32_t res_kind[kMaxChunk];
+};
+
+struct PopArgs {
+    int32_t cls, n_tasks, gang_mode, min_avail, ready_count, pad;
+};
+
+constexpr int kPopThreads = 512;  // 8 waves
+constexpr int kDepth = 3;         // post-commit keys precomputed per candidate
+
+__device__ __forceinline__ Row apply_commits(Row r, const TaskClass& c, int na, int np) {
+    r.idle_cpu -= na * c.req_cpu; r.idle_mem -= na * c.req_mem; r.idle_gpu -= na * c.req_gpu;
+    r.rel_cpu -= np * c.req_cpu; r.rel_mem -= np * c.req_mem; r.rel_gpu -= np * c.req_gpu;
+    const int n = na + np;
+    r.pods += n;
+    r.nzc += n * c.nz_cpu;
+    r.nzm += n * c.nz_mem;
+    return r;
+}
+
+template <int R>
+__global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
+                                                           uint64_t* cand, uint32_t* arrive, PopOut* out) {
+    __shared__ uint64_t wl[kPopThreads / 64][64];
+    __shared__ int last;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const TaskClass c = t.classes[a.cls];
+    // 1. evaluate R nodes per lane, wave top-64, block top-64
+    uint64_t best = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
+        uint64_t k = 0;
+        if (n < nc.n) {
+            int32_t s;
+            bool passed;
+            k = eval_node(cf, c, t, nc, n, &s, &passed);
+        }
+        k = wave_sort_desc(k);
+        best = r == 0 ? k : wave_merge_desc(best, k);
+    }
+    wl[wave][lane] = best;
+    __syncthreads();
+    if (wave == 0) {
+        uint64_t v = wl[0][lane];
+#pragma unroll
+        for (int w = 1; w < kPopThreads / 64; ++w) v = wave_merge_desc(v, wl[w][lane]);
+        cand[(int64_t)blockIdx.x * 64 + lane] = v;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(arrive, 1u) == gridDim.x - 1;
+        __threadfence();
+    }
+    __syncthreads();
+    if (!last) return;
+    // 2. last block: merge every block's list (8 waves, strided), then the 8 partials
+    {
+        uint64_t acc = 0;
+        int b = wave;
+        uint64_t nxt = b < (int)gridDim.x ? cand[(int64_t)b * 64 + lane] : 0;
+        while (b < (int)gridDim.x) {
+            const uint64_t cur = nxt;
+            const int bn = b + kPopThreads / 64;
+            nxt = bn < (int)gridDim.x ? cand[(int64_t)bn * 64 + lane] : 0;
+            acc = wave_merge_desc(acc, cur);
+            b = bn;
+        }
+        wl[wave][lane] = acc;
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    if (lane == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    uint64_t K = wl[0][lane];
+#pragma unroll
+    for (int w = 1; w < kPopThreads / 64; ++w) K = wave_merge_desc(K, wl[w][lane]);
+    // 3. placement: lane j owns candidate j (node n, key K).  Winner of each
+    // task = max over lanes of the current key (unchanged candidates keep
+    // their sweep key; the list is sorted, so its first unchanged entry is the
+    // best unchanged node anywhere).
+    const int n = K ? key_idx(K) : -1;
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (n >= 0) {
+        base = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+    }
+    uint64_t pwc[4];  // ports after one or more commits of this class
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    uint64_t chain[kDepth];
+    {
+        uint64_t cur = K;
+        int na = 0, np = 0;
+#pragma unroll
+        for (int d = 0; d < kDepth; ++d) {
+            if (cur) {
+                if (key_kind(cur) == 1) ++na; else ++np;
+                const Row r = apply_commits(base, c, na, np);
+                int32_t s;
+                bool passed;
+                cur = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+            }
+            chain[d] = cur;
+        }
+    }
+    uint64_t val = K;
+    int na = 0, np = 0;
+    int ready = a.ready_count, stop = -1, done = 0;
+    uint64_t mine = 0;  // lane i: winner key of task i
+    for (int i = 0; i < a.n_tasks; ++i) {
+        const uint64_t w = wave_max_u64(val);
+        done = i + 1;
+        if (!w) { stop = 1; break; }
+        if (lane == i) mine = w;
+        const int kind = key_kind(w);
+        if (val == w) {  // the winning lane (keys are unique)
+            if (kind == 1) ++na; else ++np;
+            const int cc = na + np;
+            if (cc <= kDepth) {
+                uint64_t x = chain[0];
+#pragma unroll
+                for (int d = 1; d < kDepth; ++d) if (cc == d + 1) x = chain[d];
+                val = x;
+            } else {
+                const Row r = apply_commits(base, c, na, np);
+                int32_t s;
+                bool passed;
+                val = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+            }
+        }
+        if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+        if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
+        if (i + 1 == a.n_tasks) stop = 0;
+    }
+    // 4. write back committed rows and the results
+    if (na + np > 0) {
+        const Row r = apply_commits(base, c, na, np);
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+    }
+    if (lane < done) {
+        out->res_node[lane] = mine ? key_idx(mine) : -1;
+        out->res_kind[lane] = mine ? key_kind(mine) : 0;
+    }
+    if (lane == 0) {
+        out->n_done = done;
+        out->stop = stop;
+        out->ready_count = ready;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
@@ -436,5 +628,31 @@ hipError_t launch_place_batch(const Conf& cf, const NodeCols& nc, const DevTable
     hipLaunchKernelGGL(k_place_batch, dim3(1), dim3(kPlaceThreads), 0, st, cf, nc, t, ctrl, cand, nb * kTopK);
     return hipGetLastError();
 }
+
+int pop_blocks(int n_nodes, int* R_out) {
+    int R = 1;
+    while ((int64_t)kPopThreads * R * 512 < n_nodes && R < 16) R <<= 1;
+    *R_out = R;
+    return (n_nodes + kPopThreads * R - 1) / (kPopThreads * R);
+}
+
+hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                            int gang_mode, int min_avail, int ready_count, uint64_t* cand, uint32_t* arrive,
+                            void* out_dev, hipStream_t st) {
+    int R;
+    const int nb = pop_blocks(nc.n, &R);
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, 0};
+    PopOut* o = (PopOut*)out_dev;
+    switch (R) {
+        case 1: hipLaunchKernelGGL(k_pop_batch<1>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 2: hipLaunchKernelGGL(k_pop_batch<2>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 4: hipLaunchKernelGGL(k_pop_batch<4>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 8: hipLaunchKernelGGL(k_pop_batch<8>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        default: hipLaunchKernelGGL(k_pop_batch<16>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+    }
+    return hipGetLastError();
+}
+
+size_t pop_out_bytes() { return sizeof(PopOut); }
 
 }  // namespace kbhip

@@ -175,6 +175,11 @@ struct Session {
         b_ctrl, b_cand, b_walk;
     PopCtrl* d_ctrl = nullptr;
     PopCtrl* h_ctrl = nullptr;  // pinned
+    DevBuf b_cand2, b_arrive;
+    uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
+    uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
+    PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device
+    void* d_out = nullptr;
     uint64_t* d_cand = nullptr;
     uint64_t* d_walk = nullptr;
     bool batched = true;
@@ -190,6 +195,7 @@ struct Session {
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (h_ctrl) (void)hipHostFree(h_ctrl);
+        if (h_out) (void)hipHostFree(h_out);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -715,6 +721,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
     int nb = topk_blocks(N, &R);
     S.d_cand = S.b_cand.alloc<uint64_t>((size_t)nb * kTopK);
     S.d_walk = S.b_walk.alloc<uint64_t>(npad);
+    {
+        int R2;
+        const int nb2 = pop_blocks(N, &R2);
+        S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)std::max(nb2, 1) * 64);
+        S.d_arrive = S.b_arrive.alloc<uint32_t>(4);
+        HIPCHK(hipMemsetAsync(S.d_arrive, 0, 4 * sizeof(uint32_t), st));
+        if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
+        HIPCHK(hipHostMalloc((void**)&S.h_out, sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
+    }
     HIPCHK(hipStreamSynchronize(st));
     // ---------------- ordering plugins OnSessionOpen ----------------
     for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
@@ -740,60 +756,78 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         if (!batch) {  // general path: take up to a chunk of mixed classes
             m = std::min(n - done, kMaxChunk);
         }
-        PopCtrl& h = *S.h_ctrl;
-        h.stop = -1;
-        h.n_done = 0;
-        h.ready_count = ready_count;
-        h.min_avail = min_avail;
-        h.gang_mode = gang_mode;
-        h.n_tasks = m;
-        h.any_bf = S.any_bf;
-        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
-        std::memset(h.arrive, 0, sizeof h.arrive);
-        std::memset(h.slot, 0, sizeof h.slot);
-        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
         // sampled HIP-event timing of the sweep launch (kbhip_set_option "time_every")
         const bool timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
-        if (timed) {
-            if (!S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
-            HIPCHK(hipEventRecord(S.ev0, S.stream));
-        }
+        if (timed && !S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
+        S.sweep_launches++;
+        int n_done, stop_c, ready_c, any_bf_c = S.any_bf;
+        const int32_t* res_node;
+        const int32_t* res_kind;
         if (batch) {
-            HIPCHK(launch_sweep_topk(S.conf, S.nc, S.tab, S.d_ctrl, S.d_cand, S.stream));
+            // one launch: sweep + per-block top-64 + merge + sequential placement
+            PopOutHost& o = *S.h_out;
+            o.n_done = -1;
+            o.stop = -1;
+            if (timed) HIPCHK(hipEventRecord(S.ev0, S.stream));
+            HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, S.d_cand2,
+                                    S.d_arrive, S.d_out, S.stream));
             if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
-            HIPCHK(launch_place_batch(S.conf, S.nc, S.tab, S.d_ctrl, S.d_cand, S.stream));
+            HIPCHK(hipStreamSynchronize(S.stream));
             S.stats.sweeps += 1;
             S.stats.batched_pops += 1;
+            n_done = o.n_done;
+            stop_c = o.stop;
+            ready_c = o.ready_count;
+            res_node = o.res_node;
+            res_kind = o.res_kind;
         } else {
+            PopCtrl& h = *S.h_ctrl;
+            h.stop = -1;
+            h.n_done = 0;
+            h.ready_count = ready_count;
+            h.min_avail = min_avail;
+            h.gang_mode = gang_mode;
+            h.n_tasks = m;
+            h.any_bf = S.any_bf;
+            for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
+            std::memset(h.arrive, 0, sizeof h.arrive);
+            std::memset(h.slot, 0, sizeof h.slot);
+            HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
             for (int i = 0; i < m; ++i) {
+                if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
                 HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
             }
             S.stats.sweeps += m;
+            HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
+            HIPCHK(hipStreamSynchronize(S.stream));
+            n_done = h.n_done;
+            stop_c = h.stop;
+            ready_c = h.ready_count;
+            any_bf_c = h.any_bf;
+            res_node = h.res_node;
+            res_kind = h.res_kind;
         }
-        S.sweep_launches++;
-        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
-        HIPCHK(hipStreamSynchronize(S.stream));
         if (timed) {
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, S.ev0, S.ev1));
             S.timed_ms += ms;
             S.timed_n++;
         }
-        if (h.stop < 0 || h.n_done < 1 || h.n_done > m) throw Error(KBHIP_EDEVICE, "device pop did not complete");
-        for (int i = 0; i < h.n_done; ++i) {
-            out_node[done + i] = h.res_node[i];
-            out_kind[done + i] = (uint8_t)h.res_kind[i];
-            const int node = h.res_node[i];
+        if (stop_c < 0 || n_done < 1 || n_done > m) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+        for (int i = 0; i < n_done; ++i) {
+            out_node[done + i] = res_node[i];
+            out_kind[done + i] = (uint8_t)res_kind[i];
+            const int node = res_node[i];
             if (node >= 0) {
                 HPod& p = S.pods[ids[done + i]];
                 S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
             }
         }
-        S.any_bf = h.any_bf;
-        ready_count = h.ready_count;
-        done += h.n_done;
-        stop = h.stop;
+        S.any_bf = any_bf_c;
+        ready_count = ready_c;
+        done += n_done;
+        stop = stop_c;
         if (stop != KBHIP_STOP_ALL) break;
     }
     *out_n_done = done;
