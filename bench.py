@@ -184,6 +184,7 @@ def main():
                    "placements_per_session": placed // args.steps, "pops_per_session": st_last["pops"],
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
+                   "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
         "roofline": {"kernel": "k_pop_batch", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -80,6 +80,8 @@ typedef struct kbhip_stats {
     int64_t batched_pops;/* pops served by the class-batched path */
     int64_t nodes;       /* nodes in the session */
     int64_t timed_launches; /* sweep launches timed with HIP events (option "time_every") */
+    double host_launch_s;   /* host time spent launching batched pop kernels */
+    double host_wait_s;     /* host time spent waiting for their results */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

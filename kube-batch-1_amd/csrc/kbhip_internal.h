@@ -33,6 +33,9 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
                             void* out_dev, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
 size_t pop_out_bytes();
+#ifdef KBHIP_STAMPS
+hipError_t set_stamp_buffer(uint64_t* p);
+#endif
 struct PopOutHost {  // host view of the device PopOut
     int32_t stop, n_done, ready_count, pad;
     int32_t res_node[kMaxChunk];

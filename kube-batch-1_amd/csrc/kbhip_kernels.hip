@@ -24,6 +24,19 @@
 
 namespace kbhip {
 
+#ifdef KBHIP_STAMPS
+// Diagnostic build only: phase stamps (s_memrealtime, 100 MHz) of k_pop_batch.
+// Layout: [block][0..3] = start, after sweep+wave sort, after block merge, after arrival;
+// [nb*4 + 0..7] = last block: merged, chain precomputed, placement done, end.
+__device__ uint64_t* g_stamps;
+#define STAMP(slot)                                                       \
+    do {                                                                  \
+        if (threadIdx.x == 0) g_stamps[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // node row + evaluation
 // ---------------------------------------------------------------------------
@@ -447,12 +460,53 @@ __device__ __forceinline__ Row apply_commits(Row r, const TaskClass& c, int na, 
     return r;
 }
 
+// 64-lane max of a u32 with DPP row shifts + row broadcasts (GFX9 family),
+// broadcast to every lane.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:1
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:2
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:4
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:8
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false); v = t > v ? t : v;  // row_bcast:15
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false); v = t > v ? t : v;  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint64_t wave_max_key(uint64_t v) {
+    const uint32_t hi = wave_max_u32((uint32_t)(v >> 32));
+    const uint32_t lo = wave_max_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0u);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Hand-off of 64-key lists between workgroups: write-through (sc1) 8-byte
+// stores drained before an agent-scope counter add, sc1 loads on the consumer
+// after its add returned (MI355X_MICROARCH.md, valid forms, table row 1).
+__device__ __forceinline__ void put_list(uint64_t* dst, uint64_t v) {
+    __hip_atomic_store(dst + (threadIdx.x & 63), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t get_list(const uint64_t* src) {
+    return __hip_atomic_load(src + (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kGroups = 8;        // second-level merge groups (blockIdx % 8)
+constexpr int kCtrStride = 32;    // one counter per 128-byte line
+
+// Tree merge of the 8 per-wave lists in wl[] into wl[0] (all waves call).
+__device__ __forceinline__ void block_tree_merge(uint64_t (*wl)[64], int wave, int lane) {
+#pragma unroll
+    for (int s = kPopThreads / 128; s >= 1; s >>= 1) {
+        if (wave < s) wl[wave][lane] = wave_merge_desc(wl[wave][lane], wl[wave + s][lane]);
+        __syncthreads();
+    }
+}
+
 template <int R>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                            uint64_t* cand, uint32_t* arrive, PopOut* out) {
     __shared__ uint64_t wl[kPopThreads / 64][64];
-    __shared__ int last;
+    __shared__ int role;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
     // 1. evaluate R nodes per lane, wave top-64, block top-64
     uint64_t best = 0;
@@ -470,85 +524,103 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     wl[wave][lane] = best;
     __syncthreads();
+    STAMP(blockIdx.x * 4 + 1);
+    block_tree_merge(wl, wave, lane);
+    const int nb = gridDim.x;
+    const int g = blockIdx.x % kGroups;
+    const int g_count = (nb - g + kGroups - 1) / kGroups;   // blocks in my group
+    const int n_groups = nb < kGroups ? nb : kGroups;
+    uint64_t* gcand = cand + (int64_t)nb * 64;               // group lists after the block lists
     if (wave == 0) {
-        uint64_t v = wl[0][lane];
-#pragma unroll
-        for (int w = 1; w < kPopThreads / 64; ++w) v = wave_merge_desc(v, wl[w][lane]);
-        cand[(int64_t)blockIdx.x * 64 + lane] = v;
+        put_list(cand + (int64_t)blockIdx.x * 64, wl[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(arrive, 1u) == gridDim.x - 1;
-        __threadfence();
-    }
+    STAMP(blockIdx.x * 4 + 2);
+    if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
     __syncthreads();
-    if (!last) return;
-    // 2. last block: merge every block's list (8 waves, strided), then the 8 partials
+    if (!role) return;
+    // 2a. last block of group g: merge the group's block lists (strided over waves)
     {
         uint64_t acc = 0;
-        int b = wave;
-        uint64_t nxt = b < (int)gridDim.x ? cand[(int64_t)b * 64 + lane] : 0;
-        while (b < (int)gridDim.x) {
-            const uint64_t cur = nxt;
-            const int bn = b + kPopThreads / 64;
-            nxt = bn < (int)gridDim.x ? cand[(int64_t)bn * 64 + lane] : 0;
-            acc = wave_merge_desc(acc, cur);
-            b = bn;
-        }
+        for (int i = wave; i < g_count; i += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(cand + (int64_t)(g + i * kGroups) * 64));
         wl[wave][lane] = acc;
+        __syncthreads();
+        block_tree_merge(wl, wave, lane);
+        if (wave == 0) {
+            put_list(gcand + (int64_t)g * 64, wl[0][lane]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1);
+        __syncthreads();
+        if (!role) return;
     }
+    STAMP(gridDim.x * 4 + 4);
+    // 2b. last group merger: merge the group lists; reset the counters for the next launch
+    wl[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : 0;
     __syncthreads();
-    if (wave != 0) return;
-    if (lane == 0) __hip_atomic_store(arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    uint64_t K = wl[0][lane];
-#pragma unroll
-    for (int w = 1; w < kPopThreads / 64; ++w) K = wave_merge_desc(K, wl[w][lane]);
-    // 3. placement: lane j owns candidate j (node n, key K).  Winner of each
-    // task = max over lanes of the current key (unchanged candidates keep
-    // their sweep key; the list is sorted, so its first unchanged entry is the
-    // best unchanged node anywhere).
+    block_tree_merge(wl, wave, lane);
+    STAMP(gridDim.x * 4 + 0);
+    if (wave == 0 && lane <= kGroups)
+        __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
+    // n, sweep key K.  The post-commit keys of each candidate (after 1..kDepth
+    // more tasks of this class, assuming every commit is an Allocate) are
+    // computed by waves 0..kDepth-1 in parallel.
+    __shared__ uint64_t chainbuf[kDepth][64];
+    const uint64_t K = wl[0][lane];
     const int n = K ? key_idx(K) : -1;
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
-    if (n >= 0) {
+    if (n >= 0 && wave <= kDepth) {
         base = load_row(nc, n);
         if (c.has_ports)
             for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
     }
     uint64_t pwc[4];  // ports after one or more commits of this class
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
-    uint64_t chain[kDepth];
-    {
-        uint64_t cur = K;
-        int na = 0, np = 0;
-#pragma unroll
-        for (int d = 0; d < kDepth; ++d) {
-            if (cur) {
-                if (key_kind(cur) == 1) ++na; else ++np;
-                const Row r = apply_commits(base, c, na, np);
-                int32_t s;
-                bool passed;
-                cur = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
-            }
-            chain[d] = cur;
+    if (wave < kDepth) {
+        uint64_t v = 0;
+        if (n >= 0) {
+            const Row r = apply_commits(base, c, wave + 1, 0);
+            int32_t s;
+            bool passed;
+            v = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
         }
+        chainbuf[wave][lane] = v;
     }
-    uint64_t val = K;
-    int na = 0, np = 0;
+    __syncthreads();
+    if (wave != 0) return;
+    STAMP(gridDim.x * 4 + 1);
+    uint64_t chain[kDepth];
+#pragma unroll
+    for (int d = 0; d < kDepth; ++d) chain[d] = chainbuf[d][lane];
+    // Winner of each task = max(first unchanged list entry, best changed entry).
+    // Changed entries are always a prefix [0, first) of the list.
+    uint64_t val = K;       // current key of this lane's candidate
+    int na = 0, np = 0;     // commits on this lane's node by kind
+    int first = 0;          // uniform
+    uint64_t bc_val = 0;    // uniform: best key among changed entries
+    int bc_lane = -1;       // uniform
     int ready = a.ready_count, stop = -1, done = 0;
     uint64_t mine = 0;  // lane i: winner key of task i
     for (int i = 0; i < a.n_tasks; ++i) {
-        const uint64_t w = wave_max_u64(val);
+        const uint64_t cu = first < 64 ? ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(K >> 32), first) << 32 |
+                                          (uint32_t)__builtin_amdgcn_readlane((int)K, first))
+                                       : 0;
+        uint64_t w;
+        int wl;
+        if (cu > bc_val) { w = cu; wl = first; ++first; }
+        else { w = bc_val; wl = bc_lane; }
         done = i + 1;
         if (!w) { stop = 1; break; }
         if (lane == i) mine = w;
         const int kind = key_kind(w);
-        if (val == w) {  // the winning lane (keys are unique)
+        if (lane == wl) {  // commit on the winner's node
             if (kind == 1) ++na; else ++np;
             const int cc = na + np;
-            if (cc <= kDepth) {
+            if (np == 0 && cc <= kDepth) {
                 uint64_t x = chain[0];
 #pragma unroll
                 for (int d = 1; d < kDepth; ++d) if (cc == d + 1) x = chain[d];
@@ -560,10 +632,21 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
                 val = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
             }
         }
+        const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), wl) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((int)val, wl);
+        if (wl == bc_lane) {  // the best changed node changed again: rescan the changed prefix
+            bc_val = wave_max_key(lane < first ? val : 0);
+            const uint64_t m = __ballot(lane < first && val == bc_val && bc_val != 0);
+            bc_lane = m ? __ffsll((unsigned long long)m) - 1 : -1;
+        } else if (nv > bc_val) {
+            bc_val = nv;
+            bc_lane = wl;
+        }
         if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
         if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
         if (i + 1 == a.n_tasks) stop = 0;
     }
+    STAMP(gridDim.x * 4 + 2);
     // 4. write back committed rows and the results
     if (na + np > 0) {
         const Row r = apply_commits(base, c, na, np);
@@ -580,10 +663,13 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         out->res_kind[lane] = mine ? key_kind(mine) : 0;
     }
     if (lane == 0) {
-        out->n_done = done;
         out->stop = stop;
         out->ready_count = ready;
     }
+    // completion flag for the host poll: every result store is visible first
+    __threadfence_system();
+    if (lane == 0) __hip_atomic_store(&out->n_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(gridDim.x * 4 + 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -654,5 +740,9 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 }
 
 size_t pop_out_bytes() { return sizeof(PopOut); }
+
+#ifdef KBHIP_STAMPS
+hipError_t set_stamp_buffer(uint64_t* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
+#endif
 
 }  // namespace kbhip

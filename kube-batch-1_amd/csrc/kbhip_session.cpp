@@ -180,6 +180,12 @@ struct Session {
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device
     void* d_out = nullptr;
+#ifdef KBHIP_STAMPS
+    DevBuf b_stamps;
+    uint64_t* d_stamps = nullptr;
+    double phase[12] = {0};  // accumulated phase durations (us)
+    int64_t phase_n = 0;
+#endif
     uint64_t* d_cand = nullptr;
     uint64_t* d_walk = nullptr;
     bool batched = true;
@@ -187,6 +193,7 @@ struct Session {
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double timed_ms = 0;          // summed duration of the timed sweep launches
+    double host_launch_s = 0, host_wait_s = 0;
     int64_t timed_n = 0;
     kbhip_stats stats{};
     vector<std::tuple<int, int, int>> log;
@@ -724,12 +731,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
     {
         int R2;
         const int nb2 = pop_blocks(N, &R2);
-        S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)std::max(nb2, 1) * 64);
-        S.d_arrive = S.b_arrive.alloc<uint32_t>(4);
-        HIPCHK(hipMemsetAsync(S.d_arrive, 0, 4 * sizeof(uint32_t), st));
+        S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
+        S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
+        HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
         HIPCHK(hipHostMalloc((void**)&S.h_out, sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
+#ifdef KBHIP_STAMPS
+        S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 8);
+        HIPCHK(set_stamp_buffer(S.d_stamps));
+#endif
     }
     HIPCHK(hipStreamSynchronize(st));
     // ---------------- ordering plugins OnSessionOpen ----------------
@@ -769,10 +780,23 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             o.n_done = -1;
             o.stop = -1;
             if (timed) HIPCHK(hipEventRecord(S.ev0, S.stream));
+            auto tl0 = std::chrono::steady_clock::now();
             HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, S.d_cand2,
                                     S.d_arrive, S.d_out, S.stream));
             if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
-            HIPCHK(hipStreamSynchronize(S.stream));
+            auto tl1 = std::chrono::steady_clock::now();
+            // the kernel stores n_done last (system scope, after a system fence):
+            // spin on it, and hand long waits to the runtime
+            bool seen = false;
+            for (int spin = 0; spin < (1 << 22); ++spin) {
+                if (__atomic_load_n(&o.n_done, __ATOMIC_ACQUIRE) != -1) { seen = true; break; }
+                __builtin_ia32_pause();
+            }
+            if (!seen) HIPCHK(hipStreamSynchronize(S.stream));
+            if (timed) HIPCHK(hipEventSynchronize(S.ev1));
+            auto tl2 = std::chrono::steady_clock::now();
+            S.host_launch_s += std::chrono::duration<double>(tl1 - tl0).count();
+            S.host_wait_s += std::chrono::duration<double>(tl2 - tl1).count();
             S.stats.sweeps += 1;
             S.stats.batched_pops += 1;
             n_done = o.n_done;
@@ -780,6 +804,34 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             ready_c = o.ready_count;
             res_node = o.res_node;
             res_kind = o.res_kind;
+#ifdef KBHIP_STAMPS
+            {
+                int R2;
+                const int nb2 = pop_blocks(S.nc.n, &R2);
+                vector<uint64_t> st((size_t)nb2 * 4 + 8);
+                HIPCHK(hipMemcpy(st.data(), S.d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+                uint64_t t0 = UINT64_MAX, tbm = 0;
+                double sw = 0, bm = 0;
+                for (int b = 0; b < nb2; ++b) {
+                    t0 = std::min(t0, st[b * 4]);
+                    tbm = std::max(tbm, st[b * 4 + 2]);
+                    sw += (st[b * 4 + 1] - st[b * 4]) * 0.01;
+                    bm += (st[b * 4 + 2] - st[b * 4 + 1]) * 0.01;
+                }
+                const uint64_t* L = st.data() + nb2 * 4;
+                S.phase[0] += sw / nb2;                    // per-block sweep + wave sort
+                S.phase[1] += bm / nb2;                    // per-block merge + store
+                S.phase[2] += (tbm - t0) * 0.01;           // first block start -> every block list stored
+                S.phase[3] += ((double)L[4] - (double)tbm) * 0.01;  // -> final merger starts
+                S.phase[4] += (L[0] - L[4]) * 0.01;        // final merge
+                S.phase[5] += (L[1] - L[0]) * 0.01;        // chain precompute
+                S.phase[6] += (L[2] - L[1]) * 0.01;        // placement loop
+                S.phase[7] += (L[3] - L[2]) * 0.01;        // write back
+                S.phase[8] += (L[3] - t0) * 0.01;          // total in-kernel span
+                S.phase[9] += m;
+                S.phase_n++;
+            }
+#endif
         } else {
             PopCtrl& h = *S.h_ctrl;
             h.stop = -1;
@@ -885,42 +937,45 @@ struct Allocator {
         return 4;
     }
     bool job_ready(const HJob& j) const { return !S.gang_ready || readiness(j) == 1; }  // session_plugins.go:167-186
-    bool job_less(int l, int r) const {  // session_plugins.go:244-268
-        const HJob &L = S.jobs[l], &R = S.jobs[r];
+    // tier dispatch compiled once: enabled order functions in tier order
+    // (session_plugins.go:244-329); codes 1 priority, 2 gang, 3 drf
+    vector<int> job_order;
+    bool queue_prop = false, task_prio = false;
+    void compile_orders() {
         for (auto& tier : S.tiers)
             for (auto& p : tier) {
-                if (p.flags & KBS_DIS_JOBORDER) continue;
-                int c;
-                if (p.name == "priority") c = L.priority > R.priority ? -1 : L.priority < R.priority ? 1 : 0;  // priority.go:60-76
-                else if (p.name == "gang") {  // gang.go:136-160
-                    bool lr = readiness(L) == 1, rr = readiness(R) == 1;
-                    c = (lr && rr) ? 0 : lr ? 1 : rr ? -1 : 0;
-                } else if (p.name == "drf") c = L.drf_share == R.drf_share ? 0 : L.drf_share < R.drf_share ? -1 : 1;  // drf.go:113-129
-                else continue;
-                if (c != 0) return c < 0;
+                if (!(p.flags & KBS_DIS_JOBORDER)) {
+                    if (p.name == "priority") job_order.push_back(1);
+                    else if (p.name == "gang") job_order.push_back(2);
+                    else if (p.name == "drf") job_order.push_back(3);
+                }
+                if (!(p.flags & KBS_DIS_QUEUEORDER) && p.name == "proportion") queue_prop = true;
+                if (!(p.flags & KBS_DIS_TASKORDER) && p.name == "priority") task_prio = true;
             }
+    }
+    bool job_less(int l, int r) const {  // session_plugins.go:244-268
+        const HJob &L = S.jobs[l], &R = S.jobs[r];
+        for (int code : job_order) {
+            int c;
+            if (code == 1) c = L.priority > R.priority ? -1 : L.priority < R.priority ? 1 : 0;  // priority.go:60-76
+            else if (code == 2) {  // gang.go:136-160
+                bool lr = readiness(L) == 1, rr = readiness(R) == 1;
+                c = (lr && rr) ? 0 : lr ? 1 : rr ? -1 : 0;
+            } else c = L.drf_share == R.drf_share ? 0 : L.drf_share < R.drf_share ? -1 : 1;  // drf.go:113-129
+            if (c != 0) return c < 0;
+        }
         if (L.ts == R.ts) return L.uid < R.uid;
         return L.ts < R.ts;
     }
     bool queue_less(int l, int r) const {  // session_plugins.go:270-295, proportion.go:144-157
         const HQueue &L = S.queues[l], &R = S.queues[r];
-        for (auto& tier : S.tiers)
-            for (auto& p : tier) {
-                if ((p.flags & KBS_DIS_QUEUEORDER) || p.name != "proportion") continue;
-                int c = L.share == R.share ? 0 : L.share < R.share ? -1 : 1;
-                if (c != 0) return c < 0;
-            }
+        if (queue_prop && L.share != R.share) return L.share < R.share;
         if (L.ts == R.ts) return L.name < R.name;
         return L.ts < R.ts;
     }
     bool task_less(int l, int r) const {  // session_plugins.go:297-329, priority.go:39-55
         const HPod &L = S.pods[l], &R = S.pods[r];
-        for (auto& tier : S.tiers)
-            for (auto& p : tier) {
-                if ((p.flags & KBS_DIS_TASKORDER) || p.name != "priority") continue;
-                int c = L.priority == R.priority ? 0 : L.priority > R.priority ? -1 : 1;
-                if (c != 0) return c < 0;
-            }
+        if (task_prio && L.priority != R.priority) return L.priority > R.priority;
         if (L.ts == R.ts) return L.uid < R.uid;
         return L.ts < R.ts;
     }
@@ -993,6 +1048,7 @@ struct Allocator {
 
     void run() {  // allocate.go:41-201
         auto t0 = std::chrono::steady_clock::now();
+        compile_orders();
         open_plugins();
         auto ql = [this](int a, int b) { return queue_less(a, b); };
         auto jl = [this](int a, int b) { return job_less(a, b); };
@@ -1052,6 +1108,7 @@ struct Allocator {
             }
             queues.push(q);
         }
+        HIPCHK(hipStreamSynchronize(S.stream));
         S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
 };
@@ -1134,8 +1191,10 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
         if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
             throw kbhip::Error(KBHIP_EINVAL, "null argument");
         HIPCHK(hipSetDevice(s->s.device));
-        return kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
-                                out_n_done, out_stop_reason);
+        int rc = kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
+                                  out_n_done, out_stop_reason);
+        HIPCHK(hipStreamSynchronize(s->s.stream));
+        return rc;
     })
 }
 
@@ -1187,6 +1246,8 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out) {
         *out = s->s.stats;
         out->device_s = s->s.timed_ms * 1e-3;
         out->timed_launches = s->s.timed_n;
+        out->host_launch_s = s->s.host_launch_s;
+        out->host_wait_s = s->s.host_wait_s;
         return KBHIP_OK;
     })
 }
@@ -1200,6 +1261,15 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         return KBHIP_OK;
     })
 }
+
+#ifdef KBHIP_STAMPS
+int kbhip_debug_phases(kb_session* s, double* out, int n) {
+    ABI_GUARD({
+        for (int i = 0; i < n && i < 12; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
+        return (int)s->s.phase_n;
+    })
+}
+#endif
 
 int kbhip_session_close(kb_session* s) {
     ABI_GUARD({

@@ -1,0 +1,21 @@
+"""Diagnostic: per-phase in-kernel time of k_pop_batch on C4 (stamps build).
+Shares only; the stamps build is never used for timing claims."""
+import ctypes, os, sys, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+import kbhip
+kbhip.LIB_PATH = os.path.join(ROOT, "kube-batch-1_amd", "_build", "libkbhip_stamps.so")
+import kbgen
+p = "/tmp/kbhip_bench/c4_100000_800000_%d.kbs" % (kbgen.BASE_SEED + 4)
+if not os.path.exists(p):
+    os.makedirs(os.path.dirname(p), exist_ok=True)
+    kbgen.gen_c4(p)
+L = kbhip.lib()
+with kbhip.Session(p) as s:
+    s.allocate()
+    out = (ctypes.c_double * 12)()
+    n = L.kbhip_debug_phases(s._h, out, 12)
+    names = ["block sweep+sort", "block merge+store", "span to all block lists stored",
+             "group merge tail to final start", "final merge", "chain precompute", "placement loop",
+             "write back", "kernel span", "tasks per launch"]
+    print(json.dumps({"pops": n, **{names[i]: round(out[i], 3) for i in range(10)}}, indent=1))
