@@ -29,17 +29,15 @@ int topk_blocks(int n_nodes, int* R_out);
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                            int gang_mode, int min_avail, int ready_count, uint64_t* cand, uint32_t* arrive,
-                            void* out_dev, hipStream_t st);
+                            int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
+                            uint32_t* arrive, void* out_dev, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
 size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);
 #endif
-struct PopOutHost {  // host view of the device PopOut
-    int32_t stop, n_done, ready_count, pad;
-    int32_t res_node[kMaxChunk];
-    int32_t res_kind[kMaxChunk];
+struct PopOutHost {  // host view of the device PopOut: self-tagged granules
+    uint64_t g[kMaxChunk];
 };
 
 }  // namespace kbhip

@@ -437,14 +437,20 @@ __device__ __forceinline__ uint64_t wave_merge_desc(uint64_t a, uint64_t b) {
     return v;
 }
 
-struct PopOut {  // written by the device into pinned host memory
-    int32_t stop, n_done, ready_count, pad;
-    int32_t res_node[kMaxChunk];
-    int32_t res_kind[kMaxChunk];
+// Results land in pinned host memory as self-tagged 8-byte granules, one per
+// consumed task, each written by ONE 8-byte store (no fence needed: the host
+// polls the tags).  granule = epoch<<48 | (stop+1)<<44 | n_done<<36 | kind<<34 | (node+1)
+struct PopOut {
+    uint64_t g[kMaxChunk];
 };
+__host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n_done, int kind, int node) {
+    return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(stop + 1) << 44) | ((uint64_t)n_done << 36) |
+           ((uint64_t)kind << 34) | (uint64_t)(uint32_t)(node + 1);
+}
 
 struct PopArgs {
-    int32_t cls, n_tasks, gang_mode, min_avail, ready_count, pad;
+    int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
+    uint32_t epoch;
 };
 
 constexpr int kPopThreads = 512;  // 8 waves
@@ -597,54 +603,75 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
 #pragma unroll
     for (int d = 0; d < kDepth; ++d) chain[d] = chainbuf[d][lane];
     // Winner of each task = max(first unchanged list entry, best changed entry).
-    // Changed entries are always a prefix [0, first) of the list.
+    // Changed entries are always a prefix [0, first) of the list.  The hot
+    // loop only reads precomputed post-commit keys; a lane whose chain is
+    // exhausted (or that was pipelined) leaves the loop for a recompute.
     uint64_t val = K;       // current key of this lane's candidate
     int na = 0, np = 0;     // commits on this lane's node by kind
     int first = 0;          // uniform
     uint64_t bc_val = 0;    // uniform: best key among changed entries
     int bc_lane = -1;       // uniform
     int ready = a.ready_count, stop = -1, done = 0;
-    uint64_t mine = 0;  // lane i: winner key of task i
-    for (int i = 0; i < a.n_tasks; ++i) {
-        const uint64_t cu = first < 64 ? ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(K >> 32), first) << 32 |
-                                          (uint32_t)__builtin_amdgcn_readlane((int)K, first))
-                                       : 0;
-        uint64_t w;
-        int wl;
-        if (cu > bc_val) { w = cu; wl = first; ++first; }
-        else { w = bc_val; wl = bc_lane; }
-        done = i + 1;
-        if (!w) { stop = 1; break; }
-        if (lane == i) mine = w;
-        const int kind = key_kind(w);
-        if (lane == wl) {  // commit on the winner's node
-            if (kind == 1) ++na; else ++np;
-            const int cc = na + np;
-            if (np == 0 && cc <= kDepth) {
+    uint64_t mine = 0;      // lane i: winner key of task i
+    int i = 0;
+    while (i < a.n_tasks && stop < 0) {
+        int slow_lane = -1;
+        for (; i < a.n_tasks; ++i) {
+            const uint64_t cu = first < 64 ? ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(K >> 32), first) << 32 |
+                                              (uint32_t)__builtin_amdgcn_readlane((int)K, first))
+                                           : 0;
+            uint64_t w;
+            int wl;
+            if (cu > bc_val) { w = cu; wl = first; ++first; }
+            else { w = bc_val; wl = bc_lane; }
+            done = i + 1;
+            if (!w) { stop = 1; break; }
+            if (lane == i) mine = w;
+            const int kind = key_kind(w);
+            bool fast = true;
+            if (lane == wl) {
+                if (kind == 1) ++na; else ++np;
+                const int cc = na + np;
+                fast = np == 0 && cc <= kDepth;
                 uint64_t x = chain[0];
 #pragma unroll
                 for (int d = 1; d < kDepth; ++d) if (cc == d + 1) x = chain[d];
-                val = x;
-            } else {
-                const Row r = apply_commits(base, c, na, np);
-                int32_t s;
-                bool passed;
-                val = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+                if (fast) val = x;
             }
+            if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+            if (!a.gang_mode || ready >= a.min_avail) stop = 2;  // allocate.go:191-195
+            else if (i + 1 == a.n_tasks) stop = 0;
+            if (!__builtin_amdgcn_readlane((int)fast, wl)) { slow_lane = wl; ++i; break; }
+            const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), wl) << 32 |
+                                (uint32_t)__builtin_amdgcn_readlane((int)val, wl);
+            if (wl == bc_lane) {  // the best changed node changed again: rescan the changed prefix
+                bc_val = wave_max_key(lane < first ? val : 0);
+                const uint64_t m = __ballot(lane < first && val == bc_val && bc_val != 0);
+                bc_lane = m ? __ffsll((unsigned long long)m) - 1 : -1;
+            } else if (nv > bc_val) {
+                bc_val = nv;
+                bc_lane = wl;
+            }
+            if (stop >= 0) { ++i; break; }
         }
-        const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), wl) << 32 |
-                            (uint32_t)__builtin_amdgcn_readlane((int)val, wl);
-        if (wl == bc_lane) {  // the best changed node changed again: rescan the changed prefix
+        if (slow_lane < 0) break;
+        // rare: re-evaluate the winner's node after its latest commit
+        if (lane == slow_lane) {
+            const Row r = apply_commits(base, c, na, np);
+            int32_t s;
+            bool passed;
+            val = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+        }
+        const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), slow_lane) << 32 |
+                            (uint32_t)__builtin_amdgcn_readlane((int)val, slow_lane);
+        if (slow_lane == bc_lane) {
             bc_val = wave_max_key(lane < first ? val : 0);
             const uint64_t m = __ballot(lane < first && val == bc_val && bc_val != 0);
             bc_lane = m ? __ffsll((unsigned long long)m) - 1 : -1;
         } else if (nv > bc_val) {
             bc_val = nv;
-            bc_lane = wl;
+            bc_lane = slow_lane;
         }
-        if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
-        if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
-        if (i + 1 == a.n_tasks) stop = 0;
     }
     STAMP(gridDim.x * 4 + 2);
     // 4. write back committed rows and the results
@@ -658,17 +685,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         if (c.has_ports)
             for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
     }
-    if (lane < done) {
-        out->res_node[lane] = mine ? key_idx(mine) : -1;
-        out->res_kind[lane] = mine ? key_kind(mine) : 0;
-    }
-    if (lane == 0) {
-        out->stop = stop;
-        out->ready_count = ready;
-    }
-    // completion flag for the host poll: every result store is visible first
-    __threadfence_system();
-    if (lane == 0) __hip_atomic_store(&out->n_done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     STAMP(gridDim.x * 4 + 3);
 }
 
@@ -723,11 +743,11 @@ int pop_blocks(int n_nodes, int* R_out) {
 }
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                            int gang_mode, int min_avail, int ready_count, uint64_t* cand, uint32_t* arrive,
-                            void* out_dev, hipStream_t st) {
+                            int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
+                            uint32_t* arrive, void* out_dev, hipStream_t st) {
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, 0};
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch};
     PopOut* o = (PopOut*)out_dev;
     switch (R) {
         case 1: hipLaunchKernelGGL(k_pop_batch<1>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;

@@ -180,6 +180,8 @@ struct Session {
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device
     void* d_out = nullptr;
+    uint32_t epoch = 0;
+    int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
 #ifdef KBHIP_STAMPS
     DevBuf b_stamps;
     uint64_t* d_stamps = nullptr;
@@ -737,6 +739,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
         HIPCHK(hipHostMalloc((void**)&S.h_out, sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
+        std::memset(S.h_out, 0, sizeof(PopOutHost));
 #ifdef KBHIP_STAMPS
         S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 8);
         HIPCHK(set_stamp_buffer(S.d_stamps));
@@ -777,33 +780,53 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         if (batch) {
             // one launch: sweep + per-block top-64 + merge + sequential placement
             PopOutHost& o = *S.h_out;
-            o.n_done = -1;
-            o.stop = -1;
+            if (((S.epoch + 1) & 0xffff) == 0) {  // tag wrap: clear stale granules, skip tag 0
+                std::memset(S.h_out, 0, sizeof(PopOutHost));
+                ++S.epoch;
+            }
+            const uint32_t epoch = (++S.epoch) & 0xffff;
             if (timed) HIPCHK(hipEventRecord(S.ev0, S.stream));
             auto tl0 = std::chrono::steady_clock::now();
-            HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, S.d_cand2,
-                                    S.d_arrive, S.d_out, S.stream));
+            HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, epoch,
+                                    S.d_cand2, S.d_arrive, S.d_out, S.stream));
             if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
             auto tl1 = std::chrono::steady_clock::now();
-            // the kernel stores n_done last (system scope, after a system fence):
-            // spin on it, and hand long waits to the runtime
-            bool seen = false;
-            for (int spin = 0; spin < (1 << 22); ++spin) {
-                if (__atomic_load_n(&o.n_done, __ATOMIC_ACQUIRE) != -1) { seen = true; break; }
+            // poll the self-tagged result granules (each one 8-byte store on the device)
+            auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
+            auto load = [&](int j) { return __atomic_load_n(&o.g[j], __ATOMIC_ACQUIRE); };
+            int got = 0;
+            n_done = -1;
+            for (long spin = 0;; ++spin) {
+                if (n_done < 0) {
+                    const uint64_t g0 = load(0);
+                    if (tag(g0) == epoch) n_done = (int)((g0 >> 36) & 0xff);
+                }
+                if (n_done >= 0) {
+                    while (got < n_done && tag(load(got)) == epoch) ++got;
+                    if (got == n_done) break;
+                }
+                if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(S.stream));  // long waits: runtime
+                if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
                 __builtin_ia32_pause();
             }
-            if (!seen) HIPCHK(hipStreamSynchronize(S.stream));
             if (timed) HIPCHK(hipEventSynchronize(S.ev1));
             auto tl2 = std::chrono::steady_clock::now();
             S.host_launch_s += std::chrono::duration<double>(tl1 - tl0).count();
             S.host_wait_s += std::chrono::duration<double>(tl2 - tl1).count();
             S.stats.sweeps += 1;
             S.stats.batched_pops += 1;
-            n_done = o.n_done;
-            stop_c = o.stop;
-            ready_c = o.ready_count;
-            res_node = o.res_node;
-            res_kind = o.res_kind;
+            if (n_done < 1 || n_done > m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+            int alloc = 0;
+            for (int j = 0; j < n_done; ++j) {
+                const uint64_t g = load(j);
+                S.res_node_buf[j] = (int32_t)(g & 0xffffffffu) - 1;
+                S.res_kind_buf[j] = (int32_t)((g >> 34) & 3);
+                if (S.res_kind_buf[j] == 1) ++alloc;
+            }
+            stop_c = (int)((load(0) >> 44) & 0xf) - 1;
+            ready_c = ready_count + alloc;
+            res_node = S.res_node_buf;
+            res_kind = S.res_kind_buf;
 #ifdef KBHIP_STAMPS
             {
                 int R2;
