@@ -124,6 +124,7 @@ typedef struct kbs_dirent {
 #include <vector>
 #include <stdexcept>
 #include <cstdio>
+#include <cstring>
 
 namespace kbs {
 

@@ -16,15 +16,17 @@ struct DevTables {
     const int64_t* valint;  // per global value id: parsed int64 (Gt/Lt)
     const uint8_t* valok;   // per global value id: strconv.ParseInt succeeded
     const uint64_t* masks;  // tolerated-taint / port-conflict / own-port words
+    // pod (anti-)affinity (kbhip_affinity.h)
+    const int32_t* aff_items;  // programs: ea pairs, ipa quads, upd triples
+    int32_t* aff_cnt;          // count tables, indexed cnt_off + domain
+    int32_t* aff_scalar;       // PA target totals, session counters
 };
 
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
                                uint64_t* walk, hipStream_t st);
-hipError_t launch_sweep_topk(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, uint64_t* cand,
-                             hipStream_t st);
-hipError_t launch_place_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
-                              const uint64_t* cand, hipStream_t st);
-int topk_blocks(int n_nodes, int* R_out);
+// Inter-pod affinity priority prepass: min / max of the raw count over all
+// nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi.
+hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st);
 
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).

@@ -13,11 +13,14 @@
 //    the last block to arrive commits the winner (Session.Allocate/Pipeline
 //    node update) and decides whether the job pop stops.
 //  * batched: when every task of a pop chunk has the same class and nothing
-//    but the winner's row can change between tasks, ONE sweep serves the whole
-//    chunk: k_sweep_topk keeps the top-64 keys of each block (bitonic sort in
-//    LDS), k_place_batch merges them and places the chunk's tasks in sequence
-//    against the sorted candidate list, re-evaluating only rows it changed.
-//    Placements are identical to per-task sweeps (tests/test_gpu_parity.py).
+//    but the winner's row can change between tasks, ONE launch serves the
+//    whole chunk: k_pop_batch sweeps, keeps the global top-64 keys and places
+//    the chunk's tasks in sequence against that sorted candidate list,
+//    re-evaluating only rows it changed.  Placements are identical to
+//    per-task sweeps (tests/test_gpu_parity.py).
+//  * pod (anti-)affinity classes always take the per-task path: their
+//    predicate and inter-pod score read count tables every commit may change
+//    (kbhip_affinity.h); k_ipa_minmax is the score's normalisation prepass.
 #include <hip/hip_runtime.h>
 
 #include "kbhip_internal.h"
@@ -116,10 +119,10 @@ __device__ __forceinline__ int64_t lr_score(int64_t req, int64_t cap) {  // leas
     return q;
 }
 
-// Score of a feasible node (nodeorder.go:281-313; the inter-pod term is 0
-// for the sessions the engine accepts).
+// Score of a feasible node (nodeorder.go:281-313).  ipa: the normalised
+// inter-pod affinity score (0 for classes without inter-pod terms).
 __device__ __forceinline__ int32_t node_score(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                              const NodeCols& nc, const Row& r, int n) {
+                                              const NodeCols& nc, const Row& r, int n, int32_t ipa) {
     if (!cf.score_mult) return 0;
     const int64_t rc = c.nz_cpu + r.nzc, rm = c.nz_mem + r.nzm;
     const int64_t lr = (lr_score(rc, r.acpu) + lr_score(rm, r.amem)) / 2;
@@ -137,14 +140,15 @@ __device__ __forceinline__ int32_t node_score(const Conf& cf, const TaskClass& c
         const Term& tm = t.terms[c.pref_term_off + i];
         if (term_match(t, nc, tm, n)) na += tm.weight;
     }
-    return ((int32_t)lr * cf.w_lr + (int32_t)bra * cf.w_bra + na * cf.w_na) * cf.score_mult;
+    return ((int32_t)lr * cf.w_lr + (int32_t)bra * cf.w_bra + na * cf.w_na + ipa * cf.w_pa) * cf.score_mult;
 }
 
 // Dynamic predicates (pod count, host ports) + fit + key, given the row.
 // passed: predicate pass and score computed (the node is in the walk).
 __device__ __forceinline__ uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t,
                                             const NodeCols& nc, const Row& r, const uint64_t* portw,
-                                            int n, bool stat_ok, int32_t* score_out, bool* passed) {
+                                            int n, bool stat_ok, int32_t* score_out, bool* passed,
+                                            int32_t ipa = 0) {
     bool ok = stat_ok;
     if (cf.pred_on) {
         if (r.maxtasks <= r.pods) ok = false;                            // predicates.go:127
@@ -155,7 +159,7 @@ __device__ __forceinline__ uint64_t dyn_key(const Conf& cf, const TaskClass& c, 
     if (ok && c.score_err) ok = false;  // NodeOrderFn error drops the node (allocate.go:141-145)
     *passed = ok;
     if (!ok) return 0;
-    const int32_t s = node_score(cf, c, t, nc, r, n);
+    const int32_t s = node_score(cf, c, t, nc, r, n, ipa);
     *score_out = s;
     // allocate.go:153 (InitResreq <= Idle + Backfilled) and :173 (<= Releasing)
     const bool fit_acc = c.ireq_cpu - (r.idle_cpu + r.bf_cpu) < kMinCPU &&
@@ -175,6 +179,114 @@ __device__ __forceinline__ uint64_t eval_node(const Conf& cf, const TaskClass& c
     if (c.has_ports)
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
     return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed);
+}
+
+// ---------------------------------------------------------------------------
+// pod (anti-)affinity (kbhip_affinity.h): count tables per term class,
+// indexed by the node's topology domain.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t dom_of(const NodeCols& nc, int space, int n) {
+    return nc.dom[(int64_t)space * nc.npad + n];
+}
+
+// predicates.go:1293-1458 for one node.
+__device__ __forceinline__ bool aff_pred(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n) {
+    // existing pods' required anti-affinity: a matching target in n's domain
+    for (int i = 0; i < c.ea_n; ++i) {
+        const int d = dom_of(nc, t.aff_items[c.ea_off + 2 * i], n);
+        if (d >= 0 && t.aff_cnt[t.aff_items[c.ea_off + 2 * i + 1] + d] > 0) return false;
+    }
+    // own required affinity: a target matching every term in n's domain tuple,
+    // or no target matches the terms anywhere and the pod matches them itself
+    if (c.pa_space >= 0) {
+        const int d = dom_of(nc, c.pa_space, n);
+        const bool match = d >= 0 && t.aff_cnt[c.pa_cnt + d] > 0;
+        if (!match && !(c.pa_self && t.aff_scalar[c.pa_total] == 0)) return false;
+    }
+    // own required anti-affinity: a target matching every term in n's domain tuple
+    if (c.paa_space >= 0) {
+        const int d = dom_of(nc, c.paa_space, n);
+        if (d >= 0 && t.aff_cnt[c.paa_cnt + d] > 0) return false;
+    }
+    return true;
+}
+
+// Raw inter-pod affinity count of node n (interpod_affinity.go:119-212):
+// sum over the task's term classes of weight x pods of the class in n's
+// domain; session-placed pods count at the fallback node F's domain.
+__device__ __forceinline__ int64_t ipa_count(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n,
+                                             int F) {
+    int64_t sum = 0;
+    for (int i = 0; i < c.ipa_n; ++i) {
+        const int32_t* it = t.aff_items + c.ipa_off + 4 * i;
+        const int d = dom_of(nc, it[0], n);
+        if (d < 0) continue;
+        int64_t x = t.aff_cnt[it[1] + d];
+        if (F >= 0 && dom_of(nc, it[0], F) == d) x += t.aff_scalar[it[2]];
+        sum += (int64_t)it[3] * x;
+    }
+    return sum;
+}
+
+// Full evaluation for the per-task path: static + affinity predicates, the
+// inter-pod score normalised by the prepass's [lo, hi] (interpod_affinity.go:228-237).
+__device__ __forceinline__ uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                                  const NodeCols& nc, int n, int64_t lo, int64_t hi, int F,
+                                                  int32_t* score_out, bool* passed) {
+    bool st = static_pred(cf, c, t, nc, n);
+    if (st && c.aff && cf.pred_on) st = aff_pred(c, t, nc, n);
+    int32_t ipa = 0;
+    if (st && c.ipa_n && hi - lo > 0)
+        ipa = (int32_t)(10.0 * ((double)(ipa_count(c, t, nc, n, F) - lo) / (double)(hi - lo)));
+    const Row r = load_row(nc, n);
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+    return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed, ipa);
+}
+
+// Count-table updates of a committed task (kind 1 Allocated, 2 Pipelined).
+__device__ void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {
+    for (int i = 0; i < c.upd_n; ++i) {
+        const int32_t* u = t.aff_items + c.upd_off + 3 * i;
+        if (u[0] == 0) {         // UPD_CNT_ALLOC: a new predicate target in n's domain
+            if (kind != 1) continue;
+            const int d = dom_of(nc, u[1], n);
+            if (d >= 0) t.aff_cnt[u[2] + d] += 1;
+        } else if (u[0] == 1) {  // UPD_SCALAR_ALLOC: target total of a PA class
+            if (kind == 1) t.aff_scalar[u[2]] += 1;
+        } else {                 // UPD_SCALAR_ANY: a session-placed pod (IPA)
+            t.aff_scalar[u[2]] += 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t, PopCtrl* ctrl, int task_i) {
+    __shared__ int64_t rlo[kBlock / 64], rhi[kBlock / 64];
+    if (ctrl->stop >= 0) return;
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
+    const TaskClass c = t.classes[cls];
+    const int F = ctrl->fallback;
+    int64_t lo = 0, hi = 0;  // maxCount / minCount start at 0 (interpod_affinity.go:214-226)
+    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+        const int64_t v = ipa_count(c, t, nc, n, F);
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0) { rlo[threadIdx.x >> 6] = lo; rhi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kBlock / 64; ++w) { lo = rlo[w] < lo ? rlo[w] : lo; hi = rhi[w] > hi ? rhi[w] : hi; }
+        lo = rlo[0] < lo ? rlo[0] : lo;
+        hi = rhi[0] > hi ? rhi[0] : hi;
+        if (lo < 0) atomicMin((long long*)&ctrl->ipa_lo[task_i], (long long)lo);
+        if (hi > 0) atomicMax((long long*)&ctrl->ipa_hi[task_i], (long long)hi);
+    }
 }
 
 // NodeInfo.AddTask for the winner (node_info.go:113-145) + the k8s NodeInfo
@@ -220,11 +332,13 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
     const TaskClass c = t.classes[cls];
     const bool track = ctrl->any_bf != 0;
+    const int64_t ilo = ctrl->ipa_lo[task_i], ihi = ctrl->ipa_hi[task_i];
+    const int F = ctrl->fallback;
     uint64_t best = 0;
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
         int32_t s = 0;
         bool passed = false;
-        const uint64_t k = eval_node(cf, c, t, nc, n, &s, &passed);
+        const uint64_t k = eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
         if (track) walk[n] = passed ? pack_key(s, n, 0) : 0;
         best = k > best ? k : best;
     }
@@ -261,6 +375,8 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
                 nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
             }
             commit_node(c, t, nc, n, kind);
+            if (c.aff) commit_aff(c, t, nc, n, kind);
+            if (ctrl->fallback < 0 || n < ctrl->fallback) ctrl->fallback = n;
             if (c.backfill) ctrl->any_bf = 1;
             after_assign(ctrl, task_i, kind);
         }
@@ -282,131 +398,6 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
 // ---------------------------------------------------------------------------
 // batched path
 // ---------------------------------------------------------------------------
-// In-LDS bitonic sort, descending, of S (power of two) keys by all threads.
-template <int S, int NT>
-__device__ __forceinline__ void bitonic_desc(uint64_t* a) {
-    for (int k = 2; k <= S; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < S / 2; i += NT) {
-                // i-th compare-exchange pair of this stage
-                const int lo = (i / j) * 2 * j + (i % j);
-                const int hi = lo + j;
-                const bool desc = (lo & k) == 0;
-                const uint64_t x = a[lo], y = a[hi];
-                if ((x < y) == desc) { a[lo] = y; a[hi] = x; }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-template <int R>
-__global__ __launch_bounds__(kBlock) void k_sweep_topk(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
-                                                       uint64_t* cand) {
-    __shared__ uint64_t keys[kBlock * R];
-    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
-    const TaskClass c = t.classes[cls];
-    const int base = blockIdx.x * kBlock * R;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int n = base + r * kBlock + threadIdx.x;
-        uint64_t k = 0;
-        if (n < nc.n) {
-            int32_t s;
-            bool passed;
-            k = eval_node(cf, c, t, nc, n, &s, &passed);
-        }
-        keys[r * kBlock + threadIdx.x] = k;
-    }
-    __syncthreads();
-    bitonic_desc<kBlock * R, kBlock>(keys);
-    if (threadIdx.x < kTopK) cand[(int64_t)blockIdx.x * kTopK + threadIdx.x] = keys[threadIdx.x];
-}
-
-// Single block: merge the per-block candidates, then place the chunk.
-constexpr int kPlaceThreads = 1024;
-constexpr int kMergeMax = 8192;  // keys sortable in LDS (64 KB)
-
-__global__ __launch_bounds__(kPlaceThreads) void k_place_batch(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
-                                                               const uint64_t* cand, int n_cand) {
-    __shared__ uint64_t keys[kMergeMax];
-    __shared__ Row rows[kTopK];
-    __shared__ uint64_t rport[kTopK][4];
-    __shared__ uint64_t cur[kTopK];      // current key of each list entry's node (after changes)
-    __shared__ int changed[kTopK];
-    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
-    const TaskClass c = t.classes[cls];
-    for (int i = threadIdx.x; i < kMergeMax; i += kPlaceThreads) keys[i] = i < n_cand ? cand[i] : 0;
-    __syncthreads();
-    bitonic_desc<kMergeMax, kPlaceThreads>(keys);
-    // keys[0..kTopK) = global top-64 (key order).  Prefetch their rows.
-    if (threadIdx.x < kTopK) {
-        const uint64_t k = keys[threadIdx.x];
-        changed[threadIdx.x] = 0;
-        cur[threadIdx.x] = k;
-        if (k) {
-            const int n = key_idx(k);
-            rows[threadIdx.x] = load_row(nc, n);
-            for (int w = 0; w < 4; ++w)
-                rport[threadIdx.x][w] = (c.has_ports && w < nc.port_words) ? nc.ports[(int64_t)w * nc.npad + n] : 0;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        // Sequential placement.  Entry j of the list is either unchanged (its
-        // key is still keys[j]) or changed (cur[j] re-evaluated after a commit).
-        // The best node is the max over unchanged entries (the first one in
-        // list order) and changed entries; with <= kTopK tasks the list cannot
-        // run out before the chunk does.
-        const int T = ctrl->n_tasks;
-        int first = 0;
-        for (int i = 0; i < T; ++i) {
-            while (first < kTopK && keys[first] && changed[first]) ++first;
-            uint64_t best = (first < kTopK) ? keys[first] : 0;
-            int bj = best ? first : -1;
-            for (int j = 0; j < first; ++j)
-                if (changed[j] && cur[j] > best) { best = cur[j]; bj = j; }
-            if (!best) {
-                ctrl->res_node[i] = -1;
-                ctrl->res_kind[i] = 0;
-                ctrl->n_done = i + 1;
-                ctrl->stop = 1;
-                break;
-            }
-            const int n = key_idx(best), kind = key_kind(best);
-            ctrl->res_node[i] = n;
-            ctrl->res_kind[i] = kind;
-            Row& r = rows[bj];
-            if (kind == 1) { r.idle_cpu -= c.req_cpu; r.idle_mem -= c.req_mem; r.idle_gpu -= c.req_gpu; }
-            else { r.rel_cpu -= c.req_cpu; r.rel_mem -= c.req_mem; r.rel_gpu -= c.req_gpu; }
-            r.pods += 1;
-            r.nzc += c.nz_cpu;
-            r.nzm += c.nz_mem;
-            if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) rport[bj][w] |= t.masks[c.pown_off + w];
-            changed[bj] = 1;
-            int32_t s = 0;
-            bool passed;
-            cur[bj] = dyn_key(cf, c, t, nc, r, rport[bj], n, true, &s, &passed);
-            after_assign(ctrl, i, kind);
-            if (ctrl->stop >= 0) break;
-        }
-    }
-    __syncthreads();
-    // write back changed rows
-    if (threadIdx.x < kTopK && changed[threadIdx.x]) {
-        const int n = key_idx(keys[threadIdx.x]);
-        const Row& r = rows[threadIdx.x];
-        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
-        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
-        nc.pods[n] = r.pods;
-        nc.nzc[n] = r.nzc;
-        nc.nzm[n] = r.nzm;
-        if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = rport[threadIdx.x][w];
-    }
-}
-
 // ---------------------------------------------------------------------------
 // batched path v2: one launch per pop chunk
 // ---------------------------------------------------------------------------
@@ -704,34 +695,11 @@ hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTabl
     return hipGetLastError();
 }
 
-int topk_blocks(int n_nodes, int* R_out) {
-    int R = 1;
-    while ((int64_t)kBlock * R * 128 < n_nodes && R < 32) R <<= 1;
-    *R_out = R;
-    return (n_nodes + kBlock * R - 1) / (kBlock * R);
-}
-
-hipError_t launch_sweep_topk(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, uint64_t* cand,
-                             hipStream_t st) {
-    int R;
-    const int nb = topk_blocks(nc.n, &R);
-    if ((int64_t)nb * kTopK > kMergeMax) return hipErrorInvalidValue;
-    switch (R) {
-        case 1: hipLaunchKernelGGL(k_sweep_topk<1>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-        case 2: hipLaunchKernelGGL(k_sweep_topk<2>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-        case 4: hipLaunchKernelGGL(k_sweep_topk<4>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-        case 8: hipLaunchKernelGGL(k_sweep_topk<8>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-        case 16: hipLaunchKernelGGL(k_sweep_topk<16>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-        default: hipLaunchKernelGGL(k_sweep_topk<32>, dim3(nb), dim3(kBlock), 0, st, cf, nc, t, ctrl, cand); break;
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_place_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
-                              const uint64_t* cand, hipStream_t st) {
-    int R;
-    const int nb = topk_blocks(nc.n, &R);
-    hipLaunchKernelGGL(k_place_batch, dim3(1), dim3(kPlaceThreads), 0, st, cf, nc, t, ctrl, cand, nb * kTopK);
+hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st) {
+    int grid = (nc.n + kBlock - 1) / kBlock;
+    if (grid > 2048) grid = 2048;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(k_ipa_minmax, dim3(grid), dim3(kBlock), 0, st, nc, t, ctrl, task_i);
     return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@
 
 #include "../../include/kbhip.h"
 #include "../../include/kbsnap.h"
+#include "kbhip_affinity.h"
 #include "kbhip_internal.h"
 
 using std::string;
@@ -166,13 +167,14 @@ struct Session {
     F3 total;
     vector<R3> used;  // NodeInfo.Used mirror (for kbhip_read_nodes)
     int any_bf = 0;
+    int32_t fallback = -1;  // lowest node index holding a session-placed pod (nodeorder.go:78-93)
     // device
     Conf conf{};
     NodeCols nc{};
     DevTables tab{};
     vector<TaskClass> classes;
     DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
-        b_ctrl, b_cand, b_walk;
+        b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
     PopCtrl* d_ctrl = nullptr;
     PopCtrl* h_ctrl = nullptr;  // pinned
     DevBuf b_cand2, b_arrive;
@@ -188,7 +190,6 @@ struct Session {
     double phase[12] = {0};  // accumulated phase durations (us)
     int64_t phase_n = 0;
 #endif
-    uint64_t* d_cand = nullptr;
     uint64_t* d_walk = nullptr;
     bool batched = true;
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
@@ -350,11 +351,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
     auto acnt = [&](const char* n) { return V32(n); };
     auto pareq_c = acnt("a_pareq_cnt"), papref_c = acnt("a_papref_cnt"), paareq_c = acnt("a_paareq_cnt"),
          paapref_c = acnt("a_paapref_cnt");
-    // inter-pod affinity is not implemented on the device yet: reject sessions
-    // in which any pod carries pod (anti-)affinity terms (scope).
-    for (size_t a = 0; a < a_flags.size(); ++a)
-        if (pareq_c[a] + papref_c[a] + paareq_c[a] + paapref_c[a] > 0)
-            fail_unsupported("pod (anti-)affinity terms are not supported by this engine build");
+    (void)pareq_c; (void)papref_c; (void)paareq_c; (void)paapref_c;
 
     S.pods.resize(P);
     vector<vector<int>> pod_ports(P);
@@ -471,6 +468,29 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
             if (allocated_status(S.pods[t].status)) j.cnt_alloc++;
             if (S.pods[t].status == AOB) j.cnt_aob++;
         }
+
+    // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
+    AffinityModel aff;
+    {
+        vector<AffPod> ap(P);
+        for (int i = 0; i < P; ++i) {
+            const HPod& p = S.pods[i];
+            AffPod& a = ap[i];
+            a.ns = p.ns;
+            a.status = p.status;
+            a.session_job = p.job >= 0;
+            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
+            a.node = on_node ? p.node : -1;
+            a.target = a.session_job && allocated_status(p.status) && on_node;
+            a.pending = a.session_job && p.status == Pending;
+        }
+        try {
+            aff.build(s, N, npad, ap, E.nss.strs, S.conf.pred_on != 0, S.conf.score_mult > 0 && S.conf.w_pa != 0);
+        } catch (const std::invalid_argument& e) {
+            fail_unsupported(e.what());
+        }
+    }
+    vector<int32_t> aff_items;
 
     // ---------------- task classes for pending tasks ----------------
     // label columns: keys referenced by selectors / node affinity of pending tasks
@@ -610,8 +630,26 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
             if (ok) tol[t / 64] |= 1ULL << (t % 64);
         }
         c.has_ports = pod_ports[i].empty() ? 0 : 1;
+        const AffProgram* pg = aff.program(i);
+        if (pg) {
+            c.aff = 1;
+            c.pred_err |= pg->pred_err;
+            c.ea_n = (int32_t)pg->ea.size() / 2;
+            c.pa_space = pg->pa_space; c.pa_cnt = pg->pa_cnt; c.pa_total = pg->pa_total; c.pa_self = pg->pa_self;
+            c.paa_space = pg->paa_space; c.paa_cnt = pg->paa_cnt;
+            c.ipa_n = (int32_t)pg->ipa.size() / 4;
+            c.upd_n = (int32_t)pg->upd.size() / 3;
+        } else {
+            c.pa_space = c.paa_space = -1;
+        }
         // class signature: the task-relative tables + the class fields (offsets are local)
         string sig((const char*)&c, sizeof(TaskClass));
+        if (pg) {
+            for (auto* v : {&pg->ea, &pg->ipa, &pg->upd}) {
+                sig.append((const char*)v->data(), v->size() * sizeof(int32_t));
+                sig.push_back('|');
+            }
+        }
         sig.append((const char*)L.reqs.data(), L.reqs.size() * sizeof(Req));
         sig.append((const char*)L.terms.data(), L.terms.size() * sizeof(Term));
         sig.append((const char*)L.vals.data(), L.vals.size() * sizeof(int32_t));
@@ -632,6 +670,14 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
         c.pref_term_off += term0;
         c.tol_off = (int32_t)E.masks.size();
         for (auto x : tol) E.masks.push_back(x);
+        if (pg) {
+            c.ea_off = (int32_t)aff_items.size();
+            aff_items.insert(aff_items.end(), pg->ea.begin(), pg->ea.end());
+            c.ipa_off = (int32_t)aff_items.size();
+            aff_items.insert(aff_items.end(), pg->ipa.begin(), pg->ipa.end());
+            c.upd_off = (int32_t)aff_items.size();
+            aff_items.insert(aff_items.end(), pg->upd.begin(), pg->upd.end());
+        }
         p.cls = (int)S.classes.size();
         class_ids.emplace(std::move(sig), p.cls);
         S.classes.push_back(c);
@@ -708,6 +754,19 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
     for (int i = 0; i < N; ++i)
         for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npad + i] |= 1ULL << (id % 64);
     S.nc.ports = upload(S.b_ports, pcol, st);
+    if (aff.active) {
+        S.nc.dom = upload(S.b_dom, aff.dom, st);
+        if (aff_items.empty()) aff_items.push_back(0);
+        S.tab.aff_items = upload(S.b_aff_items, aff_items, st);
+        S.tab.aff_cnt = upload(S.b_aff_cnt, aff.cnt, st);
+        S.tab.aff_scalar = upload(S.b_aff_scalar, aff.scalar, st);
+    } else {
+        vector<int32_t> one(1, 0);
+        S.nc.dom = upload(S.b_dom, one, st);
+        S.tab.aff_items = upload(S.b_aff_items, one, st);
+        S.tab.aff_cnt = upload(S.b_aff_cnt, one, st);
+        S.tab.aff_scalar = upload(S.b_aff_scalar, one, st);
+    }
     S.nc.n = N;
     S.nc.npad = npad;
     S.nc.n_keys = K;
@@ -726,9 +785,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
     S.tab.masks = upload(S.b_masks, E.masks, st);
     S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
     HIPCHK(hipHostMalloc((void**)&S.h_ctrl, sizeof(PopCtrl), hipHostMallocDefault));
-    int R;
-    int nb = topk_blocks(N, &R);
-    S.d_cand = S.b_cand.alloc<uint64_t>((size_t)nb * kTopK);
     S.d_walk = S.b_walk.alloc<uint64_t>(npad);
     {
         int R2;
@@ -766,7 +822,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
         const TaskClass& c = S.classes[cls0];
-        const bool batch = S.batched && !S.any_bf && !c.backfill && S.nc.port_words <= 4;
+        const bool batch = S.batched && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4;
         if (!batch) {  // general path: take up to a chunk of mixed classes
             m = std::min(n - done, kMaxChunk);
         }
@@ -864,11 +920,15 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             h.gang_mode = gang_mode;
             h.n_tasks = m;
             h.any_bf = S.any_bf;
+            h.fallback = S.fallback;
             for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
             std::memset(h.arrive, 0, sizeof h.arrive);
             std::memset(h.slot, 0, sizeof h.slot);
+            std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
+            std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
             HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
             for (int i = 0; i < m; ++i) {
+                if (S.classes[h.cls[i]].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
                 HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
@@ -897,6 +957,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             if (node >= 0) {
                 HPod& p = S.pods[ids[done + i]];
                 S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+                if (S.fallback < 0 || node < S.fallback) S.fallback = node;
             }
         }
         S.any_bf = any_bf_c;

@@ -31,6 +31,7 @@ struct NodeCols {
     int32_t *labels;                           // [n_keys][npad]
     uint64_t *taints;                          // [taint_words][npad] NoSchedule/NoExecute taint ids
     uint64_t *ports;                           // [port_words][npad] used (ip, proto, port) ids
+    int32_t *dom;                              // [n_spaces][npad] topology domain ids (-1: no domain)
     int32_t n, npad, n_keys, taint_words, port_words;
 };
 
@@ -68,6 +69,13 @@ struct TaskClass {
     int32_t has_ports;
     int32_t pred_err;   // predicates fail on every node (e.g. an invalid selector)
     int32_t score_err;  // NodeOrderFn errors on every node: all nodes dropped
+    // pod (anti-)affinity program (kbhip_affinity.h); aff != 0 -> per-task path
+    int32_t aff;
+    int32_t ea_off, ea_n;                  // aff_items pairs (space, cnt_off)
+    int32_t pa_space, pa_cnt, pa_total, pa_self;
+    int32_t paa_space, paa_cnt;
+    int32_t ipa_off, ipa_n;                // aff_items quads (space, cnt_off, sess, weight)
+    int32_t upd_off, upd_n;                // aff_items triples (type, space, off)
     int32_t pad0;
 };
 
@@ -87,12 +95,14 @@ struct PopCtrl {
     int32_t gang_mode;
     int32_t n_tasks;
     int32_t any_bf;        // some node has Backfilled != 0 (GetAccessibleResource mutates Idle)
-    int32_t pad;
+    int32_t fallback;      // lowest node holding a session-placed pod (-1 none; nodeorder.go:78-93)
     int32_t cls[kMaxChunk];        // task class of each task of the chunk
     int32_t res_node[kMaxChunk];
     int32_t res_kind[kMaxChunk];
     uint32_t arrive[kMaxChunk];    // per-task block arrival counters (general path)
     uint64_t slot[kMaxChunk];      // per-task max key (general path)
+    int64_t ipa_lo[kMaxChunk];     // inter-pod affinity min / max count over nodes (0-initialised)
+    int64_t ipa_hi[kMaxChunk];
 };
 
 // Packed selection key: max key wins = highest score, then lowest node index.
