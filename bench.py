@@ -105,6 +105,22 @@ def snapshot_path(args):
     return p
 
 
+def pmc_traffic():
+    """HBM bytes per k_pop_batch launch from the newest committed rocprofv3 PMC
+    summary (profiles/<tag>_summary.json: FETCH_SIZE x 2, the gfx950 correction
+    of MI355X_MICROARCH.md).  PMC counters cannot be read inside a timed run,
+    so this comes from the profiling pass of profiles/run_profile.sh."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime):
+        with open(p) as f:
+            d = json.load(f)
+        for name, k in d.get("kernels", {}).items():
+            if name.startswith("kbhip::k_pop_batch") and "hbm_bytes_per_launch_corrected" in k:
+                best = (k["hbm_bytes_per_launch_corrected"], os.path.basename(p))
+    return best
+
+
 def run_session(buf, device, time_every):
     t0 = time.perf_counter()
     s = kbhip.Session(buf, device=device)
@@ -163,6 +179,7 @@ def main():
             dist.destroy_process_group()
         return
     nodes = st_last["nodes"]
+    traffic = pmc_traffic()
     sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
     achieved = nodes * B_NODE / (sweep_us * 1e-6) / 1e9 if sweeps_n else 0.0
     out = {
@@ -187,7 +204,10 @@ def main():
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
         "roofline": {"kernel": "k_pop_batch", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic[0] if traffic else None,
+                     "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
+                     if traffic else None,
                      "mean_launch_us": sweep_us, "timed_launches": sweeps_n,
                      "bytes_per_launch": nodes * B_NODE},
     }

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise a run_profile.sh output directory into the files committed under
+profiles/: <tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
+<tag>_summary.json (per kernel: calls, mean duration, FETCH_SIZE per launch
+and the gfx950-corrected HBM bytes per launch).
+
+FETCH_SIZE is reported in KB by rocprofv3; on gfx950 it counts exactly half
+the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section),
+so the corrected traffic is 2 x FETCH_SIZE x 1024 bytes.
+
+Usage: python profiles/summarize.py gpurun_out/prof_<tag> <tag>
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
+
+
+def main(src, tag):
+    stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
+    pmc_csv = os.path.join(src, "pmc", "run_counter_collection.csv")
+    out = {"tag": tag, "kernels": {}}
+    with open(stats_csv) as f:
+        for row in csv.DictReader(f):
+            out["kernels"][short(row["Name"])] = {"calls": int(row["Calls"]),
+                                                  "mean_us": float(row["AverageNs"]) / 1e3,
+                                                  "min_us": float(row["MinNs"]) / 1e3,
+                                                  "max_us": float(row["MaxNs"]) / 1e3}
+    if os.path.exists(pmc_csv):
+        acc = defaultdict(lambda: [0.0, 0])
+        with open(pmc_csv) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] != "FETCH_SIZE":
+                    continue
+                a = acc[short(row["Kernel_Name"])]
+                a[0] += float(row["Counter_Value"])
+                a[1] += 1
+        for k, (tot, n) in acc.items():
+            d = out["kernels"].setdefault(k, {})
+            d["fetch_size_kb_per_launch"] = tot / n
+            d["hbm_bytes_per_launch_corrected"] = 2.0 * tot / n * 1024.0
+            d["pmc_launches"] = n
+    for name in ("bench_trace.json", "bench_pmc.json"):
+        p = os.path.join(src, name)
+        if os.path.exists(p):
+            with open(p) as f:
+                lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
+            if lines:
+                out[name.replace(".json", "")] = json.loads(lines[-1])
+    shutil.copy(stats_csv, os.path.join(HERE, f"{tag}_kernel_stats.csv"))
+    with open(os.path.join(HERE, f"{tag}_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out["kernels"], indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
