@@ -121,6 +121,21 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value);
 
 int kbhip_session_close(kb_session* s);
 
+/* Test support (not part of the placement path): encode a snapshot without a
+ * device and read the compiled host tables back by name.  Tables (int32):
+ *   "dims"       n_nodes, npad, n_spaces, n_classes
+ *   "pod_class"  task class of every pod (-1: not a pending task)
+ *   "class_aff"  per class 16 fields: aff, pred_err, ea_off, ea_n, pa_space,
+ *                pa_cnt, pa_total, pa_self, paa_space, paa_cnt, ipa_off, ipa_n,
+ *                upd_off, upd_n, score_err, 0
+ *   "aff_dom"    [n_spaces][npad] topology domain ids
+ *   "aff_cnt", "aff_scalar", "aff_items"  pod-affinity count tables / programs
+ * kbhip_debug_table returns the table size in bytes and copies it when
+ * cap_bytes is large enough.  Sessions from kbhip_debug_encode reject every
+ * call that needs a device (KBHIP_EINVAL). */
+int kbhip_debug_encode(const void* kbs_bytes, size_t len, kb_session** out);
+int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t cap_bytes);
+
 const char* kbhip_last_error(void);
 
 #ifdef __cplusplus

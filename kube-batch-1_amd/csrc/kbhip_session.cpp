@@ -200,6 +200,10 @@ struct Session {
     int64_t timed_n = 0;
     kbhip_stats stats{};
     vector<std::tuple<int, int, int>> log;
+    // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
+    bool encode_only = false;
+    vector<int32_t> h_dom, h_aff_cnt, h_aff_scalar, h_aff_items;
+    int n_spaces = 0;
 
     ~Session() {
         if (ev0) (void)hipEventDestroy(ev0);
@@ -244,7 +248,7 @@ struct Encoder {
 
 static void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
 
-static void open_session(Session& S, const kbs::Snapshot& s, int device) {
+static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false) {
     auto t0 = std::chrono::steady_clock::now();
     Encoder E(s, S);
     auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
@@ -706,6 +710,18 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device) {
             c.pown_off = (int32_t)E.masks.size();
             for (auto x : own) E.masks.push_back(x);
         }
+    }
+    if (encode_only) {  // kbhip_debug_encode: keep the compiled host tables, touch no device
+        S.encode_only = true;
+        S.h_dom = aff.dom;
+        S.h_aff_cnt = aff.cnt;
+        S.h_aff_scalar = aff.scalar;
+        S.h_aff_items = aff_items;
+        S.n_spaces = aff.n_spaces;
+        S.nc.n = N;
+        S.nc.npad = npad;
+        S.stats.nodes = N;
+        return;
     }
     // ---------------- upload ----------------
     HIPCHK(hipSetDevice(device));
@@ -1274,6 +1290,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
     ABI_GUARD({
         if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
             throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
         int rc = kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
                                   out_n_done, out_stop_reason);
@@ -1285,6 +1302,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
 int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     ABI_GUARD({
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
         s->s.log.clear();
         kbhip::Allocator a(s->s);
@@ -1302,6 +1320,7 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
     ABI_GUARD({
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         kbhip::Session& S = s->s;
         const int N = S.nc.n;
         if (n_nodes < N) throw kbhip::Error(KBHIP_EINVAL, "output too small");
@@ -1355,6 +1374,51 @@ int kbhip_debug_phases(kb_session* s, double* out, int n) {
 }
 #endif
 
+int kbhip_debug_encode(const void* bytes, size_t len, kb_session** out) {
+    ABI_GUARD({
+        if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbs::Snapshot snap;
+        snap.load_bytes(bytes, len);
+        std::unique_ptr<kb_session> s(new kb_session());
+        kbhip::open_session(s->s, snap, -1, true);
+        *out = s.release();
+        return KBHIP_OK;
+    })
+}
+int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t cap_bytes) {
+    ABI_GUARD({
+        if (!s || !name) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        const kbhip::Session& S = s->s;
+        vector<int32_t> v;
+        const string n = name;
+        if (n == "pod_class") {
+            for (auto& p : S.pods) v.push_back(p.cls);
+        } else if (n == "class_aff") {  // per class: 16 int32 fields (kbhip.h)
+            for (auto& c : S.classes) {
+                const int32_t f[16] = {c.aff, c.pred_err, c.ea_off, c.ea_n, c.pa_space, c.pa_cnt, c.pa_total,
+                                       c.pa_self, c.paa_space, c.paa_cnt, c.ipa_off, c.ipa_n, c.upd_off, c.upd_n,
+                                       c.score_err, 0};
+                v.insert(v.end(), f, f + 16);
+            }
+        } else if (n == "aff_dom") {
+            if (!S.encode_only) throw kbhip::Error(KBHIP_EINVAL, "tables are kept by encode-only sessions");
+            v = S.h_dom;
+        } else if (n == "aff_cnt") {
+            v = S.h_aff_cnt;
+        } else if (n == "aff_scalar") {
+            v = S.h_aff_scalar;
+        } else if (n == "aff_items") {
+            v = S.h_aff_items;
+        } else if (n == "dims") {  // n_nodes, npad, n_spaces, n_classes
+            v = {S.nc.n, S.nc.npad, S.n_spaces, (int32_t)S.classes.size()};
+        } else {
+            throw kbhip::Error(KBHIP_EINVAL, "unknown table " + n);
+        }
+        const int64_t bytes = (int64_t)(v.size() * sizeof(int32_t));
+        if (out && cap_bytes >= bytes && bytes) std::memcpy(out, v.data(), (size_t)bytes);
+        return bytes;
+    })
+}
 int kbhip_session_close(kb_session* s) {
     ABI_GUARD({
         delete s;

@@ -23,7 +23,7 @@ STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
 # int kbhip_* entry points declared by include/kbhip.h
 EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file", "kbhip_place_job",
            "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
-           "kbhip_session_close", "kbhip_last_error")
+           "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table")
 
 
 class KbhipError(RuntimeError):
@@ -67,6 +67,9 @@ def lib() -> ctypes.CDLL:
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
         L.kbhip_session_close.argtypes = [vp]
+        L.kbhip_debug_encode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
+        L.kbhip_debug_table.argtypes = [vp, ctypes.c_char_p, vp, i64]
+        L.kbhip_debug_table.restype = i64
         _lib = L
     return _lib
 
@@ -147,3 +150,34 @@ class Session:
         st = Stats()
         _check(lib().kbhip_get_stats(self._h, ctypes.byref(st)))
         return st.as_dict()
+
+
+class EncodedSnapshot:
+    """Test support: the engine's compiled host tables for a snapshot, built
+    without a device (kbhip_debug_encode).  It cannot place anything."""
+
+    def __init__(self, snapshot):
+        if not isinstance(snapshot, (bytes, bytearray, memoryview)):
+            with open(snapshot, "rb") as f:
+                snapshot = f.read()
+        buf = bytes(snapshot)
+        self._h = ctypes.c_void_p()
+        _check(lib().kbhip_debug_encode(ctypes.c_char_p(buf), len(buf), ctypes.byref(self._h)))
+
+    def table(self, name: str) -> np.ndarray:
+        n = lib().kbhip_debug_table(self._h, name.encode(), None, 0)
+        _check(int(n) if n < 0 else 0)
+        out = np.zeros(max(int(n) // 4, 1), np.int32)
+        _check(int(lib().kbhip_debug_table(self._h, name.encode(), _p(out), out.nbytes)) if n > 0 else 0)
+        return out[: int(n) // 4]
+
+    def close(self) -> None:
+        if self._h:
+            _check(lib().kbhip_session_close(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -792,6 +792,46 @@ static void buildPlan(const World& w, TaskPlan& tp) {
     }
 }
 
+/* the pod (anti-)affinity part of the predicate (predicates.go:1293-1458) */
+static bool podAffinityOk(const TaskPlan& tp, const NodeRec& n) {
+    for (auto& kv : n.labels) if (tp.forbidden.count(kv)) return false;  // predicates.go:1326-1331
+    if (tp.hasAffTerms) {                                                // predicates.go:1402-1458
+        bool match = false;
+        vector<int> tup;
+        bool ok = true;
+        for (int k : tp.affKeys) {
+            int v = k < 0 ? -1 : lget(n.labels, k);
+            if (v < 0) { ok = false; break; }
+            tup.push_back(v);
+        }
+        if (ok) match = std::binary_search(tp.affTuples.begin(), tp.affTuples.end(), tup);
+        if (!match && !tp.affSelfPass) return false;
+    }
+    if (tp.hasAntiTerms) {
+        vector<int> tup;
+        bool ok = true;
+        for (int k : tp.antiKeys) {
+            int v = k < 0 ? -1 : lget(n.labels, k);
+            if (v < 0) { ok = false; break; }
+            tup.push_back(v);
+        }
+        if (ok && std::binary_search(tp.antiTuples.begin(), tp.antiTuples.end(), tup)) return false;
+    }
+    return true;
+}
+
+/* raw inter-pod affinity count of a node (interpod_affinity.go:119-212) */
+static double ipaRaw(const TaskPlan& tp, const NodeRec& n) {
+    double c = 0;
+    for (int k : tp.ipaKeys) {
+        int v = lget(n.labels, k);
+        if (v < 0) continue;
+        auto it = tp.ipaAcc.find({k, v});
+        if (it != tp.ipaAcc.end()) c += it->second;
+    }
+    return c;
+}
+
 /* one node: predicate + score; returns false when the node is filtered out */
 static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* scoreOut) {
     const NodeRec& n = w.nodes[ni];
@@ -835,29 +875,7 @@ static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* sco
         }
         if (n.unsched) return false;                                         // predicates.go:107-112
         for (int t : n.taints) if (!tp.tol[t]) return false;                 // helper/helpers.go:425-440
-        for (auto& kv : n.labels) if (tp.forbidden.count(kv)) return false;  // predicates.go:1326-1331
-        if (tp.hasAffTerms) {                                                // predicates.go:1402-1458
-            bool match = false;
-            vector<int> tup;
-            bool ok = true;
-            for (int k : tp.affKeys) {
-                int v = k < 0 ? -1 : lget(n.labels, k);
-                if (v < 0) { ok = false; break; }
-                tup.push_back(v);
-            }
-            if (ok) match = std::binary_search(tp.affTuples.begin(), tp.affTuples.end(), tup);
-            if (!match && !tp.affSelfPass) return false;
-        }
-        if (tp.hasAntiTerms) {
-            vector<int> tup;
-            bool ok = true;
-            for (int k : tp.antiKeys) {
-                int v = k < 0 ? -1 : lget(n.labels, k);
-                if (v < 0) { ok = false; break; }
-                tup.push_back(v);
-            }
-            if (ok && std::binary_search(tp.antiTuples.begin(), tp.antiTuples.end(), tup)) return false;
-        }
+        if (!podAffinityOk(tp, n)) return false;
     }
     int score = 0;
     if (w.nodeorderOn) {
@@ -887,14 +905,7 @@ static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* sco
             }
         int ipa = 0;
         if (tp.ipaOn && tp.ipaMax - tp.ipaMin > 0) {
-            double c = 0;
-            for (int k : tp.ipaKeys) {
-                int v = lget(n.labels, k);
-                if (v < 0) continue;
-                auto it = tp.ipaAcc.find({k, v});
-                if (it != tp.ipaAcc.end()) c += it->second;
-            }
-            double f = 10.0 * ((c - tp.ipaMin) / (tp.ipaMax - tp.ipaMin));
+            double f = 10.0 * ((ipaRaw(tp, n) - tp.ipaMin) / (tp.ipaMax - tp.ipaMin));
             ipa = (int)f;
         }
         score = ((int)lr * w.wLR + (int)bra * w.wBRA + na * w.wNA + ipa * w.wPA) * w.noMult;
@@ -1142,12 +1153,42 @@ struct Engine {
         if (p.hasPodAff()) w.affPods.push_back(pi);
     }
 
+    // Test-only trace of the pod-affinity view of every task tried (per node:
+    // affinity predicate verdict, raw inter-pod count), for cross-checking an
+    // engine's affinity tables (tests/test_affinity_tables.py).
+    struct AffTrace {
+        vector<int32_t> pod, node, status;
+        vector<uint8_t> ok;     // [task][node]
+        vector<double> raw;     // [task][node]
+        vector<double> lohi;    // [task][2]
+        vector<uint8_t> flags;  // [task]: bit0 predErrAll, bit1 scoreErrAll, bit2 ipaOn
+    };
+    AffTrace* trace = nullptr;
+
     // one task: predicate + score sweep, select, commit.  Returns assigned.
     bool placeTask(int pi) {
+        bool r = placeTaskInner(pi);
+        if (trace) {
+            trace->pod.push_back(pi);
+            trace->node.push_back(r ? w.pods[pi].curNode : -1);
+            trace->status.push_back(r ? w.pods[pi].status : 0);
+        }
+        return r;
+    }
+    bool placeTaskInner(int pi) {
         tried++;
         TaskPlan tp;
         tp.pod = pi;
         buildPlan(w, tp);
+        if (trace) {
+            for (auto& n : w.nodes) {
+                trace->ok.push_back(w.predOn ? podAffinityOk(tp, n) : 1);
+                trace->raw.push_back(tp.ipaOn ? ipaRaw(tp, n) : 0.0);
+            }
+            trace->lohi.push_back(tp.ipaMin);
+            trace->lohi.push_back(tp.ipaMax);
+            trace->flags.push_back((tp.predErrAll ? 1 : 0) | (tp.scoreErrAll ? 2 : 0) | (tp.ipaOn ? 4 : 0));
+        }
         PodRec& p = w.pods[pi];
         int N = (int)w.nodes.size();
         int T = pool.T;
@@ -1255,6 +1296,42 @@ static thread_local std::string g_ferr;
 
 extern "C" {
 const char* fast_last_error(void) { return g_ferr.c_str(); }
+
+/* Test-only: the allocate run with the per-task affinity trace (see AffTrace).
+ * Arrays are sized by the caller: cap_tasks tasks, n_nodes nodes.  Returns the
+ * number of tasks tried (or <0 on error). */
+int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* out_pod, int32_t* out_node,
+                        int32_t* out_status, uint8_t* out_ok, double* out_raw, double* out_lohi, uint8_t* out_flags) {
+    try {
+        kbs::Snapshot snap(path);
+        fast::World w;
+        fast::Loader L(snap, w);
+        L.load();
+        if ((int)w.nodes.size() != n_nodes) throw std::runtime_error("node count mismatch");
+        fast::Engine e(w, 1);
+        fast::Engine::AffTrace tr;
+        e.trace = &tr;
+        e.openPlugins();
+        e.allocate(-1);
+        const int n = (int)tr.pod.size();
+        for (int i = 0; i < n && i < cap_tasks; ++i) {
+            out_pod[i] = tr.pod[i];
+            out_node[i] = tr.node[i];
+            out_status[i] = tr.status[i];
+            out_flags[i] = tr.flags[i];
+            out_lohi[2 * i] = tr.lohi[2 * i];
+            out_lohi[2 * i + 1] = tr.lohi[2 * i + 1];
+            for (int k = 0; k < n_nodes; ++k) {
+                out_ok[(size_t)i * n_nodes + k] = tr.ok[(size_t)i * n_nodes + k];
+                out_raw[(size_t)i * n_nodes + k] = tr.raw[(size_t)i * n_nodes + k];
+            }
+        }
+        return n;
+    } catch (const std::exception& ex) {
+        g_ferr = ex.what();
+        return -1;
+    }
+}
 
 /* Hoisted allocate.  timing[0]=open s, [1]=allocate s, [2]=pops, [3]=tasks tried, [4]=load s */
 int fast_allocate(const char* path, int threads, int max_pops, int32_t* out_pod, int32_t* out_node,

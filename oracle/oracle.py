@@ -146,3 +146,30 @@ def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
         stats.update(open_s=tm[0], allocate_s=tm[1], pops=int(tm[2]), tasks_tried=int(tm[3]),
                      load_s=tm[4])
     return Placement(pod[:n].copy(), node[:n].copy(), st[:n].copy())
+
+
+def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096) -> dict:
+    """Test support: run the hoisted allocate with the per-task pod-affinity
+    trace.  For every task tried, in order: pod, result node (-1 unassigned),
+    status, per-node pod-affinity predicate verdict (ok), per-node raw
+    inter-pod affinity count (raw), its [min, max] over nodes (lohi) and flags
+    (bit0 predicate error on every node, bit1 score error, bit2 IPA on)."""
+    lib = _lib("kbfast")
+    fn = lib.fast_trace_affinity
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7
+    pod = np.zeros(cap_tasks, np.int32)
+    node = np.zeros(cap_tasks, np.int32)
+    st = np.zeros(cap_tasks, np.int32)
+    ok = np.zeros((cap_tasks, n_nodes), np.uint8)
+    raw = np.zeros((cap_tasks, n_nodes), np.float64)
+    lohi = np.zeros((cap_tasks, 2), np.float64)
+    flags = np.zeros(cap_tasks, np.uint8)
+    n = fn(path.encode(), cap_tasks, n_nodes, _p(pod), _p(node), _p(st), _p(ok), _p(raw), _p(lohi), _p(flags))
+    if n < 0:
+        lib.fast_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.fast_last_error().decode())
+    if n > cap_tasks:
+        raise RuntimeError("trace larger than cap_tasks")
+    return {"pod": pod[:n], "node": node[:n], "status": st[:n], "ok": ok[:n], "raw": raw[:n],
+            "lohi": lohi[:n], "flags": flags[:n]}
