@@ -109,6 +109,13 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
  * order: pod index, node index, kind.  Returns the number of placements. */
 int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 
+/* Run the backfill action (actions/backfill/backfill.go:40-70) on the
+ * session's current state (normally after kbhip_allocate): every Pending task
+ * with an empty InitResreq goes to the first node (lowest index) passing the
+ * predicates.  Outputs the placements (all KBHIP_ALLOCATED) like
+ * kbhip_allocate; returns their number. */
+int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+
 /* Read the device node state: N x 12 int64 (idle, used, releasing,
  * backfilled; cpu/mem/gpu each).  `used` is maintained on the host mirror. */
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes);

@@ -245,6 +245,21 @@ __device__ __forceinline__ uint64_t eval_node_aff(const Conf& cf, const TaskClas
     return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed, ipa);
 }
 
+// Backfill's node test (backfill.go:51-56): the predicates only — no score,
+// no fit — keyed so that the max key is the lowest passing index.
+__device__ __forceinline__ uint64_t eval_first_fit(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                                   const NodeCols& nc, int n) {
+    bool ok = static_pred(cf, c, t, nc, n);
+    if (ok && cf.pred_on) {
+        if (c.aff) ok = aff_pred(c, t, nc, n);
+        if (nc.maxtasks[n] <= nc.pods[n]) ok = false;                    // predicates.go:127
+        if (c.has_ports)                                                 // host_ports.go:96-125
+            for (int w = 0; w < nc.port_words; ++w)
+                if (nc.ports[(int64_t)w * nc.npad + n] & t.masks[c.pconf_off + w]) ok = false;
+    }
+    return ok ? pack_key(0, n, 0) : 0;
+}
+
 // Count-table updates of a committed task (kind 1 Allocated, 2 Pipelined).
 __device__ void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {
     for (int i = 0; i < c.upd_n; ++i) {
@@ -331,14 +346,16 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     if (ctrl->stop >= 0) return;  // the pop already stopped (uniform)
     const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
     const TaskClass c = t.classes[cls];
-    const bool track = ctrl->any_bf != 0;
+    const bool first_fit = ctrl->mode == 1;
+    const bool track = !first_fit && ctrl->any_bf != 0;  // backfill never calls GetAccessibleResource
     const int64_t ilo = ctrl->ipa_lo[task_i], ihi = ctrl->ipa_hi[task_i];
     const int F = ctrl->fallback;
     uint64_t best = 0;
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
         int32_t s = 0;
         bool passed = false;
-        const uint64_t k = eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
+        const uint64_t k = first_fit ? eval_first_fit(cf, c, t, nc, n)
+                                     : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
         if (track) walk[n] = passed ? pack_key(s, n, 0) : 0;
         best = k > best ? k : best;
     }
@@ -362,7 +379,19 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     if (threadIdx.x == 0) {
         const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         win = k;
-        if (k == 0) {
+        if (first_fit) {  // backfill: Session.Allocate on the first passing node; no stop rule
+            ctrl->res_node[task_i] = k ? key_idx(k) : -1;
+            ctrl->res_kind[task_i] = k ? 1 : 0;
+            if (k) {
+                const int n = key_idx(k);
+                commit_node(c, t, nc, n, 1);
+                if (c.aff) commit_aff(c, t, nc, n, 1);
+                if (ctrl->fallback < 0 || n < ctrl->fallback) ctrl->fallback = n;
+                if (c.backfill) ctrl->any_bf = 1;
+            }
+            ctrl->n_done = task_i + 1;
+            if (task_i + 1 == ctrl->n_tasks) ctrl->stop = 0;
+        } else if (k == 0) {
             ctrl->res_node[task_i] = -1;
             ctrl->res_kind[task_i] = 0;
             ctrl->n_done = task_i + 1;

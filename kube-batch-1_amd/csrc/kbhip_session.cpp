@@ -825,6 +825,62 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 }
 
 // ---------------------------------------------------------------------------
+// backfill action (actions/backfill/backfill.go:40-70): every Pending task of
+// every job whose InitResreq is empty is allocated on the first node (lowest
+// index) passing the predicates.  Pinned order:
+// jobs by UID, tasks by UID, nodes by index.  Per-task first-fit sweeps of the
+// general kernel (mode 1), 64 tasks per control-block round trip.
+// ---------------------------------------------------------------------------
+static void backfill_run(Session& S) {
+    vector<int> cand;
+    for (auto& j : S.jobs)
+        for (int t : j.tasks) {
+            const HPod& p = S.pods[t];
+            if (p.status != Pending || p.cls < 0) continue;
+            if (!(p.ireq.c < kMinCPU && p.ireq.m < kMinMem && p.ireq.g < kMinGPU)) continue;  // IsEmpty
+            cand.push_back(t);
+        }
+    for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
+        const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
+        PopCtrl& h = *S.h_ctrl;
+        h.stop = -1;
+        h.n_done = 0;
+        h.ready_count = 0;
+        h.min_avail = 0;
+        h.gang_mode = 0;
+        h.n_tasks = m;
+        h.any_bf = S.any_bf;
+        h.fallback = S.fallback;
+        h.mode = 1;
+        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[cand[off + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
+        std::memset(h.arrive, 0, sizeof h.arrive);
+        std::memset(h.slot, 0, sizeof h.slot);
+        std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
+        std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
+        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+        for (int i = 0; i < m; ++i) HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
+        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+        S.stats.sweeps += m;
+        S.stats.tasks += m;
+        if (h.n_done != m || h.stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
+        for (int i = 0; i < m; ++i) {
+            const int node = h.res_node[i];
+            if (node < 0) continue;
+            HPod& p = S.pods[cand[off + i]];
+            p.status = Allocated;  // Session.Allocate(task, node, false) (session.go:237-297)
+            p.node = node;
+            S.jobs[p.job].cnt_alloc++;
+            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
+            S.stats.placed++;
+            S.log.emplace_back(cand[off + i], node, KBHIP_ALLOCATED);
+        }
+        S.any_bf = h.any_bf;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // device driver for one job pop
 // ---------------------------------------------------------------------------
 static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
@@ -937,6 +993,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             h.n_tasks = m;
             h.any_bf = S.any_bf;
             h.fallback = S.fallback;
+            h.mode = 0;
             for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
             std::memset(h.arrive, 0, sizeof h.arrive);
             std::memset(h.slot, 0, sizeof h.slot);
@@ -1317,6 +1374,22 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
     })
 }
 
+int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        s->s.log.clear();
+        kbhip::backfill_run(s->s);
+        const int64_t n = (int64_t)s->s.log.size();
+        for (int64_t i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(s->s.log[i]);
+            out_node[i] = std::get<1>(s->s.log[i]);
+            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
+        }
+        return (int)n;
+    })
+}
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
     ABI_GUARD({
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");

@@ -96,6 +96,8 @@ struct PopCtrl {
     int32_t n_tasks;
     int32_t any_bf;        // some node has Backfilled != 0 (GetAccessibleResource mutates Idle)
     int32_t fallback;      // lowest node holding a session-placed pod (-1 none; nodeorder.go:78-93)
+    int32_t mode;          // 0: allocate (best node, gang stop); 1: backfill (first fit, no stop)
+    int32_t pad;
     int32_t cls[kMaxChunk];        // task class of each task of the chunk
     int32_t res_node[kMaxChunk];
     int32_t res_kind[kMaxChunk];

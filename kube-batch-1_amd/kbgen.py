@@ -701,7 +701,7 @@ def gen_random(seed: int, n_nodes: int = 8, n_jobs: int = 6, max_tasks: int = 5,
                features: Sequence[str] = ("labels", "taints", "ports", "affinity", "init",
                                           "running", "releasing", "backfill", "selector", "nodeaffinity",
                                           "podaffinity", "unsched", "bestEffort"),
-               tiers=None, n_queues: int = 2) -> Cluster:
+               tiers=None, n_queues: int = 2, best_effort_p: float = 0.1) -> Cluster:
     """Small random cluster exercising every feature of the hot path (parity tests)."""
     rng = np.random.default_rng(seed)
     f = set(features)
@@ -769,7 +769,7 @@ def gen_random(seed: int, n_nodes: int = 8, n_jobs: int = 6, max_tasks: int = 5,
             ctrs = [rand_res()]
             if rng.random() < 0.3:
                 ctrs.append(rand_res())
-            if "bestEffort" in f and rng.random() < 0.1:
+            if "bestEffort" in f and rng.random() < best_effort_p:
                 ctrs = [{}]
             if "ports" in f and rng.random() < 0.2:
                 ctrs[0]["ports"] = [{"port": int(rng.choice([80, 8080])),

@@ -23,7 +23,8 @@ STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
 # int kbhip_* entry points declared by include/kbhip.h
 EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file", "kbhip_place_job",
            "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
-           "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table")
+           "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
+           "kbhip_backfill")
 
 
 class KbhipError(RuntimeError):
@@ -63,6 +64,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_session_open_file.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
         L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_read_nodes.argtypes = [vp, vp, i64]
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
@@ -128,6 +130,31 @@ class Session:
         if n > cap:
             raise KbhipError("placement log larger than cap")
         return pod[:n].copy(), node[:n].copy(), kind[:n].copy()
+
+    def backfill(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Run backfillAction.Execute on the current session state."""
+        pod = np.zeros(cap, np.int32)
+        node = np.zeros(cap, np.int32)
+        kind = np.zeros(cap, np.uint8)
+        n = _check(lib().kbhip_backfill(self._h, _p(pod), _p(node), _p(kind), cap))
+        if n > cap:
+            raise KbhipError("placement log larger than cap")
+        return pod[:n].copy(), node[:n].copy(), kind[:n].copy()
+
+    def run_actions(self, actions: str = "allocate") -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """The conf's actions in order (scheduler.go:93-97); supported: allocate, backfill."""
+        logs = []
+        for a in (x.strip() for x in actions.split(",")):
+            if a == "allocate":
+                logs.append(self.allocate())
+            elif a == "backfill":
+                logs.append(self.backfill())
+            else:
+                raise KbhipError(f"action {a!r} is not implemented by this engine")
+        if not logs:
+            z = np.zeros(0, np.int32)
+            return z, z.copy(), np.zeros(0, np.uint8)
+        return tuple(np.concatenate([lg[k] for lg in logs]) for k in range(3))
 
     def place_job(self, task_ids, gang_mode: int, min_available: int, ready_count: int):
         ids = np.ascontiguousarray(task_ids, dtype=np.int32)

@@ -832,8 +832,8 @@ static double ipaRaw(const TaskPlan& tp, const NodeRec& n) {
     return c;
 }
 
-/* one node: predicate + score; returns false when the node is filtered out */
-static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* scoreOut) {
+/* the predicates plugin's PredicateFn for one node (predicates.go:123-203) */
+static inline bool predOk(const World& w, const TaskPlan& tp, int ni) {
     const NodeRec& n = w.nodes[ni];
     const PodRec& pod = w.pods[tp.pod];
     if (w.predOn) {
@@ -877,6 +877,14 @@ static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* sco
         for (int t : n.taints) if (!tp.tol[t]) return false;                 // helper/helpers.go:425-440
         if (!podAffinityOk(tp, n)) return false;
     }
+    return true;
+}
+
+/* one node: predicate + score; returns false when the node is filtered out */
+static inline bool evalNode(const World& w, const TaskPlan& tp, int ni, int* scoreOut) {
+    if (!predOk(w, tp, ni)) return false;
+    const NodeRec& n = w.nodes[ni];
+    const PodRec& pod = w.pods[tp.pod];
     int score = 0;
     if (w.nodeorderOn) {
         if (tp.scoreErrAll) return false;
@@ -1243,6 +1251,51 @@ struct Engine {
         return true;
     }
 
+    // backfill action (actions/backfill/backfill.go:40-70): every Pending task
+    // of every job (pinned order: jobs by UID, tasks by UID) whose InitResreq is
+    // empty goes to the first node (by index) passing the predicates.
+    void backfill() {
+        for (size_t jb = 0; jb < w.jobs.size(); ++jb) {
+            for (int pi : w.jobs[jb].tasks) {
+                PodRec& p = w.pods[pi];
+                if (p.status != Pending || !isEmpty(p.initReq)) continue;
+                tried++;
+                TaskPlan tp;
+                tp.pod = pi;
+                buildPlan(w, tp);
+                const int N = (int)w.nodes.size();
+                int first = -1;
+                for (int ni = 0; ni < N && first < 0; ++ni)
+                    if (predOk(w, tp, ni)) first = ni;
+                if (first < 0) continue;
+                JobRec& j = w.jobs[jb];
+                p.status = Allocated;  // Session.Allocate(task, node, false)
+                j.cntAlloc++;
+                p.curNode = first;
+                nodeAddTask(pi, first, Allocated);
+                onAllocate(p);
+                w.log.emplace_back(pi, first, Allocated);
+                if (jobReady(j))
+                    for (int t : j.tasks) if (w.pods[t].status == Allocated) w.pods[t].status = Binding;
+            }
+        }
+    }
+
+    // scheduler.go:93-97 / util.go:51-58: comma-separated, trimmed action names
+    void runActions(const char* actions, int maxPops) {
+        string all = actions ? actions : "allocate", cur;
+        all.push_back(',');
+        for (char ch : all) {
+            if (ch != ',') { cur.push_back(ch); continue; }
+            size_t a = cur.find_first_not_of(" \t\n"), b = cur.find_last_not_of(" \t\n");
+            string name = a == string::npos ? string() : cur.substr(a, b - a + 1);
+            cur.clear();
+            if (name == "allocate") allocate(maxPops);
+            else if (name == "backfill") backfill();
+            else throw std::runtime_error("action '" + name + "' is not implemented by this oracle");
+        }
+    }
+
     void allocate(int maxPops) {  // allocate.go:41-201
         auto ql = [this](int a, int b) { return queueLess(a, b); };
         auto jl = [this](int a, int b) { return jobLess(a, b); };
@@ -1301,7 +1354,8 @@ const char* fast_last_error(void) { return g_ferr.c_str(); }
  * Arrays are sized by the caller: cap_tasks tasks, n_nodes nodes.  Returns the
  * number of tasks tried (or <0 on error). */
 int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* out_pod, int32_t* out_node,
-                        int32_t* out_status, uint8_t* out_ok, double* out_raw, double* out_lohi, uint8_t* out_flags) {
+                        int32_t* out_status, uint8_t* out_ok, double* out_raw, double* out_lohi, uint8_t* out_flags,
+                        const char* actions) {
     try {
         kbs::Snapshot snap(path);
         fast::World w;
@@ -1312,7 +1366,7 @@ int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* o
         fast::Engine::AffTrace tr;
         e.trace = &tr;
         e.openPlugins();
-        e.allocate(-1);
+        e.runActions(actions, -1);
         const int n = (int)tr.pod.size();
         for (int i = 0; i < n && i < cap_tasks; ++i) {
             out_pod[i] = tr.pod[i];
@@ -1335,7 +1389,7 @@ int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* o
 
 /* Hoisted allocate.  timing[0]=open s, [1]=allocate s, [2]=pops, [3]=tasks tried, [4]=load s */
 int fast_allocate(const char* path, int threads, int max_pops, int32_t* out_pod, int32_t* out_node,
-                  int32_t* out_status, int cap, double* timing) {
+                  int32_t* out_status, int cap, double* timing, const char* actions /* NULL = "allocate" */) {
     try {
         using clk = std::chrono::steady_clock;
         auto t0 = clk::now();
@@ -1347,7 +1401,7 @@ int fast_allocate(const char* path, int threads, int max_pops, int32_t* out_pod,
         fast::Engine e(w, threads < 1 ? 1 : threads);
         e.openPlugins();
         auto t2 = clk::now();
-        e.allocate(max_pops);
+        e.runActions(actions, max_pops);
         auto t3 = clk::now();
         int n = (int)w.log.size();
         for (int i = 0; i < n && i < cap; ++i) {

@@ -1656,6 +1656,53 @@ static void allocateExecute(World& w) {
     }
 }
 
+/* ---- backfill action (actions/backfill/backfill.go:40-70) --------------- */
+static void backfillExecute(World& w) {
+    Session& ssn = w.ssn;
+    for (auto* job : ssn.Jobs) {
+        auto it = job->TaskStatusIndex.find(Pending);
+        if (it == job->TaskStatusIndex.end()) continue;
+        // Go ranges over the live map; only the current task leaves the Pending
+        // index during its iteration, so a copy of the keys visits the same tasks.
+        vector<TaskInfo*> ts;
+        for (auto& kv : it->second) ts.push_back(kv.second);
+        for (auto* task : ts) {
+            if (!task->InitResreq.IsEmpty()) continue;  // "backfill for other case" is a TODO
+            for (auto* node : ssn.Nodes) {
+                if (!ssn.PredicateFn_(task, node)) continue;
+                if (!ssn.Allocate(task, node, false)) continue;
+                break;
+            }
+        }
+    }
+}
+
+// scheduler.go:93-97 runs the conf's actions in order; util.go:51-58 splits
+// the "actions" string on commas and trims each name.
+static vector<string> splitActions(const char* actions) {
+    vector<string> out;
+    string cur, all = actions ? actions : "allocate";
+    all.push_back(',');
+    for (char ch : all) {
+        if (ch == ',') {
+            size_t a = cur.find_first_not_of(" \t\n"), b = cur.find_last_not_of(" \t\n");
+            out.push_back(a == string::npos ? string() : cur.substr(a, b - a + 1));
+            cur.clear();
+        } else {
+            cur.push_back(ch);
+        }
+    }
+    return out;
+}
+
+static void runActions(World& w, const char* actions) {
+    for (auto& a : splitActions(actions)) {
+        if (a == "allocate") allocateExecute(w);
+        else if (a == "backfill") backfillExecute(w);
+        else throw std::runtime_error("action '" + a + "' is not implemented by this oracle");
+    }
+}
+
 }  // namespace ref
 
 /* ------------------------------------------------------------------------ */
@@ -1667,17 +1714,18 @@ extern "C" {
 
 const char* ref_last_error(void) { return g_err.c_str(); }
 
-/* Run the allocate action on a KBS1 snapshot.  Outputs, in placement order:
+/* Run the allocate action (or the given conf actions) on a KBS1 snapshot.  Outputs, in placement order:
  * pod index, node index, status code (ref::TaskStatus).  Returns the number
  * of placements, or -1 on error.  `cap` bounds the output arrays. */
 int ref_allocate(const char* path, int32_t* out_pod, int32_t* out_node, int32_t* out_status, int cap,
-                 double* out_node_state /* optional: N x 12 doubles: idle, used, releasing, backfilled */) {
+                 double* out_node_state /* optional: N x 12 doubles: idle, used, releasing, backfilled */,
+                 const char* actions /* comma-separated conf actions; NULL = "allocate" */) {
     try {
         ref::World w;
         w.snap.load_file(path);
         ref::loadWorld(w);
         ref::openSession(w);
-        ref::allocateExecute(w);
+        ref::runActions(w, actions);
         int n = (int)w.ssn.log.size();
         for (int i = 0; i < n && i < cap; ++i) {
             out_pod[i] = std::get<0>(w.ssn.log[i]);

@@ -68,11 +68,13 @@ class Placement:
         return np.where(self.status == PIPELINED, 2, 1).astype(np.int32)
 
 
-def ref_allocate(path: str, cap: Optional[int] = None, with_nodes: bool = False):
+def ref_allocate(path: str, cap: Optional[int] = None, with_nodes: bool = False, actions: str = "allocate"):
+    """Faithful restatement: the conf actions (default: allocate only) on the
+    snapshot; placement log in decision order."""
     lib = _lib("kbref")
     fn = lib.ref_allocate
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p]
+    fn.argtypes = [ctypes.c_char_p] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p]
     cap = cap or 1 << 20
     pod = np.zeros(cap, np.int32)
     node = np.zeros(cap, np.int32)
@@ -80,7 +82,8 @@ def ref_allocate(path: str, cap: Optional[int] = None, with_nodes: bool = False)
     nstate = None
     if with_nodes:
         nstate = np.zeros((1 << 16, 12), np.float64)
-    n = fn(path.encode(), _p(pod), _p(node), _p(st), cap, _p(nstate) if nstate is not None else None)
+    n = fn(path.encode(), _p(pod), _p(node), _p(st), cap, _p(nstate) if nstate is not None else None,
+           actions.encode())
     if n < 0:
         lib.ref_last_error.restype = ctypes.c_char_p
         raise RuntimeError(lib.ref_last_error().decode())
@@ -125,20 +128,20 @@ def ref_job_readiness(min_available: int, statuses: List[int]) -> int:
 
 
 def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
-                  max_pops: int = -1, stats: Optional[dict] = None) -> Placement:
+                  max_pops: int = -1, stats: Optional[dict] = None, actions: str = "allocate") -> Placement:
     """Hoisted restatement (CPU baseline).  ``max_pops`` bounds the number of
     job pops (a bounded sample of the session for timing)."""
     lib = _lib("kbfast")
     fn = lib.fast_allocate
     fn.restype = ctypes.c_int
     fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3 + \
-        [ctypes.c_int, ctypes.c_void_p]
+        [ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p]
     cap = cap or (1 << 21)
     pod = np.zeros(cap, np.int32)
     node = np.zeros(cap, np.int32)
     st = np.zeros(cap, np.int32)
     tm = np.zeros(8, np.float64)
-    n = fn(path.encode(), threads, max_pops, _p(pod), _p(node), _p(st), cap, _p(tm))
+    n = fn(path.encode(), threads, max_pops, _p(pod), _p(node), _p(st), cap, _p(tm), actions.encode())
     if n < 0:
         lib.fast_last_error.restype = ctypes.c_char_p
         raise RuntimeError(lib.fast_last_error().decode())
@@ -148,7 +151,7 @@ def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
     return Placement(pod[:n].copy(), node[:n].copy(), st[:n].copy())
 
 
-def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096) -> dict:
+def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096, actions: str = "allocate") -> dict:
     """Test support: run the hoisted allocate with the per-task pod-affinity
     trace.  For every task tried, in order: pod, result node (-1 unassigned),
     status, per-node pod-affinity predicate verdict (ok), per-node raw
@@ -157,7 +160,7 @@ def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096) -> dict:
     lib = _lib("kbfast")
     fn = lib.fast_trace_affinity
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + [ctypes.c_char_p]
     pod = np.zeros(cap_tasks, np.int32)
     node = np.zeros(cap_tasks, np.int32)
     st = np.zeros(cap_tasks, np.int32)
@@ -165,7 +168,8 @@ def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096) -> dict:
     raw = np.zeros((cap_tasks, n_nodes), np.float64)
     lohi = np.zeros((cap_tasks, 2), np.float64)
     flags = np.zeros(cap_tasks, np.uint8)
-    n = fn(path.encode(), cap_tasks, n_nodes, _p(pod), _p(node), _p(st), _p(ok), _p(raw), _p(lohi), _p(flags))
+    n = fn(path.encode(), cap_tasks, n_nodes, _p(pod), _p(node), _p(st), _p(ok), _p(raw), _p(lohi), _p(flags),
+           actions.encode())
     if n < 0:
         lib.fast_last_error.restype = ctypes.c_char_p
         raise RuntimeError(lib.fast_last_error().decode())

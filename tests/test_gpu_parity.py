@@ -82,6 +82,24 @@ def test_random_pod_affinity_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
         assert got == exp, f"batched={batched}"
 
 
+@pytest.mark.parametrize("seed", range(30))
+def test_allocate_then_backfill_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """actions "allocate, backfill": BestEffort tasks first-fit after allocate."""
+    tiers = [None, [["drf", "proportion"]], [["gang"], ["predicates", "nodeorder"]]][seed % 3]
+    c = kbgen_mod.gen_random(1500 + seed, n_nodes=3 + seed % 12, n_jobs=3 + seed % 8, max_tasks=1 + seed % 7,
+                             tiers=tiers, best_effort_p=0.35)
+    p = str(tmp_path / "bf.kbs")
+    c.write(p)
+    acts = "allocate, backfill"
+    exp = oracle_mod.ref_allocate(p, actions=acts).as_list()
+    for batched in (True, False):
+        with engine.Session(p) as s:
+            s.set_option("batched", 1 if batched else 0)
+            pod, node, kind = s.run_actions(acts)
+        got = [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)]
+        assert got == exp, f"batched={batched}"
+
+
 def test_c3_scaled(engine, oracle_mod, kbgen_mod, tmp_path):
     """C3 shape (zone anti-affinity, selectors, taints, 8 queues) at 2k nodes x 8k pods."""
     c = kbgen_mod.gen_c3(n_nodes=2000, n_pending=8000)
