@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--time-every", type=int, default=4, help="HIP-event time every k-th sweep launch")
+    ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
+                    help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
+                         "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")
     return ap.parse_args()
 
 
@@ -121,9 +124,17 @@ def pmc_traffic():
     return best
 
 
-def run_session(buf, device, time_every):
+def open_sharded(buf, device, rank, world, dist):
+    s = kbhip.ShardedSession(buf, device, rank, world)
+    box = [kbhip.ShardedSession.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    s.connect_rccl(box[0])
+    return s
+
+
+def run_session(buf, device, time_every, shard=None):
     t0 = time.perf_counter()
-    s = kbhip.Session(buf, device=device)
+    s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
     pod, node, kind = s.allocate(cap=1 << 21)
     st = s.stats()
@@ -158,13 +169,14 @@ def main():
     with open(path, "rb") as f:
         buf = f.read()
     device = local
+    shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
-        run_session(buf, device, 0)
+        run_session(buf, device, 0, shard)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
     for _ in range(args.steps):
-        dt, n, st = run_session(buf, device, args.time_every)
+        dt, n, st = run_session(buf, device, args.time_every, shard)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
@@ -173,15 +185,17 @@ def main():
     barrier(dist, local)
     wall = time.perf_counter() - t0
     wall = allmax(dist, local, wall)
-    total_placed = allsum(dist, local, placed)
+    # replicas: every rank schedules its own session; shard: one session shared by all ranks
+    total_placed = placed if shard else allsum(dist, local, placed)
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
         return
     nodes = st_last["nodes"]
-    traffic = pmc_traffic()
+    traffic = None if shard else pmc_traffic()
     sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
-    achieved = nodes * B_NODE / (sweep_us * 1e-6) / 1e9 if sweeps_n else 0.0
+    nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
+    achieved = nodes_per_launch * B_NODE / (sweep_us * 1e-6) / 1e9 if sweeps_n else 0.0
     out = {
         "metric": METRIC,
         "value": total_placed / wall,
@@ -192,7 +206,7 @@ def main():
         "ms_per_step": wall / args.steps * 1e3,
         "p50_session_ms": statistics.median(lat) * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (kbgen seed 20261015+4, C4 SKU mix, gang jobs minMember 8-64)",
@@ -202,14 +216,16 @@ def main():
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
-                   "parallelism": f"replicas x{world}" if world > 1 else "1 GPU"},
-        "roofline": {"kernel": "k_pop_batch", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                   "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
+                   else "1 GPU"},
+        "roofline": {"kernel": "k_sweep_argmax" if shard else "k_pop_batch", "bound": "hbm", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
                      if traffic else None,
                      "mean_launch_us": sweep_us, "timed_launches": sweeps_n,
-                     "bytes_per_launch": nodes * B_NODE},
+                     "bytes_per_launch": nodes_per_launch * B_NODE},
     }
     if args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds)

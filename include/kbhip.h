@@ -117,7 +117,8 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 
 /* Read the device node state: N x 12 int64 (idle, used, releasing,
- * backfilled; cpu/mem/gpu each).  `used` is maintained on the host mirror. */
+ * backfilled; cpu/mem/gpu each) of the session's nodes (a shard session: its
+ * range [lo, hi) only).  `used` is maintained on the host mirror. */
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes);
 
 int kbhip_get_stats(kb_session* s, kbhip_stats* out);
@@ -127,6 +128,26 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
 
 int kbhip_session_close(kb_session* s);
+
+/* Node-array sharding (one process per GPU).  A shard session
+ * holds the whole host model but only nodes [lo, hi) of the snapshot on its
+ * device, lo = N*rank/world, hi = N*(rank+1)/world; per-task sweeps reduce
+ * the 8-byte selection key (and the inter-pod affinity min/max) across
+ * shards; every shard then applies the same decision (the owner updates the
+ * node row).  Placements equal the one-GPU session's.  Connect with RCCL
+ * (kbhip_rccl_unique_id on one rank, shared out of band, then
+ * kbhip_shard_connect_rccl on every rank, collectively) or with a host
+ * callback performing the all-reduce (e.g. torch.distributed over gloo). */
+#define KBHIP_RED_MAX_U64 0
+#define KBHIP_RED_MIN_I64 1
+#define KBHIP_RED_MAX_I64 2
+typedef int (*kbhip_allreduce_fn)(void* ctx, uint64_t* vals, int32_t n, int32_t op);
+int kbhip_session_open_shard(const void* kbs_bytes, size_t len, int device, int32_t rank, int32_t world,
+                             kb_session** out);
+int kbhip_shard_info(kb_session* s, int32_t* out_rank_world_lo_hi);
+int kbhip_rccl_unique_id(void* out, int64_t cap);
+int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len);
+int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
 
 /* Test support (not part of the placement path): encode a snapshot without a
  * device and read the compiled host tables back by name.  Tables (int32):

@@ -22,8 +22,12 @@ struct DevTables {
     int32_t* aff_scalar;       // PA target totals, session counters
 };
 
+// Per-task sweep; commit_here = the last block commits (one GPU).  Sharded
+// sessions reduce ctrl->slot[task_i] across shards and then launch_commit_task.
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st);
+                               uint64_t* walk, hipStream_t st, bool commit_here = true);
+hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
+                              hipStream_t st);
 // Inter-pod affinity priority prepass: min / max of the raw count over all
 // nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi.
 hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st);

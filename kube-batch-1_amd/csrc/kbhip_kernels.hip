@@ -62,8 +62,8 @@ __device__ __forceinline__ Row load_row(const NodeCols& nc, int n) {
 __device__ __forceinline__ bool req_match(const DevTables& t, const NodeCols& nc, const Req& r, int n) {
     // labels.Requirement.Matches (apimachinery/pkg/labels/selector.go:192-236)
     switch (r.op) {
-        case OP_NAME_IN: return n == r.val_off;      // field selector metadata.name
-        case OP_NAME_NOTIN: return n != r.val_off;
+        case OP_NAME_IN: return n + nc.base == r.val_off;      // field selector metadata.name
+        case OP_NAME_NOTIN: return n + nc.base != r.val_off;
         case OP_FALSE: return false;
         default: break;
     }
@@ -168,7 +168,7 @@ __device__ __forceinline__ uint64_t dyn_key(const Conf& cf, const TaskClass& c, 
     const bool fit_rel = c.ireq_cpu - r.rel_cpu < kMinCPU && c.ireq_mem - r.rel_mem < kMinMem &&
                          c.ireq_gpu - r.rel_gpu < kMinGPU;
     if (!fit_acc && !fit_rel) return 0;
-    return pack_key(s, n, fit_acc ? 0 : 1);
+    return pack_key(s, n + nc.base, fit_acc ? 0 : 1);
 }
 
 __device__ __forceinline__ uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
@@ -185,9 +185,12 @@ __device__ __forceinline__ uint64_t eval_node(const Conf& cf, const TaskClass& c
 // pod (anti-)affinity (kbhip_affinity.h): count tables per term class,
 // indexed by the node's topology domain.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int32_t dom_of(const NodeCols& nc, int space, int n) {
-    return nc.dom[(int64_t)space * nc.npad + n];
+// Domain columns are replicated over the whole node array (every shard holds
+// them): dom_g takes a global node index, dom_of a local row of this shard.
+__device__ __forceinline__ int32_t dom_g(const NodeCols& nc, int space, int g) {
+    return nc.dom[(int64_t)space * nc.dom_stride + g];
 }
+__device__ __forceinline__ int32_t dom_of(const NodeCols& nc, int space, int n) { return dom_g(nc, space, n + nc.base); }
 
 // predicates.go:1293-1458 for one node.
 __device__ __forceinline__ bool aff_pred(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n) {
@@ -222,7 +225,7 @@ __device__ __forceinline__ int64_t ipa_count(const TaskClass& c, const DevTables
         const int d = dom_of(nc, it[0], n);
         if (d < 0) continue;
         int64_t x = t.aff_cnt[it[1] + d];
-        if (F >= 0 && dom_of(nc, it[0], F) == d) x += t.aff_scalar[it[2]];
+        if (F >= 0 && dom_g(nc, it[0], F) == d) x += t.aff_scalar[it[2]];
         sum += (int64_t)it[3] * x;
     }
     return sum;
@@ -257,16 +260,17 @@ __device__ __forceinline__ uint64_t eval_first_fit(const Conf& cf, const TaskCla
             for (int w = 0; w < nc.port_words; ++w)
                 if (nc.ports[(int64_t)w * nc.npad + n] & t.masks[c.pconf_off + w]) ok = false;
     }
-    return ok ? pack_key(0, n, 0) : 0;
+    return ok ? pack_key(0, n + nc.base, 0) : 0;
 }
 
-// Count-table updates of a committed task (kind 1 Allocated, 2 Pipelined).
-__device__ void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {
+// Count-table updates of a committed task (kind 1 Allocated, 2 Pipelined) on
+// global node g (every shard applies them).
+__device__ void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int g, int kind) {
     for (int i = 0; i < c.upd_n; ++i) {
         const int32_t* u = t.aff_items + c.upd_off + 3 * i;
         if (u[0] == 0) {         // UPD_CNT_ALLOC: a new predicate target in n's domain
             if (kind != 1) continue;
-            const int d = dom_of(nc, u[1], n);
+            const int d = dom_g(nc, u[1], g);
             if (d >= 0) t.aff_cnt[u[2] + d] += 1;
         } else if (u[0] == 1) {  // UPD_SCALAR_ALLOC: target total of a PA class
             if (kind == 1) t.aff_scalar[u[2]] += 1;
@@ -339,8 +343,71 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // ---------------------------------------------------------------------------
 // per-task path
 // ---------------------------------------------------------------------------
+// Commit of task task_i once ctrl->slot[task_i] holds the winner key over ALL
+// nodes (all shards): result, gang stop, node row (owner only), pod-affinity
+// tables and fallback node (every shard, identically), and the
+// GetAccessibleResource mutation of the visited nodes of this shard.  Run by
+// one block: the last sweep block (one GPU) or k_commit_task (sharded).
+__device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const TaskClass& c,
+                            bool first_fit, bool track, const uint64_t* walk) {
+    __shared__ uint64_t win;
+    if (threadIdx.x == 0) {
+        const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        win = k;
+        const int g = k ? key_idx(k) : -1;            // global node index
+        const int n = g - nc.base;                    // local row
+        const bool own = k && n >= 0 && n < nc.n;
+        if (first_fit) {  // backfill: Session.Allocate on the first passing node; no stop rule
+            ctrl->res_node[task_i] = g;
+            ctrl->res_kind[task_i] = k ? 1 : 0;
+            if (k) {
+                if (own) commit_node(c, t, nc, n, 1);
+                if (c.aff) commit_aff(c, t, nc, g, 1);
+                if (ctrl->fallback < 0 || g < ctrl->fallback) ctrl->fallback = g;
+                if (c.backfill) ctrl->any_bf = 1;
+            }
+            ctrl->n_done = task_i + 1;
+            if (task_i + 1 == ctrl->n_tasks) ctrl->stop = 0;
+        } else if (k == 0) {
+            ctrl->res_node[task_i] = -1;
+            ctrl->res_kind[task_i] = 0;
+            ctrl->n_done = task_i + 1;
+            ctrl->stop = 1;
+        } else {
+            const int kind = key_kind(k);
+            ctrl->res_node[task_i] = g;
+            ctrl->res_kind[task_i] = kind;
+            if (own) {
+                if (track) {  // the winner is visited too: Idle += Backfilled first (node_info.go:209-211)
+                    nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+                }
+                commit_node(c, t, nc, n, kind);
+            }
+            if (c.aff) commit_aff(c, t, nc, g, kind);
+            if (ctrl->fallback < 0 || g < ctrl->fallback) ctrl->fallback = g;
+            if (c.backfill) ctrl->any_bf = 1;
+            after_assign(ctrl, task_i, kind);
+        }
+    }
+    __syncthreads();
+    if (!track) return;
+    // GetAccessibleResource mutation for every other visited node of this shard.
+    const uint64_t k = win;
+    const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
+    const int wn = k ? key_idx(k) : -1;
+    for (int n = threadIdx.x; n < nc.n; n += kBlock) {
+        const uint64_t v = walk[n];
+        if (!v || n + nc.base == wn) continue;
+        if (k && v < wk) continue;
+        nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+    }
+}
+
+// Sweep of task task_i over this shard's nodes -> max key in ctrl->slot.
+// commit_here: the last block commits (one GPU); otherwise the slot is
+// reduced across shards first and k_commit_task commits.
 __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
-                                                         int task_i, uint64_t* walk) {
+                                                         int task_i, uint64_t* walk, int commit_here) {
     __shared__ uint64_t red[kBlock / 64];
     __shared__ int last;
     if (ctrl->stop >= 0) return;  // the pop already stopped (uniform)
@@ -356,7 +423,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
         bool passed = false;
         const uint64_t k = first_fit ? eval_first_fit(cf, c, t, nc, n)
                                      : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
-        if (track) walk[n] = passed ? pack_key(s, n, 0) : 0;
+        if (track) walk[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
         best = k > best ? k : best;
     }
     best = wave_max_u64(best);
@@ -373,55 +440,18 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
         __threadfence();
     }
     __syncthreads();
-    if (!last) return;
-    // Last block: commit.
-    __shared__ uint64_t win;
-    if (threadIdx.x == 0) {
-        const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        win = k;
-        if (first_fit) {  // backfill: Session.Allocate on the first passing node; no stop rule
-            ctrl->res_node[task_i] = k ? key_idx(k) : -1;
-            ctrl->res_kind[task_i] = k ? 1 : 0;
-            if (k) {
-                const int n = key_idx(k);
-                commit_node(c, t, nc, n, 1);
-                if (c.aff) commit_aff(c, t, nc, n, 1);
-                if (ctrl->fallback < 0 || n < ctrl->fallback) ctrl->fallback = n;
-                if (c.backfill) ctrl->any_bf = 1;
-            }
-            ctrl->n_done = task_i + 1;
-            if (task_i + 1 == ctrl->n_tasks) ctrl->stop = 0;
-        } else if (k == 0) {
-            ctrl->res_node[task_i] = -1;
-            ctrl->res_kind[task_i] = 0;
-            ctrl->n_done = task_i + 1;
-            ctrl->stop = 1;
-        } else {
-            const int n = key_idx(k), kind = key_kind(k);
-            ctrl->res_node[task_i] = n;
-            ctrl->res_kind[task_i] = kind;
-            if (track) {  // the winner is visited too: Idle += Backfilled first (node_info.go:209-211)
-                nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
-            }
-            commit_node(c, t, nc, n, kind);
-            if (c.aff) commit_aff(c, t, nc, n, kind);
-            if (ctrl->fallback < 0 || n < ctrl->fallback) ctrl->fallback = n;
-            if (c.backfill) ctrl->any_bf = 1;
-            after_assign(ctrl, task_i, kind);
-        }
-    }
-    __syncthreads();
-    if (!track) return;
-    // GetAccessibleResource mutation for every other node the walk visited.
-    const uint64_t k = win;
-    const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
-    const int wn = k ? key_idx(k) : -1;
-    for (int n = threadIdx.x; n < nc.n; n += kBlock) {
-        const uint64_t v = walk[n];
-        if (!v || n == wn) continue;
-        if (k && v < wk) continue;
-        nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
-    }
+    if (!last || !commit_here) return;
+    commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk);
+}
+
+// Sharded sessions: the commit after the cross-shard max of ctrl->slot[task_i].
+__global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t, PopCtrl* ctrl, int task_i,
+                                                        const uint64_t* walk) {
+    if (ctrl->stop >= 0) return;
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
+    const TaskClass c = t.classes[cls];
+    const bool first_fit = ctrl->mode == 1;
+    commit_task(nc, t, ctrl, task_i, c, first_fit, !first_fit && ctrl->any_bf != 0, walk);
 }
 
 // ---------------------------------------------------------------------------
@@ -716,11 +746,18 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st) {
+                               uint64_t* walk, hipStream_t st, bool commit_here) {
     int grid = (nc.n + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk);
+    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk,
+                       commit_here ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
+                              hipStream_t st) {
+    hipLaunchKernelGGL(k_commit_task, dim3(1), dim3(kBlock), 0, st, nc, t, ctrl, task_i, walk);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 //   allocate loop     actions/allocate/allocate.go:41-201
 //   placement         the HIP kernels (kbhip_kernels.hip)
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -200,12 +201,18 @@ struct Session {
     int64_t timed_n = 0;
     kbhip_stats stats{};
     vector<std::tuple<int, int, int>> log;
+    // node-array sharding: this session holds nodes [nc.base, nc.base + nc.n)
+    int rank = 0, world = 1, n_total = 0;
+    ncclComm_t comm = nullptr;                 // RCCL exchange (one GPU per rank)
+    kbhip_allreduce_fn xfn = nullptr;          // or a host-side exchange callback
+    void* xctx = nullptr;
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
     bool encode_only = false;
     vector<int32_t> h_dom, h_aff_cnt, h_aff_scalar, h_aff_items;
     int n_spaces = 0;
 
     ~Session() {
+        if (comm) (void)ncclCommDestroy(comm);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
         if (h_ctrl) (void)hipHostFree(h_ctrl);
@@ -248,7 +255,11 @@ struct Encoder {
 
 static void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
 
-static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false) {
+static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
+                         int world = 1) {
+    if (world < 1 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world");
+    S.rank = rank;
+    S.world = world;
     auto t0 = std::chrono::steady_clock::now();
     Encoder E(s, S);
     auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
@@ -728,49 +739,51 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.device = device;
     HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
     hipStream_t st = S.stream;
-    auto pad64 = [&](const vector<int64_t>& v) { vector<int64_t> o(npad, 0); std::copy(v.begin(), v.end(), o.begin()); return o; };
+    // this session's node range: the whole array, or one contiguous shard
+    const int lo = (int)((int64_t)N * S.rank / S.world), hi = (int)((int64_t)N * (S.rank + 1) / S.world);
+    const int nl = hi - lo, npl = std::max(((nl + kBlock - 1) / kBlock) * kBlock, kBlock);
     vector<int64_t> col[13];
-    for (int i = 0; i < 13; ++i) col[i].assign(npad, 0);
-    for (int i = 0; i < N; ++i) {
-        col[0][i] = idle[i].c; col[1][i] = idle[i].m; col[2][i] = idle[i].g;
-        col[3][i] = rel[i].c; col[4][i] = rel[i].m; col[5][i] = rel[i].g;
-        col[6][i] = bf[i].c; col[7][i] = bf[i].m; col[8][i] = bf[i].g;
-        col[9][i] = acpu[i]; col[10][i] = amem[i]; col[11][i] = nzc[i]; col[12][i] = nzm[i];
+    for (int i = 0; i < 13; ++i) col[i].assign(npl, 0);
+    for (int i = lo; i < hi; ++i) {
+        const int r = i - lo;
+        col[0][r] = idle[i].c; col[1][r] = idle[i].m; col[2][r] = idle[i].g;
+        col[3][r] = rel[i].c; col[4][r] = rel[i].m; col[5][r] = rel[i].g;
+        col[6][r] = bf[i].c; col[7][r] = bf[i].m; col[8][r] = bf[i].g;
+        col[9][r] = acpu[i]; col[10][r] = amem[i]; col[11][r] = nzc[i]; col[12][r] = nzm[i];
     }
-    (void)pad64;
     int64_t** dst[13] = {&S.nc.idle_cpu, &S.nc.idle_mem, &S.nc.idle_gpu, &S.nc.rel_cpu, &S.nc.rel_mem, &S.nc.rel_gpu,
                          &S.nc.bf_cpu, &S.nc.bf_mem, &S.nc.bf_gpu, &S.nc.acpu, &S.nc.amem, &S.nc.nzc, &S.nc.nzm};
     for (int i = 0; i < 13; ++i) *dst[i] = upload(S.b_cols[i], col[i], st);
-    vector<int32_t> pods_col(npad, 0), max_col(npad, 0);
-    vector<uint8_t> flags_col(npad, 0);
-    for (int i = 0; i < N; ++i) {
-        pods_col[i] = podcnt[i];
-        max_col[i] = (int32_t)apods[i];
-        flags_col[i] = (!unsched.empty() && unsched[i]) ? 1 : 0;
+    vector<int32_t> pods_col(npl, 0), max_col(npl, 0);
+    vector<uint8_t> flags_col(npl, 0);
+    for (int i = lo; i < hi; ++i) {
+        pods_col[i - lo] = podcnt[i];
+        max_col[i - lo] = (int32_t)apods[i];
+        flags_col[i - lo] = (!unsched.empty() && unsched[i]) ? 1 : 0;
     }
     S.nc.pods = upload(S.b_cols[13], pods_col, st);
     S.nc.maxtasks = upload(S.b_cols[14], max_col, st);
     S.nc.flags = upload(S.b_cols[15], flags_col, st);
     const int K = (int)E.sel_keys.size();
-    vector<int32_t> lab((size_t)std::max(K, 1) * npad, -1);
+    vector<int32_t> lab((size_t)std::max(K, 1) * npl, -1);
     for (auto& kv : E.sel_keys) {
         auto kit = E.keys_all.ids.find(kv.first);
         if (kit == E.keys_all.ids.end()) continue;  // no node has the key
         int kid = kit->second;
-        for (int i = 0; i < N; ++i)
+        for (int i = lo; i < hi; ++i)
             for (auto& lv2 : E.node_labels[i])
-                if (lv2.first == kid) lab[(size_t)kv.second * npad + i] = lv2.second;
+                if (lv2.first == kid) lab[(size_t)kv.second * npl + (i - lo)] = lv2.second;
     }
     S.nc.labels = upload(S.b_labels, lab, st);
-    vector<uint64_t> tcol((size_t)std::max(E.tw, 1) * npad, 0);
-    for (int i = 0; i < N; ++i)
-        for (int id : node_taints[i]) tcol[(size_t)(id / 64) * npad + i] |= 1ULL << (id % 64);
+    vector<uint64_t> tcol((size_t)std::max(E.tw, 1) * npl, 0);
+    for (int i = lo; i < hi; ++i)
+        for (int id : node_taints[i]) tcol[(size_t)(id / 64) * npl + (i - lo)] |= 1ULL << (id % 64);
     S.nc.taints = upload(S.b_taints, tcol, st);
-    vector<uint64_t> pcol((size_t)std::max(E.pw, 1) * npad, 0);
-    for (int i = 0; i < N; ++i)
-        for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npad + i] |= 1ULL << (id % 64);
+    vector<uint64_t> pcol((size_t)std::max(E.pw, 1) * npl, 0);
+    for (int i = lo; i < hi; ++i)
+        for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npl + (i - lo)] |= 1ULL << (id % 64);
     S.nc.ports = upload(S.b_ports, pcol, st);
-    if (aff.active) {
+    if (aff.active) {  // domain columns cover every node on every shard (winners may be remote)
         S.nc.dom = upload(S.b_dom, aff.dom, st);
         if (aff_items.empty()) aff_items.push_back(0);
         S.tab.aff_items = upload(S.b_aff_items, aff_items, st);
@@ -783,8 +796,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.tab.aff_cnt = upload(S.b_aff_cnt, one, st);
         S.tab.aff_scalar = upload(S.b_aff_scalar, one, st);
     }
-    S.nc.n = N;
-    S.nc.npad = npad;
+    S.nc.n = nl;
+    S.nc.npad = npl;
+    S.nc.base = lo;
+    S.nc.dom_stride = npad;
+    S.n_total = N;
     S.nc.n_keys = K;
     S.nc.taint_words = E.tw;
     S.nc.port_words = E.pw;
@@ -801,10 +817,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.tab.masks = upload(S.b_masks, E.masks, st);
     S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
     HIPCHK(hipHostMalloc((void**)&S.h_ctrl, sizeof(PopCtrl), hipHostMallocDefault));
-    S.d_walk = S.b_walk.alloc<uint64_t>(npad);
+    S.d_walk = S.b_walk.alloc<uint64_t>(npl);
     {
         int R2;
-        const int nb2 = pop_blocks(N, &R2);
+        const int nb2 = pop_blocks(nl, &R2);
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
         S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
@@ -822,6 +838,44 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
     S.stats.nodes = N;
     S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// ---------------------------------------------------------------------------
+// cross-shard exchange of one 8-byte value in device memory:
+// RCCL all-reduce on the session stream, or a host round trip through the
+// caller's callback (tests: several ranks sharing one GPU over gloo).
+// ---------------------------------------------------------------------------
+static void exchange(Session& S, void* dev, int op) {
+    if (S.world == 1) return;
+    if (S.comm) {
+        const ncclDataType_t dt = op == KBHIP_RED_MAX_U64 ? ncclUint64 : ncclInt64;
+        const ncclRedOp_t ro = op == KBHIP_RED_MIN_I64 ? ncclMin : ncclMax;
+        const ncclResult_t r = ncclAllReduce(dev, dev, 1, dt, ro, S.comm, S.stream);
+        if (r != ncclSuccess) throw Error(KBHIP_EDEVICE, string("ncclAllReduce: ") + ncclGetErrorString(r));
+        return;
+    }
+    if (!S.xfn) throw Error(KBHIP_EINVAL, "sharded session is not connected (kbhip_shard_connect_*)");
+    uint64_t v = 0;
+    HIPCHK(hipMemcpyAsync(&v, dev, 8, hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    if (S.xfn(S.xctx, &v, 1, op) != 0) throw Error(KBHIP_EDEVICE, "shard exchange callback failed");
+    HIPCHK(hipMemcpyAsync(dev, &v, 8, hipMemcpyHostToDevice, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+}
+
+// One task of the per-task path: [IPA min/max prepass + exchange], sweep,
+// [cross-shard max of the key + commit].
+static void sweep_task(Session& S, int i, int cls) {
+    if (S.classes[cls].ipa_n > 0) {
+        HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
+        exchange(S, &S.d_ctrl->ipa_lo[i], KBHIP_RED_MIN_I64);
+        exchange(S, &S.d_ctrl->ipa_hi[i], KBHIP_RED_MAX_I64);
+    }
+    HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1));
+    if (S.world > 1) {
+        exchange(S, &S.d_ctrl->slot[i], KBHIP_RED_MAX_U64);
+        HIPCHK(launch_commit_task(S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -858,7 +912,7 @@ static void backfill_run(Session& S) {
         std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
         std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
         HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
-        for (int i = 0; i < m; ++i) HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
+        for (int i = 0; i < m; ++i) sweep_task(S, i, h.cls[i]);
         HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
         S.stats.sweeps += m;
@@ -894,7 +948,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
         const TaskClass& c = S.classes[cls0];
-        const bool batch = S.batched && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4;
+        const bool batch = S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4;
         if (!batch) {  // general path: take up to a chunk of mixed classes
             m = std::min(n - done, kMaxChunk);
         }
@@ -1001,9 +1055,8 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
             HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
             for (int i = 0; i < m; ++i) {
-                if (S.classes[h.cls[i]].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
-                HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
+                sweep_task(S, i, h.cls[i]);
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
             }
             S.stats.sweeps += m;
@@ -1408,7 +1461,8 @@ int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
         for (int i = 0; i < N; ++i) {
             int64_t* o = out + (int64_t)i * 12;
             o[0] = buf[0][i]; o[1] = buf[1][i]; o[2] = buf[2][i];
-            o[3] = S.used[i].c; o[4] = S.used[i].m; o[5] = S.used[i].g;
+            const R3& u = S.used[i + S.nc.base];
+            o[3] = u.c; o[4] = u.m; o[5] = u.g;
             o[6] = buf[3][i]; o[7] = buf[4][i]; o[8] = buf[5][i];
             o[9] = buf[6][i]; o[10] = buf[7][i]; o[11] = buf[8][i];
         }
@@ -1447,6 +1501,61 @@ int kbhip_debug_phases(kb_session* s, double* out, int n) {
 }
 #endif
 
+int kbhip_session_open_shard(const void* bytes, size_t len, int device, int32_t rank, int32_t world,
+                             kb_session** out) {
+    ABI_GUARD({
+        if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        int nd = kbhip::device_count();
+        if (nd <= 0) throw kbhip::Error(KBHIP_ENODEV, "no gfx950 HIP device available");
+        if (device < 0 || device >= nd) throw kbhip::Error(KBHIP_EINVAL, "device index out of range");
+        kbs::Snapshot snap;
+        snap.load_bytes(bytes, len);
+        std::unique_ptr<kb_session> s(new kb_session());
+        kbhip::open_session(s->s, snap, device, false, rank, world);
+        *out = s.release();
+        return KBHIP_OK;
+    })
+}
+int kbhip_shard_info(kb_session* s, int32_t* out4) {
+    ABI_GUARD({
+        if (!s || !out4) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        out4[0] = s->s.rank;
+        out4[1] = s->s.world;
+        out4[2] = s->s.nc.base;
+        out4[3] = s->s.nc.base + s->s.nc.n;
+        return KBHIP_OK;
+    })
+}
+int kbhip_rccl_unique_id(void* out, int64_t cap) {
+    ABI_GUARD({
+        ncclUniqueId id;
+        if ((int64_t)sizeof(id) > cap || !out) throw kbhip::Error(KBHIP_EINVAL, "unique id buffer too small");
+        const ncclResult_t r = ncclGetUniqueId(&id);
+        if (r != ncclSuccess) throw kbhip::Error(KBHIP_EDEVICE, string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+        std::memcpy(out, &id, sizeof(id));
+        return (int)sizeof(id);
+    })
+}
+int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) {
+    ABI_GUARD({
+        if (!s || !unique_id) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        ncclUniqueId id;
+        if (len != (int64_t)sizeof(id)) throw kbhip::Error(KBHIP_EINVAL, "bad unique id length");
+        std::memcpy(&id, unique_id, sizeof(id));
+        HIPCHK(hipSetDevice(s->s.device));
+        const ncclResult_t r = ncclCommInitRank(&s->s.comm, s->s.world, id, s->s.rank);
+        if (r != ncclSuccess) throw kbhip::Error(KBHIP_EDEVICE, string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        return KBHIP_OK;
+    })
+}
+int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx) {
+    ABI_GUARD({
+        if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        s->s.xfn = fn;
+        s->s.xctx = ctx;
+        return KBHIP_OK;
+    })
+}
 int kbhip_debug_encode(const void* bytes, size_t len, kb_session** out) {
     ABI_GUARD({
         if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");

@@ -31,8 +31,10 @@ struct NodeCols {
     int32_t *labels;                           // [n_keys][npad]
     uint64_t *taints;                          // [taint_words][npad] NoSchedule/NoExecute taint ids
     uint64_t *ports;                           // [port_words][npad] used (ip, proto, port) ids
-    int32_t *dom;                              // [n_spaces][npad] topology domain ids (-1: no domain)
+    int32_t *dom;                              // [n_spaces][dom_stride] domain ids of ALL nodes (-1: none)
     int32_t n, npad, n_keys, taint_words, port_words;
+    int32_t base;        // global index of local row 0 (node-array shard; 0 on one GPU)
+    int32_t dom_stride;  // row stride of dom (>= total node count)
 };
 
 // A compiled label requirement (labels.Requirement over node labels).

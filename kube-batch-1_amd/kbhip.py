@@ -24,7 +24,12 @@ STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
 EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file", "kbhip_place_job",
            "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
-           "kbhip_backfill")
+           "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
+           "kbhip_shard_connect_rccl", "kbhip_shard_connect_host")
+
+RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
+                                ctypes.c_int32)
 
 
 class KbhipError(RuntimeError):
@@ -65,6 +70,11 @@ def lib() -> ctypes.CDLL:
         L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_session_open_shard.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
+        L.kbhip_shard_info.argtypes = [vp, vp]
+        L.kbhip_rccl_unique_id.argtypes = [vp, i64]
+        L.kbhip_shard_connect_rccl.argtypes = [vp, vp, i64]
+        L.kbhip_shard_connect_host.argtypes = [vp, ALLREDUCE_FN, vp]
         L.kbhip_read_nodes.argtypes = [vp, vp, i64]
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
@@ -208,3 +218,71 @@ class EncodedSnapshot:
 
     def __exit__(self, *a):
         self.close()
+
+
+def shard_range(n_nodes: int, rank: int, world: int) -> Tuple[int, int]:
+    """Node range [lo, hi) of a shard (the library's partition)."""
+    return n_nodes * rank // world, n_nodes * (rank + 1) // world
+
+
+def torch_exchange(group=None):
+    """An exchange callback for kbhip_shard_connect_host doing the all-reduce
+    with torch.distributed (any backend; gloo runs on CPU).  u64 keys are
+    mapped to i64 by flipping the top bit, which preserves their order."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(vals: np.ndarray, op: int) -> None:
+        v = vals.view(np.int64).copy()
+        if op == RED_MAX_U64:
+            v ^= np.int64(-0x8000000000000000)
+        t = torch.from_numpy(v)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN if op == RED_MIN_I64 else dist.ReduceOp.MAX, group=group)
+        out = t.numpy()
+        if op == RED_MAX_U64:
+            out = out ^ np.int64(-0x8000000000000000)
+        vals.view(np.int64)[:] = out
+    return fn
+
+
+class ShardedSession(Session):
+    """A node-array shard of a session (include/kbhip.h): this
+    rank's device holds nodes [lo, hi); every rank runs the same host loop and
+    gets the same placements.  Connect with RCCL (connect_rccl, one GPU per
+    rank) or with a Python exchange (connect_host, e.g. torch_exchange())."""
+
+    def __init__(self, snapshot, device: int, rank: int, world: int):
+        if not isinstance(snapshot, (bytes, bytearray, memoryview)):
+            with open(snapshot, "rb") as f:
+                snapshot = f.read()
+        buf = bytes(snapshot)
+        self._h = ctypes.c_void_p()
+        self._cb = None
+        _check(lib().kbhip_session_open_shard(ctypes.c_char_p(buf), len(buf), device, rank, world,
+                                              ctypes.byref(self._h)))
+
+    def info(self) -> Tuple[int, int, int, int]:
+        out = np.zeros(4, np.int32)
+        _check(lib().kbhip_shard_info(self._h, _p(out)))
+        return tuple(int(x) for x in out)
+
+    @staticmethod
+    def rccl_unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(512)
+        n = _check(lib().kbhip_rccl_unique_id(buf, 512))
+        return buf.raw[:n]
+
+    def connect_rccl(self, unique_id: bytes) -> None:
+        b = ctypes.create_string_buffer(unique_id, len(unique_id))
+        _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
+
+    def connect_host(self, fn) -> None:
+        """fn(vals: np.ndarray[uint64], op) reduces vals in place across ranks."""
+        def cb(_ctx, vals, n, op):
+            try:
+                fn(np.ctypeslib.as_array(vals, shape=(n,)), op)
+                return 0
+            except Exception:  # reported to the library as a failed exchange
+                return 1
+        self._cb = ALLREDUCE_FN(cb)  # keep the trampoline alive
+        _check(lib().kbhip_shard_connect_host(self._h, self._cb, None))

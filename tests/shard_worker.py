@@ -1,0 +1,32 @@
+"""One rank of a sharded allocate session (spawned by tests): opens the shard
+of the snapshot on GPU 0 (ranks share the card), exchanges over gloo, runs the
+given actions and writes the placement log as JSON.
+
+usage: shard_worker.py <snapshot> <rank> <world> <init_file> <out.json> <actions>
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+
+
+def main():
+    path, rank, world, init_file, out, actions = sys.argv[1:7]
+    rank, world = int(rank), int(world)
+    import torch.distributed as dist
+    import kbhip
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    with kbhip.ShardedSession(path, 0, rank, world) as s:
+        s.connect_host(kbhip.torch_exchange())
+        info = s.info()
+        pod, node, kind = s.run_actions(actions)
+    dist.barrier()
+    dist.destroy_process_group()
+    with open(out, "w") as f:
+        json.dump({"info": info, "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)]}, f)
+
+
+if __name__ == "__main__":
+    main()
