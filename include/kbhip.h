@@ -163,6 +163,16 @@ int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
  * call that needs a device (KBHIP_EINVAL). */
 int kbhip_debug_encode(const void* kbs_bytes, size_t len, kb_session** out);
 int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t cap_bytes);
+/* Test support: replay a given decision sequence on an encode-only session's
+ * host tables with the kernels' own per-node arithmetic (kbhip_eval.h).  Step
+ * i tries task pods[i] (modes[i]: 0 allocate, 1 backfill): the selection key
+ * of every node, as the device sweep computes it before the step's commit, is
+ * written to out_keys[i * n_nodes + node]; then nodes[i] (-1: unassigned) is
+ * committed with kinds[i] (KBHIP_ALLOCATED / KBHIP_PIPELINED).  No placement
+ * decision is made here: the sequence comes from the caller (the tests take
+ * it from the CPU oracle and compare the keys with the oracle's). */
+int kbhip_debug_replay(kb_session* s, int32_t n_steps, const int32_t* pods, const int32_t* modes,
+                       const int32_t* nodes, const uint8_t* kinds, uint64_t* out_keys);
 
 const char* kbhip_last_error(void);
 

@@ -28,6 +28,7 @@
 #include "../../include/kbhip.h"
 #include "../../include/kbsnap.h"
 #include "kbhip_affinity.h"
+#include "kbhip_eval.h"
 #include "kbhip_internal.h"
 
 using std::string;
@@ -135,25 +136,28 @@ struct Plugin {
     std::map<string, string> args;
 };
 
-struct DevBuf {
+struct DevBuf {  // device memory, or host memory for encode-only sessions
     void* p = nullptr;
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    template <typename T>
-    T* alloc(size_t n) {
-        if (p) (void)hipFree(p);
+    bool host = false;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) { if (host) std::free(p); else (void)hipFree(p); }
         p = nullptr;
+    }
+    template <typename T>
+    T* alloc(size_t n, bool on_host = false) {
+        release();
+        host = on_host;
         size_t bytes = std::max<size_t>(n * sizeof(T), 16);
-        if (hipMalloc(&p, bytes) != hipSuccess) throw Error(KBHIP_EDEVICE, "hipMalloc failed");
+        if (host) {
+            p = std::calloc(1, bytes);
+            if (!p) throw Error(KBHIP_EINVAL, "out of host memory");
+        } else if (hipMalloc(&p, bytes) != hipSuccess) {
+            throw Error(KBHIP_EDEVICE, "hipMalloc failed");
+        }
         return (T*)p;
     }
 };
-
-template <typename T>
-static T* upload(DevBuf& b, const vector<T>& v, hipStream_t st) {
-    T* d = b.alloc<T>(v.size());
-    if (!v.empty()) HIPCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
-    return d;
-}
 
 struct Session {
     int device = 0;
@@ -221,6 +225,17 @@ struct Session {
     }
 };
 
+// Table upload: HBM on the session stream, or a host copy for encode-only
+// sessions (kbhip_debug_encode / kbhip_debug_replay).
+template <typename T>
+static T* upload(Session& S, DevBuf& b, const vector<T>& v) {
+    T* d = b.alloc<T>(v.size(), S.encode_only);
+    if (v.empty()) return d;
+    if (S.encode_only) std::memcpy(d, v.data(), v.size() * sizeof(T));
+    else HIPCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, S.stream));
+    return d;
+}
+
 // ---------------------------------------------------------------------------
 // encoder
 // ---------------------------------------------------------------------------
@@ -260,6 +275,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     if (world < 1 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world");
     S.rank = rank;
     S.world = world;
+    S.encode_only = encode_only;
     auto t0 = std::chrono::steady_clock::now();
     Encoder E(s, S);
     auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
@@ -722,23 +738,18 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             for (auto x : own) E.masks.push_back(x);
         }
     }
-    if (encode_only) {  // kbhip_debug_encode: keep the compiled host tables, touch no device
-        S.encode_only = true;
+    if (encode_only) {  // kbhip_debug_encode: keep copies of the compiled tables, touch no device
         S.h_dom = aff.dom;
         S.h_aff_cnt = aff.cnt;
         S.h_aff_scalar = aff.scalar;
         S.h_aff_items = aff_items;
         S.n_spaces = aff.n_spaces;
-        S.nc.n = N;
-        S.nc.npad = npad;
-        S.stats.nodes = N;
-        return;
+    } else {
+        HIPCHK(hipSetDevice(device));
+        S.device = device;
+        HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
     }
     // ---------------- upload ----------------
-    HIPCHK(hipSetDevice(device));
-    S.device = device;
-    HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-    hipStream_t st = S.stream;
     // this session's node range: the whole array, or one contiguous shard
     const int lo = (int)((int64_t)N * S.rank / S.world), hi = (int)((int64_t)N * (S.rank + 1) / S.world);
     const int nl = hi - lo, npl = std::max(((nl + kBlock - 1) / kBlock) * kBlock, kBlock);
@@ -753,7 +764,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     int64_t** dst[13] = {&S.nc.idle_cpu, &S.nc.idle_mem, &S.nc.idle_gpu, &S.nc.rel_cpu, &S.nc.rel_mem, &S.nc.rel_gpu,
                          &S.nc.bf_cpu, &S.nc.bf_mem, &S.nc.bf_gpu, &S.nc.acpu, &S.nc.amem, &S.nc.nzc, &S.nc.nzm};
-    for (int i = 0; i < 13; ++i) *dst[i] = upload(S.b_cols[i], col[i], st);
+    for (int i = 0; i < 13; ++i) *dst[i] = upload(S, S.b_cols[i], col[i]);
     vector<int32_t> pods_col(npl, 0), max_col(npl, 0);
     vector<uint8_t> flags_col(npl, 0);
     for (int i = lo; i < hi; ++i) {
@@ -761,9 +772,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         max_col[i - lo] = (int32_t)apods[i];
         flags_col[i - lo] = (!unsched.empty() && unsched[i]) ? 1 : 0;
     }
-    S.nc.pods = upload(S.b_cols[13], pods_col, st);
-    S.nc.maxtasks = upload(S.b_cols[14], max_col, st);
-    S.nc.flags = upload(S.b_cols[15], flags_col, st);
+    S.nc.pods = upload(S, S.b_cols[13], pods_col);
+    S.nc.maxtasks = upload(S, S.b_cols[14], max_col);
+    S.nc.flags = upload(S, S.b_cols[15], flags_col);
     const int K = (int)E.sel_keys.size();
     vector<int32_t> lab((size_t)std::max(K, 1) * npl, -1);
     for (auto& kv : E.sel_keys) {
@@ -774,27 +785,27 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             for (auto& lv2 : E.node_labels[i])
                 if (lv2.first == kid) lab[(size_t)kv.second * npl + (i - lo)] = lv2.second;
     }
-    S.nc.labels = upload(S.b_labels, lab, st);
+    S.nc.labels = upload(S, S.b_labels, lab);
     vector<uint64_t> tcol((size_t)std::max(E.tw, 1) * npl, 0);
     for (int i = lo; i < hi; ++i)
         for (int id : node_taints[i]) tcol[(size_t)(id / 64) * npl + (i - lo)] |= 1ULL << (id % 64);
-    S.nc.taints = upload(S.b_taints, tcol, st);
+    S.nc.taints = upload(S, S.b_taints, tcol);
     vector<uint64_t> pcol((size_t)std::max(E.pw, 1) * npl, 0);
     for (int i = lo; i < hi; ++i)
         for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npl + (i - lo)] |= 1ULL << (id % 64);
-    S.nc.ports = upload(S.b_ports, pcol, st);
+    S.nc.ports = upload(S, S.b_ports, pcol);
     if (aff.active) {  // domain columns cover every node on every shard (winners may be remote)
-        S.nc.dom = upload(S.b_dom, aff.dom, st);
+        S.nc.dom = upload(S, S.b_dom, aff.dom);
         if (aff_items.empty()) aff_items.push_back(0);
-        S.tab.aff_items = upload(S.b_aff_items, aff_items, st);
-        S.tab.aff_cnt = upload(S.b_aff_cnt, aff.cnt, st);
-        S.tab.aff_scalar = upload(S.b_aff_scalar, aff.scalar, st);
+        S.tab.aff_items = upload(S, S.b_aff_items, aff_items);
+        S.tab.aff_cnt = upload(S, S.b_aff_cnt, aff.cnt);
+        S.tab.aff_scalar = upload(S, S.b_aff_scalar, aff.scalar);
     } else {
         vector<int32_t> one(1, 0);
-        S.nc.dom = upload(S.b_dom, one, st);
-        S.tab.aff_items = upload(S.b_aff_items, one, st);
-        S.tab.aff_cnt = upload(S.b_aff_cnt, one, st);
-        S.tab.aff_scalar = upload(S.b_aff_scalar, one, st);
+        S.nc.dom = upload(S, S.b_dom, one);
+        S.tab.aff_items = upload(S, S.b_aff_items, one);
+        S.tab.aff_cnt = upload(S, S.b_aff_cnt, one);
+        S.tab.aff_scalar = upload(S, S.b_aff_scalar, one);
     }
     S.nc.n = nl;
     S.nc.npad = npl;
@@ -808,13 +819,19 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     vector<int64_t> valint(E.vals.strs.size() + 1, 0);
     vector<uint8_t> valok(E.vals.strs.size() + 1, 0);
     for (size_t v = 0; v < E.vals.strs.size(); ++v) valok[v] = parse_int64(E.vals.strs[v], &valint[v]);
-    S.tab.classes = upload(S.b_classes, S.classes, st);
-    S.tab.terms = upload(S.b_terms, E.terms, st);
-    S.tab.reqs = upload(S.b_reqs, E.reqs, st);
-    S.tab.vals = upload(S.b_vals, E.vals_list, st);
-    S.tab.valint = upload(S.b_valint, valint, st);
-    S.tab.valok = upload(S.b_valok, valok, st);
-    S.tab.masks = upload(S.b_masks, E.masks, st);
+    S.tab.classes = upload(S, S.b_classes, S.classes);
+    S.tab.terms = upload(S, S.b_terms, E.terms);
+    S.tab.reqs = upload(S, S.b_reqs, E.reqs);
+    S.tab.vals = upload(S, S.b_vals, E.vals_list);
+    S.tab.valint = upload(S, S.b_valint, valint);
+    S.tab.valok = upload(S, S.b_valok, valok);
+    S.tab.masks = upload(S, S.b_masks, E.masks);
+    if (encode_only) {
+        S.stats.nodes = N;
+        S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return;
+    }
+    hipStream_t st = S.stream;
     S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
     HIPCHK(hipHostMalloc((void**)&S.h_ctrl, sizeof(PopCtrl), hipHostMallocDefault));
     S.d_walk = S.b_walk.alloc<uint64_t>(npl);
@@ -1599,6 +1616,68 @@ int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t ca
         const int64_t bytes = (int64_t)(v.size() * sizeof(int32_t));
         if (out && cap_bytes >= bytes && bytes) std::memcpy(out, v.data(), (size_t)bytes);
         return bytes;
+    })
+}
+int kbhip_debug_replay(kb_session* s, int32_t n_steps, const int32_t* pods, const int32_t* modes,
+                       const int32_t* nodes, const uint8_t* kinds, uint64_t* out_keys) {
+    ABI_GUARD({
+        if (!s || (n_steps && (!pods || !modes || !nodes || !kinds || !out_keys)))
+            throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::Session& S = s->s;
+        if (!S.encode_only) throw kbhip::Error(KBHIP_EINVAL, "replay needs an encode-only session");
+        using namespace kbhip;
+        const NodeCols& nc = S.nc;
+        const DevTables& t = S.tab;
+        const int N = nc.n;
+        int F = -1, any_bf = S.any_bf;
+        vector<uint64_t> walk(N);
+        for (int i = 0; i < n_steps; ++i) {
+            if (pods[i] < 0 || pods[i] >= (int)S.pods.size() || S.pods[pods[i]].cls < 0)
+                throw Error(KBHIP_EINVAL, "replay step is not a pending task");
+            const TaskClass& c = S.classes[S.pods[pods[i]].cls];
+            uint64_t* keys = out_keys + (int64_t)i * N;
+            const bool first_fit = modes[i] == 1;
+            const bool track = !first_fit && any_bf;
+            // the sweep: k_ipa_minmax + k_sweep_argmax, node by node
+            int64_t lo = 0, hi = 0;
+            if (!first_fit && c.ipa_n > 0)
+                for (int n = 0; n < N; ++n) {
+                    const int64_t v = ipa_count(c, t, nc, n, F);
+                    lo = std::min(lo, v);
+                    hi = std::max(hi, v);
+                }
+            for (int n = 0; n < N; ++n) {
+                int32_t sc = 0;
+                bool passed = false;
+                keys[n] = first_fit ? eval_first_fit(S.conf, c, t, nc, n)
+                                    : eval_node_aff(S.conf, c, t, nc, n, lo, hi, F, &sc, &passed);
+                walk[n] = passed ? pack_key(sc, n + nc.base, 0) : 0;
+            }
+            // the commit of the given decision: commit_task's arithmetic
+            const int w = nodes[i];
+            if (w >= N) throw Error(KBHIP_EINVAL, "replay node out of range");
+            const uint64_t k = w >= 0 ? keys[w] : 0;
+            if (w >= 0 && !k) throw Error(KBHIP_EINVAL, "replay decision on a node with key 0");
+            if (w >= 0) {
+                const int kind = first_fit ? 1 : kinds[i];
+                if (track) {
+                    nc.idle_cpu[w] += nc.bf_cpu[w]; nc.idle_mem[w] += nc.bf_mem[w]; nc.idle_gpu[w] += nc.bf_gpu[w];
+                }
+                commit_node(c, t, nc, w, kind);
+                if (c.aff) commit_aff(c, t, nc, w, kind);
+                if (F < 0 || w < F) F = w;
+                if (c.backfill) any_bf = 1;
+            }
+            if (track) {
+                const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
+                for (int n = 0; n < N; ++n) {
+                    if (!walk[n] || n == w) continue;
+                    if (k && walk[n] < wk) continue;
+                    nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+                }
+            }
+        }
+        return KBHIP_OK;
     })
 }
 int kbhip_session_close(kb_session* s) {

@@ -25,7 +25,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
-           "kbhip_shard_connect_rccl", "kbhip_shard_connect_host")
+           "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -82,6 +82,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_debug_encode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
         L.kbhip_debug_table.argtypes = [vp, ctypes.c_char_p, vp, i64]
         L.kbhip_debug_table.restype = i64
+        L.kbhip_debug_replay.argtypes = [vp, i32, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
 
@@ -207,6 +208,18 @@ class EncodedSnapshot:
         out = np.zeros(max(int(n) // 4, 1), np.int32)
         _check(int(lib().kbhip_debug_table(self._h, name.encode(), _p(out), out.nbytes)) if n > 0 else 0)
         return out[: int(n) // 4]
+
+    def replay(self, pods, modes, nodes, kinds) -> np.ndarray:
+        """Per-step, per-node selection keys along a given decision sequence
+        (kbhip_debug_replay); kinds: KBHIP_ALLOCATED / KBHIP_PIPELINED."""
+        pods = np.ascontiguousarray(pods, np.int32)
+        modes = np.ascontiguousarray(modes, np.int32)
+        nodes = np.ascontiguousarray(nodes, np.int32)
+        kinds = np.ascontiguousarray(kinds, np.uint8)
+        n_nodes = int(self.table("dims")[0])
+        out = np.zeros((len(pods), max(n_nodes, 1)), np.uint64)
+        _check(lib().kbhip_debug_replay(self._h, len(pods), _p(pods), _p(modes), _p(nodes), _p(kinds), _p(out)))
+        return out[:, :n_nodes]
 
     def close(self) -> None:
         if self._h:

@@ -1170,8 +1170,37 @@ struct Engine {
         vector<double> raw;     // [task][node]
         vector<double> lohi;    // [task][2]
         vector<uint8_t> flags;  // [task]: bit0 predErrAll, bit1 scoreErrAll, bit2 ipaOn
+        vector<uint64_t> key;   // [task][node]: the selection key the sweep implies (0 = not selectable)
+        vector<uint8_t> mode;   // [task]: 0 allocate, 1 backfill
     };
     AffTrace* trace = nullptr;
+    static uint64_t packKey(int score, int idx, int pipelined) {  // max key = best score, then lowest index
+        return ((uint64_t)((uint32_t)score ^ 0x80000000u) << 32) | ((uint64_t)(0x7fffffff - idx) << 1) |
+               (uint64_t)(pipelined & 1);
+    }
+    void traceTask(const TaskPlan& tp, int mode) {
+        const PodRec& p = w.pods[tp.pod];
+        for (int ni = 0; ni < (int)w.nodes.size(); ++ni) {
+            const NodeRec& n = w.nodes[ni];
+            trace->ok.push_back(w.predOn ? podAffinityOk(tp, n) : 1);
+            trace->raw.push_back(tp.ipaOn ? ipaRaw(tp, n) : 0.0);
+            uint64_t k = 0;
+            if (mode == 1) {
+                if (predOk(w, tp, ni)) k = packKey(0, ni, 0);
+            } else {
+                int sc;
+                if (evalNode(w, tp, ni, &sc)) {
+                    int kind = le_sum(p.initReq, n.idle, n.bf) ? 1 : le(p.initReq, n.rel) ? 2 : 0;
+                    if (kind) k = packKey(sc, ni, kind == 2);
+                }
+            }
+            trace->key.push_back(k);
+        }
+        trace->lohi.push_back(tp.ipaMin);
+        trace->lohi.push_back(tp.ipaMax);
+        trace->flags.push_back((tp.predErrAll ? 1 : 0) | (tp.scoreErrAll ? 2 : 0) | (tp.ipaOn ? 4 : 0));
+        trace->mode.push_back((uint8_t)mode);
+    }
 
     // one task: predicate + score sweep, select, commit.  Returns assigned.
     bool placeTask(int pi) {
@@ -1188,15 +1217,7 @@ struct Engine {
         TaskPlan tp;
         tp.pod = pi;
         buildPlan(w, tp);
-        if (trace) {
-            for (auto& n : w.nodes) {
-                trace->ok.push_back(w.predOn ? podAffinityOk(tp, n) : 1);
-                trace->raw.push_back(tp.ipaOn ? ipaRaw(tp, n) : 0.0);
-            }
-            trace->lohi.push_back(tp.ipaMin);
-            trace->lohi.push_back(tp.ipaMax);
-            trace->flags.push_back((tp.predErrAll ? 1 : 0) | (tp.scoreErrAll ? 2 : 0) | (tp.ipaOn ? 4 : 0));
-        }
+        if (trace) traceTask(tp, 0);
         PodRec& p = w.pods[pi];
         int N = (int)w.nodes.size();
         int T = pool.T;
@@ -1263,10 +1284,16 @@ struct Engine {
                 TaskPlan tp;
                 tp.pod = pi;
                 buildPlan(w, tp);
+                if (trace) traceTask(tp, 1);
                 const int N = (int)w.nodes.size();
                 int first = -1;
                 for (int ni = 0; ni < N && first < 0; ++ni)
                     if (predOk(w, tp, ni)) first = ni;
+                if (trace) {
+                    trace->pod.push_back(pi);
+                    trace->node.push_back(first);
+                    trace->status.push_back(first >= 0 ? Allocated : 0);
+                }
                 if (first < 0) continue;
                 JobRec& j = w.jobs[jb];
                 p.status = Allocated;  // Session.Allocate(task, node, false)
@@ -1355,7 +1382,7 @@ const char* fast_last_error(void) { return g_ferr.c_str(); }
  * number of tasks tried (or <0 on error). */
 int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* out_pod, int32_t* out_node,
                         int32_t* out_status, uint8_t* out_ok, double* out_raw, double* out_lohi, uint8_t* out_flags,
-                        const char* actions) {
+                        const char* actions, uint64_t* out_key, uint8_t* out_mode) {
     try {
         kbs::Snapshot snap(path);
         fast::World w;
@@ -1373,11 +1400,13 @@ int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* o
             out_node[i] = tr.node[i];
             out_status[i] = tr.status[i];
             out_flags[i] = tr.flags[i];
+            if (out_mode) out_mode[i] = tr.mode[i];
             out_lohi[2 * i] = tr.lohi[2 * i];
             out_lohi[2 * i + 1] = tr.lohi[2 * i + 1];
             for (int k = 0; k < n_nodes; ++k) {
                 out_ok[(size_t)i * n_nodes + k] = tr.ok[(size_t)i * n_nodes + k];
                 out_raw[(size_t)i * n_nodes + k] = tr.raw[(size_t)i * n_nodes + k];
+                if (out_key) out_key[(size_t)i * n_nodes + k] = tr.key[(size_t)i * n_nodes + k];
             }
         }
         return n;

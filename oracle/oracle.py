@@ -152,15 +152,19 @@ def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
 
 
 def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096, actions: str = "allocate") -> dict:
-    """Test support: run the hoisted allocate with the per-task pod-affinity
-    trace.  For every task tried, in order: pod, result node (-1 unassigned),
-    status, per-node pod-affinity predicate verdict (ok), per-node raw
-    inter-pod affinity count (raw), its [min, max] over nodes (lohi) and flags
-    (bit0 predicate error on every node, bit1 score error, bit2 IPA on)."""
+    """Test support: run the hoisted restatement of the actions with a
+    per-task trace.  For every task tried, in order: pod, result node (-1
+    unassigned), status, per-node pod-affinity predicate verdict (ok), per-node
+    raw inter-pod affinity count (raw), its [min, max] over nodes (lohi), flags
+    (bit0 predicate error on every node, bit1 score error, bit2 IPA on), the
+    per-node selection key the sweep implies (key: packed score / index /
+    pipelined, 0 = not selectable) and the action (mode: 0 allocate, 1
+    backfill)."""
     lib = _lib("kbfast")
     fn = lib.fast_trace_affinity
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + [ctypes.c_char_p]
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 7 + [ctypes.c_char_p] + \
+        [ctypes.c_void_p] * 2
     pod = np.zeros(cap_tasks, np.int32)
     node = np.zeros(cap_tasks, np.int32)
     st = np.zeros(cap_tasks, np.int32)
@@ -168,12 +172,14 @@ def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096, actions:
     raw = np.zeros((cap_tasks, n_nodes), np.float64)
     lohi = np.zeros((cap_tasks, 2), np.float64)
     flags = np.zeros(cap_tasks, np.uint8)
+    key = np.zeros((cap_tasks, n_nodes), np.uint64)
+    mode = np.zeros(cap_tasks, np.uint8)
     n = fn(path.encode(), cap_tasks, n_nodes, _p(pod), _p(node), _p(st), _p(ok), _p(raw), _p(lohi), _p(flags),
-           actions.encode())
+           actions.encode(), _p(key), _p(mode))
     if n < 0:
         lib.fast_last_error.restype = ctypes.c_char_p
         raise RuntimeError(lib.fast_last_error().decode())
     if n > cap_tasks:
         raise RuntimeError("trace larger than cap_tasks")
     return {"pod": pod[:n], "node": node[:n], "status": st[:n], "ok": ok[:n], "raw": raw[:n],
-            "lohi": lohi[:n], "flags": flags[:n]}
+            "lohi": lohi[:n], "flags": flags[:n], "key": key[:n], "mode": mode[:n]}
