@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--time-every", type=int, default=4, help="HIP-event time every k-th sweep launch")
+    ap.add_argument("--placement", type=int, default=0, choices=(0, 1),
+                    help="batched chunk placement: 0 sequential loop, 1 running-min levels")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
                     help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
                          "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")
@@ -132,10 +134,11 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None):
+def run_session(buf, device, time_every, shard=None, placement=0):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
+    s.set_option("placement", placement)
     pod, node, kind = s.allocate(cap=1 << 21)
     st = s.stats()
     s.close()
@@ -171,12 +174,12 @@ def main():
     device = local
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
-        run_session(buf, device, 0, shard)
+        run_session(buf, device, 0, shard, args.placement)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
     for _ in range(args.steps):
-        dt, n, st = run_session(buf, device, args.time_every, shard)
+        dt, n, st = run_session(buf, device, args.time_every, shard, args.placement)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
@@ -214,7 +217,7 @@ def main():
                                "step, default kube-batch-conf tiers", "nodes": nodes, "pending": args.pending,
                    "placements_per_session": placed // args.steps, "pops_per_session": st_last["pops"],
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
-                   "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
+                   "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"], "placement": args.placement,
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},

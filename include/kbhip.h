@@ -124,7 +124,9 @@ int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes);
 int kbhip_get_stats(kb_session* s, kbhip_stats* out);
 
 /* Engine knobs: "batched" = 0 forces the per-task sweep path (tests);
- * "time_every" = k times every k-th sweep launch with HIP events. */
+ * "time_every" = k times every k-th sweep launch with HIP events;
+ * "placement" = 1 places a batched chunk by running-min levels (parallel)
+ * instead of the sequential loop (0, default). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
 
 int kbhip_session_close(kb_session* s);

@@ -94,10 +94,22 @@ KBHIP_HD int64_t lr_score(int64_t req, int64_t cap) {  // least_requested.go:44-
     return q;
 }
 
-// Score of a feasible node (nodeorder.go:281-313).  ipa: the normalised
-// inter-pod affinity score (0 for classes without inter-pod terms).
-KBHIP_HD int32_t node_score(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                              const NodeCols& nc, const Row& r, int n, int32_t ipa) {
+// Static part of the node-affinity priority: the summed weights of the
+// preferred terms the node matches (node_affinity.go:34-74).  Node labels do
+// not change in a session, so callers compute it once per node.
+KBHIP_HD int32_t na_weight(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n) {
+    int32_t na = 0;
+    for (int i = 0; i < c.pref_term_n; ++i) {
+        const Term& tm = t.terms[c.pref_term_off + i];
+        if (term_match(t, nc, tm, n)) na += tm.weight;
+    }
+    return na;
+}
+
+// Score of a feasible node (nodeorder.go:281-313): LR and BRA from the row,
+// na = na_weight(), ipa = the normalised inter-pod affinity score (0 for
+// classes without inter-pod terms).
+KBHIP_HD int32_t node_score(const Conf& cf, const TaskClass& c, const Row& r, int32_t na, int32_t ipa) {
     if (!cf.score_mult) return 0;
     const int64_t rc = c.nz_cpu + r.nzc, rm = c.nz_mem + r.nzm;
     const int64_t lr = (lr_score(rc, r.acpu) + lr_score(rm, r.amem)) / 2;
@@ -110,11 +122,6 @@ KBHIP_HD int32_t node_score(const Conf& cf, const TaskClass& c, const DevTables&
         const double one_minus = 1.0 - d;
         bra = (int64_t)(one_minus * 10.0);
     }
-    int32_t na = 0;                                                      // node_affinity.go:34-74
-    for (int i = 0; i < c.pref_term_n; ++i) {
-        const Term& tm = t.terms[c.pref_term_off + i];
-        if (term_match(t, nc, tm, n)) na += tm.weight;
-    }
     return ((int32_t)lr * cf.w_lr + (int32_t)bra * cf.w_bra + na * cf.w_na + ipa * cf.w_pa) * cf.score_mult;
 }
 
@@ -122,7 +129,7 @@ KBHIP_HD int32_t node_score(const Conf& cf, const TaskClass& c, const DevTables&
 // passed: predicate pass and score computed (the node is in the walk).
 KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t,
                                             const NodeCols& nc, const Row& r, const uint64_t* portw,
-                                            int n, bool stat_ok, int32_t* score_out, bool* passed,
+                                            int n, bool stat_ok, int32_t na, int32_t* score_out, bool* passed,
                                             int32_t ipa = 0) {
     bool ok = stat_ok;
     if (cf.pred_on) {
@@ -134,7 +141,7 @@ KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t
     if (ok && c.score_err) ok = false;  // NodeOrderFn error drops the node (allocate.go:141-145)
     *passed = ok;
     if (!ok) return 0;
-    const int32_t s = node_score(cf, c, t, nc, r, n, ipa);
+    const int32_t s = node_score(cf, c, r, na, ipa);
     *score_out = s;
     // allocate.go:153 (InitResreq <= Idle + Backfilled) and :173 (<= Releasing)
     const bool fit_acc = c.ireq_cpu - (r.idle_cpu + r.bf_cpu) < kMinCPU &&
@@ -149,11 +156,12 @@ KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t
 KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
                                               const NodeCols& nc, int n, int32_t* score_out, bool* passed) {
     const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
-    return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed);
+    return dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
 }
 
 // ---------------------------------------------------------------------------
@@ -216,11 +224,12 @@ KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTab
     int32_t ipa = 0;
     if (st && c.ipa_n && hi - lo > 0)
         ipa = (int32_t)(10.0 * ((double)(ipa_count(c, t, nc, n, F) - lo) / (double)(hi - lo)));
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
-    return dyn_key(cf, c, t, nc, r, pw, n, st, score_out, passed, ipa);
+    return dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed, ipa);
 }
 
 // Backfill's node test (backfill.go:51-56): the predicates only — no score,

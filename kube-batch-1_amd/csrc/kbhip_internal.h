@@ -36,7 +36,7 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st);
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement = 0);
 int pop_blocks(int n_nodes, int* R_out);
 size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS

@@ -241,6 +241,7 @@ __host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n
 struct PopArgs {
     int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
     uint32_t epoch;
+    int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels
 };
 
 constexpr int kPopThreads = 512;  // 8 waves
@@ -274,6 +275,32 @@ __device__ __forceinline__ uint64_t wave_max_key(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// ---------------------------------------------------------------------------
+// Placement by levels (option "placement" = 1).  The greedy of a chunk picks,
+// task after task, the node with the largest current key; only the winner's
+// key changes.  Give candidate j the entries e(j, d) for its d-th extra
+// commit: (running minimum of its scores over levels 0..d, index, d, real
+// kind).  The greedy's choice sequence equals the entries sorted descending:
+// a node whose key RISES after a commit is picked again at once (every other
+// current key is below its previous one), which the running minimum keeps in
+// place; between nodes, equal scores go to the lower index as in pack_key.
+// Entries are generated level by level (one re-evaluation per lane), merged
+// into a sorted top-64, and generation stops when no lane's newest entry
+// reaches the current m-th entry (deeper entries of a node are smaller).
+// ---------------------------------------------------------------------------
+constexpr int kEntryIdxMax = (1 << 25) - 1;  // batched path: < 2^25 nodes
+
+__device__ __forceinline__ uint64_t level_entry(int32_t rm, int n, int d, uint64_t key) {
+    return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
+           ((uint64_t)(63 - d) << 1) | (key & 1);
+}
+__device__ __forceinline__ int entry_idx(uint64_t e) { return kEntryIdxMax - (int)((e >> 7) & kEntryIdxMax); }
+__device__ __forceinline__ int entry_kind(uint64_t e) { return (e & 1) ? 2 : 1; }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
 // Hand-off of 64-key lists between workgroups: write-through (sc1) 8-byte
 // stores drained before an agent-scope counter add, sc1 loads on the consumer
 // after its add returned (MI355X_MICROARCH.md, valid forms, table row 1).
@@ -294,6 +321,85 @@ __device__ __forceinline__ void block_tree_merge(uint64_t (*wl)[64], int wave, i
         if (wave < s) wl[wave][lane] = wave_merge_desc(wl[wave][lane], wl[wave + s][lane]);
         __syncthreads();
     }
+}
+
+// Wave 0 of the final merger: K = lane's candidate key (sorted top-64).
+__device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                             const PopArgs& a, uint64_t K, PopOut* out) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    if (n >= 0) {
+        base = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    uint64_t pwc[4];  // ports after one or more commits of this class
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    uint64_t key = K;                                  // real key of the node after `ca + cp` commits
+    int32_t rm = K ? key_score(K) : 0;                 // running minimum of its scores
+    uint64_t cur = K ? level_entry(rm, n, 0, K) : 0;   // this lane's newest entry
+    uint64_t L = cur;                                  // sorted top-64 entries: lane p holds entry p
+    int ca = 0, cp = 0;
+    for (int d = 1; d < 64; ++d) {
+        const uint64_t T = readlane64(L, m - 1);       // m-th entry: deeper entries below it never place
+        if (!__ballot(cur != 0 && cur >= T)) break;
+        uint64_t e = 0;
+        if (key) {
+            if (key & 1) ++cp; else ++ca;              // the commit of the previous level (Pipeline / Allocate)
+            const Row r = apply_commits(base, c, ca, cp);
+            int32_t s;
+            bool passed;
+            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+            if (key) {
+                rm = key_score(key) < rm ? key_score(key) : rm;
+                e = level_entry(rm, n, d, key);
+            }
+        }
+        cur = e;
+        L = wave_merge_desc(L, wave_sort_desc(e >= T ? e : 0));  // entries below T cannot reach the top m
+    }
+    STAMP(gridDim.x * 4 + 2);
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const bool valid = lane < m && L != 0;
+    const uint64_t amask = __ballot(valid && entry_kind(L) == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!valid || !a.gang_mode || ready_p >= a.min_avail));
+    int done, stop;
+    if (smask) {
+        const int p = __ffsll((unsigned long long)smask) - 1;
+        done = p + 1;
+        stop = __builtin_amdgcn_readlane((int)valid, p) ? 2 : 1;
+    } else {
+        done = m;
+        stop = 0;
+    }
+    // commits of this lane's node among the placed entries; write the row back
+    int na = 0, np = 0;
+    for (int p = 0; p < done; ++p) {
+        const uint64_t e = readlane64(L, p);
+        if (e && entry_idx(e) == n) { if (entry_kind(e) == 1) ++na; else ++np; }
+    }
+    if (n >= 0 && na + np > 0) {
+        const Row r = apply_commits(base, c, na, np);
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+    }
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, L ? entry_kind(L) : 0, L ? entry_idx(L) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(gridDim.x * 4 + 3);
 }
 
 template <int R>
@@ -360,6 +466,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     STAMP(gridDim.x * 4 + 0);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.placement == 1) {  // uniform
+        if (wave != 0) return;
+        STAMP(gridDim.x * 4 + 1);
+        place_levels(cf, nc, t, c, a, wl[0][lane], out);
+        return;
+    }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
     // n, sweep key K.  The post-commit keys of each candidate (after 1..kDepth
     // more tasks of this class, assuming every commit is an Allocate) are
@@ -369,10 +481,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     const int n = K ? key_idx(K) : -1;
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;  // static node-affinity weight of this lane's node
     if (n >= 0 && wave <= kDepth) {
         base = load_row(nc, n);
         if (c.has_ports)
             for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     uint64_t pwc[4];  // ports after one or more commits of this class
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
@@ -382,7 +496,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
             const Row r = apply_commits(base, c, wave + 1, 0);
             int32_t s;
             bool passed;
-            v = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+            v = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
         }
         chainbuf[wave][lane] = v;
     }
@@ -450,7 +564,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
             const Row r = apply_commits(base, c, na, np);
             int32_t s;
             bool passed;
-            val = dyn_key(cf, c, t, nc, r, pwc, n, true, &s, &passed);
+            val = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
         }
         const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), slow_lane) << 32 |
                             (uint32_t)__builtin_amdgcn_readlane((int)val, slow_lane);
@@ -518,10 +632,10 @@ int pop_blocks(int n_nodes, int* R_out) {
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st) {
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement) {
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch};
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement};
     PopOut* o = (PopOut*)out_dev;
     switch (R) {
         case 1: hipLaunchKernelGGL(k_pop_batch<1>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;

@@ -197,6 +197,7 @@ struct Session {
 #endif
     uint64_t* d_walk = nullptr;
     bool batched = true;
+    int placement = 0;  // batched chunk placement: 0 sequential loop, 1 running-min levels
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -965,7 +966,8 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
         const TaskClass& c = S.classes[cls0];
-        const bool batch = S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4;
+        const bool batch = S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4 &&
+                           S.nc.n < (1 << 25);
         if (!batch) {  // general path: take up to a chunk of mixed classes
             m = std::min(n - done, kMaxChunk);
         }
@@ -987,7 +989,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             if (timed) HIPCHK(hipEventRecord(S.ev0, S.stream));
             auto tl0 = std::chrono::steady_clock::now();
             HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, epoch,
-                                    S.d_cand2, S.d_arrive, S.d_out, S.stream));
+                                    S.d_cand2, S.d_arrive, S.d_out, S.stream, S.placement));
             if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
             auto tl1 = std::chrono::steady_clock::now();
             // poll the self-tagged result granules (each one 8-byte store on the device)
@@ -1504,6 +1506,10 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else if (std::strcmp(key, "placement") == 0) {
+            if (value != 0 && value != 1) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0 or 1");
+            s->s.placement = (int)value;
+        }
         else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);
         return KBHIP_OK;
     })

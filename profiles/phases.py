@@ -11,11 +11,14 @@ if not os.path.exists(p):
     os.makedirs(os.path.dirname(p), exist_ok=True)
     kbgen.gen_c4(p)
 L = kbhip.lib()
+placement = int(sys.argv[1]) if len(sys.argv) > 1 else 0  # 1: running-min levels (chain phase ~0)
 with kbhip.Session(p) as s:
+    s.set_option("placement", placement)
     s.allocate()
     out = (ctypes.c_double * 12)()
     n = L.kbhip_debug_phases(s._h, out, 12)
     names = ["block sweep+sort", "block merge+store", "span to all block lists stored",
              "group merge tail to final start", "final merge", "chain precompute", "placement loop",
              "write back", "kernel span", "tasks per launch"]
-    print(json.dumps({"pops": n, **{names[i]: round(out[i], 3) for i in range(10)}}, indent=1))
+    print(json.dumps({"pops": n, "placement": placement, **{names[i]: round(out[i], 3) for i in range(10)}},
+                     indent=1))

@@ -1,0 +1,101 @@
+"""GPU parity of the batched path's running-min level placement (option
+"placement" = 1): placement logs equal the CPU oracle's and the sequential
+placement loop's.  The selection argument is checked exhaustively on CPU in
+test_placement_levels_model below (it runs without a GPU)."""
+import os
+import random
+
+import pytest
+
+from test_gpu_parity import NO_POD_AFFINITY, _oracle_log
+
+
+def _log(engine, path, placement):
+    with engine.Session(path) as s:
+        s.set_option("placement", placement)
+        pod, node, kind = s.allocate()
+        st = s.stats()
+    return [(int(p), int(n), 4 if k == 1 else 8) for p, n, k in zip(pod, node, kind)], st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(30))
+def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    c = kbgen_mod.gen_random(4100 + seed, n_nodes=4 + seed % 12, n_jobs=4 + seed % 8, max_tasks=2 + seed % 9,
+                             features=NO_POD_AFFINITY)
+    p = str(tmp_path / "l.kbs")
+    c.write(p)
+    got, st = _log(engine, p, 1)
+    assert got == _oracle_log(oracle_mod, p)
+
+
+@pytest.mark.gpu
+def test_levels_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c2.kbs")
+    kbgen_mod.gen_c2(p)
+    got, st = _log(engine, p, 1)
+    assert st["batched_pops"] > 0
+    assert got == _oracle_log(oracle_mod, p, fast=True)
+
+
+@pytest.mark.gpu
+def test_levels_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c4s.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
+    a, _ = _log(engine, p, 0)
+    b, _ = _log(engine, p, 1)
+    assert a == b
+
+
+# ---- CPU: the selection argument (no GPU) ----------------------------------
+def _greedy(seqs, idx, m):
+    c = [0] * len(seqs)
+    out = []
+    for _ in range(m):
+        best = None
+        for j, s in enumerate(seqs):
+            if c[j] < len(s) and s[c[j]] is not None:
+                key = (s[c[j]][0], -idx[j])
+                if best is None or key > best[0]:
+                    best = (key, j, s[c[j]][1])
+        if best is None:
+            out.append(None)
+            break
+        out.append((best[1], best[2]))
+        c[best[1]] += 1
+    return out
+
+
+def _levels(seqs, idx, m):
+    ents = []
+    for j, s in enumerate(seqs):
+        rm = None
+        for d, e in enumerate(s):
+            if e is None:
+                break
+            rm = e[0] if rm is None else min(rm, e[0])
+            ents.append(((rm, -idx[j], -d), j, e[1]))
+    ents.sort(reverse=True)
+    out = [(j, k) for _, j, k in ents[:m]]
+    return out + [None] if len(out) < m else out
+
+
+def test_placement_levels_model():
+    """Sorting (running-min score, -index, -depth) entries reproduces the
+    sequential greedy, including scores that rise after a commit, ties and
+    nodes that become infeasible."""
+    rng = random.Random(7)
+    for _ in range(20000):
+        n, m = rng.randint(1, 6), rng.randint(1, 8)
+        idx = rng.sample(range(50), n)
+        seqs = []
+        for _j in range(n):
+            s = [None if rng.random() < 0.1 else (rng.randint(0, 5), rng.randint(1, 2))
+                 for _d in range(rng.randint(1, m + 1))]
+            if None in s:
+                s = s[:s.index(None) + 1]
+            elif len(s) <= m:
+                s.append(None)
+            seqs.append(s)
+        g = _greedy(seqs, idx, m)
+        assert g == _levels(seqs, idx, m)[:len(g)]
