@@ -249,18 +249,22 @@ KBHIP_HD uint64_t eval_first_fit(const Conf& cf, const TaskClass& c, const DevTa
 
 // Count-table updates of a committed task (kind 1 Allocated, 2 Pipelined) on
 // global node g (every shard applies them).
+//   UPD_CNT_ALLOC (0):    Allocated only: a new predicate target in g's domain
+//   UPD_SCALAR_ALLOC (1): Allocated only: target total of a PA class
+//   UPD_SCALAR_ANY (2):   any commit: a session-placed pod (inter-pod priority)
+// Written branch-free on purpose: the if / else-if / else form (one increment
+// per branch, two tables) is miscompiled by the ROCm 7.2 gfx950 backend when
+// it runs in a single lane — the UPD_SCALAR_ANY branch reused a stale table
+// pointer register ("toolchain note").
 KBHIP_HD void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int g, int kind) {
     for (int i = 0; i < c.upd_n; ++i) {
         const int32_t* u = t.aff_items + c.upd_off + 3 * i;
-        if (u[0] == 0) {         // UPD_CNT_ALLOC: a new predicate target in n's domain
-            if (kind != 1) continue;
-            const int d = dom_g(nc, u[1], g);
-            if (d >= 0) t.aff_cnt[u[2] + d] += 1;
-        } else if (u[0] == 1) {  // UPD_SCALAR_ALLOC: target total of a PA class
-            if (kind == 1) t.aff_scalar[u[2]] += 1;
-        } else {                 // UPD_SCALAR_ANY: a session-placed pod (IPA)
-            t.aff_scalar[u[2]] += 1;
-        }
+        const int typ = u[0];
+        const bool to_cnt = typ == 0;
+        const int d = to_cnt ? dom_g(nc, u[1], g) : 0;
+        const bool apply = (typ == 2 || kind == 1) && d >= 0;
+        int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
+        tab[u[2] + d] += apply ? 1 : 0;
     }
 }
 

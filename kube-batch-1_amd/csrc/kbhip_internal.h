@@ -22,10 +22,11 @@ struct DevTables {
     int32_t* aff_scalar;       // PA target totals, session counters
 };
 
-// Per-task sweep; commit_here = the last block commits (one GPU).  Sharded
+// Per-task sweep; dbg (debug only): per-node keys, raw inter-pod counts,
+// [lo, hi, F, max key]: rows of 2 npad + 4 words per task of the chunk; commit_here = the last block commits (one GPU).  Sharded
 // sessions reduce ctrl->slot[task_i] across shards and then launch_commit_task.
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st, bool commit_here = true);
+                               uint64_t* walk, hipStream_t st, bool commit_here = true, uint64_t* dbg = nullptr);
 hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
                               hipStream_t st);
 // Inter-pod affinity priority prepass: min / max of the raw count over all

@@ -147,7 +147,7 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
 // commit_here: the last block commits (one GPU); otherwise the slot is
 // reduced across shards first and k_commit_task commits.
 __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
-                                                         int task_i, uint64_t* walk, int commit_here) {
+                                                         int task_i, uint64_t* walk, int commit_here, uint64_t* dbg) {
     __shared__ uint64_t red[kBlock / 64];
     __shared__ int last;
     if (ctrl->stop >= 0) return;  // the pop already stopped (uniform)
@@ -164,6 +164,10 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
         const uint64_t k = first_fit ? eval_first_fit(cf, c, t, nc, n)
                                      : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
         if (track) walk[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
+        if (dbg) {  // kbhip_set_option("debug_keys")
+            dbg[(int64_t)task_i * (2 * nc.npad + 4) + n] = k;
+            dbg[(int64_t)task_i * (2 * nc.npad + 4) + nc.npad + n] = (uint64_t)(c.ipa_n ? ipa_count(c, t, nc, n, F) : 0);
+        }
         best = k > best ? k : best;
     }
     best = wave_max_u64(best);
@@ -180,7 +184,13 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
         __threadfence();
     }
     __syncthreads();
-    if (!last || !commit_here) return;
+    if (!last) return;
+    if (dbg && threadIdx.x == 0) {
+        uint64_t* d = dbg + (int64_t)task_i * (2 * nc.npad + 4) + 2 * nc.npad;
+        d[0] = (uint64_t)ilo; d[1] = (uint64_t)ihi; d[2] = (uint64_t)(int64_t)F;
+        d[3] = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!commit_here) return;
     commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk);
 }
 
@@ -600,12 +610,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st, bool commit_here) {
+                               uint64_t* walk, hipStream_t st, bool commit_here, uint64_t* dbg) {
     int grid = (nc.n + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk,
-                       commit_here ? 1 : 0);
+                       commit_here ? 1 : 0, dbg);
     return hipGetLastError();
 }
 

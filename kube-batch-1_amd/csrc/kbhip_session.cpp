@@ -196,6 +196,12 @@ struct Session {
     int64_t phase_n = 0;
 #endif
     uint64_t* d_walk = nullptr;
+    // kbhip_set_option("debug_keys"): every per-task sweep's keys, for tests
+    bool debug_keys = false;
+    DevBuf b_dbg;
+    uint64_t* d_dbg = nullptr;
+    vector<uint64_t> dbg_keys;  // rows of 2 npad + 4: keys, raw ipa counts, ipa lo, ipa hi, fallback, max key
+    vector<int32_t> dbg_pods;
     bool batched = true;
     int placement = 0;  // batched chunk placement: 0 sequential loop, 1 running-min levels
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
@@ -215,6 +221,7 @@ struct Session {
     bool encode_only = false;
     vector<int32_t> h_dom, h_aff_cnt, h_aff_scalar, h_aff_items;
     int n_spaces = 0;
+    size_t n_aff_cnt = 0, n_aff_scalar = 0;  // table sizes (device sessions read them back for tests)
 
     ~Session() {
         if (comm) (void)ncclCommDestroy(comm);
@@ -795,6 +802,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     for (int i = lo; i < hi; ++i)
         for (int id : node_ports[i]) pcol[(size_t)(id / 64) * npl + (i - lo)] |= 1ULL << (id % 64);
     S.nc.ports = upload(S, S.b_ports, pcol);
+    S.n_aff_cnt = aff.active ? aff.cnt.size() : 1;
+    S.n_aff_scalar = aff.active ? aff.scalar.size() : 1;
     if (aff.active) {  // domain columns cover every node on every shard (winners may be remote)
         S.nc.dom = upload(S, S.b_dom, aff.dom);
         if (aff_items.empty()) aff_items.push_back(0);
@@ -889,7 +898,7 @@ static void sweep_task(Session& S, int i, int cls) {
         exchange(S, &S.d_ctrl->ipa_lo[i], KBHIP_RED_MIN_I64);
         exchange(S, &S.d_ctrl->ipa_hi[i], KBHIP_RED_MAX_I64);
     }
-    HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1));
+    HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1, S.d_dbg));
     if (S.world > 1) {
         exchange(S, &S.d_ctrl->slot[i], KBHIP_RED_MAX_U64);
         HIPCHK(launch_commit_task(S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
@@ -1081,6 +1090,13 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             S.stats.sweeps += m;
             HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
             HIPCHK(hipStreamSynchronize(S.stream));
+            if (S.d_dbg) {
+                const size_t row = 2 * (size_t)S.nc.npad + 4;
+                const size_t off = S.dbg_keys.size();
+                S.dbg_keys.resize(off + row * h.n_done);
+                HIPCHK(hipMemcpy(S.dbg_keys.data() + off, S.d_dbg, row * h.n_done * 8, hipMemcpyDeviceToHost));
+                for (int i = 0; i < h.n_done; ++i) S.dbg_pods.push_back(ids[done + i]);
+            }
             n_done = h.n_done;
             stop_c = h.stop;
             ready_c = h.ready_count;
@@ -1506,6 +1522,14 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
+            kbhip::Session& S = s->s;
+            S.debug_keys = value != 0;
+            if (S.debug_keys && !S.d_dbg && !S.encode_only) {
+                HIPCHK(hipSetDevice(S.device));
+                S.d_dbg = S.b_dbg.alloc<uint64_t>((size_t)kbhip::kMaxChunk * (2 * S.nc.npad + 4));
+            }
+        }
         else if (std::strcmp(key, "placement") == 0) {
             if (value != 0 && value != 1) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0 or 1");
             s->s.placement = (int)value;
@@ -1608,12 +1632,24 @@ int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t ca
         } else if (n == "aff_dom") {
             if (!S.encode_only) throw kbhip::Error(KBHIP_EINVAL, "tables are kept by encode-only sessions");
             v = S.h_dom;
-        } else if (n == "aff_cnt") {
-            v = S.h_aff_cnt;
-        } else if (n == "aff_scalar") {
-            v = S.h_aff_scalar;
+        } else if (n == "aff_cnt" || n == "aff_scalar") {  // device sessions: the current device table
+            if (S.encode_only) {
+                v = n == "aff_cnt" ? S.h_aff_cnt : S.h_aff_scalar;
+            } else {
+                v.resize(n == "aff_cnt" ? S.n_aff_cnt : S.n_aff_scalar);
+                HIPCHK(hipSetDevice(S.device));
+                HIPCHK(hipStreamSynchronize(S.stream));
+                HIPCHK(hipMemcpy(v.data(), n == "aff_cnt" ? S.tab.aff_cnt : S.tab.aff_scalar, v.size() * 4,
+                                 hipMemcpyDeviceToHost));
+            }
         } else if (n == "aff_items") {
             v = S.h_aff_items;
+        } else if (n == "dbg_keys") {  // u64 words, rows of 2 npad + 4 (kbhip_set_option "debug_keys")
+            const int64_t bytes = (int64_t)(S.dbg_keys.size() * 8);
+            if (out && cap_bytes >= bytes && bytes) std::memcpy(out, S.dbg_keys.data(), (size_t)bytes);
+            return bytes;
+        } else if (n == "dbg_pods") {
+            v = S.dbg_pods;
         } else if (n == "dims") {  // n_nodes, npad, n_spaces, n_classes
             v = {S.nc.n, S.nc.npad, S.n_spaces, (int32_t)S.classes.size()};
         } else {

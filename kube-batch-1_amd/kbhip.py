@@ -184,6 +184,31 @@ class Session:
         _check(lib().kbhip_read_nodes(self._h, _p(out), n_nodes))
         return out
 
+    def debug_keys(self) -> Tuple[np.ndarray, np.ndarray]:
+        """Test support (after set_option("debug_keys", 1) and a run): the pod of
+        every per-task sweep and its row: per-node keys, per-node raw inter-pod
+        counts (npad each), then ipa lo, ipa hi, fallback node, max key."""
+        L = lib()
+        n = int(L.kbhip_debug_table(self._h, b"dbg_keys", None, 0))
+        _check(n if n < 0 else 0)
+        keys = np.zeros(max(n // 8, 1), np.uint64)
+        if n:
+            _check(int(L.kbhip_debug_table(self._h, b"dbg_keys", _p(keys), keys.nbytes)))
+        m = int(L.kbhip_debug_table(self._h, b"dbg_pods", None, 0))
+        pods = np.zeros(max(m // 4, 1), np.int32)
+        if m:
+            _check(int(L.kbhip_debug_table(self._h, b"dbg_pods", _p(pods), pods.nbytes)))
+        pods = pods[: m // 4]
+        return pods, keys[: n // 8].reshape(len(pods), -1) if len(pods) else keys[:0]
+
+    def table(self, name: str) -> np.ndarray:
+        """Test support: a device table read back (kbhip_debug_table)."""
+        n = lib().kbhip_debug_table(self._h, name.encode(), None, 0)
+        _check(int(n) if n < 0 else 0)
+        out = np.zeros(max(int(n) // 4, 1), np.int32)
+        _check(int(lib().kbhip_debug_table(self._h, name.encode(), _p(out), out.nbytes)) if n > 0 else 0)
+        return out[: int(n) // 4]
+
     def stats(self) -> dict:
         st = Stats()
         _check(lib().kbhip_get_stats(self._h, ctypes.byref(st)))

@@ -5,6 +5,7 @@ the CPU oracle's, both device paths."""
 import json
 import os
 
+import numpy as np
 import pytest
 
 from test_gpu_parity import GOLD, _engine_log, _oracle_log
@@ -73,3 +74,40 @@ def test_c3_scaled(engine, oracle_mod, kbgen_mod, tmp_path):
     assert st["batched_pops"] > 0
 
 
+
+
+def _decode_max(k):
+    k = int(k)
+    if not k:
+        return -1, 1
+    return 0x7fffffff - ((k >> 1) & 0x7fffffff), 2 if k & 1 else 1
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_device_keys_match_host_replay(engine, kbgen_mod, tmp_path, seed):
+    """Every per-task sweep's per-node keys and raw inter-pod counts on the
+    device equal the host replay of the same __host__ __device__ arithmetic
+    (kbhip_debug_replay) along the device's own decisions.  Catches device-only
+    divergence (codegen, stale tables) independently of the oracle."""
+    tiers = [None, [["gang"], ["predicates", "nodeorder"]],
+             [["priority", "gang", "drf"], ["predicates", "proportion", "nodeorder", "nodeorder"]]][seed % 3]
+    c = kbgen_mod.gen_random(7000 + seed, n_nodes=4 + seed % 13, n_jobs=4 + seed % 8, max_tasks=1 + seed % 8,
+                             tiers=tiers)
+    if seed % 2 == 0:
+        c.args = {"nodeorder": {"podaffinity.weight": str(1 + seed % 4)}}
+    p = str(tmp_path / "k.kbs")
+    c.write(p)
+    with engine.Session(p) as s:
+        s.set_option("batched", 0)
+        s.set_option("debug_keys", 1)
+        s.allocate()
+        pods, rows = s.debug_keys()
+    with engine.EncodedSnapshot(p) as enc:
+        n = int(enc.table("dims")[0])
+        npad = (rows.shape[1] - 4) // 2 if len(pods) else n
+        dec = [_decode_max(r[2 * npad + 3]) for r in rows]
+        nodes = np.array([d[0] for d in dec], np.int32)
+        kinds = np.array([d[1] for d in dec], np.uint8)
+        keys = enc.replay(pods, np.zeros(len(pods), np.int32), nodes, kinds)
+    for i in range(len(pods)):
+        assert np.array_equal(rows[i][:n], keys[i]), f"sweep {i} (pod {pods[i]}): device keys differ from the replay"
