@@ -52,8 +52,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--time-every", type=int, default=4, help="HIP-event time every k-th sweep launch")
-    ap.add_argument("--placement", type=int, default=0, choices=(0, 1),
-                    help="batched chunk placement: 0 sequential loop, 1 running-min levels")
+    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2),
+                    help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
                     help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
                          "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")

@@ -125,8 +125,11 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
 
 /* Engine knobs: "batched" = 0 forces the per-task sweep path (tests);
  * "time_every" = k times every k-th sweep launch with HIP events;
- * "placement" = 1 places a batched chunk by running-min levels (parallel)
- * instead of the sequential loop (0, default). */
+ * "placement" = 2 (default) places a batched chunk by parallel levels, 8
+ * depths per step; 1 by running-min levels, one depth per step; 0 by the
+ * sequential loop over precomputed chains;
+ * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
+ * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
 
 int kbhip_session_close(kb_session* s);

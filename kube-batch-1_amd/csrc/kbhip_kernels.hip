@@ -70,13 +70,55 @@ __global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t,
 }
 
 // ---------------------------------------------------------------------------
+// wave-level exchange: lane i <-> lane i ^ J without the LDS crossbar.
+// J = 1, 2: DPP quad_perm; 4: DPP row_shl:4 / row_shr:4 + select; 8: DPP
+// row_ror:8; 16 / 32: gfx950 v_permlane16_swap / v_permlane32_swap.
+// (ds_bpermute, what __shfl_xor lowers to, costs an LDS round trip per
+// 32-bit half; these are VALU ops.)  Checked against __shfl_xor on the GPU.
+// ---------------------------------------------------------------------------
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xf, 0xf, false);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+        return (lane & 4) ? dn : up;
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "xor distance");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+}
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v) {
+    return ((uint64_t)xor_lane32<J>((uint32_t)(v >> 32)) << 32) | xor_lane32<J>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t reverse_lanes64(uint64_t v) {  // lane i <- lane 63 - i (= i ^ 63)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x140, 0xf, 0xf, false);  // row_mirror
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x140, 0xf, 0xf, false);
+    return xor_lane64<32>(xor_lane64<16>(((uint64_t)hi << 32) | lo));
+}
+
+// ---------------------------------------------------------------------------
 // wave / block reductions
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t u = __shfl_xor(v, o, 64);
-        v = u > v ? u : v;
-    }
+    uint64_t u;
+    u = xor_lane64<32>(v); v = u > v ? u : v;
+    u = xor_lane64<16>(v); v = u > v ? u : v;
+    u = xor_lane64<8>(v); v = u > v ? u : v;
+    u = xor_lane64<4>(v); v = u > v ? u : v;
+    u = xor_lane64<2>(v); v = u > v ? u : v;
+    u = xor_lane64<1>(v); v = u > v ? u : v;
     return v;
 }
 
@@ -211,30 +253,47 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
 // batched path v2: one launch per pop chunk
 // ---------------------------------------------------------------------------
 // Wave-level sorting on registers: lane i holds one u64; descending order.
-__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
+// Bitonic network, every exchange a DPP / permlane op (xor_lane64).
+template <int K, int J>
+__device__ __forceinline__ uint64_t bitonic_step(uint64_t v) {
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const uint64_t o = __shfl_xor(v, j, 64);
-            const bool keep_max = ((lane & j) == 0) == ((lane & k) == 0);
-            v = keep_max ? (o > v ? o : v) : (o < v ? o : v);
-        }
-    }
-    return v;
+    const uint64_t o = xor_lane64<J>(v);
+    const bool keep_max = ((lane & J) == 0) == ((lane & K) == 0);
+    return keep_max ? (o > v ? o : v) : (o < v ? o : v);
+}
+template <int K>
+__device__ __forceinline__ uint64_t bitonic_stage(uint64_t v) {
+    if constexpr (K >= 64) v = bitonic_step<K, 32>(v);
+    if constexpr (K >= 32) v = bitonic_step<K, 16>(v);
+    if constexpr (K >= 16) v = bitonic_step<K, 8>(v);
+    if constexpr (K >= 8) v = bitonic_step<K, 4>(v);
+    if constexpr (K >= 4) v = bitonic_step<K, 2>(v);
+    return bitonic_step<K, 1>(v);
+}
+__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
+    v = bitonic_stage<2>(v);
+    v = bitonic_stage<4>(v);
+    v = bitonic_stage<8>(v);
+    v = bitonic_stage<16>(v);
+    v = bitonic_stage<32>(v);
+    return bitonic_stage<64>(v);
 }
 // Top-64 of two descending lists (lane i holds a[i], b[i]); result descending.
-__device__ __forceinline__ uint64_t wave_merge_desc(uint64_t a, uint64_t b) {
+template <int J>
+__device__ __forceinline__ uint64_t half_clean_desc(uint64_t v) {
     const int lane = threadIdx.x & 63;
-    const uint64_t br = __shfl(b, 63 - lane, 64);
+    const uint64_t o = xor_lane64<J>(v);
+    return ((lane & J) == 0) ? (o > v ? o : v) : (o < v ? o : v);
+}
+__device__ __forceinline__ uint64_t wave_merge_desc(uint64_t a, uint64_t b) {
+    const uint64_t br = reverse_lanes64(b);
     uint64_t v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
-#pragma unroll
-    for (int j = 32; j > 0; j >>= 1) {
-        const uint64_t o = __shfl_xor(v, j, 64);
-        v = ((lane & j) == 0) ? (o > v ? o : v) : (o < v ? o : v);
-    }
-    return v;
+    v = half_clean_desc<32>(v);
+    v = half_clean_desc<16>(v);
+    v = half_clean_desc<8>(v);
+    v = half_clean_desc<4>(v);
+    v = half_clean_desc<2>(v);
+    return half_clean_desc<1>(v);
 }
 
 // Results land in pinned host memory as self-tagged 8-byte granules, one per
@@ -251,7 +310,7 @@ __host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n
 struct PopArgs {
     int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
     uint32_t epoch;
-    int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels
+    int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels, 2: parallel levels
 };
 
 constexpr int kPopThreads = 512;  // 8 waves
@@ -412,6 +471,162 @@ __device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables
     STAMP(gridDim.x * 4 + 3);
 }
 
+// ---------------------------------------------------------------------------
+// Placement by parallel levels (option "placement" = 2): the same entries as
+// place_levels, but a round computes 8 depths at once — wave w evaluates
+// candidate j after d = 8r + w commits of this class — then one sort + tree
+// merge of the round's 512 entries.  Commit kinds along a chain are
+// Allocate^a Pipeline^p (once Idle + Backfilled cannot fit, later commits
+// only touch Releasing), so a first pass assumes Allocate everywhere and the
+// depths behind a lane's first Pipeline are recomputed.  The entry carries the
+// candidate's lane instead of its depth: entries of one node are
+// interchangeable for the counts, and a position's commit kind is looked up
+// by its rank among its node's entries.  Another round runs only while some
+// candidate's deepest entry still reaches the m-th entry.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lane_entry(int32_t rm, int n, int lane) {
+    return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
+           ((uint64_t)lane << 1) | 1ull;
+}
+__device__ __forceinline__ int entry_lane(uint64_t e) { return (int)((e >> 1) & 63); }
+
+__device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                               const PopArgs& a, PopOut* out, uint64_t (*wl)[64]) {
+    constexpr int kW = kPopThreads / 64;  // depths per round
+    __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
+    __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
+    __shared__ int32_t s_rm[64];          // running min through the previous round's deepest depth
+    __shared__ int32_t s_apos[64];        // first Pipeline depth (64: none yet)
+    __shared__ uint64_t s_last[64];       // entry at the round's deepest depth
+    __shared__ int32_t s_cnt[64];
+    __shared__ int s_more;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t K = wl[0][lane];
+    const int n = K ? key_idx(K) : -1;
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    if (n >= 0) {
+        base = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    uint64_t pwc[4];
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
+    __syncthreads();  // K read by every wave; wl free
+    STAMP(gridDim.x * 4 + 5);
+    auto eval_at = [&](int d, int ap, int32_t* sc) -> int {  // kind of commit d+1's key (0: infeasible)
+        if (d == 0) { *sc = key_score(K); return key_kind(K); }
+        const int na = d < ap ? d : ap;
+        const Row r = apply_commits(base, c, na, d - na);
+        int32_t s;
+        bool passed;
+        const uint64_t k = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+        *sc = k ? key_score(k) : 0;
+        return k ? key_kind(k) : 0;
+    };
+    uint64_t L = 0;      // wave 0: merged top-64 entries so far (lane p = entry p)
+    bool alive = n >= 0; // candidate still relevant (uniform over waves)
+    for (int r = 0; r < 64 / kW; ++r) {
+        const int d = r * kW + wave;
+        int ap = s_apos[lane];
+        int32_t sc = 0;
+        int kind = alive ? eval_at(d, ap, &sc) : 0;
+        s_kind[d][lane] = (uint8_t)kind;
+        __syncthreads();
+        if (ap == 64) {  // first Pipeline within this round: recompute the depths behind it
+            for (int w2 = 0; w2 < kW; ++w2)
+                if (s_kind[r * kW + w2][lane] == 2) { ap = r * kW + w2; break; }
+            if (alive && ap < d) kind = eval_at(d, ap, &sc);
+        }
+        __syncthreads();  // scans of the first-pass kinds done
+        s_sc[wave][lane] = sc;
+        s_kind[d][lane] = (uint8_t)kind;
+        if (wave == 0) s_apos[lane] = ap;
+        __syncthreads();
+        // running minimum through depth d; the chain ends at the first infeasible depth
+        bool ok = alive;
+        int32_t rm = r == 0 ? INT32_MAX : s_rm[lane];
+        for (int w2 = 0; w2 <= wave && ok; ++w2) {
+            if (s_kind[r * kW + w2][lane] == 0) ok = false;
+            const int32_t x = s_sc[w2][lane];
+            rm = x < rm ? x : rm;
+        }
+        const uint64_t e = ok ? lane_entry(rm, n, lane) : 0;
+        __syncthreads();  // s_rm reads done
+        if (r == 0) STAMP(gridDim.x * 4 + 6);
+        if (wave == kW - 1) { s_last[lane] = e; s_rm[lane] = rm; }
+        wl[wave][lane] = wave_sort_desc(e);
+        __syncthreads();
+        block_tree_merge(wl, wave, lane);
+        if (wave == 0) {
+            L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
+            if (r == 0) STAMP(gridDim.x * 4 + 7);
+            const uint64_t T = readlane64(L, m - 1);  // m-th entry: deeper entries below it never place
+            const uint64_t le = s_last[lane];
+            const bool more = le != 0 && le >= T;
+            const bool any = __ballot(more) != 0;  // all 64 lanes active
+            if (lane == 0) s_more = any;
+            s_last[lane] = more;  // reused as the alive flag of the next round
+        }
+        __syncthreads();
+        if (!s_more) break;
+        alive = s_last[lane] != 0;
+        __syncthreads();
+    }
+    if (wave != 0) return;
+    STAMP(gridDim.x * 4 + 2);
+    // commit kind of each position: rank among the entries of its node
+    const bool inm = lane < m && L != 0;
+    const int lf = entry_lane(L);
+    int rank = 0;
+    for (uint64_t rem = __ballot(inm); rem;) {
+        const int p0 = __ffsll((unsigned long long)rem) - 1;
+        const int l0 = __builtin_amdgcn_readlane(lf, p0);
+        const uint64_t mm = __ballot(inm && lf == l0);
+        if (inm && lf == l0) rank = __popcll(mm & ((1ull << lane) - 1));
+        rem &= ~mm;
+    }
+    const int kind = inm ? s_kind[rank][lf] : 0;
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
+    int done, stop;
+    if (smask) {
+        const int p = __ffsll((unsigned long long)smask) - 1;
+        done = p + 1;
+        stop = __builtin_amdgcn_readlane((int)inm, p) ? 2 : 1;
+    } else {
+        done = m;
+        stop = 0;
+    }
+    if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
+    __builtin_amdgcn_wave_barrier();
+    const int cc = s_cnt[lane];
+    if (n >= 0 && cc > 0) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
+        const int ap = s_apos[lane];
+        const int na = cc < ap ? cc : ap;
+        const Row r = apply_commits(base, c, na, cc - na);
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+    }
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_idx(L) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(gridDim.x * 4 + 3);
+}
+
 template <int R>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                            uint64_t* cand, uint32_t* arrive, PopOut* out) {
@@ -452,10 +667,21 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
     __syncthreads();
     if (!role) return;
-    // 2a. last block of group g: merge the group's block lists (strided over waves)
+    // 2a. last block of group g: merge the group's block lists (strided over
+    // waves; each wave issues its lists' loads together, then merges)
     {
         uint64_t acc = 0;
-        for (int i = wave; i < g_count; i += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(cand + (int64_t)(g + i * kGroups) * 64));
+        constexpr int kPf = 4;
+        for (int i0 = wave; i0 < g_count; i0 += kPf * (kPopThreads / 64)) {
+            uint64_t v[kPf];
+#pragma unroll
+            for (int q = 0; q < kPf; ++q) {
+                const int i = i0 + q * (kPopThreads / 64);
+                v[q] = i < g_count ? get_list(cand + (int64_t)(g + i * kGroups) * 64) : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kPf; ++q) acc = wave_merge_desc(acc, v[q]);
+        }
         wl[wave][lane] = acc;
         __syncthreads();
         block_tree_merge(wl, wave, lane);
@@ -480,6 +706,11 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
         place_levels(cf, nc, t, c, a, wl[0][lane], out);
+        return;
+    }
+    if (a.placement == 2) {  // uniform; every wave takes part
+        STAMP(gridDim.x * 4 + 1);
+        place_parallel(cf, nc, t, c, a, out, wl);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node

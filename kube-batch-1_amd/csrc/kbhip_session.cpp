@@ -192,7 +192,7 @@ struct Session {
 #ifdef KBHIP_STAMPS
     DevBuf b_stamps;
     uint64_t* d_stamps = nullptr;
-    double phase[12] = {0};  // accumulated phase durations (us)
+    double phase[16] = {0};  // accumulated phase durations (us)
     int64_t phase_n = 0;
 #endif
     uint64_t* d_walk = nullptr;
@@ -203,7 +203,7 @@ struct Session {
     vector<uint64_t> dbg_keys;  // rows of 2 npad + 4: keys, raw ipa counts, ipa lo, ipa hi, fallback, max key
     vector<int32_t> dbg_pods;
     bool batched = true;
-    int placement = 0;  // batched chunk placement: 0 sequential loop, 1 running-min levels
+    int placement = 2;  // batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels (default)
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1062,6 +1062,11 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
                 S.phase[7] += (L[3] - L[2]) * 0.01;        // write back
                 S.phase[8] += (L[3] - t0) * 0.01;          // total in-kernel span
                 S.phase[9] += m;
+                if (L[5] && L[6] && L[7] && S.placement == 2) {  // parallel-levels sub-phases
+                    S.phase[10] += (L[5] - L[1]) * 0.01;   // candidate rows loaded
+                    S.phase[11] += (L[6] - L[5]) * 0.01;   // round-0 depth evaluation
+                    S.phase[12] += (L[7] - L[6]) * 0.01;   // round-0 sort + merge
+                }
                 S.phase_n++;
             }
 #endif
@@ -1531,7 +1536,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
         }
         else if (std::strcmp(key, "placement") == 0) {
-            if (value != 0 && value != 1) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0 or 1");
+            if (value < 0 || value > 2) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1 or 2");
             s->s.placement = (int)value;
         }
         else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);
@@ -1542,7 +1547,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
 #ifdef KBHIP_STAMPS
 int kbhip_debug_phases(kb_session* s, double* out, int n) {
     ABI_GUARD({
-        for (int i = 0; i < n && i < 12; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
+        for (int i = 0; i < n && i < 16; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
         return (int)s->s.phase_n;
     })
 }

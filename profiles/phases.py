@@ -15,10 +15,11 @@ placement = int(sys.argv[1]) if len(sys.argv) > 1 else 0  # 1: running-min level
 with kbhip.Session(p) as s:
     s.set_option("placement", placement)
     s.allocate()
-    out = (ctypes.c_double * 12)()
-    n = L.kbhip_debug_phases(s._h, out, 12)
+    out = (ctypes.c_double * 16)()
+    n = L.kbhip_debug_phases(s._h, out, 16)
     names = ["block sweep+sort", "block merge+store", "span to all block lists stored",
              "group merge tail to final start", "final merge", "chain precompute", "placement loop",
-             "write back", "kernel span", "tasks per launch"]
-    print(json.dumps({"pops": n, "placement": placement, **{names[i]: round(out[i], 3) for i in range(10)}},
+             "write back", "kernel span", "tasks per launch", "pp: rows loaded", "pp: round-0 eval",
+             "pp: round-0 sort+merge"]
+    print(json.dumps({"pops": n, "placement": placement, **{names[i]: round(out[i], 3) for i in range(len(names))}},
                      indent=1))

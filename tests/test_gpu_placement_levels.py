@@ -19,23 +19,41 @@ def _log(engine, path, placement):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("placement", [1, 2])
 @pytest.mark.parametrize("seed", range(30))
-def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, placement):
     c = kbgen_mod.gen_random(4100 + seed, n_nodes=4 + seed % 12, n_jobs=4 + seed % 8, max_tasks=2 + seed % 9,
                              features=NO_POD_AFFINITY)
     p = str(tmp_path / "l.kbs")
     c.write(p)
-    got, st = _log(engine, p, 1)
+    got, st = _log(engine, p, placement)
     assert got == _oracle_log(oracle_mod, p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_parallel_levels_deep_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Few nodes, big gangs: chains deeper than one round of 8 depths, Pipelined
+    commits (releasing capacity) mid-chain."""
+    c = kbgen_mod.gen_random(4300 + seed, n_nodes=2 + seed % 3, n_jobs=3 + seed % 4, max_tasks=20 + 4 * seed,
+                             features=NO_POD_AFFINITY)
+    p = str(tmp_path / "d.kbs")
+    c.write(p)
+    exp = _oracle_log(oracle_mod, p)
+    for placement in (0, 1, 2):
+        got, _ = _log(engine, p, placement)
+        assert got == exp, f"placement {placement}"
 
 
 @pytest.mark.gpu
 def test_levels_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2.kbs")
     kbgen_mod.gen_c2(p)
-    got, st = _log(engine, p, 1)
-    assert st["batched_pops"] > 0
-    assert got == _oracle_log(oracle_mod, p, fast=True)
+    exp = _oracle_log(oracle_mod, p, fast=True)
+    for placement in (1, 2):
+        got, st = _log(engine, p, placement)
+        assert st["batched_pops"] > 0
+        assert got == exp, f"placement {placement}"
 
 
 @pytest.mark.gpu
@@ -44,7 +62,8 @@ def test_levels_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     a, _ = _log(engine, p, 0)
     b, _ = _log(engine, p, 1)
-    assert a == b
+    c, _ = _log(engine, p, 2)
+    assert a == b == c
 
 
 # ---- CPU: the selection argument (no GPU) ----------------------------------
