@@ -219,6 +219,7 @@ def main():
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"], "placement": args.placement,
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
+                   "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},
         "roofline": {"kernel": "k_sweep_argmax" if shard else "k_pop_batch", "bound": "hbm", "achieved": achieved,

@@ -82,6 +82,8 @@ typedef struct kbhip_stats {
     int64_t timed_launches; /* sweep launches timed with HIP events (option "time_every") */
     double host_launch_s;   /* host time spent launching batched pop kernels */
     double host_wait_s;     /* host time spent waiting for their results */
+    int64_t spec_hits;      /* predicted next pops launched ahead and used (kbhip_allocate) */
+    int64_t spec_missed;    /* predicted pops retracted (their node updates undone on device) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -128,6 +130,10 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "placement" = 2 (default) places a batched chunk by parallel levels, 8
  * depths per step; 1 by running-min levels, one depth per step; 0 by the
  * sequential loop over precomputed chains;
+ * "speculate" = 1 (default) lets kbhip_allocate queue the predicted next job
+ * pop behind the running one (used only if it is exactly the next pop,
+ * retracted on device otherwise; placements are unchanged), 0 = one pop at
+ * a time;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);

@@ -281,6 +281,20 @@ KBHIP_HD void commit_node(const TaskClass& c, const DevTables& t, const NodeCols
         for (int w = 0; w < nc.port_words; ++w) nc.ports[(int64_t)w * nc.npad + n] |= t.masks[c.pown_off + w];
 }
 
+// Exact inverse of commit_node for a batched-path class (integer updates; the
+// class's own host-port bits cannot have been set before its commit, since
+// they conflict with themselves).  Used to retract a mispredicted pop.
+KBHIP_HD void uncommit_node(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {
+    if (c.backfill) { nc.bf_cpu[n] -= c.req_cpu; nc.bf_mem[n] -= c.req_mem; nc.bf_gpu[n] -= c.req_gpu; }
+    if (kind == 1) { nc.idle_cpu[n] += c.req_cpu; nc.idle_mem[n] += c.req_mem; nc.idle_gpu[n] += c.req_gpu; }
+    else { nc.rel_cpu[n] += c.req_cpu; nc.rel_mem[n] += c.req_mem; nc.rel_gpu[n] += c.req_gpu; }
+    nc.pods[n] -= 1;
+    nc.nzc[n] -= c.nz_cpu;
+    nc.nzm[n] -= c.nz_mem;
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words; ++w) nc.ports[(int64_t)w * nc.npad + n] &= ~t.masks[c.pown_off + w];
+}
+
 // Gang bookkeeping after an assignment: allocate.go:191-195 + gang.go:63-66.
 KBHIP_HD void after_assign(PopCtrl* ctrl, int i, int kind) {
     if (kind == 1) ctrl->ready_count += 1;  // Pipelined is not an AllocatedStatus (types.go:82-84)

@@ -38,6 +38,9 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement = 0);
+// Inverse node updates of a batched pop's placements (a retracted prediction).
+hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
+                           const int32_t* kind, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
 size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS

@@ -850,6 +850,31 @@ hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTabl
     return hipGetLastError();
 }
 
+// Retraction of a batched pop whose prediction failed (Allocator::speculate):
+// the inverse node updates of its placements, in one lane (a node may appear
+// several times).
+struct UndoArgs {
+    int32_t cls, n;
+    int32_t node[kMaxChunk];
+    int32_t kind[kMaxChunk];
+};
+__global__ __launch_bounds__(64) void k_undo_pop(NodeCols nc, DevTables t, UndoArgs u) {
+    if (threadIdx.x != 0) return;
+    const TaskClass c = t.classes[u.cls];
+    for (int i = 0; i < u.n; ++i)
+        if (u.node[i] >= 0) uncommit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+}
+
+hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
+                           const int32_t* kind, hipStream_t st) {
+    UndoArgs u{};
+    u.cls = cls;
+    u.n = n < kMaxChunk ? n : kMaxChunk;
+    for (int i = 0; i < u.n; ++i) { u.node[i] = node[i]; u.kind[i] = kind[i]; }
+    hipLaunchKernelGGL(k_undo_pop, dim3(1), dim3(64), 0, st, nc, t, u);
+    return hipGetLastError();
+}
+
 hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
                               hipStream_t st) {
     hipLaunchKernelGGL(k_commit_task, dim3(1), dim3(kBlock), 0, st, nc, t, ctrl, task_i, walk);

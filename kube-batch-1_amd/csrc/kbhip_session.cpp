@@ -185,9 +185,16 @@ struct Session {
     DevBuf b_cand2, b_arrive;
     uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
-    PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device
+    PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
-    uint32_t epoch = 0;
+    uint32_t slot_epoch[2] = {0, 0};  // granule tags per result slot
+    int next_slot = 0;                // slot of the next batched launch (alternates)
+    hipEvent_t evb[2][2] = {};        // per-slot HIP-event pairs (sampled launch timing)
+#ifdef KBHIP_STAMPS
+    bool speculate = false;           // stamps are read per launch: no overlapped launches
+#else
+    bool speculate = true;            // queue the predicted next pop behind the running one
+#endif
     int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
 #ifdef KBHIP_STAMPS
     DevBuf b_stamps;
@@ -227,6 +234,9 @@ struct Session {
         if (comm) (void)ncclCommDestroy(comm);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
+        for (auto& pr : evb)
+            for (auto& e : pr)
+                if (e) (void)hipEventDestroy(e);
         if (h_ctrl) (void)hipHostFree(h_ctrl);
         if (h_out) (void)hipHostFree(h_out);
         if (stream) (void)hipStreamDestroy(stream);
@@ -852,9 +862,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
-        HIPCHK(hipHostMalloc((void**)&S.h_out, sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostMalloc((void**)&S.h_out, 2 * sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
-        std::memset(S.h_out, 0, sizeof(PopOutHost));
+        std::memset(S.h_out, 0, 2 * sizeof(PopOutHost));
 #ifdef KBHIP_STAMPS
         S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 8);
         HIPCHK(set_stamp_buffer(S.d_stamps));
@@ -962,6 +972,143 @@ static void backfill_run(Session& S) {
 }
 
 // ---------------------------------------------------------------------------
+// batched pop launches: one k_pop_batch per job-pop chunk of one class.  Two
+// result slots, so that the predicted next pop can be queued on the stream
+// behind a running one (Allocator::speculate) and its results told apart.
+// ---------------------------------------------------------------------------
+struct BatchLaunch {
+    int slot = 0;
+    uint32_t epoch = 0;
+    int cls = -1, m = 0;
+    bool timed = false;
+};
+
+// Nothing but the winner's row can change between the chunk's tasks: the
+// condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
+static bool batchable(const Session& S, int cls) {
+    const TaskClass& c = S.classes[cls];
+    return S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4 &&
+           S.nc.n < (1 << 25);
+}
+
+static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
+    BatchLaunch L;
+    L.slot = S.next_slot;
+    S.next_slot ^= 1;
+    uint32_t& ep = S.slot_epoch[L.slot];
+    if (((ep + 1) & 0xffff) == 0) {  // tag wrap: clear this (idle) slot's stale granules, skip tag 0
+        std::memset(S.h_out + L.slot, 0, sizeof(PopOutHost));
+        ++ep;
+    }
+    L.epoch = (++ep) & 0xffff;
+    L.cls = cls;
+    L.m = m;
+    L.timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
+    S.sweep_launches++;
+    hipEvent_t* ev = S.evb[L.slot];
+    if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
+    auto tl0 = std::chrono::steady_clock::now();
+    if (L.timed) HIPCHK(hipEventRecord(ev[0], S.stream));
+    HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
+                            S.d_arrive, (char*)S.d_out + L.slot * sizeof(PopOutHost), S.stream, S.placement));
+    if (L.timed) HIPCHK(hipEventRecord(ev[1], S.stream));
+    S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
+    return L;
+}
+
+// Wait for a batched launch's self-tagged result granules (each one 8-byte
+// store on the device) and decode them.
+static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, int* stop_out, int32_t* res_node,
+                            int32_t* res_kind) {
+    const PopOutHost& o = S.h_out[L.slot];
+    auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
+    auto load = [&](int j) { return __atomic_load_n(&o.g[j], __ATOMIC_ACQUIRE); };
+    auto tw0 = std::chrono::steady_clock::now();
+    int got = 0, n_done = -1;
+    for (long spin = 0;; ++spin) {
+        if (n_done < 0) {
+            const uint64_t g0 = load(0);
+            if (tag(g0) == L.epoch) n_done = (int)((g0 >> 36) & 0xff);
+        }
+        if (n_done >= 0) {
+            while (got < n_done && tag(load(got)) == L.epoch) ++got;
+            if (got == n_done) break;
+        }
+        if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(S.stream));  // long waits: runtime
+        if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
+        __builtin_ia32_pause();
+    }
+    if (L.timed) {
+        hipEvent_t* ev = S.evb[L.slot];
+        HIPCHK(hipEventSynchronize(ev[1]));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        S.timed_ms += ms;
+        S.timed_n++;
+    }
+    S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
+    S.stats.sweeps += 1;
+    S.stats.batched_pops += 1;
+    if (n_done < 1 || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+    for (int j = 0; j < n_done; ++j) {
+        const uint64_t g = load(j);
+        res_node[j] = (int32_t)(g & 0xffffffffu) - 1;
+        res_kind[j] = (int32_t)((g >> 34) & 3);
+    }
+    *n_done_out = n_done;
+    *stop_out = (int)((load(0) >> 44) & 0xf) - 1;
+#ifdef KBHIP_STAMPS
+    {
+        int R2;
+        const int nb2 = pop_blocks(S.nc.n, &R2);
+        vector<uint64_t> st((size_t)nb2 * 4 + 8);
+        HIPCHK(hipMemcpy(st.data(), S.d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
+        uint64_t t0 = UINT64_MAX, tbm = 0;
+        double sw = 0, bm = 0;
+        for (int b = 0; b < nb2; ++b) {
+            t0 = std::min(t0, st[b * 4]);
+            tbm = std::max(tbm, st[b * 4 + 2]);
+            sw += (st[b * 4 + 1] - st[b * 4]) * 0.01;
+            bm += (st[b * 4 + 2] - st[b * 4 + 1]) * 0.01;
+        }
+        const uint64_t* P = st.data() + nb2 * 4;
+        S.phase[0] += sw / nb2;                    // per-block sweep + wave sort
+        S.phase[1] += bm / nb2;                    // per-block merge + store
+        S.phase[2] += (tbm - t0) * 0.01;           // first block start -> every block list stored
+        S.phase[3] += ((double)P[4] - (double)tbm) * 0.01;  // -> final merger starts
+        S.phase[4] += (P[0] - P[4]) * 0.01;        // final merge
+        S.phase[5] += (P[1] - P[0]) * 0.01;        // chain precompute
+        S.phase[6] += (P[2] - P[1]) * 0.01;        // placement loop
+        S.phase[7] += (P[3] - P[2]) * 0.01;        // write back
+        S.phase[8] += (P[3] - t0) * 0.01;          // total in-kernel span
+        S.phase[9] += L.m;
+        if (P[5] && P[6] && P[7] && S.placement == 2) {  // parallel-levels sub-phases
+            S.phase[10] += (P[5] - P[1]) * 0.01;   // candidate rows loaded
+            S.phase[11] += (P[6] - P[5]) * 0.01;   // round-0 depth evaluation
+            S.phase[12] += (P[7] - P[6]) * 0.01;   // round-0 sort + merge
+        }
+        S.phase_n++;
+    }
+#endif
+}
+
+// Host mirror of the device commits of consumed tasks (NodeInfo.Used, the
+// fallback node of nodeorder.go:78-93) + the caller's output arrays.
+static void apply_results(Session& S, const int32_t* ids, int n, const int32_t* res_node, const int32_t* res_kind,
+                          int32_t* out_node, uint8_t* out_kind) {
+    for (int i = 0; i < n; ++i) {
+        out_node[i] = res_node[i];
+        out_kind[i] = (uint8_t)res_kind[i];
+        const int node = res_node[i];
+        if (node >= 0) {
+            const HPod& p = S.pods[ids[i]];
+            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // device driver for one job pop
 // ---------------------------------------------------------------------------
 static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
@@ -974,102 +1121,24 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         const int cls0 = S.pods[ids[done]].cls;
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
-        const TaskClass& c = S.classes[cls0];
-        const bool batch = S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4 &&
-                           S.nc.n < (1 << 25);
-        if (!batch) {  // general path: take up to a chunk of mixed classes
-            m = std::min(n - done, kMaxChunk);
-        }
-        // sampled HIP-event timing of the sweep launch (kbhip_set_option "time_every")
-        const bool timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
+        const bool batch = batchable(S, cls0);
+        if (!batch) m = std::min(n - done, kMaxChunk);  // general path: up to a chunk of mixed classes
+        // sampled HIP-event timing of a general-path launch (kbhip_set_option "time_every")
+        const bool timed = !batch && S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
         if (timed && !S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
-        S.sweep_launches++;
+        if (!batch) S.sweep_launches++;
         int n_done, stop_c, ready_c, any_bf_c = S.any_bf;
         const int32_t* res_node;
         const int32_t* res_kind;
         if (batch) {
-            // one launch: sweep + per-block top-64 + merge + sequential placement
-            PopOutHost& o = *S.h_out;
-            if (((S.epoch + 1) & 0xffff) == 0) {  // tag wrap: clear stale granules, skip tag 0
-                std::memset(S.h_out, 0, sizeof(PopOutHost));
-                ++S.epoch;
-            }
-            const uint32_t epoch = (++S.epoch) & 0xffff;
-            if (timed) HIPCHK(hipEventRecord(S.ev0, S.stream));
-            auto tl0 = std::chrono::steady_clock::now();
-            HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls0, m, gang_mode, min_avail, ready_count, epoch,
-                                    S.d_cand2, S.d_arrive, S.d_out, S.stream, S.placement));
-            if (timed) HIPCHK(hipEventRecord(S.ev1, S.stream));
-            auto tl1 = std::chrono::steady_clock::now();
-            // poll the self-tagged result granules (each one 8-byte store on the device)
-            auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
-            auto load = [&](int j) { return __atomic_load_n(&o.g[j], __ATOMIC_ACQUIRE); };
-            int got = 0;
-            n_done = -1;
-            for (long spin = 0;; ++spin) {
-                if (n_done < 0) {
-                    const uint64_t g0 = load(0);
-                    if (tag(g0) == epoch) n_done = (int)((g0 >> 36) & 0xff);
-                }
-                if (n_done >= 0) {
-                    while (got < n_done && tag(load(got)) == epoch) ++got;
-                    if (got == n_done) break;
-                }
-                if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(S.stream));  // long waits: runtime
-                if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
-                __builtin_ia32_pause();
-            }
-            if (timed) HIPCHK(hipEventSynchronize(S.ev1));
-            auto tl2 = std::chrono::steady_clock::now();
-            S.host_launch_s += std::chrono::duration<double>(tl1 - tl0).count();
-            S.host_wait_s += std::chrono::duration<double>(tl2 - tl1).count();
-            S.stats.sweeps += 1;
-            S.stats.batched_pops += 1;
-            if (n_done < 1 || n_done > m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+            // one launch: sweep + per-block top-64 + merge + placement of the chunk
+            const BatchLaunch L = launch_batched(S, cls0, m, gang_mode, min_avail, ready_count);
+            collect_batched(S, L, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf);
             int alloc = 0;
-            for (int j = 0; j < n_done; ++j) {
-                const uint64_t g = load(j);
-                S.res_node_buf[j] = (int32_t)(g & 0xffffffffu) - 1;
-                S.res_kind_buf[j] = (int32_t)((g >> 34) & 3);
-                if (S.res_kind_buf[j] == 1) ++alloc;
-            }
-            stop_c = (int)((load(0) >> 44) & 0xf) - 1;
+            for (int j = 0; j < n_done; ++j) alloc += S.res_kind_buf[j] == 1;
             ready_c = ready_count + alloc;
             res_node = S.res_node_buf;
             res_kind = S.res_kind_buf;
-#ifdef KBHIP_STAMPS
-            {
-                int R2;
-                const int nb2 = pop_blocks(S.nc.n, &R2);
-                vector<uint64_t> st((size_t)nb2 * 4 + 8);
-                HIPCHK(hipMemcpy(st.data(), S.d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
-                uint64_t t0 = UINT64_MAX, tbm = 0;
-                double sw = 0, bm = 0;
-                for (int b = 0; b < nb2; ++b) {
-                    t0 = std::min(t0, st[b * 4]);
-                    tbm = std::max(tbm, st[b * 4 + 2]);
-                    sw += (st[b * 4 + 1] - st[b * 4]) * 0.01;
-                    bm += (st[b * 4 + 2] - st[b * 4 + 1]) * 0.01;
-                }
-                const uint64_t* L = st.data() + nb2 * 4;
-                S.phase[0] += sw / nb2;                    // per-block sweep + wave sort
-                S.phase[1] += bm / nb2;                    // per-block merge + store
-                S.phase[2] += (tbm - t0) * 0.01;           // first block start -> every block list stored
-                S.phase[3] += ((double)L[4] - (double)tbm) * 0.01;  // -> final merger starts
-                S.phase[4] += (L[0] - L[4]) * 0.01;        // final merge
-                S.phase[5] += (L[1] - L[0]) * 0.01;        // chain precompute
-                S.phase[6] += (L[2] - L[1]) * 0.01;        // placement loop
-                S.phase[7] += (L[3] - L[2]) * 0.01;        // write back
-                S.phase[8] += (L[3] - t0) * 0.01;          // total in-kernel span
-                S.phase[9] += m;
-                if (L[5] && L[6] && L[7] && S.placement == 2) {  // parallel-levels sub-phases
-                    S.phase[10] += (L[5] - L[1]) * 0.01;   // candidate rows loaded
-                    S.phase[11] += (L[6] - L[5]) * 0.01;   // round-0 depth evaluation
-                    S.phase[12] += (L[7] - L[6]) * 0.01;   // round-0 sort + merge
-                }
-                S.phase_n++;
-            }
-#endif
         } else {
             PopCtrl& h = *S.h_ctrl;
             h.stop = -1;
@@ -1116,16 +1185,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             S.timed_n++;
         }
         if (stop_c < 0 || n_done < 1 || n_done > m) throw Error(KBHIP_EDEVICE, "device pop did not complete");
-        for (int i = 0; i < n_done; ++i) {
-            out_node[done + i] = res_node[i];
-            out_kind[done + i] = (uint8_t)res_kind[i];
-            const int node = res_node[i];
-            if (node >= 0) {
-                HPod& p = S.pods[ids[done + i]];
-                S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
-                if (S.fallback < 0 || node < S.fallback) S.fallback = node;
-            }
-        }
+        apply_results(S, ids + done, n_done, res_node, res_kind, out_node + done, out_kind + done);
         S.any_bf = any_bf_c;
         ready_count = ready_c;
         done += n_done;
@@ -1166,6 +1226,18 @@ struct GoHeap {  // container/heap over util.PriorityQueue (util/priority_queue.
         }
     }
     void push(int x) { items.push_back(x); up((int)items.size() - 1); }
+    // The element pop() would return right after push(x), without changing
+    // the heap: x only if up() would carry it to the root.
+    int peek_push(int x) const {
+        int j = (int)items.size();
+        while (j > 0) {
+            const int i = (j - 1) / 2;
+            if (!less(x, items[i])) break;
+            j = i;
+        }
+        return j == 0 ? x : items[0];
+    }
+    int top() const { return items[0]; }
     int pop() {
         int n = (int)items.size() - 1;
         std::swap(items[0], items[n]);
@@ -1313,6 +1385,149 @@ struct Allocator {
         }
         vector<int32_t> ids, onode;
         vector<uint8_t> okind;
+        const int gm = S.gang_ready ? 1 : 0;
+        auto build_pending = [&](HJob& job) {  // allocate.go:91-104; TaskOrderFn is a strict total order
+            if (job.pending_built) return;
+            for (int t : job.tasks) {
+                const HPod& p = S.pods[t];
+                if (p.status != Pending) continue;
+                if (p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU) continue;  // BestEffort
+                job.pending.push_back(t);
+            }
+            std::sort(job.pending.begin(), job.pending.end(), [this](int a, int b) { return task_less(a, b); });
+            job.pending_built = true;
+        };
+
+        // Speculation: while a batched pop runs, the host
+        // predicts the next pop — assuming this one places its tasks as
+        // Allocated up to the gang stop — with read-only peeks at the Go heaps,
+        // and queues that pop's launch behind it on the stream.  The next real
+        // pop uses the queued launch only if it is exactly the predicted one
+        // (job, first task, ready count, class, chunk), in which case the
+        // launch ran on exactly the device state the real pop sees; otherwise
+        // the launch is retracted (k_undo_pop) before anything else runs.
+        struct Spec {
+            bool on = false;
+            BatchLaunch L;
+            int jb = -1;
+            size_t cursor = 0;
+            int ready = 0;
+        } spec;
+        auto discard = [&]() {
+            int nd = 0, st = 0;
+            int32_t node[kMaxChunk], kind[kMaxChunk];
+            collect_batched(S, spec.L, &nd, &st, node, kind);
+            HIPCHK(launch_undo_pop(S.nc, S.tab, spec.L.cls, nd, node, kind, S.stream));
+            spec.on = false;
+            S.stats.spec_missed++;
+        };
+        // The pop after the current one (queue q, job jb, whose first chunk of m
+        // of its n remaining tasks is running).
+        auto speculate = [&](int q, int jb, int m, int n) {
+            HJob& job = S.jobs[jb];
+            int k, pstop;
+            if (S.gang_ready) {  // gang.go:63-66: stop once #AllocatedStatuses >= MinAvailable
+                const int need = job.min_avail - job.cnt_alloc;
+                k = need <= 1 ? 1 : need;
+                if (k <= m) pstop = KBHIP_STOP_READY;
+                else if (m == n) { k = m; pstop = KBHIP_STOP_ALL; }
+                else return;  // the pop continues past this chunk
+            } else {
+                k = 1;  // no JobReadyFn: always ready, one task per pop
+                pstop = KBHIP_STOP_READY;
+            }
+            HQueue& Q = S.queues[q];
+            const int sv_cnt = job.cnt_alloc;
+            const size_t sv_cur = job.cursor;
+            const F3 sv_drf = job.drf_alloc, sv_qa = Q.allocated;
+            const double sv_share = job.drf_share, sv_qs = Q.share;
+            job.cnt_alloc += k;  // the predicted outcome, undone below
+            job.cursor += k;
+            for (int i = 0; i < k; ++i) {
+                const HPod& p = S.pods[job.pending[sv_cur + i]];
+                if (S.drf_on) job.drf_alloc.add(p.req);
+                if (S.prop_on) Q.allocated.add(p.req);
+            }
+            if (S.drf_on) drf_update(job);
+            if (S.prop_on) prop_update(Q);
+            int jb2 = -1, ready2 = 0, cls2 = -1, m2 = 0;
+            size_t cur2 = 0;
+            do {  // the loop below: jobs.Push(job) on READY, queues.Push(queue), queues.Pop(), ...
+                const int q2 = queues.peek_push(q);
+                if (overused(q2)) break;
+                auto jit2 = jobs_map.find(q2);
+                if (jit2 == jobs_map.end()) break;
+                if (q2 == q && pstop == KBHIP_STOP_READY) jb2 = jit2->second.peek_push(jb);
+                else if (!jit2->second.empty()) jb2 = jit2->second.top();
+                if (jb2 < 0) break;
+                HJob& j2 = S.jobs[jb2];
+                build_pending(j2);
+                cur2 = j2.cursor;
+                if (cur2 >= j2.pending.size()) { jb2 = -1; break; }  // an empty pop next
+                cls2 = S.pods[j2.pending[cur2]].cls;
+                const size_t rem = j2.pending.size() - cur2;
+                while ((size_t)m2 < rem && m2 < kMaxChunk && S.pods[j2.pending[cur2 + m2]].cls == cls2) ++m2;
+                ready2 = j2.cnt_alloc;
+                if (!batchable(S, cls2)) jb2 = -1;
+            } while (false);
+            job.cnt_alloc = sv_cnt;
+            job.cursor = sv_cur;
+            job.drf_alloc = sv_drf;
+            job.drf_share = sv_share;
+            Q.allocated = sv_qa;
+            Q.share = sv_qs;
+            if (jb2 < 0) return;
+            spec.L = launch_batched(S, cls2, m2, gm, S.jobs[jb2].min_avail, ready2);
+            spec.on = true;
+            spec.jb = jb2;
+            spec.cursor = cur2;
+            spec.ready = ready2;
+        };
+        // One job pop through the device: the first chunk batched (possibly
+        // already queued by speculation), the rest through place_job.
+        auto exec_pop = [&](int q, int jb, int n, int32_t* n_done, int32_t* stop) {
+            HJob& job = S.jobs[jb];
+            const int cls0 = S.pods[ids[0]].cls;
+            int m = 1;
+            while (m < n && m < kMaxChunk && S.pods[ids[m]].cls == cls0) ++m;
+            const bool batch = batchable(S, cls0);
+            bool have = false;
+            BatchLaunch L;
+            if (spec.on) {
+                if (batch && spec.jb == jb && spec.cursor == job.cursor && spec.ready == job.cnt_alloc &&
+                    spec.L.cls == cls0 && spec.L.m == m) {
+                    L = spec.L;
+                    have = true;
+                    spec.on = false;
+                    S.stats.spec_hits++;
+                } else {
+                    discard();
+                }
+            }
+            if (!batch) {
+                place_job(S, ids.data(), n, gm, job.min_avail, job.cnt_alloc, onode.data(), okind.data(), n_done, stop);
+                return;
+            }
+            if (!have) L = launch_batched(S, cls0, m, gm, job.min_avail, job.cnt_alloc);
+            if (S.speculate) speculate(q, jb, m, n);
+            int nd = 0, st = 0;
+            collect_batched(S, L, &nd, &st, S.res_node_buf, S.res_kind_buf);
+            if (st < 0) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+            int alloc = 0;
+            for (int j = 0; j < nd; ++j) alloc += S.res_kind_buf[j] == 1;
+            apply_results(S, ids.data(), nd, S.res_node_buf, S.res_kind_buf, onode.data(), okind.data());
+            if (st == KBHIP_STOP_ALL && nd < n) {  // more chunks: the prediction assumed the pop ended here
+                if (spec.on) discard();
+                int32_t nd2 = 0, st2 = 0;
+                place_job(S, ids.data() + nd, n - nd, gm, job.min_avail, job.cnt_alloc + alloc, onode.data() + nd,
+                          okind.data() + nd, &nd2, &st2);
+                nd += nd2;
+                st = st2;
+            }
+            *n_done = nd;
+            *stop = st;
+        };
+
         while (!queues.empty()) {
             int q = queues.pop();
             if (overused(q)) continue;
@@ -1321,24 +1536,14 @@ struct Allocator {
             int jb = jit->second.pop();
             HJob& job = S.jobs[jb];
             S.stats.pops++;
-            if (!job.pending_built) {  // allocate.go:91-104; TaskOrderFn is a strict total order
-                for (int t : job.tasks) {
-                    const HPod& p = S.pods[t];
-                    if (p.status != Pending) continue;
-                    if (p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU) continue;  // BestEffort
-                    job.pending.push_back(t);
-                }
-                std::sort(job.pending.begin(), job.pending.end(), [this](int a, int b) { return task_less(a, b); });
-                job.pending_built = true;
-            }
+            build_pending(job);
             if (job.cursor < job.pending.size()) {
                 int n = (int)(job.pending.size() - job.cursor);
                 ids.assign(job.pending.begin() + job.cursor, job.pending.end());
                 onode.assign(n, -1);
                 okind.assign(n, 0);
                 int32_t n_done = 0, stop = 0;
-                place_job(S, ids.data(), n, S.gang_ready ? 1 : 0, job.min_avail, job.cnt_alloc, onode.data(),
-                          okind.data(), &n_done, &stop);
+                exec_pop(q, jb, n, &n_done, &stop);
                 S.stats.tasks += n_done;
                 for (int i = 0; i < n_done; ++i) {
                     const int pi = ids[i];
@@ -1358,6 +1563,7 @@ struct Allocator {
             }
             queues.push(q);
         }
+        if (spec.on) discard();  // predicted a pop that never came
         HIPCHK(hipStreamSynchronize(S.stream));
         S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -1527,6 +1733,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else if (std::strcmp(key, "speculate") == 0) s->s.speculate = value != 0;
         else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
             kbhip::Session& S = s->s;
             S.debug_keys = value != 0;

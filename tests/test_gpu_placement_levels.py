@@ -118,3 +118,49 @@ def test_placement_levels_model():
             seqs.append(s)
         g = _greedy(seqs, idx, m)
         assert g == _levels(seqs, idx, m)[:len(g)]
+
+
+# ---- speculation: the predicted next pop queued behind the running one -----
+def _log_spec(engine, path, speculate):
+    with engine.Session(path) as s:
+        s.set_option("speculate", speculate)
+        pod, node, kind = s.allocate()
+        st = s.stats()
+    return [(int(p), int(n), int(k)) for p, n, k in zip(pod, node, kind)], st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(16))
+def test_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Placements with speculation equal the oracle's; mispredictions (failed
+    pops, pipelined tasks, non-batchable pops next) are retracted exactly."""
+    tiers = [None, [["drf", "proportion"]], [["gang"], ["predicates", "nodeorder"]],
+             [["priority", "gang", "drf"], ["predicates", "proportion", "nodeorder"]]][seed % 4]
+    c = kbgen_mod.gen_random(4500 + seed, n_nodes=3 + seed % 10, n_jobs=6 + seed % 9, max_tasks=2 + seed % 9,
+                             features=NO_POD_AFFINITY, tiers=tiers)
+    p = str(tmp_path / "s.kbs")
+    c.write(p)
+    got, st = _log_spec(engine, p, 1)
+    exp = _oracle_log(oracle_mod, p)
+    assert [(a, b, 4 if k == 1 else 8) for a, b, k in got] == exp
+
+
+@pytest.mark.gpu
+def test_speculation_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c2.kbs")
+    kbgen_mod.gen_c2(p)
+    a, sa = _log_spec(engine, p, 1)
+    b, sb = _log_spec(engine, p, 0)
+    assert a == b
+    assert [(x, y, 4 if k == 1 else 8) for x, y, k in a] == _oracle_log(oracle_mod, p, fast=True)
+    assert sa["spec_hits"] > 0 and sb["spec_hits"] == 0 and sb["spec_missed"] == 0
+
+
+@pytest.mark.gpu
+def test_speculation_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c4s.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
+    a, sa = _log_spec(engine, p, 1)
+    b, _ = _log_spec(engine, p, 0)
+    assert a == b
+    assert sa["spec_hits"] > sa["spec_missed"]
