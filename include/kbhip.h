@@ -130,6 +130,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "placement" = 2 (default) places a batched chunk by parallel levels, 8
  * depths per step; 1 by running-min levels, one depth per step; 0 by the
  * sequential loop over precomputed chains;
+ * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
+ * when the class's score range and the node count fit (same order as the
+ * 64-bit key), 0 = always 64-bit;
  * "speculate" = 1 (default) lets kbhip_allocate queue the predicted next job
  * pop behind the running one (used only if it is exactly the next pop,
  * retracted on device otherwise; placements are unchanged), 0 = one pop at

@@ -33,11 +33,17 @@ hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* c
 // nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi.
 hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st);
 
+// Selection-key format of a batched launch: 32-bit keys when the class's
+// score range and the node count fit (kbhip_kernels.hip, PopArgs).
+struct KeyFormat {
+    bool use32 = false;
+    int32_t base = 0, shift = 0, idxmax = 0;
+};
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement = 0);
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf);
 // Inverse node updates of a batched pop's placements (a retracted prediction).
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

@@ -102,10 +102,21 @@ template <int J>
 __device__ __forceinline__ uint64_t xor_lane64(uint64_t v) {
     return ((uint64_t)xor_lane32<J>((uint32_t)(v >> 32)) << 32) | xor_lane32<J>((uint32_t)v);
 }
-__device__ __forceinline__ uint64_t reverse_lanes64(uint64_t v) {  // lane i <- lane 63 - i (= i ^ 63)
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x140, 0xf, 0xf, false);  // row_mirror
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x140, 0xf, 0xf, false);
-    return xor_lane64<32>(xor_lane64<16>(((uint64_t)hi << 32) | lo));
+template <int J, typename T>
+__device__ __forceinline__ T xor_lane(T v) {
+    if constexpr (sizeof(T) == 8) return xor_lane64<J>(v);
+    else return xor_lane32<J>(v);
+}
+template <typename T>
+__device__ __forceinline__ T reverse_lanes(T v) {  // lane i <- lane 63 - i (= i ^ 63)
+    if constexpr (sizeof(T) == 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x140, 0xf, 0xf, false);  // row_mirror
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x140, 0xf, 0xf, false);
+        return xor_lane64<32>(xor_lane64<16>(((uint64_t)hi << 32) | lo));
+    } else {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);
+        return xor_lane32<32>(xor_lane32<16>(m));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -252,17 +263,17 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
 // ---------------------------------------------------------------------------
 // batched path v2: one launch per pop chunk
 // ---------------------------------------------------------------------------
-// Wave-level sorting on registers: lane i holds one u64; descending order.
-// Bitonic network, every exchange a DPP / permlane op (xor_lane64).
-template <int K, int J>
-__device__ __forceinline__ uint64_t bitonic_step(uint64_t v) {
+// Wave-level sorting on registers: lane i holds one key (u32 or u64);
+// descending order.  Bitonic network, every exchange a DPP / permlane op.
+template <int K, int J, typename T>
+__device__ __forceinline__ T bitonic_step(T v) {
     const int lane = threadIdx.x & 63;
-    const uint64_t o = xor_lane64<J>(v);
+    const T o = xor_lane<J>(v);
     const bool keep_max = ((lane & J) == 0) == ((lane & K) == 0);
     return keep_max ? (o > v ? o : v) : (o < v ? o : v);
 }
-template <int K>
-__device__ __forceinline__ uint64_t bitonic_stage(uint64_t v) {
+template <int K, typename T>
+__device__ __forceinline__ T bitonic_stage(T v) {
     if constexpr (K >= 64) v = bitonic_step<K, 32>(v);
     if constexpr (K >= 32) v = bitonic_step<K, 16>(v);
     if constexpr (K >= 16) v = bitonic_step<K, 8>(v);
@@ -270,7 +281,8 @@ __device__ __forceinline__ uint64_t bitonic_stage(uint64_t v) {
     if constexpr (K >= 4) v = bitonic_step<K, 2>(v);
     return bitonic_step<K, 1>(v);
 }
-__device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
+template <typename T>
+__device__ __forceinline__ T wave_sort_desc(T v) {
     v = bitonic_stage<2>(v);
     v = bitonic_stage<4>(v);
     v = bitonic_stage<8>(v);
@@ -279,15 +291,16 @@ __device__ __forceinline__ uint64_t wave_sort_desc(uint64_t v) {
     return bitonic_stage<64>(v);
 }
 // Top-64 of two descending lists (lane i holds a[i], b[i]); result descending.
-template <int J>
-__device__ __forceinline__ uint64_t half_clean_desc(uint64_t v) {
+template <int J, typename T>
+__device__ __forceinline__ T half_clean_desc(T v) {
     const int lane = threadIdx.x & 63;
-    const uint64_t o = xor_lane64<J>(v);
+    const T o = xor_lane<J>(v);
     return ((lane & J) == 0) ? (o > v ? o : v) : (o < v ? o : v);
 }
-__device__ __forceinline__ uint64_t wave_merge_desc(uint64_t a, uint64_t b) {
-    const uint64_t br = reverse_lanes64(b);
-    uint64_t v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
+template <typename T>
+__device__ __forceinline__ T wave_merge_desc(T a, T b) {
+    const T br = reverse_lanes(b);
+    T v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
     v = half_clean_desc<32>(v);
     v = half_clean_desc<16>(v);
     v = half_clean_desc<8>(v);
@@ -311,7 +324,33 @@ struct PopArgs {
     int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
     uint32_t epoch;
     int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels, 2: parallel levels
+    // 32-bit selection keys (when the class's score range and the node count
+    // fit): key = (score - kbase + 1) << kshift | (kidxmax - idx) << 1 | pipelined,
+    // ordered exactly as pack_key; halves the sort / merge network work.
+    int32_t kbase, kshift, kidxmax;
 };
+
+// Selection key of the batched sweep in type T (see PopArgs).
+template <typename T>
+__device__ __forceinline__ T sweep_key(uint64_t k64, const PopArgs& a) {
+    if constexpr (sizeof(T) == 8) {
+        return k64;
+    } else {
+        if (!k64) return 0;
+        return ((uint32_t)(key_score(k64) - a.kbase + 1) << a.kshift) |
+               ((uint32_t)(a.kidxmax - key_idx(k64)) << 1) | (uint32_t)(k64 & 1);
+    }
+}
+template <typename T>
+__device__ __forceinline__ uint64_t key64_of(T k, const PopArgs& a) {
+    if constexpr (sizeof(T) == 8) {
+        return k;
+    } else {
+        if (!k) return 0;
+        return pack_key((int32_t)(k >> a.kshift) - 1 + a.kbase, a.kidxmax - (int32_t)((k >> 1) & (uint32_t)a.kidxmax),
+                        (int32_t)(k & 1));
+    }
+}
 
 constexpr int kPopThreads = 512;  // 8 waves
 constexpr int kDepth = 3;         // post-commit keys precomputed per candidate
@@ -373,10 +412,12 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 // Hand-off of 64-key lists between workgroups: write-through (sc1) 8-byte
 // stores drained before an agent-scope counter add, sc1 loads on the consumer
 // after its add returned (MI355X_MICROARCH.md, valid forms, table row 1).
-__device__ __forceinline__ void put_list(uint64_t* dst, uint64_t v) {
+template <typename T>
+__device__ __forceinline__ void put_list(T* dst, T v) {
     __hip_atomic_store(dst + (threadIdx.x & 63), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ uint64_t get_list(const uint64_t* src) {
+template <typename T>
+__device__ __forceinline__ T get_list(const T* src) {
     return __hip_atomic_load(src + (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -384,7 +425,8 @@ constexpr int kGroups = 8;        // second-level merge groups (blockIdx % 8)
 constexpr int kCtrStride = 32;    // one counter per 128-byte line
 
 // Tree merge of the 8 per-wave lists in wl[] into wl[0] (all waves call).
-__device__ __forceinline__ void block_tree_merge(uint64_t (*wl)[64], int wave, int lane) {
+template <typename T>
+__device__ __forceinline__ void block_tree_merge(T (*wl)[64], int wave, int lane) {
 #pragma unroll
     for (int s = kPopThreads / 128; s >= 1; s >>= 1) {
         if (wave < s) wl[wave][lane] = wave_merge_desc(wl[wave][lane], wl[wave + s][lane]);
@@ -627,39 +669,44 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     STAMP(gridDim.x * 4 + 3);
 }
 
-template <int R>
+template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                           uint64_t* cand, uint32_t* arrive, PopOut* out) {
-    __shared__ uint64_t wl[kPopThreads / 64][64];
+                                                           uint64_t* cand64, uint32_t* arrive, PopOut* out) {
+    __shared__ KT wlk[kPopThreads / 64][64];  // sweep / merge lists in the key type
+    __shared__ uint64_t wl64[sizeof(KT) == 8 ? 1 : kPopThreads / 64][64];
+    uint64_t (*wl)[64] = nullptr;             // placement lists (64-bit keys / entries)
+    if constexpr (sizeof(KT) == 8) wl = (uint64_t (*)[64])wlk;
+    else wl = wl64;
+    KT* cand = (KT*)cand64;
     __shared__ int role;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
     // 1. evaluate R nodes per lane, wave top-64, block top-64
-    uint64_t best = 0;
+    KT best = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
-        uint64_t k = 0;
+        KT k = 0;
         if (n < nc.n) {
             int32_t s;
             bool passed;
-            k = eval_node(cf, c, t, nc, n, &s, &passed);
+            k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed), a);
         }
         k = wave_sort_desc(k);
         best = r == 0 ? k : wave_merge_desc(best, k);
     }
-    wl[wave][lane] = best;
+    wlk[wave][lane] = best;
     __syncthreads();
     STAMP(blockIdx.x * 4 + 1);
-    block_tree_merge(wl, wave, lane);
+    block_tree_merge(wlk, wave, lane);
     const int nb = gridDim.x;
     const int g = blockIdx.x % kGroups;
     const int g_count = (nb - g + kGroups - 1) / kGroups;   // blocks in my group
     const int n_groups = nb < kGroups ? nb : kGroups;
-    uint64_t* gcand = cand + (int64_t)nb * 64;               // group lists after the block lists
+    KT* gcand = cand + (int64_t)nb * 64;                     // group lists after the block lists
     if (wave == 0) {
-        put_list(cand + (int64_t)blockIdx.x * 64, wl[0][lane]);
+        put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
@@ -670,23 +717,23 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     // 2a. last block of group g: merge the group's block lists (strided over
     // waves; each wave issues its lists' loads together, then merges)
     {
-        uint64_t acc = 0;
+        KT acc = 0;
         constexpr int kPf = 4;
         for (int i0 = wave; i0 < g_count; i0 += kPf * (kPopThreads / 64)) {
-            uint64_t v[kPf];
+            KT v[kPf];
 #pragma unroll
             for (int q = 0; q < kPf; ++q) {
                 const int i = i0 + q * (kPopThreads / 64);
-                v[q] = i < g_count ? get_list(cand + (int64_t)(g + i * kGroups) * 64) : 0;
+                v[q] = i < g_count ? get_list(cand + (int64_t)(g + i * kGroups) * 64) : (KT)0;
             }
 #pragma unroll
             for (int q = 0; q < kPf; ++q) acc = wave_merge_desc(acc, v[q]);
         }
-        wl[wave][lane] = acc;
+        wlk[wave][lane] = acc;
         __syncthreads();
-        block_tree_merge(wl, wave, lane);
+        block_tree_merge(wlk, wave, lane);
         if (wave == 0) {
-            put_list(gcand + (int64_t)g * 64, wl[0][lane]);
+            put_list(gcand + (int64_t)g * 64, wlk[0][lane]);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
@@ -696,10 +743,16 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     STAMP(gridDim.x * 4 + 4);
     // 2b. last group merger: merge the group lists; reset the counters for the next launch
-    wl[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : 0;
+    wlk[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : (KT)0;
     __syncthreads();
-    block_tree_merge(wl, wave, lane);
+    block_tree_merge(wlk, wave, lane);
     STAMP(gridDim.x * 4 + 0);
+    if constexpr (sizeof(KT) != 8) {  // placement works on 64-bit keys
+        const uint64_t k64 = key64_of(wlk[0][lane], a);
+        __syncthreads();
+        if (wave == 0) wl[0][lane] = k64;
+        __syncthreads();
+    }
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (a.placement == 1) {  // uniform
@@ -896,20 +949,27 @@ int pop_blocks(int n_nodes, int* R_out) {
     return (n_nodes + kPopThreads * R - 1) / (kPopThreads * R);
 }
 
+template <typename KT>
+static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
+                               uint64_t* cand, uint32_t* arrive, PopOut* o, hipStream_t st) {
+    switch (R) {
+        case 1: hipLaunchKernelGGL((k_pop_batch<1, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 2: hipLaunchKernelGGL((k_pop_batch<2, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 4: hipLaunchKernelGGL((k_pop_batch<4, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 8: hipLaunchKernelGGL((k_pop_batch<8, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        default: hipLaunchKernelGGL((k_pop_batch<16, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+    }
+}
+
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement) {
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf) {
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement};
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax};
     PopOut* o = (PopOut*)out_dev;
-    switch (R) {
-        case 1: hipLaunchKernelGGL(k_pop_batch<1>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 2: hipLaunchKernelGGL(k_pop_batch<2>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 4: hipLaunchKernelGGL(k_pop_batch<4>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 8: hipLaunchKernelGGL(k_pop_batch<8>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        default: hipLaunchKernelGGL(k_pop_batch<16>, dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-    }
+    if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
+    else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
     return hipGetLastError();
 }
 

@@ -178,6 +178,8 @@ struct Session {
     NodeCols nc{};
     DevTables tab{};
     vector<TaskClass> classes;
+    vector<KeyFormat> class_kf;  // batched-path selection-key format per class
+    bool keys32 = true;          // option "keys32": 32-bit keys where they fit
     DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
         b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
     PopCtrl* d_ctrl = nullptr;
@@ -839,6 +841,38 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     vector<int64_t> valint(E.vals.strs.size() + 1, 0);
     vector<uint8_t> valok(E.vals.strs.size() + 1, 0);
     for (size_t v = 0; v < E.vals.strs.size(); ++v) valok[v] = parse_int64(E.vals.strs[v], &valint[v]);
+    // 32-bit selection keys per class (PopArgs, kbhip_kernels.hip): the score
+    // of a batched-path class is mult x (w_lr lr + w_bra bra + w_na na) with
+    // lr, bra in [0, 10] and na between the sums of its negative / positive
+    // preferred-term weights; it fits when (range + 1) < 2^(31 - index bits).
+    {
+        int ibits = 1;
+        while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)nl) ++ibits;
+        S.class_kf.assign(S.classes.size(), KeyFormat{});
+        for (size_t ci = 0; ci < S.classes.size(); ++ci) {
+            const TaskClass& c = S.classes[ci];
+            int64_t na_lo = 0, na_hi = 0;
+            for (int i = 0; i < c.pref_term_n; ++i) {
+                const int64_t w = E.terms[c.pref_term_off + i].weight;
+                (w < 0 ? na_lo : na_hi) += w;
+            }
+            const int64_t mult = S.conf.score_mult;
+            auto rng = [](int64_t a, int64_t b, int64_t* lo, int64_t* hi) {
+                *lo += std::min(a, b);
+                *hi += std::max(a, b);
+            };
+            int64_t lo = 0, hi = 0;
+            rng(0, 10 * (int64_t)S.conf.w_lr, &lo, &hi);
+            rng(0, 10 * (int64_t)S.conf.w_bra, &lo, &hi);
+            rng(na_lo * S.conf.w_na, na_hi * S.conf.w_na, &lo, &hi);
+            const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
+            KeyFormat& kf = S.class_kf[ci];
+            kf.use32 = ibits <= 25 && shi - slo + 1 < ((int64_t)1 << (31 - ibits)) && slo >= INT32_MIN && shi <= INT32_MAX;
+            kf.base = (int32_t)slo;
+            kf.shift = ibits + 1;
+            kf.idxmax = (int32_t)(((int64_t)1 << ibits) - 1);
+        }
+    }
     S.tab.classes = upload(S, S.b_classes, S.classes);
     S.tab.terms = upload(S, S.b_terms, E.terms);
     S.tab.reqs = upload(S, S.b_reqs, E.reqs);
@@ -1010,7 +1044,8 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], S.stream));
     HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                            S.d_arrive, (char*)S.d_out + L.slot * sizeof(PopOutHost), S.stream, S.placement));
+                            S.d_arrive, (char*)S.d_out + L.slot * sizeof(PopOutHost), S.stream, S.placement,
+                            S.keys32 ? S.class_kf[cls] : KeyFormat{}));
     if (L.timed) HIPCHK(hipEventRecord(ev[1], S.stream));
     S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
     return L;
@@ -1734,6 +1769,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
         else if (std::strcmp(key, "speculate") == 0) s->s.speculate = value != 0;
+        else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
         else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
             kbhip::Session& S = s->s;
             S.debug_keys = value != 0;

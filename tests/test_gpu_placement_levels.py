@@ -164,3 +164,37 @@ def test_speculation_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     b, _ = _log_spec(engine, p, 0)
     assert a == b
     assert sa["spec_hits"] > sa["spec_missed"]
+
+
+# ---- 32-bit selection keys in the batched sweep ------------------------------
+def _log_opt(engine, path, **opts):
+    with engine.Session(path) as s:
+        for k, v in opts.items():
+            s.set_option(k, v)
+        pod, node, kind = s.allocate()
+    return [(int(p), int(n), 4 if k == 1 else 8) for p, n, k in zip(pod, node, kind)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(12))
+def test_keys32_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Small and huge nodeorder weights: 32-bit keys where the score range fits,
+    the 64-bit fallback where it does not; both equal the oracle."""
+    c = kbgen_mod.gen_random(4700 + seed, n_nodes=4 + seed % 12, n_jobs=5 + seed % 8, max_tasks=2 + seed % 9,
+                             features=NO_POD_AFFINITY)
+    if seed % 3 == 1:
+        c.args = {"nodeorder": {"leastrequested.weight": "100000000", "balancedresource.weight": "-3"}}
+    elif seed % 3 == 2:
+        c.args = {"nodeorder": {"nodeaffinity.weight": "-7", "balancedresource.weight": "5"}}
+    p = str(tmp_path / "k.kbs")
+    c.write(p)
+    exp = _oracle_log(oracle_mod, p)
+    assert _log_opt(engine, p, keys32=1) == exp
+    assert _log_opt(engine, p, keys32=0) == exp
+
+
+@pytest.mark.gpu
+def test_keys32_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c4k.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
+    assert _log_opt(engine, p, keys32=1) == _log_opt(engine, p, keys32=0)
