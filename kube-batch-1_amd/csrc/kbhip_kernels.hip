@@ -520,17 +520,19 @@ __device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables
 // merge of the round's 512 entries.  Commit kinds along a chain are
 // Allocate^a Pipeline^p (once Idle + Backfilled cannot fit, later commits
 // only touch Releasing), so a first pass assumes Allocate everywhere and the
-// depths behind a lane's first Pipeline are recomputed.  The entry carries the
-// candidate's lane instead of its depth: entries of one node are
-// interchangeable for the counts, and a position's commit kind is looked up
-// by its rank among its node's entries.  Another round runs only while some
-// candidate's deepest entry still reaches the m-th entry.
+// depths behind a lane's first Pipeline are recomputed.  An entry is
+// (running min, index, depth) — a position's depth is the number of commits
+// its node already took — and a small LDS hash from node index to candidate
+// lane finds the candidate's commit kinds and counts.  Another round runs
+// only while some candidate's deepest entry still reaches the m-th entry.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t lane_entry(int32_t rm, int n, int lane) {
+__device__ __forceinline__ uint64_t depth_entry(int32_t rm, int n, int d) {
     return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
-           ((uint64_t)lane << 1) | 1ull;
+           ((uint64_t)(63 - d) << 1) | 1ull;
 }
-__device__ __forceinline__ int entry_lane(uint64_t e) { return (int)((e >> 1) & 63); }
+__device__ __forceinline__ int entry_depth(uint64_t e) { return 63 - (int)((e >> 1) & 63); }
+constexpr int kHash = 256;  // node index -> candidate lane (64 keys, open addressing)
+__device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 24); }
 
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl)[64]) {
@@ -541,6 +543,8 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     __shared__ int32_t s_apos[64];        // first Pipeline depth (64: none yet)
     __shared__ uint64_t s_last[64];       // entry at the round's deepest depth
     __shared__ int32_t s_cnt[64];
+    __shared__ int32_t s_hkey[kHash];
+    __shared__ int32_t s_hlane[kHash];
     __shared__ int s_more;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t K = wl[0][lane];
@@ -558,7 +562,13 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
+    if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
     __syncthreads();  // K read by every wave; wl free
+    if (wave == 0 && n >= 0) {  // candidate nodes are distinct
+        int h = hash_slot(n);
+        while (atomicCAS(&s_hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+        s_hlane[h] = lane;
+    }
     STAMP(gridDim.x * 4 + 5);
     auto eval_at = [&](int d, int ap, int32_t* sc) -> int {  // kind of commit d+1's key (0: infeasible)
         if (d == 0) { *sc = key_score(K); return key_kind(K); }
@@ -597,7 +607,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             const int32_t x = s_sc[w2][lane];
             rm = x < rm ? x : rm;
         }
-        const uint64_t e = ok ? lane_entry(rm, n, lane) : 0;
+        const uint64_t e = ok ? depth_entry(rm, n, d) : 0;
         __syncthreads();  // s_rm reads done
         if (r == 0) STAMP(gridDim.x * 4 + 6);
         if (wave == kW - 1) { s_last[lane] = e; s_rm[lane] = rm; }
@@ -621,18 +631,16 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     }
     if (wave != 0) return;
     STAMP(gridDim.x * 4 + 2);
-    // commit kind of each position: rank among the entries of its node
+    // commit kind of each position: its node's candidate lane, the entry's depth
     const bool inm = lane < m && L != 0;
-    const int lf = entry_lane(L);
-    int rank = 0;
-    for (uint64_t rem = __ballot(inm); rem;) {
-        const int p0 = __ffsll((unsigned long long)rem) - 1;
-        const int l0 = __builtin_amdgcn_readlane(lf, p0);
-        const uint64_t mm = __ballot(inm && lf == l0);
-        if (inm && lf == l0) rank = __popcll(mm & ((1ull << lane) - 1));
-        rem &= ~mm;
+    int lf = 0;
+    if (inm) {
+        const int ni = entry_idx(L);
+        int h = hash_slot(ni);
+        while (s_hkey[h] != ni) h = (h + 1) & (kHash - 1);
+        lf = s_hlane[h];
     }
-    const int kind = inm ? s_kind[rank][lf] : 0;
+    const int kind = inm ? s_kind[entry_depth(L)][lf] : 0;
     // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
     const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
@@ -647,10 +655,12 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         done = m;
         stop = 0;
     }
+    STAMP(gridDim.x * 4 + 8);
     if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
     __builtin_amdgcn_wave_barrier();
     const int cc = s_cnt[lane];
+    STAMP(gridDim.x * 4 + 9);
     if (n >= 0 && cc > 0) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
         const int ap = s_apos[lane];
         const int na = cc < ap ? cc : ap;

@@ -900,7 +900,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
         std::memset(S.h_out, 0, 2 * sizeof(PopOutHost));
 #ifdef KBHIP_STAMPS
-        S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 8);
+        S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 16);
         HIPCHK(set_stamp_buffer(S.d_stamps));
 #endif
     }
@@ -1096,7 +1096,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     {
         int R2;
         const int nb2 = pop_blocks(S.nc.n, &R2);
-        vector<uint64_t> st((size_t)nb2 * 4 + 8);
+        vector<uint64_t> st((size_t)nb2 * 4 + 16);
         HIPCHK(hipMemcpy(st.data(), S.d_stamps, st.size() * 8, hipMemcpyDeviceToHost));
         uint64_t t0 = UINT64_MAX, tbm = 0;
         double sw = 0, bm = 0;
@@ -1121,6 +1121,10 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
             S.phase[10] += (P[5] - P[1]) * 0.01;   // candidate rows loaded
             S.phase[11] += (P[6] - P[5]) * 0.01;   // round-0 depth evaluation
             S.phase[12] += (P[7] - P[6]) * 0.01;   // round-0 sort + merge
+            if (P[8] && P[9]) {
+                S.phase[13] += (P[8] - P[2]) * 0.01;   // write back: ranks, kinds, stop rule
+                S.phase[14] += (P[9] - P[8]) * 0.01;   // write back: LDS counts
+            }
         }
         S.phase_n++;
     }

@@ -20,6 +20,6 @@ with kbhip.Session(p) as s:
     names = ["block sweep+sort", "block merge+store", "span to all block lists stored",
              "group merge tail to final start", "final merge", "chain precompute", "placement loop",
              "write back", "kernel span", "tasks per launch", "pp: rows loaded", "pp: round-0 eval",
-             "pp: round-0 sort+merge"]
+             "pp: round-0 sort+merge", "wb: ranks+stop", "wb: LDS counts"]
     print(json.dumps({"pops": n, "placement": placement, **{names[i]: round(out[i], 3) for i in range(len(names))}},
                      indent=1))
