@@ -37,6 +37,7 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 // score range and the node count fit (kbhip_kernels.hip, PopArgs).
 struct KeyFormat {
     bool use32 = false;
+    bool ent32 = false;  // parallel-levels placement entries fit 32 bits too
     int32_t base = 0, shift = 0, idxmax = 0;
 };
 // Batched path v2: one launch per pop chunk; results land in `out_dev`

@@ -328,6 +328,7 @@ struct PopArgs {
     // fit): key = (score - kbase + 1) << kshift | (kidxmax - idx) << 1 | pipelined,
     // ordered exactly as pack_key; halves the sort / merge network work.
     int32_t kbase, kshift, kidxmax;
+    int32_t ent32;  // placement entries in 32 bits: (rm - kbase + 1) fits in 32 - kshift - 5 bits
 };
 
 // Selection key of the batched sweep in type T (see PopArgs).
@@ -526,28 +527,51 @@ __device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables
 // lane finds the candidate's commit kinds and counts.  Another round runs
 // only while some candidate's deepest entry still reaches the m-th entry.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t depth_entry(int32_t rm, int n, int d) {
-    return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
-           ((uint64_t)(63 - d) << 1) | 1ull;
+// 64-bit: (rm biased) << 32 | (kEntryIdxMax - n) << 7 | (63 - d) << 1 | 1.
+// 32-bit (PopArgs::ent32): (rm - kbase + 1) << (kshift + 5) | (kidxmax - n) << 6 | (63 - d).
+template <typename ET>
+__device__ __forceinline__ ET depth_entry(int32_t rm, int n, int d, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8)
+        return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
+               ((uint64_t)(63 - d) << 1) | 1ull;
+    else
+        return ((uint32_t)(rm - a.kbase + 1) << (a.kshift + 5)) | ((uint32_t)(a.kidxmax - n) << 6) |
+               (uint32_t)(63 - d);
 }
-__device__ __forceinline__ int entry_depth(uint64_t e) { return 63 - (int)((e >> 1) & 63); }
+template <typename ET>
+__device__ __forceinline__ int entry_depth(ET e) {
+    if constexpr (sizeof(ET) == 8) return 63 - (int)((e >> 1) & 63);
+    else return 63 - (int)(e & 63);
+}
+template <typename ET>
+__device__ __forceinline__ int entry_node(ET e, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8) return entry_idx(e);
+    else return a.kidxmax - (int)((e >> 6) & (uint32_t)a.kidxmax);
+}
+template <typename T>
+__device__ __forceinline__ T readlane_t(T v, int l) {
+    if constexpr (sizeof(T) == 8) return readlane64(v, l);
+    else return (T)__builtin_amdgcn_readlane((int)v, l);
+}
 constexpr int kHash = 256;  // node index -> candidate lane (64 keys, open addressing)
 __device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 24); }
 
+template <typename ET>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                               const PopArgs& a, PopOut* out, uint64_t (*wl)[64]) {
+                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64]) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
-    __shared__ int32_t s_rm[64];          // running min through the previous round's deepest depth
+    __shared__ int32_t s_rm[2][64];       // running min through the previous round's deepest depth
     __shared__ int32_t s_apos[64];        // first Pipeline depth (64: none yet)
-    __shared__ uint64_t s_last[64];       // entry at the round's deepest depth
+    __shared__ ET s_last[64];             // entry at the round's deepest depth
     __shared__ int32_t s_cnt[64];
     __shared__ int32_t s_hkey[kHash];
     __shared__ int32_t s_hlane[kHash];
     __shared__ int s_more;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t K = wl[0][lane];
+    const uint64_t K = wl64[0][lane];
+    ET (*wl)[64] = (ET (*)[64])wl64;      // sort / merge lists of entries (same LDS)
     const int n = K ? key_idx(K) : -1;
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
@@ -580,7 +604,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         *sc = k ? key_score(k) : 0;
         return k ? key_kind(k) : 0;
     };
-    uint64_t L = 0;      // wave 0: merged top-64 entries so far (lane p = entry p)
+    ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
     bool alive = n >= 0; // candidate still relevant (uniform over waves)
     for (int r = 0; r < 64 / kW; ++r) {
         const int d = r * kW + wave;
@@ -590,35 +614,39 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         s_kind[d][lane] = (uint8_t)kind;
         __syncthreads();
         if (ap == 64) {  // first Pipeline within this round: recompute the depths behind it
+            // (no barrier before the rewrites below: they only touch depths
+            // after the first Pipeline, which every scan stops at)
             for (int w2 = 0; w2 < kW; ++w2)
                 if (s_kind[r * kW + w2][lane] == 2) { ap = r * kW + w2; break; }
-            if (alive && ap < d) kind = eval_at(d, ap, &sc);
+            if (alive && ap < d) {
+                kind = eval_at(d, ap, &sc);
+                s_kind[d][lane] = (uint8_t)kind;
+            }
         }
-        __syncthreads();  // scans of the first-pass kinds done
         s_sc[wave][lane] = sc;
-        s_kind[d][lane] = (uint8_t)kind;
         if (wave == 0) s_apos[lane] = ap;
         __syncthreads();
         // running minimum through depth d; the chain ends at the first infeasible depth
         bool ok = alive;
-        int32_t rm = r == 0 ? INT32_MAX : s_rm[lane];
-        for (int w2 = 0; w2 <= wave && ok; ++w2) {
-            if (s_kind[r * kW + w2][lane] == 0) ok = false;
+        int32_t rm = r == 0 ? INT32_MAX : s_rm[r & 1][lane];
+#pragma unroll
+        for (int w2 = 0; w2 < kW; ++w2) {
+            if (w2 > wave) break;
+            ok = ok && s_kind[r * kW + w2][lane] != 0;
             const int32_t x = s_sc[w2][lane];
             rm = x < rm ? x : rm;
         }
-        const uint64_t e = ok ? depth_entry(rm, n, d) : 0;
-        __syncthreads();  // s_rm reads done
+        const ET e = ok ? depth_entry<ET>(rm, n, d, a) : (ET)0;
         if (r == 0) STAMP(gridDim.x * 4 + 6);
-        if (wave == kW - 1) { s_last[lane] = e; s_rm[lane] = rm; }
+        if (wave == kW - 1) { s_last[lane] = e; s_rm[(r + 1) & 1][lane] = rm; }
         wl[wave][lane] = wave_sort_desc(e);
         __syncthreads();
         block_tree_merge(wl, wave, lane);
         if (wave == 0) {
             L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
             if (r == 0) STAMP(gridDim.x * 4 + 7);
-            const uint64_t T = readlane64(L, m - 1);  // m-th entry: deeper entries below it never place
-            const uint64_t le = s_last[lane];
+            const ET T = readlane_t(L, m - 1);  // m-th entry: deeper entries below it never place
+            const ET le = s_last[lane];
             const bool more = le != 0 && le >= T;
             const bool any = __ballot(more) != 0;  // all 64 lanes active
             if (lane == 0) s_more = any;
@@ -626,8 +654,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         }
         __syncthreads();
         if (!s_more) break;
-        alive = s_last[lane] != 0;
-        __syncthreads();
+        alive = s_last[lane] != 0;  // rewritten by wave kW-1 only after the next round's first barrier
     }
     if (wave != 0) return;
     STAMP(gridDim.x * 4 + 2);
@@ -635,7 +662,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     const bool inm = lane < m && L != 0;
     int lf = 0;
     if (inm) {
-        const int ni = entry_idx(L);
+        const int ni = entry_node(L, a);
         int h = hash_slot(ni);
         while (s_hkey[h] != ni) h = (h + 1) & (kHash - 1);
         lf = s_hlane[h];
@@ -674,7 +701,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
     }
     if (lane < done)
-        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_idx(L) : -1),
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_node(L, a) : -1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     STAMP(gridDim.x * 4 + 3);
 }
@@ -773,7 +800,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     if (a.placement == 2) {  // uniform; every wave takes part
         STAMP(gridDim.x * 4 + 1);
-        place_parallel(cf, nc, t, c, a, out, wl);
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
@@ -976,7 +1004,8 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf) {
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax};
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax,
+              kf.use32 && kf.ent32 ? 1 : 0};
     PopOut* o = (PopOut*)out_dev;
     if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
     else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);

@@ -868,6 +868,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
             KeyFormat& kf = S.class_kf[ci];
             kf.use32 = ibits <= 25 && shi - slo + 1 < ((int64_t)1 << (31 - ibits)) && slo >= INT32_MIN && shi <= INT32_MAX;
+            kf.ent32 = kf.use32 && ibits <= 24 && shi - slo + 1 < ((int64_t)1 << (26 - ibits));
             kf.base = (int32_t)slo;
             kf.shift = ibits + 1;
             kf.idxmax = (int32_t)(((int64_t)1 << ibits) - 1);
