@@ -144,12 +144,41 @@ class Snapshot {
         size_t got = sz > 0 ? std::fread(buf_.data(), 1, (size_t)sz, f) : 0;
         std::fclose(f);
         if (got != (size_t)sz) throw std::runtime_error("kbsnap: short read " + path);
+        data_ = buf_.data();
+        size_ = buf_.size();
         parse();
     }
 
     void load_bytes(const void* p, size_t n) {
         buf_.assign((const char*)p, (const char*)p + n);
+        data_ = buf_.data();
+        size_ = buf_.size();
         parse();
+    }
+    /* In-place view of a caller buffer that outlives this object (no copy). */
+    void view_bytes(const void* p, size_t n) {
+        buf_.clear();
+        data_ = (const char*)p;
+        size_ = n;
+        parse();
+    }
+
+    /* Non-owning typed view of a column (valid while the snapshot lives). */
+    template <typename T>
+    struct Span {
+        const T* p = nullptr;
+        size_t n = 0;
+        const T& operator[](size_t i) const { return p[i]; }
+        size_t size() const { return n; }
+        bool empty() const { return n == 0; }
+        const T* begin() const { return p; }
+        const T* end() const { return p + n; }
+    };
+    template <typename T>
+    Span<T> span(const char* name) const {
+        Span<T> sp;
+        sp.p = col<T>(name, &sp.n);
+        return sp;
     }
 
     /* Typed column access.  Returns nullptr and n=0 for a missing section. */
@@ -160,7 +189,7 @@ class Snapshot {
         if (d->elem_size != sizeof(T))
             throw std::runtime_error(std::string("kbsnap: element size mismatch for ") + name);
         *n = (size_t)d->count;
-        return reinterpret_cast<const T*>(buf_.data() + d->offset);
+        return reinterpret_cast<const T*>(data_ + d->offset);
     }
     template <typename T>
     std::vector<T> vec(const char* name) const {
@@ -195,16 +224,16 @@ class Snapshot {
         return nullptr;
     }
     void parse() {
-        if (buf_.size() < sizeof(kbs_header)) throw std::runtime_error("kbsnap: file too small");
-        const kbs_header* h = reinterpret_cast<const kbs_header*>(buf_.data());
+        if (size_ < sizeof(kbs_header)) throw std::runtime_error("kbsnap: file too small");
+        const kbs_header* h = reinterpret_cast<const kbs_header*>(data_);
         if (std::memcmp(h->magic, KBS_MAGIC, 4) != 0) throw std::runtime_error("kbsnap: bad magic");
         if (h->version != KBS_VERSION) throw std::runtime_error("kbsnap: unsupported version");
         ndir_ = h->n_sections;
-        if (sizeof(kbs_header) + (size_t)ndir_ * sizeof(kbs_dirent) > buf_.size())
+        if (sizeof(kbs_header) + (size_t)ndir_ * sizeof(kbs_dirent) > size_)
             throw std::runtime_error("kbsnap: truncated directory");
-        dir_ = reinterpret_cast<const kbs_dirent*>(buf_.data() + sizeof(kbs_header));
+        dir_ = reinterpret_cast<const kbs_dirent*>(data_ + sizeof(kbs_header));
         for (uint32_t i = 0; i < ndir_; ++i) {
-            if (dir_[i].offset + dir_[i].count * dir_[i].elem_size > buf_.size())
+            if (dir_[i].offset + dir_[i].count * dir_[i].elem_size > size_)
                 throw std::runtime_error("kbsnap: section out of range");
         }
         size_t n = 0;
@@ -214,6 +243,8 @@ class Snapshot {
     }
 
     std::vector<char> buf_;
+    const char* data_ = nullptr;
+    size_t size_ = 0;
     const kbs_dirent* dir_ = nullptr;
     uint32_t ndir_ = 0;
     const char* strtab_ = nullptr;

@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -98,7 +100,7 @@ struct F3 {  // float64 Resource of the ordering plugins
 static double share(double l, double r) { return r == 0 ? (l == 0 ? 0 : 1) : l / r; }  // helpers.go:35-48
 
 struct HPod {
-    string uid;
+    int32_t uid_rank = 0;  // rank of the pod UID (pods are written sorted by UID: normally the index)
     int ns = -1;
     int status = Pending;
     int32_t priority = 0;
@@ -297,6 +299,15 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.world = world;
     S.encode_only = encode_only;
     auto t0 = std::chrono::steady_clock::now();
+    // KBHIP_OPEN_PROFILE=1: per-phase host times of the session open on stderr (diagnostic)
+    static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;
+    auto tp = t0;
+    auto mark = [&](const char* what) {
+        if (!prof) return;
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[open] %-10s %8.2f ms\n", what, std::chrono::duration<double>(now - tp).count() * 1e3);
+        tp = now;
+    };
     Encoder E(s, S);
     auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
     // ---------------- conf (framework.go:29-51) ----------------
@@ -335,6 +346,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 if (p.name == "gang" && !(p.flags & KBS_DIS_JOBREADY)) S.gang_ready = true;
             }
     }
+    mark("conf");
     // ---------------- nodes ----------------
     auto nname = V32("n_name");
     const int N = (int)nname.size();
@@ -353,9 +365,12 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     E.node_labels.resize(N);
     vector<vector<int>> node_taints(N);
     std::map<std::tuple<string, string, string>, int> taint_ids;
+    std::unordered_map<int32_t, int> node_by_off;  // strtab offset of the name -> node (fast path)
+    node_by_off.reserve((size_t)N * 2);
     for (int i = 0; i < N; ++i) {
         S.node_names[i] = s.s(nname[i]);
         node_idx[S.node_names[i]] = i;
+        node_by_off.emplace(nname[i], i);
         for (int k = loff[i]; k < loff[i + 1]; ++k)
             E.node_labels[i].push_back({E.keys_all.get(s.s(lk[k])), E.vals.get(s.s(lv[k]))});
         for (int k = toff[i]; k < toff[i + 1]; ++k) {
@@ -378,26 +393,29 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.used.assign(N, R3{});
     for (int i = 0; i < N; ++i) idle[i] = R3{acpu[i], amem[i], agpu[i]};
 
+    mark("nodes");
     // ---------------- pods ----------------
-    auto puid = V32("p_uid");
+    // per-pod columns are read in place (1M-row columns: no copies)
+    auto S32 = [&](const char* n) { return s.span<int32_t>(n); };
+    auto puid = S32("p_uid");
     const int P = (int)puid.size();
-    auto pns = V32("p_ns"), pjob = V32("p_job"), pnode = V32("p_node"), ppri = V32("p_priority"), paff = V32("p_aff");
-    auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
-    auto pts = s.vec<int64_t>("p_ts");
+    auto pns = S32("p_ns"), pjob = S32("p_job"), pnode = S32("p_node"), ppri = S32("p_priority"), paff = S32("p_aff");
+    auto pphase = s.span<uint8_t>("p_phase"), pdel = s.span<uint8_t>("p_deleting"), pbf = s.span<uint8_t>("p_backfill");
+    auto pts = s.span<int64_t>("p_ts");
     if ((int)pns.size() != P || (int)pjob.size() != P || (int)pnode.size() != P || (int)ppri.size() != P ||
         (int)pphase.size() != P || (int)pts.size() != P)
         throw Error(KBHIP_EINVAL, "pod columns length mismatch");
     auto pco = s.offs("p_ctr_off", P);
-    auto ccpu = s.vec<int64_t>("c_cpu"), cmem = s.vec<int64_t>("c_mem"), cgpu = s.vec<int64_t>("c_gpu");
-    auto chas = s.vec<uint8_t>("c_has");
+    auto ccpu = s.span<int64_t>("c_cpu"), cmem = s.span<int64_t>("c_mem"), cgpu = s.span<int64_t>("c_gpu");
+    auto chas = s.span<uint8_t>("c_has");
     auto cpo = s.offs("c_port_off", ccpu.size());
     auto ptip = V32("pt_ip"), ptpr = V32("pt_proto"), ptpo = V32("pt_port");
     auto pio = s.offs("p_ictr_off", P);
-    auto iccpu = s.vec<int64_t>("ic_cpu"), icmem = s.vec<int64_t>("ic_mem"), icgpu = s.vec<int64_t>("ic_gpu");
+    auto iccpu = s.span<int64_t>("ic_cpu"), icmem = s.span<int64_t>("ic_mem"), icgpu = s.span<int64_t>("ic_gpu");
     auto pso = s.offs("p_nsel_off", P);
-    auto psk = V32("ps_key"), psv = V32("ps_val");
+    auto psk = S32("ps_key"), psv = S32("ps_val");
     auto pto = s.offs("p_tol_off", P);
-    auto tlk = V32("tl_key"), tlo = V32("tl_op"), tlv = V32("tl_val"), tle = V32("tl_effect");
+    auto tlk = S32("tl_key"), tlo = S32("tl_op"), tlv = S32("tl_val"), tle = S32("tl_effect");
     auto a_flags = s.vec<uint8_t>("a_flags");
     auto acnt = [&](const char* n) { return V32(n); };
     auto pareq_c = acnt("a_pareq_cnt"), papref_c = acnt("a_papref_cnt"), paareq_c = acnt("a_paareq_cnt"),
@@ -405,17 +423,34 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     (void)pareq_c; (void)papref_c; (void)paareq_c; (void)paapref_c;
 
     S.pods.resize(P);
+    {  // UID ranks: the canonical order (kbsnap.h) makes them the index; sort otherwise
+        bool sorted = true;
+        for (int i = 1; i < P && sorted; ++i) sorted = std::strcmp(s.str(puid[i - 1]), s.str(puid[i])) < 0;
+        if (sorted) {
+            for (int i = 0; i < P; ++i) S.pods[i].uid_rank = i;
+        } else {
+            vector<int> ord(P);
+            for (int i = 0; i < P; ++i) ord[i] = i;
+            std::sort(ord.begin(), ord.end(),
+                      [&](int a, int b) { return std::strcmp(s.str(puid[a]), s.str(puid[b])) < 0; });
+            for (int r = 0; r < P; ++r) S.pods[ord[r]].uid_rank = r;
+        }
+    }
     vector<vector<int>> pod_ports(P);
     vector<int64_t> pod_nzc(P, 0), pod_nzm(P, 0);
+    std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
     for (int i = 0; i < P; ++i) {
         HPod& p = S.pods[i];
-        p.uid = s.s(puid[i]);
-        p.ns = E.nss.get(s.s(pns[i]));
-        string nn = s.s(pnode[i]);
+        {
+            auto it = ns_by_off.find(pns[i]);
+            if (it == ns_by_off.end()) it = ns_by_off.emplace(pns[i], E.nss.get(s.s(pns[i]))).first;
+            p.ns = it->second;
+        }
+        const bool has_node = pnode[i] >= 0 && s.str(pnode[i])[0] != '\0';
         int ph = pphase[i];
         bool del = !pdel.empty() && pdel[i];
         if (ph == KBS_RUNNING) p.status = del ? Releasing : Running;            // api/helpers.go:35-61
-        else if (ph == KBS_PENDING) p.status = del ? Releasing : (nn.empty() ? Pending : Bound);
+        else if (ph == KBS_PENDING) p.status = del ? Releasing : (!has_node ? Pending : Bound);
         else if (ph == KBS_SUCCEEDED) p.status = Succeeded;
         else if (ph == KBS_FAILED) p.status = Failed;
         else p.status = Unknown;
@@ -445,11 +480,17 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             p.ireq.m = std::max(p.ireq.m, icmem[k]);
             p.ireq.g = std::max(p.ireq.g, icgpu[k]);
         }
-        if (!nn.empty()) {
-            auto it = node_idx.find(nn);
-            if (it == node_idx.end())
-                throw Error(KBHIP_EINVAL, "pod " + p.uid + " is bound to node " + nn + " which is not in the snapshot");
-            p.node = it->second;
+        if (has_node) {
+            auto ot = node_by_off.find(pnode[i]);
+            if (ot != node_by_off.end()) {
+                p.node = ot->second;
+            } else {
+                auto it = node_idx.find(s.s(pnode[i]));
+                if (it == node_idx.end())
+                    throw Error(KBHIP_EINVAL, "pod " + s.s(puid[i]) + " is bound to node " + s.s(pnode[i]) +
+                                                  " which is not in the snapshot");
+                p.node = it->second;
+            }
         }
         if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
             int n = p.node;
@@ -469,6 +510,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
 
+    mark("pods");
     // ---------------- queues & jobs ----------------
     auto qn = V32("q_name"), qw = V32("q_weight");
     auto qts = s.vec<int64_t>("q_ts");
@@ -487,7 +529,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
     for (int i = 0; i < P; ++i) {
         if (pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
-        if (pjob[i] < 0) srcs.push_back({S.pods[i].uid, -1, i});  // shadow PodGroup (cache/util.go:42-60)
+        if (pjob[i] < 0) srcs.push_back({s.s(puid[i]), -1, i});  // shadow PodGroup (cache/util.go:42-60)
     }
     std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
     vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
@@ -520,6 +562,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             if (S.pods[t].status == AOB) j.cnt_aob++;
         }
 
+    mark("jobs");
     // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
     AffinityModel aff;
     {
@@ -543,6 +586,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     vector<int32_t> aff_items;
 
+    mark("affinity");
     // ---------------- task classes for pending tasks ----------------
     // label columns: keys referenced by selectors / node affinity of pending tasks
     auto es = V32("nst_expr_start"), ec = V32("nst_expr_cnt"), fs = V32("nst_field_start"), fc = V32("nst_field_cnt");
@@ -628,9 +672,48 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     };
 
     std::unordered_map<string, int> class_ids;
+    auto plo = s.offs("p_label_off", P);
+    auto plk = S32("pl_key"), plv = S32("pl_val");
+    using Col = kbs::Snapshot::Span<int32_t>;
+    auto same_run = [](const vector<int32_t>& off, int a, int b, std::initializer_list<const Col*> cols) {
+        const int na = off[a + 1] - off[a];
+        if (na != off[b + 1] - off[b]) return false;
+        for (const Col* c : cols)
+            for (int k = 0; k < na; ++k)
+                if ((*c)[off[a] + k] != (*c)[off[b] + k]) return false;
+        return true;
+    };
+    auto same_prog = [&](int a, int b) {
+        const AffProgram *x = aff.program(a), *y = aff.program(b);
+        if (!x || !y) return x == y;
+        return x->ea == y->ea && x->pa_space == y->pa_space && x->pa_cnt == y->pa_cnt && x->pa_total == y->pa_total &&
+               x->pa_self == y->pa_self && x->paa_space == y->paa_space && x->paa_cnt == y->paa_cnt &&
+               x->ipa == y->ipa && x->upd == y->upd && x->pred_err == y->pred_err;
+    };
+    // Every input of the class of pod a equals pod b's (typical for the pods of
+    // one job): the class is reused without building its signature.
+    auto same_class_inputs = [&](int a, int b) {
+        const HPod &A = S.pods[a], &B = S.pods[b];
+        if (A.ns != B.ns || A.backfill != B.backfill) return false;
+        if (A.req.c != B.req.c || A.req.m != B.req.m || A.req.g != B.req.g) return false;
+        if (A.ireq.c != B.ireq.c || A.ireq.m != B.ireq.m || A.ireq.g != B.ireq.g) return false;
+        if (pod_nzc[a] != pod_nzc[b] || pod_nzm[a] != pod_nzm[b] || pod_ports[a] != pod_ports[b]) return false;
+        if ((paff.empty() ? -1 : paff[a]) != (paff.empty() ? -1 : paff[b])) return false;
+        if (!same_run(pso, a, b, {&psk, &psv})) return false;
+        if (!same_run(pto, a, b, {&tlk, &tlo, &tlv, &tle})) return false;
+        if (aff.active && !(same_run(plo, a, b, {&plk, &plv}) && same_prog(a, b))) return false;
+        return true;
+    };
+    int prev_pending = -1;
     for (int i = 0; i < P; ++i) {
         HPod& p = S.pods[i];
         if (p.status != Pending || p.job < 0) continue;
+        if (prev_pending >= 0 && same_class_inputs(prev_pending, i)) {
+            p.cls = S.pods[prev_pending].cls;
+            prev_pending = i;
+            continue;
+        }
+        prev_pending = i;
         TaskClass c{};
         c.ireq_cpu = p.ireq.c; c.ireq_mem = p.ireq.m; c.ireq_gpu = p.ireq.g;
         c.req_cpu = p.req.c; c.req_mem = p.req.m; c.req_gpu = p.req.g;
@@ -769,6 +852,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.device = device;
         HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
     }
+    mark("classes");
     // ---------------- upload ----------------
     // this session's node range: the whole array, or one contiguous shard
     const int lo = (int)((int64_t)N * S.rank / S.world), hi = (int)((int64_t)N * (S.rank + 1) / S.world);
@@ -906,6 +990,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 #endif
     }
     HIPCHK(hipStreamSynchronize(st));
+    mark("upload");
     // ---------------- ordering plugins OnSessionOpen ----------------
     for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
     S.stats.nodes = N;
@@ -1338,7 +1423,7 @@ struct Allocator {
     bool task_less(int l, int r) const {  // session_plugins.go:297-329, priority.go:39-55
         const HPod &L = S.pods[l], &R = S.pods[r];
         if (task_prio && L.priority != R.priority) return L.priority > R.priority;
-        if (L.ts == R.ts) return L.uid < R.uid;
+        if (L.ts == R.ts) return L.uid_rank < R.uid_rank;
         return L.ts < R.ts;
     }
     void drf_update(HJob& j) {  // drf.go:156-170
@@ -1667,7 +1752,7 @@ int kbhip_session_open(const void* bytes, size_t len, int device, kb_session** o
     ABI_GUARD({
         if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         kbs::Snapshot snap;
-        snap.load_bytes(bytes, len);
+        snap.view_bytes(bytes, len);  // the caller's buffer outlives the call; nothing keeps a view after it
         return open_common(snap, device, out);
     })
 }
@@ -1860,7 +1945,7 @@ int kbhip_debug_encode(const void* bytes, size_t len, kb_session** out) {
     ABI_GUARD({
         if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         kbs::Snapshot snap;
-        snap.load_bytes(bytes, len);
+        snap.view_bytes(bytes, len);
         std::unique_ptr<kb_session> s(new kb_session());
         kbhip::open_session(s->s, snap, -1, true);
         *out = s.release();
