@@ -117,7 +117,7 @@ def pmc_traffic():
     so this comes from the profiling pass of profiles/run_profile.sh."""
     import glob
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=os.path.getmtime):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):  # tags sort by round
         with open(p) as f:
             d = json.load(f)
         for name, k in d.get("kernels", {}).items():
