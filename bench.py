@@ -51,9 +51,15 @@ def parse():
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
-    ap.add_argument("--time-every", type=int, default=4, help="HIP-event time every k-th sweep launch")
+    ap.add_argument("--time-every", type=int, default=0,
+                    help="also HIP-event time every k-th sweep launch (0 = off; per-launch events stall the "
+                         "overlapped pipeline, so the roofline uses each session's device span instead)")
     ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2),
                     help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels")
+    ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2),
+                    help="predicted job pops queued ahead of the running one")
+    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
+                    help="1 = overlapped batched pops (two streams, device-side chaining)")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
                     help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
                          "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")
@@ -134,11 +140,13 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None, placement=0):
+def run_session(buf, device, time_every, shard=None, placement=0, overlap=1, speculate=2):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
     s.set_option("placement", placement)
+    s.set_option("overlap", overlap)
+    s.set_option("speculate", speculate)
     pod, node, kind = s.allocate(cap=1 << 21)
     st = s.stats()
     s.close()
@@ -174,16 +182,21 @@ def main():
     device = local
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
-        run_session(buf, device, 0, shard, args.placement)
+        run_session(buf, device, 0, shard, args.placement, args.overlap, args.speculate)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
+    dev_s, dev_pops, tasks = 0.0, 0, 0
     for _ in range(args.steps):
-        dt, n, st = run_session(buf, device, args.time_every, shard, args.placement)
+        dt, n, st = run_session(buf, device, args.time_every, shard, args.placement, args.overlap,
+                                args.speculate)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
         sweeps_n += st["timed_launches"]
+        dev_s += st["alloc_device_s"]
+        dev_pops += st["batched_pops"]
+        tasks += st["tasks"]
         st_last = st
     barrier(dist, local)
     wall = time.perf_counter() - t0
@@ -196,9 +209,16 @@ def main():
         return
     nodes = st_last["nodes"]
     traffic = None if shard else pmc_traffic()
-    sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
     nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
-    achieved = nodes_per_launch * B_NODE / (sweep_us * 1e-6) / 1e9 if sweeps_n else 0.0
+    if shard or not dev_pops:  # per-task launches: sampled HIP events around single launches
+        sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
+        timing = f"HIP events around every {args.time_every}-th sweep launch ({sweeps_n} launches)"
+    else:  # batched pops (overlapped): device span of each allocate / its launches
+        sweep_us = dev_s / dev_pops * 1e6
+        timing = (f"HIP events bracketing each session's allocate on the engine streams, / {dev_pops} "
+                  f"k_pop_batch launches (consecutive launches overlap: per-launch device period)")
+    achieved = nodes_per_launch * B_NODE / (sweep_us * 1e-6) / 1e9 if sweep_us > 0 else 0.0
+    tasks_per_launch = tasks / max(dev_pops, 1) if not shard else 1.0
     out = {
         "metric": METRIC,
         "value": total_placed / wall,
@@ -218,6 +238,7 @@ def main():
                    "placements_per_session": placed // args.steps, "pops_per_session": st_last["pops"],
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"], "placement": args.placement,
+                   "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
@@ -228,8 +249,13 @@ def main():
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
                      if traffic else None,
-                     "mean_launch_us": sweep_us, "timed_launches": sweeps_n,
-                     "bytes_per_launch": nodes_per_launch * B_NODE},
+                     "mean_launch_us": sweep_us, "timing": timing,
+                     "bytes_per_launch": nodes_per_launch * B_NODE,
+                     # SURVEY §8(d)'s per-task accounting: one launch serves tasks_per_launch tasks with ONE
+                     # sweep, so per-task algorithmic bytes exceed what the launch reads (frac > 1 is the batching)
+                     "per_task_algorithmic": {"tasks_per_launch": tasks_per_launch,
+                                              "achieved": tasks_per_launch * achieved,
+                                              "frac": tasks_per_launch * achieved / HBM_PEAK_GBS}},
     }
     if args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds)

@@ -84,6 +84,7 @@ typedef struct kbhip_stats {
     double host_wait_s;     /* host time spent waiting for their results */
     int64_t spec_hits;      /* predicted next pops launched ahead and used (kbhip_allocate) */
     int64_t spec_missed;    /* predicted pops retracted (their node updates undone on device) */
+    double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -133,10 +134,13 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;
- * "speculate" = 1 (default) lets kbhip_allocate queue the predicted next job
- * pop behind the running one (used only if it is exactly the next pop,
- * retracted on device otherwise; placements are unchanged), 0 = one pop at
- * a time;
+ * "speculate" = 2 (default) lets kbhip_allocate queue the two predicted next
+ * job pops behind the running one, 1 the next one only (used only if exactly
+ * the next pop, retracted on device otherwise; placements are unchanged),
+ * 0 = one pop at a time;
+ * "overlap" = 1 (default; placement 2) runs consecutive batched pops on two
+ * streams, the next pop's sweep overlapping the running pop's placement,
+ * chained on the device; 0 = one stream, one pop kernel at a time;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);

@@ -45,6 +45,26 @@ struct KeyFormat {
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf);
+// Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
+// done = sequence number of the last pop whose node write-back is visible;
+// cand = of the last pop whose candidates are published; touched[e & 1] = the
+// 64 candidate nodes of pop e (-1: none).  Zero flags and all-(-1) touched
+// lists at session open.
+struct PopLink {
+    uint32_t done;
+    uint32_t pad0[31];
+    uint32_t cand;
+    uint32_t pad1[31];
+    int32_t touched[2][64];
+};
+// Overlapped batched pop number `seq` (>= 1): waits on the device for pop
+// seq-1's candidates and write-back (launched before it, on another stream);
+// cand holds (blocks + 8) * 64 keys, arrive 9 * 32 counters, both private to the
+// launch's stream parity.
+hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
+                               uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
+                               uint32_t seq);
 // Inverse node updates of a batched pop's placements (a retracted prediction).
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

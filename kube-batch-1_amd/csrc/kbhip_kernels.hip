@@ -22,6 +22,7 @@
 //    predicate and inter-pod score read count tables every commit may change
 //    (kbhip_affinity.h); k_ipa_minmax is the score's normalisation prepass.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "kbhip_eval.h"
 #include "kbhip_internal.h"
@@ -929,6 +930,174 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
 }
 
 // ---------------------------------------------------------------------------
+// Overlapped batched pops (option "overlap").  Pop e runs while pop e-1
+// (launched on the other stream) may still be placing.  Every row a
+// placement writes belongs to one of its 64 candidates, which pop e-1
+// publishes (PopLink::touched, flag cand) as soon as its candidate list is
+// final — normally long before pop e's blocks finish evaluating.  Pop e's
+// sweep ranks every other node exactly (their rows are final) and leaves
+// pop e-1's candidates out; its final merger waits for pop e-1's write-back
+// (flag done), evaluates those candidates on their final rows and merges
+// them in: the top-64 of all nodes, as the non-overlapped kernel sees it.
+// Hand-offs: candidates and flag cand as sc1 stores drained by the storing
+// wave, sc1 loads after the poll (MI355X_MICROARCH.md valid forms, row 1);
+// rows behind an agent release / acquire pair around flag done.
+// ---------------------------------------------------------------------------
+template <typename KT>
+__device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
+    if constexpr (sizeof(KT) == 8) return key_idx(k);
+    else return a.kidxmax - (int)((k >> 1) & (uint32_t)a.kidxmax);
+}
+
+constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
+
+// Poll an agent-scope flag until it reaches `want` (wrapping compare); false on timeout.
+__device__ __forceinline__ bool wait_flag(const uint32_t* f, uint32_t want) {
+    long spin = 0;
+    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+        if (++spin >= kLinkSpin) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+template <int R, typename KT>
+__global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
+                                                              uint64_t* cand64, uint32_t* arrive, PopOut* out,
+                                                              PopLink* link, uint32_t seq) {
+    __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
+    __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
+    __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
+    __shared__ int role, s_ok;
+    KT* cand = (KT*)cand64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const TaskClass c = t.classes[a.cls];
+    const int base = blockIdx.x * R * kPopThreads;
+    const int prev = (seq - 1) & 1;
+    for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
+    __syncthreads();
+    if (wave == 0) {  // pop seq-1's candidates (seq 1: none)
+        bool ok = true;
+        if (lane == 0) ok = wait_flag(&link->cand, seq - 1);
+        ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+        const int x = __hip_atomic_load(&link->touched[prev][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x >= base && x < base + R * kPopThreads) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
+        if (lane == 0) s_ok = ok;
+    }
+    // 1. evaluate R nodes per lane (pop seq-1's candidates left out), wave top-64, block top-64
+    KT keys[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
+        keys[r] = 0;
+        if (n < nc.n) {
+            int32_t s;
+            bool passed;
+            keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed), a);
+        }
+    }
+    __syncthreads();
+    KT best = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int o = r * kPopThreads + threadIdx.x;
+        const KT k = wave_sort_desc((s_skip[o >> 5] >> (o & 31)) & 1u ? (KT)0 : keys[r]);
+        best = r == 0 ? k : wave_merge_desc(best, k);
+    }
+    wlk[wave][lane] = best;
+    __syncthreads();
+    block_tree_merge(wlk, wave, lane);
+    const int nb = gridDim.x;
+    const int g = blockIdx.x % kGroups;
+    const int g_count = (nb - g + kGroups - 1) / kGroups;
+    const int n_groups = nb < kGroups ? nb : kGroups;
+    KT* gcand = cand + (int64_t)nb * 64;
+    if (wave == 0) {
+        put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
+    __syncthreads();
+    if (!role) return;
+    // 2a. last block of group g merges the group's lists
+    {
+        KT acc = 0;
+        constexpr int kPf = 4;
+        for (int i0 = wave; i0 < g_count; i0 += kPf * (kPopThreads / 64)) {
+            KT v[kPf];
+#pragma unroll
+            for (int q = 0; q < kPf; ++q) {
+                const int i = i0 + q * (kPopThreads / 64);
+                v[q] = i < g_count ? get_list(cand + (int64_t)(g + i * kGroups) * 64) : (KT)0;
+            }
+#pragma unroll
+            for (int q = 0; q < kPf; ++q) acc = wave_merge_desc(acc, v[q]);
+        }
+        wlk[wave][lane] = acc;
+        __syncthreads();
+        block_tree_merge(wlk, wave, lane);
+        if (wave == 0) {
+            put_list(gcand + (int64_t)g * 64, wlk[0][lane]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1);
+        __syncthreads();
+        if (!role) return;
+    }
+    // 2b. last group merger: the top-64 of every node but pop seq-1's candidates
+    wlk[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : (KT)0;
+    __syncthreads();
+    block_tree_merge(wlk, wave, lane);
+    if (wave == 0 && lane <= kGroups)
+        __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 3. pop seq-1's write-back (consumer: relaxed poll, agent acquire, vmcnt
+    // wait, barrier, plain loads); its candidates on their final rows
+    if (threadIdx.x == 0) {
+        s_ok = s_ok && wait_flag(&link->done, seq - 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const bool ok = s_ok;
+    if (wave == 0) {
+        const int tn = ok ? link->touched[prev][lane] : -1;
+        KT e = 0;
+        if (tn >= 0) {
+            int32_t s;
+            bool passed;
+            e = sweep_key<KT>(eval_node(cf, c, t, nc, tn, &s, &passed), a);
+        }
+        const KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e));
+        // publish this pop's candidates (sc1 stores, drained, then the sc1 flag)
+        __hip_atomic_store(&link->touched[seq & 1][lane], (ok && top) ? key_node(top, a) : -1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) __hip_atomic_store(&link->cand, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wl[0][lane] = ok ? key64_of(top, a) : 0;
+    }
+    __syncthreads();
+    if (ok) {
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl);
+    } else if (wave == 0 && lane == 0) {  // broken chain: n_done = 0 tells the host
+        __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // 4. publish this pop's write-back (producer: the storing wave's vmcnt
+    // wait, agent release, vmcnt wait, relaxed flag store)
+    if (wave == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(&link->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
@@ -981,8 +1150,13 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 }
 
 int pop_blocks(int n_nodes, int* R_out) {
+    static const int forced = [] {  // KBHIP_POP_R: nodes per lane (tuning experiments only)
+        const char* e = std::getenv("KBHIP_POP_R");
+        return e ? std::atoi(e) : 0;
+    }();
     int R = 1;
     while ((int64_t)kPopThreads * R * 512 < n_nodes && R < 16) R <<= 1;
+    if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16) R = forced;
     *R_out = R;
     return (n_nodes + kPopThreads * R - 1) / (kPopThreads * R);
 }
@@ -1009,6 +1183,36 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
     PopOut* o = (PopOut*)out_dev;
     if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
     else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
+    return hipGetLastError();
+}
+
+template <typename KT>
+static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                  const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
+                                  uint32_t seq, hipStream_t st) {
+#define KBHIP_OV(RR) \
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, link, seq)
+    switch (R) {
+        case 1: KBHIP_OV(1); break;
+        case 2: KBHIP_OV(2); break;
+        case 4: KBHIP_OV(4); break;
+        case 8: KBHIP_OV(8); break;
+        default: KBHIP_OV(16); break;
+    }
+#undef KBHIP_OV
+}
+
+hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
+                               uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
+                               uint32_t seq) {
+    int R;
+    const int nb = pop_blocks(nc.n, &R);
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
+              kf.use32 && kf.ent32 ? 1 : 0};
+    PopOut* o = (PopOut*)out_dev;
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
     return hipGetLastError();
 }
 

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <set>
@@ -189,15 +190,32 @@ struct Session {
     DevBuf b_cand2, b_arrive;
     uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
+    // option "overlap" (default on, placement 2): batched pops alternate between
+    // two streams and chain on the device (k_pop_batch_ov, PopLink)
+#ifdef KBHIP_STAMPS
+    bool overlap = false;       // stamps are written by k_pop_batch only
+#else
+    bool overlap = true;
+#endif
+    hipStream_t stream_b = nullptr;
+    DevBuf b_cand_ov[2], b_arrive_ov[2], b_link;
+    uint64_t* d_cand_ov[2] = {nullptr, nullptr};
+    uint32_t* d_arrive_ov[2] = {nullptr, nullptr};
+    PopLink* d_link = nullptr;
+    uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
+    bool ov_pending = false;    // an overlapped pop may still run on either stream
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
-    uint32_t slot_epoch[2] = {0, 0};  // granule tags per result slot
-    int next_slot = 0;                // slot of the next batched launch (alternates)
-    hipEvent_t evb[2][2] = {};        // per-slot HIP-event pairs (sampled launch timing)
+    static constexpr int kSlots = 4;  // result slots: up to 3 batched pops in flight
+    uint32_t slot_epoch[kSlots] = {};  // granule tags per result slot
+    int next_slot = 0;                // slot of the next batched launch (round robin)
+    hipEvent_t evb[kSlots][2] = {};   // per-slot HIP-event pairs (sampled launch timing)
+    hipEvent_t ev_run[2] = {};        // device span of kbhip_allocate
+    double alloc_device_s = 0;
 #ifdef KBHIP_STAMPS
-    bool speculate = false;           // stamps are read per launch: no overlapped launches
+    int speculate = 0;                // stamps are read per launch: no overlapped launches
 #else
-    bool speculate = true;            // queue the predicted next pop behind the running one
+    int speculate = 2;                // predicted pops queued ahead of the running one (0..2)
 #endif
     int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
 #ifdef KBHIP_STAMPS
@@ -241,8 +259,11 @@ struct Session {
         for (auto& pr : evb)
             for (auto& e : pr)
                 if (e) (void)hipEventDestroy(e);
+        for (auto& e : ev_run)
+            if (e) (void)hipEventDestroy(e);
         if (h_ctrl) (void)hipHostFree(h_ctrl);
         if (h_out) (void)hipHostFree(h_out);
+        if (stream_b) { (void)hipStreamSynchronize(stream_b); (void)hipStreamDestroy(stream_b); }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -851,6 +872,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         HIPCHK(hipSetDevice(device));
         S.device = device;
         HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&S.stream_b, hipStreamNonBlocking));
     }
     mark("classes");
     // ---------------- upload ----------------
@@ -980,10 +1002,20 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
         S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
+        for (int k = 0; k < 2; ++k) {
+            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
+            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>(9 * 32);
+            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, 9 * 32 * sizeof(uint32_t), st));
+        }
+        S.d_link = S.b_link.alloc<PopLink>(1);
+        HIPCHK(hipMemsetAsync(S.d_link, 0xff, sizeof(PopLink), st));  // touched lists: -1
+        HIPCHK(hipMemsetAsync(&S.d_link->done, 0, sizeof(uint32_t), st));  // flags 0: pop 1 waits for nothing
+        HIPCHK(hipMemsetAsync(&S.d_link->cand, 0, sizeof(uint32_t), st));
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
-        HIPCHK(hipHostMalloc((void**)&S.h_out, 2 * sizeof(PopOutHost), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostMalloc((void**)&S.h_out, Session::kSlots * sizeof(PopOutHost),
+                             hipHostMallocMapped | hipHostMallocCoherent));
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
-        std::memset(S.h_out, 0, 2 * sizeof(PopOutHost));
+        std::memset(S.h_out, 0, Session::kSlots * sizeof(PopOutHost));
 #ifdef KBHIP_STAMPS
         S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 16);
         HIPCHK(set_stamp_buffer(S.d_stamps));
@@ -1101,7 +1133,17 @@ struct BatchLaunch {
     uint32_t epoch = 0;
     int cls = -1, m = 0;
     bool timed = false;
+    hipStream_t st = nullptr;
 };
+
+// Wait until no overlapped pop can still run (before device work that is not
+// an overlapped pop, which the device chain does not order).
+static void ov_quiesce(Session& S) {
+    if (!S.ov_pending) return;
+    HIPCHK(hipStreamSynchronize(S.stream_b));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    S.ov_pending = false;
+}
 
 // Nothing but the winner's row can change between the chunk's tasks: the
 // condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
@@ -1114,7 +1156,7 @@ static bool batchable(const Session& S, int cls) {
 static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
     BatchLaunch L;
     L.slot = S.next_slot;
-    S.next_slot ^= 1;
+    S.next_slot = (S.next_slot + 1) % Session::kSlots;
     uint32_t& ep = S.slot_epoch[L.slot];
     if (((ep + 1) & 0xffff) == 0) {  // tag wrap: clear this (idle) slot's stale granules, skip tag 0
         std::memset(S.h_out + L.slot, 0, sizeof(PopOutHost));
@@ -1127,12 +1169,24 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     S.sweep_launches++;
     hipEvent_t* ev = S.evb[L.slot];
     if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
+    const bool ov = S.overlap && S.placement == 2;
+    if (!ov) ov_quiesce(S);
+    const uint32_t seq = ov ? S.ov_seq + 1 : 0;
+    L.st = (ov && (seq & 1)) ? S.stream_b : S.stream;
     auto tl0 = std::chrono::steady_clock::now();
-    if (L.timed) HIPCHK(hipEventRecord(ev[0], S.stream));
-    HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                            S.d_arrive, (char*)S.d_out + L.slot * sizeof(PopOutHost), S.stream, S.placement,
-                            S.keys32 ? S.class_kf[cls] : KeyFormat{}));
-    if (L.timed) HIPCHK(hipEventRecord(ev[1], S.stream));
+    if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
+    void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
+    const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
+    if (ov) {
+        HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
+                                   S.d_cand_ov[seq & 1], S.d_arrive_ov[seq & 1], out, L.st, kf, S.d_link, seq));
+        S.ov_seq = seq;
+        S.ov_pending = true;
+    } else {
+        HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
+                                S.d_arrive, out, S.stream, S.placement, kf));
+    }
+    if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));
     S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
     return L;
 }
@@ -1155,7 +1209,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
             while (got < n_done && tag(load(got)) == L.epoch) ++got;
             if (got == n_done) break;
         }
-        if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(S.stream));  // long waits: runtime
+        if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(L.st));  // long waits: runtime
         if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
         __builtin_ia32_pause();
     }
@@ -1265,6 +1319,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             res_node = S.res_node_buf;
             res_kind = S.res_kind_buf;
         } else {
+            ov_quiesce(S);
             PopCtrl& h = *S.h_ctrl;
             h.stop = -1;
             h.n_done = 0;
@@ -1325,17 +1380,43 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
 // ---------------------------------------------------------------------------
 // allocate action with the Go framework's ordering (host mirror)
 // ---------------------------------------------------------------------------
+// Undo log of speculative heap operations: (heap items, position, old value);
+// position -1 records the old size.
+struct HeapJournal {
+    bool on = false;
+    struct Entry {
+        vector<int>* v;
+        int pos, val;
+    };
+    vector<Entry> e;
+    void rollback() {
+        for (auto it = e.rbegin(); it != e.rend(); ++it) {
+            if (it->pos < 0) it->v->resize(it->val);
+            else (*it->v)[it->pos] = it->val;
+        }
+        e.clear();
+    }
+};
+
 template <typename L>
-struct GoHeap {  // container/heap over util.PriorityQueue (util/priority_queue.go:25-88)
+struct GoHeap {  // Go container/heap (up/down exactly as heap.go), with an optional undo log
     vector<int> items;
     L less;
+    HeapJournal* jr = nullptr;
     explicit GoHeap(L l) : less(l) {}
     bool Less(int i, int j) { return less(items[i], items[j]); }
+    void swap_at(int i, int j) {
+        if (jr && jr->on) {
+            jr->e.push_back({&items, i, items[i]});
+            jr->e.push_back({&items, j, items[j]});
+        }
+        std::swap(items[i], items[j]);
+    }
     void up(int j) {
         for (;;) {
             int i = (j - 1) / 2;
             if (i == j || !Less(j, i)) break;
-            std::swap(items[i], items[j]);
+            swap_at(i, j);
             j = i;
         }
     }
@@ -1346,28 +1427,24 @@ struct GoHeap {  // container/heap over util.PriorityQueue (util/priority_queue.
             int j = j1, j2 = j1 + 1;
             if (j2 < n && Less(j2, j1)) j = j2;
             if (!Less(j, i)) break;
-            std::swap(items[i], items[j]);
+            swap_at(i, j);
             i = j;
         }
     }
-    void push(int x) { items.push_back(x); up((int)items.size() - 1); }
-    // The element pop() would return right after push(x), without changing
-    // the heap: x only if up() would carry it to the root.
-    int peek_push(int x) const {
-        int j = (int)items.size();
-        while (j > 0) {
-            const int i = (j - 1) / 2;
-            if (!less(x, items[i])) break;
-            j = i;
-        }
-        return j == 0 ? x : items[0];
+    void push(int x) {
+        if (jr && jr->on) jr->e.push_back({&items, -1, (int)items.size()});
+        items.push_back(x);
+        up((int)items.size() - 1);
     }
-    int top() const { return items[0]; }
     int pop() {
         int n = (int)items.size() - 1;
-        std::swap(items[0], items[n]);
+        swap_at(0, n);
         down(0, n);
         int x = items.back();
+        if (jr && jr->on) {  // rolled back in reverse: size first, then the slot
+            jr->e.push_back({&items, n, x});
+            jr->e.push_back({&items, -1, n + 1});
+        }
         items.pop_back();
         return x;
     }
@@ -1511,6 +1588,9 @@ struct Allocator {
         vector<int32_t> ids, onode;
         vector<uint8_t> okind;
         const int gm = S.gang_ready ? 1 : 0;
+        if (!S.ev_run[0]) { HIPCHK(hipEventCreate(&S.ev_run[0])); HIPCHK(hipEventCreate(&S.ev_run[1])); }
+        ov_quiesce(S);
+        HIPCHK(hipEventRecord(S.ev_run[0], S.stream));
         auto build_pending = [&](HJob& job) {  // allocate.go:91-104; TaskOrderFn is a strict total order
             if (job.pending_built) return;
             for (int t : job.tasks) {
@@ -1523,32 +1603,60 @@ struct Allocator {
             job.pending_built = true;
         };
 
-        // Speculation (DESIGN.md §4): while a batched pop runs, the host
-        // predicts the next pop — assuming this one places its tasks as
-        // Allocated up to the gang stop — with read-only peeks at the Go heaps,
-        // and queues that pop's launch behind it on the stream.  The next real
-        // pop uses the queued launch only if it is exactly the predicted one
-        // (job, first task, ready count, class, chunk), in which case the
-        // launch ran on exactly the device state the real pop sees; otherwise
-        // the launch is retracted (k_undo_pop) before anything else runs.
+        // Speculation (DESIGN.md §4.2): while a batched pop runs, the host
+        // predicts the next pops — assuming each places its tasks as Allocated
+        // up to the gang stop — by running the loop below on its own state with
+        // every change undone afterwards (heap operations through a journal,
+        // job / queue fields saved), and queues those pops' launches behind the
+        // running one.  The next real pop uses the oldest queued launch only if
+        // it is exactly that pop (job, first task, ready count, class, chunk),
+        // in which case the launch ran on exactly the device state the real pop
+        // sees; otherwise every queued launch is retracted (k_undo_pop) before
+        // anything else runs.
         struct Spec {
-            bool on = false;
             BatchLaunch L;
             int jb = -1;
             size_t cursor = 0;
             int ready = 0;
-        } spec;
-        auto discard = [&]() {
-            int nd = 0, st = 0;
-            int32_t node[kMaxChunk], kind[kMaxChunk];
-            collect_batched(S, spec.L, &nd, &st, node, kind);
-            HIPCHK(launch_undo_pop(S.nc, S.tab, spec.L.cls, nd, node, kind, S.stream));
-            spec.on = false;
-            S.stats.spec_missed++;
         };
-        // The pop after the current one (queue q, job jb, whose first chunk of m
-        // of its n remaining tasks is running).
-        auto speculate = [&](int q, int jb, int m, int n) {
+        std::deque<Spec> specs;  // launched predictions, oldest first
+        HeapJournal journal;
+        queues.jr = &journal;
+        for (auto& kv : jobs_map) kv.second.jr = &journal;
+        struct JobSave {
+            int jb, cnt;
+            size_t cur;
+            F3 drf;
+            double share;
+        };
+        struct QueueSave {
+            int q;
+            F3 alloc;
+            double share;
+        };
+        vector<JobSave> job_saves;
+        vector<QueueSave> queue_saves;
+        auto discard_all = [&]() {
+            if (specs.empty()) return;
+            vector<int32_t> node(specs.size() * kMaxChunk), kind(specs.size() * kMaxChunk);
+            vector<int> nd(specs.size());
+            for (size_t i = 0; i < specs.size(); ++i) {
+                int st = 0;
+                collect_batched(S, specs[i].L, &nd[i], &st, node.data() + i * kMaxChunk, kind.data() + i * kMaxChunk);
+            }
+            ov_quiesce(S);
+            for (size_t i = 0; i < specs.size(); ++i) {  // inverse updates commute
+                HIPCHK(launch_undo_pop(S.nc, S.tab, specs[i].L.cls, nd[i], node.data() + i * kMaxChunk,
+                                       kind.data() + i * kMaxChunk, S.stream));
+                S.stats.spec_missed++;
+            }
+            if (S.overlap) HIPCHK(hipStreamSynchronize(S.stream));  // overlapped pops are not ordered after it
+            specs.clear();
+        };
+        // The predicted outcome of pop (q, jb) whose first chunk of m of its n
+        // remaining tasks runs: k tasks Allocated, then the stop; -1 if the pop
+        // would continue past this chunk.  Saves what it changes.
+        auto apply_outcome = [&](int q, int jb, int m, int n) -> int {
             HJob& job = S.jobs[jb];
             int k, pstop;
             if (S.gang_ready) {  // gang.go:63-66: stop once #AllocatedStatuses >= MinAvailable
@@ -1556,57 +1664,98 @@ struct Allocator {
                 k = need <= 1 ? 1 : need;
                 if (k <= m) pstop = KBHIP_STOP_READY;
                 else if (m == n) { k = m; pstop = KBHIP_STOP_ALL; }
-                else return;  // the pop continues past this chunk
+                else return -1;
             } else {
                 k = 1;  // no JobReadyFn: always ready, one task per pop
                 pstop = KBHIP_STOP_READY;
             }
             HQueue& Q = S.queues[q];
-            const int sv_cnt = job.cnt_alloc;
-            const size_t sv_cur = job.cursor;
-            const F3 sv_drf = job.drf_alloc, sv_qa = Q.allocated;
-            const double sv_share = job.drf_share, sv_qs = Q.share;
-            job.cnt_alloc += k;  // the predicted outcome, undone below
-            job.cursor += k;
+            job_saves.push_back({jb, job.cnt_alloc, job.cursor, job.drf_alloc, job.drf_share});
+            queue_saves.push_back({q, Q.allocated, Q.share});
             for (int i = 0; i < k; ++i) {
-                const HPod& p = S.pods[job.pending[sv_cur + i]];
+                const HPod& p = S.pods[job.pending[job.cursor + i]];
                 if (S.drf_on) job.drf_alloc.add(p.req);
                 if (S.prop_on) Q.allocated.add(p.req);
             }
+            job.cnt_alloc += k;
+            job.cursor += k;
             if (S.drf_on) drf_update(job);
             if (S.prop_on) prop_update(Q);
-            int jb2 = -1, ready2 = 0, cls2 = -1, m2 = 0;
-            size_t cur2 = 0;
-            do {  // the loop below: jobs.Push(job) on READY, queues.Push(queue), queues.Pop(), ...
-                const int q2 = queues.peek_push(q);
-                if (overused(q2)) break;
-                auto jit2 = jobs_map.find(q2);
-                if (jit2 == jobs_map.end()) break;
-                if (q2 == q && pstop == KBHIP_STOP_READY) jb2 = jit2->second.peek_push(jb);
-                else if (!jit2->second.empty()) jb2 = jit2->second.top();
-                if (jb2 < 0) break;
-                HJob& j2 = S.jobs[jb2];
-                build_pending(j2);
-                cur2 = j2.cursor;
-                if (cur2 >= j2.pending.size()) { jb2 = -1; break; }  // an empty pop next
-                cls2 = S.pods[j2.pending[cur2]].cls;
-                const size_t rem = j2.pending.size() - cur2;
-                while ((size_t)m2 < rem && m2 < kMaxChunk && S.pods[j2.pending[cur2 + m2]].cls == cls2) ++m2;
-                ready2 = j2.cnt_alloc;
-                if (!batchable(S, cls2)) jb2 = -1;
-            } while (false);
-            job.cnt_alloc = sv_cnt;
-            job.cursor = sv_cur;
-            job.drf_alloc = sv_drf;
-            job.drf_share = sv_share;
-            Q.allocated = sv_qa;
-            Q.share = sv_qs;
-            if (jb2 < 0) return;
-            spec.L = launch_batched(S, cls2, m2, gm, S.jobs[jb2].min_avail, ready2);
-            spec.on = true;
-            spec.jb = jb2;
-            spec.cursor = cur2;
-            spec.ready = ready2;
+            return pstop;
+        };
+        struct Pred {
+            int q = -1, jb = -1, cls = -1, m = 0, n = 0, ready = 0;
+            size_t cur = 0;
+        };
+        // The loop's next pop after pop (q, jb) stopped with pstop (heaps
+        // changed through the journal); false when it is not a batched pop.
+        auto next_pop = [&](int q, int jb, int pstop, Pred* P) -> bool {
+            if (pstop == KBHIP_STOP_READY) jobs_map.at(q).push(jb);
+            queues.push(q);
+            const int q2 = queues.pop();
+            if (overused(q2)) return false;
+            auto jit2 = jobs_map.find(q2);
+            if (jit2 == jobs_map.end() || jit2->second.empty()) return false;
+            const int jb2 = jit2->second.pop();
+            HJob& j2 = S.jobs[jb2];
+            build_pending(j2);
+            const size_t cur2 = j2.cursor;
+            if (cur2 >= j2.pending.size()) return false;  // an empty pop next
+            const int cls2 = S.pods[j2.pending[cur2]].cls;
+            const size_t rem = j2.pending.size() - cur2;
+            int m2 = 0;
+            while ((size_t)m2 < rem && m2 < kMaxChunk && S.pods[j2.pending[cur2 + m2]].cls == cls2) ++m2;
+            if (!batchable(S, cls2)) return false;
+            *P = Pred{q2, jb2, cls2, m2, (int)rem, j2.cnt_alloc, cur2};
+            return true;
+        };
+        auto launch_pred = [&](const Pred& p) {
+            Spec sp;
+            sp.L = launch_batched(S, p.cls, p.m, gm, S.jobs[p.jb].min_avail, p.ready);
+            sp.jb = p.jb;
+            sp.cursor = p.cur;
+            sp.ready = p.ready;
+            specs.push_back(sp);
+        };
+        // Keep up to S.speculate predicted pops queued behind pop (q, jb).
+        auto speculate = [&](int q, int jb, int m, int n) {
+            Pred p[2];
+            int got = 0;
+            journal.on = true;
+            int ps = apply_outcome(q, jb, m, n);
+            if (ps >= 0 && next_pop(q, jb, ps, &p[0])) {
+                got = 1;
+                if (S.speculate >= 2) {
+                    ps = apply_outcome(p[0].q, p[0].jb, p[0].m, p[0].n);
+                    if (ps >= 0 && next_pop(p[0].q, p[0].jb, ps, &p[1])) got = 2;
+                }
+            }
+            journal.on = false;
+            journal.rollback();
+            for (auto it = job_saves.rbegin(); it != job_saves.rend(); ++it) {
+                HJob& j = S.jobs[it->jb];
+                j.cnt_alloc = it->cnt;
+                j.cursor = it->cur;
+                j.drf_alloc = it->drf;
+                j.drf_share = it->share;
+            }
+            for (auto it = queue_saves.rbegin(); it != queue_saves.rend(); ++it) {
+                HQueue& Q = S.queues[it->q];
+                Q.allocated = it->alloc;
+                Q.share = it->share;
+            }
+            job_saves.clear();
+            queue_saves.clear();
+            if (got == 0) return;
+            if (specs.empty()) {
+                launch_pred(p[0]);
+            } else {  // an earlier prediction of the next pop is queued: chain only behind an agreeing one
+                const Spec& s0 = specs.front();
+                if (s0.jb != p[0].jb || s0.cursor != p[0].cur || s0.ready != p[0].ready || s0.L.cls != p[0].cls ||
+                    s0.L.m != p[0].m)
+                    return;
+            }
+            if (got == 2 && specs.size() == 1) launch_pred(p[1]);
         };
         // One job pop through the device: the first chunk batched (possibly
         // already queued by speculation), the rest through place_job.
@@ -1618,15 +1767,16 @@ struct Allocator {
             const bool batch = batchable(S, cls0);
             bool have = false;
             BatchLaunch L;
-            if (spec.on) {
-                if (batch && spec.jb == jb && spec.cursor == job.cursor && spec.ready == job.cnt_alloc &&
-                    spec.L.cls == cls0 && spec.L.m == m) {
-                    L = spec.L;
+            if (!specs.empty()) {
+                const Spec& s0 = specs.front();
+                if (batch && s0.jb == jb && s0.cursor == job.cursor && s0.ready == job.cnt_alloc && s0.L.cls == cls0 &&
+                    s0.L.m == m) {
+                    L = s0.L;
                     have = true;
-                    spec.on = false;
+                    specs.pop_front();
                     S.stats.spec_hits++;
                 } else {
-                    discard();
+                    discard_all();
                 }
             }
             if (!batch) {
@@ -1634,7 +1784,7 @@ struct Allocator {
                 return;
             }
             if (!have) L = launch_batched(S, cls0, m, gm, job.min_avail, job.cnt_alloc);
-            if (S.speculate) speculate(q, jb, m, n);
+            if (S.speculate > 0) speculate(q, jb, m, n);
             int nd = 0, st = 0;
             collect_batched(S, L, &nd, &st, S.res_node_buf, S.res_kind_buf);
             if (st < 0) throw Error(KBHIP_EDEVICE, "device pop did not complete");
@@ -1642,7 +1792,7 @@ struct Allocator {
             for (int j = 0; j < nd; ++j) alloc += S.res_kind_buf[j] == 1;
             apply_results(S, ids.data(), nd, S.res_node_buf, S.res_kind_buf, onode.data(), okind.data());
             if (st == KBHIP_STOP_ALL && nd < n) {  // more chunks: the prediction assumed the pop ended here
-                if (spec.on) discard();
+                discard_all();
                 int32_t nd2 = 0, st2 = 0;
                 place_job(S, ids.data() + nd, n - nd, gm, job.min_avail, job.cnt_alloc + alloc, onode.data() + nd,
                           okind.data() + nd, &nd2, &st2);
@@ -1688,8 +1838,13 @@ struct Allocator {
             }
             queues.push(q);
         }
-        if (spec.on) discard();  // predicted a pop that never came
+        discard_all();  // predicted pops that never came
+        ov_quiesce(S);
+        HIPCHK(hipEventRecord(S.ev_run[1], S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
+        float dms = 0;
+        HIPCHK(hipEventElapsedTime(&dms, S.ev_run[0], S.ev_run[1]));
+        S.alloc_device_s += dms * 1e-3;
         S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
 };
@@ -1775,6 +1930,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
         HIPCHK(hipSetDevice(s->s.device));
         int rc = kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
                                   out_n_done, out_stop_reason);
+        kbhip::ov_quiesce(s->s);
         HIPCHK(hipStreamSynchronize(s->s.stream));
         return rc;
     })
@@ -1803,6 +1959,7 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
+        kbhip::ov_quiesce(s->s);
         s->s.log.clear();
         kbhip::backfill_run(s->s);
         const int64_t n = (int64_t)s->s.log.size();
@@ -1822,6 +1979,7 @@ int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
         const int N = S.nc.n;
         if (n_nodes < N) throw kbhip::Error(KBHIP_EINVAL, "output too small");
         HIPCHK(hipSetDevice(S.device));
+        kbhip::ov_quiesce(S);
         vector<int64_t> buf[9];
         int64_t* src[9] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem,
                            S.nc.rel_gpu, S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu};
@@ -1849,6 +2007,7 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out) {
         out->timed_launches = s->s.timed_n;
         out->host_launch_s = s->s.host_launch_s;
         out->host_wait_s = s->s.host_wait_s;
+        out->alloc_device_s = s->s.alloc_device_s;
         return KBHIP_OK;
     })
 }
@@ -1858,8 +2017,12 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
-        else if (std::strcmp(key, "speculate") == 0) s->s.speculate = value != 0;
+        else if (std::strcmp(key, "speculate") == 0) {
+            if (value < 0 || value > 2) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0, 1 or 2");
+            s->s.speculate = (int)value;
+        }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
+        else if (std::strcmp(key, "overlap") == 0) s->s.overlap = value != 0;
         else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
             kbhip::Session& S = s->s;
             S.debug_keys = value != 0;
@@ -1976,6 +2139,7 @@ int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t ca
             } else {
                 v.resize(n == "aff_cnt" ? S.n_aff_cnt : S.n_aff_scalar);
                 HIPCHK(hipSetDevice(S.device));
+                kbhip::ov_quiesce(s->s);
                 HIPCHK(hipStreamSynchronize(S.stream));
                 HIPCHK(hipMemcpy(v.data(), n == "aff_cnt" ? S.tab.aff_cnt : S.tab.aff_scalar, v.size() * 4,
                                  hipMemcpyDeviceToHost));

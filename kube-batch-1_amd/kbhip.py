@@ -41,7 +41,8 @@ class Stats(ctypes.Structure):
                 ("pops", ctypes.c_int64), ("tasks", ctypes.c_int64), ("placed", ctypes.c_int64),
                 ("sweeps", ctypes.c_int64), ("batched_pops", ctypes.c_int64), ("nodes", ctypes.c_int64),
                 ("timed_launches", ctypes.c_int64), ("host_launch_s", ctypes.c_double),
-                ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64)]
+                ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
+                ("alloc_device_s", ctypes.c_double)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

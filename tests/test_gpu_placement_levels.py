@@ -198,3 +198,52 @@ def test_keys32_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     p = str(tmp_path / "c4k.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     assert _log_opt(engine, p, keys32=1) == _log_opt(engine, p, keys32=0)
+
+
+# ---- overlapped pops (two streams, device-chained) x speculation depth -------
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(16))
+def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Every combination of overlap (0/1) and speculation depth (0/1/2) places
+    exactly as the oracle, including mispredicted pops retracted two deep."""
+    tiers = [None, [["drf", "proportion"]], [["gang"], ["predicates", "nodeorder"]],
+             [["priority", "gang", "drf"], ["predicates", "proportion", "nodeorder"]]][seed % 4]
+    c = kbgen_mod.gen_random(4900 + seed, n_nodes=3 + seed % 10, n_jobs=6 + seed % 9, max_tasks=2 + seed % 9,
+                             features=NO_POD_AFFINITY, tiers=tiers)
+    p = str(tmp_path / "o.kbs")
+    c.write(p)
+    exp = _oracle_log(oracle_mod, p)
+    for overlap in (0, 1):
+        for spec in (0, 1, 2):
+            assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
+
+
+@pytest.mark.gpu
+def test_overlap_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c2o.kbs")
+    kbgen_mod.gen_c2(p)
+    exp = _oracle_log(oracle_mod, p, fast=True)
+    assert _log_opt(engine, p, overlap=1, speculate=2) == exp
+    assert _log_opt(engine, p, overlap=0, speculate=2) == exp
+
+
+@pytest.mark.gpu
+def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
+    """Overlapped, two-deep speculative pops on a C4-shaped session equal one
+    pop at a time on one stream; the node state after the session too."""
+    p = str(tmp_path / "c4o.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
+    logs, nodes = [], []
+    for overlap, spec in ((1, 2), (1, 1), (0, 0)):
+        with engine.Session(p) as s:
+            s.set_option("overlap", overlap)
+            s.set_option("speculate", spec)
+            pod, node, kind = s.allocate()
+            st = s.stats()
+            nodes.append(s.read_nodes(20000))
+        logs.append([(int(a), int(b), int(k)) for a, b, k in zip(pod, node, kind)])
+        if spec:
+            assert st["spec_hits"] > st["spec_missed"]
+        assert st["alloc_device_s"] > 0
+    assert logs[0] == logs[1] == logs[2]
+    assert (nodes[0] == nodes[2]).all() and (nodes[1] == nodes[2]).all()
