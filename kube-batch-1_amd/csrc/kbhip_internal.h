@@ -47,15 +47,12 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
-// cand = of the last pop whose candidates are published; touched[e & 1] = the
-// 64 candidate nodes of pop e (-1: none).  Zero flags and all-(-1) touched
-// lists at session open.
+// touched[e & 1][i] = {e << 32 | node}, candidate i of pop e (node -1: none).
+// At session open: done 0, slot 0 tagged 0 with no nodes (pop 1 waits for nothing).
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
-    uint32_t cand;
-    uint32_t pad1[31];
-    int32_t touched[2][64];
+    uint64_t touched[2][64];
 };
 // Overlapped batched pop number `seq` (>= 1): waits on the device for pop
 // seq-1's candidates and write-back (launched before it, on another stream);

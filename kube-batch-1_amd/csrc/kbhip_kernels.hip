@@ -400,6 +400,54 @@ __device__ __forceinline__ uint64_t wave_max_key(uint64_t v) {
 // ---------------------------------------------------------------------------
 constexpr int kEntryIdxMax = (1 << 25) - 1;  // batched path: < 2^25 nodes
 
+// Node rows handed from one overlapped pop to the next (k_pop_batch_ov):
+// written with sc1 (write-through) stores, read with sc1 loads (L1 bypass),
+// the storing wave drained before the flag (MI355X_MICROARCH.md valid forms,
+// row 1) — no release / acquire fences on the pop-to-pop critical path.
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// load_row with the columns a batched placement writes read through sc1
+// (Backfilled, allocatable and MaxTaskNum never change on the batched path).
+__device__ __forceinline__ Row load_row_sc1(const NodeCols& nc, int n) {
+    Row r;
+    r.idle_cpu = ld_sc1(&nc.idle_cpu[n]); r.idle_mem = ld_sc1(&nc.idle_mem[n]); r.idle_gpu = ld_sc1(&nc.idle_gpu[n]);
+    r.rel_cpu = ld_sc1(&nc.rel_cpu[n]); r.rel_mem = ld_sc1(&nc.rel_mem[n]); r.rel_gpu = ld_sc1(&nc.rel_gpu[n]);
+    r.bf_cpu = nc.bf_cpu[n]; r.bf_mem = nc.bf_mem[n]; r.bf_gpu = nc.bf_gpu[n];
+    r.acpu = nc.acpu[n]; r.amem = nc.amem[n]; r.nzc = ld_sc1(&nc.nzc[n]); r.nzm = ld_sc1(&nc.nzm[n]);
+    r.pods = ld_sc1(&nc.pods[n]); r.maxtasks = nc.maxtasks[n];
+    return r;
+}
+template <bool SC1>
+__device__ __forceinline__ Row load_row_t(const NodeCols& nc, int n) {
+    if constexpr (SC1) return load_row_sc1(nc, n);
+    else return load_row(nc, n);
+}
+template <bool SC1>
+__device__ __forceinline__ uint64_t load_port_t(const NodeCols& nc, int w, int n) {
+    const uint64_t* p = nc.ports + (int64_t)w * nc.npad + n;
+    if constexpr (SC1) return ld_sc1(p);
+    else return *p;
+}
+// eval_node with the rows read through sc1.
+__device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                                  const NodeCols& nc, int n) {
+    const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+    const Row r = load_row_sc1(nc, n);
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, n);
+    int32_t s;
+    bool passed;
+    return dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+}
+
 __device__ __forceinline__ uint64_t level_entry(int32_t rm, int n, int d, uint64_t key) {
     return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
            ((uint64_t)(63 - d) << 1) | (key & 1);
@@ -557,9 +605,12 @@ __device__ __forceinline__ T readlane_t(T v, int l) {
 constexpr int kHash = 256;  // node index -> candidate lane (64 keys, open addressing)
 __device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 24); }
 
-template <typename ET>
+// SC1: rows read and written through sc1 (overlapped pops); the write-back is
+// then published as done = seq before the result stores.
+template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64]) {
+                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
+                               uint32_t seq = 0) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -578,9 +629,9 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     uint64_t pw[4] = {0, 0, 0, 0};
     int32_t na_n = 0;
     if (n >= 0) {
-        base = load_row(nc, n);
+        base = load_row_t<SC1>(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     uint64_t pwc[4];
@@ -693,13 +744,27 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         const int ap = s_apos[lane];
         const int na = cc < ap ? cc : ap;
         const Row r = apply_commits(base, c, na, cc - na);
-        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
-        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
-        nc.pods[n] = r.pods;
-        nc.nzc[n] = r.nzc;
-        nc.nzm[n] = r.nzm;
-        if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+        if constexpr (SC1) {
+            st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
+            st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
+            st_sc1(&nc.pods[n], r.pods);
+            st_sc1(&nc.nzc[n], r.nzc);
+            st_sc1(&nc.nzm[n], r.nzm);
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + n], pwc[w]);
+        } else {
+            nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+            nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+            nc.pods[n] = r.pods;
+            nc.nzc[n] = r.nzc;
+            nc.nzm[n] = r.nzm;
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+        }
+    }
+    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_sc1(done_flag, seq);
     }
     if (lane < done)
         __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_node(L, a) : -1),
@@ -933,15 +998,15 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
 // Overlapped batched pops (option "overlap").  Pop e runs while pop e-1
 // (launched on the other stream) may still be placing.  Every row a
 // placement writes belongs to one of its 64 candidates, which pop e-1
-// publishes (PopLink::touched, flag cand) as soon as its candidate list is
-// final — normally long before pop e's blocks finish evaluating.  Pop e's
-// sweep ranks every other node exactly (their rows are final) and leaves
-// pop e-1's candidates out; its final merger waits for pop e-1's write-back
-// (flag done), evaluates those candidates on their final rows and merges
-// them in: the top-64 of all nodes, as the non-overlapped kernel sees it.
-// Hand-offs: candidates and flag cand as sc1 stores drained by the storing
-// wave, sc1 loads after the poll (MI355X_MICROARCH.md valid forms, row 1);
-// rows behind an agent release / acquire pair around flag done.
+// publishes (PopLink::touched) as soon as its candidate list is final —
+// normally long before pop e's blocks finish evaluating.  Pop e's sweep ranks
+// every other node exactly (their rows are final) and leaves pop e-1's
+// candidates out; its final merger waits for pop e-1's write-back (done),
+// evaluates those candidates on their final rows and merges them in: the
+// top-64 of all nodes, as the non-overlapped kernel sees it.
+// Hand-offs: candidates as self-tagged 8-byte granules {seq, node} (one sc1
+// store each, no flag); rows as sc1 stores drained before the sc1 done flag,
+// read with sc1 loads (MI355X_MICROARCH.md valid forms, R2 and row 1).
 // ---------------------------------------------------------------------------
 template <typename KT>
 __device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
@@ -950,16 +1015,6 @@ __device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
 }
 
 constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
-
-// Poll an agent-scope flag until it reaches `want` (wrapping compare); false on timeout.
-__device__ __forceinline__ bool wait_flag(const uint32_t* f, uint32_t want) {
-    long spin = 0;
-    while ((int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-        if (++spin >= kLinkSpin) return false;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return true;
-}
 
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
@@ -973,18 +1028,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
-    const int prev = (seq - 1) & 1;
+    const uint32_t want = seq - 1;
+    const uint64_t* prev = link->touched[want & 1];
+    uint64_t tv = 0;
+    if (wave == 0) tv = ld_sc1(prev + lane);  // in flight while the rows below load
     for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
-    __syncthreads();
-    if (wave == 0) {  // pop seq-1's candidates (seq 1: none)
-        bool ok = true;
-        if (lane == 0) ok = wait_flag(&link->cand, seq - 1);
-        ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
-        const int x = __hip_atomic_load(&link->touched[prev][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (x >= base && x < base + R * kPopThreads) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
-        if (lane == 0) s_ok = ok;
-    }
-    // 1. evaluate R nodes per lane (pop seq-1's candidates left out), wave top-64, block top-64
+    // 1. evaluate R nodes per lane, then leave pop seq-1's candidates out
     KT keys[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -995,6 +1044,20 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             bool passed;
             keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed), a);
         }
+    }
+    __syncthreads();  // s_skip zeroed
+    int tn = -1;      // wave 0: pop seq-1's candidate `lane` (-1: none)
+    if (wave == 0) {
+        bool ok = true;
+        long spin = 0;
+        while (__ballot((uint32_t)(tv >> 32) != want) != 0) {  // not all published yet: re-read every granule
+            if (++spin >= kLinkSpin) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(2);
+            tv = ld_sc1(prev + lane);
+        }
+        tn = ok ? (int)(uint32_t)tv : -1;
+        if (tn >= base && tn < base + R * kPopThreads) atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
+        if (lane == 0) s_ok = ok;
     }
     __syncthreads();
     KT best = 0;
@@ -1052,48 +1115,34 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     block_tree_merge(wlk, wave, lane);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // 3. pop seq-1's write-back (consumer: relaxed poll, agent acquire, vmcnt
-    // wait, barrier, plain loads); its candidates on their final rows
+    // 3. pop seq-1's write-back (relaxed sc1 poll; every row load below is sc1)
     if (threadIdx.x == 0) {
-        s_ok = s_ok && wait_flag(&link->done, seq - 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bool ok = s_ok;
+        long spin = 0;
+        while (ok && (int32_t)(ld_sc1(&link->done) - want) < 0) {
+            if (++spin >= kLinkSpin) ok = false;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        s_ok = ok;
     }
     __syncthreads();
     const bool ok = s_ok;
     if (wave == 0) {
-        const int tn = ok ? link->touched[prev][lane] : -1;
-        KT e = 0;
-        if (tn >= 0) {
-            int32_t s;
-            bool passed;
-            e = sweep_key<KT>(eval_node(cf, c, t, nc, tn, &s, &passed), a);
-        }
+        const KT e = (ok && tn >= 0) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn), a) : (KT)0;
         const KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e));
-        // publish this pop's candidates (sc1 stores, drained, then the sc1 flag)
-        __hip_atomic_store(&link->touched[seq & 1][lane], (ok && top) ? key_node(top, a) : -1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) __hip_atomic_store(&link->cand, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // this pop's candidates, one self-tagged granule each
+        st_sc1(&link->touched[seq & 1][lane],
+               ((uint64_t)seq << 32) | (uint32_t)((ok && top) ? key_node(top, a) : -1));
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
     __syncthreads();
     if (ok) {
-        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl);
-        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl);
-    } else if (wave == 0 && lane == 0) {  // broken chain: n_done = 0 tells the host
+        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);
+        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);
+    } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
+        st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    // 4. publish this pop's write-back (producer: the storing wave's vmcnt
-    // wait, agent release, vmcnt wait, relaxed flag store)
-    if (wave == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&link->done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
     }
 }
 

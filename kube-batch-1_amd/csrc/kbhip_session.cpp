@@ -1008,9 +1008,12 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, 9 * 32 * sizeof(uint32_t), st));
         }
         S.d_link = S.b_link.alloc<PopLink>(1);
-        HIPCHK(hipMemsetAsync(S.d_link, 0xff, sizeof(PopLink), st));  // touched lists: -1
-        HIPCHK(hipMemsetAsync(&S.d_link->done, 0, sizeof(uint32_t), st));  // flags 0: pop 1 waits for nothing
-        HIPCHK(hipMemsetAsync(&S.d_link->cand, 0, sizeof(uint32_t), st));
+        {
+            PopLink init{};  // done 0; candidates of "pop 0": none, tagged 0
+            for (auto& slot : init.touched)
+                for (auto& g : slot) g = 0xffffffffull;
+            HIPCHK(hipMemcpy(S.d_link, &init, sizeof(PopLink), hipMemcpyHostToDevice));
+        }
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
         HIPCHK(hipHostMalloc((void**)&S.h_out, Session::kSlots * sizeof(PopOutHost),
                              hipHostMallocMapped | hipHostMallocCoherent));
