@@ -56,10 +56,11 @@ def parse():
                          "overlapped pipeline, so the roofline uses each session's device span instead)")
     ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2),
                     help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels")
-    ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2),
+    ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
                     help="predicted job pops queued ahead of the running one")
-    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
-                    help="1 = overlapped batched pops (two streams, device-side chaining)")
+    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2, 3),
+                    help="k > 0: batched pops rotate over k + 1 streams, up to k beside each other "
+                         "(device-side chaining); 0 = one pop kernel at a time")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
                     help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
                          "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")

@@ -134,13 +134,14 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;
- * "speculate" = 2 (default) lets kbhip_allocate queue the two predicted next
- * job pops behind the running one, 1 the next one only (used only if exactly
- * the next pop, retracted on device otherwise; placements are unchanged),
- * 0 = one pop at a time;
- * "overlap" = 1 (default; placement 2) runs consecutive batched pops on two
- * streams, the next pop's sweep overlapping the running pop's placement,
- * chained on the device; 0 = one stream, one pop kernel at a time;
+ * "speculate" = 2 (default) lets kbhip_allocate queue up to that many
+ * predicted next job pops behind the running one (0..3; each used only if it
+ * is exactly the next pop, retracted on device otherwise: placements are
+ * unchanged), 0 = one pop at a time;
+ * "overlap" = 1 (default; placement 2) rotates batched pops over overlap + 1
+ * streams so that up to `overlap` of them run beside each other (a pop's
+ * sweep during the previous pops' placement), chained on the device (0..3;
+ * 0 = one stream, one pop kernel at a time);
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);

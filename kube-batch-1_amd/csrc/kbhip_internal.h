@@ -47,21 +47,24 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
-// touched[e & 1][i] = {e << 32 | node}, candidate i of pop e (node -1: none).
-// At session open: done 0, slot 0 tagged 0 with no nodes (pop 1 waits for nothing).
+// touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
+// -1: none).  At session open: done 0, every slot tagged 0 with no nodes.
+constexpr int kMaxDep = 3;     // previous pops an overlapped pop may run beside (streams - 1)
+constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
-    uint64_t touched[2][64];
+    uint64_t touched[kLinkSlots][64];
 };
-// Overlapped batched pop number `seq` (>= 1): waits on the device for pop
-// seq-1's candidates and write-back (launched before it, on another stream);
-// cand holds (blocks + 8) * 64 keys, arrive 9 * 32 counters, both private to the
-// launch's stream parity.
+// Overlapped batched pop number `seq` (>= 1) on stream st; pops seq-1 ..
+// seq-ndep may still run on other streams (1 <= ndep <= kMaxDep): it leaves
+// their candidates out of its sweep and re-evaluates them once pop seq-1's
+// write-back is done.  cand holds (blocks + 8) * 64 keys, arrive 9 * 32
+// counters, both private to the launch's stream.
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq);
+                               uint32_t seq, int ndep);
 // Inverse node updates of a batched pop's placements (a retracted prediction).
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

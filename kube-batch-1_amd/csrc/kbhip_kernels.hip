@@ -1019,7 +1019,7 @@ constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends 
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                              PopLink* link, uint32_t seq) {
+                                                              PopLink* link, uint32_t seq, int ndep) {
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
@@ -1028,10 +1028,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
-    const uint32_t want = seq - 1;
-    const uint64_t* prev = link->touched[want & 1];
-    uint64_t tv = 0;
-    if (wave == 0) tv = ld_sc1(prev + lane);  // in flight while the rows below load
+    // the ndep pops before this one may still be writing rows: seq-1 .. seq-ndep
+    uint64_t tv[kMaxDep] = {};
+#pragma unroll
+    for (int k = 0; k < kMaxDep; ++k)  // in flight while the rows below load
+        if (wave == 0 && k < ndep && seq > (uint32_t)(k + 1))
+            tv[k] = ld_sc1(&link->touched[(seq - 1 - k) % kLinkSlots][lane]);
     for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
     // 1. evaluate R nodes per lane, then leave pop seq-1's candidates out
     KT keys[R];
@@ -1046,17 +1048,24 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
     }
     __syncthreads();  // s_skip zeroed
-    int tn = -1;      // wave 0: pop seq-1's candidate `lane` (-1: none)
+    int tn[kMaxDep];  // wave 0: candidate `lane` of pop seq-1-k (-1: none)
     if (wave == 0) {
         bool ok = true;
-        long spin = 0;
-        while (__ballot((uint32_t)(tv >> 32) != want) != 0) {  // not all published yet: re-read every granule
-            if (++spin >= kLinkSpin) { ok = false; break; }
-            __builtin_amdgcn_s_sleep(2);
-            tv = ld_sc1(prev + lane);
+#pragma unroll
+        for (int k = 0; k < kMaxDep; ++k) {
+            tn[k] = -1;
+            if (k >= ndep || seq <= (uint32_t)(k + 1)) continue;
+            const uint32_t want = seq - 1 - k;
+            long spin = 0;
+            while (ok && __ballot((uint32_t)(tv[k] >> 32) != want) != 0) {  // re-read every granule
+                if (++spin >= kLinkSpin) ok = false;
+                __builtin_amdgcn_s_sleep(2);
+                tv[k] = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+            }
+            const int x = ok ? (int)(uint32_t)tv[k] : -1;
+            tn[k] = x;
+            if (x >= base && x < base + R * kPopThreads) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
         }
-        tn = ok ? (int)(uint32_t)tv : -1;
-        if (tn >= base && tn < base + R * kPopThreads) atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
         if (lane == 0) s_ok = ok;
     }
     __syncthreads();
@@ -1109,17 +1118,18 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         __syncthreads();
         if (!role) return;
     }
-    // 2b. last group merger: the top-64 of every node but pop seq-1's candidates
+    // 2b. last group merger: the top-64 of every node but the previous pops' candidates
     wlk[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : (KT)0;
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // 3. pop seq-1's write-back (relaxed sc1 poll; every row load below is sc1)
+    // 3. pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
+    // every row load below is sc1); their candidates on their final rows
     if (threadIdx.x == 0) {
         bool ok = s_ok;
         long spin = 0;
-        while (ok && (int32_t)(ld_sc1(&link->done) - want) < 0) {
+        while (ok && (int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0) {
             if (++spin >= kLinkSpin) ok = false;
             __builtin_amdgcn_s_sleep(2);
         }
@@ -1128,10 +1138,20 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     const bool ok = s_ok;
     if (wave == 0) {
-        const KT e = (ok && tn >= 0) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn), a) : (KT)0;
-        const KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e));
+        KT top = wlk[0][lane];
+#pragma unroll
+        for (int k = 0; k < kMaxDep; ++k) {
+            if (k >= ndep) break;
+            bool dup = false;  // a node among several pops' candidates counts once
+#pragma unroll
+            for (int j = 0; j < k; ++j)
+                for (uint64_t mm = __ballot(tn[j] >= 0); mm; mm &= mm - 1)
+                    dup = dup || tn[k] == __builtin_amdgcn_readlane(tn[j], __ffsll((unsigned long long)mm) - 1);
+            const KT e = (ok && tn[k] >= 0 && !dup) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn[k]), a) : (KT)0;
+            top = wave_merge_desc(top, wave_sort_desc(e));
+        }
         // this pop's candidates, one self-tagged granule each
-        st_sc1(&link->touched[seq & 1][lane],
+        st_sc1(&link->touched[seq % kLinkSlots][lane],
                ((uint64_t)seq << 32) | (uint32_t)((ok && top) ? key_node(top, a) : -1));
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
@@ -1238,9 +1258,10 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 template <typename KT>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
-                                  uint32_t seq, hipStream_t st) {
-#define KBHIP_OV(RR) \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, link, seq)
+                                  uint32_t seq, int ndep, hipStream_t st) {
+#define KBHIP_OV(RR)                                                                                              \
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
+                       link, seq, ndep)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1254,14 +1275,15 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq) {
+                               uint32_t seq, int ndep) {
+    if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
     return hipGetLastError();
 }
 

@@ -190,23 +190,24 @@ struct Session {
     DevBuf b_cand2, b_arrive;
     uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
-    // option "overlap" (default on, placement 2): batched pops alternate between
-    // two streams and chain on the device (k_pop_batch_ov, PopLink)
+    // option "overlap" = k (placement 2): batched pops rotate over k + 1
+    // streams, up to k of them beside each other, chained on the device
+    // (k_pop_batch_ov, PopLink); 0 = one stream, one pop kernel at a time
 #ifdef KBHIP_STAMPS
-    bool overlap = false;       // stamps are written by k_pop_batch only
+    int overlap = 0;            // stamps are written by k_pop_batch only
 #else
-    bool overlap = true;
-#endif
-    hipStream_t stream_b = nullptr;
-    DevBuf b_cand_ov[2], b_arrive_ov[2], b_link;
-    uint64_t* d_cand_ov[2] = {nullptr, nullptr};
-    uint32_t* d_arrive_ov[2] = {nullptr, nullptr};
+    int overlap = 1;            // deeper rotations measured slower at C4 (the sweep of pop e waits
+#endif                          // for pop e-1's candidates, so k > 1 adds merge latency to the chain)
+    hipStream_t ov_streams[kMaxDep + 1] = {};  // [0] is `stream`
+    DevBuf b_cand_ov[kMaxDep + 1], b_arrive_ov[kMaxDep + 1], b_link;
+    uint64_t* d_cand_ov[kMaxDep + 1] = {};
+    uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
     bool ov_pending = false;    // an overlapped pop may still run on either stream
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
-    static constexpr int kSlots = 4;  // result slots: up to 3 batched pops in flight
+    static constexpr int kSlots = 8;  // result slots: up to 1 + speculate batched pops in flight
     uint32_t slot_epoch[kSlots] = {};  // granule tags per result slot
     int next_slot = 0;                // slot of the next batched launch (round robin)
     hipEvent_t evb[kSlots][2] = {};   // per-slot HIP-event pairs (sampled launch timing)
@@ -215,7 +216,7 @@ struct Session {
 #ifdef KBHIP_STAMPS
     int speculate = 0;                // stamps are read per launch: no overlapped launches
 #else
-    int speculate = 2;                // predicted pops queued ahead of the running one (0..2)
+    int speculate = 2;                // predicted pops queued ahead of the running one (0..3)
 #endif
     int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
 #ifdef KBHIP_STAMPS
@@ -263,7 +264,8 @@ struct Session {
             if (e) (void)hipEventDestroy(e);
         if (h_ctrl) (void)hipHostFree(h_ctrl);
         if (h_out) (void)hipHostFree(h_out);
-        if (stream_b) { (void)hipStreamSynchronize(stream_b); (void)hipStreamDestroy(stream_b); }
+        for (int k = 1; k <= kMaxDep; ++k)
+            if (ov_streams[k]) { (void)hipStreamSynchronize(ov_streams[k]); (void)hipStreamDestroy(ov_streams[k]); }
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -872,7 +874,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         HIPCHK(hipSetDevice(device));
         S.device = device;
         HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&S.stream_b, hipStreamNonBlocking));
+        S.ov_streams[0] = S.stream;
+        for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamCreateWithFlags(&S.ov_streams[k], hipStreamNonBlocking));
     }
     mark("classes");
     // ---------------- upload ----------------
@@ -1002,7 +1005,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
         S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k <= kMaxDep; ++k) {
             S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
             S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>(9 * 32);
             HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, 9 * 32 * sizeof(uint32_t), st));
@@ -1143,7 +1146,7 @@ struct BatchLaunch {
 // an overlapped pop, which the device chain does not order).
 static void ov_quiesce(Session& S) {
     if (!S.ov_pending) return;
-    HIPCHK(hipStreamSynchronize(S.stream_b));
+    for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
     S.ov_pending = false;
 }
@@ -1172,17 +1175,18 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     S.sweep_launches++;
     hipEvent_t* ev = S.evb[L.slot];
     if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
-    const bool ov = S.overlap && S.placement == 2;
+    const bool ov = S.overlap > 0 && S.placement == 2;
     if (!ov) ov_quiesce(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
-    L.st = (ov && (seq & 1)) ? S.stream_b : S.stream;
+    const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
+    L.st = S.ov_streams[si];
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
     const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
     if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
-                                   S.d_cand_ov[seq & 1], S.d_arrive_ov[seq & 1], out, L.st, kf, S.d_link, seq));
+                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap));
         S.ov_seq = seq;
         S.ov_pending = true;
     } else {
@@ -1653,7 +1657,7 @@ struct Allocator {
                                        kind.data() + i * kMaxChunk, S.stream));
                 S.stats.spec_missed++;
             }
-            if (S.overlap) HIPCHK(hipStreamSynchronize(S.stream));  // overlapped pops are not ordered after it
+            if (S.overlap > 0) HIPCHK(hipStreamSynchronize(S.stream));  // overlapped pops are not ordered after it
             specs.clear();
         };
         // The predicted outcome of pop (q, jb) whose first chunk of m of its n
@@ -1722,16 +1726,17 @@ struct Allocator {
         };
         // Keep up to S.speculate predicted pops queued behind pop (q, jb).
         auto speculate = [&](int q, int jb, int m, int n) {
-            Pred p[2];
+            Pred p[3];
             int got = 0;
             journal.on = true;
-            int ps = apply_outcome(q, jb, m, n);
-            if (ps >= 0 && next_pop(q, jb, ps, &p[0])) {
-                got = 1;
-                if (S.speculate >= 2) {
-                    ps = apply_outcome(p[0].q, p[0].jb, p[0].m, p[0].n);
-                    if (ps >= 0 && next_pop(p[0].q, p[0].jb, ps, &p[1])) got = 2;
-                }
+            for (int cq = q, cjb = jb, cm = m, cn = n; got < S.speculate && got < 3;) {
+                const int ps = apply_outcome(cq, cjb, cm, cn);
+                if (ps < 0 || !next_pop(cq, cjb, ps, &p[got])) break;
+                cq = p[got].q;
+                cjb = p[got].jb;
+                cm = p[got].m;
+                cn = p[got].n;
+                ++got;
             }
             journal.on = false;
             journal.rollback();
@@ -1749,16 +1754,15 @@ struct Allocator {
             }
             job_saves.clear();
             queue_saves.clear();
-            if (got == 0) return;
-            if (specs.empty()) {
-                launch_pred(p[0]);
-            } else {  // an earlier prediction of the next pop is queued: chain only behind an agreeing one
-                const Spec& s0 = specs.front();
-                if (s0.jb != p[0].jb || s0.cursor != p[0].cur || s0.ready != p[0].ready || s0.L.cls != p[0].cls ||
-                    s0.L.m != p[0].m)
+            // queued predictions are the oldest ones: chain only behind agreeing ones
+            for (size_t i = 0; i < specs.size(); ++i) {
+                if ((int)i >= got) return;
+                const Spec& s0 = specs[i];
+                if (s0.jb != p[i].jb || s0.cursor != p[i].cur || s0.ready != p[i].ready || s0.L.cls != p[i].cls ||
+                    s0.L.m != p[i].m)
                     return;
             }
-            if (got == 2 && specs.size() == 1) launch_pred(p[1]);
+            for (int i = (int)specs.size(); i < got; ++i) launch_pred(p[i]);
         };
         // One job pop through the device: the first chunk batched (possibly
         // already queued by speculation), the rest through place_job.
@@ -2021,11 +2025,18 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
         else if (std::strcmp(key, "speculate") == 0) {
-            if (value < 0 || value > 2) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0, 1 or 2");
+            if (value < 0 || value > 3) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0..3");
             s->s.speculate = (int)value;
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
-        else if (std::strcmp(key, "overlap") == 0) s->s.overlap = value != 0;
+        else if (std::strcmp(key, "overlap") == 0) {
+            if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0..3");
+            if (!s->s.encode_only) {
+                HIPCHK(hipSetDevice(s->s.device));
+                kbhip::ov_quiesce(s->s);  // the stream rotation changes
+            }
+            s->s.overlap = (int)value;
+        }
         else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
             kbhip::Session& S = s->s;
             S.debug_keys = value != 0;

@@ -204,8 +204,8 @@ def test_keys32_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(16))
 def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """Every combination of overlap (0/1) and speculation depth (0/1/2) places
-    exactly as the oracle, including mispredicted pops retracted two deep."""
+    """Overlap depths 0..3 with speculation depths 0..3 place exactly as the
+    oracle, including mispredicted pops retracted several deep."""
     tiers = [None, [["drf", "proportion"]], [["gang"], ["predicates", "nodeorder"]],
              [["priority", "gang", "drf"], ["predicates", "proportion", "nodeorder"]]][seed % 4]
     c = kbgen_mod.gen_random(4900 + seed, n_nodes=3 + seed % 10, n_jobs=6 + seed % 9, max_tasks=2 + seed % 9,
@@ -213,9 +213,8 @@ def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path,
     p = str(tmp_path / "o.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for overlap in (0, 1):
-        for spec in (0, 1, 2):
-            assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
+    for overlap, spec in ((0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (2, 3), (3, 3), (3, 1)):
+        assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
 @pytest.mark.gpu
@@ -223,8 +222,8 @@ def test_overlap_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2o.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    assert _log_opt(engine, p, overlap=1, speculate=2) == exp
-    assert _log_opt(engine, p, overlap=0, speculate=2) == exp
+    for overlap, spec in ((2, 3), (3, 3), (1, 2), (0, 2)):
+        assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
 @pytest.mark.gpu
@@ -234,7 +233,7 @@ def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     p = str(tmp_path / "c4o.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     logs, nodes = [], []
-    for overlap, spec in ((1, 2), (1, 1), (0, 0)):
+    for overlap, spec in ((2, 3), (3, 3), (1, 2), (0, 0)):
         with engine.Session(p) as s:
             s.set_option("overlap", overlap)
             s.set_option("speculate", spec)
@@ -245,5 +244,5 @@ def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
         if spec:
             assert st["spec_hits"] > st["spec_missed"]
         assert st["alloc_device_s"] > 0
-    assert logs[0] == logs[1] == logs[2]
-    assert (nodes[0] == nodes[2]).all() and (nodes[1] == nodes[2]).all()
+    assert all(lg == logs[-1] for lg in logs)
+    assert all((nd == nodes[-1]).all() for nd in nodes)
