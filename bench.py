@@ -148,10 +148,14 @@ def run_session(buf, device, time_every, shard=None, placement=0, overlap=1, spe
     s.set_option("placement", placement)
     s.set_option("overlap", overlap)
     s.set_option("speculate", speculate)
+    t1 = time.perf_counter()
     pod, node, kind = s.allocate(cap=1 << 21)
+    t2 = time.perf_counter()
     st = s.stats()
     s.close()
-    return time.perf_counter() - t0, len(pod), st
+    t3 = time.perf_counter()
+    st["phases_ms"] = {"open": (t1 - t0) * 1e3, "allocate": (t2 - t1) * 1e3, "close": (t3 - t2) * 1e3}
+    return t3 - t0, len(pod), st
 
 
 def cpu_baseline(path, target_s):
@@ -242,6 +246,7 @@ def main():
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
+                   "session_phases_ms": {k: round(v, 2) for k, v in st_last["phases_ms"].items()},
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},
         "roofline": {"kernel": "k_sweep_argmax" if shard else "k_pop_batch", "bound": "hbm", "achieved": achieved,

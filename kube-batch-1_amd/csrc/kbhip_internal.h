@@ -49,6 +49,7 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
 // -1: none).  At session open: done 0, every slot tagged 0 with no nodes.
+constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
 constexpr int kMaxDep = 3;     // previous pops an overlapped pop may run beside (streams - 1)
 constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
 struct PopLink {
@@ -59,8 +60,8 @@ struct PopLink {
 // Overlapped batched pop number `seq` (>= 1) on stream st; pops seq-1 ..
 // seq-ndep may still run on other streams (1 <= ndep <= kMaxDep): it leaves
 // their candidates out of its sweep and re-evaluates them once pop seq-1's
-// write-back is done.  cand holds (blocks + 8) * 64 keys, arrive 9 * 32
-// counters, both private to the launch's stream.
+// write-back is done.  cand holds (blocks + kMaxGroups) * 64 keys, arrive
+// (kMaxGroups + 1) * 32 counters, both private to the launch's stream.
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,

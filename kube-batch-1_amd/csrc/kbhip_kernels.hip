@@ -471,7 +471,11 @@ __device__ __forceinline__ T get_list(const T* src) {
     return __hip_atomic_load(src + (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr int kGroups = 8;        // second-level merge groups (blockIdx % 8)
+#ifndef KBHIP_GROUPS
+#define KBHIP_GROUPS 8
+#endif
+constexpr int kGroups = KBHIP_GROUPS;  // second-level merge groups (blockIdx % kGroups)
+static_assert(kGroups >= 1 && kGroups <= 32, "group lists and counters");
 constexpr int kCtrStride = 32;    // one counter per 128-byte line
 
 // Tree merge of the 8 per-wave lists in wl[] into wl[0] (all waves call).
@@ -846,7 +850,11 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     STAMP(gridDim.x * 4 + 4);
     // 2b. last group merger: merge the group lists; reset the counters for the next launch
-    wlk[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : (KT)0;
+    {
+        KT acc = 0;
+        for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
+        wlk[wave][lane] = acc;
+    }
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
     STAMP(gridDim.x * 4 + 0);
@@ -1026,6 +1034,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ int role, s_ok;
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
     // the ndep pops before this one may still be writing rows: seq-1 .. seq-ndep
@@ -1078,6 +1087,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     wlk[wave][lane] = best;
     __syncthreads();
+    STAMP(blockIdx.x * 4 + 1);
     block_tree_merge(wlk, wave, lane);
     const int nb = gridDim.x;
     const int g = blockIdx.x % kGroups;
@@ -1089,6 +1099,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    STAMP(blockIdx.x * 4 + 2);
     if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
     __syncthreads();
     if (!role) return;
@@ -1119,9 +1130,15 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         if (!role) return;
     }
     // 2b. last group merger: the top-64 of every node but the previous pops' candidates
-    wlk[wave][lane] = wave < n_groups ? get_list(gcand + (int64_t)wave * 64) : (KT)0;
+    STAMP(gridDim.x * 4 + 4);
+    {
+        KT acc = 0;
+        for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
+        wlk[wave][lane] = acc;
+    }
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
+    STAMP(gridDim.x * 4 + 0);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // 3. pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
@@ -1136,6 +1153,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         s_ok = ok;
     }
     __syncthreads();
+    STAMP(gridDim.x * 4 + 10);
     const bool ok = s_ok;
     if (wave == 0) {
         KT top = wlk[0][lane];
@@ -1156,6 +1174,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
     __syncthreads();
+    STAMP(gridDim.x * 4 + 1);
     if (ok) {
         if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);
         else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);

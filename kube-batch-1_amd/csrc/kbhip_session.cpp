@@ -22,9 +22,12 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
+#include <tuple>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -139,12 +142,117 @@ struct Plugin {
     std::map<string, string> args;
 };
 
-struct DevBuf {  // device memory, or host memory for encode-only sessions
+// Process-wide cache of device and pinned host allocations: a closed
+// session's buffers serve the next session's (hipMalloc / hipHostMalloc cost
+// up to milliseconds, hipFree synchronises the device).  A block is reused for
+// a request of at least half its size; at most kCap bytes stay cached.
+// KBHIP_NO_POOL=1 frees instead (diagnostic).
+class MemPool {
+  public:
+    enum Kind { kDevice = 0, kPinned = 1, kPinnedMapped = 2 };
+    static MemPool& get() {
+        static MemPool pool;
+        return pool;
+    }
+    // Returns a block of at least `bytes` on the current device; *cap_out = its size.
+    void* take(Kind kind, size_t bytes, size_t* cap_out) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (!off_) {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = free_.lower_bound(std::make_tuple(dev, (int)kind, bytes));
+            if (it != free_.end() && std::get<0>(it->first) == dev && std::get<1>(it->first) == (int)kind &&
+                std::get<2>(it->first) <= 2 * bytes) {
+                void* p = it->second;
+                *cap_out = std::get<2>(it->first);
+                cached_ -= *cap_out;
+                free_.erase(it);
+                return p;
+            }
+        }
+        void* p = nullptr;
+        hipError_t e = kind == kDevice ? hipMalloc(&p, bytes)
+                                       : hipHostMalloc(&p, bytes, kind == kPinned ? hipHostMallocDefault
+                                                                                   : hipHostMallocMapped |
+                                                                                         hipHostMallocCoherent);
+        if (e != hipSuccess) {  // drop the cache and retry once
+            trim();
+            e = kind == kDevice ? hipMalloc(&p, bytes)
+                                : hipHostMalloc(&p, bytes, kind == kPinned ? hipHostMallocDefault
+                                                                           : hipHostMallocMapped | hipHostMallocCoherent);
+            if (e != hipSuccess) throw Error(KBHIP_EDEVICE, kind == kDevice ? "hipMalloc failed" : "hipHostMalloc failed");
+        }
+        *cap_out = bytes;
+        return p;
+    }
+    void give(Kind kind, void* p, size_t cap, int dev) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!off_ && cached_ + cap <= kCap) {
+                free_.emplace(std::make_tuple(dev, (int)kind, cap), p);
+                cached_ += cap;
+                return;
+            }
+        }
+        release(kind, p);
+    }
+    // Non-blocking streams, reused likewise (hipStreamDestroy costs milliseconds).
+    hipStream_t take_stream() {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (!off_) {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = streams_.find(dev);
+            if (it != streams_.end()) {
+                hipStream_t st = it->second;
+                streams_.erase(it);
+                return st;
+            }
+        }
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess)
+            throw Error(KBHIP_ENODEV, "hipStreamCreate failed");
+        return st;
+    }
+    void give_stream(hipStream_t st, int dev) {  // st must be idle
+        if (!st) return;
+        if (off_) {
+            (void)hipStreamDestroy(st);
+            return;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        streams_.emplace(dev, st);
+    }
+    void trim() {
+        std::lock_guard<std::mutex> lk(mu_);
+        for (auto& kv : free_) release((Kind)std::get<1>(kv.first), kv.second);
+        free_.clear();
+        cached_ = 0;
+    }
+
+  private:
+    MemPool() : off_(std::getenv("KBHIP_NO_POOL") != nullptr) {}
+    static void release(Kind kind, void* p) {
+        if (kind == kDevice) (void)hipFree(p);
+        else (void)hipHostFree(p);
+    }
+    static constexpr size_t kCap = size_t(8) << 30;
+    std::mutex mu_;
+    std::multimap<std::tuple<int, int, size_t>, void*> free_;
+    std::multimap<int, hipStream_t> streams_;
+    size_t cached_ = 0;
+    const bool off_;
+};
+
+struct DevBuf {  // device memory (pooled), or host memory for encode-only sessions
     void* p = nullptr;
     bool host = false;
+    size_t cap = 0;
+    int dev = 0;
     ~DevBuf() { release(); }
     void release() {
-        if (p) { if (host) std::free(p); else (void)hipFree(p); }
+        if (p) { if (host) std::free(p); else MemPool::get().give(MemPool::kDevice, p, cap, dev); }
         p = nullptr;
     }
     template <typename T>
@@ -155,8 +263,9 @@ struct DevBuf {  // device memory, or host memory for encode-only sessions
         if (host) {
             p = std::calloc(1, bytes);
             if (!p) throw Error(KBHIP_EINVAL, "out of host memory");
-        } else if (hipMalloc(&p, bytes) != hipSuccess) {
-            throw Error(KBHIP_EDEVICE, "hipMalloc failed");
+        } else {
+            (void)hipGetDevice(&dev);
+            p = MemPool::get().take(MemPool::kDevice, bytes, &cap);
         }
         return (T*)p;
     }
@@ -187,6 +296,7 @@ struct Session {
         b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
     PopCtrl* d_ctrl = nullptr;
     PopCtrl* h_ctrl = nullptr;  // pinned
+    size_t h_ctrl_cap = 0, h_out_cap = 0;
     DevBuf b_cand2, b_arrive;
     uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
@@ -222,7 +332,7 @@ struct Session {
 #ifdef KBHIP_STAMPS
     DevBuf b_stamps;
     uint64_t* d_stamps = nullptr;
-    double phase[16] = {0};  // accumulated phase durations (us)
+    double phase[20] = {0};  // accumulated phase durations (us)
     int64_t phase_n = 0;
 #endif
     uint64_t* d_walk = nullptr;
@@ -253,21 +363,39 @@ struct Session {
     int n_spaces = 0;
     size_t n_aff_cnt = 0, n_aff_scalar = 0;  // table sizes (device sessions read them back for tests)
 
-    ~Session() {
+    // Device side of the teardown: drain the streams, then hand streams, pinned
+    // and device buffers back to the pool.  Idempotent.
+    void release_device() {
+        for (int k = 1; k <= kMaxDep; ++k)
+            if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
+        if (stream) (void)hipStreamSynchronize(stream);
         if (comm) (void)ncclCommDestroy(comm);
-        if (ev0) (void)hipEventDestroy(ev0);
-        if (ev1) (void)hipEventDestroy(ev1);
+        comm = nullptr;
+        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1]})
+            if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : evb)
             for (auto& e : pr)
-                if (e) (void)hipEventDestroy(e);
-        for (auto& e : ev_run)
-            if (e) (void)hipEventDestroy(e);
-        if (h_ctrl) (void)hipHostFree(h_ctrl);
-        if (h_out) (void)hipHostFree(h_out);
-        for (int k = 1; k <= kMaxDep; ++k)
-            if (ov_streams[k]) { (void)hipStreamSynchronize(ov_streams[k]); (void)hipStreamDestroy(ov_streams[k]); }
-        if (stream) (void)hipStreamDestroy(stream);
+                if (e) { (void)hipEventDestroy(e); e = nullptr; }
+        if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
+        if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
+        h_ctrl = nullptr;
+        h_out = nullptr;
+        for (int k = 1; k <= kMaxDep; ++k) MemPool::get().give_stream(ov_streams[k], device);
+        MemPool::get().give_stream(stream, device);
+        for (auto& st : ov_streams) st = nullptr;
+        stream = nullptr;
+        for (auto& b : b_cols) b.release();
+        for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
+                          &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
+                          &b_arrive, &b_link, &b_dbg})
+            b->release();
+        for (auto& b : b_cand_ov) b.release();
+        for (auto& b : b_arrive_ov) b.release();
+#ifdef KBHIP_STAMPS
+        b_stamps.release();
+#endif
     }
+    ~Session() { release_device(); }
 };
 
 // Table upload: HBM on the session stream, or a host copy for encode-only
@@ -873,9 +1001,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     } else {
         HIPCHK(hipSetDevice(device));
         S.device = device;
-        HIPCHK(hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking));
+        S.stream = MemPool::get().take_stream();
         S.ov_streams[0] = S.stream;
-        for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamCreateWithFlags(&S.ov_streams[k], hipStreamNonBlocking));
+        for (int k = 1; k <= kMaxDep; ++k) S.ov_streams[k] = MemPool::get().take_stream();
     }
     mark("classes");
     // ---------------- upload ----------------
@@ -997,18 +1125,18 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     hipStream_t st = S.stream;
     S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
-    HIPCHK(hipHostMalloc((void**)&S.h_ctrl, sizeof(PopCtrl), hipHostMallocDefault));
+    S.h_ctrl = (PopCtrl*)MemPool::get().take(MemPool::kPinned, sizeof(PopCtrl), &S.h_ctrl_cap);
     S.d_walk = S.b_walk.alloc<uint64_t>(npl);
     {
         int R2;
         const int nb2 = pop_blocks(nl, &R2);
-        S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
-        S.d_arrive = S.b_arrive.alloc<uint32_t>(9 * 32);
-        HIPCHK(hipMemsetAsync(S.d_arrive, 0, 9 * 32 * sizeof(uint32_t), st));
+        S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
+        S.d_arrive = S.b_arrive.alloc<uint32_t>((kMaxGroups + 1) * 32);
+        HIPCHK(hipMemsetAsync(S.d_arrive, 0, (kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         for (int k = 0; k <= kMaxDep; ++k) {
-            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + 8) * 64);
-            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>(9 * 32);
-            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, 9 * 32 * sizeof(uint32_t), st));
+            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
+            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((kMaxGroups + 1) * 32);
+            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
         S.d_link = S.b_link.alloc<PopLink>(1);
         {
@@ -1018,12 +1146,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             HIPCHK(hipMemcpy(S.d_link, &init, sizeof(PopLink), hipMemcpyHostToDevice));
         }
         if (sizeof(PopOutHost) != pop_out_bytes()) throw Error(KBHIP_EINVAL, "PopOut layout mismatch");
-        HIPCHK(hipHostMalloc((void**)&S.h_out, Session::kSlots * sizeof(PopOutHost),
-                             hipHostMallocMapped | hipHostMallocCoherent));
+        S.h_out = (PopOutHost*)MemPool::get().take(MemPool::kPinnedMapped, Session::kSlots * sizeof(PopOutHost),
+                                                   &S.h_out_cap);
         HIPCHK(hipHostGetDevicePointer(&S.d_out, S.h_out, 0));
         std::memset(S.h_out, 0, Session::kSlots * sizeof(PopOutHost));
 #ifdef KBHIP_STAMPS
         S.d_stamps = S.b_stamps.alloc<uint64_t>((size_t)nb2 * 4 + 16);
+        HIPCHK(hipMemsetAsync(S.d_stamps, 0, ((size_t)nb2 * 4 + 16) * 8, st));
         HIPCHK(set_stamp_buffer(S.d_stamps));
 #endif
     }
@@ -1259,7 +1388,11 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
         S.phase[2] += (tbm - t0) * 0.01;           // first block start -> every block list stored
         S.phase[3] += ((double)P[4] - (double)tbm) * 0.01;  // -> final merger starts
         S.phase[4] += (P[0] - P[4]) * 0.01;        // final merge
-        S.phase[5] += (P[1] - P[0]) * 0.01;        // chain precompute
+        if (P[10]) {                               // overlapped kernel: wait for the previous pop, patch
+            S.phase[15] += (P[10] - P[0]) * 0.01;
+            S.phase[16] += (P[1] - P[10]) * 0.01;
+        }
+        S.phase[5] += (P[1] - P[0]) * 0.01;        // chain precompute (overlapped: wait + patch)
         S.phase[6] += (P[2] - P[1]) * 0.01;        // placement loop
         S.phase[7] += (P[3] - P[2]) * 0.01;        // write back
         S.phase[8] += (P[3] - t0) * 0.01;          // total in-kernel span
@@ -2057,7 +2190,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
 #ifdef KBHIP_STAMPS
 int kbhip_debug_phases(kb_session* s, double* out, int n) {
     ABI_GUARD({
-        for (int i = 0; i < n && i < 16; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
+        for (int i = 0; i < n && i < 20; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
         return (int)s->s.phase_n;
     })
 }
@@ -2240,7 +2373,22 @@ int kbhip_debug_replay(kb_session* s, int32_t n_steps, const int32_t* pods, cons
 }
 int kbhip_session_close(kb_session* s) {
     ABI_GUARD({
-        delete s;
+        static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;
+        auto t0 = std::chrono::steady_clock::now();
+        if (s && !s->s.encode_only) {
+            (void)hipSetDevice(s->s.device);
+            s->s.release_device();
+        }
+        // The host model (millions of small objects) is freed off the caller's
+        // path; nothing of the device or the pool is touched there any more.
+        try {
+            std::thread([s]() { delete s; }).detach();
+        } catch (...) {
+            delete s;
+        }
+        if (prof)
+            std::fprintf(stderr, "[close] total      %8.2f ms\n",
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
         return KBHIP_OK;
     })
 }

@@ -15,7 +15,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "libkbhip.so")
+LIB_PATH = os.environ.get("KBHIP_LIB") or os.path.join(HERE, "_build", "libkbhip.so")  # KBHIP_LIB: tuning builds
 
 ALLOCATED, PIPELINED = 1, 2
 STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
