@@ -34,10 +34,10 @@
  * negative KBHIP_E* code on failure; nothing throws or aborts across the ABI.
  * kbhip_last_error() describes the last failure on the calling thread.
  * Inputs are caller-owned and copied; outputs are caller-allocated; the
- * session handle is engine-owned.  One session per calling thread.  The only
- * host thread the library starts is a short-lived one per kbhip_session_close
- * that frees the closed session's host-side model (device memory, pinned
- * buffers and streams go back to a process-wide pool before close returns).
+ * session handle is engine-owned.  One session per calling thread; the
+ * library starts no host threads of its own.  Device memory, pinned buffers
+ * and streams of a closed session go back to a process-wide pool and serve
+ * later sessions.
  *
  * The library has exactly one execution path: HIP on a gfx950 device.  With
  * no usable device every call fails with KBHIP_ENODEV; there is no CPU

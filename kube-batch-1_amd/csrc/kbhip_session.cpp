@@ -27,7 +27,7 @@
 #include <set>
 #include <stdexcept>
 #include <string>
-#include <thread>
+#include <string_view>
 #include <unordered_map>
 #include <vector>
 
@@ -115,8 +115,7 @@ struct HPod {
     int cls = -1;   // device task class (pending tasks)
     int node = -1;  // current node
 };
-struct HJob {
-    string uid;
+struct HJob {  // session jobs are numbered in UID order
     int queue = -1;
     int32_t min_avail = 0, priority = 0;
     int64_t ts = 0;
@@ -245,6 +244,25 @@ class MemPool {
     const bool off_;
 };
 
+// The one host array above glibc's mmap threshold (1M pods x 96 B): handed
+// from a closed session to the next, so its pages stay mapped (no page faults
+// at open, no munmap at close).
+template <typename T>
+struct SpareVec {
+    std::mutex mu;
+    vector<T> v;
+    void take(vector<T>& out) {
+        std::lock_guard<std::mutex> lk(mu);
+        out.swap(v);
+        v.clear();
+        out.clear();
+    }
+    void give(vector<T>& in) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (in.capacity() > v.capacity()) in.swap(v);
+    }
+};
+
 struct DevBuf {  // device memory (pooled), or host memory for encode-only sessions
     void* p = nullptr;
     bool host = false;
@@ -271,11 +289,15 @@ struct DevBuf {  // device memory (pooled), or host memory for encode-only sessi
     }
 };
 
+inline SpareVec<HPod>& spare_pods() {
+    static SpareVec<HPod> sp;
+    return sp;
+}
+
 struct Session {
     int device = 0;
     hipStream_t stream = nullptr;
     // host model
-    vector<string> node_names;
     vector<HPod> pods;
     vector<HJob> jobs;
     vector<HQueue> queues;
@@ -395,8 +417,13 @@ struct Session {
         b_stamps.release();
 #endif
     }
-    ~Session() { release_device(); }
+    ~Session();
 };
+
+Session::~Session() {
+    release_device();
+    spare_pods().give(pods);
+}
 
 // Table upload: HBM on the session stream, or a host copy for encode-only
 // sessions (kbhip_debug_encode / kbhip_debug_replay).
@@ -421,7 +448,8 @@ struct Encoder {
     vector<Term> terms;
     vector<int32_t> vals_list;
     vector<uint64_t> masks;
-    vector<vector<std::pair<int, int>>> node_labels;  // per node: (key id in keys_all, value id)
+    vector<int32_t> nl_off;                       // node labels, CSR: node i owns nl_kv[nl_off[i] .. nl_off[i+1])
+    vector<std::pair<int, int>> nl_kv;            // (key id in keys_all, value id)
     vector<std::tuple<string, string, string>> taint_defs;
     vector<std::tuple<int, int, int32_t>> port_defs;  // (ip id, proto id, port)
     std::map<std::tuple<int, int, int32_t>, int> port_ids;
@@ -511,19 +539,27 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     auto lk = V32("nl_key"), lv = V32("nl_val");
     auto toff = s.offs("n_taint_off", N);
     auto tk = V32("nt_key"), tv = V32("nt_val"), te = V32("nt_effect");
-    S.node_names.resize(N);
-    std::unordered_map<string, int> node_idx;
-    E.node_labels.resize(N);
+    std::unordered_map<std::string_view, int> node_idx;  // views into the snapshot's string table
+    node_idx.reserve((size_t)N * 2);
+    E.nl_off.assign(N + 1, 0);
+    E.nl_kv.clear();
+    E.nl_kv.reserve(lk.size());
+    std::unordered_map<int32_t, int> key_by_off, val_by_off;  // strtab offset -> dictionary id
     vector<vector<int>> node_taints(N);
     std::map<std::tuple<string, string, string>, int> taint_ids;
     std::unordered_map<int32_t, int> node_by_off;  // strtab offset of the name -> node (fast path)
     node_by_off.reserve((size_t)N * 2);
     for (int i = 0; i < N; ++i) {
-        S.node_names[i] = s.s(nname[i]);
-        node_idx[S.node_names[i]] = i;
+        node_idx.emplace(std::string_view(s.str(nname[i])), i);
         node_by_off.emplace(nname[i], i);
-        for (int k = loff[i]; k < loff[i + 1]; ++k)
-            E.node_labels[i].push_back({E.keys_all.get(s.s(lk[k])), E.vals.get(s.s(lv[k]))});
+        for (int k = loff[i]; k < loff[i + 1]; ++k) {
+            auto ki = key_by_off.find(lk[k]);
+            if (ki == key_by_off.end()) ki = key_by_off.emplace(lk[k], E.keys_all.get(s.s(lk[k]))).first;
+            auto vi = val_by_off.find(lv[k]);
+            if (vi == val_by_off.end()) vi = val_by_off.emplace(lv[k], E.vals.get(s.s(lv[k]))).first;
+            E.nl_kv.push_back({ki->second, vi->second});
+        }
+        E.nl_off[i + 1] = (int32_t)E.nl_kv.size();
         for (int k = toff[i]; k < toff[i + 1]; ++k) {
             string eff = s.s(te[k]);
             if (eff != "NoSchedule" && eff != "NoExecute") continue;  // predicates.go:1494-1497
@@ -573,6 +609,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
          paapref_c = acnt("a_paapref_cnt");
     (void)pareq_c; (void)papref_c; (void)paareq_c; (void)paapref_c;
 
+    spare_pods().take(S.pods);
     S.pods.resize(P);
     {  // UID ranks: the canonical order (kbsnap.h) makes them the index; sort otherwise
         bool sorted = true;
@@ -636,7 +673,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             if (ot != node_by_off.end()) {
                 p.node = ot->second;
             } else {
-                auto it = node_idx.find(s.s(pnode[i]));
+                auto it = node_idx.find(std::string_view(s.str(pnode[i])));
                 if (it == node_idx.end())
                     throw Error(KBHIP_EINVAL, "pod " + s.s(puid[i]) + " is bound to node " + s.s(pnode[i]) +
                                                   " which is not in the snapshot");
@@ -675,23 +712,57 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     auto jns = V32("j_ns"), jname = V32("j_name"), jq = V32("j_queue"), jmin = V32("j_min"), jpri = V32("j_pg_priority");
     auto jts = s.vec<int64_t>("j_ts");
-    struct Src { string uid; int row, pod; };
+    // Job UIDs: "namespace/name" of a PodGroup, the pod UID of a shadow one
+    // (cache/util.go:42-60); compared as those strings without building them.
+    struct Src {
+        const char* a;  // namespace, or the pod UID
+        const char* b;  // PodGroup name (after '/'), or nullptr
+        int row, pod;
+    };
+    auto src_less = [](const Src& x, const Src& y) {
+        const char *p = x.a, *q = y.a;
+        int sp = 0, sq = 0;  // part: 0 = a, 1 = '/', 2 = b, 3 = end
+        for (;;) {
+            if (sp == 0 && !*p) { sp = x.b ? 1 : 3; }
+            if (sq == 0 && !*q) { sq = y.b ? 1 : 3; }
+            if (sp == 2 && !*p) sp = 3;
+            if (sq == 2 && !*q) sq = 3;
+            const int cp = sp == 3 ? -1 : sp == 1 ? '/' : (unsigned char)*p;
+            const int cq = sq == 3 ? -1 : sq == 1 ? '/' : (unsigned char)*q;
+            if (cp != cq) return cp < cq;
+            if (cp < 0) return false;
+            if (sp == 1) { sp = 2; p = x.b; } else ++p;
+            if (sq == 1) { sq = 2; q = y.b; } else ++q;
+        }
+    };
     vector<Src> srcs;
-    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
+    srcs.reserve(jns.size() + 64);
+    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.str(jns[j]), s.str(jname[j]), (int)j, -1});
     for (int i = 0; i < P; ++i) {
         if (pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
-        if (pjob[i] < 0) srcs.push_back({s.s(puid[i]), -1, i});  // shadow PodGroup (cache/util.go:42-60)
+        if (pjob[i] < 0) srcs.push_back({s.str(puid[i]), nullptr, -1, i});  // shadow PodGroup
     }
-    std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+    if (!std::is_sorted(srcs.begin(), srcs.end(), src_less)) std::stable_sort(srcs.begin(), srcs.end(), src_less);
     vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
+    std::unordered_map<int32_t, int> q_by_off;  // strtab offset of a job's queue name -> queue (-1: none)
+    const auto default_q = qidx.find("default");
     for (auto& src : srcs) {
-        string qname = src.row >= 0 ? s.s(jq[src.row]) : string("default");
-        auto qit = qidx.find(qname);
+        std::map<string, int>::const_iterator qit;
+        int qslot = -1;
+        if (src.row >= 0) {
+            auto qo = q_by_off.find(jq[src.row]);
+            if (qo == q_by_off.end()) {
+                qit = qidx.find(s.s(jq[src.row]));
+                qo = q_by_off.emplace(jq[src.row], qit == qidx.end() ? -1 : qit->second).first;
+            }
+            qslot = qo->second;
+        } else {
+            qslot = default_q == qidx.end() ? -1 : default_q->second;
+        }
         int slot = -1;
-        if (qit != qidx.end()) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
+        if (qslot >= 0) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
             HJob j;
-            j.uid = src.uid;
-            j.queue = qit->second;
+            j.queue = qslot;
             j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
             j.ts = src.row >= 0 ? jts[src.row] : 0;
             j.priority = src.row >= 0 ? jpri[src.row] : 0;
@@ -701,10 +772,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
     }
-    for (int i = 0; i < P; ++i) {
-        int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
-        S.pods[i].job = slot;
-        if (slot >= 0) S.jobs[slot].tasks.push_back(i);
+    {
+        vector<int32_t> ntask(S.jobs.size(), 0);
+        for (int i = 0; i < P; ++i) {
+            int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
+            S.pods[i].job = slot;
+            if (slot >= 0) ntask[slot]++;
+        }
+        for (size_t j = 0; j < S.jobs.size(); ++j) S.jobs[j].tasks.reserve(ntask[j]);
+        for (int i = 0; i < P; ++i)
+            if (S.pods[i].job >= 0) S.jobs[S.pods[i].job].tasks.push_back(i);
     }
     for (auto& j : S.jobs)
         for (int t : j.tasks) {
@@ -1039,8 +1116,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (kit == E.keys_all.ids.end()) continue;  // no node has the key
         int kid = kit->second;
         for (int i = lo; i < hi; ++i)
-            for (auto& lv2 : E.node_labels[i])
-                if (lv2.first == kid) lab[(size_t)kv.second * npl + (i - lo)] = lv2.second;
+            for (int q = E.nl_off[i]; q < E.nl_off[i + 1]; ++q)
+                if (E.nl_kv[q].first == kid) lab[(size_t)kv.second * npl + (i - lo)] = E.nl_kv[q].second;
     }
     S.nc.labels = upload(S, S.b_labels, lab);
     vector<uint64_t> tcol((size_t)std::max(E.tw, 1) * npl, 0);
@@ -1628,7 +1705,7 @@ struct Allocator {
             } else c = L.drf_share == R.drf_share ? 0 : L.drf_share < R.drf_share ? -1 : 1;  // drf.go:113-129
             if (c != 0) return c < 0;
         }
-        if (L.ts == R.ts) return L.uid < R.uid;
+        if (L.ts == R.ts) return l < r;  // UID order: jobs are numbered in UID order at open
         return L.ts < R.ts;
     }
     bool queue_less(int l, int r) const {  // session_plugins.go:270-295, proportion.go:144-157
@@ -2379,13 +2456,7 @@ int kbhip_session_close(kb_session* s) {
             (void)hipSetDevice(s->s.device);
             s->s.release_device();
         }
-        // The host model (millions of small objects) is freed off the caller's
-        // path; nothing of the device or the pool is touched there any more.
-        try {
-            std::thread([s]() { delete s; }).detach();
-        } catch (...) {
-            delete s;
-        }
+        delete s;  // the host model: freeing it on another thread measured slower (contention with the next open)
         if (prof)
             std::fprintf(stderr, "[close] total      %8.2f ms\n",
                          std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
