@@ -609,12 +609,38 @@ __device__ __forceinline__ T readlane_t(T v, int l) {
 constexpr int kHash = 256;  // node index -> candidate lane (64 keys, open addressing)
 __device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 24); }
 
+// Rows of the nodes a placement may use, gathered before it starts (LDS):
+// the overlapped pop loads them while it waits for the previous pop, so the
+// placement reads no node row from memory.  Slot lookup by node index.
+constexpr int kRcSlots = 128;
+struct RowCache {
+    Row row[kRcSlots];
+    uint64_t pw[kRcSlots][4];
+    int32_t na[kRcSlots];
+    int32_t hkey[kHash];
+    int32_t hslot[kHash];
+};
+__device__ __forceinline__ void rc_insert(RowCache* rc, int n, int slot) {  // n distinct
+    int h = hash_slot(n);
+    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+    rc->hslot[h] = slot;
+}
+__device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
+    int h = hash_slot(n);
+    for (int i = 0; i < kHash; ++i, h = (h + 1) & (kHash - 1)) {
+        const int k = rc->hkey[h];
+        if (k == n) return rc->hslot[h];
+        if (k == -1) return -1;
+    }
+    return -1;
+}
+
 // SC1: rows read and written through sc1 (overlapped pops); the write-back is
 // then published as done = seq before the result stores.
 template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
-                               uint32_t seq = 0) {
+                               uint32_t seq = 0, const RowCache* rc = nullptr) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -632,7 +658,12 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
     int32_t na_n = 0;
-    if (n >= 0) {
+    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
+    if (rslot >= 0) {
+        base = rc->row[rslot];
+        for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
+        na_n = rc->na[rslot];
+    } else if (n >= 0) {
         base = load_row_t<SC1>(nc, n);
         if (c.has_ports)
             for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
@@ -1141,8 +1172,30 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(gridDim.x * 4 + 0);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // 3. pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
-    // every row load below is sc1); their candidates on their final rows
+    // 3. while pop seq-1 may still write back: the rows of this list's nodes
+    // (final: no pop in flight touches them) and the static parts of pop
+    // seq-1's candidates, into the row cache
+    __shared__ RowCache rc;
+    int32_t pna = 0;  // wave 0: pop seq-1's candidate `lane`: node-affinity weight, static predicates
+    bool pst = false;
+    if (wave == 0) {
+        for (int h = lane; h < kHash; h += 64) rc.hkey[h] = -1;
+        const KT lk = wlk[0][lane];
+        const int ln = lk ? key_node(lk, a) : -1;
+        if (ln >= 0) {
+            rc.row[lane] = load_row(nc, ln);
+            for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < nc.port_words) ? load_port_t<false>(nc, w, ln) : 0;
+            rc.na[lane] = cf.score_mult ? na_weight(c, t, nc, ln) : 0;
+        }
+        if (tn[0] >= 0) {
+            pst = static_pred(cf, c, t, nc, tn[0]);
+            pna = (pst && cf.score_mult) ? na_weight(c, t, nc, tn[0]) : 0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (ln >= 0) rc_insert(&rc, ln, lane);
+    }
+    // pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
+    // every load of their rows below is sc1); their candidates on final rows
     if (threadIdx.x == 0) {
         bool ok = s_ok;
         long spin = 0;
@@ -1156,9 +1209,23 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(gridDim.x * 4 + 10);
     const bool ok = s_ok;
     if (wave == 0) {
-        KT top = wlk[0][lane];
+        KT e0 = 0;
+        if (ok && tn[0] >= 0) {  // pop seq-1's candidates: rows into the cache, keys
+            const Row r = load_row_sc1(nc, tn[0]);
+            uint64_t pw[4] = {0, 0, 0, 0};
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, tn[0]);
+            rc.row[64 + lane] = r;
+            for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
+            rc.na[64 + lane] = pna;
+            rc_insert(&rc, tn[0], 64 + lane);
+            int32_t sc;
+            bool passed;
+            e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn[0], pst, pna, &sc, &passed), a);
+        }
+        KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
 #pragma unroll
-        for (int k = 0; k < kMaxDep; ++k) {
+        for (int k = 1; k < kMaxDep; ++k) {  // older pops (overlap > 1): not cached
             if (k >= ndep) break;
             bool dup = false;  // a node among several pops' candidates counts once
 #pragma unroll
@@ -1176,8 +1243,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
     if (ok) {
-        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);
-        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq);
+        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc);
+        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
