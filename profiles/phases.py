@@ -24,6 +24,6 @@ with kbhip.Session(p) as s:
              "group merge tail to final start", "final merge", "chain precompute", "placement loop",
              "write back", "kernel span", "tasks per launch", "pp: rows loaded", "pp: round-0 eval",
              "pp: round-0 sort+merge", "wb: ranks+stop", "wb: LDS counts", "ov: wait for previous pop",
-             "ov: patch (eval previous candidates + merge)"]
+             "ov: patch (eval previous candidates + merge)", "pp: rows fetched", "pp: LDS init + barrier"]
     print(json.dumps({"pops": n, "placement": placement, "overlap": overlap, **{names[i]: round(out[i], 3) for i in range(len(names))}},
                      indent=1))

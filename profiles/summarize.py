@@ -34,6 +34,29 @@ def main(src, tag):
                                                   "mean_us": float(row["AverageNs"]) / 1e3,
                                                   "min_us": float(row["MinNs"]) / 1e3,
                                                   "max_us": float(row["MaxNs"]) / 1e3}
+    trace_csv = os.path.join(src, "trace", "run_kernel_trace.csv")
+    if os.path.exists(trace_csv):  # overlapped pop kernels: per-launch device period from the timeline
+        by = defaultdict(list)
+        with open(trace_csv) as f:
+            for row in csv.DictReader(f):
+                by[short(row["Kernel_Name"])].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+        for k, iv in by.items():
+            if len(iv) < 2:
+                continue
+            iv.sort()
+            span = iv[-1][1] - iv[0][0]
+            busy, cur_s, cur_e = 0, iv[0][0], iv[0][1]  # union of the kernel intervals
+            for s0, e0 in iv[1:]:
+                if s0 > cur_e:
+                    busy += cur_e - cur_s
+                    cur_s, cur_e = s0, e0
+                else:
+                    cur_e = max(cur_e, e0)
+            busy += cur_e - cur_s
+            d = out["kernels"].setdefault(k, {})
+            d["timeline_span_us"] = span / 1e3
+            d["period_us"] = span / 1e3 / len(iv)          # launches overlap: span / launches
+            d["busy_period_us"] = busy / 1e3 / len(iv)     # union of their intervals / launches
     if os.path.exists(pmc_csv):
         acc = defaultdict(lambda: [0.0, 0])
         with open(pmc_csv) as f:
