@@ -249,7 +249,8 @@ def main():
                    "session_phases_ms": {k: round(v, 2) for k, v in st_last["phases_ms"].items()},
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},
-        "roofline": {"kernel": "k_sweep_argmax" if shard else "k_pop_batch", "bound": "hbm", "achieved": achieved,
+        "roofline": {"kernel": "k_sweep_argmax" if shard else ("k_pop_batch_ov" if args.overlap else "k_pop_batch"),
+                     "bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,
