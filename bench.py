@@ -246,6 +246,7 @@ def main():
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
+                   "unassigned_pops": st_last["unassigned_pops"],
                    "session_phases_ms": {k: round(v, 2) for k, v in st_last["phases_ms"].items()},
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},

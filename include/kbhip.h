@@ -87,6 +87,8 @@ typedef struct kbhip_stats {
     int64_t spec_hits;      /* predicted next pops launched ahead and used (kbhip_allocate) */
     int64_t spec_missed;    /* predicted pops retracted (their node updates undone on device) */
     double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
+    int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
+    int64_t fit_inexact;     /* jobs whose FitError histogram was not computed (shards, pod-affinity fallback) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -147,6 +149,15 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
+
+/* The gang plugin's OnSessionClose after kbhip_allocate (plugins/gang/gang.go:
+ * 166-187): the PodGroup Unschedulable condition message of every job that
+ * is not Ready — "<m>/<n> tasks in gang unschedulable: <JobInfo.FitError>"
+ * (job_info.go:343-372), the FitError from the job's NodesFitDelta as
+ * allocate.go:124-126 / 164-167 leave it — one line "<job uid>\t<message>\n"
+ * per job, in job UID order; empty when the gang plugin is not in the tiers.
+ * Returns the text length; copies it (NUL-terminated) when cap > length. */
+int64_t kbhip_gang_unschedulable(kb_session* s, char* out, int64_t cap);
 
 int kbhip_session_close(kb_session* s);
 

@@ -153,15 +153,33 @@ KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t
     return pack_key(s, n + nc.base, fit_acc ? 0 : 1);
 }
 
+// NodesFitDelta of a task that found no node (allocate.go:164-167: every node
+// of the walk gets Idle.FitDelta(Resreq), resource_info.go:134-147), counted
+// the way JobInfo.FitError reads it (job_info.go:343-372): bit 0 = the node is
+// in the walk (predicates pass, no NodeOrderFn error), bits 1..3 = its delta
+// is negative for cpu / memory / GPU.  The walk visits every such node, so
+// Idle is taken after GetAccessibleResource's visit (Idle += Backfilled).
+KBHIP_HD uint32_t fit_bits(const TaskClass& c, const Row& r, bool passed) {
+    if (!passed) return 0;
+    const int64_t ic = r.idle_cpu + r.bf_cpu, im = r.idle_mem + r.bf_mem, ig = r.idle_gpu + r.bf_gpu;
+    const int64_t dc = c.req_cpu > 0 ? ic - (c.req_cpu + kMinCPU) : ic;
+    const int64_t dm = c.req_mem > 0 ? im - (c.req_mem + kMinMem) : im;
+    const int64_t dg = c.req_gpu > 0 ? ig - (c.req_gpu + kMinGPU) : ig;
+    return 1u | (dc < 0 ? 2u : 0u) | (dm < 0 ? 4u : 0u) | (dg < 0 ? 8u : 0u);
+}
+
 KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                              const NodeCols& nc, int n, int32_t* score_out, bool* passed) {
+                                              const NodeCols& nc, int n, int32_t* score_out, bool* passed,
+                                              uint32_t* fit = nullptr) {
     const bool st = static_pred(cf, c, t, nc, n);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
-    return dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
+    const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
+    if (fit) *fit = fit_bits(c, r, *passed);
+    return k;
 }
 
 // ---------------------------------------------------------------------------
@@ -218,7 +236,7 @@ KBHIP_HD int64_t ipa_count(const TaskClass& c, const DevTables& t, const NodeCol
 // inter-pod score normalised by the prepass's [lo, hi] (interpod_affinity.go:228-237).
 KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTables& t,
                                                   const NodeCols& nc, int n, int64_t lo, int64_t hi, int F,
-                                                  int32_t* score_out, bool* passed) {
+                                                  int32_t* score_out, bool* passed, uint32_t* fit = nullptr) {
     bool st = static_pred(cf, c, t, nc, n);
     if (st && c.aff && cf.pred_on) st = aff_pred(c, t, nc, n);
     int32_t ipa = 0;
@@ -229,7 +247,9 @@ KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTab
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
-    return dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed, ipa);
+    const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed, ipa);
+    if (fit) *fit = fit_bits(c, r, *passed);
+    return k;
 }
 
 // Backfill's node test (backfill.go:51-56): the predicates only — no score,

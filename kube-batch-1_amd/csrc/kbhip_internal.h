@@ -66,6 +66,12 @@ hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTabl
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
                                uint32_t seq, int ndep);
+// Node updates of given placements again (after launch_undo_pop).
+hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
+                           const int32_t* kind, hipStream_t st);
+// One task's walk FitDelta histogram on the current state (kbhip_kernels.hip).
+hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int chosen,
+                            int chosen_kind, int32_t* out4, hipStream_t st);
 // Inverse node updates of a batched pop's placements (a retracted prediction).
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);
@@ -76,6 +82,7 @@ hipError_t set_stamp_buffer(uint64_t* p);
 #endif
 struct PopOutHost {  // host view of the device PopOut: self-tagged granules
     uint64_t g[kMaxChunk];
+    uint64_t fit[2];
 };
 
 }  // namespace kbhip

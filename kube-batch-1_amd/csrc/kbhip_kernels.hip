@@ -204,7 +204,9 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
                                                          int task_i, uint64_t* walk, int commit_here, uint64_t* dbg) {
     __shared__ uint64_t red[kBlock / 64];
     __shared__ int last;
+    __shared__ int32_t s_fit[4];
     if (ctrl->stop >= 0) return;  // the pop already stopped (uniform)
+    if (threadIdx.x < 4) s_fit[threadIdx.x] = 0;
     const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
     const TaskClass c = t.classes[cls];
     const bool first_fit = ctrl->mode == 1;
@@ -212,11 +214,14 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     const int64_t ilo = ctrl->ipa_lo[task_i], ihi = ctrl->ipa_hi[task_i];
     const int F = ctrl->fallback;
     uint64_t best = 0;
+    int32_t fc[4] = {0, 0, 0, 0};  // this task's FitDelta histogram, should it find no node
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
         int32_t s = 0;
         bool passed = false;
+        uint32_t fb = 0;
         const uint64_t k = first_fit ? eval_first_fit(cf, c, t, nc, n)
-                                     : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed);
+                                     : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed, &fb);
+        for (int b = 0; b < 4; ++b) fc[b] += (fb >> b) & 1;
         if (track) walk[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
         if (dbg) {  // kbhip_set_option("debug_keys")
             dbg[(int64_t)task_i * (2 * nc.npad + 4) + n] = k;
@@ -227,11 +232,16 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     best = wave_max_u64(best);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = best;
     if (track) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // walk[] stores drained before the release
+    __syncthreads();  // s_fit zeroed
+    for (int b = 0; b < 4; ++b)
+        if (fc[b]) atomicAdd(&s_fit[b], fc[b]);
     __syncthreads();
     if (threadIdx.x == 0) {
         uint64_t b = red[0];
         for (int w = 1; w < kBlock / 64; ++w) b = red[w] > b ? red[w] : b;
         if (b) atomicMax((unsigned long long*)&ctrl->slot[task_i], (unsigned long long)b);
+        for (int q = 0; q < 4; ++q)
+            if (s_fit[q]) atomicAdd(&ctrl->fit[task_i][q], s_fit[q]);
         __threadfence();
         const unsigned prev = atomicAdd(&ctrl->arrive[task_i], 1u);
         last = prev == gridDim.x - 1;
@@ -315,7 +325,21 @@ __device__ __forceinline__ T wave_merge_desc(T a, T b) {
 // polls the tags).  granule = epoch<<48 | (stop+1)<<44 | n_done<<36 | kind<<34 | (node+1)
 struct PopOut {
     uint64_t g[kMaxChunk];
+    uint64_t fit[2];  // FitDelta histogram of a task that found no node: walk nodes, cpu | memory, GPU
 };
+__host__ __device__ inline uint64_t make_fit_granule(uint32_t epoch, uint32_t a, uint32_t b) {
+    return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(b & 0xffffffu) << 24) | (uint64_t)(a & 0xffffffu);
+}
+// Per-group FitDelta counters of the batched sweep, after the arrival counters.
+__device__ __forceinline__ uint32_t* fit_counters(uint32_t* arrive) { return arrive + (kMaxGroups + 1) * 32; }
+// Block: add this lane's fit bits to the block's LDS counters (every lane of every wave).
+__device__ __forceinline__ void fit_block_add(uint32_t* s_fitb, uint32_t fb) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int cnt = __popcll(__ballot((fb >> b) & 1u));
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_fitb[b], (uint32_t)cnt);
+    }
+}
 __host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n_done, int kind, int node) {
     return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(stop + 1) << 44) | ((uint64_t)n_done << 36) |
            ((uint64_t)kind << 34) | (uint64_t)(uint32_t)(node + 1);
@@ -436,7 +460,7 @@ __device__ __forceinline__ uint64_t load_port_t(const NodeCols& nc, int w, int n
 }
 // eval_node with the rows read through sc1.
 __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                                  const NodeCols& nc, int n) {
+                                                  const NodeCols& nc, int n, uint32_t* fit = nullptr) {
     const bool st = static_pred(cf, c, t, nc, n);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const Row r = load_row_sc1(nc, n);
@@ -445,7 +469,9 @@ __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClas
         for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, n);
     int32_t s;
     bool passed;
-    return dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+    const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+    if (fit) *fit = fit_bits(c, r, passed);
+    return k;
 }
 
 __device__ __forceinline__ uint64_t level_entry(int32_t rm, int n, int d, uint64_t key) {
@@ -640,7 +666,7 @@ __device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
 template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
-                               uint32_t seq = 0, const RowCache* rc = nullptr) {
+                               uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -669,12 +695,14 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
+    STAMP(gridDim.x * 4 + 11);
     uint64_t pwc[4];
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
     if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
     __syncthreads();  // K read by every wave; wl free
+    STAMP(gridDim.x * 4 + 12);
     if (wave == 0 && n >= 0) {  // candidate nodes are distinct
         int h = hash_slot(n);
         while (atomicCAS(&s_hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
@@ -775,6 +803,31 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     __builtin_amdgcn_wave_barrier();
     const int cc = s_cnt[lane];
     STAMP(gridDim.x * 4 + 9);
+    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
+        // fit_in: every node at the state this pop started from; the candidates
+        // then carry the commits made before the failing task
+        uint32_t fb_base = 0, fb_post = 0;
+        if (n >= 0) {
+            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
+            const int ap = s_apos[lane];
+            const int na = cc < ap ? cc : ap;
+            const Row r = apply_commits(base, c, na, cc - na);
+            int32_t sc;
+            bool passed;
+            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
+            fb_post = fit_bits(c, r, passed);
+        }
+        int32_t tot[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            tot[b] = fit_in[b] + __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+        if (lane == 0) {
+            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     if (n >= 0 && cc > 0) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
         const int ap = s_apos[lane];
         const int na = cc < ap ? cc : ap;
@@ -817,25 +870,33 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     else wl = wl64;
     KT* cand = (KT*)cand64;
     __shared__ int role;
+    __shared__ uint32_t s_fitb[4];
+    __shared__ int32_t s_fitin[4];
+    uint32_t* fitc = fit_counters(arrive);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
+    if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
     // 1. evaluate R nodes per lane, wave top-64, block top-64
     KT best = 0;
+    uint32_t fbs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
         KT k = 0;
+        fbs[r] = 0;
         if (n < nc.n) {
             int32_t s;
             bool passed;
-            k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed), a);
+            k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
         k = wave_sort_desc(k);
         best = r == 0 ? k : wave_merge_desc(best, k);
     }
     wlk[wave][lane] = best;
     __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r) fit_block_add(s_fitb, fbs[r]);
     STAMP(blockIdx.x * 4 + 1);
     block_tree_merge(wlk, wave, lane);
     const int nb = gridDim.x;
@@ -844,6 +905,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     const int n_groups = nb < kGroups ? nb : kGroups;
     KT* gcand = cand + (int64_t)nb * 64;                     // group lists after the block lists
     if (wave == 0) {
+        if (lane < 4 && s_fitb[lane])
+            __hip_atomic_fetch_add(&fitc[g * kCtrStride + lane], s_fitb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -897,6 +960,15 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0 && lane < 4) {  // the sweep's FitDelta counts (every block added before it arrived)
+        int32_t tot = 0;
+        for (int gi = 0; gi < n_groups; ++gi) {
+            tot += (int32_t)ld_sc1(&fitc[gi * kCtrStride + lane]);
+            st_sc1(&fitc[gi * kCtrStride + lane], 0u);
+        }
+        s_fitin[lane] = tot;
+    }
+    __syncthreads();
     if (a.placement == 1) {  // uniform
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
@@ -905,8 +977,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     if (a.placement == 2) {  // uniform; every wave takes part
         STAMP(gridDim.x * 4 + 1);
-        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl);
-        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl);
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
@@ -1063,6 +1135,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
     __shared__ int role, s_ok;
+    __shared__ uint32_t s_fitb[4];
+    __shared__ int32_t s_fitin[4];
+    uint32_t* fitc = fit_counters(arrive);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
@@ -1075,16 +1150,19 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         if (wave == 0 && k < ndep && seq > (uint32_t)(k + 1))
             tv[k] = ld_sc1(&link->touched[(seq - 1 - k) % kLinkSlots][lane]);
     for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
+    if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
     // 1. evaluate R nodes per lane, then leave pop seq-1's candidates out
     KT keys[R];
+    uint32_t fbs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
         keys[r] = 0;
+        fbs[r] = 0;
         if (n < nc.n) {
             int32_t s;
             bool passed;
-            keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed), a);
+            keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
     }
     __syncthreads();  // s_skip zeroed
@@ -1113,7 +1191,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int o = r * kPopThreads + threadIdx.x;
-        const KT k = wave_sort_desc((s_skip[o >> 5] >> (o & 31)) & 1u ? (KT)0 : keys[r]);
+        const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: counted by the patch
+        fit_block_add(s_fitb, skip ? 0u : fbs[r]);
+        const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
         best = r == 0 ? k : wave_merge_desc(best, k);
     }
     wlk[wave][lane] = best;
@@ -1126,6 +1206,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int n_groups = nb < kGroups ? nb : kGroups;
     KT* gcand = cand + (int64_t)nb * 64;
     if (wave == 0) {
+        if (lane < 4 && s_fitb[lane])
+            __hip_atomic_fetch_add(&fitc[g * kCtrStride + lane], s_fitb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1172,6 +1254,14 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(gridDim.x * 4 + 0);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0 && lane < 4) {  // the sweep's FitDelta counts (every block added before it arrived)
+        int32_t tot = 0;
+        for (int gi = 0; gi < n_groups; ++gi) {
+            tot += (int32_t)ld_sc1(&fitc[gi * kCtrStride + lane]);
+            st_sc1(&fitc[gi * kCtrStride + lane], 0u);
+        }
+        s_fitin[lane] = tot;
+    }
     // 3. while pop seq-1 may still write back: the rows of this list's nodes
     // (final: no pop in flight touches them) and the static parts of pop
     // seq-1's candidates, into the row cache
@@ -1210,6 +1300,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const bool ok = s_ok;
     if (wave == 0) {
         KT e0 = 0;
+        uint32_t fb_prev = 0;  // FitDelta bits of the previous pops' candidates (left out of the sweep)
         if (ok && tn[0] >= 0) {  // pop seq-1's candidates: rows into the cache, keys
             const Row r = load_row_sc1(nc, tn[0]);
             uint64_t pw[4] = {0, 0, 0, 0};
@@ -1222,6 +1313,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             int32_t sc;
             bool passed;
             e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn[0], pst, pna, &sc, &passed), a);
+            fb_prev = fit_bits(c, r, passed);
         }
         KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
 #pragma unroll
@@ -1232,8 +1324,20 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             for (int j = 0; j < k; ++j)
                 for (uint64_t mm = __ballot(tn[j] >= 0); mm; mm &= mm - 1)
                     dup = dup || tn[k] == __builtin_amdgcn_readlane(tn[j], __ffsll((unsigned long long)mm) - 1);
-            const KT e = (ok && tn[k] >= 0 && !dup) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn[k]), a) : (KT)0;
+            uint32_t fbk = 0;
+            const KT e = (ok && tn[k] >= 0 && !dup) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn[k], &fbk), a)
+                                                     : (KT)0;
             top = wave_merge_desc(top, wave_sort_desc(e));
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int cnt = __popcll(__ballot((fbk >> b) & 1u));
+                if (lane == b) s_fitin[b] += cnt;
+            }
+        }
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int cnt = __popcll(__ballot((fb_prev >> b) & 1u));
+            if (lane == b) s_fitin[b] += cnt;
         }
         // this pop's candidates, one self-tagged granule each
         st_sc1(&link->touched[seq % kLinkSlots][lane],
@@ -1243,8 +1347,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
     if (ok) {
-        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc);
-        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc);
+        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin);
+        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
@@ -1287,6 +1391,67 @@ hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int 
     u.n = n < kMaxChunk ? n : kMaxChunk;
     for (int i = 0; i < u.n; ++i) { u.node[i] = node[i]; u.kind[i] = kind[i]; }
     hipLaunchKernelGGL(k_undo_pop, dim3(1), dim3(64), 0, st, nc, t, u);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(64) void k_redo_pop(NodeCols nc, DevTables t, UndoArgs u) {
+    if (threadIdx.x != 0) return;
+    const TaskClass c = t.classes[u.cls];
+    for (int i = 0; i < u.n; ++i)
+        if (u.node[i] >= 0) commit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+}
+
+hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
+                           const int32_t* kind, hipStream_t st) {
+    UndoArgs u{};
+    u.cls = cls;
+    u.n = n < kMaxChunk ? n : kMaxChunk;
+    for (int i = 0; i < u.n; ++i) { u.node[i] = node[i]; u.kind[i] = kind[i]; }
+    hipLaunchKernelGGL(k_redo_pop, dim3(1), dim3(64), 0, st, nc, t, u);
+    return hipGetLastError();
+}
+
+// The walk's FitDelta histogram (allocate.go:164-167) of one task recomputed
+// on the current node state, which must be the state the task saw (the
+// walk's GetAccessibleResource visits already applied): chosen < 0 — the task
+// found no node, every walk node counts; else the walk stopped at node
+// `chosen` with kind chosen_kind: the walk nodes before it count (walk order
+// = key order without the fit bit), and `chosen` itself when Pipelined.
+// Classes without pod-affinity terms.  out4 is zeroed by the caller.
+__global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevTables t, int cls, int chosen,
+                                                      int chosen_kind, int32_t* out4) {
+    __shared__ int32_t s_fit[4];
+    if (threadIdx.x < 4) s_fit[threadIdx.x] = 0;
+    __syncthreads();
+    const TaskClass c = t.classes[cls];
+    uint64_t wk = 0;  // walk-order key of the chosen node
+    if (chosen >= 0) {
+        int32_t s = 0;
+        bool passed = false;
+        (void)eval_node(cf, c, t, nc, chosen - nc.base, &s, &passed);
+        wk = pack_key(s, chosen, 0);
+    }
+    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+        int32_t s = 0;
+        bool passed = false;
+        (void)eval_node(cf, c, t, nc, n, &s, &passed);
+        Row r = load_row(nc, n);
+        r.bf_cpu = r.bf_mem = r.bf_gpu = 0;  // Idle as the walk left it
+        const bool in = passed && (chosen < 0 || pack_key(s, n + nc.base, 0) > wk ||
+                                   (n + nc.base == chosen && chosen_kind == 2));
+        const uint32_t fb = in ? fit_bits(c, r, true) : 0u;
+        for (int b = 0; b < 4; ++b)
+            if ((fb >> b) & 1u) atomicAdd(&s_fit[b], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x < 4 && s_fit[threadIdx.x]) atomicAdd(&out4[threadIdx.x], s_fit[threadIdx.x]);
+}
+
+hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int chosen,
+                            int chosen_kind, int32_t* out4, hipStream_t st) {
+    const int grid = (nc.n + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(k_fit_delta, dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, st, cf, nc, t, cls, chosen,
+                       chosen_kind, out4);
     return hipGetLastError();
 }
 

@@ -124,6 +124,8 @@ struct HJob {  // session jobs are numbered in UID order
     size_t cursor = 0;
     bool pending_built = false;
     int cnt_alloc = 0, cnt_aob = 0;
+    int32_t fit[4] = {0, 0, 0, 0};  // NodesFitDelta of its last task that ended a pop unplaced / not ready:
+    bool fit_exact = true;          // walk nodes, negative cpu / memory / GPU deltas (JobInfo.FitError)
     F3 drf_alloc;
     double drf_share = 0;
 };
@@ -336,6 +338,12 @@ struct Session {
     uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
+    int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
+    bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
+    DevBuf b_fit4;
+    int32_t* d_fit4 = nullptr;
+    vector<string> job_uid;              // by job slot (UID order)
+    bool gang_close = false;             // the gang plugin is in the tiers (its OnSessionClose reports)
     bool ov_pending = false;    // an overlapped pop may still run on either stream
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
@@ -409,7 +417,7 @@ struct Session {
         for (auto& b : b_cols) b.release();
         for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
-                          &b_arrive, &b_link, &b_dbg})
+                          &b_arrive, &b_link, &b_dbg, &b_fit4})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -523,6 +531,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 if (p.name == "drf") S.drf_on = true;
                 if (p.name == "proportion") S.prop_on = true;
                 if (p.name == "gang" && !(p.flags & KBS_DIS_JOBREADY)) S.gang_ready = true;
+                if (p.name == "gang") S.gang_close = true;
             }
     }
     mark("conf");
@@ -768,6 +777,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             j.priority = src.row >= 0 ? jpri[src.row] : 0;
             slot = (int)S.jobs.size();
             S.jobs.push_back(j);
+            S.job_uid.push_back(src.b ? string(src.a) + "/" + src.b : string(src.a));
         }
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
@@ -1208,12 +1218,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         int R2;
         const int nb2 = pop_blocks(nl, &R2);
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
-        S.d_arrive = S.b_arrive.alloc<uint32_t>((kMaxGroups + 1) * 32);
-        HIPCHK(hipMemsetAsync(S.d_arrive, 0, (kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
+        S.d_arrive = S.b_arrive.alloc<uint32_t>((2 * kMaxGroups + 1) * 32);
+        HIPCHK(hipMemsetAsync(S.d_arrive, 0, (2 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
+        S.d_fit4 = S.b_fit4.alloc<int32_t>(4);
         for (int k = 0; k <= kMaxDep; ++k) {
             S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
-            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((kMaxGroups + 1) * 32);
-            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
+            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((2 * kMaxGroups + 1) * 32);
+            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (2 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
         S.d_link = S.b_link.alloc<PopLink>(1);
         {
@@ -1346,6 +1357,7 @@ struct BatchLaunch {
     int cls = -1, m = 0;
     bool timed = false;
     hipStream_t st = nullptr;
+    bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
 };
 
 // Wait until no overlapped pop can still run (before device work that is not
@@ -1386,6 +1398,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
+    L.fit = S.placement == 2;
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -1445,6 +1458,20 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     }
     *n_done_out = n_done;
     *stop_out = (int)((load(0) >> 44) & 0xf) - 1;
+    S.last_fit_ok = false;
+    if (*stop_out == KBHIP_STOP_UNASSIGNED && L.fit) {
+        uint64_t f0 = 0, f1 = 0;
+        for (long spin = 0;; ++spin) {
+            f0 = __atomic_load_n(&o.fit[0], __ATOMIC_ACQUIRE);
+            f1 = __atomic_load_n(&o.fit[1], __ATOMIC_ACQUIRE);
+            if (tag(f0) == L.epoch && tag(f1) == L.epoch) break;
+            if (spin > (1L << 24)) throw Error(KBHIP_EDEVICE, "batched pop produced no FitDelta histogram");
+            __builtin_ia32_pause();
+        }
+        S.last_fit[0] = (int32_t)(f0 & 0xffffff); S.last_fit[1] = (int32_t)((f0 >> 24) & 0xffffff);
+        S.last_fit[2] = (int32_t)(f1 & 0xffffff); S.last_fit[3] = (int32_t)((f1 >> 24) & 0xffffff);
+        S.last_fit_ok = true;
+    }
 #ifdef KBHIP_STAMPS
     {
         int R2;
@@ -1465,6 +1492,10 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
         S.phase[2] += (tbm - t0) * 0.01;           // first block start -> every block list stored
         S.phase[3] += ((double)P[4] - (double)tbm) * 0.01;  // -> final merger starts
         S.phase[4] += (P[0] - P[4]) * 0.01;        // final merge
+        if (P[11] && P[12]) {
+            S.phase[17] += (P[11] - P[1]) * 0.01;  // placement: rows from cache / memory
+            S.phase[18] += (P[12] - P[11]) * 0.01; // placement: LDS init + barrier
+        }
         if (P[10]) {                               // overlapped kernel: wait for the previous pop, patch
             S.phase[15] += (P[10] - P[0]) * 0.01;
             S.phase[16] += (P[1] - P[10]) * 0.01;
@@ -1552,6 +1583,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             std::memset(h.slot, 0, sizeof h.slot);
             std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
             std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
+            std::memset(h.fit, 0, sizeof h.fit);
             HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
             for (int i = 0; i < m; ++i) {
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
@@ -1570,6 +1602,9 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             }
             n_done = h.n_done;
             stop_c = h.stop;
+            S.last_fit_ok = stop_c == KBHIP_STOP_UNASSIGNED && S.world == 1 && n_done >= 1;
+            if (S.last_fit_ok)
+                for (int q = 0; q < 4; ++q) S.last_fit[q] = h.fit[n_done - 1][q];
             ready_c = h.ready_count;
             any_bf_c = h.any_bf;
             res_node = h.res_node;
@@ -1974,6 +2009,27 @@ struct Allocator {
             }
             for (int i = (int)specs.size(); i < got; ++i) launch_pred(p[i]);
         };
+        // The walk FitDelta histogram of a pop's last task when the kernels did
+        // not report it (a pop that placed every pending task and left its job
+        // not Ready; placement modes 0/1): recomputed on the device state that
+        // task saw — queued predictions retracted, its own commit undone and
+        // redone around k_fit_delta.
+        auto fit_sync = [&](int cls, int node, int kind, HJob& job) {
+            discard_all();
+            ov_quiesce(S);
+            if (S.world != 1 || S.classes[cls].aff) {  // not covered: shards, pod-affinity classes
+                job.fit_exact = false;
+                S.stats.fit_inexact++;
+                return;
+            }
+            const int32_t nd[1] = {node}, kd[1] = {kind};
+            if (node >= 0) HIPCHK(launch_undo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
+            HIPCHK(hipMemsetAsync(S.d_fit4, 0, 4 * sizeof(int32_t), S.stream));
+            HIPCHK(launch_fit_delta(S.conf, S.nc, S.tab, cls, node, kind, S.d_fit4, S.stream));
+            if (node >= 0) HIPCHK(launch_redo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
+            HIPCHK(hipMemcpyAsync(job.fit, S.d_fit4, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, S.stream));
+            HIPCHK(hipStreamSynchronize(S.stream));
+        };
         // One job pop through the device: the first chunk batched (possibly
         // already queued by speculation), the rest through place_job.
         auto exec_pop = [&](int q, int jb, int n, int32_t* n_done, int32_t* stop) {
@@ -2051,7 +2107,17 @@ struct Allocator {
                         for (int t : job.tasks) if (S.pods[t].status == Allocated) S.pods[t].status = Binding;
                 }
                 job.cursor += n_done;
+                // NodesFitDelta (allocate.go:124-126, 164-167): what the job keeps is the walk of
+                // the task that ended its last pop; only a job left not Ready reports it
+                if (stop == KBHIP_STOP_UNASSIGNED && S.last_fit_ok) {
+                    for (int q = 0; q < 4; ++q) job.fit[q] = S.last_fit[q];
+                } else if (S.gang_close && n_done >= 1 &&
+                           (stop == KBHIP_STOP_UNASSIGNED || (stop == KBHIP_STOP_ALL && !job_ready(job)))) {
+                    const int last = n_done - 1;
+                    fit_sync(S.pods[ids[last]].cls, stop == KBHIP_STOP_UNASSIGNED ? -1 : onode[last], okind[last], job);
+                }
                 if (stop == KBHIP_STOP_READY) jit->second.push(jb);
+                if (stop == KBHIP_STOP_UNASSIGNED) S.stats.unassigned_pops++;
             }
             queues.push(q);
         }
@@ -2065,6 +2131,38 @@ struct Allocator {
         S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
 };
+
+// JobInfo.FitError (job_info.go:343-372) from the histogram of the job's last walk.
+static string fit_error(const HJob& j) {
+    if (j.fit[0] == 0) return "0 nodes are available";
+    vector<string> rs;  // "%v insufficient %v", sort.Strings
+    const std::pair<const char*, int32_t> rz[3] = {{"cpu", j.fit[1]}, {"memory", j.fit[2]}, {"GPU", j.fit[3]}};
+    for (auto& r : rz)
+        if (r.second > 0) rs.push_back(std::to_string(r.second) + " insufficient " + r.first);
+    std::sort(rs.begin(), rs.end());
+    string joined;
+    for (size_t i = 0; i < rs.size(); ++i) joined += (i ? ", " : "") + rs[i];
+    return "0/" + std::to_string(j.fit[0]) + " nodes are available, " + joined + ".";
+}
+// The gang plugin's OnSessionClose (plugins/gang/gang.go:166-187): the
+// Unschedulable condition message of every job that is not Ready, one line
+// "<job uid>\t<message>\n" per job in UID order; empty without gang.
+static string gang_close_text(const Session& S) {
+    if (!S.gang_close) return "";
+    string out;
+    for (size_t i = 0; i < S.jobs.size(); ++i) {
+        const HJob& j = S.jobs[i];
+        if (j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
+        int ready = 0;                              // readyTaskNum (gang.go:212-222)
+        for (int t : j.tasks) {
+            const int st = S.pods[t].status;
+            ready += allocated_status(st) || st == Pipelined || st == Succeeded;
+        }
+        out += S.job_uid[i] + "\t" + std::to_string(j.min_avail - ready) + "/" + std::to_string(j.tasks.size()) +
+               " tasks in gang unschedulable: " + fit_error(j) + "\n";
+    }
+    return out;
+}
 
 static int device_count() {
     int n = 0;
@@ -2448,6 +2546,15 @@ int kbhip_debug_replay(kb_session* s, int32_t n_steps, const int32_t* pods, cons
         return KBHIP_OK;
     })
 }
+int64_t kbhip_gang_unschedulable(kb_session* s, char* out, int64_t cap) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        const std::string t = kbhip::gang_close_text(s->s);
+        if (out && cap > (int64_t)t.size()) std::memcpy(out, t.c_str(), t.size() + 1);
+        return (int64_t)t.size();
+    })
+}
+
 int kbhip_session_close(kb_session* s) {
     ABI_GUARD({
         static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;

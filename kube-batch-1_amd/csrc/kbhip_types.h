@@ -107,6 +107,7 @@ struct PopCtrl {
     uint64_t slot[kMaxChunk];      // per-task max key (general path)
     int64_t ipa_lo[kMaxChunk];     // inter-pod affinity min / max count over nodes (0-initialised)
     int64_t ipa_hi[kMaxChunk];
+    int32_t fit[kMaxChunk][4];     // per task: walk nodes, negative cpu / memory / GPU FitDelta (fit_bits)
 };
 
 // Packed selection key: max key wins = highest score, then lowest node index.

@@ -25,7 +25,8 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_allocate", "kbhip_read_nodes", "kbhip_get_stats", "kbhip_set_option",
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
-           "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay")
+           "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
+           "kbhip_gang_unschedulable")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -42,7 +43,8 @@ class Stats(ctypes.Structure):
                 ("sweeps", ctypes.c_int64), ("batched_pops", ctypes.c_int64), ("nodes", ctypes.c_int64),
                 ("timed_launches", ctypes.c_int64), ("host_launch_s", ctypes.c_double),
                 ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
-                ("alloc_device_s", ctypes.c_double)]
+                ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
+                ("fit_inexact", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -83,6 +85,8 @@ def lib() -> ctypes.CDLL:
         L.kbhip_debug_encode.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(vp)]
         L.kbhip_debug_table.argtypes = [vp, ctypes.c_char_p, vp, i64]
         L.kbhip_debug_table.restype = i64
+        L.kbhip_gang_unschedulable.argtypes = [vp, ctypes.c_char_p, i64]
+        L.kbhip_gang_unschedulable.restype = i64
         L.kbhip_debug_replay.argtypes = [vp, i32, vp, vp, vp, vp, vp]
         _lib = L
     return _lib
@@ -209,6 +213,21 @@ class Session:
         out = np.zeros(max(int(n) // 4, 1), np.int32)
         _check(int(lib().kbhip_debug_table(self._h, name.encode(), _p(out), out.nbytes)) if n > 0 else 0)
         return out[: int(n) // 4]
+
+    def gang_unschedulable(self) -> dict:
+        """The gang plugin's OnSessionClose messages: {job uid: message} for
+        every job not Ready (kbhip_gang_unschedulable)."""
+        L = lib()
+        n = int(L.kbhip_gang_unschedulable(self._h, None, 0))
+        _check(n if n < 0 else 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        _check(int(L.kbhip_gang_unschedulable(self._h, buf, n + 1)))
+        out = {}
+        for line in buf.value.decode().splitlines():
+            if line:
+                uid, msg = line.split("\t", 1)
+                out[uid] = msg
+        return out
 
     def stats(self) -> dict:
         st = Stats()

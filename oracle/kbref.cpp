@@ -1656,6 +1656,46 @@ static void allocateExecute(World& w) {
     }
 }
 
+/* ---- gang OnSessionClose (plugins/gang/gang.go:166-187) ------------------ */
+// JobInfo.FitError (job_info.go:343-372): a histogram over NodesFitDelta.
+static string fitError(const JobInfo& j) {
+    if (j.NodesFitDelta.empty()) return "0 nodes are available";
+    map<string, int> reasons;
+    for (auto& kv : j.NodesFitDelta) {
+        if (kv.second.MilliCPU < 0) reasons["cpu"]++;
+        if (kv.second.Memory < 0) reasons["memory"]++;
+        if (kv.second.MilliGPU < 0) reasons["GPU"]++;
+    }
+    vector<string> rs;  // "%v insufficient %v", sort.Strings
+    for (auto& kv : reasons) rs.push_back(std::to_string(kv.second) + " insufficient " + kv.first);
+    std::sort(rs.begin(), rs.end());
+    string joined;
+    for (size_t i = 0; i < rs.size(); ++i) joined += (i ? ", " : "") + rs[i];
+    return "0/" + std::to_string(j.NodesFitDelta.size()) + " nodes are available, " + joined + ".";
+}
+// gang.go:212-222
+static int readyTaskNum(const JobInfo& j) {
+    int cnt = 0;
+    for (auto& kv : j.TaskStatusIndex)
+        if (AllocatedStatus(kv.first) || kv.first == Succeeded || kv.first == Pipelined) cnt += (int)kv.second.size();
+    return cnt;
+}
+// The PodGroup Unschedulable condition messages of OnSessionClose, one line
+// per job that is not Ready: "<job uid>\t<message>\n", jobs in UID order.
+static string gangClose(World& w) {
+    bool gang = false;
+    for (auto& tier : w.ssn.tiers)
+        for (auto& p : tier) gang = gang || p.name == "gang";
+    if (!gang) return "";
+    string out;
+    for (JobInfo* j : w.ssn.Jobs) {
+        if (j->GetReadiness() == Ready) continue;
+        out += j->UID + "\t" + std::to_string(j->MinAvailable - readyTaskNum(*j)) + "/" +
+               std::to_string(j->Tasks.size()) + " tasks in gang unschedulable: " + fitError(*j) + "\n";
+    }
+    return out;
+}
+
 /* ---- backfill action (actions/backfill/backfill.go:40-70) --------------- */
 static void backfillExecute(World& w) {
     Session& ssn = w.ssn;
@@ -1744,6 +1784,25 @@ int ref_allocate(const char* path, int32_t* out_pod, int32_t* out_node, int32_t*
             }
         }
         return n;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+/* Run the actions, then the gang plugin's OnSessionClose: the Unschedulable
+ * condition message of every job that is not Ready (gangClose).  Returns the
+ * text length (copied when cap > length), -1 on error. */
+int ref_gang_close(const char* path, const char* actions, char* out, int cap) {
+    try {
+        ref::World w;
+        w.snap.load_file(path);
+        ref::loadWorld(w);
+        ref::openSession(w);
+        ref::runActions(w, actions);
+        const std::string t = ref::gangClose(w);
+        if (out && cap > (int)t.size()) std::memcpy(out, t.c_str(), t.size() + 1);
+        return (int)t.size();
     } catch (std::exception& e) {
         g_err = e.what();
         return -1;

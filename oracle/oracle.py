@@ -91,6 +91,32 @@ def ref_allocate(path: str, cap: Optional[int] = None, with_nodes: bool = False,
     return (pl, nstate) if with_nodes else pl
 
 
+def parse_gang_close(text: str) -> dict:
+    """'<job uid>\\t<message>' lines -> {uid: message}."""
+    out = {}
+    for line in text.splitlines():
+        if line:
+            uid, msg = line.split("\t", 1)
+            out[uid] = msg
+    return out
+
+
+def ref_gang_close(path: str, actions: str = "allocate") -> dict:
+    """The gang plugin's OnSessionClose after the actions (gang.go:166-187):
+    {job uid: Unschedulable condition message} for every job not Ready."""
+    lib = _lib("kbref")
+    fn = lib.ref_gang_close
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    n = fn(path.encode(), actions.encode(), None, 0)
+    if n < 0:
+        lib.ref_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    buf = ctypes.create_string_buffer(n + 1)
+    fn(path.encode(), actions.encode(), buf, n + 1)
+    return parse_gang_close(buf.value.decode())
+
+
 def ref_open_nodes(path: str, n_nodes: int):
     lib = _lib("kbref")
     fn = lib.ref_open_nodes

@@ -78,3 +78,35 @@ def test_unknown_action_rejected(oracle_mod, kbgen_mod, tmp_path):
     kbgen_mod.gen_c1().write(p)
     with pytest.raises(RuntimeError):
         oracle_mod.ref_allocate(p, actions="allocate, preempt")
+
+
+# ---- gang OnSessionClose messages, hand-derived ---------
+def test_gang_close_fit_error_known_answer(tmp_path):
+    """Two nodes of 2 CPU / 4 GiB, a gang of 5 pods x (1 CPU, 1 GiB) with
+    minMember 5: four pods fit, the fifth finds no node.  Its walk visits both
+    nodes: Idle cpu 0 - (1000 + 10) < 0 on each, memory 2 GiB - (1 GiB + 10 MiB)
+    >= 0, so FitError = '0/2 nodes are available, 2 insufficient cpu.'; 5 - 4
+    = 1 task short of 5 (allocate.go:164-167, job_info.go:343-372,
+    gang.go:166-187).  Then a gang whose only node fails the predicates:
+    NodesFitDelta stays empty, '0 nodes are available'."""
+    import kbgen
+    import oracle
+    c = kbgen.Cluster()
+    c.add_queue("default", 1)
+    for i in range(2):
+        c.add_node(f"n{i}", 2000, 4 * kbgen.GI, 0)
+    c.add_job("ns", "g", "default", min_member=5)
+    for k in range(5):
+        c.add_pod("ns", f"g-{k}", uid=f"u{k}", group="g", containers=[kbgen.res(1000, kbgen.GI)])
+    p = str(tmp_path / "ka.kbs")
+    c.write(p)
+    assert oracle.ref_gang_close(p) == {"ns/g": "1/5 tasks in gang unschedulable: 0/2 nodes are available, "
+                                                "2 insufficient cpu."}
+    c2 = kbgen.Cluster()
+    c2.add_queue("default", 1)
+    c2.add_node("n0", 2000, 4 * kbgen.GI, 0, unschedulable=True)
+    c2.add_job("ns", "g", "default", min_member=1)
+    c2.add_pod("ns", "g-0", uid="u0", group="g", containers=[kbgen.res(1000, kbgen.GI)])
+    p2 = str(tmp_path / "ka2.kbs")
+    c2.write(p2)
+    assert oracle.ref_gang_close(p2) == {"ns/g": "1/1 tasks in gang unschedulable: 0 nodes are available"}
