@@ -44,7 +44,8 @@ struct KeyFormat {
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf);
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
+                            int fit_set);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
@@ -61,11 +62,12 @@ struct PopLink {
 // seq-ndep may still run on other streams (1 <= ndep <= kMaxDep): it leaves
 // their candidates out of its sweep and re-evaluates them once pop seq-1's
 // write-back is done.  cand holds (blocks + kMaxGroups) * 64 keys, arrive
-// (kMaxGroups + 1) * 32 counters, both private to the launch's stream.
+// (3 * kMaxGroups + 1) * 32 counters, both private to the launch's stream;
+// fit_set alternates per launch on a stream (FitDelta counter sets).
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep);
+                               uint32_t seq, int ndep, int fit_set);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

@@ -330,8 +330,12 @@ struct PopOut {
 __host__ __device__ inline uint64_t make_fit_granule(uint32_t epoch, uint32_t a, uint32_t b) {
     return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(b & 0xffffffu) << 24) | (uint64_t)(a & 0xffffffu);
 }
-// Per-group FitDelta counters of the batched sweep, after the arrival counters.
-__device__ __forceinline__ uint32_t* fit_counters(uint32_t* arrive) { return arrive + (kMaxGroups + 1) * 32; }
+// Per-group FitDelta counters of the batched sweep, after the arrival counters:
+// two sets; a launch adds to one and zeroes the other (its stream's previous
+// launch read that one and the next one adds to it).
+__device__ __forceinline__ uint32_t* fit_counters(uint32_t* arrive, int set) {
+    return arrive + (kMaxGroups + 1) * 32 + set * kMaxGroups * 32;
+}
 // Block: add this lane's fit bits to the block's LDS counters (every lane of every wave).
 __device__ __forceinline__ void fit_block_add(uint32_t* s_fitb, uint32_t fb) {
 #pragma unroll
@@ -354,6 +358,7 @@ struct PopArgs {
     // ordered exactly as pack_key; halves the sort / merge network work.
     int32_t kbase, kshift, kidxmax;
     int32_t ent32;  // placement entries in 32 bits: (rm - kbase + 1) fits in 32 - kshift - 5 bits
+    int32_t fit_set;  // FitDelta counter set of this launch (alternates per stream; the other one is zeroed)
 };
 
 // Selection key of the batched sweep in type T (see PopArgs).
@@ -661,12 +666,32 @@ __device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
     return -1;
 }
 
+__device__ __forceinline__ void fit_zero_other(uint32_t* arrive, int set) {
+    if (blockIdx.x == 0 && threadIdx.x < kGroups * 4)
+        fit_counters(arrive, 1 - set)[(threadIdx.x >> 2) * 32 + (threadIdx.x & 3)] = 0;
+}
+// Wave 0 of the final merger: lane 4g + b loads group g's count b (one round
+// trip, consumed only if a task finds no node: fit_sum).
+__device__ __forceinline__ uint32_t fit_load(const uint32_t* fitc, int n_groups) {
+    const int lane = threadIdx.x & 63;
+    uint32_t v = 0;
+    for (int gi = lane >> 2; gi < n_groups; gi += 16) v += ld_sc1(&fitc[gi * 32 + (lane & 3)]);
+    return v;
+}
+__device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b, b+4, ...
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
 // SC1: rows read and written through sc1 (overlapped pops); the write-back is
 // then published as done = seq before the result stores.
 template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
-                               uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr) {
+                               uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
+                               uint32_t fit_raw = 0) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -817,10 +842,12 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
             fb_post = fit_bits(c, r, passed);
         }
+        const uint32_t sweep = fit_sum(fit_raw);
         int32_t tot[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-            tot[b] = fit_in[b] + __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
         if (lane == 0) {
             __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -860,6 +887,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     STAMP(gridDim.x * 4 + 3);
 }
 
+
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                            uint64_t* cand64, uint32_t* arrive, PopOut* out) {
@@ -872,7 +900,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     __shared__ int role;
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
-    uint32_t* fitc = fit_counters(arrive);
+    uint32_t* fitc = fit_counters(arrive, a.fit_set);
+    fit_zero_other(arrive, a.fit_set);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
@@ -960,14 +989,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wave == 0 && lane < 4) {  // the sweep's FitDelta counts (every block added before it arrived)
-        int32_t tot = 0;
-        for (int gi = 0; gi < n_groups; ++gi) {
-            tot += (int32_t)ld_sc1(&fitc[gi * kCtrStride + lane]);
-            st_sc1(&fitc[gi * kCtrStride + lane], 0u);
-        }
-        s_fitin[lane] = tot;
-    }
+    // the sweep's FitDelta counts (every block added before it arrived), left in flight
+    const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
+    if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     __syncthreads();
     if (a.placement == 1) {  // uniform
         if (wave != 0) return;
@@ -977,8 +1001,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     if (a.placement == 2) {  // uniform; every wave takes part
         STAMP(gridDim.x * 4 + 1);
-        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin);
-        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin);
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
@@ -1137,7 +1161,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ int role, s_ok;
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
-    uint32_t* fitc = fit_counters(arrive);
+    uint32_t* fitc = fit_counters(arrive, a.fit_set);
+    fit_zero_other(arrive, a.fit_set);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
@@ -1254,14 +1279,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(gridDim.x * 4 + 0);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wave == 0 && lane < 4) {  // the sweep's FitDelta counts (every block added before it arrived)
-        int32_t tot = 0;
-        for (int gi = 0; gi < n_groups; ++gi) {
-            tot += (int32_t)ld_sc1(&fitc[gi * kCtrStride + lane]);
-            st_sc1(&fitc[gi * kCtrStride + lane], 0u);
-        }
-        s_fitin[lane] = tot;
-    }
+    // the sweep's FitDelta counts (every block added before it arrived), left in flight
+    const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
+    if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     // 3. while pop seq-1 may still write back: the rows of this list's nodes
     // (final: no pop in flight touches them) and the static parts of pop
     // seq-1's candidates, into the row cache
@@ -1347,8 +1367,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
     if (ok) {
-        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin);
-        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin);
+        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
@@ -1495,11 +1515,12 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf) {
+                            uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
+                            int fit_set) {
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0};
+              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
     if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
     else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
@@ -1526,12 +1547,12 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep) {
+                               uint32_t seq, int ndep, int fit_set) {
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0};
+              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
     if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
     else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);

@@ -344,6 +344,7 @@ struct Session {
     int32_t* d_fit4 = nullptr;
     vector<string> job_uid;              // by job slot (UID order)
     bool gang_close = false;             // the gang plugin is in the tiers (its OnSessionClose reports)
+    uint8_t fit_set[kMaxDep + 2] = {};   // FitDelta counter set of the next launch, per stream (last: k_pop_batch)
     bool ov_pending = false;    // an overlapped pop may still run on either stream
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
@@ -1218,13 +1219,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         int R2;
         const int nb2 = pop_blocks(nl, &R2);
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
-        S.d_arrive = S.b_arrive.alloc<uint32_t>((2 * kMaxGroups + 1) * 32);
-        HIPCHK(hipMemsetAsync(S.d_arrive, 0, (2 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
+        S.d_arrive = S.b_arrive.alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
+        HIPCHK(hipMemsetAsync(S.d_arrive, 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         S.d_fit4 = S.b_fit4.alloc<int32_t>(4);
         for (int k = 0; k <= kMaxDep; ++k) {
             S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
-            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((2 * kMaxGroups + 1) * 32);
-            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (2 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
+            S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
+            HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
         S.d_link = S.b_link.alloc<PopLink>(1);
         {
@@ -1405,12 +1406,15 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
     if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
-                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap));
+                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap,
+                                   S.fit_set[si]));
+        S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
     } else {
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                                S.d_arrive, out, S.stream, S.placement, kf));
+                                S.d_arrive, out, S.stream, S.placement, kf, S.fit_set[kMaxDep + 1]));
+        S.fit_set[kMaxDep + 1] ^= 1;
     }
     if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));
     S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
