@@ -187,6 +187,7 @@ class Pod:
     priority: int = 0
     ts: int = 0
     backfill: bool = False
+    priority_class: str = ""  # Spec.PriorityClassName (conformance plugin)
     labels: Dict[str, str] = field(default_factory=dict)
     # containers: dicts with optional keys cpu, mem, gpu (absent = not in Requests) and ports
     containers: List[dict] = field(default_factory=lambda: [{}])
@@ -332,6 +333,7 @@ class Cluster:
         C["p_phase"] = u8([PHASES[p.phase] for p in pods])
         C["p_deleting"] = u8([1 if p.deleting else 0 for p in pods])
         C["p_backfill"] = u8([1 if p.backfill else 0 for p in pods])
+        C["p_pclass"] = i32([st.add(p.priority_class) if p.priority_class else -1 for p in pods])
         C["p_priority"] = i32([p.priority for p in pods])
         C["p_ts"] = i64([p.ts for p in pods])
         C["p_label_off"] = _csr([len(p.labels) for p in pods])
@@ -824,5 +826,84 @@ def gen_random(seed: int, n_nodes: int = 8, n_jobs: int = 6, max_tasks: int = 5,
                       backfill=("backfill" in f and node is not None and rng.random() < 0.3),
                       labels=labels, containers=ctrs, init_containers=inits, node_selector=nsel,
                       tolerations=tols, affinity=aff)
+            uid += 1
+    return c
+
+
+def gen_preempt(seed: int, n_nodes: int = 8, n_queues: int = 3, n_run_jobs: int = 6, n_pend_jobs: int = 4,
+                max_tasks: int = 5, tiers=None, fill: float = 0.9, features: Sequence[str] = ()) -> Cluster:
+    """Random cluster for the reclaim / preempt actions (SURVEY §3.5, config C5 in
+    miniature): nodes mostly filled with Running pods of low-priority jobs spread over
+    queues of unequal weight (so some queues sit above their proportion share),
+    pending higher-priority jobs, gang sizes that make some victims protected, some
+    kube-system / system-critical pods (conformance), releasing and backfill pods.
+    Features: "selector", "taints", "ports", "init", "bestEffort", "unsched"."""
+    rng = np.random.default_rng(seed)
+    f = set(features)
+    c = Cluster(tiers=tiers)
+    for i in range(n_nodes):
+        name = f"n{i:03d}"
+        taints = []
+        if "taints" in f and rng.random() < 0.2:
+            taints.append(("dedicated", "a", "NoSchedule"))
+        c.add_node(name, int(rng.choice([4000, 8000])), int(rng.choice([8, 16])) * GI,
+                   int(rng.choice([0, 0, 4000])), int(rng.choice([4, 110])),
+                   labels={"itype": ["small", "big"][int(rng.integers(2))], "kubernetes.io/hostname": name},
+                   taints=taints, unschedulable=("unsched" in f and rng.random() < 0.1))
+    for q in range(n_queues):
+        c.add_queue(f"q{q}", int(rng.integers(1, 5)), ts=int(rng.integers(0, 2)) * SEC)
+    free = {n.name: [n.cpu, n.mem, n.gpu] for n in c.nodes}
+    names = [n.name for n in c.nodes]
+    uid = 0
+
+    def rres():
+        r = {"cpu": int(rng.choice([500, 1000, 2000])), "mem": int(rng.choice([1, 2, 4])) * GI}
+        if rng.random() < 0.2:
+            r["gpu"] = int(rng.choice([1000, 2000]))
+        return r
+
+    # running jobs: queue 0 gets the most (it is the one above its share)
+    for j in range(n_run_jobs):
+        jn, ns = f"r{j:03d}", ("kube-system" if rng.random() < 0.1 else "ns1")
+        q = 0 if rng.random() < 0.6 else int(rng.integers(n_queues))
+        ntask = int(rng.integers(1, max_tasks + 1))
+        c.add_job(ns, jn, f"q{q}", min_member=int(rng.choice([1, max(1, ntask - 1), ntask])), ts=0)
+        for k in range(ntask):
+            r = rres()
+            cands = [n for n in names if free[n][0] >= r["cpu"] and free[n][1] >= r["mem"]
+                     and free[n][2] >= r.get("gpu", 0)]
+            if not cands or rng.random() > fill:
+                node, phase = None, "Pending"
+            else:
+                node, phase = cands[int(rng.integers(len(cands)))], "Running"
+                free[node][0] -= r["cpu"]; free[node][1] -= r["mem"]; free[node][2] -= r.get("gpu", 0)
+            pc = ["", "", "", "system-node-critical", "system-cluster-critical"][int(rng.integers(5))] \
+                if rng.random() < 0.15 else ""
+            c.add_pod(ns, f"{jn}-{k}", uid=f"u{uid:05d}", group=jn, node=node, phase=phase,
+                      deleting=(node is not None and rng.random() < 0.05), priority=int(rng.choice([0, 1])),
+                      ts=int(rng.integers(0, 2)) * SEC, backfill=(node is not None and rng.random() < 0.1),
+                      priority_class=pc, labels={"job": jn}, containers=[r])
+            uid += 1
+    # pending preemptor jobs
+    for j in range(n_pend_jobs):
+        jn = f"p{j:03d}"
+        q = int(rng.integers(n_queues))
+        ntask = int(rng.integers(1, max_tasks + 1))
+        pri = int(rng.choice([5, 10]))
+        c.add_job("ns2", jn, f"q{q}", min_member=int(rng.choice([0, 1, ntask])), ts=int(rng.integers(1, 3)) * SEC,
+                  pg_priority=pri)
+        for k in range(ntask):
+            ctrs = [rres()]
+            if "bestEffort" in f and rng.random() < 0.1:
+                ctrs = [{}]
+            if "ports" in f and rng.random() < 0.2:
+                ctrs[0]["ports"] = [{"port": 80, "ip": "", "proto": ""}]
+            inits = [rres()] if ("init" in f and rng.random() < 0.2) else []
+            nsel = {"itype": "big"} if ("selector" in f and rng.random() < 0.2) else {}
+            tols = [{"key": "dedicated", "op": "Exists", "value": "", "effect": ""}] \
+                if ("taints" in f and rng.random() < 0.5) else []
+            c.add_pod("ns2", f"{jn}-{k}", uid=f"u{uid:05d}", group=jn, priority=pri,
+                      ts=int(rng.integers(1, 3)) * SEC, labels={"job": jn}, containers=ctrs,
+                      init_containers=inits, node_selector=nsel, tolerations=tols)
             uid += 1
     return c

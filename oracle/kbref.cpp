@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <functional>
 #include <map>
 #include <memory>
@@ -114,6 +115,7 @@ struct Pod {
     int32_t priority = 0;
     int64_t ts = 0;
     bool backfill = false;
+    string priorityClassName;  // Spec.PriorityClassName (conformance.go:40-45)
     vector<Container> containers, initContainers;
     map<string, string> nodeSelector;
     vector<Toleration> tolerations;
@@ -142,6 +144,9 @@ struct Resource {  // resource_info.go:26-33
     Resource& Sub(const Resource& r) { MilliCPU -= r.MilliCPU; Memory -= r.Memory; MilliGPU -= r.MilliGPU; return *this; }
     Resource& Multi(double ratio) { MilliCPU *= ratio; Memory *= ratio; MilliGPU *= ratio; return *this; }
     bool IsEmpty() const { return MilliCPU < minMilliCPU && Memory < minMemory && MilliGPU < minMilliGPU; }  // :75-77
+    bool Less(const Resource& rr) const {  // :156-158 — strict in every dimension
+        return MilliCPU < rr.MilliCPU && Memory < rr.Memory && MilliGPU < rr.MilliGPU;
+    }
     bool LessEqual(const Resource& rr) const {  // :164-168
         return (MilliCPU < rr.MilliCPU || std::fabs(rr.MilliCPU - MilliCPU) < minMilliCPU) &&
                (Memory < rr.Memory || std::fabs(rr.Memory - Memory) < minMemory) &&
@@ -254,6 +259,26 @@ struct NodeInfo {  // node_info.go:27-45
         }
         Tasks[task.pod] = ti;
         return true;
+    }
+    bool RemoveTask(const TaskInfo& ti) {  // :147-177
+        auto it = Tasks.find(ti.pod);
+        if (it == Tasks.end()) return false;
+        const TaskInfo& task = it->second;
+        if (Node) {
+            if (task.IsBackfill) Backfilled.Sub(task.Resreq);
+            switch (task.Status) {
+                case ::ref::Releasing: Releasing.Sub(task.Resreq); Idle.Add(task.Resreq); break;
+                case ::ref::Pipelined: Releasing.Add(task.Resreq); break;
+                default: Idle.Add(task.Resreq);
+            }
+            Used.Sub(task.Resreq);
+        }
+        Tasks.erase(it);
+        return true;
+    }
+    bool UpdateTask(const TaskInfo& ti) {  // :179-185
+        if (!RemoveTask(ti)) return false;
+        return AddTask(ti);
     }
     vector<Pod*> Pods() const {  // :201-207
         vector<Pod*> v;
@@ -652,9 +677,11 @@ typedef std::function<bool(TaskInfo*, NodeInfo*, int*)> NodeOrderFn;      // ret
 typedef std::function<int(JobInfo*)> JobReadyFn;
 typedef std::function<bool(QueueInfo*)> OverusedFn;
 
-struct EventHandler {
+struct EventHandler {  // framework/event.go:27-30
     std::function<void(TaskInfo*)> AllocateFunc;
+    std::function<void(TaskInfo*)> DeallocateFunc;
 };
+typedef std::function<vector<TaskInfo*>(TaskInfo*, const vector<TaskInfo*>&)> EvictableFn;  // api/types.go
 
 struct Session {
     vector<JobInfo*> Jobs;          // pinned order (by job UID)
@@ -670,6 +697,8 @@ struct Session {
     map<string, JobReadyFn> jobReadyFns;
     map<string, OverusedFn> overusedFns;
     vector<EventHandler> eventHandlers;
+    map<string, EvictableFn> preemptableFns, reclaimableFns;
+    std::deque<TaskInfo> clones;  // task.Clone() results (preempt.go:298-300, reclaim.go:138): the job keeps them after an eviction
     // observer: placement log
     vector<std::tuple<int, int, int>> log;  // (pod, node index, status)
     map<string, int> nodeIndex;
@@ -757,6 +786,57 @@ struct Session {
         return false;
     }
 
+    // Session.Reclaimable / Preemptable (session_plugins.go:67-148): per tier,
+    // the intersection (in victim order) of the enabled plugins' candidates;
+    // the first tier whose result is non-nil decides.  A nil result (no plugin
+    // yet, or a plugin that returned nothing) lets the next tier decide.
+    vector<TaskInfo*> evictable(map<string, EvictableFn>& fns, int disFlag, TaskInfo* evictor,
+                                const vector<TaskInfo*>& evictees) {
+        vector<TaskInfo*> victims;
+        bool init = false, isNil = true;
+        for (auto& tier : tiers) {
+            for (auto& p : tier) {
+                if (p.flags & disFlag) continue;
+                auto it = fns.find(p.name);
+                if (it == fns.end()) continue;
+                vector<TaskInfo*> candidates = it->second(evictor, evictees);
+                if (!init) {
+                    victims = candidates;
+                    isNil = candidates.empty();  // the plugins build their slices by append: empty == nil
+                    init = true;
+                } else {
+                    vector<TaskInfo*> inter;
+                    for (auto* v : victims)
+                        for (auto* c : candidates)
+                            if (v->uid == c->uid) inter.push_back(v);
+                    victims = inter;
+                    isNil = inter.empty();  // `var intersection []*TaskInfo` stays nil when nothing matches
+                }
+            }
+            if (!isNil) return victims;
+        }
+        return victims;
+    }
+    vector<TaskInfo*> Reclaimable(TaskInfo* t, const vector<TaskInfo*>& es) {
+        return evictable(reclaimableFns, KBS_DIS_RECLAIMABLE, t, es);
+    }
+    vector<TaskInfo*> Preemptable(TaskInfo* t, const vector<TaskInfo*>& es) {
+        return evictable(preemptableFns, KBS_DIS_PREEMPTABLE, t, es);
+    }
+    // The session-side half of an eviction (session.go:331-356, statement.go:35-67):
+    // job status -> Releasing, node copy updated, Deallocate handlers.
+    void evictInSession(TaskInfo* reclaimee) {
+        auto jit = JobByUID.find(reclaimee->jobUID);
+        if (jit != JobByUID.end()) jit->second->UpdateTaskStatus(reclaimee, Releasing);
+        auto nit = NodeByName.find(reclaimee->NodeName);
+        if (nit != NodeByName.end()) nit->second->UpdateTask(*reclaimee);
+        for (auto& eh : eventHandlers) if (eh.DeallocateFunc) eh.DeallocateFunc(reclaimee);
+    }
+    void logEvict(TaskInfo* t) { log.emplace_back(t->pod, nodeIndex[t->NodeName], Releasing); }  // cache.Evict
+    void Evict(TaskInfo* reclaimee) {  // session.go:323-359 (the fake cache's Evict never fails)
+        logEvict(reclaimee);
+        evictInSession(reclaimee);
+    }
     void Pipeline(TaskInfo* task, NodeInfo* node) {  // session.go:199-235
         auto jit = JobByUID.find(task->jobUID);
         if (jit != JobByUID.end()) jit->second->UpdateTaskStatus(task, Pipelined);
@@ -816,6 +896,37 @@ static void gangOpen(Session& ssn, const PluginOption&) {
         return 0;
     };
     ssn.jobReadyFns["gang"] = [](JobInfo* j) { return j->GetReadiness(); };
+    // preemptableFn (gang.go:107-129), registered as both Reclaimable and Preemptable
+    Session* sp = &ssn;
+    EvictableFn pf = [sp](TaskInfo*, const vector<TaskInfo*>& preemptees) {
+        vector<TaskInfo*> victims;
+        for (auto* preemptee : preemptees) {
+            JobInfo* job = sp->JobByUID[preemptee->jobUID];
+            int ready = 0;  // readyTaskNum (gang.go:212-222)
+            for (auto& kv : job->TaskStatusIndex)
+                if (AllocatedStatus(kv.first) || kv.first == Succeeded || kv.first == Pipelined)
+                    ready += (int)kv.second.size();
+            if (job->MinAvailable <= ready - 1 || job->MinAvailable == 1) victims.push_back(preemptee);
+        }
+        return victims;
+    };
+    ssn.reclaimableFns["gang"] = pf;
+    ssn.preemptableFns["gang"] = pf;
+}
+
+/* ---- conformance plugin (plugins/conformance/conformance.go:37-61) ------- */
+static void conformanceOpen(Session& ssn, const PluginOption&) {
+    EvictableFn ef = [](TaskInfo*, const vector<TaskInfo*>& evictees) {
+        vector<TaskInfo*> victims;
+        for (auto* e : evictees) {
+            const string& cls = e->P->priorityClassName;
+            if (cls == "system-cluster-critical" || cls == "system-node-critical" || e->ns == "kube-system") continue;
+            victims.push_back(e);
+        }
+        return victims;
+    };
+    ssn.preemptableFns["conformance"] = ef;
+    ssn.reclaimableFns["conformance"] = ef;
 }
 
 /* ---- drf plugin (plugins/drf/drf.go:59-170) ------------------------------ */
@@ -842,6 +953,21 @@ static void drfOpen(Session& ssn, const PluginOption&, std::shared_ptr<DrfState>
         st->allocated[job->UID] = a;
         st->share[job->UID] = drfShare(a, st->total);
     }
+    // preemptableFn (drf.go:84-109)
+    ssn.preemptableFns["drf"] = [st](TaskInfo* preemptor, const vector<TaskInfo*>& preemptees) {
+        vector<TaskInfo*> victims;
+        Resource lalloc = st->allocated[preemptor->jobUID];
+        lalloc.Add(preemptor->Resreq);
+        double ls = drfShare(lalloc, st->total);
+        map<string, Resource> allocations;
+        for (auto* preemptee : preemptees) {
+            if (!allocations.count(preemptee->jobUID)) allocations[preemptee->jobUID] = st->allocated[preemptee->jobUID];
+            Resource& ralloc = allocations[preemptee->jobUID].Sub(preemptee->Resreq);
+            double rs = drfShare(ralloc, st->total);
+            if (ls < rs || std::fabs(ls - rs) <= 0.000001) victims.push_back(preemptee);  // shareDelta (drf.go:29)
+        }
+        return victims;
+    };
     ssn.jobOrderFns["drf"] = [st](void* l, void* r) {
         double ls = st->share[((JobInfo*)l)->UID], rs = st->share[((JobInfo*)r)->UID];
         if (ls == rs) return 0;
@@ -852,6 +978,11 @@ static void drfOpen(Session& ssn, const PluginOption&, std::shared_ptr<DrfState>
     eh.AllocateFunc = [st](TaskInfo* t) {
         Resource& a = st->allocated[t->jobUID];
         a.Add(t->Resreq);
+        st->share[t->jobUID] = drfShare(a, st->total);
+    };
+    eh.DeallocateFunc = [st](TaskInfo* t) {  // drf.go:144-151
+        Resource& a = st->allocated[t->jobUID];
+        a.Sub(t->Resreq);
         st->share[t->jobUID] = drfShare(a, st->total);
     };
     ssn.eventHandlers.push_back(eh);
@@ -926,6 +1057,21 @@ static void propOpen(Session& ssn, const PluginOption&, std::shared_ptr<PropStat
         if (ls < rs) return -1;
         return 1;
     };
+    // reclaimableFn (proportion.go:159-183)
+    ssn.reclaimableFns["proportion"] = [st, &ssn](TaskInfo*, const vector<TaskInfo*>& reclaimees) {
+        vector<TaskInfo*> victims;
+        map<string, Resource> allocations;
+        for (auto* reclaimee : reclaimees) {
+            JobInfo* job = ssn.JobByUID[reclaimee->jobUID];
+            QueueAttr& attr = st->opts[job->Queue];
+            if (!allocations.count(job->Queue)) allocations[job->Queue] = attr.allocated;
+            Resource& allocated = allocations[job->Queue];
+            if (allocated.Less(reclaimee->Resreq)) continue;
+            allocated.Sub(reclaimee->Resreq);
+            if (attr.deserved.LessEqual(allocated)) victims.push_back(reclaimee);
+        }
+        return victims;
+    };
     ssn.overusedFns["proportion"] = [st](QueueInfo* q) {
         QueueAttr& a = st->opts[q->UID];
         return a.deserved.LessEqual(a.allocated);
@@ -936,6 +1082,12 @@ static void propOpen(Session& ssn, const PluginOption&, std::shared_ptr<PropStat
         JobInfo* job = sp->JobByUID[t->jobUID];
         QueueAttr& a = st->opts[job->Queue];
         a.allocated.Add(t->Resreq);
+        propUpdateShare(a);
+    };
+    eh.DeallocateFunc = [st, sp](TaskInfo* t) {  // proportion.go:211-219
+        JobInfo* job = sp->JobByUID[t->jobUID];
+        QueueAttr& a = st->opts[job->Queue];
+        a.allocated.Sub(t->Resreq);
         propUpdateShare(a);
     };
     ssn.eventHandlers.push_back(eh);
@@ -1400,6 +1552,7 @@ static void loadWorld(World& w) {
          pnode = s.vec<int32_t>("p_node"), ppri = s.vec<int32_t>("p_priority"), paff = s.vec<int32_t>("p_aff");
     auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
     auto pts = s.vec<int64_t>("p_ts");
+    auto ppc = s.vec<int32_t>("p_pclass");  // optional
     auto plo = s.offs("p_label_off", P);
     auto plk = L("pl_key"), plv = L("pl_val");
     auto pso = s.offs("p_nsel_off", P);
@@ -1428,6 +1581,7 @@ static void loadWorld(World& w) {
         p.backfill = pbf[i];
         p.priority = ppri[i];
         p.ts = pts[i];
+        if (!ppc.empty() && ppc[i] >= 0) p.priorityClassName = s.s(ppc[i]);
         for (int k = plo[i]; k < plo[i + 1]; ++k) p.labels[s.s(plk[k])] = s.s(plv[k]);
         for (int k = pso[i]; k < pso[i + 1]; ++k) p.nodeSelector[s.s(psk[k])] = s.s(psv[k]);
         for (int k = pco[i]; k < pco[i + 1]; ++k) {
@@ -1540,6 +1694,9 @@ static void openSession(World& w) {
         t.job = jk;
         t.jobUID = w.jobs[jk].UID;
     }
+    // the nodes' task copies carry the job too (TaskInfo.Job is set by NewTaskInfo, job_info.go:86-109)
+    for (auto& n : w.nodes)
+        for (auto& kv : n.Tasks) { kv.second.job = w.tasks[kv.first].job; kv.second.jobUID = w.tasks[kv.first].jobUID; }
     // Snapshot(): only jobs whose queue exists; Clone re-adds tasks (job_info.go:294-326)
     for (size_t k = 0; k < w.jobs.size(); ++k) {
         JobInfo& j = w.jobs[k];
@@ -1570,7 +1727,7 @@ static void openSession(World& w) {
             else if (opt.name == "proportion") { w.prop = std::make_shared<PropState>(); propOpen(ssn, opt, w.prop); }
             else if (opt.name == "predicates") predicatesOpen(ssn, opt);
             else if (opt.name == "nodeorder") nodeorderOpen(ssn, opt);
-            // conformance: only preemptable/reclaimable fns; nothing on the allocate path
+            else if (opt.name == "conformance") conformanceOpen(ssn, opt);
         }
     }
 }
@@ -1717,6 +1874,245 @@ static void backfillExecute(World& w) {
     }
 }
 
+/* ---- framework.Statement (framework/statement.go:25-217) ----------------- */
+struct Statement {
+    Session& ssn;
+    vector<std::pair<int, TaskInfo*>> ops;  // 0 = evict, 1 = pipeline
+    explicit Statement(Session& s) : ssn(s) {}
+    void Evict(TaskInfo* reclaimee) {  // :35-67
+        ssn.evictInSession(reclaimee);
+        ops.emplace_back(0, reclaimee);
+    }
+    void Pipeline(TaskInfo* task, const string& hostname) {  // :96-136
+        auto jit = ssn.JobByUID.find(task->jobUID);
+        if (jit != ssn.JobByUID.end()) jit->second->UpdateTaskStatus(task, Pipelined);
+        task->NodeName = hostname;
+        auto nit = ssn.NodeByName.find(hostname);
+        if (nit != ssn.NodeByName.end()) nit->second->AddTask(*task);
+        for (auto& eh : ssn.eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(task);
+        ops.emplace_back(1, task);
+    }
+    void unevict(TaskInfo* reclaimee) {  // :81-105 — node.AddTask of a task the node still holds
+        auto jit = ssn.JobByUID.find(reclaimee->jobUID);  // fails: the node keeps its Releasing copy
+        if (jit != ssn.JobByUID.end()) jit->second->UpdateTaskStatus(reclaimee, Running);
+        auto nit = ssn.NodeByName.find(reclaimee->NodeName);
+        if (nit != ssn.NodeByName.end()) nit->second->AddTask(*reclaimee);
+        for (auto& eh : ssn.eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(reclaimee);
+    }
+    void unpipeline(TaskInfo* task) {  // :141-172
+        auto jit = ssn.JobByUID.find(task->jobUID);
+        if (jit != ssn.JobByUID.end()) jit->second->UpdateTaskStatus(task, Pending);
+        auto nit = ssn.NodeByName.find(task->NodeName);
+        if (nit != ssn.NodeByName.end()) nit->second->RemoveTask(*task);
+        for (auto& eh : ssn.eventHandlers) if (eh.DeallocateFunc) eh.DeallocateFunc(task);
+    }
+    void Discard() {  // :174-186
+        for (int i = (int)ops.size() - 1; i >= 0; --i) {
+            if (ops[i].first == 0) unevict(ops[i].second);
+            else unpipeline(ops[i].second);
+        }
+    }
+    void Commit() {  // :188-198: evict -> cache.Evict (recorded); pipeline -> nothing to bind (recorded)
+        for (auto& op : ops) {
+            if (op.first == 0) ssn.logEvict(op.second);
+            else ssn.log.emplace_back(op.second->pod, ssn.nodeIndex[op.second->NodeName], Pipelined);
+        }
+    }
+};
+
+// node.Tasks filtered and cloned (preempt.go:296-302, reclaim.go:128-140);
+// the node's map iterates in pinned pod order.
+static vector<TaskInfo*> cloneNodeTasks(Session& ssn, NodeInfo* node, const std::function<bool(const TaskInfo&)>& keep) {
+    vector<TaskInfo*> out;
+    for (auto& kv : node->Tasks) {
+        if (!keep(kv.second)) continue;
+        ssn.clones.push_back(kv.second);
+        out.push_back(&ssn.clones.back());
+    }
+    return out;
+}
+
+/* preempt() (actions/preempt/preempt.go:259-353) */
+static bool preemptOne(Session& ssn, Statement& stmt, TaskInfo* preemptor,
+                       const std::function<bool(const TaskInfo&)>& filter) {
+    vector<NodeInfo*> predicateNodes;
+    map<int, vector<NodeInfo*>> nodeScores;
+    for (auto* node : ssn.Nodes)
+        if (ssn.PredicateFn_(preemptor, node)) predicateNodes.push_back(node);
+    for (auto* node : predicateNodes) {
+        int score;
+        if (ssn.NodeOrderFn_(preemptor, node, &score)) nodeScores[score].push_back(node);
+    }
+    vector<NodeInfo*> selectedNodes;  // util.SelectBestNode
+    for (auto it = nodeScores.rbegin(); it != nodeScores.rend(); ++it)
+        for (auto* n : it->second) selectedNodes.push_back(n);
+    for (auto* node : selectedNodes) {
+        Resource preempted;
+        Resource resreq = preemptor->InitResreq;
+        vector<TaskInfo*> preemptees = cloneNodeTasks(ssn, node, filter);
+        vector<TaskInfo*> victims = ssn.Preemptable(preemptor, preemptees);
+        // validateVictims (:355-370)
+        if (victims.empty()) continue;
+        Resource allRes;
+        for (auto* v : victims) allRes.Add(v->Resreq);
+        if (allRes.Less(resreq)) continue;
+        for (auto* preemptee : victims) {
+            stmt.Evict(preemptee);
+            preempted.Add(preemptee->Resreq);
+            if (resreq.LessEqual(preemptee->Resreq)) break;
+            resreq.Sub(preemptee->Resreq);
+        }
+        if (preemptor->InitResreq.LessEqual(preempted)) {
+            stmt.Pipeline(preemptor, node->Name);
+            return true;
+        }
+    }
+    return false;
+}
+
+/* preemptAction.Execute (actions/preempt/preempt.go:43-255) */
+static void preemptExecute(World& w) {
+    Session& ssn = w.ssn;
+    map<string, std::unique_ptr<PriorityQueue<JobInfo>>> preemptorsMap;
+    map<string, std::unique_ptr<PriorityQueue<TaskInfo>>> preemptorTasks;
+    vector<JobInfo*> underRequest;
+    std::set<string> queueSeen;
+    for (auto* job : ssn.Jobs) {  // :60-83 (jobs in pinned UID order)
+        if (!ssn.QueueByUID.count(job->Queue)) continue;
+        queueSeen.insert(job->Queue);
+        auto it = job->TaskStatusIndex.find(Pending);
+        if (it == job->TaskStatusIndex.end() || it->second.empty()) continue;
+        if (!preemptorsMap.count(job->Queue)) {
+            preemptorsMap[job->Queue].reset(new PriorityQueue<JobInfo>());
+            preemptorsMap[job->Queue]->lessFn = [&ssn](JobInfo* l, JobInfo* r) { return ssn.JobOrderFn(l, r); };
+        }
+        preemptorsMap[job->Queue]->Push(job);
+        underRequest.push_back(job);
+        auto* tq = new PriorityQueue<TaskInfo>();
+        tq->lessFn = [&ssn](TaskInfo* l, TaskInfo* r) { return ssn.TaskOrderFn(l, r); };
+        for (auto& kv : it->second) tq->Push(kv.second);
+        preemptorTasks[job->UID].reset(tq);
+    }
+    for (auto* queue : ssn.Queues) {  // map `queues`, pinned to queue order
+        if (!queueSeen.count(queue->UID)) continue;
+        for (;;) {  // preemption between jobs within the queue (:87-149)
+            auto pit = preemptorsMap.find(queue->UID);
+            if (pit == preemptorsMap.end() || pit->second->Empty()) break;
+            PriorityQueue<JobInfo>& preemptors = *pit->second;
+            JobInfo* preemptorJob = preemptors.Pop();
+            Statement stmt(ssn);
+            bool assigned = false;
+            for (;;) {
+                PriorityQueue<TaskInfo>& tq = *preemptorTasks[preemptorJob->UID];
+                if (tq.Empty()) break;
+                TaskInfo* preemptor = tq.Pop();
+                const string pjob = preemptorJob->UID, pq = preemptorJob->Queue, ptjob = preemptor->jobUID;
+                if (preemptOne(ssn, stmt, preemptor, [&ssn, pq, ptjob](const TaskInfo& t) {
+                        if (t.Status != Running) return false;
+                        auto jit = ssn.JobByUID.find(t.jobUID);
+                        if (jit == ssn.JobByUID.end()) return false;
+                        return jit->second->Queue == pq && ptjob != t.jobUID;
+                    }))
+                    assigned = true;
+                if (ssn.JobReady(preemptorJob)) {
+                    stmt.Commit();
+                    break;
+                }
+            }
+            if (!ssn.JobReady(preemptorJob)) {
+                stmt.Discard();
+                continue;
+            }
+            if (assigned) preemptors.Push(preemptorJob);
+        }
+        for (auto* job : underRequest) {  // preemption between tasks within a job (:151-181)
+            for (;;) {
+                auto tit = preemptorTasks.find(job->UID);
+                if (tit == preemptorTasks.end() || tit->second->Empty()) break;
+                TaskInfo* preemptor = tit->second->Pop();
+                Statement stmt(ssn);
+                const string ptjob = preemptor->jobUID;
+                bool assigned = preemptOne(ssn, stmt, preemptor, [ptjob](const TaskInfo& t) {
+                    if (t.Status != Running) return false;
+                    return ptjob == t.jobUID;
+                });
+                stmt.Commit();
+                if (!assigned) break;
+            }
+        }
+    }
+}
+
+/* reclaimAction.Execute (actions/reclaim/reclaim.go:41-196) */
+static void reclaimExecute(World& w) {
+    Session& ssn = w.ssn;
+    PriorityQueue<QueueInfo> queues;
+    queues.lessFn = [&ssn](QueueInfo* l, QueueInfo* r) { return ssn.QueueOrderFn(l, r); };
+    std::set<string> queueMap;
+    map<string, std::unique_ptr<PriorityQueue<JobInfo>>> preemptorsMap;
+    map<string, std::unique_ptr<PriorityQueue<TaskInfo>>> preemptorTasks;
+    for (auto* job : ssn.Jobs) {  // :55-83
+        auto qit = ssn.QueueByUID.find(job->Queue);
+        if (qit == ssn.QueueByUID.end()) continue;
+        if (!queueMap.count(qit->second->UID)) {
+            queueMap.insert(qit->second->UID);
+            queues.Push(qit->second);
+        }
+        auto it = job->TaskStatusIndex.find(Pending);
+        if (it == job->TaskStatusIndex.end() || it->second.empty()) continue;
+        if (!preemptorsMap.count(job->Queue)) {
+            preemptorsMap[job->Queue].reset(new PriorityQueue<JobInfo>());
+            preemptorsMap[job->Queue]->lessFn = [&ssn](JobInfo* l, JobInfo* r) { return ssn.JobOrderFn(l, r); };
+        }
+        preemptorsMap[job->Queue]->Push(job);
+        auto* tq = new PriorityQueue<TaskInfo>();
+        tq->lessFn = [&ssn](TaskInfo* l, TaskInfo* r) { return ssn.TaskOrderFn(l, r); };
+        for (auto& kv : it->second) tq->Push(kv.second);
+        preemptorTasks[job->UID].reset(tq);
+    }
+    for (;;) {
+        if (queues.Empty()) break;
+        QueueInfo* queue = queues.Pop();
+        if (ssn.Overused(queue)) continue;
+        auto jit = preemptorsMap.find(queue->UID);
+        if (jit == preemptorsMap.end() || jit->second->Empty()) continue;
+        JobInfo* job = jit->second->Pop();
+        auto tit = preemptorTasks.find(job->UID);
+        if (tit == preemptorTasks.end() || tit->second->Empty()) continue;
+        TaskInfo* task = tit->second->Pop();
+        bool assigned = false;
+        for (auto* n : ssn.Nodes) {
+            if (!ssn.PredicateFn_(task, n)) continue;
+            Resource resreq = task->InitResreq;
+            Resource reclaimed;
+            const string jq = job->Queue;
+            vector<TaskInfo*> reclaimees = cloneNodeTasks(ssn, n, [&ssn, jq](const TaskInfo& t) {
+                if (t.Status != Running) return false;
+                auto it = ssn.JobByUID.find(t.jobUID);
+                if (it == ssn.JobByUID.end()) return false;
+                return it->second->Queue != jq;
+            });
+            vector<TaskInfo*> victims = ssn.Reclaimable(task, reclaimees);
+            if (victims.empty()) continue;
+            Resource allRes;
+            for (auto* v : victims) allRes.Add(v->Resreq);
+            if (allRes.Less(resreq)) continue;
+            for (auto* reclaimee : victims) {
+                ssn.Evict(reclaimee);
+                reclaimed.Add(reclaimee->Resreq);
+                if (resreq.LessEqual(reclaimee->Resreq)) break;
+                resreq.Sub(reclaimee->Resreq);
+            }
+            if (task->InitResreq.LessEqual(reclaimed)) {
+                ssn.Pipeline(task, n);
+                assigned = true;
+                break;
+            }
+        }
+        if (assigned) queues.Push(queue);
+    }
+}
+
 // scheduler.go:93-97 runs the conf's actions in order; util.go:51-58 splits
 // the "actions" string on commas and trims each name.
 static vector<string> splitActions(const char* actions) {
@@ -1739,6 +2135,8 @@ static void runActions(World& w, const char* actions) {
     for (auto& a : splitActions(actions)) {
         if (a == "allocate") allocateExecute(w);
         else if (a == "backfill") backfillExecute(w);
+        else if (a == "preempt") preemptExecute(w);
+        else if (a == "reclaim") reclaimExecute(w);
         else throw std::runtime_error("action '" + a + "' is not implemented by this oracle");
     }
 }

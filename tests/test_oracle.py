@@ -77,7 +77,7 @@ def test_unknown_action_rejected(oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "u.kbs")
     kbgen_mod.gen_c1().write(p)
     with pytest.raises(RuntimeError):
-        oracle_mod.ref_allocate(p, actions="allocate, preempt")
+        oracle_mod.ref_allocate(p, actions="allocate, enqueue")
 
 
 # ---- gang OnSessionClose messages, hand-derived ---------
