@@ -62,6 +62,7 @@ extern "C" {
 /* placement kinds (TaskStatus after the decision) */
 #define KBHIP_ALLOCATED 1 /* Session.Allocate -> api.Allocated */
 #define KBHIP_PIPELINED 2 /* Session.Pipeline -> api.Pipelined */
+#define KBHIP_EVICTED 3   /* Session.Evict / a committed Statement.Evict -> api.Releasing (cache.Evict) */
 
 /* stop reasons of kbhip_place_job */
 #define KBHIP_STOP_ALL 0        /* every given task was placed, job not yet ready */
@@ -122,6 +123,20 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
  * predicates.  Outputs the placements (all KBHIP_ALLOCATED) like
  * kbhip_allocate; returns their number. */
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+
+/* Run the reclaim action (actions/reclaim/reclaim.go:41-196) / the preempt
+ * action (actions/preempt/preempt.go:43-353) on the session's current state.
+ * Output records in decision order: (pod, node, KBHIP_EVICTED) for every
+ * eviction that reaches the cache (reclaim: each ssn.Evict; preempt: the
+ * evictions of a committed Statement, in operation order) and
+ * (pod, node, KBHIP_PIPELINED) for every pipelined preemptor (reclaim: each
+ * ssn.Pipeline; preempt: those of a committed Statement).  Discarded
+ * statements leave no record (and, like the reference, leave the victims'
+ * node copies Releasing).  Returns the record count.  KBHIP_EUNSUPPORTED on
+ * node-sharded sessions and sessions with pod (anti-)affinity terms.
+ * Replaces the reference's reclaimAction.Execute / preemptAction.Execute. */
+int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 
 /* Read the device node state: N x 12 int64 (idle, used, releasing,
  * backfilled; cpu/mem/gpu each) of the session's nodes (a shard session: its

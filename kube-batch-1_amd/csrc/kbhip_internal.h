@@ -33,6 +33,17 @@ hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* c
 // nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi.
 hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st);
 
+// Reclaim / preempt (kbhip_evict.hip): per-node order keys of the task of
+// ctrl->cls[0] (by_score 1: predicates + score, preempt; 0: predicates only,
+// reclaim), *count += passing nodes; descending radix sort of the keys
+// (tmp == nullptr: *tmp_bytes <- the scratch size); one node-row update
+// (op 0 evict, 1 pipeline, 2 unpipeline).
+hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                             int by_score, uint64_t* keys, uint32_t* count, hipStream_t st);
+hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int n, hipStream_t st);
+hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
+                          int64_t rg, hipStream_t st);
+
 // Selection-key format of a batched launch: 32-bit keys when the class's
 // score range and the node count fit (kbhip_kernels.hip, PopArgs).
 struct KeyFormat {

@@ -93,6 +93,8 @@ struct F3 {  // float64 Resource of the ordering plugins
     void add(const R3& r) { c += (double)r.c; m += (double)r.m; g += (double)r.g; }
     void addf(const F3& r) { c += r.c; m += r.m; g += r.g; }
     void subf(const F3& r) { c -= r.c; m -= r.m; g -= r.g; }
+    void sub(const R3& r) { c -= (double)r.c; m -= (double)r.m; g -= (double)r.g; }
+    bool less(const F3& rr) const { return c < rr.c && m < rr.m && g < rr.g; }  // Resource.Less (resource_info.go:156-158)
     double get(int k) const { return k == 0 ? c : k == 1 ? m : g; }
     bool less_equal(const F3& rr) const {  // resource_info.go:164-168
         return (c < rr.c || std::fabs(rr.c - c) < (double)kMinCPU) &&
@@ -110,6 +112,8 @@ struct HPod {
     int32_t priority = 0;
     int64_t ts = 0;
     bool backfill = false;
+    bool critical = false;  // kube-system namespace or a system-*-critical priority class (conformance.go:40-45)
+    bool node_rel = false;  // the node's copy stays Releasing after an unevict (statement.go:81-105)
     R3 req, ireq;
     int job = -1;   // session job slot
     int cls = -1;   // device task class (pending tasks)
@@ -308,6 +312,14 @@ struct Session {
     F3 total;
     vector<R3> used;  // NodeInfo.Used mirror (for kbhip_read_nodes)
     int any_bf = 0;
+    bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
+    // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
+    DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt;
+    size_t rank_tmp_bytes = 0;
+    uint64_t* h_rank = nullptr;  // pinned: [0] = count, then sorted keys
+    size_t h_rank_cap = 0;
+    int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
+    vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     int32_t fallback = -1;  // lowest node index holding a session-placed pod (nodeorder.go:78-93)
     // device
     Conf conf{};
@@ -409,6 +421,8 @@ struct Session {
                 if (e) { (void)hipEventDestroy(e); e = nullptr; }
         if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
         if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
+        if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
+        h_rank = nullptr;
         h_ctrl = nullptr;
         h_out = nullptr;
         for (int k = 1; k <= kMaxDep; ++k) MemPool::get().give_stream(ov_streams[k], device);
@@ -418,7 +432,7 @@ struct Session {
         for (auto& b : b_cols) b.release();
         for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
-                          &b_arrive, &b_link, &b_dbg, &b_fit4})
+                          &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -599,6 +613,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     auto pns = S32("p_ns"), pjob = S32("p_job"), pnode = S32("p_node"), ppri = S32("p_priority"), paff = S32("p_aff");
     auto pphase = s.span<uint8_t>("p_phase"), pdel = s.span<uint8_t>("p_deleting"), pbf = s.span<uint8_t>("p_backfill");
     auto pts = s.span<int64_t>("p_ts");
+    auto ppc = s.span<int32_t>("p_pclass");  // optional: Spec.PriorityClassName
     if ((int)pns.size() != P || (int)pjob.size() != P || (int)pnode.size() != P || (int)ppri.size() != P ||
         (int)pphase.size() != P || (int)pts.size() != P)
         throw Error(KBHIP_EINVAL, "pod columns length mismatch");
@@ -654,6 +669,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         else p.status = Unknown;
         p.priority = ppri[i];
         p.ts = pts[i];
+        {
+            const char* pc = (!ppc.empty() && ppc[i] >= 0) ? s.str(ppc[i]) : "";
+            p.critical = std::strcmp(s.str(pns[i]), "kube-system") == 0 ||
+                         std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
+        }
         p.backfill = !pbf.empty() && pbf[i];
         for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
             p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
@@ -1770,6 +1790,8 @@ struct Allocator {
         q.share = res;
     }
     void open_plugins() {
+        if (S.plugins_opened) return;
+        S.plugins_opened = true;
         if (S.drf_on)
             for (auto& j : S.jobs) {  // drf.go:65-82
                 for (int t : j.tasks) if (allocated_status(S.pods[t].status)) j.drf_alloc.add(S.pods[t].req);
@@ -2104,11 +2126,13 @@ struct Allocator {
                     p.node = onode[i];
                     if (okind[i] == KBHIP_ALLOCATED) { p.status = Allocated; job.cnt_alloc++; }
                     else p.status = Pipelined;
+                    job.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
                     on_allocate(pi);
                     S.log.emplace_back(pi, onode[i], okind[i]);
                     S.stats.placed++;
                     if (p.status == Allocated && job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-294)
-                        for (int t : job.tasks) if (S.pods[t].status == Allocated) S.pods[t].status = Binding;
+                        for (int t : job.tasks)
+                            if (S.pods[t].status == Allocated) { S.pods[t].status = Binding; job.priority = S.pods[t].priority; }
                 }
                 job.cursor += n_done;
                 // NodesFitDelta (allocate.go:124-126, 164-167): what the job keeps is the walk of
@@ -2133,6 +2157,400 @@ struct Allocator {
         HIPCHK(hipEventElapsedTime(&dms, S.ev_run[0], S.ev_run[1]));
         S.alloc_device_s += dms * 1e-3;
         S.stats.allocate_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+
+    // -----------------------------------------------------------------------
+    // reclaim / preempt (actions/reclaim/reclaim.go:41-196,
+    // actions/preempt/preempt.go:43-353, framework/statement.go).  The walk
+    // order of a preemptor's nodes comes from the device (kbhip_evict.hip);
+    // victims are chosen per node on the host model, in the pinned order of
+    // NodeInfo.Tasks (pod index).  Evictions / pipelines update the device rows
+    // (Releasing, pod count, nonzero requests, ports) before the next sweep.
+    // -----------------------------------------------------------------------
+    static bool le_tol(const R3& a, const R3& b) {  // Resource.LessEqual on exact integers (Appendix A.2)
+        return a.c - b.c < kMinCPU && a.m - b.m < kMinMem && a.g - b.g < kMinGPU;
+    }
+    static bool less_strict(const R3& a, const R3& b) { return a.c < b.c && a.m < b.m && a.g < b.g; }
+    void check_evict_supported() {
+        if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt on a node-sharded session");
+        if (S.n_spaces > 0) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
+        for (auto& c : S.classes)
+            if (c.aff || c.ipa_n) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
+    }
+    void on_deallocate(int pi) {  // event handlers drf.go:144-151, proportion.go:211-219
+        const HPod& p = S.pods[pi];
+        HJob& j = S.jobs[p.job];
+        if (S.drf_on) { j.drf_alloc.sub(p.req); drf_update(j); }
+        if (S.prop_on) { HQueue& q = S.queues[j.queue]; q.allocated.sub(p.req); prop_update(q); }
+    }
+    // JobInfo.UpdateTaskStatus (job_info.go:251-264): the status index, and
+    // AddTaskInfo's "job priority = this task's priority" (:242)
+    void set_status(int pi, int st) {
+        HPod& p = S.pods[pi];
+        HJob& j = S.jobs[p.job];
+        if (allocated_status(p.status)) j.cnt_alloc--;
+        if (p.status == AOB) j.cnt_aob--;
+        p.status = st;
+        if (allocated_status(st)) j.cnt_alloc++;
+        if (st == AOB) j.cnt_aob++;
+        j.priority = p.priority;
+    }
+    void build_node_tasks() {  // NodeInfo.Tasks of every node from the host model
+        S.node_tasks.assign(S.nc.n, {});
+        for (int i = 0; i < (int)S.pods.size(); ++i) {
+            const HPod& p = S.pods[i];
+            if (p.node < 0 || p.status == Succeeded || p.status == Failed || p.status == Pending) continue;
+            S.node_tasks[p.node].push_back(i);
+        }
+    }
+    bool node_copy_running(int pi) const { return S.pods[pi].status == Running && !S.pods[pi].node_rel; }
+    // The walk order of the task of class cls: preempt (by_score) = SelectBestNode order of
+    // the nodes passing PredicateFn with a NodeOrderFn score; reclaim = passing nodes in order.
+    void rank_nodes(int cls, bool by_score, vector<int>& out) {
+        const int N = S.nc.n;
+        if (!S.b_rank_keys.p) {
+            S.b_rank_keys.alloc<uint64_t>(N);
+            S.b_rank_sorted.alloc<uint64_t>(N);
+            S.b_rank_cnt.alloc<uint32_t>(4);
+            size_t tb = 0;
+            HIPCHK(sort_keys_desc(nullptr, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p, N,
+                                  S.stream));
+            S.rank_tmp_bytes = std::max<size_t>(tb, 16);
+            S.b_rank_tmp.alloc<uint8_t>(S.rank_tmp_bytes);
+            S.h_rank = (uint64_t*)MemPool::get().take(MemPool::kPinned, (size_t)(N + 1) * sizeof(uint64_t),
+                                                      &S.h_rank_cap);
+        }
+        PopCtrl& h = *S.h_ctrl;
+        h.stop = -1;
+        h.n_done = 0;
+        h.n_tasks = 1;
+        h.mode = 0;
+        h.any_bf = S.any_bf;
+        h.fallback = S.fallback;
+        h.cls[0] = cls;
+        h.ipa_lo[0] = h.ipa_hi[0] = 0;
+        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+        HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
+        HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (uint64_t*)S.b_rank_keys.p,
+                                 (uint32_t*)S.b_rank_cnt.p, S.stream));
+        size_t tb = S.rank_tmp_bytes;
+        HIPCHK(sort_keys_desc(S.b_rank_tmp.p, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p, N,
+                              S.stream));
+        const int first = std::min(N, S.rank_first);
+        HIPCHK(hipMemcpyAsync(S.h_rank, S.b_rank_cnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipMemcpyAsync(S.h_rank + 1, S.b_rank_sorted.p, first * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+        const int cnt = (int)(uint32_t)S.h_rank[0];
+        if (cnt > first) {
+            HIPCHK(hipMemcpyAsync(S.h_rank + 1 + first, (const uint64_t*)S.b_rank_sorted.p + first,
+                                  (size_t)(cnt - first) * sizeof(uint64_t), hipMemcpyDeviceToHost, S.stream));
+            HIPCHK(hipStreamSynchronize(S.stream));
+        }
+        out.resize(cnt);
+        for (int i = 0; i < cnt; ++i) out[i] = key_idx(S.h_rank[1 + i]);
+        S.stats.sweeps++;
+        S.stats.tasks++;
+    }
+    void dev_op(int op, int pi) {
+        const HPod& p = S.pods[pi];
+        HIPCHK(launch_node_op(S.nc, S.tab, op, p.node, p.cls, p.req.c, p.req.m, p.req.g, S.stream));
+    }
+    // the session half of an eviction (session.go:331-356 / statement.go:35-67)
+    void evict_in_session(int v) {
+        set_status(v, Releasing);
+        dev_op(0, v);  // node.UpdateTask: Releasing += Resreq
+        on_deallocate(v);
+    }
+    void unevict(int v) {  // statement.go:81-105: node.AddTask fails, the node keeps its Releasing copy
+        set_status(v, Running);
+        S.pods[v].node_rel = true;
+        on_allocate(v);
+    }
+    void pipeline(int t, int n) {  // statement.go:96-136 / session.go:199-235
+        HPod& p = S.pods[t];
+        set_status(t, Pipelined);
+        p.node = n;
+        auto& nt = S.node_tasks[n];
+        nt.insert(std::lower_bound(nt.begin(), nt.end(), t), t);
+        dev_op(1, t);
+        S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+        if (S.classes[p.cls].backfill) S.any_bf = 1;
+        on_allocate(t);
+    }
+    void unpipeline(int t) {  // statement.go:141-172 (task.NodeName stays set)
+        HPod& p = S.pods[t];
+        set_status(t, Pending);
+        auto& nt = S.node_tasks[p.node];
+        nt.erase(std::lower_bound(nt.begin(), nt.end(), t));
+        dev_op(2, t);
+        S.used[p.node].c -= p.req.c; S.used[p.node].m -= p.req.m; S.used[p.node].g -= p.req.g;
+        on_deallocate(t);
+    }
+    struct Stmt {  // framework.Statement: (0 evict | 1 pipeline, pod)
+        vector<std::pair<int, int>> ops;
+    };
+    void commit(Stmt& st) {  // statement.go:188-198: evictions reach the cache (recorded), pipelines bind nothing
+        for (auto& op : st.ops)
+            S.log.emplace_back(op.second, S.pods[op.second].node, op.first == 0 ? KBHIP_EVICTED : KBHIP_PIPELINED);
+        st.ops.clear();
+    }
+    void discard(Stmt& st) {  // statement.go:174-186
+        for (auto it = st.ops.rbegin(); it != st.ops.rend(); ++it) {
+            if (it->first == 0) unevict(it->second);
+            else unpipeline(it->second);
+        }
+        st.ops.clear();
+    }
+    // Session.Preemptable / Reclaimable (session_plugins.go:67-148): per tier the
+    // intersection of the enabled plugins' victims; the first non-empty tier decides,
+    // and once a plugin has answered later tiers only intersect further.
+    void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
+        victims.clear();
+        bool init = false;
+        vector<int> cand, inter;
+        std::unordered_map<int, int> ready;  // readyTaskNum per job (gang.go:212-222)
+        std::unordered_map<int, F3> alloc;
+        for (auto& tier : S.tiers) {
+            for (auto& pl : tier) {
+                if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
+                cand.clear();
+                if (pl.name == "gang") {  // gang.go:107-129
+                    for (int e : evictees) {
+                        const HJob& j = S.jobs[S.pods[e].job];
+                        auto it = ready.find(S.pods[e].job);
+                        if (it == ready.end()) {
+                            int c = 0;
+                            for (int t : j.tasks) {
+                                const int st = S.pods[t].status;
+                                if (allocated_status(st) || st == Succeeded || st == Pipelined) ++c;
+                            }
+                            it = ready.emplace(S.pods[e].job, c).first;
+                        }
+                        if (j.min_avail <= it->second - 1 || j.min_avail == 1) cand.push_back(e);
+                    }
+                } else if (pl.name == "conformance") {  // conformance.go:37-56
+                    for (int e : evictees) if (!S.pods[e].critical) cand.push_back(e);
+                } else if (preempt && pl.name == "drf" && S.drf_on) {  // drf.go:84-109
+                    const HPod& pr = S.pods[evictor];
+                    F3 la = S.jobs[pr.job].drf_alloc;
+                    la.add(pr.req);
+                    const double ls = drf_share_of(la);
+                    alloc.clear();
+                    for (int e : evictees) {
+                        const int jb = S.pods[e].job;
+                        auto it = alloc.find(jb);
+                        if (it == alloc.end()) it = alloc.emplace(jb, S.jobs[jb].drf_alloc).first;
+                        it->second.sub(S.pods[e].req);
+                        const double rs = drf_share_of(it->second);
+                        if (ls < rs || std::fabs(ls - rs) <= 0.000001) cand.push_back(e);  // shareDelta (drf.go:29)
+                    }
+                } else if (!preempt && pl.name == "proportion" && S.prop_on) {  // proportion.go:159-183
+                    alloc.clear();
+                    for (int e : evictees) {
+                        const int qi = S.jobs[S.pods[e].job].queue;
+                        const HQueue& q = S.queues[qi];
+                        auto it = alloc.find(qi);
+                        if (it == alloc.end()) it = alloc.emplace(qi, q.allocated).first;
+                        F3 rq;
+                        rq.add(S.pods[e].req);
+                        if (it->second.less(rq)) continue;
+                        it->second.sub(S.pods[e].req);
+                        if (q.deserved.less_equal(it->second)) cand.push_back(e);
+                    }
+                } else {
+                    continue;  // the plugin registers no such function
+                }
+                if (!init) {
+                    victims = cand;
+                    init = true;
+                } else {
+                    inter.clear();
+                    for (int v : victims)
+                        for (int c : cand)
+                            if (v == c) inter.push_back(v);
+                    victims.swap(inter);
+                }
+            }
+            if (!victims.empty()) return;
+        }
+    }
+    double drf_share_of(const F3& a) const {  // drf.go:160-170
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double x = share(a.get(k), S.total.get(k)); if (x > res) res = x; }
+        return res;
+    }
+    // preempt() (preempt.go:259-353); filter over the node's task copies
+    template <typename Filter>
+    bool preempt_one(Stmt& st, int pi, Filter keep) {
+        const HPod& pr = S.pods[pi];
+        if (pr.cls < 0) throw Error(KBHIP_EUNSUPPORTED, "preemptor without a task class");
+        vector<int> order, cands, victims;
+        rank_nodes(pr.cls, true, order);
+        for (int n : order) {
+            cands.clear();
+            for (int t : S.node_tasks[n]) if (keep(t)) cands.push_back(t);
+            victims_of(true, pi, cands, victims);
+            if (victims.empty()) continue;  // validateVictims (:355-370)
+            R3 all, resreq = pr.ireq, got;
+            for (int v : victims) { all.c += S.pods[v].req.c; all.m += S.pods[v].req.m; all.g += S.pods[v].req.g; }
+            if (less_strict(all, resreq)) continue;
+            for (int v : victims) {
+                const R3 vr = S.pods[v].req;
+                evict_in_session(v);
+                st.ops.emplace_back(0, v);
+                got.c += vr.c; got.m += vr.m; got.g += vr.g;
+                if (le_tol(resreq, vr)) break;
+                resreq.c -= vr.c; resreq.m -= vr.m; resreq.g -= vr.g;
+            }
+            if (le_tol(pr.ireq, got)) {
+                pipeline(pi, n);
+                st.ops.emplace_back(1, pi);
+                return true;
+            }
+        }
+        return false;
+    }
+    // pending tasks of a job in TaskOrderFn order (a strict total order: heap pops = sorted order)
+    vector<int> pending_sorted(const HJob& j) {
+        vector<int> v;
+        for (int t : j.tasks) if (S.pods[t].status == Pending) v.push_back(t);
+        std::sort(v.begin(), v.end(), [this](int a, int b) { return task_less(a, b); });
+        return v;
+    }
+    void preempt_action() {  // preempt.go:43-255
+        compile_orders();
+        open_plugins();
+        check_evict_supported();
+        build_node_tasks();
+        auto jl = [this](int a, int b) { return job_less(a, b); };
+        std::map<int, GoHeap<decltype(jl)>> preemptors;
+        std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;  // job -> (tasks, cursor)
+        vector<int> under;
+        vector<char> seen(S.queues.size(), 0);
+        for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
+            HJob& j = S.jobs[jb];
+            seen[j.queue] = 1;
+            vector<int> pend = pending_sorted(j);
+            if (pend.empty()) continue;
+            auto it = preemptors.find(j.queue);
+            if (it == preemptors.end()) it = preemptors.emplace(j.queue, GoHeap<decltype(jl)>(jl)).first;
+            it->second.push(jb);
+            under.push_back(jb);
+            ptasks[jb] = {std::move(pend), 0};
+        }
+        Stmt st;
+        for (int qi = 0; qi < (int)S.queues.size(); ++qi) {  // map `queues`, pinned to queue order
+            if (!seen[qi]) continue;
+            for (;;) {  // between jobs of the queue (:87-149)
+                auto pit = preemptors.find(qi);
+                if (pit == preemptors.end() || pit->second.empty()) break;
+                const int pj = pit->second.pop();
+                bool assigned = false;
+                auto& tq = ptasks[pj];
+                for (;;) {
+                    if (tq.second >= tq.first.size()) break;
+                    const int pt = tq.first[tq.second++];
+                    const int pq = S.jobs[pj].queue, ptj = S.pods[pt].job;
+                    if (preempt_one(st, pt, [&](int t) {
+                            const HPod& p = S.pods[t];
+                            return node_copy_running(t) && p.job >= 0 && S.jobs[p.job].queue == pq && ptj != p.job;
+                        }))
+                        assigned = true;
+                    if (job_ready(S.jobs[pj])) {
+                        commit(st);
+                        break;
+                    }
+                }
+                if (!job_ready(S.jobs[pj])) {
+                    discard(st);
+                    continue;
+                }
+                st.ops.clear();  // neither committed nor discarded: the session keeps the operations
+                if (assigned) pit->second.push(pj);
+            }
+            for (int jb : under) {  // between tasks of a job (:151-181)
+                auto& tq = ptasks[jb];
+                for (;;) {
+                    if (tq.second >= tq.first.size()) break;
+                    const int pt = tq.first[tq.second++];
+                    Stmt s2;
+                    const int ptj = S.pods[pt].job;
+                    const bool assigned = preempt_one(s2, pt, [&](int t) {
+                        return node_copy_running(t) && ptj == S.pods[t].job;
+                    });
+                    commit(s2);
+                    if (!assigned) break;
+                }
+            }
+        }
+    }
+    void reclaim_action() {  // reclaim.go:41-196
+        compile_orders();
+        open_plugins();
+        check_evict_supported();
+        build_node_tasks();
+        auto ql = [this](int a, int b) { return queue_less(a, b); };
+        auto jl = [this](int a, int b) { return job_less(a, b); };
+        GoHeap<decltype(ql)> queues(ql);
+        vector<char> qseen(S.queues.size(), 0);
+        std::map<int, GoHeap<decltype(jl)>> preemptors;
+        std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;
+        for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
+            HJob& j = S.jobs[jb];
+            if (!qseen[j.queue]) { qseen[j.queue] = 1; queues.push(j.queue); }
+            vector<int> pend = pending_sorted(j);
+            if (pend.empty()) continue;
+            auto it = preemptors.find(j.queue);
+            if (it == preemptors.end()) it = preemptors.emplace(j.queue, GoHeap<decltype(jl)>(jl)).first;
+            it->second.push(jb);
+            ptasks[jb] = {std::move(pend), 0};
+        }
+        vector<int> order, cands, victims;
+        while (!queues.empty()) {
+            const int qi = queues.pop();
+            if (overused(qi)) continue;
+            auto pit = preemptors.find(qi);
+            if (pit == preemptors.end() || pit->second.empty()) continue;
+            const int jb = pit->second.pop();
+            auto& tq = ptasks[jb];
+            if (tq.second >= tq.first.size()) continue;
+            const int pt = tq.first[tq.second++];
+            const HPod& pr = S.pods[pt];
+            if (pr.cls < 0) throw Error(KBHIP_EUNSUPPORTED, "reclaimer without a task class");
+            const int jq = S.jobs[jb].queue;
+            bool assigned = false;
+            rank_nodes(pr.cls, false, order);
+            for (int n : order) {
+                cands.clear();
+                for (int t : S.node_tasks[n]) {
+                    const HPod& p = S.pods[t];
+                    if (node_copy_running(t) && p.job >= 0 && S.jobs[p.job].queue != jq) cands.push_back(t);
+                }
+                victims_of(false, pt, cands, victims);
+                if (victims.empty()) continue;
+                R3 all, resreq = pr.ireq, got;
+                for (int v : victims) { all.c += S.pods[v].req.c; all.m += S.pods[v].req.m; all.g += S.pods[v].req.g; }
+                if (less_strict(all, resreq)) continue;
+                for (int v : victims) {
+                    const R3 vr = S.pods[v].req;
+                    S.log.emplace_back(v, S.pods[v].node, KBHIP_EVICTED);  // ssn.Evict: cache.Evict first
+                    evict_in_session(v);
+                    got.c += vr.c; got.m += vr.m; got.g += vr.g;
+                    if (le_tol(resreq, vr)) break;
+                    resreq.c -= vr.c; resreq.m -= vr.m; resreq.g -= vr.g;
+                }
+                if (le_tol(pr.ireq, got)) {
+                    pipeline(pt, n);
+                    S.log.emplace_back(pt, n, KBHIP_PIPELINED);
+                    S.stats.placed++;
+                    assigned = true;
+                    break;
+                }
+            }
+            if (assigned) queues.push(qi);
+        }
+        HIPCHK(hipStreamSynchronize(S.stream));
     }
 };
 
@@ -2290,6 +2708,33 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
         return (int)n;
     })
 }
+static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
+                        int64_t cap) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        kbhip::ov_quiesce(s->s);
+        s->s.log.clear();
+        kbhip::Allocator a(s->s);
+        if (preempt) a.preempt_action();
+        else a.reclaim_action();
+        HIPCHK(hipStreamSynchronize(s->s.stream));
+        const int64_t n = (int64_t)s->s.log.size();
+        for (int64_t i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(s->s.log[i]);
+            out_node[i] = std::get<1>(s->s.log[i]);
+            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
+        }
+        return (int)n;
+    })
+}
+int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    return evict_action(s, false, out_pod, out_node, out_kind, cap);
+}
+int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    return evict_action(s, true, out_pod, out_node, out_kind, cap);
+}
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
     ABI_GUARD({
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
@@ -2349,7 +2794,10 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
             s->s.overlap = (int)value;
         }
-        else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
+        else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
+            if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
+            s->s.rank_first = (int)std::min<int64_t>(value, 1 << 20);
+        } else if (std::strcmp(key, "debug_keys") == 0) {  // record per-task sweep keys (tests only)
             kbhip::Session& S = s->s;
             S.debug_keys = value != 0;
             if (S.debug_keys && !S.d_dbg && !S.encode_only) {

@@ -17,7 +17,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KBHIP_LIB") or os.path.join(HERE, "_build", "libkbhip.so")  # KBHIP_LIB: tuning builds
 
-ALLOCATED, PIPELINED = 1, 2
+ALLOCATED, PIPELINED, EVICTED = 1, 2, 3
 STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
 
 # int kbhip_* entry points declared by include/kbhip.h
@@ -26,7 +26,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
-           "kbhip_gang_unschedulable")
+           "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -73,6 +73,8 @@ def lib() -> ctypes.CDLL:
         L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_preempt.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_open_shard.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
         L.kbhip_shard_info.argtypes = [vp, vp]
         L.kbhip_rccl_unique_id.argtypes = [vp, i64]
@@ -147,24 +149,39 @@ class Session:
             raise KbhipError("placement log larger than cap")
         return pod[:n].copy(), node[:n].copy(), kind[:n].copy()
 
-    def backfill(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-        """Run backfillAction.Execute on the current session state."""
+    def _action(self, fn, cap: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         pod = np.zeros(cap, np.int32)
         node = np.zeros(cap, np.int32)
         kind = np.zeros(cap, np.uint8)
-        n = _check(lib().kbhip_backfill(self._h, _p(pod), _p(node), _p(kind), cap))
+        n = _check(fn(self._h, _p(pod), _p(node), _p(kind), cap))
         if n > cap:
             raise KbhipError("placement log larger than cap")
         return pod[:n].copy(), node[:n].copy(), kind[:n].copy()
 
+    def backfill(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Run backfillAction.Execute on the current session state."""
+        return self._action(lib().kbhip_backfill, cap)
+
+    def reclaim(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Run reclaimAction.Execute: (pod, node, EVICTED | PIPELINED) records in decision order."""
+        return self._action(lib().kbhip_reclaim, cap)
+
+    def preempt(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Run preemptAction.Execute: records of the committed statements, in operation order."""
+        return self._action(lib().kbhip_preempt, cap)
+
     def run_actions(self, actions: str = "allocate") -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-        """The conf's actions in order (scheduler.go:93-97); supported: allocate, backfill."""
+        """The conf's actions in order (scheduler.go:93-97): allocate, backfill, reclaim, preempt."""
         logs = []
         for a in (x.strip() for x in actions.split(",")):
             if a == "allocate":
                 logs.append(self.allocate())
             elif a == "backfill":
                 logs.append(self.backfill())
+            elif a == "reclaim":
+                logs.append(self.reclaim())
+            elif a == "preempt":
+                logs.append(self.preempt())
             else:
                 raise KbhipError(f"action {a!r} is not implemented by this engine")
         if not logs:

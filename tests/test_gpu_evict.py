@@ -1,0 +1,99 @@
+"""GPU parity of the reclaim and preempt actions:
+the engine's records — evictions that reach the cache and pipelined
+preemptors, in decision order — and the device node state afterwards equal
+the faithful restatement's (oracle/kbref.cpp reclaimExecute / preemptExecute)
+on the same snapshot.  Records are compared as (pod, node, status) with the
+oracle's TaskStatus codes: 4 Allocated, 8 Pipelined, 128 Releasing (evicted)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+STATUS = {1: 4, 2: 8, 3: 128}
+FEATURES = ("selector", "taints", "ports", "init", "bestEffort", "unsched")
+TIERS = [
+    None,                                                          # shipped kube-batch-conf.yaml
+    [["priority", "gang", "drf", "predicates", "proportion", "nodeorder"]],  # one tier: drf / proportion intersect
+    [["drf", "predicates", "nodeorder"], ["gang", "proportion"]],
+    [["priority", "conformance"], ["drf", "proportion", "predicates", "nodeorder"]],
+]
+ACTIONS = ["reclaim", "preempt", "reclaim, allocate, backfill, preempt", "allocate, preempt"]
+
+
+def _engine(engine, path, actions):
+    with engine.Session(path) as s:
+        pod, node, kind = s.run_actions(actions)
+        n_nodes = s.stats()["nodes"]
+        ns = s.read_nodes(n_nodes)
+    return [(int(p), int(n), STATUS[int(k)]) for p, n, k in zip(pod, node, kind)], ns
+
+
+def _check(engine, oracle_mod, path, actions):
+    exp, ons = oracle_mod.ref_allocate(path, actions=actions, with_nodes=True)
+    got, ns = _engine(engine, path, actions)
+    assert got == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
+    return got
+
+
+def _hand(kbgen, pend_queue, pend_min):
+    GI = 1 << 30
+    c = kbgen.Cluster()
+    c.add_node("n0", 4000, 8 * GI, 0, 110)
+    c.add_queue("q0", 1)
+    c.add_queue("q1", 1)
+    c.add_job("ns1", "r0", "q0", min_member=1)
+    c.add_pod("ns1", "r0-0", uid="a0", group="r0", node="n0", phase="Running", containers=[kbgen.res(cpu=4000, mem=GI)])
+    c.add_job("ns2", "p0", pend_queue, min_member=pend_min)
+    c.add_pod("ns2", "p0-0", uid="b0", group="p0", priority=10, containers=[kbgen.res(cpu=2000, mem=GI)])
+    return c
+
+
+@pytest.mark.parametrize("case", [("q1", 1, "reclaim", [(0, 0, 128), (1, 0, 8)]),
+                                  ("q0", 0, "preempt", [(0, 0, 128), (1, 0, 8)]),
+                                  ("q0", 1, "preempt", [])])
+def test_known_answers(engine, oracle_mod, kbgen_mod, tmp_path, case):
+    q, mn, actions, exp = case
+    p = _hand(kbgen_mod, q, mn).write(str(tmp_path / "h.kbs"))
+    assert _check(engine, oracle_mod, p, actions) == exp
+
+
+@pytest.mark.parametrize("seed", range(48))
+def test_random_preempt_snapshots(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    c = kbgen_mod.gen_preempt(500 + seed, n_nodes=4 + seed % 10, n_queues=1 + seed % 4, n_run_jobs=4 + seed % 9,
+                              n_pend_jobs=2 + seed % 5, max_tasks=1 + seed % 6, tiers=TIERS[seed % len(TIERS)],
+                              features=FEATURES if seed % 2 else ())
+    p = c.write(str(tmp_path / "s.kbs"))
+    _check(engine, oracle_mod, p, ACTIONS[seed % len(ACTIONS)])
+
+
+@pytest.mark.parametrize("first", [1, 3])
+def test_chunked_readback(engine, oracle_mod, kbgen_mod, tmp_path, first):
+    """Passing-node lists longer than the keys read back with the count (option
+    rank_first, 2048 by default) are fetched in a second copy."""
+    exp_all = []
+    for seed in range(6):
+        c = kbgen_mod.gen_preempt(900 + seed, n_nodes=24, n_queues=3, n_run_jobs=14, n_pend_jobs=5, max_tasks=5)
+        p = c.write(str(tmp_path / f"c{seed}.kbs"))
+        actions = "reclaim, allocate, backfill, preempt"
+        exp, ons = oracle_mod.ref_allocate(p, actions=actions, with_nodes=True)
+        with engine.Session(p) as s:
+            s.set_option("rank_first", first)
+            pod, node, kind = s.run_actions(actions)
+            ns = s.read_nodes(24)
+        assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, node, kind)] == exp.as_list()
+        assert np.array_equal(ns.astype(np.float64), ons[:24])
+        exp_all += exp.as_list()
+    assert any(k == 128 for _, _, k in exp_all)
+
+
+def test_pod_affinity_rejected(engine, kbgen_mod, tmp_path):
+    c = _hand(kbgen_mod, "q1", 1)
+    term = {"selector": {"ml": {"job": "r0"}, "me": []}, "topology_key": "kubernetes.io/hostname"}
+    c.add_job("ns2", "p1", "q1", min_member=1)
+    c.add_pod("ns2", "p1-0", uid="b1", group="p1", containers=[kbgen_mod.res(cpu=100, mem=1 << 20)],
+              affinity={"anti": {"required": [term]}})
+    p = c.write(str(tmp_path / "a.kbs"))
+    with engine.Session(p) as s:
+        with pytest.raises(engine.KbhipError):
+            s.reclaim()
