@@ -1,0 +1,94 @@
+"""C5 what-if sessions (a parity-test config, not the
+headline bench line — bench.py measures C4).  Each session: open a 50k-node
+snapshot (~90 % filled, 5 % backfill pods) with a different 2k-task
+high-priority pending set, run the shipped conf's actions
+"reclaim, allocate, backfill, preempt", close.  Prints one JSON line: sessions/s,
+p50 session latency, per-action wall times, records (evictions, pipelines,
+allocations) per session, and the node-ranking sweeps (one per reclaim /
+preempt task) with their mean wall time.
+
+Usage: python bench_c5.py [--sessions S] [--warmup W] [--nodes N] [--pending T]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+import kbgen  # noqa: E402
+import kbhip  # noqa: E402
+
+ACTIONS = ("reclaim", "allocate", "backfill", "preempt")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sessions", type=int, default=8)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--nodes", type=int, default=50_000)
+    ap.add_argument("--pending", type=int, default=2000)
+    ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
+    args = ap.parse_args()
+    os.makedirs(args.cache, exist_ok=True)
+    bufs = []
+    for k in range(args.warmup + args.sessions):
+        p = os.path.join(args.cache, f"c5_{args.nodes}_{args.pending}_{k}.kbs")
+        if not os.path.exists(p):
+            kbgen.gen_c5(p + ".tmp", seed=kbgen.BASE_SEED + 5 + k, n_nodes=args.nodes, n_pending=args.pending)
+            os.replace(p + ".tmp", p)
+        with open(p, "rb") as f:
+            bufs.append(f.read())
+    lat, phases, recs, sweeps = [], {a: [] for a in ("open",) + ACTIONS + ("close",)}, [], []
+    for k, buf in enumerate(bufs):
+        t0 = time.perf_counter()
+        s = kbhip.Session(buf, device=0)
+        t = [time.perf_counter()]
+        counts = {1: 0, 2: 0, 3: 0}
+        n_rank = 0
+        for a in ACTIONS:
+            sw0 = s.stats()["sweeps"]
+            t.append(time.perf_counter())
+            _, _, kind = getattr(s, a)()
+            for v in kind.tolist():
+                counts[v] += 1
+            t[-1] = (t[-1], time.perf_counter())
+            if a in ("reclaim", "preempt"):
+                n_rank += s.stats()["sweeps"] - sw0  # one node-ranking sweep per reclaim / preempt task
+        s.close()
+        t_end = time.perf_counter()
+        if k < args.warmup:
+            continue
+        lat.append(t_end - t0)
+        phases["open"].append(t[0] - t0)
+        for i, a in enumerate(ACTIONS):
+            phases[a].append(t[i + 1][1] - t[i + 1][0])
+        phases["close"].append(t_end - t[-1][1])
+        recs.append(counts)
+        sweeps.append(n_rank)
+    evict_s = sum(statistics.mean(phases[a]) for a in ("reclaim", "preempt"))
+    out = {
+        "metric": "C5 what-if sessions/s (reclaim, allocate, backfill, preempt)",
+        "value": len(lat) / sum(lat),
+        "unit": "sessions/s",
+        "n_gpus": 1,
+        "sessions": len(lat),
+        "p50_session_ms": statistics.median(lat) * 1e3,
+        "higher_is_better": True,
+        "data": "synthetic (kbgen.gen_c5, seeds 20261015+5+k)",
+        "config": {"workload": "C5: 50k nodes ~90% filled, 5% backfill pods, 2k-task high-priority pending set per "
+                               "session, 4 queues, shipped conf", "nodes": args.nodes, "pending": args.pending},
+        "phases_ms": {a: round(statistics.mean(v) * 1e3, 3) for a, v in phases.items()},
+        "records_per_session": {"evicted": statistics.mean(r[3] for r in recs),
+                                "pipelined": statistics.mean(r[2] for r in recs),
+                                "allocated": statistics.mean(r[1] for r in recs)},
+        "rank_sweeps_per_session": statistics.mean(sweeps),
+        "reclaim_preempt_us_per_rank_sweep": evict_s / max(statistics.mean(sweeps), 1) * 1e6,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

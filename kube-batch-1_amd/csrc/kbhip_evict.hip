@@ -69,6 +69,21 @@ __global__ __launch_bounds__(64) void k_node_op(NodeCols nc, DevTables t, int op
     }
 }
 
+// Accumulated evictions (op 0 of k_node_op, summed per node on the host):
+// Releasing += d[3 i .. 3 i + 2] on node[i]; the nodes are distinct.
+__global__ __launch_bounds__(kBlock) void k_rel_add(NodeCols nc, const int32_t* node, const int64_t* d, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int v = node[i];
+    nc.rel_cpu[v] += d[3 * i]; nc.rel_mem[v] += d[3 * i + 1]; nc.rel_gpu[v] += d[3 * i + 2];
+}
+
+hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t* d, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rel_add, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, nc, node, d, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
                              int by_score, uint64_t* keys, uint32_t* count, hipStream_t st) {
     int grid = (nc.n + kBlock - 1) / kBlock;

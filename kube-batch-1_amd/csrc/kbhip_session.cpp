@@ -320,6 +320,10 @@ struct Session {
     size_t h_rank_cap = 0;
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
+    vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
+    vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
+    vector<uint8_t> rel_flag;        // node is in rel_touched
+    DevBuf b_rel_nodes, b_rel_d;
     int32_t fallback = -1;  // lowest node index holding a session-placed pod (nodeorder.go:78-93)
     // device
     Conf conf{};
@@ -2259,8 +2263,34 @@ struct Allocator {
     // the session half of an eviction (session.go:331-356 / statement.go:35-67)
     void evict_in_session(int v) {
         set_status(v, Releasing);
-        dev_op(0, v);  // node.UpdateTask: Releasing += Resreq
+        // node.UpdateTask: Releasing += Resreq.  No node ranking reads Releasing, so
+        // evictions are summed per node and applied in one launch (flush_evictions)
+        const HPod& p = S.pods[v];
+        if (S.rel_delta.empty()) { S.rel_delta.assign(S.nc.n, R3{}); S.rel_flag.assign(S.nc.n, 0); }
+        if (!S.rel_flag[p.node]) { S.rel_flag[p.node] = 1; S.rel_touched.push_back(p.node); }
+        R3& d = S.rel_delta[p.node];
+        d.c += p.req.c; d.m += p.req.m; d.g += p.req.g;
         on_deallocate(v);
+    }
+    void flush_evictions() {
+        const int n = (int)S.rel_touched.size();
+        if (!n) return;
+        vector<int32_t> nodes(n);
+        vector<int64_t> d(3 * (size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const int v = S.rel_touched[i];
+            nodes[i] = v;
+            d[3 * i] = S.rel_delta[v].c; d[3 * i + 1] = S.rel_delta[v].m; d[3 * i + 2] = S.rel_delta[v].g;
+            S.rel_delta[v] = R3{};
+            S.rel_flag[v] = 0;
+        }
+        S.rel_touched.clear();
+        int32_t* dn = S.b_rel_nodes.alloc<int32_t>(n);
+        int64_t* dd = S.b_rel_d.alloc<int64_t>(3 * (size_t)n);
+        HIPCHK(hipMemcpyAsync(dn, nodes.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, S.stream));
+        HIPCHK(hipMemcpyAsync(dd, d.data(), d.size() * sizeof(int64_t), hipMemcpyHostToDevice, S.stream));
+        HIPCHK(launch_rel_add(S.nc, dn, dd, n, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));  // the pageable sources must outlive the copies
     }
     void unevict(int v) {  // statement.go:81-105: node.AddTask fails, the node keeps its Releasing copy
         set_status(v, Running);
@@ -2484,6 +2514,7 @@ struct Allocator {
                 }
             }
         }
+        flush_evictions();
     }
     void reclaim_action() {  // reclaim.go:41-196
         compile_orders();
@@ -2550,6 +2581,7 @@ struct Allocator {
             }
             if (assigned) queues.push(qi);
         }
+        flush_evictions();
         HIPCHK(hipStreamSynchronize(S.stream));
     }
 };

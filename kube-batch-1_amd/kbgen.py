@@ -535,7 +535,7 @@ GPU_P = [0.75, 0.0625, 0.0625, 0.0625, 0.0625]
 
 def _bulk(n_nodes: int, n_pending: int, running_per_node: np.ndarray, seed: int,
           n_queues: int = 1, tiers=None, gang_lo: int = 8, gang_hi: int = 64,
-          running_gang: int = 8) -> Tuple[Dict[str, np.ndarray], StrTab, dict]:
+          running_gang: int = 8, run_res=None) -> Tuple[Dict[str, np.ndarray], StrTab, dict]:
     """Vectorised resource-only cluster (C2/C4 family) written straight to columns."""
     rng = np.random.default_rng(seed)
     st = StrTab()
@@ -572,6 +572,8 @@ def _bulk(n_nodes: int, n_pending: int, running_per_node: np.ndarray, seed: int,
     n_run = int(r_node.size)
     r_cpu = rng.choice(CPU_CHOICES, size=n_run)
     r_mem = rng.choice(MEM_CHOICES, size=n_run)
+    if run_res is not None:  # caller-chosen running requests (gen_c5: within each node's allocatable)
+        r_cpu, r_mem = run_res(r_node)
     n_rjobs = (n_run + running_gang - 1) // running_gang
     r_job = np.arange(n_run) // running_gang
 
@@ -907,3 +909,49 @@ def gen_preempt(seed: int, n_nodes: int = 8, n_queues: int = 3, n_run_jobs: int 
                       init_containers=inits, node_selector=nsel, tolerations=tols)
             uid += 1
     return c
+
+
+def gen_c5(path: str, seed: int = BASE_SEED + 5, n_nodes: int = 50_000, n_pending: int = 2000, n_queues: int = 4,
+           fill: float = 0.9, backfill_frac: float = 0.05, best_effort: int = 200, run_min1: float = 0.5) -> dict:
+    """C5: a what-if session for reclaim / allocate / backfill / preempt.
+    Nodes of the C2 SKU mix filled with Running pods up to ~`fill` of their cpu and
+    memory (a prefix of random C2-sized pods per node), 5 % of them backfill-annotated;
+    running jobs of 8 pods spread over `n_queues` queues (weights 1..n), half of them
+    with minMember 1 (their pods are gang-preemptable); `n_pending` pending tasks of
+    priority-100 jobs (minMember = size / 1 / 0), the last `best_effort` of them BestEffort.
+    Each seed is one session's pending set (the S what-if sessions differ by seed)."""
+    rng0 = np.random.default_rng(seed)  # _bulk's first draw: the node SKUs
+    sku = rng0.choice(len(SKUS), size=n_nodes, p=SKU_P)
+    sk = np.asarray(SKUS, dtype=np.int64)
+    rng = np.random.default_rng(seed + 2000)
+    K = 64
+    cpu = rng.choice(CPU_CHOICES, size=(n_nodes, K))
+    mem = rng.choice(MEM_CHOICES, size=(n_nodes, K))
+    ok = (np.cumsum(cpu, axis=1) <= fill * sk[sku, 0][:, None]) & (np.cumsum(mem, axis=1) <= fill * sk[sku, 1][:, None])
+    rpn = np.minimum(ok.cumprod(axis=1).sum(axis=1), 100).astype(np.int64)  # pods cap 110
+    keep = np.arange(K)[None, :] < rpn[:, None]
+    run_cpu, run_mem = cpu[keep], mem[keep]  # row-major = node order, matching _bulk's r_node
+
+    def run_res(r_node):
+        assert r_node.size == run_cpu.size
+        return run_cpu, run_mem
+
+    C, st, meta = _bulk(n_nodes, n_pending, rpn, seed, n_queues=n_queues, run_res=run_res)
+    n_run, n_pjobs = meta["running"], meta["pending_jobs"]
+    n_rjobs = meta["jobs"] - n_pjobs
+    C["p_backfill"][:n_run] = (rng.random(n_run) < backfill_frac).astype(np.uint8)
+    C["p_priority"][n_run:] = 100
+    C["p_priority"][:n_run] = 0
+    C["j_pg_priority"][:n_pjobs] = 100
+    jmin = C["j_min"]
+    jmin[n_pjobs:] = np.where(rng.random(n_rjobs) < run_min1, 1, jmin[n_pjobs:])
+    pick = rng.random(n_pjobs)
+    jmin[:n_pjobs] = np.where(pick < 0.15, 0, np.where(pick < 0.3, 1, jmin[:n_pjobs]))
+    if best_effort:
+        be = np.arange(n_run + n_pending - best_effort, n_run + n_pending)
+        for k in ("c_cpu", "c_mem", "c_gpu"):
+            C[k][be] = 0
+        C["c_has"][be] = 0
+    write_kbs(path, C, st)
+    meta.update(running_per_node=float(rpn.mean()), backfill_pods=int(C["p_backfill"].sum()), rpn=rpn)
+    return meta

@@ -97,3 +97,41 @@ def test_pod_affinity_rejected(engine, kbgen_mod, tmp_path):
     with engine.Session(p) as s:
         with pytest.raises(engine.KbhipError):
             s.reclaim()
+
+
+# ---- C5: the what-if session shape -----------------------------
+C5_ACTIONS = "reclaim, allocate, backfill, preempt"
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_c5_scaled_parity(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """C5's generator at a size the faithful restatement finishes in seconds."""
+    p = str(tmp_path / "c5s.kbs")
+    kbgen_mod.gen_c5(p, seed=kbgen_mod.BASE_SEED + 5 + seed, n_nodes=90, n_pending=80, best_effort=8)
+    got = _check(engine, oracle_mod, p, C5_ACTIONS)
+    assert any(k == 128 for _, _, k in got)
+
+
+def test_c5_full_size_invariants(engine, kbgen_mod, tmp_path):
+    """50k nodes x 1.45M running pods, 2k pending: properties that hold at any size —
+    evicted pods were Running on the recorded node and are evicted once; pipelined /
+    allocated pods were Pending (or BestEffort-backfilled); a second session on the
+    same snapshot reproduces the records exactly."""
+    p = str(tmp_path / "c5.kbs")
+    meta = kbgen_mod.gen_c5(p)
+    runs = []
+    for _ in range(2):
+        with engine.Session(p) as s:
+            pod, node, kind = s.run_actions(C5_ACTIONS)
+        runs.append((pod, node, kind))
+    pod, node, kind = runs[0]
+    assert all(np.array_equal(a, b) for a, b in zip(runs[0], runs[1]))
+    n_run = meta["running"]
+    ev = kind == 3
+    assert ev.any() and (kind == 2).any() and (kind == 1).any()
+    assert (pod[ev] < n_run).all()                       # running pods sort first (kbgen._bulk)
+    assert np.unique(pod[ev]).size == int(ev.sum())       # never evicted twice
+    assert (pod[~ev] >= n_run).all()                      # only pending pods are placed
+    # the recorded node of an eviction is the victim's node (running pods are laid out node by node)
+    run_node = np.repeat(np.arange(meta["nodes"]), meta["rpn"])
+    assert (run_node[pod[ev]] == node[ev]).all()
