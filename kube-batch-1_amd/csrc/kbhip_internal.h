@@ -26,7 +26,10 @@ struct DevTables {
 // [lo, hi, F, max key]: rows of 2 npad + 4 words per task of the chunk; commit_here = the last block commits (one GPU).  Sharded
 // sessions reduce ctrl->slot[task_i] across shards and then launch_commit_task.
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st, bool commit_here = true, uint64_t* dbg = nullptr);
+                               uint64_t* walk, hipStream_t st, bool commit_here = true, uint64_t* dbg = nullptr,
+                               bool defer_visits = false);
+// defer_visits (one GPU): the GetAccessibleResource mutation of the walk runs as a
+// second, grid-wide kernel (k_visit_mutate) instead of in the committing block.
 hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
                               hipStream_t st);
 // Inter-pod affinity priority prepass: min / max of the raw count over all

@@ -143,7 +143,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // GetAccessibleResource mutation of the visited nodes of this shard.  Run by
 // one block: the last sweep block (one GPU) or k_commit_task (sharded).
 __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const TaskClass& c,
-                            bool first_fit, bool track, const uint64_t* walk) {
+                            bool first_fit, bool track, const uint64_t* walk, bool defer_visits = false) {
     __shared__ uint64_t win;
     if (threadIdx.x == 0) {
         const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -184,6 +184,10 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
         }
     }
     __syncthreads();
+    if (defer_visits) {  // k_visit_mutate does the loop below over the whole grid
+        if (threadIdx.x == 0) ctrl->pad = track ? 1 : 0;
+        return;
+    }
     if (!track) return;
     // GetAccessibleResource mutation for every other visited node of this shard.
     const uint64_t k = win;
@@ -254,8 +258,27 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
         d[0] = (uint64_t)ilo; d[1] = (uint64_t)ihi; d[2] = (uint64_t)(int64_t)F;
         d[3] = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (!commit_here) return;
-    commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk);
+    if (!(commit_here & 1)) return;
+    commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk, (commit_here & 2) != 0);
+}
+
+// The GetAccessibleResource mutation of task task_i's walk (node_info.go:209-211,
+// SURVEY Appendix A.1) over the whole grid, after k_sweep_argmax committed it
+// with the mutation deferred (one block looping over every node is a chain of
+// N / kBlock dependent memory round trips).  Runs only if task_i was swept
+// (n_done == task_i + 1) and its sweep tracked the walk (pad, set by commit_task).
+__global__ __launch_bounds__(kBlock) void k_visit_mutate(NodeCols nc, const PopCtrl* ctrl, int task_i,
+                                                         const uint64_t* walk) {
+    if (ctrl->n_done != task_i + 1 || !ctrl->pad) return;  // uniform
+    const uint64_t k = ctrl->slot[task_i];
+    const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
+    const int wn = k ? key_idx(k) : -1;
+    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+        const uint64_t v = walk[n];
+        if (!v || n + nc.base == wn) continue;
+        if (k && v < wk) continue;
+        nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
+    }
 }
 
 // Sharded sessions: the commit after the cross-shard max of ctrl->slot[task_i].
@@ -1380,12 +1403,15 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st, bool commit_here, uint64_t* dbg) {
+                               uint64_t* walk, hipStream_t st, bool commit_here, uint64_t* dbg, bool defer_visits) {
     int grid = (nc.n + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk,
-                       commit_here ? 1 : 0, dbg);
+    const int mode = commit_here ? (defer_visits ? 3 : 1) : 0;
+    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk, mode, dbg);
+    if (commit_here && defer_visits)
+        hipLaunchKernelGGL(k_visit_mutate, dim3(grid), dim3(kBlock), 0, st, nc, (const PopCtrl*)ctrl, task_i,
+                           (const uint64_t*)walk);
     return hipGetLastError();
 }
 

@@ -1302,13 +1302,16 @@ static void exchange(Session& S, void* dev, int op) {
 
 // One task of the per-task path: [IPA min/max prepass + exchange], sweep,
 // [cross-shard max of the key + commit].
-static void sweep_task(Session& S, int i, int cls) {
+// defer_visits: the walk's GetAccessibleResource mutation as a grid-wide second
+// kernel (worth it whenever some node may carry Backfilled resources).
+static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
     if (S.classes[cls].ipa_n > 0) {
         HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
         exchange(S, &S.d_ctrl->ipa_lo[i], KBHIP_RED_MIN_I64);
         exchange(S, &S.d_ctrl->ipa_hi[i], KBHIP_RED_MAX_I64);
     }
-    HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1, S.d_dbg));
+    HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1, S.d_dbg,
+                               defer_visits && S.world == 1));
     if (S.world > 1) {
         exchange(S, &S.d_ctrl->slot[i], KBHIP_RED_MAX_U64);
         HIPCHK(launch_commit_task(S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));
@@ -1613,9 +1616,11 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
             std::memset(h.fit, 0, sizeof h.fit);
             HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+            bool defer = S.any_bf != 0;  // a backfill-annotated task may set any_bf on the device mid-chunk
+            for (int i = 0; i < m; ++i) defer = defer || S.classes[h.cls[i]].backfill;
             for (int i = 0; i < m; ++i) {
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
-                sweep_task(S, i, h.cls[i]);
+                sweep_task(S, i, h.cls[i], defer);
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
             }
             S.stats.sweeps += m;
