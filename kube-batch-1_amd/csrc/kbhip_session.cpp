@@ -1580,7 +1580,11 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
         const bool batch = batchable(S, cls0);
-        if (!batch) m = std::min(n - done, kMaxChunk);  // general path: up to a chunk of mixed classes
+        if (!batch) {  // general path: up to a chunk of mixed classes, no longer than the pop can run
+            m = std::min(n - done, kMaxChunk);  // (it stops once Ready: after `need` more Allocated tasks)
+            const int need = gang_mode ? min_avail - ready_count : 1;
+            m = std::min(m, std::max(need, 1));
+        }
         // sampled HIP-event timing of a general-path launch (kbhip_set_option "time_every")
         const bool timed = !batch && S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
         if (timed && !S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
