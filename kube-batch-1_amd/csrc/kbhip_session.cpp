@@ -2344,29 +2344,40 @@ struct Allocator {
     // Session.Preemptable / Reclaimable (session_plugins.go:67-148): per tier the
     // intersection of the enabled plugins' victims; the first non-empty tier decides,
     // and once a plugin has answered later tiers only intersect further.
+    // per-call scratch keyed by job / queue slot, valid where stamp == the call's epoch
+    vector<uint32_t> ready_stamp, alloc_stamp;
+    vector<int> ready_val;
+    vector<F3> alloc_val;
+    uint32_t epoch = 0;
+    vector<int> cand, inter;
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
         victims.clear();
+        if (evictees.empty()) return;  // every plugin returns nil for no candidates
         bool init = false;
-        vector<int> cand, inter;
-        std::unordered_map<int, int> ready;  // readyTaskNum per job (gang.go:212-222)
-        std::unordered_map<int, F3> alloc;
+        if (ready_stamp.empty()) {
+            const size_t J = S.jobs.size(), Q = S.queues.size();
+            ready_stamp.assign(J, 0); ready_val.assign(J, 0);
+            alloc_stamp.assign(std::max(J, Q), 0); alloc_val.assign(std::max(J, Q), F3{});
+        }
+        const uint32_t ep = ++epoch;  // readyTaskNum counts do not change within one call
         for (auto& tier : S.tiers) {
             for (auto& pl : tier) {
                 if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
                 cand.clear();
                 if (pl.name == "gang") {  // gang.go:107-129
                     for (int e : evictees) {
-                        const HJob& j = S.jobs[S.pods[e].job];
-                        auto it = ready.find(S.pods[e].job);
-                        if (it == ready.end()) {
+                        const int jb = S.pods[e].job;
+                        const HJob& j = S.jobs[jb];
+                        if (ready_stamp[jb] != ep) {  // readyTaskNum (gang.go:212-222)
                             int c = 0;
                             for (int t : j.tasks) {
                                 const int st = S.pods[t].status;
                                 if (allocated_status(st) || st == Succeeded || st == Pipelined) ++c;
                             }
-                            it = ready.emplace(S.pods[e].job, c).first;
+                            ready_stamp[jb] = ep;
+                            ready_val[jb] = c;
                         }
-                        if (j.min_avail <= it->second - 1 || j.min_avail == 1) cand.push_back(e);
+                        if (j.min_avail <= ready_val[jb] - 1 || j.min_avail == 1) cand.push_back(e);
                     }
                 } else if (pl.name == "conformance") {  // conformance.go:37-56
                     for (int e : evictees) if (!S.pods[e].critical) cand.push_back(e);
@@ -2375,27 +2386,25 @@ struct Allocator {
                     F3 la = S.jobs[pr.job].drf_alloc;
                     la.add(pr.req);
                     const double ls = drf_share_of(la);
-                    alloc.clear();
+                    const uint32_t ea = ++epoch;
                     for (int e : evictees) {
                         const int jb = S.pods[e].job;
-                        auto it = alloc.find(jb);
-                        if (it == alloc.end()) it = alloc.emplace(jb, S.jobs[jb].drf_alloc).first;
-                        it->second.sub(S.pods[e].req);
-                        const double rs = drf_share_of(it->second);
+                        if (alloc_stamp[jb] != ea) { alloc_stamp[jb] = ea; alloc_val[jb] = S.jobs[jb].drf_alloc; }
+                        alloc_val[jb].sub(S.pods[e].req);
+                        const double rs = drf_share_of(alloc_val[jb]);
                         if (ls < rs || std::fabs(ls - rs) <= 0.000001) cand.push_back(e);  // shareDelta (drf.go:29)
                     }
                 } else if (!preempt && pl.name == "proportion" && S.prop_on) {  // proportion.go:159-183
-                    alloc.clear();
+                    const uint32_t ea = ++epoch;
                     for (int e : evictees) {
                         const int qi = S.jobs[S.pods[e].job].queue;
                         const HQueue& q = S.queues[qi];
-                        auto it = alloc.find(qi);
-                        if (it == alloc.end()) it = alloc.emplace(qi, q.allocated).first;
+                        if (alloc_stamp[qi] != ea) { alloc_stamp[qi] = ea; alloc_val[qi] = q.allocated; }
                         F3 rq;
                         rq.add(S.pods[e].req);
-                        if (it->second.less(rq)) continue;
-                        it->second.sub(S.pods[e].req);
-                        if (q.deserved.less_equal(it->second)) cand.push_back(e);
+                        if (alloc_val[qi].less(rq)) continue;
+                        alloc_val[qi].sub(S.pods[e].req);
+                        if (q.deserved.less_equal(alloc_val[qi])) cand.push_back(e);
                     }
                 } else {
                     continue;  // the plugin registers no such function
