@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--pending", type=int, default=2000)
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the hoisted CPU restatement on one session")
     args = ap.parse_args()
     os.makedirs(args.cache, exist_ok=True)
     bufs = []
@@ -87,6 +88,18 @@ def main():
         "rank_sweeps_per_session": statistics.mean(sweeps),
         "reclaim_preempt_us_per_rank_sweep": evict_s / max(statistics.mean(sweeps), 1) * 1e6,
     }
+    if args.cpu_baseline:  # the hoisted C++ restatement (oracle/kbfast.cpp): one session, same actions
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # the checker / CPU baseline only (test infrastructure)
+        threads = min(16, os.cpu_count() or 1)
+        p0 = os.path.join(args.cache, f"c5_{args.nodes}_{args.pending}_{args.warmup}.kbs")
+        st = {}
+        pl = oracle.fast_allocate(p0, threads=threads, actions=", ".join(ACTIONS), stats=st)
+        sess_s = st["open_s"] + st["allocate_s"]  # plugin open + the four actions (snapshot load excluded)
+        out["cpu_baseline"] = {"value": 1.0 / sess_s, "unit": "sessions/s", "cores": threads, "kind": "port",
+                               "sample": f"one C5 session ({len(pl)} records), actions {', '.join(ACTIONS)}, "
+                                         f"hoisted C++ restatement oracle/kbfast.cpp, {threads} threads on "
+                                         f"{os.cpu_count()} host cpus, snapshot parse excluded"}
     print(json.dumps(out))
 
 

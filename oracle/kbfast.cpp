@@ -179,6 +179,8 @@ struct PodRec {
     int job = -1;  // session job slot
     string jobUID;
     int curNode = -1;  // task.NodeName (node index)
+    bool critical = false;  // kube-system or a system-*-critical priority class (conformance.go:40-45)
+    bool nodeRel = false;   // the node's copy stayed Releasing after an unevict (statement.go:81-105)
     bool hasPodAff() const { return aff && (aff->pa || aff->paa); }
 };
 struct NodeRec {
@@ -438,6 +440,7 @@ struct Loader {
         auto pname = V32("p_name"), pns = V32("p_ns"), pjob = V32("p_job"), pnode = V32("p_node"),
              ppri = V32("p_priority"), paff = V32("p_aff");
         auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+        auto ppcls = s.vec<int32_t>("p_pclass"), pns_raw = s.vec<int32_t>("p_ns");
         auto pts = s.vec<int64_t>("p_ts");
         auto plo = s.offs("p_label_off", P);
         auto plk = V32("pl_key"), plv = V32("pl_val");
@@ -481,6 +484,11 @@ struct Loader {
             p.priority = ppri[i];
             p.ts = pts[i];
             p.backfill = pbf[i];
+            {
+                const string pc = (!ppcls.empty() && ppcls[i] >= 0) ? s.s(ppcls[i]) : string();
+                p.critical = s.s(pns_raw[i]) == "kube-system" || pc == "system-cluster-critical" ||
+                             pc == "system-node-critical";
+            }
             for (int k = pco[i]; k < pco[i + 1]; ++k) {
                 p.req += Res{ccpu[k], cmem[k], cgpu[k]};
                 p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;                 // non_zero.go:43-47
@@ -1261,13 +1269,15 @@ struct Engine {
             status = Pipelined;  // Pipeline (session.go:199-235)
         }
         p.status = status;
+        j.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
         p.curNode = best.idx;
         nodeAddTask(pi, best.idx, status);
         onAllocate(p);
         w.log.emplace_back(pi, best.idx, status);
         if (status == Allocated && jobReady(j)) {
             // dispatch: Allocated -> Binding (both AllocatedStatuses; counts unchanged)
-            for (int t : j.tasks) if (w.pods[t].status == Allocated) w.pods[t].status = Binding;
+            for (int t : j.tasks)
+                if (w.pods[t].status == Allocated) { w.pods[t].status = Binding; j.priority = w.pods[t].priority; }
         }
         return true;
     }
@@ -1297,17 +1307,336 @@ struct Engine {
                 if (first < 0) continue;
                 JobRec& j = w.jobs[jb];
                 p.status = Allocated;  // Session.Allocate(task, node, false)
+                j.priority = p.priority;
                 j.cntAlloc++;
                 p.curNode = first;
                 nodeAddTask(pi, first, Allocated);
                 onAllocate(p);
                 w.log.emplace_back(pi, first, Allocated);
                 if (jobReady(j))
-                    for (int t : j.tasks) if (w.pods[t].status == Allocated) w.pods[t].status = Binding;
+                    for (int t : j.tasks)
+                        if (w.pods[t].status == Allocated) { w.pods[t].status = Binding; j.priority = w.pods[t].priority; }
             }
         }
     }
 
+
+    // ---- reclaim / preempt (hoisted restatement; actions/reclaim/reclaim.go:41-196,
+    // actions/preempt/preempt.go:43-353, framework/statement.go).  Same decisions as
+    // kbref's reclaimExecute / preemptExecute: the node walk of a preemptor is computed
+    // once (threaded O(N) sweep + sort), victims per node in pod order.
+    void requireNoPodAffinity() {
+        for (auto& p : w.pods)
+            if (p.aff && (p.aff->pa || p.aff->paa || !p.aff->paPref.empty() || !p.aff->paaPref.empty()))
+                throw std::runtime_error("reclaim / preempt with pod (anti-)affinity: not restated by this oracle");
+    }
+    static bool leTol(const Res& a, const Res& b) { return le(a, b); }
+    static bool lessStrict(const Res& a, const Res& b) { return a.cpu < b.cpu && a.mem < b.mem && a.gpu < b.gpu; }
+    void setStatus(int pi, int st) {  // JobInfo.UpdateTaskStatus
+        PodRec& p = w.pods[pi];
+        JobRec& j = w.jobs[p.job];
+        if (allocSt(p.status)) j.cntAlloc--;
+        if (p.status == AOB) j.cntAOB--;
+        p.status = st;
+        if (allocSt(st)) j.cntAlloc++;
+        if (st == AOB) j.cntAOB++;
+        j.priority = p.priority;
+    }
+    void onDeallocate(const PodRec& p) {  // drf.go:144-151, proportion.go:211-219
+        if (w.drfOn) { JobRec& j = w.jobs[p.job]; j.drfAlloc.sub(toF(p.req)); drfUpdate(j); }
+        if (w.propOn) { QueueRec& q = w.queues[w.jobs[p.job].queue]; q.allocated.sub(toF(p.req)); propUpdate(q); }
+    }
+    void evictInSession(int v) {  // node.UpdateTask Running -> Releasing: Releasing += Resreq
+        setStatus(v, Releasing);
+        w.nodes[w.pods[v].curNode].rel += w.pods[v].req;
+        onDeallocate(w.pods[v]);
+    }
+    void unevict(int v) {
+        setStatus(v, Running);
+        w.pods[v].nodeRel = true;
+        onAllocate(w.pods[v]);
+    }
+    void pipelineTask(int pi, int ni) {
+        setStatus(pi, Pipelined);
+        w.pods[pi].curNode = ni;
+        nodeAddTask(pi, ni, Pipelined);
+        onAllocate(w.pods[pi]);
+    }
+    void unpipelineTask(int pi) {  // node.RemoveTask of the Pipelined copy
+        PodRec& p = w.pods[pi];
+        NodeRec& n = w.nodes[p.curNode];
+        setStatus(pi, Pending);
+        if (p.backfill) n.bf -= p.req;
+        n.rel += p.req;
+        n.used -= p.req;
+        n.pods--;
+        n.nzc -= p.nzc;
+        n.nzm -= p.nzm;
+        for (auto& pt : p.ports) {
+            if (pt.port <= 0) continue;
+            for (size_t k = n.used_ports.size(); k-- > 0;)
+                if (n.used_ports[k].ip == pt.ip && n.used_ports[k].proto == pt.proto && n.used_ports[k].port == pt.port) {
+                    n.used_ports.erase(n.used_ports.begin() + k);
+                    break;
+                }
+        }
+        n.podList.erase(std::find(n.podList.begin(), n.podList.end(), pi));
+        onDeallocate(p);
+    }
+    bool nodeCopyRunning(int t) const {
+        const PodRec& p = w.pods[t];
+        return p.status == Running && !p.nodeRel;
+    }
+    double drfShareOf(const FRes& a) const {
+        double res = 0;
+        for (int k = 0; k < 3; ++k) { double x = share(a.get(k), w.total.get(k)); if (x > res) res = x; }
+        return res;
+    }
+    vector<int> victims(bool preempt, int evictor, const vector<int>& evictees) {  // session_plugins.go:67-148
+        vector<int> vic;
+        bool init = false;
+        for (auto& tier : w.tiers) {
+            for (auto& pl : tier) {
+                if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
+                vector<int> cand;
+                if (pl.name == "gang") {
+                    for (int e : evictees) {
+                        const JobRec& j = w.jobs[w.pods[e].job];
+                        int ready = 0;
+                        for (int t : j.tasks) {
+                            const int st = w.pods[t].status;
+                            if (allocSt(st) || st == Succeeded || st == Pipelined) ++ready;
+                        }
+                        if (j.minAvail <= ready - 1 || j.minAvail == 1) cand.push_back(e);
+                    }
+                } else if (pl.name == "conformance") {
+                    for (int e : evictees) if (!w.pods[e].critical) cand.push_back(e);
+                } else if (preempt && pl.name == "drf" && w.drfOn) {
+                    const PodRec& pr = w.pods[evictor];
+                    FRes la = w.jobs[pr.job].drfAlloc;
+                    la.add(toF(pr.req));
+                    const double ls = drfShareOf(la);
+                    std::map<int, FRes> alloc;
+                    for (int e : evictees) {
+                        const int jb = w.pods[e].job;
+                        if (!alloc.count(jb)) alloc[jb] = w.jobs[jb].drfAlloc;
+                        alloc[jb].sub(toF(w.pods[e].req));
+                        const double rs = drfShareOf(alloc[jb]);
+                        if (ls < rs || std::fabs(ls - rs) <= 0.000001) cand.push_back(e);
+                    }
+                } else if (!preempt && pl.name == "proportion" && w.propOn) {
+                    std::map<int, FRes> alloc;
+                    for (int e : evictees) {
+                        const int qi = w.jobs[w.pods[e].job].queue;
+                        if (!alloc.count(qi)) alloc[qi] = w.queues[qi].allocated;
+                        FRes& a = alloc[qi];
+                        const FRes rq = toF(w.pods[e].req);
+                        if (a.c < rq.c && a.m < rq.m && a.g < rq.g) continue;
+                        a.sub(rq);
+                        if (w.queues[qi].deserved.lessEqual(a)) cand.push_back(e);
+                    }
+                } else {
+                    continue;
+                }
+                if (!init) { vic = cand; init = true; }
+                else {
+                    vector<int> inter;
+                    for (int v : vic) for (int c : cand) if (v == c) inter.push_back(v);
+                    vic = inter;
+                }
+            }
+            if (!vic.empty()) return vic;
+        }
+        return vic;
+    }
+    vector<int> nodeTasksSorted(int ni) const {  // NodeInfo.Tasks in pinned (pod) order
+        vector<int> v = w.nodes[ni].podList;
+        std::sort(v.begin(), v.end());
+        return v;
+    }
+    vector<int> preemptWalk(int pi) {  // predicate + score sweep, util.SelectBestNode order
+        TaskPlan tp;
+        tp.pod = pi;
+        buildPlan(w, tp);
+        const int N = (int)w.nodes.size(), T = pool.T;
+        vector<uint64_t> keys(N, 0);
+        pool.run([&](int t) {
+            int lo = (int)((int64_t)N * t / T), hi = (int)((int64_t)N * (t + 1) / T);
+            for (int ni = lo; ni < hi; ++ni) {
+                int sc;
+                if (evalNode(w, tp, ni, &sc)) keys[ni] = packKey(sc, ni, 0);
+            }
+        });
+        std::sort(keys.begin(), keys.end(), std::greater<uint64_t>());
+        vector<int> order;
+        for (uint64_t k : keys) { if (!k) break; order.push_back(0x7fffffff - (int)((k >> 1) & 0x7fffffff)); }
+        return order;
+    }
+    struct Op { int kind, pod; };  // 0 evict, 1 pipeline
+    bool preemptOne(vector<Op>& ops, int pi, const std::function<bool(int)>& keep) {
+        tried++;
+        const PodRec& pr = w.pods[pi];
+        for (int ni : preemptWalk(pi)) {
+            vector<int> cands;
+            for (int t : nodeTasksSorted(ni)) if (keep(t)) cands.push_back(t);
+            vector<int> vic = victims(true, pi, cands);
+            if (vic.empty()) continue;
+            Res all{0, 0, 0}, resreq = pr.initReq, got{0, 0, 0};
+            for (int v : vic) all += w.pods[v].req;
+            if (lessStrict(all, resreq)) continue;
+            for (int v : vic) {
+                const Res vr = w.pods[v].req;
+                evictInSession(v);
+                ops.push_back({0, v});
+                got += vr;
+                if (leTol(resreq, vr)) break;
+                resreq -= vr;
+            }
+            if (leTol(pr.initReq, got)) {
+                pipelineTask(pi, ni);
+                ops.push_back({1, pi});
+                return true;
+            }
+        }
+        return false;
+    }
+    void commitOps(vector<Op>& ops) {
+        for (auto& o : ops) w.log.emplace_back(o.pod, w.pods[o.pod].curNode, o.kind == 0 ? Releasing : Pipelined);
+        ops.clear();
+    }
+    void discardOps(vector<Op>& ops) {
+        for (size_t i = ops.size(); i-- > 0;) {
+            if (ops[i].kind == 0) unevict(ops[i].pod);
+            else unpipelineTask(ops[i].pod);
+        }
+        ops.clear();
+    }
+    vector<int> pendingSorted(const JobRec& j) {
+        vector<int> v;
+        for (int t : j.tasks) if (w.pods[t].status == Pending) v.push_back(t);
+        std::sort(v.begin(), v.end(), [this](int a, int b) { return taskLess(a, b); });
+        return v;
+    }
+    void preempt() {  // preempt.go:43-255
+        requireNoPodAffinity();
+        auto jl = [this](int a, int b) { return jobLess(a, b); };
+        std::map<int, Heap<decltype(jl)>> preemptors;
+        std::map<int, std::pair<vector<int>, size_t>> ptasks;
+        vector<int> under;
+        vector<char> seen(w.queues.size(), 0);
+        for (int jb = 0; jb < (int)w.jobs.size(); ++jb) {
+            seen[w.jobs[jb].queue] = 1;
+            vector<int> pend = pendingSorted(w.jobs[jb]);
+            if (pend.empty()) continue;
+            auto it = preemptors.find(w.jobs[jb].queue);
+            if (it == preemptors.end()) it = preemptors.emplace(w.jobs[jb].queue, Heap<decltype(jl)>(jl)).first;
+            it->second.push(jb);
+            under.push_back(jb);
+            ptasks[jb] = {pend, 0};
+        }
+        vector<Op> ops;
+        for (int qi = 0; qi < (int)w.queues.size(); ++qi) {
+            if (!seen[qi]) continue;
+            for (;;) {
+                auto pit = preemptors.find(qi);
+                if (pit == preemptors.end() || pit->second.empty()) break;
+                const int pj = pit->second.pop();
+                bool assigned = false;
+                auto& tq = ptasks[pj];
+                for (;;) {
+                    if (tq.second >= tq.first.size()) break;
+                    const int pt = tq.first[tq.second++];
+                    const int pq = w.jobs[pj].queue, ptj = w.pods[pt].job;
+                    if (preemptOne(ops, pt, [&](int t) {
+                            const PodRec& p = w.pods[t];
+                            return nodeCopyRunning(t) && p.job >= 0 && w.jobs[p.job].queue == pq && ptj != p.job;
+                        }))
+                        assigned = true;
+                    if (jobReady(w.jobs[pj])) { commitOps(ops); break; }
+                }
+                if (!jobReady(w.jobs[pj])) { discardOps(ops); continue; }
+                ops.clear();
+                if (assigned) pit->second.push(pj);
+            }
+            for (int jb : under) {
+                auto& tq = ptasks[jb];
+                for (;;) {
+                    if (tq.second >= tq.first.size()) break;
+                    const int pt = tq.first[tq.second++];
+                    vector<Op> o2;
+                    const int ptj = w.pods[pt].job;
+                    const bool assigned =
+                        preemptOne(o2, pt, [&](int t) { return nodeCopyRunning(t) && ptj == w.pods[t].job; });
+                    commitOps(o2);
+                    if (!assigned) break;
+                }
+            }
+        }
+    }
+    void reclaim() {  // reclaim.go:41-196
+        requireNoPodAffinity();
+        auto ql = [this](int a, int b) { return queueLess(a, b); };
+        auto jl = [this](int a, int b) { return jobLess(a, b); };
+        Heap<decltype(ql)> queues(ql);
+        vector<char> qseen(w.queues.size(), 0);
+        std::map<int, Heap<decltype(jl)>> preemptors;
+        std::map<int, std::pair<vector<int>, size_t>> ptasks;
+        for (int jb = 0; jb < (int)w.jobs.size(); ++jb) {
+            const int q = w.jobs[jb].queue;
+            if (!qseen[q]) { qseen[q] = 1; queues.push(q); }
+            vector<int> pend = pendingSorted(w.jobs[jb]);
+            if (pend.empty()) continue;
+            auto it = preemptors.find(q);
+            if (it == preemptors.end()) it = preemptors.emplace(q, Heap<decltype(jl)>(jl)).first;
+            it->second.push(jb);
+            ptasks[jb] = {pend, 0};
+        }
+        while (!queues.empty()) {
+            const int qi = queues.pop();
+            if (overused(qi)) continue;
+            auto pit = preemptors.find(qi);
+            if (pit == preemptors.end() || pit->second.empty()) continue;
+            const int jb = pit->second.pop();
+            auto& tq = ptasks[jb];
+            if (tq.second >= tq.first.size()) continue;
+            const int pt = tq.first[tq.second++];
+            tried++;
+            TaskPlan tp;
+            tp.pod = pt;
+            buildPlan(w, tp);
+            const PodRec& pr = w.pods[pt];
+            const int jq = w.jobs[jb].queue;
+            bool assigned = false;
+            for (int ni = 0; ni < (int)w.nodes.size(); ++ni) {
+                if (!predOk(w, tp, ni)) continue;
+                vector<int> cands;
+                for (int t : nodeTasksSorted(ni)) {
+                    const PodRec& p = w.pods[t];
+                    if (nodeCopyRunning(t) && p.job >= 0 && w.jobs[p.job].queue != jq) cands.push_back(t);
+                }
+                vector<int> vic = victims(false, pt, cands);
+                if (vic.empty()) continue;
+                Res all{0, 0, 0}, resreq = pr.initReq, got{0, 0, 0};
+                for (int v : vic) all += w.pods[v].req;
+                if (lessStrict(all, resreq)) continue;
+                for (int v : vic) {
+                    const Res vr = w.pods[v].req;
+                    w.log.emplace_back(v, ni, Releasing);
+                    evictInSession(v);
+                    got += vr;
+                    if (leTol(resreq, vr)) break;
+                    resreq -= vr;
+                }
+                if (leTol(pr.initReq, got)) {
+                    pipelineTask(pt, ni);
+                    w.log.emplace_back(pt, ni, Pipelined);
+                    assigned = true;
+                    break;
+                }
+            }
+            if (assigned) queues.push(qi);
+        }
+    }
     // scheduler.go:93-97 / util.go:51-58: comma-separated, trimmed action names
     void runActions(const char* actions, int maxPops) {
         string all = actions ? actions : "allocate", cur;
@@ -1319,6 +1648,8 @@ struct Engine {
             cur.clear();
             if (name == "allocate") allocate(maxPops);
             else if (name == "backfill") backfill();
+            else if (name == "reclaim") reclaim();
+            else if (name == "preempt") preempt();
             else throw std::runtime_error("action '" + name + "' is not implemented by this oracle");
         }
     }

@@ -112,6 +112,19 @@ def test_c5_scaled_parity(engine, oracle_mod, kbgen_mod, tmp_path, seed):
     assert any(k == 128 for _, _, k in got)
 
 
+def test_c5_full_size_parity(engine, oracle_mod, kbgen_mod, tmp_path):
+    """C5 at full size (50k nodes x 1.45M running pods, 2k pending) against the hoisted
+    restatement (oracle/kbfast.cpp), record for record (~728k records)."""
+    p = str(tmp_path / "c5.kbs")
+    kbgen_mod.gen_c5(p)
+    exp = oracle_mod.fast_allocate(p, threads=16, actions=C5_ACTIONS)
+    with engine.Session(p) as s:
+        pod, node, kind = s.run_actions(C5_ACTIONS)
+    assert np.array_equal(pod, exp.pod) and np.array_equal(node, exp.node)
+    assert np.array_equal(np.array([0, 4, 8, 128])[kind], exp.status)
+    assert (kind == 3).sum() > 100_000
+
+
 def test_c5_full_size_invariants(engine, kbgen_mod, tmp_path):
     """50k nodes x 1.45M running pods, 2k pending: properties that hold at any size —
     evicted pods were Running on the recorded node and are evicted once; pipelined /

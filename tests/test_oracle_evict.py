@@ -78,3 +78,36 @@ def test_preempt_random_smoke(oracle_mod, kbgen_mod, tmp_path):
         p = c.write(str(tmp_path / f"s{seed}.kbs"))
         kinds |= {k for _, _, k in oracle_mod.ref_allocate(p, actions="reclaim, allocate, backfill, preempt").as_list()}
     assert kinds == {EVICT, PIPE, ALLOC}
+
+
+TIERS = [
+    None,
+    [["priority", "gang", "drf", "predicates", "proportion", "nodeorder"]],
+    [["drf", "predicates", "nodeorder"], ["gang", "proportion"]],
+    [["priority", "conformance"], ["drf", "proportion", "predicates", "nodeorder"]],
+]
+ACTIONS = ["reclaim", "preempt", "reclaim, allocate, backfill, preempt", "allocate, preempt"]
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_evict_faithful_vs_hoisted(oracle_mod, kbgen_mod, tmp_path, seed):
+    """The two independent restatements (kbref: per-pair recomputation; kbfast:
+    hoisted, threaded) agree on every reclaim / preempt record."""
+    c = kbgen_mod.gen_preempt(700 + seed, n_nodes=4 + seed % 10, n_queues=1 + seed % 4, n_run_jobs=4 + seed % 9,
+                              n_pend_jobs=2 + seed % 5, max_tasks=1 + seed % 6, tiers=TIERS[seed % len(TIERS)],
+                              features=("selector", "taints", "ports", "init", "bestEffort", "unsched")
+                              if seed % 2 else ())
+    p = c.write(str(tmp_path / "s.kbs"))
+    acts = ACTIONS[seed % len(ACTIONS)]
+    a = oracle_mod.ref_allocate(p, actions=acts).as_list()
+    b = oracle_mod.fast_allocate(p, threads=3, actions=acts).as_list()
+    assert a == b
+
+
+def test_evict_c5_scaled_faithful_vs_hoisted(oracle_mod, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c5.kbs")
+    kbgen_mod.gen_c5(p, n_nodes=60, n_pending=60, best_effort=6)
+    acts = "reclaim, allocate, backfill, preempt"
+    a = oracle_mod.ref_allocate(p, actions=acts).as_list()
+    b = oracle_mod.fast_allocate(p, threads=4, actions=acts).as_list()
+    assert a == b and any(k == EVICT for _, _, k in a)
