@@ -135,6 +135,18 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
  * node copies Releasing).  Returns the record count.  KBHIP_EUNSUPPORTED on
  * node-sharded sessions and sessions with pod (anti-)affinity terms.
  * Replaces the reference's reclaimAction.Execute / preemptAction.Execute. */
+/* Carry the session over to the next scheduling session (SURVEY §8(f) row 3,
+ * the delta path of cache.go:515-583's per-session Snapshot): the state the
+ * scheduler cache holds once this session's binds and evictions reached it —
+ * dispatched tasks Bound on their nodes, Allocated-not-dispatched and
+ * Pipelined tasks Pending again, evicted pods Releasing — with node rows
+ * recomputed on the host and only the changed row runs uploaded (no snapshot
+ * parse, no re-encode).  The session can then run its actions again.
+ * *out_uploaded_bytes (optional) = bytes sent to the device.
+ * KBHIP_EUNSUPPORTED on shards and with pod (anti-)affinity terms; pod
+ * arrivals / deletions need kbhip_session_open. */
+int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
+
 int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 

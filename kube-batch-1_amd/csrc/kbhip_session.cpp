@@ -115,6 +115,7 @@ struct HPod {
     bool critical = false;  // kube-system namespace or a system-*-critical priority class (conformance.go:40-45)
     bool node_rel = false;  // the node's copy stays Releasing after an unevict (statement.go:81-105)
     R3 req, ireq;
+    int64_t nzc = 0, nzm = 0;  // GetNonzeroRequests (kbhip_session_carry recomputes node rows from them)
     int job = -1;   // session job slot
     int cls = -1;   // device task class (pending tasks)
     int node = -1;  // current node
@@ -311,6 +312,9 @@ struct Session {
     bool drf_on = false, prop_on = false, gang_ready = false;
     F3 total;
     vector<R3> used;  // NodeInfo.Used mirror (for kbhip_read_nodes)
+    vector<R3> h_alloc;                       // Allocatable (cpu, mem, gpu) per node (kbhip_session_carry)
+    vector<int32_t> pod_port_off, pod_port_ids;  // host-port ids per pod, CSR (kbhip_session_carry)
+    int64_t carry_bytes = 0;                     // bytes the last kbhip_session_carry uploaded
     int any_bf = 0;
     bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
@@ -731,6 +735,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         }
     }
     for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
+    for (int i = 0; i < P; ++i) { S.pods[i].nzc = pod_nzc[i]; S.pods[i].nzm = pod_nzm[i]; }
+    S.h_alloc.resize(N);
+    for (int i = 0; i < N; ++i) S.h_alloc[i] = R3{acpu[i], amem[i], agpu[i]};
+    S.pod_port_off.assign(P + 1, 0);
+    S.pod_port_ids.clear();
+    for (int i = 0; i < P; ++i) {
+        S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
+        for (int id : pod_ports[i]) S.pod_port_ids.push_back(id);
+    }
+    S.pod_port_off[P] = (int32_t)S.pod_port_ids.size();
 
     mark("pods");
     // ---------------- queues & jobs ----------------
@@ -2758,6 +2772,110 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
         return (int)n;
     })
 }
+// kbhip_session_carry: the next scheduling session's
+// start state from this one's end state, without a new snapshot — what the
+// scheduler cache holds after the session's binds and evictions reached it
+// (cache.go:515-583 snapshots it again):
+//   dispatched (Binding) tasks  -> Bound on their node (the bind succeeded);
+//   Allocated but not dispatched, Pipelined -> Pending, no node (session-only);
+//   evicted (Releasing)         -> Releasing on their node (deleting pods);
+//   an unevicted victim         -> Running (the node copy's Releasing is session-only);
+// node rows (Idle, Releasing, Backfilled, pod count, nonzero requests, host
+// ports) are recomputed from those pods — dropping the session-only
+// GetAccessibleResource inflation of Idle — and only rows that changed are
+// uploaded (contiguous runs); jobs, queues and plugin state are re-derived as
+// at open.  New or deleted pods need a snapshot (kbhip_session_open).
+static void session_carry(Session& S) {
+    if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "carry on a node-sharded session");
+    if (S.n_spaces > 0) throw Error(KBHIP_EUNSUPPORTED, "carry with pod (anti-)affinity terms");
+    ov_quiesce(S);
+    HIPCHK(hipStreamSynchronize(S.stream));
+    const int N = S.nc.n, P = (int)S.pods.size();
+    for (auto& p : S.pods) {
+        if (p.status == Binding) p.status = Bound;
+        else if (p.status == Allocated || p.status == AOB || p.status == Pipelined) { p.status = Pending; p.node = -1; }
+        else if (p.status == Pending) p.node = -1;  // an unpipelined task keeps its NodeName in the session only
+        p.node_rel = false;
+    }
+    vector<int64_t> col[9];
+    for (auto& c : col) c.assign(N, 0);
+    vector<int32_t> podcnt(N, 0);
+    vector<int64_t> nzc(N, 0), nzm(N, 0);
+    vector<uint64_t> pcol((size_t)std::max(S.nc.port_words, 1) * S.nc.npad, 0);
+    for (int n = 0; n < N; ++n) { col[0][n] = S.h_alloc[n].c; col[1][n] = S.h_alloc[n].m; col[2][n] = S.h_alloc[n].g; }
+    S.used.assign(N, R3{});
+    S.any_bf = 0;
+    for (int i = 0; i < P; ++i) {  // cache addTask -> NodeInfo.AddTask, as at open
+        const HPod& p = S.pods[i];
+        if (p.node < 0 || p.status == Succeeded || p.status == Failed) continue;
+        const int n = p.node;
+        if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
+        if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
+        col[0][n] -= p.req.c; col[1][n] -= p.req.m; col[2][n] -= p.req.g;
+        S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+        podcnt[n]++;
+        nzc[n] += p.nzc;
+        nzm[n] += p.nzm;
+        for (int k = S.pod_port_off[i]; k < S.pod_port_off[i + 1]; ++k) {
+            const int id = S.pod_port_ids[k];
+            pcol[(size_t)(id / 64) * S.nc.npad + n] |= 1ULL << (id % 64);
+        }
+    }
+    for (int n = 0; n < N; ++n) if (col[6][n] || col[7][n] || col[8][n]) S.any_bf = 1;
+    // delta upload: read the device rows back, send only the runs that differ
+    int64_t* dcol[9] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem, S.nc.rel_gpu,
+                        S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu};
+    int64_t uploaded = 0;
+    auto sync_col = [&](void* dptr, const void* want, size_t elem) {
+        vector<uint8_t> have((size_t)N * elem);
+        HIPCHK(hipMemcpy(have.data(), dptr, have.size(), hipMemcpyDeviceToHost));
+        const uint8_t* w = (const uint8_t*)want;
+        int n = 0;
+        while (n < N) {
+            if (std::memcmp(have.data() + (size_t)n * elem, w + (size_t)n * elem, elem) == 0) { ++n; continue; }
+            int e = n + 1;
+            while (e < N && std::memcmp(have.data() + (size_t)e * elem, w + (size_t)e * elem, elem) != 0) ++e;
+            HIPCHK(hipMemcpyAsync((uint8_t*)dptr + (size_t)n * elem, w + (size_t)n * elem, (size_t)(e - n) * elem,
+                                  hipMemcpyHostToDevice, S.stream));
+            uploaded += (int64_t)(e - n) * (int64_t)elem;
+            n = e;
+        }
+    };
+    for (int k = 0; k < 9; ++k) sync_col(dcol[k], col[k].data(), sizeof(int64_t));
+    sync_col(S.nc.pods, podcnt.data(), sizeof(int32_t));
+    sync_col(S.nc.nzc, nzc.data(), sizeof(int64_t));
+    sync_col(S.nc.nzm, nzm.data(), sizeof(int64_t));
+    for (int w = 0; w < S.nc.port_words; ++w)
+        sync_col(S.nc.ports + (size_t)w * S.nc.npad, pcol.data() + (size_t)w * S.nc.npad, sizeof(uint64_t));
+    HIPCHK(hipStreamSynchronize(S.stream));  // the host sources above are about to go away
+    S.carry_bytes = uploaded;
+    // jobs, queues, plugins: as at open
+    for (auto& j : S.jobs) {
+        j.cnt_alloc = j.cnt_aob = 0;
+        j.pending.clear();
+        j.cursor = 0;
+        j.pending_built = false;
+        for (int q = 0; q < 4; ++q) j.fit[q] = 0;
+        j.fit_exact = true;
+        j.drf_alloc = F3{};
+        j.drf_share = 0;
+        for (int t : j.tasks) {
+            j.priority = S.pods[t].priority;
+            if (allocated_status(S.pods[t].status)) j.cnt_alloc++;
+        }
+    }
+    for (auto& q : S.queues) {
+        q.has_attr = false;
+        q.deserved = q.allocated = q.request = F3{};
+        q.share = 0;
+    }
+    S.plugins_opened = false;
+    S.fallback = -1;
+    S.node_tasks.clear();
+    S.log.clear();
+    S.last_fit_ok = false;
+}
+
 static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
                         int64_t cap) {
     ABI_GUARD({
@@ -2777,6 +2895,16 @@ static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* 
             out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
         }
         return (int)n;
+    })
+}
+int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        session_carry(s->s);
+        if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
+        return 0;
     })
 }
 int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
@@ -2976,6 +3104,9 @@ int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t ca
             return bytes;
         } else if (n == "dbg_pods") {
             v = S.dbg_pods;
+        } else if (n == "pod_status" || n == "pod_node") {  // the host model: TaskStatus code / node per pod
+            v.resize(S.pods.size());
+            for (size_t i = 0; i < S.pods.size(); ++i) v[i] = n == "pod_status" ? S.pods[i].status : S.pods[i].node;
         } else if (n == "dims") {  // n_nodes, npad, n_spaces, n_classes
             v = {S.nc.n, S.nc.npad, S.n_spaces, (int32_t)S.classes.size()};
         } else {

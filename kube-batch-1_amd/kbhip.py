@@ -26,7 +26,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
-           "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt")
+           "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -74,6 +74,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_session_carry.argtypes = [vp, vp]
         L.kbhip_preempt.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_open_shard.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
         L.kbhip_shard_info.argtypes = [vp, vp]
@@ -161,6 +162,12 @@ class Session:
     def backfill(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Run backfillAction.Execute on the current session state."""
         return self._action(lib().kbhip_backfill, cap)
+
+    def carry(self) -> int:
+        """kbhip_session_carry: become the next session (binds / evictions applied); bytes uploaded."""
+        out = np.zeros(1, np.int64)
+        _check(lib().kbhip_session_carry(self._h, _p(out)))
+        return int(out[0])
 
     def reclaim(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Run reclaimAction.Execute: (pod, node, EVICTED | PIPELINED) records in decision order."""

@@ -1,0 +1,74 @@
+"""kbhip_session_carry (the delta path between
+sessions): a session carried over after its actions must schedule exactly
+like a fresh session opened from the snapshot the scheduler cache would hold
+then — dispatched tasks bound to their nodes, undispatched / pipelined tasks
+pending again, evicted pods deleting (Releasing).  The fresh snapshot is
+written from the engine's end state; its records and node state come from the
+faithful oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+STATUS = {1: 4, 2: 8, 3: 128}
+BINDING, RELEASING, ALLOC, AOB, PIPE, RUNNING = 16, 128, 4, 2, 8, 64
+NO_POD_AFFINITY = ("labels", "taints", "ports", "init", "running", "releasing", "backfill", "selector",
+                   "nodeaffinity", "unsched", "bestEffort")
+ACTS = ["allocate", "allocate, backfill", "reclaim, allocate, backfill, preempt"]
+
+
+def _next_snapshot(c, status, node):
+    """The cluster the cache holds after the session: binds and evictions applied."""
+    pods = sorted(c.pods, key=lambda q: q.uid)
+    names = sorted(n.name for n in c.nodes)
+    for i, q in enumerate(pods):
+        st = int(status[i])
+        if st == BINDING:
+            q.node, q.phase = names[int(node[i])], "Pending"  # bound: Pending with a node -> Bound
+        elif st in (ALLOC, AOB, PIPE) or (st == 1 and q.node is None):
+            q.node, q.phase = None, "Pending"
+        elif st == RELEASING and not q.deleting and q.phase == "Running":
+            q.deleting = True  # cache.Evict: the pod is being deleted
+    return c
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_carry_equals_fresh_session(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    if seed % 2:
+        c = kbgen_mod.gen_preempt(300 + seed, n_nodes=4 + seed % 8, n_queues=1 + seed % 3, n_run_jobs=4 + seed % 7,
+                                  n_pend_jobs=3 + seed % 5, max_tasks=2 + seed % 5,
+                                  features=("selector", "taints", "ports", "init", "bestEffort"))
+    else:
+        c = kbgen_mod.gen_random(400 + seed, n_nodes=4 + seed % 10, n_jobs=5 + seed % 8, max_tasks=2 + seed % 6,
+                                 features=NO_POD_AFFINITY)
+    acts = ACTS[seed % len(ACTS)]
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    n_nodes = len(c.nodes)
+    with engine.Session(p1) as s:
+        s.run_actions(acts)
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+        s.carry()
+        pod, nd, kind = s.run_actions(acts)
+        ns = s.read_nodes(n_nodes)
+    p2 = _next_snapshot(c, status, node).write(str(tmp_path / "s2.kbs"))
+    exp, ons = oracle_mod.ref_allocate(p2, actions=acts, with_nodes=True)
+    assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)] == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:n_nodes])
+
+
+def test_carry_c4_scaled_uploads_a_delta(engine, kbgen_mod, tmp_path):
+    """C4-shaped, 20k nodes: the carry sends only the node rows the binds changed, and
+    the carried session schedules only tasks that are still pending."""
+    p1 = str(tmp_path / "c4.kbs")
+    kbgen_mod.gen_c4(p1, n_nodes=20_000, n_pending=60_000)
+    with engine.Session(p1) as s:
+        s.allocate()
+        st1 = s.table("pod_status").copy()
+        sent = s.carry()
+        st2 = s.table("pod_status").copy()
+        pod, nd, kind = s.allocate()
+    assert ((st1 == BINDING) == (st2 == 32)).all()           # dispatched -> Bound
+    assert (st2[np.isin(st1, (ALLOC, PIPE))] == 1).all()     # undispatched / pipelined -> Pending
+    assert len(pod) > 0 and (st2[pod] == 1).all()            # only pending tasks are placed again
+    full = 20_000 * (12 * 8 + 4)                              # the dynamic node columns
+    assert 0 < sent < full
