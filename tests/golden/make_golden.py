@@ -117,6 +117,26 @@ def regression(oracle):
     return out
 
 
+EVICT_ACTIONS = "reclaim, allocate, backfill, preempt"
+
+
+def evict_regression(oracle):
+    """Regression vectors of the reclaim / preempt actions (the shipped action list):
+    preemption-shaped snapshots (kbgen.gen_preempt) and the records the faithful
+    oracle produced (pod, node, status: 128 evicted, 8 pipelined, 4 allocated)."""
+    out = {}
+    for seed in range(8):
+        c = kbgen.gen_preempt(9000 + seed, n_nodes=5 + seed % 4, n_queues=2 + seed % 3, n_run_jobs=6 + seed % 5,
+                              n_pend_jobs=3 + seed % 3, max_tasks=4,
+                              features=("selector", "taints", "ports", "init", "bestEffort") if seed % 2 else ())
+        name = f"evict_{seed:02d}"
+        path = os.path.join(HERE, f"{name}.kbs")
+        c.write(path)
+        pl = oracle.ref_allocate(path, actions=EVICT_ACTIONS)
+        out[name] = {"records": pl.as_list(), "actions": EVICT_ACTIONS, "n_nodes": len(c.nodes)}
+    return out
+
+
 if __name__ == "__main__":
     import oracle
     oracle.build()
@@ -126,6 +146,7 @@ if __name__ == "__main__":
     golden.update(ka_pod_info())
     golden.update(ka_gang())
     golden.update(regression(oracle))
+    golden.update(evict_regression(oracle))
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(golden, f, indent=1, sort_keys=True)
     print("wrote", len(golden), "fixtures")

@@ -100,3 +100,19 @@ def test_regression_vectors_oracle(oracle_mod, golden, case):
     exp = [tuple(x) for x in golden[case]["placements"]]
     assert oracle_mod.ref_allocate(path).as_list() == exp
     assert oracle_mod.fast_allocate(path, threads=2).as_list() == exp
+
+
+def _evict_cases():
+    with open(os.path.join(GOLD, "golden.json")) as f:
+        g = json.load(f)
+    return sorted(k for k in g if k.startswith("evict_"))
+
+
+@pytest.mark.parametrize("case", _evict_cases())
+def test_evict_regression_vectors_oracle(oracle_mod, golden, case):
+    """reclaim / preempt regression vectors: both restatements reproduce the committed records."""
+    path = os.path.join(GOLD, case + ".kbs")
+    exp = [tuple(x) for x in golden[case]["records"]]
+    acts = golden[case]["actions"]
+    assert oracle_mod.ref_allocate(path, actions=acts).as_list() == exp
+    assert oracle_mod.fast_allocate(path, threads=2, actions=acts).as_list() == exp

@@ -4,6 +4,8 @@ preemptors, in decision order — and the device node state afterwards equal
 the faithful restatement's (oracle/kbref.cpp reclaimExecute / preemptExecute)
 on the same snapshot.  Records are compared as (pod, node, status) with the
 oracle's TaskStatus codes: 4 Allocated, 8 Pipelined, 128 Releasing (evicted)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -148,3 +150,19 @@ def test_c5_full_size_invariants(engine, kbgen_mod, tmp_path):
     # the recorded node of an eviction is the victim's node (running pods are laid out node by node)
     run_node = np.repeat(np.arange(meta["nodes"]), meta["rpn"])
     assert (run_node[pod[ev]] == node[ev]).all()
+
+
+def _evict_golden():
+    import json
+    import os
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with open(os.path.join(gold, "golden.json")) as f:
+        g = json.load(f)
+    return [(os.path.join(gold, k + ".kbs"), g[k]) for k in sorted(g) if k.startswith("evict_")]
+
+
+@pytest.mark.parametrize("case", _evict_golden(), ids=lambda c: os.path.basename(c[0]) if isinstance(c, tuple) else "")
+def test_evict_golden_vectors_gpu(engine, case):
+    path, g = case
+    got, _ = _engine(engine, path, g["actions"])
+    assert got == [tuple(x) for x in g["records"]]
