@@ -502,6 +502,22 @@ struct Encoder {
 
 static void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
 
+// Host-port ids of pod i: run i of the session's port CSR, compared by value.
+struct PortRun {
+    const int32_t *b, *e;
+    const int32_t* begin() const { return b; }
+    const int32_t* end() const { return e; }
+    bool empty() const { return b == e; }
+    bool operator!=(const PortRun& o) const {
+        return (e - b) != (o.e - o.b) || !std::equal(b, e, o.b);
+    }
+};
+struct PortRuns {
+    const int32_t* off;
+    const vector<int32_t>& ids;
+    PortRun operator[](int i) const { return {ids.data() + off[i], ids.data() + off[i + 1]}; }
+};
+
 static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
                          int world = 1) {
     if (world < 1 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world");
@@ -657,16 +673,24 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             for (int r = 0; r < P; ++r) S.pods[ord[r]].uid_rank = r;
         }
     }
-    vector<vector<int>> pod_ports(P);
-    vector<int64_t> pod_nzc(P, 0), pod_nzm(P, 0);
-    std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
+    // host ports per pod: CSR built in pod order (S.pod_port_off / S.pod_port_ids)
+    S.pod_port_off.assign(P + 1, 0);
+    S.pod_port_ids.clear();
+    const PortRuns pod_ports{S.pod_port_off.data(), S.pod_port_ids};
+    // strtab offset -> (namespace id, namespace is kube-system)
+    std::unordered_map<int32_t, std::pair<int, bool>> ns_by_off;
     for (int i = 0; i < P; ++i) {
         HPod& p = S.pods[i];
+        bool sys_ns;
         {
             auto it = ns_by_off.find(pns[i]);
-            if (it == ns_by_off.end()) it = ns_by_off.emplace(pns[i], E.nss.get(s.s(pns[i]))).first;
-            p.ns = it->second;
+            if (it == ns_by_off.end())
+                it = ns_by_off.emplace(pns[i], std::make_pair(E.nss.get(s.s(pns[i])),
+                                                              std::strcmp(s.str(pns[i]), "kube-system") == 0)).first;
+            p.ns = it->second.first;
+            sys_ns = it->second.second;
         }
+        S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
         const bool has_node = pnode[i] >= 0 && s.str(pnode[i])[0] != '\0';
         int ph = pphase[i];
         bool del = !pdel.empty() && pdel[i];
@@ -679,14 +703,14 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         p.ts = pts[i];
         {
             const char* pc = (!ppc.empty() && ppc[i] >= 0) ? s.str(ppc[i]) : "";
-            p.critical = std::strcmp(s.str(pns[i]), "kube-system") == 0 ||
+            p.critical = sys_ns ||
                          std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
         }
         p.backfill = !pbf.empty() && pbf[i];
         for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
             p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
-            pod_nzc[i] += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
-            pod_nzm[i] += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
+            p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
+            p.nzm += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
             for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
                 if (ptpo[q] <= 0) continue;  // HostPortInfo.Add ignores port <= 0
                 string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
@@ -697,7 +721,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 int id;
                 if (it == E.port_ids.end()) { id = (int)E.port_defs.size(); E.port_ids[key] = id; E.port_defs.push_back(key); }
                 else id = it->second;
-                pod_ports[i].push_back(id);
+                S.pod_port_ids.push_back(id);
             }
         }
         p.ireq = p.req;
@@ -729,22 +753,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             }
             S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
             podcnt[n]++;
-            nzc[n] += pod_nzc[i];
-            nzm[n] += pod_nzm[i];
-            for (int id : pod_ports[i]) node_ports[n].push_back(id);
+            nzc[n] += p.nzc;
+            nzm[n] += p.nzm;
+            for (size_t k = (size_t)S.pod_port_off[i]; k < S.pod_port_ids.size(); ++k)  // pod i's run (still open)
+                node_ports[n].push_back(S.pod_port_ids[k]);
         }
     }
+    S.pod_port_off[P] = (int32_t)S.pod_port_ids.size();
     for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
-    for (int i = 0; i < P; ++i) { S.pods[i].nzc = pod_nzc[i]; S.pods[i].nzm = pod_nzm[i]; }
     S.h_alloc.resize(N);
     for (int i = 0; i < N; ++i) S.h_alloc[i] = R3{acpu[i], amem[i], agpu[i]};
-    S.pod_port_off.assign(P + 1, 0);
-    S.pod_port_ids.clear();
-    for (int i = 0; i < P; ++i) {
-        S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
-        for (int id : pod_ports[i]) S.pod_port_ids.push_back(id);
-    }
-    S.pod_port_off[P] = (int32_t)S.pod_port_ids.size();
 
     mark("pods");
     // ---------------- queues & jobs ----------------
@@ -974,7 +992,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (A.ns != B.ns || A.backfill != B.backfill) return false;
         if (A.req.c != B.req.c || A.req.m != B.req.m || A.req.g != B.req.g) return false;
         if (A.ireq.c != B.ireq.c || A.ireq.m != B.ireq.m || A.ireq.g != B.ireq.g) return false;
-        if (pod_nzc[a] != pod_nzc[b] || pod_nzm[a] != pod_nzm[b] || pod_ports[a] != pod_ports[b]) return false;
+        if (A.nzc != B.nzc || A.nzm != B.nzm || pod_ports[a] != pod_ports[b]) return false;
         if ((paff.empty() ? -1 : paff[a]) != (paff.empty() ? -1 : paff[b])) return false;
         if (!same_run(pso, a, b, {&psk, &psv})) return false;
         if (!same_run(pto, a, b, {&tlk, &tlo, &tlv, &tle})) return false;
@@ -994,7 +1012,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         TaskClass c{};
         c.ireq_cpu = p.ireq.c; c.ireq_mem = p.ireq.m; c.ireq_gpu = p.ireq.g;
         c.req_cpu = p.req.c; c.req_mem = p.req.m; c.req_gpu = p.req.g;
-        c.nz_cpu = pod_nzc[i]; c.nz_mem = pod_nzm[i];
+        c.nz_cpu = S.pods[i].nzc; c.nz_mem = S.pods[i].nzm;
         c.backfill = p.backfill;
         c.nsel_term = -1;
         c.req_term_n = -1;
