@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -28,6 +29,7 @@
 #include <stdexcept>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -661,8 +663,22 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     spare_pods().take(S.pods);
     S.pods.resize(P);
     {  // UID ranks: the canonical order (kbsnap.h) makes them the index; sort otherwise
-        bool sorted = true;
-        for (int i = 1; i < P && sorted; ++i) sorted = std::strcmp(s.str(puid[i - 1]), s.str(puid[i])) < 0;
+        // strictly ascending? (checked in kThreads chunks: 1M string compares at C4)
+        constexpr int kThreads = 8;
+        const int per = (P + kThreads - 1) / kThreads;
+        std::atomic<bool> sorted{true};
+        auto check = [&](int lo, int hi) {
+            for (int i = std::max(lo, 1); i < hi; ++i)
+                if (std::strcmp(s.str(puid[i - 1]), s.str(puid[i])) >= 0) { sorted = false; return; }
+        };
+        if (P < (1 << 16)) {
+            check(0, P);
+        } else {
+            vector<std::thread> th;
+            for (int t = 1; t < kThreads; ++t) th.emplace_back(check, t * per, std::min(P, (t + 1) * per));
+            check(0, std::min(P, per));
+            for (auto& x : th) x.join();
+        }
         if (sorted) {
             for (int i = 0; i < P; ++i) S.pods[i].uid_rank = i;
         } else {
@@ -839,23 +855,24 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
     }
-    {
-        vector<int32_t> ntask(S.jobs.size(), 0);
+    {  // one pass in pod order; a job's tasks are its pods in pod order
+        vector<int32_t> ntask(S.jobs.size(), 0), slot_of(P);
         for (int i = 0; i < P; ++i) {
-            int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
-            S.pods[i].job = slot;
-            if (slot >= 0) ntask[slot]++;
+            const int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
+            HPod& p = S.pods[i];
+            p.job = slot;
+            slot_of[i] = slot;
+            if (slot < 0) continue;
+            ntask[slot]++;
+            HJob& j = S.jobs[slot];
+            j.priority = p.priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
+            if (allocated_status(p.status)) j.cnt_alloc++;
+            if (p.status == AOB) j.cnt_aob++;
         }
         for (size_t j = 0; j < S.jobs.size(); ++j) S.jobs[j].tasks.reserve(ntask[j]);
         for (int i = 0; i < P; ++i)
-            if (S.pods[i].job >= 0) S.jobs[S.pods[i].job].tasks.push_back(i);
+            if (slot_of[i] >= 0) S.jobs[slot_of[i]].tasks.push_back(i);
     }
-    for (auto& j : S.jobs)
-        for (int t : j.tasks) {
-            j.priority = S.pods[t].priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
-            if (allocated_status(S.pods[t].status)) j.cnt_alloc++;
-            if (S.pods[t].status == AOB) j.cnt_aob++;
-        }
 
     mark("jobs");
     // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
