@@ -589,8 +589,29 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     auto lk = V32("nl_key"), lv = V32("nl_val");
     auto toff = s.offs("n_taint_off", N);
     auto tk = V32("nt_key"), tv = V32("nt_val"), te = V32("nt_effect");
-    std::unordered_map<std::string_view, int> node_idx;  // views into the snapshot's string table
-    node_idx.reserve((size_t)N * 2);
+    // Name -> node: binary search when the names are strictly ascending (the
+    // canonical snapshot order, kbsnap.h), else a map of views into the string table.
+    bool names_sorted = true;
+    for (int i = 1; i < N && names_sorted; ++i) names_sorted = std::strcmp(s.str(nname[i - 1]), s.str(nname[i])) < 0;
+    std::unordered_map<std::string_view, int> node_idx;
+    if (!names_sorted) {
+        node_idx.reserve((size_t)N * 2);
+        for (int i = 0; i < N; ++i) node_idx.emplace(std::string_view(s.str(nname[i])), i);
+        if ((int)node_idx.size() != N) throw Error(KBHIP_EINVAL, "duplicate node names");
+    }
+    auto find_node = [&](std::string_view v) -> int {
+        if (!names_sorted) {
+            auto it = node_idx.find(v);
+            return it == node_idx.end() ? -1 : it->second;
+        }
+        int lo = 0, hi = N;
+        while (lo < hi) {
+            const int m = (lo + hi) / 2;
+            if (std::string_view(s.str(nname[m])) < v) lo = m + 1;
+            else hi = m;
+        }
+        return lo < N && std::string_view(s.str(nname[lo])) == v ? lo : -1;
+    };
     E.nl_off.assign(N + 1, 0);
     E.nl_kv.clear();
     E.nl_kv.reserve(lk.size());
@@ -600,7 +621,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     std::unordered_map<int32_t, int> node_by_off;  // strtab offset of the name -> node (fast path)
     node_by_off.reserve((size_t)N * 2);
     for (int i = 0; i < N; ++i) {
-        node_idx.emplace(std::string_view(s.str(nname[i])), i);
         node_by_off.emplace(nname[i], i);
         for (int k = loff[i]; k < loff[i + 1]; ++k) {
             auto ki = key_by_off.find(lk[k]);
@@ -621,7 +641,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             node_taints[i].push_back(id);
         }
     }
-    if ((int)node_idx.size() != N) throw Error(KBHIP_EINVAL, "duplicate node names");
     // host-side node state (NewNodeInfo + AddTask replay, node_info.go:62-145)
     vector<R3> idle(N), rel(N), bf(N);
     vector<int64_t> nzc(N, 0), nzm(N, 0);
@@ -751,11 +770,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             if (ot != node_by_off.end()) {
                 p.node = ot->second;
             } else {
-                auto it = node_idx.find(std::string_view(s.str(pnode[i])));
-                if (it == node_idx.end())
+                const int n = find_node(std::string_view(s.str(pnode[i])));
+                if (n < 0)
                     throw Error(KBHIP_EINVAL, "pod " + s.s(puid[i]) + " is bound to node " + s.s(pnode[i]) +
                                                   " which is not in the snapshot");
-                p.node = it->second;
+                p.node = n;
             }
         }
         if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
@@ -965,9 +984,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 int op = nsr_op[k];
                 if ((op != OP_IN && op != OP_NOTIN) || vs.size() != 1) { bad = true; continue; }
                 if (s.s(nsr_key[k]) == "metadata.name") {
-                    auto it = node_idx.find(vs[0]);
-                    rs.push_back(Req{0, op == OP_IN ? OP_NAME_IN : OP_NAME_NOTIN, 0,
-                                     it == node_idx.end() ? -1 : it->second, 0});
+                    rs.push_back(Req{0, op == OP_IN ? OP_NAME_IN : OP_NAME_NOTIN, 0, find_node(vs[0]), 0});
                 } else if ((op == OP_IN) != vs[0].empty()) {  // any other field reads ""
                     rs.push_back(Req{0, OP_FALSE, 0, 0, 0});
                 }
