@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <exception>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -708,44 +709,86 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             for (int r = 0; r < P; ++r) S.pods[ord[r]].uid_rank = r;
         }
     }
+    mark("pods:init");
     // host ports per pod: CSR built in pod order (S.pod_port_off / S.pod_port_ids)
     S.pod_port_off.assign(P + 1, 0);
     S.pod_port_ids.clear();
     const PortRuns pod_ports{S.pod_port_off.data(), S.pod_port_ids};
-    // strtab offset -> (namespace id, namespace is kube-system)
-    std::unordered_map<int32_t, std::pair<int, bool>> ns_by_off;
+    // Pass A (parallel over pod ranges): the per-pod fields that need no
+    // dictionary -- status, priority, requests, nonzero requests, node.
+    auto pod_fields = [&](int lo, int hi) {
+        for (int i = lo; i < hi; ++i) {
+            HPod& p = S.pods[i];
+            const bool has_node = pnode[i] >= 0 && s.str(pnode[i])[0] != '\0';
+            int ph = pphase[i];
+            bool del = !pdel.empty() && pdel[i];
+            if (ph == KBS_RUNNING) p.status = del ? Releasing : Running;            // api/helpers.go:35-61
+            else if (ph == KBS_PENDING) p.status = del ? Releasing : (!has_node ? Pending : Bound);
+            else if (ph == KBS_SUCCEEDED) p.status = Succeeded;
+            else if (ph == KBS_FAILED) p.status = Failed;
+            else p.status = Unknown;
+            p.priority = ppri[i];
+            p.ts = pts[i];
+            {
+                const char* pc = (!ppc.empty() && ppc[i] >= 0) ? s.str(ppc[i]) : "";
+                p.critical = std::strcmp(s.str(pns[i]), "kube-system") == 0 ||
+                             std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
+            }
+            p.backfill = !pbf.empty() && pbf[i];
+            for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
+                p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
+                p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
+                p.nzm += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
+            }
+            p.ireq = p.req;
+            for (int k = pio[i]; k < pio[i + 1]; ++k) {
+                p.ireq.c = std::max(p.ireq.c, iccpu[k]);
+                p.ireq.m = std::max(p.ireq.m, icmem[k]);
+                p.ireq.g = std::max(p.ireq.g, icgpu[k]);
+            }
+            if (has_node) {
+                auto ot = node_by_off.find(pnode[i]);
+                if (ot != node_by_off.end()) {
+                    p.node = ot->second;
+                } else {
+                    const int n = find_node(std::string_view(s.str(pnode[i])));
+                    if (n < 0)
+                        throw Error(KBHIP_EINVAL, "pod " + s.s(puid[i]) + " is bound to node " + s.s(pnode[i]) +
+                                                      " which is not in the snapshot");
+                    p.node = n;
+                }
+            }
+        }
+    };
+    {
+        constexpr int kThreads = 8;
+        if (P < (1 << 16)) {
+            pod_fields(0, P);
+        } else {  // the first failing range's error is rethrown (its lowest pod)
+            const int per = (P + kThreads - 1) / kThreads;
+            vector<std::exception_ptr> err(kThreads);
+            auto run = [&](int t) {
+                try { pod_fields(t * per, std::min(P, (t + 1) * per)); } catch (...) { err[t] = std::current_exception(); }
+            };
+            vector<std::thread> th;
+            for (int t = 1; t < kThreads; ++t) th.emplace_back(run, t);
+            run(0);
+            for (auto& x : th) x.join();
+            for (auto& e : err) if (e) std::rethrow_exception(e);
+        }
+    }
+    mark("pods:A");
+    // Pass B (pod order): namespace and host-port dictionaries, node accumulation.
+    std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
     for (int i = 0; i < P; ++i) {
         HPod& p = S.pods[i];
-        bool sys_ns;
         {
             auto it = ns_by_off.find(pns[i]);
-            if (it == ns_by_off.end())
-                it = ns_by_off.emplace(pns[i], std::make_pair(E.nss.get(s.s(pns[i])),
-                                                              std::strcmp(s.str(pns[i]), "kube-system") == 0)).first;
-            p.ns = it->second.first;
-            sys_ns = it->second.second;
+            if (it == ns_by_off.end()) it = ns_by_off.emplace(pns[i], E.nss.get(s.s(pns[i]))).first;
+            p.ns = it->second;
         }
         S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
-        const bool has_node = pnode[i] >= 0 && s.str(pnode[i])[0] != '\0';
-        int ph = pphase[i];
-        bool del = !pdel.empty() && pdel[i];
-        if (ph == KBS_RUNNING) p.status = del ? Releasing : Running;            // api/helpers.go:35-61
-        else if (ph == KBS_PENDING) p.status = del ? Releasing : (!has_node ? Pending : Bound);
-        else if (ph == KBS_SUCCEEDED) p.status = Succeeded;
-        else if (ph == KBS_FAILED) p.status = Failed;
-        else p.status = Unknown;
-        p.priority = ppri[i];
-        p.ts = pts[i];
-        {
-            const char* pc = (!ppc.empty() && ppc[i] >= 0) ? s.str(ppc[i]) : "";
-            p.critical = sys_ns ||
-                         std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
-        }
-        p.backfill = !pbf.empty() && pbf[i];
-        for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
-            p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
-            p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
-            p.nzm += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
+        for (int k = pco[i]; k < pco[i + 1]; ++k) {
             for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
                 if (ptpo[q] <= 0) continue;  // HostPortInfo.Add ignores port <= 0
                 string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
@@ -757,24 +800,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 if (it == E.port_ids.end()) { id = (int)E.port_defs.size(); E.port_ids[key] = id; E.port_defs.push_back(key); }
                 else id = it->second;
                 S.pod_port_ids.push_back(id);
-            }
-        }
-        p.ireq = p.req;
-        for (int k = pio[i]; k < pio[i + 1]; ++k) {
-            p.ireq.c = std::max(p.ireq.c, iccpu[k]);
-            p.ireq.m = std::max(p.ireq.m, icmem[k]);
-            p.ireq.g = std::max(p.ireq.g, icgpu[k]);
-        }
-        if (has_node) {
-            auto ot = node_by_off.find(pnode[i]);
-            if (ot != node_by_off.end()) {
-                p.node = ot->second;
-            } else {
-                const int n = find_node(std::string_view(s.str(pnode[i])));
-                if (n < 0)
-                    throw Error(KBHIP_EINVAL, "pod " + s.s(puid[i]) + " is bound to node " + s.s(pnode[i]) +
-                                                  " which is not in the snapshot");
-                p.node = n;
             }
         }
         if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
@@ -799,7 +824,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.h_alloc.resize(N);
     for (int i = 0; i < N; ++i) S.h_alloc[i] = R3{acpu[i], amem[i], agpu[i]};
 
-    mark("pods");
+    mark("pods:B");
     // ---------------- queues & jobs ----------------
     auto qn = V32("q_name"), qw = V32("q_weight");
     auto qts = s.vec<int64_t>("q_ts");
