@@ -267,6 +267,11 @@ struct SpareVec {
         v.clear();
         out.clear();
     }
+    void take_keep(vector<T>& out) {  // the elements stay (the caller resets the ones it uses)
+        std::lock_guard<std::mutex> lk(mu);
+        out.swap(v);
+        v.clear();
+    }
     void give(vector<T>& in) {
         std::lock_guard<std::mutex> lk(mu);
         if (in.capacity() > v.capacity()) in.swap(v);
@@ -680,8 +685,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
          paapref_c = acnt("a_paapref_cnt");
     (void)pareq_c; (void)papref_c; (void)paareq_c; (void)paapref_c;
 
-    spare_pods().take(S.pods);
+    spare_pods().take_keep(S.pods);  // old pods are reset in pass A below (in parallel)
     S.pods.resize(P);
+    vector<int32_t> uid_rank_of;  // UID ranks when the pods are not in UID order
     {  // UID ranks: the canonical order (kbsnap.h) makes them the index; sort otherwise
         // strictly ascending? (checked in kThreads chunks: 1M string compares at C4)
         constexpr int kThreads = 8;
@@ -699,14 +705,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             check(0, std::min(P, per));
             for (auto& x : th) x.join();
         }
-        if (sorted) {
-            for (int i = 0; i < P; ++i) S.pods[i].uid_rank = i;
-        } else {
+        if (!sorted) {  // ranks assigned after pass A; sorted: rank = index, set there
             vector<int> ord(P);
             for (int i = 0; i < P; ++i) ord[i] = i;
             std::sort(ord.begin(), ord.end(),
                       [&](int a, int b) { return std::strcmp(s.str(puid[a]), s.str(puid[b])) < 0; });
-            for (int r = 0; r < P; ++r) S.pods[ord[r]].uid_rank = r;
+            uid_rank_of.resize(P);
+            for (int r = 0; r < P; ++r) uid_rank_of[ord[r]] = r;
         }
     }
     mark("pods:init");
@@ -719,6 +724,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     auto pod_fields = [&](int lo, int hi) {
         for (int i = lo; i < hi; ++i) {
             HPod& p = S.pods[i];
+            p = HPod{};
+            p.uid_rank = uid_rank_of.empty() ? i : uid_rank_of[i];
             const bool has_node = pnode[i] >= 0 && s.str(pnode[i])[0] != '\0';
             int ph = pphase[i];
             bool del = !pdel.empty() && pdel[i];
