@@ -785,53 +785,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         }
     }
     mark("pods:A");
-    // Pass B (pod order): namespace and host-port dictionaries, node accumulation.
-    std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
-    for (int i = 0; i < P; ++i) {
-        HPod& p = S.pods[i];
-        {
-            auto it = ns_by_off.find(pns[i]);
-            if (it == ns_by_off.end()) it = ns_by_off.emplace(pns[i], E.nss.get(s.s(pns[i]))).first;
-            p.ns = it->second;
-        }
-        S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
-        for (int k = pco[i]; k < pco[i + 1]; ++k) {
-            for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
-                if (ptpo[q] <= 0) continue;  // HostPortInfo.Add ignores port <= 0
-                string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
-                if (ip.empty()) ip = "0.0.0.0";
-                if (pr.empty()) pr = "TCP";
-                auto key = std::make_tuple(E.ip_dict.get(ip), E.proto_dict.get(pr), (int32_t)ptpo[q]);
-                auto it = E.port_ids.find(key);
-                int id;
-                if (it == E.port_ids.end()) { id = (int)E.port_defs.size(); E.port_ids[key] = id; E.port_defs.push_back(key); }
-                else id = it->second;
-                S.pod_port_ids.push_back(id);
-            }
-        }
-        if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
-            int n = p.node;
-            if (p.backfill) { bf[n].c += p.req.c; bf[n].m += p.req.m; bf[n].g += p.req.g; }
-            if (p.status == Releasing) {
-                rel[n].c += p.req.c; rel[n].m += p.req.m; rel[n].g += p.req.g;
-                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
-            } else {
-                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
-            }
-            S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
-            podcnt[n]++;
-            nzc[n] += p.nzc;
-            nzm[n] += p.nzm;
-            for (size_t k = (size_t)S.pod_port_off[i]; k < S.pod_port_ids.size(); ++k)  // pod i's run (still open)
-                node_ports[n].push_back(S.pod_port_ids[k]);
-        }
-    }
-    S.pod_port_off[P] = (int32_t)S.pod_port_ids.size();
-    for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
-    S.h_alloc.resize(N);
-    for (int i = 0; i < N; ++i) S.h_alloc[i] = R3{acpu[i], amem[i], agpu[i]};
-
-    mark("pods:B");
     // ---------------- queues & jobs ----------------
     auto qn = V32("q_name"), qw = V32("q_weight");
     auto qts = s.vec<int64_t>("q_ts");
@@ -906,20 +859,72 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
     }
-    {  // one pass in pod order; a job's tasks are its pods in pod order
-        vector<int32_t> ntask(S.jobs.size(), 0), slot_of(P);
-        for (int i = 0; i < P; ++i) {
+    mark("jobs:slots");
+    // Pass B (pod order): namespace and host-port dictionaries, node accumulation,
+    // job slots (a job's tasks are its pods in pod order).
+    vector<int32_t> ntask(S.jobs.size(), 0), slot_of(P);
+    std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
+    int32_t last_ns_off = -1, last_ns = -1;       // consecutive pods (one job) share a namespace
+    for (int i = 0; i < P; ++i) {
+        HPod& p = S.pods[i];
+        if (pns[i] != last_ns_off) {
+            auto it = ns_by_off.find(pns[i]);
+            if (it == ns_by_off.end()) it = ns_by_off.emplace(pns[i], E.nss.get(s.s(pns[i]))).first;
+            last_ns_off = pns[i];
+            last_ns = it->second;
+        }
+        p.ns = last_ns;
+        {
             const int slot = pjob[i] >= 0 ? row_slot[pjob[i]] : shadow_slot[i];
-            HPod& p = S.pods[i];
             p.job = slot;
             slot_of[i] = slot;
-            if (slot < 0) continue;
-            ntask[slot]++;
-            HJob& j = S.jobs[slot];
-            j.priority = p.priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
-            if (allocated_status(p.status)) j.cnt_alloc++;
-            if (p.status == AOB) j.cnt_aob++;
+            if (slot >= 0) {
+                ntask[slot]++;
+                HJob& j = S.jobs[slot];
+                j.priority = p.priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
+                if (allocated_status(p.status)) j.cnt_alloc++;
+                if (p.status == AOB) j.cnt_aob++;
+            }
         }
+        S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
+        for (int k = pco[i]; k < pco[i + 1]; ++k) {
+            for (int q = cpo[k]; q < cpo[k + 1]; ++q) {
+                if (ptpo[q] <= 0) continue;  // HostPortInfo.Add ignores port <= 0
+                string ip = s.s(ptip[q]), pr = s.s(ptpr[q]);
+                if (ip.empty()) ip = "0.0.0.0";
+                if (pr.empty()) pr = "TCP";
+                auto key = std::make_tuple(E.ip_dict.get(ip), E.proto_dict.get(pr), (int32_t)ptpo[q]);
+                auto it = E.port_ids.find(key);
+                int id;
+                if (it == E.port_ids.end()) { id = (int)E.port_defs.size(); E.port_ids[key] = id; E.port_defs.push_back(key); }
+                else id = it->second;
+                S.pod_port_ids.push_back(id);
+            }
+        }
+        if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
+            int n = p.node;
+            if (p.backfill) { bf[n].c += p.req.c; bf[n].m += p.req.m; bf[n].g += p.req.g; }
+            if (p.status == Releasing) {
+                rel[n].c += p.req.c; rel[n].m += p.req.m; rel[n].g += p.req.g;
+                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
+            } else {
+                idle[n].c -= p.req.c; idle[n].m -= p.req.m; idle[n].g -= p.req.g;
+            }
+            S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+            podcnt[n]++;
+            nzc[n] += p.nzc;
+            nzm[n] += p.nzm;
+            for (size_t k = (size_t)S.pod_port_off[i]; k < S.pod_port_ids.size(); ++k)  // pod i's run (still open)
+                node_ports[n].push_back(S.pod_port_ids[k]);
+        }
+    }
+    S.pod_port_off[P] = (int32_t)S.pod_port_ids.size();
+    for (int i = 0; i < N; ++i) if (bf[i].c || bf[i].m || bf[i].g) S.any_bf = 1;
+    S.h_alloc.resize(N);
+    for (int i = 0; i < N; ++i) S.h_alloc[i] = R3{acpu[i], amem[i], agpu[i]};
+
+    mark("pods:B");
+    {
         for (size_t j = 0; j < S.jobs.size(); ++j) S.jobs[j].tasks.reserve(ntask[j]);
         for (int i = 0; i < P; ++i)
             if (slot_of[i] >= 0) S.jobs[slot_of[i]].tasks.push_back(i);
