@@ -1070,6 +1070,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (aff.active && !(same_run(plo, a, b, {&plk, &plv}) && same_prog(a, b))) return false;
         return true;
     };
+    vector<int> cls_pod;  // class -> its first pod
     int prev_pending = -1;
     for (int i = 0; i < P; ++i) {
         HPod& p = S.pods[i];
@@ -1181,13 +1182,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         p.cls = (int)S.classes.size();
         class_ids.emplace(std::move(sig), p.cls);
         S.classes.push_back(c);
+        cls_pod.push_back(i);  // classes are created in pod order: i is the class's first pod
     }
+    mark("classes:loop");
     // port masks per class (conflict = CheckConflict, own = HostPortInfo.Add)
     if (E.port_defs.size() > 256) fail_unsupported("more than 256 distinct host ports");
     E.pw = ((int)E.port_defs.size() + 63) / 64;
     {
-        vector<int> cls_pod(S.classes.size(), -1);
-        for (int i = 0; i < P; ++i) if (S.pods[i].cls >= 0 && cls_pod[S.pods[i].cls] < 0) cls_pod[S.pods[i].cls] = i;
         int zero_ip = E.ip_dict.get("0.0.0.0");
         for (size_t ci = 0; ci < S.classes.size(); ++ci) {
             TaskClass& c = S.classes[ci];
