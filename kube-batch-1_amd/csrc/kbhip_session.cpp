@@ -863,6 +863,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     // Pass B (pod order): namespace and host-port dictionaries, node accumulation,
     // job slots (a job's tasks are its pods in pod order).
     vector<int32_t> ntask(S.jobs.size(), 0), slot_of(P);
+    vector<AffPod> ap(P);  // the pod (anti-)affinity model's view of each pod
     std::unordered_map<int32_t, int> ns_by_off;  // strtab offset -> namespace id
     int32_t last_ns_off = -1, last_ns = -1;       // consecutive pods (one job) share a namespace
     for (int i = 0; i < P; ++i) {
@@ -885,6 +886,14 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 if (allocated_status(p.status)) j.cnt_alloc++;
                 if (p.status == AOB) j.cnt_aob++;
             }
+            AffPod& a = ap[i];
+            a.ns = p.ns;
+            a.status = p.status;
+            a.session_job = slot >= 0;
+            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
+            a.node = on_node ? p.node : -1;
+            a.target = a.session_job && allocated_status(p.status) && on_node;
+            a.pending = a.session_job && p.status == Pending;
         }
         S.pod_port_off[i] = (int32_t)S.pod_port_ids.size();
         for (int k = pco[i]; k < pco[i + 1]; ++k) {
@@ -933,19 +942,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     mark("jobs");
     // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
     AffinityModel aff;
-    {
-        vector<AffPod> ap(P);
-        for (int i = 0; i < P; ++i) {
-            const HPod& p = S.pods[i];
-            AffPod& a = ap[i];
-            a.ns = p.ns;
-            a.status = p.status;
-            a.session_job = p.job >= 0;
-            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
-            a.node = on_node ? p.node : -1;
-            a.target = a.session_job && allocated_status(p.status) && on_node;
-            a.pending = a.session_job && p.status == Pending;
-        }
+    {  // ap: filled in pass B
         try {
             aff.build(s, N, npad, ap, E.nss.strs, S.conf.pred_on != 0, S.conf.score_mult > 0 && S.conf.w_pa != 0);
         } catch (const std::invalid_argument& e) {
