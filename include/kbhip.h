@@ -124,6 +124,26 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
  * kbhip_allocate; returns their number. */
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 
+/* SURVEY §8(b) per-task entry points, for a Go host that keeps the
+ * reference's own backfill / preempt loops and offloads only their sweeps.
+ *
+ * kbhip_first_fit <- the node loop of backfillAction.Execute
+ *   (pkg/scheduler/actions/backfill/backfill.go:51-65): each task, in the
+ *   given order, goes to the lowest-index node passing Session.PredicateFn and
+ *   is committed with Session.Allocate (framework/session.go:237-297, including
+ *   the drf / proportion AllocateFunc and the dispatch of a Ready job).
+ *   out_node[i] = node index or -1.  Tasks must be Pending tasks of the
+ *   session.  Returns the number placed.
+ * kbhip_sweep_scores <- the PredicateFn + NodeOrderFn sweep of preempt()
+ *   (pkg/scheduler/actions/preempt/preempt.go:270-287): out_keys[n]
+ *   (optional, n_nodes entries) = pack_key(score, n) — score in bits 63..32
+ *   biased by 2^31, (0x7fffffff - n) << 1 below — for a node that passes
+ *   PredicateFn and has a NodeOrderFn score, 0 otherwise; sorting the keys
+ *   descending is util.SelectBestNode's order (util/sort.go:25-37).  The
+ *   session state is not changed.  Returns the number of passing nodes. */
+int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node);
+int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys);
+
 /* Run the reclaim action (actions/reclaim/reclaim.go:41-196) / the preempt
  * action (actions/preempt/preempt.go:43-353) on the session's current state.
  * Output records in decision order: (pod, node, KBHIP_EVICTED) for every
@@ -134,7 +154,12 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
  * statements leave no record (and, like the reference, leave the victims'
  * node copies Releasing).  Returns the record count.  KBHIP_EUNSUPPORTED on
  * node-sharded sessions and sessions with pod (anti-)affinity terms.
- * Replaces the reference's reclaimAction.Execute / preemptAction.Execute. */
+ * Replaces the reference's reclaimAction.Execute / preemptAction.Execute.
+ * If an action fails part-way (negative return) the session's host model may
+ * hold a partial action: close it and open a new one. */
+int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
+
 /* Carry the session over to the next scheduling session (SURVEY §8(f) row 3,
  * the delta path of cache.go:515-583's per-session Snapshot): the state the
  * scheduler cache holds once this session's binds and evictions reached it —
@@ -143,12 +168,10 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
  * recomputed on the host and only the changed row runs uploaded (no snapshot
  * parse, no re-encode).  The session can then run its actions again.
  * *out_uploaded_bytes (optional) = bytes sent to the device.
- * KBHIP_EUNSUPPORTED on shards and with pod (anti-)affinity terms; pod
- * arrivals / deletions need kbhip_session_open. */
+ * KBHIP_EUNSUPPORTED on shards and when a pending task class reads the pod
+ * (anti-)affinity count tables; pod arrivals / deletions need
+ * kbhip_session_open. */
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
-
-int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
-int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap);
 
 /* Read the device node state: N x 12 int64 (idle, used, releasing,
  * backfilled; cpu/mem/gpu each) of the session's nodes (a shard session: its

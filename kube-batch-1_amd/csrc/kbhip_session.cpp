@@ -571,7 +571,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                     for (int k = 0; k < 4; ++k) {  // nodeorder.go:177-249
                         auto it = p.args.find(names[k]);
                         int64_t v;
-                        if (it != p.args.end() && !it->second.empty() && parse_int64(it->second, &v)) w[k] = (int)v;
+                        if (it != p.args.end() && !it->second.empty() && parse_int64(it->second, &v)) {
+                            // Go's int is 64-bit; the device score is int32 (checked per class below)
+                            if (v > INT32_MAX || v < INT32_MIN) fail_unsupported("nodeorder weight outside int32: " + it->second);
+                            w[k] = (int)v;
+                        }
                     }
                     S.conf.w_lr = w[0]; S.conf.w_bra = w[1]; S.conf.w_na = w[2]; S.conf.w_pa = w[3];
                 }
@@ -1205,12 +1209,12 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             for (auto x : own) E.masks.push_back(x);
         }
     }
+    S.n_spaces = aff.n_spaces;
     if (encode_only) {  // kbhip_debug_encode: keep copies of the compiled tables, touch no device
         S.h_dom = aff.dom;
         S.h_aff_cnt = aff.cnt;
         S.h_aff_scalar = aff.scalar;
         S.h_aff_items = aff_items;
-        S.n_spaces = aff.n_spaces;
     } else {
         HIPCHK(hipSetDevice(device));
         S.device = device;
@@ -1316,6 +1320,14 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             rng(0, 10 * (int64_t)S.conf.w_bra, &lo, &hi);
             rng(na_lo * S.conf.w_na, na_hi * S.conf.w_na, &lo, &hi);
             const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
+            {  // nodeorder.go:287-313 sums in Go's 64-bit int; the kernels' score is int32 (kbhip_eval.h
+               // node_score): sessions whose score range (with the inter-pod term) leaves int32 are refused
+                int64_t flo = lo, fhi = hi;
+                rng(0, 10 * (int64_t)S.conf.w_pa, &flo, &fhi);
+                const int64_t a = flo * mult, b = fhi * mult;
+                if (std::min(a, b) < INT32_MIN || std::max(a, b) > INT32_MAX)
+                    fail_unsupported("nodeorder score range leaves int32 (weights x terms x tiers)");
+            }
             KeyFormat& kf = S.class_kf[ci];
             kf.use32 = ibits <= 25 && shi - slo + 1 < ((int64_t)1 << (31 - ibits)) && slo >= INT32_MIN && shi <= INT32_MAX;
             kf.ent32 = kf.use32 && ibits <= 24 && shi - slo + 1 < ((int64_t)1 << (26 - ibits));
@@ -1420,62 +1432,6 @@ static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
 }
 
 // ---------------------------------------------------------------------------
-// backfill action (actions/backfill/backfill.go:40-70): every Pending task of
-// every job whose InitResreq is empty is allocated on the first node (lowest
-// index) passing the predicates.  Pinned order (SURVEY Appendix B.1 item 6):
-// jobs by UID, tasks by UID, nodes by index.  Per-task first-fit sweeps of the
-// general kernel (mode 1), 64 tasks per control-block round trip.
-// ---------------------------------------------------------------------------
-static void backfill_run(Session& S) {
-    vector<int> cand;
-    for (auto& j : S.jobs)
-        for (int t : j.tasks) {
-            const HPod& p = S.pods[t];
-            if (p.status != Pending || p.cls < 0) continue;
-            if (!(p.ireq.c < kMinCPU && p.ireq.m < kMinMem && p.ireq.g < kMinGPU)) continue;  // IsEmpty
-            cand.push_back(t);
-        }
-    for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
-        const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
-        PopCtrl& h = *S.h_ctrl;
-        h.stop = -1;
-        h.n_done = 0;
-        h.ready_count = 0;
-        h.min_avail = 0;
-        h.gang_mode = 0;
-        h.n_tasks = m;
-        h.any_bf = S.any_bf;
-        h.fallback = S.fallback;
-        h.mode = 1;
-        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[cand[off + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
-        std::memset(h.arrive, 0, sizeof h.arrive);
-        std::memset(h.slot, 0, sizeof h.slot);
-        std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
-        std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
-        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
-        for (int i = 0; i < m; ++i) sweep_task(S, i, h.cls[i]);
-        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
-        HIPCHK(hipStreamSynchronize(S.stream));
-        S.stats.sweeps += m;
-        S.stats.tasks += m;
-        if (h.n_done != m || h.stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
-        for (int i = 0; i < m; ++i) {
-            const int node = h.res_node[i];
-            if (node < 0) continue;
-            HPod& p = S.pods[cand[off + i]];
-            p.status = Allocated;  // Session.Allocate(task, node, false) (session.go:237-297)
-            p.node = node;
-            S.jobs[p.job].cnt_alloc++;
-            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
-            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
-            S.stats.placed++;
-            S.log.emplace_back(cand[off + i], node, KBHIP_ALLOCATED);
-        }
-        S.any_bf = h.any_bf;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // batched pop launches: one k_pop_batch per job-pop chunk of one class.  Two
 // result slots, so that the predicted next pop can be queued on the stream
 // behind a running one (Allocator::speculate) and its results told apart.
@@ -1500,6 +1456,17 @@ static void ov_quiesce(Session& S) {
 
 // Nothing but the winner's row can change between the chunk's tasks: the
 // condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
+// Some task class reads or writes the pod (anti-)affinity count tables
+// (kbhip_affinity.h): its program has predicate terms, inter-pod priority
+// terms or commit updates.  The tables are built from the snapshot at open;
+// paths that change pod statuses outside allocate / backfill (evictions,
+// carry) do not rebuild them, so they refuse such sessions.
+static bool has_aff_classes(const Session& S) {
+    for (auto& c : S.classes)
+        if (c.aff || c.ipa_n || c.upd_n) return true;
+    return false;
+}
+
 static bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
     return S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4 &&
@@ -2287,9 +2254,7 @@ struct Allocator {
     static bool less_strict(const R3& a, const R3& b) { return a.c < b.c && a.m < b.m && a.g < b.g; }
     void check_evict_supported() {
         if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt on a node-sharded session");
-        if (S.n_spaces > 0) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
-        for (auto& c : S.classes)
-            if (c.aff || c.ipa_n) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
+        if (has_aff_classes(S)) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
     }
     void on_deallocate(int pi) {  // event handlers drf.go:144-151, proportion.go:211-219
         const HPod& p = S.pods[pi];
@@ -2322,7 +2287,7 @@ struct Allocator {
     // the nodes passing PredicateFn with a NodeOrderFn score; reclaim = passing nodes in order.
     void rank_nodes(int cls, bool by_score, vector<int>& out) {
         const int N = S.nc.n;
-        if (!S.b_rank_keys.p) {
+        if (!S.b_rank_sorted.p) {
             S.b_rank_keys.alloc<uint64_t>(N);
             S.b_rank_sorted.alloc<uint64_t>(N);
             S.b_rank_cnt.alloc<uint32_t>(4);
@@ -2705,6 +2670,128 @@ struct Allocator {
     }
 };
 
+// ---------------------------------------------------------------------------
+// backfill action (actions/backfill/backfill.go:40-70): every Pending task of
+// every job whose InitResreq is empty is allocated on the first node (lowest
+// index) passing the predicates.  Pinned order (SURVEY Appendix B.1 item 6):
+// jobs by UID, tasks by UID, nodes by index.  Per-task first-fit sweeps of the
+// general kernel (mode 1), 64 tasks per control-block round trip.
+// ---------------------------------------------------------------------------
+// first_fit: the inner loop of backfill.go:51-65 for the given tasks, in
+// order: each goes to the lowest-index node passing PredicateFn and is
+// committed with Session.Allocate (session.go:237-297); out_node[i] = that
+// node or -1.  Tasks must be Pending tasks of the session (task class >= 0).
+static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) {
+    vector<int> cand(ids, ids + n);
+    for (int t : cand)
+        if (t < 0 || t >= (int)S.pods.size() || S.pods[t].cls < 0 || S.pods[t].status != Pending)
+            throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
+    std::fill(out_node, out_node + n, -1);
+    ov_quiesce(S);
+    Allocator A(S);
+    A.compile_orders();
+    A.open_plugins();
+    for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
+        const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
+        PopCtrl& h = *S.h_ctrl;
+        h.stop = -1;
+        h.n_done = 0;
+        h.ready_count = 0;
+        h.min_avail = 0;
+        h.gang_mode = 0;
+        h.n_tasks = m;
+        h.any_bf = S.any_bf;
+        h.fallback = S.fallback;
+        h.mode = 1;
+        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[cand[off + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
+        std::memset(h.arrive, 0, sizeof h.arrive);
+        std::memset(h.slot, 0, sizeof h.slot);
+        std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
+        std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
+        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+        for (int i = 0; i < m; ++i) sweep_task(S, i, h.cls[i]);
+        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+        S.stats.sweeps += m;
+        S.stats.tasks += m;
+        if (h.n_done != m || h.stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
+        for (int i = 0; i < m; ++i) {
+            const int node = h.res_node[i];
+            out_node[off + i] = node;
+            if (node < 0) continue;
+            const int pi = cand[off + i];
+            HPod& p = S.pods[pi];
+            HJob& job = S.jobs[p.job];
+            p.status = Allocated;  // Session.Allocate(task, node, false) (session.go:237-297)
+            p.node = node;
+            job.cnt_alloc++;
+            job.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
+            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
+            A.on_allocate(pi);  // drf / proportion AllocateFunc
+            S.stats.placed++;
+            S.log.emplace_back(pi, node, KBHIP_ALLOCATED);
+            if (A.job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-321)
+                for (int t : job.tasks)
+                    if (S.pods[t].status == Allocated) { S.pods[t].status = Binding; job.priority = S.pods[t].priority; }
+        }
+        S.any_bf = h.any_bf;
+    }
+}
+
+static void backfill_run(Session& S) {
+    vector<int32_t> cand;
+    for (auto& j : S.jobs)
+        for (int t : j.tasks) {
+            const HPod& p = S.pods[t];
+            if (p.status != Pending || p.cls < 0) continue;
+            if (!(p.ireq.c < kMinCPU && p.ireq.m < kMinMem && p.ireq.g < kMinGPU)) continue;  // IsEmpty
+            cand.push_back(t);
+        }
+    vector<int32_t> node(cand.size());
+    first_fit(S, cand.data(), (int)cand.size(), node.data());
+}
+
+// The nodeorder sweep of one task as the preempt action uses it
+// (preempt.go:270-287): per node, pack_key(score, index) when the node passes
+// PredicateFn and has a NodeOrderFn score, 0 otherwise; sorting the keys
+// descending gives util.SelectBestNode's order.  Reads the session state,
+// changes nothing.  Returns the number of passing nodes.
+static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
+    if (pod < 0 || pod >= (int)S.pods.size() || S.pods[pod].cls < 0)
+        throw Error(KBHIP_EINVAL, "task id has no task class (not a pending task of the session)");
+    if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "sweep_scores on a node-sharded session");
+    ov_quiesce(S);
+    const int cls = S.pods[pod].cls;
+    const int N = S.nc.n;
+    if (!S.b_rank_keys.p) {
+        S.b_rank_keys.alloc<uint64_t>(std::max(N, 1));
+        S.b_rank_cnt.alloc<uint32_t>(4);
+    }
+    PopCtrl& h = *S.h_ctrl;
+    h.stop = -1;
+    h.n_done = 0;
+    h.n_tasks = 1;
+    h.mode = 0;
+    h.any_bf = S.any_bf;
+    h.fallback = S.fallback;
+    h.cls[0] = cls;
+    h.ipa_lo[0] = h.ipa_hi[0] = 0;
+    HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+    if (S.classes[cls].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
+    HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
+    HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, 1, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_cnt.p,
+                             S.stream));
+    uint32_t cnt = 0;
+    HIPCHK(hipMemcpyAsync(&cnt, S.b_rank_cnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+    if (out_keys && N)
+        HIPCHK(hipMemcpyAsync(out_keys, S.b_rank_keys.p, (size_t)N * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    S.stats.sweeps++;
+    return (int)cnt;
+}
+
 // JobInfo.FitError (job_info.go:343-372) from the histogram of the job's last walk.
 static string fit_error(const HJob& j) {
     if (j.fit[0] == 0) return "0 nodes are available";
@@ -2719,7 +2806,9 @@ static string fit_error(const HJob& j) {
 }
 // The gang plugin's OnSessionClose (plugins/gang/gang.go:166-187): the
 // Unschedulable condition message of every job that is not Ready, one line
-// "<job uid>\t<message>\n" per job in UID order; empty without gang.
+// "<job uid>\t<message>\n" per job in UID order; empty without gang.  A job
+// with an IsBackfill task gets the PodGroupBackfilled condition instead, which
+// has no message (gang.go:189-199): "<job uid>\tBackfilled\n".
 static string gang_close_text(const Session& S) {
     if (!S.gang_close) return "";
     string out;
@@ -2727,9 +2816,15 @@ static string gang_close_text(const Session& S) {
         const HJob& j = S.jobs[i];
         if (j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
         int ready = 0;                              // readyTaskNum (gang.go:212-222)
+        bool backfill = false;
         for (int t : j.tasks) {
             const int st = S.pods[t].status;
             ready += allocated_status(st) || st == Pipelined || st == Succeeded;
+            backfill = backfill || S.pods[t].backfill;
+        }
+        if (backfill) {
+            out += S.job_uid[i] + "\tBackfilled\n";
+            continue;
         }
         out += S.job_uid[i] + "\t" + std::to_string(j.min_avail - ready) + "/" + std::to_string(j.tasks.size()) +
                " tasks in gang unschedulable: " + fit_error(j) + "\n";
@@ -2781,6 +2876,16 @@ const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
 
 int kbhip_device_count(void) { ABI_GUARD(return kbhip::device_count();) }
 
+// Arguments of the actions that return a record log: a device session and,
+// when cap > 0, three output arrays of at least cap entries.
+static void check_log_args(kb_session* s, const int32_t* out_pod, const int32_t* out_node, const uint8_t* out_kind,
+                           int64_t cap) {
+    if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+    if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+    if (cap < 0 || (cap > 0 && (!out_pod || !out_node || !out_kind)))
+        throw kbhip::Error(KBHIP_EINVAL, "null output array with cap > 0");
+}
+
 static int open_common(const kbs::Snapshot& snap, int device, kb_session** out) {
     int nd = kbhip::device_count();
     if (nd <= 0) throw kbhip::Error(KBHIP_ENODEV, "no gfx950 HIP device available");
@@ -2826,8 +2931,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
 
 int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     ABI_GUARD({
-        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         s->s.log.clear();
         kbhip::Allocator a(s->s);
@@ -2844,8 +2948,7 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     ABI_GUARD({
-        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
         s->s.log.clear();
@@ -2857,6 +2960,28 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
             out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
         }
         return (int)n;
+    })
+}
+
+int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node) {
+    ABI_GUARD({
+        if (!s || n < 0 || (n > 0 && (!task_ids || !out_node))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        s->s.log.clear();
+        kbhip::first_fit(s->s, task_ids, n, out_node);
+        int placed = 0;
+        for (int i = 0; i < n; ++i) placed += out_node[i] >= 0;
+        return placed;
+    })
+}
+
+int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::sweep_scores(s->s, task_id, out_keys);
     })
 }
 // kbhip_session_carry: the next scheduling session's
@@ -2874,7 +2999,7 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 // at open.  New or deleted pods need a snapshot (kbhip_session_open).
 static void session_carry(Session& S) {
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "carry on a node-sharded session");
-    if (S.n_spaces > 0) throw Error(KBHIP_EUNSUPPORTED, "carry with pod (anti-)affinity terms");
+    if (has_aff_classes(S)) throw Error(KBHIP_EUNSUPPORTED, "carry with pod (anti-)affinity terms");
     ov_quiesce(S);
     HIPCHK(hipStreamSynchronize(S.stream));
     const int N = S.nc.n, P = (int)S.pods.size();
@@ -2966,8 +3091,7 @@ static void session_carry(Session& S) {
 static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
                         int64_t cap) {
     ABI_GUARD({
-        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
         s->s.log.clear();

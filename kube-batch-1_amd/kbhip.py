@@ -26,7 +26,8 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_session_close", "kbhip_last_error", "kbhip_debug_encode", "kbhip_debug_table",
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
-           "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry")
+           "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
+           "kbhip_first_fit", "kbhip_sweep_scores")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -73,6 +74,8 @@ def lib() -> ctypes.CDLL:
         L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
+        L.kbhip_first_fit.argtypes = [vp, vp, i32, vp]
+        L.kbhip_sweep_scores.argtypes = [vp, i32, vp]
         L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_carry.argtypes = [vp, vp]
         L.kbhip_preempt.argtypes = [vp, vp, vp, vp, i64]
@@ -162,6 +165,22 @@ class Session:
     def backfill(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Run backfillAction.Execute on the current session state."""
         return self._action(lib().kbhip_backfill, cap)
+
+    def first_fit(self, task_ids) -> np.ndarray:
+        """kbhip_first_fit: backfill.go:51-65 for the given pending tasks, in
+        order (lowest-index node passing the predicates, Session.Allocate);
+        returns the node per task (-1: none)."""
+        ids = np.ascontiguousarray(task_ids, dtype=np.int32)
+        out = np.full(max(ids.size, 1), -1, np.int32)
+        _check(lib().kbhip_first_fit(self._h, _p(ids), ids.size, _p(out)))
+        return out[: ids.size].copy()
+
+    def sweep_scores(self, task_id: int, n_nodes: int) -> Tuple[int, np.ndarray]:
+        """kbhip_sweep_scores: preempt.go:270-287's predicate + score sweep of
+        one task: (passing nodes, per-node packed keys; 0 = node fails)."""
+        keys = np.zeros(max(n_nodes, 1), np.uint64)
+        n = _check(lib().kbhip_sweep_scores(self._h, int(task_id), _p(keys)))
+        return n, keys[:n_nodes].copy()
 
     def carry(self) -> int:
         """kbhip_session_carry: become the next session (binds / evictions applied); bytes uploaded."""

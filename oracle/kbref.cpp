@@ -1838,7 +1838,9 @@ static int readyTaskNum(const JobInfo& j) {
     return cnt;
 }
 // The PodGroup Unschedulable condition messages of OnSessionClose, one line
-// per job that is not Ready: "<job uid>\t<message>\n", jobs in UID order.
+// per job that is not Ready: "<job uid>\t<message>\n", jobs in UID order.  A
+// job with an IsBackfill task gets the PodGroupBackfilled condition instead,
+// which carries no message (gang.go:189-199): "<job uid>\tBackfilled\n".
 static string gangClose(World& w) {
     bool gang = false;
     for (auto& tier : w.ssn.tiers)
@@ -1847,6 +1849,12 @@ static string gangClose(World& w) {
     string out;
     for (JobInfo* j : w.ssn.Jobs) {
         if (j->GetReadiness() == Ready) continue;
+        bool backfill = false;
+        for (auto& kv : j->Tasks) backfill = backfill || kv.second->IsBackfill;
+        if (backfill) {
+            out += j->UID + "\tBackfilled\n";
+            continue;
+        }
         out += j->UID + "\t" + std::to_string(j->MinAvailable - readyTaskNum(*j)) + "/" +
                std::to_string(j->Tasks.size()) + " tasks in gang unschedulable: " + fitError(*j) + "\n";
     }
@@ -2201,6 +2209,43 @@ int ref_gang_close(const char* path, const char* actions, char* out, int cap) {
         const std::string t = ref::gangClose(w);
         if (out && cap > (int)t.size()) std::memcpy(out, t.c_str(), t.size() + 1);
         return (int)t.size();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+/* After the actions: preempt()'s sweep for the task of pod `pod`
+ * (preempt.go:270-287) — per node, in snapshot order, the packed key
+ * (score + 2^31) << 32 | (0x7fffffff - node) << 1 when Session.PredicateFn
+ * passes and Session.NodeOrderFn returns a score, else 0.  Returns the number
+ * of such nodes, -1 on error (also when the pod is not a task of a session job). */
+int ref_sweep_scores(const char* path, const char* actions, int pod, uint64_t* out_keys) {
+    try {
+        ref::World w;
+        w.snap.load_file(path);
+        ref::loadWorld(w);
+        ref::openSession(w);
+        if (actions && *actions) ref::runActions(w, actions);
+        ref::TaskInfo* task = nullptr;
+        for (auto* j : w.ssn.Jobs) {
+            auto it = j->Tasks.find(pod);
+            if (it != j->Tasks.end()) task = it->second;
+        }
+        if (!task) throw std::runtime_error("pod is not a task of a session job");
+        int cnt = 0;
+        for (size_t i = 0; i < w.ssn.Nodes.size(); ++i) {
+            ref::NodeInfo* node = w.ssn.Nodes[i];
+            const int idx = w.ssn.nodeIndex[node->Name];
+            uint64_t k = 0;
+            int score = 0;
+            if (w.ssn.PredicateFn_(task, node) && w.ssn.NodeOrderFn_(task, node, &score)) {
+                k = ((uint64_t)((uint32_t)score ^ 0x80000000u) << 32) | ((uint64_t)(0x7fffffff - idx) << 1);
+                ++cnt;
+            }
+            out_keys[idx] = k;
+        }
+        return cnt;
     } catch (std::exception& e) {
         g_err = e.what();
         return -1;

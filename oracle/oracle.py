@@ -209,3 +209,19 @@ def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096, actions:
         raise RuntimeError("trace larger than cap_tasks")
     return {"pod": pod[:n], "node": node[:n], "status": st[:n], "ok": ok[:n], "raw": raw[:n],
             "lohi": lohi[:n], "flags": flags[:n], "key": key[:n], "mode": mode[:n]}
+
+
+def ref_sweep_scores(path: str, pod: int, n_nodes: int, actions: str = "") -> Tuple[int, np.ndarray]:
+    """Faithful restatement of preempt()'s predicate + score sweep
+    (preempt.go:270-287) for one task after the given actions: (passing nodes,
+    per-node packed keys, 0 = node fails)."""
+    lib = _lib("kbref")
+    fn = lib.ref_sweep_scores
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_void_p]
+    keys = np.zeros(max(n_nodes, 1), np.uint64)
+    n = fn(path.encode(), actions.encode(), pod, _p(keys))
+    if n < 0:
+        lib.ref_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.ref_last_error().decode())
+    return n, keys[:n_nodes]

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Golden fixtures for full-size parity (tests/golden/fullsize.json).
+
+BASELINE.json's headline config C4 (100k nodes x 1M pods) and C3 (20k nodes,
+labels / taints / zone anti-affinity / 8 queues) are too large to commit as
+placement logs, so the fixture pins them by digest:
+
+* snap_sha256 — SHA-256 of the KBS1 snapshot kbgen writes for the config's
+  seed (pins the generator: the GPU test regenerates the same bytes);
+* n, log_sha256 — the number of placements and the SHA-256 of the CPU
+  oracle's placement log (int32 array [3][n]: pod index, node index, status
+  code 4 Allocated / 8 Pipelined, in decision order) from the hoisted
+  restatement oracle/kbfast.cpp (itself cross-checked against the faithful
+  oracle/kbref.cpp on smaller snapshots, tests/test_oracle.py);
+* head — the first 64 placements verbatim (readable diffs on a mismatch).
+
+Usage: python tests/golden/make_fullsize.py [c3] [c4]   (C4 takes ~8 min on 8 cores)
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+
+OUT = os.path.join(HERE, "fullsize.json")
+
+
+def log_digest(pod, node, status):
+    arr = np.stack([np.asarray(pod), np.asarray(node), np.asarray(status)]).astype(np.int32)
+    return hashlib.sha256(arr.tobytes()).hexdigest()
+
+
+def snapshot(cfg, path):
+    import kbgen
+    if cfg == "c4":
+        kbgen.gen_c4(path)
+    elif cfg == "c3":
+        kbgen.gen_c3().write(path)
+    else:
+        raise ValueError(cfg)
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def main(cfgs):
+    import oracle
+    oracle.build()
+    gold = json.load(open(OUT)) if os.path.exists(OUT) else {}
+    for cfg in cfgs:
+        path = f"/tmp/kbhip_golden_{cfg}.kbs"
+        h = snapshot(cfg, path)
+        t0 = time.time()
+        pl = oracle.fast_allocate(path, threads=os.cpu_count() or 8)
+        gold[cfg] = {"snap_sha256": h, "n": len(pl), "log_sha256": log_digest(pl.pod, pl.node, pl.status),
+                     "head": [list(map(int, x)) for x in pl.as_list()[:64]],
+                     "oracle": "oracle/kbfast.cpp fast_allocate", "oracle_s": round(time.time() - t0, 1)}
+        print(cfg, gold[cfg]["n"], gold[cfg]["oracle_s"], "s", flush=True)
+        with open(OUT, "w") as f:
+            json.dump(gold, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["c3", "c4"])

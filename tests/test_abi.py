@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
@@ -39,3 +41,31 @@ def test_no_device_is_an_error_not_a_fallback(engine_lib):
     rc = engine_lib.kbhip_session_open_file(os.path.join(HERE, "golden", "c1_default.kbs").encode(), 0,
                                             ctypes.byref(h))
     assert rc == -2  # KBHIP_ENODEV
+
+
+def test_score_outside_int32_rejected(engine_lib, tmp_path):
+    """nodeorder weights whose score range leaves int32 (Go sums in 64-bit int,
+    nodeorder.go:209-246, 287-313) are refused with KBHIP_EUNSUPPORTED, not
+    silently wrapped."""
+    import kbgen
+    import kbhip
+    for w in ("3000000000", "300000000"):
+        c = kbgen.gen_c1()
+        c.args = {"nodeorder": {"leastrequested.weight": w}}
+        p = str(tmp_path / f"w{w}.kbs")
+        c.write(p)
+        with pytest.raises(kbhip.KbhipError, match="int32"):
+            kbhip.EncodedSnapshot(p)
+    c = kbgen.gen_c1()
+    c.args = {"nodeorder": {"leastrequested.weight": "30000000"}}  # 10 x 3e7 fits
+    p = str(tmp_path / "ok.kbs")
+    c.write(p)
+    kbhip.EncodedSnapshot(p).close()
+
+
+def test_log_actions_validate_outputs(engine_lib):
+    """A null session or null output arrays with cap > 0 return KBHIP_EINVAL."""
+    import ctypes
+    L = engine_lib
+    for fn in (L.kbhip_allocate, L.kbhip_backfill, L.kbhip_reclaim, L.kbhip_preempt):
+        assert fn(None, None, None, None, 4) == -1

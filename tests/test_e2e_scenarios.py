@@ -1,0 +1,270 @@
+"""The reference's e2e scenarios (test/e2e/*.go) restated as snapshots.
+
+The reference's e2e suite needs a live cluster (kube-apiserver, kubelets, job
+controller), so it cannot run here.  Each scenario below rebuilds the cluster
+state its test creates at the moment the job of interest is submitted —
+earlier jobs of the test as Running pods bound where that test put them — and
+runs ONE scheduling session with the shipped conf (config/kube-batch-conf.yaml
+tiers; actions allocate, or the default "reclaim, allocate, backfill,
+preempt").  Each asserts the e2e test's own qualitative expectation on the
+faithful CPU oracle (kbref) and, under ``-m gpu``, that the engine's records
+equal the oracle's.
+
+Three scenarios reach their e2e outcome only over several sessions (the job
+controller recreating evicted pods, later sessions) or not at all in this
+fork's code (preempt.go:134-143 commits a cross-job statement only for a Ready
+job, and gang's JobReady counts AllocatedStatuses only): for queue_reclaim,
+preemption_session and backfill_scheduling_session the ONE session's outcome
+is asserted as derived from the reference code, with the derivation in the
+builder's docstring.
+
+Cluster: three worker nodes w-a, w-b, w-c of 4 CPU / 8 GiB / 110 pods with
+kubernetes.io/hostname labels (the e2e kind cluster's shape); oneCPU = 1000m,
+halfCPU = 500m (test/e2e/util.go:51-52), pods without a memory request.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import kbgen
+
+HOST = "kubernetes.io/hostname"
+ONE, HALF = 1000, 500
+NODES = ("w-a", "w-b", "w-c")
+KIND_CODE = {1: 4, 2: 8, 3: 128}  # engine kinds -> oracle TaskStatus codes (Allocated, Pipelined, Releasing)
+
+
+def _cluster(queues=("default",), taints=None):
+    c = kbgen.Cluster()
+    for q in queues:
+        c.add_queue(q, 1)
+    for n in NODES:
+        c.add_node(n, 4000, 8 * kbgen.GI, 0, 110, labels={HOST: n}, taints=list(taints or []))
+    return c
+
+
+def _job(c, name, queue, n, cpu, min_member, node=None, phase="Pending", ts=0, **pod):
+    """n pods of one PodGroup; node: one node for all, or a list per pod."""
+    c.add_job("e2e", name, queue, min_member=min_member, ts=ts)
+    for k in range(n):
+        nd = node[k] if isinstance(node, (list, tuple)) else node
+        c.add_pod("e2e", f"{name}-{k}", uid=f"{name}-{k:03d}", group=name, node=nd,
+                  phase="Running" if nd else phase, ts=ts, containers=[kbgen.res(cpu)], **pod)
+
+
+def _pod_index(c):
+    return {p.uid: i for i, p in enumerate(sorted(c.pods, key=lambda p: p.uid))}
+
+
+def _node_name(i):
+    return sorted(NODES)[i]
+
+
+def _write(c, tmp_path, name):
+    p = str(tmp_path / f"{name}.kbs")
+    c.write(p)
+    return p
+
+
+# ---- scenario builders: (cluster, actions, check(records, cluster)) --------
+def nodeorder_node_affinity():
+    """test/e2e/nodeorder.go:29-72: preferred node affinity (weight 100) to
+    hostname nodeNames[0] -> the pod lands there.  The target is w-c, made the
+    least attractive by LeastRequested (2 CPU already running there)."""
+    c = _cluster()
+    _job(c, "load", "default", 2, ONE, 1, node="w-c")
+    aff = {"node": {"preferred": [(100, {"expr": [(HOST, "In", ["w-c"])]})]}}
+    _job(c, "pa-job", "default", 1, ONE, 1, ts=kbgen.SEC, affinity=aff)
+
+    def check(recs, c):
+        got = {_pod_uid(c, p): n for p, n, k in recs}
+        assert got == {"pa-job-000": NODES.index("w-c")}
+    return c, "allocate", check
+
+
+def nodeorder_pod_affinity():
+    """nodeorder.go:74-136: pa-job1 (halfCPU, label test=e2e) runs on some
+    node; pa-job2 with a preferred pod affinity (weight 100) to test=e2e on
+    hostname lands on the same node.  pa-job1 sits on w-b, which
+    LeastRequested alone would not pick."""
+    c = _cluster()
+    _job(c, "pa-job1", "default", 1, HALF, 1, node="w-b", labels={"test": "e2e"})
+    aff = {"pod": {"preferred": [(100, {"selector": {"me": [("test", "In", ["e2e"])]}, "topology_key": HOST})]}}
+    _job(c, "pa-job2", "default", 1, HALF, 1, ts=kbgen.SEC, affinity=aff)
+
+    def check(recs, c):
+        got = {_pod_uid(c, p): n for p, n, k in recs}
+        assert got == {"pa-job2-000": NODES.index("w-b")}
+    return c, "allocate", check
+
+
+def nodeorder_least_requested():
+    """nodeorder.go:138-237: 3 x halfCPU pinned to nodeNames[0] and 3 x
+    halfCPU to nodeNames[1] (earlier sessions: Running there); a 1-CPU pod
+    avoids both."""
+    c = _cluster()
+    _job(c, "pa-job", "default", 3, HALF, 3, node="w-a")
+    _job(c, "pa-job1", "default", 3, HALF, 3, node="w-b")
+    _job(c, "pa-test-job", "default", 1, ONE, 1, ts=kbgen.SEC)
+
+    def check(recs, c):
+        got = {_pod_uid(c, p): n for p, n, k in recs}
+        assert set(got) == {"pa-test-job-000"}
+        assert got["pa-test-job-000"] not in (NODES.index("w-a"), NODES.index("w-b"))
+    return c, "allocate", check
+
+
+def predicates_node_affinity_fields():
+    """test/e2e/predicates.go:29-76: required node affinity by MatchFields
+    metadata.name In [computeNode()] -> the pod lands on that node.  w-a is
+    full, so computeNode returns w-b; w-c is emptier (LeastRequested would
+    pick it)."""
+    c = _cluster()
+    _job(c, "fill", "default", 4, ONE, 1, node="w-a")
+    _job(c, "some", "default", 1, ONE, 1, node="w-b")
+    aff = {"node": {"required": [{"fields": [("metadata.name", "In", ["w-b"])]}]}}
+    _job(c, "na-job", "default", 1, ONE, 1, ts=kbgen.SEC, affinity=aff)
+
+    def check(recs, c):
+        got = {_pod_uid(c, p): n for p, n, k in recs}
+        assert got == {"na-job-000": NODES.index("w-b")}
+    return c, "allocate", check
+
+
+def predicates_hostport():
+    """predicates.go:78-104: a job of 2 x nn pods (min nn) with hostPort
+    28080 -> exactly nn run (one per node), nn stay pending."""
+    c = _cluster()
+    nn = len(NODES)
+    _job(c, "hp-job", "default", 2 * nn, ONE, nn)
+    for p in c.pods:
+        p.containers = [dict(cpu=ONE, ports=[{"port": 28080}])]
+
+    def check(recs, c):
+        nodes = [n for p, n, k in recs]
+        assert len(recs) == nn and sorted(nodes) == list(range(nn))
+    return c, "allocate", check
+
+
+def predicates_pod_affinity():
+    """predicates.go:106-153: rep pods (min rep, label foo=bar) with required
+    pod affinity to foo=bar on hostname, rep = the slots of computeNode's node
+    -> all on one node.  w-a has 3 CPU free (rep 3)."""
+    c = _cluster()
+    _job(c, "busy", "default", 1, ONE, 1, node="w-a")
+    aff = {"pod": {"required": [{"selector": {"ml": {"foo": "bar"}}, "topology_key": HOST}]}}
+    _job(c, "pa-job", "default", 3, ONE, 3, ts=kbgen.SEC, affinity=aff, labels={"foo": "bar"})
+
+    def check(recs, c):
+        assert len(recs) == 3 and len({n for p, n, k in recs}) == 1
+    return c, "allocate", check
+
+
+def predicates_taints(tainted=True):
+    """predicates.go:155-192: NoSchedule taint on every node -> the job
+    stays pending; once the taints are removed it is scheduled."""
+    c = _cluster(taints=[("test-taint-key", "test-taint-val", "NoSchedule")] if tainted else None)
+    _job(c, "tt-job", "default", 1, ONE, 1)
+
+    def check(recs, c):
+        assert len(recs) == (0 if tainted else 1)
+    return c, "allocate", check
+
+
+def queue_reclaim():
+    """test/e2e/queue.go:26-71: queues q1, q2 (weight 1); q1-qj-1 (rep pods of
+    oneCPU, min 1) fills the cluster; q2-qj-2 (same shape) is submitted.  One
+    session: reclaim pops q2's job, evicts one q1 pod (proportion: q1 is above
+    its deserved half) and pipelines one q2 pod; the popped job is not pushed
+    back (reclaim.go:100-111, 185-187), so that is all for this session."""
+    c = _cluster(queues=("q1", "q2"))
+    rep = 4 * len(NODES)
+    _job(c, "q1-qj-1", "q1", rep, ONE, 1, node=[NODES[k % 3] for k in range(rep)])
+    _job(c, "q2-qj-2", "q2", rep, ONE, 1, ts=kbgen.SEC)
+
+    def check(recs, c):
+        kinds = sorted((k, _pod_uid(c, p)[:2]) for p, n, k in recs)
+        assert kinds == [(8, "q2"), (128, "q1")]
+    return c, "reclaim, allocate, backfill, preempt", check
+
+
+def preemption_session():
+    """test/e2e/job.go:151-180 (same queue, preemptee-qj fills the cluster,
+    preemptor-qj submitted; expected eventually rep/2 of each).  In this fork
+    preempt.go:87-149 commits a cross-job statement only once the preemptor
+    job is Ready, and gang's JobReady counts AllocatedStatuses only
+    (job_info.go:374-388), which a Pipelined preemptor is not: every such
+    statement is discarded, so the session records nothing.  (The e2e outcome
+    needs the job controller and later sessions.)"""
+    c = _cluster()
+    rep = 4 * len(NODES)
+    _job(c, "preemptee-qj", "default", rep, ONE, 1, node=[NODES[k % 3] for k in range(rep)])
+    _job(c, "preemptor-qj", "default", rep, ONE, 1, ts=kbgen.SEC)
+
+    def check(recs, c):
+        assert recs == []
+    return c, "reclaim, allocate, backfill, preempt", check
+
+
+def backfill_scheduling_session():
+    """test/e2e/job.go:420-470: a ReplicaSet of maxCnt - 2 one-CPU pods runs;
+    gang-qj (maxCnt pods, min maxCnt) cannot fit; bf-qj (1 pod) is submitted.
+    The session's allocate pops gang-qj first (older; job order ties), which
+    takes the 2 free CPUs and stops at its first unplaced task without
+    rollback (allocate.go:187-189); bf-qj then finds no node, and backfill
+    (backfill.go:40-70) only places BestEffort tasks.  So in one session
+    gang-qj holds 2 Allocated (not dispatched) tasks and bf-qj none."""
+    c = _cluster()
+    max_cnt = 4 * len(NODES)
+    for k in range(max_cnt - 2):  # ReplicaSet pods: no PodGroup (shadow pod groups)
+        c.add_pod("e2e", f"rs-1-{k}", uid=f"rs-1-{k:03d}", node=NODES[k % 3], phase="Running",
+                  containers=[kbgen.res(ONE)])
+    _job(c, "gang-qj", "default", max_cnt, ONE, max_cnt, ts=kbgen.SEC)
+    _job(c, "bf-qj", "default", 1, ONE, 1, ts=2 * kbgen.SEC)
+
+    def check(recs, c):
+        uids = [_pod_uid(c, p) for p, n, k in recs]
+        assert len(uids) == 2 and all(u.startswith("gang-qj-") for u in uids)
+        assert all(k == 4 for p, n, k in recs)
+    return c, "reclaim, allocate, backfill, preempt", check
+
+
+def _pod_uid(c, i):
+    return sorted(c.pods, key=lambda p: p.uid)[i].uid
+
+
+SCENARIOS = {
+    "nodeorder_node_affinity": nodeorder_node_affinity,
+    "nodeorder_pod_affinity": nodeorder_pod_affinity,
+    "nodeorder_least_requested": nodeorder_least_requested,
+    "predicates_node_affinity_fields": predicates_node_affinity_fields,
+    "predicates_hostport": predicates_hostport,
+    "predicates_pod_affinity": predicates_pod_affinity,
+    "predicates_taints_on": lambda: predicates_taints(True),
+    "predicates_taints_off": lambda: predicates_taints(False),
+    "queue_reclaim": queue_reclaim,
+    "preemption_session": preemption_session,
+    "backfill_scheduling_session": backfill_scheduling_session,
+}
+
+
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_e2e_scenario_oracle(oracle_mod, tmp_path, name):
+    c, actions, check = SCENARIOS[name]()
+    p = _write(c, tmp_path, name)
+    recs = oracle_mod.ref_allocate(p, actions=actions).as_list()
+    check(recs, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(SCENARIOS))
+def test_e2e_scenario_gpu(engine, oracle_mod, tmp_path, name):
+    c, actions, check = SCENARIOS[name]()
+    p = _write(c, tmp_path, name)
+    exp = oracle_mod.ref_allocate(p, actions=actions).as_list()
+    with engine.Session(p) as s:
+        pod, node, kind = s.run_actions(actions)
+    got = [(int(a), int(b), KIND_CODE[int(k)]) for a, b, k in zip(pod, node, kind)]
+    assert got == exp
+    check(got, c)

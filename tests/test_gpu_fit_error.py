@@ -81,3 +81,16 @@ def test_fit_error_known_answer_gpu(engine, kbgen_mod, tmp_path):
     for opts in PATHS:
         got, _ = _engine_close(engine, p, **opts)
         assert got == {"ns/g": "1/5 tasks in gang unschedulable: 0/2 nodes are available, 2 insufficient cpu."}, opts
+
+
+@pytest.mark.gpu
+def test_gang_close_backfilled_gpu(engine, oracle_mod, tmp_path):
+    """The PodGroupBackfilled case (gang.go:189-199) on every device path."""
+    from test_oracle import _backfill_gang_cluster
+    p = str(tmp_path / "bf.kbs")
+    _backfill_gang_cluster().write(p)
+    exp = oracle_mod.ref_gang_close(p)
+    assert exp["ns/g"] == "Backfilled"
+    for opts in PATHS:
+        got, _ = _engine_close(engine, p, **opts)
+        assert got == exp, opts

@@ -110,3 +110,32 @@ def test_gang_close_fit_error_known_answer(tmp_path):
     p2 = str(tmp_path / "ka2.kbs")
     c2.write(p2)
     assert oracle.ref_gang_close(p2) == {"ns/g": "1/1 tasks in gang unschedulable: 0 nodes are available"}
+
+
+def _backfill_gang_cluster():
+    """A gang of 3 pods (minMember 3) on one 2-CPU node: two fit, the third
+    does not, so the job stays not Ready.  One of its pods carries the backfill
+    annotation (TaskInfo.IsBackfill)."""
+    import kbgen
+    c = kbgen.Cluster()
+    c.add_queue("default", 1)
+    c.add_node("n0", 2000, 4 * kbgen.GI, 0)
+    c.add_job("ns", "g", "default", min_member=3)
+    for k in range(3):
+        c.add_pod("ns", f"g-{k}", uid=f"u{k}", group="g", containers=[kbgen.res(1000, kbgen.GI)], backfill=k == 2)
+    c.add_job("ns", "h", "default", min_member=2)
+    for k in range(2):
+        c.add_pod("ns", f"h-{k}", uid=f"v{k}", group="h", containers=[kbgen.res(4000, kbgen.GI)])
+    return c
+
+
+def test_gang_close_backfilled_known_answer(tmp_path):
+    """gang.go:189-199: a not-Ready job with an IsBackfill task gets the
+    PodGroupBackfilled condition (no message) instead of Unschedulable; the
+    other not-Ready job keeps its FitError message."""
+    import oracle
+    p = str(tmp_path / "bf.kbs")
+    _backfill_gang_cluster().write(p)
+    got = oracle.ref_gang_close(p)
+    assert got["ns/g"] == "Backfilled"
+    assert got["ns/h"].startswith("2/2 tasks in gang unschedulable: 0/1 nodes are available")
