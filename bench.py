@@ -61,9 +61,10 @@ def parse():
     ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2, 3),
                     help="k > 0: batched pops rotate over k + 1 streams, up to k beside each other "
                          "(device-side chaining); 0 = one pop kernel at a time")
-    ap.add_argument("--mode", choices=("replicas", "shard"), default="replicas",
-                    help="N>1: independent sessions per GPU (replicas) or one session node-sharded over the GPUs "
-                         "(per-task RCCL all-reduce of the selection key, SURVEY.md §8e)")
+    ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
+                    help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
+                         "each shard sweeps its node range to its top-64, one RCCL all-gather, identical placement "
+                         "on every shard), or N independent replica sessions")
     return ap.parse_args()
 
 

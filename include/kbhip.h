@@ -90,6 +90,7 @@ typedef struct kbhip_stats {
     double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
     int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
     int64_t fit_inexact;     /* jobs whose FitError histogram was not computed (shards, pod-affinity fallback) */
+    int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -213,23 +214,33 @@ int kbhip_session_close(kb_session* s);
 
 /* Node-array sharding (one process per GPU).  A shard session
  * holds the whole host model but only nodes [lo, hi) of the snapshot on its
- * device, lo = N*rank/world, hi = N*(rank+1)/world; per-task sweeps reduce
- * the 8-byte selection key (and the inter-pod affinity min/max) across
- * shards; every shard then applies the same decision (the owner updates the
- * node row).  Placements equal the one-GPU session's.  Connect with RCCL
- * (kbhip_rccl_unique_id on one rank, shared out of band, then
- * kbhip_shard_connect_rccl on every rank, collectively) or with a host
- * callback performing the all-reduce (e.g. torch.distributed over gloo). */
+ * device, lo = N*rank/world, hi = N*(rank+1)/world (world <= 16).  Every rank
+ * runs the same host loop; placements equal the one-GPU session's.
+ *   Batched pops (the common case): each shard sweeps its range to its top-64
+ *   candidates with their rows; ONE all-gather per pop exchanges them; every
+ *   shard runs the identical chunk placement on the merged list (the global
+ *   top-64) and writes back the rows it owns.
+ *   Per-task pops (pod-affinity classes, Backfilled nodes): the 8-byte
+ *   selection key (and the inter-pod affinity min/max) is all-reduced per task.
+ * Connect with RCCL (kbhip_rccl_unique_id on one rank, shared out of band, then
+ * kbhip_shard_connect_rccl on every rank, collectively: all-gather and
+ * all-reduce on the session stream) or with host callbacks (e.g.
+ * torch.distributed over gloo): kbhip_shard_connect_host for the all-reduce
+ * and kbhip_shard_connect_host_gather for the all-gather; without the latter
+ * every pop takes the per-task path. */
 #define KBHIP_RED_MAX_U64 0
 #define KBHIP_RED_MIN_I64 1
 #define KBHIP_RED_MAX_I64 2
 typedef int (*kbhip_allreduce_fn)(void* ctx, uint64_t* vals, int32_t n, int32_t op);
+/* recv <- the `bytes` sent by every rank, concatenated in rank order */
+typedef int (*kbhip_allgather_fn)(void* ctx, const void* send, void* recv, int64_t bytes);
 int kbhip_session_open_shard(const void* kbs_bytes, size_t len, int device, int32_t rank, int32_t world,
                              kb_session** out);
 int kbhip_shard_info(kb_session* s, int32_t* out_rank_world_lo_hi);
 int kbhip_rccl_unique_id(void* out, int64_t cap);
 int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len);
 int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
+int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx);
 
 /* Test support (not part of the placement path): encode a snapshot without a
  * device and read the compiled host tables back by name.  Tables (int32):

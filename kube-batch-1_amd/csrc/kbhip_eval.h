@@ -24,6 +24,22 @@ struct Row {  // the dynamic part of a node's state
     int32_t pods, maxtasks;
 };
 
+// Node-array shards, batched pops: what each shard contributes
+// to a pop — its top-64 keys with the rows the placement needs — exchanged by
+// one all-gather; every shard then places the chunk on the merged list.
+struct ShardCand {
+    uint64_t key;    // 64-bit selection key (global node index), 0 = none
+    int32_t node;    // global node index, -1 = none
+    int32_t na;      // static node-affinity weight of the node for the class
+    Row row;
+    uint64_t pw[4];  // host-port words
+};
+struct ShardMsg {
+    uint32_t fit[4];  // the shard's sweep FitDelta counts (walk nodes, cpu, memory, GPU)
+    uint32_t pad[2];
+    ShardCand c[kTopK];
+};
+
 KBHIP_HD Row load_row(const NodeCols& nc, int n) {
     Row r;
     r.idle_cpu = nc.idle_cpu[n]; r.idle_mem = nc.idle_mem[n]; r.idle_gpu = nc.idle_gpu[n];

@@ -55,12 +55,20 @@ struct KeyFormat {
     bool ent32 = false;  // parallel-levels placement entries fit 32 bits too
     int32_t base = 0, shift = 0, idxmax = 0;
 };
+struct ShardMsg;  // kbhip_eval.h
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
+// placement 3 (node-array shards): no placement; the shard's top-64 with rows
+// goes to shard_out for the all-gather, then launch_shard_place places.
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
-                            int fit_set);
+                            int fit_set, ShardMsg* shard_out = nullptr);
+// The placement of a sharded batched pop on the gathered ShardMsgs (world of
+// them, rank order): identical on every shard; each writes back its own rows.
+hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                              int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node

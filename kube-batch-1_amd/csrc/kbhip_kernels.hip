@@ -714,7 +714,10 @@ template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
-                               uint32_t fit_raw = 0) {
+                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff) {
+    // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
+    // (a node-array shard writes back only its own; one GPU: all of them).
+    // Node indices in keys and entries are global.
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -878,26 +881,27 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (n >= 0 && cc > 0) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
+    const int ln = n - wb_base;  // local row of the written-back node
+    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
         const int ap = s_apos[lane];
         const int na = cc < ap ? cc : ap;
         const Row r = apply_commits(base, c, na, cc - na);
         if constexpr (SC1) {
-            st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
-            st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
-            st_sc1(&nc.pods[n], r.pods);
-            st_sc1(&nc.nzc[n], r.nzc);
-            st_sc1(&nc.nzm[n], r.nzm);
+            st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
+            st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
+            st_sc1(&nc.pods[ln], r.pods);
+            st_sc1(&nc.nzc[ln], r.nzc);
+            st_sc1(&nc.nzm[ln], r.nzm);
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + n], pwc[w]);
+                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
         } else {
-            nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
-            nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
-            nc.pods[n] = r.pods;
-            nc.nzc[n] = r.nzc;
-            nc.nzm[n] = r.nzm;
+            nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
+            nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
+            nc.pods[ln] = r.pods;
+            nc.nzc[ln] = r.nzc;
+            nc.nzm[ln] = r.nzm;
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
         }
     }
     if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
@@ -911,9 +915,32 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
 }
 
 
+// The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
+// writes this shard's top-64 with their rows and the sweep's FitDelta counts.
+__device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
+                           uint32_t fit_raw, ShardMsg* msg) {
+    const int lane = threadIdx.x & 63;
+    ShardCand e{};
+    e.node = -1;
+    if (K) {
+        const int g = key_idx(K);
+        const int n = g - nc.base;
+        e.key = K;
+        e.node = g;
+        e.row = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) e.pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+    }
+    msg->c[lane] = e;
+    const uint32_t sweep = fit_sum(fit_raw);
+    if (lane < 4) msg->fit[lane] = sweep;
+}
+
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                           uint64_t* cand64, uint32_t* arrive, PopOut* out) {
+                                                           uint64_t* cand64, uint32_t* arrive, PopOut* out,
+                                                           ShardMsg* smsg) {
     __shared__ KT wlk[kPopThreads / 64][64];  // sweep / merge lists in the key type
     __shared__ uint64_t wl64[sizeof(KT) == 8 ? 1 : kPopThreads / 64][64];
     uint64_t (*wl)[64] = nullptr;             // placement lists (64-bit keys / entries)
@@ -1016,6 +1043,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     __syncthreads();
+    if (a.placement == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
+        if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg);
+        return;
+    }
     if (a.placement == 1) {  // uniform
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
@@ -1427,7 +1458,8 @@ __global__ __launch_bounds__(64) void k_undo_pop(NodeCols nc, DevTables t, UndoA
     if (threadIdx.x != 0) return;
     const TaskClass c = t.classes[u.cls];
     for (int i = 0; i < u.n; ++i)
-        if (u.node[i] >= 0) uncommit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+        if (u.node[i] - nc.base >= 0 && u.node[i] - nc.base < nc.n)  // this shard's rows only
+            uncommit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
 }
 
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
@@ -1444,7 +1476,8 @@ __global__ __launch_bounds__(64) void k_redo_pop(NodeCols nc, DevTables t, UndoA
     if (threadIdx.x != 0) return;
     const TaskClass c = t.classes[u.cls];
     for (int i = 0; i < u.n; ++i)
-        if (u.node[i] >= 0) commit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+        if (u.node[i] - nc.base >= 0 && u.node[i] - nc.base < nc.n)
+            commit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
 }
 
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
@@ -1529,27 +1562,100 @@ int pop_blocks(int n_nodes, int* R_out) {
 
 template <typename KT>
 static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
-                               uint64_t* cand, uint32_t* arrive, PopOut* o, hipStream_t st) {
+                               uint64_t* cand, uint32_t* arrive, PopOut* o, ShardMsg* m, hipStream_t st) {
+#define KBHIP_PB(RR) \
+    hipLaunchKernelGGL((k_pop_batch<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, m)
     switch (R) {
-        case 1: hipLaunchKernelGGL((k_pop_batch<1, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 2: hipLaunchKernelGGL((k_pop_batch<2, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 4: hipLaunchKernelGGL((k_pop_batch<4, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        case 8: hipLaunchKernelGGL((k_pop_batch<8, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
-        default: hipLaunchKernelGGL((k_pop_batch<16, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o); break;
+        case 1: KBHIP_PB(1); break;
+        case 2: KBHIP_PB(2); break;
+        case 4: KBHIP_PB(4); break;
+        case 8: KBHIP_PB(8); break;
+        default: KBHIP_PB(16); break;
     }
+#undef KBHIP_PB
 }
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
-                            int fit_set) {
+                            int fit_set, ShardMsg* shard_out) {
+    if (placement == 3 && !shard_out) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
-    else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, st);
+    if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, st);
+    else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, st);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Node-array shards, batched pops: after the all-gather of
+// every shard's ShardMsg, each shard runs this identical placement on the
+// merged list — the global top-64, since every shard's list holds its own
+// top-64 — and writes back the rows it owns.  One workgroup.
+// ---------------------------------------------------------------------------
+constexpr int kShardHash = 2048;  // node -> (rank, slot) of the gathered candidates (<= 16 ranks x 64)
+__global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols nc, DevTables t, PopArgs a,
+                                                             const ShardMsg* msgs, int world, PopOut* out) {
+    __shared__ uint64_t wl[kPopThreads / 64][64];
+    __shared__ RowCache rc;
+    __shared__ int32_t s_hk[kShardHash];
+    __shared__ int16_t s_hv[kShardHash];
+    __shared__ int32_t s_fitin[4];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const TaskClass c = t.classes[a.cls];
+    for (int i = threadIdx.x; i < kShardHash; i += kPopThreads) s_hk[i] = -1;
+    for (int i = threadIdx.x; i < kHash; i += kPopThreads) rc.hkey[i] = -1;
+    if (threadIdx.x < 4) {
+        uint32_t f = 0;
+        for (int r = 0; r < world; ++r) f += msgs[r].fit[threadIdx.x];
+        s_fitin[threadIdx.x] = (int32_t)f;
+    }
+    __syncthreads();
+    // every gathered candidate into the node -> entry table; lists merged by waves
+    uint64_t acc = 0;
+    for (int r = wave; r < world; r += kPopThreads / 64) {
+        const ShardCand& e = msgs[r].c[lane];
+        if (e.node >= 0) {
+            int h = (int)(((uint32_t)e.node * 2654435761u) >> 21);
+            while (atomicCAS(&s_hk[h], -1, e.node) != -1) h = (h + 1) & (kShardHash - 1);
+            s_hv[h] = (int16_t)(r * 64 + lane);
+        }
+        acc = wave_merge_desc(acc, e.key);
+    }
+    wl[wave][lane] = acc;
+    __syncthreads();
+    block_tree_merge(wl, wave, lane);  // wl[0]: the global top-64 keys
+    if (wave == 0) {  // their rows into the row cache (slot = lane)
+        const uint64_t K = wl[0][lane];
+        if (K) {
+            const int g = key_idx(K);
+            int h = (int)(((uint32_t)g * 2654435761u) >> 21);
+            while (s_hk[h] != g) h = (h + 1) & (kShardHash - 1);
+            const int src = s_hv[h];
+            const ShardCand& e = msgs[src >> 6].c[src & 63];
+            rc.row[lane] = e.row;
+            for (int w = 0; w < 4; ++w) rc.pw[lane][w] = e.pw[w];
+            rc.na[lane] = e.na;
+            rc_insert(&rc, g, lane);
+        }
+    }
+    __syncthreads();
+    NodeCols ncg = nc;  // keys / entries carry global node indices
+    ncg.base = 0;
+    if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+    else place_parallel<uint64_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+}
+
+hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                              int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st) {
+    if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
+              kf.use32 && kf.ent32 ? 1 : 0, 0};
+    hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev);
     return hipGetLastError();
 }
 

@@ -416,6 +416,12 @@ struct Session {
     ncclComm_t comm = nullptr;                 // RCCL exchange (one GPU per rank)
     kbhip_allreduce_fn xfn = nullptr;          // or a host-side exchange callback
     void* xctx = nullptr;
+    kbhip_allgather_fn xgfn = nullptr;         // host all-gather (batched pops of a shard session)
+    void* xgctx = nullptr;
+    DevBuf b_shard_send, b_shard_recv;         // this shard's ShardMsg / all of them (rank order)
+    ShardMsg* d_shard_send = nullptr;
+    ShardMsg* d_shard_recv = nullptr;
+    vector<uint8_t> h_shard;                   // host staging of the host all-gather
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
     bool encode_only = false;
     vector<int32_t> h_dom, h_aff_cnt, h_aff_scalar, h_aff_items;
@@ -448,7 +454,8 @@ struct Session {
         for (auto& b : b_cols) b.release();
         for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
-                          &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt})
+                          &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt,
+                          &b_shard_send, &b_shard_recv})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -528,7 +535,7 @@ struct PortRuns {
 
 static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
                          int world = 1) {
-    if (world < 1 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world");
+    if (world < 1 || world > 16 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world (1..16)");
     S.rank = rank;
     S.world = world;
     S.encode_only = encode_only;
@@ -1300,8 +1307,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     // lr, bra in [0, 10] and na between the sums of its negative / positive
     // preferred-term weights; it fits when (range + 1) < 2^(31 - index bits).
     {
-        int ibits = 1;
-        while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)nl) ++ibits;
+        int ibits = 1;  // keys carry global node indices (shards too)
+        while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)N) ++ibits;
         S.class_kf.assign(S.classes.size(), KeyFormat{});
         for (size_t ci = 0; ci < S.classes.size(); ++ci) {
             const TaskClass& c = S.classes[ci];
@@ -1359,6 +1366,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.d_arrive = S.b_arrive.alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         S.d_fit4 = S.b_fit4.alloc<int32_t>(4);
+        if (S.world > 1) {
+            S.d_shard_send = S.b_shard_send.alloc<ShardMsg>(1);
+            S.d_shard_recv = S.b_shard_recv.alloc<ShardMsg>(S.world);
+        }
         for (int k = 0; k <= kMaxDep; ++k) {
             S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
             S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
@@ -1397,6 +1408,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 // ---------------------------------------------------------------------------
 static void exchange(Session& S, void* dev, int op) {
     if (S.world == 1) return;
+    S.stats.collectives++;
     if (S.comm) {
         const ncclDataType_t dt = op == KBHIP_RED_MAX_U64 ? ncclUint64 : ncclInt64;
         const ncclRedOp_t ro = op == KBHIP_RED_MIN_I64 ? ncclMin : ncclMax;
@@ -1411,6 +1423,28 @@ static void exchange(Session& S, void* dev, int op) {
     if (S.xfn(S.xctx, &v, 1, op) != 0) throw Error(KBHIP_EDEVICE, "shard exchange callback failed");
     HIPCHK(hipMemcpyAsync(dev, &v, 8, hipMemcpyHostToDevice, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
+}
+
+// The all-gather of a batched pop on a node-array shard: every rank's
+// ShardMsg into d_shard_recv in rank order.  RCCL on the session stream (no
+// host synchronisation), or the host callback around two copies.
+static void shard_gather(Session& S) {
+    const size_t bytes = sizeof(ShardMsg);
+    S.stats.collectives++;
+    if (S.comm) {
+        const ncclResult_t r = ncclAllGather(S.d_shard_send, S.d_shard_recv, bytes, ncclUint8, S.comm, S.stream);
+        if (r != ncclSuccess) throw Error(KBHIP_EDEVICE, string("ncclAllGather: ") + ncclGetErrorString(r));
+        return;
+    }
+    if (!S.xgfn) throw Error(KBHIP_EINVAL, "sharded session has no all-gather (kbhip_shard_connect_*)");
+    S.h_shard.resize(bytes * (S.world + 1));
+    uint8_t* send = S.h_shard.data() + bytes * S.world;
+    HIPCHK(hipMemcpyAsync(send, S.d_shard_send, bytes, hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    if (S.xgfn(S.xgctx, send, S.h_shard.data(), (int64_t)bytes) != 0)
+        throw Error(KBHIP_EDEVICE, "shard all-gather callback failed");
+    HIPCHK(hipMemcpyAsync(S.d_shard_recv, S.h_shard.data(), bytes * S.world, hipMemcpyHostToDevice, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));  // the staging buffer is reused by the next pop
 }
 
 // One task of the per-task path: [IPA min/max prepass + exchange], sweep,
@@ -1469,8 +1503,8 @@ static bool has_aff_classes(const Session& S) {
 
 static bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
-    return S.batched && S.world == 1 && !S.any_bf && !c.backfill && !c.aff && S.nc.port_words <= 4 &&
-           S.nc.n < (1 << 25);
+    return S.batched && (S.world == 1 || S.comm || S.xgfn) && !S.any_bf && !c.backfill && !c.aff &&
+           S.nc.port_words <= 4 && S.n_total < (1 << 25);
 }
 
 static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
@@ -1489,7 +1523,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     S.sweep_launches++;
     hipEvent_t* ev = S.evb[L.slot];
     if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
-    const bool ov = S.overlap > 0 && S.placement == 2;
+    const bool ov = S.overlap > 0 && S.placement == 2 && S.world == 1;
     if (!ov) ov_quiesce(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
@@ -1499,7 +1533,14 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
     const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
-    if (ov) {
+    if (S.world > 1) {  // node-array shard: sweep -> all-gather of the shards' lists -> identical placement
+        HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
+                                S.d_arrive, out, S.stream, 3, kf, S.fit_set[kMaxDep + 1], S.d_shard_send));
+        S.fit_set[kMaxDep + 1] ^= 1;
+        shard_gather(S);
+        HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
+                                  S.d_shard_recv, S.world, out, S.stream));
+    } else if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
                                    S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap,
                                    S.fit_set[si]));
@@ -3264,6 +3305,14 @@ int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx) {
         if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         s->s.xfn = fn;
         s->s.xctx = ctx;
+        return KBHIP_OK;
+    })
+}
+int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx) {
+    ABI_GUARD({
+        if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        s->s.xgfn = fn;
+        s->s.xgctx = ctx;
         return KBHIP_OK;
     })
 }

@@ -27,11 +27,12 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
-           "kbhip_first_fit", "kbhip_sweep_scores")
+           "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
                                 ctypes.c_int32)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
 
 
 class KbhipError(RuntimeError):
@@ -45,7 +46,7 @@ class Stats(ctypes.Structure):
                 ("timed_launches", ctypes.c_int64), ("host_launch_s", ctypes.c_double),
                 ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
-                ("fit_inexact", ctypes.c_int64)]
+                ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -84,6 +85,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_rccl_unique_id.argtypes = [vp, i64]
         L.kbhip_shard_connect_rccl.argtypes = [vp, vp, i64]
         L.kbhip_shard_connect_host.argtypes = [vp, ALLREDUCE_FN, vp]
+        L.kbhip_shard_connect_host_gather.argtypes = [vp, ALLGATHER_FN, vp]
         L.kbhip_read_nodes.argtypes = [vp, vp, i64]
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
@@ -326,6 +328,21 @@ def shard_range(n_nodes: int, rank: int, world: int) -> Tuple[int, int]:
     return n_nodes * rank // world, n_nodes * (rank + 1) // world
 
 
+def torch_gather(group=None):
+    """An all-gather callback for kbhip_shard_connect_host_gather over
+    torch.distributed (any backend; gloo runs on CPU): recv <- every rank's
+    `send` bytes in rank order."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(send: np.ndarray, recv: np.ndarray) -> None:
+        world = dist.get_world_size(group)
+        out = [torch.empty(send.size, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(out, torch.from_numpy(send.copy()), group=group)
+        recv[:] = torch.cat(out).numpy()
+    return fn
+
+
 def torch_exchange(group=None):
     """An exchange callback for kbhip_shard_connect_host doing the all-reduce
     with torch.distributed (any backend; gloo runs on CPU).  u64 keys are
@@ -377,8 +394,11 @@ class ShardedSession(Session):
         b = ctypes.create_string_buffer(unique_id, len(unique_id))
         _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
 
-    def connect_host(self, fn) -> None:
-        """fn(vals: np.ndarray[uint64], op) reduces vals in place across ranks."""
+    def connect_host(self, fn, gather=None) -> None:
+        """fn(vals: np.ndarray[uint64], op) reduces vals in place across ranks
+        (per-task pops); gather(send: np.ndarray[uint8], recv) fills recv with
+        every rank's send bytes in rank order (batched pops; without it every
+        pop takes the per-task path)."""
         def cb(_ctx, vals, n, op):
             try:
                 fn(np.ctypeslib.as_array(vals, shape=(n,)), op)
@@ -387,3 +407,17 @@ class ShardedSession(Session):
                 return 1
         self._cb = ALLREDUCE_FN(cb)  # keep the trampoline alive
         _check(lib().kbhip_shard_connect_host(self._h, self._cb, None))
+        if gather is not None:
+            world = self.info()[1]
+
+            def gcb(_ctx, send, recv, nbytes):
+                try:
+                    s_arr = np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+                    r_arr = np.ctypeslib.as_array(ctypes.cast(recv, ctypes.POINTER(ctypes.c_uint8)),
+                                                  shape=(nbytes * world,))
+                    gather(s_arr, r_arr)
+                    return 0
+                except Exception:
+                    return 1
+            self._gcb = ALLGATHER_FN(gcb)
+            _check(lib().kbhip_shard_connect_host_gather(self._h, self._gcb, None))

@@ -39,6 +39,12 @@ def main():
         v = np.array([x], dtype=np.int64).view(np.uint64)
         fn(v, kbhip.RED_MAX_I64)
         res["max_i64"].append(int(v.view(np.int64)[0]))
+    # all-gather of a per-rank byte record (the batched shard path's ShardMsg exchange)
+    g = kbhip.torch_gather()
+    send = (np.arange(40, dtype=np.uint8) * (rank + 1)).astype(np.uint8)
+    recv = np.zeros(40 * world, dtype=np.uint8)
+    g(send, recv)
+    res["gather"] = [int(x) for x in recv]
     dist.destroy_process_group()
     with open(out, "w") as f:
         json.dump(res, f)

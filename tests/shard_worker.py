@@ -2,7 +2,8 @@
 of the snapshot on GPU 0 (ranks share the card), exchanges over gloo, runs the
 given actions and writes the placement log as JSON.
 
-usage: shard_worker.py <snapshot> <rank> <world> <init_file> <out.json> <actions>
+usage: shard_worker.py <snapshot> <rank> <world> <init_file> <out.json> <actions> [batched]
+(batched 1, default: the per-pop all-gather path is connected; 0: per-task only)
 """
 import json
 import os
@@ -14,18 +15,21 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 
 def main():
     path, rank, world, init_file, out, actions = sys.argv[1:7]
+    batched = int(sys.argv[7]) if len(sys.argv) > 7 else 1
     rank, world = int(rank), int(world)
     import torch.distributed as dist
     import kbhip
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     with kbhip.ShardedSession(path, 0, rank, world) as s:
-        s.connect_host(kbhip.torch_exchange())
+        s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched else None)
         info = s.info()
         pod, node, kind = s.run_actions(actions)
+        st = s.stats()
     dist.barrier()
     dist.destroy_process_group()
     with open(out, "w") as f:
-        json.dump({"info": info, "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)]}, f)
+        json.dump({"info": info, "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)],
+                   "batched_pops": st["batched_pops"], "sweeps": st["sweeps"], "collectives": st["collectives"]}, f)
 
 
 if __name__ == "__main__":

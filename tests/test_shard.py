@@ -47,6 +47,8 @@ def test_exchange_gloo(world, tmp_path):
         assert res[r]["max_u64"] == [int(x) for x in keys.max(axis=0)]
         assert res[r]["min_i64"] == [int(x) for x in ints.min(axis=0)]
         assert res[r]["max_i64"] == [int(x) for x in ints.max(axis=0)]
+        exp = np.concatenate([(np.arange(40, dtype=np.uint8) * (q + 1)).astype(np.uint8) for q in range(world)])
+        assert res[r]["gather"] == [int(x) for x in exp]
 
 
 def test_shard_ranges_partition(engine_lib):
@@ -59,12 +61,13 @@ def test_shard_ranges_partition(engine_lib):
             assert all(hi - lo in (n // world, n // world + 1) for lo, hi in rs)
 
 
-def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate"):
+def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, exp=None):
     p = str(tmp_path / "s.kbs")
     c.write(p)
-    exp = oracle_mod.ref_allocate(p, actions=actions).as_list()
+    if exp is None:
+        exp = oracle_mod.ref_allocate(p, actions=actions).as_list()
     res = _run_ranks("shard_worker.py", world, tmp_path,
-                     lambda r, init, out: [p, str(r), str(world), init, out, actions], timeout=600)
+                     lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=600)
     n_nodes = len(c.nodes)
     import kbhip
     for r in range(world):
@@ -72,17 +75,71 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate"):
         assert res[r]["info"] == [r, world, lo, hi]
         got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
         assert got == exp, f"rank {r}"
+    return res
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(6))
-def test_sharded_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """2 or 3 ranks on one GPU, every feature (pod affinity, backfill, ports...)."""
+@pytest.mark.parametrize("batched", [1, 0])
+def test_sharded_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, batched):
+    """2 or 3 ranks on one GPU, every feature (pod affinity, backfill, ports...);
+    batched 1: per-pop all-gather path where the class allows it, 0: per-task only."""
     c = kbgen_mod.gen_random(2200 + seed, n_nodes=6 + seed * 3, n_jobs=6, max_tasks=5, best_effort_p=0.2)
-    _shard_case(oracle_mod, tmp_path, c, 2 + seed % 2, actions="allocate, backfill")
+    _shard_case(oracle_mod, tmp_path, c, 2 + seed % 2, actions="allocate, backfill", batched=batched)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Batched-path features only (no pod affinity / backfill): every pop is one all-gather."""
+    from test_gpu_parity import NO_POD_AFFINITY
+    feats = tuple(f for f in NO_POD_AFFINITY if f != "backfill")
+    c = kbgen_mod.gen_random(2400 + seed, n_nodes=10 + seed * 7, n_jobs=8, max_tasks=8, features=feats,
+                             tiers=[["priority", "gang", "conformance"], ["drf", "predicates", "proportion",
+                                                                           "nodeorder"]])
+    res = _shard_case(oracle_mod, tmp_path, c, 2 + seed % 3)
+    assert all(r["batched_pops"] > 0 for r in res)
+
+
+@pytest.mark.gpu
+def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
+    """C4 shape at 20k nodes (2 and 3 ranks sharing the GPU over gloo): the
+    shard logs equal the one-GPU session's, and every batched pop is exactly
+    one collective (one all-gather)."""
+    p = str(tmp_path / "c4s.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=60000)
+    with engine.Session(p) as s:
+        pod, node, kind = s.allocate(cap=1 << 20)
+        st1 = s.stats()
+    exp = [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)]
+    assert st1["batched_pops"] == st1["sweeps"] > 1000
+    for world in (2, 3):
+        res = _run_ranks("shard_worker.py", world, tmp_path,
+                         lambda r, init, out: [p, str(r), str(world), init, out, "allocate", "1"], timeout=900)
+        for r in range(world):
+            got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
+            assert got == exp, f"world {world} rank {r}"
+            assert res[r]["batched_pops"] == st1["batched_pops"]
+            assert res[r]["collectives"] == res[r]["batched_pops"]  # one all-gather per pop, nothing else
 
 
 @pytest.mark.gpu
 def test_sharded_c3_small_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     c = kbgen_mod.gen_c3(n_nodes=90, n_pending=400)
     _shard_case(oracle_mod, tmp_path, c, 2)
+
+
+@pytest.mark.gpu
+def test_sharded_rccl_two_devices(engine, oracle_mod, kbgen_mod, tmp_path):
+    """The RCCL exchange (ncclAllGather / ncclAllReduce on the session stream):
+    two ranks on two devices.  Skipped on a one-GPU box (RCCL does not run two
+    ranks on one device)."""
+    if engine.device_count() < 2:
+        pytest.skip("needs two gfx950 devices")
+    c = kbgen_mod.gen_random(2600, n_nodes=40, n_jobs=10, max_tasks=8, best_effort_p=0.2)
+    p = str(tmp_path / "r.kbs")
+    c.write(p)
+    exp = oracle_mod.ref_allocate(p, actions="allocate, backfill").as_list()
+    res = _run_ranks("rccl_worker.py", 2, tmp_path, lambda r, init, out: [p, str(r), "2", init, out], timeout=300)
+    for r in range(2):
+        assert [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]] == exp
