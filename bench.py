@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--time-every", type=int, default=0,
                     help="also HIP-event time every k-th sweep launch (0 = off; per-launch events stall the "
                          "overlapped pipeline, so the roofline uses each session's device span instead)")
-    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2),
-                    help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels")
+    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2, 4),
+                    help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels, "
+                         "4 insertion (one wave)")
     ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
                     help="predicted job pops queued ahead of the running one")
     ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2, 3),

@@ -915,6 +915,165 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
 }
 
 
+// ---------------------------------------------------------------------------
+// Placement by insertion (option "placement" = 4): one wave, no sort
+// networks.  The greedy order is the descending order of the entries
+// e(j, d) = (running min of node j's scores over depths 0..d, index, depth)
+// (see place_levels).  The depth-0 entries are the sorted candidate list
+// itself; a node's entries decrease with depth, so the top-m entries hold a
+// prefix of each node's sequence.  Rounds: every lane whose newest entry is
+// still among the top m evaluates its next depth (its own row, its own
+// Allocate^a Pipeline^p chain, no fix-ups); new entries above the m-th are
+// inserted into the sorted list one at a time (a ballot gives the position,
+// a DPP wave shift moves the tail).  A round that inserts nothing ends it —
+// typically after one or two rounds, as a commit lowers a node's score.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v) {  // lane i <- lane i - 1 (lane 0 <- 0)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+// L sorted descending over the lanes, e not in L: L with e inserted (the last entry drops off).
+__device__ __forceinline__ uint64_t wave_insert_desc(uint64_t L, uint64_t e) {
+    const int lane = threadIdx.x & 63;
+    const int pos = __popcll(__ballot(L > e));
+    const uint64_t sh = wave_shr1_64(L);
+    return lane < pos ? L : (lane == pos ? e : sh);
+}
+
+template <bool SC1 = false>
+__device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                             const PopArgs& a, PopOut* out, uint64_t K, uint32_t* done_flag = nullptr,
+                             uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
+                             uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;  // global node index (keys are global)
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
+    if (rslot >= 0) {
+        base = rc->row[rslot];
+        for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
+        na_n = rc->na[rslot];
+    } else if (n >= 0) {
+        base = load_row_t<SC1>(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    uint64_t pwc[4];  // ports after one or more commits of this class
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    // this lane's chain: depth d of its newest entry, commits by kind behind it, first Pipeline depth
+    int d = 0, ca = 0, cp = 0, apos = 64;
+    uint64_t key = K;  // key at depth d (its kind is the kind of commit d + 1)
+    int32_t rm = K ? key_score(K) : 0;
+    uint64_t last = K ? level_entry(rm, n, 0, K) : 0;  // newest entry
+    uint64_t L = last;  // lane p: entry p of the sorted top entries (depth-0 entries are the sorted list)
+    uint64_t T = readlane64(L, m - 1);
+    for (int round = 1; round < 64; ++round) {
+        const bool act = last != 0 && last >= T;  // its newest entry is among the top m
+        if (!__ballot(act)) break;
+        uint64_t e = 0;
+        if (act) {
+            if (key & 1) { ++cp; if (apos == 64) apos = d; } else ++ca;  // commit d + 1 takes the depth-d kind
+            ++d;
+            const Row r = apply_commits(base, c, ca, cp);
+            int32_t s;
+            bool passed;
+            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+            if (key) {
+                rm = key_score(key) < rm ? key_score(key) : rm;
+                e = level_entry(rm, n, d, key);
+            }
+            last = e;
+        }
+        // insert the new entries that beat the m-th (T only rises: one below it never enters)
+        for (uint64_t q = __ballot(e != 0 && e > T); q; q &= q - 1) {
+            const uint64_t x = readlane64(e, __ffsll((unsigned long long)q) - 1);
+            if (x > T) {
+                L = wave_insert_desc(L, x);
+                T = readlane64(L, m - 1);
+            }
+        }
+    }
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const bool inm = lane < m && L != 0;
+    const int kind = inm ? entry_kind(L) : 0;
+    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
+    int done, stop;
+    if (smask) {
+        const int p = __ffsll((unsigned long long)smask) - 1;
+        done = p + 1;
+        stop = __builtin_amdgcn_readlane((int)inm, p) ? 2 : 1;
+    } else {
+        done = m;
+        stop = 0;
+    }
+    // commits of this lane's node among the placed entries
+    int cc = 0;
+    for (int p = 0; p < done; ++p) {
+        const uint64_t x = readlane64(L, p);
+        cc += (x != 0 && entry_idx(x) == n) ? 1 : 0;
+    }
+    const int nal = cc < apos ? cc : apos;  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
+    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
+        uint32_t fb_base = 0, fb_post = 0;
+        if (n >= 0) {
+            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
+            const Row r = apply_commits(base, c, nal, cc - nal);
+            int32_t sc;
+            bool passed;
+            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
+            fb_post = fit_bits(c, r, passed);
+        }
+        const uint32_t sweep = fit_sum(fit_raw);
+        int32_t tot[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+        if (lane == 0) {
+            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const int ln = n - wb_base;
+    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {
+        const Row r = apply_commits(base, c, nal, cc - nal);
+        if constexpr (SC1) {
+            st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
+            st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
+            st_sc1(&nc.pods[ln], r.pods);
+            st_sc1(&nc.nzc[ln], r.nzc);
+            st_sc1(&nc.nzm[ln], r.nzm);
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
+        } else {
+            nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
+            nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
+            nc.pods[ln] = r.pods;
+            nc.nzc[ln] = r.nzc;
+            nc.nzm[ln] = r.nzm;
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
+        }
+    }
+    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_sc1(done_flag, seq);
+    }
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_idx(L) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
 // writes this shard's top-64 with their rows and the sweep's FitDelta counts.
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
@@ -1051,6 +1210,13 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
         place_levels(cf, nc, t, c, a, wl[0][lane], out);
+        return;
+    }
+    if (a.placement == 4) {  // uniform
+        if (wave != 0) return;
+        STAMP(gridDim.x * 4 + 1);
+        place_insert<false>(cf, nc, t, c, a, out, wl[0][lane], nullptr, 0, nullptr, s_fitin, fit_raw);
+        STAMP(gridDim.x * 4 + 3);
         return;
     }
     if (a.placement == 2) {  // uniform; every wave takes part
@@ -1420,7 +1586,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
-    if (ok) {
+    if (ok && a.placement == 4) {
+        if (wave == 0) place_insert<true>(cf, nc, t, c, a, out, wl[0][lane], &link->done, seq, &rc, s_fitin, fit_raw);
+    } else if (ok) {
         if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
         else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
@@ -1645,15 +1813,17 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
     __syncthreads();
     NodeCols ncg = nc;  // keys / entries carry global node indices
     ncg.base = 0;
-    if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+    if (a.placement == 4) {
+        if (wave == 0) place_insert<false>(cf, ncg, t, c, a, out, wl[0][lane], nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+    } else if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
     else place_parallel<uint64_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
 }
 
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st) {
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, int placement) {
     if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement == 4 ? 4 : 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, 0};
     hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev);
     return hipGetLastError();
@@ -1679,12 +1849,12 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep, int fit_set) {
+                               uint32_t seq, int ndep, int fit_set, int placement) {
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement == 4 ? 4 : 2, kf.base, kf.shift,
+              kf.idxmax, kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
     if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
     else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);

@@ -1523,12 +1523,12 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     S.sweep_launches++;
     hipEvent_t* ev = S.evb[L.slot];
     if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
-    const bool ov = S.overlap > 0 && S.placement == 2 && S.world == 1;
+    const bool ov = S.overlap > 0 && (S.placement == 2 || S.placement == 4) && S.world == 1;
     if (!ov) ov_quiesce(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
-    L.fit = S.placement == 2;
+    L.fit = S.placement == 2 || S.placement == 4 || S.world > 1;
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -1539,11 +1539,11 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.fit_set[kMaxDep + 1] ^= 1;
         shard_gather(S);
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
-                                  S.d_shard_recv, S.world, out, S.stream));
+                                  S.d_shard_recv, S.world, out, S.stream, S.placement));
     } else if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
                                    S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap,
-                                   S.fit_set[si]));
+                                   S.fit_set[si], S.placement));
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
@@ -2962,11 +2962,11 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
             throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
-        int rc = kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
-                                  out_n_done, out_stop_reason);
-        kbhip::ov_quiesce(s->s);
-        HIPCHK(hipStreamSynchronize(s->s.stream));
-        return rc;
+        // results come back through the pinned result granules; device work still in flight (an
+        // overlapped pop's write-back) is ordered before the next pop by the device chain, and
+        // before anything else by ov_quiesce in the entry point that runs it
+        return kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
+                                out_n_done, out_stop_reason);
     })
 }
 
@@ -3236,7 +3236,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
         }
         else if (std::strcmp(key, "placement") == 0) {
-            if (value < 0 || value > 2) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1 or 2");
+            if (value < 0 || value > 4 || value == 3) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1, 2 or 4");
             s->s.placement = (int)value;
         }
         else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);

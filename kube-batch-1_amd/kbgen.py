@@ -138,6 +138,72 @@ def _csr(lengths: Sequence[int]) -> np.ndarray:
     return out
 
 
+def read_kbs(path: str) -> Tuple[Dict[str, np.ndarray], bytes]:
+    """Read a KBS1 file back: (columns, string table)."""
+    inv = {v[0]: k for k, v in _DT.items()}
+    with open(path, "rb") as f:
+        data = f.read()
+    magic, ver, nsec, _ = struct.unpack_from("<4sIII", data, 0)
+    if magic != b"KBS1":
+        raise ValueError("not a KBS1 file")
+    cols, st = {}, b""
+    for k in range(nsec):
+        name, code, esz, n, off = struct.unpack_from("<24sIIQQ", data, 16 + 48 * k)
+        name = name.rstrip(b"\0").decode()
+        raw = data[off:off + n * esz]
+        if name == "strtab":
+            st = raw
+        else:
+            cols[name] = np.frombuffer(raw, dtype=inv[code]).copy()
+    return cols, st
+
+
+def cluster_from_kbs(path: str) -> "Cluster":
+    """The object model of a KBS1 snapshot, as far as the host-side ordering
+    needs it (tests/gohost.py): nodes (name, allocatable), queues, jobs and pods
+    (UID, namespace, PodGroup, node, phase, priority, timestamp, container
+    requests).  Labels, affinity, ports and tolerations are left out."""
+    C, st = read_kbs(path)
+
+    def s(off):
+        if off < 0:
+            return None
+        return st[off:st.index(b"\0", off)].decode()
+    c = Cluster(tiers=[], actions=s(int(C["conf_actions"][0])) if "conf_actions" in C else DEFAULT_ACTIONS)
+    tiers: Dict[int, List[str]] = {}
+    flags: Dict[str, List[str]] = {}
+    inv_dis = {v: k for k, v in DIS.items()}
+    for n, t, fl in zip(C["conf_plugin_name"], C["conf_plugin_tier"], C["conf_plugin_flags"]):
+        tiers.setdefault(int(t), []).append(s(int(n)))
+        for bit, name in inv_dis.items():
+            if int(fl) & bit:
+                flags.setdefault(s(int(n)), []).append(name)
+    c.tiers = [tiers[k] for k in sorted(tiers)]
+    c.flags = flags
+    for q, w, ts in zip(C["q_name"], C["q_weight"], C["q_ts"]):
+        c.add_queue(s(int(q)), int(w), int(ts))
+    for i in range(len(C["n_name"])):
+        c.add_node(s(int(C["n_name"][i])), int(C["n_alloc_cpu"][i]), int(C["n_alloc_mem"][i]),
+                   int(C["n_alloc_gpu"][i]), int(C["n_alloc_pods"][i]))
+    jname = [s(int(x)) for x in C["j_name"]]
+    for k in range(len(jname)):
+        c.add_job(s(int(C["j_ns"][k])), jname[k], s(int(C["j_queue"][k])), min_member=int(C["j_min"][k]),
+                  ts=int(C["j_ts"][k]), pg_priority=int(C["j_pg_priority"][k]))
+    inv_ph = {v: k for k, v in PHASES.items()}
+    off = C["p_ctr_off"]
+    dele = C.get("p_deleting")
+    for i in range(len(C["p_uid"])):
+        j = int(C["p_job"][i])
+        ctrs = [dict(cpu=int(C["c_cpu"][q]), mem=int(C["c_mem"][q]), gpu=int(C["c_gpu"][q]))
+                for q in range(int(off[i]), int(off[i + 1]))]
+        c.add_pod(s(int(C["p_ns"][i])), s(int(C["p_name"][i])) if "p_name" in C else s(int(C["p_uid"][i])),
+                  uid=s(int(C["p_uid"][i])), group=jname[j] if j >= 0 else None,
+                  node=s(int(C["p_node"][i])) or None, phase=inv_ph[int(C["p_phase"][i])],
+                  deleting=bool(dele[i]) if dele is not None else False, priority=int(C["p_priority"][i]),
+                  ts=int(C["p_ts"][i]), containers=ctrs)
+    return c
+
+
 # ----------------------------------------------------------------------------
 # object-level builder
 # ----------------------------------------------------------------------------

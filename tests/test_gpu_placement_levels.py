@@ -1,6 +1,6 @@
-"""GPU parity of the batched path's running-min level placement (option
-"placement" = 1): placement logs equal the CPU oracle's and the sequential
-placement loop's.  The selection argument is checked exhaustively on CPU in
+"""GPU parity of the batched path's running-min level placements (option
+"placement": 1 levels, 2 parallel levels, 4 insertion): placement logs equal
+the CPU oracle's and the sequential placement loop's.  The selection argument is checked exhaustively on CPU in
 test_placement_levels_model below (it runs without a GPU)."""
 import os
 import random
@@ -19,7 +19,7 @@ def _log(engine, path, placement):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("placement", [1, 2])
+@pytest.mark.parametrize("placement", [1, 2, 4])
 @pytest.mark.parametrize("seed", range(30))
 def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, placement):
     c = kbgen_mod.gen_random(4100 + seed, n_nodes=4 + seed % 12, n_jobs=4 + seed % 8, max_tasks=2 + seed % 9,
@@ -40,7 +40,7 @@ def test_parallel_levels_deep_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed)
     p = str(tmp_path / "d.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for placement in (0, 1, 2):
+    for placement in (0, 1, 2, 4):
         got, _ = _log(engine, p, placement)
         assert got == exp, f"placement {placement}"
 
@@ -50,7 +50,7 @@ def test_levels_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    for placement in (1, 2):
+    for placement in (1, 2, 4):
         got, st = _log(engine, p, placement)
         assert st["batched_pops"] > 0
         assert got == exp, f"placement {placement}"
@@ -63,7 +63,8 @@ def test_levels_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     a, _ = _log(engine, p, 0)
     b, _ = _log(engine, p, 1)
     c, _ = _log(engine, p, 2)
-    assert a == b == c
+    d, _ = _log(engine, p, 4)
+    assert a == b == c == d
 
 
 # ---- CPU: the selection argument (no GPU) ----------------------------------
