@@ -11,13 +11,18 @@ starts (the session upload is part of every step, as in the reference where
 every session re-snapshots the cache).
 
 N > 1: one process per GPU (torch.distributed over RCCL for the barrier and
-the max-over-ranks time).  This round every rank runs an independent replica
-session on its own GPU (node-array sharding is the next step).
+the max-over-ranks time).  Default --mode shard: ONE C4 session node-sharded
+over the GPUs: per batched pop each rank sweeps its node
+range to its top-64 with rows, one ncclAllGather, and every rank runs the
+same placement (strong scaling).  --mode replicas: N independent sessions.
 
 Also reported:
-* roofline of the fused pop kernel (k_pop_batch: sweep + top-64 + placement): algorithmic bytes = nodes x
-  113 B per launch / its mean duration measured with HIP
-  events on the engine's stream during the timed steps;
+* roofline of the fused pop kernel (k_pop_batch_ov: sweep + top-64 + placement):
+  algorithmic bytes = nodes x 113 B per launch / its mean
+  duration, measured with HIP events around every launch on the stream it
+  runs on during the timed steps (the same quantity as rocprofv3's kernel
+  duration; consecutive pops overlap, so it includes the wait for the previous
+  pop's write-back);
 * cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
   cores, on a bounded sample (the first job pops of the same session).
 """
@@ -51,10 +56,10 @@ def parse():
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
-    ap.add_argument("--time-every", type=int, default=0,
-                    help="also HIP-event time every k-th sweep launch (0 = off; per-launch events stall the "
-                         "overlapped pipeline, so the roofline uses each session's device span instead)")
-    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2, 4),
+    ap.add_argument("--time-every", type=int, default=50,
+                    help="HIP-event time every k-th batched pop launch on its own stream (the roofline's kernel "
+                         "duration; 0 = off)")
+    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2, 4, 5),
                     help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels, "
                          "4 insertion (one wave)")
     ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
@@ -193,7 +198,7 @@ def main():
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
-    dev_s, dev_pops, tasks = 0.0, 0, 0
+    dev_s, dev_pops = 0.0, 0
     for _ in range(args.steps):
         dt, n, st = run_session(buf, device, args.time_every, shard, args.placement, args.overlap,
                                 args.speculate)
@@ -203,7 +208,6 @@ def main():
         sweeps_n += st["timed_launches"]
         dev_s += st["alloc_device_s"]
         dev_pops += st["batched_pops"]
-        tasks += st["tasks"]
         st_last = st
     barrier(dist, local)
     wall = time.perf_counter() - t0
@@ -217,15 +221,13 @@ def main():
     nodes = st_last["nodes"]
     traffic = None if shard else pmc_traffic()
     nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
-    if shard or not dev_pops:  # per-task launches: sampled HIP events around single launches
-        sweep_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3
-        timing = f"HIP events around every {args.time_every}-th sweep launch ({sweeps_n} launches)"
-    else:  # batched pops (overlapped): device span of each allocate / its launches
-        sweep_us = dev_s / dev_pops * 1e6
-        timing = (f"HIP events bracketing each session's allocate on the engine streams, / {dev_pops} "
-                  f"k_pop_batch launches (consecutive launches overlap: per-launch device period)")
-    achieved = nodes_per_launch * B_NODE / (sweep_us * 1e-6) / 1e9 if sweep_us > 0 else 0.0
-    tasks_per_launch = tasks / max(dev_pops, 1) if not shard else 1.0
+    # the hot kernel's mean duration: HIP events around every batched pop launch on the stream it runs on
+    # (overlapped pops: the duration includes the wait for the previous pop's write-back, as rocprof's does)
+    launch_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3 if sweeps_n else 0.0
+    kernel = "k_pop_batch (shard sweep, placement 3)" if shard else (
+        "k_pop_batch_ov" if args.overlap else "k_pop_batch")
+    achieved = nodes_per_launch * B_NODE / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
+    period_us = dev_s / dev_pops * 1e6 if dev_pops else 0.0
     out = {
         "metric": METRIC,
         "value": total_placed / wall,
@@ -248,24 +250,20 @@ def main():
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
-                   "unassigned_pops": st_last["unassigned_pops"],
+                   "unassigned_pops": st_last["unassigned_pops"], "collectives": st_last["collectives"],
                    "session_phases_ms": {k: round(v, 2) for k, v in st_last["phases_ms"].items()},
+                   "device_period_us": period_us,  # allocate's device span / batched launches (launches overlap)
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU"},
-        "roofline": {"kernel": "k_sweep_argmax" if shard else ("k_pop_batch_ov" if args.overlap else "k_pop_batch"),
-                     "bound": "hbm", "achieved": achieved,
-                     "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
                      if traffic else None,
-                     "mean_launch_us": sweep_us, "timing": timing,
-                     "bytes_per_launch": nodes_per_launch * B_NODE,
-                     # SURVEY §8(d)'s per-task accounting: one launch serves tasks_per_launch tasks with ONE
-                     # sweep, so per-task algorithmic bytes exceed what the launch reads (frac > 1 is the batching)
-                     "per_task_algorithmic": {"tasks_per_launch": tasks_per_launch,
-                                              "achieved": tasks_per_launch * achieved,
-                                              "frac": tasks_per_launch * achieved / HBM_PEAK_GBS}},
+                     "mean_launch_us": launch_us, "timed_launches": sweeps_n,
+                     "timing": f"HIP events around every {args.time_every}-th batched pop launch on its stream, "
+                               f"read back after the session ({sweeps_n} launches)",
+                     "bytes_per_launch": nodes_per_launch * B_NODE},
     }
     if args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds)

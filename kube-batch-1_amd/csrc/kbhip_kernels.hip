@@ -710,7 +710,29 @@ __device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b
 
 // SC1: rows read and written through sc1 (overlapped pops); the write-back is
 // then published as done = seq before the result stores.
-template <typename ET, bool SC1 = false>
+// L sorted descending over the lanes, e not in L: L with e inserted (the last
+// entry drops off).  A ballot gives the position, a DPP wave_shr:1 moves the tail.
+template <typename T>
+__device__ __forceinline__ T wave_shr1(T v) {  // lane i <- lane i - 1 (lane 0 <- 0)
+    if constexpr (sizeof(T) == 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
+        return ((uint64_t)hi << 32) | lo;
+    } else {
+        return (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T wave_insert_sorted(T L, T e) {
+    const int lane = threadIdx.x & 63;
+    const int pos = __popcll(__ballot(L > e));
+    const T sh = wave_shr1(L);
+    return lane < pos ? L : (lane == pos ? e : sh);
+}
+
+// INS: the round's entries join the running list by insertion (only those
+// above the m-th entry; usually a few) instead of a sort + merge tree.
+template <typename ET, bool SC1 = false, bool INS = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
@@ -805,11 +827,32 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         const ET e = ok ? depth_entry<ET>(rm, n, d, a) : (ET)0;
         if (r == 0) STAMP(gridDim.x * 4 + 6);
         if (wave == kW - 1) { s_last[lane] = e; s_rm[(r + 1) & 1][lane] = rm; }
-        wl[wave][lane] = wave_sort_desc(e);
-        __syncthreads();
-        block_tree_merge(wl, wave, lane);
+        if constexpr (INS) {
+            wl[wave][lane] = e;
+            __syncthreads();
+            if (wave == 0) {
+                // depth 0 (round 0, wave 0): the candidate list itself, already sorted
+                int w0 = 0;
+                if (r == 0) { L = e; w0 = 1; }
+                ET T = readlane_t(L, m - 1);
+                for (int w2 = w0; w2 < kW; ++w2) {
+                    const ET x = wl[w2][lane];
+                    for (uint64_t q = __ballot(x > T); q; q &= q - 1) {
+                        const ET y = readlane_t(x, __ffsll((unsigned long long)q) - 1);
+                        if (y > T) {
+                            L = wave_insert_sorted(L, y);
+                            T = readlane_t(L, m - 1);
+                        }
+                    }
+                }
+            }
+        } else {
+            wl[wave][lane] = wave_sort_desc(e);
+            __syncthreads();
+            block_tree_merge(wl, wave, lane);
+            if (wave == 0) L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
+        }
         if (wave == 0) {
-            L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
             if (r == 0) STAMP(gridDim.x * 4 + 7);
             const ET T = readlane_t(L, m - 1);  // m-th entry: deeper entries below it never place
             const ET le = s_last[lane];
@@ -1096,7 +1139,12 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
     if (lane < 4) msg->fit[lane] = sweep;
 }
 
-template <int R, typename KT>
+// PL: the placement compiled into this instantiation — 2 parallel levels,
+// 5 parallel levels merged by insertion, 3 the node-array shard's sweep only
+// (no placement: the exchange follows), -1 the test-only modes 0 / 1 / 4 —
+// so that a kernel's registers (and the occupancy of its sweep blocks) are
+// those of one placement path.
+template <int R, typename KT, int PL>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                            uint64_t* cand64, uint32_t* arrive, PopOut* out,
                                                            ShardMsg* smsg) {
@@ -1202,10 +1250,16 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     __syncthreads();
-    if (a.placement == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
+    if constexpr (PL == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
         if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg);
         return;
-    }
+    } else {
+    if constexpr (PL == 2 || PL == 5) {  // every wave takes part
+        STAMP(gridDim.x * 4 + 1);
+        if (a.ent32) place_parallel<uint32_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
+        else place_parallel<uint64_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
+        return;
+    } else {
     if (a.placement == 1) {  // uniform
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
@@ -1217,12 +1271,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         STAMP(gridDim.x * 4 + 1);
         place_insert<false>(cf, nc, t, c, a, out, wl[0][lane], nullptr, 0, nullptr, s_fitin, fit_raw);
         STAMP(gridDim.x * 4 + 3);
-        return;
-    }
-    if (a.placement == 2) {  // uniform; every wave takes part
-        STAMP(gridDim.x * 4 + 1);
-        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
-        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
@@ -1347,6 +1395,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
                            make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     STAMP(gridDim.x * 4 + 3);
+    }  // placement 0
+    }  // PL != 3
 }
 
 // ---------------------------------------------------------------------------
@@ -1371,7 +1421,10 @@ __device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
 
 constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
 
-template <int R, typename KT>
+// INS: the placement merges each round by insertion (placement 5) instead of
+// sort + merge trees (placement 2); one placement per instantiation keeps the
+// kernel's registers (and so the occupancy of its sweep blocks) at one path's.
+template <int R, typename KT, bool INS>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
                                                               PopLink* link, uint32_t seq, int ndep) {
@@ -1586,11 +1639,9 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
-    if (ok && a.placement == 4) {
-        if (wave == 0) place_insert<true>(cf, nc, t, c, a, out, wl[0][lane], &link->done, seq, &rc, s_fitin, fit_raw);
-    } else if (ok) {
-        if (a.ent32) place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
-        else place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+    if (ok) {
+        if (a.ent32) place_parallel<uint32_t, true, INS>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        else place_parallel<uint64_t, true, INS>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
@@ -1731,8 +1782,17 @@ int pop_blocks(int n_nodes, int* R_out) {
 template <typename KT>
 static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
                                uint64_t* cand, uint32_t* arrive, PopOut* o, ShardMsg* m, hipStream_t st) {
-#define KBHIP_PB(RR) \
-    hipLaunchKernelGGL((k_pop_batch<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, m)
+#define KBHIP_PB1(RR, PP) \
+    hipLaunchKernelGGL((k_pop_batch<RR, KT, PP>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, m)
+#define KBHIP_PB(RR)                                                   \
+    do {                                                               \
+        switch (a.placement) {                                         \
+            case 2: KBHIP_PB1(RR, 2); break;                           \
+            case 3: KBHIP_PB1(RR, 3); break;                           \
+            case 5: KBHIP_PB1(RR, 5); break;                           \
+            default: KBHIP_PB1(RR, -1); break;                         \
+        }                                                              \
+    } while (0)
     switch (R) {
         case 1: KBHIP_PB(1); break;
         case 2: KBHIP_PB(2); break;
@@ -1741,6 +1801,7 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
         default: KBHIP_PB(16); break;
     }
 #undef KBHIP_PB
+#undef KBHIP_PB1
 }
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
@@ -1815,6 +1876,9 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
     ncg.base = 0;
     if (a.placement == 4) {
         if (wave == 0) place_insert<false>(cf, ncg, t, c, a, out, wl[0][lane], nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+    } else if (a.placement == 5) {
+        if (a.ent32) place_parallel<uint32_t, false, true>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+        else place_parallel<uint64_t, false, true>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
     } else if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
     else place_parallel<uint64_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
 }
@@ -1823,19 +1887,20 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
                               const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, int placement) {
     if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement == 4 ? 4 : 2, kf.base, kf.shift, kf.idxmax,
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, (placement == 4 || placement == 5) ? placement : 2,
+              kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, 0};
     hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev);
     return hipGetLastError();
 }
 
-template <typename KT>
+template <typename KT, bool INS>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
                                   uint32_t seq, int ndep, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
-                       link, seq, ndep)
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT, INS>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, \
+                       o, link, seq, ndep)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1853,11 +1918,17 @@ hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTabl
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement == 4 ? 4 : 2, kf.base, kf.shift,
-              kf.idxmax, kf.use32 && kf.ent32 ? 1 : 0, fit_set};
+    const bool ins = placement == 5;
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, ins ? 5 : 2, kf.base, kf.shift, kf.idxmax,
+              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+    if (kf.use32) {
+        if (ins) launch_pop_batch_ov_t<uint32_t, true>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+        else launch_pop_batch_ov_t<uint32_t, false>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+    } else {
+        if (ins) launch_pop_batch_ov_t<uint64_t, true>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+        else launch_pop_batch_ov_t<uint64_t, false>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+    }
     return hipGetLastError();
 }
 

@@ -379,7 +379,12 @@ struct Session {
     static constexpr int kSlots = 8;  // result slots: up to 1 + speculate batched pops in flight
     uint32_t slot_epoch[kSlots] = {};  // granule tags per result slot
     int next_slot = 0;                // slot of the next batched launch (round robin)
-    hipEvent_t evb[kSlots][2] = {};   // per-slot HIP-event pairs (sampled launch timing)
+    // HIP-event pairs around batched pop launches (option "time_every"): a ring, each
+    // pair read back when it comes round again (long complete by then) or at the end
+    static constexpr int kEvRing = 256;
+    hipEvent_t ev_ring[kEvRing][2] = {};
+    bool ev_used[kEvRing] = {};
+    int ev_next = 0;
     hipEvent_t ev_run[2] = {};        // device span of kbhip_allocate
     double alloc_device_s = 0;
 #ifdef KBHIP_STAMPS
@@ -438,7 +443,7 @@ struct Session {
         comm = nullptr;
         for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1]})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
-        for (auto& pr : evb)
+        for (auto& pr : ev_ring)
             for (auto& e : pr)
                 if (e) { (void)hipEventDestroy(e); e = nullptr; }
         if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
@@ -1490,6 +1495,21 @@ static void ov_quiesce(Session& S) {
 
 // Nothing but the winner's row can change between the chunk's tasks: the
 // condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
+// Duration of the timed launch in event pair k (waits for it if needed).
+static void ev_harvest(Session& S, int k) {
+    hipEvent_t* ev = S.ev_ring[k];
+    if (!S.ev_used[k]) return;
+    HIPCHK(hipEventSynchronize(ev[1]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    S.timed_ms += ms;
+    S.timed_n++;
+    S.ev_used[k] = false;
+}
+static void ev_harvest_all(Session& S) {
+    for (int k = 0; k < Session::kEvRing; ++k) ev_harvest(S, k);
+}
+
 // Some task class reads or writes the pod (anti-)affinity count tables
 // (kbhip_affinity.h): its program has predicate terms, inter-pod priority
 // terms or commit updates.  The tables are built from the snapshot at open;
@@ -1521,14 +1541,21 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     L.m = m;
     L.timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
     S.sweep_launches++;
-    hipEvent_t* ev = S.evb[L.slot];
-    if (L.timed && !ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
-    const bool ov = S.overlap > 0 && (S.placement == 2 || S.placement == 4) && S.world == 1;
+    hipEvent_t* ev = nullptr;
+    if (L.timed) {
+        const int k = S.ev_next;
+        S.ev_next = (S.ev_next + 1) % Session::kEvRing;
+        ev = S.ev_ring[k];
+        if (S.ev_used[k]) ev_harvest(S, k);
+        if (!ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
+        S.ev_used[k] = true;
+    }
+    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1;
     if (!ov) ov_quiesce(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
-    L.fit = S.placement == 2 || S.placement == 4 || S.world > 1;
+    L.fit = S.placement >= 2 || S.world > 1;
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -1536,6 +1563,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     if (S.world > 1) {  // node-array shard: sweep -> all-gather of the shards' lists -> identical placement
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
                                 S.d_arrive, out, S.stream, 3, kf, S.fit_set[kMaxDep + 1], S.d_shard_send));
+        if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));  // timed: the shard's sweep kernel
         S.fit_set[kMaxDep + 1] ^= 1;
         shard_gather(S);
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
@@ -1552,7 +1580,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
                                 S.d_arrive, out, S.stream, S.placement, kf, S.fit_set[kMaxDep + 1]));
         S.fit_set[kMaxDep + 1] ^= 1;
     }
-    if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));
+    if (L.timed && S.world == 1) HIPCHK(hipEventRecord(ev[1], L.st));
     S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
     return L;
 }
@@ -1578,14 +1606,6 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
         if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(L.st));  // long waits: runtime
         if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
         __builtin_ia32_pause();
-    }
-    if (L.timed) {
-        hipEvent_t* ev = S.evb[L.slot];
-        HIPCHK(hipEventSynchronize(ev[1]));
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
-        S.timed_ms += ms;
-        S.timed_n++;
     }
     S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
     S.stats.sweeps += 1;
@@ -2273,6 +2293,7 @@ struct Allocator {
         }
         discard_all();  // predicted pops that never came
         ov_quiesce(S);
+        ev_harvest_all(S);
         HIPCHK(hipEventRecord(S.ev_run[1], S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
         float dms = 0;
@@ -3196,6 +3217,10 @@ int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
 int kbhip_get_stats(kb_session* s, kbhip_stats* out) {
     ABI_GUARD({
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (!s->s.encode_only) {
+            HIPCHK(hipSetDevice(s->s.device));
+            kbhip::ev_harvest_all(s->s);
+        }
         *out = s->s.stats;
         out->device_s = s->s.timed_ms * 1e-3;
         out->timed_launches = s->s.timed_n;
@@ -3236,7 +3261,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
         }
         else if (std::strcmp(key, "placement") == 0) {
-            if (value < 0 || value > 4 || value == 3) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1, 2 or 4");
+            if (value < 0 || value > 5 || value == 3) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1, 2, 4 or 5");
             s->s.placement = (int)value;
         }
         else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);

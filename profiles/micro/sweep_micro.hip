@@ -159,22 +159,22 @@ int main(int argc, char** argv) {
         PopArgs b = a;
         b.epoch = (uint32_t)(i + 2) & 0xffff;
         b.fit_set = i & 1;
-        hipLaunchKernelGGL((k_pop_batch<1, uint32_t>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
+        hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 2>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
                            (ShardMsg*)nullptr);
     });
-    timeit("k_pop_batch (insert, m=36)", [&](int i) {
+    timeit("k_pop_batch (par+insert, m=36)", [&](int i) {
         PopArgs b = a;
-        b.placement = 4;
+        b.placement = 5;
         b.epoch = (uint32_t)(i + 2) & 0xffff;
         b.fit_set = i & 1;
-        hipLaunchKernelGGL((k_pop_batch<1, uint32_t>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
+        hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 5>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
                            (ShardMsg*)nullptr);
     });
     timeit("k_pop_batch (shard emit)", [&](int i) {
         PopArgs b = a;
         b.placement = 3;
         b.fit_set = i & 1;
-        hipLaunchKernelGGL((k_pop_batch<1, uint32_t>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
+        hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 3>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
                            (ShardMsg*)out64);
     });
     CK(hipDeviceSynchronize());
@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
         std::vector<uint64_t> h(ns);
         double acc[8] = {0};
         const int reps = 300;
-        for (int pl : {2, 4, 3}) {
+        for (int pl : {2, 5, 4, 3}) {
             for (auto& x : acc) x = 0;
             for (int i = 0; i < reps; ++i) {
                 CK(hipMemset(st, 0, ns * 8));
@@ -191,8 +191,18 @@ int main(int argc, char** argv) {
                 b.placement = pl;
                 b.epoch = (uint32_t)(i + 5000) & 0xffff;
                 b.fit_set = i & 1;
-                hipLaunchKernelGGL((k_pop_batch<1, uint32_t>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand, arrive, po,
-                                   (ShardMsg*)out64);
+                if (pl == 3)
+                    hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 3>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand,
+                                       arrive, po, (ShardMsg*)out64);
+                else if (pl == 2)
+                    hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 2>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand,
+                                       arrive, po, (ShardMsg*)out64);
+                else if (pl == 5)
+                    hipLaunchKernelGGL((k_pop_batch<1, uint32_t, 5>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand,
+                                       arrive, po, (ShardMsg*)out64);
+                else
+                    hipLaunchKernelGGL((k_pop_batch<1, uint32_t, -1>), dim3(nb), dim3(512), 0, 0, cf, nc, t, b, cand,
+                                       arrive, po, (ShardMsg*)out64);
                 CK(hipDeviceSynchronize());
                 CK(hipMemcpy(h.data(), st, ns * 8, hipMemcpyDeviceToHost));
                 uint64_t t0 = UINT64_MAX, smax = 0, sorted_max = 0, stored_max = 0;

@@ -10,7 +10,8 @@ import pytest
 from test_gpu_parity import NO_POD_AFFINITY
 
 PATHS = [dict(), dict(overlap=0), dict(batched=0), dict(placement=1), dict(placement=0, overlap=0),
-         dict(speculate=0), dict(placement=4), dict(placement=4, overlap=0)]
+         dict(speculate=0), dict(placement=4), dict(placement=4, overlap=0), dict(placement=5),
+         dict(placement=5, overlap=0)]
 
 
 def _engine_close(engine, path, **opts):

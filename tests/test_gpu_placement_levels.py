@@ -19,7 +19,7 @@ def _log(engine, path, placement):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("placement", [1, 2, 4])
+@pytest.mark.parametrize("placement", [1, 2, 4, 5])
 @pytest.mark.parametrize("seed", range(30))
 def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, placement):
     c = kbgen_mod.gen_random(4100 + seed, n_nodes=4 + seed % 12, n_jobs=4 + seed % 8, max_tasks=2 + seed % 9,
@@ -40,7 +40,7 @@ def test_parallel_levels_deep_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed)
     p = str(tmp_path / "d.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for placement in (0, 1, 2, 4):
+    for placement in (0, 1, 2, 4, 5):
         got, _ = _log(engine, p, placement)
         assert got == exp, f"placement {placement}"
 
@@ -50,7 +50,7 @@ def test_levels_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    for placement in (1, 2, 4):
+    for placement in (1, 2, 4, 5):
         got, st = _log(engine, p, placement)
         assert st["batched_pops"] > 0
         assert got == exp, f"placement {placement}"
@@ -64,7 +64,8 @@ def test_levels_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     b, _ = _log(engine, p, 1)
     c, _ = _log(engine, p, 2)
     d, _ = _log(engine, p, 4)
-    assert a == b == c == d
+    e, _ = _log(engine, p, 5)
+    assert a == b == c == d == e
 
 
 # ---- CPU: the selection argument (no GPU) ----------------------------------
