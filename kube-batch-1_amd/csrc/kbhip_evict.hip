@@ -11,8 +11,10 @@
 // node's tasks) is per-node host logic on the host model.  The device produces
 // the order: one HBM sweep writes a key per node — pack_key(score, idx) for
 // preempt (descending = SelectBestNode order), pack_key(0, idx) for reclaim —
-// zero for a node that fails; a device radix sort orders the keys, and the
-// host reads the passing prefix back.  Traffic per task: the per-task sweep's
+// zero for a node that fails; a stable counting sort over the class's small
+// score range orders them (launch_rank_sorted; a library radix sort only for
+// classes whose score range exceeds 256 values), and the host reads the
+// passing prefix back.  Traffic per task: the per-task sweep's
 // B_node bytes per node + 8 B written per node + the sort's passes over 8 B keys.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -96,6 +98,118 @@ hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables
 hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int n, hipStream_t st) {
     return hipcub::DeviceRadixSort::SortKeysDescending(tmp, *tmp_bytes, in, out, n, 0, 64, st);
 }
+
+// ---------------------------------------------------------------------------
+// The walk order by a stable counting sort over the score (hand-written; the
+// score range of a class is small: <= kRankBuckets values).  Order wanted:
+// score descending, then node index ascending (= the descending key order).
+//   k_rank_bucket   one node per thread, blocks over contiguous node ranges:
+//                   key, bucket = shi - score (0 = best), per-block bucket
+//                   counts -> hist[bucket * nblk + block], passing count
+//   k_rank_scan     exclusive scan of hist in (bucket, block) order -> offsets
+//   k_rank_scatter  position = offset + rank among the same bucket before it in
+//                   the block (wave ballots, then earlier waves' counts)
+// ---------------------------------------------------------------------------
+constexpr int kRankBuckets = 256;
+__global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
+                                                        int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
+                                                        uint32_t* count) {
+    __shared__ uint32_t s_h[kRankBuckets];
+    for (int i = threadIdx.x; i < nb; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
+    const TaskClass c = t.classes[cls];
+    const int n = blockIdx.x * kBlock + threadIdx.x;
+    uint64_t k = 0;
+    if (n < nc.n) {
+        if (by_score) {
+            int32_t s = 0;
+            bool passed = false;
+            (void)eval_node_aff(cf, c, t, nc, n, ctrl->ipa_lo[0], ctrl->ipa_hi[0], ctrl->fallback, &s, &passed);
+            k = passed ? pack_key(s, n + nc.base, 0) : 0;
+        } else {
+            k = eval_first_fit(cf, c, t, nc, n);
+        }
+        const int b = k ? (by_score ? shi - key_score(k) : 0) : -1;
+        if (b >= nb) {  // outside the class's score range: never sorted; the host fails loudly on count[1]
+            atomicAdd(&count[1], 1u);
+            k = 0;
+        }
+        keys[n] = k;
+        if (k) atomicAdd(&s_h[b], 1u);
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    for (int i = threadIdx.x; i < nb; i += kBlock) {
+        hist[(size_t)i * gridDim.x + blockIdx.x] = s_h[i];
+        tot += s_h[i];
+    }
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(count, tot);
+}
+
+__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n) {  // in-place exclusive scan, one block
+    __shared__ uint32_t s_sum[1024];
+    const int per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint32_t acc = 0;
+    for (int i = lo; i < hi; ++i) acc += v[i];
+    s_sum[threadIdx.x] = acc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the chunk sums
+        const uint32_t x = threadIdx.x >= (unsigned)o ? s_sum[threadIdx.x - o] : 0u;
+        __syncthreads();
+        s_sum[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = threadIdx.x ? s_sum[threadIdx.x - 1] : 0u;
+    for (int i = lo; i < hi; ++i) {
+        const uint32_t x = v[i];
+        v[i] = run;
+        run += x;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, const uint64_t* keys, const uint32_t* offs,
+                                                         int by_score, int shi, int nb, uint64_t* sorted) {
+    __shared__ uint32_t s_cnt[kBlock / 64][kRankBuckets];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = lane; i < kRankBuckets; i += 64) s_cnt[wave][i] = 0;
+    const int n = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t k = n < nc.n ? keys[n] : 0;
+    const int b = k ? (by_score ? shi - key_score(k) : 0) : -1;  // k_rank_bucket zeroed keys outside [0, nb)
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
+    uint32_t rank = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint64_t todo = __ballot(b >= 0); todo;) {  // each bucket present in the wave
+        const int bv = __builtin_amdgcn_readlane(b, __ffsll((unsigned long long)todo) - 1);
+        const uint64_t m = __ballot(b == bv);
+        if (b == bv) rank = __popcll(m & lt);
+        if (lane == 0) s_cnt[wave][bv] = __popcll(m);
+        todo &= ~m;
+    }
+    __syncthreads();
+    if (b >= 0) {
+        uint32_t base = offs[(size_t)b * gridDim.x + blockIdx.x];
+        for (int w = 0; w < wave; ++w) base += s_cnt[w][b];
+        sorted[base + rank] = k;
+    }
+}
+
+hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                              int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
+                              uint32_t* count, hipStream_t st) {
+    const int nb = by_score ? shi - slo + 1 : 1;
+    if (nb < 1 || nb > kRankBuckets) return hipErrorInvalidValue;
+    const int nblk = (nc.n + kBlock - 1) / kBlock;
+    if (nblk < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_rank_bucket, dim3(nblk), dim3(kBlock), 0, st, cf, nc, t, ctrl, by_score, shi, nb, keys, hist,
+                       count);
+    hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, st, hist, nb * nblk);
+    hipLaunchKernelGGL(k_rank_scatter, dim3(nblk), dim3(kBlock), 0, st, nc, (const uint64_t*)keys,
+                       (const uint32_t*)hist, by_score, shi, nb, sorted);
+    return hipGetLastError();
+}
+size_t rank_hist_words(int n_nodes) { return (size_t)kRankBuckets * ((n_nodes + kBlock - 1) / kBlock + 1); }
 
 hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
                           int64_t rg, hipStream_t st) {

@@ -44,6 +44,14 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
                              int by_score, uint64_t* keys, uint32_t* count, hipStream_t st);
 hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int n, hipStream_t st);
+// The walk order by a hand-written stable counting sort over the score (class
+// score range [slo, shi] of at most 256 values; hipErrorInvalidValue beyond):
+// keys, sorted (descending key order), *count += passing nodes; hist holds
+// rank_hist_words(n) words of scratch.
+hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                              int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
+                              uint32_t* count, hipStream_t st);
+size_t rank_hist_words(int n_nodes);
 hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t* d, int n, hipStream_t st);
 hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
                           int64_t rg, hipStream_t st);

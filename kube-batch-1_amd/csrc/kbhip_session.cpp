@@ -331,6 +331,7 @@ struct Session {
     uint64_t* h_rank = nullptr;  // pinned: [0] = count, then sorted keys
     size_t h_rank_cap = 0;
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
+    bool force_radix = false;  // option "rank_radix": the library radix sort for every class (tests)
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
     vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
@@ -343,6 +344,7 @@ struct Session {
     DevTables tab{};
     vector<TaskClass> classes;
     vector<KeyFormat> class_kf;  // batched-path selection-key format per class
+    vector<std::pair<int64_t, int64_t>> class_srange;  // score range [lo, hi] per class (no inter-pod term)
     bool keys32 = true;          // option "keys32": 32-bit keys where they fit
     DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
         b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
@@ -1315,6 +1317,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         int ibits = 1;  // keys carry global node indices (shards too)
         while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)N) ++ibits;
         S.class_kf.assign(S.classes.size(), KeyFormat{});
+        S.class_srange.assign(S.classes.size(), {0, 0});
         for (size_t ci = 0; ci < S.classes.size(); ++ci) {
             const TaskClass& c = S.classes[ci];
             int64_t na_lo = 0, na_hi = 0;
@@ -1332,6 +1335,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             rng(0, 10 * (int64_t)S.conf.w_bra, &lo, &hi);
             rng(na_lo * S.conf.w_na, na_hi * S.conf.w_na, &lo, &hi);
             const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
+            S.class_srange[ci] = {slo, shi};
             {  // nodeorder.go:287-313 sums in Go's 64-bit int; the kernels' score is int32 (kbhip_eval.h
                // node_score): sessions whose score range (with the inter-pod term) leaves int32 are refused
                 int64_t flo = lo, fhi = hi;
@@ -2356,7 +2360,7 @@ struct Allocator {
             size_t tb = 0;
             HIPCHK(sort_keys_desc(nullptr, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p, N,
                                   S.stream));
-            S.rank_tmp_bytes = std::max<size_t>(tb, 16);
+            S.rank_tmp_bytes = std::max<size_t>({tb, (size_t)16, rank_hist_words(N) * sizeof(uint32_t)});
             S.b_rank_tmp.alloc<uint8_t>(S.rank_tmp_bytes);
             S.h_rank = (uint64_t*)MemPool::get().take(MemPool::kPinned, (size_t)(N + 1) * sizeof(uint64_t),
                                                       &S.h_rank_cap);
@@ -2371,18 +2375,28 @@ struct Allocator {
         h.cls[0] = cls;
         h.ipa_lo[0] = h.ipa_hi[0] = 0;
         HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
-        HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
-        HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (uint64_t*)S.b_rank_keys.p,
-                                 (uint32_t*)S.b_rank_cnt.p, S.stream));
-        size_t tb = S.rank_tmp_bytes;
-        HIPCHK(sort_keys_desc(S.b_rank_tmp.p, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p, N,
-                              S.stream));
+        HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, 2 * sizeof(uint32_t), S.stream));
+        const auto sr = S.class_srange[cls];
+        const bool counting = !S.force_radix && sr.second - sr.first < 256 && sr.first >= INT32_MIN &&
+                              sr.second <= INT32_MAX;
+        if (counting) {  // hand-written stable counting sort over the score
+            HIPCHK(launch_rank_sorted(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first, (int)sr.second,
+                                      (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
+                                      (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p, S.stream));
+        } else {  // wide score ranges (large nodeorder weights): library radix sort of the 64-bit keys
+            HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (uint64_t*)S.b_rank_keys.p,
+                                     (uint32_t*)S.b_rank_cnt.p, S.stream));
+            size_t tb = S.rank_tmp_bytes;
+            HIPCHK(sort_keys_desc(S.b_rank_tmp.p, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p,
+                                  N, S.stream));
+        }
         const int first = std::min(N, S.rank_first);
-        HIPCHK(hipMemcpyAsync(S.h_rank, S.b_rank_cnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+        HIPCHK(hipMemcpyAsync(S.h_rank, S.b_rank_cnt.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
         HIPCHK(hipMemcpyAsync(S.h_rank + 1, S.b_rank_sorted.p, first * sizeof(uint64_t), hipMemcpyDeviceToHost,
                               S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
         const int cnt = (int)(uint32_t)S.h_rank[0];
+        if (S.h_rank[0] >> 32) throw Error(KBHIP_EDEVICE, "rank_nodes: node score outside the class score range");
         if (cnt > first) {
             HIPCHK(hipMemcpyAsync(S.h_rank + 1 + first, (const uint64_t*)S.b_rank_sorted.p + first,
                                   (size_t)(cnt - first) * sizeof(uint64_t), hipMemcpyDeviceToHost, S.stream));
@@ -3249,6 +3263,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
             s->s.overlap = (int)value;
         }
+        else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
             s->s.rank_first = (int)std::min<int64_t>(value, 1 << 20);

@@ -166,3 +166,24 @@ def test_evict_golden_vectors_gpu(engine, case):
     path, g = case
     got, _ = _engine(engine, path, g["actions"])
     assert got == [tuple(x) for x in g["records"]]
+
+
+@pytest.mark.parametrize("radix", [0, 1])
+@pytest.mark.parametrize("seed", range(4))
+def test_rank_sort_paths(engine, oracle_mod, kbgen_mod, tmp_path, radix, seed):
+    """The walk order of reclaim / preempt: the hand-written counting sort over a
+    class's score range (default) and the library radix sort (option rank_radix,
+    kept for score ranges beyond 256 values) both give the oracle's records, on
+    node counts that span many sort blocks and waves."""
+    c = kbgen_mod.gen_preempt(700 + seed, n_nodes=300 + 170 * seed, n_queues=2 + seed % 3, n_run_jobs=40,
+                              n_pend_jobs=6, max_tasks=6, tiers=TIERS[seed % len(TIERS)],
+                              features=FEATURES if seed % 2 else ())
+    p = c.write(str(tmp_path / "r.kbs"))
+    actions = ACTIONS[seed % len(ACTIONS)]
+    exp, ons = oracle_mod.ref_allocate(p, actions=actions, with_nodes=True)
+    with engine.Session(p) as s:
+        s.set_option("rank_radix", radix)
+        pod, node, kind = s.run_actions(actions)
+        ns = s.read_nodes(s.stats()["nodes"])
+    assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, node, kind)] == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
