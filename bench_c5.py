@@ -38,6 +38,7 @@ def main():
     for k in range(args.warmup + args.sessions):
         p = os.path.join(args.cache, f"c5_{args.nodes}_{args.pending}_{k}.kbs")
         if not os.path.exists(p):
+            print(f"generating C5 snapshot {k}", file=sys.stderr, flush=True)
             kbgen.gen_c5(p + ".tmp", seed=kbgen.BASE_SEED + 5 + k, n_nodes=args.nodes, n_pending=args.pending)
             os.replace(p + ".tmp", p)
         with open(p, "rb") as f:
@@ -49,15 +50,20 @@ def main():
         t = [time.perf_counter()]
         counts = {1: 0, 2: 0, 3: 0}
         n_rank = 0
+        launches = {}
         for a in ACTIONS:
-            sw0 = s.stats()["sweeps"]
+            st0 = s.stats()
             t.append(time.perf_counter())
             _, _, kind = getattr(s, a)()
             for v in kind.tolist():
                 counts[v] += 1
             t[-1] = (t[-1], time.perf_counter())
+            st1 = s.stats()
             if a in ("reclaim", "preempt"):
-                n_rank += s.stats()["sweeps"] - sw0  # one node-ranking sweep per reclaim / preempt task
+                n_rank += st1["sweeps"] - st0["sweeps"]  # one node-ranking sweep per reclaim / preempt task
+            else:  # batched pops (one launch places a chunk) vs per-task sweeps
+                bp = st1["batched_pops"] - st0["batched_pops"]
+                launches[a] = {"batched_pops": bp, "per_task_sweeps": st1["sweeps"] - st0["sweeps"] - bp}
         s.close()
         t_end = time.perf_counter()
         if k < args.warmup:
@@ -69,6 +75,7 @@ def main():
         phases["close"].append(t_end - t[-1][1])
         recs.append(counts)
         sweeps.append(n_rank)
+        last_launches = launches
     evict_s = sum(statistics.mean(phases[a]) for a in ("reclaim", "preempt"))
     out = {
         "metric": "C5 what-if sessions/s (reclaim, allocate, backfill, preempt)",
@@ -86,6 +93,7 @@ def main():
                                 "pipelined": statistics.mean(r[2] for r in recs),
                                 "allocated": statistics.mean(r[1] for r in recs)},
         "rank_sweeps_per_session": statistics.mean(sweeps),
+        "launches_last_session": last_launches,
         "reclaim_preempt_us_per_rank_sweep": evict_s / max(statistics.mean(sweeps), 1) * 1e6,
     }
     if args.cpu_baseline:  # the hoisted C++ restatement (oracle/kbfast.cpp): one session, same actions

@@ -198,6 +198,27 @@ KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables&
     return k;
 }
 
+// The batched sweep of a session with Backfilled nodes (placement 6): a node
+// in the walk that cannot fit yet stays a candidate when it carries Backfilled
+// resources — each visit of a walk adds them to its Idle (GetAccessibleResource,
+// node_info.go:209-211), so it may fit a later task of the pop — keyed by its
+// walk position (score, index; kind bit 0).
+KBHIP_HD uint64_t eval_node_walk(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                 const NodeCols& nc, int n, uint32_t* fit) {
+    const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+    const Row r = load_row(nc, n);
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+    int32_t s = 0;
+    bool passed = false;
+    uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+    if (!k && passed && (r.bf_cpu | r.bf_mem | r.bf_gpu)) k = pack_key(s, n + nc.base, 0);
+    *fit = fit_bits(c, r, passed);
+    return k;
+}
+
 // ---------------------------------------------------------------------------
 // pod (anti-)affinity (kbhip_affinity.h): count tables per term class,
 // indexed by the node's topology domain.

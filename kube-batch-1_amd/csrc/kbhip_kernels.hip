@@ -1117,6 +1117,84 @@ __device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---------------------------------------------------------------------------
+// Placement of a session with Backfilled nodes (placement 6; one wave, task
+// after task).  Visiting a node in a walk adds its Backfilled to its Idle
+// (GetAccessibleResource, node_info.go:209-211; allocate.go:150-180): every
+// node ahead of the winner in the walk order, and the winner itself, before
+// its commit.  So nodes other than the winner change between the pop's tasks,
+// and the entry order of the other placements does not hold.  Lane j holds
+// candidate j of the sweep's list — the top 64 of the walk keys of nodes that
+// fit or carry Backfilled (eval_node_walk) — with its row; per task:
+//   winner  = the largest current key (fitting nodes: walk key + kind);
+//   visited = lanes whose walk key is above the winner's (only nodes with
+//             Backfilled change);
+// exact while the winner's walk key is at least the list's last one (every
+// node above it that could be visited or win is in the list; nodes outside
+// do not change).  Otherwise the launch ends before that task (done < m,
+// stop 0; done = 0 asks the host for the general path for one task), and a
+// task that finds no node is left to the general path too (its walk covers
+// every node and reports the FitDelta histogram).
+// ---------------------------------------------------------------------------
+__device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                         const PopArgs& a, PopOut* out, uint64_t K) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;
+    Row r{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    if (n >= 0) {
+        r = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    const bool has_bf = (r.bf_cpu | r.bf_mem | r.bf_gpu) != 0;
+    const uint64_t t0w = readlane64(K, 63) >> 1;  // walk key of the list's last entry (0: the list holds all)
+    int32_t s = 0;
+    bool passed = false;
+    uint64_t key = n >= 0 ? dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed) : 0;
+    uint64_t wk = (n >= 0 && passed) ? pack_key(s, n, 0) >> 1 : 0;  // walk key (0: not in the walk)
+    bool changed = false;
+    int ready = a.ready_count, done = 0, stop = 0;
+    uint64_t mine = 0;  // lane i: winner key of task i
+    for (int i = 0; i < a.n_tasks; ++i) {
+        const uint64_t w = wave_max_key(key);
+        if (!w || (w >> 1) < t0w) break;  // no node, or one outside the list may come first: the host goes on
+        if (lane == i) mine = w;
+        const bool win = n >= 0 && key == w;
+        const bool visit = has_bf && (win || wk > (w >> 1));
+        if (visit) { r.idle_cpu += r.bf_cpu; r.idle_mem += r.bf_mem; r.idle_gpu += r.bf_gpu; }
+        const int kind = key_kind(w);
+        if (win) {
+            r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
+            if (c.has_ports)
+                for (int q = 0; q < 4; ++q) pw[q] |= (q < nc.port_words) ? t.masks[c.pown_off + q] : 0;
+        }
+        if (visit || win) {
+            changed = true;
+            key = dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed);
+            wk = passed ? pack_key(s, n, 0) >> 1 : 0;
+        }
+        done = i + 1;
+        if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+        if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
+    }
+    if (changed) {
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pw[w];
+    }
+    if (lane < done || (done == 0 && lane == 0))
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
 // writes this shard's top-64 with their rows and the sweep's FitDelta counts.
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
@@ -1140,7 +1218,8 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
 }
 
 // PL: the placement compiled into this instantiation — 2 parallel levels,
-// 5 parallel levels merged by insertion, 3 the node-array shard's sweep only
+// 5 parallel levels merged by insertion, 6 sessions with Backfilled nodes
+// (walk keys, sequential placement), 3 the node-array shard's sweep only
 // (no placement: the exchange follows), -1 the test-only modes 0 / 1 / 4 —
 // so that a kernel's registers (and the occupancy of its sweep blocks) are
 // those of one placement path.
@@ -1174,7 +1253,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         if (n < nc.n) {
             int32_t s;
             bool passed;
-            k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
+            if constexpr (PL == 6) k = sweep_key<KT>(eval_node_walk(cf, c, t, nc, n, &fbs[r]), a);
+            else k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
         k = wave_sort_desc(k);
         best = r == 0 ? k : wave_merge_desc(best, k);
@@ -1252,6 +1332,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     __syncthreads();
     if constexpr (PL == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
         if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg);
+        return;
+    } else if constexpr (PL == 6) {  // Backfilled nodes in the session
+        if (wave != 0) return;
+        STAMP(gridDim.x * 4 + 1);
+        place_bf(cf, nc, t, c, a, out, wl[0][lane]);
+        STAMP(gridDim.x * 4 + 3);
         return;
     } else {
     if constexpr (PL == 2 || PL == 5) {  // every wave takes part
@@ -1790,6 +1876,7 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
             case 2: KBHIP_PB1(RR, 2); break;                           \
             case 3: KBHIP_PB1(RR, 3); break;                           \
             case 5: KBHIP_PB1(RR, 5); break;                           \
+            case 6: KBHIP_PB1(RR, 6); break;                           \
             default: KBHIP_PB1(RR, -1); break;                         \
         }                                                              \
     } while (0)

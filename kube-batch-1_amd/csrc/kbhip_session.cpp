@@ -131,6 +131,7 @@ struct HJob {  // session jobs are numbered in UID order
     vector<int> pending;  // pending non-BestEffort tasks in TaskOrderFn order (built at first pop)
     size_t cursor = 0;
     bool pending_built = false;
+    bool maybe_pending = false;  // had a Pending non-BestEffort task at open (a superset of "has one now")
     int cnt_alloc = 0, cnt_aob = 0;
     int32_t fit[4] = {0, 0, 0, 0};  // NodesFitDelta of its last task that ended a pop unplaced / not ready:
     bool fit_exact = true;          // walk nodes, negative cpu / memory / GPU deltas (JobInfo.FitError)
@@ -139,6 +140,7 @@ struct HJob {  // session jobs are numbered in UID order
 };
 struct HQueue {
     string name;
+    int32_t rank = 0;  // rank of name among the session's queue names (QueueOrderFn's final string compare)
     int32_t weight = 1;
     int64_t ts = 0;
     bool has_attr = false;
@@ -332,6 +334,7 @@ struct Session {
     size_t h_rank_cap = 0;
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
     bool force_radix = false;  // option "rank_radix": the library radix sort for every class (tests)
+    bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
     vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
@@ -814,6 +817,12 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.queues[i].ts = qts.empty() ? 0 : qts[i];
         qidx[S.queues[i].name] = (int)i;
     }
+    {
+        int r = 0;  // equal names share a rank (the map holds each name once, in string order)
+        std::map<string, int> rank;
+        for (auto& kv : qidx) rank[kv.first] = r++;
+        for (auto& q : S.queues) q.rank = rank[q.name];
+    }
     auto jns = V32("j_ns"), jname = V32("j_name"), jq = V32("j_queue"), jmin = V32("j_min"), jpri = V32("j_pg_priority");
     auto jts = s.vec<int64_t>("j_ts");
     // Job UIDs: "namespace/name" of a PodGroup, the pod UID of a shadow one
@@ -954,7 +963,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     {
         for (size_t j = 0; j < S.jobs.size(); ++j) S.jobs[j].tasks.reserve(ntask[j]);
         for (int i = 0; i < P; ++i)
-            if (slot_of[i] >= 0) S.jobs[slot_of[i]].tasks.push_back(i);
+            if (slot_of[i] >= 0) {
+                HJob& j = S.jobs[slot_of[i]];
+                j.tasks.push_back(i);
+                const HPod& p = S.pods[i];
+                if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU))
+                    j.maybe_pending = true;
+            }
     }
 
     mark("jobs");
@@ -1486,6 +1501,7 @@ struct BatchLaunch {
     bool timed = false;
     hipStream_t st = nullptr;
     bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
+    bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
 };
 
 // Wait until no overlapped pop can still run (before device work that is not
@@ -1527,7 +1543,9 @@ static bool has_aff_classes(const Session& S) {
 
 static bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
-    return S.batched && (S.world == 1 || S.comm || S.xgfn) && !S.any_bf && !c.backfill && !c.aff &&
+    // Backfilled nodes (some Idle grows on each walk visit): placement 6, one GPU only
+    const bool bf_ok = !S.any_bf || (S.world == 1 && S.bf_batch);
+    return S.batched && (S.world == 1 || S.comm || S.xgfn) && bf_ok && !c.backfill && !c.aff &&
            S.nc.port_words <= 4 && S.n_total < (1 << 25);
 }
 
@@ -1554,12 +1572,13 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         if (!ev[0]) { HIPCHK(hipEventCreate(&ev[0])); HIPCHK(hipEventCreate(&ev[1])); }
         S.ev_used[k] = true;
     }
-    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1;
+    L.bf = S.any_bf != 0;
+    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1 && !L.bf;
     if (!ov) ov_quiesce(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
-    L.fit = S.placement >= 2 || S.world > 1;
+    L.fit = !L.bf && (S.placement >= 2 || S.world > 1);
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -1581,7 +1600,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.ov_pending = true;
     } else {
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                                S.d_arrive, out, S.stream, S.placement, kf, S.fit_set[kMaxDep + 1]));
+                                S.d_arrive, out, S.stream, L.bf ? 6 : S.placement, kf, S.fit_set[kMaxDep + 1]));
         S.fit_set[kMaxDep + 1] ^= 1;
     }
     if (L.timed && S.world == 1) HIPCHK(hipEventRecord(ev[1], L.st));
@@ -1614,7 +1633,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
     S.stats.sweeps += 1;
     S.stats.batched_pops += 1;
-    if (n_done < 1 || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+    if (n_done < (L.bf ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
     for (int j = 0; j < n_done; ++j) {
         const uint64_t g = load(j);
         res_node[j] = (int32_t)(g & 0xffffffffu) - 1;
@@ -1712,8 +1731,19 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         const int cls0 = S.pods[ids[done]].cls;
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
-        const bool batch = batchable(S, cls0);
-        if (!batch) {  // general path: up to a chunk of mixed classes, no longer than the pop can run
+        bool batch = batchable(S, cls0);
+        int n_done, stop_c, ready_c, any_bf_c = S.any_bf;
+        const int32_t* res_node;
+        const int32_t* res_kind;
+        if (batch) {
+            // one launch: sweep + per-block top-64 + merge + placement of the chunk
+            const BatchLaunch L = launch_batched(S, cls0, m, gang_mode, min_avail, ready_count);
+            collect_batched(S, L, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf);
+            if (n_done == 0) {  // placement 6 could not place the first task exactly: general path for it
+                batch = false;
+                m = 1;
+            }
+        } else {  // general path: up to a chunk of mixed classes, no longer than the pop can run
             m = std::min(n - done, kMaxChunk);  // (it stops once Ready: after `need` more Allocated tasks)
             const int need = gang_mode ? min_avail - ready_count : 1;
             m = std::min(m, std::max(need, 1));
@@ -1722,13 +1752,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         const bool timed = !batch && S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
         if (timed && !S.ev0) { HIPCHK(hipEventCreate(&S.ev0)); HIPCHK(hipEventCreate(&S.ev1)); }
         if (!batch) S.sweep_launches++;
-        int n_done, stop_c, ready_c, any_bf_c = S.any_bf;
-        const int32_t* res_node;
-        const int32_t* res_kind;
         if (batch) {
-            // one launch: sweep + per-block top-64 + merge + placement of the chunk
-            const BatchLaunch L = launch_batched(S, cls0, m, gang_mode, min_avail, ready_count);
-            collect_batched(S, L, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf);
             int alloc = 0;
             for (int j = 0; j < n_done; ++j) alloc += S.res_kind_buf[j] == 1;
             ready_c = ready_count + alloc;
@@ -1873,6 +1897,35 @@ struct GoHeap {  // Go container/heap (up/down exactly as heap.go), with an opti
     bool empty() const { return items.empty(); }
 };
 
+// A queue's job heap in allocate (allocate.go:48-63, 87): a job's order key
+// (priority, gang readiness, DRF share, creation time, UID) changes only
+// while the job is popped, so the heap never holds a stale key and pops in
+// exact key order (a strict total order) whatever its layout.  Jobs with no
+// pending task when the action starts are never pushed back and never change
+// key: they wait in a list sorted by key, and a pop takes the smaller of its
+// head and the heap's top.  Only the jobs with pending tasks pay heap work
+// (C5: ~180k running jobs, a few hundred pending ones).
+template <typename L>
+struct JobQueue {
+    GoHeap<L> heap;
+    vector<int> idle;       // jobs without pending tasks, ascending key
+    vector<int> head{0};    // next idle job (a vector: the speculation journal restores it)
+    L less;
+    explicit JobQueue(L l) : heap(l), less(l) {}
+    void set_journal(HeapJournal* jr) { heap.jr = jr; }
+    void push(int x) { heap.push(x); }
+    bool empty() const { return head[0] >= (int)idle.size() && heap.empty(); }
+    int pop() {
+        const int h = head[0];
+        if (h < (int)idle.size() && (heap.empty() || less(idle[h], heap.items[0]))) {
+            if (heap.jr && heap.jr->on) heap.jr->e.push_back({&head, 0, h});
+            head[0] = h + 1;
+            return idle[h];
+        }
+        return heap.pop();
+    }
+};
+
 struct Allocator {
     Session& S;
     explicit Allocator(Session& s) : S(s) {}
@@ -1900,6 +1953,7 @@ struct Allocator {
             }
     }
     bool job_less(int l, int r) const {  // session_plugins.go:244-268
+        if (l == r) return false;
         const HJob &L = S.jobs[l], &R = S.jobs[r];
         for (int code : job_order) {
             int c;
@@ -1913,10 +1967,53 @@ struct Allocator {
         if (L.ts == R.ts) return l < r;  // UID order: jobs are numbered in UID order at open
         return L.ts < R.ts;
     }
+    // jobs in job_less order, sorted on compact keys: job_less's comparisons in
+    // turn as unsigned digits (priority descending, gang-ready last, DRF share
+    // ascending — non-negative doubles order as their bits — creation time),
+    // then the job index (UID order)
+    void sort_jobs(vector<int>& v) const {
+        struct K {
+            uint64_t d[3];
+            int64_t ts;
+            int j;
+        };
+        const int nd = (int)job_order.size();
+        bool neg = false;  // (DRF shares are sums of requests over totals: never negative)
+        for (int j : v) neg = neg || S.jobs[j].drf_share < 0;
+        if (nd > 3 || neg) {  // more order codes than digits (repeated plugins): the comparator itself
+            std::sort(v.begin(), v.end(), [this](int a, int b) { return job_less(a, b); });
+            return;
+        }
+        vector<K> k(v.size());
+        for (size_t i = 0; i < v.size(); ++i) {
+            const HJob& J = S.jobs[v[i]];
+            K& x = k[i];
+            for (int c = 0; c < nd; ++c) {
+                const int code = job_order[c];
+                if (code == 1) x.d[c] = (uint64_t)((int64_t)INT32_MAX - (int64_t)J.priority);
+                else if (code == 2) x.d[c] = readiness(J) == 1 ? 1 : 0;
+                else {
+                    uint64_t b = 0;
+                    if (J.drf_share != 0) std::memcpy(&b, &J.drf_share, 8);
+                    x.d[c] = b;
+                }
+            }
+            x.ts = J.ts;
+            x.j = v[i];
+        }
+        std::sort(k.begin(), k.end(), [nd](const K& a, const K& b) {
+            for (int c = 0; c < nd; ++c)
+                if (a.d[c] != b.d[c]) return a.d[c] < b.d[c];
+            if (a.ts != b.ts) return a.ts < b.ts;
+            return a.j < b.j;
+        });
+        for (size_t i = 0; i < v.size(); ++i) v[i] = k[i].j;
+    }
     bool queue_less(int l, int r) const {  // session_plugins.go:270-295, proportion.go:144-157
+        if (l == r) return false;  // copies of one queue (one heap entry per job) are equal
         const HQueue &L = S.queues[l], &R = S.queues[r];
         if (queue_prop && L.share != R.share) return L.share < R.share;
-        if (L.ts == R.ts) return L.name < R.name;
+        if (L.ts == R.ts) return L.rank < R.rank;
         return L.ts < R.ts;
     }
     bool task_less(int l, int r) const {  // session_plugins.go:297-329, priority.go:39-55
@@ -2001,14 +2098,31 @@ struct Allocator {
         auto ql = [this](int a, int b) { return queue_less(a, b); };
         auto jl = [this](int a, int b) { return job_less(a, b); };
         GoHeap<decltype(ql)> queues(ql);
-        std::map<int, GoHeap<decltype(jl)>> jobs_map;
+        std::map<int, JobQueue<decltype(jl)>> jobs_map;
         for (size_t j = 0; j < S.jobs.size(); ++j) {
-            int q = S.jobs[j].queue;
+            const HJob& job = S.jobs[j];
+            int q = job.queue;
             queues.push(q);
             auto it = jobs_map.find(q);
-            if (it == jobs_map.end()) it = jobs_map.emplace(q, GoHeap<decltype(jl)>(jl)).first;
-            it->second.push((int)j);
+            if (it == jobs_map.end()) it = jobs_map.emplace(q, JobQueue<decltype(jl)>(jl)).first;
+            bool work = false;  // allocate.go:91-104: a pending task that is not BestEffort
+            if (job.pending_built) work = job.cursor < job.pending.size();
+            else if (job.maybe_pending)
+                for (int t : job.tasks) {
+                    const HPod& p = S.pods[t];
+                    if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) {
+                        work = true;
+                        break;
+                    }
+                }
+            if (work) {
+                it->second.push((int)j);
+            } else {
+                it->second.idle.push_back((int)j);
+                S.jobs[j].pending_built = true;  // what build_pending would find: nothing
+            }
         }
+        for (auto& kv : jobs_map) sort_jobs(kv.second.idle);
         vector<int32_t> ids, onode;
         vector<uint8_t> okind;
         const int gm = S.gang_ready ? 1 : 0;
@@ -2046,7 +2160,7 @@ struct Allocator {
         std::deque<Spec> specs;  // launched predictions, oldest first
         HeapJournal journal;
         queues.jr = &journal;
-        for (auto& kv : jobs_map) kv.second.jr = &journal;
+        for (auto& kv : jobs_map) kv.second.set_journal(&journal);
         struct JobSave {
             int jb, cnt;
             size_t cur;
@@ -2229,7 +2343,7 @@ struct Allocator {
                 return;
             }
             if (!have) L = launch_batched(S, cls0, m, gm, job.min_avail, job.cnt_alloc);
-            if (S.speculate > 0) speculate(q, jb, m, n);
+            if (S.speculate > 0 && !S.any_bf) speculate(q, jb, m, n);  // the undo of a pop has no visit rule
             int nd = 0, st = 0;
             collect_batched(S, L, &nd, &st, S.res_node_buf, S.res_kind_buf);
             if (st < 0) throw Error(KBHIP_EDEVICE, "device pop did not complete");
@@ -3264,6 +3378,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             s->s.overlap = (int)value;
         }
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
+        else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
             s->s.rank_first = (int)std::min<int64_t>(value, 1 << 20);
