@@ -91,6 +91,7 @@ typedef struct kbhip_stats {
     int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
     int64_t fit_inexact;     /* jobs whose FitError histogram was not computed (shards, pod-affinity fallback) */
     int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
+    int64_t pp_retries;      /* pop chunks the persistent placer could not start (swept again without it) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -184,8 +185,16 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
 /* Engine knobs: "batched" = 0 forces the per-task sweep path (tests);
  * "time_every" = k times every k-th sweep launch with HIP events;
  * "placement" = 2 (default) places a batched chunk by parallel levels, 8
- * depths per step; 1 by running-min levels, one depth per step; 0 by the
- * sequential loop over precomputed chains;
+ * depths per step; 5 the same merged by insertion; 4 by one-wave insertion;
+ * 1 by running-min levels, one depth per step; 0 by the sequential loop over
+ * precomputed chains;
+ * "pp" = 1 runs kbhip_allocate's batched pops through the persistent placer
+ * (one sweep launch per pop, one resident workgroup placing them in order;
+ * overrides "overlap"), 0 (default) = the overlapped pop kernel;
+ * "bf_batch" = 1 (default) batches pops in sessions with Backfilled nodes
+ * (placement 6), 0 = per-task sweeps there;
+ * "rank_radix" = 1 orders reclaim / preempt walks with the library radix sort
+ * instead of the counting sort (tests);
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;

@@ -1,0 +1,1059 @@
+// kbhip_batch.h — device building blocks of the batched placement path,
+// shared by the pop kernels (kbhip_kernels.hip) and the persistent placer
+// (kbhip_pp.hip): wave exchange / sort / merge networks, selection keys,
+// the placements (levels, parallel levels, insertion, Backfilled), the
+// result granules and the row cache.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "kbhip_eval.h"
+#include "kbhip_internal.h"
+
+namespace kbhip {
+
+#if defined(KBHIP_STAMPS) && !defined(KBHIP_STAMPS_OFF)
+// Diagnostic build only: phase stamps (s_memrealtime, 100 MHz) of k_pop_batch.
+// Layout: [block][0..3] = start, after sweep+wave sort, after block merge, after arrival;
+// [nb*4 + 0..7] = last block: merged, chain precomputed, placement done, end.
+static __device__ uint64_t* g_stamps;
+#define STAMP(slot)                                                       \
+    do {                                                                  \
+        if (threadIdx.x == 0) g_stamps[(slot)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define STAMP(slot) do {} while (0)
+#endif
+#ifndef PSTAMP  // placement phase accumulation (the persistent placer's profile build)
+#define PSTAMP(k) do {} while (0)
+#endif
+
+// ---------------------------------------------------------------------------
+// wave-level exchange: lane i <-> lane i ^ J without the LDS crossbar.
+// J = 1, 2: DPP quad_perm; 4: DPP row_shl:4 / row_shr:4 + select; 8: DPP
+// row_ror:8; 16 / 32: gfx950 v_permlane16_swap / v_permlane32_swap.
+// (ds_bpermute, what __shfl_xor lowers to, costs an LDS round trip per
+// 32-bit half; these are VALU ops.)  Checked against __shfl_xor on the GPU.
+// ---------------------------------------------------------------------------
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane32(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+    if constexpr (J == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    } else if constexpr (J == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    } else if constexpr (J == 4) {
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x104, 0xf, 0xf, false);  // row_shl:4
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+        return (lane & 4) ? dn : up;
+    } else if constexpr (J == 8) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+    } else if constexpr (J == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane & 16) ? r[0] : r[1];
+    } else {
+        static_assert(J == 32, "xor distance");
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane & 32) ? r[0] : r[1];
+    }
+}
+template <int J>
+__device__ __forceinline__ uint64_t xor_lane64(uint64_t v) {
+    return ((uint64_t)xor_lane32<J>((uint32_t)(v >> 32)) << 32) | xor_lane32<J>((uint32_t)v);
+}
+template <int J, typename T>
+__device__ __forceinline__ T xor_lane(T v) {
+    if constexpr (sizeof(T) == 8) return xor_lane64<J>(v);
+    else return xor_lane32<J>(v);
+}
+template <typename T>
+__device__ __forceinline__ T reverse_lanes(T v) {  // lane i <- lane 63 - i (= i ^ 63)
+    if constexpr (sizeof(T) == 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x140, 0xf, 0xf, false);  // row_mirror
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x140, 0xf, 0xf, false);
+        return xor_lane64<32>(xor_lane64<16>(((uint64_t)hi << 32) | lo));
+    } else {
+        const uint32_t m = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false);
+        return xor_lane32<32>(xor_lane32<16>(m));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// wave / block reductions
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    uint64_t u;
+    u = xor_lane64<32>(v); v = u > v ? u : v;
+    u = xor_lane64<16>(v); v = u > v ? u : v;
+    u = xor_lane64<8>(v); v = u > v ? u : v;
+    u = xor_lane64<4>(v); v = u > v ? u : v;
+    u = xor_lane64<2>(v); v = u > v ? u : v;
+    u = xor_lane64<1>(v); v = u > v ? u : v;
+    return v;
+}
+
+// ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// batched path v2: one launch per pop chunk
+// ---------------------------------------------------------------------------
+// Wave-level sorting on registers: lane i holds one key (u32 or u64);
+// descending order.  Bitonic network, every exchange a DPP / permlane op.
+template <int K, int J, typename T>
+__device__ __forceinline__ T bitonic_step(T v) {
+    const int lane = threadIdx.x & 63;
+    const T o = xor_lane<J>(v);
+    const bool keep_max = ((lane & J) == 0) == ((lane & K) == 0);
+    return keep_max ? (o > v ? o : v) : (o < v ? o : v);
+}
+template <int K, typename T>
+__device__ __forceinline__ T bitonic_stage(T v) {
+    if constexpr (K >= 64) v = bitonic_step<K, 32>(v);
+    if constexpr (K >= 32) v = bitonic_step<K, 16>(v);
+    if constexpr (K >= 16) v = bitonic_step<K, 8>(v);
+    if constexpr (K >= 8) v = bitonic_step<K, 4>(v);
+    if constexpr (K >= 4) v = bitonic_step<K, 2>(v);
+    return bitonic_step<K, 1>(v);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sort_desc(T v) {
+    v = bitonic_stage<2>(v);
+    v = bitonic_stage<4>(v);
+    v = bitonic_stage<8>(v);
+    v = bitonic_stage<16>(v);
+    v = bitonic_stage<32>(v);
+    return bitonic_stage<64>(v);
+}
+// Top-64 of two descending lists (lane i holds a[i], b[i]); result descending.
+template <int J, typename T>
+__device__ __forceinline__ T half_clean_desc(T v) {
+    const int lane = threadIdx.x & 63;
+    const T o = xor_lane<J>(v);
+    return ((lane & J) == 0) ? (o > v ? o : v) : (o < v ? o : v);
+}
+template <typename T>
+__device__ __forceinline__ T wave_merge_desc(T a, T b) {
+    const T br = reverse_lanes(b);
+    T v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
+    v = half_clean_desc<32>(v);
+    v = half_clean_desc<16>(v);
+    v = half_clean_desc<8>(v);
+    v = half_clean_desc<4>(v);
+    v = half_clean_desc<2>(v);
+    return half_clean_desc<1>(v);
+}
+
+// Results land in pinned host memory as self-tagged 8-byte granules, one per
+// consumed task, each written by ONE 8-byte store (no fence needed: the host
+// polls the tags).  granule = epoch<<48 | (stop+1)<<44 | n_done<<36 | kind<<34 | (node+1)
+struct PopOut {
+    uint64_t g[kMaxChunk];
+    uint64_t fit[2];  // FitDelta histogram of a task that found no node: walk nodes, cpu | memory, GPU
+};
+__host__ __device__ inline uint64_t make_fit_granule(uint32_t epoch, uint32_t a, uint32_t b) {
+    return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(b & 0xffffffu) << 24) | (uint64_t)(a & 0xffffffu);
+}
+// Per-group FitDelta counters of the batched sweep, after the arrival counters:
+// two sets; a launch adds to one and zeroes the other (its stream's previous
+// launch read that one and the next one adds to it).
+__device__ __forceinline__ uint32_t* fit_counters(uint32_t* arrive, int set) {
+    return arrive + (kMaxGroups + 1) * 32 + set * kMaxGroups * 32;
+}
+// Block: add this lane's fit bits to the block's LDS counters (every lane of every wave).
+__device__ __forceinline__ void fit_block_add(uint32_t* s_fitb, uint32_t fb) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int cnt = __popcll(__ballot((fb >> b) & 1u));
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_fitb[b], (uint32_t)cnt);
+    }
+}
+__host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n_done, int kind, int node) {
+    return ((uint64_t)(epoch & 0xffff) << 48) | ((uint64_t)(stop + 1) << 44) | ((uint64_t)n_done << 36) |
+           ((uint64_t)kind << 34) | (uint64_t)(uint32_t)(node + 1);
+}
+
+struct PopArgs {
+    int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
+    uint32_t epoch;
+    int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels, 2: parallel levels
+    // 32-bit selection keys (when the class's score range and the node count
+    // fit): key = (score - kbase + 1) << kshift | (kidxmax - idx) << 1 | pipelined,
+    // ordered exactly as pack_key; halves the sort / merge network work.
+    int32_t kbase, kshift, kidxmax;
+    int32_t ent32;  // placement entries in 32 bits: (rm - kbase + 1) fits in 32 - kshift - 5 bits
+    int32_t fit_set;  // FitDelta counter set of this launch (alternates per stream; the other one is zeroed)
+};
+
+// Selection key of the batched sweep in type T (see PopArgs).
+template <typename T>
+__device__ __forceinline__ T sweep_key(uint64_t k64, const PopArgs& a) {
+    if constexpr (sizeof(T) == 8) {
+        return k64;
+    } else {
+        if (!k64) return 0;
+        return ((uint32_t)(key_score(k64) - a.kbase + 1) << a.kshift) |
+               ((uint32_t)(a.kidxmax - key_idx(k64)) << 1) | (uint32_t)(k64 & 1);
+    }
+}
+template <typename T>
+__device__ __forceinline__ uint64_t key64_of(T k, const PopArgs& a) {
+    if constexpr (sizeof(T) == 8) {
+        return k;
+    } else {
+        if (!k) return 0;
+        return pack_key((int32_t)(k >> a.kshift) - 1 + a.kbase, a.kidxmax - (int32_t)((k >> 1) & (uint32_t)a.kidxmax),
+                        (int32_t)(k & 1));
+    }
+}
+
+constexpr int kPopThreads = 512;  // 8 waves
+constexpr int kDepth = 3;         // post-commit keys precomputed per candidate
+
+__device__ __forceinline__ Row apply_commits(Row r, const TaskClass& c, int na, int np) {
+    r.idle_cpu -= na * c.req_cpu; r.idle_mem -= na * c.req_mem; r.idle_gpu -= na * c.req_gpu;
+    r.rel_cpu -= np * c.req_cpu; r.rel_mem -= np * c.req_mem; r.rel_gpu -= np * c.req_gpu;
+    const int n = na + np;
+    r.pods += n;
+    r.nzc += n * c.nz_cpu;
+    r.nzm += n * c.nz_mem;
+    return r;
+}
+
+// 64-lane max of a u32 with DPP row shifts + row broadcasts (GFX9 family),
+// broadcast to every lane.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    uint32_t t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:1
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:2
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:4
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xf, 0xf, false); v = t > v ? t : v;  // row_shr:8
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false); v = t > v ? t : v;  // row_bcast:15
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false); v = t > v ? t : v;  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint64_t wave_max_key(uint64_t v) {
+    const uint32_t hi = wave_max_u32((uint32_t)(v >> 32));
+    const uint32_t lo = wave_max_u32((uint32_t)(v >> 32) == hi ? (uint32_t)v : 0u);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ---------------------------------------------------------------------------
+// Placement by levels (option "placement" = 1).  The greedy of a chunk picks,
+// task after task, the node with the largest current key; only the winner's
+// key changes.  Give candidate j the entries e(j, d) for its d-th extra
+// commit: (running minimum of its scores over levels 0..d, index, d, real
+// kind).  The greedy's choice sequence equals the entries sorted descending:
+// a node whose key RISES after a commit is picked again at once (every other
+// current key is below its previous one), which the running minimum keeps in
+// place; between nodes, equal scores go to the lower index as in pack_key.
+// Entries are generated level by level (one re-evaluation per lane), merged
+// into a sorted top-64, and generation stops when no lane's newest entry
+// reaches the current m-th entry (deeper entries of a node are smaller).
+// ---------------------------------------------------------------------------
+constexpr int kEntryIdxMax = (1 << 25) - 1;  // batched path: < 2^25 nodes
+
+// Node rows handed from one overlapped pop to the next (k_pop_batch_ov):
+// written with sc1 (write-through) stores, read with sc1 loads (L1 bypass),
+// the storing wave drained before the flag (MI355X_MICROARCH.md valid forms,
+// row 1) — no release / acquire fences on the pop-to-pop critical path.
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// load_row with the columns a batched placement writes read through sc1
+// (Backfilled, allocatable and MaxTaskNum never change on the batched path).
+__device__ __forceinline__ Row load_row_sc1(const NodeCols& nc, int n) {
+    Row r;
+    r.idle_cpu = ld_sc1(&nc.idle_cpu[n]); r.idle_mem = ld_sc1(&nc.idle_mem[n]); r.idle_gpu = ld_sc1(&nc.idle_gpu[n]);
+    r.rel_cpu = ld_sc1(&nc.rel_cpu[n]); r.rel_mem = ld_sc1(&nc.rel_mem[n]); r.rel_gpu = ld_sc1(&nc.rel_gpu[n]);
+    r.bf_cpu = nc.bf_cpu[n]; r.bf_mem = nc.bf_mem[n]; r.bf_gpu = nc.bf_gpu[n];
+    r.acpu = nc.acpu[n]; r.amem = nc.amem[n]; r.nzc = ld_sc1(&nc.nzc[n]); r.nzm = ld_sc1(&nc.nzm[n]);
+    r.pods = ld_sc1(&nc.pods[n]); r.maxtasks = nc.maxtasks[n];
+    return r;
+}
+template <bool SC1>
+__device__ __forceinline__ Row load_row_t(const NodeCols& nc, int n) {
+    if constexpr (SC1) return load_row_sc1(nc, n);
+    else return load_row(nc, n);
+}
+template <bool SC1>
+__device__ __forceinline__ uint64_t load_port_t(const NodeCols& nc, int w, int n) {
+    const uint64_t* p = nc.ports + (int64_t)w * nc.npad + n;
+    if constexpr (SC1) return ld_sc1(p);
+    else return *p;
+}
+// eval_node with the rows read through sc1.
+__device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                                  const NodeCols& nc, int n, uint32_t* fit = nullptr) {
+    const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+    const Row r = load_row_sc1(nc, n);
+    uint64_t pw[4] = {0, 0, 0, 0};
+    if (c.has_ports)
+        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, n);
+    int32_t s;
+    bool passed;
+    const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+    if (fit) *fit = fit_bits(c, r, passed);
+    return k;
+}
+
+__device__ __forceinline__ uint64_t level_entry(int32_t rm, int n, int d, uint64_t key) {
+    return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
+           ((uint64_t)(63 - d) << 1) | (key & 1);
+}
+__device__ __forceinline__ int entry_idx(uint64_t e) { return kEntryIdxMax - (int)((e >> 7) & kEntryIdxMax); }
+__device__ __forceinline__ int entry_kind(uint64_t e) { return (e & 1) ? 2 : 1; }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Hand-off of 64-key lists between workgroups: write-through (sc1) 8-byte
+// stores drained before an agent-scope counter add, sc1 loads on the consumer
+// after its add returned (MI355X_MICROARCH.md, valid forms, table row 1).
+template <typename T>
+__device__ __forceinline__ void put_list(T* dst, T v) {
+    __hip_atomic_store(dst + (threadIdx.x & 63), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T get_list(const T* src) {
+    return __hip_atomic_load(src + (threadIdx.x & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+#ifndef KBHIP_GROUPS
+#define KBHIP_GROUPS 8
+#endif
+constexpr int kGroups = KBHIP_GROUPS;  // second-level merge groups (blockIdx % kGroups)
+static_assert(kGroups >= 1 && kGroups <= 32, "group lists and counters");
+constexpr int kCtrStride = 32;    // one counter per 128-byte line
+
+// Tree merge of the 8 per-wave lists in wl[] into wl[0] (all waves call).
+template <typename T>
+__device__ __forceinline__ void block_tree_merge(T (*wl)[64], int wave, int lane) {
+#pragma unroll
+    for (int s = kPopThreads / 128; s >= 1; s >>= 1) {
+        if (wave < s) wl[wave][lane] = wave_merge_desc(wl[wave][lane], wl[wave + s][lane]);
+        __syncthreads();
+    }
+}
+
+// Wave 0 of the final merger: K = lane's candidate key (sorted top-64).
+__device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                             const PopArgs& a, uint64_t K, PopOut* out) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    if (n >= 0) {
+        base = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    uint64_t pwc[4];  // ports after one or more commits of this class
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    uint64_t key = K;                                  // real key of the node after `ca + cp` commits
+    int32_t rm = K ? key_score(K) : 0;                 // running minimum of its scores
+    uint64_t cur = K ? level_entry(rm, n, 0, K) : 0;   // this lane's newest entry
+    uint64_t L = cur;                                  // sorted top-64 entries: lane p holds entry p
+    int ca = 0, cp = 0;
+    for (int d = 1; d < 64; ++d) {
+        const uint64_t T = readlane64(L, m - 1);       // m-th entry: deeper entries below it never place
+        if (!__ballot(cur != 0 && cur >= T)) break;
+        uint64_t e = 0;
+        if (key) {
+            if (key & 1) ++cp; else ++ca;              // the commit of the previous level (Pipeline / Allocate)
+            const Row r = apply_commits(base, c, ca, cp);
+            int32_t s;
+            bool passed;
+            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+            if (key) {
+                rm = key_score(key) < rm ? key_score(key) : rm;
+                e = level_entry(rm, n, d, key);
+            }
+        }
+        cur = e;
+        L = wave_merge_desc(L, wave_sort_desc(e >= T ? e : 0));  // entries below T cannot reach the top m
+    }
+    STAMP(gridDim.x * 4 + 2);
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const bool valid = lane < m && L != 0;
+    const uint64_t amask = __ballot(valid && entry_kind(L) == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!valid || !a.gang_mode || ready_p >= a.min_avail));
+    int done, stop;
+    if (smask) {
+        const int p = __ffsll((unsigned long long)smask) - 1;
+        done = p + 1;
+        stop = __builtin_amdgcn_readlane((int)valid, p) ? 2 : 1;
+    } else {
+        done = m;
+        stop = 0;
+    }
+    // commits of this lane's node among the placed entries; write the row back
+    int na = 0, np = 0;
+    for (int p = 0; p < done; ++p) {
+        const uint64_t e = readlane64(L, p);
+        if (e && entry_idx(e) == n) { if (entry_kind(e) == 1) ++na; else ++np; }
+    }
+    if (n >= 0 && na + np > 0) {
+        const Row r = apply_commits(base, c, na, np);
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+    }
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, L ? entry_kind(L) : 0, L ? entry_idx(L) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(gridDim.x * 4 + 3);
+}
+
+// ---------------------------------------------------------------------------
+// Placement by parallel levels (option "placement" = 2): the same entries as
+// place_levels, but a round computes 8 depths at once — wave w evaluates
+// candidate j after d = 8r + w commits of this class — then one sort + tree
+// merge of the round's 512 entries.  Commit kinds along a chain are
+// Allocate^a Pipeline^p (once Idle + Backfilled cannot fit, later commits
+// only touch Releasing), so a first pass assumes Allocate everywhere and the
+// depths behind a lane's first Pipeline are recomputed.  An entry is
+// (running min, index, depth) — a position's depth is the number of commits
+// its node already took — and a small LDS hash from node index to candidate
+// lane finds the candidate's commit kinds and counts.  Another round runs
+// only while some candidate's deepest entry still reaches the m-th entry.
+// ---------------------------------------------------------------------------
+// 64-bit: (rm biased) << 32 | (kEntryIdxMax - n) << 7 | (63 - d) << 1 | 1.
+// 32-bit (PopArgs::ent32): (rm - kbase + 1) << (kshift + 5) | (kidxmax - n) << 6 | (63 - d).
+template <typename ET>
+__device__ __forceinline__ ET depth_entry(int32_t rm, int n, int d, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8)
+        return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
+               ((uint64_t)(63 - d) << 1) | 1ull;
+    else
+        return ((uint32_t)(rm - a.kbase + 1) << (a.kshift + 5)) | ((uint32_t)(a.kidxmax - n) << 6) |
+               (uint32_t)(63 - d);
+}
+template <typename ET>
+__device__ __forceinline__ int entry_depth(ET e) {
+    if constexpr (sizeof(ET) == 8) return 63 - (int)((e >> 1) & 63);
+    else return 63 - (int)(e & 63);
+}
+template <typename ET>
+__device__ __forceinline__ int entry_node(ET e, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8) return entry_idx(e);
+    else return a.kidxmax - (int)((e >> 6) & (uint32_t)a.kidxmax);
+}
+template <typename T>
+__device__ __forceinline__ T readlane_t(T v, int l) {
+    if constexpr (sizeof(T) == 8) return readlane64(v, l);
+    else return (T)__builtin_amdgcn_readlane((int)v, l);
+}
+constexpr int kHash = 256;  // node index -> candidate lane (64 keys, open addressing)
+__device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 24); }
+
+// Rows of the nodes a placement may use, gathered before it starts (LDS):
+// the overlapped pop loads them while it waits for the previous pop, so the
+// placement reads no node row from memory.  Slot lookup by node index.
+constexpr int kRcSlots = 128;
+struct RowCache {
+    Row row[kRcSlots];
+    uint64_t pw[kRcSlots][4];
+    int32_t na[kRcSlots];
+    int32_t hkey[kHash];
+    int32_t hslot[kHash];
+};
+__device__ __forceinline__ void rc_insert(RowCache* rc, int n, int slot) {  // n distinct
+    int h = hash_slot(n);
+    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+    rc->hslot[h] = slot;
+}
+__device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
+    int h = hash_slot(n);
+    for (int i = 0; i < kHash; ++i, h = (h + 1) & (kHash - 1)) {
+        const int k = rc->hkey[h];
+        if (k == n) return rc->hslot[h];
+        if (k == -1) return -1;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ void fit_zero_other(uint32_t* arrive, int set) {
+    if (blockIdx.x == 0 && threadIdx.x < kGroups * 4)
+        fit_counters(arrive, 1 - set)[(threadIdx.x >> 2) * 32 + (threadIdx.x & 3)] = 0;
+}
+// Wave 0 of the final merger: lane 4g + b loads group g's count b (one round
+// trip, consumed only if a task finds no node: fit_sum).
+__device__ __forceinline__ uint32_t fit_load(const uint32_t* fitc, int n_groups) {
+    const int lane = threadIdx.x & 63;
+    uint32_t v = 0;
+    for (int gi = lane >> 2; gi < n_groups; gi += 16) v += ld_sc1(&fitc[gi * 32 + (lane & 3)]);
+    return v;
+}
+__device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b, b+4, ...
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    return v + __shfl_xor(v, 32, 64);
+}
+
+// SC1: rows read and written through sc1 (overlapped pops); the write-back is
+// then published as done = seq before the result stores.
+// L sorted descending over the lanes, e not in L: L with e inserted (the last
+// entry drops off).  A ballot gives the position, a DPP wave_shr:1 moves the tail.
+template <typename T>
+__device__ __forceinline__ T wave_shr1(T v) {  // lane i <- lane i - 1 (lane 0 <- 0)
+    if constexpr (sizeof(T) == 8) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
+        return ((uint64_t)hi << 32) | lo;
+    } else {
+        return (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+    }
+}
+template <typename T>
+__device__ __forceinline__ T wave_insert_sorted(T L, T e) {
+    const int lane = threadIdx.x & 63;
+    const int pos = __popcll(__ballot(L > e));
+    const T sh = wave_shr1(L);
+    return lane < pos ? L : (lane == pos ? e : sh);
+}
+
+// INS: the round's entries join the running list by insertion (only those
+// above the m-th entry; usually a few) instead of a sort + merge tree.
+// Running-minimum score of a placement entry.
+template <typename ET>
+__device__ __forceinline__ int32_t entry_rm(ET e, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8) return (int32_t)((uint32_t)(e >> 32) ^ 0x80000000u);
+    else return (int32_t)(e >> (a.kshift + 5)) - 1 + a.kbase;
+}
+// The rows a placement committed, compacted (persistent placer, kbhip_pp.hip).
+struct PPHistOut {
+    int32_t n;
+    int32_t node[64];
+    Row row[64];
+    uint64_t pw[64][4];
+};
+
+template <typename ET, bool SC1 = false, bool INS = false>
+__device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
+                               uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
+                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
+                               PPHistOut* ho = nullptr) {
+    // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
+    // (a node-array shard writes back only its own; one GPU: all of them).
+    // t0 (persistent placer): the candidates are exact down to the selection
+    // key t0 only — a node outside them may beat an entry below it — so the
+    // launch places the entries at or above it and leaves the rest of the
+    // chunk to the host (stop 0 with done < m; done 0 when none).  ho: the
+    // committed rows, compacted, for the placer's history.
+    // Node indices in keys and entries are global.
+    constexpr int kW = kPopThreads / 64;  // depths per round
+    __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
+    __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
+    __shared__ int32_t s_rm[2][64];       // running min through the previous round's deepest depth
+    __shared__ int32_t s_apos[64];        // first Pipeline depth (64: none yet)
+    __shared__ ET s_last[64];             // entry at the round's deepest depth
+    __shared__ int32_t s_cnt[64];
+    __shared__ int32_t s_hkey[kHash];
+    __shared__ int32_t s_hlane[kHash];
+    __shared__ int s_more;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t K = wl64[0][lane];
+    ET (*wl)[64] = (ET (*)[64])wl64;      // sort / merge lists of entries (same LDS)
+    const int n = K ? key_idx(K) : -1;
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
+    if (rslot >= 0) {
+        base = rc->row[rslot];
+        for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
+        na_n = rc->na[rslot];
+    } else if (n >= 0) {
+        base = load_row_t<SC1>(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    STAMP(gridDim.x * 4 + 11); PSTAMP(1);
+    uint64_t pwc[4];
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
+    if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
+    __syncthreads();  // K read by every wave; wl free
+    STAMP(gridDim.x * 4 + 12); PSTAMP(2);
+    if (wave == 0 && n >= 0) {  // candidate nodes are distinct
+        int h = hash_slot(n);
+        while (atomicCAS(&s_hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+        s_hlane[h] = lane;
+    }
+    STAMP(gridDim.x * 4 + 5); PSTAMP(3);
+    auto eval_at = [&](int d, int ap, int32_t* sc) -> int {  // kind of commit d+1's key (0: infeasible)
+        if (d == 0) { *sc = key_score(K); return key_kind(K); }
+        const int na = d < ap ? d : ap;
+        const Row r = apply_commits(base, c, na, d - na);
+        int32_t s;
+        bool passed;
+        const uint64_t k = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+        *sc = k ? key_score(k) : 0;
+        return k ? key_kind(k) : 0;
+    };
+    ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
+    bool alive = n >= 0; // candidate still relevant (uniform over waves)
+    for (int r = 0; r < 64 / kW; ++r) {
+        const int d = r * kW + wave;
+        int ap = s_apos[lane];
+        int32_t sc = 0;
+        int kind = alive ? eval_at(d, ap, &sc) : 0;
+        s_kind[d][lane] = (uint8_t)kind;
+        __syncthreads();
+        if (ap == 64) {  // first Pipeline within this round: recompute the depths behind it
+            // (no barrier before the rewrites below: they only touch depths
+            // after the first Pipeline, which every scan stops at)
+            for (int w2 = 0; w2 < kW; ++w2)
+                if (s_kind[r * kW + w2][lane] == 2) { ap = r * kW + w2; break; }
+            if (alive && ap < d) {
+                kind = eval_at(d, ap, &sc);
+                s_kind[d][lane] = (uint8_t)kind;
+            }
+        }
+        s_sc[wave][lane] = sc;
+        if (wave == 0) s_apos[lane] = ap;
+        __syncthreads();
+        // running minimum through depth d; the chain ends at the first infeasible depth
+        bool ok = alive;
+        int32_t rm = r == 0 ? INT32_MAX : s_rm[r & 1][lane];
+#pragma unroll
+        for (int w2 = 0; w2 < kW; ++w2) {
+            if (w2 > wave) break;
+            ok = ok && s_kind[r * kW + w2][lane] != 0;
+            const int32_t x = s_sc[w2][lane];
+            rm = x < rm ? x : rm;
+        }
+        const ET e = ok ? depth_entry<ET>(rm, n, d, a) : (ET)0;
+        if (r == 0) { STAMP(gridDim.x * 4 + 6); PSTAMP(4); }
+        if (wave == kW - 1) { s_last[lane] = e; s_rm[(r + 1) & 1][lane] = rm; }
+        if constexpr (INS) {
+            wl[wave][lane] = e;
+            __syncthreads();
+            if (wave == 0) {
+                // depth 0 (round 0, wave 0): the candidate list itself, already sorted
+                int w0 = 0;
+                if (r == 0) { L = e; w0 = 1; }
+                ET T = readlane_t(L, m - 1);
+                for (int w2 = w0; w2 < kW; ++w2) {
+                    const ET x = wl[w2][lane];
+                    for (uint64_t q = __ballot(x > T); q; q &= q - 1) {
+                        const ET y = readlane_t(x, __ffsll((unsigned long long)q) - 1);
+                        if (y > T) {
+                            L = wave_insert_sorted(L, y);
+                            T = readlane_t(L, m - 1);
+                        }
+                    }
+                }
+            }
+        } else {
+            wl[wave][lane] = wave_sort_desc(e);
+            __syncthreads();
+            block_tree_merge(wl, wave, lane);
+            if (wave == 0) L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
+        }
+        if (wave == 0) {
+            if (r == 0) { STAMP(gridDim.x * 4 + 7); PSTAMP(5); }
+            const ET T = readlane_t(L, m - 1);  // m-th entry: deeper entries below it never place
+            const ET le = s_last[lane];
+            const bool more = le != 0 && le >= T;
+            const bool any = __ballot(more) != 0;  // all 64 lanes active
+            if (lane == 0) s_more = any;
+            s_last[lane] = more;  // reused as the alive flag of the next round
+        }
+        __syncthreads();
+        if (!s_more) break;
+        alive = s_last[lane] != 0;  // rewritten by wave kW-1 only after the next round's first barrier
+    }
+    if (wave != 0) return;
+    STAMP(gridDim.x * 4 + 2); PSTAMP(6);
+    // commit kind of each position: its node's candidate lane, the entry's depth
+    const bool inm = lane < m && L != 0;
+    int lf = 0;
+    if (inm) {
+        const int ni = entry_node(L, a);
+        int h = hash_slot(ni);
+        while (s_hkey[h] != ni) h = (h + 1) & (kHash - 1);
+        lf = s_hlane[h];
+    }
+    const int kind = inm ? s_kind[entry_depth(L)][lf] : 0;
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
+    int cap = m;  // positions decided exactly (a prefix: the entries are sorted)
+    if (t0) {
+        const int32_t s0 = key_score(t0);
+        const int i0 = key_idx(t0);
+        const int32_t rm = inm ? entry_rm<ET>(L, a) : 0;
+        const bool ex = inm && (rm > s0 || (rm == s0 && entry_node(L, a) <= i0));
+        cap = __popcll(__ballot(ex && lane < m));
+    }
+    int done, stop;
+    const int p0 = smask ? __ffsll((unsigned long long)smask) - 1 : 64;
+    if (p0 < cap) {
+        done = p0 + 1;
+        stop = __builtin_amdgcn_readlane((int)inm, p0) ? 2 : 1;
+    } else {
+        done = cap;  // cap == m: every task placed, the pop goes on (stop 0)
+        stop = 0;
+    }
+    STAMP(gridDim.x * 4 + 8); PSTAMP(7);
+    if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
+    __builtin_amdgcn_wave_barrier();
+    const int cc = s_cnt[lane];
+    STAMP(gridDim.x * 4 + 9); PSTAMP(8);
+    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
+        // fit_in: every node at the state this pop started from; the candidates
+        // then carry the commits made before the failing task
+        uint32_t fb_base = 0, fb_post = 0;
+        if (n >= 0) {
+            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
+            const int ap = s_apos[lane];
+            const int na = cc < ap ? cc : ap;
+            const Row r = apply_commits(base, c, na, cc - na);
+            int32_t sc;
+            bool passed;
+            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
+            fb_post = fit_bits(c, r, passed);
+        }
+        const uint32_t sweep = fit_sum(fit_raw);
+        int32_t tot[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+        if (lane == 0) {
+            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const int ln = n - wb_base;  // local row of the written-back node
+    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
+        const int ap = s_apos[lane];
+        const int na = cc < ap ? cc : ap;
+        const Row r = apply_commits(base, c, na, cc - na);
+        if constexpr (SC1) {
+            st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
+            st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
+            st_sc1(&nc.pods[ln], r.pods);
+            st_sc1(&nc.nzc[ln], r.nzc);
+            st_sc1(&nc.nzm[ln], r.nzm);
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
+        } else {
+            nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
+            nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
+            nc.pods[ln] = r.pods;
+            nc.nzc[ln] = r.nzc;
+            nc.nzm[ln] = r.nzm;
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
+        }
+    }
+    if (ho) {  // committed rows, compacted (lane order)
+        const bool wr = n >= 0 && cc > 0;
+        const uint64_t wm = __ballot(wr);
+        if (wr) {
+            const int pos = __popcll(wm & ((1ull << lane) - 1));
+            const int ap = s_apos[lane];
+            const int na = cc < ap ? cc : ap;
+            ho->node[pos] = n;
+            ho->row[pos] = apply_commits(base, c, na, cc - na);
+            for (int w = 0; w < 4; ++w) ho->pw[pos][w] = pwc[w];
+        }
+        if (lane == 0) ho->n = __popcll(wm);
+    }
+    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_sc1(done_flag, seq);
+    }
+    if (lane < done || (done == 0 && lane == 0))
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, lane < done ? kind : 0,
+                                                       (lane < done && inm) ? entry_node(L, a) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    STAMP(gridDim.x * 4 + 3); PSTAMP(9);
+}
+
+
+// ---------------------------------------------------------------------------
+// Placement by insertion (option "placement" = 4): one wave, no sort
+// networks.  The greedy order is the descending order of the entries
+// e(j, d) = (running min of node j's scores over depths 0..d, index, depth)
+// (see place_levels).  The depth-0 entries are the sorted candidate list
+// itself; a node's entries decrease with depth, so the top-m entries hold a
+// prefix of each node's sequence.  Rounds: every lane whose newest entry is
+// still among the top m evaluates its next depth (its own row, its own
+// Allocate^a Pipeline^p chain, no fix-ups); new entries above the m-th are
+// inserted into the sorted list one at a time (a ballot gives the position,
+// a DPP wave shift moves the tail).  A round that inserts nothing ends it —
+// typically after one or two rounds, as a commit lowers a node's score.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v) {  // lane i <- lane i - 1 (lane 0 <- 0)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+// L sorted descending over the lanes, e not in L: L with e inserted (the last entry drops off).
+__device__ __forceinline__ uint64_t wave_insert_desc(uint64_t L, uint64_t e) {
+    const int lane = threadIdx.x & 63;
+    const int pos = __popcll(__ballot(L > e));
+    const uint64_t sh = wave_shr1_64(L);
+    return lane < pos ? L : (lane == pos ? e : sh);
+}
+
+template <bool SC1 = false>
+__device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                             const PopArgs& a, PopOut* out, uint64_t K, uint32_t* done_flag = nullptr,
+                             uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
+                             uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;  // global node index (keys are global)
+    Row base{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
+    if (rslot >= 0) {
+        base = rc->row[rslot];
+        for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
+        na_n = rc->na[rslot];
+    } else if (n >= 0) {
+        base = load_row_t<SC1>(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    uint64_t pwc[4];  // ports after one or more commits of this class
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    const int m = a.n_tasks;
+    // this lane's chain: depth d of its newest entry, commits by kind behind it, first Pipeline depth
+    int d = 0, ca = 0, cp = 0, apos = 64;
+    uint64_t key = K;  // key at depth d (its kind is the kind of commit d + 1)
+    int32_t rm = K ? key_score(K) : 0;
+    uint64_t last = K ? level_entry(rm, n, 0, K) : 0;  // newest entry
+    uint64_t L = last;  // lane p: entry p of the sorted top entries (depth-0 entries are the sorted list)
+    uint64_t T = readlane64(L, m - 1);
+    for (int round = 1; round < 64; ++round) {
+        const bool act = last != 0 && last >= T;  // its newest entry is among the top m
+        if (!__ballot(act)) break;
+        uint64_t e = 0;
+        if (act) {
+            if (key & 1) { ++cp; if (apos == 64) apos = d; } else ++ca;  // commit d + 1 takes the depth-d kind
+            ++d;
+            const Row r = apply_commits(base, c, ca, cp);
+            int32_t s;
+            bool passed;
+            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
+            if (key) {
+                rm = key_score(key) < rm ? key_score(key) : rm;
+                e = level_entry(rm, n, d, key);
+            }
+            last = e;
+        }
+        // insert the new entries that beat the m-th (T only rises: one below it never enters)
+        for (uint64_t q = __ballot(e != 0 && e > T); q; q &= q - 1) {
+            const uint64_t x = readlane64(e, __ffsll((unsigned long long)q) - 1);
+            if (x > T) {
+                L = wave_insert_desc(L, x);
+                T = readlane64(L, m - 1);
+            }
+        }
+    }
+    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
+    const bool inm = lane < m && L != 0;
+    const int kind = inm ? entry_kind(L) : 0;
+    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
+    int done, stop;
+    if (smask) {
+        const int p = __ffsll((unsigned long long)smask) - 1;
+        done = p + 1;
+        stop = __builtin_amdgcn_readlane((int)inm, p) ? 2 : 1;
+    } else {
+        done = m;
+        stop = 0;
+    }
+    // commits of this lane's node among the placed entries
+    int cc = 0;
+    for (int p = 0; p < done; ++p) {
+        const uint64_t x = readlane64(L, p);
+        cc += (x != 0 && entry_idx(x) == n) ? 1 : 0;
+    }
+    const int nal = cc < apos ? cc : apos;  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
+    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
+        uint32_t fb_base = 0, fb_post = 0;
+        if (n >= 0) {
+            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
+            const Row r = apply_commits(base, c, nal, cc - nal);
+            int32_t sc;
+            bool passed;
+            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
+            fb_post = fit_bits(c, r, passed);
+        }
+        const uint32_t sweep = fit_sum(fit_raw);
+        int32_t tot[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+        if (lane == 0) {
+            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const int ln = n - wb_base;
+    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {
+        const Row r = apply_commits(base, c, nal, cc - nal);
+        if constexpr (SC1) {
+            st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
+            st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
+            st_sc1(&nc.pods[ln], r.pods);
+            st_sc1(&nc.nzc[ln], r.nzc);
+            st_sc1(&nc.nzm[ln], r.nzm);
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
+        } else {
+            nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
+            nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
+            nc.pods[ln] = r.pods;
+            nc.nzc[ln] = r.nzc;
+            nc.nzm[ln] = r.nzm;
+            if (c.has_ports)
+                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
+        }
+    }
+    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) st_sc1(done_flag, seq);
+    }
+    if (lane < done)
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_idx(L) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ---------------------------------------------------------------------------
+// Placement of a session with Backfilled nodes (placement 6; one wave, task
+// after task).  Visiting a node in a walk adds its Backfilled to its Idle
+// (GetAccessibleResource, node_info.go:209-211; allocate.go:150-180): every
+// node ahead of the winner in the walk order, and the winner itself, before
+// its commit.  So nodes other than the winner change between the pop's tasks,
+// and the entry order of the other placements does not hold.  Lane j holds
+// candidate j of the sweep's list — the top 64 of the walk keys of nodes that
+// fit or carry Backfilled (eval_node_walk) — with its row; per task:
+//   winner  = the largest current key (fitting nodes: walk key + kind);
+//   visited = lanes whose walk key is above the winner's (only nodes with
+//             Backfilled change);
+// exact while the winner's walk key is at least the list's last one (every
+// node above it that could be visited or win is in the list; nodes outside
+// do not change).  Otherwise the launch ends before that task (done < m,
+// stop 0; done = 0 asks the host for the general path for one task), and a
+// task that finds no node is left to the general path too (its walk covers
+// every node and reports the FitDelta histogram).
+// ---------------------------------------------------------------------------
+__device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                         const PopArgs& a, PopOut* out, uint64_t K) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;
+    Row r{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    if (n >= 0) {
+        r = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    const bool has_bf = (r.bf_cpu | r.bf_mem | r.bf_gpu) != 0;
+    const uint64_t t0w = readlane64(K, 63) >> 1;  // walk key of the list's last entry (0: the list holds all)
+    int32_t s = 0;
+    bool passed = false;
+    uint64_t key = n >= 0 ? dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed) : 0;
+    uint64_t wk = (n >= 0 && passed) ? pack_key(s, n, 0) >> 1 : 0;  // walk key (0: not in the walk)
+    bool changed = false;
+    int ready = a.ready_count, done = 0, stop = 0;
+    uint64_t mine = 0;  // lane i: winner key of task i
+    for (int i = 0; i < a.n_tasks; ++i) {
+        const uint64_t w = wave_max_key(key);
+        if (!w || (w >> 1) < t0w) break;  // no node, or one outside the list may come first: the host goes on
+        if (lane == i) mine = w;
+        const bool win = n >= 0 && key == w;
+        const bool visit = has_bf && (win || wk > (w >> 1));
+        if (visit) { r.idle_cpu += r.bf_cpu; r.idle_mem += r.bf_mem; r.idle_gpu += r.bf_gpu; }
+        const int kind = key_kind(w);
+        if (win) {
+            r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
+            if (c.has_ports)
+                for (int q = 0; q < 4; ++q) pw[q] |= (q < nc.port_words) ? t.masks[c.pown_off + q] : 0;
+        }
+        if (visit || win) {
+            changed = true;
+            key = dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed);
+            wk = passed ? pack_key(s, n, 0) >> 1 : 0;
+        }
+        done = i + 1;
+        if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+        if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
+    }
+    if (changed) {
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pw[w];
+    }
+    if (lane < done || (done == 0 && lane == 0))
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
+// writes this shard's top-64 with their rows and the sweep's FitDelta counts.
+__device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
+                           uint32_t fit_raw, ShardMsg* msg) {
+    const int lane = threadIdx.x & 63;
+    ShardCand e{};
+    e.node = -1;
+    if (K) {
+        const int g = key_idx(K);
+        const int n = g - nc.base;
+        e.key = K;
+        e.node = g;
+        e.row = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) e.pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+    }
+    msg->c[lane] = e;
+    const uint32_t sweep = fit_sum(fit_raw);
+    if (lane < 4) msg->fit[lane] = sweep;
+}
+}  // namespace kbhip

@@ -64,6 +64,24 @@ struct KeyFormat {
     int32_t base = 0, shift = 0, idxmax = 0;
 };
 struct ShardMsg;  // kbhip_eval.h
+// Persistent placer (kbhip_pp.hip, option "pp"): sizes of its device records,
+// the per-pop sweep (command `seq` into ring slot seq % pp_slots(); lists,
+// arrive and fitw are that slot's), the placer (one resident workgroup from
+// command seq0 on; it leaves on a STOP command or after 20 ms without one and
+// records in the pinned mapped host record where it stopped) and STOP.
+size_t pp_slot_bytes();
+size_t pp_ctrl_bytes();
+size_t pp_host_bytes();
+int pp_slots();
+size_t pp_list_keys(int n_nodes);
+size_t pp_arrive_words();
+hipError_t launch_pp_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
+                           int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
+                           void* ring, void* lists, uint32_t* arrive, uint32_t* fitw, const void* ctrl, uint32_t seq,
+                           uint32_t out_slot, hipStream_t st);
+hipError_t launch_pp_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, void* ring, void* ctrl, void* outs,
+                            const uint32_t* fitw, int64_t fitw_words, void* host, uint32_t seq0, hipStream_t st);
+hipError_t launch_pp_stop(void* ring, uint32_t seq, hipStream_t st);
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 // placement 3 (node-array shards): no placement; the shard's top-64 with rows

@@ -235,6 +235,38 @@ class MemPool {
         std::lock_guard<std::mutex> lk(mu_);
         streams_.emplace(dev, st);
     }
+    // A stream on a hardware queue of its own: created with a CU mask (a queue
+    // property, so the runtime never shares it with other streams, whose
+    // queues it round-robins once GPU_MAX_HW_QUEUES are in use).  The
+    // persistent placer runs there: a resident kernel on a shared queue would
+    // hold back every launch queued behind it.
+    hipStream_t take_own_queue_stream() {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (!off_) {
+            std::lock_guard<std::mutex> lk(mu_);
+            auto it = own_streams_.find(dev);
+            if (it != own_streams_.end()) {
+                hipStream_t st = it->second;
+                own_streams_.erase(it);
+                return st;
+            }
+        }
+        uint32_t mask[8] = {0xffu, 0, 0, 0, 0, 0, 0, 0};  // 8 CUs: the placer is one workgroup
+        hipStream_t st = nullptr;
+        if (hipExtStreamCreateWithCUMask(&st, 8, mask) != hipSuccess)
+            throw Error(KBHIP_ENODEV, "hipExtStreamCreateWithCUMask failed");
+        return st;
+    }
+    void give_own_queue_stream(hipStream_t st, int dev) {
+        if (!st) return;
+        if (off_) {
+            (void)hipStreamDestroy(st);
+            return;
+        }
+        std::lock_guard<std::mutex> lk(mu_);
+        own_streams_.emplace(dev, st);
+    }
     void trim() {
         std::lock_guard<std::mutex> lk(mu_);
         for (auto& kv : free_) release((Kind)std::get<1>(kv.first), kv.second);
@@ -251,7 +283,7 @@ class MemPool {
     static constexpr size_t kCap = size_t(8) << 30;
     std::mutex mu_;
     std::multimap<std::tuple<int, int, size_t>, void*> free_;
-    std::multimap<int, hipStream_t> streams_;
+    std::multimap<int, hipStream_t> streams_, own_streams_;
     size_t cached_ = 0;
     const bool off_;
 };
@@ -371,6 +403,21 @@ struct Session {
     uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
+    // persistent placer (kbhip_pp.hip): option "pp"; used by kbhip_allocate's pop loop
+    int pp = 0;                 // off by default: per pop it measured slower than the overlapped kernel
+                                // (C4-scaled 16.8 vs 12.5 us; profiles/r02_pp_profile.txt)
+    bool pp_active = false;     // inside Allocator::run
+    bool pp_running = false;    // a placer was launched and has not been stopped
+    bool pp_skip = false;       // the next batched launch goes without the placer (after a pop it could not start)
+    uint32_t pp_seq = 0;        // last command posted
+    uint32_t pp_next_stream = 0;
+    hipStream_t pp_stream = nullptr;
+    DevBuf b_pp_ring, b_pp_ctrl, b_pp_lists, b_pp_arrive, b_pp_fitw;
+    uint32_t* h_pp = nullptr;   // pinned, mapped: [0] command the placer stopped at, [1] exited
+    void* d_pp = nullptr;
+    size_t h_pp_cap = 0;
+    size_t pp_list_stride = 0;  // keys per ring slot
+    int64_t pp_fitw_words = 0;  // nibble words per ring slot
     int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
     bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
     DevBuf b_fit4;
@@ -441,6 +488,12 @@ struct Session {
     // Device side of the teardown: drain the streams, then hand streams, pinned
     // and device buffers back to the pool.  Idempotent.
     void release_device() {
+        if (pp_running && stream) {  // the placer leaves on a STOP command (or 20 ms without one)
+            (void)launch_pp_stop(b_pp_ring.p, ++pp_seq, stream);
+            (void)hipStreamSynchronize(pp_stream);
+            pp_running = false;
+        }
+        if (pp_stream) (void)hipStreamSynchronize(pp_stream);
         for (int k = 1; k <= kMaxDep; ++k)
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -454,6 +507,11 @@ struct Session {
         if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
         if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
+        if (h_pp) MemPool::get().give(MemPool::kPinnedMapped, h_pp, h_pp_cap, device);
+        h_pp = nullptr;
+        MemPool::get().give_own_queue_stream(pp_stream, device);
+        pp_stream = nullptr;
+        for (DevBuf* b : {&b_pp_ring, &b_pp_ctrl, &b_pp_lists, &b_pp_arrive, &b_pp_fitw}) b->release();
         h_rank = nullptr;
         h_ctrl = nullptr;
         h_out = nullptr;
@@ -1502,15 +1560,91 @@ struct BatchLaunch {
     hipStream_t st = nullptr;
     bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
     bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
+    bool pp = false;   // through the persistent placer: may end before its first task (n_done 0)
+    uint32_t pp_seq = 0;
 };
 
-// Wait until no overlapped pop can still run (before device work that is not
-// an overlapped pop, which the device chain does not order).
-static void ov_quiesce(Session& S) {
+// Wait until no overlapped pop can still run.
+static void ov_drain(Session& S) {
     if (!S.ov_pending) return;
     for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
     S.ov_pending = false;
+}
+
+// ---------------------------------------------------------------------------
+// persistent placer (kbhip_pp.hip): commands are numbered from 1 in the
+// session (PPCtrl::written counts them); a run of kbhip_allocate's batched
+// pops posts one sweep per pop, the placer (launched at the run's first pop)
+// places them in order; the run ends with a STOP.
+// ---------------------------------------------------------------------------
+static void pp_init(Session& S) {
+    if (S.b_pp_ring.p) return;
+    const int Q = pp_slots();
+    S.b_pp_ring.alloc<uint8_t>(pp_slot_bytes() * Q);
+    S.b_pp_ctrl.alloc<uint8_t>(pp_ctrl_bytes());
+    S.pp_list_stride = pp_list_keys(S.nc.n);
+    S.b_pp_lists.alloc<uint64_t>(S.pp_list_stride * Q);
+    S.b_pp_arrive.alloc<uint32_t>(pp_arrive_words() * Q);
+    S.pp_fitw_words = (S.nc.n + 7) / 8 + 1;
+    S.b_pp_fitw.alloc<uint32_t>((size_t)S.pp_fitw_words * Q);
+    HIPCHK(hipMemsetAsync(S.b_pp_ring.p, 0, pp_slot_bytes() * Q, S.stream));
+    HIPCHK(hipMemsetAsync(S.b_pp_ctrl.p, 0, pp_ctrl_bytes(), S.stream));
+    HIPCHK(hipMemsetAsync(S.b_pp_arrive.p, 0, pp_arrive_words() * Q * sizeof(uint32_t), S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    S.h_pp = (uint32_t*)MemPool::get().take(MemPool::kPinnedMapped, pp_host_bytes(), &S.h_pp_cap);
+    std::memset(S.h_pp, 0, pp_host_bytes());
+    HIPCHK(hipHostGetDevicePointer(&S.d_pp, S.h_pp, 0));
+    S.pp_stream = MemPool::get().take_own_queue_stream();
+}
+// Launch the placer at command seq0; fresh: no command before seq0 is in
+// flight (every row is in memory), so the progress counter is set to seq0 - 1.
+static void pp_launch(Session& S, uint32_t seq0, bool fresh) {
+    if (fresh) {
+        const uint32_t w = seq0 - 1;
+        HIPCHK(hipMemcpyAsync(S.b_pp_ctrl.p, &w, sizeof(w), hipMemcpyHostToDevice, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+    }
+    __atomic_store_n(&S.h_pp[1], 0u, __ATOMIC_RELEASE);
+    HIPCHK(launch_pp_placer(S.conf, S.nc, S.tab, S.b_pp_ring.p, S.b_pp_ctrl.p, S.d_out, (const uint32_t*)S.b_pp_fitw.p,
+                            S.pp_fitw_words, S.d_pp, seq0, S.pp_stream));
+    S.pp_running = true;
+}
+static void pp_stop(Session& S) {
+    if (!S.pp_running) return;
+    const uint32_t e = ++S.pp_seq;
+    HIPCHK(launch_pp_stop(S.b_pp_ring.p, e, S.stream));
+    HIPCHK(hipStreamSynchronize(S.pp_stream));  // the placer left (at this STOP, or idle before it)
+    for (int k = 0; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
+    S.pp_running = false;
+    static const bool prof = std::getenv("KBHIP_PP_PROFILE") != nullptr;  // development aid
+    if (prof) {
+        uint64_t pr[8];
+        HIPCHK(hipMemcpy(pr, (char*)S.b_pp_ctrl.p + 64, sizeof(pr), hipMemcpyDeviceToHost));
+        const double n = pr[6] ? (double)pr[6] : 1.0;
+        std::fprintf(stderr, "pp: %llu pops, us/pop wait %.2f list+dirty %.2f keys+merge %.2f rows %.2f place %.2f tail %.2f\n",
+                     (unsigned long long)pr[6], pr[0] / n / 100, pr[1] / n / 100, pr[2] / n / 100, pr[3] / n / 100,
+                     pr[4] / n / 100, pr[5] / n / 100);
+        uint64_t pp[16];
+        HIPCHK(hipMemcpy(pp, (char*)S.b_pp_ctrl.p + 128, sizeof(pp), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "pp place: us/pop");
+        for (int k = 1; k <= 9; ++k) std::fprintf(stderr, " [%d] %.2f", k, pp[k] / n / 100);
+        std::fprintf(stderr, "\n");
+        HIPCHK(hipMemset((char*)S.b_pp_ctrl.p + 64, 0, sizeof(pr) + sizeof(pp)));
+    }
+}
+// The placer left idle while command e was outstanding: start it again there.
+static void pp_revive(Session& S) {
+    if (!S.pp_running || !__atomic_load_n(&S.h_pp[1], __ATOMIC_ACQUIRE)) return;
+    HIPCHK(hipStreamSynchronize(S.pp_stream));
+    pp_launch(S, __atomic_load_n(&S.h_pp[0], __ATOMIC_ACQUIRE), false);
+}
+
+// Wait until no batched pop can still run (before device work that is not a
+// batched pop, which neither the overlap chain nor the placer orders).
+static void ov_quiesce(Session& S) {
+    pp_stop(S);
+    ov_drain(S);
 }
 
 // Nothing but the winner's row can change between the chunk's tasks: the
@@ -1573,8 +1707,32 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.ev_used[k] = true;
     }
     L.bf = S.any_bf != 0;
+    L.pp = S.pp_active && S.pp && !S.pp_skip && S.placement >= 2 && S.world == 1 && !L.bf;
+    S.pp_skip = false;
+    if (L.pp) {  // one sweep per pop, any stream; the resident placer places them in order
+        ov_drain(S);
+        pp_init(S);
+        if (!S.pp_running) pp_launch(S, S.pp_seq + 1, true);
+        const uint32_t e = ++S.pp_seq;
+        L.pp_seq = e;
+        const int Q = pp_slots();
+        L.st = S.ov_streams[S.pp_next_stream++ % (kMaxDep + 1)];
+        L.fit = true;
+        auto tl0 = std::chrono::steady_clock::now();
+        if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
+        const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
+        HIPCHK(launch_pp_sweep(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
+                               S.b_pp_ring.p, (uint64_t*)S.b_pp_lists.p + (e % Q) * S.pp_list_stride,
+                               (uint32_t*)S.b_pp_arrive.p + (e % Q) * pp_arrive_words(),
+                               (uint32_t*)S.b_pp_fitw.p + (e % Q) * S.pp_fitw_words, S.b_pp_ctrl.p, e,
+                               (uint32_t)L.slot, L.st));
+        if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));
+        S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
+        return L;
+    }
     const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1 && !L.bf;
     if (!ov) ov_quiesce(S);
+    else pp_stop(S);
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
@@ -1626,6 +1784,10 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
             while (got < n_done && tag(load(got)) == L.epoch) ++got;
             if (got == n_done) break;
         }
+        if (L.pp && (spin & 4095) == 4095 && __atomic_load_n(&S.h_pp[1], __ATOMIC_ACQUIRE)) {
+            pp_revive(S);  // the placer left idle before this pop's sweep was posted
+            spin = 0;
+        }
         if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(L.st));  // long waits: runtime
         if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
         __builtin_ia32_pause();
@@ -1633,7 +1795,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
     S.stats.sweeps += 1;
     S.stats.batched_pops += 1;
-    if (n_done < (L.bf ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+    if (n_done < (L.bf || L.pp ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
     for (int j = 0; j < n_done; ++j) {
         const uint64_t g = load(j);
         res_node[j] = (int32_t)(g & 0xffffffffu) - 1;
@@ -1641,6 +1803,13 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     }
     *n_done_out = n_done;
     *stop_out = (int)((load(0) >> 44) & 0xf) - 1;
+    static const bool ppdbg = std::getenv("KBHIP_PP_DEBUG") != nullptr;  // development aid
+    if (ppdbg) {
+        std::fprintf(stderr, "launch pp %d seq %u cls %d m %d done %d stop %d:", (int)L.pp, L.pp_seq, L.cls, L.m, n_done,
+                     *stop_out);
+        for (int j = 0; j < n_done; ++j) std::fprintf(stderr, " %d/%d", res_node[j], res_kind[j]);
+        std::fprintf(stderr, "\n");
+    }
     S.last_fit_ok = false;
     if (*stop_out == KBHIP_STOP_UNASSIGNED && L.fit) {
         uint64_t f0 = 0, f1 = 0;
@@ -1739,6 +1908,11 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             // one launch: sweep + per-block top-64 + merge + placement of the chunk
             const BatchLaunch L = launch_batched(S, cls0, m, gang_mode, min_avail, ready_count);
             collect_batched(S, L, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf);
+            if (n_done == 0 && L.pp) {  // the placer could not start this chunk: once more without it
+                S.stats.pp_retries++;
+                S.pp_skip = true;
+                continue;
+            }
             if (n_done == 0) {  // placement 6 could not place the first task exactly: general path for it
                 batch = false;
                 m = 1;
@@ -2128,6 +2302,7 @@ struct Allocator {
         const int gm = S.gang_ready ? 1 : 0;
         if (!S.ev_run[0]) { HIPCHK(hipEventCreate(&S.ev_run[0])); HIPCHK(hipEventCreate(&S.ev_run[1])); }
         ov_quiesce(S);
+        S.pp_active = S.world == 1;
         HIPCHK(hipEventRecord(S.ev_run[0], S.stream));
         auto build_pending = [&](HJob& job) {  // allocate.go:91-104; TaskOrderFn is a strict total order
             if (job.pending_built) return;
@@ -2411,6 +2586,7 @@ struct Allocator {
         }
         discard_all();  // predicted pops that never came
         ov_quiesce(S);
+        S.pp_active = false;
         ev_harvest_all(S);
         HIPCHK(hipEventRecord(S.ev_run[1], S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
@@ -3379,6 +3555,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
+        else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
             s->s.rank_first = (int)std::min<int64_t>(value, 1 << 20);

@@ -46,7 +46,8 @@ class Stats(ctypes.Structure):
                 ("timed_launches", ctypes.c_int64), ("host_launch_s", ctypes.c_double),
                 ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
-                ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64)]
+                ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64),
+                ("pp_retries", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
