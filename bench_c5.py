@@ -7,7 +7,8 @@ p50 session latency, per-action wall times, records (evictions, pipelines,
 allocations) per session, and the node-ranking sweeps (one per reclaim /
 preempt task) with their mean wall time.
 
-Usage: python bench_c5.py [--sessions S] [--warmup W] [--nodes N] [--pending T]
+Usage: python bench_c5.py [--sessions S] [--warmup W] [--nodes N] [--pending T] [--concurrent C]
+(--concurrent 1: one session at a time with per-action wall times)
 """
 import argparse
 import json
@@ -32,6 +33,8 @@ def main():
     ap.add_argument("--pending", type=int, default=2000)
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the hoisted CPU restatement on one session")
+    ap.add_argument("--concurrent", type=int, default=8,
+                    help="what-if sessions in flight (host threads); their node rankings share launches")
     args = ap.parse_args()
     os.makedirs(args.cache, exist_ok=True)
     bufs = []
@@ -44,6 +47,8 @@ def main():
         with open(p, "rb") as f:
             bufs.append(f.read())
     lat, phases, recs, sweeps = [], {a: [] for a in ("open",) + ACTIONS + ("close",)}, [], []
+    if args.concurrent > 1:
+        return concurrent(args, bufs)
     for k, buf in enumerate(bufs):
         t0 = time.perf_counter()
         s = kbhip.Session(buf, device=0)
@@ -104,6 +109,84 @@ def main():
         st = {}
         pl = oracle.fast_allocate(p0, threads=threads, actions=", ".join(ACTIONS), stats=st)
         sess_s = st["open_s"] + st["allocate_s"]  # plugin open + the four actions (snapshot load excluded)
+        out["cpu_baseline"] = {"value": 1.0 / sess_s, "unit": "sessions/s", "cores": threads, "kind": "port",
+                               "sample": f"one C5 session ({len(pl)} records), actions {', '.join(ACTIONS)}, "
+                                         f"hoisted C++ restatement oracle/kbfast.cpp, {threads} threads on "
+                                         f"{os.cpu_count()} host cpus, snapshot parse excluded"}
+    print(json.dumps(out))
+
+
+def one_session(buf, group, barrier=None):
+    t0 = time.perf_counter()
+    s = kbhip.Session(buf, device=0)
+    if group:
+        s.set_option("rank_group", 1)
+    if barrier is not None:
+        barrier.wait()
+    counts = {1: 0, 2: 0, 3: 0}
+    for a in ACTIONS:
+        _, _, kind = getattr(s, a)()
+        for v in kind.tolist():
+            counts[v] += 1
+    st = s.stats()
+    s.close()
+    return time.perf_counter() - t0, counts, st
+
+
+def concurrent(args, bufs):
+    """S what-if sessions in flight from S host threads (the engine releases the
+    GIL); their reclaim / preempt node rankings are batched into shared
+    launches (option rank_group, kbhip_session.cpp RankBatcher)."""
+    from concurrent.futures import ThreadPoolExecutor
+    # the sessions of one wave of `concurrent` start together (a barrier after
+    # their opens), as a what-if sweep over one cluster state would
+    warm, timed = bufs[:args.warmup], bufs[args.warmup:]
+    import threading
+
+    def waves(ex, bs):
+        out = []
+        for w in range(0, len(bs), args.concurrent):
+            chunk = bs[w:w + args.concurrent]
+            bar = threading.Barrier(len(chunk))
+            out += list(ex.map(lambda b: one_session(b, True, bar), chunk))
+        return out
+
+    with ThreadPoolExecutor(args.concurrent) as ex:
+        waves(ex, warm)
+        t0 = time.perf_counter()
+        res = waves(ex, timed)
+        wall = time.perf_counter() - t0
+    lat = [r[0] for r in res]
+    req = sum(r[2]["rank_requests"] for r in res)
+    bsum = sum(r[2]["rank_batch_sum"] for r in res)
+    seq_lat, _, _ = one_session(timed[0], False)  # one session alone, for the latency beside the throughput
+    out = {
+        "metric": "C5 what-if sessions/s (reclaim, allocate, backfill, preempt)",
+        "value": len(timed) / wall,
+        "unit": "sessions/s",
+        "n_gpus": 1,
+        "sessions": len(timed),
+        "concurrent_sessions": args.concurrent,
+        "p50_session_ms": statistics.median(lat) * 1e3,
+        "alone_session_ms": seq_lat * 1e3,
+        "higher_is_better": True,
+        "data": "synthetic (kbgen.gen_c5, seeds 20261015+5+k)",
+        "config": {"workload": "C5: 50k nodes ~90% filled, 5% backfill pods, 2k-task high-priority pending set per "
+                               "session, 4 queues, shipped conf", "nodes": args.nodes, "pending": args.pending},
+        "records_per_session": {"evicted": statistics.mean(r[1][3] for r in res),
+                                "pipelined": statistics.mean(r[1][2] for r in res),
+                                "allocated": statistics.mean(r[1][1] for r in res)},
+        "rank_launch_requests": req,
+        "sessions_per_rank_launch": bsum / max(req, 1),
+    }
+    if args.cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # the checker / CPU baseline only (test infrastructure)
+        threads = min(16, os.cpu_count() or 1)
+        p0 = os.path.join(args.cache, f"c5_{args.nodes}_{args.pending}_{args.warmup}.kbs")
+        st = {}
+        pl = oracle.fast_allocate(p0, threads=threads, actions=", ".join(ACTIONS), stats=st)
+        sess_s = st["open_s"] + st["allocate_s"]
         out["cpu_baseline"] = {"value": 1.0 / sess_s, "unit": "sessions/s", "cores": threads, "kind": "port",
                                "sample": f"one C5 session ({len(pl)} records), actions {', '.join(ACTIONS)}, "
                                          f"hoisted C++ restatement oracle/kbfast.cpp, {threads} threads on "

@@ -92,6 +92,8 @@ typedef struct kbhip_stats {
     int64_t fit_inexact;     /* jobs whose FitError histogram was not computed (shards, pod-affinity fallback) */
     int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
     int64_t pp_retries;      /* pop chunks the persistent placer could not start (swept again without it) */
+    int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if batcher ("rank_group") */
+    int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -195,6 +197,10 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * (placement 6), 0 = per-task sweeps there;
  * "rank_radix" = 1 orders reclaim / preempt walks with the library radix sort
  * instead of the counting sort (tests);
+ * "rank_group" = 1 makes this session one of a group of what-if sessions run
+ * from concurrent host threads: their reclaim / preempt node rankings are
+ * batched into shared launches (blockIdx.y = session; kbhip_stats
+ * rank_batch_sum / rank_requests = sessions per launch);
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;

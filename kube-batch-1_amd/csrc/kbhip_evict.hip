@@ -111,15 +111,16 @@ hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint
 //                   the block (wave ballots, then earlier waves' counts)
 // ---------------------------------------------------------------------------
 constexpr int kRankBuckets = 256;
-__global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
-                                                        int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
-                                                        uint32_t* count) {
+// blk / nblk: this block's node range and the number of blocks of the ranking
+__device__ __forceinline__ void rank_bucket(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                                            int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
+                                            uint32_t* count, int blk, int nblk) {
     __shared__ uint32_t s_h[kRankBuckets];
     for (int i = threadIdx.x; i < nb; i += kBlock) s_h[i] = 0;
     __syncthreads();
     const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
     const TaskClass c = t.classes[cls];
-    const int n = blockIdx.x * kBlock + threadIdx.x;
+    const int n = blk * kBlock + threadIdx.x;
     uint64_t k = 0;
     if (n < nc.n) {
         if (by_score) {
@@ -141,14 +142,14 @@ __global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, De
     __syncthreads();
     uint32_t tot = 0;
     for (int i = threadIdx.x; i < nb; i += kBlock) {
-        hist[(size_t)i * gridDim.x + blockIdx.x] = s_h[i];
+        hist[(size_t)i * nblk + blk] = s_h[i];
         tot += s_h[i];
     }
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
     if ((threadIdx.x & 63) == 0 && tot) atomicAdd(count, tot);
 }
 
-__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n) {  // in-place exclusive scan, one block
+__device__ __forceinline__ void rank_scan(uint32_t* v, int n) {  // in-place exclusive scan, one 1024-thread block
     __shared__ uint32_t s_sum[1024];
     const int per = (n + 1023) / 1024, lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
     uint32_t acc = 0;
@@ -169,14 +170,14 @@ __global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n) {  // in
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, const uint64_t* keys, const uint32_t* offs,
-                                                         int by_score, int shi, int nb, uint64_t* sorted) {
+__device__ __forceinline__ void rank_scatter(const NodeCols& nc, const uint64_t* keys, const uint32_t* offs,
+                                             int by_score, int shi, uint64_t* sorted, int blk, int nblk) {
     __shared__ uint32_t s_cnt[kBlock / 64][kRankBuckets];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int i = lane; i < kRankBuckets; i += 64) s_cnt[wave][i] = 0;
-    const int n = blockIdx.x * kBlock + threadIdx.x;
+    const int n = blk * kBlock + threadIdx.x;
     const uint64_t k = n < nc.n ? keys[n] : 0;
-    const int b = k ? (by_score ? shi - key_score(k) : 0) : -1;  // k_rank_bucket zeroed keys outside [0, nb)
+    const int b = k ? (by_score ? shi - key_score(k) : 0) : -1;  // rank_bucket zeroed keys outside [0, nb)
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes below this one
     uint32_t rank = 0;
     __builtin_amdgcn_wave_barrier();
@@ -189,10 +190,22 @@ __global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, cons
     }
     __syncthreads();
     if (b >= 0) {
-        uint32_t base = offs[(size_t)b * gridDim.x + blockIdx.x];
+        uint32_t base = offs[(size_t)b * nblk + blk];
         for (int w = 0; w < wave; ++w) base += s_cnt[w][b];
         sorted[base + rank] = k;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
+                                                        int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
+                                                        uint32_t* count) {
+    rank_bucket(cf, nc, t, ctrl, by_score, shi, nb, keys, hist, count, blockIdx.x, gridDim.x);
+}
+__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n) { rank_scan(v, n); }
+__global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, const uint64_t* keys, const uint32_t* offs,
+                                                         int by_score, int shi, int nb, uint64_t* sorted) {
+    (void)nb;
+    rank_scatter(nc, keys, offs, by_score, shi, sorted, blockIdx.x, gridDim.x);
 }
 
 hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
@@ -207,6 +220,44 @@ hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTable
     hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, st, hist, nb * nblk);
     hipLaunchKernelGGL(k_rank_scatter, dim3(nblk), dim3(kBlock), 0, st, nc, (const uint64_t*)keys,
                        (const uint32_t*)hist, by_score, shi, nb, sorted);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The same for a batch of what-if sessions:
+// one launch of each kernel ranks the nodes of every session in the batch —
+// blockIdx.y is the session, its descriptor (RankDesc) says where its node
+// rows, tables, request and outputs are.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_rank_bucket_multi(const RankDesc* d) {
+    const RankDesc& q = d[blockIdx.y];
+    if ((int)blockIdx.x >= q.nblk) return;  // uniform
+    rank_bucket(q.cf, q.nc, q.t, q.ctrl, q.by_score, q.shi, q.nb, q.keys, q.hist, q.count, blockIdx.x, q.nblk);
+}
+__global__ __launch_bounds__(1024) void k_rank_scan_multi(const RankDesc* d) {
+    const RankDesc& q = d[blockIdx.x];
+    rank_scan(q.hist, q.nb * q.nblk);
+}
+__global__ __launch_bounds__(kBlock) void k_rank_scatter_multi(const RankDesc* d) {
+    const RankDesc& q = d[blockIdx.y];
+    if ((int)blockIdx.x >= q.nblk) return;
+    rank_scatter(q.nc, q.keys, q.hist, q.by_score, q.shi, q.sorted, blockIdx.x, q.nblk);
+}
+
+hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                          int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
+                          uint32_t* count) {
+    const int nb = by_score ? shi - slo + 1 : 1;
+    if (nb < 1 || nb > kRankBuckets) return hipErrorInvalidValue;
+    *q = RankDesc{cf, nc, t, ctrl, by_score ? 1 : 0, shi, nb, (nc.n + kBlock - 1) / kBlock, keys, hist, sorted, count};
+    return hipSuccess;
+}
+
+hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_nblk, hipStream_t st) {
+    if (n_desc < 1 || max_nblk < 1) return hipSuccess;
+    hipLaunchKernelGGL(k_rank_bucket_multi, dim3(max_nblk, n_desc), dim3(kBlock), 0, st, d_desc);
+    hipLaunchKernelGGL(k_rank_scan_multi, dim3(n_desc), dim3(1024), 0, st, d_desc);
+    hipLaunchKernelGGL(k_rank_scatter_multi, dim3(max_nblk, n_desc), dim3(kBlock), 0, st, d_desc);
     return hipGetLastError();
 }
 size_t rank_hist_words(int n_nodes) { return (size_t)kRankBuckets * ((n_nodes + kBlock - 1) / kBlock + 1); }

@@ -52,6 +52,22 @@ hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTable
                               int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
                               uint32_t* count, hipStream_t st);
 size_t rank_hist_words(int n_nodes);
+// One session's ranking request in a batched launch (what-if sessions).
+struct RankDesc {
+    Conf cf;
+    NodeCols nc;
+    DevTables t;
+    const PopCtrl* ctrl;
+    int by_score, shi, nb, nblk;
+    uint64_t* keys;
+    uint32_t* hist;
+    uint64_t* sorted;
+    uint32_t* count;
+};
+hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
+                          int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
+                          uint32_t* count);
+hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_nblk, hipStream_t st);
 hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t* d, int n, hipStream_t st);
 hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
                           int64_t rg, hipStream_t st);

@@ -511,7 +511,7 @@ constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends 
 // INS: the placement merges each round by insertion (placement 5) instead of
 // sort + merge trees (placement 2); one placement per instantiation keeps the
 // kernel's registers (and so the occupancy of its sweep blocks) at one path's.
-template <int R, typename KT, bool INS>
+template <int R, typename KT, int PLV>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
                                                               PopLink* link, uint32_t seq, int ndep) {
@@ -727,8 +727,13 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
     if (ok) {
-        if (a.ent32) place_parallel<uint32_t, true, INS>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
-        else place_parallel<uint64_t, true, INS>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        if constexpr (PLV == 4) {  // one-wave insertion: no barriers, depths only where they can matter
+            if (wave == 0) place_insert<true>(cf, nc, t, c, a, out, wl[0][lane], &link->done, seq, &rc, s_fitin, fit_raw);
+        } else if (a.ent32) {
+            place_parallel<uint32_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        } else {
+            place_parallel<uint64_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        }
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
@@ -982,12 +987,12 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
     return hipGetLastError();
 }
 
-template <typename KT, bool INS>
+template <typename KT, int PLV>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
                                   uint32_t seq, int ndep, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT, INS>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, \
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT, PLV>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, \
                        o, link, seq, ndep)
     switch (R) {
         case 1: KBHIP_OV(1); break;
@@ -1006,17 +1011,19 @@ hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTabl
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
-    const bool ins = placement == 5;
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, ins ? 5 : 2, kf.base, kf.shift, kf.idxmax,
+    const int plv = placement == 5 || placement == 4 ? placement : 2;
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, plv, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) {
-        if (ins) launch_pop_batch_ov_t<uint32_t, true>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
-        else launch_pop_batch_ov_t<uint32_t, false>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
-    } else {
-        if (ins) launch_pop_batch_ov_t<uint64_t, true>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
-        else launch_pop_batch_ov_t<uint64_t, false>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st);
+#define KBHIP_OVP(KT)                                                                                       \
+    switch (plv) {                                                                                          \
+        case 5: launch_pop_batch_ov_t<KT, 5>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
+        case 4: launch_pop_batch_ov_t<KT, 4>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
+        default: launch_pop_batch_ov_t<KT, 2>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
     }
+    if (kf.use32) { KBHIP_OVP(uint32_t); }
+    else { KBHIP_OVP(uint64_t); }
+#undef KBHIP_OVP
     return hipGetLastError();
 }
 

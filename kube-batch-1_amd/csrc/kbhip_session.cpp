@@ -24,6 +24,7 @@
 #include <exception>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <tuple>
 #include <set>
@@ -367,6 +368,7 @@ struct Session {
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
     bool force_radix = false;  // option "rank_radix": the library radix sort for every class (tests)
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
+    bool rank_group = false;   // option "rank_group": node rankings batched with concurrent sessions (RankBatcher)
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
     vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
@@ -1564,6 +1566,105 @@ struct BatchLaunch {
     uint32_t pp_seq = 0;
 };
 
+// ---------------------------------------------------------------------------
+// What-if sessions batched per launch:
+// sessions opened with option "rank_group" = 1 and driven from concurrent
+// host threads hand their reclaim / preempt node rankings to this
+// process-wide batcher; one launch of the multi-session counting sort
+// (kbhip_evict.hip, blockIdx.y = session) ranks the pending requests as soon
+// as every grouped session inside a reclaim / preempt action waits for one
+// (they then step in lockstep), or kRankWait after the first arrived.
+// The launching thread's stream runs it; every requester's inputs are on the
+// device before it asks (its stream synchronised), its outputs are read on
+// its own stream after the batch completed.
+// ---------------------------------------------------------------------------
+struct RankBatcher {
+    static RankBatcher& get() {
+        static RankBatcher b;
+        return b;
+    }
+    struct Req {
+        RankDesc desc;
+        hipStream_t st = nullptr;
+        bool done = false;
+        hipError_t err = hipSuccess;
+        int batch = 0;  // sessions in the launch that served it
+    };
+    static constexpr auto kRankWait = std::chrono::microseconds(3000);
+    std::mutex mu;
+    std::condition_variable cv;
+    vector<Req*> pending;
+    int members = 0;  // grouped sessions inside a reclaim / preempt action
+    bool busy = false;
+    RankDesc* h_desc = nullptr;  // pinned, mapped: the kernels read the descriptors in place
+    void* d_desc = nullptr;
+    size_t cap_bytes = 0, n_cap = 0;
+    void join() {
+        std::lock_guard<std::mutex> lk(mu);
+        ++members;
+    }
+    void leave() {
+        std::lock_guard<std::mutex> lk(mu);
+        --members;
+        cv.notify_all();
+    }
+    hipError_t run(const vector<Req*>& batch, hipStream_t st) {
+        if (batch.size() > n_cap) {
+            if (h_desc) MemPool::get().give(MemPool::kPinnedMapped, h_desc, cap_bytes, 0);
+            n_cap = std::max<size_t>(64, batch.size());
+            h_desc = (RankDesc*)MemPool::get().take(MemPool::kPinnedMapped, n_cap * sizeof(RankDesc), &cap_bytes);
+            hipError_t e = hipHostGetDevicePointer(&d_desc, h_desc, 0);
+            if (e != hipSuccess) return e;
+        }
+        int max_nblk = 1;
+        for (size_t i = 0; i < batch.size(); ++i) {
+            h_desc[i] = batch[i]->desc;
+            max_nblk = std::max(max_nblk, batch[i]->desc.nblk);
+        }
+        hipError_t e = launch_rank_sorted_multi((const RankDesc*)d_desc, (int)batch.size(), max_nblk, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        return e;
+    }
+    void submit(Req& r) {
+        std::unique_lock<std::mutex> lk(mu);
+        pending.push_back(&r);
+        cv.notify_all();
+        const auto deadline = std::chrono::steady_clock::now() + kRankWait;
+        while (!r.done) {
+            const bool all_in = (int)pending.size() >= members;
+            if (!busy && !pending.empty() && (all_in || std::chrono::steady_clock::now() >= deadline)) {
+                busy = true;
+                vector<Req*> batch;
+                batch.swap(pending);
+                lk.unlock();
+                const hipError_t e = run(batch, r.st);
+                lk.lock();
+                for (Req* q : batch) {
+                    q->err = e;
+                    q->batch = (int)batch.size();
+                    q->done = true;
+                }
+                busy = false;
+                cv.notify_all();
+                continue;
+            }
+            if (busy) cv.wait(lk);
+            else cv.wait_until(lk, deadline);
+        }
+    }
+};
+
+// A grouped session inside a reclaim / preempt action (RankBatcher members).
+struct RankGroupScope {
+    bool on;
+    explicit RankGroupScope(bool o) : on(o) {
+        if (on) RankBatcher::get().join();
+    }
+    ~RankGroupScope() {
+        if (on) RankBatcher::get().leave();
+    }
+};
+
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
     if (!S.ov_pending) return;
@@ -2669,7 +2770,18 @@ struct Allocator {
         const auto sr = S.class_srange[cls];
         const bool counting = !S.force_radix && sr.second - sr.first < 256 && sr.first >= INT32_MIN &&
                               sr.second <= INT32_MAX;
-        if (counting) {  // hand-written stable counting sort over the score
+        if (counting && S.rank_group) {  // one launch with the concurrent what-if sessions' rankings
+            RankBatcher::Req r;
+            HIPCHK(fill_rank_desc(&r.desc, S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first,
+                                  (int)sr.second, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
+                                  (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p));
+            r.st = S.stream;
+            HIPCHK(hipStreamSynchronize(S.stream));  // this request's control block and counters are in place
+            RankBatcher::get().submit(r);
+            HIPCHK(r.err);
+            S.stats.rank_requests++;
+            S.stats.rank_batch_sum += r.batch;
+        } else if (counting) {  // hand-written stable counting sort over the score
             HIPCHK(launch_rank_sorted(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first, (int)sr.second,
                                       (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
                                       (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p, S.stream));
@@ -2899,6 +3011,7 @@ struct Allocator {
         return v;
     }
     void preempt_action() {  // preempt.go:43-255
+        RankGroupScope group(S.rank_group);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -2967,6 +3080,7 @@ struct Allocator {
         flush_evictions();
     }
     void reclaim_action() {  // reclaim.go:41-196
+        RankGroupScope group(S.rank_group);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -3556,6 +3670,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;
+        else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
             s->s.rank_first = (int)std::min<int64_t>(value, 1 << 20);

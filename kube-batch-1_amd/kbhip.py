@@ -47,7 +47,8 @@ class Stats(ctypes.Structure):
                 ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
                 ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64),
-                ("pp_retries", ctypes.c_int64)]
+                ("pp_retries", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
+                ("rank_batch_sum", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,0 +1,45 @@
+"""What-if sessions batched per launch:
+sessions with option rank_group run from concurrent host threads and their
+reclaim / preempt node rankings share launches of the multi-session counting
+sort (blockIdx.y = session).  Each session's records equal the faithful
+restatement's and the same session run alone; the launches served more than
+one session."""
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ACTIONS = "reclaim, allocate, backfill, preempt"
+STATUS = {1: 4, 2: 8, 3: 128}
+
+
+def _run(engine, path, group, barrier=None):
+    with engine.Session(path) as s:
+        if group:
+            s.set_option("rank_group", 1)
+        if barrier is not None:  # the sessions start their actions together
+            barrier.wait()
+        pod, node, kind = s.run_actions(ACTIONS)
+        st = s.stats()
+    return [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, node, kind)], st
+
+
+@pytest.mark.parametrize("n_sessions", [2, 6])
+def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sessions):
+    paths = []
+    for k in range(n_sessions):
+        p = str(tmp_path / f"w{k}.kbs")
+        kbgen_mod.gen_c5(p, seed=kbgen_mod.BASE_SEED + 70 + k, n_nodes=150, n_pending=120, best_effort=8)
+        paths.append(p)
+    alone = [_run(engine, p, False)[0] for p in paths]
+    bar = threading.Barrier(n_sessions)
+    with ThreadPoolExecutor(n_sessions) as ex:
+        res = list(ex.map(lambda p: _run(engine, p, True, bar), paths))
+    for p, a, (got, st) in zip(paths, alone, res):
+        assert got == a
+        assert got == oracle_mod.ref_allocate(p, actions=ACTIONS).as_list()
+    req = sum(st["rank_requests"] for _, st in res)
+    bsum = sum(st["rank_batch_sum"] for _, st in res)
+    assert req > 0 and bsum > req  # some launch ranked more than one session's nodes
