@@ -1035,6 +1035,125 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---------------------------------------------------------------------------
+// Placement of a pod-affinity class (placement 7; one wave, task after task;
+// classes with aff_batchable, kbhip_eval.h).  A placement adds the pod to
+// count tables (commit_aff), which can only turn nodes of the placed pod's
+// topology domains infeasible for the class's later tasks (a required
+// anti-affinity target now exists there, predicates.go:1293-1458); no node's
+// key rises.  Lane j holds candidate j of the sweep's list (keys with the
+// affinity predicates, eval_node_aff) with its row and the count-table slots
+// its predicates read (slot = table offset + the node's domain, -1 without
+// the key) and their counts.  Per task: winner = the largest current key;
+// the winner's count-table updates are broadcast as slots and every lane
+// whose predicate reads one of them adds to its count; a lane whose
+// predicate now fails drops out; the winner's row is committed and its key
+// re-evaluated.  Nodes outside the list had keys below the list's last one
+// and can only fall, so the choice is exact while the winner's key is at
+// least the list's last key; otherwise (or when no node is left) the launch
+// ends before that task and the host goes on (n_done 0: the general path for
+// one task, which also reports a no-node task's FitDelta histogram).
+// ---------------------------------------------------------------------------
+__device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                          const PopArgs& a, PopOut* out, uint64_t K) {
+    const int lane = threadIdx.x & 63;
+    const int n = K ? key_idx(K) : -1;  // one GPU: global index = row
+    Row r{};
+    uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t na_n = 0;
+    int32_t slot[kAffItems], cnt[kAffItems];
+    const int n_ea = c.ea_n;
+    const int n_items = n_ea + (c.paa_space >= 0 ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < kAffItems; ++k) {
+        slot[k] = -1;
+        cnt[k] = 0;
+        if (k < n_items && n >= 0) {
+            const int space = k < n_ea ? t.aff_items[c.ea_off + 2 * k] : c.paa_space;
+            const int tab = k < n_ea ? t.aff_items[c.ea_off + 2 * k + 1] : c.paa_cnt;
+            const int d = dom_of(nc, space, n);
+            if (d >= 0) {
+                slot[k] = tab + d;
+                cnt[k] = t.aff_cnt[tab + d];
+            }
+        }
+    }
+    if (n >= 0) {
+        r = load_row(nc, n);
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
+    }
+    const uint64_t t0 = readlane64(K, 63);  // the list's last key (0: the list holds every feasible node)
+    uint64_t key = K;
+    bool changed = false;
+    int ready = a.ready_count, done = 0, stop = 0;
+    uint64_t mine = 0;  // lane i: winner key of task i
+    for (int i = 0; i < a.n_tasks; ++i) {
+        const uint64_t w = wave_max_key(key);
+        if (!w || w < t0) break;  // no node, or one outside the list may come first: the host goes on
+        if (lane == i) mine = w;
+        const bool win = n >= 0 && key == w;
+        const int wl = __ffsll((unsigned long long)__ballot(win)) - 1;
+        const int kind = key_kind(w);
+        // the winner's count-table updates (UPD_CNT_ALLOC: Allocated only), as slots
+        for (int u = 0; u < c.upd_n; ++u) {
+            const int32_t* it = t.aff_items + c.upd_off + 3 * u;
+            int us = -1;
+            if (win && it[0] == 0 && kind == 1) {
+                const int d = dom_g(nc, it[1], n);
+                if (d >= 0) us = it[2] + d;
+            }
+            us = __builtin_amdgcn_readlane(us, wl);
+            if (us >= 0) {
+#pragma unroll
+                for (int k = 0; k < kAffItems; ++k) cnt[k] += (slot[k] == us) ? 1 : 0;
+            }
+        }
+        bool aff_ok = true;
+#pragma unroll
+        for (int k = 0; k < kAffItems; ++k) aff_ok = aff_ok && !(slot[k] >= 0 && cnt[k] > 0);
+        if (win) {
+            // the device tables (later launches read them): atomics, since winners of
+            // successive tasks are different lanes and may update the same entries
+            for (int u = 0; u < c.upd_n; ++u) {
+                const int32_t* it = t.aff_items + c.upd_off + 3 * u;
+                const bool to_cnt = it[0] == 0;
+                const int d = to_cnt ? dom_g(nc, it[1], n) : 0;
+                const bool apply = (it[0] == 2 || kind == 1) && d >= 0;
+                int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
+                __hip_atomic_fetch_add(tab + it[2] + (d >= 0 ? d : 0), apply ? 1 : 0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
+            if (c.has_ports)
+                for (int q = 0; q < 4; ++q) pw[q] |= (q < nc.port_words) ? t.masks[c.pown_off + q] : 0;
+            changed = true;
+            int32_t s = 0;
+            bool passed = false;
+            key = aff_ok ? dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed) : 0;
+        } else if (!aff_ok) {
+            key = 0;
+        }
+        done = i + 1;
+        if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
+        if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
+    }
+    if (changed) {
+        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
+        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
+        nc.pods[n] = r.pods;
+        nc.nzc[n] = r.nzc;
+        nc.nzm[n] = r.nzm;
+        if (c.has_ports)
+            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pw[w];
+    }
+    if (lane < done || (done == 0 && lane == 0))
+        __hip_atomic_store(&out->g[lane],
+                           make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
 // writes this shard's top-64 with their rows and the sweep's FitDelta counts.
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,

@@ -325,6 +325,33 @@ KBHIP_HD void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols&
     }
 }
 
+// Exact inverse of commit_aff (a retracted prediction, or the undo around a
+// FitDelta recomputation); same branch-free form.
+KBHIP_HD void uncommit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int g, int kind) {
+    for (int i = 0; i < c.upd_n; ++i) {
+        const int32_t* u = t.aff_items + c.upd_off + 3 * i;
+        const int typ = u[0];
+        const bool to_cnt = typ == 0;
+        const int d = to_cnt ? dom_g(nc, u[1], g) : 0;
+        const bool apply = (typ == 2 || kind == 1) && d >= 0;
+        int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
+        tab[u[2] + d] -= apply ? 1 : 0;
+    }
+}
+
+// Pod-affinity classes the batched pop places (placement 7): predicate terms
+// that only ever turn nodes infeasible as pods are placed — existing pods'
+// required anti-affinity (EA) and own required anti-affinity (PAA) — with no
+// own required affinity (PA: placements make nodes feasible) and no inter-pod
+// priority terms (their normalisation moves every node's score).  Lanes keep
+// the count-table entries their node's predicate reads in registers.
+constexpr int kAffItems = 4;  // EA pairs + PAA the placement tracks per candidate
+constexpr int kAffUpd = 8;    // commit updates of the class
+KBHIP_HD bool aff_batchable(const TaskClass& c) {
+    return c.aff && !c.pred_err && c.pa_space < 0 && c.ipa_n == 0 &&
+           c.ea_n + (c.paa_space >= 0 ? 1 : 0) <= kAffItems && c.upd_n <= kAffUpd;
+}
+
 // NodeInfo.AddTask for the winner (node_info.go:113-145) + the k8s NodeInfo
 // aggregates the predicates/nodeorder read (k8s cache/node_info.go:498-521).
 KBHIP_HD void commit_node(const TaskClass& c, const DevTables& t, const NodeCols& nc, int n, int kind) {

@@ -220,7 +220,8 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
 // batched path
 // PL: the placement compiled into this instantiation — 2 parallel levels,
 // 5 parallel levels merged by insertion, 6 sessions with Backfilled nodes
-// (walk keys, sequential placement), 3 the node-array shard's sweep only
+// (walk keys, sequential placement), 7 pod-affinity classes (affinity
+// predicates in the sweep, sequential placement with count-table slots), 3 the node-array shard's sweep only
 // (no placement: the exchange follows), -1 the test-only modes 0 / 1 / 4 —
 // so that a kernel's registers (and the occupancy of its sweep blocks) are
 // those of one placement path.
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
             int32_t s;
             bool passed;
             if constexpr (PL == 6) k = sweep_key<KT>(eval_node_walk(cf, c, t, nc, n, &fbs[r]), a);
+            else if constexpr (PL == 7) k = sweep_key<KT>(eval_node_aff(cf, c, t, nc, n, 0, 0, -1, &s, &passed, &fbs[r]), a);
             else k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
         k = wave_sort_desc(k);
@@ -338,6 +340,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         if (wave != 0) return;
         STAMP(gridDim.x * 4 + 1);
         place_bf(cf, nc, t, c, a, out, wl[0][lane]);
+        STAMP(gridDim.x * 4 + 3);
+        return;
+    } else if constexpr (PL == 7) {  // pod-affinity class (aff_batchable)
+        if (wave != 0) return;
+        STAMP(gridDim.x * 4 + 1);
+        place_aff(cf, nc, t, c, a, out, wl[0][lane]);
         STAMP(gridDim.x * 4 + 3);
         return;
     } else {
@@ -768,9 +776,11 @@ struct UndoArgs {
 __global__ __launch_bounds__(64) void k_undo_pop(NodeCols nc, DevTables t, UndoArgs u) {
     if (threadIdx.x != 0) return;
     const TaskClass c = t.classes[u.cls];
-    for (int i = 0; i < u.n; ++i)
+    for (int i = 0; i < u.n; ++i) {
         if (u.node[i] - nc.base >= 0 && u.node[i] - nc.base < nc.n)  // this shard's rows only
             uncommit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+        if (c.aff && u.node[i] >= 0) uncommit_aff(c, t, nc, u.node[i], u.kind[i]);  // replicated tables
+    }
 }
 
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
@@ -786,9 +796,11 @@ hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int 
 __global__ __launch_bounds__(64) void k_redo_pop(NodeCols nc, DevTables t, UndoArgs u) {
     if (threadIdx.x != 0) return;
     const TaskClass c = t.classes[u.cls];
-    for (int i = 0; i < u.n; ++i)
+    for (int i = 0; i < u.n; ++i) {
         if (u.node[i] - nc.base >= 0 && u.node[i] - nc.base < nc.n)
             commit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
+        if (c.aff && u.node[i] >= 0) commit_aff(c, t, nc, u.node[i], u.kind[i]);
+    }
 }
 
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
@@ -807,7 +819,8 @@ hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int 
 // found no node, every walk node counts; else the walk stopped at node
 // `chosen` with kind chosen_kind: the walk nodes before it count (walk order
 // = key order without the fit bit), and `chosen` itself when Pipelined.
-// Classes without pod-affinity terms.  out4 is zeroed by the caller.
+// Classes without inter-pod priority terms (pod-affinity predicates are
+// evaluated on the current tables).  out4 is zeroed by the caller.
 __global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevTables t, int cls, int chosen,
                                                       int chosen_kind, int32_t* out4) {
     __shared__ int32_t s_fit[4];
@@ -818,13 +831,13 @@ __global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevT
     if (chosen >= 0) {
         int32_t s = 0;
         bool passed = false;
-        (void)eval_node(cf, c, t, nc, chosen - nc.base, &s, &passed);
+        (void)eval_node_aff(cf, c, t, nc, chosen - nc.base, 0, 0, -1, &s, &passed);
         wk = pack_key(s, chosen, 0);
     }
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
         int32_t s = 0;
         bool passed = false;
-        (void)eval_node(cf, c, t, nc, n, &s, &passed);
+        (void)eval_node_aff(cf, c, t, nc, n, 0, 0, -1, &s, &passed);
         Row r = load_row(nc, n);
         r.bf_cpu = r.bf_mem = r.bf_gpu = 0;  // Idle as the walk left it
         const bool in = passed && (chosen < 0 || pack_key(s, n + nc.base, 0) > wk ||
@@ -883,6 +896,7 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
             case 3: KBHIP_PB1(RR, 3); break;                           \
             case 5: KBHIP_PB1(RR, 5); break;                           \
             case 6: KBHIP_PB1(RR, 6); break;                           \
+            case 7: KBHIP_PB1(RR, 7); break;                           \
             default: KBHIP_PB1(RR, -1); break;                         \
         }                                                              \
     } while (0)

@@ -368,6 +368,7 @@ struct Session {
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
     bool force_radix = false;  // option "rank_radix": the library radix sort for every class (tests)
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
+    bool aff_batch = true;     // option "aff_batch": batched pops (placement 7) of anti-affinity classes
     bool rank_group = false;   // option "rank_group": node rankings batched with concurrent sessions (RankBatcher)
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
@@ -465,6 +466,8 @@ struct Session {
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_nonov = nullptr;  // after a non-overlapped batched pop: the next overlapped one waits for it
+    bool nonov_pending = false;
     double timed_ms = 0;          // summed duration of the timed sweep launches
     double host_launch_s = 0, host_wait_s = 0;
     int64_t timed_n = 0;
@@ -501,7 +504,7 @@ struct Session {
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm) (void)ncclCommDestroy(comm);
         comm = nullptr;
-        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1]})
+        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : ev_ring)
             for (auto& e : pr)
@@ -1562,6 +1565,7 @@ struct BatchLaunch {
     hipStream_t st = nullptr;
     bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
     bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
+    bool aff = false;  // placement 7 (pod-affinity class): may end before its first task (n_done 0)
     bool pp = false;   // through the persistent placer: may end before its first task (n_done 0)
     uint32_t pp_seq = 0;
 };
@@ -1780,7 +1784,9 @@ static bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
     // Backfilled nodes (some Idle grows on each walk visit): placement 6, one GPU only
     const bool bf_ok = !S.any_bf || (S.world == 1 && S.bf_batch);
-    return S.batched && (S.world == 1 || S.comm || S.xgfn) && bf_ok && !c.backfill && !c.aff &&
+    // pod-affinity classes: placement 7 (anti-affinity predicates only), one GPU, no Backfilled nodes
+    const bool aff_ok = !c.aff || (S.aff_batch && S.world == 1 && !S.any_bf && aff_batchable(c));
+    return S.batched && (S.world == 1 || S.comm || S.xgfn) && bf_ok && !c.backfill && aff_ok &&
            S.nc.port_words <= 4 && S.n_total < (1 << 25);
 }
 
@@ -1808,10 +1814,15 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.ev_used[k] = true;
     }
     L.bf = S.any_bf != 0;
-    L.pp = S.pp_active && S.pp && !S.pp_skip && S.placement >= 2 && S.world == 1 && !L.bf;
+    L.aff = !L.bf && S.classes[cls].aff;
+    L.pp = S.pp_active && S.pp && !S.pp_skip && S.placement >= 2 && S.world == 1 && !L.bf && !L.aff;
     S.pp_skip = false;
     if (L.pp) {  // one sweep per pop, any stream; the resident placer places them in order
         ov_drain(S);
+        if (S.nonov_pending) {  // a non-overlapped batched pop may still run on stream 0
+            HIPCHK(hipStreamSynchronize(S.stream));
+            S.nonov_pending = false;
+        }
         pp_init(S);
         if (!S.pp_running) pp_launch(S, S.pp_seq + 1, true);
         const uint32_t e = ++S.pp_seq;
@@ -1831,13 +1842,22 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
         return L;
     }
-    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1 && !L.bf;
+    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1 && !L.bf && !L.aff;
     if (!ov) ov_quiesce(S);
     else pp_stop(S);
+
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
     L.st = S.ov_streams[si];
-    L.fit = !L.bf && (S.placement >= 2 || S.world > 1);
+    // an overlapped pop chains on the device only behind overlapped pops (its
+    // sweep runs beside the previous pop, ordered after the pop before that by
+    // its stream): after a non-overlapped batched pop (stream 0), every
+    // overlap stream waits for that pop's end before its next launch
+    if (ov && S.nonov_pending) {
+        for (int k = 0; k <= S.overlap; ++k) HIPCHK(hipStreamWaitEvent(S.ov_streams[k], S.ev_nonov, 0));
+        S.nonov_pending = false;
+    }
+    L.fit = !L.bf && !L.aff && (S.placement >= 2 || S.world > 1);
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -1859,8 +1879,14 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.ov_pending = true;
     } else {
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                                S.d_arrive, out, S.stream, L.bf ? 6 : S.placement, kf, S.fit_set[kMaxDep + 1]));
+                                S.d_arrive, out, S.stream, L.bf ? 6 : L.aff ? 7 : S.placement, kf,
+                                S.fit_set[kMaxDep + 1]));
         S.fit_set[kMaxDep + 1] ^= 1;
+        if (S.overlap > 0) {
+            if (!S.ev_nonov) HIPCHK(hipEventCreateWithFlags(&S.ev_nonov, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(S.ev_nonov, S.stream));
+            S.nonov_pending = true;
+        }
     }
     if (L.timed && S.world == 1) HIPCHK(hipEventRecord(ev[1], L.st));
     S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
@@ -1896,7 +1922,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
     S.stats.sweeps += 1;
     S.stats.batched_pops += 1;
-    if (n_done < (L.bf || L.pp ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+    if (n_done < (L.bf || L.aff || L.pp ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
     for (int j = 0; j < n_done; ++j) {
         const uint64_t g = load(j);
         res_node[j] = (int32_t)(g & 0xffffffffu) - 1;
@@ -2014,7 +2040,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
                 S.pp_skip = true;
                 continue;
             }
-            if (n_done == 0) {  // placement 6 could not place the first task exactly: general path for it
+            if (n_done == 0) {  // placement 6 / 7 could not place the first task exactly: general path for it
                 batch = false;
                 m = 1;
             }
@@ -2579,7 +2605,7 @@ struct Allocator {
         auto fit_sync = [&](int cls, int node, int kind, HJob& job) {
             discard_all();
             ov_quiesce(S);
-            if (S.world != 1 || S.classes[cls].aff) {  // not covered: shards, pod-affinity classes
+            if (S.world != 1 || S.classes[cls].ipa_n) {  // not covered: shards, inter-pod priority classes
                 job.fit_exact = false;
                 S.stats.fit_inexact++;
                 return;
@@ -3669,6 +3695,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
+        else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
         else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count

@@ -11,7 +11,7 @@ Then kbref (the faithful restatement, per-(task,node) recomputation) on the C2
 generator at N in {100, 300, 1000} nodes x T = 1000 pending tasks, and a power
 fit of its allocate time in N.
 
-Usage (repo root, GPU box): python3 profiles/baseline_table.py [out.json] [--fit]
+Usage (repo root, GPU box): python3 profiles/baseline_table.py [out.json] [--fit] [--only=C3,C4]
 Test infrastructure: the oracle here is the checker and the CPU baseline only.
 """
 import json
@@ -85,7 +85,10 @@ def main():
         ("C3", lambda p: kbgen.gen_c3().write(p), 3, 1),
         ("C4", lambda p: kbgen.gen_c4(p), 3, 1),
     ]
+    only = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--only=")]
     for name, gen, greps, creps in cfgs:
+        if only and name not in only[0].split(","):
+            continue
         p = os.path.join(tmp, name + ".kbs")
         t = time.perf_counter()
         gen(p)
