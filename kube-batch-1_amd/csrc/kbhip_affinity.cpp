@@ -14,6 +14,9 @@
 #include "kbhip_affinity.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <unordered_map>
 
@@ -33,6 +36,21 @@ struct SDict {
         ids.emplace(s, (int)strs.size());
         strs.push_back(s);
         return (int)strs.size() - 1;
+    }
+};
+
+// Dictionary lookups by string-table offset: the same offset is the same
+// string, so each distinct offset is hashed as a string once.
+struct ODict {
+    SDict& d;
+    const kbs::Snapshot& s;
+    std::unordered_map<int32_t, int> by_off;
+    int get(int32_t off) {
+        auto it = by_off.find(off);
+        if (it != by_off.end()) return it->second;
+        const int id = d.get(s.s(off));
+        by_off.emplace(off, id);
+        return id;
     }
 };
 
@@ -123,9 +141,18 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     active = used && (pred_on || ipa_on);
     if (!active) return;
 
+    static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;
+    auto tp = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!prof) return;
+        auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[aff]  %-12s %6.2f ms\n", what, std::chrono::duration<double, std::milli>(t - tp).count());
+        tp = t;
+    };
     // ---------------- dictionaries, selectors, affinity rows ----------------
     SDict keys, vals, nss;
     for (auto& n : ns_names) nss.get(n);
+    ODict okeys{keys, s, {}}, ovals{vals, s, {}}, onss{nss, s, {}};
     auto pat_sel = V32("pat_sel"), pat_topo = V32("pat_topo"), patns = V32("patns");
     auto pat_ns = s.offs("pat_ns_off", pat_sel.size());
     auto ls_ml = V32("ls_ml_off"), ls_me = V32("ls_me_off"), lkv_k = V32("lkv_key"), lkv_v = V32("lkv_val");
@@ -136,6 +163,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     auto wpat_w = V32("wpat_weight"), wpat_t = V32("wpat_term");
     vector<LSel> sels;
     std::map<int, int> sel_of_row;  // lsel row -> parsed selector (-1 row: nil)
+    std::unordered_map<string, int> sel_of_canon;  // equal selectors share one index
     auto parse_sel = [&](int sr) -> int {
         auto it = sel_of_row.find(sr);
         if (it != sel_of_row.end()) return it->second;
@@ -149,10 +177,10 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
             // MatchLabels -> Equals requirements; MatchExpressions In/NotIn/Exists/DoesNotExist
             // (metav1.LabelSelectorAsSelector); an invalid requirement errors the selector.
             for (int k = ls_ml[sr]; k < ls_ml[sr + 1]; ++k)
-                L.reqs.push_back(LReq{keys.get(s.s(lkv_k[k])), L_IN, {vals.get(s.s(lkv_v[k]))}});
+                L.reqs.push_back(LReq{okeys.get(lkv_k[k]), L_IN, {ovals.get(lkv_v[k])}});
             for (int k = ls_me[sr]; k < ls_me[sr + 1]; ++k) {
-                LReq r{keys.get(s.s(lsr_key[k])), (int)lsr_op[k], {}};
-                for (int q = lsr_voff[k]; q < lsr_voff[k + 1]; ++q) r.vals.push_back(vals.get(s.s(lsrv[q])));
+                LReq r{okeys.get(lsr_key[k]), (int)lsr_op[k], {}};
+                for (int q = lsr_voff[k]; q < lsr_voff[k + 1]; ++q) r.vals.push_back(ovals.get(lsrv[q]));
                 const bool nv = r.vals.empty();
                 if (r.op == L_IN || r.op == L_NOTIN) { if (nv) L.err = true; }
                 else if (r.op == L_EXISTS || r.op == L_DNE) { if (!nv) L.err = true; }
@@ -173,7 +201,13 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
             L.canon = L.err ? "X" + std::to_string(sr) : "S";
             for (auto& p : parts) L.canon += p + ";";
         }
+        auto ci = sel_of_canon.find(L.canon);
+        if (ci != sel_of_canon.end()) {
+            sel_of_row[sr] = ci->second;
+            return ci->second;
+        }
         sels.push_back(std::move(L));
+        sel_of_canon.emplace(sels.back().canon, (int)sels.size() - 1);
         sel_of_row[sr] = (int)sels.size() - 1;
         return (int)sels.size() - 1;
     };
@@ -181,7 +215,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         if (row < 0 || row >= (int)pat_sel.size()) throw std::invalid_argument("pod affinity term row out of range");
         PTerm t;
         t.sel = parse_sel(pat_sel[row]);
-        for (int k = pat_ns[row]; k < pat_ns[row + 1]; ++k) t.ns.push_back(nss.get(s.s(patns[k])));
+        for (int k = pat_ns[row]; k < pat_ns[row + 1]; ++k) t.ns.push_back(onss.get(patns[k]));
         t.key = s.s(pat_topo[row]);
         return t;
     };
@@ -201,6 +235,22 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         return (a >= 0 && (size_t)a < A && rows[a].any()) ? &rows[a] : nullptr;
     };
 
+    // keys any selector reads (pod labels) / any term's topology key (node labels):
+    // labels under other keys never matter here and are not encoded
+    vector<char> sel_key(keys.strs.size(), 0);
+    for (auto& L : sels)
+        for (auto& r : L.reqs) sel_key[r.key] = 1;
+    std::unordered_map<string, int> topo_keys;
+    for (auto& r : rows) {
+        for (auto* v : {&r.pa_req, &r.paa_req})
+            for (auto& t : *v) topo_keys.emplace(t.key, 0);
+        for (auto* v : {&r.pa_pref, &r.paa_pref})
+            for (auto& wt : *v) topo_keys.emplace(wt.second.key, 0);
+    }
+    for (auto& kv : topo_keys) kv.second = keys.get(kv.first);
+    vector<char> topo_key(keys.strs.size(), 0);
+    for (auto& kv : topo_keys) topo_key[kv.second] = 1;
+    mark("rows");
     // ---------------- pod label groups (namespace + labels) ----------------
     auto plo = s.offs("p_label_off", P);
     auto plk = V32("pl_key"), plv = V32("pl_val");
@@ -211,7 +261,10 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         std::map<std::pair<int, LSet>, int> gid;
         for (int i = 0; i < P; ++i) {
             LSet l;
-            for (int k = plo[i]; k < plo[i + 1]; ++k) l.push_back({keys.get(s.s(plk[k])), vals.get(s.s(plv[k]))});
+            for (int k = plo[i]; k < plo[i + 1]; ++k) {
+                const int key = okeys.get(plk[k]);
+                if (key < (int)sel_key.size() && sel_key[key]) l.push_back({key, ovals.get(plv[k])});
+            }
             std::sort(l.begin(), l.end());
             auto key = std::make_pair(pods[i].ns, l);
             auto it = gid.find(key);
@@ -224,12 +277,16 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         }
     }
 
+    mark("groups");
     // ---------------- topology spaces ----------------
     auto nlo = s.offs("n_label_off", N);
     auto nlk = V32("nl_key"), nlv = V32("nl_val");
     vector<LSet> n_labels(N);
     for (int n = 0; n < N; ++n) {
-        for (int k = nlo[n]; k < nlo[n + 1]; ++k) n_labels[n].push_back({keys.get(s.s(nlk[k])), vals.get(s.s(nlv[k]))});
+        for (int k = nlo[n]; k < nlo[n + 1]; ++k) {
+            const int key = okeys.get(nlk[k]);
+            if (key < (int)topo_key.size() && topo_key[key]) n_labels[n].push_back({key, ovals.get(nlv[k])});
+        }
         std::sort(n_labels[n].begin(), n_labels[n].end());
     }
     std::map<vector<string>, int> space_ids;
@@ -259,6 +316,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         return sp;
     };
 
+    mark("node labels");
     // ---------------- term classes ----------------
     vector<TClass> classes;
     std::map<string, int> class_ids;
@@ -274,7 +332,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         string sig = std::to_string(kind) + "|" + std::to_string(weight) + "|";
         for (auto& p : props) {
             for (int x : p.ns) sig += std::to_string(x) + ",";
-            sig += "/" + sels[p.sel].canon + "|";
+            sig += "/" + std::to_string(p.sel) + "|";  // selectors are deduplicated by canonical form
         }
         for (auto& k : ks) { sig += k; sig.push_back('\0'); }
         auto it = class_ids.find(sig);
@@ -352,6 +410,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
                 for (auto& wt : r->paa_pref) add_r(wt.second, -wt.first);
         }
     }
+    mark("term classes");
     n_spaces = (int)space_size.size();
     if (n_spaces == 0) dom.assign(npad, -1);
     // table offsets
@@ -382,17 +441,40 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         memo.emplace(k, ok);
         return ok;
     };
-    vector<int> cls_pa_paa, cls_q, cls_r, cls_ea;
-    for (int c = 0; c < (int)classes.size(); ++c) {
-        switch (classes[c].kind) {
-            case K_PA: case K_PAA: cls_pa_paa.push_back(c); break;
-            case K_Q: cls_q.push_back(c); break;
-            case K_R: cls_r.push_back(c); break;
-            default: cls_ea.push_back(c); break;
-        }
-    }
     auto dom_at = [&](int c, int n) { return dom[(size_t)classes[c].space * npad + n]; };
+    // Candidate classes per label group: a class whose first property's
+    // selector requires some (key, value) (an In requirement) can only match a
+    // group carrying one of those labels; the rest are checked for every
+    // group.  Keeps the membership tests per group proportional to the classes
+    // that mention its labels (C3: one self-anti-affinity class per gang).
+    std::unordered_map<int64_t, vector<int>> by_label;  // key << 32 | value -> classes (ascending)
+    vector<int> unanchored;
+    for (int c = 0; c < (int)classes.size(); ++c) {
+        const LSel* sl = classes[c].props.empty() ? nullptr : &sels[classes[c].props[0].sel];
+        const LReq* in = nullptr;
+        if (sl && !sl->nothing && !sl->err)
+            for (const LReq& r : sl->reqs)
+                if (r.op == L_IN && (!in || r.vals.size() < in->vals.size())) in = &r;
+        if (!in) { unanchored.push_back(c); continue; }
+        for (int v : in->vals) by_label[((int64_t)in->key << 32) | (uint32_t)v].push_back(c);
+    }
+    vector<vector<int>> g_cands(g_labels.size());
+    vector<char> g_cands_built(g_labels.size(), 0);
+    auto cands = [&](int g) -> const vector<int>& {
+        vector<int>& v = g_cands[g];
+        if (g_cands_built[g]) return v;
+        g_cands_built[g] = 1;
+        v = unanchored;
+        for (auto& kv : g_labels[g]) {
+            auto it = by_label.find(((int64_t)kv.first << 32) | (uint32_t)kv.second);
+            if (it != by_label.end()) v.insert(v.end(), it->second.begin(), it->second.end());
+        }
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+        return v;
+    };
 
+    mark("tables+index");
     // ---------------- initial counts ----------------
     for (int i = 0; i < P; ++i) {
         const AffPod& p = pods[i];
@@ -401,16 +483,16 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
                 const int d = dom_at(c, p.node);
                 if (d >= 0) cnt[classes[c].cnt_off + d]++;
             }
-            for (int c : cls_pa_paa)
-                if (matches(c, group[i])) {
+            for (int c : cands(group[i]))
+                if ((classes[c].kind == K_PA || classes[c].kind == K_PAA) && matches(c, group[i])) {
                     if (classes[c].kind == K_PA) scalar[classes[c].scal]++;
                     const int d = dom_at(c, p.node);
                     if (d >= 0) cnt[classes[c].cnt_off + d]++;
                 }
         }
         if (p.node >= 0) {  // IPA pods: every pod on a node, at its (raw) node
-            for (int c : cls_q)
-                if (matches(c, group[i])) {
+            for (int c : cands(group[i]))
+                if (classes[c].kind == K_Q && matches(c, group[i])) {
                     const int d = dom_at(c, p.node);
                     if (d >= 0) cnt[classes[c].cnt_off + d]++;
                 }
@@ -421,19 +503,25 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         }
     }
 
+    mark("counts");
     // ---------------- programs of pending tasks ----------------
-    std::map<std::pair<int, int>, AffProgram> cache;  // (label group, affinity row) -> program
+    // (label group, the pod's own term classes) -> program
+    std::map<vector<int>, AffProgram> cache;
+    vector<int> ck;
     for (int i = 0; i < P; ++i) {
         if (!pods[i].pending) continue;
-        const int a = row_of(i) ? paff[i] : -1;
-        auto ck = std::make_pair(group[i], a);
+        ck.assign({group[i], own_pred_err[i], own_pa[i], own_paa[i], (int)own_ea[i].size(), (int)own_q[i].size()});
+        ck.insert(ck.end(), own_ea[i].begin(), own_ea[i].end());
+        for (auto& q : own_q[i]) ck.insert(ck.end(), {q.first, q.second});
+        ck.insert(ck.end(), own_r[i].begin(), own_r[i].end());
         auto it = cache.find(ck);
         if (it == cache.end()) {
             AffProgram pg;
             const int g = group[i];
             pg.pred_err = own_pred_err[i];
-            for (int c : cls_ea)
-                if (matches(c, g)) { pg.ea.push_back(classes[c].space); pg.ea.push_back(classes[c].cnt_off); }
+            const vector<int>& cg = cands(g);
+            for (int c : cg)
+                if (classes[c].kind == K_EA && matches(c, g)) { pg.ea.push_back(classes[c].space); pg.ea.push_back(classes[c].cnt_off); }
             if (own_pa[i] >= 0) {
                 const TClass& c = classes[own_pa[i]];
                 pg.pa_space = c.space; pg.pa_cnt = c.cnt_off; pg.pa_total = c.scal;
@@ -447,25 +535,26 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
                 const TClass& c = classes[q.first];
                 pg.ipa.insert(pg.ipa.end(), {c.space, c.cnt_off, c.scal, q.second});
             }
-            for (int c : cls_r)
-                if (matches(c, g)) {
+            for (int c : cg)
+                if (classes[c].kind == K_R && matches(c, g)) {
                     const TClass& rc = classes[c];
                     pg.ipa.insert(pg.ipa.end(), {rc.space, rc.cnt_off, rc.scal, rc.weight});
                 }
             // commit updates: what this task changes once it is placed
             for (int c : own_ea[i]) pg.upd.insert(pg.upd.end(), {UPD_CNT_ALLOC, classes[c].space, classes[c].cnt_off});
-            for (int c : cls_pa_paa)
-                if (matches(c, g)) {
+            for (int c : cg)
+                if ((classes[c].kind == K_PA || classes[c].kind == K_PAA) && matches(c, g)) {
                     pg.upd.insert(pg.upd.end(), {UPD_CNT_ALLOC, classes[c].space, classes[c].cnt_off});
                     if (classes[c].kind == K_PA) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ALLOC, 0, classes[c].scal});
                 }
-            for (int c : cls_q)
-                if (matches(c, g)) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ANY, 0, classes[c].scal});
+            for (int c : cg)
+                if (classes[c].kind == K_Q && matches(c, g)) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ANY, 0, classes[c].scal});
             for (int c : own_r[i]) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ANY, 0, classes[c].scal});
             it = cache.emplace(ck, std::move(pg)).first;
         }
         if (!it->second.empty()) progs_.emplace(i, it->second);
     }
+    mark("programs");
 }
 
 }  // namespace kbhip
