@@ -441,7 +441,6 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         memo.emplace(k, ok);
         return ok;
     };
-    auto dom_at = [&](int c, int n) { return dom[(size_t)classes[c].space * npad + n]; };
     // Candidate classes per label group: a class whose first property's
     // selector requires some (key, value) (an In requirement) can only match a
     // group carrying one of those labels; the rest are checked for every
@@ -475,34 +474,23 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     };
 
     mark("tables+index");
+    // ---------------- retained for recount / target_updates ----------------
+    npad_ = npad;
+    cls_.clear();
+    for (auto& c : classes) cls_.push_back(CInfo{c.kind, c.space, c.cnt_off, c.scal});
+    pod_group_ = group;
+    own_ea_ = own_ea;
+    own_r_ = own_r;
+    g_tgt_.assign(g_labels.size(), {});
+    g_q_.assign(g_labels.size(), {});
+    for (int g = 0; g < (int)g_labels.size(); ++g)
+        for (int c : cands(g)) {
+            const int k = classes[c].kind;
+            if ((k == K_PA || k == K_PAA) && matches(c, g)) g_tgt_[g].push_back(c);
+            else if (k == K_Q && matches(c, g)) g_q_[g].push_back(c);
+        }
     // ---------------- initial counts ----------------
-    for (int i = 0; i < P; ++i) {
-        const AffPod& p = pods[i];
-        if (p.target && p.node >= 0) {
-            for (int c : own_ea[i]) {
-                const int d = dom_at(c, p.node);
-                if (d >= 0) cnt[classes[c].cnt_off + d]++;
-            }
-            for (int c : cands(group[i]))
-                if ((classes[c].kind == K_PA || classes[c].kind == K_PAA) && matches(c, group[i])) {
-                    if (classes[c].kind == K_PA) scalar[classes[c].scal]++;
-                    const int d = dom_at(c, p.node);
-                    if (d >= 0) cnt[classes[c].cnt_off + d]++;
-                }
-        }
-        if (p.node >= 0) {  // IPA pods: every pod on a node, at its (raw) node
-            for (int c : cands(group[i]))
-                if (classes[c].kind == K_Q && matches(c, group[i])) {
-                    const int d = dom_at(c, p.node);
-                    if (d >= 0) cnt[classes[c].cnt_off + d]++;
-                }
-            for (int c : own_r[i]) {
-                const int d = dom_at(c, p.node);
-                if (d >= 0) cnt[classes[c].cnt_off + d]++;
-            }
-        }
-    }
-
+    recount(pods);
     mark("counts");
     // ---------------- programs of pending tasks ----------------
     // (label group, the pod's own term classes) -> program
@@ -555,6 +543,48 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         if (!it->second.empty()) progs_.emplace(i, it->second);
     }
     mark("programs");
+}
+
+void AffinityModel::recount(const vector<AffPod>& pods) {
+    if (!active) return;
+    std::fill(cnt.begin(), cnt.end(), 0);
+    std::fill(scalar.begin(), scalar.end(), 0);
+    auto dom_at = [&](int c, int n) { return dom[(size_t)cls_[c].space * npad_ + n]; };
+    for (int i = 0; i < (int)pods.size(); ++i) {
+        const AffPod& p = pods[i];
+        const int g = pod_group_[i];
+        if (p.target && p.node >= 0) {  // predicate targets (predicates.go:59-94)
+            for (int c : own_ea_[i]) {
+                const int d = dom_at(c, p.node);
+                if (d >= 0) cnt[cls_[c].cnt_off + d]++;
+            }
+            for (int c : g_tgt_[g]) {
+                if (cls_[c].kind == K_PA) scalar[cls_[c].scal]++;
+                const int d = dom_at(c, p.node);
+                if (d >= 0) cnt[cls_[c].cnt_off + d]++;
+            }
+        }
+        if (p.node >= 0) {  // IPA pods: every pod on a node, at its (raw) node
+            for (int c : g_q_[g]) {
+                const int d = dom_at(c, p.node);
+                if (d >= 0) cnt[cls_[c].cnt_off + d]++;
+            }
+            for (int c : own_r_[i]) {
+                const int d = dom_at(c, p.node);
+                if (d >= 0) cnt[cls_[c].cnt_off + d]++;
+            }
+        }
+    }
+}
+
+void AffinityModel::target_updates(int pod, vector<int32_t>& out) const {
+    out.clear();
+    if (!active || pod < 0 || pod >= (int)pod_group_.size()) return;
+    for (int c : own_ea_[pod]) out.insert(out.end(), {UPD_CNT_ALLOC, cls_[c].space, cls_[c].cnt_off});
+    for (int c : g_tgt_[pod_group_[pod]]) {
+        out.insert(out.end(), {UPD_CNT_ALLOC, cls_[c].space, cls_[c].cnt_off});
+        if (cls_[c].kind == K_PA) out.insert(out.end(), {UPD_SCALAR_ALLOC, 0, cls_[c].scal});
+    }
 }
 
 }  // namespace kbhip

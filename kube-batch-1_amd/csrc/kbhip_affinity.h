@@ -77,9 +77,28 @@ class AffinityModel {
         auto it = progs_.find(pod);
         return it == progs_.end() ? nullptr : &it->second;
     }
+    // Counts of every table for the given pod states (same term classes and
+    // programs as built: the pods' statuses / nodes may have changed, e.g. a
+    // session carried over or victims evicted).  build() uses it for the
+    // initial counts.
+    void recount(const std::vector<AffPod>& pods);
+    // What pod i contributes while it is a predicate target (an
+    // AllocatedStatuses task of a session job on a node): (type, space, off)
+    // triples as in AffProgram::upd (UPD_CNT_ALLOC / UPD_SCALAR_ALLOC).  An
+    // eviction (Running -> Releasing) withdraws them, an unevict restores them.
+    void target_updates(int pod, std::vector<int32_t>& out) const;
+    int npad() const { return npad_; }
 
   private:
     std::map<int, AffProgram> progs_;
+    struct CInfo {
+        int kind, space, cnt_off, scal;
+    };
+    std::vector<CInfo> cls_;                          // term classes
+    std::vector<int> pod_group_;                      // label group of each pod
+    std::vector<std::vector<int>> own_ea_, own_r_;    // per pod: its own EA / R term classes
+    std::vector<std::vector<int>> g_tgt_, g_q_;       // per label group: PA / PAA, Q classes it matches
+    int npad_ = 0;
 };
 
 }  // namespace kbhip

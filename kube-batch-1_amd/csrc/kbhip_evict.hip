@@ -65,10 +65,31 @@ __global__ __launch_bounds__(64) void k_node_op(NodeCols nc, DevTables t, int op
     if (op == 0) {
         nc.rel_cpu[n] += rc; nc.rel_mem[n] += rm; nc.rel_gpu[n] += rg;
     } else if (op == 1) {
-        commit_node(t.classes[cls], t, nc, n, 2);
+        const TaskClass c = t.classes[cls];
+        commit_node(c, t, nc, n, 2);
+        if (c.aff) commit_aff(c, t, nc, n + nc.base, 2);  // a session-placed pod (inter-pod priority)
     } else {
-        uncommit_node(t.classes[cls], t, nc, n, 2);
+        const TaskClass c = t.classes[cls];
+        uncommit_node(c, t, nc, n, 2);
+        if (c.aff) uncommit_aff(c, t, nc, n + nc.base, 2);
     }
+}
+
+// Count-table changes queued on the host (evictions / unevicts of predicate
+// targets, kbhip_session.cpp flush_tables): idx >= 0 -> aff_cnt[idx],
+// idx < 0 -> aff_scalar[-1 - idx]; the indices are distinct.
+__global__ __launch_bounds__(kBlock) void k_tab_add(DevTables t, const int32_t* idx, const int32_t* delta, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int32_t x = idx[i];
+    if (x >= 0) t.aff_cnt[x] += delta[i];
+    else t.aff_scalar[-1 - x] += delta[i];
+}
+
+hipError_t launch_tab_add(const DevTables& t, const int32_t* idx, const int32_t* delta, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_tab_add, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, t, idx, delta, n);
+    return hipGetLastError();
 }
 
 // Accumulated evictions (op 0 of k_node_op, summed per node on the host):

@@ -68,6 +68,8 @@ hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const
                           int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
                           uint32_t* count);
 hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_nblk, hipStream_t st);
+// Count-table deltas (pod (anti-)affinity): idx >= 0 aff_cnt, < 0 aff_scalar[-1 - idx]; distinct indices.
+hipError_t launch_tab_add(const DevTables& t, const int32_t* idx, const int32_t* delta, int n, hipStream_t st);
 hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t* d, int n, hipStream_t st);
 hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
                           int64_t rg, hipStream_t st);

@@ -362,6 +362,7 @@ struct Session {
     bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
     DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt;
+    DevBuf b_tab_idx;  // count-table deltas (flush_tables)
     size_t rank_tmp_bytes = 0;
     uint64_t* h_rank = nullptr;  // pinned: [0] = count, then sorted keys
     size_t h_rank_cap = 0;
@@ -376,6 +377,9 @@ struct Session {
     vector<uint8_t> rel_flag;        // node is in rel_touched
     DevBuf b_rel_nodes, b_rel_d;
     int32_t fallback = -1;  // lowest node index holding a session-placed pod (nodeorder.go:78-93)
+    vector<int32_t> sess_cnt;  // per node: session-placed pods on it (fallback after an unpipeline)
+    std::unique_ptr<AffinityModel> aff;       // pod (anti-)affinity model (kept for evictions / carry)
+    std::map<int64_t, int32_t> tab_delta;     // pending count-table changes: idx >= 0 cnt, < 0 scalar (-1 - idx)
     // device
     Conf conf{};
     NodeCols nc{};
@@ -528,7 +532,7 @@ struct Session {
         for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
                           &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt,
-                          &b_shard_send, &b_shard_recv})
+                          &b_shard_send, &b_shard_recv, &b_tab_idx})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -1037,7 +1041,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 
     mark("jobs");
     // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
-    AffinityModel aff;
+    S.aff.reset(new AffinityModel());
+    AffinityModel& aff = *S.aff;
     {  // ap: filled in pass B
         try {
             aff.build(s, N, npad, ap, E.nss.strs, S.conf.pred_on != 0, S.conf.score_mult > 0 && S.conf.w_pa != 0);
@@ -1769,17 +1774,6 @@ static void ev_harvest_all(Session& S) {
     for (int k = 0; k < Session::kEvRing; ++k) ev_harvest(S, k);
 }
 
-// Some task class reads or writes the pod (anti-)affinity count tables
-// (kbhip_affinity.h): its program has predicate terms, inter-pod priority
-// terms or commit updates.  The tables are built from the snapshot at open;
-// paths that change pod statuses outside allocate / backfill (evictions,
-// carry) do not rebuild them, so they refuse such sessions.
-static bool has_aff_classes(const Session& S) {
-    for (auto& c : S.classes)
-        if (c.aff || c.ipa_n || c.upd_n) return true;
-    return false;
-}
-
 static bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
     // Backfilled nodes (some Idle grows on each walk visit): placement 6, one GPU only
@@ -1998,6 +1992,54 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
 #endif
 }
 
+// A session-placed pod (its Spec.NodeName is still "") arrives on / leaves
+// node n: the inter-pod priority's fallback node is the lowest such node
+// (nodeorder.go:78-93).
+static void sess_placed(Session& S, int n, int d) {
+    if (S.sess_cnt.empty()) S.sess_cnt.assign(S.nc.n, 0);
+    S.sess_cnt[n] += d;
+    if (d > 0 && (S.fallback < 0 || n < S.fallback)) S.fallback = n;
+    if (d < 0 && S.sess_cnt[n] == 0 && n == S.fallback) {
+        S.fallback = -1;
+        for (int k = n + 1; k < S.nc.n; ++k)
+            if (S.sess_cnt[k] > 0) { S.fallback = k; break; }
+    }
+}
+
+// Count-table changes of a predicate target leaving / re-entering the target
+// set (eviction / unevict, AffinityModel::target_updates), queued on the host
+// and applied before the next device read of the tables (flush_tables).
+static void queue_target(Session& S, int pi, int sign) {
+    if (!S.aff || !S.aff->active) return;
+    const HPod& p = S.pods[pi];
+    if (p.node < 0) return;
+    static thread_local vector<int32_t> upd;
+    S.aff->target_updates(pi, upd);
+    const int npad = S.aff->npad();
+    for (size_t k = 0; k + 2 < upd.size(); k += 3) {
+        if (upd[k] == UPD_CNT_ALLOC) {
+            const int d = S.aff->dom[(size_t)upd[k + 1] * npad + p.node];
+            if (d >= 0) S.tab_delta[(int64_t)upd[k + 2] + d] += sign;
+        } else if (upd[k] == UPD_SCALAR_ALLOC) {
+            S.tab_delta[-1 - (int64_t)upd[k + 2]] += sign;
+        }
+    }
+}
+static void flush_tables(Session& S) {
+    if (S.tab_delta.empty()) return;
+    vector<int32_t> idx, val;
+    for (auto& kv : S.tab_delta)
+        if (kv.second) { idx.push_back((int32_t)kv.first); val.push_back(kv.second); }
+    S.tab_delta.clear();
+    if (idx.empty()) return;
+    const int n = (int)idx.size();
+    int32_t* di = S.b_tab_idx.alloc<int32_t>(2 * (size_t)n);
+    idx.insert(idx.end(), val.begin(), val.end());
+    HIPCHK(hipMemcpyAsync(di, idx.data(), idx.size() * sizeof(int32_t), hipMemcpyHostToDevice, S.stream));
+    HIPCHK(launch_tab_add(S.tab, di, di + n, n, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));  // the pageable source must outlive the copy
+}
+
 // Host mirror of the device commits of consumed tasks (NodeInfo.Used, the
 // fallback node of nodeorder.go:78-93) + the caller's output arrays.
 static void apply_results(Session& S, const int32_t* ids, int n, const int32_t* res_node, const int32_t* res_kind,
@@ -2009,7 +2051,7 @@ static void apply_results(Session& S, const int32_t* ids, int n, const int32_t* 
         if (node >= 0) {
             const HPod& p = S.pods[ids[i]];
             S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
-            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
+            sess_placed(S, node, +1);
         }
     }
 }
@@ -2737,7 +2779,6 @@ struct Allocator {
     static bool less_strict(const R3& a, const R3& b) { return a.c < b.c && a.m < b.m && a.g < b.g; }
     void check_evict_supported() {
         if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt on a node-sharded session");
-        if (has_aff_classes(S)) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt with pod (anti-)affinity terms");
     }
     void on_deallocate(int pi) {  // event handlers drf.go:144-151, proportion.go:211-219
         const HPod& p = S.pods[pi];
@@ -2791,9 +2832,16 @@ struct Allocator {
         h.fallback = S.fallback;
         h.cls[0] = cls;
         h.ipa_lo[0] = h.ipa_hi[0] = 0;
+        flush_tables(S);  // evictions / unevicts so far change pod-affinity predicates
         HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
         HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, 2 * sizeof(uint32_t), S.stream));
-        const auto sr = S.class_srange[cls];
+        auto sr = S.class_srange[cls];
+        if (by_score && S.classes[cls].ipa_n > 0) {  // inter-pod priority: normalisation prepass, wider range
+            HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
+            const int64_t w = 10 * (int64_t)S.conf.w_pa * S.conf.score_mult;
+            sr.first += std::min<int64_t>(0, w);
+            sr.second += std::max<int64_t>(0, w);
+        }
         const bool counting = !S.force_radix && sr.second - sr.first < 256 && sr.first >= INT32_MIN &&
                               sr.second <= INT32_MAX;
         if (counting && S.rank_group) {  // one launch with the concurrent what-if sessions' rankings
@@ -2841,6 +2889,7 @@ struct Allocator {
     }
     // the session half of an eviction (session.go:331-356 / statement.go:35-67)
     void evict_in_session(int v) {
+        if (allocated_status(S.pods[v].status)) queue_target(S, v, -1);  // no longer a predicate target
         set_status(v, Releasing);
         // node.UpdateTask: Releasing += Resreq.  No node ranking reads Releasing, so
         // evictions are summed per node and applied in one launch (flush_evictions)
@@ -2870,9 +2919,11 @@ struct Allocator {
         HIPCHK(hipMemcpyAsync(dd, d.data(), d.size() * sizeof(int64_t), hipMemcpyHostToDevice, S.stream));
         HIPCHK(launch_rel_add(S.nc, dn, dd, n, S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));  // the pageable sources must outlive the copies
+        flush_tables(S);
     }
     void unevict(int v) {  // statement.go:81-105: node.AddTask fails, the node keeps its Releasing copy
         set_status(v, Running);
+        queue_target(S, v, +1);  // a predicate target again (the lister reads the job's status index)
         S.pods[v].node_rel = true;
         on_allocate(v);
     }
@@ -2884,6 +2935,7 @@ struct Allocator {
         nt.insert(std::lower_bound(nt.begin(), nt.end(), t), t);
         dev_op(1, t);
         S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+        sess_placed(S, n, +1);
         if (S.classes[p.cls].backfill) S.any_bf = 1;
         on_allocate(t);
     }
@@ -2894,6 +2946,7 @@ struct Allocator {
         nt.erase(std::lower_bound(nt.begin(), nt.end(), t));
         dev_op(2, t);
         S.used[p.node].c -= p.req.c; S.used[p.node].m -= p.req.m; S.used[p.node].g -= p.req.g;
+        sess_placed(S, p.node, -1);
         on_deallocate(t);
     }
     struct Stmt {  // framework.Statement: (0 evict | 1 pipeline, pod)
@@ -3233,7 +3286,7 @@ static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) 
             job.cnt_alloc++;
             job.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
             S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
-            if (S.fallback < 0 || node < S.fallback) S.fallback = node;
+            sess_placed(S, node, +1);
             A.on_allocate(pi);  // drf / proportion AllocateFunc
             S.stats.placed++;
             S.log.emplace_back(pi, node, KBHIP_ALLOCATED);
@@ -3505,7 +3558,6 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // at open.  New or deleted pods need a snapshot (kbhip_session_open).
 static void session_carry(Session& S) {
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "carry on a node-sharded session");
-    if (has_aff_classes(S)) throw Error(KBHIP_EUNSUPPORTED, "carry with pod (anti-)affinity terms");
     ov_quiesce(S);
     HIPCHK(hipStreamSynchronize(S.stream));
     const int N = S.nc.n, P = (int)S.pods.size();
@@ -3587,8 +3639,33 @@ static void session_carry(Session& S) {
         q.deserved = q.allocated = q.request = F3{};
         q.share = 0;
     }
+    // pod (anti)-affinity count tables of the carried pod states (the term
+    // classes and programs do not depend on statuses; their counts do)
+    S.tab_delta.clear();
+    if (S.aff && S.aff->active) {
+        vector<AffPod> ap(P);
+        for (int i = 0; i < P; ++i) {
+            const HPod& p = S.pods[i];
+            AffPod& a = ap[i];
+            a.ns = p.ns;
+            a.status = p.status;
+            a.session_job = p.job >= 0;
+            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
+            a.node = on_node ? p.node : -1;
+            a.target = a.session_job && allocated_status(p.status) && on_node;
+            a.pending = a.session_job && p.status == Pending;
+        }
+        S.aff->recount(ap);
+        HIPCHK(hipMemcpyAsync(S.tab.aff_cnt, S.aff->cnt.data(), S.aff->cnt.size() * sizeof(int32_t),
+                              hipMemcpyHostToDevice, S.stream));
+        HIPCHK(hipMemcpyAsync(S.tab.aff_scalar, S.aff->scalar.data(), S.aff->scalar.size() * sizeof(int32_t),
+                              hipMemcpyHostToDevice, S.stream));
+        HIPCHK(hipStreamSynchronize(S.stream));
+        S.carry_bytes += (int64_t)(S.aff->cnt.size() + S.aff->scalar.size()) * (int64_t)sizeof(int32_t);
+    }
     S.plugins_opened = false;
     S.fallback = -1;
+    S.sess_cnt.clear();
     S.node_tasks.clear();
     S.log.clear();
     S.last_fit_ok = false;

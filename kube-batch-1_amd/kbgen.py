@@ -905,19 +905,45 @@ def gen_preempt(seed: int, n_nodes: int = 8, n_queues: int = 3, n_run_jobs: int 
     queues of unequal weight (so some queues sit above their proportion share),
     pending higher-priority jobs, gang sizes that make some victims protected, some
     kube-system / system-critical pods (conformance), releasing and backfill pods.
-    Features: "selector", "taints", "ports", "init", "bestEffort", "unsched"."""
+    Features: "selector", "taints", "ports", "init", "bestEffort", "unsched", "podaffinity"
+    (zone labels; running and pending pods with app labels and required / preferred pod
+    (anti-)affinity terms by zone or hostname)."""
     rng = np.random.default_rng(seed)
     f = set(features)
     c = Cluster(tiers=tiers)
+    zones = ["za", "zb", "zc"]
     for i in range(n_nodes):
         name = f"n{i:03d}"
         taints = []
         if "taints" in f and rng.random() < 0.2:
             taints.append(("dedicated", "a", "NoSchedule"))
+        labels = {"itype": ["small", "big"][int(rng.integers(2))], "kubernetes.io/hostname": name}
         c.add_node(name, int(rng.choice([4000, 8000])), int(rng.choice([8, 16])) * GI,
                    int(rng.choice([0, 0, 4000])), int(rng.choice([4, 110])),
-                   labels={"itype": ["small", "big"][int(rng.integers(2))], "kubernetes.io/hostname": name},
-                   taints=taints, unschedulable=("unsched" in f and rng.random() < 0.1))
+                   labels=labels, taints=taints, unschedulable=("unsched" in f and rng.random() < 0.1))
+        if "podaffinity" in f:
+            labels["zone"] = zones[int(rng.integers(3))]
+
+    def paff(own_job):
+        """(labels, affinity) of a pod under the "podaffinity" feature."""
+        labels = {"job": own_job}
+        if rng.random() < 0.5:
+            labels["app"] = ["x", "y"][int(rng.integers(2))]
+        if rng.random() >= 0.45:
+            return labels, None
+        tk = ["zone", "kubernetes.io/hostname"][int(rng.integers(2))]
+        sel = {"ml": {"app": ["x", "y"][int(rng.integers(2))]}} if rng.random() < 0.7 else {"ml": {"job": own_job}}
+        term = {"selector": sel, "topology_key": tk}
+        kind = int(rng.integers(4))
+        if kind == 0:
+            aff = {"anti": {"required": [term]}}
+        elif kind == 1:
+            aff = {"pod": {"required": [term]}}
+        elif kind == 2:
+            aff = {"pod": {"preferred": [(int(rng.integers(1, 10)), term)]}}
+        else:
+            aff = {"anti": {"preferred": [(int(rng.integers(1, 10)), term)], "required": [term]}}
+        return labels, aff
     for q in range(n_queues):
         c.add_queue(f"q{q}", int(rng.integers(1, 5)), ts=int(rng.integers(0, 2)) * SEC)
     free = {n.name: [n.cpu, n.mem, n.gpu] for n in c.nodes}
@@ -947,10 +973,11 @@ def gen_preempt(seed: int, n_nodes: int = 8, n_queues: int = 3, n_run_jobs: int 
                 free[node][0] -= r["cpu"]; free[node][1] -= r["mem"]; free[node][2] -= r.get("gpu", 0)
             pc = ["", "", "", "system-node-critical", "system-cluster-critical"][int(rng.integers(5))] \
                 if rng.random() < 0.15 else ""
+            labels, aff = paff(jn) if "podaffinity" in f else ({"job": jn}, None)
             c.add_pod(ns, f"{jn}-{k}", uid=f"u{uid:05d}", group=jn, node=node, phase=phase,
                       deleting=(node is not None and rng.random() < 0.05), priority=int(rng.choice([0, 1])),
                       ts=int(rng.integers(0, 2)) * SEC, backfill=(node is not None and rng.random() < 0.1),
-                      priority_class=pc, labels={"job": jn}, containers=[r])
+                      priority_class=pc, labels=labels, containers=[r], affinity=aff)
             uid += 1
     # pending preemptor jobs
     for j in range(n_pend_jobs):
@@ -970,9 +997,10 @@ def gen_preempt(seed: int, n_nodes: int = 8, n_queues: int = 3, n_run_jobs: int 
             nsel = {"itype": "big"} if ("selector" in f and rng.random() < 0.2) else {}
             tols = [{"key": "dedicated", "op": "Exists", "value": "", "effect": ""}] \
                 if ("taints" in f and rng.random() < 0.5) else []
+            labels, aff = paff(jn) if "podaffinity" in f else ({"job": jn}, None)
             c.add_pod("ns2", f"{jn}-{k}", uid=f"u{uid:05d}", group=jn, priority=pri,
-                      ts=int(rng.integers(1, 3)) * SEC, labels={"job": jn}, containers=ctrs,
-                      init_containers=inits, node_selector=nsel, tolerations=tols)
+                      ts=int(rng.integers(1, 3)) * SEC, labels=labels, containers=ctrs,
+                      init_containers=inits, node_selector=nsel, tolerations=tols, affinity=aff)
             uid += 1
     return c
 

@@ -56,6 +56,32 @@ def test_carry_equals_fresh_session(engine, oracle_mod, kbgen_mod, tmp_path, see
     assert np.array_equal(ns.astype(np.float64), ons[:n_nodes])
 
 
+@pytest.mark.parametrize("seed", range(16))
+def test_carry_pod_affinity(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Sessions with pod (anti-)affinity terms: the carried session's count
+    tables are recounted from the carried pod states."""
+    if seed % 2:
+        c = kbgen_mod.gen_preempt(2300 + seed, n_nodes=4 + seed % 8, n_queues=1 + seed % 3, n_run_jobs=4 + seed % 7,
+                                  n_pend_jobs=3 + seed % 5, max_tasks=2 + seed % 5, features=("podaffinity", "ports"))
+    else:
+        c = kbgen_mod.gen_random(2400 + seed, n_nodes=4 + seed % 10, n_jobs=5 + seed % 8, max_tasks=2 + seed % 6)
+    if seed % 4 == 0:
+        c.args = {"nodeorder": {"podaffinity.weight": "2"}}
+    acts = ACTS[seed % len(ACTS)]
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    n_nodes = len(c.nodes)
+    with engine.Session(p1) as s:
+        s.run_actions(acts)
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+        s.carry()
+        pod, nd, kind = s.run_actions(acts)
+        ns = s.read_nodes(n_nodes)
+    p2 = _next_snapshot(c, status, node).write(str(tmp_path / "s2.kbs"))
+    exp, ons = oracle_mod.ref_allocate(p2, actions=acts, with_nodes=True)
+    assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)] == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:n_nodes])
+
+
 def test_carry_c4_scaled_uploads_a_delta(engine, kbgen_mod, tmp_path):
     """C4-shaped, 20k nodes: the carry sends only the node rows the binds changed, and
     the carried session schedules only tasks that are still pending."""

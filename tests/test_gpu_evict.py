@@ -69,6 +69,21 @@ def test_random_preempt_snapshots(engine, oracle_mod, kbgen_mod, tmp_path, seed)
     _check(engine, oracle_mod, p, ACTIONS[seed % len(ACTIONS)])
 
 
+@pytest.mark.parametrize("seed", range(40))
+def test_random_preempt_pod_affinity(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Pod (anti-)affinity and inter-pod priority terms on running and pending
+    pods: evicting a predicate target withdraws it from the count tables, an
+    unevict restores it, a pipelined preemptor counts for the inter-pod
+    priority at the fallback node (predicates.go:59-94, nodeorder.go:78-93)."""
+    c = kbgen_mod.gen_preempt(1500 + seed, n_nodes=4 + seed % 10, n_queues=1 + seed % 4, n_run_jobs=4 + seed % 9,
+                              n_pend_jobs=2 + seed % 5, max_tasks=1 + seed % 6, tiers=TIERS[seed % len(TIERS)],
+                              features=("podaffinity",) + (FEATURES if seed % 2 else ()))
+    if seed % 3 == 0:
+        c.args = {"nodeorder": {"podaffinity.weight": str(1 + seed % 4)}}
+    p = c.write(str(tmp_path / "a.kbs"))
+    _check(engine, oracle_mod, p, ACTIONS[seed % len(ACTIONS)])
+
+
 @pytest.mark.parametrize("first", [1, 3])
 def test_chunked_readback(engine, oracle_mod, kbgen_mod, tmp_path, first):
     """Passing-node lists longer than the keys read back with the count (option
@@ -89,16 +104,19 @@ def test_chunked_readback(engine, oracle_mod, kbgen_mod, tmp_path, first):
     assert any(k == 128 for _, _, k in exp_all)
 
 
-def test_pod_affinity_rejected(engine, kbgen_mod, tmp_path):
+def test_pod_affinity_hand(engine, oracle_mod, kbgen_mod, tmp_path):
+    """A pending pod with required anti-affinity against the running pod's
+    labels (by hostname) beside a plain reclaimer: records equal the faithful
+    restatement's (the pod-affinity lister lists AllocatedStatuses tasks only,
+    predicates.go:59-94)."""
     c = _hand(kbgen_mod, "q1", 1)
     term = {"selector": {"ml": {"job": "r0"}, "me": []}, "topology_key": "kubernetes.io/hostname"}
     c.add_job("ns2", "p1", "q1", min_member=1)
-    c.add_pod("ns2", "p1-0", uid="b1", group="p1", containers=[kbgen_mod.res(cpu=100, mem=1 << 20)],
+    c.add_pod("ns2", "p1-0", uid="b1", group="p1", priority=10, containers=[kbgen_mod.res(cpu=100, mem=1 << 20)],
               affinity={"anti": {"required": [term]}})
     p = c.write(str(tmp_path / "a.kbs"))
-    with engine.Session(p) as s:
-        with pytest.raises(engine.KbhipError):
-            s.reclaim()
+    got = _check(engine, oracle_mod, p, "reclaim")
+    assert (0, 0, 128) in got
 
 
 # ---- C5 (SURVEY §8(d)): the what-if session shape -----------------------------
