@@ -1996,12 +1996,12 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
 // node n: the inter-pod priority's fallback node is the lowest such node
 // (nodeorder.go:78-93).
 static void sess_placed(Session& S, int n, int d) {
-    if (S.sess_cnt.empty()) S.sess_cnt.assign(S.nc.n, 0);
+    if (S.sess_cnt.empty()) S.sess_cnt.assign(S.n_total, 0);  // global node indices (shards too)
     S.sess_cnt[n] += d;
     if (d > 0 && (S.fallback < 0 || n < S.fallback)) S.fallback = n;
     if (d < 0 && S.sess_cnt[n] == 0 && n == S.fallback) {
         S.fallback = -1;
-        for (int k = n + 1; k < S.nc.n; ++k)
+        for (int k = n + 1; k < S.n_total; ++k)
             if (S.sess_cnt[k] > 0) { S.fallback = k; break; }
     }
 }
