@@ -292,7 +292,7 @@ __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClas
     const Row r = load_row_sc1(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, n);
+        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, n);
     int32_t s;
     bool passed;
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
@@ -351,11 +351,11 @@ __device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables
     if (n >= 0) {
         base = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     uint64_t key = K;                                  // real key of the node after `ca + cp` commits
     int32_t rm = K ? key_score(K) : 0;                 // running minimum of its scores
@@ -410,7 +410,7 @@ __device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pwc[w];
     }
     if (lane < done)
         __hip_atomic_store(&out->g[lane],
@@ -583,12 +583,12 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     } else if (n >= 0) {
         base = load_row_t<SC1>(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     STAMP(gridDim.x * 4 + 11); PSTAMP(1);
     uint64_t pwc[4];
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
     if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
@@ -762,7 +762,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             st_sc1(&nc.nzc[ln], r.nzc);
             st_sc1(&nc.nzm[ln], r.nzm);
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
+                for (int w = 0; w < port_win(c, nc); ++w) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
         } else {
             nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
             nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
@@ -770,7 +770,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             nc.nzc[ln] = r.nzc;
             nc.nzm[ln] = r.nzm;
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
+                for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
         }
     }
     if (ho) {  // committed rows, compacted (lane order)
@@ -842,11 +842,11 @@ __device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables
     } else if (n >= 0) {
         base = load_row_t<SC1>(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<SC1>(nc, w, n);
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     // this lane's chain: depth d of its newest entry, commits by kind behind it, first Pipeline depth
     int d = 0, ca = 0, cp = 0, apos = 64;
@@ -937,7 +937,7 @@ __device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables
             st_sc1(&nc.nzc[ln], r.nzc);
             st_sc1(&nc.nzm[ln], r.nzm);
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) st_sc1(&nc.ports[(int64_t)w * nc.npad + ln], pwc[w]);
+                for (int w = 0; w < port_win(c, nc); ++w) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
         } else {
             nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
             nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
@@ -945,7 +945,7 @@ __device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables
             nc.nzc[ln] = r.nzc;
             nc.nzm[ln] = r.nzm;
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + ln] = pwc[w];
+                for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
         }
     }
     if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
@@ -986,7 +986,7 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
     if (n >= 0) {
         r = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     const bool has_bf = (r.bf_cpu | r.bf_mem | r.bf_gpu) != 0;
@@ -1009,7 +1009,7 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
         if (win) {
             r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
             if (c.has_ports)
-                for (int q = 0; q < 4; ++q) pw[q] |= (q < nc.port_words) ? t.masks[c.pown_off + q] : 0;
+                for (int q = 0; q < 4; ++q) pw[q] |= (q < port_win(c, nc)) ? t.masks[c.pown_off + q] : 0;
         }
         if (visit || win) {
             changed = true;
@@ -1027,7 +1027,7 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pw[w];
+            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pw[w];
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane],
@@ -1081,7 +1081,7 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
     if (n >= 0) {
         r = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     const uint64_t t0 = readlane64(K, 63);  // the list's last key (0: the list holds every feasible node)
@@ -1127,7 +1127,7 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
             }
             r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
             if (c.has_ports)
-                for (int q = 0; q < 4; ++q) pw[q] |= (q < nc.port_words) ? t.masks[c.pown_off + q] : 0;
+                for (int q = 0; q < 4; ++q) pw[q] |= (q < port_win(c, nc)) ? t.masks[c.pown_off + q] : 0;
             changed = true;
             int32_t s = 0;
             bool passed = false;
@@ -1146,7 +1146,7 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pw[w];
+            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pw[w];
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane],
@@ -1168,7 +1168,7 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
         e.node = g;
         e.row = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) e.pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < port_win(c, nc); ++w) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
         e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
     }
     msg->c[lane] = e;

@@ -40,6 +40,15 @@ struct ShardMsg {
     ShardCand c[kTopK];
 };
 
+// Host-port words of a class: its window of the port columns (TaskClass::pw_lo).
+KBHIP_HD int port_win(const TaskClass& c, const NodeCols& nc) {
+    const int k = nc.port_words - c.pw_lo;
+    return k < kPortWin ? k : kPortWin;
+}
+KBHIP_HD int64_t port_at(const TaskClass& c, const NodeCols& nc, int w, int n) {
+    return (int64_t)(c.pw_lo + w) * nc.npad + n;
+}
+
 KBHIP_HD Row load_row(const NodeCols& nc, int n) {
     Row r;
     r.idle_cpu = nc.idle_cpu[n]; r.idle_mem = nc.idle_mem[n]; r.idle_gpu = nc.idle_gpu[n];
@@ -151,7 +160,7 @@ KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t
     if (cf.pred_on) {
         if (r.maxtasks <= r.pods) ok = false;                            // predicates.go:127
         if (c.has_ports)                                                 // host_ports.go:96-125
-            for (int w = 0; w < nc.port_words; ++w)
+            for (int w = 0; w < port_win(c, nc); ++w)
                 if (portw[w] & t.masks[c.pconf_off + w]) ok = false;
     }
     if (ok && c.score_err) ok = false;  // NodeOrderFn error drops the node (allocate.go:141-145)
@@ -192,7 +201,7 @@ KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables&
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
     if (fit) *fit = fit_bits(c, r, *passed);
     return k;
@@ -210,7 +219,7 @@ KBHIP_HD uint64_t eval_node_walk(const Conf& cf, const TaskClass& c, const DevTa
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
     int32_t s = 0;
     bool passed = false;
     uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
@@ -283,7 +292,7 @@ KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTab
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed, ipa);
     if (fit) *fit = fit_bits(c, r, *passed);
     return k;
@@ -298,8 +307,8 @@ KBHIP_HD uint64_t eval_first_fit(const Conf& cf, const TaskClass& c, const DevTa
         if (c.aff) ok = aff_pred(c, t, nc, n);
         if (nc.maxtasks[n] <= nc.pods[n]) ok = false;                    // predicates.go:127
         if (c.has_ports)                                                 // host_ports.go:96-125
-            for (int w = 0; w < nc.port_words; ++w)
-                if (nc.ports[(int64_t)w * nc.npad + n] & t.masks[c.pconf_off + w]) ok = false;
+            for (int w = 0; w < port_win(c, nc); ++w)
+                if (nc.ports[port_at(c, nc, w, n)] & t.masks[c.pconf_off + w]) ok = false;
     }
     return ok ? pack_key(0, n + nc.base, 0) : 0;
 }
@@ -362,7 +371,7 @@ KBHIP_HD void commit_node(const TaskClass& c, const DevTables& t, const NodeCols
     nc.nzc[n] += c.nz_cpu;
     nc.nzm[n] += c.nz_mem;
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words; ++w) nc.ports[(int64_t)w * nc.npad + n] |= t.masks[c.pown_off + w];
+        for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] |= t.masks[c.pown_off + w];
 }
 
 // Exact inverse of commit_node for a batched-path class (integer updates; the
@@ -376,7 +385,7 @@ KBHIP_HD void uncommit_node(const TaskClass& c, const DevTables& t, const NodeCo
     nc.nzc[n] -= c.nz_cpu;
     nc.nzm[n] -= c.nz_mem;
     if (c.has_ports)
-        for (int w = 0; w < nc.port_words; ++w) nc.ports[(int64_t)w * nc.npad + n] &= ~t.masks[c.pown_off + w];
+        for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] &= ~t.masks[c.pown_off + w];
 }
 
 // Gang bookkeeping after an assignment: allocate.go:191-195 + gang.go:63-66.

@@ -381,11 +381,11 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     if (n >= 0 && wave <= kDepth) {
         base = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = nc.ports[(int64_t)w * nc.npad + n];
+            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < nc.port_words) ? t.masks[c.pown_off + w] : 0);
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     if (wave < kDepth) {
         uint64_t v = 0;
         if (n >= 0) {
@@ -483,7 +483,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < nc.port_words && w < 4; ++w) nc.ports[(int64_t)w * nc.npad + n] = pwc[w];
+            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pwc[w];
     }
     if (lane < done)
         __hip_atomic_store(&out->g[lane],
@@ -662,7 +662,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         const int ln = lk ? key_node(lk, a) : -1;
         if (ln >= 0) {
             rc.row[lane] = load_row(nc, ln);
-            for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < nc.port_words) ? load_port_t<false>(nc, w, ln) : 0;
+            for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < port_win(c, nc)) ? load_port_t<false>(nc, c.pw_lo + w, ln) : 0;
             rc.na[lane] = cf.score_mult ? na_weight(c, t, nc, ln) : 0;
         }
         if (tn[0] >= 0) {
@@ -693,7 +693,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             const Row r = load_row_sc1(nc, tn[0]);
             uint64_t pw[4] = {0, 0, 0, 0};
             if (c.has_ports)
-                for (int w = 0; w < nc.port_words && w < 4; ++w) pw[w] = load_port_t<true>(nc, w, tn[0]);
+                for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn[0]);
             rc.row[64 + lane] = r;
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;

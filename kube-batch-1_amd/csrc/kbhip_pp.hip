@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pp_sweep(Conf cf, NodeCols nc, 
             st_row_sc1(&slot->row[j], load_row_sc1(nc, n));
             for (int w = 0; w < 4; ++w)
                 // the node's port words whatever this class asks: the placer keeps the row for later pops
-                st_sc1(&slot->pw[j][w], (uint64_t)(w < nc.port_words ? load_port_t<true>(nc, w, n) : 0ull));
+                st_sc1(&slot->pw[j][w], (uint64_t)(w < port_win(c, nc) ? load_port_t<true>(nc, c.pw_lo + w, n) : 0ull));
             st_sc1(&slot->na[j], cf.score_mult ? na_weight(c, t, nc, n) : 0);
         }
     } else if (wave == 2) {

@@ -1283,21 +1283,55 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         cls_pod.push_back(i);  // classes are created in pod order: i is the class's first pod
     }
     mark("classes:loop");
-    // port masks per class (conflict = CheckConflict, own = HostPortInfo.Add)
-    if (E.port_defs.size() > 256) fail_unsupported("more than 256 distinct host ports");
+    // port masks per class (conflict = CheckConflict, own = HostPortInfo.Add).
+    // Port ids are renumbered in (protocol, port, IP) order, so the ids one
+    // (protocol, port) can conflict with are contiguous; a class's masks then
+    // cover a window of kPortWin words (TaskClass::pw_lo) of the node columns.
+    {
+        const size_t U = E.port_defs.size();
+        vector<int> order(U), new_id(U);
+        for (size_t u = 0; u < U; ++u) order[u] = (int)u;
+        std::sort(order.begin(), order.end(), [&](int a, int b) {
+            auto [aip, apr, aport] = E.port_defs[a];
+            auto [bip, bpr, bport] = E.port_defs[b];
+            return std::make_tuple(apr, aport, aip) < std::make_tuple(bpr, bport, bip);
+        });
+        vector<std::tuple<int, int, int32_t>> defs(U);
+        for (size_t k = 0; k < U; ++k) { new_id[order[k]] = (int)k; defs[k] = E.port_defs[order[k]]; }
+        E.port_defs.swap(defs);
+        for (auto& id : S.pod_port_ids) id = new_id[id];
+        for (auto& v : node_ports)
+            for (auto& id : v) id = new_id[id];
+        E.port_ids.clear();
+    }
     E.pw = ((int)E.port_defs.size() + 63) / 64;
     {
         int zero_ip = E.ip_dict.get("0.0.0.0");
         for (size_t ci = 0; ci < S.classes.size(); ++ci) {
             TaskClass& c = S.classes[ci];
-            vector<uint64_t> conf(E.pw, 0), own(E.pw, 0);
+            int lo = INT32_MAX, hi = -1;  // ids the class's masks touch
+            auto touch = [&](int id) { lo = std::min(lo, id); hi = std::max(hi, id); };
             for (int id : pod_ports[cls_pod[ci]]) {
                 auto [ip, pr, port] = E.port_defs[id];
-                own[id / 64] |= 1ULL << (id % 64);
+                touch(id);
                 for (size_t u = 0; u < E.port_defs.size(); ++u) {
                     auto [uip, upr, uport] = E.port_defs[u];
                     if (upr != pr || uport != port) continue;
-                    if (ip == zero_ip || uip == zero_ip || uip == ip) conf[u / 64] |= 1ULL << (u % 64);
+                    if (ip == zero_ip || uip == zero_ip || uip == ip) touch((int)u);
+                }
+            }
+            c.pw_lo = hi < 0 ? 0 : lo / 64;
+            if (hi >= 0 && hi / 64 - c.pw_lo >= kPortWin)
+                fail_unsupported("a pod's host ports and their conflicts span more than " +
+                                 std::to_string(kPortWin * 64) + " port ids");
+            vector<uint64_t> conf(kPortWin, 0), own(kPortWin, 0);
+            for (int id : pod_ports[cls_pod[ci]]) {
+                auto [ip, pr, port] = E.port_defs[id];
+                own[id / 64 - c.pw_lo] |= 1ULL << (id % 64);
+                for (size_t u = 0; u < E.port_defs.size(); ++u) {
+                    auto [uip, upr, uport] = E.port_defs[u];
+                    if (upr != pr || uport != port) continue;
+                    if (ip == zero_ip || uip == zero_ip || uip == ip) conf[u / 64 - c.pw_lo] |= 1ULL << (u % 64);
                 }
             }
             c.pconf_off = (int32_t)E.masks.size();
@@ -1781,7 +1815,7 @@ static bool batchable(const Session& S, int cls) {
     // pod-affinity classes: placement 7 (anti-affinity predicates only), one GPU, no Backfilled nodes
     const bool aff_ok = !c.aff || (S.aff_batch && S.world == 1 && !S.any_bf && aff_batchable(c));
     return S.batched && (S.world == 1 || S.comm || S.xgfn) && bf_ok && !c.backfill && aff_ok &&
-           S.nc.port_words <= 4 && S.n_total < (1 << 25);
+           S.n_total < (1 << 25);
 }
 
 static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {

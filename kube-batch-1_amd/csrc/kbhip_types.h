@@ -78,8 +78,10 @@ struct TaskClass {
     int32_t paa_space, paa_cnt;
     int32_t ipa_off, ipa_n;                // aff_items quads (space, cnt_off, sess, weight)
     int32_t upd_off, upd_n;                // aff_items triples (type, space, off)
-    int32_t pad0;
+    int32_t pw_lo;  // host-port window: the class's conflict / own masks cover port words
+                    // pw_lo .. pw_lo + kPortWin - 1 (port ids sorted by protocol, port, IP)
 };
+constexpr int kPortWin = 4;  // port words a class's masks span (its ports' 256-id window)
 
 // Session-wide constants of the plugin configuration.
 struct Conf {

@@ -42,4 +42,6 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
         assert got == oracle_mod.ref_allocate(p, actions=ACTIONS).as_list()
     req = sum(st["rank_requests"] for _, st in res)
     bsum = sum(st["rank_batch_sum"] for _, st in res)
-    assert req > 0 and bsum > req  # some launch ranked more than one session's nodes
+    assert req > 0 and bsum >= req
+    if n_sessions > 2:  # two threads need not meet in a ranking; six do
+        assert bsum > req  # some launch ranked more than one session's nodes
