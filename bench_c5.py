@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--pending", type=int, default=2000)
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the hoisted CPU restatement on one session")
+    ap.add_argument("--pop-group", type=int, default=0,
+                    help="1 = concurrent sessions' allocate pops share launches (option pop_group, PopBatcher; "
+                         "measured slower here: the sessions reach their pops at different times)")
     ap.add_argument("--concurrent", type=int, default=8,
                     help="what-if sessions in flight (host threads); their node rankings share launches")
     args = ap.parse_args()
@@ -116,11 +119,15 @@ def main():
     print(json.dumps(out))
 
 
+POP_GROUP = [1]
+
+
 def one_session(buf, group, barrier=None):
     t0 = time.perf_counter()
     s = kbhip.Session(buf, device=0)
     if group:
         s.set_option("rank_group", 1)
+        s.set_option("pop_group", POP_GROUP[0])
     if barrier is not None:
         barrier.wait()
     counts = {1: 0, 2: 0, 3: 0}
@@ -135,12 +142,14 @@ def one_session(buf, group, barrier=None):
 
 def concurrent(args, bufs):
     """S what-if sessions in flight from S host threads (the engine releases the
-    GIL); their reclaim / preempt node rankings are batched into shared
-    launches (option rank_group, kbhip_session.cpp RankBatcher)."""
+    GIL); their reclaim / preempt node rankings and their allocate pops are
+    batched into shared launches (option rank_group, kbhip_session.cpp
+    RankBatcher / PopBatcher)."""
     from concurrent.futures import ThreadPoolExecutor
     # the sessions of one wave of `concurrent` start together (a barrier after
     # their opens), as a what-if sweep over one cluster state would
     warm, timed = bufs[:args.warmup], bufs[args.warmup:]
+    POP_GROUP[0] = args.pop_group
     import threading
 
     def waves(ex, bs):
@@ -159,6 +168,8 @@ def concurrent(args, bufs):
     lat = [r[0] for r in res]
     req = sum(r[2]["rank_requests"] for r in res)
     bsum = sum(r[2]["rank_batch_sum"] for r in res)
+    preq = sum(r[2]["pop_requests"] for r in res)  # allocate pops batched across sessions
+    pbsum = sum(r[2]["pop_batch_sum"] for r in res)
     seq_lat, _, _ = one_session(timed[0], False)  # one session alone, for the latency beside the throughput
     out = {
         "metric": "C5 what-if sessions/s (reclaim, allocate, backfill, preempt)",
@@ -178,6 +189,9 @@ def concurrent(args, bufs):
                                 "allocated": statistics.mean(r[1][1] for r in res)},
         "rank_launch_requests": req,
         "sessions_per_rank_launch": bsum / max(req, 1),
+        "pop_group": args.pop_group,
+        "pop_launch_requests": preq,
+        "sessions_per_pop_launch": pbsum / max(preq, 1),
     }
     if args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -94,6 +94,8 @@ typedef struct kbhip_stats {
     int64_t pp_retries;      /* pop chunks the persistent placer could not start (swept again without it) */
     int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if batcher ("rank_group") */
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
+    int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
+    int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

@@ -145,6 +145,24 @@ hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables&
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
+// A batched pop of one session in a multi-session launch (what-if sessions,
+// placement 6 or 7): the arguments of launch_pop_batch.
+constexpr int kPopMulti = 8;  // sessions per launch (kernel argument space)
+struct PopReq {
+    Conf cf;
+    NodeCols nc;
+    DevTables t;
+    int cls, n_tasks, gang_mode, min_avail, ready_count;
+    uint32_t epoch;
+    KeyFormat kf;
+    uint64_t* cand;
+    uint32_t* arrive;
+    void* out;
+    int placement, fit_set;
+};
+// Launches every request (grouped by nodes per lane, key type and placement,
+// kPopMulti per launch; *launches = launches made).
+hipError_t launch_pop_batch_multi(const PopReq* reqs, int n, hipStream_t st, int* launches);
 size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);

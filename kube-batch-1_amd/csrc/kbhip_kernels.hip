@@ -23,6 +23,7 @@
 //    (kbhip_affinity.h); k_ipa_minmax is the score's normalisation prepass.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <vector>
 
 #include "kbhip_batch.h"
 #include "kbhip_internal.h"
@@ -225,10 +226,29 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
 // (no placement: the exchange follows), -1 the test-only modes 0 / 1 / 4 —
 // so that a kernel's registers (and the occupancy of its sweep blocks) are
 // those of one placement path.
+// One session's batched pop in a multi-session launch (k_pop_batch_multi):
+// the kernel arguments carry kPopMulti descriptors (4 KB kernarg limit).
+struct PopDesc {
+    Conf cf;
+    NodeCols nc;
+    DevTables t;
+    PopArgs a;
+    uint64_t* cand;
+    uint32_t* arrive;
+    void* out;
+    int nb;
+};
+struct PopDescs {
+    PopDesc d[kPopMulti];
+};
+static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed the kernel argument space");
+
+// The batched pop's body: block `bid` of `nb_` (k_pop_batch: the grid's own;
+// k_pop_batch_multi: one session's blocks within a multi-session grid).
 template <int R, typename KT, int PL>
-__global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                           uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                           ShardMsg* smsg) {
+__device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
+                                               uint64_t* cand64, uint32_t* arrive, PopOut* out, ShardMsg* smsg,
+                                               const int bid, const int nb_) {
     __shared__ KT wlk[kPopThreads / 64][64];  // sweep / merge lists in the key type
     __shared__ uint64_t wl64[sizeof(KT) == 8 ? 1 : kPopThreads / 64][64];
     uint64_t (*wl)[64] = nullptr;             // placement lists (64-bit keys / entries)
@@ -241,7 +261,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     uint32_t* fitc = fit_counters(arrive, a.fit_set);
     fit_zero_other(arrive, a.fit_set);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    STAMP(blockIdx.x * 4 + 0);
+    STAMP(bid * 4 + 0);
     const TaskClass c = t.classes[a.cls];
     if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
     // 1. evaluate R nodes per lane, wave top-64, block top-64
@@ -249,7 +269,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     uint32_t fbs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
+        const int n = (bid * R + r) * kPopThreads + threadIdx.x;
         KT k = 0;
         fbs[r] = 0;
         if (n < nc.n) {
@@ -266,21 +286,21 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < R; ++r) fit_block_add(s_fitb, fbs[r]);
-    STAMP(blockIdx.x * 4 + 1);
+    STAMP(bid * 4 + 1);
     block_tree_merge(wlk, wave, lane);
-    const int nb = gridDim.x;
-    const int g = blockIdx.x % kGroups;
+    const int nb = nb_;
+    const int g = bid % kGroups;
     const int g_count = (nb - g + kGroups - 1) / kGroups;   // blocks in my group
     const int n_groups = nb < kGroups ? nb : kGroups;
     KT* gcand = cand + (int64_t)nb * 64;                     // group lists after the block lists
     if (wave == 0) {
         if (lane < 4 && s_fitb[lane])
             __hip_atomic_fetch_add(&fitc[g * kCtrStride + lane], s_fitb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
+        put_list(cand + (int64_t)bid * 64, wlk[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    STAMP(blockIdx.x * 4 + 2);
+    STAMP(bid * 4 + 2);
     if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
     __syncthreads();
     if (!role) return;
@@ -311,7 +331,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         __syncthreads();
         if (!role) return;
     }
-    STAMP(gridDim.x * 4 + 4);
+    STAMP(nb_ * 4 + 4);
     // 2b. last group merger: merge the group lists; reset the counters for the next launch
     {
         KT acc = 0;
@@ -320,7 +340,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
-    STAMP(gridDim.x * 4 + 0);
+    STAMP(nb_ * 4 + 0);
     if constexpr (sizeof(KT) != 8) {  // placement works on 64-bit keys
         const uint64_t k64 = key64_of(wlk[0][lane], a);
         __syncthreads();
@@ -338,34 +358,34 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         return;
     } else if constexpr (PL == 6) {  // Backfilled nodes in the session
         if (wave != 0) return;
-        STAMP(gridDim.x * 4 + 1);
+        STAMP(nb_ * 4 + 1);
         place_bf(cf, nc, t, c, a, out, wl[0][lane]);
-        STAMP(gridDim.x * 4 + 3);
+        STAMP(nb_ * 4 + 3);
         return;
     } else if constexpr (PL == 7) {  // pod-affinity class (aff_batchable)
         if (wave != 0) return;
-        STAMP(gridDim.x * 4 + 1);
+        STAMP(nb_ * 4 + 1);
         place_aff(cf, nc, t, c, a, out, wl[0][lane]);
-        STAMP(gridDim.x * 4 + 3);
+        STAMP(nb_ * 4 + 3);
         return;
     } else {
     if constexpr (PL == 2 || PL == 5) {  // every wave takes part
-        STAMP(gridDim.x * 4 + 1);
+        STAMP(nb_ * 4 + 1);
         if (a.ent32) place_parallel<uint32_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
         else place_parallel<uint64_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
         return;
     } else {
     if (a.placement == 1) {  // uniform
         if (wave != 0) return;
-        STAMP(gridDim.x * 4 + 1);
+        STAMP(nb_ * 4 + 1);
         place_levels(cf, nc, t, c, a, wl[0][lane], out);
         return;
     }
     if (a.placement == 4) {  // uniform
         if (wave != 0) return;
-        STAMP(gridDim.x * 4 + 1);
+        STAMP(nb_ * 4 + 1);
         place_insert<false>(cf, nc, t, c, a, out, wl[0][lane], nullptr, 0, nullptr, s_fitin, fit_raw);
-        STAMP(gridDim.x * 4 + 3);
+        STAMP(nb_ * 4 + 3);
         return;
     }
     // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
@@ -398,7 +418,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
     }
     __syncthreads();
     if (wave != 0) return;
-    STAMP(gridDim.x * 4 + 1);
+    STAMP(nb_ * 4 + 1);
     uint64_t chain[kDepth];
 #pragma unroll
     for (int d = 0; d < kDepth; ++d) chain[d] = chainbuf[d][lane];
@@ -473,7 +493,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
             bc_lane = slow_lane;
         }
     }
-    STAMP(gridDim.x * 4 + 2);
+    STAMP(nb_ * 4 + 2);
     // 4. write back committed rows and the results
     if (na + np > 0) {
         const Row r = apply_commits(base, c, na, np);
@@ -489,9 +509,27 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc,
         __hip_atomic_store(&out->g[lane],
                            make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    STAMP(gridDim.x * 4 + 3);
+    STAMP(nb_ * 4 + 3);
     }  // placement 0
     }  // PL != 3
+}
+
+template <int R, typename KT, int PL>
+__global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
+                                                           uint64_t* cand64, uint32_t* arrive, PopOut* out,
+                                                           ShardMsg* smsg) {
+    pop_batch_body<R, KT, PL>(cf, nc, t, a, cand64, arrive, out, smsg, blockIdx.x, gridDim.x);
+}
+
+// What-if sessions batched per launch: one launch
+// serves the batched pops of up to kPopMulti concurrent sessions, session
+// blockIdx.y with its own node columns, tables, candidates, counters and
+// result slot (descriptors in the kernel arguments).
+template <int R, typename KT, int PL>
+__global__ __launch_bounds__(kPopThreads) void k_pop_batch_multi(PopDescs d) {
+    const PopDesc& q = d.d[blockIdx.y];
+    if ((int)blockIdx.x >= q.nb) return;
+    pop_batch_body<R, KT, PL>(q.cf, q.nc, q.t, q.a, q.cand, q.arrive, (PopOut*)q.out, nullptr, blockIdx.x, q.nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -909,6 +947,67 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
     }
 #undef KBHIP_PB
 #undef KBHIP_PB1
+}
+
+// Multi-session launches: requests grouped by (nodes per lane, key type,
+// placement), up to kPopMulti per launch.
+template <int R, typename KT, int PL>
+static void launch_multi_t(const PopDescs& d, int n, int max_nb, hipStream_t st) {
+    hipLaunchKernelGGL((k_pop_batch_multi<R, KT, PL>), dim3(max_nb, n), dim3(kPopThreads), 0, st, d);
+}
+template <typename KT, int PL>
+static void launch_multi_r(int R, const PopDescs& d, int n, int max_nb, hipStream_t st) {
+    switch (R) {
+        case 1: launch_multi_t<1, KT, PL>(d, n, max_nb, st); break;
+        case 2: launch_multi_t<2, KT, PL>(d, n, max_nb, st); break;
+        case 4: launch_multi_t<4, KT, PL>(d, n, max_nb, st); break;
+        case 8: launch_multi_t<8, KT, PL>(d, n, max_nb, st); break;
+        default: launch_multi_t<16, KT, PL>(d, n, max_nb, st); break;
+    }
+}
+hipError_t launch_pop_batch_multi(const PopReq* reqs, int n, hipStream_t st, int* launches) {
+    std::vector<char> used(n, 0);
+    int nl = 0;
+    for (int i = 0; i < n; ++i) {
+        if (used[i]) continue;
+        int Ri;
+        (void)pop_blocks(reqs[i].nc.n, &Ri);
+        const bool k32 = reqs[i].kf.use32;
+        const int pl = reqs[i].placement;
+        if (pl != 6 && pl != 7) return hipErrorInvalidValue;  // the sequential placements only
+        PopDescs d{};
+        int m = 0, max_nb = 1;
+        for (int j = i; j < n && m < kPopMulti; ++j) {
+            int Rj;
+            const int nbj = pop_blocks(reqs[j].nc.n, &Rj);
+            if (used[j] || Rj != Ri || reqs[j].kf.use32 != k32 || reqs[j].placement != pl) continue;
+            used[j] = 1;
+            const PopReq& q = reqs[j];
+            PopDesc& e = d.d[m++];
+            e.cf = q.cf;
+            e.nc = q.nc;
+            e.t = q.t;
+            e.a = PopArgs{q.cls, q.n_tasks, q.gang_mode, q.min_avail, q.ready_count, q.epoch, pl, q.kf.base, q.kf.shift,
+                          q.kf.idxmax, q.kf.use32 && q.kf.ent32 ? 1 : 0, q.fit_set};
+            e.cand = q.cand;
+            e.arrive = q.arrive;
+            e.out = q.out;
+            e.nb = nbj;
+            max_nb = nbj > max_nb ? nbj : max_nb;
+        }
+        if (k32) {
+            if (pl == 6) launch_multi_r<uint32_t, 6>(Ri, d, m, max_nb, st);
+            else launch_multi_r<uint32_t, 7>(Ri, d, m, max_nb, st);
+        } else {
+            if (pl == 6) launch_multi_r<uint64_t, 6>(Ri, d, m, max_nb, st);
+            else launch_multi_r<uint64_t, 7>(Ri, d, m, max_nb, st);
+        }
+        ++nl;
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (launches) *launches = nl;
+    return hipSuccess;
 }
 
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,

@@ -371,6 +371,8 @@ struct Session {
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
     bool aff_batch = true;     // option "aff_batch": batched pops (placement 7) of anti-affinity classes
     bool rank_group = false;   // option "rank_group": node rankings batched with concurrent sessions (RankBatcher)
+    bool pop_group = false;    // option "pop_group": batched pops of Backfilled sessions share launches (PopBatcher)
+    hipEvent_t ev_pop = nullptr;  // this session's stream before a PopBatcher request
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
     vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
@@ -508,7 +510,7 @@ struct Session {
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm) (void)ncclCommDestroy(comm);
         comm = nullptr;
-        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov})
+        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : ev_ring)
             for (auto& e : pr)
@@ -1697,6 +1699,87 @@ struct RankBatcher {
     }
 };
 
+// The allocate pops of what-if sessions with Backfilled nodes (option
+// "pop_group"; placement 6: not overlapped, no speculation — one pop in
+// flight per session) share launches of the multi-session pop kernel
+// (k_pop_batch_multi, blockIdx.y = session).  Requests queue while a launch
+// is being issued and go out together in the next one (no waiting for
+// stragglers); every launch is on one process-wide stream per device, and
+// events order it after each requester's earlier device work and each
+// requester's later work after it.  Results are the sessions' own granules.
+struct PopBatcher {
+    static PopBatcher& get() {
+        static PopBatcher b;
+        return b;
+    }
+    struct Req {
+        PopReq q;
+        int device = 0;
+        hipEvent_t before = nullptr;  // recorded on the requester's stream: its earlier work
+        hipEvent_t after = nullptr;   // recorded on the batcher's stream after the launch that served it
+        bool done = false;
+        hipError_t err = hipSuccess;
+        int batch = 0;
+    };
+    std::mutex mu;
+    std::condition_variable cv;
+    vector<Req*> pending;
+    bool busy = false;
+    std::map<int, std::pair<hipStream_t, vector<hipEvent_t>>> dev;  // device -> (stream, event ring)
+    size_t ring_next = 0;
+    hipError_t issue(vector<Req*>& batch) {
+        std::map<int, vector<Req*>> by_dev;
+        for (Req* q : batch) by_dev[q->device].push_back(q);
+        for (auto& kv : by_dev) {
+            hipError_t e = hipSetDevice(kv.first);
+            if (e != hipSuccess) return e;
+            auto& d = dev[kv.first];
+            if (!d.first) {
+                if ((e = hipStreamCreateWithFlags(&d.first, hipStreamNonBlocking)) != hipSuccess) return e;
+                d.second.assign(8, nullptr);
+                for (auto& ev : d.second)
+                    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+            }
+            vector<PopReq> qs;
+            for (Req* q : kv.second) {
+                if ((e = hipStreamWaitEvent(d.first, q->before, 0)) != hipSuccess) return e;
+                qs.push_back(q->q);
+            }
+            int nl = 0;
+            if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), d.first, &nl)) != hipSuccess) return e;
+            hipEvent_t ev = d.second[ring_next++ % d.second.size()];
+            if ((e = hipEventRecord(ev, d.first)) != hipSuccess) return e;
+            for (Req* q : kv.second) q->after = ev;
+        }
+        return hipSuccess;
+    }
+    void submit(Req& r) {
+        std::unique_lock<std::mutex> lk(mu);
+        pending.push_back(&r);
+        while (!r.done) {
+            if (!busy) {  // launch everything queued; requests arriving meanwhile go in the next launch
+                busy = true;
+                while (!pending.empty()) {
+                    vector<Req*> batch;
+                    batch.swap(pending);
+                    lk.unlock();
+                    const hipError_t e = issue(batch);
+                    lk.lock();
+                    for (Req* q : batch) {
+                        q->err = e;
+                        q->batch = (int)batch.size();
+                        q->done = true;
+                    }
+                }
+                busy = false;
+                cv.notify_all();
+                continue;
+            }
+            cv.wait(lk);
+        }
+    }
+};
+
 // A grouped session inside a reclaim / preempt action (RankBatcher members).
 struct RankGroupScope {
     bool on;
@@ -1905,6 +1988,21 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
+    } else if (L.bf && S.pop_group) {  // what-if sessions: pops batched across sessions (PopBatcher)
+        PopBatcher::Req r;
+        r.q = PopReq{S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf, S.d_cand2,
+                     S.d_arrive, out, 6, S.fit_set[kMaxDep + 1]};
+        S.fit_set[kMaxDep + 1] ^= 1;
+        r.device = S.device;
+        if (!S.ev_pop) HIPCHK(hipEventCreateWithFlags(&S.ev_pop, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(S.ev_pop, S.stream));
+        r.before = S.ev_pop;
+        PopBatcher::get().submit(r);
+        HIPCHK(hipSetDevice(S.device));
+        HIPCHK(r.err);
+        HIPCHK(hipStreamWaitEvent(S.stream, r.after, 0));  // this session's later work follows the launch
+        S.stats.pop_requests++;
+        S.stats.pop_batch_sum += r.batch;
     } else {
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
                                 S.d_arrive, out, S.stream, L.bf ? 6 : L.aff ? 7 : S.placement, kf,
@@ -3807,6 +3905,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
+        else if (std::strcmp(key, "pop_group") == 0) s->s.pop_group = value != 0 && s->s.world == 1;
         else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count

@@ -48,7 +48,8 @@ class Stats(ctypes.Structure):
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
                 ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64),
                 ("pp_retries", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
-                ("rank_batch_sum", ctypes.c_int64)]
+                ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
+                ("pop_batch_sum", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -1,7 +1,8 @@
 """What-if sessions batched per launch:
 sessions with option rank_group run from concurrent host threads and their
 reclaim / preempt node rankings share launches of the multi-session counting
-sort (blockIdx.y = session).  Each session's records equal the faithful
+sort and their allocate pops share launches of the multi-session pop kernel
+(blockIdx.y = session).  Each session's records equal the faithful
 restatement's and the same session run alone; the launches served more than
 one session."""
 import threading
@@ -19,6 +20,7 @@ def _run(engine, path, group, barrier=None):
     with engine.Session(path) as s:
         if group:
             s.set_option("rank_group", 1)
+            s.set_option("pop_group", 1)
         if barrier is not None:  # the sessions start their actions together
             barrier.wait()
         pod, node, kind = s.run_actions(ACTIONS)
@@ -45,3 +47,8 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
     assert req > 0 and bsum >= req
     if n_sessions > 2:  # two threads need not meet in a ranking; six do
         assert bsum > req  # some launch ranked more than one session's nodes
+    preq = sum(st["pop_requests"] for _, st in res)  # allocate pops batched across sessions
+    pbsum = sum(st["pop_batch_sum"] for _, st in res)
+    assert preq > 0 and pbsum >= preq
+    if n_sessions > 2:
+        assert pbsum > preq
