@@ -74,6 +74,14 @@ def parse():
     return ap.parse_args()
 
 
+# Rehearsal knobs (not used by the driver's runs): KBHIP_BENCH_BACKEND=gloo and
+# KBHIP_BENCH_ONE_DEVICE=1 run the N-rank path with every rank on GPU 0 (the
+# engine's RCCL communicator then cannot form and the exchange falls back to
+# the torch.distributed callbacks).
+BACKEND = os.environ.get("KBHIP_BENCH_BACKEND", "nccl")
+ONE_DEVICE = os.environ.get("KBHIP_BENCH_ONE_DEVICE", "0") == "1"
+
+
 def dist_setup(n):
     if n <= 1:
         return 0, 1, 0, None
@@ -81,17 +89,21 @@ def dist_setup(n):
     import torch.distributed as dist
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
-    local = int(os.environ.get("LOCAL_RANK", rank))
+    local = 0 if ONE_DEVICE else int(os.environ.get("LOCAL_RANK", rank))
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl")
+    dist.init_process_group(BACKEND)
     return rank, world, local, dist
+
+
+def _dev(local):
+    return f"cuda:{local}" if BACKEND == "nccl" else "cpu"
 
 
 def barrier(dist, local):
     if dist is None:
         return
     import torch
-    t = torch.zeros(1, device=f"cuda:{local}")
+    t = torch.zeros(1, device=_dev(local))
     dist.all_reduce(t)
     torch.cuda.synchronize(local)
 
@@ -100,8 +112,15 @@ def allmax(dist, local, x):
     if dist is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(local))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def allmin(dist, local, x):
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(local))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
     return float(t.item())
 
 
@@ -109,7 +128,7 @@ def allsum(dist, local, x):
     if dist is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    t = torch.tensor([x], dtype=torch.float64, device=_dev(local))
     dist.all_reduce(t)
     return float(t.item())
 
@@ -140,11 +159,32 @@ def pmc_traffic():
     return best
 
 
+EXCHANGE = ["rccl"]
+
+
 def open_sharded(buf, device, rank, world, dist):
+    """The shard of the session on this rank's GPU, connected over RCCL (the
+    engine's own communicator: ncclAllGather / ncclAllReduce on the session
+    stream).  If that communicator cannot be created, the exchange goes
+    through torch.distributed's RCCL process group as host callbacks instead
+    (same placements; reported in config.exchange)."""
     s = kbhip.ShardedSession(buf, device, rank, world)
-    box = [kbhip.ShardedSession.rccl_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
-    s.connect_rccl(box[0])
+    if ONE_DEVICE:  # RCCL forms no communicator with two ranks on one GPU
+        EXCHANGE[0] = f"torch.distributed {BACKEND} (host callbacks)"
+    if EXCHANGE[0] == "rccl":
+        box = [kbhip.ShardedSession.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        try:
+            s.connect_rccl(box[0])
+            ok = 1.0
+        except kbhip.KbhipError as e:
+            print(f"rank {rank}: engine RCCL communicator failed ({e}); torch.distributed callbacks", file=sys.stderr)
+            ok = 0.0
+        if allmin(dist, device, ok) < 1.0:
+            EXCHANGE[0] = f"torch.distributed {BACKEND} (host callbacks)"
+    if EXCHANGE[0] != "rccl":
+        dev = f"cuda:{device}" if BACKEND == "nccl" else None
+        s.connect_host(kbhip.torch_exchange(device=dev), kbhip.torch_gather(device=dev))
     return s
 
 
@@ -254,7 +294,8 @@ def main():
                    "session_phases_ms": {k: round(v, 2) for k, v in st_last["phases_ms"].items()},
                    "device_period_us": period_us,  # allocate's device span / batched launches (launches overlap)
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
-                   else "1 GPU"},
+                   else "1 GPU",
+                   "exchange": EXCHANGE[0] if shard else None},
         "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,

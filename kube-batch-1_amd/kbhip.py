@@ -331,25 +331,27 @@ def shard_range(n_nodes: int, rank: int, world: int) -> Tuple[int, int]:
     return n_nodes * rank // world, n_nodes * (rank + 1) // world
 
 
-def torch_gather(group=None):
+def torch_gather(group=None, device=None):
     """An all-gather callback for kbhip_shard_connect_host_gather over
-    torch.distributed (any backend; gloo runs on CPU): recv <- every rank's
-    `send` bytes in rank order."""
+    torch.distributed (gloo on CPU tensors; device = a cuda device for the
+    nccl (RCCL) backend): recv <- every rank's `send` bytes in rank order."""
     import torch
     import torch.distributed as dist
 
     def fn(send: np.ndarray, recv: np.ndarray) -> None:
         world = dist.get_world_size(group)
-        out = [torch.empty(send.size, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(out, torch.from_numpy(send.copy()), group=group)
-        recv[:] = torch.cat(out).numpy()
+        out = [torch.empty(send.size, dtype=torch.uint8, device=device) for _ in range(world)]
+        dist.all_gather(out, torch.from_numpy(send.copy()).to(device) if device is not None
+                        else torch.from_numpy(send.copy()), group=group)
+        recv[:] = torch.cat(out).cpu().numpy()
     return fn
 
 
-def torch_exchange(group=None):
+def torch_exchange(group=None, device=None):
     """An exchange callback for kbhip_shard_connect_host doing the all-reduce
-    with torch.distributed (any backend; gloo runs on CPU).  u64 keys are
-    mapped to i64 by flipping the top bit, which preserves their order."""
+    with torch.distributed (gloo on CPU tensors; device = a cuda device for the
+    nccl backend).  u64 keys are mapped to i64 by flipping the top bit, which
+    preserves their order."""
     import torch
     import torch.distributed as dist
 
@@ -358,8 +360,10 @@ def torch_exchange(group=None):
         if op == RED_MAX_U64:
             v ^= np.int64(-0x8000000000000000)
         t = torch.from_numpy(v)
+        if device is not None:
+            t = t.to(device)
         dist.all_reduce(t, op=dist.ReduceOp.MIN if op == RED_MIN_I64 else dist.ReduceOp.MAX, group=group)
-        out = t.numpy()
+        out = t.cpu().numpy()
         if op == RED_MAX_U64:
             out = out ^ np.int64(-0x8000000000000000)
         vals.view(np.int64)[:] = out
