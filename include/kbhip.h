@@ -159,7 +159,7 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys);
  * ssn.Pipeline; preempt: those of a committed Statement).  Discarded
  * statements leave no record (and, like the reference, leave the victims'
  * node copies Releasing).  Returns the record count.  KBHIP_EUNSUPPORTED on
- * node-sharded sessions and sessions with pod (anti-)affinity terms.
+ * node-sharded sessions.
  * Replaces the reference's reclaimAction.Execute / preemptAction.Execute.
  * If an action fails part-way (negative return) the session's host model may
  * hold a partial action: close it and open a new one. */
@@ -173,11 +173,25 @@ int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* o
  * Pipelined tasks Pending again, evicted pods Releasing — with node rows
  * recomputed on the host and only the changed row runs uploaded (no snapshot
  * parse, no re-encode).  The session can then run its actions again.
- * *out_uploaded_bytes (optional) = bytes sent to the device.
- * KBHIP_EUNSUPPORTED on shards and when a pending task class reads the pod
- * (anti-)affinity count tables; pod arrivals / deletions need
+ * *out_uploaded_bytes (optional) = bytes sent to the device.  Pod
+ * (anti-)affinity count tables are recounted from the carried pod states.
+ * KBHIP_EUNSUPPORTED on shards; pod arrivals and node changes need
  * kbhip_session_open. */
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
+
+/* kbhip_session_carry plus the scheduler cache's events on existing pods
+ * between the two sessions (pkg/scheduler/cache/event_handlers.go), applied
+ * in order after the carry: KBHIP_EV_DELETE — deletePod -> deleteTask, the
+ * pod leaves its job and its node (a shadow job left without pods leaves the
+ * cache); KBHIP_EV_SUCCEEDED / KBHIP_EV_FAILED — updatePod to a terminal phase
+ * (isTerminated: the task stays in its job, its node no longer counts it).
+ * pods[i] are pod indices of the opened snapshot (they stay the session's pod
+ * ids; a deleted pod never appears in a later record).  Every event is
+ * validated first (KBHIP_EINVAL: index out of range, unknown event, an event
+ * on a deleted pod) and nothing changes on error. */
+enum { KBHIP_EV_DELETE = 1, KBHIP_EV_SUCCEEDED = 2, KBHIP_EV_FAILED = 3 };
+int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t* events, int64_t n,
+                               int64_t* out_uploaded_bytes);
 
 /* Read the device node state: N x 12 int64 (idle, used, releasing,
  * backfilled; cpu/mem/gpu each) of the session's nodes (a shard session: its

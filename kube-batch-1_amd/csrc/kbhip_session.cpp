@@ -60,7 +60,8 @@ struct Error : std::runtime_error {
     } while (0)
 
 enum St { Pending = 1, AOB = 2, Allocated = 4, Pipelined = 8, Binding = 16, Bound = 32, Running = 64,
-          Releasing = 128, Succeeded = 256, Failed = 512, Unknown = 1024 };
+          Releasing = 128, Succeeded = 256, Failed = 512, Unknown = 1024,
+          Gone = 2048 };  // Gone: deleted from the cache between sessions (kbhip_session_carry_events)
 static inline bool allocated_status(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
 
 struct Dict {
@@ -127,6 +128,9 @@ struct HPod {
 struct HJob {  // session jobs are numbered in UID order
     int queue = -1;
     int32_t min_avail = 0, priority = 0;
+    int32_t pg_priority = 0;  // the PodGroup's priority before any task's (JobInfo.SetPodGroup)
+    bool shadow = false;      // shadow PodGroup of a group-less pod (cache/util.go:42-60)
+    bool gone = false;        // a shadow job whose pod was deleted between sessions: not in the cache
     int64_t ts = 0;
     vector<int> tasks;
     vector<int> pending;  // pending non-BestEffort tasks in TaskOrderFn order (built at first pop)
@@ -947,7 +951,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             j.queue = qslot;
             j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
             j.ts = src.row >= 0 ? jts[src.row] : 0;
-            j.priority = src.row >= 0 ? jpri[src.row] : 0;
+            j.priority = j.pg_priority = src.row >= 0 ? jpri[src.row] : 0;
+            j.shadow = src.row < 0;
             slot = (int)S.jobs.size();
             S.jobs.push_back(j);
             S.job_uid.push_back(src.b ? string(src.a) + "/" + src.b : string(src.a));
@@ -2512,11 +2517,13 @@ struct Allocator {
         S.plugins_opened = true;
         if (S.drf_on)
             for (auto& j : S.jobs) {  // drf.go:65-82
+                if (j.gone) continue;
                 for (int t : j.tasks) if (allocated_status(S.pods[t].status)) j.drf_alloc.add(S.pods[t].req);
                 drf_update(j);
             }
         if (S.prop_on) {  // proportion.go:65-142
             for (auto& j : S.jobs) {
+                if (j.gone) continue;
                 HQueue& q = S.queues[j.queue];
                 q.has_attr = true;
                 for (int t : j.tasks) {
@@ -2576,6 +2583,7 @@ struct Allocator {
         std::map<int, JobQueue<decltype(jl)>> jobs_map;
         for (size_t j = 0; j < S.jobs.size(); ++j) {
             const HJob& job = S.jobs[j];
+            if (job.gone) continue;
             int q = job.queue;
             queues.push(q);
             auto it = jobs_map.find(q);
@@ -3234,6 +3242,7 @@ struct Allocator {
         vector<char> seen(S.queues.size(), 0);
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
+            if (j.gone) continue;
             seen[j.queue] = 1;
             vector<int> pend = pending_sorted(j);
             if (pend.empty()) continue;
@@ -3304,6 +3313,7 @@ struct Allocator {
         std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
+            if (j.gone) continue;
             if (!qseen[j.queue]) { qseen[j.queue] = 1; queues.push(j.queue); }
             vector<int> pend = pending_sorted(j);
             if (pend.empty()) continue;
@@ -3505,7 +3515,7 @@ static string gang_close_text(const Session& S) {
     string out;
     for (size_t i = 0; i < S.jobs.size(); ++i) {
         const HJob& j = S.jobs[i];
-        if (j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
+        if (j.gone || j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
         int ready = 0;                              // readyTaskNum (gang.go:212-222)
         bool backfill = false;
         for (int t : j.tasks) {
@@ -3687,17 +3697,51 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // ports) are recomputed from those pods — dropping the session-only
 // GetAccessibleResource inflation of Idle — and only rows that changed are
 // uploaded (contiguous runs); jobs, queues and plugin state are re-derived as
-// at open.  New or deleted pods need a snapshot (kbhip_session_open).
-static void session_carry(Session& S) {
+// at open.  Cache events of existing pods between the sessions follow
+// (event_handlers.go): deletePod -> deleteTask (the pod leaves its job and
+// its node; a shadow job left without pods leaves the cache), updatePod to
+// Succeeded / Failed (isTerminated: the task stays in its job, off its node).
+// New pods and node changes need a snapshot (kbhip_session_open).
+static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0) {
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "carry on a node-sharded session");
+    const int N = S.nc.n, P = (int)S.pods.size();
+    {  // validate the events before anything changes
+        vector<char> gone(P, 0);
+        for (int64_t k = 0; k < n_ev; ++k) {
+            const int32_t i = ev_pod[k];
+            if (i < 0 || i >= P) throw Error(KBHIP_EINVAL, "event pod index out of range");
+            if (ev[k] != KBHIP_EV_DELETE && ev[k] != KBHIP_EV_SUCCEEDED && ev[k] != KBHIP_EV_FAILED)
+                throw Error(KBHIP_EINVAL, "unknown cache event");
+            if (gone[i] || S.pods[i].status == Gone) throw Error(KBHIP_EINVAL, "event on a deleted pod");
+            if (ev[k] == KBHIP_EV_DELETE) gone[i] = 1;
+        }
+    }
     ov_quiesce(S);
     HIPCHK(hipStreamSynchronize(S.stream));
-    const int N = S.nc.n, P = (int)S.pods.size();
     for (auto& p : S.pods) {
         if (p.status == Binding) p.status = Bound;
         else if (p.status == Allocated || p.status == AOB || p.status == Pipelined) { p.status = Pending; p.node = -1; }
         else if (p.status == Pending) p.node = -1;  // an unpipelined task keeps its NodeName in the session only
         p.node_rel = false;
+    }
+    if (n_ev > 0) {
+        vector<char> del(P, 0);
+        for (int64_t k = 0; k < n_ev; ++k) {
+            HPod& p = S.pods[ev_pod[k]];
+            if (ev[k] == KBHIP_EV_DELETE) {
+                p.status = Gone;
+                p.node = -1;
+                del[ev_pod[k]] = 1;
+            } else {
+                p.status = ev[k] == KBHIP_EV_SUCCEEDED ? Succeeded : Failed;  // keeps its NodeName
+            }
+        }
+        for (auto& j : S.jobs) {  // JobInfo.DeleteTaskInfo
+            size_t w = 0;
+            for (int t : j.tasks) if (!del[t]) j.tasks[w++] = t;
+            j.tasks.resize(w);
+            if (j.shadow && j.tasks.empty()) j.gone = true;
+        }
     }
     vector<int64_t> col[9];
     for (auto& c : col) c.assign(N, 0);
@@ -3761,6 +3805,7 @@ static void session_carry(Session& S) {
         j.fit_exact = true;
         j.drf_alloc = F3{};
         j.drf_share = 0;
+        j.priority = j.pg_priority;
         for (int t : j.tasks) {
             j.priority = S.pods[t].priority;
             if (allocated_status(S.pods[t].status)) j.cnt_alloc++;
@@ -3829,6 +3874,18 @@ int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
         session_carry(s->s);
+        if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
+        return 0;
+    })
+}
+int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t* events, int64_t n,
+                               int64_t* out_uploaded_bytes) {
+    ABI_GUARD({
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (n < 0 || (n > 0 && (!pods || !events))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        session_carry(s->s, pods, events, n);
         if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
         return 0;
     })

@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("KBHIP_LIB") or os.path.join(HERE, "_build", "libkbhip.so")  # KBHIP_LIB: tuning builds
 
 ALLOCATED, PIPELINED, EVICTED = 1, 2, 3
+EV_DELETE, EV_SUCCEEDED, EV_FAILED = 1, 2, 3  # kbhip_session_carry_events
 STOP_ALL, STOP_UNASSIGNED, STOP_READY = 0, 1, 2
 
 # int kbhip_* entry points declared by include/kbhip.h
@@ -27,7 +28,8 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_backfill", "kbhip_session_open_shard", "kbhip_shard_info", "kbhip_rccl_unique_id",
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
-           "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather")
+           "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
+           "kbhip_session_carry_events")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -82,6 +84,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_sweep_scores.argtypes = [vp, i32, vp]
         L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_carry.argtypes = [vp, vp]
+        L.kbhip_session_carry_events.argtypes = [vp, vp, vp, i64, vp]
         L.kbhip_preempt.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_open_shard.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
         L.kbhip_shard_info.argtypes = [vp, vp]
@@ -191,6 +194,17 @@ class Session:
         """kbhip_session_carry: become the next session (binds / evictions applied); bytes uploaded."""
         out = np.zeros(1, np.int64)
         _check(lib().kbhip_session_carry(self._h, _p(out)))
+        return int(out[0])
+
+    def carry_events(self, pods, events) -> int:
+        """kbhip_session_carry_events: carry, then the cache's events on existing pods
+        (EV_DELETE / EV_SUCCEEDED / EV_FAILED per pod index); bytes uploaded."""
+        p = np.ascontiguousarray(pods, np.int32)
+        e = np.ascontiguousarray(events, np.uint8)
+        if p.shape != e.shape:
+            raise ValueError("pods and events differ in length")
+        out = np.zeros(1, np.int64)
+        _check(lib().kbhip_session_carry_events(self._h, _p(p), _p(e), int(p.size), _p(out)))
         return int(out[0])
 
     def reclaim(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

@@ -98,3 +98,90 @@ def test_carry_c4_scaled_uploads_a_delta(engine, kbgen_mod, tmp_path):
     assert len(pod) > 0 and (st2[pod] == 1).all()            # only pending tasks are placed again
     full = 20_000 * (12 * 8 + 4)                              # the dynamic node columns
     assert 0 < sent < full
+
+
+EV_DELETE, EV_SUCCEEDED, EV_FAILED = 1, 2, 3
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_carry_events_equal_fresh_session(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """kbhip_session_carry_events: the session's own binds / evictions, then
+    cache events on existing pods (event_handlers.go deletePod / updatePod to
+    Succeeded or Failed) — evicted pods finishing, running pods completing,
+    pending pods withdrawn, shadow (group-less) pods deleted.  The carried
+    session must schedule like a fresh one opened from the cache's snapshot
+    (deleted pods absent); the oracle's pod indices are mapped back through
+    the UIDs."""
+    rng = np.random.default_rng(7000 + seed)
+    if seed % 2:
+        c = kbgen_mod.gen_preempt(5300 + seed, n_nodes=4 + seed % 8, n_queues=1 + seed % 3, n_run_jobs=4 + seed % 7,
+                                  n_pend_jobs=3 + seed % 5, max_tasks=2 + seed % 5,
+                                  features=("selector", "taints", "ports", "init", "bestEffort")
+                                  + (("podaffinity",) if seed % 4 == 1 else ()))
+    else:
+        c = kbgen_mod.gen_random(5400 + seed, n_nodes=4 + seed % 10, n_jobs=5 + seed % 8, max_tasks=2 + seed % 6,
+                                 features=NO_POD_AFFINITY if seed % 4 else
+                                 tuple(NO_POD_AFFINITY) + ("podaffinity",))
+    queues = sorted(q.name for q in c.queues)
+    if "default" not in queues:
+        c.add_queue("default")
+    node_names = sorted(n.name for n in c.nodes)
+    for k in range(2 + seed % 3):  # shadow PodGroups: group-less pods, one job each
+        running = k % 2 == 0
+        c.add_pod("default", f"solo-{k}", uid=f"zsolo{seed:02d}{k}", group=None,
+                  node=node_names[k % len(node_names)] if running else None,
+                  phase="Running" if running else "Pending", containers=[{"cpu": 100, "mem": 1 << 20}])
+    acts = ACTS[seed % len(ACTS)]
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    n_nodes = len(c.nodes)
+    pods_sorted = sorted(c.pods, key=lambda q: q.uid)
+    with engine.Session(p1) as s:
+        s.run_actions(acts)
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+        # events: every shadow pod deleted, evicted pods gone, some running pods done, some pending withdrawn
+        ev = {}
+        for i, q in enumerate(pods_sorted):
+            st = int(status[i])
+            if q.group is None:
+                ev[i] = EV_DELETE
+            elif st == RELEASING and rng.random() < 0.7:
+                ev[i] = EV_DELETE
+            elif st in (RUNNING, BINDING, 32) and rng.random() < 0.15:
+                ev[i] = EV_SUCCEEDED if rng.random() < 0.7 else EV_FAILED
+            elif st == 1 and rng.random() < 0.1:
+                ev[i] = EV_DELETE
+        order = list(rng.permutation(sorted(ev)))
+        s.carry_events(np.array(order, np.int32), np.array([ev[i] for i in order], np.uint8))
+        st2 = s.table("pod_status").copy()
+        pod, nd, kind = s.run_actions(acts)
+        ns = s.read_nodes(n_nodes)
+    c2 = _next_snapshot(c, status, node)
+    for i, e in ev.items():
+        if e != EV_DELETE:
+            pods_sorted[i].phase = "Succeeded" if e == EV_SUCCEEDED else "Failed"
+    gone = {pods_sorted[i].uid for i, e in ev.items() if e == EV_DELETE}
+    c2.pods = [q for q in c2.pods if q.uid not in gone]
+    p2 = c2.write(str(tmp_path / "s2.kbs"))
+    exp, ons = oracle_mod.ref_allocate(p2, actions=acts, with_nodes=True)
+    idx = {q.uid: i for i, q in enumerate(pods_sorted)}
+    fresh = sorted(c2.pods, key=lambda q: q.uid)
+    exp_engine = [(idx[fresh[a].uid], b, k) for a, b, k in exp.as_list()]
+    assert all(int(st2[i]) == 2048 for i, e in ev.items() if e == EV_DELETE)
+    assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)] == exp_engine
+    assert np.array_equal(ns.astype(np.float64), ons[:n_nodes])
+
+
+def test_carry_events_rejects_bad_input(engine, kbgen_mod, tmp_path):
+    c = kbgen_mod.gen_random(77, n_nodes=4, n_jobs=4, max_tasks=3, features=NO_POD_AFFINITY)
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    n = len(c.pods)
+    with engine.Session(p1) as s:
+        s.allocate()
+        before = s.table("pod_status").copy()
+        for pods, evs in (([n], [EV_DELETE]), ([0], [9]), ([0, 0], [EV_DELETE, EV_SUCCEEDED])):
+            with pytest.raises(engine.KbhipError):
+                s.carry_events(np.array(pods, np.int32), np.array(evs, np.uint8))
+            assert np.array_equal(s.table("pod_status"), before)  # nothing changed
+        s.carry_events(np.array([0], np.int32), np.array([EV_DELETE], np.uint8))
+        with pytest.raises(engine.KbhipError):  # already deleted
+            s.carry_events(np.array([0], np.int32), np.array([EV_SUCCEEDED], np.uint8))
