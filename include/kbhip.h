@@ -96,6 +96,7 @@ typedef struct kbhip_stats {
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
+    int64_t msg_pops;        /* overlapped pops that took the previous pop's rows from its rows message ("ov_msg") */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -211,6 +212,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * overrides "overlap"), 0 (default) = the overlapped pop kernel;
  * "bf_batch" = 1 (default) batches pops in sessions with Backfilled nodes
  * (placement 6), 0 = per-task sweeps there;
+ * "ov_msg" = 1: an overlapped pop takes the previous pop's written rows from
+ * its rows message and commit granules instead of waiting for its write-back;
+ * 0 (default, faster at C4) = waits for the write-back and re-reads the rows;
  * "rank_radix" = 1 orders reclaim / preempt walks with the library radix sort
  * instead of the counting sort (tests);
  * "rank_group" = 1 makes this session one of a group of what-if sessions run

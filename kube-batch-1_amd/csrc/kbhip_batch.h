@@ -180,6 +180,12 @@ struct PopArgs {
     int32_t kbase, kshift, kidxmax;
     int32_t ent32;  // placement entries in 32 bits: (rm - kbase + 1) fits in 32 - kshift - 5 bits
     int32_t fit_set;  // FitDelta counter set of this launch (alternates per stream; the other one is zeroed)
+    // overlapped pops (k_pop_batch_ov, one previous pop in flight): 1 = rebuild
+    // the previous pop's written rows from its PopLink rows + commit granules
+    // instead of waiting for its write-back (the host sets it only when that
+    // pop was the last device work on the node rows); prev_cls = its class
+    int32_t msg, prev_cls;  // zero-initialised by the launchers' aggregate initialisers
+    int32_t pub;            // publish the rows message / ready / commit granules (the next pop may use them)
 };
 
 // Selection key of the batched sweep in type T (see PopArgs).
@@ -549,7 +555,11 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
                                uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
-                               PPHistOut* ho = nullptr) {
+                               PPHistOut* ho = nullptr, PopLink* lk = nullptr, bool wait_prev = false) {
+    // lk (overlapped pops): publish ready[seq] after round 0 (the candidate
+    // rows stored before this call are drained by then) and the commit
+    // granules before the write-back; wait_prev: pop seq-1's write-back may
+    // still be in flight (PopArgs::msg) -- wait for it before writing rows.
     // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
     // (a node-array shard writes back only its own; one GPU: all of them).
     // t0 (persistent placer): the candidates are exact down to the selection
@@ -644,6 +654,10 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         }
         const ET e = ok ? depth_entry<ET>(rm, n, d, a) : (ET)0;
         if (r == 0) { STAMP(gridDim.x * 4 + 6); PSTAMP(4); }
+        if (r == 0 && lk && wave == 0) {  // the rows message went out before the placement began
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane == 0) st_sc1(&lk->ready[seq % kLinkSlots][0], (uint64_t)seq);
+        }
         if (wave == kW - 1) { s_last[lane] = e; s_rm[(r + 1) & 1][lane] = rm; }
         if constexpr (INS) {
             wl[wave][lane] = e;
@@ -684,6 +698,8 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         alive = s_last[lane] != 0;  // rewritten by wave kW-1 only after the next round's first barrier
     }
     if (wave != 0) return;
+    // pop seq-1's done, in flight during the stop rule below (wait_prev)
+    uint32_t prev_done = wait_prev ? ld_sc1(done_flag) : 0u;
     STAMP(gridDim.x * 4 + 2); PSTAMP(6);
     // commit kind of each position: its node's candidate lane, the entry's depth
     const bool inm = lane < m && L != 0;
@@ -748,6 +764,19 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                                __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (lk) {  // commit granules: pop seq+1 rebuilds the rows written below from them
+        const int ap = s_apos[lane];
+        const int na = (n >= 0 && cc > 0) ? (cc < ap ? cc : ap) : 0;
+        const int np = (n >= 0 && cc > 0) ? cc - na : 0;
+        st_sc1(&lk->commits[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint64_t)(na << 8) | (uint64_t)np);
+    }
+    if (wait_prev) {  // rows of pop seq-1's candidates: its stores must land before ours
+        long spin = 0;
+        while ((int32_t)(prev_done - (seq - 1)) < 0 && ++spin < (1L << 21)) {
+            __builtin_amdgcn_s_sleep(2);
+            prev_done = ld_sc1(done_flag);
         }
     }
     const int ln = n - wb_base;  // local row of the written-back node

@@ -196,12 +196,15 @@ KBHIP_HD uint32_t fit_bits(const TaskClass& c, const Row& r, bool passed) {
 KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
                                               const NodeCols& nc, int n, int32_t* score_out, bool* passed,
                                               uint32_t* fit = nullptr) {
-    const bool st = static_pred(cf, c, t, nc, n);
-    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+    // the row and port words first: their loads do not depend on the
+    // predicates' early exits, so they share one memory round trip with the
+    // flag / taint loads instead of following them
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+    const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
     if (fit) *fit = fit_bits(c, r, *passed);
     return k;
@@ -214,12 +217,12 @@ KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables&
 // walk position (score, index; kind bit 0).
 KBHIP_HD uint64_t eval_node_walk(const Conf& cf, const TaskClass& c, const DevTables& t,
                                  const NodeCols& nc, int n, uint32_t* fit) {
-    const bool st = static_pred(cf, c, t, nc, n);
-    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
-    const Row r = load_row(nc, n);
+    const Row r = load_row(nc, n);  // before the predicates' early exits (eval_node)
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+    const bool st = static_pred(cf, c, t, nc, n);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     int32_t s = 0;
     bool passed = false;
     uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);

@@ -120,11 +120,28 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
 constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
 constexpr int kMaxDep = 3;     // previous pops an overlapped pop may run beside (streams - 1)
 constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
+struct PopLinkRow {  // a candidate's row before the pop's commits (Row of kbhip_eval.h, 112 bytes)
+    int64_t v[13];
+    int32_t pods, maxtasks;
+};
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
     uint64_t touched[kLinkSlots][64];
+    // Row hand-off without the write-back on the chain (PopArgs::msg): pop seq
+    // publishes its candidates' rows as they were before its commits
+    // (rows[seq]), then ready[seq] = seq once they are drained (early in its
+    // placement), then per candidate a self-tagged commit granule
+    // {seq << 32 | allocs << 8 | pipelines} (commits[seq]) before its row
+    // write-back; pop seq+1 rebuilds the written rows from those.
+    PopLinkRow rows[kLinkSlots][64];
+    uint64_t ready[kLinkSlots][8];
+    uint64_t commits[kLinkSlots][64];
 };
+// pub: publish this pop's rows message for the next pop (option "ov_msg").
+// prev_cls >= 0: pop seq-1 (class prev_cls) was the last device work on the
+// node rows, and this class has no host ports: its written rows are rebuilt
+// from its PopLink rows message and commit granules (PopArgs::msg).
 // Overlapped batched pop number `seq` (>= 1) on stream st; pops seq-1 ..
 // seq-ndep may still run on other streams (1 <= ndep <= kMaxDep): it leaves
 // their candidates out of its sweep and re-evaluates them once pop seq-1's
@@ -134,7 +151,8 @@ struct PopLink {
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep, int fit_set, int placement = 2);
+                               uint32_t seq, int ndep, int fit_set, int placement = 2, int prev_cls = -1,
+                               bool pub = false);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

@@ -694,6 +694,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ RowCache rc;
     int32_t pna = 0;  // wave 0: pop seq-1's candidate `lane`: node-affinity weight, static predicates
     bool pst = false;
+    const bool msg = a.msg && ndep == 1;  // rebuild pop seq-1's rows (PopLink rows + commit granules)
+    Row mrow{};                           // wave 0, msg: pop seq-1's candidate `lane` before its commits
     if (wave == 0) {
         for (int h = lane; h < kHash; h += 64) rc.hkey[h] = -1;
         const KT lk = wlk[0][lane];
@@ -709,10 +711,42 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         __builtin_amdgcn_wave_barrier();
         if (ln >= 0) rc_insert(&rc, ln, lane);
+        if (msg && __ballot(tn[0] >= 0) != 0) {  // pop seq-1's rows message (drained before its ready)
+            const uint32_t want = seq - 1;
+            long spin = 0;
+            bool okr = s_ok;
+            while (okr && (uint32_t)ld_sc1(&link->ready[want % kLinkSlots][0]) != want) {
+                if (++spin >= kLinkSpin) okr = false;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (tn[0] >= 0 && okr) {
+                const PopLinkRow* pr = &link->rows[want % kLinkSlots][lane];
+                int64_t v[13];
+#pragma unroll
+                for (int k = 0; k < 13; ++k) v[k] = ld_sc1(&pr->v[k]);
+                mrow = Row{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12],
+                           ld_sc1(&pr->pods), ld_sc1(&pr->maxtasks)};
+            }
+            if (lane == 0 && !okr) s_ok = 0;
+        }
     }
     // pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
     // every load of their rows below is sc1); their candidates on final rows
-    if (threadIdx.x == 0) {
+    uint64_t pcg = 0;  // wave 0, msg: pop seq-1's commit granule of candidate `lane`
+    if (msg) {
+        if (wave == 0) {  // its commits (self-tagged granules), not its write-back
+            const uint32_t want = seq - 1;
+            bool ok = s_ok;
+            long spin = 0;
+            if (tn[0] >= 0) pcg = ld_sc1(&link->commits[want % kLinkSlots][lane]);
+            while (ok && __ballot(tn[0] >= 0 && (uint32_t)(pcg >> 32) != want) != 0) {
+                if (++spin >= kLinkSpin) ok = false;
+                __builtin_amdgcn_s_sleep(2);
+                if (tn[0] >= 0) pcg = ld_sc1(&link->commits[want % kLinkSlots][lane]);
+            }
+            if (lane == 0) s_ok = ok;
+        }
+    } else if (threadIdx.x == 0) {
         bool ok = s_ok;
         long spin = 0;
         while (ok && (int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0) {
@@ -728,10 +762,16 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         KT e0 = 0;
         uint32_t fb_prev = 0;  // FitDelta bits of the previous pops' candidates (left out of the sweep)
         if (ok && tn[0] >= 0) {  // pop seq-1's candidates: rows into the cache, keys
-            const Row r = load_row_sc1(nc, tn[0]);
+            Row r;
             uint64_t pw[4] = {0, 0, 0, 0};
-            if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn[0]);
+            if (msg) {  // as pop seq-1 writes them back (no host ports in this class: the host checks)
+                const TaskClass& pc = t.classes[a.prev_cls];
+                r = apply_commits(mrow, pc, (int)((pcg >> 8) & 0xff), (int)(pcg & 0xff));
+            } else {
+                r = load_row_sc1(nc, tn[0]);
+                if (c.has_ports)
+                    for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn[0]);
+            }
             rc.row[64 + lane] = r;
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;
@@ -765,9 +805,22 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             const int cnt = __popcll(__ballot((fb_prev >> b) & 1u));
             if (lane == b) s_fitin[b] += cnt;
         }
+        // this pop's candidates' rows before its commits (the next pop's rows message;
+        // drained before ready[seq], which the placement publishes after its round 0)
+        const int tnode = (ok && top) ? key_node(top, a) : -1;
+        if (tnode >= 0 && PLV != 4 && a.pub) {
+            const int sl = rc_find(&rc, tnode);  // -1: an older pop's node (overlap > 1, no rows message)
+            const Row& rr = rc.row[sl < 0 ? 0 : sl];
+            PopLinkRow* pr = &link->rows[seq % kLinkSlots][lane];
+            const int64_t v[13] = {rr.idle_cpu, rr.idle_mem, rr.idle_gpu, rr.rel_cpu, rr.rel_mem, rr.rel_gpu,
+                                   rr.bf_cpu, rr.bf_mem, rr.bf_gpu, rr.acpu, rr.amem, rr.nzc, rr.nzm};
+#pragma unroll
+            for (int k = 0; k < 13; ++k) st_sc1(&pr->v[k], v[k]);
+            st_sc1(&pr->pods, rr.pods);
+            st_sc1(&pr->maxtasks, rr.maxtasks);
+        }
         // this pop's candidates, one self-tagged granule each
-        st_sc1(&link->touched[seq % kLinkSlots][lane],
-               ((uint64_t)seq << 32) | (uint32_t)((ok && top) ? key_node(top, a) : -1));
+        st_sc1(&link->touched[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint32_t)tnode);
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
     __syncthreads();
@@ -776,11 +829,17 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         if constexpr (PLV == 4) {  // one-wave insertion: no barriers, depths only where they can matter
             if (wave == 0) place_insert<true>(cf, nc, t, c, a, out, wl[0][lane], &link->done, seq, &rc, s_fitin, fit_raw);
         } else if (a.ent32) {
-            place_parallel<uint32_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+            place_parallel<uint32_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw,
+                                                      0, 0x7fffffff, 0, nullptr, a.pub ? link : nullptr, msg);
         } else {
-            place_parallel<uint64_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+            place_parallel<uint64_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw,
+                                                      0, 0x7fffffff, 0, nullptr, a.pub ? link : nullptr, msg);
         }
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
+        if (msg) {  // done stays monotonic: pop seq-1 publishes its own first
+            long spin = 0;
+            while ((int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0 && ++spin < kLinkSpin) __builtin_amdgcn_s_sleep(2);
+        }
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1120,13 +1179,20 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep, int fit_set, int placement) {
+                               uint32_t seq, int ndep, int fit_set, int placement, int prev_cls, bool pub) {
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     const int plv = placement == 5 || placement == 4 ? placement : 2;
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, plv, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
+    // rows hand-off (PopArgs::msg): one previous pop in flight, placed by place_parallel
+    // (it publishes the rows message), and no host-port words in this class
+    a.pub = pub && ndep == 1 && plv != 4;
+    if (prev_cls >= 0 && a.pub) {
+        a.msg = 1;
+        a.prev_cls = prev_cls;
+    }
     PopOut* o = (PopOut*)out_dev;
 #define KBHIP_OVP(KT)                                                                                       \
     switch (plv) {                                                                                          \

@@ -416,6 +416,17 @@ struct Session {
     uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
+    // option "ov_msg" (default 0): an overlapped pop rebuilds the previous pop's
+    // written rows from its rows message + commit granules (PopArgs::msg) when
+    // that pop was the last device work on the node rows (ov_msg_ok: cleared by
+    // ov_drain, which every other kind of device work goes through first).
+    // Exact (parity-tested) but measured slower at C4 (period 14.2 vs 12.8 us,
+    // profiles/r02_ab_ovmsg.json): the rows-message drain and the tail wait
+    // for the previous write-back lengthen each kernel, whose end the next
+    // sweep on its stream waits for.
+    bool ov_msg = false;
+    bool ov_msg_ok = false;
+    int ov_prev_cls = -1;
     // persistent placer (kbhip_pp.hip): option "pp"; used by kbhip_allocate's pop loop
     int pp = 0;                 // off by default: per pop it measured slower than the overlapped kernel
                                 // (C4-scaled 16.8 vs 12.5 us; profiles/r02_pp_profile.txt)
@@ -1798,6 +1809,7 @@ struct RankGroupScope {
 
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
+    S.ov_msg_ok = false;
     if (!S.ov_pending) return;
     for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
@@ -1987,9 +1999,14 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
                                   S.d_shard_recv, S.world, out, S.stream, S.placement));
     } else if (ov) {
+        const int prev = (S.ov_msg && S.ov_msg_ok && S.overlap == 1 && !S.classes[cls].has_ports && S.ov_prev_cls >= 0)
+                             ? S.ov_prev_cls : -1;
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
                                    S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap,
-                                   S.fit_set[si], S.placement));
+                                   S.fit_set[si], S.placement, prev, S.ov_msg && S.overlap == 1));
+        if (prev >= 0 && S.placement != 4) S.stats.msg_pops++;
+        S.ov_prev_cls = cls;
+        S.ov_msg_ok = true;
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
@@ -3961,6 +3978,10 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
+        else if (std::strcmp(key, "ov_msg") == 0) {
+            s->s.ov_msg = value != 0;
+            s->s.ov_msg_ok = false;  // the previous pop may not have published its rows message
+        }
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
         else if (std::strcmp(key, "pop_group") == 0) s->s.pop_group = value != 0 && s->s.world == 1;
         else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;

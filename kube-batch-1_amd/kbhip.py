@@ -51,7 +51,7 @@ class Stats(ctypes.Structure):
                 ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64),
                 ("pp_retries", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
                 ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
-                ("pop_batch_sum", ctypes.c_int64)]
+                ("pop_batch_sum", ctypes.c_int64), ("msg_pops", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

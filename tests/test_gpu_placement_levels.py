@@ -248,3 +248,41 @@ def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
         assert st["alloc_device_s"] > 0
     assert all(lg == logs[-1] for lg in logs)
     assert all((nd == nodes[-1]).all() for nd in nodes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(16))
+def test_ov_rows_message_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Overlapped pops that rebuild the previous pop's written rows from its
+    rows message + commit granules (option "ov_msg", default off) against
+    the write-back re-read (ov_msg 0) and the oracle: records and the device
+    node state after the session."""
+    c = kbgen_mod.gen_random(4700 + seed, n_nodes=3 + seed % 9, n_jobs=6 + seed % 10, max_tasks=4 + seed % 12,
+                             features=NO_POD_AFFINITY)
+    p = str(tmp_path / "m.kbs")
+    c.write(p)
+    exp = _oracle_log(oracle_mod, p)
+    states = []
+    for msg in (1, 0):
+        with engine.Session(p) as s:
+            s.set_option("ov_msg", msg)
+            pod, node, kind = s.allocate()
+            st = s.stats()
+            states.append(s.read_nodes(len(c.nodes)))
+        assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp, f"ov_msg {msg}"
+        if msg == 0:
+            assert st["msg_pops"] == 0
+    assert (states[0] == states[1]).all()
+
+
+@pytest.mark.gpu
+def test_ov_rows_message_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
+    p = str(tmp_path / "c2.kbs")
+    kbgen_mod.gen_c2(p)
+    exp = _oracle_log(oracle_mod, p, fast=True)
+    with engine.Session(p) as s:
+        s.set_option("ov_msg", 1)
+        pod, node, kind = s.allocate()
+        st = s.stats()
+    assert st["msg_pops"] > st["batched_pops"] // 2  # most pops follow an overlapped pop directly
+    assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
