@@ -186,6 +186,7 @@ struct PopArgs {
     // pop was the last device work on the node rows); prev_cls = its class
     int32_t msg, prev_cls;  // zero-initialised by the launchers' aggregate initialisers
     int32_t pub;            // publish the rows message / ready / commit granules (the next pop may use them)
+    int32_t npb;            // k_pop_batch_ov: nodes per block and node slot (<= kPopThreads; 0 = kPopThreads)
 };
 
 // Selection key of the batched sweep in type T (see PopArgs).

@@ -163,6 +163,7 @@ hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables&
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
+int pop_blocks_ov(int n_nodes, int* R_out);  // k_pop_batch_ov's grid (nodes per block: KBHIP_POP_NPB)
 // A batched pop of one session in a multi-session launch (what-if sessions,
 // placement 6 or 7): the arguments of launch_pop_batch.
 constexpr int kPopMulti = 8;  // sessions per launch (kernel argument space)

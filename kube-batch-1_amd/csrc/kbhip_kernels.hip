@@ -573,7 +573,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
-    const int base = blockIdx.x * R * kPopThreads;
+    // a.npb nodes per slot: fewer than the block's threads spreads a small node
+    // array over more blocks (CUs); the extra threads only merge and place
+    const int npb = a.npb ? a.npb : kPopThreads;
+    const int base = blockIdx.x * R * npb;
     // the ndep pops before this one may still be writing rows: seq-1 .. seq-ndep
     uint64_t tv[kMaxDep] = {};
 #pragma unroll
@@ -587,10 +590,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     uint32_t fbs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int n = (blockIdx.x * R + r) * kPopThreads + threadIdx.x;
+        const int n = (blockIdx.x * R + r) * npb + threadIdx.x;
         keys[r] = 0;
         fbs[r] = 0;
-        if (n < nc.n) {
+        if ((int)threadIdx.x < npb && n < nc.n) {
             int32_t s;
             bool passed;
             keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             }
             const int x = ok ? (int)(uint32_t)tv[k] : -1;
             tn[k] = x;
-            if (x >= base && x < base + R * kPopThreads) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
+            if (x >= base && x < base + R * npb) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
         }
         if (lane == 0) s_ok = ok;
     }
@@ -621,8 +624,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     KT best = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int o = r * kPopThreads + threadIdx.x;
-        const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: counted by the patch
+        const int o = r * npb + threadIdx.x;
+        const bool skip = (int)threadIdx.x < npb && ((s_skip[o >> 5] >> (o & 31)) & 1u);  // rows in flight: counted by the patch
         fit_block_add(s_fitb, skip ? 0u : fbs[r]);
         const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
         best = r == 0 ? k : wave_merge_desc(best, k);
@@ -969,6 +972,23 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
     return hipGetLastError();
 }
 
+// Nodes per block slot of the overlapped pop kernel (KBHIP_POP_NPB, a multiple
+// of 64 up to kPopThreads; tuning experiments), and its grid.
+int pop_npb() {
+    static const int v = [] {
+        const char* e = std::getenv("KBHIP_POP_NPB");
+        const int x = e ? std::atoi(e) : kPopThreads;
+        return (x >= 64 && x <= kPopThreads && x % 64 == 0) ? x : kPopThreads;
+    }();
+    return v;
+}
+int pop_blocks_ov(int n_nodes, int* R_out) {
+    const int nb = pop_blocks(n_nodes, R_out);
+    if (*R_out != 1) return nb;
+    const int npb = pop_npb();
+    return (n_nodes + npb - 1) / npb;
+}
+
 int pop_blocks(int n_nodes, int* R_out) {
     static const int forced = [] {  // KBHIP_POP_R: nodes per lane (tuning experiments only)
         const char* e = std::getenv("KBHIP_POP_R");
@@ -1182,13 +1202,14 @@ hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTabl
                                uint32_t seq, int ndep, int fit_set, int placement, int prev_cls, bool pub) {
     if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
     int R;
-    const int nb = pop_blocks(nc.n, &R);
+    const int nb = pop_blocks_ov(nc.n, &R);
     const int plv = placement == 5 || placement == 4 ? placement : 2;
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, plv, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     // rows hand-off (PopArgs::msg): one previous pop in flight, placed by place_parallel
     // (it publishes the rows message), and no host-port words in this class
     a.pub = pub && ndep == 1 && plv != 4;
+    a.npb = R == 1 ? pop_npb() : kPopThreads;
     if (prev_cls >= 0 && a.pub) {
         a.msg = 1;
         a.prev_cls = prev_cls;

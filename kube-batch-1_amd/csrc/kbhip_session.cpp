@@ -1514,8 +1514,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             S.d_shard_send = S.b_shard_send.alloc<ShardMsg>(1);
             S.d_shard_recv = S.b_shard_recv.alloc<ShardMsg>(S.world);
         }
+        int R3;
+        const int nb3 = std::max(nb2, pop_blocks_ov(nl, &R3));
         for (int k = 0; k <= kMaxDep; ++k) {
-            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
+            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb3, 1) + kMaxGroups) * 64);
             S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
             HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
