@@ -160,6 +160,7 @@ def pmc_traffic():
 
 
 EXCHANGE = ["rccl"]
+RCCL_ID = [None]  # one unique id per run: every session's connect reuses the engine's pooled communicator
 
 
 def open_sharded(buf, device, rank, world, dist):
@@ -172,10 +173,12 @@ def open_sharded(buf, device, rank, world, dist):
     if ONE_DEVICE:  # RCCL forms no communicator with two ranks on one GPU
         EXCHANGE[0] = f"torch.distributed {BACKEND} (host callbacks)"
     if EXCHANGE[0] == "rccl":
-        box = [kbhip.ShardedSession.rccl_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
+        if RCCL_ID[0] is None:  # ncclCommInitRank once per run, not per session (kbhip CommPool)
+            box = [kbhip.ShardedSession.rccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            RCCL_ID[0] = box[0]
         try:
-            s.connect_rccl(box[0])
+            s.connect_rccl(RCCL_ID[0])
             ok = 1.0
         except kbhip.KbhipError as e:
             print(f"rank {rank}: engine RCCL communicator failed ({e}); torch.distributed callbacks", file=sys.stderr)

@@ -34,10 +34,17 @@
  * negative KBHIP_E* code on failure; nothing throws or aborts across the ABI.
  * kbhip_last_error() describes the last failure on the calling thread.
  * Inputs are caller-owned and copied; outputs are caller-allocated; the
- * session handle is engine-owned.  One session per calling thread; the
- * library starts no host threads of its own.  Device memory, pinned buffers
- * and streams of a closed session go back to a process-wide pool and serve
- * later sessions.
+ * session handle is engine-owned.  One session per calling thread; no host
+ * thread of the library outlives a call (kbhip_session_open splits its pod
+ * pass over up to 8 worker threads it joins before returning).  Device
+ * memory, pinned buffers and streams of a closed session go back to a
+ * process-wide pool and serve later sessions.
+ *
+ * Deviations from SURVEY.md §8(b)'s sketch: kbhip_session_open takes one KBS1
+ * buffer that carries the plugin conf too (tiers, nodeorder arguments) instead
+ * of separate kb_snapshot / kb_conf structs; node-array sharding over GPUs is
+ * kbhip_session_open_shard (rank, world) instead of an n_gpus argument; the
+ * open splits its pod pass over worker threads (above).
  *
  * The library has exactly one execution path: HIP on a gfx950 device.  With
  * no usable device every call fails with KBHIP_ENODEV; there is no CPU
@@ -273,6 +280,11 @@ int kbhip_session_open_shard(const void* kbs_bytes, size_t len, int device, int3
                              kb_session** out);
 int kbhip_shard_info(kb_session* s, int32_t* out_rank_world_lo_hi);
 int kbhip_rccl_unique_id(void* out, int64_t cap);
+/* kbhip_shard_connect_rccl returns 0 after a new ncclCommInitRank and 1 when
+ * it takes the communicator a closed earlier session of this process left
+ * with the same unique id, rank, world and device (communicators are pooled
+ * for the process's lifetime: reuse one unique id across scheduling cycles
+ * and the bootstrap is paid once; every rank must then reuse together). */
 int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len);
 int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
 int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx);

@@ -152,6 +152,48 @@ struct HQueue {
     F3 deserved, allocated, request;
     double share = 0;
 };
+// Process-wide RCCL communicators kept across sessions: a scheduler (or the
+// bench) opens a node-sharded session per scheduling cycle, and
+// ncclCommInitRank (a bootstrap over sockets, a collective over every rank)
+// costs more than a whole session.  A later session connecting with the same
+// unique id, rank, world and device takes the communicator its predecessor
+// left (one session uses a communicator at a time); kept until process exit.
+struct CommPool {
+    struct Entry {
+        string id;
+        int rank, world, device;
+        ncclComm_t comm;
+        bool busy;
+    };
+    std::mutex mu;
+    vector<Entry> v;
+    static CommPool& get() {
+        static CommPool p;
+        return p;
+    }
+};
+static ncclComm_t comm_acquire(const string& id, int rank, int world, int device) {
+    CommPool& P = CommPool::get();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto& e : P.v)
+        if (!e.busy && e.id == id && e.rank == rank && e.world == world && e.device == device) {
+            e.busy = true;
+            return e.comm;
+        }
+    return nullptr;
+}
+static void comm_add(const string& id, int rank, int world, int device, ncclComm_t c) {
+    CommPool& P = CommPool::get();
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.v.push_back({id, rank, world, device, c, true});
+}
+static void comm_release(ncclComm_t c) {
+    CommPool& P = CommPool::get();
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (auto& e : P.v)
+        if (e.comm == c) e.busy = false;
+}
+
 struct Plugin {
     string name;
     int flags = 0;
@@ -497,6 +539,7 @@ struct Session {
     // node-array sharding: this session holds nodes [nc.base, nc.base + nc.n)
     int rank = 0, world = 1, n_total = 0;
     ncclComm_t comm = nullptr;                 // RCCL exchange (one GPU per rank)
+    bool comm_pooled = false;                  // comm belongs to the process-wide CommPool
     kbhip_allreduce_fn xfn = nullptr;          // or a host-side exchange callback
     void* xctx = nullptr;
     kbhip_allgather_fn xgfn = nullptr;         // host all-gather (batched pops of a shard session)
@@ -523,8 +566,12 @@ struct Session {
         for (int k = 1; k <= kMaxDep; ++k)
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
-        if (comm) (void)ncclCommDestroy(comm);
+        if (comm) {
+            if (comm_pooled) comm_release(comm);
+            else (void)ncclCommDestroy(comm);
+        }
         comm = nullptr;
+        comm_pooled = false;
         for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : ev_ring)
@@ -4058,9 +4105,20 @@ int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) 
         ncclUniqueId id;
         if (len != (int64_t)sizeof(id)) throw kbhip::Error(KBHIP_EINVAL, "bad unique id length");
         std::memcpy(&id, unique_id, sizeof(id));
+        if (s->s.comm) throw kbhip::Error(KBHIP_EINVAL, "session already connected");
         HIPCHK(hipSetDevice(s->s.device));
-        const ncclResult_t r = ncclCommInitRank(&s->s.comm, s->s.world, id, s->s.rank);
+        const string key((const char*)unique_id, sizeof(id));
+        if (ncclComm_t c = kbhip::comm_acquire(key, s->s.rank, s->s.world, s->s.device)) {
+            s->s.comm = c;  // a previous session's communicator (same id, rank, world, device)
+            s->s.comm_pooled = true;
+            return 1;
+        }
+        ncclComm_t c = nullptr;
+        const ncclResult_t r = ncclCommInitRank(&c, s->s.world, id, s->s.rank);
         if (r != ncclSuccess) throw kbhip::Error(KBHIP_EDEVICE, string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        kbhip::comm_add(key, s->s.rank, s->s.world, s->s.device, c);
+        s->s.comm = c;
+        s->s.comm_pooled = true;
         return KBHIP_OK;
     })
 }

@@ -411,9 +411,10 @@ class ShardedSession(Session):
         n = _check(lib().kbhip_rccl_unique_id(buf, 512))
         return buf.raw[:n]
 
-    def connect_rccl(self, unique_id: bytes) -> None:
+    def connect_rccl(self, unique_id: bytes) -> int:
+        """1 when a pooled communicator of an earlier session was reused, 0 after a new init."""
         b = ctypes.create_string_buffer(unique_id, len(unique_id))
-        _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
+        return _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
 
     def connect_host(self, fn, gather=None) -> None:
         """fn(vals: np.ndarray[uint64], op) reduces vals in place across ranks

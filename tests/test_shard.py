@@ -143,3 +143,25 @@ def test_sharded_rccl_two_devices(engine, oracle_mod, kbgen_mod, tmp_path):
     res = _run_ranks("rccl_worker.py", 2, tmp_path, lambda r, init, out: [p, str(r), "2", init, out], timeout=300)
     for r in range(2):
         assert [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]] == exp
+
+
+@pytest.mark.gpu
+def test_rccl_communicator_pooled_across_sessions(engine, oracle_mod, kbgen_mod, tmp_path):
+    """kbhip_shard_connect_rccl on one device (world 1, the only RCCL
+    communicator a one-GPU box can form): the first session pays
+    ncclCommInitRank, later sessions with the same unique id reuse the pooled
+    communicator (return 1), and every session schedules like the oracle."""
+    c = kbgen_mod.gen_random(2610, n_nodes=12, n_jobs=8, max_tasks=6)
+    p = str(tmp_path / "w1.kbs")
+    c.write(p)
+    exp = oracle_mod.ref_allocate(p).as_list()
+    uid = engine.ShardedSession.rccl_unique_id()
+    buf = open(p, "rb").read()
+    reused = []
+    for _ in range(3):
+        s = engine.ShardedSession(buf, 0, 0, 1)
+        reused.append(s.connect_rccl(uid))
+        pod, node, kind = s.allocate()
+        s.close()
+        assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
+    assert reused == [0, 1, 1]
