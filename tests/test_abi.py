@@ -69,3 +69,31 @@ def test_log_actions_validate_outputs(engine_lib):
     L = engine_lib
     for fn in (L.kbhip_allocate, L.kbhip_backfill, L.kbhip_reclaim, L.kbhip_preempt):
         assert fn(None, None, None, None, 4) == -1
+
+
+def test_header_constants_match_binding():
+    """Cache-event codes, placement kinds and stop reasons: the values the
+    Python binding passes are the header's."""
+    import kbhip
+    src = open(os.path.join(ROOT, "include", "kbhip.h")).read()
+    enum = dict(re.findall(r"\b(KBHIP_EV_[A-Z]+)\s*=\s*(\d+)", src))
+    assert {k: int(v) for k, v in enum.items()} == {"KBHIP_EV_DELETE": kbhip.EV_DELETE,
+                                                    "KBHIP_EV_SUCCEEDED": kbhip.EV_SUCCEEDED,
+                                                    "KBHIP_EV_FAILED": kbhip.EV_FAILED}
+    defs = {k: int(v) for k, v in re.findall(r"#define\s+(KBHIP_[A-Z_]+)\s+(-?\d+)", src)}
+    assert (defs["KBHIP_ALLOCATED"], defs["KBHIP_PIPELINED"], defs["KBHIP_EVICTED"]) == \
+        (kbhip.ALLOCATED, kbhip.PIPELINED, kbhip.EVICTED)
+    assert (defs["KBHIP_STOP_ALL"], defs["KBHIP_STOP_UNASSIGNED"], defs["KBHIP_STOP_READY"]) == \
+        (kbhip.STOP_ALL, kbhip.STOP_UNASSIGNED, kbhip.STOP_READY)
+
+
+def test_stats_struct_matches_header():
+    """kbhip_stats: the ctypes mirror has the header's fields in order."""
+    import kbhip
+    src = open(os.path.join(ROOT, "include", "kbhip.h")).read()
+    body = re.search(r"typedef struct kbhip_stats \{(.*?)\} kbhip_stats;", src, re.S).group(1)
+    fields = re.findall(r"\b(double|int64_t)\s+([a-z_0-9]+);", body)
+    mirror = list(kbhip.Stats._fields_)
+    assert [n for _, n in fields] == [n for n, _ in mirror]
+    ctype = {"double": ctypes.c_double, "int64_t": ctypes.c_int64}
+    assert all(ctype[t] is m for (t, _), (_, m) in zip(fields, mirror))
