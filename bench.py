@@ -59,14 +59,11 @@ def parse():
     ap.add_argument("--time-every", type=int, default=50,
                     help="HIP-event time every k-th batched pop launch on its own stream (the roofline's kernel "
                          "duration; 0 = off)")
-    ap.add_argument("--placement", type=int, default=2, choices=(0, 1, 2, 4, 5),
-                    help="batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels, "
-                         "4 insertion (one wave)")
     ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
                     help="predicted job pops queued ahead of the running one")
-    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2, 3),
-                    help="k > 0: batched pops rotate over k + 1 streams, up to k beside each other "
-                         "(device-side chaining); 0 = one pop kernel at a time")
+    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
+                    help="1: batched pops alternate over two streams, a pop's sweep beside the previous pop's "
+                         "placement (device-side chaining); 0 = one pop kernel at a time")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
                     help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
                          "each shard sweeps its node range to its top-64, one RCCL all-gather, identical placement "
@@ -191,11 +188,10 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None, placement=0, overlap=1, speculate=2):
+def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
-    s.set_option("placement", placement)
     s.set_option("overlap", overlap)
     s.set_option("speculate", speculate)
     t1 = time.perf_counter()
@@ -237,13 +233,13 @@ def main():
     device = local
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
-        run_session(buf, device, 0, shard, args.placement, args.overlap, args.speculate)
+        run_session(buf, device, 0, shard, args.overlap, args.speculate)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
     dev_s, dev_pops = 0.0, 0
     for _ in range(args.steps):
-        dt, n, st = run_session(buf, device, args.time_every, shard, args.placement, args.overlap,
+        dt, n, st = run_session(buf, device, args.time_every, shard, args.overlap,
                                 args.speculate)
         lat.append(dt)
         placed += n
@@ -289,7 +285,7 @@ def main():
                                "step, default kube-batch-conf tiers", "nodes": nodes, "pending": args.pending,
                    "placements_per_session": placed // args.steps, "pops_per_session": st_last["pops"],
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
-                   "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"], "placement": args.placement,
+                   "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],

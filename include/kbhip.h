@@ -96,14 +96,11 @@ typedef struct kbhip_stats {
     int64_t spec_missed;    /* predicted pops retracted (their node updates undone on device) */
     double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
     int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
-    int64_t fit_inexact;     /* jobs whose FitError histogram was not computed (shards, pod-affinity fallback) */
     int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
-    int64_t pp_retries;      /* pop chunks the persistent placer could not start (swept again without it) */
     int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if batcher ("rank_group") */
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
-    int64_t msg_pops;        /* overlapped pops that took the previous pop's rows from its rows message ("ov_msg") */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -210,24 +207,18 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
 
 /* Engine knobs: "batched" = 0 forces the per-task sweep path (tests);
  * "time_every" = k times every k-th sweep launch with HIP events;
- * "placement" = 2 (default) places a batched chunk by parallel levels, 8
- * depths per step; 5 the same merged by insertion; 4 by one-wave insertion;
- * 1 by running-min levels, one depth per step; 0 by the sequential loop over
- * precomputed chains;
- * "pp" = 1 runs kbhip_allocate's batched pops through the persistent placer
- * (one sweep launch per pop, one resident workgroup placing them in order;
- * overrides "overlap"), 0 (default) = the overlapped pop kernel;
  * "bf_batch" = 1 (default) batches pops in sessions with Backfilled nodes
  * (placement 6), 0 = per-task sweeps there;
- * "ov_msg" = 1: an overlapped pop takes the previous pop's written rows from
- * its rows message and commit granules instead of waiting for its write-back;
- * 0 (default, faster at C4) = waits for the write-back and re-reads the rows;
+ * "aff_batch" = 1 (default) batches pops of pod anti-affinity classes
+ * (placement 7), 0 = per-task sweeps for them;
  * "rank_radix" = 1 orders reclaim / preempt walks with the library radix sort
  * instead of the counting sort (tests);
  * "rank_group" = 1 makes this session one of a group of what-if sessions run
  * from concurrent host threads: their reclaim / preempt node rankings are
  * batched into shared launches (blockIdx.y = session; kbhip_stats
  * rank_batch_sum / rank_requests = sessions per launch);
+ * "pop_group" = 1: the batched allocate pops of such sessions share launches too;
+ * "rank_first" = k: reclaim / preempt read the first k sorted keys with the count;
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;
@@ -235,10 +226,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * predicted next job pops behind the running one (0..3; each used only if it
  * is exactly the next pop, retracted on device otherwise: placements are
  * unchanged), 0 = one pop at a time;
- * "overlap" = 1 (default; placement 2) rotates batched pops over overlap + 1
- * streams so that up to `overlap` of them run beside each other (a pop's
- * sweep during the previous pops' placement), chained on the device (0..3;
- * 0 = one stream, one pop kernel at a time);
+ * "overlap" = 1 (default) alternates batched pops over two streams so that a
+ * pop's sweep runs beside the previous pop's placement, chained on the
+ * device; 0 = one stream, one pop kernel at a time;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
@@ -273,6 +263,7 @@ int kbhip_session_close(kb_session* s);
 #define KBHIP_RED_MAX_U64 0
 #define KBHIP_RED_MIN_I64 1
 #define KBHIP_RED_MAX_I64 2
+#define KBHIP_RED_SUM_I64 3 /* FitDelta counts of a task's walk over the shards */
 typedef int (*kbhip_allreduce_fn)(void* ctx, uint64_t* vals, int32_t n, int32_t op);
 /* recv <- the `bytes` sent by every rank, concatenated in rank order */
 typedef int (*kbhip_allgather_fn)(void* ctx, const void* send, void* recv, int64_t bytes);

@@ -1,8 +1,7 @@
-// kbhip_batch.h — device building blocks of the batched placement path,
-// shared by the pop kernels (kbhip_kernels.hip) and the persistent placer
-// (kbhip_pp.hip): wave exchange / sort / merge networks, selection keys,
-// the placements (levels, parallel levels, insertion, Backfilled), the
-// result granules and the row cache.
+// kbhip_batch.h — device building blocks of the batched placement path
+// (kbhip_kernels.hip): wave exchange / sort / merge networks, selection keys,
+// the placements (parallel levels, Backfilled nodes, pod-affinity classes,
+// node-array shards), the result granules and the row cache.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -22,9 +21,6 @@ static __device__ uint64_t* g_stamps;
     } while (0)
 #else
 #define STAMP(slot) do {} while (0)
-#endif
-#ifndef PSTAMP  // placement phase accumulation (the persistent placer's profile build)
-#define PSTAMP(k) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -173,20 +169,13 @@ __host__ __device__ inline uint64_t make_granule(uint32_t epoch, int stop, int n
 struct PopArgs {
     int32_t cls, n_tasks, gang_mode, min_avail, ready_count;
     uint32_t epoch;
-    int32_t placement;  // 0: sequential loop over precomputed chains, 1: running-min levels, 2: parallel levels
+    int32_t placement;  // 2 parallel levels, 3 node-array shard sweep, 6 Backfilled nodes, 7 pod-affinity class
     // 32-bit selection keys (when the class's score range and the node count
     // fit): key = (score - kbase + 1) << kshift | (kidxmax - idx) << 1 | pipelined,
     // ordered exactly as pack_key; halves the sort / merge network work.
     int32_t kbase, kshift, kidxmax;
     int32_t ent32;  // placement entries in 32 bits: (rm - kbase + 1) fits in 32 - kshift - 5 bits
     int32_t fit_set;  // FitDelta counter set of this launch (alternates per stream; the other one is zeroed)
-    // overlapped pops (k_pop_batch_ov, one previous pop in flight): 1 = rebuild
-    // the previous pop's written rows from its PopLink rows + commit granules
-    // instead of waiting for its write-back (the host sets it only when that
-    // pop was the last device work on the node rows); prev_cls = its class
-    int32_t msg, prev_cls;  // zero-initialised by the launchers' aggregate initialisers
-    int32_t pub;            // publish the rows message / ready / commit granules (the next pop may use them)
-    int32_t npb;            // k_pop_batch_ov: nodes per block and node slot (<= kPopThreads; 0 = kPopThreads)
 };
 
 // Selection key of the batched sweep in type T (see PopArgs).
@@ -242,19 +231,6 @@ __device__ __forceinline__ uint64_t wave_max_key(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// ---------------------------------------------------------------------------
-// Placement by levels (option "placement" = 1).  The greedy of a chunk picks,
-// task after task, the node with the largest current key; only the winner's
-// key changes.  Give candidate j the entries e(j, d) for its d-th extra
-// commit: (running minimum of its scores over levels 0..d, index, d, real
-// kind).  The greedy's choice sequence equals the entries sorted descending:
-// a node whose key RISES after a commit is picked again at once (every other
-// current key is below its previous one), which the running minimum keeps in
-// place; between nodes, equal scores go to the lower index as in pack_key.
-// Entries are generated level by level (one re-evaluation per lane), merged
-// into a sorted top-64, and generation stops when no lane's newest entry
-// reaches the current m-th entry (deeper entries of a node are smaller).
-// ---------------------------------------------------------------------------
 constexpr int kEntryIdxMax = (1 << 25) - 1;  // batched path: < 2^25 nodes
 
 // Node rows handed from one overlapped pop to the next (k_pop_batch_ov):
@@ -307,12 +283,7 @@ __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClas
     return k;
 }
 
-__device__ __forceinline__ uint64_t level_entry(int32_t rm, int n, int d, uint64_t key) {
-    return ((uint64_t)((uint32_t)rm ^ 0x80000000u) << 32) | ((uint64_t)(kEntryIdxMax - n) << 7) |
-           ((uint64_t)(63 - d) << 1) | (key & 1);
-}
 __device__ __forceinline__ int entry_idx(uint64_t e) { return kEntryIdxMax - (int)((e >> 7) & kEntryIdxMax); }
-__device__ __forceinline__ int entry_kind(uint64_t e) { return (e & 1) ? 2 : 1; }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32 |
            (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -347,90 +318,19 @@ __device__ __forceinline__ void block_tree_merge(T (*wl)[64], int wave, int lane
     }
 }
 
-// Wave 0 of the final merger: K = lane's candidate key (sorted top-64).
-__device__ void place_levels(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                             const PopArgs& a, uint64_t K, PopOut* out) {
-    const int lane = threadIdx.x & 63;
-    const int n = K ? key_idx(K) : -1;
-    Row base{};
-    uint64_t pw[4] = {0, 0, 0, 0};
-    int32_t na_n = 0;
-    if (n >= 0) {
-        base = load_row(nc, n);
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
-        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
-    }
-    uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
-    const int m = a.n_tasks;
-    uint64_t key = K;                                  // real key of the node after `ca + cp` commits
-    int32_t rm = K ? key_score(K) : 0;                 // running minimum of its scores
-    uint64_t cur = K ? level_entry(rm, n, 0, K) : 0;   // this lane's newest entry
-    uint64_t L = cur;                                  // sorted top-64 entries: lane p holds entry p
-    int ca = 0, cp = 0;
-    for (int d = 1; d < 64; ++d) {
-        const uint64_t T = readlane64(L, m - 1);       // m-th entry: deeper entries below it never place
-        if (!__ballot(cur != 0 && cur >= T)) break;
-        uint64_t e = 0;
-        if (key) {
-            if (key & 1) ++cp; else ++ca;              // the commit of the previous level (Pipeline / Allocate)
-            const Row r = apply_commits(base, c, ca, cp);
-            int32_t s;
-            bool passed;
-            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
-            if (key) {
-                rm = key_score(key) < rm ? key_score(key) : rm;
-                e = level_entry(rm, n, d, key);
-            }
-        }
-        cur = e;
-        L = wave_merge_desc(L, wave_sort_desc(e >= T ? e : 0));  // entries below T cannot reach the top m
-    }
-    STAMP(gridDim.x * 4 + 2);
-    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
-    const bool valid = lane < m && L != 0;
-    const uint64_t amask = __ballot(valid && entry_kind(L) == 1);  // Pipelined is not an AllocatedStatus
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    const int ready_p = a.ready_count + __popcll(amask & upto);
-    const uint64_t smask = __ballot(lane < m && (!valid || !a.gang_mode || ready_p >= a.min_avail));
-    int done, stop;
-    if (smask) {
-        const int p = __ffsll((unsigned long long)smask) - 1;
-        done = p + 1;
-        stop = __builtin_amdgcn_readlane((int)valid, p) ? 2 : 1;
-    } else {
-        done = m;
-        stop = 0;
-    }
-    // commits of this lane's node among the placed entries; write the row back
-    int na = 0, np = 0;
-    for (int p = 0; p < done; ++p) {
-        const uint64_t e = readlane64(L, p);
-        if (e && entry_idx(e) == n) { if (entry_kind(e) == 1) ++na; else ++np; }
-    }
-    if (n >= 0 && na + np > 0) {
-        const Row r = apply_commits(base, c, na, np);
-        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
-        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
-        nc.pods[n] = r.pods;
-        nc.nzc[n] = r.nzc;
-        nc.nzm[n] = r.nzm;
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pwc[w];
-    }
-    if (lane < done)
-        __hip_atomic_store(&out->g[lane],
-                           make_granule(a.epoch, stop, done, L ? entry_kind(L) : 0, L ? entry_idx(L) : -1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    STAMP(gridDim.x * 4 + 3);
-}
-
 // ---------------------------------------------------------------------------
-// Placement by parallel levels (option "placement" = 2): the same entries as
-// place_levels, but a round computes 8 depths at once — wave w evaluates
-// candidate j after d = 8r + w commits of this class — then one sort + tree
-// merge of the round's 512 entries.  Commit kinds along a chain are
+// Placement by parallel levels.  The greedy of a chunk picks, task after
+// task, the node with the largest current key; only the winner's key changes.
+// Give candidate j the entries e(j, d) for its d-th extra commit: (running
+// minimum of its scores over depths 0..d, index, d, real kind).  The greedy's
+// choice sequence equals the entries sorted descending: a node whose key
+// RISES after a commit is picked again at once (every other current key is
+// below its previous one), which the running minimum keeps in place; between
+// nodes, equal scores go to the lower index as in pack_key
+// (tests/test_gpu_placement_levels.py checks the argument exhaustively on
+// CPU).  A round computes 8 depths at once — wave w evaluates candidate j
+// after d = 8r + w commits of this class — then one sort + tree merge of the
+// round's 512 entries.  Commit kinds along a chain are
 // Allocate^a Pipeline^p (once Idle + Backfilled cannot fit, later commits
 // only touch Releasing), so a first pass assumes Allocate everywhere and the
 // depths behind a lane's first Pipeline are recomputed.  An entry is
@@ -459,6 +359,12 @@ template <typename ET>
 __device__ __forceinline__ int entry_node(ET e, const PopArgs& a) {
     if constexpr (sizeof(ET) == 8) return entry_idx(e);
     else return a.kidxmax - (int)((e >> 6) & (uint32_t)a.kidxmax);
+}
+// Running-minimum score of a placement entry.
+template <typename ET>
+__device__ __forceinline__ int32_t entry_rm(ET e, const PopArgs& a) {
+    if constexpr (sizeof(ET) == 8) return (int32_t)((uint32_t)(e >> 32) ^ 0x80000000u);
+    else return (int32_t)(e >> (a.kshift + 5)) - 1 + a.kbase;
 }
 template <typename T>
 __device__ __forceinline__ T readlane_t(T v, int l) {
@@ -513,61 +419,17 @@ __device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b
     return v + __shfl_xor(v, 32, 64);
 }
 
-// SC1: rows read and written through sc1 (overlapped pops); the write-back is
-// then published as done = seq before the result stores.
-// L sorted descending over the lanes, e not in L: L with e inserted (the last
-// entry drops off).  A ballot gives the position, a DPP wave_shr:1 moves the tail.
-template <typename T>
-__device__ __forceinline__ T wave_shr1(T v) {  // lane i <- lane i - 1 (lane 0 <- 0)
-    if constexpr (sizeof(T) == 8) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
-        return ((uint64_t)hi << 32) | lo;
-    } else {
-        return (T)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
-    }
-}
-template <typename T>
-__device__ __forceinline__ T wave_insert_sorted(T L, T e) {
-    const int lane = threadIdx.x & 63;
-    const int pos = __popcll(__ballot(L > e));
-    const T sh = wave_shr1(L);
-    return lane < pos ? L : (lane == pos ? e : sh);
-}
-
-// INS: the round's entries join the running list by insertion (only those
-// above the m-th entry; usually a few) instead of a sort + merge tree.
-// Running-minimum score of a placement entry.
-template <typename ET>
-__device__ __forceinline__ int32_t entry_rm(ET e, const PopArgs& a) {
-    if constexpr (sizeof(ET) == 8) return (int32_t)((uint32_t)(e >> 32) ^ 0x80000000u);
-    else return (int32_t)(e >> (a.kshift + 5)) - 1 + a.kbase;
-}
-// The rows a placement committed, compacted (persistent placer, kbhip_pp.hip).
-struct PPHistOut {
-    int32_t n;
-    int32_t node[64];
-    Row row[64];
-    uint64_t pw[64][4];
-};
-
-template <typename ET, bool SC1 = false, bool INS = false>
+template <typename ET, bool SC1 = false>
 __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
-                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
-                               PPHistOut* ho = nullptr, PopLink* lk = nullptr, bool wait_prev = false) {
-    // lk (overlapped pops): publish ready[seq] after round 0 (the candidate
-    // rows stored before this call are drained by then) and the commit
-    // granules before the write-back; wait_prev: pop seq-1's write-back may
-    // still be in flight (PopArgs::msg) -- wait for it before writing rows.
+                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0) {
     // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
     // (a node-array shard writes back only its own; one GPU: all of them).
-    // t0 (persistent placer): the candidates are exact down to the selection
-    // key t0 only — a node outside them may beat an entry below it — so the
-    // launch places the entries at or above it and leaves the rest of the
-    // chunk to the host (stop 0 with done < m; done 0 when none).  ho: the
-    // committed rows, compacted, for the placer's history.
+    // t0 (a cut): the candidates are exact down to the selection key t0 only
+    // — a node outside them may beat an entry below it — so the launch places
+    // the entries at or above it and leaves the rest of the chunk to the host
+    // (stop 0 with done < m; done 0 when none).
     // Node indices in keys and entries are global.
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
@@ -597,20 +459,20 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
-    STAMP(gridDim.x * 4 + 11); PSTAMP(1);
+    STAMP(gridDim.x * 4 + 11);
     uint64_t pwc[4];
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
     if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
     __syncthreads();  // K read by every wave; wl free
-    STAMP(gridDim.x * 4 + 12); PSTAMP(2);
+    STAMP(gridDim.x * 4 + 12);
     if (wave == 0 && n >= 0) {  // candidate nodes are distinct
         int h = hash_slot(n);
         while (atomicCAS(&s_hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
         s_hlane[h] = lane;
     }
-    STAMP(gridDim.x * 4 + 5); PSTAMP(3);
+    STAMP(gridDim.x * 4 + 5);
     auto eval_at = [&](int d, int ap, int32_t* sc) -> int {  // kind of commit d+1's key (0: infeasible)
         if (d == 0) { *sc = key_score(K); return key_kind(K); }
         const int na = d < ap ? d : ap;
@@ -654,39 +516,14 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             rm = x < rm ? x : rm;
         }
         const ET e = ok ? depth_entry<ET>(rm, n, d, a) : (ET)0;
-        if (r == 0) { STAMP(gridDim.x * 4 + 6); PSTAMP(4); }
-        if (r == 0 && lk && wave == 0) {  // the rows message went out before the placement began
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) st_sc1(&lk->ready[seq % kLinkSlots][0], (uint64_t)seq);
-        }
+        if (r == 0) { STAMP(gridDim.x * 4 + 6); }
         if (wave == kW - 1) { s_last[lane] = e; s_rm[(r + 1) & 1][lane] = rm; }
-        if constexpr (INS) {
-            wl[wave][lane] = e;
-            __syncthreads();
-            if (wave == 0) {
-                // depth 0 (round 0, wave 0): the candidate list itself, already sorted
-                int w0 = 0;
-                if (r == 0) { L = e; w0 = 1; }
-                ET T = readlane_t(L, m - 1);
-                for (int w2 = w0; w2 < kW; ++w2) {
-                    const ET x = wl[w2][lane];
-                    for (uint64_t q = __ballot(x > T); q; q &= q - 1) {
-                        const ET y = readlane_t(x, __ffsll((unsigned long long)q) - 1);
-                        if (y > T) {
-                            L = wave_insert_sorted(L, y);
-                            T = readlane_t(L, m - 1);
-                        }
-                    }
-                }
-            }
-        } else {
-            wl[wave][lane] = wave_sort_desc(e);
-            __syncthreads();
-            block_tree_merge(wl, wave, lane);
-            if (wave == 0) L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
-        }
+        wl[wave][lane] = wave_sort_desc(e);
+        __syncthreads();
+        block_tree_merge(wl, wave, lane);
+        if (wave == 0) L = r == 0 ? wl[0][lane] : wave_merge_desc(L, wl[0][lane]);
         if (wave == 0) {
-            if (r == 0) { STAMP(gridDim.x * 4 + 7); PSTAMP(5); }
+            if (r == 0) { STAMP(gridDim.x * 4 + 7); }
             const ET T = readlane_t(L, m - 1);  // m-th entry: deeper entries below it never place
             const ET le = s_last[lane];
             const bool more = le != 0 && le >= T;
@@ -699,9 +536,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         alive = s_last[lane] != 0;  // rewritten by wave kW-1 only after the next round's first barrier
     }
     if (wave != 0) return;
-    // pop seq-1's done, in flight during the stop rule below (wait_prev)
-    uint32_t prev_done = wait_prev ? ld_sc1(done_flag) : 0u;
-    STAMP(gridDim.x * 4 + 2); PSTAMP(6);
+    STAMP(gridDim.x * 4 + 2);
     // commit kind of each position: its node's candidate lane, the entry's depth
     const bool inm = lane < m && L != 0;
     int lf = 0;
@@ -734,12 +569,12 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         done = cap;  // cap == m: every task placed, the pop goes on (stop 0)
         stop = 0;
     }
-    STAMP(gridDim.x * 4 + 8); PSTAMP(7);
+    STAMP(gridDim.x * 4 + 8);
     if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
     __builtin_amdgcn_wave_barrier();
     const int cc = s_cnt[lane];
-    STAMP(gridDim.x * 4 + 9); PSTAMP(8);
+    STAMP(gridDim.x * 4 + 9);
     if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
         // fit_in: every node at the state this pop started from; the candidates
         // then carry the commits made before the failing task
@@ -767,19 +602,6 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    if (lk) {  // commit granules: pop seq+1 rebuilds the rows written below from them
-        const int ap = s_apos[lane];
-        const int na = (n >= 0 && cc > 0) ? (cc < ap ? cc : ap) : 0;
-        const int np = (n >= 0 && cc > 0) ? cc - na : 0;
-        st_sc1(&lk->commits[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint64_t)(na << 8) | (uint64_t)np);
-    }
-    if (wait_prev) {  // rows of pop seq-1's candidates: its stores must land before ours
-        long spin = 0;
-        while ((int32_t)(prev_done - (seq - 1)) < 0 && ++spin < (1L << 21)) {
-            __builtin_amdgcn_s_sleep(2);
-            prev_done = ld_sc1(done_flag);
-        }
-    }
     const int ln = n - wb_base;  // local row of the written-back node
     if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
         const int ap = s_apos[lane];
@@ -803,19 +625,6 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                 for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
         }
     }
-    if (ho) {  // committed rows, compacted (lane order)
-        const bool wr = n >= 0 && cc > 0;
-        const uint64_t wm = __ballot(wr);
-        if (wr) {
-            const int pos = __popcll(wm & ((1ull << lane) - 1));
-            const int ap = s_apos[lane];
-            const int na = cc < ap ? cc : ap;
-            ho->node[pos] = n;
-            ho->row[pos] = apply_commits(base, c, na, cc - na);
-            for (int w = 0; w < 4; ++w) ho->pw[pos][w] = pwc[w];
-        }
-        if (lane == 0) ho->n = __popcll(wm);
-    }
     if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) st_sc1(done_flag, seq);
@@ -824,168 +633,9 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, lane < done ? kind : 0,
                                                        (lane < done && inm) ? entry_node(L, a) : -1),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    STAMP(gridDim.x * 4 + 3); PSTAMP(9);
+    STAMP(gridDim.x * 4 + 3);
 }
 
-
-// ---------------------------------------------------------------------------
-// Placement by insertion (option "placement" = 4): one wave, no sort
-// networks.  The greedy order is the descending order of the entries
-// e(j, d) = (running min of node j's scores over depths 0..d, index, depth)
-// (see place_levels).  The depth-0 entries are the sorted candidate list
-// itself; a node's entries decrease with depth, so the top-m entries hold a
-// prefix of each node's sequence.  Rounds: every lane whose newest entry is
-// still among the top m evaluates its next depth (its own row, its own
-// Allocate^a Pipeline^p chain, no fix-ups); new entries above the m-th are
-// inserted into the sorted list one at a time (a ballot gives the position,
-// a DPP wave shift moves the tail).  A round that inserts nothing ends it —
-// typically after one or two rounds, as a commit lowers a node's score.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v) {  // lane i <- lane i - 1 (lane 0 <- 0)
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, false);
-    return ((uint64_t)hi << 32) | lo;
-}
-// L sorted descending over the lanes, e not in L: L with e inserted (the last entry drops off).
-__device__ __forceinline__ uint64_t wave_insert_desc(uint64_t L, uint64_t e) {
-    const int lane = threadIdx.x & 63;
-    const int pos = __popcll(__ballot(L > e));
-    const uint64_t sh = wave_shr1_64(L);
-    return lane < pos ? L : (lane == pos ? e : sh);
-}
-
-template <bool SC1 = false>
-__device__ void place_insert(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                             const PopArgs& a, PopOut* out, uint64_t K, uint32_t* done_flag = nullptr,
-                             uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
-                             uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff) {
-    const int lane = threadIdx.x & 63;
-    const int n = K ? key_idx(K) : -1;  // global node index (keys are global)
-    Row base{};
-    uint64_t pw[4] = {0, 0, 0, 0};
-    int32_t na_n = 0;
-    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
-    if (rslot >= 0) {
-        base = rc->row[rslot];
-        for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
-        na_n = rc->na[rslot];
-    } else if (n >= 0) {
-        base = load_row_t<SC1>(nc, n);
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
-        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
-    }
-    uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
-    const int m = a.n_tasks;
-    // this lane's chain: depth d of its newest entry, commits by kind behind it, first Pipeline depth
-    int d = 0, ca = 0, cp = 0, apos = 64;
-    uint64_t key = K;  // key at depth d (its kind is the kind of commit d + 1)
-    int32_t rm = K ? key_score(K) : 0;
-    uint64_t last = K ? level_entry(rm, n, 0, K) : 0;  // newest entry
-    uint64_t L = last;  // lane p: entry p of the sorted top entries (depth-0 entries are the sorted list)
-    uint64_t T = readlane64(L, m - 1);
-    for (int round = 1; round < 64; ++round) {
-        const bool act = last != 0 && last >= T;  // its newest entry is among the top m
-        if (!__ballot(act)) break;
-        uint64_t e = 0;
-        if (act) {
-            if (key & 1) { ++cp; if (apos == 64) apos = d; } else ++ca;  // commit d + 1 takes the depth-d kind
-            ++d;
-            const Row r = apply_commits(base, c, ca, cp);
-            int32_t s;
-            bool passed;
-            key = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
-            if (key) {
-                rm = key_score(key) < rm ? key_score(key) : rm;
-                e = level_entry(rm, n, d, key);
-            }
-            last = e;
-        }
-        // insert the new entries that beat the m-th (T only rises: one below it never enters)
-        for (uint64_t q = __ballot(e != 0 && e > T); q; q &= q - 1) {
-            const uint64_t x = readlane64(e, __ffsll((unsigned long long)q) - 1);
-            if (x > T) {
-                L = wave_insert_desc(L, x);
-                T = readlane64(L, m - 1);
-            }
-        }
-    }
-    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
-    const bool inm = lane < m && L != 0;
-    const int kind = inm ? entry_kind(L) : 0;
-    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    const int ready_p = a.ready_count + __popcll(amask & upto);
-    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
-    int done, stop;
-    if (smask) {
-        const int p = __ffsll((unsigned long long)smask) - 1;
-        done = p + 1;
-        stop = __builtin_amdgcn_readlane((int)inm, p) ? 2 : 1;
-    } else {
-        done = m;
-        stop = 0;
-    }
-    // commits of this lane's node among the placed entries
-    int cc = 0;
-    for (int p = 0; p < done; ++p) {
-        const uint64_t x = readlane64(L, p);
-        cc += (x != 0 && entry_idx(x) == n) ? 1 : 0;
-    }
-    const int nal = cc < apos ? cc : apos;  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
-    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
-        uint32_t fb_base = 0, fb_post = 0;
-        if (n >= 0) {
-            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
-            const Row r = apply_commits(base, c, nal, cc - nal);
-            int32_t sc;
-            bool passed;
-            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
-            fb_post = fit_bits(c, r, passed);
-        }
-        const uint32_t sweep = fit_sum(fit_raw);
-        int32_t tot[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
-                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
-        if (lane == 0) {
-            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    const int ln = n - wb_base;
-    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {
-        const Row r = apply_commits(base, c, nal, cc - nal);
-        if constexpr (SC1) {
-            st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
-            st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
-            st_sc1(&nc.pods[ln], r.pods);
-            st_sc1(&nc.nzc[ln], r.nzc);
-            st_sc1(&nc.nzm[ln], r.nzm);
-            if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
-        } else {
-            nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
-            nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
-            nc.pods[ln] = r.pods;
-            nc.nzc[ln] = r.nzc;
-            nc.nzm[ln] = r.nzm;
-            if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
-        }
-    }
-    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) st_sc1(done_flag, seq);
-    }
-    if (lane < done)
-        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, kind, inm ? entry_idx(L) : -1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 // ---------------------------------------------------------------------------
 // Placement of a session with Backfilled nodes (placement 6; one wave, task

@@ -82,28 +82,12 @@ struct KeyFormat {
     int32_t base = 0, shift = 0, idxmax = 0;
 };
 struct ShardMsg;  // kbhip_eval.h
-// Persistent placer (kbhip_pp.hip, option "pp"): sizes of its device records,
-// the per-pop sweep (command `seq` into ring slot seq % pp_slots(); lists,
-// arrive and fitw are that slot's), the placer (one resident workgroup from
-// command seq0 on; it leaves on a STOP command or after 20 ms without one and
-// records in the pinned mapped host record where it stopped) and STOP.
-size_t pp_slot_bytes();
-size_t pp_ctrl_bytes();
-size_t pp_host_bytes();
-int pp_slots();
-size_t pp_list_keys(int n_nodes);
-size_t pp_arrive_words();
-hipError_t launch_pp_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                           int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                           void* ring, void* lists, uint32_t* arrive, uint32_t* fitw, const void* ctrl, uint32_t seq,
-                           uint32_t out_slot, hipStream_t st);
-hipError_t launch_pp_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, void* ring, void* ctrl, void* outs,
-                            const uint32_t* fitw, int64_t fitw_words, void* host, uint32_t seq0, hipStream_t st);
-hipError_t launch_pp_stop(void* ring, uint32_t seq, hipStream_t st);
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
-// placement 3 (node-array shards): no placement; the shard's top-64 with rows
-// goes to shard_out for the all-gather, then launch_shard_place places.
+// placement 2: parallel levels; 6: sessions with Backfilled nodes; 7:
+// pod-affinity classes; 3 (node-array shards): no placement — the shard's
+// top-64 with rows goes to shard_out for the all-gather, then
+// launch_shard_place places.
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
@@ -112,58 +96,45 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 // them, rank order): identical on every shard; each writes back its own rows.
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, int placement = 2);
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
 // -1: none).  At session open: done 0, every slot tagged 0 with no nodes.
 constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
-constexpr int kMaxDep = 3;     // previous pops an overlapped pop may run beside (streams - 1)
-constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
-struct PopLinkRow {  // a candidate's row before the pop's commits (Row of kbhip_eval.h, 112 bytes)
-    int64_t v[13];
-    int32_t pods, maxtasks;
-};
+constexpr int kMaxDep = 1;     // previous pops an overlapped pop runs beside (streams - 1)
+constexpr int kLinkSlots = 2;  // > kMaxDep: a slot is rewritten only after its readers finished
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
     uint64_t touched[kLinkSlots][64];
-    // Row hand-off without the write-back on the chain (PopArgs::msg): pop seq
-    // publishes its candidates' rows as they were before its commits
-    // (rows[seq]), then ready[seq] = seq once they are drained (early in its
-    // placement), then per candidate a self-tagged commit granule
-    // {seq << 32 | allocs << 8 | pipelines} (commits[seq]) before its row
-    // write-back; pop seq+1 rebuilds the written rows from those.
-    PopLinkRow rows[kLinkSlots][64];
-    uint64_t ready[kLinkSlots][8];
-    uint64_t commits[kLinkSlots][64];
 };
-// pub: publish this pop's rows message for the next pop (option "ov_msg").
-// prev_cls >= 0: pop seq-1 (class prev_cls) was the last device work on the
-// node rows, and this class has no host ports: its written rows are rebuilt
-// from its PopLink rows message and commit granules (PopArgs::msg).
-// Overlapped batched pop number `seq` (>= 1) on stream st; pops seq-1 ..
-// seq-ndep may still run on other streams (1 <= ndep <= kMaxDep): it leaves
-// their candidates out of its sweep and re-evaluates them once pop seq-1's
-// write-back is done.  cand holds (blocks + kMaxGroups) * 64 keys, arrive
-// (3 * kMaxGroups + 1) * 32 counters, both private to the launch's stream;
-// fit_set alternates per launch on a stream (FitDelta counter sets).
+// Overlapped batched pop number `seq` (>= 1) on stream st; pop seq-1 may
+// still run on the other stream: it leaves that pop's candidates out of its
+// sweep and re-evaluates them once pop seq-1's write-back is done.  cand
+// holds (blocks + kMaxGroups) * 64 keys, arrive (3 * kMaxGroups + 1) * 32
+// counters, both private to the launch's stream; fit_set alternates per
+// launch on a stream (FitDelta counter sets).
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep, int fit_set, int placement = 2, int prev_cls = -1,
-                               bool pub = false);
+                               uint32_t seq, int fit_set);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);
-// One task's walk FitDelta histogram on the current state (kbhip_kernels.hip).
-hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int chosen,
+// One task's walk FitDelta histogram on the current state (kbhip_kernels.hip):
+// the task is ctrl's task 0 (class, fallback node, inter-pod affinity min /
+// max); chosen >= 0: the node its walk stopped at (ctrl->slot[0] <- its walk
+// key on this shard, 0 elsewhere: all-reduce MAX before the histogram on
+// shards — launch_fit_key, then launch_fit_count).
+hipError_t launch_fit_key(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int chosen,
+                          hipStream_t st);
+hipError_t launch_fit_count(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int chosen,
                             int chosen_kind, int32_t* out4, hipStream_t st);
 // Inverse node updates of a batched pop's placements (a retracted prediction).
 hipError_t launch_undo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);
 int pop_blocks(int n_nodes, int* R_out);
-int pop_blocks_ov(int n_nodes, int* R_out);  // k_pop_batch_ov's grid (nodes per block: KBHIP_POP_NPB)
 // A batched pop of one session in a multi-session launch (what-if sessions,
 // placement 6 or 7): the arguments of launch_pop_batch.
 constexpr int kPopMulti = 8;  // sessions per launch (kernel argument space)

@@ -220,12 +220,13 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
 // ---------------------------------------------------------------------------
 // batched path
 // PL: the placement compiled into this instantiation — 2 parallel levels,
-// 5 parallel levels merged by insertion, 6 sessions with Backfilled nodes
-// (walk keys, sequential placement), 7 pod-affinity classes (affinity
-// predicates in the sweep, sequential placement with count-table slots), 3 the node-array shard's sweep only
-// (no placement: the exchange follows), -1 the test-only modes 0 / 1 / 4 —
-// so that a kernel's registers (and the occupancy of its sweep blocks) are
-// those of one placement path.
+// 6 sessions with Backfilled nodes (walk keys, sequential placement), 7
+// pod-affinity classes (affinity predicates in the sweep, sequential
+// placement with count-table slots), 3 the node-array shard's sweep only (no
+// placement: the exchange follows) — so that a kernel's registers (and the
+// occupancy of its sweep blocks) are those of one placement path: compiling
+// several placements into one kernel raised it from 101 to 194 VGPRs and
+// halved the sweep's occupancy.
 // One session's batched pop in a multi-session launch (k_pop_batch_multi):
 // the kernel arguments carry kPopMulti descriptors (4 KB kernarg limit).
 struct PopDesc {
@@ -368,150 +369,12 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
         place_aff(cf, nc, t, c, a, out, wl[0][lane]);
         STAMP(nb_ * 4 + 3);
         return;
-    } else {
-    if constexpr (PL == 2 || PL == 5) {  // every wave takes part
+    } else {  // PL == 2: parallel levels, every wave takes part
+        static_assert(PL == 2, "batched placements: 2, 3, 6, 7");
         STAMP(nb_ * 4 + 1);
-        if (a.ent32) place_parallel<uint32_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
-        else place_parallel<uint64_t, false, PL == 5>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
-        return;
-    } else {
-    if (a.placement == 1) {  // uniform
-        if (wave != 0) return;
-        STAMP(nb_ * 4 + 1);
-        place_levels(cf, nc, t, c, a, wl[0][lane], out);
-        return;
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
     }
-    if (a.placement == 4) {  // uniform
-        if (wave != 0) return;
-        STAMP(nb_ * 4 + 1);
-        place_insert<false>(cf, nc, t, c, a, out, wl[0][lane], nullptr, 0, nullptr, s_fitin, fit_raw);
-        STAMP(nb_ * 4 + 3);
-        return;
-    }
-    // 3. placement.  Lane j owns candidate j of the sorted global top-64: node
-    // n, sweep key K.  The post-commit keys of each candidate (after 1..kDepth
-    // more tasks of this class, assuming every commit is an Allocate) are
-    // computed by waves 0..kDepth-1 in parallel.
-    __shared__ uint64_t chainbuf[kDepth][64];
-    const uint64_t K = wl[0][lane];
-    const int n = K ? key_idx(K) : -1;
-    Row base{};
-    uint64_t pw[4] = {0, 0, 0, 0};
-    int32_t na_n = 0;  // static node-affinity weight of this lane's node
-    if (n >= 0 && wave <= kDepth) {
-        base = load_row(nc, n);
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
-        if (cf.score_mult) na_n = na_weight(c, t, nc, n);
-    }
-    uint64_t pwc[4];  // ports after one or more commits of this class
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
-    if (wave < kDepth) {
-        uint64_t v = 0;
-        if (n >= 0) {
-            const Row r = apply_commits(base, c, wave + 1, 0);
-            int32_t s;
-            bool passed;
-            v = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
-        }
-        chainbuf[wave][lane] = v;
-    }
-    __syncthreads();
-    if (wave != 0) return;
-    STAMP(nb_ * 4 + 1);
-    uint64_t chain[kDepth];
-#pragma unroll
-    for (int d = 0; d < kDepth; ++d) chain[d] = chainbuf[d][lane];
-    // Winner of each task = max(first unchanged list entry, best changed entry).
-    // Changed entries are always a prefix [0, first) of the list.  The hot
-    // loop only reads precomputed post-commit keys; a lane whose chain is
-    // exhausted (or that was pipelined) leaves the loop for a recompute.
-    uint64_t val = K;       // current key of this lane's candidate
-    int na = 0, np = 0;     // commits on this lane's node by kind
-    int first = 0;          // uniform
-    uint64_t bc_val = 0;    // uniform: best key among changed entries
-    int bc_lane = -1;       // uniform
-    int ready = a.ready_count, stop = -1, done = 0;
-    uint64_t mine = 0;      // lane i: winner key of task i
-    int i = 0;
-    while (i < a.n_tasks && stop < 0) {
-        int slow_lane = -1;
-        for (; i < a.n_tasks; ++i) {
-            const uint64_t cu = first < 64 ? ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(K >> 32), first) << 32 |
-                                              (uint32_t)__builtin_amdgcn_readlane((int)K, first))
-                                           : 0;
-            uint64_t w;
-            int wl;
-            if (cu > bc_val) { w = cu; wl = first; ++first; }
-            else { w = bc_val; wl = bc_lane; }
-            done = i + 1;
-            if (!w) { stop = 1; break; }
-            if (lane == i) mine = w;
-            const int kind = key_kind(w);
-            bool fast = true;
-            if (lane == wl) {
-                if (kind == 1) ++na; else ++np;
-                const int cc = na + np;
-                fast = np == 0 && cc <= kDepth;
-                uint64_t x = chain[0];
-#pragma unroll
-                for (int d = 1; d < kDepth; ++d) if (cc == d + 1) x = chain[d];
-                if (fast) val = x;
-            }
-            if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
-            if (!a.gang_mode || ready >= a.min_avail) stop = 2;  // allocate.go:191-195
-            else if (i + 1 == a.n_tasks) stop = 0;
-            if (!__builtin_amdgcn_readlane((int)fast, wl)) { slow_lane = wl; ++i; break; }
-            const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), wl) << 32 |
-                                (uint32_t)__builtin_amdgcn_readlane((int)val, wl);
-            if (wl == bc_lane) {  // the best changed node changed again: rescan the changed prefix
-                bc_val = wave_max_key(lane < first ? val : 0);
-                const uint64_t m = __ballot(lane < first && val == bc_val && bc_val != 0);
-                bc_lane = m ? __ffsll((unsigned long long)m) - 1 : -1;
-            } else if (nv > bc_val) {
-                bc_val = nv;
-                bc_lane = wl;
-            }
-            if (stop >= 0) { ++i; break; }
-        }
-        if (slow_lane < 0) break;
-        // rare: re-evaluate the winner's node after its latest commit
-        if (lane == slow_lane) {
-            const Row r = apply_commits(base, c, na, np);
-            int32_t s;
-            bool passed;
-            val = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
-        }
-        const uint64_t nv = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(val >> 32), slow_lane) << 32 |
-                            (uint32_t)__builtin_amdgcn_readlane((int)val, slow_lane);
-        if (slow_lane == bc_lane) {
-            bc_val = wave_max_key(lane < first ? val : 0);
-            const uint64_t m = __ballot(lane < first && val == bc_val && bc_val != 0);
-            bc_lane = m ? __ffsll((unsigned long long)m) - 1 : -1;
-        } else if (nv > bc_val) {
-            bc_val = nv;
-            bc_lane = slow_lane;
-        }
-    }
-    STAMP(nb_ * 4 + 2);
-    // 4. write back committed rows and the results
-    if (na + np > 0) {
-        const Row r = apply_commits(base, c, na, np);
-        nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;
-        nc.rel_cpu[n] = r.rel_cpu; nc.rel_mem[n] = r.rel_mem; nc.rel_gpu[n] = r.rel_gpu;
-        nc.pods[n] = r.pods;
-        nc.nzc[n] = r.nzc;
-        nc.nzm[n] = r.nzm;
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pwc[w];
-    }
-    if (lane < done)
-        __hip_atomic_store(&out->g[lane],
-                           make_granule(a.epoch, stop, done, mine ? key_kind(mine) : 0, mine ? key_idx(mine) : -1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    STAMP(nb_ * 4 + 3);
-    }  // placement 0
-    }  // PL != 3
 }
 
 template <int R, typename KT, int PL>
@@ -554,13 +417,10 @@ __device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
 
 constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
 
-// INS: the placement merges each round by insertion (placement 5) instead of
-// sort + merge trees (placement 2); one placement per instantiation keeps the
-// kernel's registers (and so the occupancy of its sweep blocks) at one path's.
-template <int R, typename KT, int PLV>
+template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                              PopLink* link, uint32_t seq, int ndep) {
+                                                              PopLink* link, uint32_t seq) {
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
@@ -573,16 +433,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
     const TaskClass c = t.classes[a.cls];
-    // a.npb nodes per slot: fewer than the block's threads spreads a small node
-    // array over more blocks (CUs); the extra threads only merge and place
-    const int npb = a.npb ? a.npb : kPopThreads;
-    const int base = blockIdx.x * R * npb;
-    // the ndep pops before this one may still be writing rows: seq-1 .. seq-ndep
-    uint64_t tv[kMaxDep] = {};
-#pragma unroll
-    for (int k = 0; k < kMaxDep; ++k)  // in flight while the rows below load
-        if (wave == 0 && k < ndep && seq > (uint32_t)(k + 1))
-            tv[k] = ld_sc1(&link->touched[(seq - 1 - k) % kLinkSlots][lane]);
+    const int base = blockIdx.x * R * kPopThreads;
+    // pop seq-1 may still be writing rows: its candidates, in flight while the rows below load
+    uint64_t tv = 0;
+    if (wave == 0 && seq > 1) tv = ld_sc1(&link->touched[(seq - 1) % kLinkSlots][lane]);
     for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
     if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
     // 1. evaluate R nodes per lane, then leave pop seq-1's candidates out
@@ -590,33 +444,30 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     uint32_t fbs[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int n = (blockIdx.x * R + r) * npb + threadIdx.x;
+        const int n = base + r * kPopThreads + threadIdx.x;
         keys[r] = 0;
         fbs[r] = 0;
-        if ((int)threadIdx.x < npb && n < nc.n) {
+        if (n < nc.n) {
             int32_t s;
             bool passed;
             keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
     }
     __syncthreads();  // s_skip zeroed
-    int tn[kMaxDep];  // wave 0: candidate `lane` of pop seq-1-k (-1: none)
+    int tn = -1;  // wave 0: candidate `lane` of pop seq-1 (-1: none)
     if (wave == 0) {
         bool ok = true;
-#pragma unroll
-        for (int k = 0; k < kMaxDep; ++k) {
-            tn[k] = -1;
-            if (k >= ndep || seq <= (uint32_t)(k + 1)) continue;
-            const uint32_t want = seq - 1 - k;
+        if (seq > 1) {
+            const uint32_t want = seq - 1;
             long spin = 0;
-            while (ok && __ballot((uint32_t)(tv[k] >> 32) != want) != 0) {  // re-read every granule
+            while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
                 if (++spin >= kLinkSpin) ok = false;
                 __builtin_amdgcn_s_sleep(2);
-                tv[k] = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+                tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
             }
-            const int x = ok ? (int)(uint32_t)tv[k] : -1;
-            tn[k] = x;
-            if (x >= base && x < base + R * npb) atomicOr(&s_skip[(x - base) >> 5], 1u << ((x - base) & 31));
+            tn = ok ? (int)(uint32_t)tv : -1;
+            if (tn >= base && tn < base + R * kPopThreads)
+                atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
         }
         if (lane == 0) s_ok = ok;
     }
@@ -624,8 +475,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     KT best = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const int o = r * npb + threadIdx.x;
-        const bool skip = (int)threadIdx.x < npb && ((s_skip[o >> 5] >> (o & 31)) & 1u);  // rows in flight: counted by the patch
+        const int o = r * kPopThreads + threadIdx.x;
+        const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: counted by the patch
         fit_block_add(s_fitb, skip ? 0u : fbs[r]);
         const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
         best = r == 0 ? k : wave_merge_desc(best, k);
@@ -676,7 +527,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         __syncthreads();
         if (!role) return;
     }
-    // 2b. last group merger: the top-64 of every node but the previous pops' candidates
+    // 2b. last group merger: the top-64 of every node but the previous pop's candidates
     STAMP(gridDim.x * 4 + 4);
     {
         KT acc = 0;
@@ -697,8 +548,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ RowCache rc;
     int32_t pna = 0;  // wave 0: pop seq-1's candidate `lane`: node-affinity weight, static predicates
     bool pst = false;
-    const bool msg = a.msg && ndep == 1;  // rebuild pop seq-1's rows (PopLink rows + commit granules)
-    Row mrow{};                           // wave 0, msg: pop seq-1's candidate `lane` before its commits
     if (wave == 0) {
         for (int h = lane; h < kHash; h += 64) rc.hkey[h] = -1;
         const KT lk = wlk[0][lane];
@@ -708,48 +557,16 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < port_win(c, nc)) ? load_port_t<false>(nc, c.pw_lo + w, ln) : 0;
             rc.na[lane] = cf.score_mult ? na_weight(c, t, nc, ln) : 0;
         }
-        if (tn[0] >= 0) {
-            pst = static_pred(cf, c, t, nc, tn[0]);
-            pna = (pst && cf.score_mult) ? na_weight(c, t, nc, tn[0]) : 0;
+        if (tn >= 0) {
+            pst = static_pred(cf, c, t, nc, tn);
+            pna = (pst && cf.score_mult) ? na_weight(c, t, nc, tn) : 0;
         }
         __builtin_amdgcn_wave_barrier();
         if (ln >= 0) rc_insert(&rc, ln, lane);
-        if (msg && __ballot(tn[0] >= 0) != 0) {  // pop seq-1's rows message (drained before its ready)
-            const uint32_t want = seq - 1;
-            long spin = 0;
-            bool okr = s_ok;
-            while (okr && (uint32_t)ld_sc1(&link->ready[want % kLinkSlots][0]) != want) {
-                if (++spin >= kLinkSpin) okr = false;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (tn[0] >= 0 && okr) {
-                const PopLinkRow* pr = &link->rows[want % kLinkSlots][lane];
-                int64_t v[13];
-#pragma unroll
-                for (int k = 0; k < 13; ++k) v[k] = ld_sc1(&pr->v[k]);
-                mrow = Row{v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12],
-                           ld_sc1(&pr->pods), ld_sc1(&pr->maxtasks)};
-            }
-            if (lane == 0 && !okr) s_ok = 0;
-        }
     }
-    // pop seq-1's write-back, which follows seq-2's ... (relaxed sc1 poll;
-    // every load of their rows below is sc1); their candidates on final rows
-    uint64_t pcg = 0;  // wave 0, msg: pop seq-1's commit granule of candidate `lane`
-    if (msg) {
-        if (wave == 0) {  // its commits (self-tagged granules), not its write-back
-            const uint32_t want = seq - 1;
-            bool ok = s_ok;
-            long spin = 0;
-            if (tn[0] >= 0) pcg = ld_sc1(&link->commits[want % kLinkSlots][lane]);
-            while (ok && __ballot(tn[0] >= 0 && (uint32_t)(pcg >> 32) != want) != 0) {
-                if (++spin >= kLinkSpin) ok = false;
-                __builtin_amdgcn_s_sleep(2);
-                if (tn[0] >= 0) pcg = ld_sc1(&link->commits[want % kLinkSlots][lane]);
-            }
-            if (lane == 0) s_ok = ok;
-        }
-    } else if (threadIdx.x == 0) {
+    // pop seq-1's write-back, which follows seq-2's (relaxed sc1 poll; every
+    // load of their rows below is sc1); its candidates on final rows
+    if (threadIdx.x == 0) {
         bool ok = s_ok;
         long spin = 0;
         while (ok && (int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0) {
@@ -763,86 +580,40 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const bool ok = s_ok;
     if (wave == 0) {
         KT e0 = 0;
-        uint32_t fb_prev = 0;  // FitDelta bits of the previous pops' candidates (left out of the sweep)
-        if (ok && tn[0] >= 0) {  // pop seq-1's candidates: rows into the cache, keys
-            Row r;
+        uint32_t fb_prev = 0;  // FitDelta bits of the previous pop's candidates (left out of the sweep)
+        if (ok && tn >= 0) {  // pop seq-1's candidates: rows into the cache, keys
+            const Row r = load_row_sc1(nc, tn);
             uint64_t pw[4] = {0, 0, 0, 0};
-            if (msg) {  // as pop seq-1 writes them back (no host ports in this class: the host checks)
-                const TaskClass& pc = t.classes[a.prev_cls];
-                r = apply_commits(mrow, pc, (int)((pcg >> 8) & 0xff), (int)(pcg & 0xff));
-            } else {
-                r = load_row_sc1(nc, tn[0]);
-                if (c.has_ports)
-                    for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn[0]);
-            }
+            if (c.has_ports)
+                for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn);
             rc.row[64 + lane] = r;
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;
-            rc_insert(&rc, tn[0], 64 + lane);
+            rc_insert(&rc, tn, 64 + lane);
             int32_t sc;
             bool passed;
-            e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn[0], pst, pna, &sc, &passed), a);
+            e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn, pst, pna, &sc, &passed), a);
             fb_prev = fit_bits(c, r, passed);
         }
-        KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
-#pragma unroll
-        for (int k = 1; k < kMaxDep; ++k) {  // older pops (overlap > 1): not cached
-            if (k >= ndep) break;
-            bool dup = false;  // a node among several pops' candidates counts once
-#pragma unroll
-            for (int j = 0; j < k; ++j)
-                for (uint64_t mm = __ballot(tn[j] >= 0); mm; mm &= mm - 1)
-                    dup = dup || tn[k] == __builtin_amdgcn_readlane(tn[j], __ffsll((unsigned long long)mm) - 1);
-            uint32_t fbk = 0;
-            const KT e = (ok && tn[k] >= 0 && !dup) ? sweep_key<KT>(eval_node_sc1(cf, c, t, nc, tn[k], &fbk), a)
-                                                     : (KT)0;
-            top = wave_merge_desc(top, wave_sort_desc(e));
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int cnt = __popcll(__ballot((fbk >> b) & 1u));
-                if (lane == b) s_fitin[b] += cnt;
-            }
-        }
+        const KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const int cnt = __popcll(__ballot((fb_prev >> b) & 1u));
             if (lane == b) s_fitin[b] += cnt;
         }
-        // this pop's candidates' rows before its commits (the next pop's rows message;
-        // drained before ready[seq], which the placement publishes after its round 0)
-        const int tnode = (ok && top) ? key_node(top, a) : -1;
-        if (tnode >= 0 && PLV != 4 && a.pub) {
-            const int sl = rc_find(&rc, tnode);  // -1: an older pop's node (overlap > 1, no rows message)
-            const Row& rr = rc.row[sl < 0 ? 0 : sl];
-            PopLinkRow* pr = &link->rows[seq % kLinkSlots][lane];
-            const int64_t v[13] = {rr.idle_cpu, rr.idle_mem, rr.idle_gpu, rr.rel_cpu, rr.rel_mem, rr.rel_gpu,
-                                   rr.bf_cpu, rr.bf_mem, rr.bf_gpu, rr.acpu, rr.amem, rr.nzc, rr.nzm};
-#pragma unroll
-            for (int k = 0; k < 13; ++k) st_sc1(&pr->v[k], v[k]);
-            st_sc1(&pr->pods, rr.pods);
-            st_sc1(&pr->maxtasks, rr.maxtasks);
-        }
         // this pop's candidates, one self-tagged granule each
+        const int tnode = (ok && top) ? key_node(top, a) : -1;
         st_sc1(&link->touched[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint32_t)tnode);
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
     if (ok) {
-        if constexpr (PLV == 4) {  // one-wave insertion: no barriers, depths only where they can matter
-            if (wave == 0) place_insert<true>(cf, nc, t, c, a, out, wl[0][lane], &link->done, seq, &rc, s_fitin, fit_raw);
-        } else if (a.ent32) {
-            place_parallel<uint32_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw,
-                                                      0, 0x7fffffff, 0, nullptr, a.pub ? link : nullptr, msg);
-        } else {
-            place_parallel<uint64_t, true, PLV == 5>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw,
-                                                      0, 0x7fffffff, 0, nullptr, a.pub ? link : nullptr, msg);
-        }
+        if (a.ent32)
+            place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+        else
+            place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
-        if (msg) {  // done stays monotonic: pop seq-1 publishes its own first
-            long spin = 0;
-            while ((int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0 && ++spin < kLinkSpin) __builtin_amdgcn_s_sleep(2);
-        }
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
@@ -915,33 +686,40 @@ hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int 
 
 // The walk's FitDelta histogram (allocate.go:164-167) of one task recomputed
 // on the current node state, which must be the state the task saw (the
-// walk's GetAccessibleResource visits already applied): chosen < 0 — the task
-// found no node, every walk node counts; else the walk stopped at node
-// `chosen` with kind chosen_kind: the walk nodes before it count (walk order
-// = key order without the fit bit), and `chosen` itself when Pipelined.
-// Classes without inter-pod priority terms (pod-affinity predicates are
-// evaluated on the current tables).  out4 is zeroed by the caller.
-__global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevTables t, int cls, int chosen,
-                                                      int chosen_kind, int32_t* out4) {
+// walk's GetAccessibleResource visits already applied; the host undoes the
+// task's own commit around it).  The task's class, the inter-pod affinity
+// normalisation (ctrl->ipa_lo / ipa_hi[0], from k_ipa_minmax on that state)
+// and the fallback node are ctrl's task 0.  chosen < 0: the task found no
+// node, every walk node counts; else the walk stopped at node `chosen` with
+// kind chosen_kind: the walk nodes before it count (walk order = key order
+// without the fit bit, ctrl->slot[0] = the chosen node's walk key from
+// k_fit_key, all-reduced over shards), and `chosen` itself when Pipelined.
+// out4 (zeroed by the caller) gets this shard's counts.
+__device__ __forceinline__ uint64_t fit_walk_key(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                                 const PopCtrl* ctrl, const TaskClass& c, int n) {
+    int32_t s = 0;
+    bool passed = false;
+    (void)eval_node_aff(cf, c, t, nc, n, ctrl->ipa_lo[0], ctrl->ipa_hi[0], ctrl->fallback, &s, &passed);
+    return passed ? pack_key(s, n + nc.base, 0) : 0;
+}
+__global__ __launch_bounds__(64) void k_fit_key(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl, int chosen) {
+    if (threadIdx.x != 0) return;
+    const TaskClass c = t.classes[ctrl->cls[0]];
+    const int n = chosen - nc.base;
+    ctrl->slot[0] = (n >= 0 && n < nc.n) ? fit_walk_key(cf, nc, t, ctrl, c, n) : 0;
+}
+__global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
+                                                      int chosen, int chosen_kind, int32_t* out4) {
     __shared__ int32_t s_fit[4];
     if (threadIdx.x < 4) s_fit[threadIdx.x] = 0;
     __syncthreads();
-    const TaskClass c = t.classes[cls];
-    uint64_t wk = 0;  // walk-order key of the chosen node
-    if (chosen >= 0) {
-        int32_t s = 0;
-        bool passed = false;
-        (void)eval_node_aff(cf, c, t, nc, chosen - nc.base, 0, 0, -1, &s, &passed);
-        wk = pack_key(s, chosen, 0);
-    }
+    const TaskClass c = t.classes[ctrl->cls[0]];
+    const uint64_t wk = ctrl->slot[0];  // walk-order key of the chosen node
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
-        int32_t s = 0;
-        bool passed = false;
-        (void)eval_node_aff(cf, c, t, nc, n, 0, 0, -1, &s, &passed);
+        const uint64_t k = fit_walk_key(cf, nc, t, ctrl, c, n);
         Row r = load_row(nc, n);
         r.bf_cpu = r.bf_mem = r.bf_gpu = 0;  // Idle as the walk left it
-        const bool in = passed && (chosen < 0 || pack_key(s, n + nc.base, 0) > wk ||
-                                   (n + nc.base == chosen && chosen_kind == 2));
+        const bool in = k && (chosen < 0 || k > wk || (n + nc.base == chosen && chosen_kind == 2));
         const uint32_t fb = in ? fit_bits(c, r, true) : 0u;
         for (int b = 0; b < 4; ++b)
             if ((fb >> b) & 1u) atomicAdd(&s_fit[b], 1);
@@ -950,11 +728,16 @@ __global__ __launch_bounds__(kBlock) void k_fit_delta(Conf cf, NodeCols nc, DevT
     if (threadIdx.x < 4 && s_fit[threadIdx.x]) atomicAdd(&out4[threadIdx.x], s_fit[threadIdx.x]);
 }
 
-hipError_t launch_fit_delta(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int chosen,
+hipError_t launch_fit_key(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int chosen,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(k_fit_key, dim3(1), dim3(64), 0, st, cf, nc, t, ctrl, chosen);
+    return hipGetLastError();
+}
+hipError_t launch_fit_count(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int chosen,
                             int chosen_kind, int32_t* out4, hipStream_t st) {
     const int grid = (nc.n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_fit_delta, dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, st, cf, nc, t, cls, chosen,
-                       chosen_kind, out4);
+    hipLaunchKernelGGL(k_fit_delta, dim3(grid > 0 ? grid : 1), dim3(kBlock), 0, st, cf, nc, t, (const PopCtrl*)ctrl,
+                       chosen, chosen_kind, out4);
     return hipGetLastError();
 }
 
@@ -972,31 +755,11 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
     return hipGetLastError();
 }
 
-// Nodes per block slot of the overlapped pop kernel (KBHIP_POP_NPB, a multiple
-// of 64 up to kPopThreads; tuning experiments), and its grid.
-int pop_npb() {
-    static const int v = [] {
-        const char* e = std::getenv("KBHIP_POP_NPB");
-        const int x = e ? std::atoi(e) : kPopThreads;
-        return (x >= 64 && x <= kPopThreads && x % 64 == 0) ? x : kPopThreads;
-    }();
-    return v;
-}
-int pop_blocks_ov(int n_nodes, int* R_out) {
-    const int nb = pop_blocks(n_nodes, R_out);
-    if (*R_out != 1) return nb;
-    const int npb = pop_npb();
-    return (n_nodes + npb - 1) / npb;
-}
-
+// Grid of the batched pop kernels: nodes per lane R (a power of two, 1 up
+// to 262k nodes) so that the block lists stay few enough for the merge tree.
 int pop_blocks(int n_nodes, int* R_out) {
-    static const int forced = [] {  // KBHIP_POP_R: nodes per lane (tuning experiments only)
-        const char* e = std::getenv("KBHIP_POP_R");
-        return e ? std::atoi(e) : 0;
-    }();
     int R = 1;
     while ((int64_t)kPopThreads * R * 512 < n_nodes && R < 16) R <<= 1;
-    if (forced == 1 || forced == 2 || forced == 4 || forced == 8 || forced == 16) R = forced;
     *R_out = R;
     return (n_nodes + kPopThreads * R - 1) / (kPopThreads * R);
 }
@@ -1009,12 +772,10 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
 #define KBHIP_PB(RR)                                                   \
     do {                                                               \
         switch (a.placement) {                                         \
-            case 2: KBHIP_PB1(RR, 2); break;                           \
             case 3: KBHIP_PB1(RR, 3); break;                           \
-            case 5: KBHIP_PB1(RR, 5); break;                           \
             case 6: KBHIP_PB1(RR, 6); break;                           \
             case 7: KBHIP_PB1(RR, 7); break;                           \
-            default: KBHIP_PB1(RR, -1); break;                         \
+            default: KBHIP_PB1(RR, 2); break;                          \
         }                                                              \
     } while (0)
     switch (R) {
@@ -1159,33 +920,27 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
     __syncthreads();
     NodeCols ncg = nc;  // keys / entries carry global node indices
     ncg.base = 0;
-    if (a.placement == 4) {
-        if (wave == 0) place_insert<false>(cf, ncg, t, c, a, out, wl[0][lane], nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
-    } else if (a.placement == 5) {
-        if (a.ent32) place_parallel<uint32_t, false, true>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
-        else place_parallel<uint64_t, false, true>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
-    } else if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
+    if (a.ent32) place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
     else place_parallel<uint64_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
 }
 
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, int placement) {
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st) {
     if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, (placement == 4 || placement == 5) ? placement : 2,
-              kf.base, kf.shift, kf.idxmax,
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, 0};
     hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev);
     return hipGetLastError();
 }
 
-template <typename KT, int PLV>
+template <typename KT>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
-                                  uint32_t seq, int ndep, hipStream_t st) {
+                                  uint32_t seq, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT, PLV>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, \
-                       o, link, seq, ndep)
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
+                       link, seq)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1199,31 +954,15 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int ndep, int fit_set, int placement, int prev_cls, bool pub) {
-    if (ndep < 1 || ndep > kMaxDep) return hipErrorInvalidValue;
+                               uint32_t seq, int fit_set) {
+    if (seq < 1) return hipErrorInvalidValue;
     int R;
-    const int nb = pop_blocks_ov(nc.n, &R);
-    const int plv = placement == 5 || placement == 4 ? placement : 2;
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, plv, kf.base, kf.shift, kf.idxmax,
+    const int nb = pop_blocks(nc.n, &R);
+    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
-    // rows hand-off (PopArgs::msg): one previous pop in flight, placed by place_parallel
-    // (it publishes the rows message), and no host-port words in this class
-    a.pub = pub && ndep == 1 && plv != 4;
-    a.npb = R == 1 ? pop_npb() : kPopThreads;
-    if (prev_cls >= 0 && a.pub) {
-        a.msg = 1;
-        a.prev_cls = prev_cls;
-    }
     PopOut* o = (PopOut*)out_dev;
-#define KBHIP_OVP(KT)                                                                                       \
-    switch (plv) {                                                                                          \
-        case 5: launch_pop_batch_ov_t<KT, 5>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
-        case 4: launch_pop_batch_ov_t<KT, 4>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
-        default: launch_pop_batch_ov_t<KT, 2>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, ndep, st); break; \
-    }
-    if (kf.use32) { KBHIP_OVP(uint32_t); }
-    else { KBHIP_OVP(uint64_t); }
-#undef KBHIP_OVP
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
     return hipGetLastError();
 }
 

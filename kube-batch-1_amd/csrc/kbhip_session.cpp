@@ -139,7 +139,7 @@ struct HJob {  // session jobs are numbered in UID order
     bool maybe_pending = false;  // had a Pending non-BestEffort task at open (a superset of "has one now")
     int cnt_alloc = 0, cnt_aob = 0;
     int32_t fit[4] = {0, 0, 0, 0};  // NodesFitDelta of its last task that ended a pop unplaced / not ready:
-    bool fit_exact = true;          // walk nodes, negative cpu / memory / GPU deltas (JobInfo.FitError)
+                                    // walk nodes, negative cpu / memory / GPU deltas (JobInfo.FitError)
     F3 drf_alloc;
     double drf_share = 0;
 };
@@ -282,38 +282,6 @@ class MemPool {
         std::lock_guard<std::mutex> lk(mu_);
         streams_.emplace(dev, st);
     }
-    // A stream on a hardware queue of its own: created with a CU mask (a queue
-    // property, so the runtime never shares it with other streams, whose
-    // queues it round-robins once GPU_MAX_HW_QUEUES are in use).  The
-    // persistent placer runs there: a resident kernel on a shared queue would
-    // hold back every launch queued behind it.
-    hipStream_t take_own_queue_stream() {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        if (!off_) {
-            std::lock_guard<std::mutex> lk(mu_);
-            auto it = own_streams_.find(dev);
-            if (it != own_streams_.end()) {
-                hipStream_t st = it->second;
-                own_streams_.erase(it);
-                return st;
-            }
-        }
-        uint32_t mask[8] = {0xffu, 0, 0, 0, 0, 0, 0, 0};  // 8 CUs: the placer is one workgroup
-        hipStream_t st = nullptr;
-        if (hipExtStreamCreateWithCUMask(&st, 8, mask) != hipSuccess)
-            throw Error(KBHIP_ENODEV, "hipExtStreamCreateWithCUMask failed");
-        return st;
-    }
-    void give_own_queue_stream(hipStream_t st, int dev) {
-        if (!st) return;
-        if (off_) {
-            (void)hipStreamDestroy(st);
-            return;
-        }
-        std::lock_guard<std::mutex> lk(mu_);
-        own_streams_.emplace(dev, st);
-    }
     void trim() {
         std::lock_guard<std::mutex> lk(mu_);
         for (auto& kv : free_) release((Kind)std::get<1>(kv.first), kv.second);
@@ -330,7 +298,7 @@ class MemPool {
     static constexpr size_t kCap = size_t(8) << 30;
     std::mutex mu_;
     std::multimap<std::tuple<int, int, size_t>, void*> free_;
-    std::multimap<int, hipStream_t> streams_, own_streams_;
+    std::multimap<int, hipStream_t> streams_;
     size_t cached_ = 0;
     const bool off_;
 };
@@ -458,32 +426,6 @@ struct Session {
     uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
-    // option "ov_msg" (default 0): an overlapped pop rebuilds the previous pop's
-    // written rows from its rows message + commit granules (PopArgs::msg) when
-    // that pop was the last device work on the node rows (ov_msg_ok: cleared by
-    // ov_drain, which every other kind of device work goes through first).
-    // Exact (parity-tested) but measured slower at C4 (period 14.2 vs 12.8 us,
-    // profiles/r02_ab_ovmsg.json): the rows-message drain and the tail wait
-    // for the previous write-back lengthen each kernel, whose end the next
-    // sweep on its stream waits for.
-    bool ov_msg = false;
-    bool ov_msg_ok = false;
-    int ov_prev_cls = -1;
-    // persistent placer (kbhip_pp.hip): option "pp"; used by kbhip_allocate's pop loop
-    int pp = 0;                 // off by default: per pop it measured slower than the overlapped kernel
-                                // (C4-scaled 16.8 vs 12.5 us; profiles/r02_pp_profile.txt)
-    bool pp_active = false;     // inside Allocator::run
-    bool pp_running = false;    // a placer was launched and has not been stopped
-    bool pp_skip = false;       // the next batched launch goes without the placer (after a pop it could not start)
-    uint32_t pp_seq = 0;        // last command posted
-    uint32_t pp_next_stream = 0;
-    hipStream_t pp_stream = nullptr;
-    DevBuf b_pp_ring, b_pp_ctrl, b_pp_lists, b_pp_arrive, b_pp_fitw;
-    uint32_t* h_pp = nullptr;   // pinned, mapped: [0] command the placer stopped at, [1] exited
-    void* d_pp = nullptr;
-    size_t h_pp_cap = 0;
-    size_t pp_list_stride = 0;  // keys per ring slot
-    int64_t pp_fitw_words = 0;  // nibble words per ring slot
     int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
     bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
     DevBuf b_fit4;
@@ -525,7 +467,6 @@ struct Session {
     vector<uint64_t> dbg_keys;  // rows of 2 npad + 4: keys, raw ipa counts, ipa lo, ipa hi, fallback, max key
     vector<int32_t> dbg_pods;
     bool batched = true;
-    int placement = 2;  // batched chunk placement: 0 sequential loop, 1 running-min levels, 2 parallel levels (default)
     int64_t time_every = 0;       // time every k-th sweep launch with HIP events (0 = off)
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -557,12 +498,6 @@ struct Session {
     // Device side of the teardown: drain the streams, then hand streams, pinned
     // and device buffers back to the pool.  Idempotent.
     void release_device() {
-        if (pp_running && stream) {  // the placer leaves on a STOP command (or 20 ms without one)
-            (void)launch_pp_stop(b_pp_ring.p, ++pp_seq, stream);
-            (void)hipStreamSynchronize(pp_stream);
-            pp_running = false;
-        }
-        if (pp_stream) (void)hipStreamSynchronize(pp_stream);
         for (int k = 1; k <= kMaxDep; ++k)
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -580,11 +515,6 @@ struct Session {
         if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
         if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
-        if (h_pp) MemPool::get().give(MemPool::kPinnedMapped, h_pp, h_pp_cap, device);
-        h_pp = nullptr;
-        MemPool::get().give_own_queue_stream(pp_stream, device);
-        pp_stream = nullptr;
-        for (DevBuf* b : {&b_pp_ring, &b_pp_ctrl, &b_pp_lists, &b_pp_arrive, &b_pp_fitw}) b->release();
         h_rank = nullptr;
         h_ctrl = nullptr;
         h_out = nullptr;
@@ -1556,15 +1486,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         S.d_cand2 = S.b_cand2.alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
         S.d_arrive = S.b_arrive.alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
         HIPCHK(hipMemsetAsync(S.d_arrive, 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
-        S.d_fit4 = S.b_fit4.alloc<int32_t>(4);
+        S.d_fit4 = S.b_fit4.alloc<int32_t>(4 + 8);  // device counters + an int64[4] exchange slot
         if (S.world > 1) {
             S.d_shard_send = S.b_shard_send.alloc<ShardMsg>(1);
             S.d_shard_recv = S.b_shard_recv.alloc<ShardMsg>(S.world);
         }
-        int R3;
-        const int nb3 = std::max(nb2, pop_blocks_ov(nl, &R3));
         for (int k = 0; k <= kMaxDep; ++k) {
-            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb3, 1) + kMaxGroups) * 64);
+            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
             S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
             HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
@@ -1595,27 +1523,40 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 }
 
 // ---------------------------------------------------------------------------
-// cross-shard exchange of one 8-byte value in device memory:
+// cross-shard exchange of n 8-byte values in device memory:
 // RCCL all-reduce on the session stream, or a host round trip through the
 // caller's callback (tests: several ranks sharing one GPU over gloo).
 // ---------------------------------------------------------------------------
-static void exchange(Session& S, void* dev, int op) {
+static void exchange(Session& S, void* dev, int op, int n = 1) {
     if (S.world == 1) return;
     S.stats.collectives++;
     if (S.comm) {
         const ncclDataType_t dt = op == KBHIP_RED_MAX_U64 ? ncclUint64 : ncclInt64;
-        const ncclRedOp_t ro = op == KBHIP_RED_MIN_I64 ? ncclMin : ncclMax;
-        const ncclResult_t r = ncclAllReduce(dev, dev, 1, dt, ro, S.comm, S.stream);
+        const ncclRedOp_t ro = op == KBHIP_RED_MIN_I64 ? ncclMin : op == KBHIP_RED_SUM_I64 ? ncclSum : ncclMax;
+        const ncclResult_t r = ncclAllReduce(dev, dev, n, dt, ro, S.comm, S.stream);
         if (r != ncclSuccess) throw Error(KBHIP_EDEVICE, string("ncclAllReduce: ") + ncclGetErrorString(r));
         return;
     }
     if (!S.xfn) throw Error(KBHIP_EINVAL, "sharded session is not connected (kbhip_shard_connect_*)");
-    uint64_t v = 0;
-    HIPCHK(hipMemcpyAsync(&v, dev, 8, hipMemcpyDeviceToHost, S.stream));
+    uint64_t v[8];
+    if (n < 1 || n > 8) throw Error(KBHIP_EINVAL, "exchange of more than 8 values");
+    HIPCHK(hipMemcpyAsync(v, dev, 8 * (size_t)n, hipMemcpyDeviceToHost, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
-    if (S.xfn(S.xctx, &v, 1, op) != 0) throw Error(KBHIP_EDEVICE, "shard exchange callback failed");
-    HIPCHK(hipMemcpyAsync(dev, &v, 8, hipMemcpyHostToDevice, S.stream));
+    if (S.xfn(S.xctx, v, n, op) != 0) throw Error(KBHIP_EDEVICE, "shard exchange callback failed");
+    HIPCHK(hipMemcpyAsync(dev, v, 8 * (size_t)n, hipMemcpyHostToDevice, S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
+}
+
+// The FitDelta counts of one task summed over the shards (in place; one GPU: nothing).
+static void fit_allreduce(Session& S, int32_t* fit4) {
+    if (S.world == 1) return;
+    int64_t* d = (int64_t*)S.d_fit4 + 2;  // after the device counters (int32[4])
+    int64_t h[4] = {fit4[0], fit4[1], fit4[2], fit4[3]};
+    HIPCHK(hipMemcpyAsync(d, h, sizeof h, hipMemcpyHostToDevice, S.stream));
+    exchange(S, d, KBHIP_RED_SUM_I64, 4);
+    HIPCHK(hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    for (int q = 0; q < 4; ++q) fit4[q] = (int32_t)h[q];
 }
 
 // The all-gather of a batched pop on a node-array shard: every rank's
@@ -1672,8 +1613,6 @@ struct BatchLaunch {
     bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
     bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
     bool aff = false;  // placement 7 (pod-affinity class): may end before its first task (n_done 0)
-    bool pp = false;   // through the persistent placer: may end before its first task (n_done 0)
-    uint32_t pp_seq = 0;
 };
 
 // ---------------------------------------------------------------------------
@@ -1858,87 +1797,15 @@ struct RankGroupScope {
 
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
-    S.ov_msg_ok = false;
     if (!S.ov_pending) return;
     for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
     S.ov_pending = false;
 }
 
-// ---------------------------------------------------------------------------
-// persistent placer (kbhip_pp.hip): commands are numbered from 1 in the
-// session (PPCtrl::written counts them); a run of kbhip_allocate's batched
-// pops posts one sweep per pop, the placer (launched at the run's first pop)
-// places them in order; the run ends with a STOP.
-// ---------------------------------------------------------------------------
-static void pp_init(Session& S) {
-    if (S.b_pp_ring.p) return;
-    const int Q = pp_slots();
-    S.b_pp_ring.alloc<uint8_t>(pp_slot_bytes() * Q);
-    S.b_pp_ctrl.alloc<uint8_t>(pp_ctrl_bytes());
-    S.pp_list_stride = pp_list_keys(S.nc.n);
-    S.b_pp_lists.alloc<uint64_t>(S.pp_list_stride * Q);
-    S.b_pp_arrive.alloc<uint32_t>(pp_arrive_words() * Q);
-    S.pp_fitw_words = (S.nc.n + 7) / 8 + 1;
-    S.b_pp_fitw.alloc<uint32_t>((size_t)S.pp_fitw_words * Q);
-    HIPCHK(hipMemsetAsync(S.b_pp_ring.p, 0, pp_slot_bytes() * Q, S.stream));
-    HIPCHK(hipMemsetAsync(S.b_pp_ctrl.p, 0, pp_ctrl_bytes(), S.stream));
-    HIPCHK(hipMemsetAsync(S.b_pp_arrive.p, 0, pp_arrive_words() * Q * sizeof(uint32_t), S.stream));
-    HIPCHK(hipStreamSynchronize(S.stream));
-    S.h_pp = (uint32_t*)MemPool::get().take(MemPool::kPinnedMapped, pp_host_bytes(), &S.h_pp_cap);
-    std::memset(S.h_pp, 0, pp_host_bytes());
-    HIPCHK(hipHostGetDevicePointer(&S.d_pp, S.h_pp, 0));
-    S.pp_stream = MemPool::get().take_own_queue_stream();
-}
-// Launch the placer at command seq0; fresh: no command before seq0 is in
-// flight (every row is in memory), so the progress counter is set to seq0 - 1.
-static void pp_launch(Session& S, uint32_t seq0, bool fresh) {
-    if (fresh) {
-        const uint32_t w = seq0 - 1;
-        HIPCHK(hipMemcpyAsync(S.b_pp_ctrl.p, &w, sizeof(w), hipMemcpyHostToDevice, S.stream));
-        HIPCHK(hipStreamSynchronize(S.stream));
-    }
-    __atomic_store_n(&S.h_pp[1], 0u, __ATOMIC_RELEASE);
-    HIPCHK(launch_pp_placer(S.conf, S.nc, S.tab, S.b_pp_ring.p, S.b_pp_ctrl.p, S.d_out, (const uint32_t*)S.b_pp_fitw.p,
-                            S.pp_fitw_words, S.d_pp, seq0, S.pp_stream));
-    S.pp_running = true;
-}
-static void pp_stop(Session& S) {
-    if (!S.pp_running) return;
-    const uint32_t e = ++S.pp_seq;
-    HIPCHK(launch_pp_stop(S.b_pp_ring.p, e, S.stream));
-    HIPCHK(hipStreamSynchronize(S.pp_stream));  // the placer left (at this STOP, or idle before it)
-    for (int k = 0; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
-    S.pp_running = false;
-    static const bool prof = std::getenv("KBHIP_PP_PROFILE") != nullptr;  // development aid
-    if (prof) {
-        uint64_t pr[8];
-        HIPCHK(hipMemcpy(pr, (char*)S.b_pp_ctrl.p + 64, sizeof(pr), hipMemcpyDeviceToHost));
-        const double n = pr[6] ? (double)pr[6] : 1.0;
-        std::fprintf(stderr, "pp: %llu pops, us/pop wait %.2f list+dirty %.2f keys+merge %.2f rows %.2f place %.2f tail %.2f\n",
-                     (unsigned long long)pr[6], pr[0] / n / 100, pr[1] / n / 100, pr[2] / n / 100, pr[3] / n / 100,
-                     pr[4] / n / 100, pr[5] / n / 100);
-        uint64_t pp[16];
-        HIPCHK(hipMemcpy(pp, (char*)S.b_pp_ctrl.p + 128, sizeof(pp), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "pp place: us/pop");
-        for (int k = 1; k <= 9; ++k) std::fprintf(stderr, " [%d] %.2f", k, pp[k] / n / 100);
-        std::fprintf(stderr, "\n");
-        HIPCHK(hipMemset((char*)S.b_pp_ctrl.p + 64, 0, sizeof(pr) + sizeof(pp)));
-    }
-}
-// The placer left idle while command e was outstanding: start it again there.
-static void pp_revive(Session& S) {
-    if (!S.pp_running || !__atomic_load_n(&S.h_pp[1], __ATOMIC_ACQUIRE)) return;
-    HIPCHK(hipStreamSynchronize(S.pp_stream));
-    pp_launch(S, __atomic_load_n(&S.h_pp[0], __ATOMIC_ACQUIRE), false);
-}
-
 // Wait until no batched pop can still run (before device work that is not a
-// batched pop, which neither the overlap chain nor the placer orders).
-static void ov_quiesce(Session& S) {
-    pp_stop(S);
-    ov_drain(S);
-}
+// batched pop, which the overlap chain does not order).
+static void ov_quiesce(Session& S) { ov_drain(S); }
 
 // Nothing but the winner's row can change between the chunk's tasks: the
 // condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
@@ -1992,36 +1859,8 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     }
     L.bf = S.any_bf != 0;
     L.aff = !L.bf && S.classes[cls].aff;
-    L.pp = S.pp_active && S.pp && !S.pp_skip && S.placement >= 2 && S.world == 1 && !L.bf && !L.aff;
-    S.pp_skip = false;
-    if (L.pp) {  // one sweep per pop, any stream; the resident placer places them in order
-        ov_drain(S);
-        if (S.nonov_pending) {  // a non-overlapped batched pop may still run on stream 0
-            HIPCHK(hipStreamSynchronize(S.stream));
-            S.nonov_pending = false;
-        }
-        pp_init(S);
-        if (!S.pp_running) pp_launch(S, S.pp_seq + 1, true);
-        const uint32_t e = ++S.pp_seq;
-        L.pp_seq = e;
-        const int Q = pp_slots();
-        L.st = S.ov_streams[S.pp_next_stream++ % (kMaxDep + 1)];
-        L.fit = true;
-        auto tl0 = std::chrono::steady_clock::now();
-        if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
-        const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
-        HIPCHK(launch_pp_sweep(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
-                               S.b_pp_ring.p, (uint64_t*)S.b_pp_lists.p + (e % Q) * S.pp_list_stride,
-                               (uint32_t*)S.b_pp_arrive.p + (e % Q) * pp_arrive_words(),
-                               (uint32_t*)S.b_pp_fitw.p + (e % Q) * S.pp_fitw_words, S.b_pp_ctrl.p, e,
-                               (uint32_t)L.slot, L.st));
-        if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));
-        S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0).count();
-        return L;
-    }
-    const bool ov = S.overlap > 0 && S.placement >= 2 && S.world == 1 && !L.bf && !L.aff;
+    const bool ov = S.overlap > 0 && S.world == 1 && !L.bf && !L.aff;
     if (!ov) ov_quiesce(S);
-    else pp_stop(S);
 
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
@@ -2034,7 +1873,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         for (int k = 0; k <= S.overlap; ++k) HIPCHK(hipStreamWaitEvent(S.ov_streams[k], S.ev_nonov, 0));
         S.nonov_pending = false;
     }
-    L.fit = !L.bf && !L.aff && (S.placement >= 2 || S.world > 1);
+    L.fit = !L.bf && !L.aff;
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
@@ -2046,16 +1885,10 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.fit_set[kMaxDep + 1] ^= 1;
         shard_gather(S);
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
-                                  S.d_shard_recv, S.world, out, S.stream, S.placement));
+                                  S.d_shard_recv, S.world, out, S.stream));
     } else if (ov) {
-        const int prev = (S.ov_msg && S.ov_msg_ok && S.overlap == 1 && !S.classes[cls].has_ports && S.ov_prev_cls >= 0)
-                             ? S.ov_prev_cls : -1;
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
-                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.overlap,
-                                   S.fit_set[si], S.placement, prev, S.ov_msg && S.overlap == 1));
-        if (prev >= 0 && S.placement != 4) S.stats.msg_pops++;
-        S.ov_prev_cls = cls;
-        S.ov_msg_ok = true;
+                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.fit_set[si]));
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
@@ -2076,7 +1909,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.stats.pop_batch_sum += r.batch;
     } else {
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
-                                S.d_arrive, out, S.stream, L.bf ? 6 : L.aff ? 7 : S.placement, kf,
+                                S.d_arrive, out, S.stream, L.bf ? 6 : L.aff ? 7 : 2, kf,
                                 S.fit_set[kMaxDep + 1]));
         S.fit_set[kMaxDep + 1] ^= 1;
         if (S.overlap > 0) {
@@ -2108,10 +1941,6 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
             while (got < n_done && tag(load(got)) == L.epoch) ++got;
             if (got == n_done) break;
         }
-        if (L.pp && (spin & 4095) == 4095 && __atomic_load_n(&S.h_pp[1], __ATOMIC_ACQUIRE)) {
-            pp_revive(S);  // the placer left idle before this pop's sweep was posted
-            spin = 0;
-        }
         if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(L.st));  // long waits: runtime
         if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
         __builtin_ia32_pause();
@@ -2119,7 +1948,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
     S.stats.sweeps += 1;
     S.stats.batched_pops += 1;
-    if (n_done < (L.bf || L.aff || L.pp ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
+    if (n_done < (L.bf || L.aff ? 0 : 1) || n_done > L.m) throw Error(KBHIP_EDEVICE, "batched pop returned a bad task count");
     for (int j = 0; j < n_done; ++j) {
         const uint64_t g = load(j);
         res_node[j] = (int32_t)(g & 0xffffffffu) - 1;
@@ -2127,13 +1956,6 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     }
     *n_done_out = n_done;
     *stop_out = (int)((load(0) >> 44) & 0xf) - 1;
-    static const bool ppdbg = std::getenv("KBHIP_PP_DEBUG") != nullptr;  // development aid
-    if (ppdbg) {
-        std::fprintf(stderr, "launch pp %d seq %u cls %d m %d done %d stop %d:", (int)L.pp, L.pp_seq, L.cls, L.m, n_done,
-                     *stop_out);
-        for (int j = 0; j < n_done; ++j) std::fprintf(stderr, " %d/%d", res_node[j], res_kind[j]);
-        std::fprintf(stderr, "\n");
-    }
     S.last_fit_ok = false;
     if (*stop_out == KBHIP_STOP_UNASSIGNED && L.fit) {
         uint64_t f0 = 0, f1 = 0;
@@ -2181,7 +2003,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
         S.phase[7] += (P[3] - P[2]) * 0.01;        // write back
         S.phase[8] += (P[3] - t0) * 0.01;          // total in-kernel span
         S.phase[9] += L.m;
-        if (P[5] && P[6] && P[7] && S.placement == 2) {  // parallel-levels sub-phases
+        if (P[5] && P[6] && P[7]) {  // parallel-levels sub-phases
             S.phase[10] += (P[5] - P[1]) * 0.01;   // candidate rows loaded
             S.phase[11] += (P[6] - P[5]) * 0.01;   // round-0 depth evaluation
             S.phase[12] += (P[7] - P[6]) * 0.01;   // round-0 sort + merge
@@ -2280,11 +2102,6 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             // one launch: sweep + per-block top-64 + merge + placement of the chunk
             const BatchLaunch L = launch_batched(S, cls0, m, gang_mode, min_avail, ready_count);
             collect_batched(S, L, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf);
-            if (n_done == 0 && L.pp) {  // the placer could not start this chunk: once more without it
-                S.stats.pp_retries++;
-                S.pp_skip = true;
-                continue;
-            }
             if (n_done == 0) {  // placement 6 / 7 could not place the first task exactly: general path for it
                 batch = false;
                 m = 1;
@@ -2342,9 +2159,11 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             }
             n_done = h.n_done;
             stop_c = h.stop;
-            S.last_fit_ok = stop_c == KBHIP_STOP_UNASSIGNED && S.world == 1 && n_done >= 1;
-            if (S.last_fit_ok)
+            S.last_fit_ok = stop_c == KBHIP_STOP_UNASSIGNED && n_done >= 1;
+            if (S.last_fit_ok) {  // this shard's counts of the walk of the task that found no node
                 for (int q = 0; q < 4; ++q) S.last_fit[q] = h.fit[n_done - 1][q];
+                fit_allreduce(S, S.last_fit);
+            }
             ready_c = h.ready_count;
             any_bf_c = h.any_bf;
             res_node = h.res_node;
@@ -2677,7 +2496,6 @@ struct Allocator {
         const int gm = S.gang_ready ? 1 : 0;
         if (!S.ev_run[0]) { HIPCHK(hipEventCreate(&S.ev_run[0])); HIPCHK(hipEventCreate(&S.ev_run[1])); }
         ov_quiesce(S);
-        S.pp_active = S.world == 1;
         HIPCHK(hipEventRecord(S.ev_run[0], S.stream));
         auto build_pending = [&](HJob& job) {  // allocate.go:91-104; TaskOrderFn is a strict total order
             if (job.pending_built) return;
@@ -2847,24 +2665,47 @@ struct Allocator {
         };
         // The walk FitDelta histogram of a pop's last task when the kernels did
         // not report it (a pop that placed every pending task and left its job
-        // not Ready; placement modes 0/1): recomputed on the device state that
-        // task saw — queued predictions retracted, its own commit undone and
-        // redone around k_fit_delta.
+        // not Ready): recomputed on the device state that task saw — queued
+        // predictions retracted, its own commit undone and redone around the
+        // recount (k_fit_key / k_fit_delta), the fallback node as it was before
+        // that commit, and for a class with inter-pod priority terms the
+        // score's min / max prepass on that state.  Shards: the chosen node's
+        // walk key (its owner computes it) and the counts are all-reduced.
         auto fit_sync = [&](int cls, int node, int kind, HJob& job) {
             discard_all();
             ov_quiesce(S);
-            if (S.world != 1 || S.classes[cls].ipa_n) {  // not covered: shards, inter-pod priority classes
-                job.fit_exact = false;
-                S.stats.fit_inexact++;
-                return;
-            }
             const int32_t nd[1] = {node}, kd[1] = {kind};
-            if (node >= 0) HIPCHK(launch_undo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
+            if (node >= 0) {
+                HIPCHK(launch_undo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
+                sess_placed(S, node, -1);  // the fallback node the task saw
+            }
+            PopCtrl& h = *S.h_ctrl;
+            h.stop = -1;
+            h.n_done = 0;
+            h.n_tasks = 1;
+            h.mode = 0;
+            h.any_bf = S.any_bf;
+            h.fallback = S.fallback;
+            h.cls[0] = cls;
+            h.ipa_lo[0] = h.ipa_hi[0] = 0;
+            h.slot[0] = 0;
+            HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+            if (node >= 0) sess_placed(S, node, +1);
+            if (S.classes[cls].ipa_n > 0) {
+                HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
+                exchange(S, &S.d_ctrl->ipa_lo[0], KBHIP_RED_MIN_I64);
+                exchange(S, &S.d_ctrl->ipa_hi[0], KBHIP_RED_MAX_I64);
+            }
+            if (node >= 0) {
+                HIPCHK(launch_fit_key(S.conf, S.nc, S.tab, S.d_ctrl, node, S.stream));
+                exchange(S, &S.d_ctrl->slot[0], KBHIP_RED_MAX_U64);
+            }
             HIPCHK(hipMemsetAsync(S.d_fit4, 0, 4 * sizeof(int32_t), S.stream));
-            HIPCHK(launch_fit_delta(S.conf, S.nc, S.tab, cls, node, kind, S.d_fit4, S.stream));
+            HIPCHK(launch_fit_count(S.conf, S.nc, S.tab, S.d_ctrl, node, kind, S.d_fit4, S.stream));
             if (node >= 0) HIPCHK(launch_redo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
             HIPCHK(hipMemcpyAsync(job.fit, S.d_fit4, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, S.stream));
             HIPCHK(hipStreamSynchronize(S.stream));
+            fit_allreduce(S, job.fit);
         };
         // One job pop through the device: the first chunk batched (possibly
         // already queued by speculation), the rest through place_job.
@@ -2961,7 +2802,6 @@ struct Allocator {
         }
         discard_all();  // predicted pops that never came
         ov_quiesce(S);
-        S.pp_active = false;
         ev_harvest_all(S);
         HIPCHK(hipEventRecord(S.ev_run[1], S.stream));
         HIPCHK(hipStreamSynchronize(S.stream));
@@ -3868,7 +3708,6 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
         j.cursor = 0;
         j.pending_built = false;
         for (int q = 0; q < 4; ++q) j.fit[q] = 0;
-        j.fit_exact = true;
         j.drf_alloc = F3{};
         j.drf_share = 0;
         j.priority = j.pg_priority;
@@ -4018,7 +3857,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
         else if (std::strcmp(key, "overlap") == 0) {
-            if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0..3");
+            if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0 or 1");
             if (!s->s.encode_only) {
                 HIPCHK(hipSetDevice(s->s.device));
                 kbhip::ov_quiesce(s->s);  // the stream rotation changes
@@ -4027,13 +3866,8 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
-        else if (std::strcmp(key, "ov_msg") == 0) {
-            s->s.ov_msg = value != 0;
-            s->s.ov_msg_ok = false;  // the previous pop may not have published its rows message
-        }
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
         else if (std::strcmp(key, "pop_group") == 0) s->s.pop_group = value != 0 && s->s.world == 1;
-        else if (std::strcmp(key, "pp") == 0) s->s.pp = value != 0;
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");
@@ -4045,10 +3879,6 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
                 HIPCHK(hipSetDevice(S.device));
                 S.d_dbg = S.b_dbg.alloc<uint64_t>((size_t)kbhip::kMaxChunk * (2 * S.nc.npad + 4));
             }
-        }
-        else if (std::strcmp(key, "placement") == 0) {
-            if (value < 0 || value > 5 || value == 3) throw kbhip::Error(KBHIP_EINVAL, "placement must be 0, 1, 2, 4 or 5");
-            s->s.placement = (int)value;
         }
         else throw kbhip::Error(KBHIP_EINVAL, string("unknown option ") + key);
         return KBHIP_OK;

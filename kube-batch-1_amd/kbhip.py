@@ -31,7 +31,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
            "kbhip_session_carry_events")
 
-RED_MAX_U64, RED_MIN_I64, RED_MAX_I64 = 0, 1, 2
+RED_MAX_U64, RED_MIN_I64, RED_MAX_I64, RED_SUM_I64 = 0, 1, 2, 3
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
                                 ctypes.c_int32)
 ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
@@ -48,10 +48,9 @@ class Stats(ctypes.Structure):
                 ("timed_launches", ctypes.c_int64), ("host_launch_s", ctypes.c_double),
                 ("host_wait_s", ctypes.c_double), ("spec_hits", ctypes.c_int64), ("spec_missed", ctypes.c_int64),
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
-                ("fit_inexact", ctypes.c_int64), ("collectives", ctypes.c_int64),
-                ("pp_retries", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
+                ("collectives", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
                 ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
-                ("pop_batch_sum", ctypes.c_int64), ("msg_pops", ctypes.c_int64)]
+                ("pop_batch_sum", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -376,7 +375,8 @@ def torch_exchange(group=None, device=None):
         t = torch.from_numpy(v)
         if device is not None:
             t = t.to(device)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN if op == RED_MIN_I64 else dist.ReduceOp.MAX, group=group)
+        rop = {RED_MIN_I64: dist.ReduceOp.MIN, RED_SUM_I64: dist.ReduceOp.SUM}.get(op, dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=rop, group=group)
         out = t.cpu().numpy()
         if op == RED_MAX_U64:
             out = out ^ np.int64(-0x8000000000000000)

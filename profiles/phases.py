@@ -11,10 +11,8 @@ if not os.path.exists(p):
     os.makedirs(os.path.dirname(p), exist_ok=True)
     kbgen.gen_c4(p)
 L = kbhip.lib()
-placement = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-overlap = int(sys.argv[2]) if len(sys.argv) > 2 else 0  # 1: the overlapped kernel, one pop at a time
+overlap = int(sys.argv[1]) if len(sys.argv) > 1 else 0  # 1: the overlapped kernel, one pop at a time
 with kbhip.Session(p) as s:
-    s.set_option("placement", placement)
     s.set_option("overlap", overlap)
     s.set_option("speculate", 0)  # stamps are read per launch
     s.allocate()
@@ -22,8 +20,8 @@ with kbhip.Session(p) as s:
     n = L.kbhip_debug_phases(s._h, out, 20)
     names = ["block sweep+sort", "block merge+store", "span to all block lists stored",
              "group merge tail to final start", "final merge", "chain precompute", "placement loop",
-             "write back", "kernel span", "tasks per launch", "pp: rows loaded", "pp: round-0 eval",
-             "pp: round-0 sort+merge", "wb: ranks+stop", "wb: LDS counts", "ov: wait for previous pop",
-             "ov: patch (eval previous candidates + merge)", "pp: rows fetched", "pp: LDS init + barrier"]
-    print(json.dumps({"pops": n, "placement": placement, "overlap": overlap, **{names[i]: round(out[i], 3) for i in range(len(names))}},
+             "write back", "kernel span", "tasks per launch", "placement: rows loaded", "placement: round-0 eval",
+             "placement: round-0 sort+merge", "wb: ranks+stop", "wb: LDS counts", "ov: wait for previous pop",
+             "ov: patch (eval previous candidates + merge)", "placement: rows fetched", "placement: LDS init + barrier"]
+    print(json.dumps({"pops": n, "overlap": overlap, **{names[i]: round(out[i], 3) for i in range(len(names))}},
                      indent=1))

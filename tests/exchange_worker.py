@@ -27,7 +27,7 @@ def main():
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     fn = kbhip.torch_exchange()
     keys, ints = values(rank)
-    res = {"max_u64": [], "min_i64": [], "max_i64": []}
+    res = {"max_u64": [], "min_i64": [], "max_i64": [], "sum_i64": []}
     for k in keys:
         v = np.array([k], dtype=np.uint64)
         fn(v, kbhip.RED_MAX_U64)
@@ -39,6 +39,10 @@ def main():
         v = np.array([x], dtype=np.int64).view(np.uint64)
         fn(v, kbhip.RED_MAX_I64)
         res["max_i64"].append(int(v.view(np.int64)[0]))
+    # several values per call, summed (the FitDelta counts of a walk over the shards)
+    v = ints.copy().view(np.uint64)
+    fn(v, kbhip.RED_SUM_I64)
+    res["sum_i64"] = [int(x) for x in v.view(np.int64)]
     # all-gather of a per-rank byte record (the batched shard path's ShardMsg exchange)
     g = kbhip.torch_gather()
     send = (np.arange(40, dtype=np.uint8) * (rank + 1)).astype(np.uint8)

@@ -25,11 +25,13 @@ def main():
         info = s.info()
         pod, node, kind = s.run_actions(actions)
         st = s.stats()
+        close = s.gang_unschedulable()
     dist.barrier()
     dist.destroy_process_group()
     with open(out, "w") as f:
         json.dump({"info": info, "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)],
-                   "batched_pops": st["batched_pops"], "sweeps": st["sweeps"], "collectives": st["collectives"]}, f)
+                   "batched_pops": st["batched_pops"], "sweeps": st["sweeps"], "collectives": st["collectives"],
+                   "close": close}, f)
 
 
 if __name__ == "__main__":

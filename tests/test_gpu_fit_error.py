@@ -4,14 +4,14 @@ unschedulable: <JobInfo.FitError>" for every job left not Ready — equal the
 oracle's (kbref: allocate.go:124-126 / 164-167, job_info.go:343-372,
 gang.go:166-187), on every device path: batched (in-kernel histogram, with and
 without overlapped pops), per task, and the synchronous fallback (placement
-modes 0/1, pops that place every task and stay not Ready)."""
+(pops that place every task and stay not Ready), for every class including
+those with inter-pod affinity priority terms.  Node-array shards are checked
+in tests/test_shard.py."""
 import pytest
 
 from test_gpu_parity import NO_POD_AFFINITY
 
-PATHS = [dict(), dict(overlap=0), dict(batched=0), dict(placement=1), dict(placement=0, overlap=0),
-         dict(speculate=0), dict(placement=4), dict(placement=4, overlap=0), dict(placement=5),
-         dict(placement=5, overlap=0)]
+PATHS = [dict(), dict(overlap=0), dict(batched=0), dict(speculate=0), dict(overlap=0, speculate=0)]
 
 
 def _engine_close(engine, path, **opts):
@@ -34,23 +34,42 @@ def test_fit_error_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
     exp = oracle_mod.ref_gang_close(p)
     for opts in PATHS:
         got, st = _engine_close(engine, p, **opts)
-        assert st["fit_inexact"] == 0
         assert got == exp, opts
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(40))
 def test_fit_error_full_features_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """Pod (anti-)affinity classes too (per-task path, in-kernel counts)."""
+    """Every feature, pod (anti-)affinity and inter-pod priority classes too
+    (per-task path: in-kernel counts; pops that leave their job not Ready:
+    the recount with the priority's min / max prepass on the task's state)."""
     c = kbgen_mod.gen_random(5300 + seed, n_nodes=4 + seed % 8, n_jobs=5 + seed % 7, max_tasks=2 + seed % 7)
     p = str(tmp_path / "ff.kbs")
     c.write(p)
     exp = oracle_mod.ref_gang_close(p)
-    got, st = _engine_close(engine, p)
-    if st["fit_inexact"] == 0:
-        assert got == exp
-    else:  # only the affinity-class fallback is not covered: every other job still matches
-        assert set(got) == set(exp)
+    for opts in (dict(), dict(batched=0)):
+        got, _ = _engine_close(engine, p, **opts)
+        assert got == exp, opts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(16))
+def test_fit_error_interpod_priority_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Sessions where most pending pods carry preferred pod (anti-)affinity
+    terms (inter-pod priority classes) and gangs that cannot become Ready:
+    the close messages come from walks ordered by the normalised inter-pod
+    score."""
+    c = kbgen_mod.gen_random(5500 + seed, n_nodes=3 + seed % 6, n_jobs=6 + seed % 5, max_tasks=3 + seed % 6,
+                             features=("labels", "running", "podaffinity", "init"))
+    for j in c.jobs:  # gangs larger than their pods: every pop ends not Ready
+        j.min_member = j.min_member + 2
+    p = str(tmp_path / "ip.kbs")
+    c.write(p)
+    exp = oracle_mod.ref_gang_close(p)
+    assert exp
+    for opts in (dict(), dict(batched=0)):
+        got, _ = _engine_close(engine, p, **opts)
+        assert got == exp, opts
 
 
 @pytest.mark.gpu

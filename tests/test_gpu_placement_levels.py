@@ -1,7 +1,7 @@
-"""GPU parity of the batched path's running-min level placements (option
-"placement": 1 levels, 2 parallel levels, 4 insertion): placement logs equal
-the CPU oracle's and the sequential placement loop's.  The selection argument is checked exhaustively on CPU in
-test_placement_levels_model below (it runs without a GPU)."""
+"""GPU parity of the batched path's running-min level placement (parallel
+levels, kbhip_batch.h place_parallel): placement logs equal the CPU oracle's
+and the per-task path's.  The selection argument is checked exhaustively on
+CPU in test_placement_levels_model below (it runs without a GPU)."""
 import os
 import random
 
@@ -10,24 +10,26 @@ import pytest
 from test_gpu_parity import NO_POD_AFFINITY, _oracle_log
 
 
-def _log(engine, path, placement):
+def _log(engine, path, **opts):
     with engine.Session(path) as s:
-        s.set_option("placement", placement)
+        for k, v in opts.items():
+            s.set_option(k, v)
         pod, node, kind = s.allocate()
         st = s.stats()
     return [(int(p), int(n), 4 if k == 1 else 8) for p, n, k in zip(pod, node, kind)], st
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("placement", [1, 2, 4, 5])
 @pytest.mark.parametrize("seed", range(30))
-def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, placement):
+def test_levels_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
     c = kbgen_mod.gen_random(4100 + seed, n_nodes=4 + seed % 12, n_jobs=4 + seed % 8, max_tasks=2 + seed % 9,
                              features=NO_POD_AFFINITY)
     p = str(tmp_path / "l.kbs")
     c.write(p)
-    got, st = _log(engine, p, placement)
-    assert got == _oracle_log(oracle_mod, p)
+    exp = _oracle_log(oracle_mod, p)
+    for opts in (dict(), dict(overlap=0)):
+        got, st = _log(engine, p, **opts)
+        assert got == exp, opts
 
 
 @pytest.mark.gpu
@@ -40,9 +42,9 @@ def test_parallel_levels_deep_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed)
     p = str(tmp_path / "d.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for placement in (0, 1, 2, 4, 5):
-        got, _ = _log(engine, p, placement)
-        assert got == exp, f"placement {placement}"
+    for opts in (dict(), dict(overlap=0), dict(batched=0)):
+        got, _ = _log(engine, p, **opts)
+        assert got == exp, opts
 
 
 @pytest.mark.gpu
@@ -50,22 +52,20 @@ def test_levels_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    for placement in (1, 2, 4, 5):
-        got, st = _log(engine, p, placement)
+    for opts in (dict(), dict(overlap=0)):
+        got, st = _log(engine, p, **opts)
         assert st["batched_pops"] > 0
-        assert got == exp, f"placement {placement}"
+        assert got == exp, opts
 
 
 @pytest.mark.gpu
 def test_levels_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     p = str(tmp_path / "c4s.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
-    a, _ = _log(engine, p, 0)
-    b, _ = _log(engine, p, 1)
-    c, _ = _log(engine, p, 2)
-    d, _ = _log(engine, p, 4)
-    e, _ = _log(engine, p, 5)
-    assert a == b == c == d == e
+    a, _ = _log(engine, p)
+    b, _ = _log(engine, p, overlap=0)
+    c, _ = _log(engine, p, batched=0)
+    assert a == b == c
 
 
 # ---- CPU: the selection argument (no GPU) ----------------------------------
@@ -206,7 +206,7 @@ def test_keys32_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(16))
 def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """Overlap depths 0..3 with speculation depths 0..3 place exactly as the
+    """Overlap on / off with speculation depths 0..3 place exactly as the
     oracle, including mispredicted pops retracted several deep."""
     tiers = [None, [["drf", "proportion"]], [["gang"], ["predicates", "nodeorder"]],
              [["priority", "gang", "drf"], ["predicates", "proportion", "nodeorder"]]][seed % 4]
@@ -215,7 +215,7 @@ def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path,
     p = str(tmp_path / "o.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for overlap, spec in ((0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (2, 3), (3, 3), (3, 1)):
+    for overlap, spec in ((0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (1, 3), (0, 3)):
         assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
@@ -224,7 +224,7 @@ def test_overlap_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2o.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    for overlap, spec in ((2, 3), (3, 3), (1, 2), (0, 2)):
+    for overlap, spec in ((1, 3), (1, 2), (0, 2)):
         assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
@@ -235,7 +235,7 @@ def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     p = str(tmp_path / "c4o.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     logs, nodes = [], []
-    for overlap, spec in ((2, 3), (3, 3), (1, 2), (0, 0)):
+    for overlap, spec in ((1, 3), (1, 2), (0, 0)):
         with engine.Session(p) as s:
             s.set_option("overlap", overlap)
             s.set_option("speculate", spec)
@@ -248,41 +248,3 @@ def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
         assert st["alloc_device_s"] > 0
     assert all(lg == logs[-1] for lg in logs)
     assert all((nd == nodes[-1]).all() for nd in nodes)
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(16))
-def test_ov_rows_message_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """Overlapped pops that rebuild the previous pop's written rows from its
-    rows message + commit granules (option "ov_msg", default off) against
-    the write-back re-read (ov_msg 0) and the oracle: records and the device
-    node state after the session."""
-    c = kbgen_mod.gen_random(4700 + seed, n_nodes=3 + seed % 9, n_jobs=6 + seed % 10, max_tasks=4 + seed % 12,
-                             features=NO_POD_AFFINITY)
-    p = str(tmp_path / "m.kbs")
-    c.write(p)
-    exp = _oracle_log(oracle_mod, p)
-    states = []
-    for msg in (1, 0):
-        with engine.Session(p) as s:
-            s.set_option("ov_msg", msg)
-            pod, node, kind = s.allocate()
-            st = s.stats()
-            states.append(s.read_nodes(len(c.nodes)))
-        assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp, f"ov_msg {msg}"
-        if msg == 0:
-            assert st["msg_pops"] == 0
-    assert (states[0] == states[1]).all()
-
-
-@pytest.mark.gpu
-def test_ov_rows_message_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
-    p = str(tmp_path / "c2.kbs")
-    kbgen_mod.gen_c2(p)
-    exp = _oracle_log(oracle_mod, p, fast=True)
-    with engine.Session(p) as s:
-        s.set_option("ov_msg", 1)
-        pod, node, kind = s.allocate()
-        st = s.stats()
-    assert st["msg_pops"] > st["batched_pops"] // 2  # most pops follow an overlapped pop directly
-    assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp

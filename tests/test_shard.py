@@ -47,6 +47,7 @@ def test_exchange_gloo(world, tmp_path):
         assert res[r]["max_u64"] == [int(x) for x in keys.max(axis=0)]
         assert res[r]["min_i64"] == [int(x) for x in ints.min(axis=0)]
         assert res[r]["max_i64"] == [int(x) for x in ints.max(axis=0)]
+        assert res[r]["sum_i64"] == [int(x) for x in ints.sum(axis=0)]
         exp = np.concatenate([(np.arange(40, dtype=np.uint8) * (q + 1)).astype(np.uint8) for q in range(world)])
         assert res[r]["gather"] == [int(x) for x in exp]
 
@@ -66,6 +67,8 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, e
     c.write(p)
     if exp is None:
         exp = oracle_mod.ref_allocate(p, actions=actions).as_list()
+    # the gang plugin's close messages (FitError histograms summed over the shards)
+    exp_close = oracle_mod.ref_gang_close(p) if actions == "allocate" else None
     res = _run_ranks("shard_worker.py", world, tmp_path,
                      lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=600)
     n_nodes = len(c.nodes)
@@ -75,6 +78,8 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, e
         assert res[r]["info"] == [r, world, lo, hi]
         got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
         assert got == exp, f"rank {r}"
+        if exp_close is not None:
+            assert res[r]["close"] == exp_close, f"rank {r}"
     return res
 
 
@@ -86,6 +91,19 @@ def test_sharded_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, batch
     batched 1: per-pop all-gather path where the class allows it, 0: per-task only."""
     c = kbgen_mod.gen_random(2200 + seed, n_nodes=6 + seed * 3, n_jobs=6, max_tasks=5, best_effort_p=0.2)
     _shard_case(oracle_mod, tmp_path, c, 2 + seed % 2, actions="allocate, backfill", batched=batched)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("batched", [1, 0])
+def test_sharded_close_messages_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, batched):
+    """FitError on shards: every feature (inter-pod priority classes, pod
+    affinity, ports), gangs that cannot become Ready; the close messages of
+    every rank equal the oracle's (walk histograms summed over the shards)."""
+    c = kbgen_mod.gen_random(2700 + seed, n_nodes=5 + seed * 2, n_jobs=7, max_tasks=5, best_effort_p=0.1)
+    for j in c.jobs[::2]:
+        j.min_member += 2
+    _shard_case(oracle_mod, tmp_path, c, 2 + seed % 2, batched=batched)
 
 
 @pytest.mark.gpu
@@ -111,6 +129,7 @@ def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     with engine.Session(p) as s:
         pod, node, kind = s.allocate(cap=1 << 20)
         st1 = s.stats()
+        close1 = s.gang_unschedulable()
     exp = [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)]
     assert st1["batched_pops"] == st1["sweeps"] > 1000
     for world in (2, 3):
@@ -119,6 +138,7 @@ def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
         for r in range(world):
             got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
             assert got == exp, f"world {world} rank {r}"
+            assert res[r]["close"] == close1, f"world {world} rank {r}"
             assert res[r]["batched_pops"] == st1["batched_pops"]
             assert res[r]["collectives"] == res[r]["batched_pops"]  # one all-gather per pop, nothing else
 
