@@ -182,6 +182,9 @@ def open_sharded(buf, device, rank, world, dist):
             ok = 0.0
         if allmin(dist, device, ok) < 1.0:
             EXCHANGE[0] = f"torch.distributed {BACKEND} (host callbacks)"
+            if ok:  # this rank's engine communicator formed: drop it, so every rank exchanges the same way
+                s.close()
+                s = kbhip.ShardedSession(buf, device, rank, world)
     if EXCHANGE[0] != "rccl":
         dev = f"cuda:{device}" if BACKEND == "nccl" else None
         s.connect_host(kbhip.torch_exchange(device=dev), kbhip.torch_gather(device=dev))

@@ -101,6 +101,7 @@ typedef struct kbhip_stats {
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
+    int64_t comm_reused;     /* 1: kbhip_shard_connect_rccl took a pooled communicator of an earlier session */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -193,7 +194,15 @@ int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
  * pods[i] are pod indices of the opened snapshot (they stay the session's pod
  * ids; a deleted pod never appears in a later record).  Every event is
  * validated first (KBHIP_EINVAL: index out of range, unknown event, an event
- * on a deleted pod) and nothing changes on error. */
+ * on a deleted pod) and nothing changes on error.
+ * Deliberate deviation: the reference's deletePod builds NewTaskInfo(pod),
+ * whose Job is empty for a pod without a PodGroup (api/job_info.go:60-70), so
+ * the cache takes a deleted group-less pod off its node only — the task stays
+ * in its shadow job (cache/event_handlers.go:119-165) and the next session
+ * still counts it (a Pending one is allocated again).  The engine removes the
+ * pod from its shadow job, and a shadow job left without pods from the cache:
+ * the state a fresh snapshot of the cluster holds, which is what the parity
+ * tests compare against (tests/test_gpu_carry.py). */
 enum { KBHIP_EV_DELETE = 1, KBHIP_EV_SUCCEEDED = 2, KBHIP_EV_FAILED = 3 };
 int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t* events, int64_t n,
                                int64_t* out_uploaded_bytes);
@@ -271,11 +280,14 @@ int kbhip_session_open_shard(const void* kbs_bytes, size_t len, int device, int3
                              kb_session** out);
 int kbhip_shard_info(kb_session* s, int32_t* out_rank_world_lo_hi);
 int kbhip_rccl_unique_id(void* out, int64_t cap);
-/* kbhip_shard_connect_rccl returns 0 after a new ncclCommInitRank and 1 when
- * it takes the communicator a closed earlier session of this process left
- * with the same unique id, rank, world and device (communicators are pooled
- * for the process's lifetime: reuse one unique id across scheduling cycles
- * and the bootstrap is paid once; every rank must then reuse together). */
+/* kbhip_shard_connect_rccl forms the session's communicator with a new
+ * ncclCommInitRank, or takes the one a closed earlier session of this process
+ * left with the same unique id, rank, world and device (communicators are
+ * pooled for the process's lifetime: reuse one unique id across scheduling
+ * cycles and the bootstrap is paid once; every rank must then reuse together;
+ * kbhip_stats.comm_reused says which happened).  A session on which an ABI
+ * call failed while it was connected, or whose communicator reports an
+ * asynchronous error, aborts the communicator at close instead of pooling it. */
 int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len);
 int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
 int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx);

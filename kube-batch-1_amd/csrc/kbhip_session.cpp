@@ -175,11 +175,18 @@ struct CommPool {
 static ncclComm_t comm_acquire(const string& id, int rank, int world, int device) {
     CommPool& P = CommPool::get();
     std::lock_guard<std::mutex> lk(P.mu);
-    for (auto& e : P.v)
-        if (!e.busy && e.id == id && e.rank == rank && e.world == world && e.device == device) {
-            e.busy = true;
-            return e.comm;
+    for (size_t i = 0; i < P.v.size(); ++i) {
+        auto& e = P.v[i];
+        if (e.busy || e.id != id || e.rank != rank || e.world != world || e.device != device) continue;
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(e.comm, &ae) != ncclSuccess || ae != ncclSuccess) {  // broken: never reused
+            (void)ncclCommAbort(e.comm);
+            P.v.erase(P.v.begin() + (long)i);
+            return nullptr;  // the caller forms a new one (every rank sees the same failure)
         }
+        e.busy = true;
+        return e.comm;
+    }
     return nullptr;
 }
 static void comm_add(const string& id, int rank, int world, int device, ncclComm_t c) {
@@ -192,6 +199,18 @@ static void comm_release(ncclComm_t c) {
     std::lock_guard<std::mutex> lk(P.mu);
     for (auto& e : P.v)
         if (e.comm == c) e.busy = false;
+}
+// A communicator whose session failed part-way (an ABI call returned an error
+// while it was connected: the ranks' collective sequences may no longer
+// match) or that reports an asynchronous error is aborted and leaves the pool.
+static void comm_drop(ncclComm_t c) {
+    {
+        CommPool& P = CommPool::get();
+        std::lock_guard<std::mutex> lk(P.mu);
+        for (size_t i = 0; i < P.v.size(); ++i)
+            if (P.v[i].comm == c) { P.v.erase(P.v.begin() + (long)i); break; }
+    }
+    (void)ncclCommAbort(c);
 }
 
 struct Plugin {
@@ -481,6 +500,7 @@ struct Session {
     int rank = 0, world = 1, n_total = 0;
     ncclComm_t comm = nullptr;                 // RCCL exchange (one GPU per rank)
     bool comm_pooled = false;                  // comm belongs to the process-wide CommPool
+    bool comm_bad = false;                     // an ABI call failed while comm was connected (not reused)
     kbhip_allreduce_fn xfn = nullptr;          // or a host-side exchange callback
     void* xctx = nullptr;
     kbhip_allgather_fn xgfn = nullptr;         // host all-gather (batched pops of a shard session)
@@ -502,11 +522,15 @@ struct Session {
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
         if (comm) {
-            if (comm_pooled) comm_release(comm);
+            ncclResult_t ae = ncclSuccess;
+            const bool async_err = ncclCommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess;
+            if (comm_bad || async_err) comm_drop(comm);
+            else if (comm_pooled) comm_release(comm);
             else (void)ncclCommDestroy(comm);
         }
         comm = nullptr;
         comm_pooled = false;
+        comm_bad = false;
         for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : ev_ring)
@@ -1634,7 +1658,8 @@ struct RankBatcher {
     }
     struct Req {
         RankDesc desc;
-        hipStream_t st = nullptr;
+        hipStream_t st = nullptr;  // the requester's stream (on its device)
+        int device = 0;
         bool done = false;
         hipError_t err = hipSuccess;
         int batch = 0;  // sessions in the launch that served it
@@ -1645,9 +1670,13 @@ struct RankBatcher {
     vector<Req*> pending;
     int members = 0;  // grouped sessions inside a reclaim / preempt action
     bool busy = false;
-    RankDesc* h_desc = nullptr;  // pinned, mapped: the kernels read the descriptors in place
-    void* d_desc = nullptr;
-    size_t cap_bytes = 0, n_cap = 0;
+    // pinned, mapped descriptors (the kernels read them in place), one area per device
+    struct Descs {
+        RankDesc* h = nullptr;
+        void* d = nullptr;
+        size_t cap_bytes = 0, n_cap = 0;
+    };
+    std::map<int, Descs> descs;
     void join() {
         std::lock_guard<std::mutex> lk(mu);
         ++members;
@@ -1657,22 +1686,34 @@ struct RankBatcher {
         --members;
         cv.notify_all();
     }
-    hipError_t run(const vector<Req*>& batch, hipStream_t st) {
-        if (batch.size() > n_cap) {
-            if (h_desc) MemPool::get().give(MemPool::kPinnedMapped, h_desc, cap_bytes, 0);
-            n_cap = std::max<size_t>(64, batch.size());
-            h_desc = (RankDesc*)MemPool::get().take(MemPool::kPinnedMapped, n_cap * sizeof(RankDesc), &cap_bytes);
-            hipError_t e = hipHostGetDevicePointer(&d_desc, h_desc, 0);
+    // One launch per device: a session's columns and buffers live on its own
+    // device, so requests from different devices never share a launch; each
+    // launch runs on the first of its requesters' streams.
+    hipError_t run(const vector<Req*>& batch) {
+        std::map<int, vector<Req*>> by_dev;
+        for (Req* q : batch) by_dev[q->device].push_back(q);
+        for (auto& kv : by_dev) {
+            hipError_t e = hipSetDevice(kv.first);
+            if (e != hipSuccess) return e;
+            Descs& D = descs[kv.first];
+            const vector<Req*>& b = kv.second;
+            if (b.size() > D.n_cap) {
+                if (D.h) MemPool::get().give(MemPool::kPinnedMapped, D.h, D.cap_bytes, kv.first);
+                D.n_cap = std::max<size_t>(64, b.size());
+                D.h = (RankDesc*)MemPool::get().take(MemPool::kPinnedMapped, D.n_cap * sizeof(RankDesc), &D.cap_bytes);
+                if ((e = hipHostGetDevicePointer(&D.d, D.h, 0)) != hipSuccess) return e;
+            }
+            int max_nblk = 1;
+            for (size_t i = 0; i < b.size(); ++i) {
+                D.h[i] = b[i]->desc;
+                max_nblk = std::max(max_nblk, b[i]->desc.nblk);
+            }
+            hipStream_t st = b[0]->st;
+            e = launch_rank_sorted_multi((const RankDesc*)D.d, (int)b.size(), max_nblk, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
             if (e != hipSuccess) return e;
         }
-        int max_nblk = 1;
-        for (size_t i = 0; i < batch.size(); ++i) {
-            h_desc[i] = batch[i]->desc;
-            max_nblk = std::max(max_nblk, batch[i]->desc.nblk);
-        }
-        hipError_t e = launch_rank_sorted_multi((const RankDesc*)d_desc, (int)batch.size(), max_nblk, st);
-        if (e == hipSuccess) e = hipStreamSynchronize(st);
-        return e;
+        return hipSuccess;
     }
     void submit(Req& r) {
         std::unique_lock<std::mutex> lk(mu);
@@ -1686,7 +1727,7 @@ struct RankBatcher {
                 vector<Req*> batch;
                 batch.swap(pending);
                 lk.unlock();
-                const hipError_t e = run(batch, r.st);
+                const hipError_t e = run(batch);
                 lk.lock();
                 for (Req* q : batch) {
                     q->err = e;
@@ -2896,8 +2937,10 @@ struct Allocator {
                                   (int)sr.second, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
                                   (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p));
             r.st = S.stream;
+            r.device = S.device;
             HIPCHK(hipStreamSynchronize(S.stream));  // this request's control block and counters are in place
             RankBatcher::get().submit(r);
+            HIPCHK(hipSetDevice(S.device));
             HIPCHK(r.err);
             S.stats.rank_requests++;
             S.stats.rank_batch_sum += r.batch;
@@ -3472,12 +3515,33 @@ using namespace kbhip;
         kbhip::g_err = "unknown error";                      \
         return KBHIP_EINVAL;                                 \
     }
+// The same for calls on a session: a failure while the session's RCCL
+// communicator is connected taints it (aborted at close, never pooled).
+#define ABI_GUARD_S(sp, ...)                                 \
+    try {                                                    \
+        __VA_ARGS__                                          \
+    } catch (kbhip::Error & e) {                             \
+        kbhip::g_err = e.what();                             \
+        taint_comm(sp);                                      \
+        return e.code;                                       \
+    } catch (std::exception & e) {                           \
+        kbhip::g_err = e.what();                             \
+        taint_comm(sp);                                      \
+        return KBHIP_EINVAL;                                 \
+    } catch (...) {                                          \
+        kbhip::g_err = "unknown error";                      \
+        taint_comm(sp);                                      \
+        return KBHIP_EINVAL;                                 \
+    }
 
 extern "C" {
 
 struct kb_session {
     kbhip::Session s;
 };
+static void taint_comm(kb_session* s) {
+    if (s && s->s.comm) s->s.comm_bad = true;
+}
 
 const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
 
@@ -3523,7 +3587,7 @@ int kbhip_session_open_file(const char* path, int device, kb_session** out) {
 int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode, int32_t min_available,
                     int32_t ready_count, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
                     int32_t* out_stop_reason) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
             throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
@@ -3537,7 +3601,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
 }
 
 int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         s->s.log.clear();
@@ -3554,7 +3618,7 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 }
 
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
@@ -3571,7 +3635,7 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 }
 
 int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s || n < 0 || (n > 0 && (!task_ids || !out_node))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
@@ -3584,7 +3648,7 @@ int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* 
 }
 
 int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
@@ -3755,7 +3819,7 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
 
 static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
                         int64_t cap) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
@@ -3774,7 +3838,7 @@ static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* 
     })
 }
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         HIPCHK(hipSetDevice(s->s.device));
@@ -3785,7 +3849,7 @@ int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
 }
 int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t* events, int64_t n,
                                int64_t* out_uploaded_bytes) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (n < 0 || (n > 0 && (!pods || !events))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
@@ -3802,7 +3866,7 @@ int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* o
     return evict_action(s, true, out_pod, out_node, out_kind, cap);
 }
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
-    ABI_GUARD({
+    ABI_GUARD_S(s, {
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         kbhip::Session& S = s->s;
@@ -3941,7 +4005,8 @@ int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) 
         if (ncclComm_t c = kbhip::comm_acquire(key, s->s.rank, s->s.world, s->s.device)) {
             s->s.comm = c;  // a previous session's communicator (same id, rank, world, device)
             s->s.comm_pooled = true;
-            return 1;
+            s->s.stats.comm_reused = 1;
+            return KBHIP_OK;
         }
         ncclComm_t c = nullptr;
         const ncclResult_t r = ncclCommInitRank(&c, s->s.world, id, s->s.rank);

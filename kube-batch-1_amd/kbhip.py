@@ -50,7 +50,7 @@ class Stats(ctypes.Structure):
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
                 ("collectives", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
                 ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
-                ("pop_batch_sum", ctypes.c_int64)]
+                ("pop_batch_sum", ctypes.c_int64), ("comm_reused", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -414,7 +414,8 @@ class ShardedSession(Session):
     def connect_rccl(self, unique_id: bytes) -> int:
         """1 when a pooled communicator of an earlier session was reused, 0 after a new init."""
         b = ctypes.create_string_buffer(unique_id, len(unique_id))
-        return _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
+        _check(lib().kbhip_shard_connect_rccl(self._h, b, len(unique_id)))
+        return int(self.stats()["comm_reused"])
 
     def connect_host(self, fn, gather=None) -> None:
         """fn(vals: np.ndarray[uint64], op) reduces vals in place across ranks

@@ -185,3 +185,32 @@ def test_rccl_communicator_pooled_across_sessions(engine, oracle_mod, kbgen_mod,
         s.close()
         assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
     assert reused == [0, 1, 1]
+
+
+@pytest.mark.gpu
+def test_rccl_communicator_dropped_after_failure(engine, oracle_mod, kbgen_mod, tmp_path):
+    """A session whose ABI call fails while its RCCL communicator is connected
+    (here: kbhip_place_job with a task that is not pending) aborts the
+    communicator at close instead of pooling it; the next session with the
+    same unique id forms a new one (comm_reused 0) and schedules like the
+    oracle, and the one after that reuses it again."""
+    c = kbgen_mod.gen_random(2620, n_nodes=10, n_jobs=6, max_tasks=5)
+    p = str(tmp_path / "w1f.kbs")
+    c.write(p)
+    exp = oracle_mod.ref_allocate(p).as_list()
+    uid = engine.ShardedSession.rccl_unique_id()
+    buf = open(p, "rb").read()
+    s = engine.ShardedSession(buf, 0, 0, 1)
+    assert s.connect_rccl(uid) == 0
+    with pytest.raises(engine.KbhipError):
+        s.place_job([-5], 1, 1, 0)
+    s.close()
+    reused = []
+    for _ in range(2):
+        s = engine.ShardedSession(buf, 0, 0, 1)
+        reused.append(s.connect_rccl(uid))
+        pod, node, kind = s.allocate()
+        s.close()
+        assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
+    assert reused == [0, 1]
+
