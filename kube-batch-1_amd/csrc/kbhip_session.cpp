@@ -167,6 +167,7 @@ struct CommPool {
     };
     std::mutex mu;
     vector<Entry> v;
+    std::set<string> aborted;  // unique ids whose communicator was aborted: a new init with one would hang
     static CommPool& get() {
         static CommPool p;
         return p;
@@ -181,8 +182,9 @@ static ncclComm_t comm_acquire(const string& id, int rank, int world, int device
         ncclResult_t ae = ncclSuccess;
         if (ncclCommGetAsyncError(e.comm, &ae) != ncclSuccess || ae != ncclSuccess) {  // broken: never reused
             (void)ncclCommAbort(e.comm);
+            P.aborted.insert(e.id);
             P.v.erase(P.v.begin() + (long)i);
-            return nullptr;  // the caller forms a new one (every rank sees the same failure)
+            return nullptr;
         }
         e.busy = true;
         return e.comm;
@@ -208,9 +210,20 @@ static void comm_drop(ncclComm_t c) {
         CommPool& P = CommPool::get();
         std::lock_guard<std::mutex> lk(P.mu);
         for (size_t i = 0; i < P.v.size(); ++i)
-            if (P.v[i].comm == c) { P.v.erase(P.v.begin() + (long)i); break; }
+            if (P.v[i].comm == c) {
+                P.aborted.insert(P.v[i].id);
+                P.v.erase(P.v.begin() + (long)i);
+                break;
+            }
     }
     (void)ncclCommAbort(c);
+}
+// A unique id serves one ncclCommInitRank bootstrap (its root listens once):
+// after its communicator was aborted, the ranks connect with a new id.
+static bool comm_id_aborted(const string& id) {
+    CommPool& P = CommPool::get();
+    std::lock_guard<std::mutex> lk(P.mu);
+    return P.aborted.count(id) != 0;
 }
 
 struct Plugin {
@@ -1551,9 +1564,13 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
 // RCCL all-reduce on the session stream, or a host round trip through the
 // caller's callback (tests: several ranks sharing one GPU over gloo).
 // ---------------------------------------------------------------------------
+// KBHIP_TRACE_SHARD=1: every collective of a shard session on stderr (diagnostic)
+static const bool g_trace_shard = std::getenv("KBHIP_TRACE_SHARD") != nullptr;
 static void exchange(Session& S, void* dev, int op, int n = 1) {
     if (S.world == 1) return;
     S.stats.collectives++;
+    if (g_trace_shard)
+        std::fprintf(stderr, "[shard %d] #%lld all-reduce op %d n %d\n", S.rank, (long long)S.stats.collectives, op, n);
     if (S.comm) {
         const ncclDataType_t dt = op == KBHIP_RED_MAX_U64 ? ncclUint64 : ncclInt64;
         const ncclRedOp_t ro = op == KBHIP_RED_MIN_I64 ? ncclMin : op == KBHIP_RED_SUM_I64 ? ncclSum : ncclMax;
@@ -1589,6 +1606,9 @@ static void fit_allreduce(Session& S, int32_t* fit4) {
 static void shard_gather(Session& S) {
     const size_t bytes = sizeof(ShardMsg);
     S.stats.collectives++;
+    if (g_trace_shard)
+        std::fprintf(stderr, "[shard %d] #%lld all-gather (pop %lld)\n", S.rank, (long long)S.stats.collectives,
+                     (long long)S.stats.pops);
     if (S.comm) {
         const ncclResult_t r = ncclAllGather(S.d_shard_send, S.d_shard_recv, bytes, ncclUint8, S.comm, S.stream);
         if (r != ncclSuccess) throw Error(KBHIP_EDEVICE, string("ncclAllGather: ") + ncclGetErrorString(r));
@@ -4008,6 +4028,9 @@ int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) 
             s->s.stats.comm_reused = 1;
             return KBHIP_OK;
         }
+        if (kbhip::comm_id_aborted(key))
+            throw kbhip::Error(KBHIP_EINVAL, "the communicator of this unique id was aborted after a failed session; "
+                                             "connect with a new kbhip_rccl_unique_id");
         ncclComm_t c = nullptr;
         const ncclResult_t r = ncclCommInitRank(&c, s->s.world, id, s->s.rank);
         if (r != ncclSuccess) throw kbhip::Error(KBHIP_EDEVICE, string("ncclCommInitRank: ") + ncclGetErrorString(r));

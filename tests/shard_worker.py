@@ -14,16 +14,26 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 
 
 def main():
+    import faulthandler  # a rank stuck for minutes prints where (the test's timeout then ends it)
+    faulthandler.dump_traceback_later(120, repeat=True)
     path, rank, world, init_file, out, actions = sys.argv[1:7]
     batched = int(sys.argv[7]) if len(sys.argv) > 7 else 1
     rank, world = int(rank), int(world)
     import torch.distributed as dist
     import kbhip
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+    import time
+    t0 = time.time()
+
+    def mark(what):  # progress on stderr: a slow or stuck rank shows where
+        print(f"rank {rank}/{world}: {what} at {time.time() - t0:.1f} s", file=sys.stderr, flush=True)
+    mark("process group formed")
     with kbhip.ShardedSession(path, 0, rank, world) as s:
+        mark("session open")
         s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched else None)
         info = s.info()
         pod, node, kind = s.run_actions(actions)
+        mark("actions done")
         st = s.stats()
         close = s.gang_unschedulable()
     dist.barrier()

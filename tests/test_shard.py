@@ -17,13 +17,16 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _run_ranks(script, world, tmp_path, extra, timeout=300):
-    init = str(tmp_path / "init")
+    import uuid
+    init = str(tmp_path / f"init_{world}_{uuid.uuid4().hex}")  # a fresh rendezvous file per group
     outs = [str(tmp_path / f"out{r}.json") for r in range(world)]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, script)] + extra(r, init, outs[r]), env=env)
              for r in range(world)]
     try:
         rcs = [p.wait(timeout=timeout) for p in procs]
+    except subprocess.TimeoutExpired:
+        pytest.fail(f"shard ranks did not finish within {timeout} s")
     finally:
         for p in procs:
             if p.poll() is None:
@@ -70,7 +73,7 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, e
     # the gang plugin's close messages (FitError histograms summed over the shards)
     exp_close = oracle_mod.ref_gang_close(p) if actions == "allocate" else None
     res = _run_ranks("shard_worker.py", world, tmp_path,
-                     lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=600)
+                     lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=240)
     n_nodes = len(c.nodes)
     import kbhip
     for r in range(world):
@@ -134,7 +137,7 @@ def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     assert st1["batched_pops"] == st1["sweeps"] > 1000
     for world in (2, 3):
         res = _run_ranks("shard_worker.py", world, tmp_path,
-                         lambda r, init, out: [p, str(r), str(world), init, out, "allocate", "1"], timeout=900)
+                         lambda r, init, out: [p, str(r), str(world), init, out, "allocate", "1"], timeout=240)
         for r in range(world):
             got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
             assert got == exp, f"world {world} rank {r}"
@@ -191,9 +194,10 @@ def test_rccl_communicator_pooled_across_sessions(engine, oracle_mod, kbgen_mod,
 def test_rccl_communicator_dropped_after_failure(engine, oracle_mod, kbgen_mod, tmp_path):
     """A session whose ABI call fails while its RCCL communicator is connected
     (here: kbhip_place_job with a task that is not pending) aborts the
-    communicator at close instead of pooling it; the next session with the
-    same unique id forms a new one (comm_reused 0) and schedules like the
-    oracle, and the one after that reuses it again."""
+    communicator at close instead of pooling it.  Its unique id is then
+    refused (a second bootstrap on it would hang); the ranks connect with a
+    new id — a new communicator (comm_reused 0), reused by the next session —
+    and schedule like the oracle."""
     c = kbgen_mod.gen_random(2620, n_nodes=10, n_jobs=6, max_tasks=5)
     p = str(tmp_path / "w1f.kbs")
     c.write(p)
@@ -205,12 +209,16 @@ def test_rccl_communicator_dropped_after_failure(engine, oracle_mod, kbgen_mod, 
     with pytest.raises(engine.KbhipError):
         s.place_job([-5], 1, 1, 0)
     s.close()
+    s = engine.ShardedSession(buf, 0, 0, 1)
+    with pytest.raises(engine.KbhipError, match="aborted"):
+        s.connect_rccl(uid)
+    s.close()
+    uid2 = engine.ShardedSession.rccl_unique_id()
     reused = []
     for _ in range(2):
         s = engine.ShardedSession(buf, 0, 0, 1)
-        reused.append(s.connect_rccl(uid))
+        reused.append(s.connect_rccl(uid2))
         pod, node, kind = s.allocate()
         s.close()
         assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
     assert reused == [0, 1]
-
