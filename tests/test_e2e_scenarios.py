@@ -230,6 +230,235 @@ def backfill_scheduling_session():
     return c, "reclaim, allocate, backfill, preempt", check
 
 
+# ---- test/e2e/job.go ---------------------------------------------------------
+# createJob (test/e2e/util.go:280-340): one batch Job per task spec, pods
+# annotated with the PodGroup, PodGroup MinMember = sum of the task specs'
+# min (or minMember); clusterSize(oneCPU) = 12 on the three 4-CPU workers.
+# Priority classes (util.go:93-113): master-pri 100, worker-pri 1.  A
+# ReplicaSet's pods carry no PodGroup (shadow pod groups, cache/util.go:42-60).
+REP = 4 * len(NODES)
+MASTER, WORKER = 100, 1
+
+
+def _rs(c, n, name="rs-1", cpu=ONE):
+    """n ReplicaSet pods Running, spread over the workers."""
+    for k in range(n):
+        c.add_pod("e2e", f"{name}-{k}", uid=f"{name}-{k:03d}", node=NODES[k % 3], phase="Running",
+                  containers=[kbgen.res(cpu)])
+
+
+def _tasks(c, name, specs, min_member=None, queue="default", ts=kbgen.SEC, ns="e2e", pg_priority=0, node=None):
+    """A createJob job: specs = [(rep, cpu, min, priority)] (cpu None: BestEffort)."""
+    mm = sum(m for _, _, m, _ in specs) if min_member is None else min_member
+    c.add_job(ns, name, queue, min_member=mm, ts=ts, pg_priority=pg_priority)
+    for i, (rep, cpu, _m, pri) in enumerate(specs):
+        for k in range(rep):
+            nd = node[k % len(node)] if node else None
+            c.add_pod(ns, f"{name}-{i}-{k}", uid=f"{name}-{i}-{k:03d}", group=name, node=nd,
+                      phase="Running" if nd else "Pending", ts=ts, priority=pri,
+                      containers=[kbgen.res(cpu) if cpu is not None else {}])
+
+
+def _by_job(c, recs):
+    out = {}
+    for p, n, k in recs:
+        uid = _pod_uid(c, p)
+        job = uid.rsplit("-", 2)[0]
+        out.setdefault(job, []).append((uid, n, k))
+    return out
+
+
+def job_schedule():
+    """job.go:28-47 Schedule Job: qj-1 (rep = clusterSize pods of oneCPU,
+    min 2) -> Ready: every pod placed in one session."""
+    c = _cluster()
+    _tasks(c, "qj-1", [(REP, ONE, 2, 0)])
+
+    def check(recs, c):
+        assert len(recs) == REP and all(k == 4 for p, n, k in recs)
+    return c, "allocate", check
+
+
+def job_multiple():
+    """job.go:49-81 Schedule Multiple Jobs: three jobs of rep oneCPU pods,
+    min 2 each, one queue -> all three Ready.  Gang's JobOrderFn puts jobs
+    not yet Ready first (gang.go:136-160), so each gets its 2, then DRF
+    (drf.go:113-131) shares the rest round robin: 4 + 4 + 4."""
+    c = _cluster()
+    for name in ("mqj-1", "mqj-2", "mqj-3"):
+        _tasks(c, name, [(REP, ONE, 2, 0)])
+
+    def check(recs, c):
+        got = _by_job(c, recs)
+        assert sorted(got) == ["mqj-1", "mqj-2", "mqj-3"]
+        assert all(len(v) == REP // 3 for v in got.values())
+    return c, "allocate", check
+
+
+def job_gang(rs_running=True):
+    """job.go:83-118 Gang scheduling: a ReplicaSet of rep/2 + 1 = 7 oneCPU pods
+    runs; gang-qj (7 pods, min 7) then stays Pending / Unschedulable: its pop
+    places the 5 free slots and stops at the first task without a node, no
+    rollback, not Ready (nothing dispatched; the gang plugin's close message
+    says 2/7 unschedulable).  After the ReplicaSet is deleted (rs_running
+    False) the next session makes it Ready."""
+    c = _cluster()
+    rep = REP // 2 + 1
+    if rs_running:
+        _rs(c, rep)
+    _tasks(c, "gang-qj", [(rep, ONE, rep, 0)], ns="test")
+
+    def check(recs, c):
+        assert len(recs) == (REP - rep if rs_running else rep)
+
+    def close_check(close):
+        if rs_running:
+            assert close["test/gang-qj"].startswith(f"{rep - (REP - rep)}/{rep} tasks in gang unschedulable: ")
+        else:
+            assert "test/gang-qj" not in close
+    return c, "allocate", check, close_check
+
+
+def job_gang_full_occupied():
+    """job.go:120-149 Gang scheduling: Full Occupied: gang-fq-qj1 (rep pods,
+    min rep) runs on the whole cluster; gang-fq-qj2 (same shape) stays Pending
+    and qj1 stays Ready: no placement, no eviction (preempt needs a Ready
+    preemptor job, preempt.go:87-149).  The one queue holds the whole cluster,
+    so proportion calls it overused (proportion.go:186-197) and allocate never
+    pops qj2 (allocate.go:76-79): its NodesFitDelta stays empty, and the close
+    message is the "0 nodes are available" form (job_info.go:343-347)."""
+    c = _cluster()
+    _tasks(c, "gang-fq-qj1", [(REP, ONE, REP, 0)], ns="test", ts=0, node=NODES)
+    _tasks(c, "gang-fq-qj2", [(REP, ONE, REP, 0)], ns="test")
+
+    def check(recs, c):
+        assert recs == []
+
+    def close_check(close):
+        assert set(close) == {"test/gang-fq-qj2"}
+        assert close["test/gang-fq-qj2"] == f"{REP}/{REP} tasks in gang unschedulable: 0 nodes are available"
+    return c, "reclaim, allocate, backfill, preempt", check, close_check
+
+
+def job_multiple_preemption():
+    """job.go:183-222 Multiple Preemption: preemptee-qj (rep, min 1) fills the
+    cluster, preemptor-qj1 and -qj2 (same shape, same queue) are submitted;
+    expected eventually rep/3 each.  As in preemption_session, one session of
+    this fork records nothing: reclaim works across queues only
+    (reclaim.go:123-131), and preempt commits a cross-job statement only for a
+    Ready preemptor job (preempt.go:134-143), which a Pipelined task never
+    makes (job_info.go:374-388)."""
+    c = _cluster()
+    _tasks(c, "preemptee-qj", [(REP, ONE, 1, 0)], ts=0, node=NODES)
+    _tasks(c, "preemptor-qj1", [(REP, ONE, 1, 0)])
+    _tasks(c, "preemptor-qj2", [(REP, ONE, 1, 0)])
+
+    def check(recs, c):
+        assert recs == []
+    return c, "reclaim, allocate, backfill, preempt", check
+
+
+def job_best_effort():
+    """job.go:224-252 Schedule BestEffort Job: task 0 rep oneCPU pods (min 2),
+    task 1 rep/2 BestEffort pods (min 2) -> Ready.  Allocate skips BestEffort
+    tasks (allocate.go:91-104) and places the rep resourced pods; backfill
+    (backfill.go:40-70) then places the BestEffort pods on the first node
+    passing the predicates."""
+    c = _cluster()
+    _tasks(c, "test", [(REP, ONE, 2, 0), (REP // 2, None, 2, 0)])
+
+    def check(recs, c):
+        got = [_pod_uid(c, p) for p, n, k in recs]
+        assert len(got) == REP + REP // 2
+        assert all(u.startswith("test-0-") for u in got[:REP]) and all(u.startswith("test-1-") for u in got[REP:])
+        assert {n for p, n, k in recs[REP:]} == {0}  # first fit: the lowest node index passing the predicates
+    return c, "reclaim, allocate, backfill, preempt", check
+
+
+def job_statement():
+    """job.go:254-289 Statement: st-qj-1 (rep, min rep) runs on the whole
+    cluster; st-qj-2 (same shape) stays Unschedulable and st-qj-1 sees no
+    eviction: preempt tries st-qj-2's tasks inside one Statement and
+    discards it when the job does not become Ready (preempt.go:134-149,
+    statement.go:174-186), so no eviction reaches the cache."""
+    c = _cluster()
+    _tasks(c, "st-qj-1", [(REP, ONE, REP, 0)], ns="test", ts=0, node=NODES)
+    _tasks(c, "st-qj-2", [(REP, ONE, REP, 0)], ns="test")
+
+    def check(recs, c):
+        assert recs == []
+
+    def close_check(close):
+        assert set(close) == {"test/st-qj-2"}
+    return c, "reclaim, allocate, backfill, preempt", check, close_check
+
+
+def job_task_priority():
+    """job.go:291-329 TaskPriority: a ReplicaSet of rep/2 oneCPU pods runs;
+    multi-pod-job has rep worker-pri pods (min rep/2 - 1) and one master-pri
+    pod (min 1) -> exactly 1 master and rep/2 - 1 workers run.  The priority
+    plugin's TaskOrderFn (priority.go:39-55) tries the master first; the job
+    is Ready at rep/2 placements (min = rep/2) and the next worker finds no
+    node."""
+    c = _cluster()
+    _rs(c, REP // 2)
+    _tasks(c, "multi-pod-job", [(REP, ONE, REP // 2 - 1, WORKER), (1, ONE, 1, MASTER)])
+
+    def check(recs, c):
+        got = [_pod_uid(c, p) for p, n, k in recs]
+        assert got[0] == "multi-pod-job-1-000"  # the master first
+        assert sum(u.startswith("multi-pod-job-1-") for u in got) == 1
+        assert sum(u.startswith("multi-pod-job-0-") for u in got) == REP // 2 - 1
+    return c, "allocate", check
+
+
+def job_mixed_requests():
+    """job.go:331-370 "Try to fit unassigned task with different resource
+    requests in one loop": a ReplicaSet of rep - 1 oneCPU pods runs (1 CPU
+    free), the job has a master-pri task of twoCPU and a worker-pri task of
+    halfCPU, minMember 1; the e2e test expects the halfCPU task to run.  In
+    this fork allocate's inner loop breaks at the first task without a node
+    (allocate.go:187-189): TaskOrderFn tries the 2-CPU master first, it fits
+    nowhere, and the pop ends before the worker is tried — the session
+    places nothing, and the close message reports the master's walk."""
+    c = _cluster()
+    _rs(c, REP - 1)
+    _tasks(c, "multi-task-diff-resource-job", [(1, 2 * ONE, 1, MASTER), (1, HALF, 1, WORKER)], min_member=1)
+
+    def check(recs, c):
+        assert recs == []
+
+    def close_check(close):
+        assert close == {"e2e/multi-task-diff-resource-job":
+                         "1/2 tasks in gang unschedulable: 0/3 nodes are available, 3 insufficient cpu."}
+    return c, "allocate", check, close_check
+
+
+def job_priority():
+    """job.go:372-418 Job Priority: pri-job-1 (PodGroup class worker-pri) and
+    pri-job-2 (master-pri), rep oneCPU pods each, min rep/2 + 1, submitted
+    while a ReplicaSet fills the cluster, which is then deleted; the e2e
+    test expects pri-job-2 Ready.  In this fork the job priority the
+    priority plugin orders by (priority.go:60-76) is JobInfo.Priority, which
+    Snapshot sets from the PodGroup's class and JobInfo.Clone then overwrites
+    with the last task's pod priority (cache.go:563-575, job_info.go:242,
+    294-326): both jobs' pods have no class (priority 0), so the jobs tie on
+    priority and the older pri-job-1 is popped first and becomes Ready;
+    pri-job-2 gets the remaining rep/2 - 1 slots and stays not Ready."""
+    c = _cluster()
+    _tasks(c, "pri-job-1", [(REP, ONE, REP // 2 + 1, 0)], pg_priority=WORKER)
+    _tasks(c, "pri-job-2", [(REP, ONE, REP // 2 + 1, 0)], pg_priority=MASTER)
+
+    def check(recs, c):
+        got = _by_job(c, recs)
+        assert len(got["pri-job-1"]) == REP // 2 + 1
+        assert len(got["pri-job-2"]) == REP - (REP // 2 + 1)
+
+    def close_check(close):
+        assert set(close) == {"e2e/pri-job-2"}
+    return c, "allocate", check, close_check
+
+
 def _pod_uid(c, i):
     return sorted(c.pods, key=lambda p: p.uid)[i].uid
 
@@ -246,25 +475,42 @@ SCENARIOS = {
     "queue_reclaim": queue_reclaim,
     "preemption_session": preemption_session,
     "backfill_scheduling_session": backfill_scheduling_session,
+    "job_schedule": job_schedule,
+    "job_multiple": job_multiple,
+    "job_gang": lambda: job_gang(True),
+    "job_gang_rs_deleted": lambda: job_gang(False),
+    "job_gang_full_occupied": job_gang_full_occupied,
+    "job_multiple_preemption": job_multiple_preemption,
+    "job_best_effort": job_best_effort,
+    "job_statement": job_statement,
+    "job_task_priority": job_task_priority,
+    "job_mixed_requests": job_mixed_requests,
+    "job_priority": job_priority,
 }
 
 
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_e2e_scenario_oracle(oracle_mod, tmp_path, name):
-    c, actions, check = SCENARIOS[name]()
+    c, actions, check, *close_check = SCENARIOS[name]()
     p = _write(c, tmp_path, name)
     recs = oracle_mod.ref_allocate(p, actions=actions).as_list()
     check(recs, c)
+    if close_check:  # the gang plugin's PodGroup conditions at session close
+        close_check[0](oracle_mod.ref_gang_close(p, actions=actions))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", sorted(SCENARIOS))
 def test_e2e_scenario_gpu(engine, oracle_mod, tmp_path, name):
-    c, actions, check = SCENARIOS[name]()
+    c, actions, check, *close_check = SCENARIOS[name]()
     p = _write(c, tmp_path, name)
     exp = oracle_mod.ref_allocate(p, actions=actions).as_list()
     with engine.Session(p) as s:
         pod, node, kind = s.run_actions(actions)
+        close = s.gang_unschedulable()
     got = [(int(a), int(b), KIND_CODE[int(k)]) for a, b, k in zip(pod, node, kind)]
     assert got == exp
     check(got, c)
+    assert close == oracle_mod.ref_gang_close(p, actions=actions)
+    if close_check:
+        close_check[0](close)
