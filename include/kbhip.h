@@ -290,6 +290,19 @@ int kbhip_rccl_unique_id(void* out, int64_t cap);
  * asynchronous error, aborts the communicator at close instead of pooling it. */
 int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len);
 int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
+/* Peer mailboxes for the batched pops of a shard session (SURVEY §8(e)'s
+ * device-side exchange): every rank's device holds a mailbox (exportable
+ * device memory, uncached where the runtime allows); fn all-gathers the
+ * ranks' IPC handles once (every rank calls this collectively), each rank
+ * maps the others' (hipIpcOpenMemHandle: xGMI across GPUs, the same memory for
+ * ranks sharing one GPU).  Per batched pop every shard's sweep kernel writes
+ * its top-64 with rows into every rank's mailbox and raises a flag; each
+ * rank's placement kernel waits for the W flags on the device — no host
+ * step and no collective launch per pop.  Takes precedence over the RCCL /
+ * host all-gather for batched pops; per-task pops still use the all-reduce
+ * of kbhip_shard_connect_rccl / kbhip_shard_connect_host.  Mailboxes and
+ * mappings are kept per process and reused by later sessions. */
+int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx);
 int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx);
 
 /* Test support (not part of the placement path): encode a snapshot without a

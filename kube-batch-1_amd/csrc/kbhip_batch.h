@@ -834,10 +834,39 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// System-scope (sc0 sc1) 8-byte accesses: what crosses between ranks' devices
+// through the mailboxes (and what a placement reads of them).
+__device__ __forceinline__ void st_sys(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld_sys(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ __forceinline__ void store_words_sys(T* dst, const T& v) {
+    uint64_t w[sizeof(T) / 8];
+    __builtin_memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); ++i) st_sys((uint64_t*)dst + i, w[i]);
+}
+template <typename T>
+__device__ __forceinline__ T load_words_sys(const T* src) {
+    uint64_t w[sizeof(T) / 8];
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 8); ++i) w[i] = ld_sys((const uint64_t*)src + i);
+    T v;
+    __builtin_memcpy(&v, w, sizeof(T));
+    return v;
+}
+
 // The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
-// writes this shard's top-64 with their rows and the sweep's FitDelta counts.
+// writes this shard's top-64 with their rows and the sweep's FitDelta counts
+// — to its own exchange buffer (msg, for the all-gather), or straight into
+// every rank's mailbox (mb.world > 0): the 64 candidates per destination,
+// the wave's stores drained, then one flag word per destination (lane p
+// writes rank p's), read by k_shard_place with system-scope loads.
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
-                           uint32_t fit_raw, ShardMsg* msg) {
+                           uint32_t fit_raw, ShardMsg* msg, const MboxArgs& mb) {
     const int lane = threadIdx.x & 63;
     ShardCand e{};
     e.node = -1;
@@ -851,8 +880,23 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
             for (int w = 0; w < port_win(c, nc); ++w) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
         e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
     }
-    msg->c[lane] = e;
-    const uint32_t sweep = fit_sum(fit_raw);
-    if (lane < 4) msg->fit[lane] = sweep;
+    const uint32_t sweep = fit_sum(fit_raw);  // count b in lane b
+    if (mb.world == 0) {
+        msg->c[lane] = e;
+        if (lane < 4) msg->fit[lane] = sweep;
+        return;
+    }
+    const int slot = (int)(mb.seq & (kMboxSlots - 1));
+    const uint64_t f01 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 0) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 1) << 32;
+    const uint64_t f23 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 2) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 3) << 32;
+    for (int p = 0; p < mb.world; ++p) {
+        ShardMsg* m = &mb.dst[p]->msg[slot][mb.rank];
+        store_words_sys(&m->c[lane], e);
+        if (lane == 0) { st_sys((uint64_t*)m->fit, f01); st_sys((uint64_t*)m->fit + 1, f23); }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's message stores completed
+    if (lane < mb.world) st_sys(&mb.dst[lane]->flag[slot][mb.rank][0], (uint64_t)mb.seq);
 }
 }  // namespace kbhip

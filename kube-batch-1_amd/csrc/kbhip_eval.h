@@ -39,6 +39,27 @@ struct ShardMsg {
     uint32_t pad[2];
     ShardCand c[kTopK];
 };
+static_assert(sizeof(ShardCand) % 8 == 0 && sizeof(ShardMsg) % 8 == 0, "mailbox copies move 8-byte words");
+
+// Peer mailboxes (kbhip_shard_connect_mailbox): every rank's device holds one;
+// for each batched pop every shard writes its ShardMsg straight into every
+// rank's mailbox (its own included) — over xGMI when the ranks are on
+// different GPUs — and then a self-tagged flag word {pop sequence number}
+// per destination; the placement kernel of each rank waits for the W flags of
+// its own mailbox.  Two slots (sequence parity): a shard can run at most one
+// pop ahead of the slowest, whose reads of the other slot are then done.
+constexpr int kMaxWorld = 16;
+constexpr int kMboxSlots = 2;
+struct Mailbox {
+    uint64_t flag[kMboxSlots][kMaxWorld][16];  // [slot][source][0]: sequence number (a 128-B line each)
+    ShardMsg msg[kMboxSlots][kMaxWorld];
+};
+struct MboxArgs {                 // kernel argument of a shard's sweep (world 0: no mailbox)
+    Mailbox* dst[kMaxWorld];      // every rank's mailbox as mapped in this process
+    int32_t rank, world;
+    uint32_t seq;
+    int32_t pad;
+};
 
 // Host-port words of a class: its window of the port columns (TaskClass::pw_lo).
 KBHIP_HD int port_win(const TaskClass& c, const NodeCols& nc) {

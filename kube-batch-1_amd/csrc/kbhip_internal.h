@@ -82,6 +82,7 @@ struct KeyFormat {
     int32_t base = 0, shift = 0, idxmax = 0;
 };
 struct ShardMsg;  // kbhip_eval.h
+struct MboxArgs;  // kbhip_eval.h
 // Batched path v2: one launch per pop chunk; results land in `out_dev`
 // (device pointer of a pinned host PopOut, pop_out_bytes() long).
 // placement 2: parallel levels; 6: sessions with Backfilled nodes; 7:
@@ -91,12 +92,15 @@ struct ShardMsg;  // kbhip_eval.h
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
-                            int fit_set, ShardMsg* shard_out = nullptr);
+                            int fit_set, ShardMsg* shard_out = nullptr, const struct MboxArgs* mbox = nullptr);
 // The placement of a sharded batched pop on the gathered ShardMsgs (world of
 // them, rank order): identical on every shard; each writes back its own rows.
+// flags (mailbox exchange): this rank's mailbox flags of the pop's slot —
+// the kernel waits until rank r's flag (flags[16 r]) reads seq.
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st);
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st,
+                              const uint64_t* flags = nullptr, uint32_t seq = 0);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node

@@ -249,6 +249,7 @@ static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed th
 template <int R, typename KT, int PL>
 __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
                                                uint64_t* cand64, uint32_t* arrive, PopOut* out, ShardMsg* smsg,
+                                               const MboxArgs& mb,
                                                const int bid, const int nb_) {
     __shared__ KT wlk[kPopThreads / 64][64];  // sweep / merge lists in the key type
     __shared__ uint64_t wl64[sizeof(KT) == 8 ? 1 : kPopThreads / 64][64];
@@ -355,7 +356,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     __syncthreads();
     if constexpr (PL == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
-        if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg);
+        if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg, mb);
         return;
     } else if constexpr (PL == 6) {  // Backfilled nodes in the session
         if (wave != 0) return;
@@ -380,8 +381,8 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
 template <int R, typename KT, int PL>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                            uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                           ShardMsg* smsg) {
-    pop_batch_body<R, KT, PL>(cf, nc, t, a, cand64, arrive, out, smsg, blockIdx.x, gridDim.x);
+                                                           ShardMsg* smsg, MboxArgs mb) {
+    pop_batch_body<R, KT, PL>(cf, nc, t, a, cand64, arrive, out, smsg, mb, blockIdx.x, gridDim.x);
 }
 
 // What-if sessions batched per launch: one launch
@@ -392,7 +393,8 @@ template <int R, typename KT, int PL>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_multi(PopDescs d) {
     const PopDesc& q = d.d[blockIdx.y];
     if ((int)blockIdx.x >= q.nb) return;
-    pop_batch_body<R, KT, PL>(q.cf, q.nc, q.t, q.a, q.cand, q.arrive, (PopOut*)q.out, nullptr, blockIdx.x, q.nb);
+    const MboxArgs none{};
+    pop_batch_body<R, KT, PL>(q.cf, q.nc, q.t, q.a, q.cand, q.arrive, (PopOut*)q.out, nullptr, none, blockIdx.x, q.nb);
 }
 
 // ---------------------------------------------------------------------------
@@ -766,9 +768,10 @@ int pop_blocks(int n_nodes, int* R_out) {
 
 template <typename KT>
 static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
-                               uint64_t* cand, uint32_t* arrive, PopOut* o, ShardMsg* m, hipStream_t st) {
+                               uint64_t* cand, uint32_t* arrive, PopOut* o, ShardMsg* m, const MboxArgs& mb,
+                               hipStream_t st) {
 #define KBHIP_PB1(RR, PP) \
-    hipLaunchKernelGGL((k_pop_batch<RR, KT, PP>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, m)
+    hipLaunchKernelGGL((k_pop_batch<RR, KT, PP>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, m, mb)
 #define KBHIP_PB(RR)                                                   \
     do {                                                               \
         switch (a.placement) {                                         \
@@ -853,15 +856,16 @@ hipError_t launch_pop_batch_multi(const PopReq* reqs, int n, hipStream_t st, int
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
-                            int fit_set, ShardMsg* shard_out) {
-    if (placement == 3 && !shard_out) return hipErrorInvalidValue;
+                            int fit_set, ShardMsg* shard_out, const MboxArgs* mbox) {
+    if (placement == 3 && !shard_out && !mbox) return hipErrorInvalidValue;
+    const MboxArgs mb = mbox ? *mbox : MboxArgs{};
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, placement, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, st);
-    else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, st);
+    if (kf.use32) launch_pop_batch_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, mb, st);
+    else launch_pop_batch_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, shard_out, mb, st);
     return hipGetLastError();
 }
 
@@ -872,27 +876,52 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 // top-64 — and writes back the rows it owns.  One workgroup.
 // ---------------------------------------------------------------------------
 constexpr int kShardHash = 2048;  // node -> (rank, slot) of the gathered candidates (<= 16 ranks x 64)
+constexpr long kMboxSpin = 1L << 23;  // mailbox poll bound (seconds): a lost rank ends the pop with an error
 __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                             const ShardMsg* msgs, int world, PopOut* out) {
+                                                             const ShardMsg* msgs, int world, PopOut* out,
+                                                             const uint64_t* flags, uint32_t seq) {
     __shared__ uint64_t wl[kPopThreads / 64][64];
     __shared__ RowCache rc;
     __shared__ int32_t s_hk[kShardHash];
     __shared__ int16_t s_hv[kShardHash];
     __shared__ int32_t s_fitin[4];
+    __shared__ int s_ok;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const TaskClass c = t.classes[a.cls];
     for (int i = threadIdx.x; i < kShardHash; i += kPopThreads) s_hk[i] = -1;
     for (int i = threadIdx.x; i < kHash; i += kPopThreads) rc.hkey[i] = -1;
+    if (wave == 0) {  // mailbox: every shard's message of pop `seq` has arrived (lane r polls rank r's flag)
+        bool ok = true;
+        if (flags && lane < world) {
+            long spin = 0;
+            while (ld_sys(&flags[lane * 16]) != (uint64_t)seq) {
+                if (++spin >= kMboxSpin) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        const bool all = __ballot(!ok) == 0;
+        if (lane == 0) s_ok = all;
+    }
+    __syncthreads();
+    if (!s_ok) {  // n_done 0 on a shard pop: the host reports a lost exchange
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (threadIdx.x < 4) {
         uint32_t f = 0;
-        for (int r = 0; r < world; ++r) f += msgs[r].fit[threadIdx.x];
+        for (int r = 0; r < world; ++r) {
+            const uint64_t w = ld_sys((const uint64_t*)msgs[r].fit + (threadIdx.x >> 1));
+            f += (uint32_t)(w >> (32 * (threadIdx.x & 1)));
+        }
         s_fitin[threadIdx.x] = (int32_t)f;
     }
     __syncthreads();
     // every gathered candidate into the node -> entry table; lists merged by waves
     uint64_t acc = 0;
     for (int r = wave; r < world; r += kPopThreads / 64) {
-        const ShardCand& e = msgs[r].c[lane];
+        const ShardCand e = load_words_sys(&msgs[r].c[lane]);
         if (e.node >= 0) {
             int h = (int)(((uint32_t)e.node * 2654435761u) >> 21);
             while (atomicCAS(&s_hk[h], -1, e.node) != -1) h = (h + 1) & (kShardHash - 1);
@@ -910,7 +939,7 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
             int h = (int)(((uint32_t)g * 2654435761u) >> 21);
             while (s_hk[h] != g) h = (h + 1) & (kShardHash - 1);
             const int src = s_hv[h];
-            const ShardCand& e = msgs[src >> 6].c[src & 63];
+            const ShardCand e = load_words_sys(&msgs[src >> 6].c[src & 63]);
             rc.row[lane] = e.row;
             for (int w = 0; w < 4; ++w) rc.pw[lane][w] = e.pw[w];
             rc.na[lane] = e.na;
@@ -926,11 +955,13 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
 
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st) {
+                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, const uint64_t* flags,
+                              uint32_t seq) {
     if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, 0};
-    hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev);
+    hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev,
+                       flags, seq);
     return hipGetLastError();
 }
 

@@ -226,6 +226,21 @@ static bool comm_id_aborted(const string& id) {
     return P.aborted.count(id) != 0;
 }
 
+// Peer mailboxes (kbhip_shard_connect_mailbox): a process keeps its mailbox
+// allocations (one per device, reused by the next session: its IPC handle,
+// and so the peers' mappings of it, stay valid) and every peer mailbox it
+// opened (hipIpcOpenMemHandle, keyed by the handle's bytes) for its lifetime —
+// a mailbox is never freed while another process may still map it.
+struct MboxPool {
+    std::mutex mu;
+    std::multimap<int, std::pair<Mailbox*, int>> free_own;  // device -> (mailbox, allocation kind)
+    std::map<string, void*> opened;                         // peer handle bytes -> mapping
+    static MboxPool& get() {
+        static MboxPool p;
+        return p;
+    }
+};
+
 struct Plugin {
     string name;
     int flags = 0;
@@ -521,6 +536,10 @@ struct Session {
     DevBuf b_shard_send, b_shard_recv;         // this shard's ShardMsg / all of them (rank order)
     ShardMsg* d_shard_send = nullptr;
     ShardMsg* d_shard_recv = nullptr;
+    Mailbox* mbox_own = nullptr;               // peer mailboxes (kbhip_shard_connect_mailbox): this rank's,
+    int mbox_kind = 0;                         // its allocation (0 uncached, 1 fine-grained, 2 default)
+    Mailbox* mbox_peer[kMaxWorld] = {};        // and every rank's as mapped here (own included)
+    uint32_t mbox_seq = 0;                     // sequence number of the last batched pop sent
     vector<uint8_t> h_shard;                   // host staging of the host all-gather
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
     bool encode_only = false;
@@ -534,6 +553,13 @@ struct Session {
         for (int k = 1; k <= kMaxDep; ++k)
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (mbox_own) {  // back to the process's pool (peers may keep their mapping of it)
+            MboxPool& P = MboxPool::get();
+            std::lock_guard<std::mutex> lk(P.mu);
+            P.free_own.emplace(device, std::make_pair(mbox_own, mbox_kind));
+        }
+        mbox_own = nullptr;
+        for (auto& m : mbox_peer) m = nullptr;
         if (comm) {
             ncclResult_t ae = ncclSuccess;
             const bool async_err = ncclCommGetAsyncError(comm, &ae) != ncclSuccess || ae != ncclSuccess;
@@ -1891,7 +1917,7 @@ static bool batchable(const Session& S, int cls) {
     const bool bf_ok = !S.any_bf || (S.world == 1 && S.bf_batch);
     // pod-affinity classes: placement 7 (anti-affinity predicates only), one GPU, no Backfilled nodes
     const bool aff_ok = !c.aff || (S.aff_batch && S.world == 1 && !S.any_bf && aff_batchable(c));
-    return S.batched && (S.world == 1 || S.comm || S.xgfn) && bf_ok && !c.backfill && aff_ok &&
+    return S.batched && (S.world == 1 || S.comm || S.xgfn || S.mbox_own) && bf_ok && !c.backfill && aff_ok &&
            S.n_total < (1 << 25);
 }
 
@@ -1939,7 +1965,21 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
     const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
-    if (S.world > 1) {  // node-array shard: sweep -> all-gather of the shards' lists -> identical placement
+    if (S.world > 1 && S.mbox_own) {  // node-array shard, peer mailboxes: no host step between the two kernels
+        MboxArgs mb{};
+        for (int p = 0; p < S.world; ++p) mb.dst[p] = S.mbox_peer[p];
+        mb.rank = S.rank;
+        mb.world = S.world;
+        mb.seq = ++S.mbox_seq;
+        S.stats.collectives++;
+        HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
+                                S.d_arrive, out, S.stream, 3, kf, S.fit_set[kMaxDep + 1], nullptr, &mb));
+        S.fit_set[kMaxDep + 1] ^= 1;
+        const int slot = (int)(mb.seq & (kMboxSlots - 1));
+        HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
+                                  &S.mbox_own->msg[slot][0], S.world, out, S.stream, &S.mbox_own->flag[slot][0][0],
+                                  mb.seq));
+    } else if (S.world > 1) {  // node-array shard: sweep -> all-gather of the shards' lists -> identical placement
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
                                 S.d_arrive, out, S.stream, 3, kf, S.fit_set[kMaxDep + 1], S.d_shard_send));
         if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));  // timed: the shard's sweep kernel
@@ -4037,6 +4077,67 @@ int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) 
         kbhip::comm_add(key, s->s.rank, s->s.world, s->s.device, c);
         s->s.comm = c;
         s->s.comm_pooled = true;
+        return KBHIP_OK;
+    })
+}
+int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx) {
+    ABI_GUARD_S(s, {
+        if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::Session& S = s->s;
+        if (S.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        if (S.mbox_own) throw kbhip::Error(KBHIP_EINVAL, "session already has a mailbox");
+        HIPCHK(hipSetDevice(S.device));
+        using kbhip::Mailbox;
+        {  // this rank's mailbox: the pooled one of this device, else a new allocation (uncached memory,
+           // else fine-grained, else default) that can be exported
+            kbhip::MboxPool& P = kbhip::MboxPool::get();
+            std::lock_guard<std::mutex> lk(P.mu);
+            auto it = P.free_own.find(S.device);
+            if (it != P.free_own.end()) {
+                S.mbox_own = it->second.first;
+                S.mbox_kind = it->second.second;
+                P.free_own.erase(it);
+            }
+        }
+        hipIpcMemHandle_t h;
+        if (!S.mbox_own) {
+            const unsigned kinds[3] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained, hipDeviceMallocDefault};
+            for (int k = 0; k < 3 && !S.mbox_own; ++k) {
+                void* p = nullptr;
+                if (hipExtMallocWithFlags(&p, sizeof(Mailbox), kinds[k]) != hipSuccess) { (void)hipGetLastError(); continue; }
+                if (hipIpcGetMemHandle(&h, p) != hipSuccess) {
+                    (void)hipGetLastError();
+                    (void)hipFree(p);
+                    continue;
+                }
+                S.mbox_own = (Mailbox*)p;
+                S.mbox_kind = k;
+            }
+            if (!S.mbox_own) throw kbhip::Error(KBHIP_EDEVICE, "no exportable device memory for the shard mailbox");
+        }
+        HIPCHK(hipIpcGetMemHandle(&h, S.mbox_own));
+        HIPCHK(hipMemsetAsync(S.mbox_own, 0, sizeof(Mailbox), S.stream));  // flags 0: no pop yet
+        HIPCHK(hipStreamSynchronize(S.stream));
+        // the handles of every rank (the gather also orders every rank's zeroing before any pop)
+        vector<uint8_t> recv(sizeof(h) * (size_t)S.world);
+        if (fn(ctx, &h, recv.data(), (int64_t)sizeof(h)) != 0)
+            throw kbhip::Error(KBHIP_EDEVICE, "mailbox handle all-gather callback failed");
+        for (int p = 0; p < S.world; ++p) {
+            if (p == S.rank) { S.mbox_peer[p] = S.mbox_own; continue; }
+            const string key((const char*)recv.data() + sizeof(h) * (size_t)p, sizeof(h));
+            kbhip::MboxPool& P = kbhip::MboxPool::get();
+            std::lock_guard<std::mutex> lk(P.mu);
+            auto it = P.opened.find(key);
+            if (it == P.opened.end()) {
+                hipIpcMemHandle_t ph;
+                std::memcpy(&ph, key.data(), sizeof(ph));
+                void* ptr = nullptr;
+                HIPCHK(hipIpcOpenMemHandle(&ptr, ph, hipIpcMemLazyEnablePeerAccess));
+                it = P.opened.emplace(key, ptr).first;
+            }
+            S.mbox_peer[p] = (Mailbox*)it->second;
+        }
+        S.mbox_seq = 0;
         return KBHIP_OK;
     })
 }

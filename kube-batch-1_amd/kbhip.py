@@ -29,7 +29,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
-           "kbhip_session_carry_events")
+           "kbhip_session_carry_events", "kbhip_shard_connect_mailbox")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64, RED_SUM_I64 = 0, 1, 2, 3
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_shard_connect_rccl.argtypes = [vp, vp, i64]
         L.kbhip_shard_connect_host.argtypes = [vp, ALLREDUCE_FN, vp]
         L.kbhip_shard_connect_host_gather.argtypes = [vp, ALLGATHER_FN, vp]
+        L.kbhip_shard_connect_mailbox.argtypes = [vp, ALLGATHER_FN, vp]
         L.kbhip_read_nodes.argtypes = [vp, vp, i64]
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]
@@ -444,3 +445,19 @@ class ShardedSession(Session):
                     return 1
             self._gcb = ALLGATHER_FN(gcb)
             _check(lib().kbhip_shard_connect_host_gather(self._h, self._gcb, None))
+
+    def connect_mailbox(self, gather) -> None:
+        """Peer mailboxes for the batched pops (kbhip_shard_connect_mailbox):
+        gather(send, recv) all-gathers the ranks' IPC handles once."""
+        world = self.info()[1]
+
+        def mcb(_ctx, send, recv, nbytes):
+            try:
+                s_arr = np.ctypeslib.as_array(ctypes.cast(send, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes,))
+                r_arr = np.ctypeslib.as_array(ctypes.cast(recv, ctypes.POINTER(ctypes.c_uint8)), shape=(nbytes * world,))
+                gather(s_arr.copy(), r_arr)
+                return 0
+            except Exception:
+                return 1
+        cb = ALLGATHER_FN(mcb)
+        _check(lib().kbhip_shard_connect_mailbox(self._h, cb, None))

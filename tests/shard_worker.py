@@ -30,7 +30,10 @@ def main():
     mark("process group formed")
     with kbhip.ShardedSession(path, 0, rank, world) as s:
         mark("session open")
-        s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched else None)
+        exchange = os.environ.get("KBHIP_TEST_EXCHANGE", "host")
+        s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched and exchange == "host" else None)
+        if batched and exchange == "mailbox":  # batched pops through the peer mailboxes
+            s.connect_mailbox(kbhip.torch_gather())
         info = s.info()
         pod, node, kind = s.run_actions(actions)
         mark("actions done")
@@ -38,8 +41,16 @@ def main():
         close = s.gang_unschedulable()
     dist.barrier()
     dist.destroy_process_group()
+    import hashlib
+
+    import numpy as np
+    status = np.where(np.asarray(kind) == 1, 4, 8)
+    digest = hashlib.sha256(np.stack([pod, node, status]).astype(np.int32).tobytes()).hexdigest()
+    full = os.environ.get("KBHIP_TEST_DIGEST_ONLY") is None
     with open(out, "w") as f:
-        json.dump({"info": info, "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)],
+        json.dump({"info": info, "n": int(len(pod)), "log_sha256": digest,
+                   "head": [[int(a), int(b), int(k)] for a, b, k in zip(pod[:64], node[:64], kind[:64])],
+                   "log": [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)] if full else None,
                    "batched_pops": st["batched_pops"], "sweeps": st["sweeps"], "collectives": st["collectives"],
                    "close": close}, f)
 

@@ -16,11 +16,11 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _run_ranks(script, world, tmp_path, extra, timeout=300):
+def _run_ranks(script, world, tmp_path, extra, timeout=300, env=None):
     import uuid
     init = str(tmp_path / f"init_{world}_{uuid.uuid4().hex}")  # a fresh rendezvous file per group
     outs = [str(tmp_path / f"out{r}.json") for r in range(world)]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env or {}))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, script)] + extra(r, init, outs[r]), env=env)
              for r in range(world)]
     try:
@@ -65,7 +65,7 @@ def test_shard_ranges_partition(engine_lib):
             assert all(hi - lo in (n // world, n // world + 1) for lo, hi in rs)
 
 
-def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, exp=None):
+def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, exp=None, exchange="host"):
     p = str(tmp_path / "s.kbs")
     c.write(p)
     if exp is None:
@@ -73,7 +73,8 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, e
     # the gang plugin's close messages (FitError histograms summed over the shards)
     exp_close = oracle_mod.ref_gang_close(p) if actions == "allocate" else None
     res = _run_ranks("shard_worker.py", world, tmp_path,
-                     lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=240)
+                     lambda r, init, out: [p, str(r), str(world), init, out, actions, str(batched)], timeout=240,
+                     env={"KBHIP_TEST_EXCHANGE": exchange})
     n_nodes = len(c.nodes)
     import kbhip
     for r in range(world):
@@ -110,23 +111,26 @@ def test_sharded_close_messages_gpu(engine, oracle_mod, kbgen_mod, tmp_path, see
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["host", "mailbox"])
 @pytest.mark.parametrize("seed", range(8))
-def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
-    """Batched-path features only (no pod affinity / backfill): every pop is one all-gather."""
+def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, exchange):
+    """Batched-path features only (no pod affinity / backfill): every pop is
+    one exchange — a host all-gather, or the peer mailboxes (kernels only)."""
     from test_gpu_parity import NO_POD_AFFINITY
     feats = tuple(f for f in NO_POD_AFFINITY if f != "backfill")
     c = kbgen_mod.gen_random(2400 + seed, n_nodes=10 + seed * 7, n_jobs=8, max_tasks=8, features=feats,
                              tiers=[["priority", "gang", "conformance"], ["drf", "predicates", "proportion",
                                                                            "nodeorder"]])
-    res = _shard_case(oracle_mod, tmp_path, c, 2 + seed % 3)
+    res = _shard_case(oracle_mod, tmp_path, c, 2 + seed % 3, exchange=exchange)
     assert all(r["batched_pops"] > 0 for r in res)
 
 
 @pytest.mark.gpu
-def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
-    """C4 shape at 20k nodes (2 and 3 ranks sharing the GPU over gloo): the
-    shard logs equal the one-GPU session's, and every batched pop is exactly
-    one collective (one all-gather)."""
+@pytest.mark.parametrize("exchange", ["host", "mailbox"])
+def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path, exchange):
+    """C4 shape at 20k nodes (2 and 3 ranks sharing the GPU): the shard logs
+    and close messages equal the one-GPU session's, and every batched pop is
+    exactly one exchange (one all-gather over gloo, or one mailbox round)."""
     p = str(tmp_path / "c4s.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=60000)
     with engine.Session(p) as s:
@@ -137,13 +141,39 @@ def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     assert st1["batched_pops"] == st1["sweeps"] > 1000
     for world in (2, 3):
         res = _run_ranks("shard_worker.py", world, tmp_path,
-                         lambda r, init, out: [p, str(r), str(world), init, out, "allocate", "1"], timeout=240)
+                         lambda r, init, out: [p, str(r), str(world), init, out, "allocate", "1"], timeout=240,
+                         env={"KBHIP_TEST_EXCHANGE": exchange})
         for r in range(world):
             got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
             assert got == exp, f"world {world} rank {r}"
             assert res[r]["close"] == close1, f"world {world} rank {r}"
             assert res[r]["batched_pops"] == st1["batched_pops"]
             assert res[r]["collectives"] == res[r]["batched_pops"]  # one all-gather per pop, nothing else
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exchange", ["host", "mailbox"])
+def test_sharded_c4_full_size_gpu(engine, kbgen_mod, tmp_path, exchange):
+    """BASELINE.json's sharded config at full size: the bench snapshot (100k
+    nodes x 1M pods) on 2 ranks sharing the GPU; every rank's placement log
+    equals the pinned digest of the CPU oracle's (tests/golden/fullsize.json,
+    as tests/test_gpu_fullsize.py checks the one-GPU session) and every
+    batched pop is exactly one exchange."""
+    import hashlib
+    gold = json.load(open(os.path.join(HERE, "golden", "fullsize.json")))["c4"]
+    p = str(tmp_path / "c4.kbs")
+    kbgen_mod.gen_c4(p)
+    with open(p, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == gold["snap_sha256"]
+    res = _run_ranks("shard_worker.py", 2, tmp_path,
+                     lambda r, init, out: [p, str(r), "2", init, out, "allocate", "1"], timeout=420,
+                     env={"KBHIP_TEST_EXCHANGE": exchange, "KBHIP_TEST_DIGEST_ONLY": "1"})
+    for r in range(2):
+        assert res[r]["n"] == gold["n"]
+        assert [[a, b, 4 if k == 1 else 8] for a, b, k in res[r]["head"]] == gold["head"][:64]
+        assert res[r]["log_sha256"] == gold["log_sha256"], f"rank {r}"
+        assert res[r]["batched_pops"] > 20000
+        assert res[r]["collectives"] == res[r]["batched_pops"]
 
 
 @pytest.mark.gpu
