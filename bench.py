@@ -13,8 +13,10 @@ every session re-snapshots the cache).
 N > 1: one process per GPU (torch.distributed over RCCL for the barrier and
 the max-over-ranks time).  Default --mode shard: ONE C4 session node-sharded
 over the GPUs: per batched pop each rank sweeps its node
-range to its top-64 with rows, one ncclAllGather, and every rank runs the
-same placement (strong scaling).  --mode replicas: N independent sessions.
+range to its top-64 with rows and writes them into every rank's mailbox over
+xGMI (--exchange mailbox, default; --exchange rccl: one ncclAllGather), and
+every rank runs the same placement (strong scaling).  --mode replicas: N
+independent sessions.
 
 Also reported:
 * roofline of the fused pop kernel (k_pop_batch_ov: sweep + top-64 + placement):
@@ -68,7 +70,15 @@ def parse():
                     help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
                          "each shard sweeps its node range to its top-64, one RCCL all-gather, identical placement "
                          "on every shard), or N independent replica sessions")
-    return ap.parse_args()
+    ap.add_argument("--exchange", choices=("mailbox", "rccl"), default="mailbox",
+                    help="shard mode: batched pops exchange their top-64 lists through peer mailboxes written by "
+                         "the kernels over xGMI (default; kbhip_shard_connect_mailbox), or one ncclAllGather per pop")
+    args = ap.parse_args()
+    EXCHANGE_MODE[0] = args.exchange
+    return args
+
+
+EXCHANGE_MODE = ["mailbox"]
 
 
 # Rehearsal knobs (not used by the driver's runs): KBHIP_BENCH_BACKEND=gloo and
@@ -185,9 +195,11 @@ def open_sharded(buf, device, rank, world, dist):
             if ok:  # this rank's engine communicator formed: drop it, so every rank exchanges the same way
                 s.close()
                 s = kbhip.ShardedSession(buf, device, rank, world)
+    dev = f"cuda:{device}" if BACKEND == "nccl" else None
     if EXCHANGE[0] != "rccl":
-        dev = f"cuda:{device}" if BACKEND == "nccl" else None
         s.connect_host(kbhip.torch_exchange(device=dev), kbhip.torch_gather(device=dev))
+    if EXCHANGE_MODE[0] == "mailbox":  # batched pops: peer mailboxes; the all-reduce above stays for per-task pops
+        s.connect_mailbox(kbhip.torch_gather(device=dev))
     return s
 
 
@@ -297,7 +309,8 @@ def main():
                    "device_period_us": period_us,  # allocate's device span / batched launches (launches overlap)
                    "parallelism": (f"node-sharded x{world}" if shard else f"replicas x{world}") if world > 1
                    else "1 GPU",
-                   "exchange": EXCHANGE[0] if shard else None},
+                   "exchange": (f"peer mailboxes (per-task pops: {EXCHANGE[0]})" if EXCHANGE_MODE[0] == "mailbox"
+                                else EXCHANGE[0]) if shard else None},
         "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,

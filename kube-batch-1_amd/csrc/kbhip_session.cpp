@@ -1974,6 +1974,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.stats.collectives++;
         HIPCHK(launch_pop_batch(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, S.d_cand2,
                                 S.d_arrive, out, S.stream, 3, kf, S.fit_set[kMaxDep + 1], nullptr, &mb));
+        if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));  // timed: the shard's sweep kernel
         S.fit_set[kMaxDep + 1] ^= 1;
         const int slot = (int)(mb.seq & (kMboxSlots - 1));
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
