@@ -859,44 +859,73 @@ __device__ __forceinline__ T load_words_sys(const T* src) {
     return v;
 }
 
-// The shard epilogue of k_pop_batch (placement 3): wave 0 of the final merger
-// writes this shard's top-64 with their rows and the sweep's FitDelta counts
-// — to its own exchange buffer (msg, for the all-gather), or straight into
-// every rank's mailbox (mb.world > 0): the 64 candidates per destination,
-// the wave's stores drained, then one flag word per destination (lane p
-// writes rank p's), read by k_shard_place with system-scope loads.
+// 16-byte system-scope store (sc0 sc1, a vector store): mailbox payload.
+typedef unsigned int kb_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sys16(void* p, kb_u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
+// The shard epilogue of k_pop_batch (placement 3), run by every thread of
+// the final merger: this shard's top-64 (wave 0 lane j: candidate j) with
+// their rows and the sweep's FitDelta counts go to its own exchange buffer
+// (msg, for the all-gather), or straight into every rank's mailbox (mb.world
+// > 0): the candidates are staged in LDS, every thread of the block stores
+// its share of (destination, candidate, 16-byte chunk) — a class without
+// host ports leaves the port words out — each wave drains its stores, the
+// block meets, and lane p of wave 0 raises rank p's flag.  k_shard_place
+// reads them with system-scope loads.
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
                            uint32_t fit_raw, ShardMsg* msg, const MboxArgs& mb) {
-    const int lane = threadIdx.x & 63;
-    ShardCand e{};
-    e.node = -1;
-    if (K) {
-        const int g = key_idx(K);
-        const int n = g - nc.base;
-        e.key = K;
-        e.node = g;
-        e.row = load_row(nc, n);
-        if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
-        e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+    __shared__ ShardCand s_c[kTopK];
+    __shared__ uint64_t s_fit[2];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave == 0) {
+        ShardCand e{};
+        e.node = -1;
+        if (K) {
+            const int g = key_idx(K);
+            const int n = g - nc.base;
+            e.key = K;
+            e.node = g;
+            e.row = load_row(nc, n);
+            if (c.has_ports)
+                for (int w = 0; w < port_win(c, nc); ++w) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
+            e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+        }
+        const uint32_t sweep = fit_sum(fit_raw);  // count b in lane b
+        if (mb.world == 0) {
+            msg->c[lane] = e;
+            if (lane < 4) msg->fit[lane] = sweep;
+            return;
+        }
+        s_c[lane] = e;
+        if (lane == 0) {
+            s_fit[0] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 0) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 1) << 32;
+            s_fit[1] = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 2) |
+                       (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 3) << 32;
+        }
     }
-    const uint32_t sweep = fit_sum(fit_raw);  // count b in lane b
-    if (mb.world == 0) {
-        msg->c[lane] = e;
-        if (lane < 4) msg->fit[lane] = sweep;
-        return;
-    }
+    if (mb.world == 0) return;  // (uniform)
+    __syncthreads();
     const int slot = (int)(mb.seq & (kMboxSlots - 1));
-    const uint64_t f01 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 0) |
-                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 1) << 32;
-    const uint64_t f23 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 2) |
-                         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)sweep, 3) << 32;
-    for (int p = 0; p < mb.world; ++p) {
+    constexpr int kChunks = (int)(sizeof(ShardCand) / 16);
+    constexpr int kPortChunks = (int)(sizeof(((ShardCand*)nullptr)->pw) / 16);  // the last chunks
+    const int chunks = c.has_ports ? kChunks : kChunks - kPortChunks;
+    const int items = mb.world * kTopK * chunks;
+    for (int i = threadIdx.x; i < items; i += kPopThreads) {
+        const int p = i / (kTopK * chunks), rem = i - p * (kTopK * chunks);
+        const int j = rem / chunks, q = rem - j * chunks;
         ShardMsg* m = &mb.dst[p]->msg[slot][mb.rank];
-        store_words_sys(&m->c[lane], e);
-        if (lane == 0) { st_sys((uint64_t*)m->fit, f01); st_sys((uint64_t*)m->fit + 1, f23); }
+        st_sys16((char*)&m->c[j] + 16 * q, *(const kb_u32x4*)((const char*)&s_c[j] + 16 * q));
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's message stores completed
-    if (lane < mb.world) st_sys(&mb.dst[lane]->flag[slot][mb.rank][0], (uint64_t)mb.seq);
+    if (threadIdx.x < mb.world) {
+        ShardMsg* m = &mb.dst[threadIdx.x]->msg[slot][mb.rank];
+        st_sys((uint64_t*)m->fit, s_fit[0]);
+        st_sys((uint64_t*)m->fit + 1, s_fit[1]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's mailbox stores completed
+    __syncthreads();                                   // ... and every other wave's
+    if (threadIdx.x < mb.world) st_sys(&mb.dst[threadIdx.x]->flag[slot][mb.rank][0], (uint64_t)mb.seq);
 }
 }  // namespace kbhip

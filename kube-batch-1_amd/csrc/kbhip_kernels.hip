@@ -356,7 +356,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     __syncthreads();
     if constexpr (PL == 3) {  // node-array shard: emit the shard's list, the placement runs after the exchange
-        if (wave == 0) shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg, mb);
+        shard_emit(cf, nc, t, c, wl[0][lane], fit_raw, smsg, mb);
         return;
     } else if constexpr (PL == 6) {  // Backfilled nodes in the session
         if (wave != 0) return;
@@ -921,7 +921,10 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
     // every gathered candidate into the node -> entry table; lists merged by waves
     uint64_t acc = 0;
     for (int r = wave; r < world; r += kPopThreads / 64) {
-        const ShardCand e = load_words_sys(&msgs[r].c[lane]);
+        struct { uint64_t key; int32_t node, na; } e;  // the candidate's first 16 bytes
+        const uint64_t w1 = ld_sys((const uint64_t*)&msgs[r].c[lane] + 1);
+        e.key = ld_sys((const uint64_t*)&msgs[r].c[lane]);
+        e.node = (int32_t)(uint32_t)w1;
         if (e.node >= 0) {
             int h = (int)(((uint32_t)e.node * 2654435761u) >> 21);
             while (atomicCAS(&s_hk[h], -1, e.node) != -1) h = (h + 1) & (kShardHash - 1);
