@@ -220,8 +220,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * (placement 6), 0 = per-task sweeps there;
  * "aff_batch" = 1 (default) batches pops of pod anti-affinity classes
  * (placement 7), 0 = per-task sweeps for them;
- * "rank_radix" = 1 orders reclaim / preempt walks with the library radix sort
- * instead of the counting sort (tests);
+ * "rank_radix" = 1 orders reclaim / preempt walks with the wide-range radix
+ * passes (four 8-bit counting passes over the score) instead of the one-pass
+ * counting sort (tests);
  * "rank_group" = 1 makes this session one of a group of what-if sessions run
  * from concurrent host threads: their reclaim / preempt node rankings are
  * batched into shared launches (blockIdx.y = session; kbhip_stats

@@ -12,12 +12,11 @@
 // the order: one HBM sweep writes a key per node — pack_key(score, idx) for
 // preempt (descending = SelectBestNode order), pack_key(0, idx) for reclaim —
 // zero for a node that fails; a stable counting sort over the class's small
-// score range orders them (launch_rank_sorted; a library radix sort only for
-// classes whose score range exceeds 256 values), and the host reads the
-// passing prefix back.  Traffic per task: the per-task sweep's
+// score range orders them (launch_rank_sorted; classes whose score range
+// exceeds 256 values: four stable 8-bit counting passes over the score,
+// launch_rank_radix), and the host reads the passing prefix back.  Traffic per task: the per-task sweep's
 // B_node bytes per node + 8 B written per node + the sort's passes over 8 B keys.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "kbhip_eval.h"
 #include "kbhip_internal.h"
@@ -116,8 +115,76 @@ hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables
     return hipGetLastError();
 }
 
-hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int n, hipStream_t st) {
-    return hipcub::DeviceRadixSort::SortKeysDescending(tmp, *tmp_bytes, in, out, n, 0, 64, st);
+// ---------------------------------------------------------------------------
+// Wide score ranges: an LSD radix sort of the passing nodes' keys by their
+// score, 8 bits per pass from the lowest, digits taken descending; every
+// pass is a stable counting sort (per-block digit counts, one scan, a
+// scatter that keeps the order within a block by wave ballots), so ties in
+// score keep the node order of the first pass's input (index ascending): the
+// result is the descending key order, as util.SelectBestNode walks it.
+// Pass 0 reads k_rank_nodes' keys (0 = failing node, dropped), later passes
+// the previous pass's output (count[0] entries).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int radix_digit(uint64_t k, int shift) {  // 0 = best (highest score digit)
+    return 255 - (int)(((uint32_t)(k >> 32) >> shift) & 255u);
+}
+__global__ __launch_bounds__(kBlock) void k_radix_bucket(const uint64_t* in, int n_in, const uint32_t* count,
+                                                         int shift, uint32_t* hist, int nblk) {
+    __shared__ uint32_t s_h[256];
+    for (int i = threadIdx.x; i < 256; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+    const int n = count ? (int)count[0] : n_in;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t k = i < n ? in[i] : 0;
+    if (k) atomicAdd(&s_h[radix_digit(k, shift)], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < 256; b += kBlock) hist[(size_t)b * nblk + blockIdx.x] = s_h[b];
+}
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* in, int n_in, const uint32_t* count,
+                                                          int shift, const uint32_t* offs, int nblk, uint64_t* out) {
+    __shared__ uint32_t s_cnt[kBlock / 64][256];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = lane; i < 256; i += 64) s_cnt[wave][i] = 0;
+    const int n = count ? (int)count[0] : n_in;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const uint64_t k = i < n ? in[i] : 0;
+    const int b = k ? radix_digit(k, shift) : -1;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t rank = 0;
+    __builtin_amdgcn_wave_barrier();
+    for (uint64_t todo = __ballot(b >= 0); todo;) {
+        const int bv = __builtin_amdgcn_readlane(b, __ffsll((unsigned long long)todo) - 1);
+        const uint64_t m = __ballot(b == bv);
+        if (b == bv) rank = __popcll(m & lt);
+        if (lane == 0) s_cnt[wave][bv] = __popcll(m);
+        todo &= ~m;
+    }
+    __syncthreads();
+    if (b >= 0) {
+        uint32_t base = offs[(size_t)b * nblk + blockIdx.x];
+        for (int w = 0; w < wave; ++w) base += s_cnt[w][b];
+        out[base + rank] = k;
+    }
+}
+__global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n);
+
+hipError_t launch_rank_radix(const uint64_t* keys, int n, const uint32_t* count, uint32_t* hist, uint64_t* tmp,
+                             uint64_t* sorted, hipStream_t st) {
+    const int nblk = (n + kBlock - 1) / kBlock;
+    if (nblk < 1) return hipSuccess;
+    // pass 0: keys -> sorted, 1: sorted -> tmp, 2: tmp -> sorted, 3: sorted -> tmp ... ending in sorted
+    const uint64_t* in = keys;
+    uint64_t* bufs[2] = {tmp, sorted};
+    for (int p = 0; p < 4; ++p) {
+        uint64_t* out = bufs[(p + 1) & 1];
+        const uint32_t* cnt = p == 0 ? nullptr : count;  // pass 0 drops the failing nodes' zero keys
+        hipLaunchKernelGGL(k_radix_bucket, dim3(nblk), dim3(kBlock), 0, st, in, n, cnt, 8 * p, hist, nblk);
+        hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, st, hist, 256 * nblk);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(kBlock), 0, st, in, n, cnt, 8 * p, (const uint32_t*)hist,
+                           nblk, out);
+        in = out;
+    }
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -38,12 +38,15 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 
 // Reclaim / preempt (kbhip_evict.hip): per-node order keys of the task of
 // ctrl->cls[0] (by_score 1: predicates + score, preempt; 0: predicates only,
-// reclaim), *count += passing nodes; descending radix sort of the keys
-// (tmp == nullptr: *tmp_bytes <- the scratch size); one node-row update
-// (op 0 evict, 1 pipeline, 2 unpipeline).
+// reclaim), *count += passing nodes; one node-row update (op 0 evict, 1
+// pipeline, 2 unpipeline).
 hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
                              int by_score, uint64_t* keys, uint32_t* count, hipStream_t st);
-hipError_t sort_keys_desc(void* tmp, size_t* tmp_bytes, const uint64_t* in, uint64_t* out, int n, hipStream_t st);
+// Wide score ranges: the passing keys of launch_rank_nodes (n keys, zeros
+// dropped; *count = passing nodes) sorted descending by four stable 8-bit
+// counting passes over the score (hist: rank_hist_words(n) words; tmp: n keys).
+hipError_t launch_rank_radix(const uint64_t* keys, int n, const uint32_t* count, uint32_t* hist, uint64_t* tmp,
+                             uint64_t* sorted, hipStream_t st);
 // The walk order by a hand-written stable counting sort over the score (class
 // score range [slo, shi] of at most 256 values; hipErrorInvalidValue beyond):
 // keys, sorted (descending key order), *count += passing nodes; hist holds

@@ -422,13 +422,13 @@ struct Session {
     int any_bf = 0;
     bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
-    DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt;
+    DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt, b_rank_radix;
     DevBuf b_tab_idx;  // count-table deltas (flush_tables)
     size_t rank_tmp_bytes = 0;
     uint64_t* h_rank = nullptr;  // pinned: [0] = count, then sorted keys
     size_t h_rank_cap = 0;
     int rank_first = 2048;  // sorted keys read back with the count (option "rank_first"); the rest on demand
-    bool force_radix = false;  // option "rank_radix": the library radix sort for every class (tests)
+    bool force_radix = false;  // option "rank_radix": the wide-range radix passes for every class (tests)
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
     bool aff_batch = true;     // option "aff_batch": batched pops (placement 7) of anti-affinity classes
     bool rank_group = false;   // option "rank_group": node rankings batched with concurrent sessions (RankBatcher)
@@ -589,6 +589,7 @@ struct Session {
         for (DevBuf* b : {&b_labels, &b_taints, &b_ports, &b_classes, &b_terms, &b_reqs, &b_vals, &b_valint, &b_valok,
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
                           &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt,
+                          &b_rank_radix,
                           &b_shard_send, &b_shard_recv, &b_tab_idx})
             b->release();
         for (auto& b : b_cand_ov) b.release();
@@ -2963,11 +2964,9 @@ struct Allocator {
             S.b_rank_keys.alloc<uint64_t>(N);
             S.b_rank_sorted.alloc<uint64_t>(N);
             S.b_rank_cnt.alloc<uint32_t>(4);
-            size_t tb = 0;
-            HIPCHK(sort_keys_desc(nullptr, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p, N,
-                                  S.stream));
-            S.rank_tmp_bytes = std::max<size_t>({tb, (size_t)16, rank_hist_words(N) * sizeof(uint32_t)});
+            S.rank_tmp_bytes = std::max<size_t>((size_t)16, rank_hist_words(N) * sizeof(uint32_t));
             S.b_rank_tmp.alloc<uint8_t>(S.rank_tmp_bytes);
+            S.b_rank_radix.alloc<uint64_t>(std::max(N, 1));
             S.h_rank = (uint64_t*)MemPool::get().take(MemPool::kPinned, (size_t)(N + 1) * sizeof(uint64_t),
                                                       &S.h_rank_cap);
         }
@@ -3009,12 +3008,12 @@ struct Allocator {
             HIPCHK(launch_rank_sorted(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first, (int)sr.second,
                                       (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
                                       (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p, S.stream));
-        } else {  // wide score ranges (large nodeorder weights): library radix sort of the 64-bit keys
+        } else {  // wide score ranges (large nodeorder weights): 8-bit LSD radix passes over the score
             HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (uint64_t*)S.b_rank_keys.p,
                                      (uint32_t*)S.b_rank_cnt.p, S.stream));
-            size_t tb = S.rank_tmp_bytes;
-            HIPCHK(sort_keys_desc(S.b_rank_tmp.p, &tb, (const uint64_t*)S.b_rank_keys.p, (uint64_t*)S.b_rank_sorted.p,
-                                  N, S.stream));
+            HIPCHK(launch_rank_radix((const uint64_t*)S.b_rank_keys.p, N, (const uint32_t*)S.b_rank_cnt.p,
+                                     (uint32_t*)S.b_rank_tmp.p, (uint64_t*)S.b_rank_radix.p,
+                                     (uint64_t*)S.b_rank_sorted.p, S.stream));
         }
         const int first = std::min(N, S.rank_first);
         HIPCHK(hipMemcpyAsync(S.h_rank, S.b_rank_cnt.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));

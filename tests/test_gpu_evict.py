@@ -190,7 +190,7 @@ def test_evict_golden_vectors_gpu(engine, case):
 @pytest.mark.parametrize("seed", range(4))
 def test_rank_sort_paths(engine, oracle_mod, kbgen_mod, tmp_path, radix, seed):
     """The walk order of reclaim / preempt: the hand-written counting sort over a
-    class's score range (default) and the library radix sort (option rank_radix,
+    class's score range (default) and the wide-range radix passes (option rank_radix,
     kept for score ranges beyond 256 values) both give the oracle's records, on
     node counts that span many sort blocks and waves."""
     c = kbgen_mod.gen_preempt(700 + seed, n_nodes=300 + 170 * seed, n_queues=2 + seed % 3, n_run_jobs=40,
@@ -205,3 +205,23 @@ def test_rank_sort_paths(engine, oracle_mod, kbgen_mod, tmp_path, radix, seed):
         ns = s.read_nodes(s.stats()["nodes"])
     assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, node, kind)] == exp.as_list()
     assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_rank_wide_score_range(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Large nodeorder weights (plain Atoi arguments, nodeorder.go:209-246):
+    a class's score range exceeds the counting sort's 256 values, so preempt's
+    walk order comes from the radix passes without any option; records and
+    node state equal the oracle's."""
+    c = kbgen_mod.gen_preempt(760 + seed, n_nodes=200 + 90 * seed, n_queues=2, n_run_jobs=30, n_pend_jobs=5,
+                              max_tasks=5, tiers=TIERS[seed % len(TIERS)])
+    c.args = {"nodeorder": {"leastrequested.weight": str([1000, 70000, 3, 123456][seed]),
+                            "balancedresource.weight": str([-7, 500, 1000000, 2][seed])}}
+    p = c.write(str(tmp_path / "w.kbs"))
+    exp, ons = oracle_mod.ref_allocate(p, actions="preempt, reclaim", with_nodes=True)
+    with engine.Session(p) as s:
+        pod, node, kind = s.run_actions("preempt, reclaim")
+        ns = s.read_nodes(s.stats()["nodes"])
+    assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, node, kind)] == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
+
