@@ -35,6 +35,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <unistd.h>
+
 #include "../../include/kbhip.h"
 #include "../../include/kbsnap.h"
 #include "kbhip_affinity.h"
@@ -4118,13 +4120,21 @@ int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx)
         HIPCHK(hipIpcGetMemHandle(&h, S.mbox_own));
         HIPCHK(hipMemsetAsync(S.mbox_own, 0, sizeof(Mailbox), S.stream));  // flags 0: no pop yet
         HIPCHK(hipStreamSynchronize(S.stream));
-        // the handles of every rank (the gather also orders every rank's zeroing before any pop)
-        vector<uint8_t> recv(sizeof(h) * (size_t)S.world);
-        if (fn(ctx, &h, recv.data(), (int64_t)sizeof(h)) != 0)
+        // every rank's record: its handle, process id and pointer (ranks of one process — threads
+        // driving several shard sessions — use each other's pointers directly); the gather also
+        // orders every rank's zeroing before any pop
+        struct Rec {
+            hipIpcMemHandle_t h;
+            int64_t pid;
+            uint64_t ptr;
+        } mine{h, (int64_t)getpid(), (uint64_t)(uintptr_t)S.mbox_own};
+        vector<Rec> recv((size_t)S.world);
+        if (fn(ctx, &mine, recv.data(), (int64_t)sizeof(Rec)) != 0)
             throw kbhip::Error(KBHIP_EDEVICE, "mailbox handle all-gather callback failed");
         for (int p = 0; p < S.world; ++p) {
             if (p == S.rank) { S.mbox_peer[p] = S.mbox_own; continue; }
-            const string key((const char*)recv.data() + sizeof(h) * (size_t)p, sizeof(h));
+            if (recv[p].pid == (int64_t)getpid()) { S.mbox_peer[p] = (Mailbox*)(uintptr_t)recv[p].ptr; continue; }
+            const string key((const char*)&recv[p].h, sizeof(h));
             kbhip::MboxPool& P = kbhip::MboxPool::get();
             std::lock_guard<std::mutex> lk(P.mu);
             auto it = P.opened.find(key);
