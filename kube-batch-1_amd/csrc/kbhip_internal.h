@@ -22,6 +22,8 @@ struct DevTables {
     int32_t* aff_scalar;       // PA target totals, session counters
 };
 
+// The per-task path's control block set up on the device (CtrlInit, kbhip_types.h).
+hipError_t launch_ctrl_init(PopCtrl* ctrl, const CtrlInit& ci, hipStream_t st);
 // Per-task sweep; dbg (debug only): per-node keys, raw inter-pod counts,
 // [lo, hi, F, max key]: rows of 2 npad + 4 words per task of the chunk; commit_here = the last block commits (one GPU).  Sharded
 // sessions reduce ctrl->slot[task_i] across shards and then launch_commit_task.

@@ -63,6 +63,59 @@ __global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t,
 // ---------------------------------------------------------------------------
 // per-task path
 // ---------------------------------------------------------------------------
+// The chunk's control block: the request fields from the kernel argument,
+// every per-task counter and result cleared.
+__global__ __launch_bounds__(kBlock) void k_ctrl_init(PopCtrl* ctrl, CtrlInit ci) {
+    const int i = threadIdx.x;
+    if (i == 0) {
+        ctrl->stop = -1;
+        ctrl->n_done = 0;
+        ctrl->ready_count = ci.ready_count;
+        ctrl->min_avail = ci.min_avail;
+        ctrl->gang_mode = ci.gang_mode;
+        ctrl->n_tasks = ci.n_tasks;
+        ctrl->any_bf = ci.any_bf;
+        ctrl->fallback = ci.fallback;
+        ctrl->mode = ci.mode;
+        ctrl->pad = 0;
+        ctrl->epoch = ci.epoch;
+        ctrl->out = ci.out;
+    }
+    if (i < kMaxChunk) {
+        ctrl->cls[i] = ci.cls[i];
+        ctrl->res_node[i] = -1;
+        ctrl->res_kind[i] = 0;
+        ctrl->arrive[i] = 0;
+        ctrl->slot[i] = 0;
+        ctrl->ipa_lo[i] = 0;
+        ctrl->ipa_hi[i] = 0;
+        for (int q = 0; q < 4; ++q) ctrl->fit[i][q] = 0;
+    }
+}
+hipError_t launch_ctrl_init(PopCtrl* ctrl, const CtrlInit& ci, hipStream_t st) {
+    hipLaunchKernelGGL(k_ctrl_init, dim3(1), dim3(kBlock), 0, st, ctrl, ci);
+    return hipGetLastError();
+}
+
+// The result of task task_i as a self-tagged granule in pinned host memory
+// (the batched path's PopOut format; the host polls instead of copying the
+// control block back): stop after this task, tasks consumed, kind, node; a
+// task that found no node also sends this shard's walk FitDelta counts.
+__device__ void task_granule(PopCtrl* ctrl, int task_i, int kind, int node) {
+    PopOut* out = (PopOut*)ctrl->out;
+    if (!out) return;
+    if (ctrl->stop == 1) {
+        int32_t f[4];
+        for (int q = 0; q < 4; ++q)
+            f[q] = __hip_atomic_load(&ctrl->fit[task_i][q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&out->fit[0], make_fit_granule(ctrl->epoch, f[0], f[1]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&out->fit[1], make_fit_granule(ctrl->epoch, f[2], f[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __hip_atomic_store(&out->g[task_i], make_granule(ctrl->epoch, ctrl->stop, ctrl->n_done, kind, node),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 // Commit of task task_i once ctrl->slot[task_i] holds the winner key over ALL
 // nodes (all shards): result, gang stop, node row (owner only), pod-affinity
 // tables and fallback node (every shard, identically), and the
@@ -88,11 +141,13 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
             }
             ctrl->n_done = task_i + 1;
             if (task_i + 1 == ctrl->n_tasks) ctrl->stop = 0;
+            task_granule(ctrl, task_i, k ? 1 : 0, g);
         } else if (k == 0) {
             ctrl->res_node[task_i] = -1;
             ctrl->res_kind[task_i] = 0;
             ctrl->n_done = task_i + 1;
             ctrl->stop = 1;
+            task_granule(ctrl, task_i, 0, -1);
         } else {
             const int kind = key_kind(k);
             ctrl->res_node[task_i] = g;
@@ -107,6 +162,7 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
             if (ctrl->fallback < 0 || g < ctrl->fallback) ctrl->fallback = g;
             if (c.backfill) ctrl->any_bf = 1;
             after_assign(ctrl, task_i, kind);
+            task_granule(ctrl, task_i, kind, g);
         }
     }
     __syncthreads();

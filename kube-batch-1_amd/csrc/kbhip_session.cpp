@@ -456,8 +456,7 @@ struct Session {
     DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
         b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
     PopCtrl* d_ctrl = nullptr;
-    PopCtrl* h_ctrl = nullptr;  // pinned
-    size_t h_ctrl_cap = 0, h_out_cap = 0;
+    size_t h_out_cap = 0;
     DevBuf b_cand2, b_arrive;
     uint64_t* d_cand2 = nullptr;  // per-block candidate lists of the v2 batched kernel
     uint32_t* d_arrive = nullptr; // its block-arrival counter (reset by the last block)
@@ -577,11 +576,9 @@ struct Session {
         for (auto& pr : ev_ring)
             for (auto& e : pr)
                 if (e) { (void)hipEventDestroy(e); e = nullptr; }
-        if (h_ctrl) MemPool::get().give(MemPool::kPinned, h_ctrl, h_ctrl_cap, device);
         if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
         h_rank = nullptr;
-        h_ctrl = nullptr;
         h_out = nullptr;
         for (int k = 1; k <= kMaxDep; ++k) MemPool::get().give_stream(ov_streams[k], device);
         MemPool::get().give_stream(stream, device);
@@ -1544,7 +1541,6 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     hipStream_t st = S.stream;
     S.d_ctrl = S.b_ctrl.alloc<PopCtrl>(1);
-    S.h_ctrl = (PopCtrl*)MemPool::get().take(MemPool::kPinned, sizeof(PopCtrl), &S.h_ctrl_cap);
     S.d_walk = S.b_walk.alloc<uint64_t>(npl);
     {
         int R2;
@@ -1924,16 +1920,80 @@ static bool batchable(const Session& S, int cls) {
            S.n_total < (1 << 25);
 }
 
-static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
-    BatchLaunch L;
-    L.slot = S.next_slot;
+// The next result slot (pinned, mapped PopOutHost) and its granules' tag.
+static int take_slot(Session& S, uint32_t* epoch) {
+    const int slot = S.next_slot;
     S.next_slot = (S.next_slot + 1) % Session::kSlots;
-    uint32_t& ep = S.slot_epoch[L.slot];
+    uint32_t& ep = S.slot_epoch[slot];
     if (((ep + 1) & 0xffff) == 0) {  // tag wrap: clear this (idle) slot's stale granules, skip tag 0
-        std::memset(S.h_out + L.slot, 0, sizeof(PopOutHost));
+        std::memset(S.h_out + slot, 0, sizeof(PopOutHost));
         ++ep;
     }
-    L.epoch = (++ep) & 0xffff;
+    *epoch = (++ep) & 0xffff;
+    return slot;
+}
+
+// The per-task path's chunk: control block set up on the device (k_ctrl_init,
+// no copy), results as tagged granules in result slot `slot`.
+static void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_avail, int gang, int mode, int slot,
+                       uint32_t epoch) {
+    CtrlInit ci{};
+    ci.ready_count = ready;
+    ci.min_avail = min_avail;
+    ci.gang_mode = gang;
+    ci.n_tasks = m;
+    ci.any_bf = S.any_bf;
+    ci.fallback = S.fallback;
+    ci.mode = mode;
+    ci.epoch = slot >= 0 ? epoch : 0;
+    ci.out = slot >= 0 ? (uint64_t*)((char*)S.d_out + (size_t)slot * sizeof(PopOutHost)) : nullptr;
+    for (int i = 0; i < m; ++i) ci.cls[i] = cls[i];
+    HIPCHK(launch_ctrl_init(S.d_ctrl, ci, S.stream));
+}
+
+// Poll the per-task granules of a chunk (written by commit_task): results up
+// to the task whose granule carries the chunk's stop; fit4 (optional) gets
+// that task's walk FitDelta counts when it found no node.
+static void collect_tasks(Session& S, int slot, uint32_t epoch, int m, int* n_done, int* stop, int32_t* node,
+                          int32_t* kind, int32_t* fit4) {
+    const PopOutHost& o = S.h_out[slot];
+    auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
+    auto tw0 = std::chrono::steady_clock::now();
+    int j = 0, st = -1;
+    for (long spin = 0; j < m && st < 0; ++spin) {
+        const uint64_t g = __atomic_load_n(&o.g[j], __ATOMIC_ACQUIRE);
+        if (tag(g) == epoch) {
+            node[j] = (int32_t)(g & 0xffffffffu) - 1;
+            kind[j] = (int32_t)((g >> 34) & 3);
+            st = (int)((g >> 44) & 0xf) - 1;
+            ++j;
+            spin = 0;
+            continue;
+        }
+        if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(S.stream));  // long waits: runtime (errors)
+        if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "per-task sweeps produced no result");
+        __builtin_ia32_pause();
+    }
+    S.host_wait_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw0).count();
+    *n_done = j;
+    *stop = st;
+    if (fit4 && st == KBHIP_STOP_UNASSIGNED) {
+        uint64_t f0 = 0, f1 = 0;
+        for (long spin = 0;; ++spin) {
+            f0 = __atomic_load_n(&o.fit[0], __ATOMIC_ACQUIRE);
+            f1 = __atomic_load_n(&o.fit[1], __ATOMIC_ACQUIRE);
+            if (tag(f0) == epoch && tag(f1) == epoch) break;
+            if (spin > (1L << 24)) throw Error(KBHIP_EDEVICE, "per-task sweep produced no FitDelta histogram");
+            __builtin_ia32_pause();
+        }
+        fit4[0] = (int32_t)(f0 & 0xffffff); fit4[1] = (int32_t)((f0 >> 24) & 0xffffff);
+        fit4[2] = (int32_t)(f1 & 0xffffff); fit4[3] = (int32_t)((f1 >> 24) & 0xffffff);
+    }
+}
+
+static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
+    BatchLaunch L;
+    L.slot = take_slot(S, &L.epoch);
     L.cls = cls;
     L.m = m;
     L.timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
@@ -2228,51 +2288,42 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             res_kind = S.res_kind_buf;
         } else {
             ov_quiesce(S);
-            PopCtrl& h = *S.h_ctrl;
-            h.stop = -1;
-            h.n_done = 0;
-            h.ready_count = ready_count;
-            h.min_avail = min_avail;
-            h.gang_mode = gang_mode;
-            h.n_tasks = m;
-            h.any_bf = S.any_bf;
-            h.fallback = S.fallback;
-            h.mode = 0;
-            for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[ids[done + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
-            std::memset(h.arrive, 0, sizeof h.arrive);
-            std::memset(h.slot, 0, sizeof h.slot);
-            std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
-            std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
-            std::memset(h.fit, 0, sizeof h.fit);
-            HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+            int cls[kMaxChunk];
+            for (int i = 0; i < m; ++i) cls[i] = S.pods[ids[done + i]].cls;
+            uint32_t epoch = 0;
+            const int slot = take_slot(S, &epoch);
+            ctrl_setup(S, m, cls, ready_count, min_avail, gang_mode, 0, slot, epoch);
             bool defer = S.any_bf != 0;  // a backfill-annotated task may set any_bf on the device mid-chunk
-            for (int i = 0; i < m; ++i) defer = defer || S.classes[h.cls[i]].backfill;
+            for (int i = 0; i < m; ++i) defer = defer || S.classes[cls[i]].backfill;
             for (int i = 0; i < m; ++i) {
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
-                sweep_task(S, i, h.cls[i], defer);
+                sweep_task(S, i, cls[i], defer);
                 if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
             }
             S.stats.sweeps += m;
-            HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
-            HIPCHK(hipStreamSynchronize(S.stream));
+            int32_t fit4[4] = {0, 0, 0, 0};
+            collect_tasks(S, slot, epoch, m, &n_done, &stop_c, S.res_node_buf, S.res_kind_buf, fit4);
             if (S.d_dbg) {
+                HIPCHK(hipStreamSynchronize(S.stream));
                 const size_t row = 2 * (size_t)S.nc.npad + 4;
                 const size_t off = S.dbg_keys.size();
-                S.dbg_keys.resize(off + row * h.n_done);
-                HIPCHK(hipMemcpy(S.dbg_keys.data() + off, S.d_dbg, row * h.n_done * 8, hipMemcpyDeviceToHost));
-                for (int i = 0; i < h.n_done; ++i) S.dbg_pods.push_back(ids[done + i]);
+                S.dbg_keys.resize(off + row * n_done);
+                HIPCHK(hipMemcpy(S.dbg_keys.data() + off, S.d_dbg, row * n_done * 8, hipMemcpyDeviceToHost));
+                for (int i = 0; i < n_done; ++i) S.dbg_pods.push_back(ids[done + i]);
             }
-            n_done = h.n_done;
-            stop_c = h.stop;
             S.last_fit_ok = stop_c == KBHIP_STOP_UNASSIGNED && n_done >= 1;
             if (S.last_fit_ok) {  // this shard's counts of the walk of the task that found no node
-                for (int q = 0; q < 4; ++q) S.last_fit[q] = h.fit[n_done - 1][q];
+                for (int q = 0; q < 4; ++q) S.last_fit[q] = fit4[q];
                 fit_allreduce(S, S.last_fit);
             }
-            ready_c = h.ready_count;
-            any_bf_c = h.any_bf;
-            res_node = h.res_node;
-            res_kind = h.res_kind;
+            int alloc = 0;
+            for (int j = 0; j < n_done; ++j) {
+                alloc += S.res_kind_buf[j] == 1;
+                if (S.res_node_buf[j] >= 0 && S.classes[cls[j]].backfill) any_bf_c = 1;  // IsBackfill commit
+            }
+            ready_c = ready_count + alloc;
+            res_node = S.res_node_buf;
+            res_kind = S.res_kind_buf;
         }
         if (timed) {
             float ms = 0;
@@ -2784,17 +2835,7 @@ struct Allocator {
                 HIPCHK(launch_undo_pop(S.nc, S.tab, cls, 1, nd, kd, S.stream));
                 sess_placed(S, node, -1);  // the fallback node the task saw
             }
-            PopCtrl& h = *S.h_ctrl;
-            h.stop = -1;
-            h.n_done = 0;
-            h.n_tasks = 1;
-            h.mode = 0;
-            h.any_bf = S.any_bf;
-            h.fallback = S.fallback;
-            h.cls[0] = cls;
-            h.ipa_lo[0] = h.ipa_hi[0] = 0;
-            h.slot[0] = 0;
-            HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+            ctrl_setup(S, 1, &cls, 0, 0, 0, 0, -1, 0);
             if (node >= 0) sess_placed(S, node, +1);
             if (S.classes[cls].ipa_n > 0) {
                 HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
@@ -2972,17 +3013,8 @@ struct Allocator {
             S.h_rank = (uint64_t*)MemPool::get().take(MemPool::kPinned, (size_t)(N + 1) * sizeof(uint64_t),
                                                       &S.h_rank_cap);
         }
-        PopCtrl& h = *S.h_ctrl;
-        h.stop = -1;
-        h.n_done = 0;
-        h.n_tasks = 1;
-        h.mode = 0;
-        h.any_bf = S.any_bf;
-        h.fallback = S.fallback;
-        h.cls[0] = cls;
-        h.ipa_lo[0] = h.ipa_hi[0] = 0;
         flush_tables(S);  // evictions / unevicts so far change pod-affinity predicates
-        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+        ctrl_setup(S, 1, &cls, 0, 0, 0, 0, -1, 0);
         HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, 2 * sizeof(uint32_t), S.stream));
         auto sr = S.class_srange[cls];
         if (by_score && S.classes[cls].ipa_n > 0) {  // inter-pod priority: normalisation prepass, wider range
@@ -3405,30 +3437,19 @@ static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) 
     A.open_plugins();
     for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
         const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
-        PopCtrl& h = *S.h_ctrl;
-        h.stop = -1;
-        h.n_done = 0;
-        h.ready_count = 0;
-        h.min_avail = 0;
-        h.gang_mode = 0;
-        h.n_tasks = m;
-        h.any_bf = S.any_bf;
-        h.fallback = S.fallback;
-        h.mode = 1;
-        for (int i = 0; i < m; ++i) { h.cls[i] = S.pods[cand[off + i]].cls; h.res_node[i] = -1; h.res_kind[i] = 0; }
-        std::memset(h.arrive, 0, sizeof h.arrive);
-        std::memset(h.slot, 0, sizeof h.slot);
-        std::memset(h.ipa_lo, 0, sizeof h.ipa_lo);
-        std::memset(h.ipa_hi, 0, sizeof h.ipa_hi);
-        HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
-        for (int i = 0; i < m; ++i) sweep_task(S, i, h.cls[i]);
-        HIPCHK(hipMemcpyAsync(&h, S.d_ctrl, sizeof(PopCtrl), hipMemcpyDeviceToHost, S.stream));
-        HIPCHK(hipStreamSynchronize(S.stream));
+        int cls[kMaxChunk];
+        for (int i = 0; i < m; ++i) cls[i] = S.pods[cand[off + i]].cls;
+        uint32_t epoch = 0;
+        const int slot = take_slot(S, &epoch);
+        ctrl_setup(S, m, cls, 0, 0, 0, 1, slot, epoch);
+        for (int i = 0; i < m; ++i) sweep_task(S, i, cls[i]);
+        int n_done = 0, stop = -1;
+        collect_tasks(S, slot, epoch, m, &n_done, &stop, S.res_node_buf, S.res_kind_buf, nullptr);
         S.stats.sweeps += m;
         S.stats.tasks += m;
-        if (h.n_done != m || h.stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
+        if (n_done != m || stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
         for (int i = 0; i < m; ++i) {
-            const int node = h.res_node[i];
+            const int node = S.res_node_buf[i];
             out_node[off + i] = node;
             if (node < 0) continue;
             const int pi = cand[off + i];
@@ -3446,8 +3467,8 @@ static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) 
             if (A.job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-321)
                 for (int t : job.tasks)
                     if (S.pods[t].status == Allocated) { S.pods[t].status = Binding; job.priority = S.pods[t].priority; }
+            if (S.classes[cls[i]].backfill) S.any_bf = 1;  // IsBackfill commit (commit_task)
         }
-        S.any_bf = h.any_bf;
     }
 }
 
@@ -3480,16 +3501,7 @@ static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
         S.b_rank_keys.alloc<uint64_t>(std::max(N, 1));
         S.b_rank_cnt.alloc<uint32_t>(4);
     }
-    PopCtrl& h = *S.h_ctrl;
-    h.stop = -1;
-    h.n_done = 0;
-    h.n_tasks = 1;
-    h.mode = 0;
-    h.any_bf = S.any_bf;
-    h.fallback = S.fallback;
-    h.cls[0] = cls;
-    h.ipa_lo[0] = h.ipa_hi[0] = 0;
-    HIPCHK(hipMemcpyAsync(S.d_ctrl, &h, sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+    ctrl_setup(S, 1, &cls, 0, 0, 0, 0, -1, 0);
     if (S.classes[cls].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
     HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
     HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, 1, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_cnt.p,

@@ -102,6 +102,9 @@ struct PopCtrl {
     int32_t fallback;      // lowest node holding a session-placed pod (-1 none; nodeorder.go:78-93)
     int32_t mode;          // 0: allocate (best node, gang stop); 1: backfill (first fit, no stop)
     int32_t pad;
+    uint32_t epoch;        // tag of the result granules (0: none are written)
+    int32_t pad2;
+    uint64_t* out;         // result granules in pinned host memory (PopOut of kbhip_batch.h) or null
     int32_t cls[kMaxChunk];        // task class of each task of the chunk
     int32_t res_node[kMaxChunk];
     int32_t res_kind[kMaxChunk];
@@ -110,6 +113,15 @@ struct PopCtrl {
     int64_t ipa_lo[kMaxChunk];     // inter-pod affinity min / max count over nodes (0-initialised)
     int64_t ipa_hi[kMaxChunk];
     int32_t fit[kMaxChunk][4];     // per task: walk nodes, negative cpu / memory / GPU FitDelta (fit_bits)
+};
+
+// The per-task path's chunk set-up (k_ctrl_init writes it into the device
+// PopCtrl: no host-to-device copy per chunk).
+struct CtrlInit {
+    int32_t ready_count, min_avail, gang_mode, n_tasks, any_bf, fallback, mode;
+    uint32_t epoch;
+    uint64_t* out;
+    int32_t cls[kMaxChunk];
 };
 
 // Packed selection key: max key wins = highest score, then lowest node index.
