@@ -33,9 +33,10 @@ def main():
     ap.add_argument("--pending", type=int, default=2000)
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the hoisted CPU restatement on one session")
-    ap.add_argument("--pop-group", type=int, default=0,
-                    help="1 = concurrent sessions' allocate pops share launches (option pop_group, PopBatcher; "
-                         "measured slower here: the sessions reach their pops at different times)")
+    ap.add_argument("--group", type=int, default=1,
+                    help="1 = the concurrent sessions form a lockstep what-if group (option rank_group): their "
+                         "allocate pops and reclaim / preempt rankings go out as multi-session launches; "
+                         "0 = every session launches alone")
     ap.add_argument("--concurrent", type=int, default=8,
                     help="what-if sessions in flight (host threads); their node rankings share launches")
     args = ap.parse_args()
@@ -119,15 +120,14 @@ def main():
     print(json.dumps(out))
 
 
-POP_GROUP = [1]
+GROUP = [1]
 
 
 def one_session(buf, group, barrier=None):
     t0 = time.perf_counter()
     s = kbhip.Session(buf, device=0)
-    if group:
+    if group and GROUP[0]:
         s.set_option("rank_group", 1)
-        s.set_option("pop_group", POP_GROUP[0])
     if barrier is not None:
         barrier.wait()
     counts = {1: 0, 2: 0, 3: 0}
@@ -143,13 +143,13 @@ def one_session(buf, group, barrier=None):
 def concurrent(args, bufs):
     """S what-if sessions in flight from S host threads (the engine releases the
     GIL); their reclaim / preempt node rankings and their allocate pops are
-    batched into shared launches (option rank_group, kbhip_session.cpp
-    RankBatcher / PopBatcher)."""
+    issued in lockstep as shared multi-session launches (option rank_group,
+    kbhip_session.cpp StepBatcher)."""
     from concurrent.futures import ThreadPoolExecutor
     # the sessions of one wave of `concurrent` start together (a barrier after
     # their opens), as a what-if sweep over one cluster state would
     warm, timed = bufs[:args.warmup], bufs[args.warmup:]
-    POP_GROUP[0] = args.pop_group
+    GROUP[0] = args.group
     import threading
 
     def waves(ex, bs):
@@ -189,7 +189,7 @@ def concurrent(args, bufs):
                                 "allocated": statistics.mean(r[1][1] for r in res)},
         "rank_launch_requests": req,
         "sessions_per_rank_launch": bsum / max(req, 1),
-        "pop_group": args.pop_group,
+        "group": args.group,
         "pop_launch_requests": preq,
         "sessions_per_pop_launch": pbsum / max(preq, 1),
     }

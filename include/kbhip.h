@@ -97,7 +97,7 @@ typedef struct kbhip_stats {
     double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
     int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
     int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
-    int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if batcher ("rank_group") */
+    int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if lockstep group ("rank_group") */
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
@@ -223,11 +223,13 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "rank_radix" = 1 orders reclaim / preempt walks with the wide-range radix
  * passes (four 8-bit counting passes over the score) instead of the one-pass
  * counting sort (tests);
- * "rank_group" = 1 makes this session one of a group of what-if sessions run
- * from concurrent host threads: their reclaim / preempt node rankings are
- * batched into shared launches (blockIdx.y = session; kbhip_stats
- * rank_batch_sum / rank_requests = sessions per launch);
- * "pop_group" = 1: the batched allocate pops of such sessions share launches too;
+ * "rank_group" = 1 makes this session one of a lockstep group of what-if
+ * sessions run from concurrent host threads: while inside allocate / reclaim
+ * / preempt, their allocate pops of placements 6 / 7 and their reclaim /
+ * preempt node rankings are issued in steps, once every member has a request
+ * in, as shared multi-session launches (blockIdx.y = session; kbhip_stats
+ * rank_batch_sum / rank_requests and pop_batch_sum / pop_requests = requests
+ * per launch);
  * "rank_first" = k: reclaim / preempt read the first k sorted keys with the count;
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the

@@ -433,9 +433,8 @@ struct Session {
     bool force_radix = false;  // option "rank_radix": the wide-range radix passes for every class (tests)
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
     bool aff_batch = true;     // option "aff_batch": batched pops (placement 7) of anti-affinity classes
-    bool rank_group = false;   // option "rank_group": node rankings batched with concurrent sessions (RankBatcher)
-    bool pop_group = false;    // option "pop_group": batched pops of Backfilled sessions share launches (PopBatcher)
-    hipEvent_t ev_pop = nullptr;  // this session's stream before a PopBatcher request
+    bool rank_group = false;   // option "rank_group": a what-if session of the lockstep group (StepBatcher)
+    hipEvent_t ev_pop = nullptr;  // this session's stream before a StepBatcher pop request
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
     vector<R3> rel_delta;            // evictions not yet applied on the device: Releasing += per node
     vector<int32_t> rel_touched;     // nodes with a rel_delta entry, in first-touch order
@@ -1686,198 +1685,159 @@ struct BatchLaunch {
 
 // ---------------------------------------------------------------------------
 // What-if sessions batched per launch:
-// sessions opened with option "rank_group" = 1 and driven from concurrent
-// host threads hand their reclaim / preempt node rankings to this
-// process-wide batcher; one launch of the multi-session counting sort
-// (kbhip_evict.hip, blockIdx.y = session) ranks the pending requests as soon
-// as every grouped session inside a reclaim / preempt action waits for one
-// (they then step in lockstep), or kRankWait after the first arrived.
-// The launching thread's stream runs it; every requester's inputs are on the
-// device before it asks (its stream synchronised), its outputs are read on
-// its own stream after the batch completed.
+// sessions opened with option "rank_group" = 1, each driven by its own host
+// thread, join a process-wide lockstep group while they run an action.  Their
+// device requests — the allocate pops of sessions with Backfilled nodes or of
+// pod-affinity classes (placements 6 / 7: one pop in flight per session) and
+// the reclaim / preempt node rankings — go to this batcher, which issues a
+// STEP once every member has a request in (a member doing other work — a
+// per-task sweep, host bookkeeping — is waited for; one that leaves its action
+// leaves the group): one multi-session launch per kind and device
+// (k_pop_batch_multi / the k_rank_*_multi sorts, blockIdx.y = session), up to
+// kPopMulti pops per launch.  Pops are ordered by events after each session's
+// earlier device work and before its later work; their results are the
+// sessions' own granules.  Rankings complete before their requesters resume.
+// No timeouts: the sessions step together.
 // ---------------------------------------------------------------------------
-struct RankBatcher {
-    static RankBatcher& get() {
-        static RankBatcher b;
+struct StepBatcher {
+    static StepBatcher& get() {
+        static StepBatcher b;
         return b;
     }
+    enum Kind { kPop = 0, kRank = 1 };
     struct Req {
-        RankDesc desc;
-        hipStream_t st = nullptr;  // the requester's stream (on its device)
+        int kind = kPop;
         int device = 0;
+        PopReq pop{};
+        hipEvent_t before = nullptr;  // pop: recorded on the requester's stream (its earlier work)
+        hipEvent_t after = nullptr;   // pop: recorded after the launch that served it
+        RankDesc rank{};
+        hipStream_t st = nullptr;     // rank: the requester's stream
         bool done = false;
         hipError_t err = hipSuccess;
-        int batch = 0;  // sessions in the launch that served it
+        int batch = 0;                // requests of its kind in the launch that served it
     };
-    static constexpr auto kRankWait = std::chrono::microseconds(3000);
     std::mutex mu;
     std::condition_variable cv;
     vector<Req*> pending;
-    int members = 0;  // grouped sessions inside a reclaim / preempt action
+    int members = 0;  // grouped sessions inside an action
     bool busy = false;
-    // pinned, mapped descriptors (the kernels read them in place), one area per device
-    struct Descs {
-        RankDesc* h = nullptr;
-        void* d = nullptr;
+    int64_t steps = 0;
+    struct Dev {
+        hipStream_t st = nullptr;  // pop launches
+        vector<hipEvent_t> ring;
+        size_t next = 0;
+        RankDesc* h_desc = nullptr;  // pinned, mapped: the ranking kernels read the descriptors in place
+        void* d_desc = nullptr;
         size_t cap_bytes = 0, n_cap = 0;
     };
-    std::map<int, Descs> descs;
+    std::map<int, Dev> dev;
+
     void join() {
         std::lock_guard<std::mutex> lk(mu);
         ++members;
     }
     void leave() {
-        std::lock_guard<std::mutex> lk(mu);
+        std::unique_lock<std::mutex> lk(mu);
         --members;
+        if (ready()) issue(lk);
         cv.notify_all();
-    }
-    // One launch per device: a session's columns and buffers live on its own
-    // device, so requests from different devices never share a launch; each
-    // launch runs on the first of its requesters' streams.
-    hipError_t run(const vector<Req*>& batch) {
-        std::map<int, vector<Req*>> by_dev;
-        for (Req* q : batch) by_dev[q->device].push_back(q);
-        for (auto& kv : by_dev) {
-            hipError_t e = hipSetDevice(kv.first);
-            if (e != hipSuccess) return e;
-            Descs& D = descs[kv.first];
-            const vector<Req*>& b = kv.second;
-            if (b.size() > D.n_cap) {
-                if (D.h) MemPool::get().give(MemPool::kPinnedMapped, D.h, D.cap_bytes, kv.first);
-                D.n_cap = std::max<size_t>(64, b.size());
-                D.h = (RankDesc*)MemPool::get().take(MemPool::kPinnedMapped, D.n_cap * sizeof(RankDesc), &D.cap_bytes);
-                if ((e = hipHostGetDevicePointer(&D.d, D.h, 0)) != hipSuccess) return e;
-            }
-            int max_nblk = 1;
-            for (size_t i = 0; i < b.size(); ++i) {
-                D.h[i] = b[i]->desc;
-                max_nblk = std::max(max_nblk, b[i]->desc.nblk);
-            }
-            hipStream_t st = b[0]->st;
-            e = launch_rank_sorted_multi((const RankDesc*)D.d, (int)b.size(), max_nblk, st);
-            if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) return e;
-        }
-        return hipSuccess;
-    }
-    void submit(Req& r) {
-        std::unique_lock<std::mutex> lk(mu);
-        pending.push_back(&r);
-        cv.notify_all();
-        const auto deadline = std::chrono::steady_clock::now() + kRankWait;
-        while (!r.done) {
-            const bool all_in = (int)pending.size() >= members;
-            if (!busy && !pending.empty() && (all_in || std::chrono::steady_clock::now() >= deadline)) {
-                busy = true;
-                vector<Req*> batch;
-                batch.swap(pending);
-                lk.unlock();
-                const hipError_t e = run(batch);
-                lk.lock();
-                for (Req* q : batch) {
-                    q->err = e;
-                    q->batch = (int)batch.size();
-                    q->done = true;
-                }
-                busy = false;
-                cv.notify_all();
-                continue;
-            }
-            if (busy) cv.wait(lk);
-            else cv.wait_until(lk, deadline);
-        }
-    }
-};
-
-// The allocate pops of what-if sessions with Backfilled nodes (option
-// "pop_group"; placement 6: not overlapped, no speculation — one pop in
-// flight per session) share launches of the multi-session pop kernel
-// (k_pop_batch_multi, blockIdx.y = session).  Requests queue while a launch
-// is being issued and go out together in the next one (no waiting for
-// stragglers); every launch is on one process-wide stream per device, and
-// events order it after each requester's earlier device work and each
-// requester's later work after it.  Results are the sessions' own granules.
-struct PopBatcher {
-    static PopBatcher& get() {
-        static PopBatcher b;
-        return b;
-    }
-    struct Req {
-        PopReq q;
-        int device = 0;
-        hipEvent_t before = nullptr;  // recorded on the requester's stream: its earlier work
-        hipEvent_t after = nullptr;   // recorded on the batcher's stream after the launch that served it
-        bool done = false;
-        hipError_t err = hipSuccess;
-        int batch = 0;
-    };
-    std::mutex mu;
-    std::condition_variable cv;
-    vector<Req*> pending;
-    bool busy = false;
-    std::map<int, std::pair<hipStream_t, vector<hipEvent_t>>> dev;  // device -> (stream, event ring)
-    size_t ring_next = 0;
-    hipError_t issue(vector<Req*>& batch) {
-        std::map<int, vector<Req*>> by_dev;
-        for (Req* q : batch) by_dev[q->device].push_back(q);
-        for (auto& kv : by_dev) {
-            hipError_t e = hipSetDevice(kv.first);
-            if (e != hipSuccess) return e;
-            auto& d = dev[kv.first];
-            if (!d.first) {
-                if ((e = hipStreamCreateWithFlags(&d.first, hipStreamNonBlocking)) != hipSuccess) return e;
-                d.second.assign(8, nullptr);
-                for (auto& ev : d.second)
-                    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
-            }
-            vector<PopReq> qs;
-            for (Req* q : kv.second) {
-                if ((e = hipStreamWaitEvent(d.first, q->before, 0)) != hipSuccess) return e;
-                qs.push_back(q->q);
-            }
-            int nl = 0;
-            if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), d.first, &nl)) != hipSuccess) return e;
-            hipEvent_t ev = d.second[ring_next++ % d.second.size()];
-            if ((e = hipEventRecord(ev, d.first)) != hipSuccess) return e;
-            for (Req* q : kv.second) q->after = ev;
-        }
-        return hipSuccess;
     }
     void submit(Req& r) {
         std::unique_lock<std::mutex> lk(mu);
         pending.push_back(&r);
         while (!r.done) {
-            if (!busy) {  // launch everything queued; requests arriving meanwhile go in the next launch
-                busy = true;
-                while (!pending.empty()) {
-                    vector<Req*> batch;
-                    batch.swap(pending);
-                    lk.unlock();
-                    const hipError_t e = issue(batch);
-                    lk.lock();
-                    for (Req* q : batch) {
-                        q->err = e;
-                        q->batch = (int)batch.size();
-                        q->done = true;
-                    }
-                }
-                busy = false;
-                cv.notify_all();
+            if (ready()) {
+                issue(lk);
                 continue;
             }
             cv.wait(lk);
         }
     }
+
+  private:
+    bool ready() const { return !busy && !pending.empty() && (int)pending.size() >= members; }
+    // One step: every pending request (the lock is released while launching).
+    void issue(std::unique_lock<std::mutex>& lk) {
+        busy = true;
+        vector<Req*> batch;
+        batch.swap(pending);
+        ++steps;
+        lk.unlock();
+        std::map<std::pair<int, int>, vector<Req*>> by;  // (device, kind) -> requests
+        for (Req* q : batch) by[{q->device, q->kind}].push_back(q);
+        for (auto& kv : by) {
+            const hipError_t e = kv.first.second == kPop ? launch_pops(kv.first.first, kv.second)
+                                                         : launch_ranks(kv.first.first, kv.second);
+            for (Req* q : kv.second) {
+                q->err = e;
+                q->batch = (int)kv.second.size();
+            }
+        }
+        lk.lock();
+        for (Req* q : batch) q->done = true;
+        busy = false;
+        cv.notify_all();
+    }
+    Dev& device(int d, hipError_t* e) {
+        Dev& D = dev[d];
+        *e = hipSuccess;
+        if (!D.st) {
+            if ((*e = hipStreamCreateWithFlags(&D.st, hipStreamNonBlocking)) != hipSuccess) return D;
+            D.ring.assign(64, nullptr);
+            for (auto& ev : D.ring)
+                if ((*e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return D;
+        }
+        return D;
+    }
+    hipError_t launch_pops(int d, const vector<Req*>& b) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        vector<PopReq> qs;
+        for (Req* q : b) {
+            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
+            qs.push_back(q->pop);
+        }
+        int nl = 0;
+        if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), D.st, &nl)) != hipSuccess) return e;
+        hipEvent_t ev = D.ring[D.next++ % D.ring.size()];
+        if ((e = hipEventRecord(ev, D.st)) != hipSuccess) return e;
+        for (Req* q : b) q->after = ev;
+        return hipSuccess;
+    }
+    hipError_t launch_ranks(int d, const vector<Req*>& b) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        if (b.size() > D.n_cap) {
+            if (D.h_desc) MemPool::get().give(MemPool::kPinnedMapped, D.h_desc, D.cap_bytes, d);
+            D.n_cap = std::max<size_t>(64, b.size());
+            D.h_desc = (RankDesc*)MemPool::get().take(MemPool::kPinnedMapped, D.n_cap * sizeof(RankDesc), &D.cap_bytes);
+            if ((e = hipHostGetDevicePointer(&D.d_desc, D.h_desc, 0)) != hipSuccess) return e;
+        }
+        int max_nblk = 1;
+        for (size_t i = 0; i < b.size(); ++i) {
+            D.h_desc[i] = b[i]->rank;
+            max_nblk = std::max(max_nblk, b[i]->rank.nblk);
+        }
+        hipStream_t st = b[0]->st;  // a stream of this device; every requester's inputs are in place
+        if ((e = launch_rank_sorted_multi((const RankDesc*)D.d_desc, (int)b.size(), max_nblk, st)) != hipSuccess)
+            return e;
+        return hipStreamSynchronize(st);
+    }
 };
 
-// A grouped session inside a reclaim / preempt action (RankBatcher members).
-struct RankGroupScope {
+// A grouped session inside an action (StepBatcher member).
+struct GroupScope {
     bool on;
-    explicit RankGroupScope(bool o) : on(o) {
-        if (on) RankBatcher::get().join();
+    explicit GroupScope(bool o) : on(o) {
+        if (on) StepBatcher::get().join();
     }
-    ~RankGroupScope() {
-        if (on) RankBatcher::get().leave();
+    ~GroupScope() {
+        if (on) StepBatcher::get().leave();
     }
 };
 
@@ -2057,16 +2017,17 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
-    } else if (L.bf && S.pop_group) {  // what-if sessions: pops batched across sessions (PopBatcher)
-        PopBatcher::Req r;
-        r.q = PopReq{S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf, S.d_cand2,
-                     S.d_arrive, out, 6, S.fit_set[kMaxDep + 1]};
+    } else if (S.rank_group && S.world == 1) {  // what-if sessions: pops batched across sessions (StepBatcher)
+        StepBatcher::Req r;
+        r.kind = StepBatcher::kPop;
+        r.pop = PopReq{S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf, S.d_cand2,
+                       S.d_arrive, out, L.bf ? 6 : 7, S.fit_set[kMaxDep + 1]};
         S.fit_set[kMaxDep + 1] ^= 1;
         r.device = S.device;
         if (!S.ev_pop) HIPCHK(hipEventCreateWithFlags(&S.ev_pop, hipEventDisableTiming));
         HIPCHK(hipEventRecord(S.ev_pop, S.stream));
         r.before = S.ev_pop;
-        PopBatcher::get().submit(r);
+        StepBatcher::get().submit(r);
         HIPCHK(hipSetDevice(S.device));
         HIPCHK(r.err);
         HIPCHK(hipStreamWaitEvent(S.stream, r.after, 0));  // this session's later work follows the launch
@@ -2615,6 +2576,7 @@ struct Allocator {
     }
 
     void run() {  // allocate.go:41-201
+        GroupScope group(S.rank_group && S.world == 1);  // what-if sessions: pops step with the group
         auto t0 = std::chrono::steady_clock::now();
         compile_orders();
         open_plugins();
@@ -3026,14 +2988,15 @@ struct Allocator {
         const bool counting = !S.force_radix && sr.second - sr.first < 256 && sr.first >= INT32_MIN &&
                               sr.second <= INT32_MAX;
         if (counting && S.rank_group) {  // one launch with the concurrent what-if sessions' rankings
-            RankBatcher::Req r;
-            HIPCHK(fill_rank_desc(&r.desc, S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first,
+            StepBatcher::Req r;
+            r.kind = StepBatcher::kRank;
+            HIPCHK(fill_rank_desc(&r.rank, S.conf, S.nc, S.tab, S.d_ctrl, by_score ? 1 : 0, (int)sr.first,
                                   (int)sr.second, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_tmp.p,
                                   (uint64_t*)S.b_rank_sorted.p, (uint32_t*)S.b_rank_cnt.p));
             r.st = S.stream;
             r.device = S.device;
             HIPCHK(hipStreamSynchronize(S.stream));  // this request's control block and counters are in place
-            RankBatcher::get().submit(r);
+            StepBatcher::get().submit(r);
             HIPCHK(hipSetDevice(S.device));
             HIPCHK(r.err);
             S.stats.rank_requests++;
@@ -3273,7 +3236,7 @@ struct Allocator {
         return v;
     }
     void preempt_action() {  // preempt.go:43-255
-        RankGroupScope group(S.rank_group);
+        GroupScope group(S.rank_group);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -3343,7 +3306,7 @@ struct Allocator {
         flush_evictions();
     }
     void reclaim_action() {  // reclaim.go:41-196
-        RankGroupScope group(S.rank_group);
+        GroupScope group(S.rank_group);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -4005,7 +3968,6 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
-        else if (std::strcmp(key, "pop_group") == 0) s->s.pop_group = value != 0 && s->s.world == 1;
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");

@@ -1,8 +1,8 @@
 """What-if sessions batched per launch:
 sessions with option rank_group run from concurrent host threads and their
-reclaim / preempt node rankings share launches of the multi-session counting
-sort and their allocate pops share launches of the multi-session pop kernel
-(blockIdx.y = session).  Each session's records equal the faithful
+reclaim / preempt node rankings and their allocate pops are issued in
+lockstep steps as multi-session launches (counting sort / pop kernel,
+blockIdx.y = session).  Each session's records equal the faithful
 restatement's and the same session run alone; the launches served more than
 one session."""
 import threading
@@ -20,7 +20,6 @@ def _run(engine, path, group, barrier=None):
     with engine.Session(path) as s:
         if group:
             s.set_option("rank_group", 1)
-            s.set_option("pop_group", 1)
         if barrier is not None:  # the sessions start their actions together
             barrier.wait()
         pod, node, kind = s.run_actions(ACTIONS)
@@ -52,3 +51,4 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
     assert preq > 0 and pbsum >= preq
     if n_sessions > 2:
         assert pbsum > preq
+    assert pbsum / preq > 1.5  # lockstep: most pop launches serve several sessions
