@@ -1713,12 +1713,11 @@ struct StepBatcher {
         hipEvent_t after = nullptr;   // pop: recorded after the launch that served it
         RankDesc rank{};
         hipStream_t st = nullptr;     // rank: the requester's stream
-        bool done = false;
+        std::atomic<bool> done{false};
         hipError_t err = hipSuccess;
         int batch = 0;                // requests of its kind in the launch that served it
     };
     std::mutex mu;
-    std::condition_variable cv;
     vector<Req*> pending;
     int members = 0;  // grouped sessions inside an action
     bool busy = false;
@@ -1741,17 +1740,19 @@ struct StepBatcher {
         std::unique_lock<std::mutex> lk(mu);
         --members;
         if (ready()) issue(lk);
-        cv.notify_all();
     }
+    // The member whose request (or departure) completes the step issues it;
+    // the others spin on their own request (a step is microseconds of host
+    // work: a sleeping wait would cost every member a wake-up per step).
     void submit(Req& r) {
-        std::unique_lock<std::mutex> lk(mu);
-        pending.push_back(&r);
-        while (!r.done) {
-            if (ready()) {
-                issue(lk);
-                continue;
-            }
-            cv.wait(lk);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            pending.push_back(&r);
+            if (ready()) issue(lk);
+        }
+        for (long spin = 0; !r.done.load(std::memory_order_acquire); ++spin) {
+            if ((spin & 1023) == 1023) std::this_thread::yield();
+            else __builtin_ia32_pause();
         }
     }
 
@@ -1767,17 +1768,18 @@ struct StepBatcher {
         std::map<std::pair<int, int>, vector<Req*>> by;  // (device, kind) -> requests
         for (Req* q : batch) by[{q->device, q->kind}].push_back(q);
         for (auto& kv : by) {
-            const hipError_t e = kv.first.second == kPop ? launch_pops(kv.first.first, kv.second)
+            int launches = 1;
+            const hipError_t e = kv.first.second == kPop ? launch_pops(kv.first.first, kv.second, &launches)
                                                          : launch_ranks(kv.first.first, kv.second);
             for (Req* q : kv.second) {
                 q->err = e;
-                q->batch = (int)kv.second.size();
+                q->batch = (int)((kv.second.size() + launches - 1) / launches);  // requests per launch
             }
         }
         lk.lock();
-        for (Req* q : batch) q->done = true;
         busy = false;
-        cv.notify_all();
+        for (Req* q : batch) q->done.store(true, std::memory_order_release);  // q may go away after this
+        if (ready()) issue(lk);  // requests that came in while this step was being launched
     }
     Dev& device(int d, hipError_t* e) {
         Dev& D = dev[d];
@@ -1790,7 +1792,7 @@ struct StepBatcher {
         }
         return D;
     }
-    hipError_t launch_pops(int d, const vector<Req*>& b) {
+    hipError_t launch_pops(int d, const vector<Req*>& b, int* launches) {
         hipError_t e = hipSetDevice(d);
         if (e != hipSuccess) return e;
         Dev& D = device(d, &e);
@@ -1802,6 +1804,7 @@ struct StepBatcher {
         }
         int nl = 0;
         if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), D.st, &nl)) != hipSuccess) return e;
+        *launches = std::max(nl, 1);
         hipEvent_t ev = D.ring[D.next++ % D.ring.size()];
         if ((e = hipEventRecord(ev, D.st)) != hipSuccess) return e;
         for (Req* q : b) q->after = ev;
