@@ -102,6 +102,9 @@ typedef struct kbhip_stats {
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
     int64_t comm_reused;     /* 1: kbhip_shard_connect_rccl took a pooled communicator of an earlier session */
+    int64_t async_launched;  /* kbhip_place_job_submit: pops launched ahead of their wait */
+    int64_t async_retracted; /* ... launches withdrawn (cancelled, or behind a pop that ran synchronously) */
+    int64_t async_cancelled; /* tickets withdrawn by kbhip_place_job_cancel */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -124,6 +127,33 @@ int kbhip_session_open_file(const char* path, int device, kb_session** out);
 int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
                     int32_t min_available, int32_t ready_count, int32_t* out_node, uint8_t* out_kind,
                     int32_t* out_n_done, int32_t* out_stop_reason);
+
+/* Asynchronous per-pop entry points: the pipelining kbhip_allocate does
+ * internally, for a host that keeps allocate.go's loop
+ * (allocate.go:110-196) itself.  While pop e runs, the host predicts pop e+1
+ * (assuming e places its tasks as Allocated up to the gang stop), submits it,
+ * and only then waits for e; if e's results show the prediction wrong, it
+ * cancels e+1 and submits the real next pop.
+ *
+ * kbhip_place_job_submit queues one job pop with kbhip_place_job's arguments
+ * and returns a ticket (>= 0).  A pop runs on the session state that every
+ * earlier submitted pop leaves, exactly as a sequence of kbhip_place_job calls
+ * would: a pop that is one batched chunk (at most 16 tasks of one task class)
+ * is launched at once, up to 4 ahead of the oldest wait; any other pop, and
+ * every pop behind it, is launched when the pops ahead of it have been waited
+ * for, or runs inside its own wait.
+ * kbhip_place_job_wait returns the results of the OLDEST outstanding ticket
+ * (outputs as kbhip_place_job); naming any other ticket is KBHIP_EINVAL.
+ * kbhip_place_job_cancel withdraws `ticket` and every later one: their device
+ * updates are undone and they are never reported.  Returns the number
+ * withdrawn.
+ * Every other session call fails with KBHIP_EINVAL while tickets are
+ * outstanding; kbhip_session_close drops them. */
+int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
+                               int32_t min_available, int32_t ready_count);
+int kbhip_place_job_wait(kb_session* s, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                         int32_t* out_stop_reason);
+int kbhip_place_job_cancel(kb_session* s, int64_t ticket);
 
 /* Run the whole allocate action.  Outputs the placement log in decision
  * order: pod index, node index, kind.  Returns the number of placements. */

@@ -407,6 +407,33 @@ inline SpareVec<HPod>& spare_pods() {
     return sp;
 }
 
+// ---------------------------------------------------------------------------
+// batched pop launches: one k_pop_batch per job-pop chunk of one class.  Two
+// result slots, so that the predicted next pop can be queued on the stream
+// behind a running one (Allocator::speculate) and its results told apart.
+// ---------------------------------------------------------------------------
+struct BatchLaunch {
+    int slot = 0;
+    uint32_t epoch = 0;
+    int cls = -1, m = 0;
+    bool timed = false;
+    hipStream_t st = nullptr;
+    bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
+    bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
+    bool aff = false;  // placement 7 (pod-affinity class): may end before its first task (n_done 0)
+};
+
+// A job pop submitted through the asynchronous per-pop ABI
+// (kbhip_place_job_submit): launched at submit time when it is one batched
+// chunk and nothing deferred is ahead of it, else run at its wait.
+struct PopTicket {
+    int64_t id = 0;
+    bool launched = false;
+    BatchLaunch L;
+    vector<int32_t> ids;
+    int gang = 0, min_avail = 0, ready = 0;
+};
+
 struct Session {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -500,6 +527,8 @@ struct Session {
     int speculate = 2;                // predicted pops queued ahead of the running one (0..3)
 #endif
     int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
+    std::deque<PopTicket> tickets;    // asynchronous per-pop ABI: outstanding pops, oldest first
+    int64_t next_ticket = 0;
 #ifdef KBHIP_STAMPS
     DevBuf b_stamps;
     uint64_t* d_stamps = nullptr;
@@ -1668,22 +1697,6 @@ static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
 }
 
 // ---------------------------------------------------------------------------
-// batched pop launches: one k_pop_batch per job-pop chunk of one class.  Two
-// result slots, so that the predicted next pop can be queued on the stream
-// behind a running one (Allocator::speculate) and its results told apart.
-// ---------------------------------------------------------------------------
-struct BatchLaunch {
-    int slot = 0;
-    uint32_t epoch = 0;
-    int cls = -1, m = 0;
-    bool timed = false;
-    hipStream_t st = nullptr;
-    bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
-    bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
-    bool aff = false;  // placement 7 (pod-affinity class): may end before its first task (n_done 0)
-};
-
-// ---------------------------------------------------------------------------
 // What-if sessions batched per launch:
 // sessions opened with option "rank_group" = 1, each driven by its own host
 // thread, join a process-wide lockstep group while they run an action.  Their
@@ -2213,12 +2226,16 @@ static void apply_results(Session& S, const int32_t* ids, int n, const int32_t* 
 // ---------------------------------------------------------------------------
 // device driver for one job pop
 // ---------------------------------------------------------------------------
-static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
-                     int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop) {
-    int done = 0, stop = KBHIP_STOP_ALL;
+static void check_task_ids(const Session& S, const int32_t* ids, int n) {
     for (int i = 0; i < n; ++i)
         if (ids[i] < 0 || ids[i] >= (int)S.pods.size() || S.pods[ids[i]].cls < 0)
             throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
+}
+
+static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
+                     int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop) {
+    int done = 0, stop = KBHIP_STOP_ALL;
+    check_task_ids(S, ids, n);
     while (done < n) {
         const int cls0 = S.pods[ids[done]].cls;
         int m = 1;
@@ -2306,6 +2323,126 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
     *out_n_done = done;
     *out_stop = stop;
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// asynchronous per-pop ABI (kbhip_place_job_submit / _wait / _cancel): the
+// pipelining of kbhip_allocate's speculation (Allocator::speculate), offered
+// to a host that keeps allocate.go's loop itself.  A submitted pop runs on the
+// device state its predecessors leave; launched tickets form a prefix of the
+// queue (a deferred one, run at its wait, holds back the ones behind it).
+// ---------------------------------------------------------------------------
+static constexpr int kMaxLaunchedTickets = 4;  // < Session::kSlots result slots in flight
+static constexpr size_t kMaxTickets = 64;
+
+static void require_no_tickets(const Session& S) {
+    if (!S.tickets.empty())
+        throw Error(KBHIP_EINVAL, "submitted job pops are outstanding (kbhip_place_job_wait / _cancel them first)");
+}
+
+// One batched chunk of one class, no Backfilled nodes (the undo of a pop has no visit rule).
+static bool ticket_launchable(Session& S, const PopTicket& t) {
+    const int n = (int)t.ids.size();
+    if (n < 1 || n > kMaxChunk || S.any_bf) return false;
+    const int cls0 = S.pods[t.ids[0]].cls;
+    for (int i = 1; i < n; ++i)
+        if (S.pods[t.ids[i]].cls != cls0) return false;
+    return batchable(S, cls0);
+}
+
+// Launch deferred tickets in queue order while they can run as one batched launch.
+static void promote_tickets(Session& S) {
+    int launched = 0;
+    for (PopTicket& t : S.tickets) {
+        if (t.launched) { ++launched; continue; }
+        if (launched >= kMaxLaunchedTickets || !ticket_launchable(S, t)) return;
+        t.L = launch_batched(S, S.pods[t.ids[0]].cls, (int)t.ids.size(), t.gang, t.min_avail, t.ready);
+        t.launched = true;
+        S.stats.async_launched++;
+        ++launched;
+    }
+}
+
+// Withdraw the launches of tickets [from, end): collect, then undo their node
+// updates on the device (inverse updates commute); the tickets become deferred.
+static void retract_tickets(Session& S, size_t from) {
+    int32_t fit_save[4];
+    std::memcpy(fit_save, S.last_fit, sizeof fit_save);
+    const bool fit_ok = S.last_fit_ok;
+    struct Got { int cls, n; int32_t node[kMaxChunk], kind[kMaxChunk]; };
+    vector<Got> got;
+    for (size_t i = from; i < S.tickets.size(); ++i) {
+        PopTicket& t = S.tickets[i];
+        if (!t.launched) continue;
+        Got g;
+        int st = 0;
+        g.cls = t.L.cls;
+        collect_batched(S, t.L, &g.n, &st, g.node, g.kind);
+        got.push_back(g);
+        t.launched = false;
+    }
+    std::memcpy(S.last_fit, fit_save, sizeof fit_save);
+    S.last_fit_ok = fit_ok;
+    if (got.empty()) return;
+    ov_quiesce(S);
+    for (const Got& g : got) {
+        HIPCHK(launch_undo_pop(S.nc, S.tab, g.cls, g.n, g.node, g.kind, S.stream));
+        S.stats.async_retracted++;
+    }
+    if (S.overlap > 0) HIPCHK(hipStreamSynchronize(S.stream));  // overlapped pops are not ordered after it
+}
+
+static int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail,
+                                int ready_count) {
+    check_task_ids(S, ids, n);
+    if (S.tickets.size() >= kMaxTickets) throw Error(KBHIP_EINVAL, "too many outstanding job pops");
+    PopTicket t;
+    t.id = S.next_ticket++;
+    t.ids.assign(ids, ids + n);
+    t.gang = gang_mode;
+    t.min_avail = min_avail;
+    t.ready = ready_count;
+    S.tickets.push_back(std::move(t));
+    promote_tickets(S);
+    return S.tickets.back().id;
+}
+
+static int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                          int32_t* out_stop) {
+    if (S.tickets.empty() || S.tickets.front().id != ticket)
+        throw Error(KBHIP_EINVAL, "kbhip_place_job_wait must name the oldest outstanding ticket");
+    PopTicket t = std::move(S.tickets.front());
+    S.tickets.pop_front();
+    const int n = (int)t.ids.size();
+    bool sync = !t.launched;
+    if (t.launched) {
+        int nd = 0, st = 0;
+        collect_batched(S, t.L, &nd, &st, S.res_node_buf, S.res_kind_buf);
+        if (nd == 0) {  // placement 7 could not place the first task exactly: the pop runs synchronously,
+            retract_tickets(S, 0);  // and the launches behind it ran on a state it is about to change
+            sync = true;
+        } else {
+            if (st < 0 || nd > n) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+            apply_results(S, t.ids.data(), nd, S.res_node_buf, S.res_kind_buf, out_node, out_kind);
+            *out_n_done = nd;
+            *out_stop = st;
+        }
+    }
+    if (sync) place_job(S, t.ids.data(), n, t.gang, t.min_avail, t.ready, out_node, out_kind, out_n_done, out_stop);
+    promote_tickets(S);
+    return 0;
+}
+
+static int place_job_cancel(Session& S, int64_t ticket) {
+    size_t from = 0;
+    while (from < S.tickets.size() && S.tickets[from].id < ticket) ++from;
+    if (from == S.tickets.size() || S.tickets[from].id != ticket)
+        throw Error(KBHIP_EINVAL, "kbhip_place_job_cancel names no outstanding ticket");
+    retract_tickets(S, from);
+    const int k = (int)(S.tickets.size() - from);
+    S.tickets.erase(S.tickets.begin() + from, S.tickets.end());
+    S.stats.async_cancelled += k;
+    return k;
 }
 
 // ---------------------------------------------------------------------------
@@ -3631,6 +3768,7 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
         if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
             throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         // results come back through the pinned result granules; device work still in flight (an
         // overlapped pop's write-back) is ordered before the next pop by the device chain, and
@@ -3640,9 +3778,38 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
     })
 }
 
+int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
+                               int32_t min_available, int32_t ready_count) {
+    ABI_GUARD_S(s, {
+        if (!s || (!task_ids && n_tasks) || n_tasks < 0) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_submit(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count);
+    })
+}
+
+int kbhip_place_job_wait(kb_session* s, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                         int32_t* out_stop_reason) {
+    ABI_GUARD_S(s, {
+        if (!s || !out_node || !out_kind || !out_n_done || !out_stop_reason)
+            throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_wait(s->s, ticket, out_node, out_kind, out_n_done, out_stop_reason);
+    })
+}
+
+int kbhip_place_job_cancel(kb_session* s, int64_t ticket) {
+    ABI_GUARD_S(s, {
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_cancel(s->s, ticket);
+    })
+}
+
 int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         s->s.log.clear();
         kbhip::Allocator a(s->s);
@@ -3660,6 +3827,7 @@ int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
         s->s.log.clear();
@@ -3678,6 +3846,7 @@ int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* 
     ABI_GUARD_S(s, {
         if (!s || n < 0 || (n > 0 && (!task_ids || !out_node))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         s->s.log.clear();
         kbhip::first_fit(s->s, task_ids, n, out_node);
@@ -3691,6 +3860,7 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
     ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         return kbhip::sweep_scores(s->s, task_id, out_keys);
     })
@@ -3861,6 +4031,7 @@ static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* 
                         int64_t cap) {
     ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
         s->s.log.clear();
@@ -3881,6 +4052,7 @@ int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
     ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         session_carry(s->s);
         if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
@@ -3893,6 +4065,7 @@ int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
         if (n < 0 || (n > 0 && (!pods || !events))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         session_carry(s->s, pods, events, n);
         if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
@@ -3910,6 +4083,7 @@ int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         kbhip::Session& S = s->s;
+        kbhip::require_no_tickets(S);
         const int N = S.nc.n;
         if (n_nodes < N) throw kbhip::Error(KBHIP_EINVAL, "output too small");
         HIPCHK(hipSetDevice(S.device));

@@ -29,7 +29,8 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
-           "kbhip_session_carry_events", "kbhip_shard_connect_mailbox")
+           "kbhip_session_carry_events", "kbhip_shard_connect_mailbox", "kbhip_place_job_submit",
+           "kbhip_place_job_wait", "kbhip_place_job_cancel")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64, RED_SUM_I64 = 0, 1, 2, 3
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -50,7 +51,9 @@ class Stats(ctypes.Structure):
                 ("alloc_device_s", ctypes.c_double), ("unassigned_pops", ctypes.c_int64),
                 ("collectives", ctypes.c_int64), ("rank_requests", ctypes.c_int64),
                 ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
-                ("pop_batch_sum", ctypes.c_int64), ("comm_reused", ctypes.c_int64)]
+                ("pop_batch_sum", ctypes.c_int64), ("comm_reused", ctypes.c_int64),
+                ("async_launched", ctypes.c_int64), ("async_retracted", ctypes.c_int64),
+                ("async_cancelled", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -77,6 +80,10 @@ def lib() -> ctypes.CDLL:
         L.kbhip_session_open.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(vp)]
         L.kbhip_session_open_file.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(vp)]
         L.kbhip_place_job.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, vp, vp]
+        L.kbhip_place_job_submit.argtypes = [vp, vp, i32, i32, i32, i32]
+        L.kbhip_place_job_submit.restype = i64
+        L.kbhip_place_job_wait.argtypes = [vp, i64, vp, vp, vp, vp]
+        L.kbhip_place_job_cancel.argtypes = [vp, i64]
         L.kbhip_allocate.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_first_fit.argtypes = [vp, vp, i32, vp]
@@ -245,6 +252,33 @@ class Session:
                                      _p(kind), _p(done), _p(stop)))
         d = int(done[0])
         return node[:d].copy(), kind[:d].copy(), int(stop[0])
+
+    def place_job_submit(self, task_ids, gang_mode: int, min_available: int, ready_count: int) -> int:
+        """kbhip_place_job_submit: queue a job pop (run on the state the earlier submitted pops leave); a ticket."""
+        ids = np.ascontiguousarray(task_ids, dtype=np.int32)
+        t = int(lib().kbhip_place_job_submit(self._h, _p(ids), ids.size, gang_mode, min_available, ready_count))
+        _check(t if t < 0 else 0)
+        self._tix = getattr(self, "_tix", {})
+        self._tix[t] = max(ids.size, 1)
+        return t
+
+    def place_job_wait(self, ticket: int):
+        """kbhip_place_job_wait: results of the oldest outstanding ticket, as place_job."""
+        n = getattr(self, "_tix", {}).pop(ticket, 1)
+        node = np.full(n, -1, np.int32)
+        kind = np.zeros(n, np.uint8)
+        done = np.zeros(1, np.int32)
+        stop = np.zeros(1, np.int32)
+        _check(lib().kbhip_place_job_wait(self._h, int(ticket), _p(node), _p(kind), _p(done), _p(stop)))
+        d = int(done[0])
+        return node[:d].copy(), kind[:d].copy(), int(stop[0])
+
+    def place_job_cancel(self, ticket: int) -> int:
+        """kbhip_place_job_cancel: withdraw `ticket` and every later one; the number withdrawn."""
+        k = _check(lib().kbhip_place_job_cancel(self._h, int(ticket)))
+        for t in [t for t in getattr(self, "_tix", {}) if t >= ticket]:
+            del self._tix[t]
+        return k
 
     def read_nodes(self, n_nodes: int) -> np.ndarray:
         out = np.zeros((n_nodes, 12), np.int64)

@@ -97,3 +97,15 @@ def test_stats_struct_matches_header():
     assert [n for _, n in fields] == [n for n, _ in mirror]
     ctype = {"double": ctypes.c_double, "int64_t": ctypes.c_int64}
     assert all(ctype[t] is m for (t, _), (_, m) in zip(fields, mirror))
+
+
+def test_host_loop_binary_built():
+    """kube-batch-1_amd/_build/kbhost (the C++ host loop over the per-pop ABI)
+    is built with the library; without arguments it prints its usage."""
+    import subprocess
+    exe = os.path.join(ROOT, "kube-batch-1_amd", "_build", "kbhost")
+    if not os.path.exists(exe):
+        import kbhip
+        kbhip.build()
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and "usage" in r.stderr
