@@ -1,0 +1,4 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03a_pytest.log 2>&1 && \
+timeout -k 10 300 python -u bench.py > gpurun_out/r03a_bench.json 2> gpurun_out/r03a_bench.err

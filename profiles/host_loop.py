@@ -4,7 +4,7 @@ kbhip_place_job_submit / _wait / _cancel with `depth` predicted pops in
 flight) timed beside kbhip_allocate on the same snapshot; all three logs must
 be identical.  Writes one JSON line (stdout and --out).
 
-usage: python profiles/host_loop.py [--nodes 100000] [--pending 1000000] [--reps 3] [--depth 2] [--out F]"""
+usage: python profiles/host_loop.py [--nodes 100000] [--pending 800000] [--reps 3] [--depth 2] [--out F]"""
 import argparse
 import json
 import os
@@ -20,7 +20,7 @@ import kbgen  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=100_000)
-    ap.add_argument("--pending", type=int, default=1_000_000)
+    ap.add_argument("--pending", type=int, default=800_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--depth", type=int, default=2)
     ap.add_argument("--modes", default="allocate,sync,async")
