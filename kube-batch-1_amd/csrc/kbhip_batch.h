@@ -23,6 +23,28 @@ static __device__ uint64_t* g_stamps;
 #define STAMP(slot) do {} while (0)
 #endif
 
+#ifdef KBHIP_TIMELINE
+// Diagnostic build only: steady-state timeline of the overlapped pops at full
+// speed (s_memrealtime, 100 MHz), kTlSlots pops x kTlEvents words by sequence
+// number: TL = one writer, TL_MAX = the latest over the grid's blocks.
+constexpr int kTlSlots = 32768, kTlEvents = 16;
+static __device__ uint64_t* g_tl;
+#define TL(seq, ev)                                                                             \
+    do {                                                                                        \
+        g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime();         \
+    } while (0)
+#define TL_VAL(seq, ev, v) do { g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = (v); } while (0)
+#define TL_MAX(seq, ev)                                                                         \
+    do {                                                                                        \
+        atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],            \
+                  (unsigned long long)__builtin_amdgcn_s_memrealtime());                        \
+    } while (0)
+#else
+#define TL(seq, ev) do {} while (0)
+#define TL_VAL(seq, ev, v) do {} while (0)
+#define TL_MAX(seq, ev) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // wave-level exchange: lane i <-> lane i ^ J without the LDS crossbar.
 // J = 1, 2: DPP quad_perm; 4: DPP row_shl:4 / row_shr:4 + select; 8: DPP
@@ -463,6 +485,46 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     uint64_t pwc[4];
     for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
+    // Fast path (no second commit reaches the chunk): T0 = the m-th depth-0
+    // entry.  A second entry of any candidate is its running minimum after one
+    // commit at depth 1, and deeper entries are below it; if none of the first
+    // m candidates' depth-1 entries reaches T0, the chunk's top m entries are
+    // the first m candidates once each, in list order.  Every wave evaluates
+    // the same test on the same inputs (no barrier); waves 1.. then leave.
+    bool fast = false;
+    {
+        const uint64_t Km = m >= 1 && m <= 64 ? readlane64(K, m - 1) : 0;
+        if (Km) {  // the first m candidates are all feasible
+            const int ap0 = key_kind(K) == 2 ? 0 : 64;
+            bool reach = false;
+            if (lane < m) {
+                const int na = ap0 == 0 ? 0 : 1;
+                const Row r1 = apply_commits(base, c, na, 1 - na);
+                int32_t s1;
+                bool passed1;
+                const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
+                if (k1) {
+                    const int32_t s0 = key_score(K), sm = key_score(Km);
+                    const int32_t rm = key_score(k1) < s0 ? key_score(k1) : s0;
+                    // (rm, n, depth 1) vs (sm, node of Km, depth 0): higher score, lower index, lower depth
+                    reach = rm > sm || (rm == sm && n < key_idx(Km));
+                }
+            }
+            fast = __ballot(reach) == 0;
+        }
+    }
+    ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
+    int lf = 0, kind = 0, cc = 0, ap_l = 64;
+    bool inm = false;
+    if (fast) {
+        if (wave != 0) return;
+        STAMP(gridDim.x * 4 + 13);
+        inm = lane < m;
+        L = inm ? depth_entry<ET>(key_score(K), n, 0, a) : (ET)0;
+        lf = lane;
+        kind = inm ? key_kind(K) : 0;
+        ap_l = key_kind(K) == 2 ? 0 : 64;
+    } else {
     if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
     if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
     __syncthreads();  // K read by every wave; wl free
@@ -483,14 +545,13 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         *sc = k ? key_score(k) : 0;
         return k ? key_kind(k) : 0;
     };
-    ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
     bool alive = n >= 0; // candidate still relevant (uniform over waves)
     for (int r = 0; r < 64 / kW; ++r) {
         const int d = r * kW + wave;
         int ap = s_apos[lane];
         int32_t sc = 0;
-        int kind = alive ? eval_at(d, ap, &sc) : 0;
-        s_kind[d][lane] = (uint8_t)kind;
+        int kd = alive ? eval_at(d, ap, &sc) : 0;
+        s_kind[d][lane] = (uint8_t)kd;
         __syncthreads();
         if (ap == 64) {  // first Pipeline within this round: recompute the depths behind it
             // (no barrier before the rewrites below: they only touch depths
@@ -498,8 +559,8 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             for (int w2 = 0; w2 < kW; ++w2)
                 if (s_kind[r * kW + w2][lane] == 2) { ap = r * kW + w2; break; }
             if (alive && ap < d) {
-                kind = eval_at(d, ap, &sc);
-                s_kind[d][lane] = (uint8_t)kind;
+                kd = eval_at(d, ap, &sc);
+                s_kind[d][lane] = (uint8_t)kd;
             }
         }
         s_sc[wave][lane] = sc;
@@ -538,15 +599,16 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     if (wave != 0) return;
     STAMP(gridDim.x * 4 + 2);
     // commit kind of each position: its node's candidate lane, the entry's depth
-    const bool inm = lane < m && L != 0;
-    int lf = 0;
+    inm = lane < m && L != 0;
     if (inm) {
         const int ni = entry_node(L, a);
         int h = hash_slot(ni);
         while (s_hkey[h] != ni) h = (h + 1) & (kHash - 1);
         lf = s_hlane[h];
     }
-    const int kind = inm ? s_kind[entry_depth(L)][lf] : 0;
+    kind = inm ? s_kind[entry_depth(L)][lf] : 0;
+    ap_l = s_apos[lane];
+    }  // slow path
     // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
     const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
     const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
@@ -570,18 +632,25 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         stop = 0;
     }
     STAMP(gridDim.x * 4 + 8);
-    if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
-    __builtin_amdgcn_wave_barrier();
-    const int cc = s_cnt[lane];
+    if (fast) {  // position p is candidate p, once
+        cc = lane < done ? 1 : 0;
+    } else {
+        if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
+        __builtin_amdgcn_wave_barrier();
+        cc = s_cnt[lane];
+    }
     STAMP(gridDim.x * 4 + 9);
+    if constexpr (SC1) {
+        if (lane == 0) { TL(seq, 7); TL_VAL(seq, 9, fast ? 1 : 2); TL_VAL(seq, 10, (uint64_t)done); }
+    }
     if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
         // fit_in: every node at the state this pop started from; the candidates
         // then carry the commits made before the failing task
         uint32_t fb_base = 0, fb_post = 0;
         if (n >= 0) {
             fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
-            const int ap = s_apos[lane];
+            const int ap = ap_l;
             const int na = cc < ap ? cc : ap;
             const Row r = apply_commits(base, c, na, cc - na);
             int32_t sc;
@@ -604,7 +673,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     }
     const int ln = n - wb_base;  // local row of the written-back node
     if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
-        const int ap = s_apos[lane];
+        const int ap = ap_l;
         const int na = cc < ap ? cc : ap;
         const Row r = apply_commits(base, c, na, cc - na);
         if constexpr (SC1) {
@@ -627,7 +696,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     }
     if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) st_sc1(done_flag, seq);
+        if (lane == 0) { st_sc1(done_flag, seq); TL(seq, 8); }
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, lane < done ? kind : 0,

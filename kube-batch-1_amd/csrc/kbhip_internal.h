@@ -166,6 +166,9 @@ size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);
 #endif
+#ifdef KBHIP_TIMELINE
+hipError_t set_timeline_buffer(uint64_t* p);
+#endif
 struct PopOutHost {  // host view of the device PopOut: self-tagged granules
     uint64_t g[kMaxChunk];
     uint64_t fit[2];

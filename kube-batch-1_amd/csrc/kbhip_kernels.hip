@@ -28,9 +28,16 @@
 #include "kbhip_batch.h"
 #include "kbhip_internal.h"
 
+// Built as three translation units (Makefile: KBHIP_PART 1, 2, 3) so that the
+// template instantiations compile in parallel; KBHIP_PART 0 = all of it.
+#ifndef KBHIP_PART
+#define KBHIP_PART 0
+#endif
+
 namespace kbhip {
 
 
+#if KBHIP_PART <= 1  // everything but the batched-pop launchers of parts 2 / 3
 __global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t, PopCtrl* ctrl, int task_i) {
     __shared__ int64_t rlo[kBlock / 64], rhi[kBlock / 64];
     if (ctrl->stop >= 0) return;
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_commit_task(NodeCols nc, DevTables t
     commit_task(nc, t, ctrl, task_i, c, first_fit, !first_fit && ctrl->any_bf != 0, walk);
 }
 
+#endif
 // ---------------------------------------------------------------------------
 // batched path
 // PL: the placement compiled into this instantiation — 2 parallel levels,
@@ -490,6 +498,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     STAMP(blockIdx.x * 4 + 0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) TL(seq, 0);
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
     // pop seq-1 may still be writing rows: its candidates, in flight while the rows below load
@@ -527,7 +536,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             if (tn >= base && tn < base + R * kPopThreads)
                 atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
         }
-        if (lane == 0) s_ok = ok;
+        if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
     }
     __syncthreads();
     KT best = 0;
@@ -556,7 +565,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     __syncthreads();
     STAMP(blockIdx.x * 4 + 2);
-    if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
+    if (threadIdx.x == 0) { TL_MAX(seq, 2); role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1); }
     __syncthreads();
     if (!role) return;
     // 2a. last block of group g merges the group's lists
@@ -581,7 +590,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        if (threadIdx.x == 0) role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1);
+        if (threadIdx.x == 0) { TL_MAX(seq, 3); role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1); }
         __syncthreads();
         if (!role) return;
     }
@@ -595,6 +604,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
     STAMP(gridDim.x * 4 + 0);
+    if (threadIdx.x == 0) TL(seq, 4);
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the sweep's FitDelta counts (every block added before it arrived), left in flight
@@ -632,6 +642,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             __builtin_amdgcn_s_sleep(2);
         }
         s_ok = ok;
+        TL(seq, 5);
     }
     __syncthreads();
     STAMP(gridDim.x * 4 + 10);
@@ -662,6 +673,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         // this pop's candidates, one self-tagged granule each
         const int tnode = (ok && top) ? key_node(top, a) : -1;
         st_sc1(&link->touched[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint32_t)tnode);
+        if (lane == 0) TL(seq, 6);
         wl[0][lane] = ok ? key64_of(top, a) : 0;
     }
     __syncthreads();
@@ -678,6 +690,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
 }
 
+#if KBHIP_PART <= 1
 // ---------------------------------------------------------------------------
 // launchers (host)
 // ---------------------------------------------------------------------------
@@ -822,6 +835,8 @@ int pop_blocks(int n_nodes, int* R_out) {
     return (n_nodes + kPopThreads * R - 1) / (kPopThreads * R);
 }
 
+#endif
+#if KBHIP_PART == 0 || KBHIP_PART == 2  // k_pop_batch (placements 2, 3, 6, 7)
 template <typename KT>
 static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopArgs& a,
                                uint64_t* cand, uint32_t* arrive, PopOut* o, ShardMsg* m, const MboxArgs& mb,
@@ -848,6 +863,8 @@ static void launch_pop_batch_t(int R, int nb, const Conf& cf, const NodeCols& nc
 #undef KBHIP_PB1
 }
 
+#endif
+#if KBHIP_PART == 0 || KBHIP_PART == 3  // k_pop_batch_multi
 // Multi-session launches: requests grouped by (nodes per lane, key type,
 // placement), up to kPopMulti per launch.
 template <int R, typename KT, int PL>
@@ -909,6 +926,8 @@ hipError_t launch_pop_batch_multi(const PopReq* reqs, int n, hipStream_t st, int
     return hipSuccess;
 }
 
+#endif
+#if KBHIP_PART == 0 || KBHIP_PART == 2
 hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                             int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                             uint32_t* arrive, void* out_dev, hipStream_t st, int placement, const KeyFormat& kf,
@@ -925,6 +944,8 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
     return hipGetLastError();
 }
 
+#endif
+#if KBHIP_PART <= 1
 // ---------------------------------------------------------------------------
 // Node-array shards, batched pops: after the all-gather of
 // every shard's ShardMsg, each shard runs this identical placement on the
@@ -1061,5 +1082,9 @@ size_t pop_out_bytes() { return sizeof(PopOut); }
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
 #endif
+#ifdef KBHIP_TIMELINE
+hipError_t set_timeline_buffer(uint64_t* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_tl), &p, sizeof(p)); }
+#endif
 
+#endif
 }  // namespace kbhip

@@ -1703,9 +1703,10 @@ static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
 // device requests — the allocate pops of sessions with Backfilled nodes or of
 // pod-affinity classes (placements 6 / 7: one pop in flight per session) and
 // the reclaim / preempt node rankings — go to this batcher, which issues a
-// STEP once every member has a request in (a member doing other work — a
-// per-task sweep, host bookkeeping — is waited for; one that leaves its action
-// leaves the group): one multi-session launch per kind and device
+// STEP of a kind once every member inside an action of that kind (allocate for
+// pops; reclaim / preempt for rankings) has a request in (a member doing other
+// work in its action — a per-task sweep, host bookkeeping — is waited for; one
+// that leaves its action leaves that lane): one multi-session launch per kind and device
 // (k_pop_batch_multi / the k_rank_*_multi sorts, blockIdx.y = session), up to
 // kPopMulti pops per launch.  Pops are ordered by events after each session's
 // earlier device work and before its later work; their results are the
@@ -1731,9 +1732,15 @@ struct StepBatcher {
         int batch = 0;                // requests of its kind in the launch that served it
     };
     std::mutex mu;
-    vector<Req*> pending;
-    int members = 0;  // grouped sessions inside an action
-    bool busy = false;
+    // One lockstep lane per request kind: the members inside allocate step
+    // their pops together, the members inside reclaim / preempt their rankings;
+    // a session busy in another action's host work never holds a lane up.
+    struct Lane {
+        vector<Req*> pending;
+        int members = 0;  // grouped sessions inside an action of this kind
+        bool busy = false;
+    };
+    Lane lane[2];
     int64_t steps = 0;
     struct Dev {
         hipStream_t st = nullptr;  // pop launches
@@ -1745,14 +1752,14 @@ struct StepBatcher {
     };
     std::map<int, Dev> dev;
 
-    void join() {
+    void join(int kind) {
         std::lock_guard<std::mutex> lk(mu);
-        ++members;
+        ++lane[kind].members;
     }
-    void leave() {
+    void leave(int kind) {
         std::unique_lock<std::mutex> lk(mu);
-        --members;
-        if (ready()) issue(lk);
+        --lane[kind].members;
+        if (ready(kind)) issue(lk, kind);
     }
     // The member whose request (or departure) completes the step issues it;
     // the others spin on their own request (a step is microseconds of host
@@ -1760,8 +1767,8 @@ struct StepBatcher {
     void submit(Req& r) {
         {
             std::unique_lock<std::mutex> lk(mu);
-            pending.push_back(&r);
-            if (ready()) issue(lk);
+            lane[r.kind].pending.push_back(&r);
+            if (ready(r.kind)) issue(lk, r.kind);
         }
         for (long spin = 0; !r.done.load(std::memory_order_acquire); ++spin) {
             if ((spin & 1023) == 1023) std::this_thread::yield();
@@ -1770,29 +1777,34 @@ struct StepBatcher {
     }
 
   private:
-    bool ready() const { return !busy && !pending.empty() && (int)pending.size() >= members; }
-    // One step: every pending request (the lock is released while launching).
-    void issue(std::unique_lock<std::mutex>& lk) {
-        busy = true;
+    bool ready(int kind) const {
+        const Lane& L = lane[kind];
+        return !L.busy && !L.pending.empty() && (int)L.pending.size() >= L.members;
+    }
+    // One step of one lane: every pending request of that kind (the lock is
+    // released while launching).
+    void issue(std::unique_lock<std::mutex>& lk, int kind) {
+        Lane& L = lane[kind];
+        L.busy = true;
         vector<Req*> batch;
-        batch.swap(pending);
+        batch.swap(L.pending);
         ++steps;
         lk.unlock();
-        std::map<std::pair<int, int>, vector<Req*>> by;  // (device, kind) -> requests
-        for (Req* q : batch) by[{q->device, q->kind}].push_back(q);
+        std::map<int, vector<Req*>> by;  // device -> requests
+        for (Req* q : batch) by[q->device].push_back(q);
         for (auto& kv : by) {
             int launches = 1;
-            const hipError_t e = kv.first.second == kPop ? launch_pops(kv.first.first, kv.second, &launches)
-                                                         : launch_ranks(kv.first.first, kv.second);
+            const hipError_t e = kind == kPop ? launch_pops(kv.first, kv.second, &launches)
+                                              : launch_ranks(kv.first, kv.second);
             for (Req* q : kv.second) {
                 q->err = e;
                 q->batch = (int)((kv.second.size() + launches - 1) / launches);  // requests per launch
             }
         }
         lk.lock();
-        busy = false;
+        L.busy = false;
         for (Req* q : batch) q->done.store(true, std::memory_order_release);  // q may go away after this
-        if (ready()) issue(lk);  // requests that came in while this step was being launched
+        if (ready(kind)) issue(lk, kind);  // requests that came in while this step was being launched
     }
     Dev& device(int d, hipError_t* e) {
         Dev& D = dev[d];
@@ -1849,11 +1861,12 @@ struct StepBatcher {
 // A grouped session inside an action (StepBatcher member).
 struct GroupScope {
     bool on;
-    explicit GroupScope(bool o) : on(o) {
-        if (on) StepBatcher::get().join();
+    int kind;
+    GroupScope(bool o, int k) : on(o), kind(k) {
+        if (on) StepBatcher::get().join(kind);
     }
     ~GroupScope() {
-        if (on) StepBatcher::get().leave();
+        if (on) StepBatcher::get().leave(kind);
     }
 };
 
@@ -2716,7 +2729,7 @@ struct Allocator {
     }
 
     void run() {  // allocate.go:41-201
-        GroupScope group(S.rank_group && S.world == 1);  // what-if sessions: pops step with the group
+        GroupScope group(S.rank_group && S.world == 1, StepBatcher::kPop);  // what-if sessions: pops step with the group
         auto t0 = std::chrono::steady_clock::now();
         compile_orders();
         open_plugins();
@@ -3376,7 +3389,7 @@ struct Allocator {
         return v;
     }
     void preempt_action() {  // preempt.go:43-255
-        GroupScope group(S.rank_group);
+        GroupScope group(S.rank_group, StepBatcher::kRank);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -3446,7 +3459,7 @@ struct Allocator {
         flush_evictions();
     }
     void reclaim_action() {  // reclaim.go:41-196
-        GroupScope group(S.rank_group);
+        GroupScope group(S.rank_group, StepBatcher::kRank);
         compile_orders();
         open_plugins();
         check_evict_supported();
@@ -4167,6 +4180,28 @@ int kbhip_debug_phases(kb_session* s, double* out, int n) {
     ABI_GUARD({
         for (int i = 0; i < n && i < 20; ++i) out[i] = s->s.phase_n ? s->s.phase[i] / s->s.phase_n : 0;
         return (int)s->s.phase_n;
+    })
+}
+#endif
+
+#ifdef KBHIP_TIMELINE
+// Diagnostic build only (libkbhip_tl.so): the overlapped pops' event timeline
+// (kbhip_batch.h TL events), 32768 pops x 16 words by sequence number.
+// reset != 0 zeroes the buffer (allocating it once); otherwise copies it out.
+int64_t kbhip_debug_timeline(kb_session* s, uint64_t* out, int64_t cap_words, int reset) {
+    ABI_GUARD({
+        static uint64_t* d_tl = nullptr;
+        const size_t words = (size_t)32768 * 16;
+        HIPCHK(hipSetDevice(s->s.device));
+        if (!d_tl) {
+            HIPCHK(hipMalloc(&d_tl, words * 8));
+            HIPCHK(kbhip::set_timeline_buffer(d_tl));
+        }
+        HIPCHK(hipDeviceSynchronize());
+        if (reset) HIPCHK(hipMemset(d_tl, 0, words * 8));
+        else if (out && cap_words >= (int64_t)words) HIPCHK(hipMemcpy(out, d_tl, words * 8, hipMemcpyDeviceToHost));
+        HIPCHK(hipDeviceSynchronize());
+        return (int64_t)words;
     })
 }
 #endif
