@@ -114,8 +114,101 @@ struct TClass {
 
 }  // namespace
 
+vector<int> canon_aff_rows(const kbs::Snapshot& s) {
+    auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
+    auto a_flags = s.vec<uint8_t>("a_flags");
+    const size_t A = a_flags.size();
+    vector<int> out(A, -1);
+    if (A == 0) return out;
+    auto cnt_of = [&](const char* n) {
+        auto v = V32(n);
+        if (v.size() != A) v.assign(A, 0);
+        return v;
+    };
+    const auto nareq_s = cnt_of("a_nareq_start"), nareq_c = cnt_of("a_nareq_cnt"),
+               napref_s = cnt_of("a_napref_start"), napref_c = cnt_of("a_napref_cnt"),
+               pareq_s = cnt_of("a_pareq_start"), pareq_c = cnt_of("a_pareq_cnt"),
+               papref_s = cnt_of("a_papref_start"), papref_c = cnt_of("a_papref_cnt"),
+               paareq_s = cnt_of("a_paareq_start"), paareq_c = cnt_of("a_paareq_cnt"),
+               paapref_s = cnt_of("a_paapref_start"), paapref_c = cnt_of("a_paapref_cnt");
+    const auto es = V32("nst_expr_start"), ec = V32("nst_expr_cnt"), fs = V32("nst_field_start"),
+               fc = V32("nst_field_cnt"), nsr_key = V32("nsr_key"), nsrv = V32("nsrv"), pst_w = V32("pst_weight"),
+               pst_t = V32("pst_term");
+    const auto nsr_op = s.vec<uint8_t>("nsr_op");
+    const auto nsr_voff = s.offs("nsr_val_off", nsr_key.size());
+    const auto pat_sel = V32("pat_sel"), pat_topo = V32("pat_topo"), patns = V32("patns");
+    const auto pat_ns = s.offs("pat_ns_off", pat_sel.size());
+    const auto ls_ml = V32("ls_ml_off"), ls_me = V32("ls_me_off"), lkv_k = V32("lkv_key"), lkv_v = V32("lkv_val");
+    const auto lsr_key = V32("lsr_key"), lsrv = V32("lsrv");
+    const auto lsr_op = s.vec<uint8_t>("lsr_op");
+    const auto lsr_voff = s.offs("lsr_val_off", lsr_key.size());
+    const auto wpat_w = V32("wpat_weight"), wpat_t = V32("wpat_term");
+    vector<int32_t> sig, prev;
+    auto at = [](const vector<int32_t>& v, int64_t i) -> int32_t {
+        if (i < 0 || i >= (int64_t)v.size()) throw std::invalid_argument("affinity row reference out of range");
+        return v[i];
+    };
+    auto nsr_row = [&](int k) {  // one NodeSelectorRequirement
+        sig.push_back(at(nsr_key, k));
+        sig.push_back(k < (int)nsr_op.size() ? nsr_op[k] : -1);
+        sig.push_back(nsr_voff[k + 1] - nsr_voff[k]);
+        for (int q = nsr_voff[k]; q < nsr_voff[k + 1]; ++q) sig.push_back(at(nsrv, q));
+    };
+    auto nst = [&](int row) {  // one NodeSelectorTerm
+        sig.push_back(at(ec, row));
+        for (int k = at(es, row); k < es[row] + ec[row]; ++k) nsr_row(k);
+        sig.push_back(at(fc, row));
+        for (int k = at(fs, row); k < fs[row] + fc[row]; ++k) nsr_row(k);
+    };
+    auto pat = [&](int row) {  // one PodAffinityTerm
+        const int sr = at(pat_sel, row);
+        sig.push_back(sr < 0 ? -1 : 1);
+        if (sr >= 0) {
+            for (int k = at(ls_ml, sr); k < at(ls_ml, sr + 1); ++k) { sig.push_back(at(lkv_k, k)); sig.push_back(at(lkv_v, k)); }
+            sig.push_back(-2);
+            for (int k = at(ls_me, sr); k < at(ls_me, sr + 1); ++k) {
+                sig.push_back(at(lsr_key, k));
+                sig.push_back(k < (int)lsr_op.size() ? lsr_op[k] : -1);
+                sig.push_back(lsr_voff[k + 1] - lsr_voff[k]);
+                for (int q = lsr_voff[k]; q < lsr_voff[k + 1]; ++q) sig.push_back(at(lsrv, q));
+            }
+        }
+        sig.push_back(pat_ns[row + 1] - pat_ns[row]);
+        for (int k = pat_ns[row]; k < pat_ns[row + 1]; ++k) sig.push_back(at(patns, k));
+        sig.push_back(at(pat_topo, row));
+    };
+    std::unordered_map<string, int> ids;
+    ids.reserve(A);
+    for (size_t a = 0; a < A; ++a) {
+        sig.clear();
+        sig.push_back(a_flags[a]);
+        sig.push_back(nareq_c[a]);
+        for (int k = nareq_s[a]; k < nareq_s[a] + nareq_c[a]; ++k) nst(k);
+        sig.push_back(napref_c[a]);
+        for (int k = napref_s[a]; k < napref_s[a] + napref_c[a]; ++k) { sig.push_back(at(pst_w, k)); nst(at(pst_t, k)); }
+        for (auto* r : {&pareq_s, &paareq_s}) {
+            const auto& cnt = r == &pareq_s ? pareq_c : paareq_c;
+            sig.push_back(cnt[a]);
+            for (int k = (*r)[a]; k < (*r)[a] + cnt[a]; ++k) pat(k);
+        }
+        for (auto* r : {&papref_s, &paapref_s}) {
+            const auto& cnt = r == &papref_s ? papref_c : paapref_c;
+            sig.push_back(cnt[a]);
+            for (int k = (*r)[a]; k < (*r)[a] + cnt[a]; ++k) { sig.push_back(at(wpat_w, k)); pat(at(wpat_t, k)); }
+        }
+        if (a > 0 && sig == prev) {  // the previous row's content (consecutive pods of a gang)
+            out[a] = out[a - 1];
+            continue;
+        }
+        string key((const char*)sig.data(), sig.size() * sizeof(int32_t));
+        out[a] = ids.emplace(std::move(key), (int)a).first->second;  // id = the first row with this content
+        prev.swap(sig);
+    }
+    return out;
+}
+
 void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<AffPod>& pods,
-                          const vector<string>& ns_names, bool pred_on, bool ipa_on) {
+                          const vector<string>& ns_names, bool pred_on, bool ipa_on, const vector<int>& canon) {
     auto V32 = [&](const char* n) { return s.vec<int32_t>(n); };
     const int P = (int)pods.size();
     auto paff = V32("p_aff");
@@ -219,8 +312,10 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
         t.key = s.s(pat_topo[row]);
         return t;
     };
+    if (canon.size() != A) throw std::invalid_argument("affinity row ids do not match the rows");
     vector<ARow> rows(A);
     for (size_t a = 0; a < A; ++a) {
+        if (canon[a] != (int)a) continue;  // parsed once per content (rows[canon[a]])
         ARow& r = rows[a];
         r.pa = a_flags[a] & KBS_AFF_PA;
         r.paa = a_flags[a] & KBS_AFF_PAA;
@@ -232,7 +327,7 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     }
     auto row_of = [&](int i) -> const ARow* {
         const int a = paff.empty() ? -1 : paff[i];
-        return (a >= 0 && (size_t)a < A && rows[a].any()) ? &rows[a] : nullptr;
+        return (a >= 0 && (size_t)a < A && rows[canon[a]].any()) ? &rows[canon[a]] : nullptr;
     };
 
     // keys any selector reads (pod labels) / any term's topology key (node labels):
@@ -260,6 +355,12 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     {
         std::map<std::pair<int, LSet>, int> gid;
         for (int i = 0; i < P; ++i) {
+            if (i > 0 && pods[i].ns == pods[i - 1].ns && plo[i + 1] - plo[i] == plo[i] - plo[i - 1]) {
+                bool same = true;  // the previous pod's labels, offset for offset (a gang's pods)
+                for (int k = 0; k < plo[i + 1] - plo[i] && same; ++k)
+                    same = plk[plo[i] + k] == plk[plo[i - 1] + k] && plv[plo[i] + k] == plv[plo[i - 1] + k];
+                if (same) { group[i] = group[i - 1]; continue; }
+            }
             LSet l;
             for (int k = plo[i]; k < plo[i + 1]; ++k) {
                 const int key = okeys.get(plk[k]);
@@ -352,11 +453,34 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     vector<int> own_pa(P, -1), own_paa(P, -1);
     vector<vector<std::pair<int, int>>> own_q(P);  // (class, weight)
     vector<char> own_pred_err(P, 0);
+    // the term classes of a pod follow from its row's content, its namespace
+    // (the default of a term's namespaces) and three flags: computed once per
+    // combination, then copied
+    std::unordered_map<uint64_t, int> tc_memo;  // (canonical row, ns, flags) -> first pod
+    uint64_t last_mk = ~0ull;
+    int last_j = -1;
     for (int i = 0; i < P; ++i) {
         const ARow* r = row_of(i);
         if (!r) continue;
         const AffPod& p = pods[i];
         const bool can_target = p.session_job && (p.target || p.pending);
+        const uint64_t mk = ((uint64_t)(uint32_t)canon[paff[i]] << 32) | ((uint64_t)(uint32_t)p.ns << 3) |
+                            (can_target ? 4u : 0u) | (p.pending ? 2u : 0u) | (p.node >= 0 ? 1u : 0u);
+        if (p.ns < (1 << 28)) {
+            int j = -1;
+            if (mk == last_mk) j = last_j;  // the previous pod with a row (a gang's pods)
+            else if (auto mi = tc_memo.find(mk); mi != tc_memo.end()) j = mi->second;
+            if (j >= 0) {
+                last_mk = mk;
+                last_j = j;
+                own_ea[i] = own_ea[j]; own_r[i] = own_r[j]; own_q[i] = own_q[j];
+                own_pa[i] = own_pa[j]; own_paa[i] = own_paa[j]; own_pred_err[i] = own_pred_err[j];
+                continue;
+            }
+            tc_memo.emplace(mk, i);
+            last_mk = mk;
+            last_j = i;
+        }
         if (pred_on && can_target && r->paa) {
             for (auto& t : r->paa_req) {
                 if (bad_sel(t)) throw std::invalid_argument("invalid label selector in a required anti-affinity term");
@@ -494,14 +618,21 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
     mark("counts");
     // ---------------- programs of pending tasks ----------------
     // (label group, the pod's own term classes) -> program
-    std::map<vector<int>, AffProgram> cache;
-    vector<int> ck;
+    std::map<vector<int>, int> cache;  // -> index into progs_ (-1: empty program)
+    progs_.clear();
+    prog_of_.assign(P, -1);
+    vector<int> ck, prev_ck;
+    int prev_prog = -1;
     for (int i = 0; i < P; ++i) {
         if (!pods[i].pending) continue;
         ck.assign({group[i], own_pred_err[i], own_pa[i], own_paa[i], (int)own_ea[i].size(), (int)own_q[i].size()});
         ck.insert(ck.end(), own_ea[i].begin(), own_ea[i].end());
         for (auto& q : own_q[i]) ck.insert(ck.end(), {q.first, q.second});
         ck.insert(ck.end(), own_r[i].begin(), own_r[i].end());
+        if (!prev_ck.empty() && ck == prev_ck) {  // the previous pending pod's (a gang's pods)
+            prog_of_[i] = prev_prog;
+            continue;
+        }
         auto it = cache.find(ck);
         if (it == cache.end()) {
             AffProgram pg;
@@ -538,9 +669,16 @@ void AffinityModel::build(const kbs::Snapshot& s, int N, int npad, const vector<
             for (int c : cg)
                 if (classes[c].kind == K_Q && matches(c, g)) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ANY, 0, classes[c].scal});
             for (int c : own_r[i]) pg.upd.insert(pg.upd.end(), {UPD_SCALAR_ANY, 0, classes[c].scal});
-            it = cache.emplace(ck, std::move(pg)).first;
+            int k = -1;
+            if (!pg.empty()) {
+                k = (int)progs_.size();
+                progs_.push_back(std::move(pg));
+            }
+            it = cache.emplace(ck, k).first;
         }
-        if (!it->second.empty()) progs_.emplace(i, it->second);
+        prog_of_[i] = it->second;
+        prev_ck.swap(ck);
+        prev_prog = it->second;
     }
     mark("programs");
 }

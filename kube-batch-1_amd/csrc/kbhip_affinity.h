@@ -61,6 +61,13 @@ struct AffPod {  // what the model needs to know about each pod
     int node = -1;            // node index when on a node (node.Pods()), else -1
 };
 
+// Canonical affinity rows: rows whose raw contents (flags, node-affinity terms,
+// pod (anti-)affinity terms with their selectors, namespaces and topology keys,
+// as string-table offsets) are equal get one id, the index of the first such
+// row — the snapshot's string table is interned (kbsnap.h), so equal offsets
+// are equal strings.  The pods of one gang carry equal rows.
+std::vector<int> canon_aff_rows(const kbs::Snapshot& s);
+
 class AffinityModel {
   public:
     bool active = false;         // some pod carries pod (anti-)affinity terms
@@ -71,12 +78,16 @@ class AffinityModel {
 
     // Builds classes, tables, initial counts and the pending tasks' programs.
     // Throws std::invalid_argument for inputs outside the supported domain.
+    // row_canon: canon_aff_rows(s) (pods whose rows have one id share their terms).
     void build(const kbs::Snapshot& s, int n_nodes, int npad, const std::vector<AffPod>& pods,
-               const std::vector<std::string>& ns_names, bool pred_on, bool ipa_on);
+               const std::vector<std::string>& ns_names, bool pred_on, bool ipa_on,
+               const std::vector<int>& row_canon);
     const AffProgram* program(int pod) const {
-        auto it = progs_.find(pod);
-        return it == progs_.end() ? nullptr : &it->second;
+        const int k = pod >= 0 && pod < (int)prog_of_.size() ? prog_of_[pod] : -1;
+        return k < 0 ? nullptr : &progs_[k];
     }
+    // Programs of two pods are the same object (a sufficient test of equality).
+    int program_id(int pod) const { return pod >= 0 && pod < (int)prog_of_.size() ? prog_of_[pod] : -1; }
     // Counts of every table for the given pod states (same term classes and
     // programs as built: the pods' statuses / nodes may have changed, e.g. a
     // session carried over or victims evicted).  build() uses it for the
@@ -90,7 +101,8 @@ class AffinityModel {
     int npad() const { return npad_; }
 
   private:
-    std::map<int, AffProgram> progs_;
+    std::vector<AffProgram> progs_;  // distinct programs
+    std::vector<int> prog_of_;       // per pod: index into progs_ (-1: none)
     struct CInfo {
         int kind, space, cnt_off, scal;
     };

@@ -29,15 +29,17 @@ static __device__ uint64_t* g_stamps;
 // number: TL = one writer, TL_MAX = the latest over the grid's blocks.
 constexpr int kTlSlots = 32768, kTlEvents = 16;
 static __device__ uint64_t* g_tl;
+// (no buffer set: nothing is written)
 #define TL(seq, ev)                                                                             \
     do {                                                                                        \
-        g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime();         \
+        if (g_tl) g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
-#define TL_VAL(seq, ev, v) do { g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = (v); } while (0)
+#define TL_VAL(seq, ev, v) do { if (g_tl) g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = (v); } while (0)
 #define TL_MAX(seq, ev)                                                                         \
     do {                                                                                        \
-        atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],            \
-                  (unsigned long long)__builtin_amdgcn_s_memrealtime());                        \
+        if (g_tl)                                                                               \
+            atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],        \
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());                    \
     } while (0)
 #else
 #define TL(seq, ev) do {} while (0)
@@ -147,16 +149,30 @@ __device__ __forceinline__ T half_clean_desc(T v) {
     const T o = xor_lane<J>(v);
     return ((lane & J) == 0) ? (o > v ? o : v) : (o < v ? o : v);
 }
+// A bitonic 64-sequence sorted descending (half-cleaners at 32 .. 1).
 template <typename T>
-__device__ __forceinline__ T wave_merge_desc(T a, T b) {
-    const T br = reverse_lanes(b);
-    T v = a > br ? a : br;  // bitonic, holds the top 64 of a U b
+__device__ __forceinline__ T bitonic_clean_desc(T v) {
     v = half_clean_desc<32>(v);
     v = half_clean_desc<16>(v);
     v = half_clean_desc<8>(v);
     v = half_clean_desc<4>(v);
     v = half_clean_desc<2>(v);
     return half_clean_desc<1>(v);
+}
+template <typename T>
+__device__ __forceinline__ T wave_merge_desc(T a, T b) {
+    const T br = reverse_lanes(b);
+    return bitonic_clean_desc(a > br ? a : br);  // bitonic, holds the top 64 of a U b
+}
+// Top 128 of two descending 128-lists held as (ranks 0..63, ranks 64..127):
+// c[i] = max(a[i], b[127 - i]) is bitonic and holds them; one exchange at
+// distance 64, then each half is cleaned.
+template <typename T>
+__device__ __forceinline__ void wave_merge128_desc(T& a0, T& a1, T b0, T b1) {
+    const T r1 = reverse_lanes(b1), r0 = reverse_lanes(b0);
+    const T c0 = a0 > r1 ? a0 : r1, c1 = a1 > r0 ? a1 : r0;
+    a0 = bitonic_clean_desc(c0 > c1 ? c0 : c1);
+    a1 = bitonic_clean_desc(c0 > c1 ? c1 : c0);
 }
 
 // Results land in pinned host memory as self-tagged 8-byte granules, one per
@@ -329,6 +345,28 @@ __device__ __forceinline__ T get_list(const T* src) {
 constexpr int kGroups = KBHIP_GROUPS;  // second-level merge groups (blockIdx % kGroups)
 static_assert(kGroups >= 1 && kGroups <= 32, "group lists and counters");
 constexpr int kCtrStride = 32;    // one counter per 128-byte line
+
+// Tree merge of the 8 per-wave sorted lists in wl[] into the block's sorted
+// top 128: ranks 0..63 in wl[0], 64..127 in wl2[0] (all waves call).
+template <typename T>
+__device__ __forceinline__ void block_tree_merge128(T (*wl)[64], T (*wl2)[64], int wave, int lane) {
+    if (wave < kPopThreads / 128) {  // two 64-lists -> one sorted 128-list
+        const T a = wl[wave][lane], b = reverse_lanes(wl[wave + kPopThreads / 128][lane]);
+        wl[wave][lane] = bitonic_clean_desc(a > b ? a : b);
+        wl2[wave][lane] = bitonic_clean_desc(a > b ? b : a);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = kPopThreads / 256; s >= 1; s >>= 1) {
+        if (wave < s) {
+            T a0 = wl[wave][lane], a1 = wl2[wave][lane];
+            wave_merge128_desc(a0, a1, wl[wave + s][lane], wl2[wave + s][lane]);
+            wl[wave][lane] = a0;
+            wl2[wave][lane] = a1;
+        }
+        __syncthreads();
+    }
+}
 
 // Tree merge of the 8 per-wave lists in wl[] into wl[0] (all waves call).
 template <typename T>

@@ -520,38 +520,93 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
     }
-    __syncthreads();  // s_skip zeroed
     int tn = -1;  // wave 0: candidate `lane` of pop seq-1 (-1: none)
-    if (wave == 0) {
-        bool ok = true;
-        if (seq > 1) {
-            const uint32_t want = seq - 1;
-            long spin = 0;
-            while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
-                if (++spin >= kLinkSpin) ok = false;
-                __builtin_amdgcn_s_sleep(2);
-                tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+    if constexpr (R == 1) {
+        // The block's top 128 over all its nodes, sorted and merged before pop
+        // seq-1's candidates are known (they arrive at the end of its patch);
+        // then those of them in this block (at most 64) leave the list and
+        // the counts, and the first 64 left are the block's exact top 64.
+        __shared__ KT wlk2[kPopThreads / 64][64];  // ranks 64..127 of the block merge
+        __shared__ uint8_t s_fb[kPopThreads];      // FitDelta bits per node
+        s_fb[threadIdx.x] = (uint8_t)fbs[0];
+        fit_block_add(s_fitb, fbs[0]);
+        wlk[wave][lane] = wave_sort_desc(keys[0]);
+        __syncthreads();  // s_skip, s_fitb zeroed; wave lists and s_fb written
+        STAMP(blockIdx.x * 4 + 1);
+        block_tree_merge128(wlk, wlk2, wave, lane);
+        if (wave == 0) {
+            bool ok = true;
+            if (seq > 1) {
+                const uint32_t want = seq - 1;
+                long spin = 0;
+                while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
+                    if (++spin >= kLinkSpin) ok = false;
+                    __builtin_amdgcn_s_sleep(2);
+                    tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+                }
+                tn = ok ? (int)(uint32_t)tv : -1;
             }
-            tn = ok ? (int)(uint32_t)tv : -1;
-            if (tn >= base && tn < base + R * kPopThreads)
-                atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
-        }
-        if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
-    }
-    __syncthreads();
-    KT best = 0;
+            if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
+            const bool mine = tn >= base && tn < base + kPopThreads;  // rows in flight: counted by the patch
+            if (mine) atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
+            const uint32_t fb = mine ? s_fb[tn - base] : 0u;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int o = r * kPopThreads + threadIdx.x;
-        const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: counted by the patch
-        fit_block_add(s_fitb, skip ? 0u : fbs[r]);
-        const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
-        best = r == 0 ? k : wave_merge_desc(best, k);
+            for (int b = 0; b < 4; ++b) {
+                const int cnt = __popcll(__ballot((fb >> b) & 1u));
+                if (lane == b && cnt) s_fitb[b] -= (uint32_t)cnt;
+            }
+            const KT k0 = wlk[0][lane], k1 = wlk2[0][lane];
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's s_skip bits and list reads
+            __builtin_amdgcn_wave_barrier();
+            auto kept = [&](KT k) {
+                if (!k) return false;
+                const int o = key_node(k, a) - base;
+                return ((s_skip[o >> 5] >> (o & 31)) & 1u) == 0;
+            };
+            const bool c0 = kept(k0), c1 = kept(k1);
+            const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+            const int q0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0));
+            const int q1 = __popcll(m0) +
+                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0));
+            wlk[0][lane] = 0;  // LDS operations of one wave complete in order
+            if (c0) wlk[0][q0] = k0;  // q0 < 64
+            if (c1 && q1 < 64) wlk[0][q1] = k1;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+        }
+    } else {
+        __syncthreads();  // s_skip zeroed
+        if (wave == 0) {
+            bool ok = true;
+            if (seq > 1) {
+                const uint32_t want = seq - 1;
+                long spin = 0;
+                while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
+                    if (++spin >= kLinkSpin) ok = false;
+                    __builtin_amdgcn_s_sleep(2);
+                    tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+                }
+                tn = ok ? (int)(uint32_t)tv : -1;
+                if (tn >= base && tn < base + R * kPopThreads)
+                    atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
+            }
+            if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
+        }
+        __syncthreads();
+        KT best = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int o = r * kPopThreads + threadIdx.x;
+            const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: counted by the patch
+            fit_block_add(s_fitb, skip ? 0u : fbs[r]);
+            const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
+            best = r == 0 ? k : wave_merge_desc(best, k);
+        }
+        wlk[wave][lane] = best;
+        __syncthreads();
+        STAMP(blockIdx.x * 4 + 1);
+        block_tree_merge(wlk, wave, lane);
     }
-    wlk[wave][lane] = best;
-    __syncthreads();
-    STAMP(blockIdx.x * 4 + 1);
-    block_tree_merge(wlk, wave, lane);
     const int nb = gridDim.x;
     const int g = blockIdx.x % kGroups;
     const int g_count = (nb - g + kGroups - 1) / kGroups;
@@ -596,10 +651,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     // 2b. last group merger: the top-64 of every node but the previous pop's candidates
     STAMP(gridDim.x * 4 + 4);
+    __shared__ RowCache rc;
     {
         KT acc = 0;
         for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
         wlk[wave][lane] = acc;
+        for (int h = threadIdx.x; h < kHash; h += kPopThreads) rc.hkey[h] = -1;  // before either wave inserts
     }
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
@@ -610,44 +667,37 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     // the sweep's FitDelta counts (every block added before it arrived), left in flight
     const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
-    // 3. while pop seq-1 may still write back: the rows of this list's nodes
-    // (final: no pop in flight touches them) and the static parts of pop
-    // seq-1's candidates, into the row cache
-    __shared__ RowCache rc;
-    int32_t pna = 0;  // wave 0: pop seq-1's candidate `lane`: node-affinity weight, static predicates
-    bool pst = false;
-    if (wave == 0) {
-        for (int h = lane; h < kHash; h += 64) rc.hkey[h] = -1;
+    // 3. Wave 1: the rows of this list's nodes (final: no pop in flight
+    // touches them) into the row cache.  Wave 0 at the same time: pop seq-1's
+    // write-back (which follows seq-2's; relaxed sc1 poll, issued together with
+    // the static parts of pop seq-1's candidates), then those candidates on
+    // their final rows (sc1 loads) merged into the list.
+    if (wave == 1) {
         const KT lk = wlk[0][lane];
         const int ln = lk ? key_node(lk, a) : -1;
         if (ln >= 0) {
             rc.row[lane] = load_row(nc, ln);
             for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < port_win(c, nc)) ? load_port_t<false>(nc, c.pw_lo + w, ln) : 0;
             rc.na[lane] = cf.score_mult ? na_weight(c, t, nc, ln) : 0;
+            rc_insert(&rc, ln, lane);
         }
+        if (lane == 0) TL(seq, 12);
+    }
+    if (wave == 0) {
+        bool ok = s_ok;
+        int32_t pna = 0;  // pop seq-1's candidate `lane`: node-affinity weight, static predicates
+        bool pst = false;
         if (tn >= 0) {
             pst = static_pred(cf, c, t, nc, tn);
             pna = (pst && cf.score_mult) ? na_weight(c, t, nc, tn) : 0;
         }
-        __builtin_amdgcn_wave_barrier();
-        if (ln >= 0) rc_insert(&rc, ln, lane);
-    }
-    // pop seq-1's write-back, which follows seq-2's (relaxed sc1 poll; every
-    // load of their rows below is sc1); its candidates on final rows
-    if (threadIdx.x == 0) {
-        bool ok = s_ok;
         long spin = 0;
-        while (ok && (int32_t)(ld_sc1(&link->done) - (seq - 1)) < 0) {
+        while (ok && (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
             if (++spin >= kLinkSpin) ok = false;
             __builtin_amdgcn_s_sleep(2);
         }
-        s_ok = ok;
-        TL(seq, 5);
-    }
-    __syncthreads();
-    STAMP(gridDim.x * 4 + 10);
-    const bool ok = s_ok;
-    if (wave == 0) {
+        if (lane == 0) TL(seq, 5);
+        STAMP(gridDim.x * 4 + 10);
         KT e0 = 0;
         uint32_t fb_prev = 0;  // FitDelta bits of the previous pop's candidates (left out of the sweep)
         if (ok && tn >= 0) {  // pop seq-1's candidates: rows into the cache, keys
@@ -659,6 +709,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;
             rc_insert(&rc, tn, 64 + lane);
+            TL(seq, 13);
             int32_t sc;
             bool passed;
             e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn, pst, pna, &sc, &passed), a);
@@ -675,10 +726,12 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         st_sc1(&link->touched[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint32_t)tnode);
         if (lane == 0) TL(seq, 6);
         wl[0][lane] = ok ? key64_of(top, a) : 0;
+        if (lane == 0) s_ok = ok;
     }
     __syncthreads();
     STAMP(gridDim.x * 4 + 1);
-    if (ok) {
+    if (threadIdx.x == 0) TL(seq, 11);
+    if (s_ok) {
         if (a.ent32)
             place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
         else

@@ -1129,9 +1129,12 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     // ---------------- pod (anti-)affinity model (kbhip_affinity.h) ----------------
     S.aff.reset(new AffinityModel());
     AffinityModel& aff = *S.aff;
+    vector<int> row_canon;  // canonical affinity row of every row (kbhip_affinity.h)
     {  // ap: filled in pass B
         try {
-            aff.build(s, N, npad, ap, E.nss.strs, S.conf.pred_on != 0, S.conf.score_mult > 0 && S.conf.w_pa != 0);
+            row_canon = canon_aff_rows(s);
+            aff.build(s, N, npad, ap, E.nss.strs, S.conf.pred_on != 0, S.conf.score_mult > 0 && S.conf.w_pa != 0,
+                      row_canon);
         } catch (const std::invalid_argument& e) {
             fail_unsupported(e.what());
         }
@@ -1234,6 +1237,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         return true;
     };
     auto same_prog = [&](int a, int b) {
+        if (aff.program_id(a) == aff.program_id(b)) return true;
         const AffProgram *x = aff.program(a), *y = aff.program(b);
         if (!x || !y) return x == y;
         return x->ea == y->ea && x->pa_space == y->pa_space && x->pa_cnt == y->pa_cnt && x->pa_total == y->pa_total &&
@@ -1248,7 +1252,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (A.req.c != B.req.c || A.req.m != B.req.m || A.req.g != B.req.g) return false;
         if (A.ireq.c != B.ireq.c || A.ireq.m != B.ireq.m || A.ireq.g != B.ireq.g) return false;
         if (A.nzc != B.nzc || A.nzm != B.nzm || pod_ports[a] != pod_ports[b]) return false;
-        if ((paff.empty() ? -1 : paff[a]) != (paff.empty() ? -1 : paff[b])) return false;
+        auto row = [&](int i) {  // equal contents, equal id
+            const int r = paff.empty() ? -1 : paff[i];
+            return r >= 0 && r < (int)row_canon.size() ? row_canon[r] : r;
+        };
+        if (row(a) != row(b)) return false;
         if (!same_run(pso, a, b, {&psk, &psv})) return false;
         if (!same_run(pto, a, b, {&tlk, &tlo, &tlv, &tle})) return false;
         if (aff.active && !(same_run(plo, a, b, {&plk, &plv}) && same_prog(a, b))) return false;

@@ -7,7 +7,9 @@ loop.  Never used for timing claims (the events cost a few stores per pop).
 Events per pop e: 0 first block started, 1 last block saw pop e-1's candidates,
 2 last block stored its list, 3 last group list stored, 4 final merge done,
 5 pop e-1's done seen, 6 own candidates published, 7 placement decided,
-8 done written; 9 = 1 fast placement / 2 levels; 10 = tasks placed.
+8 done written; 9 = 1 fast placement / 2 levels; 10 = tasks placed; 11 placement
+start (after the barrier); 12 wave 1 gathered the list rows; 13 previous
+candidates' rows loaded (the last lane's store).
 usage: python profiles/timeline.py [--out F]"""
 import ctypes, json, os, sys
 import numpy as np
@@ -26,6 +28,7 @@ L.kbhip_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_in
 W = 32768 * 16
 buf = np.zeros(W, dtype=np.uint64)
 with kbhip.Session(p) as s:
+    assert L.kbhip_debug_timeline(s._h, None, 0, 1) == W  # the buffer exists before any kernel runs
     s.allocate()  # warm
 with kbhip.Session(p) as s:
     assert L.kbhip_debug_timeline(s._h, None, 0, 1) == W
@@ -53,6 +56,10 @@ out = {
     "done(e-1) written -> seen": us(cur[:, 5] - prev[:, 8]),
     "done(e-1) seen -> touched(e) published (patch)": us(cur[:, 6] - cur[:, 5]),
     "touched(e) -> placement decided": us(cur[:, 7] - cur[:, 6]),
+    "done(e-1) seen -> previous candidates' rows loaded": us(cur[:, 13] - cur[:, 5]),
+    "final merge done -> list rows gathered (wave 1)": us(cur[:, 12] - cur[:, 4]),
+    "touched(e) -> placement start (barrier)": us(cur[:, 11] - cur[:, 6]),
+    "placement start -> placement decided": us(cur[:, 7] - cur[:, 11]),
     "placement decided -> done(e)": us(cur[:, 8] - cur[:, 7]),
     "touched(e-1) -> done(e-1)": us(prev[:, 8] - prev[:, 6]),
     "touched(e-1) -> final merge done(e)": us(cur[:, 4] - prev[:, 6]),
