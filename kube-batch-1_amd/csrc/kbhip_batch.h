@@ -27,7 +27,7 @@ static __device__ uint64_t* g_stamps;
 // Diagnostic build only: steady-state timeline of the overlapped pops at full
 // speed (s_memrealtime, 100 MHz), kTlSlots pops x kTlEvents words by sequence
 // number: TL = one writer, TL_MAX = the latest over the grid's blocks.
-constexpr int kTlSlots = 32768, kTlEvents = 16;
+constexpr int kTlSlots = 32768, kTlEvents = 32;
 static __device__ uint64_t* g_tl;
 // (no buffer set: nothing is written)
 #define TL(seq, ev)                                                                             \
@@ -41,10 +41,17 @@ static __device__ uint64_t* g_tl;
             atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],        \
                       (unsigned long long)__builtin_amdgcn_s_memrealtime());                    \
     } while (0)
+#define TL_MIN(seq, ev)                                                                         \
+    do {                                                                                        \
+        if (g_tl)                                                                               \
+            atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],        \
+                      ~(unsigned long long)__builtin_amdgcn_s_memrealtime());                   \
+    } while (0)
 #else
 #define TL(seq, ev) do {} while (0)
 #define TL_VAL(seq, ev, v) do {} while (0)
 #define TL_MAX(seq, ev) do {} while (0)
+#define TL_MIN(seq, ev) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -313,7 +320,7 @@ __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClas
     const Row r = load_row_sc1(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, n);
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, n);
     int32_t s;
     bool passed;
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
@@ -516,7 +523,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     } else if (n >= 0) {
         base = load_row_t<SC1>(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     STAMP(gridDim.x * 4 + 11);
@@ -527,10 +534,14 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
     // entry.  A second entry of any candidate is its running minimum after one
     // commit at depth 1, and deeper entries are below it; if none of the first
     // m candidates' depth-1 entries reaches T0, the chunk's top m entries are
-    // the first m candidates once each, in list order.  Every wave evaluates
-    // the same test on the same inputs (no barrier); waves 1.. then leave.
-    bool fast = false;
-    {
+    // the first m candidates once each, in list order.  Wave 0 decides; the
+    // other waves learn it at the barrier the levels need anyway.
+    __shared__ int s_fast;
+    if constexpr (SC1) {
+        if (threadIdx.x == 0) TL(seq, 14);
+    }
+    if (wave == 0) {
+        bool fast0 = false;
         const uint64_t Km = m >= 1 && m <= 64 ? readlane64(K, m - 1) : 0;
         if (Km) {  // the first m candidates are all feasible
             const int ap0 = key_kind(K) == 2 ? 0 : 64;
@@ -548,8 +559,16 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
                     reach = rm > sm || (rm == sm && n < key_idx(Km));
                 }
             }
-            fast = __ballot(reach) == 0;
+            fast0 = __ballot(reach) == 0;
         }
+        if (lane == 0) s_fast = fast0;
+        if (!fast0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
+    }
+    if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
+    __syncthreads();  // the decision; K read by every wave; wl free
+    const bool fast = s_fast != 0;
+    if constexpr (SC1) {
+        if (threadIdx.x == 0) TL(seq, 15);
     }
     ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
     int lf = 0, kind = 0, cc = 0, ap_l = 64;
@@ -563,9 +582,6 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
         kind = inm ? key_kind(K) : 0;
         ap_l = key_kind(K) == 2 ? 0 : 64;
     } else {
-    if (wave == 0) { s_apos[lane] = 64; s_cnt[lane] = 0; }
-    if (threadIdx.x < kHash) s_hkey[threadIdx.x] = -1;
-    __syncthreads();  // K read by every wave; wl free
     STAMP(gridDim.x * 4 + 12);
     if (wave == 0 && n >= 0) {  // candidate nodes are distinct
         int h = hash_slot(n);
@@ -721,7 +737,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             st_sc1(&nc.nzc[ln], r.nzc);
             st_sc1(&nc.nzm[ln], r.nzm);
             if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
         } else {
             nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
             nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
@@ -729,7 +745,7 @@ __device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTabl
             nc.nzc[ln] = r.nzc;
             nc.nzm[ln] = r.nzm;
             if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
         }
     }
     if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
@@ -773,7 +789,7 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
     if (n >= 0) {
         r = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     const bool has_bf = (r.bf_cpu | r.bf_mem | r.bf_gpu) != 0;
@@ -814,7 +830,7 @@ __device__ void place_bf(const Conf& cf, const NodeCols& nc, const DevTables& t,
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pw[w];
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, n)] = pw[w];
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane],
@@ -868,7 +884,7 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
     if (n >= 0) {
         r = load_row(nc, n);
         if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     const uint64_t t0 = readlane64(K, 63);  // the list's last key (0: the list holds every feasible node)
@@ -933,7 +949,7 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         nc.nzc[n] = r.nzc;
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
-            for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] = pw[w];
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, n)] = pw[w];
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane],
@@ -996,7 +1012,7 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
             e.node = g;
             e.row = load_row(nc, n);
             if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
             e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
         }
         const uint32_t sweep = fit_sum(fit_raw);  // count b in lane b

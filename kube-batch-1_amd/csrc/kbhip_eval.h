@@ -181,7 +181,7 @@ KBHIP_HD uint64_t dyn_key(const Conf& cf, const TaskClass& c, const DevTables& t
     if (cf.pred_on) {
         if (r.maxtasks <= r.pods) ok = false;                            // predicates.go:127
         if (c.has_ports)                                                 // host_ports.go:96-125
-            for (int w = 0; w < port_win(c, nc); ++w)
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc))
                 if (portw[w] & t.masks[c.pconf_off + w]) ok = false;
     }
     if (ok && c.score_err) ok = false;  // NodeOrderFn error drops the node (allocate.go:141-145)
@@ -223,7 +223,7 @@ KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables&
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
     const bool st = static_pred(cf, c, t, nc, n);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
@@ -241,7 +241,7 @@ KBHIP_HD uint64_t eval_node_walk(const Conf& cf, const TaskClass& c, const DevTa
     const Row r = load_row(nc, n);  // before the predicates' early exits (eval_node)
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
     const bool st = static_pred(cf, c, t, nc, n);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     int32_t s = 0;
@@ -316,7 +316,7 @@ KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTab
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) pw[w] = nc.ports[port_at(c, nc, w, n)];
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed, ipa);
     if (fit) *fit = fit_bits(c, r, *passed);
     return k;
@@ -331,7 +331,7 @@ KBHIP_HD uint64_t eval_first_fit(const Conf& cf, const TaskClass& c, const DevTa
         if (c.aff) ok = aff_pred(c, t, nc, n);
         if (nc.maxtasks[n] <= nc.pods[n]) ok = false;                    // predicates.go:127
         if (c.has_ports)                                                 // host_ports.go:96-125
-            for (int w = 0; w < port_win(c, nc); ++w)
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc))
                 if (nc.ports[port_at(c, nc, w, n)] & t.masks[c.pconf_off + w]) ok = false;
     }
     return ok ? pack_key(0, n + nc.base, 0) : 0;
@@ -395,7 +395,7 @@ KBHIP_HD void commit_node(const TaskClass& c, const DevTables& t, const NodeCols
     nc.nzc[n] += c.nz_cpu;
     nc.nzm[n] += c.nz_mem;
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] |= t.masks[c.pown_off + w];
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, n)] |= t.masks[c.pown_off + w];
 }
 
 // Exact inverse of commit_node for a batched-path class (integer updates; the
@@ -409,7 +409,7 @@ KBHIP_HD void uncommit_node(const TaskClass& c, const DevTables& t, const NodeCo
     nc.nzc[n] -= c.nz_cpu;
     nc.nzm[n] -= c.nz_mem;
     if (c.has_ports)
-        for (int w = 0; w < port_win(c, nc); ++w) nc.ports[port_at(c, nc, w, n)] &= ~t.masks[c.pown_off + w];
+        for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, n)] &= ~t.masks[c.pown_off + w];
 }
 
 // Gang bookkeeping after an assignment: allocate.go:191-195 + gang.go:63-66.

@@ -111,6 +111,9 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
 // -1: none).  At session open: done 0, every slot tagged 0 with no nodes.
 constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
+// Overlapped pops' lists as self-tagged granules: 64 keys + 4 FitDelta counts
+// per block and per group, 80 words (5 lines) apart.
+constexpr int kCandStride = 80;
 constexpr int kMaxDep = 1;     // previous pops an overlapped pop runs beside (streams - 1)
 constexpr int kLinkSlots = 2;  // > kMaxDep: a slot is rewritten only after its readers finished
 struct PopLink {

@@ -490,15 +490,20 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
-    __shared__ int role, s_ok;
+    __shared__ int role, s_ok, s_bad;
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
     uint32_t* fitc = fit_counters(arrive, a.fit_set);
     fit_zero_other(arrive, a.fit_set);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_bad = 0;  // a merger's poll timed out (before the first barrier)
+    // one node per lane, 32-bit keys: the blocks' and groups' lists travel as
+    // self-tagged granules to fixed mergers (else: counters, last arriver merges)
+    constexpr bool kTagged = R == 1 && sizeof(KT) == 4;
     STAMP(blockIdx.x * 4 + 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) TL(seq, 0);
+    if (threadIdx.x == 0) { TL_MIN(seq, 16); TL_MAX(seq, 17); }
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
     // pop seq-1 may still be writing rows: its candidates, in flight while the rows below load
@@ -534,6 +539,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         __syncthreads();  // s_skip, s_fitb zeroed; wave lists and s_fb written
         STAMP(blockIdx.x * 4 + 1);
         block_tree_merge128(wlk, wlk2, wave, lane);
+        if (threadIdx.x == 0) { TL_MAX(seq, 18); TL_MIN(seq, 19); }
         if (wave == 0) {
             bool ok = true;
             if (seq > 1) {
@@ -553,7 +559,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int cnt = __popcll(__ballot((fb >> b) & 1u));
-                if (lane == b && cnt) s_fitb[b] -= (uint32_t)cnt;
+                if (lane == b && cnt) atomicSub(&s_fitb[b], (uint32_t)cnt);  // group mergers' waves add concurrently
             }
             const KT k0 = wlk[0][lane], k1 = wlk2[0][lane];
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's s_skip bits and list reads
@@ -611,6 +617,97 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int g = blockIdx.x % kGroups;
     const int g_count = (nb - g + kGroups - 1) / kGroups;
     const int n_groups = nb < kGroups ? nb : kGroups;
+    __shared__ RowCache rc;
+    uint32_t fit_raw = 0;  // wave 0 of the final merger: the sweep's FitDelta counts (fit_sum layout)
+    if constexpr (kTagged) {
+        // Merge tree by self-tagged granules {seq, key} (MI355X_MICROARCH.md
+        // handoff-1to1: no drain, no counter): block b of group g = b % 8
+        // stores its list and counts; fixed mergers — block g merges group g,
+        // block 0 then merges the groups — poll them.
+        uint64_t* G = cand64;
+        if ((int)blockIdx.x >= n_groups) {
+            if (wave == 0) {
+                uint64_t* dst = G + (int64_t)blockIdx.x * kCandStride;
+                st_sc1(&dst[lane], ((uint64_t)seq << 32) | (uint32_t)wlk[0][lane]);
+                if (lane < 4) st_sc1(&dst[64 + lane], ((uint64_t)seq << 32) | s_fitb[lane]);
+            }
+            if (threadIdx.x == 0) TL_MAX(seq, 2);
+            return;
+        }
+        // poll the granules of `cnt` lists at src[0], src[stride], ...; merge
+        // their keys into acc and add their counts to s_fitb (0: timed out)
+        auto gather = [&](const uint64_t* src, int cnt, int64_t stride, KT& acc) -> bool {
+            constexpr int kQ = 4;
+            for (int q0 = 0; q0 < cnt; q0 += kQ) {
+                uint64_t v[kQ], f[kQ];
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) {
+                    const uint64_t* p = src + (int64_t)(q0 + q) * stride;
+                    const bool in = q0 + q < cnt;
+                    v[q] = in ? ld_sc1(&p[lane]) : ((uint64_t)seq << 32);
+                    f[q] = (in && lane < 4) ? ld_sc1(&p[64 + lane]) : ((uint64_t)seq << 32);
+                }
+                long spin = 0;
+                for (;;) {
+                    bool miss = false;
+#pragma unroll
+                    for (int q = 0; q < kQ; ++q) {
+                        if (__ballot((uint32_t)(v[q] >> 32) != seq || (uint32_t)(f[q] >> 32) != seq) == 0) continue;
+                        miss = true;
+                        const uint64_t* p = src + (int64_t)(q0 + q) * stride;
+                        v[q] = ld_sc1(&p[lane]);
+                        if (lane < 4) f[q] = ld_sc1(&p[64 + lane]);
+                    }
+                    if (!miss) break;
+                    if (++spin >= kLinkSpin) return false;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) {
+                    acc = wave_merge_desc(acc, (KT)(uint32_t)v[q]);
+                    if (lane < 4 && (uint32_t)f[q]) atomicAdd(&s_fitb[lane], (uint32_t)f[q]);
+                }
+            }
+            return true;
+        };
+        // 2a. group g: this block's list (wave 0) and the lists of blocks g + 8i, i >= 1, over the waves
+        KT acc = wave == 0 ? wlk[0][lane] : (KT)0;
+        {
+            const int per = (g_count - 1 + kPopThreads / 64 - 1) / (kPopThreads / 64);  // lists per wave
+            const int i0 = 1 + wave * per;
+            const int cnt = i0 < g_count ? (g_count - i0 < per ? g_count - i0 : per) : 0;
+            if (cnt > 0 && !gather(G + (int64_t)(g + i0 * kGroups) * kCandStride, cnt, (int64_t)kGroups * kCandStride, acc))
+                s_bad = 1;
+        }
+        __syncthreads();  // wlk[0] read by wave 0 above; every wave's counts added
+        wlk[wave][lane] = acc;
+        for (int h = threadIdx.x; h < kHash; h += kPopThreads) rc.hkey[h] = -1;  // before the row cache fills
+        __syncthreads();
+        block_tree_merge(wlk, wave, lane);
+        if (g != 0) {  // publish group g (a timed-out merger publishes nothing: the final merger times out too)
+            if (wave == 0 && !s_bad) {
+                uint64_t* dst = G + (int64_t)(nb + g) * kCandStride;
+                st_sc1(&dst[lane], ((uint64_t)seq << 32) | (uint32_t)wlk[0][lane]);
+                if (lane < 4) st_sc1(&dst[64 + lane], ((uint64_t)seq << 32) | s_fitb[lane]);
+            }
+            if (threadIdx.x == 0) TL_MAX(seq, 3);
+            return;
+        }
+        // 2b. block 0: group 0's list (wave 0) and groups 1 .. n_groups-1 (wave w: group w)
+        acc = wave == 0 ? wlk[0][lane] : (KT)0;
+        if (wave >= 1 && wave < n_groups && !gather(G + (int64_t)(nb + wave) * kCandStride, 1, kCandStride, acc))
+            s_bad = 1;
+        __syncthreads();
+        wlk[wave][lane] = acc;
+        __syncthreads();
+        block_tree_merge(wlk, wave, lane);
+        if (wave == 0) {
+            fit_raw = lane < 4 ? s_fitb[lane] : 0u;
+            if (lane == 0 && s_bad) s_ok = 0;
+        }
+        STAMP(gridDim.x * 4 + 0);
+        if (threadIdx.x == 0) TL(seq, 4);
+    } else {
     KT* gcand = cand + (int64_t)nb * 64;
     if (wave == 0) {
         if (lane < 4 && s_fitb[lane])
@@ -651,7 +748,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     // 2b. last group merger: the top-64 of every node but the previous pop's candidates
     STAMP(gridDim.x * 4 + 4);
-    __shared__ RowCache rc;
     {
         KT acc = 0;
         for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
@@ -665,7 +761,8 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     if (wave == 0 && lane <= kGroups)
         __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // the sweep's FitDelta counts (every block added before it arrived), left in flight
-    const uint32_t fit_raw = wave == 0 ? fit_load(fitc, n_groups) : 0u;
+    if (wave == 0) fit_raw = fit_load(fitc, n_groups);
+    }
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
     // 3. Wave 1: the rows of this list's nodes (final: no pop in flight
     // touches them) into the row cache.  Wave 0 at the same time: pop seq-1's
@@ -704,7 +801,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             const Row r = load_row_sc1(nc, tn);
             uint64_t pw[4] = {0, 0, 0, 0};
             if (c.has_ports)
-                for (int w = 0; w < port_win(c, nc); ++w) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn);
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn);
             rc.row[64 + lane] = r;
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;

@@ -1590,7 +1590,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             S.d_shard_recv = S.b_shard_recv.alloc<ShardMsg>(S.world);
         }
         for (int k = 0; k <= kMaxDep; ++k) {
-            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>((size_t)(std::max(nb2, 1) + kMaxGroups) * 64);
+            const size_t cw = (size_t)(std::max(nb2, 1) + kMaxGroups) * kCandStride;  // tagged granules (seq >= 1)
+            S.d_cand_ov[k] = S.b_cand_ov[k].alloc<uint64_t>(cw);
+            HIPCHK(hipMemsetAsync(S.d_cand_ov[k], 0, cw * sizeof(uint64_t), st));
             S.d_arrive_ov[k] = S.b_arrive_ov[k].alloc<uint32_t>((3 * kMaxGroups + 1) * 32);
             HIPCHK(hipMemsetAsync(S.d_arrive_ov[k], 0, (3 * kMaxGroups + 1) * 32 * sizeof(uint32_t), st));
         }
@@ -4194,12 +4196,12 @@ int kbhip_debug_phases(kb_session* s, double* out, int n) {
 
 #ifdef KBHIP_TIMELINE
 // Diagnostic build only (libkbhip_tl.so): the overlapped pops' event timeline
-// (kbhip_batch.h TL events), 32768 pops x 16 words by sequence number.
+// (kbhip_batch.h TL events), 32768 pops x 32 words by sequence number.
 // reset != 0 zeroes the buffer (allocating it once); otherwise copies it out.
 int64_t kbhip_debug_timeline(kb_session* s, uint64_t* out, int64_t cap_words, int reset) {
     ABI_GUARD({
         static uint64_t* d_tl = nullptr;
-        const size_t words = (size_t)32768 * 16;
+        const size_t words = (size_t)32768 * 32;
         HIPCHK(hipSetDevice(s->s.device));
         if (!d_tl) {
             HIPCHK(hipMalloc(&d_tl, words * 8));

@@ -9,7 +9,9 @@ Events per pop e: 0 first block started, 1 last block saw pop e-1's candidates,
 5 pop e-1's done seen, 6 own candidates published, 7 placement decided,
 8 done written; 9 = 1 fast placement / 2 levels; 10 = tasks placed; 11 placement
 start (after the barrier); 12 wave 1 gathered the list rows; 13 previous
-candidates' rows loaded (the last lane's store).
+candidates' rows loaded (the last lane's store); 14 placement rows read from
+the row cache; 15 fast / levels decision known by every wave; 16 / 17 first /
+last block start; 18 / 19 last / first block done with its sort and 128-merge.
 usage: python profiles/timeline.py [--out F]"""
 import ctypes, json, os, sys
 import numpy as np
@@ -25,7 +27,7 @@ if not os.path.exists(p):
 L = kbhip.lib()
 L.kbhip_debug_timeline.restype = ctypes.c_int64
 L.kbhip_debug_timeline.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]
-W = 32768 * 16
+W = 32768 * 32
 buf = np.zeros(W, dtype=np.uint64)
 with kbhip.Session(p) as s:
     assert L.kbhip_debug_timeline(s._h, None, 0, 1) == W  # the buffer exists before any kernel runs
@@ -34,7 +36,9 @@ with kbhip.Session(p) as s:
     assert L.kbhip_debug_timeline(s._h, None, 0, 1) == W
     s.allocate()
     L.kbhip_debug_timeline(s._h, buf.ctypes.data, W, 0)
-T = buf.reshape(32768, 16).astype(np.int64)
+T = buf.reshape(32768, 32).astype(np.int64)
+for ev in (16, 19):  # minima were stored inverted (atomic max of ~t)
+    T[:, ev] = np.where(T[:, ev] != 0, ~T[:, ev], 0)
 valid = (T[:, 0] > 0) & (T[:, 8] > 0) & (T[:, 6] > 0)
 idx = np.nonzero(valid)[0]
 # consecutive pops only, skip the first 1000 (ramp) — slots are seq % 32768
@@ -60,9 +64,17 @@ out = {
     "final merge done -> list rows gathered (wave 1)": us(cur[:, 12] - cur[:, 4]),
     "touched(e) -> placement start (barrier)": us(cur[:, 11] - cur[:, 6]),
     "placement start -> placement decided": us(cur[:, 7] - cur[:, 11]),
+    "placement start -> rows from the cache": us(cur[:, 14] - cur[:, 11]),
+    "rows from the cache -> fast decision known": us(cur[:, 15] - cur[:, 14]),
+    "fast decision known -> placement decided": us(cur[:, 7] - cur[:, 15]),
     "placement decided -> done(e)": us(cur[:, 8] - cur[:, 7]),
     "touched(e-1) -> done(e-1)": us(prev[:, 8] - prev[:, 6]),
     "touched(e-1) -> final merge done(e)": us(cur[:, 4] - prev[:, 6]),
+    "kernel start -> first block start": us(cur[:, 16] - cur[:, 0]),
+    "first block start -> last block start": us(cur[:, 17] - cur[:, 16]),
+    "kernel start -> first block merged (before touched)": us(cur[:, 19] - cur[:, 0]),
+    "kernel start -> last block merged (before touched)": us(cur[:, 18] - cur[:, 0]),
+    "touched(e-1) published -> last block merged (before touched)": us(cur[:, 18] - prev[:, 6]),
     "fast placements": float(np.mean(cur[:, 9] == 1)),
     "tasks per pop": float(np.mean(cur[:, 10])),
 }
