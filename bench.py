@@ -63,7 +63,7 @@ def parse():
                          "duration; 0 = off)")
     ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
                     help="predicted job pops queued ahead of the running one")
-    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1),
+    ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2),
                     help="1: batched pops alternate over two streams, a pop's sweep beside the previous pop's "
                          "placement (device-side chaining); 0 = one pop kernel at a time")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",

@@ -25,33 +25,30 @@ static __device__ uint64_t* g_stamps;
 
 #ifdef KBHIP_TIMELINE
 // Diagnostic build only: steady-state timeline of the overlapped pops at full
-// speed (s_memrealtime, 100 MHz), kTlSlots pops x kTlEvents words by sequence
-// number: TL = one writer, TL_MAX = the latest over the grid's blocks.
+// speed (s_memrealtime, 100 MHz).  TL: one writer per event, kTlSlots pops x
+// kTlEvents words by sequence number.  TLB: per-block events of every 64th
+// pop (kTlbSamples x kTlbBlocks x 8 words after the TL area) — plain stores
+// to a block's own slots, no atomics on shared words (those perturbed the
+// timing they measured).
 constexpr int kTlSlots = 32768, kTlEvents = 32;
-static __device__ uint64_t* g_tl;
-// (no buffer set: nothing is written)
+constexpr int kTlbSamples = 512, kTlbBlocks = 256;
+static __constant__ uint64_t* g_tl;  // scalar-loaded: no vector-memory wait per event
 #define TL(seq, ev)                                                                             \
     do {                                                                                        \
         if (g_tl) g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #define TL_VAL(seq, ev, v) do { if (g_tl) g_tl[((seq) % kTlSlots) * kTlEvents + (ev)] = (v); } while (0)
-#define TL_MAX(seq, ev)                                                                         \
+#define TLB(seq, ev)                                                                            \
     do {                                                                                        \
-        if (g_tl)                                                                               \
-            atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],        \
-                      (unsigned long long)__builtin_amdgcn_s_memrealtime());                    \
-    } while (0)
-#define TL_MIN(seq, ev)                                                                         \
-    do {                                                                                        \
-        if (g_tl)                                                                               \
-            atomicMax((unsigned long long*)&g_tl[((seq) % kTlSlots) * kTlEvents + (ev)],        \
-                      ~(unsigned long long)__builtin_amdgcn_s_memrealtime());                   \
+        if (g_tl && ((seq) & 63) == 0 && blockIdx.x < kTlbBlocks)                               \
+            g_tl[(size_t)kTlSlots * kTlEvents +                                                 \
+                 ((size_t)(((seq) >> 6) % kTlbSamples) * kTlbBlocks + blockIdx.x) * 8 + (ev)] =  \
+                __builtin_amdgcn_s_memrealtime();                                               \
     } while (0)
 #else
 #define TL(seq, ev) do {} while (0)
 #define TL_VAL(seq, ev, v) do {} while (0)
-#define TL_MAX(seq, ev) do {} while (0)
-#define TL_MIN(seq, ev) do {} while (0)
+#define TLB(seq, ev) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -444,22 +441,25 @@ __device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 26
 // Rows of the nodes a placement may use, gathered before it starts (LDS):
 // the overlapped pop loads them while it waits for the previous pop, so the
 // placement reads no node row from memory.  Slot lookup by node index.
-constexpr int kRcSlots = 128;
+// Slots: 0..63 the sweep's list, 64..127 pop seq-1's candidates, 128..191
+// pop seq-2's (overlap depth 2).
+constexpr int kRcSlots = 192, kRcHash = 512;
+__device__ __forceinline__ int rc_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 23); }
 struct RowCache {
     Row row[kRcSlots];
     uint64_t pw[kRcSlots][4];
     int32_t na[kRcSlots];
-    int32_t hkey[kHash];
-    int32_t hslot[kHash];
+    int32_t hkey[kRcHash];
+    int32_t hslot[kRcHash];
 };
 __device__ __forceinline__ void rc_insert(RowCache* rc, int n, int slot) {  // n distinct
-    int h = hash_slot(n);
-    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+    int h = rc_slot(n);
+    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kRcHash - 1);
     rc->hslot[h] = slot;
 }
 __device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
-    int h = hash_slot(n);
-    for (int i = 0; i < kHash; ++i, h = (h + 1) & (kHash - 1)) {
+    int h = rc_slot(n);
+    for (int i = 0; i < kRcHash; ++i, h = (h + 1) & (kRcHash - 1)) {
         const int k = rc->hkey[h];
         if (k == n) return rc->hslot[h];
         if (k == -1) return -1;
@@ -487,7 +487,7 @@ __device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b
 }
 
 template <typename ET, bool SC1 = false>
-__device__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+__device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
                                uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0) {

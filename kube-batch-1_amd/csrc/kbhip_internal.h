@@ -114,8 +114,8 @@ constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
 // Overlapped pops' lists as self-tagged granules: 64 keys + 4 FitDelta counts
 // per block and per group, 80 words (5 lines) apart.
 constexpr int kCandStride = 80;
-constexpr int kMaxDep = 1;     // previous pops an overlapped pop runs beside (streams - 1)
-constexpr int kLinkSlots = 2;  // > kMaxDep: a slot is rewritten only after its readers finished
+constexpr int kMaxDep = 2;     // previous pops an overlapped pop runs beside (streams - 1)
+constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
@@ -130,7 +130,7 @@ struct PopLink {
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set);
+                               uint32_t seq, int fit_set, int dep);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

@@ -486,10 +486,10 @@ constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends 
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                              PopLink* link, uint32_t seq) {
+                                                              PopLink* link, uint32_t seq, int dep) {
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
-    __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's candidates
+    __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
     __shared__ int role, s_ok, s_bad;
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
@@ -503,12 +503,28 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     constexpr bool kTagged = R == 1 && sizeof(KT) == 4;
     STAMP(blockIdx.x * 4 + 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) TL(seq, 0);
-    if (threadIdx.x == 0) { TL_MIN(seq, 16); TL_MAX(seq, 17); }
+    if (threadIdx.x == 0) TLB(seq, 0);
     const TaskClass c = t.classes[a.cls];
     const int base = blockIdx.x * R * kPopThreads;
-    // pop seq-1 may still be writing rows: its candidates, in flight while the rows below load
-    uint64_t tv = 0;
+    // pop seq-1 (and with dep 2 pop seq-2) may still be writing rows: their
+    // candidates, in flight while the rows below load
+    uint64_t tv = 0, tv2 = 0;
     if (wave == 0 && seq > 1) tv = ld_sc1(&link->touched[(seq - 1) % kLinkSlots][lane]);
+    const bool dep2 = dep > 1 && seq > 2;
+    if (wave == 0 && dep2) tv2 = ld_sc1(&link->touched[(seq - 2) % kLinkSlots][lane]);
+    // wave 0: wait for the candidates of pop `want`, mark this block's among them (0: timed out)
+    auto wait_touched = [&](uint64_t& v, uint32_t want, int* node) -> bool {
+        long spin = 0;
+        while (__ballot((uint32_t)(v >> 32) != want) != 0) {  // re-read every granule
+            if (++spin >= kLinkSpin) { *node = -1; return false; }
+            __builtin_amdgcn_s_sleep(2);
+            v = ld_sc1(&link->touched[want % kLinkSlots][lane]);
+        }
+        *node = (int)(uint32_t)v;
+        if (*node >= base && *node < base + R * kPopThreads)
+            atomicOr(&s_skip[(*node - base) >> 5], 1u << ((*node - base) & 31));
+        return true;
+    };
     for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
     if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
     // 1. evaluate R nodes per lane, then leave pop seq-1's candidates out
@@ -525,37 +541,43 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
     }
-    int tn = -1;  // wave 0: candidate `lane` of pop seq-1 (-1: none)
+    int tn = -1, tn2 = -1;  // wave 0: candidate `lane` of pop seq-1 / seq-2 (-1: none)
+    bool ok2 = true;
+    __shared__ int32_t s_tn[64], s_tn2[64];  // pop seq-1's / seq-2's candidates (the final merger's other waves)
+    if (dep2) {  // pop seq-2's candidates (published about one period before this kernel began) leave the sweep
+        __syncthreads();  // s_skip zeroed
+        if (wave == 0) {
+            ok2 = wait_touched(tv2, seq - 2, &tn2);
+            s_tn2[lane] = tn2;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int o = r * kPopThreads + threadIdx.x;
+            if ((s_skip[o >> 5] >> (o & 31)) & 1u) { keys[r] = 0; fbs[r] = 0; }  // counted by the patch
+        }
+    }
     if constexpr (R == 1) {
         // The block's top 128 over all its nodes, sorted and merged before pop
         // seq-1's candidates are known (they arrive at the end of its patch);
         // then those of them in this block (at most 64) leave the list and
         // the counts, and the first 64 left are the block's exact top 64.
         __shared__ KT wlk2[kPopThreads / 64][64];  // ranks 64..127 of the block merge
-        __shared__ uint8_t s_fb[kPopThreads];      // FitDelta bits per node
+        __shared__ uint8_t s_fb[kPopThreads];      // FitDelta bits per node (0: left out already)
         s_fb[threadIdx.x] = (uint8_t)fbs[0];
         fit_block_add(s_fitb, fbs[0]);
         wlk[wave][lane] = wave_sort_desc(keys[0]);
         __syncthreads();  // s_skip, s_fitb zeroed; wave lists and s_fb written
         STAMP(blockIdx.x * 4 + 1);
         block_tree_merge128(wlk, wlk2, wave, lane);
-        if (threadIdx.x == 0) { TL_MAX(seq, 18); TL_MIN(seq, 19); }
+        if (threadIdx.x == 0) TLB(seq, 1);
         if (wave == 0) {
-            bool ok = true;
-            if (seq > 1) {
-                const uint32_t want = seq - 1;
-                long spin = 0;
-                while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
-                    if (++spin >= kLinkSpin) ok = false;
-                    __builtin_amdgcn_s_sleep(2);
-                    tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
-                }
-                tn = ok ? (int)(uint32_t)tv : -1;
-            }
-            if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
+            bool ok = ok2;
+            if (seq > 1 && !wait_touched(tv, seq - 1, &tn)) ok = false;
+            s_tn[lane] = tn;
+            if (lane == 0) { s_ok = ok; TLB(seq, 2); }
             const bool mine = tn >= base && tn < base + kPopThreads;  // rows in flight: counted by the patch
-            if (mine) atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
-            const uint32_t fb = mine ? s_fb[tn - base] : 0u;
+            const uint32_t fb = mine ? s_fb[tn - base] : 0u;  // 0 for a node of pop seq-2's too
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
                 const int cnt = __popcll(__ballot((fb >> b) & 1u));
@@ -583,20 +605,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     } else {
         __syncthreads();  // s_skip zeroed
         if (wave == 0) {
-            bool ok = true;
-            if (seq > 1) {
-                const uint32_t want = seq - 1;
-                long spin = 0;
-                while (ok && __ballot((uint32_t)(tv >> 32) != want) != 0) {  // re-read every granule
-                    if (++spin >= kLinkSpin) ok = false;
-                    __builtin_amdgcn_s_sleep(2);
-                    tv = ld_sc1(&link->touched[want % kLinkSlots][lane]);
-                }
-                tn = ok ? (int)(uint32_t)tv : -1;
-                if (tn >= base && tn < base + R * kPopThreads)
-                    atomicOr(&s_skip[(tn - base) >> 5], 1u << ((tn - base) & 31));
-            }
-            if (lane == 0) { s_ok = ok; TL_MAX(seq, 1); }
+            bool ok = ok2;
+            if (seq > 1 && !wait_touched(tv, seq - 1, &tn)) ok = false;
+            s_tn[lane] = tn;
+            if (lane == 0) { s_ok = ok; TLB(seq, 2); }
         }
         __syncthreads();
         KT best = 0;
@@ -631,7 +643,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
                 st_sc1(&dst[lane], ((uint64_t)seq << 32) | (uint32_t)wlk[0][lane]);
                 if (lane < 4) st_sc1(&dst[64 + lane], ((uint64_t)seq << 32) | s_fitb[lane]);
             }
-            if (threadIdx.x == 0) TL_MAX(seq, 2);
+            if (threadIdx.x == 0) TLB(seq, 3);
             return;
         }
         // poll the granules of `cnt` lists at src[0], src[stride], ...; merge
@@ -681,7 +693,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         __syncthreads();  // wlk[0] read by wave 0 above; every wave's counts added
         wlk[wave][lane] = acc;
-        for (int h = threadIdx.x; h < kHash; h += kPopThreads) rc.hkey[h] = -1;  // before the row cache fills
+        for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;  // before the row cache fills
         __syncthreads();
         block_tree_merge(wlk, wave, lane);
         if (g != 0) {  // publish group g (a timed-out merger publishes nothing: the final merger times out too)
@@ -690,7 +702,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
                 st_sc1(&dst[lane], ((uint64_t)seq << 32) | (uint32_t)wlk[0][lane]);
                 if (lane < 4) st_sc1(&dst[64 + lane], ((uint64_t)seq << 32) | s_fitb[lane]);
             }
-            if (threadIdx.x == 0) TL_MAX(seq, 3);
+            if (threadIdx.x == 0) TLB(seq, 4);
             return;
         }
         // 2b. block 0: group 0's list (wave 0) and groups 1 .. n_groups-1 (wave w: group w)
@@ -717,7 +729,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     }
     __syncthreads();
     STAMP(blockIdx.x * 4 + 2);
-    if (threadIdx.x == 0) { TL_MAX(seq, 2); role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1); }
+    if (threadIdx.x == 0) { TLB(seq, 3); role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1); }
     __syncthreads();
     if (!role) return;
     // 2a. last block of group g merges the group's lists
@@ -742,7 +754,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        if (threadIdx.x == 0) { TL_MAX(seq, 3); role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1); }
+        if (threadIdx.x == 0) { TLB(seq, 4); role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1); }
         __syncthreads();
         if (!role) return;
     }
@@ -752,7 +764,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         KT acc = 0;
         for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
         wlk[wave][lane] = acc;
-        for (int h = threadIdx.x; h < kHash; h += kPopThreads) rc.hkey[h] = -1;  // before either wave inserts
+        for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;  // before either wave inserts
     }
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
@@ -780,8 +792,50 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         if (lane == 0) TL(seq, 12);
     }
-    if (wave == 0) {
+    // Wave 2 (overlap depth 2) meanwhile: pop seq-2's candidates not among
+    // pop seq-1's — their rows are final once seq-1's done is seen (seq-1
+    // waited for seq-2's) — into the cache, their keys into s_e1.
+    __shared__ KT s_e1[64];
+    __shared__ uint8_t s_fb1[64];
+    if (wave == 2 && dep2) {
+        const int n2 = s_tn2[lane];
+        bool dup = n2 < 0;
+        for (int i = 0; i < 64; ++i) dup = dup || s_tn[i] == n2;
         bool ok = s_ok;
+        bool pst2 = false;
+        int32_t pna2 = 0;
+        if (!dup) {
+            pst2 = static_pred(cf, c, t, nc, n2);
+            pna2 = (pst2 && cf.score_mult) ? na_weight(c, t, nc, n2) : 0;
+        }
+        long spin = 0;
+        while (ok && (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
+            if (++spin >= kLinkSpin) ok = false;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        KT e = 0;
+        uint32_t fb = 0;
+        if (ok && !dup) {
+            const Row r = load_row_sc1(nc, n2);
+            uint64_t pw[4] = {0, 0, 0, 0};
+            if (c.has_ports)
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, n2);
+            rc.row[128 + lane] = r;
+            for (int w = 0; w < 4; ++w) rc.pw[128 + lane][w] = pw[w];
+            rc.na[128 + lane] = pna2;
+            rc_insert(&rc, n2, 128 + lane);
+            int32_t sc;
+            bool passed;
+            e = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, n2, pst2, pna2, &sc, &passed), a);
+            fb = fit_bits(c, r, passed);
+        }
+        s_e1[lane] = e;
+        s_fb1[lane] = (uint8_t)fb;
+    }
+    KT e0 = 0;
+    uint32_t fb_prev = 0;  // wave 0: FitDelta bits of pop seq-1's candidates (left out of the sweep)
+    bool ok = s_ok;
+    if (wave == 0) {
         int32_t pna = 0;  // pop seq-1's candidate `lane`: node-affinity weight, static predicates
         bool pst = false;
         if (tn >= 0) {
@@ -795,9 +849,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         if (lane == 0) TL(seq, 5);
         STAMP(gridDim.x * 4 + 10);
-        KT e0 = 0;
-        uint32_t fb_prev = 0;  // FitDelta bits of the previous pop's candidates (left out of the sweep)
-        if (ok && tn >= 0) {  // pop seq-1's candidates: rows into the cache, keys
+        if (ok && tn >= 0) {  // pop seq-1's candidates on their final rows: into the cache, keys
             const Row r = load_row_sc1(nc, tn);
             uint64_t pw[4] = {0, 0, 0, 0};
             if (c.has_ports)
@@ -806,16 +858,23 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
             rc.na[64 + lane] = pna;
             rc_insert(&rc, tn, 64 + lane);
-            TL(seq, 13);
             int32_t sc;
             bool passed;
             e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn, pst, pna, &sc, &passed), a);
             fb_prev = fit_bits(c, r, passed);
         }
-        const KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
+        TL(seq, 13);
+    }
+    if (dep2) __syncthreads();  // wave 2's keys (dep2 is uniform over the grid)
+    if (wave == 0) {
+        KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
+        if (dep2) {
+            top = wave_merge_desc(top, wave_sort_desc(s_e1[lane]));
+            fb_prev |= (uint32_t)s_fb1[lane] << 4;
+        }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int cnt = __popcll(__ballot((fb_prev >> b) & 1u));
+            const int cnt = __popcll(__ballot((fb_prev >> b) & 1u)) + __popcll(__ballot((fb_prev >> (b + 4)) & 1u));
             if (lane == b) s_fitin[b] += cnt;
         }
         // this pop's candidates, one self-tagged granule each
@@ -1116,7 +1175,7 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const TaskClass c = t.classes[a.cls];
     for (int i = threadIdx.x; i < kShardHash; i += kPopThreads) s_hk[i] = -1;
-    for (int i = threadIdx.x; i < kHash; i += kPopThreads) rc.hkey[i] = -1;
+    for (int i = threadIdx.x; i < kRcHash; i += kPopThreads) rc.hkey[i] = -1;
     if (wave == 0) {  // mailbox: every shard's message of pop `seq` has arrived (lane r polls rank r's flag)
         bool ok = true;
         if (flags && lane < world) {
@@ -1198,10 +1257,10 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
 template <typename KT>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
-                                  uint32_t seq, hipStream_t st) {
+                                  uint32_t seq, int dep, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
     hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
-                       link, seq)
+                       link, seq, dep)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1215,15 +1274,15 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set) {
-    if (seq < 1) return hipErrorInvalidValue;
+                               uint32_t seq, int fit_set, int dep) {
+    if (seq < 1 || dep < 1 || dep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, st);
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, st);
     return hipGetLastError();
 }
 

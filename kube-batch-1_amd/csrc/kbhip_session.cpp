@@ -2052,7 +2052,8 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
                                   S.d_shard_recv, S.world, out, S.stream));
     } else if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
-                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.fit_set[si]));
+                                   S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.fit_set[si],
+                                   S.overlap));
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
@@ -4158,7 +4159,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
         else if (std::strcmp(key, "overlap") == 0) {
-            if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0 or 1");
+            if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0, 1 or 2");
             if (!s->s.encode_only) {
                 HIPCHK(hipSetDevice(s->s.device));
                 kbhip::ov_quiesce(s->s);  // the stream rotation changes
@@ -4196,12 +4197,12 @@ int kbhip_debug_phases(kb_session* s, double* out, int n) {
 
 #ifdef KBHIP_TIMELINE
 // Diagnostic build only (libkbhip_tl.so): the overlapped pops' event timeline
-// (kbhip_batch.h TL events), 32768 pops x 32 words by sequence number.
+// (kbhip_batch.h TL / TLB events).
 // reset != 0 zeroes the buffer (allocating it once); otherwise copies it out.
 int64_t kbhip_debug_timeline(kb_session* s, uint64_t* out, int64_t cap_words, int reset) {
     ABI_GUARD({
         static uint64_t* d_tl = nullptr;
-        const size_t words = (size_t)32768 * 32;
+        const size_t words = (size_t)32768 * 32 + (size_t)512 * 256 * 8;  // TL + TLB areas
         HIPCHK(hipSetDevice(s->s.device));
         if (!d_tl) {
             HIPCHK(hipMalloc(&d_tl, words * 8));

@@ -11,7 +11,7 @@ import pytest
 
 from test_gpu_parity import NO_POD_AFFINITY
 
-PATHS = [dict(), dict(overlap=0), dict(batched=0), dict(speculate=0), dict(overlap=0, speculate=0)]
+PATHS = [dict(), dict(overlap=0), dict(overlap=2), dict(batched=0), dict(speculate=0), dict(overlap=0, speculate=0)]
 
 
 def _engine_close(engine, path, **opts):

@@ -202,7 +202,7 @@ def test_keys32_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
     assert _log_opt(engine, p, keys32=1) == _log_opt(engine, p, keys32=0)
 
 
-# ---- overlapped pops (two streams, device-chained) x speculation depth -------
+# ---- overlapped pops (two / three streams, device-chained) x speculation depth -------
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(16))
 def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
@@ -215,7 +215,7 @@ def test_overlap_speculation_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path,
     p = str(tmp_path / "o.kbs")
     c.write(p)
     exp = _oracle_log(oracle_mod, p)
-    for overlap, spec in ((0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (1, 3), (0, 3)):
+    for overlap, spec in ((0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (1, 3), (0, 3), (2, 0), (2, 2), (2, 3)):
         assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
@@ -224,18 +224,19 @@ def test_overlap_c2_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
     p = str(tmp_path / "c2o.kbs")
     kbgen_mod.gen_c2(p)
     exp = _oracle_log(oracle_mod, p, fast=True)
-    for overlap, spec in ((1, 3), (1, 2), (0, 2)):
+    for overlap, spec in ((1, 3), (1, 2), (0, 2), (2, 2), (2, 3)):
         assert _log_opt(engine, p, overlap=overlap, speculate=spec) == exp, (overlap, spec)
 
 
 @pytest.mark.gpu
 def test_overlap_c4_scaled_gpu(engine, kbgen_mod, tmp_path):
-    """Overlapped, two-deep speculative pops on a C4-shaped session equal one
-    pop at a time on one stream; the node state after the session too."""
+    """Overlapped (two and three streams), speculative pops on a C4-shaped
+    session equal one pop at a time on one stream; the node state after the
+    session too."""
     p = str(tmp_path / "c4o.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     logs, nodes = [], []
-    for overlap, spec in ((1, 3), (1, 2), (0, 0)):
+    for overlap, spec in ((1, 3), (1, 2), (2, 2), (2, 3), (0, 0)):
         with engine.Session(p) as s:
             s.set_option("overlap", overlap)
             s.set_option("speculate", spec)
