@@ -490,14 +490,17 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
-    __shared__ int role, s_ok, s_bad;
+    __shared__ int role, s_ok, s_bad, s_list_ready;
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
     uint32_t* fitc = fit_counters(arrive, a.fit_set);
     fit_zero_other(arrive, a.fit_set);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_bad = 0;  // a merger's poll timed out (before the first barrier)
+    if (threadIdx.x == 0) { s_bad = 0; s_list_ready = 0; }  // (before the first barrier)
+    __shared__ RowCache rc;  // the final merger's (block 0 in the tagged path)
+    if (blockIdx.x == 0)
+        for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;
     // one node per lane, 32-bit keys: the blocks' and groups' lists travel as
     // self-tagged granules to fixed mergers (else: counters, last arriver merges)
     constexpr bool kTagged = R == 1 && sizeof(KT) == 4;
@@ -629,7 +632,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     const int g = blockIdx.x % kGroups;
     const int g_count = (nb - g + kGroups - 1) / kGroups;
     const int n_groups = nb < kGroups ? nb : kGroups;
-    __shared__ RowCache rc;
     uint32_t fit_raw = 0;  // wave 0 of the final merger: the sweep's FitDelta counts (fit_sum layout)
     if constexpr (kTagged) {
         // Merge tree by self-tagged granules {seq, key} (MI355X_MICROARCH.md
@@ -693,7 +695,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         __syncthreads();  // wlk[0] read by wave 0 above; every wave's counts added
         wlk[wave][lane] = acc;
-        for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;  // before the row cache fills
         __syncthreads();
         block_tree_merge(wlk, wave, lane);
         if (g != 0) {  // publish group g (a timed-out merger publishes nothing: the final merger times out too)
@@ -705,20 +706,21 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             if (threadIdx.x == 0) TLB(seq, 4);
             return;
         }
-        // 2b. block 0: group 0's list (wave 0) and groups 1 .. n_groups-1 (wave w: group w)
-        acc = wave == 0 ? wlk[0][lane] : (KT)0;
-        if (wave >= 1 && wave < n_groups && !gather(G + (int64_t)(nb + wave) * kCandStride, 1, kCandStride, acc))
-            s_bad = 1;
-        __syncthreads();
-        wlk[wave][lane] = acc;
-        __syncthreads();
-        block_tree_merge(wlk, wave, lane);
+        // 2b. block 0, the final merger.  Wave 0 alone merges group 0's list
+        // with groups 1 .. n_groups-1 (no block-wide barrier: waves 6 / 7
+        // are meanwhile patching with the previous pops' candidates, §3) and
+        // flags the final list in LDS for wave 1.
         if (wave == 0) {
-            fit_raw = lane < 4 ? s_fitb[lane] : 0u;
-            if (lane == 0 && s_bad) s_ok = 0;
+            KT fin = wlk[0][lane];
+            if (n_groups > 1 && !gather(G + (int64_t)(nb + 1) * kCandStride, n_groups - 1, kCandStride, fin))
+                s_bad = 1;
+            wlk[0][lane] = fin;
+            fit_raw = lane < 4 ? s_fitb[lane] : 0u;  // every block's counts: this wave added the groups'
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the list is in LDS before the flag
+            if (lane == 0) __hip_atomic_store(&s_list_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            STAMP(gridDim.x * 4 + 0);
+            if (lane == 0) TL(seq, 4);
         }
-        STAMP(gridDim.x * 4 + 0);
-        if (threadIdx.x == 0) TL(seq, 4);
     } else {
     KT* gcand = cand + (int64_t)nb * 64;
     if (wave == 0) {
@@ -776,12 +778,61 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     if (wave == 0) fit_raw = fit_load(fitc, n_groups);
     }
     if (wave == 0 && lane < 4) s_fitin[lane] = 0;  // + the counts of nodes the sweep left out
-    // 3. Wave 1: the rows of this list's nodes (final: no pop in flight
-    // touches them) into the row cache.  Wave 0 at the same time: pop seq-1's
-    // write-back (which follows seq-2's; relaxed sc1 poll, issued together with
-    // the static parts of pop seq-1's candidates), then those candidates on
-    // their final rows (sc1 loads) merged into the list.
+    // 3. Waves of the final merger, side by side:
+    //   wave 1: the rows of the final list's nodes (final: no pop in flight
+    //     touches them) into the row cache (tagged: once wave 0 flags the list);
+    //   wave kP1 (tagged 6, else 0): pop seq-1's candidates — static parts,
+    //     then pop seq-1's done (relaxed sc1 poll), then their final rows
+    //     (sc1 loads) into the cache and their keys into s_e0;
+    //   wave kP2 (tagged 7, else 2; depth 2): the same for pop seq-2's
+    //     candidates not among seq-1's (final too once seq-1's done is seen:
+    //     seq-1 waited for seq-2's).
+    // Then wave 0 merges the keys into the list and publishes the candidates.
+    constexpr int kP1 = kTagged ? 6 : 0, kP2 = kTagged ? 7 : 2;
+    __shared__ KT s_e[2][64];
+    __shared__ uint8_t s_fbp[2][64];
+    auto patch = [&](int q, int node, bool skip) {
+        bool okp = true;
+        bool pst = false;
+        int32_t pna = 0;
+        const bool use = node >= 0 && !skip;
+        if (use) {
+            pst = static_pred(cf, c, t, nc, node);
+            pna = (pst && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
+        }
+        long spin = 0;
+        while ((int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
+            if (++spin >= kLinkSpin) { okp = false; break; }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (q == 0 && lane == 0) TL(seq, 5);
+        KT e = 0;
+        uint32_t fb = 0;
+        if (okp && use) {
+            const Row r = load_row_sc1(nc, node);
+            uint64_t pw[4] = {0, 0, 0, 0};
+            if (c.has_ports)
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, node);
+            const int slot = 64 * (q + 1) + lane;
+            rc.row[slot] = r;
+            for (int w = 0; w < 4; ++w) rc.pw[slot][w] = pw[w];
+            rc.na[slot] = pna;
+            rc_insert(&rc, node, slot);
+            int32_t sc;
+            bool passed;
+            e = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, node, pst, pna, &sc, &passed), a);
+            fb = fit_bits(c, r, passed);
+        }
+        if (q == 0) TL(seq, 13);
+        s_e[q][lane] = e;
+        s_fbp[q][lane] = (uint8_t)fb;
+        if (!okp && lane == 0) s_bad = 1;
+    };
     if (wave == 1) {
+        if constexpr (kTagged) {
+            while (__hip_atomic_load(&s_list_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                __builtin_amdgcn_s_sleep(1);
+        }
         const KT lk = wlk[0][lane];
         const int ln = lk ? key_node(lk, a) : -1;
         if (ln >= 0) {
@@ -792,85 +843,21 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         }
         if (lane == 0) TL(seq, 12);
     }
-    // Wave 2 (overlap depth 2) meanwhile: pop seq-2's candidates not among
-    // pop seq-1's — their rows are final once seq-1's done is seen (seq-1
-    // waited for seq-2's) — into the cache, their keys into s_e1.
-    __shared__ KT s_e1[64];
-    __shared__ uint8_t s_fb1[64];
-    if (wave == 2 && dep2) {
+    if (wave == kP1) patch(0, s_tn[lane], false);
+    if (wave == kP2 && dep2) {
         const int n2 = s_tn2[lane];
-        bool dup = n2 < 0;
+        bool dup = false;
         for (int i = 0; i < 64; ++i) dup = dup || s_tn[i] == n2;
-        bool ok = s_ok;
-        bool pst2 = false;
-        int32_t pna2 = 0;
-        if (!dup) {
-            pst2 = static_pred(cf, c, t, nc, n2);
-            pna2 = (pst2 && cf.score_mult) ? na_weight(c, t, nc, n2) : 0;
-        }
-        long spin = 0;
-        while (ok && (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
-            if (++spin >= kLinkSpin) ok = false;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        KT e = 0;
-        uint32_t fb = 0;
-        if (ok && !dup) {
-            const Row r = load_row_sc1(nc, n2);
-            uint64_t pw[4] = {0, 0, 0, 0};
-            if (c.has_ports)
-                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, n2);
-            rc.row[128 + lane] = r;
-            for (int w = 0; w < 4; ++w) rc.pw[128 + lane][w] = pw[w];
-            rc.na[128 + lane] = pna2;
-            rc_insert(&rc, n2, 128 + lane);
-            int32_t sc;
-            bool passed;
-            e = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, n2, pst2, pna2, &sc, &passed), a);
-            fb = fit_bits(c, r, passed);
-        }
-        s_e1[lane] = e;
-        s_fb1[lane] = (uint8_t)fb;
+        patch(1, n2, dup);
     }
-    KT e0 = 0;
-    uint32_t fb_prev = 0;  // wave 0: FitDelta bits of pop seq-1's candidates (left out of the sweep)
-    bool ok = s_ok;
+    __syncthreads();  // the list, the cache, the patch keys
     if (wave == 0) {
-        int32_t pna = 0;  // pop seq-1's candidate `lane`: node-affinity weight, static predicates
-        bool pst = false;
-        if (tn >= 0) {
-            pst = static_pred(cf, c, t, nc, tn);
-            pna = (pst && cf.score_mult) ? na_weight(c, t, nc, tn) : 0;
-        }
-        long spin = 0;
-        while (ok && (int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
-            if (++spin >= kLinkSpin) ok = false;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (lane == 0) TL(seq, 5);
-        STAMP(gridDim.x * 4 + 10);
-        if (ok && tn >= 0) {  // pop seq-1's candidates on their final rows: into the cache, keys
-            const Row r = load_row_sc1(nc, tn);
-            uint64_t pw[4] = {0, 0, 0, 0};
-            if (c.has_ports)
-                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, tn);
-            rc.row[64 + lane] = r;
-            for (int w = 0; w < 4; ++w) rc.pw[64 + lane][w] = pw[w];
-            rc.na[64 + lane] = pna;
-            rc_insert(&rc, tn, 64 + lane);
-            int32_t sc;
-            bool passed;
-            e0 = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, tn, pst, pna, &sc, &passed), a);
-            fb_prev = fit_bits(c, r, passed);
-        }
-        TL(seq, 13);
-    }
-    if (dep2) __syncthreads();  // wave 2's keys (dep2 is uniform over the grid)
-    if (wave == 0) {
-        KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(e0));  // all 64 lanes: cross-lane networks
+        const bool ok = s_ok && !s_bad;
+        KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(s_e[0][lane]));  // all 64 lanes: cross-lane networks
+        uint32_t fb_prev = s_fbp[0][lane];  // FitDelta bits of the candidates the sweep left out
         if (dep2) {
-            top = wave_merge_desc(top, wave_sort_desc(s_e1[lane]));
-            fb_prev |= (uint32_t)s_fb1[lane] << 4;
+            top = wave_merge_desc(top, wave_sort_desc(s_e[1][lane]));
+            fb_prev |= (uint32_t)s_fbp[1][lane] << 4;
         }
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
