@@ -449,9 +449,25 @@ struct RowCache {
     Row row[kRcSlots];
     uint64_t pw[kRcSlots][4];
     int32_t na[kRcSlots];
+    int32_t s1[kRcSlots];  // score after one more commit (depth-1 key; INT32_MIN: infeasible)
     int32_t hkey[kRcHash];
     int32_t hslot[kRcHash];
 };
+// Score of candidate n after one more commit of class c (Allocate unless its
+// key is a Pipeline), INT32_MIN when that key is infeasible: the placement's
+// fast-path test (place_parallel), computed where the row is loaded.
+__device__ __forceinline__ int32_t depth1_score(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                                const TaskClass& c, const Row& r, const uint64_t* pw, int n,
+                                                int32_t na_n, uint64_t k0) {
+    const int na = key_kind(k0) == 2 ? 0 : 1;
+    const Row r1 = apply_commits(r, c, na, 1 - na);
+    uint64_t pwc[4];
+    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
+    int32_t s1;
+    bool passed1;
+    const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
+    return k1 ? key_score(k1) : INT32_MIN;
+}
 __device__ __forceinline__ void rc_insert(RowCache* rc, int n, int slot) {  // n distinct
     int h = rc_slot(n);
     while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kRcHash - 1);
@@ -547,14 +563,20 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
             const int ap0 = key_kind(K) == 2 ? 0 : 64;
             bool reach = false;
             if (lane < m) {
-                const int na = ap0 == 0 ? 0 : 1;
-                const Row r1 = apply_commits(base, c, na, 1 - na);
-                int32_t s1;
-                bool passed1;
-                const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
-                if (k1) {
+                int32_t s1d;  // the row cache holds it (computed beside the row load), else computed here
+                if (rslot >= 0) {
+                    s1d = rc->s1[rslot];
+                } else {
+                    const int na = ap0 == 0 ? 0 : 1;
+                    const Row r1 = apply_commits(base, c, na, 1 - na);
+                    int32_t s1;
+                    bool passed1;
+                    const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
+                    s1d = k1 ? key_score(k1) : INT32_MIN;
+                }
+                if (s1d != INT32_MIN) {
                     const int32_t s0 = key_score(K), sm = key_score(Km);
-                    const int32_t rm = key_score(k1) < s0 ? key_score(k1) : s0;
+                    const int32_t rm = s1d < s0 ? s1d : s0;
                     // (rm, n, depth 1) vs (sm, node of Km, depth 0): higher score, lower index, lower depth
                     reach = rm > sm || (rm == sm && n < key_idx(Km));
                 }

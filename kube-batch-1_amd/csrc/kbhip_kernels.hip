@@ -490,14 +490,14 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
-    __shared__ int role, s_ok, s_bad, s_list_ready;
+    __shared__ int role, s_ok, s_bad, s_list_ready, s_pdone[2];
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
     uint32_t* fitc = fit_counters(arrive, a.fit_set);
     fit_zero_other(arrive, a.fit_set);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) { s_bad = 0; s_list_ready = 0; }  // (before the first barrier)
+    if (threadIdx.x == 0) { s_bad = 0; s_list_ready = 0; s_pdone[0] = s_pdone[1] = 0; }  // (before the first barrier)
     __shared__ RowCache rc;  // the final merger's (block 0 in the tagged path)
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         // poll the granules of `cnt` lists at src[0], src[stride], ...; merge
         // their keys into acc and add their counts to s_fitb (0: timed out)
         auto gather = [&](const uint64_t* src, int cnt, int64_t stride, KT& acc) -> bool {
-            constexpr int kQ = 4;
+            constexpr int kQ = 8;  // all of a wave's lists in one round trip (group: <= 4 per wave; final: 7)
             for (int q0 = 0; q0 < cnt; q0 += kQ) {
                 uint64_t v[kQ], f[kQ];
 #pragma unroll
@@ -820,13 +820,17 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             rc_insert(&rc, node, slot);
             int32_t sc;
             bool passed;
-            e = sweep_key<KT>(dyn_key(cf, c, t, nc, r, pw, node, pst, pna, &sc, &passed), a);
+            const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, pst, pna, &sc, &passed);
+            e = sweep_key<KT>(k0, a);
             fb = fit_bits(c, r, passed);
+            rc.s1[slot] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, pna, k0) : INT32_MIN;
         }
         if (q == 0) TL(seq, 13);
         s_e[q][lane] = e;
         s_fbp[q][lane] = (uint8_t)fb;
         if (!okp && lane == 0) s_bad = 1;
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the keys and the cache are in LDS before the flag
+        if (lane == 0) __hip_atomic_store(&s_pdone[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
     if (wave == 1) {
         if constexpr (kTagged) {
@@ -839,6 +843,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             rc.row[lane] = load_row(nc, ln);
             for (int w = 0; w < 4; ++w) rc.pw[lane][w] = (c.has_ports && w < port_win(c, nc)) ? load_port_t<false>(nc, c.pw_lo + w, ln) : 0;
             rc.na[lane] = cf.score_mult ? na_weight(c, t, nc, ln) : 0;
+            rc.s1[lane] = depth1_score(cf, nc, t, c, rc.row[lane], rc.pw[lane], ln, rc.na[lane], key64_of(lk, a));
             rc_insert(&rc, ln, lane);
         }
         if (lane == 0) TL(seq, 12);
@@ -850,8 +855,10 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         for (int i = 0; i < 64; ++i) dup = dup || s_tn[i] == n2;
         patch(1, n2, dup);
     }
-    __syncthreads();  // the list, the cache, the patch keys
-    if (wave == 0) {
+    if (wave == 0) {  // the patch keys (LDS flags: the list rows are needed only by the placement)
+        while ((kP1 != 0 && __hip_atomic_load(&s_pdone[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) ||
+               (dep2 && __hip_atomic_load(&s_pdone[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0))
+            __builtin_amdgcn_s_sleep(1);
         const bool ok = s_ok && !s_bad;
         KT top = wave_merge_desc(wlk[0][lane], wave_sort_desc(s_e[0][lane]));  // all 64 lanes: cross-lane networks
         uint32_t fb_prev = s_fbp[0][lane];  // FitDelta bits of the candidates the sweep left out
@@ -1219,6 +1226,7 @@ __global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols n
             rc.row[lane] = e.row;
             for (int w = 0; w < 4; ++w) rc.pw[lane][w] = e.pw[w];
             rc.na[lane] = e.na;
+            rc.s1[lane] = depth1_score(cf, nc, t, c, e.row, e.pw, g - nc.base, e.na, K);  // (the score only)
             rc_insert(&rc, g, lane);
         }
     }
