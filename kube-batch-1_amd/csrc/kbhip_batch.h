@@ -325,6 +325,30 @@ __device__ __forceinline__ uint64_t eval_node_sc1(const Conf& cf, const TaskClas
     return k;
 }
 
+// A candidate's row as kRowWords self-tagged 32-bit halves (PopLink::rows):
+// idle, releasing (cpu, mem, gpu), allocatable cpu / mem, nonzero requests
+// cpu / mem (two halves each), pod count, MaxTaskNum.  Backfilled is 0 in
+// every session whose pops overlap.
+__device__ __forceinline__ void row_words(const Row& r, uint32_t* w) {
+    const int64_t v[10] = {r.idle_cpu, r.idle_mem, r.idle_gpu, r.rel_cpu, r.rel_mem, r.rel_gpu,
+                           r.acpu, r.amem, r.nzc, r.nzm};
+#pragma unroll
+    for (int i = 0; i < 10; ++i) { w[2 * i] = (uint32_t)v[i]; w[2 * i + 1] = (uint32_t)((uint64_t)v[i] >> 32); }
+    w[20] = (uint32_t)r.pods;
+    w[21] = (uint32_t)r.maxtasks;
+}
+__device__ __forceinline__ Row words_row(const uint32_t* w) {
+    auto v = [&](int i) { return (int64_t)(((uint64_t)w[2 * i + 1] << 32) | w[2 * i]); };
+    Row r;
+    r.idle_cpu = v(0); r.idle_mem = v(1); r.idle_gpu = v(2);
+    r.rel_cpu = v(3); r.rel_mem = v(4); r.rel_gpu = v(5);
+    r.bf_cpu = r.bf_mem = r.bf_gpu = 0;
+    r.acpu = v(6); r.amem = v(7); r.nzc = v(8); r.nzm = v(9);
+    r.pods = (int32_t)w[20];
+    r.maxtasks = (int32_t)w[21];
+    return r;
+}
+
 __device__ __forceinline__ int entry_idx(uint64_t e) { return kEntryIdxMax - (int)((e >> 7) & kEntryIdxMax); }
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32 |
@@ -506,7 +530,8 @@ template <typename ET, bool SC1 = false>
 __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
                                uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
-                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0) {
+                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
+                               uint64_t (*row_msg)[64] = nullptr) {
     // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
     // (a node-array shard writes back only its own; one GPU: all of them).
     // t0 (a cut): the candidates are exact down to the selection key t0 only
@@ -770,8 +795,19 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
                 for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
         }
     }
-    if constexpr (SC1) {  // the only storing wave drained, then the flag (sc1)
+    if constexpr (SC1) {  // the only storing wave drained, then the row message, then the flag (sc1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (row_msg) {  // every candidate's row after this pop (self-tagged halves, PopLink::rows)
+            Row rw = base;
+            if (cc > 0) {
+                const int na = cc < ap_l ? cc : ap_l;
+                rw = apply_commits(base, c, na, cc - na);
+            }
+            uint32_t w[kRowWords];
+            row_words(rw, w);
+#pragma unroll
+            for (int f = 0; f < kRowWords; ++f) st_sc1(&row_msg[f][lane], ((uint64_t)seq << 32) | w[f]);
+        }
         if (lane == 0) { st_sc1(done_flag, seq); TL(seq, 8); }
     }
     if (lane < done || (done == 0 && lane == 0))

@@ -116,10 +116,18 @@ constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
 constexpr int kCandStride = 80;
 constexpr int kMaxDep = 2;     // previous pops an overlapped pop runs beside (streams - 1)
 constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
+// rows[e % kLinkSlots][f][i] = {e << 32 | half f of candidate i's row after
+// pop e} — kRowWords 32-bit halves of Row's dynamic and static fields (not
+// Backfilled: overlapped pops run only in sessions without it), written after
+// pop e's write-back drained: the next pops read their previous pops'
+// candidates' rows from here (contiguous, self-tagged) instead of polling
+// `done` and gathering the node columns.
+constexpr int kRowWords = 22;
 struct PopLink {
     uint32_t done;
     uint32_t pad0[31];
     uint64_t touched[kLinkSlots][64];
+    uint64_t rows[kLinkSlots][kRowWords][64];
 };
 // Overlapped batched pop number `seq` (>= 1) on stream st; pop seq-1 may
 // still run on the other stream: it leaves that pop's candidates out of its
@@ -130,7 +138,7 @@ struct PopLink {
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set, int dep);
+                               uint32_t seq, int fit_set, int dep, uint32_t msg_from);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

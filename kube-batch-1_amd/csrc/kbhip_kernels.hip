@@ -483,10 +483,25 @@ __device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
 
 constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
 
+// Relaxed sc1 poll of a sequence word until it reaches `want`, with two
+// loads in flight (a store that lands just after one load was issued is
+// seen by the next, about half a round trip later).  false: timed out.
+__device__ __forceinline__ bool poll_done(const uint32_t* p, uint32_t want) {
+    uint32_t a = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(p));
+    uint32_t b = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(p));
+    for (long spin = 0; spin < kLinkSpin; ++spin) {
+        if ((int32_t)(a - want) >= 0) return true;
+        a = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(p));
+        if ((int32_t)(b - want) >= 0) return true;
+        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(p));
+    }
+    return false;
+}
+
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
                                                               uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                              PopLink* link, uint32_t seq, int dep) {
+                                                              PopLink* link, uint32_t seq, int dep, uint32_t msg_from) {
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
@@ -517,11 +532,17 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     if (wave == 0 && dep2) tv2 = ld_sc1(&link->touched[(seq - 2) % kLinkSlots][lane]);
     // wave 0: wait for the candidates of pop `want`, mark this block's among them (0: timed out)
     auto wait_touched = [&](uint64_t& v, uint32_t want, int* node) -> bool {
+        // two re-reads of every granule in flight: a granule that lands just
+        // after one was issued is seen by the next, half a round trip later
+        const uint64_t* src = &link->touched[want % kLinkSlots][lane];
+        uint64_t w = ld_sc1(src);
         long spin = 0;
-        while (__ballot((uint32_t)(v >> 32) != want) != 0) {  // re-read every granule
+        for (;;) {
+            if (__ballot((uint32_t)(v >> 32) != want) == 0) break;
+            v = ld_sc1(src);
+            if (__ballot((uint32_t)(w >> 32) != want) == 0) { v = w; break; }
+            w = ld_sc1(src);
             if (++spin >= kLinkSpin) { *node = -1; return false; }
-            __builtin_amdgcn_s_sleep(2);
-            v = ld_sc1(&link->touched[want % kLinkSlots][lane]);
         }
         *node = (int)(uint32_t)v;
         if (*node >= base && *node < base + R * kPopThreads)
@@ -800,17 +821,37 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             pst = static_pred(cf, c, t, nc, node);
             pna = (pst && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
         }
-        long spin = 0;
-        while ((int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&link->done)) - (seq - 1)) < 0) {
-            if (++spin >= kLinkSpin) { okp = false; break; }
-            __builtin_amdgcn_s_sleep(2);
+        // the rows of pop `src`'s candidates as it left them: its row message
+        // (written after its write-back drained), self-tagged
+        const uint32_t src = seq - 1 - q;
+        const uint64_t (*m)[64] = link->rows[src % kLinkSlots];
+        uint32_t w[kRowWords];
+        const bool via_msg = src >= msg_from;  // else: device work outside the chain ran since (the node columns)
+        if (!via_msg) {
+            okp = poll_done(&link->done, seq - 1);
+        } else {
+            // poll the message itself: every read brings the data with its
+            // tags, so the round trip that sees them complete is the last
+            long spin = 0;
+            for (;;) {
+                bool bad = false;
+#pragma unroll
+                for (int f = 0; f < kRowWords; ++f) {
+                    const uint64_t x = ld_sc1(&m[f][lane]);
+                    bad |= (uint32_t)(x >> 32) != src;
+                    w[f] = (uint32_t)x;
+                }
+                if (__ballot(bad) == 0) break;
+                if (++spin >= kLinkSpin) { okp = false; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
         if (q == 0 && lane == 0) TL(seq, 5);
         KT e = 0;
         uint32_t fb = 0;
         if (okp && use) {
-            const Row r = load_row_sc1(nc, node);
-            uint64_t pw[4] = {0, 0, 0, 0};
+            const Row r = via_msg ? words_row(w) : load_row_sc1(nc, node);
+            uint64_t pw[4] = {0, 0, 0, 0};  // (port words: the node columns, written before the message)
             if (c.has_ports)
                 for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, node);
             const int slot = 64 * (q + 1) + lane;
@@ -882,10 +923,13 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(gridDim.x * 4 + 1);
     if (threadIdx.x == 0) TL(seq, 11);
     if (s_ok) {
+        uint64_t (*msg)[64] = link->rows[seq % kLinkSlots];
         if (a.ent32)
-            place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+            place_parallel<uint32_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw, 0,
+                                           0x7fffffff, 0, msg);
         else
-            place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw);
+            place_parallel<uint64_t, true>(cf, nc, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, fit_raw, 0,
+                                           0x7fffffff, 0, msg);
     } else if (wave == 0 && lane == 0) {  // broken chain: keep the chain going, n_done = 0 tells the host
         st_sc1(&link->done, seq);
         __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
@@ -1252,10 +1296,10 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
 template <typename KT>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
                                   const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
-                                  uint32_t seq, int dep, hipStream_t st) {
+                                  uint32_t seq, int dep, uint32_t msg_from, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
     hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
-                       link, seq, dep)
+                       link, seq, dep, msg_from)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1269,15 +1313,15 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                                int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
                                uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set, int dep) {
+                               uint32_t seq, int fit_set, int dep, uint32_t msg_from) {
     if (seq < 1 || dep < 1 || dep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, st);
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, msg_from, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, msg_from, st);
     return hipGetLastError();
 }
 

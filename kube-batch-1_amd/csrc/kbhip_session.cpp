@@ -500,6 +500,7 @@ struct Session {
     uint32_t* d_arrive_ov[kMaxDep + 1] = {};
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
+    uint32_t msg_from = 1;      // PopLink row messages of pops from this one on are current (none drained since)
     int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
     bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
     DevBuf b_fit4;
@@ -1882,6 +1883,7 @@ struct GroupScope {
 
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
+    S.msg_from = S.ov_seq + 1;  // device work outside the chain may follow: earlier row messages go stale
     if (!S.ov_pending) return;
     for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
@@ -2053,7 +2055,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     } else if (ov) {
         HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
                                    S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.fit_set[si],
-                                   S.overlap));
+                                   S.overlap, S.msg_from));
         S.fit_set[si] ^= 1;
         S.ov_seq = seq;
         S.ov_pending = true;
