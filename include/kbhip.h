@@ -268,9 +268,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * predicted next job pops behind the running one (0..3; each used only if it
  * is exactly the next pop, retracted on device otherwise: placements are
  * unchanged), 0 = one pop at a time;
- * "overlap" = 1 (default) alternates batched pops over two streams so that a
- * pop's sweep runs beside the previous pop's placement, chained on the
- * device; 0 = one stream, one pop kernel at a time;
+ * "overlap" = k rotates batched pops over k + 1 streams so that a pop's sweep
+ * runs beside the previous k pops' placements, chained on the device (1, the
+ * default, or 2); 0 = one stream, one pop kernel at a time;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
