@@ -505,14 +505,14 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
-    __shared__ int role, s_ok, s_bad, s_list_ready, s_pdone[2];
+    __shared__ int role, s_ok, s_bad, s_list_ready, s_pdone[2], s_prow[2];
     __shared__ uint32_t s_fitb[4];
     __shared__ int32_t s_fitin[4];
     uint32_t* fitc = fit_counters(arrive, a.fit_set);
     fit_zero_other(arrive, a.fit_set);
     KT* cand = (KT*)cand64;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) { s_bad = 0; s_list_ready = 0; s_pdone[0] = s_pdone[1] = 0; }  // (before the first barrier)
+    if (threadIdx.x == 0) { s_bad = 0; s_list_ready = 0; s_pdone[0] = s_pdone[1] = 0; s_prow[0] = s_prow[1] = 0; }  // (before the first barrier)
     __shared__ RowCache rc;  // the final merger's (block 0 in the tagged path)
     if (blockIdx.x == 0)
         for (int h = threadIdx.x; h < kRcHash; h += kPopThreads) rc.hkey[h] = -1;
@@ -812,6 +812,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     constexpr int kP1 = kTagged ? 6 : 0, kP2 = kTagged ? 7 : 2;
     __shared__ KT s_e[2][64];
     __shared__ uint8_t s_fbp[2][64];
+    __shared__ uint8_t s_pst[2][64];  // tagged: 1 = the candidate's row is in the cache, 2 = its static predicates pass
     auto patch = [&](int q, int node, bool skip) {
         bool okp = true;
         bool pst = false;
@@ -849,22 +850,30 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
         if (q == 0 && lane == 0) TL(seq, 5);
         KT e = 0;
         uint32_t fb = 0;
+        const int slot = 64 * (q + 1) + lane;
+        Row r{};
+        uint64_t pw[4] = {0, 0, 0, 0};  // (port words: the node columns, written before the message)
         if (okp && use) {
-            const Row r = via_msg ? words_row(w) : load_row_sc1(nc, node);
-            uint64_t pw[4] = {0, 0, 0, 0};  // (port words: the node columns, written before the message)
+            r = via_msg ? words_row(w) : load_row_sc1(nc, node);
             if (c.has_ports)
                 for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<true>(nc, c.pw_lo + w, node);
-            const int slot = 64 * (q + 1) + lane;
             rc.row[slot] = r;
             for (int w = 0; w < 4; ++w) rc.pw[slot][w] = pw[w];
             rc.na[slot] = pna;
             rc_insert(&rc, node, slot);
+        }
+        if constexpr (kTagged) {  // the rows are in the cache: a helper wave takes the depth-1 scores
+            s_pst[q][lane] = (okp && use) ? (uint8_t)(1 | (pst ? 2 : 0)) : (uint8_t)0;
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            if (lane == 0) __hip_atomic_store(&s_prow[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (okp && use) {
             int32_t sc;
             bool passed;
             const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, pst, pna, &sc, &passed);
             e = sweep_key<KT>(k0, a);
             fb = fit_bits(c, r, passed);
-            rc.s1[slot] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, pna, k0) : INT32_MIN;
+            if constexpr (!kTagged) rc.s1[slot] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, pna, k0) : INT32_MIN;
         }
         if (q == 0) TL(seq, 13);
         s_e[q][lane] = e;
@@ -888,6 +897,30 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
             rc_insert(&rc, ln, lane);
         }
         if (lane == 0) TL(seq, 12);
+    }
+    if constexpr (kTagged) {
+        // waves 3 / 5: the depth-1 scores of pop seq-1's / seq-2's candidates
+        // (read by the placement only), off the path to the candidates'
+        // publication, on SIMDs other than the patching waves' (wave w runs on
+        // SIMD w % 4: 0 merges, 6 and 7 patch, 1 gathers rows)
+        if (wave == 3 || (wave == 5 && dep2)) {
+            const int q = wave == 3 ? 0 : 1;
+            while (__hip_atomic_load(&s_prow[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+                __builtin_amdgcn_s_sleep(1);
+            const uint32_t st = s_pst[q][lane];
+            if (st & 1u) {
+                const int slot = 64 * (q + 1) + lane;
+                const int node = q == 0 ? s_tn[lane] : s_tn2[lane];
+                const Row r = rc.row[slot];
+                uint64_t pw[4];
+                for (int w = 0; w < 4; ++w) pw[w] = rc.pw[slot][w];
+                const int32_t pna = rc.na[slot];
+                int32_t sc;
+                bool passed;
+                const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, (st & 2u) != 0, pna, &sc, &passed);
+                rc.s1[slot] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, pna, k0) : INT32_MIN;
+            }
+        }
     }
     if (wave == kP1) patch(0, s_tn[lane], false);
     if (wave == kP2 && dep2) {
