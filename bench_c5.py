@@ -170,6 +170,8 @@ def concurrent(args, bufs):
     bsum = sum(r[2]["rank_batch_sum"] for r in res)
     preq = sum(r[2]["pop_requests"] for r in res)  # allocate pops batched across sessions
     pbsum = sum(r[2]["pop_batch_sum"] for r in res)
+    sreq = sum(r[2]["sweep_requests"] for r in res)  # per-task chunks (general path, backfill) batched
+    sbsum = sum(r[2]["sweep_batch_sum"] for r in res)
     seq_lat, _, _ = one_session(timed[0], False)  # one session alone, for the latency beside the throughput
     out = {
         "metric": "C5 what-if sessions/s (reclaim, allocate, backfill, preempt)",
@@ -192,6 +194,8 @@ def concurrent(args, bufs):
         "group": args.group,
         "pop_launch_requests": preq,
         "sessions_per_pop_launch": pbsum / max(preq, 1),
+        "sweep_chunk_requests": sreq,
+        "sessions_per_sweep_launch": sbsum / max(sreq, 1),
     }
     if args.cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -105,6 +105,8 @@ typedef struct kbhip_stats {
     int64_t async_launched;  /* kbhip_place_job_submit: pops launched ahead of their wait */
     int64_t async_retracted; /* ... launches withdrawn (cancelled, or behind a pop that ran synchronously) */
     int64_t async_cancelled; /* tickets withdrawn by kbhip_place_job_cancel */
+    int64_t sweep_requests;  /* per-task chunks (allocate's general path, backfill) served by the what-if batcher */
+    int64_t sweep_batch_sum; /* sum over those of the sessions per launch that served them */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -254,11 +256,14 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * passes (four 8-bit counting passes over the score) instead of the one-pass
  * counting sort (tests);
  * "rank_group" = 1 makes this session one of a lockstep group of what-if
- * sessions run from concurrent host threads: while inside allocate / reclaim
- * / preempt, their allocate pops of placements 6 / 7 and their reclaim /
- * preempt node rankings are issued in steps, once every member has a request
- * in, as shared multi-session launches (blockIdx.y = session; kbhip_stats
- * rank_batch_sum / rank_requests and pop_batch_sum / pop_requests = requests
+ * sessions run from concurrent host threads: while inside allocate /
+ * backfill / reclaim / preempt, their allocate pops of placements 6 / 7, their
+ * per-task chunks and their reclaim / preempt node rankings are issued in
+ * steps, once every member has a request in, as shared multi-session launches
+ * (blockIdx.y = session; kbhip_stats
+ * rank_batch_sum / rank_requests, pop_batch_sum / pop_requests and
+ * sweep_batch_sum / sweep_requests (per-task chunks: allocate's general path
+ * and backfill first-fits, k_sweep_argmax_multi) = requests
  * per launch);
  * "rank_first" = k: reclaim / preempt read the first k sorted keys with the count;
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep

@@ -173,6 +173,19 @@ struct PopReq {
 // Launches every request (grouped by nodes per lane, key type and placement,
 // kPopMulti per launch; *launches = launches made).
 hipError_t launch_pop_batch_multi(const PopReq* reqs, int n, hipStream_t st, int* launches);
+// A what-if session's per-task chunk (k_sweep_argmax_multi): m tasks of the
+// control block `ctrl`, committed on the device (defer: the visited nodes'
+// GetAccessibleResource mutation by k_visit_mutate_multi).
+struct SweepReq {
+    Conf cf;
+    NodeCols nc;
+    DevTables t;
+    PopCtrl* ctrl;
+    uint64_t* walk;
+    int m;
+    int defer;
+};
+hipError_t launch_sweep_multi(const SweepReq* reqs, int n, int k, hipStream_t st, int* launches);
 size_t pop_out_bytes();
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);

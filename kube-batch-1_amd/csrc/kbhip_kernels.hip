@@ -193,8 +193,11 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
 // Sweep of task task_i over this shard's nodes -> max key in ctrl->slot.
 // commit_here: the last block commits (one GPU); otherwise the slot is
 // reduced across shards first and k_commit_task commits.
-__global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
-                                                         int task_i, uint64_t* walk, int commit_here, uint64_t* dbg) {
+// (bx, nbx: this block's index among the session's nbx blocks — blockIdx.x /
+// gridDim.x, or one session's blocks of a multi-session grid)
+__device__ __forceinline__ void sweep_body(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
+                                           int task_i, uint64_t* walk, int commit_here, uint64_t* dbg, int bx,
+                                           int nbx) {
     __shared__ uint64_t red[kBlock / 64];
     __shared__ int last;
     __shared__ int32_t s_fit[4];
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     const int F = ctrl->fallback;
     uint64_t best = 0;
     int32_t fc[4] = {0, 0, 0, 0};  // this task's FitDelta histogram, should it find no node
-    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+    for (int n = bx * kBlock + threadIdx.x; n < nc.n; n += nbx * kBlock) {
         int32_t s = 0;
         bool passed = false;
         uint32_t fb = 0;
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
             if (s_fit[q]) atomicAdd(&ctrl->fit[task_i][q], s_fit[q]);
         __threadfence();
         const unsigned prev = atomicAdd(&ctrl->arrive[task_i], 1u);
-        last = prev == gridDim.x - 1;
+        last = prev == (unsigned)nbx - 1;
         __threadfence();
     }
     __syncthreads();
@@ -250,24 +253,59 @@ __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, D
     if (!(commit_here & 1)) return;
     commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk, (commit_here & 2) != 0);
 }
+__global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
+                                                         int task_i, uint64_t* walk, int commit_here, uint64_t* dbg) {
+    sweep_body(cf, nc, t, ctrl, task_i, walk, commit_here, dbg, blockIdx.x, gridDim.x);
+}
 
 // The GetAccessibleResource mutation of task task_i's walk (node_info.go:209-211,
 // SURVEY Appendix A.1) over the whole grid, after k_sweep_argmax committed it
 // with the mutation deferred (one block looping over every node is a chain of
 // N / kBlock dependent memory round trips).  Runs only if task_i was swept
 // (n_done == task_i + 1) and its sweep tracked the walk (pad, set by commit_task).
-__global__ __launch_bounds__(kBlock) void k_visit_mutate(NodeCols nc, const PopCtrl* ctrl, int task_i,
-                                                         const uint64_t* walk) {
+__device__ __forceinline__ void visit_body(const NodeCols& nc, const PopCtrl* ctrl, int task_i, const uint64_t* walk,
+                                           int bx, int nbx) {
     if (ctrl->n_done != task_i + 1 || !ctrl->pad) return;  // uniform
     const uint64_t k = ctrl->slot[task_i];
     const uint64_t wk = k ? pack_key(key_score(k), key_idx(k), 0) : 0;
     const int wn = k ? key_idx(k) : -1;
-    for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
+    for (int n = bx * kBlock + threadIdx.x; n < nc.n; n += nbx * kBlock) {
         const uint64_t v = walk[n];
         if (!v || n + nc.base == wn) continue;
         if (k && v < wk) continue;
         nc.idle_cpu[n] += nc.bf_cpu[n]; nc.idle_mem[n] += nc.bf_mem[n]; nc.idle_gpu[n] += nc.bf_gpu[n];
     }
+}
+__global__ __launch_bounds__(kBlock) void k_visit_mutate(NodeCols nc, const PopCtrl* ctrl, int task_i,
+                                                         const uint64_t* walk) {
+    visit_body(nc, ctrl, task_i, walk, blockIdx.x, gridDim.x);
+}
+
+// What-if sessions stepping together (StepBatcher, option rank_group): task
+// k of the per-task chunks of up to kPopMulti sessions in one launch,
+// blockIdx.y = session, each session's blocks sweeping its own node columns
+// and committing into its own control block exactly as k_sweep_argmax does.
+struct SweepDesc {
+    Conf cf;
+    NodeCols nc;
+    DevTables t;
+    PopCtrl* ctrl;
+    uint64_t* walk;
+    int task_i, mode, nb;
+};
+struct SweepDescs {
+    SweepDesc d[kPopMulti];
+};
+static_assert(sizeof(SweepDescs) <= 4000, "multi-session sweep descriptors exceed the kernel argument space");
+__global__ __launch_bounds__(kBlock) void k_sweep_argmax_multi(SweepDescs d) {
+    const SweepDesc& q = d.d[blockIdx.y];
+    if ((int)blockIdx.x >= q.nb) return;
+    sweep_body(q.cf, q.nc, q.t, q.ctrl, q.task_i, q.walk, q.mode, nullptr, blockIdx.x, q.nb);
+}
+__global__ __launch_bounds__(kBlock) void k_visit_mutate_multi(SweepDescs d) {
+    const SweepDesc& q = d.d[blockIdx.y];
+    if ((int)blockIdx.x >= q.nb || (q.mode & 2) == 0) return;
+    visit_body(q.nc, q.ctrl, q.task_i, q.walk, blockIdx.x, q.nb);
 }
 
 // Sharded sessions: the commit after the cross-shard max of ctrl->slot[task_i].
@@ -984,6 +1022,36 @@ hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTabl
     if (commit_here && defer_visits)
         hipLaunchKernelGGL(k_visit_mutate, dim3(grid), dim3(kBlock), 0, st, nc, (const PopCtrl*)ctrl, task_i,
                            (const uint64_t*)walk);
+    return hipGetLastError();
+}
+
+// Task k of every request whose chunk has more than k tasks, kPopMulti
+// sessions per launch (requests in order: each session's tasks run in order
+// on the one stream).
+hipError_t launch_sweep_multi(const SweepReq* reqs, int n, int k, hipStream_t st, int* launches) {
+    SweepDescs d{};
+    int cnt = 0, max_nb = 1, any_defer = 0;
+    auto flush = [&]() {
+        if (!cnt) return;
+        hipLaunchKernelGGL(k_sweep_argmax_multi, dim3(max_nb, cnt), dim3(kBlock), 0, st, d);
+        if (any_defer) hipLaunchKernelGGL(k_visit_mutate_multi, dim3(max_nb, cnt), dim3(kBlock), 0, st, d);
+        ++*launches;
+        d = SweepDescs{};
+        cnt = 0;
+        max_nb = 1;
+        any_defer = 0;
+    };
+    for (int i = 0; i < n; ++i) {
+        const SweepReq& r = reqs[i];
+        if (k >= r.m) continue;
+        int nb = (r.nc.n + kBlock - 1) / kBlock;
+        nb = nb > 2048 ? 2048 : nb < 1 ? 1 : nb;
+        d.d[cnt] = SweepDesc{r.cf, r.nc, r.t, r.ctrl, r.walk, k, r.defer ? 3 : 1, nb};
+        max_nb = nb > max_nb ? nb : max_nb;
+        any_defer |= r.defer;
+        if (++cnt == kPopMulti) flush();
+    }
+    flush();
     return hipGetLastError();
 }
 

@@ -1729,11 +1729,15 @@ struct StepBatcher {
         static StepBatcher b;
         return b;
     }
-    enum Kind { kPop = 0, kRank = 1 };
+    // kSweep requests (per-task chunks) step in the pop lane: the same members
+    // (sessions inside allocate or backfill) send either
+    enum Kind { kPop = 0, kRank = 1, kSweep = 2 };
+    static int lane_of(int kind) { return kind == kRank ? 1 : 0; }
     struct Req {
         int kind = kPop;
         int device = 0;
         PopReq pop{};
+        SweepReq sweep{};
         hipEvent_t before = nullptr;  // pop: recorded on the requester's stream (its earlier work)
         hipEvent_t after = nullptr;   // pop: recorded after the launch that served it
         RankDesc rank{};
@@ -1765,12 +1769,13 @@ struct StepBatcher {
 
     void join(int kind) {
         std::lock_guard<std::mutex> lk(mu);
-        ++lane[kind].members;
+        ++lane[lane_of(kind)].members;
     }
     void leave(int kind) {
         std::unique_lock<std::mutex> lk(mu);
-        --lane[kind].members;
-        if (ready(kind)) issue(lk, kind);
+        const int l = lane_of(kind);
+        --lane[l].members;
+        if (ready(l)) issue(lk, l);
     }
     // The member whose request (or departure) completes the step issues it;
     // the others spin on their own request (a step is microseconds of host
@@ -1778,8 +1783,9 @@ struct StepBatcher {
     void submit(Req& r) {
         {
             std::unique_lock<std::mutex> lk(mu);
-            lane[r.kind].pending.push_back(&r);
-            if (ready(r.kind)) issue(lk, r.kind);
+            const int l = lane_of(r.kind);
+            lane[l].pending.push_back(&r);
+            if (ready(l)) issue(lk, l);
         }
         for (long spin = 0; !r.done.load(std::memory_order_acquire); ++spin) {
             if ((spin & 1023) == 1023) std::this_thread::yield();
@@ -1788,14 +1794,14 @@ struct StepBatcher {
     }
 
   private:
-    bool ready(int kind) const {
-        const Lane& L = lane[kind];
+    bool ready(int l) const {
+        const Lane& L = lane[l];
         return !L.busy && !L.pending.empty() && (int)L.pending.size() >= L.members;
     }
-    // One step of one lane: every pending request of that kind (the lock is
+    // One step of one lane: every pending request of that lane (the lock is
     // released while launching).
-    void issue(std::unique_lock<std::mutex>& lk, int kind) {
-        Lane& L = lane[kind];
+    void issue(std::unique_lock<std::mutex>& lk, int l) {
+        Lane& L = lane[l];
         L.busy = true;
         vector<Req*> batch;
         batch.swap(L.pending);
@@ -1804,18 +1810,25 @@ struct StepBatcher {
         std::map<int, vector<Req*>> by;  // device -> requests
         for (Req* q : batch) by[q->device].push_back(q);
         for (auto& kv : by) {
-            int launches = 1;
-            const hipError_t e = kind == kPop ? launch_pops(kv.first, kv.second, &launches)
-                                              : launch_ranks(kv.first, kv.second);
-            for (Req* q : kv.second) {
-                q->err = e;
-                q->batch = (int)((kv.second.size() + launches - 1) / launches);  // requests per launch
+            if (l == 1) {
+                const hipError_t e = launch_ranks(kv.first, kv.second);
+                for (Req* q : kv.second) { q->err = e; q->batch = (int)kv.second.size(); }
+                continue;
             }
+            vector<Req*> pops, sweeps;
+            for (Req* q : kv.second) (q->kind == kSweep ? sweeps : pops).push_back(q);
+            int pl = 0, sl = 0, sw_tasks = 0;
+            hipError_t e = pops.empty() ? hipSuccess : launch_pops(kv.first, pops, &pl);
+            if (e == hipSuccess && !sweeps.empty()) e = launch_sweeps(kv.first, sweeps, &sl, &sw_tasks);
+            if (e == hipSuccess) e = record_after(kv.first, kv.second);
+            for (Req* q : pops) q->batch = (int)((pops.size() + std::max(pl, 1) - 1) / std::max(pl, 1));
+            for (Req* q : sweeps) q->batch = (int)((sw_tasks + std::max(sl, 1) - 1) / std::max(sl, 1));
+            for (Req* q : kv.second) q->err = e;
         }
         lk.lock();
         L.busy = false;
         for (Req* q : batch) q->done.store(true, std::memory_order_release);  // q may go away after this
-        if (ready(kind)) issue(lk, kind);  // requests that came in while this step was being launched
+        if (ready(l)) issue(lk, l);  // requests that came in while this step was being launched
     }
     Dev& device(int d, hipError_t* e) {
         Dev& D = dev[d];
@@ -1841,6 +1854,33 @@ struct StepBatcher {
         int nl = 0;
         if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), D.st, &nl)) != hipSuccess) return e;
         *launches = std::max(nl, 1);
+        return hipSuccess;
+    }
+    // Task k of every chunk for k = 0, 1, ...: each session's tasks in order on
+    // the one stream, the sessions side by side (*tasks: session-tasks swept).
+    hipError_t launch_sweeps(int d, const vector<Req*>& b, int* launches, int* tasks) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        vector<SweepReq> qs;
+        int max_m = 0;
+        for (Req* q : b) {
+            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
+            qs.push_back(q->sweep);
+            max_m = std::max(max_m, q->sweep.m);
+            *tasks += q->sweep.m;
+        }
+        for (int k = 0; k < max_m; ++k)
+            if ((e = launch_sweep_multi(qs.data(), (int)qs.size(), k, D.st, launches)) != hipSuccess) return e;
+        return hipSuccess;
+    }
+    // Every request of the step follows its launches on the requester's stream.
+    hipError_t record_after(int d, const vector<Req*>& b) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
         hipEvent_t ev = D.ring[D.next++ % D.ring.size()];
         if ((e = hipEventRecord(ev, D.st)) != hipSuccess) return e;
         for (Req* q : b) q->after = ev;
@@ -1880,6 +1920,34 @@ struct GroupScope {
         if (on) StepBatcher::get().leave(kind);
     }
 };
+
+// The sweeps of a per-task chunk (tasks 0 .. m-1 of the control block): one
+// k_sweep_argmax launch per task, or, for a what-if session of the lockstep
+// group, one request that the StepBatcher serves together with the group's
+// other chunks (k_sweep_argmax_multi: task k of every chunk in one launch).
+// Classes with inter-pod priority terms (their k_ipa_minmax prepass) and
+// debug-key sessions keep the per-task launches.
+static void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task = false) {
+    bool group = S.rank_group && S.world == 1 && !S.d_dbg && !per_task;
+    for (int i = 0; i < m && group; ++i) group = S.classes[cls[i]].ipa_n == 0;
+    if (!group) {
+        for (int i = 0; i < m; ++i) sweep_task(S, i, cls[i], defer);
+        return;
+    }
+    StepBatcher::Req r;
+    r.kind = StepBatcher::kSweep;
+    r.sweep = SweepReq{S.conf, S.nc, S.tab, S.d_ctrl, S.d_walk, m, defer ? 1 : 0};
+    r.device = S.device;
+    if (!S.ev_pop) HIPCHK(hipEventCreateWithFlags(&S.ev_pop, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(S.ev_pop, S.stream));  // the control block's setup is in
+    r.before = S.ev_pop;
+    StepBatcher::get().submit(r);
+    HIPCHK(hipSetDevice(S.device));
+    HIPCHK(r.err);
+    HIPCHK(hipStreamWaitEvent(S.stream, r.after, 0));  // this session's later work follows the launches
+    S.stats.sweep_requests++;
+    S.stats.sweep_batch_sum += r.batch;
+}
 
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
@@ -2302,10 +2370,14 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             ctrl_setup(S, m, cls, ready_count, min_avail, gang_mode, 0, slot, epoch);
             bool defer = S.any_bf != 0;  // a backfill-annotated task may set any_bf on the device mid-chunk
             for (int i = 0; i < m; ++i) defer = defer || S.classes[cls[i]].backfill;
-            for (int i = 0; i < m; ++i) {
-                if (timed && i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
-                sweep_task(S, i, cls[i], defer);
-                if (timed && i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
+            if (timed) {
+                for (int i = 0; i < m; ++i) {
+                    if (i == 0) HIPCHK(hipEventRecord(S.ev0, S.stream));
+                    sweep_task(S, i, cls[i], defer);
+                    if (i == 0) HIPCHK(hipEventRecord(S.ev1, S.stream));
+                }
+            } else {
+                sweep_chunk(S, m, cls, defer);
             }
             S.stats.sweeps += m;
             int32_t fit4[4] = {0, 0, 0, 0};
@@ -3571,7 +3643,7 @@ static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) 
         uint32_t epoch = 0;
         const int slot = take_slot(S, &epoch);
         ctrl_setup(S, m, cls, 0, 0, 0, 1, slot, epoch);
-        for (int i = 0; i < m; ++i) sweep_task(S, i, cls[i]);
+        sweep_chunk(S, m, cls, false);
         int n_done = 0, stop = -1;
         collect_tasks(S, slot, epoch, m, &n_done, &stop, S.res_node_buf, S.res_kind_buf, nullptr);
         S.stats.sweeps += m;
@@ -3602,6 +3674,7 @@ static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) 
 }
 
 static void backfill_run(Session& S) {
+    GroupScope group(S.rank_group && S.world == 1, StepBatcher::kPop);  // what-if sessions: first-fits step with the group
     vector<int32_t> cand;
     for (auto& j : S.jobs)
         for (int t : j.tasks) {

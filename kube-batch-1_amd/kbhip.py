@@ -53,7 +53,8 @@ class Stats(ctypes.Structure):
                 ("rank_batch_sum", ctypes.c_int64), ("pop_requests", ctypes.c_int64),
                 ("pop_batch_sum", ctypes.c_int64), ("comm_reused", ctypes.c_int64),
                 ("async_launched", ctypes.c_int64), ("async_retracted", ctypes.c_int64),
-                ("async_cancelled", ctypes.c_int64)]
+                ("async_cancelled", ctypes.c_int64), ("sweep_requests", ctypes.c_int64),
+                ("sweep_batch_sum", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

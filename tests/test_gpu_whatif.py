@@ -52,3 +52,8 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
     if n_sessions > 2:
         assert pbsum > preq
     assert pbsum / preq > 1.5  # lockstep: most pop launches serve several sessions
+    sreq = sum(st["sweep_requests"] for _, st in res)  # per-task chunks (backfill first-fits, general path)
+    sbsum = sum(st["sweep_batch_sum"] for _, st in res)
+    assert sreq >= n_sessions and sbsum >= sreq  # every session's backfill chunk went through the group
+    if n_sessions > 2:
+        assert sbsum > sreq  # some sweep launch served several sessions' chunks
