@@ -213,8 +213,9 @@ int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* o
  * parse, no re-encode).  The session can then run its actions again.
  * *out_uploaded_bytes (optional) = bytes sent to the device.  Pod
  * (anti-)affinity count tables are recounted from the carried pod states.
- * KBHIP_EUNSUPPORTED on shards; pod arrivals and node changes need
- * kbhip_session_open. */
+ * On a node-sharded session every rank carries (identically on its
+ * replicated host model; each uploads its own rows; no collective).  Pod
+ * arrivals and node changes need kbhip_session_open. */
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
 
 /* kbhip_session_carry plus the scheduler cache's events on existing pods

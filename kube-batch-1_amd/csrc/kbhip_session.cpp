@@ -3982,8 +3982,9 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // Succeeded / Failed (isTerminated: the task stays in its job, off its node).
 // New pods and node changes need a snapshot (kbhip_session_open).
 static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0) {
-    if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "carry on a node-sharded session");
-    const int N = S.nc.n, P = (int)S.pods.size();
+    // every node's row is recomputed on the host (a shard's host model holds
+    // all of them); this device's rows [lo, lo + Nl) are compared and uploaded
+    const int N = (int)S.h_alloc.size(), Nl = S.nc.n, lo = S.nc.base, P = (int)S.pods.size();
     {  // validate the events before anything changes
         vector<char> gone(P, 0);
         for (int64_t k = 0; k < n_ev; ++k) {
@@ -4026,7 +4027,7 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     for (auto& c : col) c.assign(N, 0);
     vector<int32_t> podcnt(N, 0);
     vector<int64_t> nzc(N, 0), nzm(N, 0);
-    vector<uint64_t> pcol((size_t)std::max(S.nc.port_words, 1) * S.nc.npad, 0);
+    vector<uint64_t> pcol((size_t)std::max(S.nc.port_words, 1) * S.nc.npad, 0);  // this device's rows
     for (int n = 0; n < N; ++n) { col[0][n] = S.h_alloc[n].c; col[1][n] = S.h_alloc[n].m; col[2][n] = S.h_alloc[n].g; }
     S.used.assign(N, R3{});
     S.any_bf = 0;
@@ -4041,9 +4042,10 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
         podcnt[n]++;
         nzc[n] += p.nzc;
         nzm[n] += p.nzm;
+        if (n < lo || n >= lo + Nl) continue;
         for (int k = S.pod_port_off[i]; k < S.pod_port_off[i + 1]; ++k) {
             const int id = S.pod_port_ids[k];
-            pcol[(size_t)(id / 64) * S.nc.npad + n] |= 1ULL << (id % 64);
+            pcol[(size_t)(id / 64) * S.nc.npad + (n - lo)] |= 1ULL << (id % 64);
         }
     }
     for (int n = 0; n < N; ++n) if (col[6][n] || col[7][n] || col[8][n]) S.any_bf = 1;
@@ -4051,25 +4053,25 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     int64_t* dcol[9] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem, S.nc.rel_gpu,
                         S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu};
     int64_t uploaded = 0;
-    auto sync_col = [&](void* dptr, const void* want, size_t elem) {
-        vector<uint8_t> have((size_t)N * elem);
+    auto sync_col = [&](void* dptr, const void* want, size_t elem) {  // want: this device's rows
+        vector<uint8_t> have((size_t)Nl * elem);
         HIPCHK(hipMemcpy(have.data(), dptr, have.size(), hipMemcpyDeviceToHost));
         const uint8_t* w = (const uint8_t*)want;
         int n = 0;
-        while (n < N) {
+        while (n < Nl) {
             if (std::memcmp(have.data() + (size_t)n * elem, w + (size_t)n * elem, elem) == 0) { ++n; continue; }
             int e = n + 1;
-            while (e < N && std::memcmp(have.data() + (size_t)e * elem, w + (size_t)e * elem, elem) != 0) ++e;
+            while (e < Nl && std::memcmp(have.data() + (size_t)e * elem, w + (size_t)e * elem, elem) != 0) ++e;
             HIPCHK(hipMemcpyAsync((uint8_t*)dptr + (size_t)n * elem, w + (size_t)n * elem, (size_t)(e - n) * elem,
                                   hipMemcpyHostToDevice, S.stream));
             uploaded += (int64_t)(e - n) * (int64_t)elem;
             n = e;
         }
     };
-    for (int k = 0; k < 9; ++k) sync_col(dcol[k], col[k].data(), sizeof(int64_t));
-    sync_col(S.nc.pods, podcnt.data(), sizeof(int32_t));
-    sync_col(S.nc.nzc, nzc.data(), sizeof(int64_t));
-    sync_col(S.nc.nzm, nzm.data(), sizeof(int64_t));
+    for (int k = 0; k < 9; ++k) sync_col(dcol[k], col[k].data() + lo, sizeof(int64_t));
+    sync_col(S.nc.pods, podcnt.data() + lo, sizeof(int32_t));
+    sync_col(S.nc.nzc, nzc.data() + lo, sizeof(int64_t));
+    sync_col(S.nc.nzm, nzm.data() + lo, sizeof(int64_t));
     for (int w = 0; w < S.nc.port_words; ++w)
         sync_col(S.nc.ports + (size_t)w * S.nc.npad, pcol.data() + (size_t)w * S.nc.npad, sizeof(uint64_t));
     HIPCHK(hipStreamSynchronize(S.stream));  // the host sources above are about to go away

@@ -126,6 +126,33 @@ def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, see
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(6))
+def test_sharded_carry_gpu(engine, kbgen_mod, tmp_path, seed):
+    """Session carry-over on shards: every rank carries its replicated host
+    model and uploads its own rows; the second session's log equals the
+    one-GPU session's after the same carry (tests/test_gpu_carry.py pins that
+    one against the faithful oracle)."""
+    from test_gpu_carry import NO_POD_AFFINITY
+    c = kbgen_mod.gen_random(2900 + seed, n_nodes=6 + seed * 3, n_jobs=7, max_tasks=5, features=NO_POD_AFFINITY)
+    p = str(tmp_path / "s.kbs")
+    c.write(p)
+    acts = "allocate, backfill"
+    with engine.Session(p) as s:
+        s.run_actions(acts)
+        st = s.table("pod_status")
+        dels = [int(i) for i in np.nonzero((st == 16) | (st == 64))[0][:4]]  # bound / running pods leave
+        s.carry_events(dels, [1] * len(dels))  # KBHIP_EV_DELETE
+        pod, node, kind = s.run_actions(acts)
+    exp = [[int(a), int(b), int(k)] for a, b, k in zip(pod, node, kind)]
+    world = 2 + seed % 2
+    res = _run_ranks("shard_worker.py", world, tmp_path,
+                     lambda r, init, out: [p, str(r), str(world), init, out, acts, "1"], timeout=240,
+                     env={"KBHIP_TEST_CARRY": ",".join(map(str, dels))})
+    for r in range(world):
+        assert res[r]["log"] == exp, f"rank {r}"
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("exchange", ["host", "mailbox"])
 def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path, exchange):
     """C4 shape at 20k nodes (2 and 3 ranks sharing the GPU): the shard logs
