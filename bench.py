@@ -20,13 +20,18 @@ independent sessions.
 
 Also reported:
 * roofline of the fused pop kernel (k_pop_batch_ov: sweep + top-64 + placement):
-  algorithmic bytes = nodes x 113 B per launch / its mean
-  duration, measured with HIP events around every launch on the stream it
-  runs on during the timed steps (the same quantity as rocprofv3's kernel
-  duration; consecutive pops overlap, so it includes the wait for the previous
-  pop's write-back);
+  algorithmic bytes = nodes x 113 B per launch / the
+  kernel's device busy period per launch (allocate's device span, HIP events
+  on the engine streams, / launches: consecutive launches overlap, so their
+  own spans — also reported, `span_us` — add up to more than the step);
+  beside it the standalone predicate + score sweep (`sweep`: the product
+  kernel k_rank_nodes behind kbhip_sweep_scores, one launch per task over all
+  nodes, each launch timed with HIP events on its stream);
 * cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
-  cores, on a bounded sample (the first job pops of the same session).
+  cores, timed on a stratified sample of the same session: pop windows early,
+  mid and late in the session, the pops between them fast-forwarded from the
+  engine's placement log (the swept decisions are checked against it); the
+  whole-session CPU allocate time is extrapolated per stratum.
 """
 import argparse
 import json
@@ -203,7 +208,7 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2):
+def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2, keep_log=False):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
@@ -216,24 +221,66 @@ def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2):
     s.close()
     t3 = time.perf_counter()
     st["phases_ms"] = {"open": (t1 - t0) * 1e3, "allocate": (t2 - t1) * 1e3, "close": (t3 - t2) * 1e3}
+    if keep_log:
+        st["log"] = (pod, node, kind)
     return t3 - t0, len(pod), st
 
 
-def cpu_baseline(path, target_s):
+def sweep_roofline(buf, device, pods, n_tasks=256):
+    """The standalone predicate + score sweep at full size: kbhip_sweep_scores
+    (the product kernel k_rank_nodes: every node's PredicateFn + NodeOrderFn key,
+    preempt.go:270-287) for n_tasks pending tasks of the session, each launch
+    timed with HIP events on the engine stream (outside the timed steps)."""
+    with kbhip.Session(buf, device=device) as s:
+        s.set_option("time_every", 1)
+        step = max(1, len(pods) // n_tasks)
+        for p in pods[::step][:n_tasks]:
+            s.sweep_scores(int(p), 0, keys=False)
+        st = s.stats()
+    n = st["score_sweeps"]
+    mean_us = st["score_sweep_s"] / max(n, 1) * 1e6
+    nodes = st["nodes"]
+    achieved = nodes * B_NODE / (mean_us * 1e-6) / 1e9 if mean_us > 0 else 0.0
+    return {"kernel": "k_rank_nodes (kbhip_sweep_scores)", "launches": n, "mean_us": mean_us,
+            "bytes_per_launch": nodes * B_NODE, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
+            "note": "reads 113 B/node (SURVEY §8(d)) and writes an 8-byte key per node (not counted)"}
+
+
+def cpu_baseline(path, target_s, log, session_pops):
+    """The hoisted restatement on a stratified sample of the same session:
+    three pop windows (around 1/6, 1/2 and 5/6 of the session's pops) swept
+    and timed; the rest fast-forwarded from the engine's log."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the checker / CPU baseline only (test infrastructure)
     threads = min(16, os.cpu_count() or 1)
-    probe_pops = 50
-    st = {}
-    pl = oracle.fast_allocate(path, threads=threads, max_pops=probe_pops, stats=st)
-    per_pop = st["allocate_s"] / max(st["pops"], 1)
-    pops = int(max(probe_pops, min(20000, target_s / max(per_pop, 1e-6))))
-    st = {}
-    pl = oracle.fast_allocate(path, threads=threads, max_pops=pops, stats=st)
-    return {"value": len(pl) / st["allocate_s"], "unit": "placements/s", "cores": threads, "kind": "port",
-            "sample": f"first {st['pops']} job pops ({len(pl)} placements) of the same C4 session, "
-                      f"allocate action only, hoisted C++ restatement oracle/kbfast.cpp, "
-                      f"{threads} threads on {os.cpu_count()} host cpus"}
+    pod, node, kind = log
+    status = np.where(kind == kbhip.ALLOCATED, 4, 8).astype(np.int32)  # api.Allocated / api.Pipelined
+    P = session_pops
+    centers = (P // 6, P // 2, 5 * P // 6)
+    probe = oracle.fast_allocate_sampled(path, pod, node, status, [(c, c + 20) for c in centers], threads=threads)
+    per_pop = probe["timed_s"] / max(probe["timed_pops"], 1)
+    P = probe["session_pops"]  # the restatement's own count of the session's job pops
+    centers = (P // 6, P // 2, 5 * P // 6)
+    W = int(max(20, min(P // 6, target_s / 3 / max(per_pop, 1e-6))))
+    strata, placed, secs, mism = [], 0, 0.0, probe["mismatches"]
+    est_alloc_s = 0.0
+    for c in centers:
+        lo = max(0, c - W // 2)
+        r = oracle.fast_allocate_sampled(path, pod, node, status, [(lo, lo + W)], threads=threads)
+        strata.append({"pops": [lo, lo + r["timed_pops"]], "placed": r["placed"], "s": round(r["timed_s"], 3)})
+        placed += r["placed"]
+        secs += r["timed_s"]
+        mism += r["mismatches"]
+        est_alloc_s += r["timed_s"] / max(r["timed_pops"], 1) * (P / 3)  # this stratum's third of the pops
+    return {"value": placed / secs, "unit": "placements/s", "cores": threads, "kind": "port",
+            "p50_allocate_ms_est": est_alloc_s * 1e3,
+            "session_placements_per_s_est": len(pod) / est_alloc_s,
+            "strata": strata, "log_mismatches": mism,
+            "sample": f"3 windows of {W} job pops (around 1/6, 1/2, 5/6 of the session's {P} pops) of the same "
+                      f"C4 session, swept and timed; the pops between fast-forwarded from the engine's placement "
+                      f"log (the swept decisions are checked against it: {mism} differ); allocate action only, "
+                      f"hoisted C++ restatement oracle/kbfast.cpp, {threads} threads on {os.cpu_count()} host cpus; "
+                      f"p50_allocate_ms_est = the whole session's allocate extrapolated per stratum"}
 
 
 def main():
@@ -253,15 +300,17 @@ def main():
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
     dev_s, dev_pops = 0.0, 0
-    for _ in range(args.steps):
+    for i in range(args.steps):
         dt, n, st = run_session(buf, device, args.time_every, shard, args.overlap,
-                                args.speculate)
+                                args.speculate, keep_log=(i == 0 and rank == 0))
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
         sweeps_n += st["timed_launches"]
         dev_s += st["alloc_device_s"]
         dev_pops += st["batched_pops"]
+        if "log" in st:
+            log0 = st.pop("log")
         st_last = st
     barrier(dist, local)
     wall = time.perf_counter() - t0
@@ -274,14 +323,17 @@ def main():
         return
     nodes = st_last["nodes"]
     traffic = None if shard else pmc_traffic()
+    sweep = None if shard else sweep_roofline(buf, device, log0[0])
     nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
     # the hot kernel's mean duration: HIP events around every batched pop launch on the stream it runs on
     # (overlapped pops: the duration includes the wait for the previous pop's write-back, as rocprof's does)
     launch_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3 if sweeps_n else 0.0
     kernel = "k_pop_batch (shard sweep, placement 3)" if shard else (
         "k_pop_batch_ov" if args.overlap else "k_pop_batch")
-    achieved = nodes_per_launch * B_NODE / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
     period_us = dev_s / dev_pops * 1e6 if dev_pops else 0.0
+    # the kernel's busy period per launch: allocate's device span (HIP events on the engine streams) / launches
+    achieved = nodes_per_launch * B_NODE / (period_us * 1e-6) / 1e9 if period_us > 0 else 0.0
+    span_achieved = nodes_per_launch * B_NODE / (launch_us * 1e-6) / 1e9 if launch_us > 0 else 0.0
     out = {
         "metric": METRIC,
         "value": total_placed / wall,
@@ -316,13 +368,20 @@ def main():
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
                      if traffic else None,
-                     "mean_launch_us": launch_us, "timed_launches": sweeps_n,
-                     "timing": f"HIP events around every {args.time_every}-th batched pop launch on its stream, "
-                               f"read back after the session ({sweeps_n} launches)",
-                     "bytes_per_launch": nodes_per_launch * B_NODE},
+                     "busy_period_us": period_us,
+                     "timing": "busy period = allocate's device span (HIP events on the engine streams around the "
+                               "allocate action, summed over the timed sessions) / batched pop launches: the launches "
+                               "overlap, so this is the device time each one adds; the sum over launches = the span",
+                     "span_us": launch_us, "span_frac": span_achieved / HBM_PEAK_GBS,
+                     "span_timing": f"each launch's own start-to-end span (HIP events around every "
+                                    f"{args.time_every}-th launch on its stream, {sweeps_n} launches): it includes the "
+                                    f"wait for the previous pop, so consecutive spans overlap",
+                     "bytes_per_launch": nodes_per_launch * B_NODE,
+                     "sweep": sweep},
     }
     if args.cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds, log0, st_last["pops"])
+        out["cpu_baseline"]["gpu_p50_session_ms"] = out["p50_session_ms"]
     print(json.dumps(out))
     if dist is not None:
         dist.destroy_process_group()

@@ -107,6 +107,9 @@ typedef struct kbhip_stats {
     int64_t async_cancelled; /* tickets withdrawn by kbhip_place_job_cancel */
     int64_t sweep_requests;  /* per-task chunks (allocate's general path, backfill) served by the what-if batcher */
     int64_t sweep_batch_sum; /* sum over those of the sessions per launch that served them */
+    double score_sweep_s;    /* kbhip_sweep_scores with "time_every" > 0: summed HIP-event duration of its
+                                standalone predicate + score sweep kernel (k_rank_nodes) */
+    int64_t score_sweeps;    /* ... launches timed */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -140,8 +143,8 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
  * kbhip_place_job_submit queues one job pop with kbhip_place_job's arguments
  * and returns a ticket (>= 0).  A pop runs on the session state that every
  * earlier submitted pop leaves, exactly as a sequence of kbhip_place_job calls
- * would: a pop that is one batched chunk (at most 16 tasks of one task class)
- * is launched at once, up to 4 ahead of the oldest wait; any other pop, and
+ * would: a pop that is one batched chunk (at most 64 tasks, kMaxChunk, of one
+ * task class) is launched at once, up to 4 ahead of the oldest wait; any other pop, and
  * every pop behind it, is launched when the pops ahead of it have been waited
  * for, or runs inside its own wait.
  * kbhip_place_job_wait returns the results of the OLDEST outstanding ticket
@@ -149,8 +152,14 @@ int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int
  * kbhip_place_job_cancel withdraws `ticket` and every later one: their device
  * updates are undone and they are never reported.  Returns the number
  * withdrawn.
- * Every other session call fails with KBHIP_EINVAL while tickets are
- * outstanding; kbhip_session_close drops them. */
+ * Every call that runs or changes the session (actions, carry, place_job,
+ * kbhip_set_option, the kbhip_shard_connect_* calls, read-backs of device
+ * state) fails with KBHIP_EINVAL while tickets are outstanding; read-only host
+ * queries (kbhip_get_stats, kbhip_gang_unschedulable, kbhip_debug_table) are
+ * allowed; kbhip_session_close drops them.
+ * KBHIP_EUNSUPPORTED on node-sharded sessions (world > 1): a shard's launch
+ * waits inside the cross-rank exchange and a retraction would need every rank
+ * to cancel identically; shards use kbhip_place_job. */
 int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
                                int32_t min_available, int32_t ready_count);
 int kbhip_place_job_wait(kb_session* s, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,

@@ -429,6 +429,8 @@ struct BatchLaunch {
 struct PopTicket {
     int64_t id = 0;
     bool launched = false;
+    bool collected = false;  // place_job_wait: results read back (c_nd / c_st; rows in res_*_buf)
+    int c_nd = 0, c_st = 0;
     BatchLaunch L;
     vector<int32_t> ids;
     int gang = 0, min_avail = 0, ready = 0;
@@ -550,6 +552,7 @@ struct Session {
     hipEvent_t ev_nonov = nullptr;  // after a non-overlapped batched pop: the next overlapped one waits for it
     bool nonov_pending = false;
     double timed_ms = 0;          // summed duration of the timed sweep launches
+    hipEvent_t ev_sweep[2] = {nullptr, nullptr};  // kbhip_sweep_scores' standalone sweep (time_every > 0)
     double host_launch_s = 0, host_wait_s = 0;
     int64_t timed_n = 0;
     kbhip_stats stats{};
@@ -600,7 +603,7 @@ struct Session {
         comm = nullptr;
         comm_pooled = false;
         comm_bad = false;
-        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop})
+        for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop, &ev_sweep[0], &ev_sweep[1]})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
         for (auto& pr : ev_ring)
             for (auto& e : pr)
@@ -2077,7 +2080,12 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         S.ev_used[k] = true;
     }
     L.bf = S.any_bf != 0;
-    L.aff = !L.bf && S.classes[cls].aff;
+    // A session of the what-if lockstep group takes every batched pop through the group (a grouped
+    // session running an overlapped pop would hold the group's pop lane up until it left allocate):
+    // a pop without Backfilled nodes uses placement 7, which is exact for any class — with no
+    // pod-affinity program it is the plain greedy over the list, ending where a node outside it could win.
+    const bool grouped = S.rank_group && S.world == 1;
+    L.aff = !L.bf && (S.classes[cls].aff || grouped);
     const bool ov = S.overlap > 0 && S.world == 1 && !L.bf && !L.aff;
     if (!ov) ov_quiesce(S);
 
@@ -2500,22 +2508,40 @@ static int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_
     t.gang = gang_mode;
     t.min_avail = min_avail;
     t.ready = ready_count;
+    const int64_t id = t.id;
     S.tickets.push_back(std::move(t));
-    promote_tickets(S);
-    return S.tickets.back().id;
+    try {
+        promote_tickets(S);
+    } catch (...) {
+        // the caller gets an error and no ticket id: the new ticket must not stay queued
+        // (a launch that failed left it deferred; earlier tickets keep their state)
+        if (!S.tickets.empty() && S.tickets.back().id == id && !S.tickets.back().launched) S.tickets.pop_back();
+        throw;
+    }
+    return id;
 }
 
 static int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
                           int32_t* out_stop) {
     if (S.tickets.empty() || S.tickets.front().id != ticket)
         throw Error(KBHIP_EINVAL, "kbhip_place_job_wait must name the oldest outstanding ticket");
+    if (S.tickets.front().launched) {
+        // collected before the ticket leaves the queue: if the collection fails, the launched pop stays
+        // outstanding (its device updates can still be collected by a retried wait or undone by a cancel)
+        PopTicket& f = S.tickets.front();
+        int nd = 0, st = 0;
+        collect_batched(S, f.L, &nd, &st, S.res_node_buf, S.res_kind_buf);
+        f.launched = false;
+        f.collected = true;
+        f.c_nd = nd;
+        f.c_st = st;
+    }
     PopTicket t = std::move(S.tickets.front());
     S.tickets.pop_front();
     const int n = (int)t.ids.size();
-    bool sync = !t.launched;
-    if (t.launched) {
-        int nd = 0, st = 0;
-        collect_batched(S, t.L, &nd, &st, S.res_node_buf, S.res_kind_buf);
+    bool sync = !t.collected;
+    if (t.collected) {
+        const int nd = t.c_nd, st = t.c_st;
         if (nd == 0) {  // placement 7 could not place the first task exactly: the pop runs synchronously,
             retract_tickets(S, 0);  // and the launches behind it ran on a state it is about to change
             sync = true;
@@ -3706,14 +3732,26 @@ static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
     ctrl_setup(S, 1, &cls, 0, 0, 0, 0, -1, 0);
     if (S.classes[cls].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
     HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
+    const bool timed = S.time_every > 0;  // the standalone sweep's own duration (bench.py's sweep roofline)
+    if (timed) {
+        if (!S.ev_sweep[0]) { HIPCHK(hipEventCreate(&S.ev_sweep[0])); HIPCHK(hipEventCreate(&S.ev_sweep[1])); }
+        HIPCHK(hipEventRecord(S.ev_sweep[0], S.stream));
+    }
     HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, 1, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_cnt.p,
                              S.stream));
+    if (timed) HIPCHK(hipEventRecord(S.ev_sweep[1], S.stream));
     uint32_t cnt = 0;
     HIPCHK(hipMemcpyAsync(&cnt, S.b_rank_cnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
     if (out_keys && N)
         HIPCHK(hipMemcpyAsync(out_keys, S.b_rank_keys.p, (size_t)N * sizeof(uint64_t), hipMemcpyDeviceToHost,
                               S.stream));
     HIPCHK(hipStreamSynchronize(S.stream));
+    if (timed) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, S.ev_sweep[0], S.ev_sweep[1]));
+        S.stats.score_sweep_s += ms * 1e-3;
+        S.stats.score_sweeps++;
+    }
     S.stats.sweeps++;
     return (int)cnt;
 }
@@ -3882,6 +3920,10 @@ int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n
     ABI_GUARD_S(s, {
         if (!s || (!task_ids && n_tasks) || n_tasks < 0) throw kbhip::Error(KBHIP_EINVAL, "null argument");
         if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        // a shard's launch would block inside the exchange, and a retraction needs every rank to cancel
+        // identically: node-sharded sessions use the synchronous kbhip_place_job
+        if (s->s.world > 1)
+            throw kbhip::Error(KBHIP_EUNSUPPORTED, "kbhip_place_job_submit on a node-sharded session (use kbhip_place_job)");
         HIPCHK(hipSetDevice(s->s.device));
         return kbhip::place_job_submit(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count);
     })
@@ -4228,6 +4270,7 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out) {
 int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
     ABI_GUARD({
         if (!s || !key) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::require_no_tickets(s->s);  // options change how queued pops would run
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
         else if (std::strcmp(key, "speculate") == 0) {
@@ -4336,6 +4379,7 @@ int kbhip_shard_connect_rccl(kb_session* s, const void* unique_id, int64_t len) 
         if (len != (int64_t)sizeof(id)) throw kbhip::Error(KBHIP_EINVAL, "bad unique id length");
         std::memcpy(&id, unique_id, sizeof(id));
         if (s->s.comm) throw kbhip::Error(KBHIP_EINVAL, "session already connected");
+        kbhip::require_no_tickets(s->s);
         HIPCHK(hipSetDevice(s->s.device));
         const string key((const char*)unique_id, sizeof(id));
         if (ncclComm_t c = kbhip::comm_acquire(key, s->s.rank, s->s.world, s->s.device)) {
@@ -4362,6 +4406,7 @@ int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx)
         kbhip::Session& S = s->s;
         if (S.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
         if (S.mbox_own) throw kbhip::Error(KBHIP_EINVAL, "session already has a mailbox");
+        kbhip::require_no_tickets(S);  // a new mailbox restarts its sequence under launched pops
         HIPCHK(hipSetDevice(S.device));
         using kbhip::Mailbox;
         {  // this rank's mailbox: the pooled one of this device, else a new allocation (uncached memory,
@@ -4428,6 +4473,7 @@ int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx)
 int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx) {
     ABI_GUARD({
         if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::require_no_tickets(s->s);
         s->s.xfn = fn;
         s->s.xctx = ctx;
         return KBHIP_OK;
@@ -4436,6 +4482,7 @@ int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx) {
 int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx) {
     ABI_GUARD({
         if (!s || !fn) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbhip::require_no_tickets(s->s);
         s->s.xgfn = fn;
         s->s.xgctx = ctx;
         return KBHIP_OK;

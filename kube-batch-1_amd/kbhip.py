@@ -54,7 +54,8 @@ class Stats(ctypes.Structure):
                 ("pop_batch_sum", ctypes.c_int64), ("comm_reused", ctypes.c_int64),
                 ("async_launched", ctypes.c_int64), ("async_retracted", ctypes.c_int64),
                 ("async_cancelled", ctypes.c_int64), ("sweep_requests", ctypes.c_int64),
-                ("sweep_batch_sum", ctypes.c_int64)]
+                ("sweep_batch_sum", ctypes.c_int64), ("score_sweep_s", ctypes.c_double),
+                ("score_sweeps", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -191,12 +192,15 @@ class Session:
         _check(lib().kbhip_first_fit(self._h, _p(ids), ids.size, _p(out)))
         return out[: ids.size].copy()
 
-    def sweep_scores(self, task_id: int, n_nodes: int) -> Tuple[int, np.ndarray]:
+    def sweep_scores(self, task_id: int, n_nodes: int, keys: bool = True) -> Tuple[int, np.ndarray]:
         """kbhip_sweep_scores: preempt.go:270-287's predicate + score sweep of
-        one task: (passing nodes, per-node packed keys; 0 = node fails)."""
-        keys = np.zeros(max(n_nodes, 1), np.uint64)
-        n = _check(lib().kbhip_sweep_scores(self._h, int(task_id), _p(keys)))
-        return n, keys[:n_nodes].copy()
+        one task: (passing nodes, per-node packed keys; 0 = node fails).
+        keys=False: the count only (no copy of the keys)."""
+        if not keys:
+            return _check(lib().kbhip_sweep_scores(self._h, int(task_id), None)), np.zeros(0, np.uint64)
+        out = np.zeros(max(n_nodes, 1), np.uint64)
+        n = _check(lib().kbhip_sweep_scores(self._h, int(task_id), _p(out)))
+        return n, out[:n_nodes].copy()
 
     def carry(self) -> int:
         """kbhip_session_carry: become the next session (binds / evictions applied); bytes uploaded."""
@@ -265,12 +269,18 @@ class Session:
 
     def place_job_wait(self, ticket: int):
         """kbhip_place_job_wait: results of the oldest outstanding ticket, as place_job."""
-        n = getattr(self, "_tix", {}).pop(ticket, 1)
+        # the result arrays hold every task of the ticket; its size leaves the
+        # table only once the wait succeeded (a refused wait can be retried)
+        tix = getattr(self, "_tix", {})
+        if ticket not in tix:
+            raise KbhipError(f"ticket {ticket} is not outstanding in this binding")
+        n = tix[ticket]
         node = np.full(n, -1, np.int32)
         kind = np.zeros(n, np.uint8)
         done = np.zeros(1, np.int32)
         stop = np.zeros(1, np.int32)
         _check(lib().kbhip_place_job_wait(self._h, int(ticket), _p(node), _p(kind), _p(done), _p(stop)))
+        del tix[ticket]
         d = int(done[0])
         return node[:d].copy(), kind[:d].copy(), int(stop[0])
 

@@ -1220,6 +1220,27 @@ struct Engine {
         }
         return r;
     }
+    // Stratified CPU-baseline sampling (bench.py): outside the timed pop
+    // windows a task takes its decision from a given log (the engine's; any
+    // correct log reproduces the session state exactly) without sweeping;
+    // inside them it is swept for real and checked against the log.
+    const std::unordered_map<int, std::pair<int, int>>* replay = nullptr;  // pod -> (node, status)
+    vector<std::pair<int, int>> windows;  // timed pops [lo, hi)
+    double winTime = 0;
+    int winPops = 0, winTasks = 0, winPlaced = 0, mismatches = 0;
+    bool inWindow(int pop) const {
+        for (auto& wd : windows)
+            if (pop >= wd.first && pop < wd.second) return true;
+        return false;
+    }
+    bool replayTask(int pi) {
+        // (a walk over Backfilled nodes would mutate Idle: GetAccessibleResource)
+        if (w.anyBackfilled) throw std::runtime_error("sampled timing: Backfilled nodes appeared in the session");
+        auto it = replay->find(pi);
+        if (it == replay->end()) return false;  // the log's unassigned task
+        commitTask(pi, it->second.first, it->second.second == Allocated ? 1 : 2);
+        return true;
+    }
     bool placeTaskInner(int pi) {
         tried++;
         TaskPlan tp;
@@ -1259,9 +1280,15 @@ struct Engine {
             }
         }
         if (best.idx < 0) return false;
+        commitTask(pi, best.idx, best.kind);
+        return true;
+    }
+    // Session.Allocate (kind 1) / Session.Pipeline (kind 2) of task pi on node idx.
+    void commitTask(int pi, int idx, int kind) {
+        PodRec& p = w.pods[pi];
         JobRec& j = w.jobs[p.job];
         int status;
-        if (best.kind == 1) {
+        if (kind == 1) {
             // Allocate (session.go:237-297); usingBackfillTaskRes is always false here (Appendix A.1)
             status = Allocated;
             j.cntAlloc++;
@@ -1270,16 +1297,15 @@ struct Engine {
         }
         p.status = status;
         j.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
-        p.curNode = best.idx;
-        nodeAddTask(pi, best.idx, status);
+        p.curNode = idx;
+        nodeAddTask(pi, idx, status);
         onAllocate(p);
-        w.log.emplace_back(pi, best.idx, status);
+        w.log.emplace_back(pi, idx, status);
         if (status == Allocated && jobReady(j)) {
             // dispatch: Allocated -> Binding (both AllocatedStatuses; counts unchanged)
             for (int t : j.tasks)
                 if (w.pods[t].status == Allocated) { w.pods[t].status = Binding; j.priority = w.pods[t].priority; }
         }
-        return true;
     }
 
     // backfill action (actions/backfill/backfill.go:40-70): every Pending task
@@ -1675,6 +1701,8 @@ struct Engine {
             auto jit = jobsMap.find(q);
             if (jit == jobsMap.end() || jit->second.empty()) continue;
             int jb = jit->second.pop();
+            const bool timed = !replay || inWindow(pops);
+            const auto tp0 = std::chrono::steady_clock::now();
             pops++;
             auto pit = pending.find(jb);
             if (pit == pending.end()) {
@@ -1690,13 +1718,32 @@ struct Engine {
             auto& tasks = pit->second;
             while (!tasks.empty()) {
                 int t = tasks.pop();
-                if (!placeTask(t)) break;
+                bool ok;
+                if (timed) {
+                    ok = placeTask(t);
+                    if (replay) {  // the sampled sweep against the log it fast-forwarded with
+                        auto it = replay->find(t);
+                        const bool exp = it != replay->end();
+                        if (ok != exp || (ok && (std::get<1>(w.log.back()) != it->second.first ||
+                                                 std::get<2>(w.log.back()) != it->second.second)))
+                            mismatches++;
+                        winTasks++;
+                        winPlaced += ok;
+                    }
+                } else {
+                    ok = replayTask(t);
+                }
+                if (!ok) break;
                 if (jobReady(w.jobs[jb])) {
                     jit->second.push(jb);
                     break;
                 }
             }
             queues.push(q);
+            if (replay && timed) {
+                winTime += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
+                winPops++;
+            }
         }
     }
 };
@@ -1742,6 +1789,47 @@ int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* o
         }
         return n;
     } catch (const std::exception& ex) {
+        g_ferr = ex.what();
+        return -1;
+    }
+}
+
+/* Stratified timing of the hoisted allocate (bench.py's CPU baseline): the
+ * session runs to the end; pops in [win_lo[i], win_hi[i]) are swept for real
+ * and timed, every other task takes its decision from the given log (pod,
+ * node, status) without a sweep.  out[0] = timed seconds, [1] = timed pops,
+ * [2] = tasks swept, [3] = of them placed, [4] = swept decisions that differ
+ * from the log, [5] = pops in the session, [6] = placements, [7] = load s. */
+int fast_allocate_sampled(const char* path, int threads, int n_log, const int32_t* log_pod, const int32_t* log_node,
+                          const int32_t* log_status, int n_win, const int32_t* win_lo, const int32_t* win_hi,
+                          double* out) {
+    try {
+        using clk = std::chrono::steady_clock;
+        auto t0 = clk::now();
+        kbs::Snapshot snap(path);
+        fast::World w;
+        fast::Loader L(snap, w);
+        L.load();
+        auto t1 = clk::now();
+        fast::Engine e(w, threads < 1 ? 1 : threads);
+        e.openPlugins();
+        if (w.anyBackfilled) throw std::runtime_error("sampled timing needs a session without Backfilled nodes");
+        std::unordered_map<int, std::pair<int, int>> rp;
+        rp.reserve((size_t)n_log * 2);
+        for (int i = 0; i < n_log; ++i) rp[log_pod[i]] = {log_node[i], log_status[i]};
+        e.replay = &rp;
+        for (int i = 0; i < n_win; ++i) e.windows.emplace_back(win_lo[i], win_hi[i]);
+        e.runActions("allocate", -1);
+        out[0] = e.winTime;
+        out[1] = e.winPops;
+        out[2] = e.winTasks;
+        out[3] = e.winPlaced;
+        out[4] = e.mismatches;
+        out[5] = e.pops;
+        out[6] = (double)w.log.size();
+        out[7] = std::chrono::duration<double>(t1 - t0).count();
+        return 0;
+    } catch (std::exception& ex) {
         g_ferr = ex.what();
         return -1;
     }

@@ -177,6 +177,31 @@ def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
     return Placement(pod[:n].copy(), node[:n].copy(), st[:n].copy())
 
 
+def fast_allocate_sampled(path: str, log_pod, log_node, log_status, windows, threads: int = 16) -> dict:
+    """Stratified timing of the hoisted allocate (bench.py's CPU baseline):
+    the whole session runs, the pops in each [lo, hi) window are swept for
+    real and timed, every other task takes its decision from the given
+    placement log (statuses ALLOCATED=4 / PIPELINED=8) without a sweep; the
+    swept decisions are checked against the log (``mismatches``)."""
+    lib = _lib("kbfast")
+    fn = lib.fast_allocate_sampled
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 3 + \
+        [ctypes.c_int] + [ctypes.c_void_p] * 3
+    pod = np.ascontiguousarray(log_pod, np.int32)
+    node = np.ascontiguousarray(log_node, np.int32)
+    st = np.ascontiguousarray(log_status, np.int32)
+    lo = np.ascontiguousarray([w[0] for w in windows], np.int32)
+    hi = np.ascontiguousarray([w[1] for w in windows], np.int32)
+    out = np.zeros(8, np.float64)
+    if fn(path.encode(), threads, len(pod), _p(pod), _p(node), _p(st), len(lo), _p(lo), _p(hi), _p(out)) < 0:
+        lib.fast_last_error.restype = ctypes.c_char_p
+        raise RuntimeError(lib.fast_last_error().decode())
+    return {"timed_s": out[0], "timed_pops": int(out[1]), "tasks_swept": int(out[2]), "placed": int(out[3]),
+            "mismatches": int(out[4]), "session_pops": int(out[5]), "session_placements": int(out[6]),
+            "load_s": out[7]}
+
+
 def fast_trace_affinity(path: str, n_nodes: int, cap_tasks: int = 4096, actions: str = "allocate") -> dict:
     """Test support: run the hoisted restatement of the actions with a
     per-task trace.  For every task tried, in order: pod, result node (-1

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Summarise a run_profile.sh output directory into the files committed under
 profiles/: <tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
-<tag>_summary.json (per kernel: calls, mean duration, FETCH_SIZE per launch
-and the gfx950-corrected HBM bytes per launch).
+<tag>_summary.json (per kernel: calls, mean duration, the union busy period
+of overlapping launches, FETCH_SIZE per launch and the gfx950-corrected HBM
+bytes per launch, SQ occupancy / stall counters per launch with VGPR / SGPR /
+LDS of the kernel).
 
 FETCH_SIZE is reported in KB by rocprofv3; on gfx950 it counts exactly half
 the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section),
@@ -71,6 +73,29 @@ def main(src, tag):
             d["fetch_size_kb_per_launch"] = tot / n
             d["hbm_bytes_per_launch_corrected"] = 2.0 * tot / n * 1024.0
             d["pmc_launches"] = n
+    sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
+    if os.path.exists(sq_csv):  # occupancy / stall counters, per launch, with the kernel's resources
+        acc = defaultdict(lambda: defaultdict(float))
+        res, disp = {}, defaultdict(set)
+        with open(sq_csv) as f:
+            for row in csv.DictReader(f):
+                k = short(row["Kernel_Name"])
+                acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                disp[k].add(row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                res[k] = {"grid": int(row.get("Grid_Size", 0) or 0), "wg": int(row.get("Workgroup_Size", 0) or 0),
+                          "lds": int(row.get("LDS_Block_Size", 0) or 0), "vgpr": int(row.get("VGPR_Count", 0) or 0),
+                          "agpr": int(row.get("Accum_VGPR_Count", 0) or 0), "sgpr": int(row.get("SGPR_Count", 0) or 0)}
+        for k, c in acc.items():
+            n = max(len(disp[k]), 1)
+            per = {name: v / n for name, v in sorted(c.items())}
+            d = out["kernels"].setdefault(k, {})
+            d["sq"] = {"launches": n, **res[k], "per_launch": per}
+            wc = per.get("SQ_WAVE_CYCLES", 0.0)
+            if wc > 0:
+                for key, name in (("wait_any_frac", "SQ_WAIT_ANY"), ("wait_inst_frac", "SQ_WAIT_INST_ANY"),
+                                  ("active_inst_frac", "SQ_ACTIVE_INST_ANY"), ("valu_frac", "SQ_ACTIVE_INST_VALU")):
+                    if name in per:
+                        d["sq"][key] = round(per[name] / wc, 3)
     for name in ("bench_trace.json", "bench_pmc.json"):
         p = os.path.join(src, name)
         if os.path.exists(p):

@@ -162,6 +162,32 @@ def test_ticket_rules(engine, kbgen_mod, tmp_path):
         assert _same(s.place_job(*calls[0][:4]), calls[0][4])
 
 
+def test_refused_wait_keeps_ticket(engine, kbgen_mod, tmp_path):
+    """A wait refused with EINVAL (not the oldest ticket) leaves that ticket's
+    result arrays sized for all its tasks: the retried wait of a multi-task
+    pop reports every task (the binding lost the size)."""
+    c = kbgen_mod.gen_random(9601, n_nodes=24, n_jobs=6, max_tasks=12, features=NO_POD_AFFINITY,
+                             tiers=[["gang"], ["predicates", "nodeorder"]])
+    p = str(tmp_path / "r.kbs")
+    c.write(p)
+    calls, _, _ = _record(engine, p, c)
+    multi = [i for i, x in enumerate(calls) if len(x[4][0]) > 1]
+    assert multi, "the generator gave no multi-task pop"
+    i = multi[0]
+    assert i + 1 < len(calls) or i > 0
+    with engine.Session(p) as s:
+        for x in calls[:i]:
+            assert _same(s.place_job(*x[:4]), x[4])
+        a = s.place_job_submit(*calls[i][:4])
+        b = s.place_job_submit(*calls[i + 1][:4]) if i + 1 < len(calls) else None
+        if b is not None:
+            with pytest.raises(engine.KbhipError, match="oldest"):
+                s.place_job_wait(b)  # refused: b's size stays in the binding
+        assert _same(s.place_job_wait(a), calls[i][4])
+        if b is not None:
+            assert _same(s.place_job_wait(b), calls[i + 1][4])
+
+
 def test_deferred_pops_keep_order(engine, kbgen_mod, tmp_path):
     """Pops longer than one chunk (or of mixed classes) run inside their wait;
     the pops behind them launch only after."""
