@@ -246,41 +246,41 @@ def sweep_roofline(buf, device, pods, n_tasks=256):
             "note": "reads 113 B/node (SURVEY §8(d)) and writes an 8-byte key per node (not counted)"}
 
 
-def cpu_baseline(path, target_s, log, session_pops):
+def cpu_baseline(path, target_s, log):
     """The hoisted restatement on a stratified sample of the same session:
-    three pop windows (around 1/6, 1/2 and 5/6 of the session's pops) swept
-    and timed; the rest fast-forwarded from the engine's log."""
+    three windows of the session's task sequence (around 1/6, 1/2 and 5/6 of
+    the tasks tried) swept and timed; every other task fast-forwarded from
+    the engine's log."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # the checker / CPU baseline only (test infrastructure)
     threads = min(16, os.cpu_count() or 1)
     pod, node, kind = log
     status = np.where(kind == kbhip.ALLOCATED, 4, 8).astype(np.int32)  # api.Allocated / api.Pipelined
-    P = session_pops
-    centers = (P // 6, P // 2, 5 * P // 6)
-    probe = oracle.fast_allocate_sampled(path, pod, node, status, [(c, c + 20) for c in centers], threads=threads)
-    per_pop = probe["timed_s"] / max(probe["timed_pops"], 1)
-    P = probe["session_pops"]  # the restatement's own count of the session's job pops
-    centers = (P // 6, P // 2, 5 * P // 6)
-    W = int(max(20, min(P // 6, target_s / 3 / max(per_pop, 1e-6))))
-    strata, placed, secs, mism = [], 0, 0.0, probe["mismatches"]
+    probe = oracle.fast_allocate_sampled(path, pod, node, status, [(0, 200)], threads=threads)
+    T = probe["session_tasks"]
+    per_task = probe["timed_s"] / max(probe["tasks_swept"], 1)
+    W = int(max(50, min(T // 6, target_s / 3 / max(per_task, 1e-9))))
+    strata, placed, secs, swept, mism = [], 0, 0.0, 0, probe["mismatches"]
     est_alloc_s = 0.0
-    for c in centers:
+    for c in (T // 6, T // 2, 5 * T // 6):
         lo = max(0, c - W // 2)
         r = oracle.fast_allocate_sampled(path, pod, node, status, [(lo, lo + W)], threads=threads)
-        strata.append({"pops": [lo, lo + r["timed_pops"]], "placed": r["placed"], "s": round(r["timed_s"], 3)})
+        strata.append({"tasks": [lo, lo + r["tasks_swept"]], "placed": r["placed"], "s": round(r["timed_s"], 3)})
         placed += r["placed"]
+        swept += r["tasks_swept"]
         secs += r["timed_s"]
         mism += r["mismatches"]
-        est_alloc_s += r["timed_s"] / max(r["timed_pops"], 1) * (P / 3)  # this stratum's third of the pops
+        est_alloc_s += r["timed_s"] / max(r["tasks_swept"], 1) * (T / 3)  # this stratum's third of the tasks
     return {"value": placed / secs, "unit": "placements/s", "cores": threads, "kind": "port",
             "p50_allocate_ms_est": est_alloc_s * 1e3,
             "session_placements_per_s_est": len(pod) / est_alloc_s,
             "strata": strata, "log_mismatches": mism,
-            "sample": f"3 windows of {W} job pops (around 1/6, 1/2, 5/6 of the session's {P} pops) of the same "
-                      f"C4 session, swept and timed; the pops between fast-forwarded from the engine's placement "
-                      f"log (the swept decisions are checked against it: {mism} differ); allocate action only, "
-                      f"hoisted C++ restatement oracle/kbfast.cpp, {threads} threads on {os.cpu_count()} host cpus; "
-                      f"p50_allocate_ms_est = the whole session's allocate extrapolated per stratum"}
+            "sample": f"3 windows of {W} tasks (around 1/6, 1/2, 5/6 of the {T} tasks the session tries) of the "
+                      f"same C4 session, swept and timed ({swept} tasks, {placed} placements); every other task "
+                      f"fast-forwarded from the engine's placement log (the swept decisions are checked against it: "
+                      f"{mism} differ); allocate action only, hoisted C++ restatement oracle/kbfast.cpp, {threads} "
+                      f"threads on {os.cpu_count()} host cpus; p50_allocate_ms_est = the whole session's allocate "
+                      f"extrapolated per stratum"}
 
 
 def main():
@@ -380,7 +380,7 @@ def main():
                      "sweep": sweep},
     }
     if args.cpu_baseline and world == 1:
-        out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds, log0, st_last["pops"])
+        out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds, log0)
         out["cpu_baseline"]["gpu_p50_session_ms"] = out["p50_session_ms"]
     print(json.dumps(out))
     if dist is not None:

@@ -1225,12 +1225,12 @@ struct Engine {
     // correct log reproduces the session state exactly) without sweeping;
     // inside them it is swept for real and checked against the log.
     const std::unordered_map<int, std::pair<int, int>>* replay = nullptr;  // pod -> (node, status)
-    vector<std::pair<int, int>> windows;  // timed pops [lo, hi)
+    vector<std::pair<int, int>> windows;  // timed tasks [lo, hi) of the session's task sequence
     double winTime = 0;
-    int winPops = 0, winTasks = 0, winPlaced = 0, mismatches = 0;
-    bool inWindow(int pop) const {
+    int winTasks = 0, winPlaced = 0, mismatches = 0, taskSeq = 0;
+    bool inWindow(int i) const {
         for (auto& wd : windows)
-            if (pop >= wd.first && pop < wd.second) return true;
+            if (i >= wd.first && i < wd.second) return true;
         return false;
     }
     bool replayTask(int pi) {
@@ -1701,8 +1701,6 @@ struct Engine {
             auto jit = jobsMap.find(q);
             if (jit == jobsMap.end() || jit->second.empty()) continue;
             int jb = jit->second.pop();
-            const bool timed = !replay || inWindow(pops);
-            const auto tp0 = std::chrono::steady_clock::now();
             pops++;
             auto pit = pending.find(jb);
             if (pit == pending.end()) {
@@ -1719,8 +1717,12 @@ struct Engine {
             while (!tasks.empty()) {
                 int t = tasks.pop();
                 bool ok;
+                const bool timed = !replay || inWindow(taskSeq);  // windows over the session's task sequence
+                taskSeq++;
                 if (timed) {
+                    const auto tp0 = std::chrono::steady_clock::now();
                     ok = placeTask(t);
+                    if (replay) winTime += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
                     if (replay) {  // the sampled sweep against the log it fast-forwarded with
                         auto it = replay->find(t);
                         const bool exp = it != replay->end();
@@ -1740,10 +1742,6 @@ struct Engine {
                 }
             }
             queues.push(q);
-            if (replay && timed) {
-                winTime += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
-                winPops++;
-            }
         }
     }
 };
@@ -1795,9 +1793,10 @@ int fast_trace_affinity(const char* path, int cap_tasks, int n_nodes, int32_t* o
 }
 
 /* Stratified timing of the hoisted allocate (bench.py's CPU baseline): the
- * session runs to the end; pops in [win_lo[i], win_hi[i]) are swept for real
- * and timed, every other task takes its decision from the given log (pod,
- * node, status) without a sweep.  out[0] = timed seconds, [1] = timed pops,
+ * session runs to the end; the tasks tried at positions [win_lo[i],
+ * win_hi[i]) of the session's task sequence are swept for real and timed,
+ * every other task takes its decision from the given log (pod, node, status)
+ * without a sweep.  out[0] = timed seconds, [1] = tasks tried in the session,
  * [2] = tasks swept, [3] = of them placed, [4] = swept decisions that differ
  * from the log, [5] = pops in the session, [6] = placements, [7] = load s. */
 int fast_allocate_sampled(const char* path, int threads, int n_log, const int32_t* log_pod, const int32_t* log_node,
@@ -1821,7 +1820,7 @@ int fast_allocate_sampled(const char* path, int threads, int n_log, const int32_
         for (int i = 0; i < n_win; ++i) e.windows.emplace_back(win_lo[i], win_hi[i]);
         e.runActions("allocate", -1);
         out[0] = e.winTime;
-        out[1] = e.winPops;
+        out[1] = e.taskSeq;
         out[2] = e.winTasks;
         out[3] = e.winPlaced;
         out[4] = e.mismatches;

@@ -179,8 +179,8 @@ def fast_allocate(path: str, threads: int = 16, cap: Optional[int] = None,
 
 def fast_allocate_sampled(path: str, log_pod, log_node, log_status, windows, threads: int = 16) -> dict:
     """Stratified timing of the hoisted allocate (bench.py's CPU baseline):
-    the whole session runs, the pops in each [lo, hi) window are swept for
-    real and timed, every other task takes its decision from the given
+    the whole session runs, the tasks at positions [lo, hi) of the session's
+    task sequence are swept for real and timed, every other task takes its decision from the given
     placement log (statuses ALLOCATED=4 / PIPELINED=8) without a sweep; the
     swept decisions are checked against the log (``mismatches``)."""
     lib = _lib("kbfast")
@@ -197,7 +197,7 @@ def fast_allocate_sampled(path: str, log_pod, log_node, log_status, windows, thr
     if fn(path.encode(), threads, len(pod), _p(pod), _p(node), _p(st), len(lo), _p(lo), _p(hi), _p(out)) < 0:
         lib.fast_last_error.restype = ctypes.c_char_p
         raise RuntimeError(lib.fast_last_error().decode())
-    return {"timed_s": out[0], "timed_pops": int(out[1]), "tasks_swept": int(out[2]), "placed": int(out[3]),
+    return {"timed_s": out[0], "session_tasks": int(out[1]), "tasks_swept": int(out[2]), "placed": int(out[3]),
             "mismatches": int(out[4]), "session_pops": int(out[5]), "session_placements": int(out[6]),
             "load_s": out[7]}
 
