@@ -1,7 +1,11 @@
 """Session carry-over cost at C4: time kbhip_session_carry
 (next session's start state from this session's end state, changed node rows
-uploaded) against kbhip_session_open of the C4 snapshot (parse + encode + upload).
-Prints one JSON line.  Usage: python bench_carry.py [--rounds R]"""
+uploaded) against kbhip_session_open of the C4 snapshot (parse + encode + upload),
+and kbhip_session_carry_snapshot with pod arrivals: the cache's next snapshot
+(this session's binds applied, --arrivals x pods arriving in new gang jobs
+with new request shapes) carried over, against opening that snapshot; the
+carried session's allocate log must equal the freshly opened one's.
+Prints one JSON line.  Usage: python bench_carry.py [--rounds R] [--arrivals F]"""
 import argparse
 import json
 import os
@@ -15,9 +19,75 @@ import kbgen  # noqa: E402
 import kbhip  # noqa: E402
 
 
+class _Strtab:  # write_kbs takes an object with bytes()
+    def __init__(self, b):
+        self.b = b
+
+    def bytes(self):
+        return self.b
+
+
+def next_snapshot_with_arrivals(C, st, status, node, frac, seed=4242):
+    """The C4 cache state after a session (its binds applied: Binding -> bound,
+    Pending with a node) plus frac x P new pods in new gang jobs (8..64 tasks,
+    request shapes outside the C4 mix: new task classes), appended in UID
+    order ("v..." after the pending "u..." pods; jobs "jq..." between the
+    pending "jp..." and running "jr..." jobs).  Returns (columns, strtab,
+    old_pod, old_node)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    C = {k: v.copy() for k, v in C.items()}
+    P, N = len(C["p_uid"]), len(C["n_name"])
+    bound = status == 16  # Binding: cache.Bind succeeded -> Bound on its node
+    C["p_node"][bound] = C["n_name"][node[bound]]
+    A = int(P * frac)
+    sizes = []
+    while sum(sizes) < A:
+        sizes.append(int(min(rng.integers(8, 65), A - sum(sizes))))
+    J_new = len(sizes)
+    extra = bytearray()
+    base = len(st)
+
+    def add(sv):
+        nonlocal extra
+        off = base + len(extra)
+        extra += sv.encode() + b"\0"
+        return off
+    uid_off = np.array([add(f"v{i:08d}") for i in range(A)], np.int32)
+    job_off = np.array([add(f"jq{i:07d}") for i in range(J_new)], np.int32)
+    n_pj = int(np.searchsorted([st[o:st.index(b"\0", o)].decode() for o in C["j_name"]], "jq"))
+    pj = np.repeat(np.arange(J_new), sizes).astype(np.int32)
+    cpu = rng.choice([750, 1500, 3000], size=J_new)[pj].astype(np.int64)
+    mem = (rng.choice([3, 6], size=J_new)[pj] << 30).astype(np.int64)
+    gpu = np.zeros(A, np.int64)
+    # jobs: insert the new ones at n_pj; old job indices >= n_pj shift
+    for k, newv in (("j_ns", np.full(J_new, C["j_ns"][0], np.int32)), ("j_name", job_off),
+                    ("j_queue", np.full(J_new, C["j_queue"][0], np.int32)),
+                    ("j_min", np.asarray(sizes, np.int32)), ("j_pg_priority", np.zeros(J_new, np.int32)),
+                    ("j_ts", np.full(J_new, 10**12, np.int64))):
+        C[k] = np.concatenate([C[k][:n_pj], newv, C[k][n_pj:]]).astype(C[k].dtype)
+    pjob = C["p_job"].copy()
+    pjob[pjob >= n_pj] += J_new
+    C["p_job"] = np.concatenate([pjob, n_pj + pj]).astype(np.int32)
+    for k, newv in (("p_uid", uid_off), ("p_name", uid_off), ("p_ns", np.full(A, C["p_ns"][0], np.int32)),
+                    ("p_node", np.full(A, -1, np.int32)), ("p_phase", np.zeros(A, np.uint8)),
+                    ("p_deleting", np.zeros(A, np.uint8)), ("p_backfill", np.zeros(A, np.uint8)),
+                    ("p_priority", np.zeros(A, np.int32)), ("p_ts", np.full(A, 10**12, np.int64)),
+                    ("c_cpu", cpu), ("c_mem", mem), ("c_gpu", gpu),
+                    ("c_has", np.full(A, C["c_has"][0], np.uint8)), ("p_aff", np.full(A, -1, np.int32))):
+        C[k] = np.concatenate([C[k], newv]).astype(C[k].dtype)
+    for k in ("p_label_off", "p_nsel_off", "p_ictr_off", "p_tol_off", "c_port_off"):
+        assert not C[k].any(), k  # the C4 shape: one container per pod, nothing else
+        C[k] = np.zeros(P + A + 1, np.int32)
+    C["p_ctr_off"] = np.arange(P + A + 1, dtype=np.int32)
+    old_pod = np.concatenate([np.arange(P, dtype=np.int32), np.full(A, -1, np.int32)])
+    return C, _Strtab(bytes(st) + bytes(extra)), old_pod, np.arange(N, dtype=np.int32)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--arrivals", type=float, default=0.01, help="pods arriving between the sessions / pods")
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     args = ap.parse_args()
     os.makedirs(args.cache, exist_ok=True)
@@ -38,9 +108,40 @@ def main():
         carries.append(time.perf_counter() - t1)
         placed2.append(len(s.allocate()[0]))
         s.close()
+    # arrivals: the cache's next snapshot, carried over vs opened fresh
+    import numpy as np
+    C, st = kbgen.read_kbs(p)
+    with kbhip.Session(buf, device=0) as s:
+        s.allocate()
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+    C2, st2, old_pod, old_node = next_snapshot_with_arrivals(C, st, status, node, args.arrivals)
+    p2 = os.path.join(args.cache, f"c4_next_{args.arrivals}.kbs")
+    kbgen.write_kbs(p2, C2, st2)
+    with open(p2, "rb") as f:
+        buf2 = f.read()
+    arr_open, arr_carry, arr_sent, equal = [], [], [], True
+    for _ in range(args.rounds):
+        t0 = time.perf_counter()
+        f = kbhip.Session(buf2, device=0)
+        arr_open.append(time.perf_counter() - t0)
+        fresh = f.allocate()
+        f.close()
+        s = kbhip.Session(buf, device=0)
+        s.allocate()
+        t1 = time.perf_counter()
+        arr_sent.append(s.carry_snapshot(buf2, old_pod, old_node))
+        arr_carry.append(time.perf_counter() - t1)
+        got = s.allocate()
+        s.close()
+        equal = equal and all(np.array_equal(a, b) for a, b in zip(got, fresh))
     print(json.dumps({"metric": "C4 session start: open vs carry (ms)", "open_ms": statistics.median(opens) * 1e3,
                       "carry_ms": statistics.median(carries) * 1e3, "carry_bytes_uploaded": statistics.median(sent),
-                      "second_session_placements": statistics.median(placed2), "rounds": args.rounds}))
+                      "second_session_placements": statistics.median(placed2), "rounds": args.rounds,
+                      "arrivals": {"pods": int((old_pod < 0).sum()), "frac": args.arrivals,
+                                   "open_ms": statistics.median(arr_open) * 1e3,
+                                   "carry_snapshot_ms": statistics.median(arr_carry) * 1e3,
+                                   "carry_snapshot_bytes_uploaded": statistics.median(arr_sent),
+                                   "placements": int(len(fresh[0])), "log_equal_to_fresh_open": bool(equal)}}))
 
 
 if __name__ == "__main__":

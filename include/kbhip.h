@@ -197,6 +197,14 @@ int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* 
 int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node);
 int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys);
 
+/* Measurement hook (bench.py's sweep roofline): kbhip_sweep_scores' sweep
+ * kernel for each given task, launched back to back on the session stream
+ * with no copies in between; *out_mean_us = device time per launch (one
+ * HIP-event pair around the sequence, launch boundaries included).  Changes
+ * nothing.  KBHIP_EUNSUPPORTED for classes with inter-pod priority terms
+ * (their sweep needs a min / max prepass per task). */
+int kbhip_time_sweeps(kb_session* s, const int32_t* task_ids, int32_t n, double* out_mean_us);
+
 /* Run the reclaim action (actions/reclaim/reclaim.go:41-196) / the preempt
  * action (actions/preempt/preempt.go:43-353) on the session's current state.
  * Output records in decision order: (pod, node, KBHIP_EVICTED) for every
@@ -224,28 +232,51 @@ int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* o
  * (anti-)affinity count tables are recounted from the carried pod states.
  * On a node-sharded session every rank carries (identically on its
  * replicated host model; each uploads its own rows; no collective).  Pod
- * arrivals and node changes need kbhip_session_open. */
+ * arrivals, node and PodGroup changes: kbhip_session_carry_snapshot. */
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes);
 
 /* kbhip_session_carry plus the scheduler cache's events on existing pods
  * between the two sessions (pkg/scheduler/cache/event_handlers.go), applied
- * in order after the carry: KBHIP_EV_DELETE — deletePod -> deleteTask, the
- * pod leaves its job and its node (a shadow job left without pods leaves the
- * cache); KBHIP_EV_SUCCEEDED / KBHIP_EV_FAILED — updatePod to a terminal phase
- * (isTerminated: the task stays in its job, its node no longer counts it).
+ * in order after the carry:
+ *   KBHIP_EV_DELETE — deletePod -> deleteTask on NewTaskInfo(pod)
+ *     (event_handlers.go:119-165).  A pod of a PodGroup leaves its job and
+ *     its node.  A group-less pod's TaskInfo has an empty Job
+ *     (api/job_info.go:60-70), so the cache keeps it in its shadow job with
+ *     its status and NodeName and only takes it off its node (the pod is
+ *     "detached", kbsnap.h p_detached: it still counts for its job's
+ *     readiness and the drf / proportion shares; a pending one is allocated
+ *     again).  No job is deleted (JobTerminated needs a nil PodGroup).
+ *   KBHIP_EV_SUCCEEDED / KBHIP_EV_FAILED — updatePod to a terminal phase
+ *     (isTerminated: the task stays in its job, its node no longer counts it).
  * pods[i] are pod indices of the opened snapshot (they stay the session's pod
  * ids; a deleted pod never appears in a later record).  Every event is
  * validated first (KBHIP_EINVAL: index out of range, unknown event, an event
- * on a deleted pod) and nothing changes on error.
- * Deliberate deviation: the reference's deletePod builds NewTaskInfo(pod),
- * whose Job is empty for a pod without a PodGroup (api/job_info.go:60-70), so
- * the cache takes a deleted group-less pod off its node only — the task stays
- * in its shadow job (cache/event_handlers.go:119-165) and the next session
- * still counts it (a Pending one is allocated again).  The engine removes the
- * pod from its shadow job, and a shadow job left without pods from the cache:
- * the state a fresh snapshot of the cluster holds, which is what the parity
- * tests compare against (tests/test_gpu_carry.py). */
+ * on a deleted or detached pod; KBHIP_EUNSUPPORTED: detaching a pod in a
+ * session with pod (anti)-affinity terms — the predicate lister's
+ * NodeInfo.Filter would leave it out at its own node only) and nothing
+ * changes on error. */
 enum { KBHIP_EV_DELETE = 1, KBHIP_EV_SUCCEEDED = 2, KBHIP_EV_FAILED = 3 };
+
+/* The next scheduling session from the scheduler cache's snapshot of it
+ * (cache.go:515-583 after the informer events of event_handlers.go: pod
+ * arrivals, deletions and phase changes, node add / update / delete, PodGroup
+ * and queue add / update), re-deriving only what changed.  kbs: the new KBS1
+ * snapshot (canonical order, kbsnap.h); old_pod[i] / old_node[n]: the index
+ * in THIS session of the new snapshot's pod i / node n, -1 for a new object
+ * (a pod whose spec or labels changed — updatePod re-adds it, event_handlers.go
+ * :101-110 — is new too).  Afterwards the session's pod and node indices are
+ * the new snapshot's.  Fast path when the node set, node labels / taints and
+ * the conf are unchanged, no pod carries pod (anti-)affinity terms and new
+ * pods have no host ports, nodeSelector or node affinity: mapped pods keep
+ * their dictionary ids and task classes, new pods are classed against the
+ * kept dictionaries, jobs / queues / plugin state and node rows are
+ * re-derived, and only node rows that differ (plus grown class tables) are
+ * uploaded.  Any other change re-opens the session in place (same handle,
+ * same options; *out_uploaded_bytes = -1).  KBHIP_EUNSUPPORTED on
+ * node-sharded sessions; KBHIP_EINVAL for a malformed map.  On error the
+ * session may hold a partial state: close it. */
+int kbhip_session_carry_snapshot(kb_session* s, const void* kbs, size_t len, const int32_t* old_pod,
+                                 const int32_t* old_node, int64_t* out_uploaded_bytes);
 int kbhip_session_carry_events(kb_session* s, const int32_t* pods, const uint8_t* events, int64_t n,
                                int64_t* out_uploaded_bytes);
 

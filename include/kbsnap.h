@@ -95,6 +95,11 @@ typedef struct kbs_dirent {
  * p_job                       i32[P]  job index (-1 = no pod group)
  * p_node                      i32[P]  str Spec.NodeName (-1 = "")
  * p_phase p_deleting p_backfill u8[P]
+ * p_detached                  u8[P]   optional: 1 = the scheduler cache deleted this group-less
+ *                                     pod, which takes it off its node only (deletePod builds
+ *                                     NewTaskInfo with an empty Job, cache/event_handlers.go:
+ *                                     119-165): the task stays in its shadow job with its status
+ *                                     and NodeName but is not in that node's task list
  * p_priority                  i32[P]  *Spec.Priority
  * p_ts                        i64[P]  CreationTimestamp (ns)
  * p_label_off (P+1) pl_key pl_val

@@ -113,11 +113,11 @@ KBHIP_HD bool term_match(const DevTables& t, const NodeCols& nc, const Term& tm,
 
 // The static part of the predicates: selector / node affinity, unschedulable,
 // taints.  Does not change while a session runs.
-KBHIP_HD bool static_pred(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                            const NodeCols& nc, int n) {
+KBHIP_HD bool static_pred_f(const Conf& cf, const TaskClass& c, const DevTables& t, const NodeCols& nc, int n,
+                            uint8_t flags) {  // flags = nc.flags[n], loaded by the caller with the row
     if (!cf.pred_on) return true;
     if (c.pred_err) return false;
-    if (nc.flags[n] & 1) return false;                                   // predicates.go:107-112
+    if (flags & 1) return false;                                         // predicates.go:107-112
     for (int w = 0; w < nc.taint_words; ++w)                             // helper/helpers.go:425-440
         if (nc.taints[(int64_t)w * nc.npad + n] & ~t.masks[c.tol_off + w]) return false;
     if (c.nsel_term >= 0 && !term_match(t, nc, t.terms[c.nsel_term], n)) return false;  // predicates.go:809-814
@@ -127,6 +127,9 @@ KBHIP_HD bool static_pred(const Conf& cf, const TaskClass& c, const DevTables& t
         if (!any) return false;
     }
     return true;
+}
+KBHIP_HD bool static_pred(const Conf& cf, const TaskClass& c, const DevTables& t, const NodeCols& nc, int n) {
+    return static_pred_f(cf, c, t, nc, n, cf.pred_on ? nc.flags[n] : (uint8_t)0);
 }
 
 // ((cap - req) * 10) / cap for 0 <= req <= cap, cap > 0: the quotient is in
@@ -217,14 +220,15 @@ KBHIP_HD uint32_t fit_bits(const TaskClass& c, const Row& r, bool passed) {
 KBHIP_HD uint64_t eval_node(const Conf& cf, const TaskClass& c, const DevTables& t,
                                               const NodeCols& nc, int n, int32_t* score_out, bool* passed,
                                               uint32_t* fit = nullptr) {
-    // the row and port words first: their loads do not depend on the
-    // predicates' early exits, so they share one memory round trip with the
-    // flag / taint loads instead of following them
+    // the flags, row and port words first: their loads do not depend on the
+    // predicates' early exits, so they share one memory round trip instead of
+    // following each other
+    const uint8_t fl = nc.flags[n];
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};
     if (c.has_ports)
         for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
-    const bool st = static_pred(cf, c, t, nc, n);
+    const bool st = static_pred_f(cf, c, t, nc, n, fl);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, score_out, passed);
     if (fit) *fit = fit_bits(c, r, *passed);

@@ -53,6 +53,95 @@ __global__ __launch_bounds__(kBlock) void k_rank_nodes(Conf cf, NodeCols nc, Dev
     if (threadIdx.x == 0 && s_cnt) atomicAdd(count, s_cnt);
 }
 
+// The standalone predicate + score sweep of one task (kbhip_sweep_scores:
+// preempt.go:270-287's PredicateFn + NodeOrderFn over every node): per node
+// pack_key(score, index) when it passes, 0 otherwise; the passing count in
+// kGroups counters on separate lines, block b adding to counter b % kGroups
+// (one device-scope counter taking an add from every block serialises the
+// tail of the launch: MI355X_MICROARCH.md fanin).  PLAIN: a class without pod
+// (anti-)affinity or inter-pod terms (eval_node: the row loads are issued
+// before the predicates' early exits); otherwise eval_node_aff.
+constexpr int kSweepGroups = 8;
+// TB threads per block, NPT nodes per thread (node = block base + r * TB + thread:
+// every load instruction of a wave stays coalesced); all of a thread's row loads
+// are issued before its first evaluation.
+template <bool PLAIN, int TB, int NPT>
+__global__ __launch_bounds__(TB) void k_score_sweep(Conf cf, NodeCols nc, DevTables t, TaskClass c,
+                                                    const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts) {
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    const int n0 = blockIdx.x * TB * NPT + threadIdx.x;
+    uint32_t cnt = 0;
+    if constexpr (PLAIN && NPT > 1) {
+        Row r[NPT];
+        uint8_t fl[NPT];
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) {
+            const int n = n0 + q * TB;
+            if (n < nc.n) { fl[q] = nc.flags[n]; r[q] = load_row(nc, n); }
+        }
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) {
+            const int n = n0 + q * TB;
+            bool passed = false;
+            if (n < nc.n) {
+                uint64_t pw[4] = {0, 0, 0, 0};
+                if (c.has_ports)
+                    for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
+                const bool st = static_pred_f(cf, c, t, nc, n, fl[q]);
+                const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+                int32_t s = 0;
+                (void)dyn_key(cf, c, t, nc, r[q], pw, n, st, na, &s, &passed);
+                keys[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
+            }
+            cnt += (uint32_t)__popcll(__ballot(passed));
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) {
+            const int n = n0 + q * TB;
+            bool passed = false;
+            if (n < nc.n) {
+                int32_t s = 0;
+                if constexpr (PLAIN) (void)eval_node(cf, c, t, nc, n, &s, &passed);
+                else (void)eval_node_aff(cf, c, t, nc, n, ctrl->ipa_lo[0], ctrl->ipa_hi[0], ctrl->fallback, &s, &passed);
+                keys[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
+            }
+            cnt += (uint32_t)__popcll(__ballot(passed));
+        }
+    }
+    __syncthreads();  // s_cnt zeroed
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cnt) atomicAdd(&counts[(blockIdx.x % kSweepGroups) * 32], s_cnt);
+}
+
+// variant (option "sweep_variant", a tuning knob): 0 = 256 threads x 1 node,
+// 1 = 512 x 1, 2 = 256 x 2, 3 = 256 x 4
+static int g_sweep_variant = 0;
+void set_sweep_variant(int v) { g_sweep_variant = v; }
+template <int TB, int NPT>
+static void launch_sweep_t(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                           const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts, hipStream_t st) {
+    const int per = TB * NPT;
+    const int grid = nc.n > 0 ? (nc.n + per - 1) / per : 1;
+    if (!c.aff && c.ipa_n == 0)
+        hipLaunchKernelGGL((k_score_sweep<true, TB, NPT>), dim3(grid), dim3(TB), 0, st, cf, nc, t, c, ctrl, keys, counts);
+    else
+        hipLaunchKernelGGL((k_score_sweep<false, TB, NPT>), dim3(grid), dim3(TB), 0, st, cf, nc, t, c, ctrl, keys,
+                           counts);
+}
+hipError_t launch_score_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                              const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts, hipStream_t st) {
+    switch (g_sweep_variant) {
+        case 1: launch_sweep_t<512, 1>(cf, nc, t, c, ctrl, keys, counts, st); break;
+        case 2: launch_sweep_t<256, 2>(cf, nc, t, c, ctrl, keys, counts, st); break;
+        case 3: launch_sweep_t<256, 4>(cf, nc, t, c, ctrl, keys, counts, st); break;
+        default: launch_sweep_t<256, 1>(cf, nc, t, c, ctrl, keys, counts, st); break;
+    }
+    return hipGetLastError();
+}
+
 // One node-row update of a reclaim / preempt operation, in one lane:
 //   op 0 evict       NodeInfo.UpdateTask Running -> Releasing: Releasing += Resreq
 //                    (node_info.go:147-185; Idle / Used / Backfilled net unchanged)

@@ -42,6 +42,11 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 // ctrl->cls[0] (by_score 1: predicates + score, preempt; 0: predicates only,
 // reclaim), *count += passing nodes; one node-row update (op 0 evict, 1
 // pipeline, 2 unpipeline).
+// kbhip_sweep_scores' standalone sweep: keys per node, the passing count in
+// 8 counters (counts[32 g], g = 0..7; the caller zeroes and sums them).
+void set_sweep_variant(int v);  // option "sweep_variant" (process-wide tuning knob)
+hipError_t launch_score_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                              const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts, hipStream_t st);
 hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
                              int by_score, uint64_t* keys, uint32_t* count, hipStream_t st);
 // Wide score ranges: the passing keys of launch_rank_nodes (n keys, zeros
@@ -135,10 +140,10 @@ struct PopLink {
 // holds (blocks + kMaxGroups) * 64 keys, arrive (3 * kMaxGroups + 1) * 32
 // counters, both private to the launch's stream; fit_set alternates per
 // launch on a stream (FitDelta counter sets).
-hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                               uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set, int dep, uint32_t msg_from);
+hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, const TaskClass& cl,
+                               int n_tasks, int gang_mode, int min_avail, int ready_count, uint32_t epoch,
+                               uint64_t* cand, uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf,
+                               PopLink* link, uint32_t seq, int fit_set, int dep, uint32_t msg_from);
 // Node updates of given placements again (after launch_undo_pop).
 hipError_t launch_redo_pop(const NodeCols& nc, const DevTables& t, int cls, int n, const int32_t* node,
                            const int32_t* kind, hipStream_t st);

@@ -536,10 +536,14 @@ __device__ __forceinline__ bool poll_done(const uint32_t* p, uint32_t want) {
     return false;
 }
 
+// The pop's task class comes by value in the kernel arguments (cl = the
+// session's classes[a.cls]): the sweep's row loads wait for no dependent load
+// of the class record.
 template <int R, typename KT>
 __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                              uint64_t* cand64, uint32_t* arrive, PopOut* out,
-                                                              PopLink* link, uint32_t seq, int dep, uint32_t msg_from) {
+                                                              TaskClass cl, uint64_t* cand64, uint32_t* arrive,
+                                                              PopOut* out, PopLink* link, uint32_t seq, int dep,
+                                                              uint32_t msg_from) {
     __shared__ KT wlk[kPopThreads / 64][64];               // sweep / merge lists in the key type
     __shared__ uint64_t wl[kPopThreads / 64][64];          // placement lists (64-bit keys / entries)
     __shared__ uint32_t s_skip[R * kPopThreads / 32];      // this block's nodes among pop seq-1's (and seq-2's) candidates
@@ -560,7 +564,7 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
     STAMP(blockIdx.x * 4 + 0);
     if (blockIdx.x == 0 && threadIdx.x == 0) TL(seq, 0);
     if (threadIdx.x == 0) TLB(seq, 0);
-    const TaskClass c = t.classes[a.cls];
+    const TaskClass& c = cl;
     const int base = blockIdx.x * R * kPopThreads;
     // pop seq-1 (and with dep 2 pop seq-2) may still be writing rows: their
     // candidates, in flight while the rows below load
@@ -1396,11 +1400,11 @@ hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTable
 
 template <typename KT>
 static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
-                                  const PopArgs& a, uint64_t* cand, uint32_t* arrive, PopOut* o, PopLink* link,
-                                  uint32_t seq, int dep, uint32_t msg_from, hipStream_t st) {
+                                  const PopArgs& a, const TaskClass& cl, uint64_t* cand, uint32_t* arrive, PopOut* o,
+                                  PopLink* link, uint32_t seq, int dep, uint32_t msg_from, hipStream_t st) {
 #define KBHIP_OV(RR)                                                                                              \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cand, arrive, o, \
-                       link, seq, dep, msg_from)
+    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cl, cand, arrive, \
+                       o, link, seq, dep, msg_from)
     switch (R) {
         case 1: KBHIP_OV(1); break;
         case 2: KBHIP_OV(2); break;
@@ -1411,18 +1415,18 @@ static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols&
 #undef KBHIP_OV
 }
 
-hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, uint64_t* cand,
-                               uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf, PopLink* link,
-                               uint32_t seq, int fit_set, int dep, uint32_t msg_from) {
+hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, const TaskClass& cl,
+                               int n_tasks, int gang_mode, int min_avail, int ready_count, uint32_t epoch,
+                               uint64_t* cand, uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf,
+                               PopLink* link, uint32_t seq, int fit_set, int dep, uint32_t msg_from) {
     if (seq < 1 || dep < 1 || dep > kMaxDep) return hipErrorInvalidValue;
     int R;
     const int nb = pop_blocks(nc.n, &R);
     PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
               kf.use32 && kf.ent32 ? 1 : 0, fit_set};
     PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, msg_from, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cand, arrive, o, link, seq, dep, msg_from, st);
+    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cl, cand, arrive, o, link, seq, dep, msg_from, st);
+    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cl, cand, arrive, o, link, seq, dep, msg_from, st);
     return hipGetLastError();
 }
 

@@ -121,18 +121,25 @@ struct HPod {
     bool backfill = false;
     bool critical = false;  // kube-system namespace or a system-*-critical priority class (conformance.go:40-45)
     bool node_rel = false;  // the node's copy stays Releasing after an unevict (statement.go:81-105)
+    bool groupless = false; // no PodGroup: a shadow job of its own (cache/util.go:42-60)
+    bool detached = false;  // the cache deleted this group-less pod: it keeps its shadow job, status and
+                            // NodeName but is off the node (deletePod, event_handlers.go:119-165; kbsnap.h p_detached)
     R3 req, ireq;
     int64_t nzc = 0, nzm = 0;  // GetNonzeroRequests (kbhip_session_carry recomputes node rows from them)
     int job = -1;   // session job slot
     int cls = -1;   // device task class (pending tasks)
     int node = -1;  // current node
 };
+// The pod is in its node's task list (NodeInfo.Tasks): bound, not terminated
+// (cache addTask, event_handlers.go:63-79), not taken off by a deletePod.
+static inline bool on_node_of(const HPod& p) {
+    return p.node >= 0 && !p.detached && p.status != Succeeded && p.status != Failed;
+}
 struct HJob {  // session jobs are numbered in UID order
     int queue = -1;
     int32_t min_avail = 0, priority = 0;
     int32_t pg_priority = 0;  // the PodGroup's priority before any task's (JobInfo.SetPodGroup)
     bool shadow = false;      // shadow PodGroup of a group-less pod (cache/util.go:42-60)
-    bool gone = false;        // a shadow job whose pod was deleted between sessions: not in the cache
     int64_t ts = 0;
     vector<int> tasks;
     vector<int> pending;  // pending non-BestEffort tasks in TaskOrderFn order (built at first pop)
@@ -426,6 +433,19 @@ struct BatchLaunch {
 // A job pop submitted through the asynchronous per-pop ABI
 // (kbhip_place_job_submit): launched at submit time when it is one batched
 // chunk and nothing deferred is ahead of it, else run at its wait.
+// What kbhip_session_carry_snapshot's fast path keeps from the open: the
+// dictionaries and class table a new pod's class is compiled against, and
+// digests of the snapshot parts it does not re-derive (conf, node labels and
+// taints).  Filled at the end of open_session.
+struct CarryKeep {
+    bool ok = false;                                     // a one-GPU session without pod affinity
+    std::unordered_map<string, int> class_ids;           // class signature -> class
+    vector<uint64_t> masks;                              // host copy of DevTables::masks
+    vector<std::tuple<string, string, string>> taint_defs;  // taint ids (key, value, effect)
+    Dict nss;                                            // namespace ids
+    uint64_t conf_digest = 0, node_spec_digest = 0;
+};
+
 struct PopTicket {
     int64_t id = 0;
     bool launched = false;
@@ -455,6 +475,7 @@ struct Session {
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
     DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt, b_rank_radix;
     DevBuf b_tab_idx;  // count-table deltas (flush_tables)
+    DevBuf b_sweep_cnt;  // kbhip_sweep_scores' passing counts (8 counters, one 128-B line each)
     size_t rank_tmp_bytes = 0;
     uint64_t* h_rank = nullptr;  // pinned: [0] = count, then sorted keys
     size_t h_rank_cap = 0;
@@ -472,6 +493,7 @@ struct Session {
     int32_t fallback = -1;  // lowest node index holding a session-placed pod (nodeorder.go:78-93)
     vector<int32_t> sess_cnt;  // per node: session-placed pods on it (fallback after an unpipeline)
     std::unique_ptr<AffinityModel> aff;       // pod (anti-)affinity model (kept for evictions / carry)
+    CarryKeep keep;                           // kbhip_session_carry_snapshot's fast path
     std::map<int64_t, int32_t> tab_delta;     // pending count-table changes: idx >= 0 cnt, < 0 scalar (-1 - idx)
     // device
     Conf conf{};
@@ -621,7 +643,7 @@ struct Session {
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
                           &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt,
                           &b_rank_radix,
-                          &b_shard_send, &b_shard_recv, &b_tab_idx})
+                          &b_shard_send, &b_shard_recv, &b_tab_idx, &b_sweep_cnt})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -698,6 +720,86 @@ struct PortRuns {
     const vector<int32_t>& ids;
     PortRun operator[](int i) const { return {ids.data() + off[i], ids.data() + off[i + 1]}; }
 };
+
+// 32-bit selection keys per class (PopArgs, kbhip_kernels.hip): the score
+// of a batched-path class is mult x (w_lr lr + w_bra bra + w_na na) with
+// lr, bra in [0, 10] and na between the sums of its negative / positive
+// preferred-term weights; it fits when (range + 1) < 2^(31 - index bits).
+static void class_key_format(const Session& S, const TaskClass& c, const vector<Term>& terms, int N, KeyFormat* kf_out,
+                             std::pair<int64_t, int64_t>* range_out) {
+    int ibits = 1;  // keys carry global node indices (shards too)
+    while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)N) ++ibits;
+    int64_t na_lo = 0, na_hi = 0;
+    for (int i = 0; i < c.pref_term_n; ++i) {
+        const int64_t w = terms[c.pref_term_off + i].weight;
+        (w < 0 ? na_lo : na_hi) += w;
+    }
+    const int64_t mult = S.conf.score_mult;
+    auto rng = [](int64_t a, int64_t b, int64_t* lo, int64_t* hi) {
+        *lo += std::min(a, b);
+        *hi += std::max(a, b);
+    };
+    int64_t lo = 0, hi = 0;
+    rng(0, 10 * (int64_t)S.conf.w_lr, &lo, &hi);
+    rng(0, 10 * (int64_t)S.conf.w_bra, &lo, &hi);
+    rng(na_lo * S.conf.w_na, na_hi * S.conf.w_na, &lo, &hi);
+    const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
+    *range_out = {slo, shi};
+    {  // nodeorder.go:287-313 sums in Go's 64-bit int; the kernels' score is int32 (kbhip_eval.h
+       // node_score): sessions whose score range (with the inter-pod term) leaves int32 are refused
+        int64_t flo = lo, fhi = hi;
+        rng(0, 10 * (int64_t)S.conf.w_pa, &flo, &fhi);
+        const int64_t a = flo * mult, b = fhi * mult;
+        if (std::min(a, b) < INT32_MIN || std::max(a, b) > INT32_MAX)
+            fail_unsupported("nodeorder score range leaves int32 (weights x terms x tiers)");
+    }
+    KeyFormat& kf = *kf_out;
+    kf = KeyFormat{};
+    kf.use32 = ibits <= 25 && shi - slo + 1 < ((int64_t)1 << (31 - ibits)) && slo >= INT32_MIN && shi <= INT32_MAX;
+    kf.ent32 = kf.use32 && ibits <= 24 && shi - slo + 1 < ((int64_t)1 << (26 - ibits));
+    kf.base = (int32_t)slo;
+    kf.shift = ibits + 1;
+    kf.idxmax = (int32_t)(((int64_t)1 << ibits) - 1);
+}
+
+// FNV-1a digests of the snapshot parts kbhip_session_carry_snapshot's fast
+// path takes over unchanged: the conf sections, and every node's labels and
+// taints (as strings, in node order).
+static uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) { h ^= b[i]; h *= 1099511628211ULL; }
+    return h;
+}
+static uint64_t fnv_str(uint64_t h, const char* z) { return fnv(h, z, std::strlen(z) + 1); }
+static uint64_t conf_digest(const kbs::Snapshot& s) {
+    uint64_t h = 1469598103934665603ULL;
+    for (const char* n : {"conf_plugin_name", "conf_arg_key", "conf_arg_val", "conf_actions"})
+        for (int32_t o : s.vec<int32_t>(n)) h = fnv_str(h, s.str(o));
+    for (const char* n : {"conf_plugin_tier", "conf_plugin_flags", "conf_arg_plugin"}) {
+        auto v = s.vec<int32_t>(n);
+        h = fnv(h, v.data(), v.size() * sizeof(int32_t));
+        h = fnv(h, "|", 1);
+    }
+    return h;
+}
+static uint64_t node_spec_digest(const kbs::Snapshot& s) {
+    uint64_t h = 1469598103934665603ULL;
+    const size_t N = s.rows("n_name");
+    auto loff = s.offs("n_label_off", N), toff = s.offs("n_taint_off", N);
+    auto lk = s.span<int32_t>("nl_key"), lv = s.span<int32_t>("nl_val");
+    auto tk = s.span<int32_t>("nt_key"), tv = s.span<int32_t>("nt_val"), te = s.span<int32_t>("nt_effect");
+    for (size_t i = 0; i < N; ++i) {
+        for (int k = loff[i]; k < loff[i + 1]; ++k) { h = fnv_str(h, s.str(lk[k])); h = fnv_str(h, s.str(lv[k])); }
+        h = fnv(h, "|", 1);
+        for (int k = toff[i]; k < toff[i + 1]; ++k) {
+            h = fnv_str(h, s.str(tk[k]));
+            h = fnv_str(h, s.str(tv[k]));
+            h = fnv_str(h, s.str(te[k]));
+        }
+        h = fnv(h, "#", 1);
+    }
+    return h;
+}
 
 static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
                          int world = 1) {
@@ -842,6 +944,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     auto pphase = s.span<uint8_t>("p_phase"), pdel = s.span<uint8_t>("p_deleting"), pbf = s.span<uint8_t>("p_backfill");
     auto pts = s.span<int64_t>("p_ts");
     auto ppc = s.span<int32_t>("p_pclass");  // optional: Spec.PriorityClassName
+    auto pdet = s.span<uint8_t>("p_detached");  // optional: group-less pods the cache took off their node
     if ((int)pns.size() != P || (int)pjob.size() != P || (int)pnode.size() != P || (int)ppri.size() != P ||
         (int)pphase.size() != P || (int)pts.size() != P)
         throw Error(KBHIP_EINVAL, "pod columns length mismatch");
@@ -919,6 +1022,8 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                              std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
             }
             p.backfill = !pbf.empty() && pbf[i];
+            p.groupless = pjob[i] < 0;
+            p.detached = has_node && !pdet.empty() && pdet[i];
             for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
                 p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
                 p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
@@ -1074,7 +1179,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             a.ns = p.ns;
             a.status = p.status;
             a.session_job = slot >= 0;
-            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
+            const bool on_node = on_node_of(p);
             a.node = on_node ? p.node : -1;
             a.target = a.session_job && allocated_status(p.status) && on_node;
             a.pending = a.session_job && p.status == Pending;
@@ -1094,7 +1199,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 S.pod_port_ids.push_back(id);
             }
         }
-        if (p.node >= 0 && p.status != Succeeded && p.status != Failed) {  // cache addTask -> NodeInfo.AddTask
+        if (on_node_of(p)) {  // cache addTask -> NodeInfo.AddTask
             int n = p.node;
             if (p.backfill) { bf[n].c += p.req.c; bf[n].m += p.req.m; bf[n].g += p.req.g; }
             if (p.status == Releasing) {
@@ -1142,6 +1247,9 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         } catch (const std::invalid_argument& e) {
             fail_unsupported(e.what());
         }
+        if (aff.active)  // the predicate lister's NodeInfo.Filter leaves such a pod out at its own node only
+            for (int i = 0; i < P; ++i)
+                if (S.pods[i].detached) fail_unsupported("detached pods (p_detached) in a session with pod (anti-)affinity");
     }
     vector<int32_t> aff_items;
 
@@ -1524,49 +1632,11 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     vector<int64_t> valint(E.vals.strs.size() + 1, 0);
     vector<uint8_t> valok(E.vals.strs.size() + 1, 0);
     for (size_t v = 0; v < E.vals.strs.size(); ++v) valok[v] = parse_int64(E.vals.strs[v], &valint[v]);
-    // 32-bit selection keys per class (PopArgs, kbhip_kernels.hip): the score
-    // of a batched-path class is mult x (w_lr lr + w_bra bra + w_na na) with
-    // lr, bra in [0, 10] and na between the sums of its negative / positive
-    // preferred-term weights; it fits when (range + 1) < 2^(31 - index bits).
-    {
-        int ibits = 1;  // keys carry global node indices (shards too)
-        while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)N) ++ibits;
-        S.class_kf.assign(S.classes.size(), KeyFormat{});
-        S.class_srange.assign(S.classes.size(), {0, 0});
-        for (size_t ci = 0; ci < S.classes.size(); ++ci) {
-            const TaskClass& c = S.classes[ci];
-            int64_t na_lo = 0, na_hi = 0;
-            for (int i = 0; i < c.pref_term_n; ++i) {
-                const int64_t w = E.terms[c.pref_term_off + i].weight;
-                (w < 0 ? na_lo : na_hi) += w;
-            }
-            const int64_t mult = S.conf.score_mult;
-            auto rng = [](int64_t a, int64_t b, int64_t* lo, int64_t* hi) {
-                *lo += std::min(a, b);
-                *hi += std::max(a, b);
-            };
-            int64_t lo = 0, hi = 0;
-            rng(0, 10 * (int64_t)S.conf.w_lr, &lo, &hi);
-            rng(0, 10 * (int64_t)S.conf.w_bra, &lo, &hi);
-            rng(na_lo * S.conf.w_na, na_hi * S.conf.w_na, &lo, &hi);
-            const int64_t slo = std::min(lo * mult, hi * mult), shi = std::max(lo * mult, hi * mult);
-            S.class_srange[ci] = {slo, shi};
-            {  // nodeorder.go:287-313 sums in Go's 64-bit int; the kernels' score is int32 (kbhip_eval.h
-               // node_score): sessions whose score range (with the inter-pod term) leaves int32 are refused
-                int64_t flo = lo, fhi = hi;
-                rng(0, 10 * (int64_t)S.conf.w_pa, &flo, &fhi);
-                const int64_t a = flo * mult, b = fhi * mult;
-                if (std::min(a, b) < INT32_MIN || std::max(a, b) > INT32_MAX)
-                    fail_unsupported("nodeorder score range leaves int32 (weights x terms x tiers)");
-            }
-            KeyFormat& kf = S.class_kf[ci];
-            kf.use32 = ibits <= 25 && shi - slo + 1 < ((int64_t)1 << (31 - ibits)) && slo >= INT32_MIN && shi <= INT32_MAX;
-            kf.ent32 = kf.use32 && ibits <= 24 && shi - slo + 1 < ((int64_t)1 << (26 - ibits));
-            kf.base = (int32_t)slo;
-            kf.shift = ibits + 1;
-            kf.idxmax = (int32_t)(((int64_t)1 << ibits) - 1);
-        }
-    }
+    // 32-bit selection keys per class (class_key_format)
+    S.class_kf.assign(S.classes.size(), KeyFormat{});
+    S.class_srange.assign(S.classes.size(), {0, 0});
+    for (size_t ci = 0; ci < S.classes.size(); ++ci)
+        class_key_format(S, S.classes[ci], E.terms, N, &S.class_kf[ci], &S.class_srange[ci]);
     S.tab.classes = upload(S, S.b_classes, S.classes);
     S.tab.terms = upload(S, S.b_terms, E.terms);
     S.tab.reqs = upload(S, S.b_reqs, E.reqs);
@@ -1620,6 +1690,16 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     }
     HIPCHK(hipStreamSynchronize(st));
     mark("upload");
+    // ---------------- kbhip_session_carry_snapshot's fast path ----------------
+    S.keep.ok = S.world == 1 && !aff.active;
+    if (S.keep.ok) {
+        S.keep.class_ids = std::move(class_ids);
+        S.keep.masks = E.masks;
+        S.keep.taint_defs = E.taint_defs;
+        S.keep.nss = E.nss;
+        S.keep.conf_digest = conf_digest(s);
+        S.keep.node_spec_digest = node_spec_digest(s);
+    }
     // ---------------- ordering plugins OnSessionOpen ----------------
     for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
     S.stats.nodes = N;
@@ -2129,7 +2209,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
         HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
                                   S.d_shard_recv, S.world, out, S.stream));
     } else if (ov) {
-        HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch,
+        HIPCHK(launch_pop_batch_ov(S.conf, S.nc, S.tab, cls, S.classes[cls], m, gang_mode, min_avail, ready_count, L.epoch,
                                    S.d_cand_ov[si], S.d_arrive_ov[si], out, L.st, kf, S.d_link, seq, S.fit_set[si],
                                    S.overlap, S.msg_from));
         S.fit_set[si] ^= 1;
@@ -2783,13 +2863,11 @@ struct Allocator {
         S.plugins_opened = true;
         if (S.drf_on)
             for (auto& j : S.jobs) {  // drf.go:65-82
-                if (j.gone) continue;
                 for (int t : j.tasks) if (allocated_status(S.pods[t].status)) j.drf_alloc.add(S.pods[t].req);
                 drf_update(j);
             }
         if (S.prop_on) {  // proportion.go:65-142
             for (auto& j : S.jobs) {
-                if (j.gone) continue;
                 HQueue& q = S.queues[j.queue];
                 q.has_attr = true;
                 for (int t : j.tasks) {
@@ -2850,7 +2928,6 @@ struct Allocator {
         std::map<int, JobQueue<decltype(jl)>> jobs_map;
         for (size_t j = 0; j < S.jobs.size(); ++j) {
             const HJob& job = S.jobs[j];
-            if (job.gone) continue;
             int q = job.queue;
             queues.push(q);
             auto it = jobs_map.find(q);
@@ -3220,7 +3297,7 @@ struct Allocator {
         S.node_tasks.assign(S.nc.n, {});
         for (int i = 0; i < (int)S.pods.size(); ++i) {
             const HPod& p = S.pods[i];
-            if (p.node < 0 || p.status == Succeeded || p.status == Failed || p.status == Pending) continue;
+            if (!on_node_of(p) || p.status == Pending) continue;
             S.node_tasks[p.node].push_back(i);
         }
     }
@@ -3512,7 +3589,6 @@ struct Allocator {
         vector<char> seen(S.queues.size(), 0);
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
-            if (j.gone) continue;
             seen[j.queue] = 1;
             vector<int> pend = pending_sorted(j);
             if (pend.empty()) continue;
@@ -3583,7 +3659,6 @@ struct Allocator {
         std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
-            if (j.gone) continue;
             if (!qseen[j.queue]) { qseen[j.queue] = 1; queues.push(j.queue); }
             vector<int> pend = pending_sorted(j);
             if (pend.empty()) continue;
@@ -3729,19 +3804,21 @@ static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
         S.b_rank_keys.alloc<uint64_t>(std::max(N, 1));
         S.b_rank_cnt.alloc<uint32_t>(4);
     }
+    if (!S.b_sweep_cnt.p) S.b_sweep_cnt.alloc<uint32_t>(8 * 32);
     ctrl_setup(S, 1, &cls, 0, 0, 0, 0, -1, 0);
-    if (S.classes[cls].ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
-    HIPCHK(hipMemsetAsync(S.b_rank_cnt.p, 0, sizeof(uint32_t), S.stream));
+    const TaskClass& c = S.classes[cls];
+    if (c.ipa_n > 0) HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
+    HIPCHK(hipMemsetAsync(S.b_sweep_cnt.p, 0, 8 * 32 * sizeof(uint32_t), S.stream));
     const bool timed = S.time_every > 0;  // the standalone sweep's own duration (bench.py's sweep roofline)
     if (timed) {
         if (!S.ev_sweep[0]) { HIPCHK(hipEventCreate(&S.ev_sweep[0])); HIPCHK(hipEventCreate(&S.ev_sweep[1])); }
         HIPCHK(hipEventRecord(S.ev_sweep[0], S.stream));
     }
-    HIPCHK(launch_rank_nodes(S.conf, S.nc, S.tab, S.d_ctrl, 1, (uint64_t*)S.b_rank_keys.p, (uint32_t*)S.b_rank_cnt.p,
-                             S.stream));
+    HIPCHK(launch_score_sweep(S.conf, S.nc, S.tab, c, S.d_ctrl, (uint64_t*)S.b_rank_keys.p,
+                              (uint32_t*)S.b_sweep_cnt.p, S.stream));
     if (timed) HIPCHK(hipEventRecord(S.ev_sweep[1], S.stream));
-    uint32_t cnt = 0;
-    HIPCHK(hipMemcpyAsync(&cnt, S.b_rank_cnt.p, sizeof(uint32_t), hipMemcpyDeviceToHost, S.stream));
+    uint32_t cnt[8 * 32];
+    HIPCHK(hipMemcpyAsync(cnt, S.b_sweep_cnt.p, sizeof cnt, hipMemcpyDeviceToHost, S.stream));
     if (out_keys && N)
         HIPCHK(hipMemcpyAsync(out_keys, S.b_rank_keys.p, (size_t)N * sizeof(uint64_t), hipMemcpyDeviceToHost,
                               S.stream));
@@ -3753,7 +3830,52 @@ static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
         S.stats.score_sweeps++;
     }
     S.stats.sweeps++;
-    return (int)cnt;
+    uint32_t total = 0;
+    for (int g = 0; g < 8; ++g) total += cnt[32 * g];
+    return (int)total;
+}
+
+// kbhip_time_sweeps: the standalone sweep of each task, launched back to back
+// (no copies in between), one HIP-event pair around the whole sequence: the
+// device time per sweep launch, boundaries between launches included.
+static double time_sweeps(Session& S, const int32_t* ids, int n) {
+    if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "time_sweeps on a node-sharded session");
+    for (int i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= (int)S.pods.size() || S.pods[ids[i]].cls < 0)
+            throw Error(KBHIP_EINVAL, "task id has no task class (not a pending task of the session)");
+    bool any_ipa = false;
+    for (int i = 0; i < n; ++i) any_ipa |= S.classes[S.pods[ids[i]].cls].ipa_n > 0;
+    if (any_ipa) throw Error(KBHIP_EUNSUPPORTED, "time_sweeps: classes with inter-pod terms need their prepass");
+    ov_quiesce(S);
+    const int N = S.nc.n;
+    if (!S.b_rank_keys.p) {
+        S.b_rank_keys.alloc<uint64_t>(std::max(N, 1));
+        S.b_rank_cnt.alloc<uint32_t>(4);
+    }
+    if (!S.b_sweep_cnt.p) S.b_sweep_cnt.alloc<uint32_t>(8 * 32);
+    // one control block per task (the kernel reads its class from ctrl->cls[0])
+    DevBuf ctl;
+    vector<PopCtrl> h(n);
+    for (int i = 0; i < n; ++i) {
+        std::memset(&h[i], 0, sizeof(PopCtrl));
+        h[i].cls[0] = S.pods[ids[i]].cls;
+        h[i].fallback = -1;
+    }
+    PopCtrl* d = ctl.alloc<PopCtrl>(std::max(n, 1));
+    HIPCHK(hipMemcpyAsync(d, h.data(), (size_t)n * sizeof(PopCtrl), hipMemcpyHostToDevice, S.stream));
+    HIPCHK(hipMemsetAsync(S.b_sweep_cnt.p, 0, 8 * 32 * sizeof(uint32_t), S.stream));
+    if (!S.ev_sweep[0]) { HIPCHK(hipEventCreate(&S.ev_sweep[0])); HIPCHK(hipEventCreate(&S.ev_sweep[1])); }
+    HIPCHK(hipEventRecord(S.ev_sweep[0], S.stream));
+    for (int i = 0; i < n; ++i) {
+        HIPCHK(launch_score_sweep(S.conf, S.nc, S.tab, S.classes[h[i].cls[0]], d + i, (uint64_t*)S.b_rank_keys.p,
+                                  (uint32_t*)S.b_sweep_cnt.p, S.stream));
+    }
+    HIPCHK(hipEventRecord(S.ev_sweep[1], S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, S.ev_sweep[0], S.ev_sweep[1]));
+    ctl.release();
+    return n > 0 ? (double)ms * 1e3 / n : 0.0;
 }
 
 // JobInfo.FitError (job_info.go:343-372) from the histogram of the job's last walk.
@@ -3778,7 +3900,7 @@ static string gang_close_text(const Session& S) {
     string out;
     for (size_t i = 0; i < S.jobs.size(); ++i) {
         const HJob& j = S.jobs[i];
-        if (j.gone || j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
+        if (j.cnt_alloc >= j.min_avail) continue;  // JobInfo.GetReadiness() == Ready
         int ready = 0;                              // readyTaskNum (gang.go:212-222)
         bool backfill = false;
         for (int t : j.tasks) {
@@ -3997,6 +4119,17 @@ int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* 
     })
 }
 
+int kbhip_time_sweeps(kb_session* s, const int32_t* task_ids, int32_t n, double* out_mean_us) {
+    ABI_GUARD_S(s, {
+        if (!s || (!task_ids && n) || n < 0 || !out_mean_us) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        *out_mean_us = kbhip::time_sweeps(s->s, task_ids, n);
+        return KBHIP_OK;
+    })
+}
+
 int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
     ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
@@ -4019,23 +4152,30 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // GetAccessibleResource inflation of Idle — and only rows that changed are
 // uploaded (contiguous runs); jobs, queues and plugin state are re-derived as
 // at open.  Cache events of existing pods between the sessions follow
-// (event_handlers.go): deletePod -> deleteTask (the pod leaves its job and
-// its node; a shadow job left without pods leaves the cache), updatePod to
+// (event_handlers.go): deletePod -> deleteTask on NewTaskInfo(pod) — a pod of
+// a PodGroup leaves its job and its node; a group-less pod's TaskInfo has an
+// empty Job, so it stays in its shadow job with its status and NodeName and
+// only its node drops it (detached); no job is deleted — and updatePod to
 // Succeeded / Failed (isTerminated: the task stays in its job, off its node).
-// New pods and node changes need a snapshot (kbhip_session_open).
+// New pods, node and PodGroup changes: kbhip_session_carry_snapshot.
 static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0) {
     // every node's row is recomputed on the host (a shard's host model holds
     // all of them); this device's rows [lo, lo + Nl) are compared and uploaded
     const int N = (int)S.h_alloc.size(), Nl = S.nc.n, lo = S.nc.base, P = (int)S.pods.size();
     {  // validate the events before anything changes
         vector<char> gone(P, 0);
+        const bool aff = S.aff && S.aff->active;
         for (int64_t k = 0; k < n_ev; ++k) {
             const int32_t i = ev_pod[k];
             if (i < 0 || i >= P) throw Error(KBHIP_EINVAL, "event pod index out of range");
             if (ev[k] != KBHIP_EV_DELETE && ev[k] != KBHIP_EV_SUCCEEDED && ev[k] != KBHIP_EV_FAILED)
                 throw Error(KBHIP_EINVAL, "unknown cache event");
-            if (gone[i] || S.pods[i].status == Gone) throw Error(KBHIP_EINVAL, "event on a deleted pod");
+            if (gone[i] || S.pods[i].status == Gone || S.pods[i].detached)
+                throw Error(KBHIP_EINVAL, "event on a deleted pod");
             if (ev[k] == KBHIP_EV_DELETE) gone[i] = 1;
+            if (aff && ev[k] == KBHIP_EV_DELETE && S.pods[i].groupless && S.pods[i].node >= 0)
+                throw Error(KBHIP_EUNSUPPORTED, "deleting a bound group-less pod (it stays in its shadow job, "
+                                                "detached) in a session with pod (anti-)affinity");
         }
     }
     ov_quiesce(S);
@@ -4048,22 +4188,34 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     }
     if (n_ev > 0) {
         vector<char> del(P, 0);
+        bool any_del = false;
         for (int64_t k = 0; k < n_ev; ++k) {
             HPod& p = S.pods[ev_pod[k]];
             if (ev[k] == KBHIP_EV_DELETE) {
-                p.status = Gone;
-                p.node = -1;
-                del[ev_pod[k]] = 1;
+                // deletePod -> deleteTask on NewTaskInfo(pod) (event_handlers.go:119-165).  A pod of a
+                // PodGroup leaves its job (JobInfo.DeleteTaskInfo) and its node.  A group-less pod's
+                // TaskInfo has an empty Job (job_info.go:60-70): its shadow job keeps the task with
+                // its status and NodeName, only the node drops it (a pending or terminated one is on
+                // no node: nothing changes).  No job is ever deleted (JobTerminated needs a nil
+                // PodGroup, job_info.go / event_handlers.go:165-168).
+                if (p.groupless) {
+                    if (on_node_of(p)) p.detached = true;
+                } else {
+                    p.status = Gone;
+                    p.node = -1;
+                    del[ev_pod[k]] = 1;
+                    any_del = true;
+                }
             } else {
                 p.status = ev[k] == KBHIP_EV_SUCCEEDED ? Succeeded : Failed;  // keeps its NodeName
             }
         }
-        for (auto& j : S.jobs) {  // JobInfo.DeleteTaskInfo
-            size_t w = 0;
-            for (int t : j.tasks) if (!del[t]) j.tasks[w++] = t;
-            j.tasks.resize(w);
-            if (j.shadow && j.tasks.empty()) j.gone = true;
-        }
+        if (any_del)
+            for (auto& j : S.jobs) {  // JobInfo.DeleteTaskInfo
+                size_t w = 0;
+                for (int t : j.tasks) if (!del[t]) j.tasks[w++] = t;
+                j.tasks.resize(w);
+            }
     }
     vector<int64_t> col[9];
     for (auto& c : col) c.assign(N, 0);
@@ -4075,7 +4227,7 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     S.any_bf = 0;
     for (int i = 0; i < P; ++i) {  // cache addTask -> NodeInfo.AddTask, as at open
         const HPod& p = S.pods[i];
-        if (p.node < 0 || p.status == Succeeded || p.status == Failed) continue;
+        if (!on_node_of(p)) continue;
         const int n = p.node;
         if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
         if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
@@ -4149,7 +4301,7 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
             a.ns = p.ns;
             a.status = p.status;
             a.session_job = p.job >= 0;
-            const bool on_node = p.node >= 0 && p.status != Succeeded && p.status != Failed;
+            const bool on_node = on_node_of(p);
             a.node = on_node ? p.node : -1;
             a.target = a.session_job && allocated_status(p.status) && on_node;
             a.pending = a.session_job && p.status == Pending;
@@ -4168,6 +4320,439 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     S.node_tasks.clear();
     S.log.clear();
     S.last_fit_ok = false;
+}
+
+// ---------------------------------------------------------------------------
+// kbhip_session_carry_snapshot: the next session from the
+// scheduler cache's snapshot of it (cache.go:515-583) — pod arrivals, deletions
+// and phase changes, node updates, PodGroup and queue changes — re-deriving
+// only what the changes touch.  old_pod[i] / old_node[n]: the index in this
+// session of the new snapshot's pod i / node n (-1: new).  Fast path (the
+// common shape: same node set, same labels / taints / conf, no pod affinity,
+// new pods without host ports, nodeSelector or node affinity): mapped pods
+// keep their dictionary ids, ports and task class; new pods are decoded and
+// classed against the kept dictionaries; jobs, queues and node rows are
+// re-derived; only changed node rows and the grown tables are uploaded.
+// Anything else re-opens the session in place (same handle and options).
+// ---------------------------------------------------------------------------
+struct SavedOptions {
+    bool batched, keys32, bf_batch, aff_batch, rank_group, force_radix, debug_keys;
+    int64_t time_every;
+    int speculate, overlap, rank_first;
+};
+static SavedOptions save_options(const Session& S) {
+    return SavedOptions{S.batched, S.keys32, S.bf_batch, S.aff_batch, S.rank_group, S.force_radix, S.debug_keys,
+                        S.time_every, S.speculate, S.overlap, S.rank_first};
+}
+static void restore_options(Session& S, const SavedOptions& o) {
+    S.batched = o.batched; S.keys32 = o.keys32; S.bf_batch = o.bf_batch; S.aff_batch = o.aff_batch;
+    S.rank_group = o.rank_group; S.force_radix = o.force_radix; S.time_every = o.time_every;
+    S.speculate = o.speculate; S.overlap = o.overlap; S.rank_first = o.rank_first;
+    S.debug_keys = o.debug_keys;
+    if (S.debug_keys && !S.d_dbg && !S.encode_only)
+        S.d_dbg = S.b_dbg.alloc<uint64_t>((size_t)kMaxChunk * (2 * S.nc.npad + 4));
+}
+
+// pass A of open_session for one pod (status, priority, requests, node)
+struct PodView {
+    const kbs::Snapshot& s;
+    kbs::Snapshot::Span<int32_t> puid, pns, pjob, pnode, ppri, paff, ppc;
+    kbs::Snapshot::Span<uint8_t> pphase, pdel, pbf, pdet;
+    kbs::Snapshot::Span<int64_t> pts;
+    vector<int32_t> pco, pio, pso, pto, cpo;
+    kbs::Snapshot::Span<int64_t> ccpu, cmem, cgpu, iccpu, icmem, icgpu;
+    kbs::Snapshot::Span<uint8_t> chas;
+    int P;
+    explicit PodView(const kbs::Snapshot& s_) : s(s_) {
+        puid = s.span<int32_t>("p_uid");
+        P = (int)puid.size();
+        pns = s.span<int32_t>("p_ns"); pjob = s.span<int32_t>("p_job"); pnode = s.span<int32_t>("p_node");
+        ppri = s.span<int32_t>("p_priority"); paff = s.span<int32_t>("p_aff"); ppc = s.span<int32_t>("p_pclass");
+        pphase = s.span<uint8_t>("p_phase"); pdel = s.span<uint8_t>("p_deleting"); pbf = s.span<uint8_t>("p_backfill");
+        pdet = s.span<uint8_t>("p_detached");
+        pts = s.span<int64_t>("p_ts");
+        if ((int)pns.size() != P || (int)pjob.size() != P || (int)pnode.size() != P || (int)ppri.size() != P ||
+            (int)pphase.size() != P || (int)pts.size() != P)
+            throw Error(KBHIP_EINVAL, "pod columns length mismatch");
+        pco = s.offs("p_ctr_off", P);
+        pio = s.offs("p_ictr_off", P);
+        pso = s.offs("p_nsel_off", P);
+        pto = s.offs("p_tol_off", P);
+        ccpu = s.span<int64_t>("c_cpu"); cmem = s.span<int64_t>("c_mem"); cgpu = s.span<int64_t>("c_gpu");
+        chas = s.span<uint8_t>("c_has");
+        cpo = s.offs("c_port_off", ccpu.size());
+        iccpu = s.span<int64_t>("ic_cpu"); icmem = s.span<int64_t>("ic_mem"); icgpu = s.span<int64_t>("ic_gpu");
+    }
+    bool has_node(int i) const { return pnode[i] >= 0 && s.str(pnode[i])[0] != '\0'; }
+    int status(int i) const {  // api/helpers.go:35-61
+        const int ph = pphase[i];
+        const bool del = !pdel.empty() && pdel[i];
+        if (ph == KBS_RUNNING) return del ? Releasing : Running;
+        if (ph == KBS_PENDING) return del ? Releasing : (!has_node(i) ? Pending : Bound);
+        if (ph == KBS_SUCCEEDED) return Succeeded;
+        if (ph == KBS_FAILED) return Failed;
+        return Unknown;
+    }
+    bool has_ports(int i) const {
+        for (int k = pco[i]; k < pco[i + 1]; ++k)
+            if (cpo[k + 1] > cpo[k]) return true;
+        return false;
+    }
+    // the spec-derived fields (everything but status, node and the session ids)
+    void spec(int i, HPod& p) const {
+        p.priority = ppri[i];
+        p.ts = pts[i];
+        const char* pc = (!ppc.empty() && ppc[i] >= 0) ? s.str(ppc[i]) : "";
+        p.critical = std::strcmp(s.str(pns[i]), "kube-system") == 0 ||
+                     std::strcmp(pc, "system-cluster-critical") == 0 || std::strcmp(pc, "system-node-critical") == 0;
+        p.backfill = !pbf.empty() && pbf[i];
+        p.groupless = pjob[i] < 0;
+        p.req = p.ireq = R3{};
+        p.nzc = p.nzm = 0;
+        for (int k = pco[i]; k < pco[i + 1]; ++k) {  // pod_info.go:51-71, non_zero.go:37-52
+            p.req.c += ccpu[k]; p.req.m += cmem[k]; p.req.g += cgpu[k];
+            p.nzc += (chas[k] & KBS_HAS_CPU) ? ccpu[k] : 100;
+            p.nzm += (chas[k] & KBS_HAS_MEM) ? cmem[k] : 200LL * 1024 * 1024;
+        }
+        p.ireq = p.req;
+        for (int k = pio[i]; k < pio[i + 1]; ++k) {
+            p.ireq.c = std::max(p.ireq.c, iccpu[k]);
+            p.ireq.m = std::max(p.ireq.m, icmem[k]);
+            p.ireq.g = std::max(p.ireq.g, icgpu[k]);
+        }
+    }
+};
+
+static void reopen_in_place(kb_session* ks, const kbs::Snapshot& s) {
+    Session& S = ks->s;
+    const SavedOptions o = save_options(S);
+    const int dev = S.device;
+    S.~Session();
+    new (&S) Session();
+    open_session(S, s, dev);
+    restore_options(S, o);
+    S.carry_bytes = -1;  // every table uploaded
+}
+
+// Whether the fast path can take the new snapshot (else: reopen_in_place).
+static bool carry_fast_ok(const Session& S, const kbs::Snapshot& s, const PodView& v, const int32_t* old_pod,
+                          const int32_t* old_node) {
+    if (!S.keep.ok || S.world != 1) return false;
+    const int N = (int)s.rows("n_name");
+    if (N != (int)S.h_alloc.size()) return false;
+    for (int n = 0; n < N; ++n) if (old_node[n] != n) return false;
+    if (conf_digest(s) != S.keep.conf_digest || node_spec_digest(s) != S.keep.node_spec_digest) return false;
+    auto a_flags = s.vec<uint8_t>("a_flags");
+    for (uint8_t f : a_flags) if (f & (KBS_AFF_PA | KBS_AFF_PAA)) return false;  // pod (anti-)affinity
+    for (int i = 0; i < v.P; ++i) {
+        if (old_pod[i] >= 0) continue;
+        if (v.pso[i + 1] > v.pso[i] || v.has_ports(i)) return false;   // nodeSelector / host ports
+        if (!v.paff.empty() && v.paff[i] >= 0 && (a_flags[v.paff[i]] & KBS_AFF_NA)) return false;  // node affinity
+    }
+    return true;
+}
+
+static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t* old_pod, const int32_t* old_node) {
+    Session& S = ks->s;
+    if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "kbhip_session_carry_snapshot on a node-sharded session");
+    require_no_tickets(S);
+    const PodView v(s);
+    const int P = v.P, Pold = (int)S.pods.size(), N = (int)s.rows("n_name"), Nold = (int)S.h_alloc.size();
+    {  // the maps: indices in range, each old pod / node at most once
+        vector<char> seen(std::max(Pold, Nold), 0);
+        for (int i = 0; i < P; ++i) {
+            const int o = old_pod[i];
+            if (o < -1 || o >= Pold || (o >= 0 && seen[o]++)) throw Error(KBHIP_EINVAL, "bad old_pod map");
+        }
+        std::fill(seen.begin(), seen.end(), 0);
+        for (int n = 0; n < N; ++n) {
+            const int o = old_node[n];
+            if (o < -1 || o >= Nold || (o >= 0 && seen[o]++)) throw Error(KBHIP_EINVAL, "bad old_node map");
+        }
+    }
+    ov_quiesce(S);
+    HIPCHK(hipStreamSynchronize(S.stream));
+    if (!carry_fast_ok(S, s, v, old_pod, old_node)) {
+        reopen_in_place(ks, s);
+        return;
+    }
+    // UID order (kbsnap.h canonical order): the UID rank of a pod is its index
+    {
+        constexpr int kThreads = 8;
+        const int per = (P + kThreads - 1) / kThreads;
+        std::atomic<bool> sorted{true};
+        auto check = [&](int lo, int hi) {
+            for (int i = std::max(lo, 1); i < hi; ++i)
+                if (std::strcmp(s.str(v.puid[i - 1]), s.str(v.puid[i])) >= 0) { sorted = false; return; }
+        };
+        if (P < (1 << 16)) {
+            check(0, P);
+        } else {
+            vector<std::thread> th;
+            for (int t = 1; t < kThreads; ++t) th.emplace_back(check, t * per, std::min(P, (t + 1) * per));
+            check(0, std::min(P, per));
+            for (auto& x : th) x.join();
+        }
+        if (!sorted) {  // the fast path keeps UID ranks as indices
+            reopen_in_place(ks, s);
+            return;
+        }
+    }
+    // ---------------- nodes: allocatable, pods, unschedulable (labels / taints unchanged) ----------------
+    auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"), agpu = s.vec<int64_t>("n_alloc_gpu"),
+         apods = s.vec<int64_t>("n_alloc_pods");
+    if ((int)acpu.size() != N || (int)amem.size() != N || (int)agpu.size() != N || (int)apods.size() != N)
+        throw Error(KBHIP_EINVAL, "node columns length mismatch");
+    auto unsched = s.vec<uint8_t>("n_unsched");
+    auto nname = s.span<int32_t>("n_name");
+    std::unordered_map<std::string_view, int> node_idx;  // names of the nodes new pods are bound to
+    auto find_node = [&](std::string_view nm) -> int {
+        if (node_idx.empty()) {
+            node_idx.reserve((size_t)N * 2);
+            for (int n = 0; n < N; ++n) node_idx.emplace(std::string_view(s.str(nname[n])), n);
+        }
+        auto it = node_idx.find(nm);
+        return it == node_idx.end() ? -1 : it->second;
+    };
+    // ---------------- pods ----------------
+    vector<HPod> pods(P);
+    vector<int32_t> port_off(P + 1, 0), port_ids;
+    port_ids.reserve(S.pod_port_ids.size());
+    const int tw = ((int)S.keep.taint_defs.size() + 63) / 64;
+    auto pns = v.pns;
+    auto tlk = s.span<int32_t>("tl_key"), tlo = s.span<int32_t>("tl_op"), tlv = s.span<int32_t>("tl_val"),
+         tle = s.span<int32_t>("tl_effect");
+    vector<int> new_classes;  // classes this carry appended
+    for (int i = 0; i < P; ++i) {
+        HPod& p = pods[i];
+        const int o = old_pod[i];
+        if (o >= 0) {
+            p = S.pods[o];  // spec-derived fields and session ids (namespace, class) kept
+        } else {
+            p = HPod{};
+            v.spec(i, p);
+            p.ns = S.keep.nss.get(s.s(pns[i]));
+        }
+        p.uid_rank = i;
+        p.status = v.status(i);
+        p.node = -1;
+        p.node_rel = false;
+        p.detached = false;
+        p.groupless = v.pjob[i] < 0;
+        if (v.has_node(i)) {
+            const int n = o >= 0 && S.pods[o].node >= 0 && S.pods[o].node < N &&
+                                  std::strcmp(s.str(nname[S.pods[o].node]), s.str(v.pnode[i])) == 0
+                              ? S.pods[o].node
+                              : find_node(std::string_view(s.str(v.pnode[i])));
+            if (n < 0)
+                throw Error(KBHIP_EINVAL, "pod " + s.s(v.puid[i]) + " is bound to node " + s.s(v.pnode[i]) +
+                                              " which is not in the snapshot");
+            p.node = n;
+            p.detached = !v.pdet.empty() && v.pdet[i];
+        }
+        port_off[i] = (int32_t)port_ids.size();
+        if (o >= 0)
+            port_ids.insert(port_ids.end(), S.pod_port_ids.begin() + S.pod_port_off[o],
+                            S.pod_port_ids.begin() + S.pod_port_off[o + 1]);
+    }
+    port_off[P] = (int32_t)port_ids.size();
+    // ---------------- queues & jobs (as at open) ----------------
+    auto qn = s.vec<int32_t>("q_name"), qw = s.vec<int32_t>("q_weight");
+    auto qts = s.vec<int64_t>("q_ts");
+    std::map<string, int> qidx;
+    vector<HQueue> queues(qn.size());
+    for (size_t i = 0; i < qn.size(); ++i) {
+        queues[i].name = s.s(qn[i]);
+        queues[i].weight = qw[i];
+        queues[i].ts = qts.empty() ? 0 : qts[i];
+        qidx[queues[i].name] = (int)i;
+    }
+    {
+        int r = 0;
+        std::map<string, int> rank;
+        for (auto& kv : qidx) rank[kv.first] = r++;
+        for (auto& q : queues) q.rank = rank[q.name];
+    }
+    auto jns = s.vec<int32_t>("j_ns"), jname = s.vec<int32_t>("j_name"), jq = s.vec<int32_t>("j_queue"),
+         jmin = s.vec<int32_t>("j_min"), jpri = s.vec<int32_t>("j_pg_priority");
+    auto jts = s.vec<int64_t>("j_ts");
+    struct Src { string uid; int row, pod; };
+    vector<Src> srcs;
+    srcs.reserve(jns.size() + 64);
+    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
+    for (int i = 0; i < P; ++i) {
+        if (v.pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
+        if (v.pjob[i] < 0) srcs.push_back({s.s(v.puid[i]), -1, i});  // shadow PodGroup
+    }
+    if (!std::is_sorted(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; }))
+        std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+    vector<HJob> jobs;
+    vector<string> job_uid;
+    vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
+    const auto default_q = qidx.find("default");
+    for (auto& src : srcs) {
+        int qslot = -1;
+        if (src.row >= 0) {
+            auto qit = qidx.find(s.s(jq[src.row]));
+            qslot = qit == qidx.end() ? -1 : qit->second;
+        } else {
+            qslot = default_q == qidx.end() ? -1 : default_q->second;
+        }
+        int slot = -1;
+        if (qslot >= 0) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
+            HJob j;
+            j.queue = qslot;
+            j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
+            j.ts = src.row >= 0 ? jts[src.row] : 0;
+            j.priority = j.pg_priority = src.row >= 0 ? jpri[src.row] : 0;
+            j.shadow = src.row < 0;
+            slot = (int)jobs.size();
+            jobs.push_back(std::move(j));
+            job_uid.push_back(src.uid);
+        }
+        if (src.row >= 0) row_slot[src.row] = slot;
+        else shadow_slot[src.pod] = slot;
+    }
+    for (int i = 0; i < P; ++i) {
+        HPod& p = pods[i];
+        const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
+        p.job = slot;
+        if (slot < 0) continue;
+        HJob& j = jobs[slot];
+        j.tasks.push_back(i);
+        j.priority = p.priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
+        if (allocated_status(p.status)) j.cnt_alloc++;
+        if (p.status == AOB) j.cnt_aob++;
+        if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) j.maybe_pending = true;
+    }
+    // ---------------- task classes of pending tasks without one (new pods) ----------------
+    for (int i = 0; i < P; ++i) {
+        HPod& p = pods[i];
+        if (p.status != Pending || p.job < 0) { if (old_pod[i] < 0) p.cls = -1; continue; }
+        if (p.cls >= 0) continue;  // kept: the pod's spec did not change
+        TaskClass c{};
+        c.ireq_cpu = p.ireq.c; c.ireq_mem = p.ireq.m; c.ireq_gpu = p.ireq.g;
+        c.req_cpu = p.req.c; c.req_mem = p.req.m; c.req_gpu = p.req.g;
+        c.nz_cpu = p.nzc; c.nz_mem = p.nzm;
+        c.backfill = p.backfill;
+        c.nsel_term = -1;
+        c.req_term_n = -1;
+        vector<uint64_t> tol(tw, 0);  // tolerations -> tolerated taint ids (toleration.go:37-56)
+        for (size_t t = 0; t < S.keep.taint_defs.size(); ++t) {
+            bool ok = false;
+            for (int k = v.pto[i]; k < v.pto[i + 1] && !ok; ++k) {
+                string key = s.s(tlk[k]), op = s.s(tlo[k]), val = s.s(tlv[k]), eff = s.s(tle[k]);
+                if (!eff.empty() && eff != std::get<2>(S.keep.taint_defs[t])) continue;
+                if (!key.empty() && key != std::get<0>(S.keep.taint_defs[t])) continue;
+                if (op.empty() || op == "Equal") ok = val == std::get<1>(S.keep.taint_defs[t]);
+                else if (op == "Exists") ok = true;
+            }
+            if (ok) tol[t / 64] |= 1ULL << (t % 64);
+        }
+        c.pa_space = c.paa_space = -1;
+        // the class signature exactly as open_session builds it (no selector terms, no ports, no program)
+        string sig((const char*)&c, sizeof(TaskClass));
+        sig.append((const char*)tol.data(), tol.size() * sizeof(uint64_t));
+        auto it = S.keep.class_ids.find(sig);
+        if (it != S.keep.class_ids.end()) { p.cls = it->second; continue; }
+        c.tol_off = (int32_t)S.keep.masks.size();
+        for (auto x : tol) S.keep.masks.push_back(x);
+        c.pconf_off = (int32_t)S.keep.masks.size();
+        for (int w = 0; w < kPortWin; ++w) S.keep.masks.push_back(0);
+        c.pown_off = (int32_t)S.keep.masks.size();
+        for (int w = 0; w < kPortWin; ++w) S.keep.masks.push_back(0);
+        p.cls = (int)S.classes.size();
+        S.keep.class_ids.emplace(std::move(sig), p.cls);
+        S.classes.push_back(c);
+        new_classes.push_back(p.cls);
+    }
+    // ---------------- node rows from the pods (cache addTask -> NodeInfo.AddTask) ----------------
+    const int Nl = S.nc.n;
+    vector<int64_t> col[13];
+    for (auto& c : col) c.assign(N, 0);
+    vector<int32_t> podcnt(N, 0), maxc(N, 0);
+    vector<uint8_t> flg(N, 0);
+    vector<uint64_t> pcol((size_t)std::max(S.nc.port_words, 1) * S.nc.npad, 0);
+    S.used.assign(N, R3{});
+    for (int n = 0; n < N; ++n) {
+        col[0][n] = acpu[n]; col[1][n] = amem[n]; col[2][n] = agpu[n];
+        col[9][n] = acpu[n]; col[10][n] = amem[n];
+        maxc[n] = (int32_t)apods[n];
+        flg[n] = (!unsched.empty() && unsched[n]) ? 1 : 0;
+    }
+    for (int i = 0; i < P; ++i) {
+        const HPod& p = pods[i];
+        if (!on_node_of(p)) continue;
+        const int n = p.node;
+        if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
+        if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
+        col[0][n] -= p.req.c; col[1][n] -= p.req.m; col[2][n] -= p.req.g;
+        S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+        podcnt[n]++;
+        col[11][n] += p.nzc;
+        col[12][n] += p.nzm;
+        for (int k = port_off[i]; k < port_off[i + 1]; ++k) {
+            const int id = port_ids[k];
+            pcol[(size_t)(id / 64) * S.nc.npad + n] |= 1ULL << (id % 64);
+        }
+    }
+    S.any_bf = 0;
+    for (int n = 0; n < N; ++n) if (col[6][n] || col[7][n] || col[8][n]) S.any_bf = 1;
+    // ---------------- device: the node rows that differ, the grown class tables ----------------
+    int64_t uploaded = 0;
+    auto sync_col = [&](void* dptr, const void* want, size_t elem) {
+        vector<uint8_t> have((size_t)Nl * elem);
+        HIPCHK(hipMemcpy(have.data(), dptr, have.size(), hipMemcpyDeviceToHost));
+        const uint8_t* w = (const uint8_t*)want;
+        int n = 0;
+        while (n < Nl) {
+            if (std::memcmp(have.data() + (size_t)n * elem, w + (size_t)n * elem, elem) == 0) { ++n; continue; }
+            int e = n + 1;
+            while (e < Nl && std::memcmp(have.data() + (size_t)e * elem, w + (size_t)e * elem, elem) != 0) ++e;
+            HIPCHK(hipMemcpyAsync((uint8_t*)dptr + (size_t)n * elem, w + (size_t)n * elem, (size_t)(e - n) * elem,
+                                  hipMemcpyHostToDevice, S.stream));
+            uploaded += (int64_t)(e - n) * (int64_t)elem;
+            n = e;
+        }
+    };
+    int64_t* dcol[13] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem, S.nc.rel_gpu,
+                         S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu, S.nc.acpu, S.nc.amem, S.nc.nzc, S.nc.nzm};
+    for (int k = 0; k < 13; ++k) sync_col(dcol[k], col[k].data(), sizeof(int64_t));
+    sync_col(S.nc.pods, podcnt.data(), sizeof(int32_t));
+    sync_col(S.nc.maxtasks, maxc.data(), sizeof(int32_t));
+    sync_col(S.nc.flags, flg.data(), sizeof(uint8_t));
+    for (int w = 0; w < S.nc.port_words; ++w)
+        sync_col(S.nc.ports + (size_t)w * S.nc.npad, pcol.data() + (size_t)w * S.nc.npad, sizeof(uint64_t));
+    if (!new_classes.empty()) {
+        S.class_kf.resize(S.classes.size());
+        S.class_srange.resize(S.classes.size());
+        static const vector<Term> no_terms;
+        for (int ci : new_classes) class_key_format(S, S.classes[ci], no_terms, N, &S.class_kf[ci], &S.class_srange[ci]);
+        S.tab.classes = upload(S, S.b_classes, S.classes);
+        S.tab.masks = upload(S, S.b_masks, S.keep.masks);
+        uploaded += (int64_t)(S.classes.size() * sizeof(TaskClass) + S.keep.masks.size() * sizeof(uint64_t));
+    }
+    HIPCHK(hipStreamSynchronize(S.stream));  // the host sources above are about to go away
+    // ---------------- the host model of the new session ----------------
+    spare_pods().give(S.pods);
+    S.pods.swap(pods);
+    S.pod_port_off.swap(port_off);
+    S.pod_port_ids.swap(port_ids);
+    S.jobs.swap(jobs);
+    S.job_uid.swap(job_uid);
+    S.queues.swap(queues);
+    for (int n = 0; n < N; ++n) S.h_alloc[n] = R3{acpu[n], amem[n], agpu[n]};
+    S.total = F3{};
+    for (int n = 0; n < N; ++n) S.total.add(S.h_alloc[n]);  // drf.go:61-63, proportion.go:59-61
+    S.carry_bytes = uploaded;
+    S.tab_delta.clear();
+    S.plugins_opened = false;
+    S.fallback = -1;
+    S.sess_cnt.clear();
+    S.node_tasks.clear();
+    S.log.clear();
+    S.last_fit_ok = false;
+    S.stats.nodes = N;
 }
 
 static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
@@ -4221,6 +4806,24 @@ int kbhip_reclaim(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* o
 int kbhip_preempt(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
     return evict_action(s, true, out_pod, out_node, out_kind, cap);
 }
+int kbhip_session_carry_snapshot(kb_session* s, const void* kbs_bytes, size_t len, const int32_t* old_pod,
+                                 const int32_t* old_node, int64_t* out_uploaded_bytes) {
+    ABI_GUARD_S(s, {
+        if (!s || !kbs_bytes) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbs::Snapshot snap;
+        snap.view_bytes(kbs_bytes, len);
+        const size_t P = snap.rows("p_uid"), N = snap.rows("n_name");
+        if ((P && !old_pod) || (N && !old_node)) throw kbhip::Error(KBHIP_EINVAL, "null index map");
+        HIPCHK(hipSetDevice(s->s.device));
+        auto t0 = std::chrono::steady_clock::now();
+        carry_snapshot(s, snap, old_pod, old_node);
+        s->s.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (out_uploaded_bytes) *out_uploaded_bytes = s->s.carry_bytes;
+        return KBHIP_OK;
+    })
+}
+
 int kbhip_read_nodes(kb_session* s, int64_t* out, int64_t n_nodes) {
     ABI_GUARD_S(s, {
         if (!s || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
@@ -4273,6 +4876,10 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         kbhip::require_no_tickets(s->s);  // options change how queued pops would run
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else if (std::strcmp(key, "sweep_variant") == 0) {  // kbhip_sweep_scores' kernel shape (tuning)
+            if (value < 0 || value > 3) throw kbhip::Error(KBHIP_EINVAL, "sweep_variant must be 0..3");
+            kbhip::set_sweep_variant((int)value);
+        }
         else if (std::strcmp(key, "speculate") == 0) {
             if (value < 0 || value > 3) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0..3");
             s->s.speculate = (int)value;

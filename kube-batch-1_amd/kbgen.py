@@ -250,6 +250,11 @@ class Pod:
     node: Optional[str] = None
     phase: str = "Pending"
     deleting: bool = False
+    # detached: the scheduler cache deleted this group-less pod, which takes it
+    # off its node only (deletePod builds NewTaskInfo with an empty Job,
+    # cache/event_handlers.go:119-165): the task stays in its shadow job with
+    # its status and NodeName, but is not in the node's task list
+    detached: bool = False
     priority: int = 0
     ts: int = 0
     backfill: bool = False
@@ -398,6 +403,8 @@ class Cluster:
         C["p_node"] = i32([st.add(p.node) if p.node else -1 for p in pods])
         C["p_phase"] = u8([PHASES[p.phase] for p in pods])
         C["p_deleting"] = u8([1 if p.deleting else 0 for p in pods])
+        if any(p.detached for p in pods):
+            C["p_detached"] = u8([1 if p.detached else 0 for p in pods])
         C["p_backfill"] = u8([1 if p.backfill else 0 for p in pods])
         C["p_pclass"] = i32([st.add(p.priority_class) if p.priority_class else -1 for p in pods])
         C["p_priority"] = i32([p.priority for p in pods])

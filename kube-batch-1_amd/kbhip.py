@@ -30,7 +30,8 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
            "kbhip_session_carry_events", "kbhip_shard_connect_mailbox", "kbhip_place_job_submit",
-           "kbhip_place_job_wait", "kbhip_place_job_cancel")
+           "kbhip_place_job_wait", "kbhip_place_job_cancel", "kbhip_time_sweeps",
+           "kbhip_session_carry_snapshot")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64, RED_SUM_I64 = 0, 1, 2, 3
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32,
@@ -90,9 +91,11 @@ def lib() -> ctypes.CDLL:
         L.kbhip_backfill.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_first_fit.argtypes = [vp, vp, i32, vp]
         L.kbhip_sweep_scores.argtypes = [vp, i32, vp]
+        L.kbhip_time_sweeps.argtypes = [vp, vp, i32, vp]
         L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_carry.argtypes = [vp, vp]
         L.kbhip_session_carry_events.argtypes = [vp, vp, vp, i64, vp]
+        L.kbhip_session_carry_snapshot.argtypes = [vp, vp, ctypes.c_size_t, vp, vp, vp]
         L.kbhip_preempt.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_open_shard.argtypes = [vp, ctypes.c_size_t, ctypes.c_int, i32, i32, ctypes.POINTER(vp)]
         L.kbhip_shard_info.argtypes = [vp, vp]
@@ -202,6 +205,14 @@ class Session:
         n = _check(lib().kbhip_sweep_scores(self._h, int(task_id), _p(out)))
         return n, out[:n_nodes].copy()
 
+    def time_sweeps(self, task_ids) -> float:
+        """kbhip_time_sweeps: device time per launch (us) of the standalone sweep,
+        one launch per task, back to back."""
+        ids = np.ascontiguousarray(task_ids, dtype=np.int32)
+        out = np.zeros(1, np.float64)
+        _check(lib().kbhip_time_sweeps(self._h, _p(ids), ids.size, _p(out)))
+        return float(out[0])
+
     def carry(self) -> int:
         """kbhip_session_carry: become the next session (binds / evictions applied); bytes uploaded."""
         out = np.zeros(1, np.int64)
@@ -217,6 +228,21 @@ class Session:
             raise ValueError("pods and events differ in length")
         out = np.zeros(1, np.int64)
         _check(lib().kbhip_session_carry_events(self._h, _p(p), _p(e), int(p.size), _p(out)))
+        return int(out[0])
+
+    def carry_snapshot(self, snapshot, old_pod, old_node) -> int:
+        """kbhip_session_carry_snapshot: become the session of the cache's next
+        snapshot (KBS1 bytes or a path); old_pod / old_node map its pods / nodes
+        to this session's indices (-1: new).  Bytes uploaded (-1: re-opened)."""
+        if not isinstance(snapshot, (bytes, bytearray, memoryview)):
+            with open(snapshot, "rb") as f:
+                snapshot = f.read()
+        buf = bytes(snapshot)
+        op = np.ascontiguousarray(old_pod, np.int32)
+        on = np.ascontiguousarray(old_node, np.int32)
+        out = np.zeros(1, np.int64)
+        _check(lib().kbhip_session_carry_snapshot(self._h, ctypes.c_char_p(buf), len(buf), _p(op) if op.size else None,
+                                                  _p(on) if on.size else None, _p(out)))
         return int(out[0])
 
     def reclaim(self, cap: int = 1 << 21) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
@@ -272,15 +298,14 @@ class Session:
         # the result arrays hold every task of the ticket; its size leaves the
         # table only once the wait succeeded (a refused wait can be retried)
         tix = getattr(self, "_tix", {})
-        if ticket not in tix:
-            raise KbhipError(f"ticket {ticket} is not outstanding in this binding")
-        n = tix[ticket]
+        # a ticket this binding does not hold is refused by the library (EINVAL): arrays as large as any held one
+        n = tix.get(ticket, max(list(tix.values()) + [1]))
         node = np.full(n, -1, np.int32)
         kind = np.zeros(n, np.uint8)
         done = np.zeros(1, np.int32)
         stop = np.zeros(1, np.int32)
         _check(lib().kbhip_place_job_wait(self._h, int(ticket), _p(node), _p(kind), _p(done), _p(stop)))
-        del tix[ticket]
+        tix.pop(ticket, None)
         d = int(done[0])
         return node[:d].copy(), kind[:d].copy(), int(stop[0])
 

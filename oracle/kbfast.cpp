@@ -179,6 +179,7 @@ struct PodRec {
     int job = -1;  // session job slot
     string jobUID;
     int curNode = -1;  // task.NodeName (node index)
+    bool detached = false;  // p_detached: in its job with its NodeName, off the node
     bool critical = false;  // kube-system or a system-*-critical priority class (conformance.go:40-45)
     bool nodeRel = false;   // the node's copy stayed Releasing after an unevict (statement.go:81-105)
     bool hasPodAff() const { return aff && (aff->pa || aff->paa); }
@@ -440,6 +441,7 @@ struct Loader {
         auto pname = V32("p_name"), pns = V32("p_ns"), pjob = V32("p_job"), pnode = V32("p_node"),
              ppri = V32("p_priority"), paff = V32("p_aff");
         auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+        auto pdet = s.vec<uint8_t>("p_detached");  // optional (kbsnap.h)
         auto ppcls = s.vec<int32_t>("p_pclass"), pns_raw = s.vec<int32_t>("p_ns");
         auto pts = s.vec<int64_t>("p_ts");
         auto plo = s.offs("p_label_off", P);
@@ -584,9 +586,12 @@ struct Loader {
             }
         }
         // place pods on nodes (cache addTask -> NodeInfo.AddTask; terminated pods skipped)
+        bool anyDetached = false;
         for (size_t i = 0; i < P; ++i) {
             PodRec& p = w.pods[i];
             p.curNode = p.nodeRaw;
+            // a detached pod (cache deletePod of a group-less pod) keeps its job and NodeName, off the node
+            if (!pdet.empty() && pdet[i] && p.nodeRaw >= 0) { p.detached = true; anyDetached = true; continue; }
             if (p.nodeRaw < 0 || p.status == Succeeded || p.status == Failed) continue;
             NodeRec& n = w.nodes[p.nodeRaw];
             if (p.backfill) n.bf += p.req;
@@ -601,9 +606,13 @@ struct Loader {
             n.podList.push_back((int)i);
         }
         for (auto& n : w.nodes) if (n.bf.cpu || n.bf.mem || n.bf.gpu) w.anyBackfilled = true;
-        for (size_t i = 0; i < P; ++i) if (w.pods[i].hasPodAff() && w.pods[i].curNode >= 0 &&
+        for (size_t i = 0; i < P; ++i) if (w.pods[i].hasPodAff() && w.pods[i].curNode >= 0 && !w.pods[i].detached &&
                                              w.pods[i].status != Succeeded && w.pods[i].status != Failed)
             w.affPods.push_back((int)i);
+        if (anyDetached)  // the predicate lister's NodeInfo.Filter excludes such a pod at its own node only
+            for (auto& p : w.pods)
+                if (p.aff && (p.aff->pa || p.aff->paa || !p.aff->paPref.empty() || !p.aff->paaPref.empty()))
+                    throw std::runtime_error("detached pods with pod (anti-)affinity in the session: kbref only");
         // plugins (framework.go:33-48: one object per name, last entry's arguments;
         // dispatch loops over tier entries, so an enabled duplicate entry counts twice)
         for (auto& tier : w.tiers)

@@ -112,6 +112,7 @@ struct Pod {
     string nodeName;  // Spec.NodeName
     int phase = KBS_PENDING;
     bool deleting = false;
+    bool detached = false;  // p_detached (kbsnap.h): in its job, off its node's task list
     int32_t priority = 0;
     int64_t ts = 0;
     bool backfill = false;
@@ -1551,6 +1552,7 @@ static void loadWorld(World& w) {
     auto pname = s.vec<int32_t>("p_name"), pns = s.vec<int32_t>("p_ns"), pjob = s.vec<int32_t>("p_job"),
          pnode = s.vec<int32_t>("p_node"), ppri = s.vec<int32_t>("p_priority"), paff = s.vec<int32_t>("p_aff");
     auto pphase = s.vec<uint8_t>("p_phase"), pdel = s.vec<uint8_t>("p_deleting"), pbf = s.vec<uint8_t>("p_backfill");
+    auto pdet = s.vec<uint8_t>("p_detached");  // optional
     auto pts = s.vec<int64_t>("p_ts");
     auto ppc = s.vec<int32_t>("p_pclass");  // optional
     auto plo = s.offs("p_label_off", P);
@@ -1578,6 +1580,7 @@ static void loadWorld(World& w) {
         p.nodeName = s.s(pnode[i]);
         p.phase = pphase[i];
         p.deleting = pdel[i];
+        p.detached = !pdet.empty() && pdet[i];
         p.backfill = pbf[i];
         p.priority = ppri[i];
         p.ts = pts[i];
@@ -1634,7 +1637,9 @@ static void openSession(World& w) {
         if (!p.nodeName.empty()) {
             if (!nodeByName.count(p.nodeName))
                 throw std::runtime_error("pod " + p.uid + " bound to unknown node " + p.nodeName);
-            if (t.Status != Succeeded && t.Status != Failed) w.nodes[nodeByName[p.nodeName]].AddTask(t);
+            // a detached pod (cache deletePod of a group-less pod, event_handlers.go:119-165) stays in
+            // its shadow job with its NodeName, off the node's task list
+            if (t.Status != Succeeded && t.Status != Failed && !p.detached) w.nodes[nodeByName[p.nodeName]].AddTask(t);
         }
     }
     // queues

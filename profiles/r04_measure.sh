@@ -26,4 +26,7 @@ timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc -o run
 timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $OUT/sq -o run --output-format csv -- \
     python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --time-every 0 > $OUT/bench_sq.json 2> $OUT/sq.err || exit 1
+# summarise on the box (the raw traces exceed what gpurun copies back)
+python3 profiles/summarize.py $OUT ${TAG} gpurun_out > $OUT/summary.log 2>&1 || exit 1
+rm -rf $OUT/trace $OUT/pmc $OUT/sq
 echo done

@@ -10,7 +10,7 @@ FETCH_SIZE is reported in KB by rocprofv3; on gfx950 it counts exactly half
 the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM section),
 so the corrected traffic is 2 x FETCH_SIZE x 1024 bytes.
 
-Usage: python profiles/summarize.py gpurun_out/prof_<tag> <tag>
+Usage: python profiles/summarize.py gpurun_out/prof_<tag> <tag> [dest dir, default profiles/]
 """
 import csv
 import json
@@ -26,7 +26,7 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
-def main(src, tag):
+def main(src, tag, dest=None):
     stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
     pmc_csv = os.path.join(src, "pmc", "run_counter_collection.csv")
     out = {"tag": tag, "kernels": {}}
@@ -103,11 +103,12 @@ def main(src, tag):
                 lines = [ln for ln in f.read().splitlines() if ln.startswith("{")]
             if lines:
                 out[name.replace(".json", "")] = json.loads(lines[-1])
-    shutil.copy(stats_csv, os.path.join(HERE, f"{tag}_kernel_stats.csv"))
-    with open(os.path.join(HERE, f"{tag}_summary.json"), "w") as f:
+    dest = dest or HERE
+    shutil.copy(stats_csv, os.path.join(dest, f"{tag}_kernel_stats.csv"))
+    with open(os.path.join(dest, f"{tag}_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["kernels"], indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)

@@ -109,10 +109,14 @@ def test_carry_events_equal_fresh_session(engine, oracle_mod, kbgen_mod, tmp_pat
     cache events on existing pods (event_handlers.go deletePod / updatePod to
     Succeeded or Failed) — evicted pods finishing, running pods completing,
     pending pods withdrawn, shadow (group-less) pods deleted.  The carried
-    session must schedule like a fresh one opened from the cache's snapshot
-    (deleted pods absent); the oracle's pod indices are mapped back through
-    the UIDs."""
+    session must schedule like a fresh one opened from the snapshot the
+    reference cache holds then: a deleted pod of a PodGroup is gone; a deleted
+    group-less pod stays in its shadow job (deletePod's TaskInfo has an empty
+    Job) — off its node if it had one (p_detached), unchanged (and allocated
+    again) if it was pending.  The oracle's pod indices are mapped back
+    through the UIDs."""
     rng = np.random.default_rng(7000 + seed)
+    aff = seed % 4 in (0, 1)
     if seed % 2:
         c = kbgen_mod.gen_preempt(5300 + seed, n_nodes=4 + seed % 8, n_queues=1 + seed % 3, n_run_jobs=4 + seed % 7,
                                   n_pend_jobs=3 + seed % 5, max_tasks=2 + seed % 5,
@@ -143,7 +147,9 @@ def test_carry_events_equal_fresh_session(engine, oracle_mod, kbgen_mod, tmp_pat
         for i, q in enumerate(pods_sorted):
             st = int(status[i])
             if q.group is None:
-                ev[i] = EV_DELETE
+                # a bound group-less pod is detached, which pod-affinity sessions refuse (tested below)
+                on_node = st in (RUNNING, BINDING, 32, RELEASING)
+                ev[i] = EV_SUCCEEDED if (aff and on_node) else EV_DELETE
             elif st == RELEASING and rng.random() < 0.7:
                 ev[i] = EV_DELETE
             elif st in (RUNNING, BINDING, 32) and rng.random() < 0.15:
@@ -157,16 +163,20 @@ def test_carry_events_equal_fresh_session(engine, oracle_mod, kbgen_mod, tmp_pat
         ns = s.read_nodes(n_nodes)
     c2 = _next_snapshot(c, status, node)
     for i, e in ev.items():
+        q = pods_sorted[i]
         if e != EV_DELETE:
-            pods_sorted[i].phase = "Succeeded" if e == EV_SUCCEEDED else "Failed"
-    gone = {pods_sorted[i].uid for i, e in ev.items() if e == EV_DELETE}
+            q.phase = "Succeeded" if e == EV_SUCCEEDED else "Failed"
+        elif q.group is None and q.node is not None and q.phase not in ("Succeeded", "Failed"):
+            q.detached = True  # deletePod of a group-less pod: off its node, still in its shadow job
+    gone = {pods_sorted[i].uid for i, e in ev.items() if e == EV_DELETE and pods_sorted[i].group is not None}
     c2.pods = [q for q in c2.pods if q.uid not in gone]
     p2 = c2.write(str(tmp_path / "s2.kbs"))
     exp, ons = oracle_mod.ref_allocate(p2, actions=acts, with_nodes=True)
     idx = {q.uid: i for i, q in enumerate(pods_sorted)}
     fresh = sorted(c2.pods, key=lambda q: q.uid)
     exp_engine = [(idx[fresh[a].uid], b, k) for a, b, k in exp.as_list()]
-    assert all(int(st2[i]) == 2048 for i, e in ev.items() if e == EV_DELETE)
+    assert all(int(st2[i]) == 2048 for i, e in ev.items() if e == EV_DELETE and pods_sorted[i].group is not None)
+    assert all(int(st2[i]) != 2048 for i, e in ev.items() if e == EV_DELETE and pods_sorted[i].group is None)
     assert [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)] == exp_engine
     assert np.array_equal(ns.astype(np.float64), ons[:n_nodes])
 
@@ -185,3 +195,25 @@ def test_carry_events_rejects_bad_input(engine, kbgen_mod, tmp_path):
         s.carry_events(np.array([0], np.int32), np.array([EV_DELETE], np.uint8))
         with pytest.raises(engine.KbhipError):  # already deleted
             s.carry_events(np.array([0], np.int32), np.array([EV_SUCCEEDED], np.uint8))
+
+
+def test_carry_events_detach_refused_with_pod_affinity(engine, kbgen_mod, tmp_path):
+    """Deleting a bound group-less pod detaches it (it stays in its shadow
+    job); with pod (anti-)affinity terms in the session the predicate lister
+    would leave it out at its own node only (NodeInfo.Filter), which the count
+    tables do not model: KBHIP_EUNSUPPORTED, nothing changed."""
+    c = kbgen_mod.gen_random(5501, n_nodes=6, n_jobs=5, max_tasks=3,
+                             features=tuple(NO_POD_AFFINITY) + ("podaffinity",))
+    if "default" not in {q.name for q in c.queues}:
+        c.add_queue("default")
+    node0 = sorted(n.name for n in c.nodes)[0]
+    c.add_pod("default", "solo", uid="zsolo", group=None, node=node0, phase="Running",
+              containers=[{"cpu": 100, "mem": 1 << 20}])
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    solo = sorted(q.uid for q in c.pods).index("zsolo")
+    with engine.Session(p1) as s:
+        s.allocate()
+        before = s.table("pod_status").copy()
+        with pytest.raises(engine.KbhipError, match="affinity"):
+            s.carry_events(np.array([solo], np.int32), np.array([EV_DELETE], np.uint8))
+        assert np.array_equal(s.table("pod_status"), before)
