@@ -110,6 +110,10 @@ typedef struct kbhip_stats {
     double score_sweep_s;    /* kbhip_sweep_scores with "time_every" > 0: summed HIP-event duration of its
                                 standalone predicate + score sweep kernel (k_rank_nodes) */
     int64_t score_sweeps;    /* ... launches timed */
+    int64_t pertask_sweeps;  /* tasks swept one launch each (the general path: k_sweep_argmax) */
+    int64_t seq_launches;    /* batched pops with a sequential placement (6: Backfilled nodes, 7: pod affinity) */
+    int64_t seq_cut;         /* ... that ended before their chunk (a node outside the list could win next) */
+    int64_t seq_none;        /* ... that placed nothing (the task went to the general path) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

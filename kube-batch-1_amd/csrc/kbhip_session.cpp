@@ -2011,6 +2011,7 @@ struct GroupScope {
 // Classes with inter-pod priority terms (their k_ipa_minmax prepass) and
 // debug-key sessions keep the per-task launches.
 static void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task = false) {
+    S.stats.pertask_sweeps += m;
     bool group = S.rank_group && S.world == 1 && !S.d_dbg && !per_task;
     for (int i = 0; i < m && group; ++i) group = S.classes[cls[i]].ipa_n == 0;
     if (!group) {
@@ -2280,6 +2281,11 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
     }
     *n_done_out = n_done;
     *stop_out = (int)((load(0) >> 44) & 0xf) - 1;
+    if (L.aff || L.bf) {  // the sequential placements: how often a launch ends before its chunk does
+        S.stats.seq_launches++;
+        if (n_done == 0) S.stats.seq_none++;
+        else if (*stop_out == KBHIP_STOP_ALL && n_done < L.m) S.stats.seq_cut++;
+    }
     S.last_fit_ok = false;
     if (*stop_out == KBHIP_STOP_UNASSIGNED && L.fit) {
         uint64_t f0 = 0, f1 = 0;
@@ -2627,9 +2633,22 @@ static int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t
             sync = true;
         } else {
             if (st < 0 || nd > n) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+            int alloc = 0;
+            for (int j = 0; j < nd; ++j) alloc += S.res_kind_buf[j] == 1;
             apply_results(S, t.ids.data(), nd, S.res_node_buf, S.res_kind_buf, out_node, out_kind);
             *out_n_done = nd;
             *out_stop = st;
+            if (st == KBHIP_STOP_ALL && nd < n) {
+                // the launch ended before its chunk did (a sequential placement whose list ran out): the
+                // pop goes on with its remaining tasks (allocate.go:110-196), synchronously; the launches
+                // behind it ran on a state it is about to change
+                retract_tickets(S, 0);
+                int32_t nd2 = 0, st2 = 0;
+                place_job(S, t.ids.data() + nd, n - nd, t.gang, t.min_avail, t.ready + alloc, out_node + nd,
+                          out_kind + nd, &nd2, &st2);
+                *out_n_done = nd + nd2;
+                *out_stop = st2;
+            }
         }
     }
     if (sync) place_job(S, t.ids.data(), n, t.gang, t.min_avail, t.ready, out_node, out_kind, out_n_done, out_stop);
@@ -4173,7 +4192,12 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
             if (gone[i] || S.pods[i].status == Gone || S.pods[i].detached)
                 throw Error(KBHIP_EINVAL, "event on a deleted pod");
             if (ev[k] == KBHIP_EV_DELETE) gone[i] = 1;
-            if (aff && ev[k] == KBHIP_EV_DELETE && S.pods[i].groupless && S.pods[i].node >= 0)
+            const HPod& q = S.pods[i];
+            // on a node once the carry's transitions ran (session-only Allocated / Pipelined: Pending again)
+            const bool carried_on_node = q.node >= 0 && q.status != Allocated && q.status != AOB &&
+                                         q.status != Pipelined && q.status != Pending && q.status != Succeeded &&
+                                         q.status != Failed;
+            if (aff && ev[k] == KBHIP_EV_DELETE && q.groupless && carried_on_node)
                 throw Error(KBHIP_EUNSUPPORTED, "deleting a bound group-less pod (it stays in its shadow job, "
                                                 "detached) in a session with pod (anti-)affinity");
         }

@@ -69,6 +69,30 @@ def test_kbhost_c2(engine, oracle_mod, kbgen_mod, tmp_path):
     print(json.dumps(rec))
 
 
+def test_kbhost_c3_scaled(engine, oracle_mod, kbgen_mod, tmp_path):
+    """C3-shaped (zone anti-affinity gangs, selectors, taints, 8 queues), 2k
+    nodes: anti-affinity pops are launched at submit (placement 7); a launch
+    whose candidate list runs out goes on synchronously inside its wait."""
+    p = str(tmp_path / "c3.kbs")
+    kbgen_mod.gen_c3(n_nodes=2000, n_pending=6000).write(p)
+    exp = oracle_mod.fast_allocate(p, threads=8).as_list()
+    rec, logs = _kbhost(p, tmp_path, reps=1)
+    assert rec["equal"], rec
+    assert logs["async"] == exp and logs["sync"] == exp
+    assert rec["async"]["async_launched"] > 0
+
+
+def test_kbhost_c5_scaled(engine, oracle_mod, kbgen_mod, tmp_path):
+    """C5-shaped (Backfilled nodes: every pop's walk mutates Idle), 600 nodes:
+    the pipelined host loop runs each pop inside its wait and equals the oracle."""
+    p = str(tmp_path / "c5.kbs")
+    kbgen_mod.gen_c5(p, n_nodes=600, n_pending=300, best_effort=20)
+    exp = oracle_mod.fast_allocate(p, threads=8).as_list()
+    rec, logs = _kbhost(p, tmp_path, reps=1)
+    assert rec["equal"], rec
+    assert logs["async"] == exp and logs["sync"] == exp
+
+
 def _record(engine, path, cluster):
     """The pop sequence of a synchronous run: [(ids, gm, min, ready, (nodes, kinds, stop))]."""
     calls = []
