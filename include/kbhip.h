@@ -108,12 +108,16 @@ typedef struct kbhip_stats {
     int64_t sweep_requests;  /* per-task chunks (allocate's general path, backfill) served by the what-if batcher */
     int64_t sweep_batch_sum; /* sum over those of the sessions per launch that served them */
     double score_sweep_s;    /* kbhip_sweep_scores with "time_every" > 0: summed HIP-event duration of its
-                                standalone predicate + score sweep kernel (k_rank_nodes) */
+                                standalone predicate + score sweep kernel (k_score_sweep) */
     int64_t score_sweeps;    /* ... launches timed */
     int64_t pertask_sweeps;  /* tasks swept one launch each (the general path: k_sweep_argmax) */
     int64_t seq_launches;    /* batched pops with a sequential placement (6: Backfilled nodes, 7: pod affinity) */
     int64_t seq_cut;         /* ... that ended before their chunk (a node outside the list could win next) */
     int64_t seq_none;        /* ... that placed nothing (the task went to the general path) */
+    double evict_rank_s;     /* reclaim / preempt: host wall time in the node rankings (device sweep + copy) */
+    double evict_walk_s;     /* reclaim / preempt: host wall time walking the ranked nodes (victims, evictions) */
+    int64_t evict_visits;    /* reclaim / preempt: nodes whose victims were asked for (Reclaimable / Preemptable) */
+    int64_t evict_cands;     /* ... candidates handed to those calls */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -297,6 +301,9 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * (placement 6), 0 = per-task sweeps there;
  * "aff_batch" = 1 (default) batches pops of pod anti-affinity classes
  * (placement 7), 0 = per-task sweeps for them;
+ * "aff_fence" = 1 (default) orders a placement-7 pop behind the overlapped
+ * pops before it on the device (stream events; the host keeps predicted pops
+ * queued), 0 = the host drains the overlap streams first;
  * "rank_radix" = 1 orders reclaim / preempt walks with the wide-range radix
  * passes (four 8-bit counting passes over the score) instead of the one-pass
  * counting sort (tests);

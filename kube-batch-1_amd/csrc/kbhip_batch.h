@@ -999,6 +999,9 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         done = i + 1;
         if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
         if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195
+        // per-domain candidates: only an Allocated placement closes its domain; after a
+        // Pipelined one a node of the winner's domain left out by the sweep may come next
+        if (c.dd_space >= 0 && kind != 1) break;
     }
     if (changed) {
         nc.idle_cpu[n] = r.idle_cpu; nc.idle_mem[n] = r.idle_mem; nc.idle_gpu[n] = r.idle_gpu;

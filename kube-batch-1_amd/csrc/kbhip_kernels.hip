@@ -346,6 +346,33 @@ struct PopDescs {
 };
 static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed the kernel argument space");
 
+// Placement 7 with per-domain candidates (TaskClass::dd_space, kbhip_session.cpp
+// dedup_space): of the block's nodes of one domain of the space only the one
+// with the largest key stays (keys are unique: they carry the node index);
+// nodes without the topology key stay as they are.  The block's list then
+// holds at most one node per domain, so the pop's 64 candidates reach across
+// up to 64 domains instead of stopping at the first few domains' best nodes.
+template <typename KT, int R>
+__device__ __forceinline__ void dedup_domains(const NodeCols& nc, int space, int bid, KT (&keys)[R]) {
+    __shared__ KT dmax[kDedupMax];
+    for (int i = threadIdx.x; i < kDedupMax; i += kPopThreads) dmax[i] = 0;
+    __syncthreads();
+    int d[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int n = (bid * R + r) * kPopThreads + threadIdx.x;
+        d[r] = (keys[r] != 0 && n < nc.n) ? dom_of(nc, space, n) : -1;
+        if (d[r] >= 0) {
+            if constexpr (sizeof(KT) == 8) atomicMax((unsigned long long*)&dmax[d[r]], (unsigned long long)keys[r]);
+            else atomicMax((unsigned int*)&dmax[d[r]], (unsigned int)keys[r]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (d[r] >= 0 && dmax[d[r]] != keys[r]) keys[r] = 0;
+}
+
 // The batched pop's body: block `bid` of `nb_` (k_pop_batch: the grid's own;
 // k_pop_batch_multi: one session's blocks within a multi-session grid).
 template <int R, typename KT, int PL>
@@ -371,6 +398,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
     // 1. evaluate R nodes per lane, wave top-64, block top-64
     KT best = 0;
     uint32_t fbs[R];
+    KT keys[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int n = (bid * R + r) * kPopThreads + threadIdx.x;
@@ -383,7 +411,14 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
             else if constexpr (PL == 7) k = sweep_key<KT>(eval_node_aff(cf, c, t, nc, n, 0, 0, -1, &s, &passed, &fbs[r]), a);
             else k = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
         }
-        k = wave_sort_desc(k);
+        keys[r] = k;
+    }
+    if constexpr (PL == 7) {
+        if (c.dd_space >= 0) dedup_domains<KT, R>(nc, c.dd_space, bid, keys);  // uniform: the pop's class
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const KT k = wave_sort_desc(keys[r]);
         best = r == 0 ? k : wave_merge_desc(best, k);
     }
     wlk[wave][lane] = best;

@@ -135,6 +135,31 @@ struct HPod {
 static inline bool on_node_of(const HPod& p) {
     return p.node >= 0 && !p.detached && p.status != Succeeded && p.status != Failed;
 }
+// Placement 7's per-domain candidates (kbhip_batch.h place_aff): the sweep may
+// keep only the best node of each domain of topology space S when every
+// count the class's predicates read is indexed by S-domain (its EA pairs and
+// PAA on space S) and an Allocated placement adds to one of those counts in
+// its own domain (a self-matching anti-affinity term): a node beaten by one
+// of its domain fails exactly when that one does, or ranks below it.  -1:
+// the class keeps plain candidates.  space_ndom: domains per space.
+static int32_t dedup_space(const AffProgram& pg, const vector<int>& space_ndom) {
+    if (pg.pa_space >= 0 || !pg.ipa.empty() || pg.pred_err) return -1;
+    int32_t sp = pg.paa_space;
+    vector<int32_t> offs;
+    if (pg.paa_space >= 0) offs.push_back(pg.paa_cnt);
+    for (size_t k = 0; k + 1 < pg.ea.size(); k += 2) {
+        if (sp < 0) sp = pg.ea[k];
+        if (pg.ea[k] != sp) return -1;
+        offs.push_back(pg.ea[k + 1]);
+    }
+    if (sp < 0 || sp >= (int32_t)space_ndom.size() || space_ndom[sp] > kDedupMax) return -1;
+    for (size_t k = 0; k + 2 < pg.upd.size(); k += 3)
+        if (pg.upd[k] == UPD_CNT_ALLOC && pg.upd[k + 1] == sp &&
+            std::find(offs.begin(), offs.end(), pg.upd[k + 2]) != offs.end())
+            return sp;
+    return -1;
+}
+
 struct HJob {  // session jobs are numbered in UID order
     int queue = -1;
     int32_t min_avail = 0, priority = 0;
@@ -483,6 +508,8 @@ struct Session {
     bool force_radix = false;  // option "rank_radix": the wide-range radix passes for every class (tests)
     bool bf_batch = true;      // option "bf_batch": batched pops (placement 6) in sessions with Backfilled nodes
     bool aff_batch = true;     // option "aff_batch": batched pops (placement 7) of anti-affinity classes
+    bool aff_fence = true;     // option "aff_fence": placement-7 pops ordered behind overlapped ones on the
+                               // device (ov_fence) instead of a host drain
     bool rank_group = false;   // option "rank_group": a what-if session of the lockstep group (StepBatcher)
     hipEvent_t ev_pop = nullptr;  // this session's stream before a StepBatcher pop request
     vector<vector<int>> node_tasks;  // NodeInfo.Tasks (pod indices, pinned order), rebuilt per evicting action
@@ -572,6 +599,7 @@ struct Session {
     int64_t sweep_launches = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_nonov = nullptr;  // after a non-overlapped batched pop: the next overlapped one waits for it
+    hipEvent_t ev_fence[kMaxDep + 1] = {};  // ov_fence: the overlap streams' ends, waited on by the session stream
     bool nonov_pending = false;
     double timed_ms = 0;          // summed duration of the timed sweep launches
     hipEvent_t ev_sweep[2] = {nullptr, nullptr};  // kbhip_sweep_scores' standalone sweep (time_every > 0)
@@ -627,6 +655,8 @@ struct Session {
         comm_bad = false;
         for (hipEvent_t* e : {&ev0, &ev1, &ev_run[0], &ev_run[1], &ev_nonov, &ev_pop, &ev_sweep[0], &ev_sweep[1]})
             if (*e) { (void)hipEventDestroy(*e); *e = nullptr; }
+        for (auto& e : ev_fence)
+            if (e) { (void)hipEventDestroy(e); e = nullptr; }
         for (auto& pr : ev_ring)
             for (auto& e : pr)
                 if (e) { (void)hipEventDestroy(e); e = nullptr; }
@@ -1252,6 +1282,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
                 if (S.pods[i].detached) fail_unsupported("detached pods (p_detached) in a session with pod (anti-)affinity");
     }
     vector<int32_t> aff_items;
+    // domains per topology space (placement 7's per-domain candidates, dedup_space)
+    vector<int> space_ndom(aff.active ? aff.n_spaces : 0, 0);
+    for (int sp = 0; sp < (int)space_ndom.size(); ++sp)
+        for (int n = 0; n < N; ++n) space_ndom[sp] = std::max(space_ndom[sp], aff.dom[(size_t)sp * npad + n] + 1);
 
     mark("affinity");
     // ---------------- task classes for pending tasks ----------------
@@ -1444,8 +1478,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             c.paa_space = pg->paa_space; c.paa_cnt = pg->paa_cnt;
             c.ipa_n = (int32_t)pg->ipa.size() / 4;
             c.upd_n = (int32_t)pg->upd.size() / 3;
+            c.dd_space = dedup_space(*pg, space_ndom);
         } else {
             c.pa_space = c.paa_space = -1;
+            c.dd_space = -1;
         }
         // class signature: the task-relative tables + the class fields (offsets are local)
         string sig((const char*)&c, sizeof(TaskClass));
@@ -2046,6 +2082,21 @@ static void ov_drain(Session& S) {
 // batched pop, which the overlap chain does not order).
 static void ov_quiesce(Session& S) { ov_drain(S); }
 
+// The device-side form of ov_quiesce for a non-overlapped batched pop on the
+// session stream (placement 7): that stream waits for the end of every
+// overlap stream's work, without the host waiting.  Row messages of earlier
+// pops go stale as after a drain (the pop writes rows outside their
+// candidate lists); the overlapped pops after it wait for it (ev_nonov).
+static void ov_fence(Session& S) {
+    S.msg_from = S.ov_seq + 1;
+    if (!S.ov_pending) return;
+    for (int k = 1; k <= S.overlap; ++k) {
+        if (!S.ev_fence[k]) HIPCHK(hipEventCreateWithFlags(&S.ev_fence[k], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(S.ev_fence[k], S.ov_streams[k]));
+        HIPCHK(hipStreamWaitEvent(S.stream, S.ev_fence[k], 0));
+    }
+}
+
 // Nothing but the winner's row can change between the chunk's tasks: the
 // condition under which one sweep serves a whole chunk (kbhip_kernels.hip).
 // Duration of the timed launch in event pair k (waits for it if needed).
@@ -2168,7 +2219,12 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     const bool grouped = S.rank_group && S.world == 1;
     L.aff = !L.bf && (S.classes[cls].aff || grouped);
     const bool ov = S.overlap > 0 && S.world == 1 && !L.bf && !L.aff;
-    if (!ov) ov_quiesce(S);
+    // a placement-7 pop between overlapped ones is ordered on the device (ov_fence), so the
+    // host can keep predicted pops queued behind it; the other non-overlapped pops drain
+    if (!ov) {
+        if (L.aff && S.world == 1 && !grouped && S.overlap > 0 && S.aff_fence) ov_fence(S);
+        else ov_quiesce(S);
+    }
 
     const uint32_t seq = ov ? S.ov_seq + 1 : 0;
     const int si = ov ? (int)(seq % (uint32_t)(S.overlap + 1)) : 0;  // pop seq-overlap-1 ran on it before
@@ -3302,9 +3358,12 @@ struct Allocator {
     }
     // JobInfo.UpdateTaskStatus (job_info.go:251-264): the status index, and
     // AddTaskInfo's "job priority = this task's priority" (:242)
+    static bool gang_ready_status(int st) { return allocated_status(st) || st == Succeeded || st == Pipelined; }
     void set_status(int pi, int st) {
         HPod& p = S.pods[pi];
         HJob& j = S.jobs[p.job];
+        if (p.job < (int)ready_ok.size() && ready_ok[p.job])  // keep the cached readyTaskNum exact
+            ready_val[p.job] += (int)gang_ready_status(st) - (int)gang_ready_status(p.status);
         if (allocated_status(p.status)) j.cnt_alloc--;
         if (p.status == AOB) j.cnt_aob--;
         p.status = st;
@@ -3324,6 +3383,11 @@ struct Allocator {
     // The walk order of the task of class cls: preempt (by_score) = SelectBestNode order of
     // the nodes passing PredicateFn with a NodeOrderFn score; reclaim = passing nodes in order.
     void rank_nodes(int cls, bool by_score, vector<int>& out) {
+        const auto tr0 = std::chrono::steady_clock::now();
+        rank_nodes_inner(cls, by_score, out);
+        S.stats.evict_rank_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - tr0).count();
+    }
+    void rank_nodes_inner(int cls, bool by_score, vector<int>& out) {
         const int N = S.nc.n;
         if (!S.b_rank_sorted.p) {
             S.b_rank_keys.alloc<uint64_t>(N);
@@ -3473,22 +3537,33 @@ struct Allocator {
     // Session.Preemptable / Reclaimable (session_plugins.go:67-148): per tier the
     // intersection of the enabled plugins' victims; the first non-empty tier decides,
     // and once a plugin has answered later tiers only intersect further.
-    // per-call scratch keyed by job / queue slot, valid where stamp == the call's epoch
-    vector<uint32_t> ready_stamp, alloc_stamp;
+    // readyTaskNum per job (gang.go:212-222), computed on first use in an
+    // eviction action and kept exact by set_status (every status change of the
+    // action goes through it); reset at the start of each action
+    vector<uint8_t> ready_ok;
     vector<int> ready_val;
+    // per-call scratch keyed by job / queue slot, valid where stamp == the call's epoch
+    vector<uint32_t> alloc_stamp;
     vector<F3> alloc_val;
     uint32_t epoch = 0;
     vector<int> cand, inter;
+    vector<uint32_t> mark;  // pod -> epoch: membership in the plugin's answer (the tier intersection)
+    void reset_ready_cache() {
+        ready_ok.assign(S.jobs.size(), 0);
+        ready_val.assign(S.jobs.size(), 0);
+    }
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
         victims.clear();
+        S.stats.evict_visits++;
+        S.stats.evict_cands += (int64_t)evictees.size();
         if (evictees.empty()) return;  // every plugin returns nil for no candidates
         bool init = false;
-        if (ready_stamp.empty()) {
+        if (alloc_stamp.empty()) {
             const size_t J = S.jobs.size(), Q = S.queues.size();
-            ready_stamp.assign(J, 0); ready_val.assign(J, 0);
             alloc_stamp.assign(std::max(J, Q), 0); alloc_val.assign(std::max(J, Q), F3{});
+            mark.assign(S.pods.size(), 0);
         }
-        const uint32_t ep = ++epoch;  // readyTaskNum counts do not change within one call
+        if (ready_ok.size() != S.jobs.size()) reset_ready_cache();
         for (auto& tier : S.tiers) {
             for (auto& pl : tier) {
                 if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
@@ -3497,13 +3572,10 @@ struct Allocator {
                     for (int e : evictees) {
                         const int jb = S.pods[e].job;
                         const HJob& j = S.jobs[jb];
-                        if (ready_stamp[jb] != ep) {  // readyTaskNum (gang.go:212-222)
+                        if (!ready_ok[jb]) {  // readyTaskNum (gang.go:212-222)
                             int c = 0;
-                            for (int t : j.tasks) {
-                                const int st = S.pods[t].status;
-                                if (allocated_status(st) || st == Succeeded || st == Pipelined) ++c;
-                            }
-                            ready_stamp[jb] = ep;
+                            for (int t : j.tasks) c += gang_ready_status(S.pods[t].status);
+                            ready_ok[jb] = 1;
                             ready_val[jb] = c;
                         }
                         if (j.min_avail <= ready_val[jb] - 1 || j.min_avail == 1) cand.push_back(e);
@@ -3541,11 +3613,12 @@ struct Allocator {
                 if (!init) {
                     victims = cand;
                     init = true;
-                } else {
+                } else {  // victims in their order, kept where the plugin also answered them
+                    const uint32_t em = ++epoch;
+                    for (int c : cand) mark[c] = em;
                     inter.clear();
                     for (int v : victims)
-                        for (int c : cand)
-                            if (v == c) inter.push_back(v);
+                        if (mark[v] == em) inter.push_back(v);
                     victims.swap(inter);
                 }
             }
@@ -3595,7 +3668,20 @@ struct Allocator {
         std::sort(v.begin(), v.end(), [this](int a, int b) { return task_less(a, b); });
         return v;
     }
+    // host wall time of an eviction action minus its node rankings (stats.evict_walk_s)
+    struct WalkTimer {
+        Session& S;
+        std::chrono::steady_clock::time_point t0;
+        double rank0;
+        explicit WalkTimer(Session& s) : S(s), t0(std::chrono::steady_clock::now()), rank0(s.stats.evict_rank_s) {}
+        ~WalkTimer() {
+            S.stats.evict_walk_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() -
+                                    (S.stats.evict_rank_s - rank0);
+        }
+    };
     void preempt_action() {  // preempt.go:43-255
+        WalkTimer wt(S);
+        reset_ready_cache();
         GroupScope group(S.rank_group, StepBatcher::kRank);
         compile_orders();
         open_plugins();
@@ -3665,6 +3751,8 @@ struct Allocator {
         flush_evictions();
     }
     void reclaim_action() {  // reclaim.go:41-196
+        WalkTimer wt(S);
+        reset_ready_cache();
         GroupScope group(S.rank_group, StepBatcher::kRank);
         compile_orders();
         open_plugins();
@@ -4360,16 +4448,18 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
 // Anything else re-opens the session in place (same handle and options).
 // ---------------------------------------------------------------------------
 struct SavedOptions {
-    bool batched, keys32, bf_batch, aff_batch, rank_group, force_radix, debug_keys;
+    bool batched, keys32, bf_batch, aff_batch, aff_fence, rank_group, force_radix, debug_keys;
     int64_t time_every;
     int speculate, overlap, rank_first;
 };
 static SavedOptions save_options(const Session& S) {
-    return SavedOptions{S.batched, S.keys32, S.bf_batch, S.aff_batch, S.rank_group, S.force_radix, S.debug_keys,
+    return SavedOptions{S.batched, S.keys32, S.bf_batch, S.aff_batch, S.aff_fence, S.rank_group, S.force_radix,
+                        S.debug_keys,
                         S.time_every, S.speculate, S.overlap, S.rank_first};
 }
 static void restore_options(Session& S, const SavedOptions& o) {
     S.batched = o.batched; S.keys32 = o.keys32; S.bf_batch = o.bf_batch; S.aff_batch = o.aff_batch;
+    S.aff_fence = o.aff_fence;
     S.rank_group = o.rank_group; S.force_radix = o.force_radix; S.time_every = o.time_every;
     S.speculate = o.speculate; S.overlap = o.overlap; S.rank_first = o.rank_first;
     S.debug_keys = o.debug_keys;
@@ -4674,6 +4764,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
             if (ok) tol[t / 64] |= 1ULL << (t % 64);
         }
         c.pa_space = c.paa_space = -1;
+        c.dd_space = -1;
         // the class signature exactly as open_session builds it (no selector terms, no ports, no program)
         string sig((const char*)&c, sizeof(TaskClass));
         sig.append((const char*)tol.data(), tol.size() * sizeof(uint64_t));
@@ -4920,6 +5011,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         else if (std::strcmp(key, "rank_radix") == 0) s->s.force_radix = value != 0;
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
+        else if (std::strcmp(key, "aff_fence") == 0) s->s.aff_fence = value != 0;
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");

@@ -80,7 +80,11 @@ struct TaskClass {
     int32_t upd_off, upd_n;                // aff_items triples (type, space, off)
     int32_t pw_lo;  // host-port window: the class's conflict / own masks cover port words
                     // pw_lo .. pw_lo + kPortWin - 1 (port ids sorted by protocol, port, IP)
+    int32_t dd_space;  // placement 7: the topology space whose domains the batched sweep keeps one
+                       // candidate of (the class kills a domain by placing into it), -1: none
+    int32_t dd_pad;
 };
+constexpr int kDedupMax = 1024;  // domains of a dd_space (the sweep's per-block LDS table)
 constexpr int kPortWin = 4;  // port words a class's masks span (its ports' 256-id window)
 
 // Session-wide constants of the plugin configuration.

@@ -121,3 +121,24 @@ def test_c3_scaled_aff_batch(engine, oracle_mod, kbgen_mod, tmp_path):
     ref, ns0, st0, close0 = _run(engine, p, aff_batch=0)
     assert ref == got and np.array_equal(ns0, ns) and close0 == close
     assert st["sweeps"] < st0["sweeps"]
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_per_domain_candidates_pipelined(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Zone-self-anti-affine gangs (per-domain candidates, TaskClass dd_space)
+    on nodes whose Idle is mostly taken by Releasing pods: many placements are
+    Pipelined, which do not close their domain, so a launch ends after one and
+    the host goes on.  Records, node state and close messages equal the
+    faithful restatement's and the per-task path's."""
+    rng = np.random.default_rng(8800 + seed)
+    c = _anti_cluster(kbgen_mod, 8700 + seed, n_nodes=20 + 7 * (seed % 6), n_jobs=5 + seed % 6, n_zones=3 + seed % 4)
+    guarded = {q.node for q in c.pods if q.node is not None}
+    for i, n in enumerate(list(c.nodes)):
+        if rng.random() < 0.85:  # a deleting pod holding most of the node: mostly Pipelined fits
+            free = 1000 if n.name in guarded else 0
+            c.add_pod("ns", f"rel{i}", uid=f"q{i:05d}", node=n.name, phase="Running", deleting=True,
+                      containers=[kbgen_mod.res(cpu=n.cpu - free - 600 - 1000 * int(rng.integers(0, 2)),
+                                                mem=n.mem - GI - GI // 2 - GI * int(rng.integers(0, 3)))])
+    p = c.write(str(tmp_path / "p.kbs"))
+    st, st0 = _check(engine, oracle_mod, p)
+    assert st["batched_pops"] >= st0["batched_pops"]
