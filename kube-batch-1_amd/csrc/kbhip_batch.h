@@ -1058,8 +1058,13 @@ __device__ __forceinline__ void st_sys16(void* p, kb_u32x4 v) {
 // host ports leaves the port words out — each wave drains its stores, the
 // block meets, and lane p of wave 0 raises rank p's flag.  k_shard_place
 // reads them with system-scope loads.
+// SC1: the rows are read through sc1 (an overlapped shard sweep: some of its
+// candidates were just written back by the previous pop's placement on this
+// device, from another XCD).  bad: the chain broke; the message says so
+// (count word 0xffffffff) and k_shard_place reports a lost exchange.
+template <bool SC1 = false>
 __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c, uint64_t K,
-                           uint32_t fit_raw, ShardMsg* msg, const MboxArgs& mb) {
+                           uint32_t fit_raw, ShardMsg* msg, const MboxArgs& mb, bool bad = false) {
     __shared__ ShardCand s_c[kTopK];
     __shared__ uint64_t s_fit[2];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1071,12 +1076,13 @@ __device__ void shard_emit(const Conf& cf, const NodeCols& nc, const DevTables& 
             const int n = g - nc.base;
             e.key = K;
             e.node = g;
-            e.row = load_row(nc, n);
+            e.row = load_row_t<SC1>(nc, n);
             if (c.has_ports)
-                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) e.pw[w] = nc.ports[port_at(c, nc, w, n)];
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) e.pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
             e.na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
         }
-        const uint32_t sweep = fit_sum(fit_raw);  // count b in lane b
+        uint32_t sweep = fit_sum(fit_raw);  // count b in lane b
+        if (bad && lane == 0) sweep = 0xffffffffu;
         if (mb.world == 0) {
             msg->c[lane] = e;
             if (lane < 4) msg->fit[lane] = sweep;

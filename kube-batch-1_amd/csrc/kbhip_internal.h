@@ -110,7 +110,7 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
                               int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
                               const ShardMsg* msgs, int world, void* out_dev, hipStream_t st,
-                              const uint64_t* flags = nullptr, uint32_t seq = 0);
+                              const uint64_t* flags = nullptr, uint32_t seq = 0, struct PopLink* link = nullptr);
 // Chain state of overlapped batched pops (kbhip_kernels.hip, k_pop_batch_ov):
 // done = sequence number of the last pop whose node write-back is visible;
 // touched[e % kLinkSlots][i] = {e << 32 | node}, candidate i of pop e (node
@@ -134,6 +134,16 @@ struct PopLink {
     uint64_t touched[kLinkSlots][64];
     uint64_t rows[kLinkSlots][kRowWords][64];
 };
+// Overlapped shard pops (mailbox exchange): this shard's sweep of pop mb.seq
+// beside pop mb.seq-1's k_shard_place (launch_shard_place with `link`), whose
+// candidates it leaves out and then re-evaluates once that pop's write-back on
+// this device is done (prev_chained: pop mb.seq-1 ran as such a pop and
+// published its candidates in `link`).  Sends the shard's message like
+// placement 3.
+hipError_t launch_shard_sweep_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, const TaskClass& cl,
+                                 int n_tasks, int gang_mode, int min_avail, int ready_count, uint32_t epoch,
+                                 uint64_t* cand, uint32_t* arrive, const KeyFormat& kf, int fit_set, PopLink* link,
+                                 int prev_chained, const MboxArgs& mb, hipStream_t st);
 // Overlapped batched pop number `seq` (>= 1) on stream st; pop seq-1 may
 // still run on the other stream: it leaves that pop's candidates out of its
 // sweep and re-evaluates them once pop seq-1's write-back is done.  cand

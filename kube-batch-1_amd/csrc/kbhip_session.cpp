@@ -623,6 +623,9 @@ struct Session {
     int mbox_kind = 0;                         // its allocation (0 uncached, 1 fine-grained, 2 default)
     Mailbox* mbox_peer[kMaxWorld] = {};        // and every rank's as mapped here (own included)
     uint32_t mbox_seq = 0;                     // sequence number of the last batched pop sent
+    uint32_t sh_chained_seq = 0;               // the last overlapped shard pop (k_shard_sweep_ov), 0: none
+    bool shard_overlap = true;                 // option "shard_overlap": overlapped shard pops (with "overlap" > 0)
+    bool chain_fence = false;                  // device work ran on the session stream after the last drain
     vector<uint8_t> h_shard;                   // host staging of the host all-gather
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
     bool encode_only = false;
@@ -2072,6 +2075,7 @@ static void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
     S.msg_from = S.ov_seq + 1;  // device work outside the chain may follow: earlier row messages go stale
+    S.chain_fence = true;       // ... on the session stream: the next chained pop is ordered after it
     if (!S.ov_pending) return;
     for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
     HIPCHK(hipStreamSynchronize(S.stream));
@@ -2219,9 +2223,11 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     const bool grouped = S.rank_group && S.world == 1;
     L.aff = !L.bf && (S.classes[cls].aff || grouped);
     const bool ov = S.overlap > 0 && S.world == 1 && !L.bf && !L.aff;
+    // node-array shard over peer mailboxes: pop e's sweep beside pop e-1's placement (k_shard_sweep_ov)
+    const bool shov = S.overlap > 0 && S.world > 1 && S.mbox_own && S.shard_overlap && !L.bf && !L.aff;
     // a placement-7 pop between overlapped ones is ordered on the device (ov_fence), so the
     // host can keep predicted pops queued behind it; the other non-overlapped pops drain
-    if (!ov) {
+    if (!ov && !shov) {
         if (L.aff && S.world == 1 && !grouped && S.overlap > 0 && S.aff_fence) ov_fence(S);
         else ov_quiesce(S);
     }
@@ -2233,16 +2239,44 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     // sweep runs beside the previous pop, ordered after the pop before that by
     // its stream): after a non-overlapped batched pop (stream 0), every
     // overlap stream waits for that pop's end before its next launch
-    if (ov && S.nonov_pending) {
-        for (int k = 0; k <= S.overlap; ++k) HIPCHK(hipStreamWaitEvent(S.ov_streams[k], S.ev_nonov, 0));
+    if ((ov || shov) && S.chain_fence && !S.nonov_pending) {  // work issued after a drain (the per-task path)
+        if (!S.ev_nonov) HIPCHK(hipEventCreateWithFlags(&S.ev_nonov, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(S.ev_nonov, S.stream));
+        S.nonov_pending = true;
+    }
+    if ((ov || shov) && S.nonov_pending) {
+        for (int k = 0; k <= std::max(S.overlap, 1); ++k) HIPCHK(hipStreamWaitEvent(S.ov_streams[k], S.ev_nonov, 0));
         S.nonov_pending = false;
     }
+    if (ov || shov) S.chain_fence = false;
     L.fit = !L.bf && !L.aff;
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
     const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
-    if (S.world > 1 && S.mbox_own) {  // node-array shard, peer mailboxes: no host step between the two kernels
+    if (shov) {  // overlapped shard pops: both kernels on stream seq % 2, chained to pop seq-1 on the device
+        MboxArgs mb{};
+        for (int p = 0; p < S.world; ++p) mb.dst[p] = S.mbox_peer[p];
+        mb.rank = S.rank;
+        mb.world = S.world;
+        mb.seq = ++S.mbox_seq;
+        S.stats.collectives++;
+        const int si = (int)(mb.seq & 1u);
+        L.st = S.ov_streams[si];
+        if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
+        const int prev_chained = S.sh_chained_seq != 0 && S.sh_chained_seq == mb.seq - 1;
+        HIPCHK(launch_shard_sweep_ov(S.conf, S.nc, S.tab, cls, S.classes[cls], m, gang_mode, min_avail, ready_count,
+                                     L.epoch, S.d_cand_ov[si], S.d_arrive_ov[si], kf, S.fit_set[si], S.d_link,
+                                     prev_chained, mb, L.st));
+        if (L.timed) HIPCHK(hipEventRecord(ev[1], L.st));  // timed: the shard's sweep kernel
+        S.fit_set[si] ^= 1;
+        const int slot = (int)(mb.seq & (kMboxSlots - 1));
+        HIPCHK(launch_shard_place(S.conf, S.nc, S.tab, cls, m, gang_mode, min_avail, ready_count, L.epoch, kf,
+                                  &S.mbox_own->msg[slot][0], S.world, out, L.st, &S.mbox_own->flag[slot][0][0],
+                                  mb.seq, S.d_link));
+        S.sh_chained_seq = mb.seq;
+        S.ov_pending = true;
+    } else if (S.world > 1 && S.mbox_own) {  // node-array shard, peer mailboxes: no host step between the two kernels
         MboxArgs mb{};
         for (int p = 0; p < S.world; ++p) mb.dst[p] = S.mbox_peer[p];
         mb.rank = S.rank;
@@ -4448,18 +4482,20 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
 // Anything else re-opens the session in place (same handle and options).
 // ---------------------------------------------------------------------------
 struct SavedOptions {
-    bool batched, keys32, bf_batch, aff_batch, aff_fence, rank_group, force_radix, debug_keys;
+    bool batched, keys32, bf_batch, aff_batch, aff_fence, shard_overlap, rank_group, force_radix, debug_keys;
     int64_t time_every;
     int speculate, overlap, rank_first;
 };
 static SavedOptions save_options(const Session& S) {
-    return SavedOptions{S.batched, S.keys32, S.bf_batch, S.aff_batch, S.aff_fence, S.rank_group, S.force_radix,
+    return SavedOptions{S.batched, S.keys32, S.bf_batch, S.aff_batch, S.aff_fence, S.shard_overlap, S.rank_group,
+                        S.force_radix,
                         S.debug_keys,
                         S.time_every, S.speculate, S.overlap, S.rank_first};
 }
 static void restore_options(Session& S, const SavedOptions& o) {
     S.batched = o.batched; S.keys32 = o.keys32; S.bf_batch = o.bf_batch; S.aff_batch = o.aff_batch;
     S.aff_fence = o.aff_fence;
+    S.shard_overlap = o.shard_overlap;
     S.rank_group = o.rank_group; S.force_radix = o.force_radix; S.time_every = o.time_every;
     S.speculate = o.speculate; S.overlap = o.overlap; S.rank_first = o.rank_first;
     S.debug_keys = o.debug_keys;
@@ -5012,6 +5048,13 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         else if (std::strcmp(key, "bf_batch") == 0) s->s.bf_batch = value != 0;
         else if (std::strcmp(key, "aff_batch") == 0) s->s.aff_batch = value != 0;
         else if (std::strcmp(key, "aff_fence") == 0) s->s.aff_fence = value != 0;
+        else if (std::strcmp(key, "shard_overlap") == 0) {
+            if (!s->s.encode_only) {
+                HIPCHK(hipSetDevice(s->s.device));
+                kbhip::ov_quiesce(s->s);
+            }
+            s->s.shard_overlap = value != 0;
+        }
         else if (std::strcmp(key, "rank_group") == 0) s->s.rank_group = value != 0;
         else if (std::strcmp(key, "rank_first") == 0) {  // reclaim / preempt: keys read back with the count
             if (value < 1) throw kbhip::Error(KBHIP_EINVAL, "rank_first must be >= 1");

@@ -32,8 +32,11 @@ def main():
         mark("session open")
         exchange = os.environ.get("KBHIP_TEST_EXCHANGE", "host")
         s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched and exchange == "host" else None)
-        if batched and exchange == "mailbox":  # batched pops through the peer mailboxes
+        if batched and exchange in ("mailbox", "mailbox_serial"):  # batched pops through the peer mailboxes
             s.connect_mailbox(kbhip.torch_gather())
+            # "mailbox": a shard's sweep of pop e beside pop e-1's placement (the default);
+            # "mailbox_serial": sweep, exchange and placement one after another
+            s.set_option("shard_overlap", 0 if exchange == "mailbox_serial" else 1)
         info = s.info()
         pod, node, kind = s.run_actions(actions)
         if os.environ.get("KBHIP_TEST_CARRY") is not None:  # carry over (deleting the listed pods), run again

@@ -111,11 +111,12 @@ def test_sharded_close_messages_gpu(engine, oracle_mod, kbgen_mod, tmp_path, see
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["host", "mailbox"])
+@pytest.mark.parametrize("exchange", ["host", "mailbox", "mailbox_serial"])
 @pytest.mark.parametrize("seed", range(8))
 def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, exchange):
     """Batched-path features only (no pod affinity / backfill): every pop is
-    one exchange — a host all-gather, or the peer mailboxes (kernels only)."""
+    one exchange — a host all-gather, or the peer mailboxes (kernels only;
+    a shard's sweep of the next pop beside the placement, or serial)."""
     from test_gpu_parity import NO_POD_AFFINITY
     feats = tuple(f for f in NO_POD_AFFINITY if f != "backfill")
     c = kbgen_mod.gen_random(2400 + seed, n_nodes=10 + seed * 7, n_jobs=8, max_tasks=8, features=feats,
@@ -153,7 +154,7 @@ def test_sharded_carry_gpu(engine, kbgen_mod, tmp_path, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["host", "mailbox"])
+@pytest.mark.parametrize("exchange", ["host", "mailbox", "mailbox_serial"])
 def test_sharded_c4_scaled_gpu(engine, kbgen_mod, tmp_path, exchange):
     """C4 shape at 20k nodes (2 and 3 ranks sharing the GPU): the shard logs
     and close messages equal the one-GPU session's, and every batched pop is
