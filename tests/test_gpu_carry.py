@@ -209,6 +209,11 @@ def test_carry_events_detach_refused_with_pod_affinity(engine, kbgen_mod, tmp_pa
     node0 = sorted(n.name for n in c.nodes)[0]
     c.add_pod("default", "solo", uid="zsolo", group=None, node=node0, phase="Running",
               containers=[{"cpu": 100, "mem": 1 << 20}])
+    c.add_job("default", "anti", sorted(q.name for q in c.queues)[0], min_member=1, ts=99)
+    c.add_pod("default", "anti-0", uid="zanti", group="anti", ts=99, labels={"app": "anti"},
+              containers=[{"cpu": 100, "mem": 1 << 20}],
+              affinity={"anti": {"required": [{"selector": {"ml": {"app": "anti"}},
+                                               "topology_key": "kubernetes.io/hostname"}]}})
     p1 = c.write(str(tmp_path / "s1.kbs"))
     solo = sorted(q.uid for q in c.pods).index("zsolo")
     with engine.Session(p1) as s:

@@ -57,3 +57,28 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
     assert sreq >= n_sessions and sbsum >= sreq  # every session's backfill chunk went through the group
     if n_sessions > 2:
         assert sbsum > sreq  # some sweep launch served several sessions' chunks
+
+
+def test_whatif_full_size_grouped(engine, kbgen_mod, tmp_path):
+    """C5 at full size (50k nodes ~90 % filled, 2k-task pending sets): four
+    grouped sessions run concurrently record exactly what each records alone
+    (tests/test_gpu_evict.py pins the session alone against the hoisted
+    restatement at full size)."""
+    import os
+    cache = os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench")
+    os.makedirs(cache, exist_ok=True)
+    paths = []
+    for k in range(4):  # bench_c5.py's snapshots (same names): generated once per box
+        p = os.path.join(cache, f"c5_50000_2000_{k}.kbs")
+        if not os.path.exists(p):
+            kbgen_mod.gen_c5(p + ".tmp", seed=kbgen_mod.BASE_SEED + 5 + k, n_nodes=50_000, n_pending=2000)
+            os.replace(p + ".tmp", p)
+        paths.append(p)
+    alone = [_run(engine, p, False)[0] for p in paths]
+    bar = threading.Barrier(len(paths))
+    with ThreadPoolExecutor(len(paths)) as ex:
+        res = list(ex.map(lambda p: _run(engine, p, True, bar), paths))
+    for a, (got, st) in zip(alone, res):
+        assert len(got) > 100_000
+        assert got == a
+    assert sum(st["rank_batch_sum"] for _, st in res) > sum(st["rank_requests"] for _, st in res)
