@@ -939,12 +939,29 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
             }
         }
     }
+    // the class's commit updates as this lane's node would apply them (commit_aff): table slot
+    // (offset + the node's domain; -1: the node lacks the key) — loaded once, off the task loop
+    int32_t uslot[kAffUpd];
+    const int n_upd = c.upd_n;
+#pragma unroll
+    for (int u = 0; u < kAffUpd; ++u) {
+        uslot[u] = -1;
+        if (u < n_upd && n >= 0) {
+            const int32_t* it = t.aff_items + c.upd_off + 3 * u;
+            const int d = it[0] == 0 ? dom_g(nc, it[1], n) : 0;
+            if (d >= 0) uslot[u] = it[2] + d;
+        }
+    }
+    int32_t utype[kAffUpd];  // uniform: the class's items
+#pragma unroll
+    for (int u = 0; u < kAffUpd; ++u) utype[u] = u < n_upd ? t.aff_items[c.upd_off + 3 * u] : -1;
     if (n >= 0) {
         r = load_row(nc, n);
         if (c.has_ports)
             for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
+    int wins_alloc = 0, wins_pipe = 0;  // this lane's node: placements (the device tables after the loop)
     const uint64_t t0 = readlane64(K, 63);  // the list's last key (0: the list holds every feasible node)
     uint64_t key = K;
     bool changed = false;
@@ -958,34 +975,23 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         const int wl = __ffsll((unsigned long long)__ballot(win)) - 1;
         const int kind = key_kind(w);
         // the winner's count-table updates (UPD_CNT_ALLOC: Allocated only), as slots
-        for (int u = 0; u < c.upd_n; ++u) {
-            const int32_t* it = t.aff_items + c.upd_off + 3 * u;
-            int us = -1;
-            if (win && it[0] == 0 && kind == 1) {
-                const int d = dom_g(nc, it[1], n);
-                if (d >= 0) us = it[2] + d;
-            }
-            us = __builtin_amdgcn_readlane(us, wl);
-            if (us >= 0) {
+        if (kind == 1) {
 #pragma unroll
-                for (int k = 0; k < kAffItems; ++k) cnt[k] += (slot[k] == us) ? 1 : 0;
+            for (int u = 0; u < kAffUpd; ++u) {
+                if (utype[u] != 0) continue;  // (uniform)
+                const int us = __builtin_amdgcn_readlane(uslot[u], wl);
+                if (us >= 0) {
+#pragma unroll
+                    for (int k = 0; k < kAffItems; ++k) cnt[k] += (slot[k] == us) ? 1 : 0;
+                }
             }
         }
         bool aff_ok = true;
 #pragma unroll
         for (int k = 0; k < kAffItems; ++k) aff_ok = aff_ok && !(slot[k] >= 0 && cnt[k] > 0);
         if (win) {
-            // the device tables (later launches read them): atomics, since winners of
-            // successive tasks are different lanes and may update the same entries
-            for (int u = 0; u < c.upd_n; ++u) {
-                const int32_t* it = t.aff_items + c.upd_off + 3 * u;
-                const bool to_cnt = it[0] == 0;
-                const int d = to_cnt ? dom_g(nc, it[1], n) : 0;
-                const bool apply = (it[0] == 2 || kind == 1) && d >= 0;
-                int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
-                __hip_atomic_fetch_add(tab + it[2] + (d >= 0 ? d : 0), apply ? 1 : 0, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (kind == 1) ++wins_alloc;
+            else ++wins_pipe;
             r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
             if (c.has_ports)
                 for (int q = 0; q < 4; ++q) pw[q] |= (q < port_win(c, nc)) ? t.masks[c.pown_off + q] : 0;
@@ -1011,6 +1017,15 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         nc.nzm[n] = r.nzm;
         if (c.has_ports)
             for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, n)] = pw[w];
+        // the device tables (later launches read them; commit_aff per placement): every winning
+        // lane adds its placements at once — atomics, since lanes may share entries
+#pragma unroll
+        for (int u = 0; u < kAffUpd; ++u) {
+            const int add = utype[u] == 2 ? wins_alloc + wins_pipe : wins_alloc;
+            if (uslot[u] >= 0 && add > 0)
+                __hip_atomic_fetch_add((utype[u] == 0 ? t.aff_cnt : t.aff_scalar) + uslot[u], add, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if (lane < done || (done == 0 && lane == 0))
         __hip_atomic_store(&out->g[lane],

@@ -20,6 +20,9 @@ struct DevTables {
     const int32_t* aff_items;  // programs: ea pairs, ipa quads, upd triples
     int32_t* aff_cnt;          // count tables, indexed cnt_off + domain
     int32_t* aff_scalar;       // PA target totals, session counters
+    // placement 7 with per-domain candidates: the best key of every domain of the
+    // class's dd_space over all blocks (kDedupMax entries; zero between launches)
+    uint64_t* dd_max;
 };
 
 // The per-task path's control block set up on the device (CtrlInit, kbhip_types.h).

@@ -346,16 +346,26 @@ struct PopDescs {
 };
 static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed the kernel argument space");
 
+// The node index of a selection key.
+template <typename KT>
+__device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
+    if constexpr (sizeof(KT) == 8) return key_idx(k);
+    else return a.kidxmax - (int)((k >> 1) & (uint32_t)a.kidxmax);
+}
+
 // Placement 7 with per-domain candidates (TaskClass::dd_space, kbhip_session.cpp
 // dedup_space): of the block's nodes of one domain of the space only the one
 // with the largest key stays (keys are unique: they carry the node index);
 // nodes without the topology key stay as they are.  The block's list then
 // holds at most one node per domain, so the pop's 64 candidates reach across
 // up to 64 domains instead of stopping at the first few domains' best nodes.
+// Every block also adds its domain maxima to the session's dd_max table, from
+// which the final merger takes the best node of every domain (dedup_final).
 template <typename KT, int R>
-__device__ __forceinline__ void dedup_domains(const NodeCols& nc, int space, int bid, KT (&keys)[R]) {
+__device__ __forceinline__ void dedup_domains(const NodeCols& nc, const DevTables& t, int space, int ndom, int bid,
+                                              KT (&keys)[R]) {
     __shared__ KT dmax[kDedupMax];
-    for (int i = threadIdx.x; i < kDedupMax; i += kPopThreads) dmax[i] = 0;
+    for (int i = threadIdx.x; i < ndom; i += kPopThreads) dmax[i] = 0;
     __syncthreads();
     int d[R];
 #pragma unroll
@@ -371,6 +381,34 @@ __device__ __forceinline__ void dedup_domains(const NodeCols& nc, int space, int
 #pragma unroll
     for (int r = 0; r < R; ++r)
         if (d[r] >= 0 && dmax[d[r]] != keys[r]) keys[r] = 0;
+    for (int i = threadIdx.x; i < ndom; i += kPopThreads) {  // (drained before the block arrives)
+        const KT v = dmax[i];
+        if (v) atomicMax((unsigned long long*)&t.dd_max[i], (unsigned long long)v);
+    }
+}
+
+// The final merger of a placement-7 pop with per-domain candidates (wave 0):
+// the merged list keeps its nodes without the topology key; every domain
+// contributes its best node from dd_max (all blocks added theirs before they
+// arrived), which is reset for the next launch.  The top 64 of those: at most
+// one node per domain.
+template <typename KT>
+__device__ __forceinline__ KT dedup_final(const NodeCols& nc, const DevTables& t, const TaskClass& c, const PopArgs& a,
+                                          KT k) {
+    const int lane = threadIdx.x & 63;
+    const int nd = k ? key_node(k, a) : -1;
+    const bool keep = nd >= 0 && dom_g(nc, c.dd_space, nd) < 0;
+    KT acc = wave_sort_desc(keep ? k : (KT)0);
+    for (int j0 = 0; j0 < c.dd_ndom; j0 += 64) {
+        const int j = j0 + lane;
+        uint64_t v = 0;
+        if (j < c.dd_ndom) {
+            v = ld_sc1(&t.dd_max[j]);
+            if (v) st_sc1(&t.dd_max[j], (uint64_t)0);
+        }
+        acc = wave_merge_desc(acc, wave_sort_desc((KT)v));
+    }
+    return acc;
 }
 
 // The batched pop's body: block `bid` of `nb_` (k_pop_batch: the grid's own;
@@ -414,7 +452,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
         keys[r] = k;
     }
     if constexpr (PL == 7) {
-        if (c.dd_space >= 0) dedup_domains<KT, R>(nc, c.dd_space, bid, keys);  // uniform: the pop's class
+        if (c.dd_space >= 0) dedup_domains<KT, R>(nc, t, c.dd_space, c.dd_ndom, bid, keys);  // uniform: the pop's class
     }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -438,6 +476,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
         put_list(cand + (int64_t)bid * 64, wlk[0][lane]);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    if constexpr (PL == 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's dd_max atomics
     __syncthreads();
     STAMP(bid * 4 + 2);
     if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
@@ -480,6 +519,12 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
     __syncthreads();
     block_tree_merge(wlk, wave, lane);
     STAMP(nb_ * 4 + 0);
+    if constexpr (PL == 7) {
+        if (c.dd_space >= 0) {  // (uniform)
+            if (wave == 0) wlk[0][lane] = dedup_final<KT>(nc, t, c, a, wlk[0][lane]);
+            __syncthreads();
+        }
+    }
     if constexpr (sizeof(KT) != 8) {  // placement works on 64-bit keys
         const uint64_t k64 = key64_of(wlk[0][lane], a);
         __syncthreads();
@@ -548,11 +593,6 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_multi(PopDescs d) {
 // store each, no flag); rows as sc1 stores drained before the sc1 done flag,
 // read with sc1 loads (MI355X_MICROARCH.md valid forms, R2 and row 1).
 // ---------------------------------------------------------------------------
-template <typename KT>
-__device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
-    if constexpr (sizeof(KT) == 8) return key_idx(k);
-    else return a.kidxmax - (int)((k >> 1) & (uint32_t)a.kidxmax);
-}
 
 constexpr long kLinkSpin = 1L << 21;  // poll bound (~1 s): a broken chain ends the pop with an error
 
@@ -1102,13 +1142,49 @@ struct UndoArgs {
     int32_t node[kMaxChunk];
     int32_t kind[kMaxChunk];
 };
+// One lane per task, every update an atomic add: the inverse updates commute
+// (a node may appear several times), so the pop's tasks are retracted side by
+// side instead of as one lane's chain of dependent read-modify-writes.
+template <typename T>
+__device__ __forceinline__ void atomic_add_dev(T* p, T v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __global__ __launch_bounds__(64) void k_undo_pop(NodeCols nc, DevTables t, UndoArgs u) {
-    if (threadIdx.x != 0) return;
+    const int i = threadIdx.x;
+    if (i >= u.n) return;
     const TaskClass c = t.classes[u.cls];
-    for (int i = 0; i < u.n; ++i) {
-        if (u.node[i] - nc.base >= 0 && u.node[i] - nc.base < nc.n)  // this shard's rows only
-            uncommit_node(c, t, nc, u.node[i] - nc.base, u.kind[i]);
-        if (c.aff && u.node[i] >= 0) uncommit_aff(c, t, nc, u.node[i], u.kind[i]);  // replicated tables
+    const int g = u.node[i], kind = u.kind[i];
+    const int n = g - nc.base;
+    if (g >= 0 && n >= 0 && n < nc.n) {  // this shard's rows only: uncommit_node, atomically
+        if (c.backfill) {
+            atomic_add_dev(&nc.bf_cpu[n], -c.req_cpu); atomic_add_dev(&nc.bf_mem[n], -c.req_mem);
+            atomic_add_dev(&nc.bf_gpu[n], -c.req_gpu);
+        }
+        if (kind == 1) {
+            atomic_add_dev(&nc.idle_cpu[n], c.req_cpu); atomic_add_dev(&nc.idle_mem[n], c.req_mem);
+            atomic_add_dev(&nc.idle_gpu[n], c.req_gpu);
+        } else {
+            atomic_add_dev(&nc.rel_cpu[n], c.req_cpu); atomic_add_dev(&nc.rel_mem[n], c.req_mem);
+            atomic_add_dev(&nc.rel_gpu[n], c.req_gpu);
+        }
+        atomic_add_dev(&nc.pods[n], -1);
+        atomic_add_dev(&nc.nzc[n], -c.nz_cpu);
+        atomic_add_dev(&nc.nzm[n], -c.nz_mem);
+        if (c.has_ports)
+            for (int w = 0; w < 4; ++w)
+                if (w < port_win(c, nc))
+                    __hip_atomic_fetch_and(&nc.ports[port_at(c, nc, w, n)], ~t.masks[c.pown_off + w], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (c.aff && g >= 0) {  // replicated tables: uncommit_aff, atomically
+        for (int q = 0; q < c.upd_n; ++q) {
+            const int32_t* it = t.aff_items + c.upd_off + 3 * q;
+            const bool to_cnt = it[0] == 0;
+            const int d = to_cnt ? dom_g(nc, it[1], g) : 0;
+            const bool apply = (it[0] == 2 || kind == 1) && d >= 0;
+            int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
+            atomic_add_dev(tab + it[2] + (d >= 0 ? d : 0), apply ? -1 : 0);
+        }
     }
 }
 

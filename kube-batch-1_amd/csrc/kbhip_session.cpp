@@ -531,7 +531,7 @@ struct Session {
     vector<std::pair<int64_t, int64_t>> class_srange;  // score range [lo, hi] per class (no inter-pod term)
     bool keys32 = true;          // option "keys32": 32-bit keys where they fit
     DevBuf b_cols[20], b_labels, b_taints, b_ports, b_classes, b_terms, b_reqs, b_vals, b_valint, b_valok, b_masks,
-        b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar;
+        b_ctrl, b_walk, b_dom, b_aff_items, b_aff_cnt, b_aff_scalar, b_dd_max;
     PopCtrl* d_ctrl = nullptr;
     size_t h_out_cap = 0;
     DevBuf b_cand2, b_arrive;
@@ -676,7 +676,7 @@ struct Session {
                           &b_masks, &b_ctrl, &b_walk, &b_dom, &b_aff_items, &b_aff_cnt, &b_aff_scalar, &b_cand2,
                           &b_arrive, &b_link, &b_dbg, &b_fit4, &b_rank_keys, &b_rank_sorted, &b_rank_tmp, &b_rank_cnt,
                           &b_rank_radix,
-                          &b_shard_send, &b_shard_recv, &b_tab_idx, &b_sweep_cnt})
+                          &b_shard_send, &b_shard_recv, &b_tab_idx, &b_sweep_cnt, &b_dd_max})
             b->release();
         for (auto& b : b_cand_ov) b.release();
         for (auto& b : b_arrive_ov) b.release();
@@ -1482,6 +1482,7 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             c.ipa_n = (int32_t)pg->ipa.size() / 4;
             c.upd_n = (int32_t)pg->upd.size() / 3;
             c.dd_space = dedup_space(*pg, space_ndom);
+            c.dd_ndom = c.dd_space >= 0 ? space_ndom[c.dd_space] : 0;
         } else {
             c.pa_space = c.paa_space = -1;
             c.dd_space = -1;
@@ -1683,6 +1684,10 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.tab.valint = upload(S, S.b_valint, valint);
     S.tab.valok = upload(S, S.b_valok, valok);
     S.tab.masks = upload(S, S.b_masks, E.masks);
+    {
+        static const vector<uint64_t> zero(kDedupMax, 0);  // (outlives the asynchronous copy)
+        S.tab.dd_max = upload(S, S.b_dd_max, zero);
+    }
     if (encode_only) {
         S.stats.nodes = N;
         S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -4605,6 +4610,14 @@ static bool carry_fast_ok(const Session& S, const kbs::Snapshot& s, const PodVie
 static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t* old_pod, const int32_t* old_node) {
     Session& S = ks->s;
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "kbhip_session_carry_snapshot on a node-sharded session");
+    static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;  // per-phase host times (diagnostic)
+    auto tp = std::chrono::steady_clock::now();
+    auto mark = [&](const char* what) {
+        if (!prof) return;
+        auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[carry] %-10s %8.2f ms\n", what, std::chrono::duration<double>(now - tp).count() * 1e3);
+        tp = now;
+    };
     require_no_tickets(S);
     const PodView v(s);
     const int P = v.P, Pold = (int)S.pods.size(), N = (int)s.rows("n_name"), Nold = (int)S.h_alloc.size();
@@ -4620,6 +4633,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
             if (o < -1 || o >= Nold || (o >= 0 && seen[o]++)) throw Error(KBHIP_EINVAL, "bad old_node map");
         }
     }
+    mark("maps");
     ov_quiesce(S);
     HIPCHK(hipStreamSynchronize(S.stream));
     if (!carry_fast_ok(S, s, v, old_pod, old_node)) {
@@ -4648,6 +4662,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
             return;
         }
     }
+    mark("checks");
     // ---------------- nodes: allocatable, pods, unschedulable (labels / taints unchanged) ----------------
     auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"), agpu = s.vec<int64_t>("n_alloc_gpu"),
          apods = s.vec<int64_t>("n_alloc_pods");
@@ -4706,6 +4721,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
                             S.pod_port_ids.begin() + S.pod_port_off[o + 1]);
     }
     port_off[P] = (int32_t)port_ids.size();
+    mark("pods");
     // ---------------- queues & jobs (as at open) ----------------
     auto qn = s.vec<int32_t>("q_name"), qw = s.vec<int32_t>("q_weight");
     auto qts = s.vec<int64_t>("q_ts");
@@ -4775,6 +4791,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         if (p.status == AOB) j.cnt_aob++;
         if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) j.maybe_pending = true;
     }
+    mark("jobs");
     // ---------------- task classes of pending tasks without one (new pods) ----------------
     for (int i = 0; i < P; ++i) {
         HPod& p = pods[i];
@@ -4817,6 +4834,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         S.classes.push_back(c);
         new_classes.push_back(p.cls);
     }
+    mark("classes");
     // ---------------- node rows from the pods (cache addTask -> NodeInfo.AddTask) ----------------
     const int Nl = S.nc.n;
     vector<int64_t> col[13];
@@ -4849,6 +4867,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     }
     S.any_bf = 0;
     for (int n = 0; n < N; ++n) if (col[6][n] || col[7][n] || col[8][n]) S.any_bf = 1;
+    mark("rows");
     // ---------------- device: the node rows that differ, the grown class tables ----------------
     int64_t uploaded = 0;
     auto sync_col = [&](void* dptr, const void* want, size_t elem) {
@@ -4884,6 +4903,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         uploaded += (int64_t)(S.classes.size() * sizeof(TaskClass) + S.keep.masks.size() * sizeof(uint64_t));
     }
     HIPCHK(hipStreamSynchronize(S.stream));  // the host sources above are about to go away
+    mark("upload");
     // ---------------- the host model of the new session ----------------
     spare_pods().give(S.pods);
     S.pods.swap(pods);
@@ -4904,6 +4924,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     S.log.clear();
     S.last_fit_ok = false;
     S.stats.nodes = N;
+    mark("swap");
 }
 
 static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,

@@ -82,7 +82,7 @@ struct TaskClass {
                     // pw_lo .. pw_lo + kPortWin - 1 (port ids sorted by protocol, port, IP)
     int32_t dd_space;  // placement 7: the topology space whose domains the batched sweep keeps one
                        // candidate of (the class kills a domain by placing into it), -1: none
-    int32_t dd_pad;
+    int32_t dd_ndom;   // ... its number of domains (<= kDedupMax)
 };
 constexpr int kDedupMax = 1024;  // domains of a dd_space (the sweep's per-block LDS table)
 constexpr int kPortWin = 4;  // port words a class's masks span (its ports' 256-id window)
