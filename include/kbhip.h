@@ -118,6 +118,7 @@ typedef struct kbhip_stats {
     double evict_walk_s;     /* reclaim / preempt: host wall time walking the ranked nodes (victims, evictions) */
     int64_t evict_visits;    /* reclaim / preempt: nodes whose victims were asked for (Reclaimable / Preemptable) */
     int64_t evict_cands;     /* ... candidates handed to those calls */
+    int64_t fit_syncs;       /* allocate: FitDelta histograms recounted after a pop (a job left not Ready) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),
@@ -328,10 +329,10 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "overlap" = k rotates batched pops over k + 1 streams so that a pop's sweep
  * runs beside the previous k pops' placements, chained on the device (1, the
  * default, or 2); 0 = one stream, one pop kernel at a time;
- * "shard_overlap" = 1 (default; node-array shards with peer mailboxes and
- * "overlap" > 0): a shard's sweep of pop e runs beside pop e-1's placement,
- * leaving that pop's candidates out and re-evaluating them once its
- * write-back is done; 0 = sweep, exchange and placement one after another;
+ * "shard_overlap" = 1 (node-array shards with peer mailboxes and "overlap" >
+ * 0): a shard's sweep of pop e runs beside pop e-1's placement, leaving that
+ * pop's candidates out and re-evaluating them once its write-back is done;
+ * 0 (default) = sweep, exchange and placement one after another;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
  * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);

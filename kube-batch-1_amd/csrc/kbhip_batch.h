@@ -962,6 +962,13 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
     int wins_alloc = 0, wins_pipe = 0;  // this lane's node: placements (the device tables after the loop)
+    // uniform loop bounds in scalar registers: the task loop is one wave's serial chain, so
+    // every item it skips with a scalar branch instead of a masked vector step counts
+    const int nit = __builtin_amdgcn_readfirstlane(n_items);
+    uint32_t m0bits = 0;  // the UPD_CNT_ALLOC items
+#pragma unroll
+    for (int u = 0; u < kAffUpd; ++u) m0bits |= (u < n_upd && utype[u] == 0) ? (1u << u) : 0u;
+    const uint32_t m0mask = (uint32_t)__builtin_amdgcn_readfirstlane((int)m0bits);
     const uint64_t t0 = readlane64(K, 63);  // the list's last key (0: the list holds every feasible node)
     uint64_t key = K;
     bool changed = false;
@@ -978,17 +985,22 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
         if (kind == 1) {
 #pragma unroll
             for (int u = 0; u < kAffUpd; ++u) {
-                if (utype[u] != 0) continue;  // (uniform)
+                if (!((m0mask >> u) & 1u)) continue;  // (scalar)
                 const int us = __builtin_amdgcn_readlane(uslot[u], wl);
-                if (us >= 0) {
+                if (us >= 0) {  // (scalar)
 #pragma unroll
-                    for (int k = 0; k < kAffItems; ++k) cnt[k] += (slot[k] == us) ? 1 : 0;
+                    for (int k = 0; k < kAffItems; ++k)
+                        if (k < nit) cnt[k] += (slot[k] == us) ? 1 : 0;
                 }
             }
         }
         bool aff_ok = true;
 #pragma unroll
-        for (int k = 0; k < kAffItems; ++k) aff_ok = aff_ok && !(slot[k] >= 0 && cnt[k] > 0);
+        for (int k = 0; k < kAffItems; ++k)
+            if (k < nit) aff_ok = aff_ok && !(slot[k] >= 0 && cnt[k] > 0);
+        // the winner's next key: only if its own predicates still pass (a self-anti-affine
+        // winner's domain is closed): a scalar branch around the key evaluation
+        const bool alive = __builtin_amdgcn_readlane((int)aff_ok, wl) != 0;
         if (win) {
             if (kind == 1) ++wins_alloc;
             else ++wins_pipe;
@@ -996,12 +1008,17 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
             if (c.has_ports)
                 for (int q = 0; q < 4; ++q) pw[q] |= (q < port_win(c, nc)) ? t.masks[c.pown_off + q] : 0;
             changed = true;
-            int32_t s = 0;
-            bool passed = false;
-            key = aff_ok ? dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed) : 0;
-        } else if (!aff_ok) {
+        }
+        if (alive) {
+            if (win) {
+                int32_t s = 0;
+                bool passed = false;
+                key = dyn_key(cf, c, t, nc, r, pw, n, true, na_n, &s, &passed);
+            }
+        } else if (win) {
             key = 0;
         }
+        if (!win && !aff_ok) key = 0;
         done = i + 1;
         if (kind == 1) ++ready;  // Pipelined is not an AllocatedStatus (types.go:82-84)
         if (!a.gang_mode || ready >= a.min_avail) { stop = 2; break; }  // allocate.go:191-195

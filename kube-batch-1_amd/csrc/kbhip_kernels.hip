@@ -550,6 +550,7 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
         if (wave != 0) return;
         STAMP(nb_ * 4 + 1);
         place_aff(cf, nc, t, c, a, out, wl[0][lane]);
+        STAMP(nb_ * 4 + 2);
         STAMP(nb_ * 4 + 3);
         return;
     } else {  // PL == 2: parallel levels, every wave takes part

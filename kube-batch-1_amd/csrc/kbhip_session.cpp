@@ -624,7 +624,8 @@ struct Session {
     Mailbox* mbox_peer[kMaxWorld] = {};        // and every rank's as mapped here (own included)
     uint32_t mbox_seq = 0;                     // sequence number of the last batched pop sent
     uint32_t sh_chained_seq = 0;               // the last overlapped shard pop (k_shard_sweep_ov), 0: none
-    bool shard_overlap = true;                 // option "shard_overlap": overlapped shard pops (with "overlap" > 0)
+    bool shard_overlap = false;                // option "shard_overlap": overlapped shard pops (with "overlap" > 0;
+                                               // off: measured slower in the one-chip rehearsal)
     bool chain_fence = false;                  // device work ran on the session stream after the last drain
     vector<uint8_t> h_shard;                   // host staging of the host all-gather
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
@@ -3245,6 +3246,7 @@ struct Allocator {
         // score's min / max prepass on that state.  Shards: the chosen node's
         // walk key (its owner computes it) and the counts are all-reduced.
         auto fit_sync = [&](int cls, int node, int kind, HJob& job) {
+            S.stats.fit_syncs++;
             discard_all();
             ov_quiesce(S);
             const int32_t nd[1] = {node}, kd[1] = {kind};
@@ -4688,39 +4690,83 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     auto tlk = s.span<int32_t>("tl_key"), tlo = s.span<int32_t>("tl_op"), tlv = s.span<int32_t>("tl_val"),
          tle = s.span<int32_t>("tl_effect");
     vector<int> new_classes;  // classes this carry appended
-    for (int i = 0; i < P; ++i) {
-        HPod& p = pods[i];
-        const int o = old_pod[i];
-        if (o >= 0) {
-            p = S.pods[o];  // spec-derived fields and session ids (namespace, class) kept
-        } else {
-            p = HPod{};
-            v.spec(i, p);
-            p.ns = S.keep.nss.get(s.s(pns[i]));
+    {
+        // node names of new bound pods and of pods whose node changed are looked up in a map
+        // built up front (read-only in the parallel pass below)
+        bool need_map = false;
+        for (int i = 0; i < P && !need_map; ++i) need_map = old_pod[i] < 0 && v.has_node(i);
+        if (need_map) find_node("");
+        std::atomic<int> bad_pod{-1};
+        vector<int32_t> pcount(P, 0);
+        auto pass = [&](int lo, int hi) {  // the pods' records (kept or decoded), status and node
+            for (int i = lo; i < hi; ++i) {
+                HPod& p = pods[i];
+                const int o = old_pod[i];
+                if (o >= 0) {
+                    p = S.pods[o];  // spec-derived fields and session ids (namespace, class) kept
+                } else {
+                    p = HPod{};
+                    v.spec(i, p);
+                }
+                p.uid_rank = i;
+                p.status = v.status(i);
+                p.node = -1;
+                p.node_rel = false;
+                p.detached = false;
+                p.groupless = v.pjob[i] < 0;
+                if (v.has_node(i)) {
+                    int n = -1;
+                    if (o >= 0 && S.pods[o].node >= 0 && S.pods[o].node < N &&
+                        std::strcmp(s.str(nname[S.pods[o].node]), s.str(v.pnode[i])) == 0)
+                        n = S.pods[o].node;
+                    else if (!node_idx.empty()) {
+                        auto it = node_idx.find(std::string_view(s.str(v.pnode[i])));
+                        n = it == node_idx.end() ? -1 : it->second;
+                    }
+                    if (n < 0) {
+                        int want = -1;
+                        bad_pod.compare_exchange_strong(want, i);
+                        continue;
+                    }
+                    p.node = n;
+                    p.detached = !v.pdet.empty() && v.pdet[i];
+                }
+                pcount[i] = o >= 0 ? S.pod_port_off[o + 1] - S.pod_port_off[o] : 0;
+            }
+        };
+        constexpr int kThreads = 8;
+        auto run = [&]() {
+            if (P < (1 << 15)) {
+                pass(0, P);
+            } else {
+                const int per = (P + kThreads - 1) / kThreads;
+                vector<std::thread> th;
+                for (int t = 1; t < kThreads; ++t) th.emplace_back(pass, t * per, std::min(P, (t + 1) * per));
+                pass(0, std::min(P, per));
+                for (auto& x : th) x.join();
+            }
+        };
+        run();
+        if (bad_pod >= 0 && node_idx.empty()) {  // a kept pod moved to another node: again, with the map
+            find_node("");
+            bad_pod = -1;
+            run();
         }
-        p.uid_rank = i;
-        p.status = v.status(i);
-        p.node = -1;
-        p.node_rel = false;
-        p.detached = false;
-        p.groupless = v.pjob[i] < 0;
-        if (v.has_node(i)) {
-            const int n = o >= 0 && S.pods[o].node >= 0 && S.pods[o].node < N &&
-                                  std::strcmp(s.str(nname[S.pods[o].node]), s.str(v.pnode[i])) == 0
-                              ? S.pods[o].node
-                              : find_node(std::string_view(s.str(v.pnode[i])));
-            if (n < 0)
-                throw Error(KBHIP_EINVAL, "pod " + s.s(v.puid[i]) + " is bound to node " + s.s(v.pnode[i]) +
-                                              " which is not in the snapshot");
-            p.node = n;
-            p.detached = !v.pdet.empty() && v.pdet[i];
+        if (bad_pod >= 0) {
+            const int i = bad_pod;
+            throw Error(KBHIP_EINVAL, "pod " + s.s(v.puid[i]) + " is bound to node " + s.s(v.pnode[i]) +
+                                          " which is not in the snapshot");
         }
-        port_off[i] = (int32_t)port_ids.size();
-        if (o >= 0)
-            port_ids.insert(port_ids.end(), S.pod_port_ids.begin() + S.pod_port_off[o],
-                            S.pod_port_ids.begin() + S.pod_port_off[o + 1]);
+        for (int i = 0; i < P; ++i) {  // namespace ids of new pods (the kept dictionary grows in order)
+            if (old_pod[i] < 0) pods[i].ns = S.keep.nss.get(s.s(pns[i]));
+            port_off[i + 1] = port_off[i] + pcount[i];
+        }
+        port_ids.resize(port_off[P]);
+        for (int i = 0; i < P; ++i)
+            if (pcount[i])
+                std::copy(S.pod_port_ids.begin() + S.pod_port_off[old_pod[i]],
+                          S.pod_port_ids.begin() + S.pod_port_off[old_pod[i] + 1], port_ids.begin() + port_off[i]);
     }
-    port_off[P] = (int32_t)port_ids.size();
     mark("pods");
     // ---------------- queues & jobs (as at open) ----------------
     auto qn = s.vec<int32_t>("q_name"), qw = s.vec<int32_t>("q_weight");
@@ -4778,6 +4824,14 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         }
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
+    }
+    {
+        vector<int32_t> ntask(jobs.size(), 0);
+        for (int i = 0; i < P; ++i) {
+            const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
+            if (slot >= 0) ntask[slot]++;
+        }
+        for (size_t j = 0; j < jobs.size(); ++j) jobs[j].tasks.reserve(ntask[j]);
     }
     for (int i = 0; i < P; ++i) {
         HPod& p = pods[i];

@@ -1,8 +1,10 @@
-"""C3 (20k nodes, selectors, taints, zone anti-affinity, 8 queues): one
+"""C3 (20k nodes, selectors, taints, zone anti-affinity, 8 queues) — or with
+--c5, C5's allocate (50k nodes with Backfilled resources, after reclaim): one
 session's allocate with the engine's path counters — batched pops, the
-sequential placements (7: pod anti-affinity classes) and how they ended,
-per-task sweeps, unassigned pops — plus open / allocate times.  Prints one
-JSON line; run under rocprofv3 --kernel-trace --stats for the kernel split."""
+sequential placements (6: Backfilled nodes, 7: pod anti-affinity classes) and
+how they ended, per-task sweeps, unassigned pops, FitDelta recounts — plus
+open / allocate times.  Prints one JSON line; run under rocprofv3
+--kernel-trace --stats for the kernel split."""
 import json
 import os
 import statistics
@@ -16,11 +18,16 @@ import kbhip  # noqa: E402
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    p = "/tmp/kbhip_bench/c3.kbs"
+    c5 = "--c5" in sys.argv
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    reps = int(args[0]) if args else 3
+    p = "/tmp/kbhip_bench/c5_50000_2000_0.kbs" if c5 else "/tmp/kbhip_bench/c3.kbs"
     if not os.path.exists(p):
         os.makedirs(os.path.dirname(p), exist_ok=True)
-        kbgen.gen_c3().write(p + ".tmp")
+        if c5:
+            kbgen.gen_c5(p + ".tmp", seed=kbgen.BASE_SEED + 5, n_nodes=50_000, n_pending=2000)
+        else:
+            kbgen.gen_c3().write(p + ".tmp")
         os.replace(p + ".tmp", p)
     with open(p, "rb") as f:
         buf = f.read()
@@ -29,6 +36,10 @@ def main():
         t0 = time.perf_counter()
         s = kbhip.Session(buf)
         t1 = time.perf_counter()
+        if c5:
+            s.reclaim()  # the shipped actions' order: allocate runs after reclaim (not timed)
+            t0 += time.perf_counter() - t1
+            t1 = time.perf_counter()
         pod, node, kind = s.allocate()
         t2 = time.perf_counter()
         st = s.stats()
@@ -36,9 +47,9 @@ def main():
         opens.append(t1 - t0)
         allocs.append(t2 - t1)
     keys = ("pops", "tasks", "placed", "sweeps", "batched_pops", "pertask_sweeps", "seq_launches", "seq_cut",
-            "seq_none", "unassigned_pops", "spec_hits", "spec_missed", "alloc_device_s", "host_launch_s",
+            "seq_none", "unassigned_pops", "spec_hits", "spec_missed", "fit_syncs", "alloc_device_s", "host_launch_s",
             "host_wait_s")
-    print(json.dumps({"config": "C3", "placements": int(len(pod)), "open_ms": statistics.median(opens) * 1e3,
+    print(json.dumps({"config": "C5 allocate" if c5 else "C3", "placements": int(len(pod)), "open_ms": statistics.median(opens) * 1e3,
                       "allocate_ms": statistics.median(allocs) * 1e3, **{k: st[k] for k in keys}}))
 
 
