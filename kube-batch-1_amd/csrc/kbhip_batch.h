@@ -974,7 +974,45 @@ __device__ void place_aff(const Conf& cf, const NodeCols& nc, const DevTables& t
     bool changed = false;
     int ready = a.ready_count, done = 0, stop = 0;
     uint64_t mine = 0;  // lane i: winner key of task i
-    for (int i = 0; i < a.n_tasks; ++i) {
+    // Per-domain candidates (dd_space): the list holds at most one node per domain, and an
+    // Allocated placement closes its winner's domain and nothing else the class reads, so
+    // while the winners are Allocated nodes that carry the key, task i takes list entry i:
+    // the whole run at once (ballots and a scalar walk for the stops) instead of the task
+    // loop.  A node without the key at the head of the list takes the loop.
+    bool fast = false;
+    if (c.dd_space >= 0 && nit > 0) {  // (uniform)
+        const bool keyed = n >= 0 && slot[0] >= 0;
+        const uint64_t V = __ballot(K != 0 && keyed);
+        const uint64_t Z = __ballot(K != 0);
+        if ((V & 1ull) || !(Z & 1ull)) {
+            fast = true;
+            const uint64_t P2 = __ballot(K != 0 && key_kind(K) == 2);
+            const int len = V == ~0ull ? 64 : __builtin_ctzll(~V);
+            const int m = len < a.n_tasks ? len : a.n_tasks;
+            int r_s = a.ready_count, d_s = 0, st_s = 0;
+            for (int i = 0; i < m; ++i) {  // scalar: the loop's stop rules over list order
+                const bool pipe = (P2 >> i) & 1ull;
+                d_s = i + 1;
+                if (!pipe) ++r_s;
+                if (!a.gang_mode || r_s >= a.min_avail) { st_s = 2; break; }
+                if (pipe) break;  // a Pipelined winner does not close its domain
+            }
+            done = d_s;
+            stop = st_s;
+            ready = r_s;
+            if (lane < done) {
+                mine = K;
+                const int kind = key_kind(K);
+                if (kind == 1) ++wins_alloc;
+                else ++wins_pipe;
+                r = apply_commits(r, c, kind == 1 ? 1 : 0, kind == 1 ? 0 : 1);
+                if (c.has_ports)
+                    for (int q = 0; q < 4; ++q) pw[q] |= (q < port_win(c, nc)) ? t.masks[c.pown_off + q] : 0;
+                changed = true;
+            }
+        }
+    }
+    for (int i = 0; i < a.n_tasks && !fast; ++i) {
         const uint64_t w = wave_max_key(key);
         if (!w || w < t0) break;  // no node, or one outside the list may come first: the host goes on
         if (lane == i) mine = w;

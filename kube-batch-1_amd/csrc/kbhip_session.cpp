@@ -4682,7 +4682,9 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         return it == node_idx.end() ? -1 : it->second;
     };
     // ---------------- pods ----------------
-    vector<HPod> pods(P);
+    vector<HPod> pods;  // the pooled array (its pages already mapped): every element is assigned below
+    spare_pods().take_keep(pods);
+    pods.resize(P);
     vector<int32_t> port_off(P + 1, 0), port_ids;
     port_ids.reserve(S.pod_port_ids.size());
     const int tw = ((int)S.keep.taint_defs.size() + 63) / 64;
@@ -4798,15 +4800,21 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     }
     if (!std::is_sorted(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; }))
         std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+    mark("jobs:srcs");
     vector<HJob> jobs;
     vector<string> job_uid;
     vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
     const auto default_q = qidx.find("default");
+    std::unordered_map<int32_t, int> qslot_of;  // queue name (interned string offset) -> queue slot
     for (auto& src : srcs) {
         int qslot = -1;
         if (src.row >= 0) {
-            auto qit = qidx.find(s.s(jq[src.row]));
-            qslot = qit == qidx.end() ? -1 : qit->second;
+            auto qc = qslot_of.find(jq[src.row]);
+            if (qc == qslot_of.end()) {
+                auto qit = qidx.find(s.s(jq[src.row]));
+                qc = qslot_of.emplace(jq[src.row], qit == qidx.end() ? -1 : qit->second).first;
+            }
+            qslot = qc->second;
         } else {
             qslot = default_q == qidx.end() ? -1 : default_q->second;
         }
@@ -4825,6 +4833,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
     }
+    mark("jobs:slots");
     {
         vector<int32_t> ntask(jobs.size(), 0);
         for (int i = 0; i < P; ++i) {
