@@ -27,13 +27,14 @@ class _Strtab:  # write_kbs takes an object with bytes()
         return self.b
 
 
-def next_snapshot_with_arrivals(C, st, status, node, frac, seed=4242):
+def next_snapshot_with_arrivals(C, st, status, node, frac, seed=4242, tag=""):
     """The C4 cache state after a session (its binds applied: Binding -> bound,
     Pending with a node) plus frac x P new pods in new gang jobs (8..64 tasks,
     request shapes outside the C4 mix: new task classes), appended in UID
     order ("v..." after the pending "u..." pods; jobs "jq..." between the
     pending "jp..." and running "jr..." jobs).  Returns (columns, strtab,
-    old_pod, old_node)."""
+    old_pod, old_node).  tag: a second application on its own output ("w":
+    pods "w...", jobs "jqw..." sort after the first round's)."""
     import numpy as np
     rng = np.random.default_rng(seed)
     C = {k: v.copy() for k, v in C.items()}
@@ -53,9 +54,9 @@ def next_snapshot_with_arrivals(C, st, status, node, frac, seed=4242):
         off = base + len(extra)
         extra += sv.encode() + b"\0"
         return off
-    uid_off = np.array([add(f"v{i:08d}") for i in range(A)], np.int32)
-    job_off = np.array([add(f"jq{i:07d}") for i in range(J_new)], np.int32)
-    n_pj = int(np.searchsorted([st[o:st.index(b"\0", o)].decode() for o in C["j_name"]], "jq"))
+    uid_off = np.array([add(f"{tag or 'v'}{i:08d}") for i in range(A)], np.int32)
+    job_off = np.array([add(f"jq{tag}{i:07d}") for i in range(J_new)], np.int32)
+    n_pj = int(np.searchsorted([st[o:st.index(b"\0", o)].decode() for o in C["j_name"]], "jq" + tag))
     pj = np.repeat(np.arange(J_new), sizes).astype(np.int32)
     cpu = rng.choice([750, 1500, 3000], size=J_new)[pj].astype(np.int64)
     mem = (rng.choice([3, 6], size=J_new)[pj] << 30).astype(np.int64)
@@ -119,27 +120,45 @@ def main():
     kbgen.write_kbs(p2, C2, st2)
     with open(p2, "rb") as f:
         buf2 = f.read()
-    arr_open, arr_carry, arr_sent, equal = [], [], [], True
+    # a third snapshot: the cache after the second session plus arrivals (the steady state: a
+    # carried session carried again, the previous pod array back in the engine's pool)
+    with kbhip.Session(buf2, device=0) as s:
+        s.allocate()
+        status2, node2 = s.table("pod_status").copy(), s.table("pod_node").copy()
+    C3_, st3, old_pod3, old_node3 = next_snapshot_with_arrivals(C2, st2.bytes(), status2, node2, args.arrivals, tag="w")
+    p3 = os.path.join(args.cache, f"c4_next2_{args.arrivals}.kbs")
+    kbgen.write_kbs(p3, C3_, st3)
+    with open(p3, "rb") as f:
+        buf3 = f.read()
+    arr_open, arr_carry, arr_sent, arr_carry2, equal = [], [], [], [], True
     for _ in range(args.rounds):
         t0 = time.perf_counter()
         f = kbhip.Session(buf2, device=0)
         arr_open.append(time.perf_counter() - t0)
         fresh = f.allocate()
         f.close()
+        with kbhip.Session(buf3, device=0) as f3:
+            fresh3 = f3.allocate()
         s = kbhip.Session(buf, device=0)
         s.allocate()
         t1 = time.perf_counter()
         arr_sent.append(s.carry_snapshot(buf2, old_pod, old_node))
         arr_carry.append(time.perf_counter() - t1)
         got = s.allocate()
+        t2 = time.perf_counter()
+        s.carry_snapshot(buf3, old_pod3, old_node3)
+        arr_carry2.append(time.perf_counter() - t2)
+        got3 = s.allocate()
         s.close()
         equal = equal and all(np.array_equal(a, b) for a, b in zip(got, fresh))
+        equal = equal and all(np.array_equal(a, b) for a, b in zip(got3, fresh3))
     print(json.dumps({"metric": "C4 session start: open vs carry (ms)", "open_ms": statistics.median(opens) * 1e3,
                       "carry_ms": statistics.median(carries) * 1e3, "carry_bytes_uploaded": statistics.median(sent),
                       "second_session_placements": statistics.median(placed2), "rounds": args.rounds,
                       "arrivals": {"pods": int((old_pod < 0).sum()), "frac": args.arrivals,
                                    "open_ms": statistics.median(arr_open) * 1e3,
                                    "carry_snapshot_ms": statistics.median(arr_carry) * 1e3,
+                                   "carry_snapshot_chained_ms": statistics.median(arr_carry2) * 1e3,
                                    "carry_snapshot_bytes_uploaded": statistics.median(arr_sent),
                                    "placements": int(len(fresh[0])), "log_equal_to_fresh_open": bool(equal)}}))
 

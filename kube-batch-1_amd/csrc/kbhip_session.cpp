@@ -4685,6 +4685,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     vector<HPod> pods;  // the pooled array (its pages already mapped): every element is assigned below
     spare_pods().take_keep(pods);
     pods.resize(P);
+    mark("pods:array");
     vector<int32_t> port_off(P + 1, 0), port_ids;
     port_ids.reserve(S.pod_port_ids.size());
     const int tw = ((int)S.keep.taint_defs.size() + 63) / 64;
@@ -4835,24 +4836,60 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     }
     mark("jobs:slots");
     {
-        vector<int32_t> ntask(jobs.size(), 0);
-        for (int i = 0; i < P; ++i) {
-            const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
-            if (slot >= 0) ntask[slot]++;
+        // job task lists in pod order, filled by kThreads pod ranges: per-range counts per job
+        // give every range its first position in each job's list
+        constexpr int kThreads = 8;
+        const int J = (int)jobs.size();
+        const int nth = P < (1 << 15) ? 1 : kThreads;
+        const int per = (P + nth - 1) / nth;
+        vector<vector<int32_t>> cnt(nth, vector<int32_t>(J, 0));
+        auto par = [&](auto&& fn) {
+            vector<std::thread> th;
+            for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
+            fn(0);
+            for (auto& x : th) x.join();
+        };
+        par([&](int t) {
+            const int lo = t * per, hi = std::min(P, lo + per);
+            int32_t* c = cnt[t].data();
+            for (int i = lo; i < hi; ++i) {
+                const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
+                pods[i].job = slot;
+                if (slot >= 0) c[slot]++;
+            }
+        });
+        for (int j = 0; j < J; ++j) {  // per job: the ranges' offsets, the list's size
+            int32_t off = 0;
+            for (int t = 0; t < nth; ++t) {
+                const int32_t k = cnt[t][j];
+                cnt[t][j] = off;
+                off += k;
+            }
+            jobs[j].tasks.resize(off);
         }
-        for (size_t j = 0; j < jobs.size(); ++j) jobs[j].tasks.reserve(ntask[j]);
-    }
-    for (int i = 0; i < P; ++i) {
-        HPod& p = pods[i];
-        const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
-        p.job = slot;
-        if (slot < 0) continue;
-        HJob& j = jobs[slot];
-        j.tasks.push_back(i);
-        j.priority = p.priority;  // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
-        if (allocated_status(p.status)) j.cnt_alloc++;
-        if (p.status == AOB) j.cnt_aob++;
-        if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) j.maybe_pending = true;
+        par([&](int t) {
+            const int lo = t * per, hi = std::min(P, lo + per);
+            int32_t* c = cnt[t].data();
+            for (int i = lo; i < hi; ++i) {
+                const int slot = pods[i].job;
+                if (slot >= 0) jobs[slot].tasks[c[slot]++] = i;
+            }
+        });
+        par([&](int t) {  // job fields from their tasks (jobs split by ranges of job slots)
+            const int jlo = (int)((int64_t)J * t / nth), jhi = (int)((int64_t)J * (t + 1) / nth);
+            for (int j = jlo; j < jhi; ++j) {
+                HJob& job = jobs[j];
+                for (int i : job.tasks) {
+                    const HPod& p = pods[i];
+                    if (allocated_status(p.status)) job.cnt_alloc++;
+                    if (p.status == AOB) job.cnt_aob++;
+                    if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU))
+                        job.maybe_pending = true;
+                }
+                // JobInfo.AddTaskInfo: the last task's priority (job_info.go:242)
+                if (!job.tasks.empty()) job.priority = pods[job.tasks.back()].priority;
+            }
+        });
     }
     mark("jobs");
     // ---------------- task classes of pending tasks without one (new pods) ----------------
