@@ -496,6 +496,10 @@ struct Session {
     vector<int32_t> pod_port_off, pod_port_ids;  // host-port ids per pod, CSR (kbhip_session_carry)
     int64_t carry_bytes = 0;                     // bytes the last kbhip_session_carry uploaded
     int any_bf = 0;
+    // placement 6 backoff per class: a batched pop of the class that placed nothing (the
+    // fitting node lies below the list of walked nodes, or there is none) sends the class's
+    // next pops to the general path directly (same records either way)
+    vector<uint8_t> bf_backoff;
     bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
     DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt, b_rank_radix;
@@ -2516,6 +2520,7 @@ static void check_task_ids(const Session& S, const int32_t* ids, int n) {
             throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
 }
 
+constexpr uint8_t kBfBackoff = 4;  // pops of a class sent to the general path after a placement-6 miss
 static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
                      int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop) {
     int done = 0, stop = KBHIP_STOP_ALL;
@@ -2525,6 +2530,10 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
         int m = 1;
         while (done + m < n && m < kMaxChunk && S.pods[ids[done + m]].cls == cls0) ++m;
         bool batch = batchable(S, cls0);
+        if (batch && S.any_bf && cls0 < (int)S.bf_backoff.size() && S.bf_backoff[cls0] > 0) {
+            S.bf_backoff[cls0]--;
+            batch = false;
+        }
         int n_done, stop_c, ready_c, any_bf_c = S.any_bf;
         const int32_t* res_node;
         const int32_t* res_kind;
@@ -2535,6 +2544,10 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
             if (n_done == 0) {  // placement 6 / 7 could not place the first task exactly: general path for it
                 batch = false;
                 m = 1;
+                if (L.bf) {
+                    if (S.bf_backoff.size() < S.classes.size()) S.bf_backoff.resize(S.classes.size(), 0);
+                    S.bf_backoff[cls0] = kBfBackoff;
+                }
             }
         } else {  // general path: up to a chunk of mixed classes, no longer than the pop can run
             m = std::min(n - done, kMaxChunk);  // (it stops once Ready: after `need` more Allocated tasks)
@@ -3041,10 +3054,16 @@ struct Allocator {
         auto jl = [this](int a, int b) { return job_less(a, b); };
         GoHeap<decltype(ql)> queues(ql);
         std::map<int, JobQueue<decltype(jl)>> jobs_map;
+        // A job without a pending non-BestEffort task is, in allocate.go, popped once (in its
+        // order), gives no task and is not pushed back; its queue's copy goes back to the
+        // queue heap.  The job and queue orders are strict (creation time, then UID), so
+        // such pops change neither the order of the other jobs nor the queues' shares:
+        // they are left out, with their queue copies (a queue keeps at least one copy
+        // while it has jobs to pop; an overused queue, dropped at its first pop, stays
+        // overused — allocations only grow).  C5: ~180 k running jobs, ~370 real pops.
         for (size_t j = 0; j < S.jobs.size(); ++j) {
             const HJob& job = S.jobs[j];
             int q = job.queue;
-            queues.push(q);
             auto it = jobs_map.find(q);
             if (it == jobs_map.end()) it = jobs_map.emplace(q, JobQueue<decltype(jl)>(jl)).first;
             bool work = false;  // allocate.go:91-104: a pending task that is not BestEffort
@@ -3058,13 +3077,12 @@ struct Allocator {
                     }
                 }
             if (work) {
+                queues.push(q);
                 it->second.push((int)j);
             } else {
-                it->second.idle.push_back((int)j);
                 S.jobs[j].pending_built = true;  // what build_pending would find: nothing
             }
         }
-        for (auto& kv : jobs_map) sort_jobs(kv.second.idle);
         vector<int32_t> ids, onode;
         vector<uint8_t> okind;
         const int gm = S.gang_ready ? 1 : 0;
@@ -3279,7 +3297,11 @@ struct Allocator {
             const int cls0 = S.pods[ids[0]].cls;
             int m = 1;
             while (m < n && m < kMaxChunk && S.pods[ids[m]].cls == cls0) ++m;
-            const bool batch = batchable(S, cls0);
+            bool batch = batchable(S, cls0);
+            if (batch && S.any_bf && cls0 < (int)S.bf_backoff.size() && S.bf_backoff[cls0] > 0) {
+                S.bf_backoff[cls0]--;  // placement 6 missed for this class recently (place_job)
+                batch = false;
+            }
             bool have = false;
             BatchLaunch L;
             if (!specs.empty()) {
@@ -3303,6 +3325,10 @@ struct Allocator {
             int nd = 0, st = 0;
             collect_batched(S, L, &nd, &st, S.res_node_buf, S.res_kind_buf);
             if (st < 0) throw Error(KBHIP_EDEVICE, "device pop did not complete");
+            if (nd == 0 && L.bf) {  // placed nothing: the rest of this pop and the class's next pops take
+                if (S.bf_backoff.size() < S.classes.size()) S.bf_backoff.resize(S.classes.size(), 0);
+                S.bf_backoff[cls0] = kBfBackoff + 1;  // the general path (place_job below consumes one)
+            }
             int alloc = 0;
             for (int j = 0; j < nd; ++j) alloc += S.res_kind_buf[j] == 1;
             apply_results(S, ids.data(), nd, S.res_node_buf, S.res_kind_buf, onode.data(), okind.data());
@@ -3413,8 +3439,18 @@ struct Allocator {
         j.priority = p.priority;
     }
     void build_node_tasks() {  // NodeInfo.Tasks of every node from the host model
-        S.node_tasks.assign(S.nc.n, {});
-        for (int i = 0; i < (int)S.pods.size(); ++i) {
+        const int N = S.nc.n, P = (int)S.pods.size();
+        vector<int32_t> cnt(N, 0);  // sized first: one allocation per node, lists kept across actions
+        for (int i = 0; i < P; ++i) {
+            const HPod& p = S.pods[i];
+            if (on_node_of(p) && p.status != Pending) cnt[p.node]++;
+        }
+        S.node_tasks.resize(N);
+        for (int n = 0; n < N; ++n) {
+            S.node_tasks[n].clear();
+            S.node_tasks[n].reserve(cnt[n]);
+        }
+        for (int i = 0; i < P; ++i) {
             const HPod& p = S.pods[i];
             if (!on_node_of(p) || p.status == Pending) continue;
             S.node_tasks[p.node].push_back(i);
