@@ -3054,16 +3054,13 @@ struct Allocator {
         auto jl = [this](int a, int b) { return job_less(a, b); };
         GoHeap<decltype(ql)> queues(ql);
         std::map<int, JobQueue<decltype(jl)>> jobs_map;
-        // A job without a pending non-BestEffort task is, in allocate.go, popped once (in its
-        // order), gives no task and is not pushed back; its queue's copy goes back to the
-        // queue heap.  The job and queue orders are strict (creation time, then UID), so
-        // such pops change neither the order of the other jobs nor the queues' shares:
-        // they are left out, with their queue copies (a queue keeps at least one copy
-        // while it has jobs to pop; an overused queue, dropped at its first pop, stays
-        // overused — allocations only grow).  C5: ~180 k running jobs, ~370 real pops.
         for (size_t j = 0; j < S.jobs.size(); ++j) {
             const HJob& job = S.jobs[j];
             int q = job.queue;
+            // one queue copy per job, as allocate.go pushes them: a queue's share changes while
+            // its other copies sit in the heap, so the Go heap's layout — which the copies of
+            // jobs without pending tasks shape too — decides later pops (exactness needs them)
+            queues.push(q);
             auto it = jobs_map.find(q);
             if (it == jobs_map.end()) it = jobs_map.emplace(q, JobQueue<decltype(jl)>(jl)).first;
             bool work = false;  // allocate.go:91-104: a pending task that is not BestEffort
@@ -3077,12 +3074,13 @@ struct Allocator {
                     }
                 }
             if (work) {
-                queues.push(q);
                 it->second.push((int)j);
             } else {
+                it->second.idle.push_back((int)j);
                 S.jobs[j].pending_built = true;  // what build_pending would find: nothing
             }
         }
+        for (auto& kv : jobs_map) sort_jobs(kv.second.idle);
         vector<int32_t> ids, onode;
         vector<uint8_t> okind;
         const int gm = S.gang_ready ? 1 : 0;

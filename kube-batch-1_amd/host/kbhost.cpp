@@ -518,7 +518,16 @@ struct Host {
         if (next_pop(&p)) q.push_back({submit(p), p});
         vector<int32_t> node;
         vector<uint8_t> kind;
+        // predictions pay off only if the engine launches them ahead (it runs a pop it cannot
+        // launch at submit — e.g. in a session with Backfilled nodes — inside its wait): after
+        // 16 pops without a launch ahead, the loop stops predicting (same records either way)
+        int64_t waited = 0;
         while (!q.empty()) {
+            if (depth > 0 && waited == 16) {
+                kbhip_stats st{};
+                check(kbhip_get_stats(s, &st), "kbhip_get_stats");
+                if (st.async_launched == 0) depth = 0;
+            }
             // predictions behind the running pop, replayed on the journaled model, topped up to `depth`
             jr.on = true;
             Pop pc = q.front().second;
@@ -551,6 +560,7 @@ struct Host {
             int32_t nd = 0, stop = 0;
             check(kbhip_place_job_wait(s, cur.first, node.data(), kind.data(), &nd, &stop), "kbhip_place_job_wait");
             ++pops;
+            ++waited;
             apply(cur.second, nd, node.data(), kind.data(), stop, true);
             Pop nx;
             const bool has = next_pop(&nx);
