@@ -119,6 +119,7 @@ typedef struct kbhip_stats {
     int64_t evict_visits;    /* reclaim / preempt: nodes whose victims were asked for (Reclaimable / Preemptable) */
     int64_t evict_cands;     /* ... candidates handed to those calls */
     int64_t fit_syncs;       /* allocate: FitDelta histograms recounted after a pop (a job left not Ready) */
+    double alloc_setup_s;    /* allocate: host time before the first pop (plugin open, job and queue heaps) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

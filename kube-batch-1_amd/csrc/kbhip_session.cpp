@@ -2955,12 +2955,29 @@ struct Allocator {
             x.ts = J.ts;
             x.j = v[i];
         }
-        std::sort(k.begin(), k.end(), [nd](const K& a, const K& b) {
+        auto lt = [nd](const K& a, const K& b) {
             for (int c = 0; c < nd; ++c)
                 if (a.d[c] != b.d[c]) return a.d[c] < b.d[c];
             if (a.ts != b.ts) return a.ts < b.ts;
             return a.j < b.j;
-        });
+        };
+        const size_t n = k.size();
+        if (n < (1u << 15)) {
+            std::sort(k.begin(), k.end(), lt);
+        } else {  // C5: ~180 k running jobs without pending tasks: 8 sorted runs in parallel, merged
+            constexpr int kRuns = 8;
+            vector<size_t> cut(kRuns + 1);
+            for (int r = 0; r <= kRuns; ++r) cut[r] = n * r / kRuns;
+            vector<std::thread> th;
+            for (int r = 1; r < kRuns; ++r)
+                th.emplace_back([&, r]() { std::sort(k.begin() + cut[r], k.begin() + cut[r + 1], lt); });
+            std::sort(k.begin(), k.begin() + cut[1], lt);
+            for (auto& x : th) x.join();
+            for (int w = 1; w < kRuns; w *= 2)  // the keys are distinct (job index last): a strict order
+                for (int r = 0; r + w < kRuns; r += 2 * w)
+                    std::inplace_merge(k.begin() + cut[r], k.begin() + cut[r + w],
+                                       k.begin() + cut[std::min(r + 2 * w, kRuns)], lt);
+        }
         for (size_t i = 0; i < v.size(); ++i) v[i] = k[i].j;
     }
     bool queue_less(int l, int r) const {  // session_plugins.go:270-295, proportion.go:144-157
@@ -2989,11 +3006,21 @@ struct Allocator {
     void open_plugins() {
         if (S.plugins_opened) return;
         S.plugins_opened = true;
-        if (S.drf_on)
-            for (auto& j : S.jobs) {  // drf.go:65-82
-                for (int t : j.tasks) if (allocated_status(S.pods[t].status)) j.drf_alloc.add(S.pods[t].req);
-                drf_update(j);
-            }
+        if (S.drf_on) {  // drf.go:65-82 (each job's sum over its own tasks, in order: job ranges in parallel)
+            const int J = (int)S.jobs.size();
+            const int nth = J < (1 << 14) ? 1 : 8;
+            auto drf = [&](int t) {
+                for (int jb = (int)((int64_t)J * t / nth); jb < (int)((int64_t)J * (t + 1) / nth); ++jb) {
+                    HJob& j = S.jobs[jb];
+                    for (int k : j.tasks) if (allocated_status(S.pods[k].status)) j.drf_alloc.add(S.pods[k].req);
+                    drf_update(j);
+                }
+            };
+            vector<std::thread> th;
+            for (int t = 1; t < nth; ++t) th.emplace_back(drf, t);
+            drf(0);
+            for (auto& x : th) x.join();
+        }
         if (S.prop_on) {  // proportion.go:65-142
             for (auto& j : S.jobs) {
                 HQueue& q = S.queues[j.queue];
@@ -3086,6 +3113,7 @@ struct Allocator {
         const int gm = S.gang_ready ? 1 : 0;
         if (!S.ev_run[0]) { HIPCHK(hipEventCreate(&S.ev_run[0])); HIPCHK(hipEventCreate(&S.ev_run[1])); }
         ov_quiesce(S);
+        S.stats.alloc_setup_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         HIPCHK(hipEventRecord(S.ev_run[0], S.stream));
         auto build_pending = [&](HJob& job) {  // allocate.go:91-104; TaskOrderFn is a strict total order
             if (job.pending_built) return;
@@ -4927,10 +4955,31 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     }
     mark("jobs");
     // ---------------- task classes of pending tasks without one (new pods) ----------------
+    int prev_new = -1;  // the last new pending pod classed here: a gang's pods share one spec
+    auto same_spec = [&](int x, int y) {  // the class inputs the fast path reads (no selectors, ports, affinity)
+        const HPod &X = pods[x], &Y = pods[y];
+        if (X.job != Y.job || X.backfill != Y.backfill || X.nzc != Y.nzc || X.nzm != Y.nzm ||
+            X.req.c != Y.req.c || X.req.m != Y.req.m || X.req.g != Y.req.g || X.ireq.c != Y.ireq.c ||
+            X.ireq.m != Y.ireq.m || X.ireq.g != Y.ireq.g)
+            return false;
+        const int nx = v.pto[x + 1] - v.pto[x];
+        if (nx != v.pto[y + 1] - v.pto[y]) return false;
+        for (int k = 0; k < nx; ++k) {
+            const int kx = v.pto[x] + k, ky = v.pto[y] + k;
+            if (tlk[kx] != tlk[ky] || tlo[kx] != tlo[ky] || tlv[kx] != tlv[ky] || tle[kx] != tle[ky]) return false;
+        }
+        return true;
+    };
     for (int i = 0; i < P; ++i) {
         HPod& p = pods[i];
         if (p.status != Pending || p.job < 0) { if (old_pod[i] < 0) p.cls = -1; continue; }
         if (p.cls >= 0) continue;  // kept: the pod's spec did not change
+        if (prev_new >= 0 && same_spec(prev_new, i)) {  // (string offsets compared: the table is interned)
+            p.cls = pods[prev_new].cls;
+            prev_new = i;
+            continue;
+        }
+        prev_new = i;
         TaskClass c{};
         c.ireq_cpu = p.ireq.c; c.ireq_mem = p.ireq.m; c.ireq_gpu = p.ireq.g;
         c.req_cpu = p.req.c; c.req_mem = p.req.m; c.req_gpu = p.req.g;
@@ -4983,21 +5032,34 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         maxc[n] = (int32_t)apods[n];
         flg[n] = (!unsched.empty() && unsched[n]) ? 1 : 0;
     }
-    for (int i = 0; i < P; ++i) {
-        const HPod& p = pods[i];
-        if (!on_node_of(p)) continue;
-        const int n = p.node;
-        if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
-        if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
-        col[0][n] -= p.req.c; col[1][n] -= p.req.m; col[2][n] -= p.req.g;
-        S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
-        podcnt[n]++;
-        col[11][n] += p.nzc;
-        col[12][n] += p.nzm;
-        for (int k = port_off[i]; k < port_off[i + 1]; ++k) {
-            const int id = port_ids[k];
-            pcol[(size_t)(id / 64) * S.nc.npad + n] |= 1ULL << (id % 64);
-        }
+    {
+        // every thread scans all pods and adds the ones on its own node range (no shared writes;
+        // per node the additions keep pod order, as the serial pass would)
+        constexpr int kThreads = 8;
+        const int nth = P < (1 << 15) ? 1 : kThreads;
+        auto rows = [&](int t) {
+            const int nlo = (int)((int64_t)N * t / nth), nhi = (int)((int64_t)N * (t + 1) / nth);
+            for (int i = 0; i < P; ++i) {
+                const HPod& p = pods[i];
+                const int n = p.node;
+                if (n < nlo || n >= nhi || !on_node_of(p)) continue;
+                if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
+                if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
+                col[0][n] -= p.req.c; col[1][n] -= p.req.m; col[2][n] -= p.req.g;
+                S.used[n].c += p.req.c; S.used[n].m += p.req.m; S.used[n].g += p.req.g;
+                podcnt[n]++;
+                col[11][n] += p.nzc;
+                col[12][n] += p.nzm;
+                for (int k = port_off[i]; k < port_off[i + 1]; ++k) {
+                    const int id = port_ids[k];
+                    pcol[(size_t)(id / 64) * S.nc.npad + n] |= 1ULL << (id % 64);
+                }
+            }
+        };
+        vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(rows, t);
+        rows(0);
+        for (auto& x : th) x.join();
     }
     S.any_bf = 0;
     for (int n = 0; n < N; ++n) if (col[6][n] || col[7][n] || col[8][n]) S.any_bf = 1;

@@ -47,7 +47,7 @@ def main():
         opens.append(t1 - t0)
         allocs.append(t2 - t1)
     keys = ("pops", "tasks", "placed", "sweeps", "batched_pops", "pertask_sweeps", "seq_launches", "seq_cut",
-            "seq_none", "unassigned_pops", "spec_hits", "spec_missed", "fit_syncs", "alloc_device_s", "host_launch_s",
+            "seq_none", "unassigned_pops", "spec_hits", "spec_missed", "fit_syncs", "alloc_setup_s", "alloc_device_s", "host_launch_s",
             "host_wait_s")
     print(json.dumps({"config": "C5 allocate" if c5 else "C3", "placements": int(len(pod)), "open_ms": statistics.median(opens) * 1e3,
                       "allocate_ms": statistics.median(allocs) * 1e3, **{k: st[k] for k in keys}}))

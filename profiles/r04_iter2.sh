@@ -19,3 +19,6 @@ timeout -k 10 300 python -u profiles/c3_probe.py 3 > gpurun_out/$TAG/c3.json 2> 
 cat gpurun_out/$TAG/c3.json
 timeout -k 10 600 python -u bench.py --steps 10 --warmup 3 > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { tail -20 gpurun_out/$TAG/bench.err; exit 1; }
 python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print({k: d[k] for k in ('value','ms_per_step','p50_session_ms')}, d['config']['device_period_us'], d['config']['session_phases_ms'], d['roofline']['frac'])" gpurun_out/$TAG/bench.json
+KBHIP_OPEN_PROFILE=1 timeout -k 10 400 python -u bench_carry.py --rounds 2 > gpurun_out/$TAG/carry.json 2> gpurun_out/$TAG/carry.err || { tail -20 gpurun_out/$TAG/carry.err; exit 1; }
+cat gpurun_out/$TAG/carry.json
+grep "^\[carry\]" gpurun_out/$TAG/carry.err | tail -12
