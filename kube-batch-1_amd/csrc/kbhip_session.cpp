@@ -3651,9 +3651,37 @@ struct Allocator {
     uint32_t epoch = 0;
     vector<int> cand, inter;
     vector<uint32_t> mark;  // pod -> epoch: membership in the plugin's answer (the tier intersection)
+    // per action: the victim functions in tier order as codes (1 gang, 2 conformance, 3 drf,
+    // 4 proportion; the tiers' plugin names compared once, not per node visited), and per pod
+    // its job's queue and MinAvailable (read for every candidate of every visit)
+    vector<vector<int>> vic_tiers;
+    int vic_mode = -1;  // the action vic_tiers was compiled for (1 preempt, 0 reclaim)
+    vector<int32_t> pod_queue, pod_min;
     void reset_ready_cache() {
         ready_ok.assign(S.jobs.size(), 0);
         ready_val.assign(S.jobs.size(), 0);
+    }
+    void compile_victims(bool preempt) {
+        vic_mode = preempt ? 1 : 0;
+        vic_tiers.clear();
+        for (auto& tier : S.tiers) {
+            vector<int> codes;
+            for (auto& pl : tier) {
+                if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
+                if (pl.name == "gang") codes.push_back(1);
+                else if (pl.name == "conformance") codes.push_back(2);
+                else if (preempt && pl.name == "drf" && S.drf_on) codes.push_back(3);
+                else if (!preempt && pl.name == "proportion" && S.prop_on) codes.push_back(4);
+            }
+            vic_tiers.push_back(std::move(codes));
+        }
+        const int P = (int)S.pods.size();
+        pod_queue.assign(P, -1);
+        pod_min.assign(P, 0);
+        for (int i = 0; i < P; ++i) {
+            const int jb = S.pods[i].job;
+            if (jb >= 0) { pod_queue[i] = S.jobs[jb].queue; pod_min[i] = S.jobs[jb].min_avail; }
+        }
     }
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
         victims.clear();
@@ -3667,25 +3695,25 @@ struct Allocator {
             mark.assign(S.pods.size(), 0);
         }
         if (ready_ok.size() != S.jobs.size()) reset_ready_cache();
-        for (auto& tier : S.tiers) {
-            for (auto& pl : tier) {
-                if (pl.flags & (preempt ? KBS_DIS_PREEMPTABLE : KBS_DIS_RECLAIMABLE)) continue;
+        if (vic_mode != (preempt ? 1 : 0) || pod_queue.size() != S.pods.size()) compile_victims(preempt);
+        for (auto& tier : vic_tiers) {
+            for (int code : tier) {
                 cand.clear();
-                if (pl.name == "gang") {  // gang.go:107-129
+                if (code == 1) {  // gang.go:107-129
                     for (int e : evictees) {
                         const int jb = S.pods[e].job;
-                        const HJob& j = S.jobs[jb];
                         if (!ready_ok[jb]) {  // readyTaskNum (gang.go:212-222)
                             int c = 0;
-                            for (int t : j.tasks) c += gang_ready_status(S.pods[t].status);
+                            for (int t : S.jobs[jb].tasks) c += gang_ready_status(S.pods[t].status);
                             ready_ok[jb] = 1;
                             ready_val[jb] = c;
                         }
-                        if (j.min_avail <= ready_val[jb] - 1 || j.min_avail == 1) cand.push_back(e);
+                        const int mn = pod_min[e];
+                        if (mn <= ready_val[jb] - 1 || mn == 1) cand.push_back(e);
                     }
-                } else if (pl.name == "conformance") {  // conformance.go:37-56
+                } else if (code == 2) {  // conformance.go:37-56
                     for (int e : evictees) if (!S.pods[e].critical) cand.push_back(e);
-                } else if (preempt && pl.name == "drf" && S.drf_on) {  // drf.go:84-109
+                } else if (code == 3) {  // drf.go:84-109
                     const HPod& pr = S.pods[evictor];
                     F3 la = S.jobs[pr.job].drf_alloc;
                     la.add(pr.req);
@@ -3698,10 +3726,10 @@ struct Allocator {
                         const double rs = drf_share_of(alloc_val[jb]);
                         if (ls < rs || std::fabs(ls - rs) <= 0.000001) cand.push_back(e);  // shareDelta (drf.go:29)
                     }
-                } else if (!preempt && pl.name == "proportion" && S.prop_on) {  // proportion.go:159-183
+                } else if (code == 4) {  // proportion.go:159-183
                     const uint32_t ea = ++epoch;
                     for (int e : evictees) {
-                        const int qi = S.jobs[S.pods[e].job].queue;
+                        const int qi = pod_queue[e];
                         const HQueue& q = S.queues[qi];
                         if (alloc_stamp[qi] != ea) { alloc_stamp[qi] = ea; alloc_val[qi] = q.allocated; }
                         F3 rq;
@@ -3710,8 +3738,6 @@ struct Allocator {
                         alloc_val[qi].sub(S.pods[e].req);
                         if (q.deserved.less_equal(alloc_val[qi])) cand.push_back(e);
                     }
-                } else {
-                    continue;  // the plugin registers no such function
                 }
                 if (!init) {
                     victims = cand;
@@ -3790,6 +3816,7 @@ struct Allocator {
         open_plugins();
         check_evict_supported();
         build_node_tasks();
+        compile_victims(true);
         auto jl = [this](int a, int b) { return job_less(a, b); };
         std::map<int, GoHeap<decltype(jl)>> preemptors;
         std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;  // job -> (tasks, cursor)
@@ -3821,7 +3848,7 @@ struct Allocator {
                     const int pq = S.jobs[pj].queue, ptj = S.pods[pt].job;
                     if (preempt_one(st, pt, [&](int t) {
                             const HPod& p = S.pods[t];
-                            return node_copy_running(t) && p.job >= 0 && S.jobs[p.job].queue == pq && ptj != p.job;
+                            return node_copy_running(t) && p.job >= 0 && pod_queue[t] == pq && ptj != p.job;
                         }))
                         assigned = true;
                     if (job_ready(S.jobs[pj])) {
@@ -3861,6 +3888,7 @@ struct Allocator {
         open_plugins();
         check_evict_supported();
         build_node_tasks();
+        compile_victims(false);
         auto ql = [this](int a, int b) { return queue_less(a, b); };
         auto jl = [this](int a, int b) { return job_less(a, b); };
         GoHeap<decltype(ql)> queues(ql);
@@ -3896,7 +3924,7 @@ struct Allocator {
                 cands.clear();
                 for (int t : S.node_tasks[n]) {
                     const HPod& p = S.pods[t];
-                    if (node_copy_running(t) && p.job >= 0 && S.jobs[p.job].queue != jq) cands.push_back(t);
+                    if (node_copy_running(t) && p.job >= 0 && pod_queue[t] != jq) cands.push_back(t);
                 }
                 victims_of(false, pt, cands, victims);
                 if (victims.empty()) continue;
