@@ -3457,6 +3457,7 @@ struct Allocator {
         HJob& j = S.jobs[p.job];
         if (p.job < (int)ready_ok.size() && ready_ok[p.job])  // keep the cached readyTaskNum exact
             ready_val[p.job] += (int)gang_ready_status(st) - (int)gang_ready_status(p.status);
+        if (pi < (int)run_copy.size()) run_copy[pi] = (st == Running && !p.node_rel) ? 1 : 0;
         if (allocated_status(p.status)) j.cnt_alloc--;
         if (p.status == AOB) j.cnt_aob--;
         p.status = st;
@@ -3483,6 +3484,9 @@ struct Allocator {
         }
     }
     bool node_copy_running(int pi) const { return S.pods[pi].status == Running && !S.pods[pi].node_rel; }
+    // node_copy_running per pod as a byte (the candidate filters read it for every task of every
+    // node visited): built with pod_queue, kept exact by set_status and unevict
+    vector<uint8_t> run_copy;
     // The walk order of the task of class cls: preempt (by_score) = SelectBestNode order of
     // the nodes passing PredicateFn with a NodeOrderFn score; reclaim = passing nodes in order.
     void rank_nodes(int cls, bool by_score, vector<int>& out) {
@@ -3598,6 +3602,7 @@ struct Allocator {
         set_status(v, Running);
         queue_target(S, v, +1);  // a predicate target again (the lister reads the job's status index)
         S.pods[v].node_rel = true;
+        if (v < (int)run_copy.size()) run_copy[v] = 0;
         on_allocate(v);
     }
     void pipeline(int t, int n) {  // statement.go:96-136 / session.go:199-235
@@ -3678,9 +3683,11 @@ struct Allocator {
         const int P = (int)S.pods.size();
         pod_queue.assign(P, -1);
         pod_min.assign(P, 0);
+        run_copy.assign(P, 0);
         for (int i = 0; i < P; ++i) {
             const int jb = S.pods[i].job;
             if (jb >= 0) { pod_queue[i] = S.jobs[jb].queue; pod_min[i] = S.jobs[jb].min_avail; }
+            run_copy[i] = node_copy_running(i) ? 1 : 0;
         }
     }
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
@@ -3848,7 +3855,7 @@ struct Allocator {
                     const int pq = S.jobs[pj].queue, ptj = S.pods[pt].job;
                     if (preempt_one(st, pt, [&](int t) {
                             const HPod& p = S.pods[t];
-                            return node_copy_running(t) && p.job >= 0 && pod_queue[t] == pq && ptj != p.job;
+                            return run_copy[t] && p.job >= 0 && pod_queue[t] == pq && ptj != p.job;
                         }))
                         assigned = true;
                     if (job_ready(S.jobs[pj])) {
@@ -3871,7 +3878,7 @@ struct Allocator {
                     Stmt s2;
                     const int ptj = S.pods[pt].job;
                     const bool assigned = preempt_one(s2, pt, [&](int t) {
-                        return node_copy_running(t) && ptj == S.pods[t].job;
+                        return run_copy[t] && ptj == S.pods[t].job;
                     });
                     commit(s2);
                     if (!assigned) break;
@@ -3922,10 +3929,8 @@ struct Allocator {
             rank_nodes(pr.cls, false, order);
             for (int n : order) {
                 cands.clear();
-                for (int t : S.node_tasks[n]) {
-                    const HPod& p = S.pods[t];
-                    if (node_copy_running(t) && p.job >= 0 && pod_queue[t] != jq) cands.push_back(t);
-                }
+                for (int t : S.node_tasks[n])
+                    if (run_copy[t] && pod_queue[t] >= 0 && pod_queue[t] != jq) cands.push_back(t);
                 victims_of(false, pt, cands, victims);
                 if (victims.empty()) continue;
                 R3 all, resreq = pr.ireq, got;
