@@ -3684,11 +3684,9 @@ struct Allocator {
         pod_queue.assign(P, -1);
         pod_min.assign(P, 0);
         run_copy.assign(P, 0);
-        for (int i = 0; i < P; ++i) {
-            const int jb = S.pods[i].job;
-            if (jb >= 0) { pod_queue[i] = S.jobs[jb].queue; pod_min[i] = S.jobs[jb].min_avail; }
-            run_copy[i] = node_copy_running(i) ? 1 : 0;
-        }
+        for (const HJob& J : S.jobs)  // job-major: a job's tasks are neighbouring pods (not a job lookup per pod)
+            for (int t : J.tasks) { pod_queue[t] = J.queue; pod_min[t] = J.min_avail; }
+        for (int i = 0; i < P; ++i) run_copy[i] = node_copy_running(i) ? 1 : 0;
     }
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
         victims.clear();
