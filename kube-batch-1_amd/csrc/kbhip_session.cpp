@@ -500,6 +500,10 @@ struct Session {
     // fitting node lies below the list of walked nodes, or there is none) sends the class's
     // next pops to the general path directly (same records either way)
     vector<uint8_t> bf_backoff;
+    // reclaim / preempt: each pod's job queue and MinAvailable (Allocator::compile_victims), valid
+    // while pod_queue_gen == model_gen (every carry-over bumps model_gen)
+    vector<int32_t> pod_queue, pod_min;
+    uint64_t model_gen = 0, pod_queue_gen = ~0ull;
     bool plugins_opened = false;  // OnSessionOpen state of drf / proportion (once per session, every action sees it)
     // reclaim / preempt (kbhip_evict.hip): per-node order keys, their sorted copy, sort scratch, passing count
     DevBuf b_rank_keys, b_rank_sorted, b_rank_tmp, b_rank_cnt, b_rank_radix;
@@ -3466,22 +3470,26 @@ struct Allocator {
         j.priority = p.priority;
     }
     void build_node_tasks() {  // NodeInfo.Tasks of every node from the host model
+        // one pass over the pod records (≈ 160 MB at C5): the (node, pod) pairs, each pod's
+        // running-copy byte; then the lists, sized first (one allocation per node, kept across actions)
         const int N = S.nc.n, P = (int)S.pods.size();
-        vector<int32_t> cnt(N, 0);  // sized first: one allocation per node, lists kept across actions
+        vector<int32_t> cnt(N, 0);
+        vector<std::pair<int32_t, int32_t>> on;
+        on.reserve(P);
+        run_copy.assign(P, 0);
         for (int i = 0; i < P; ++i) {
             const HPod& p = S.pods[i];
-            if (on_node_of(p) && p.status != Pending) cnt[p.node]++;
+            run_copy[i] = (p.status == Running && !p.node_rel) ? 1 : 0;
+            if (!on_node_of(p) || p.status == Pending) continue;
+            cnt[p.node]++;
+            on.emplace_back(p.node, i);
         }
         S.node_tasks.resize(N);
         for (int n = 0; n < N; ++n) {
             S.node_tasks[n].clear();
             S.node_tasks[n].reserve(cnt[n]);
         }
-        for (int i = 0; i < P; ++i) {
-            const HPod& p = S.pods[i];
-            if (!on_node_of(p) || p.status == Pending) continue;
-            S.node_tasks[p.node].push_back(i);
-        }
+        for (auto& x : on) S.node_tasks[x.first].push_back(x.second);
     }
     bool node_copy_running(int pi) const { return S.pods[pi].status == Running && !S.pods[pi].node_rel; }
     // node_copy_running per pod as a byte (the candidate filters read it for every task of every
@@ -3661,7 +3669,6 @@ struct Allocator {
     // its job's queue and MinAvailable (read for every candidate of every visit)
     vector<vector<int>> vic_tiers;
     int vic_mode = -1;  // the action vic_tiers was compiled for (1 preempt, 0 reclaim)
-    vector<int32_t> pod_queue, pod_min;
     void reset_ready_cache() {
         ready_ok.assign(S.jobs.size(), 0);
         ready_val.assign(S.jobs.size(), 0);
@@ -3681,12 +3688,17 @@ struct Allocator {
             vic_tiers.push_back(std::move(codes));
         }
         const int P = (int)S.pods.size();
-        pod_queue.assign(P, -1);
-        pod_min.assign(P, 0);
-        run_copy.assign(P, 0);
-        for (const HJob& J : S.jobs)  // job-major: a job's tasks are neighbouring pods (not a job lookup per pod)
-            for (int t : J.tasks) { pod_queue[t] = J.queue; pod_min[t] = J.min_avail; }
-        for (int i = 0; i < P; ++i) run_copy[i] = node_copy_running(i) ? 1 : 0;
+        if ((int)run_copy.size() != P) {  // (build_node_tasks fills it in its pass over the pods)
+            run_copy.assign(P, 0);
+            for (int i = 0; i < P; ++i) run_copy[i] = node_copy_running(i) ? 1 : 0;
+        }
+        if ((int)S.pod_queue.size() != P || S.pod_queue_gen != S.model_gen) {  // once per session model
+            S.pod_queue.assign(P, -1);
+            S.pod_min.assign(P, 0);
+            for (const HJob& J : S.jobs)  // job-major: a job's tasks are neighbouring pods
+                for (int t : J.tasks) { S.pod_queue[t] = J.queue; S.pod_min[t] = J.min_avail; }
+            S.pod_queue_gen = S.model_gen;
+        }
     }
     void victims_of(bool preempt, int evictor, const vector<int>& evictees, vector<int>& victims) {
         victims.clear();
@@ -3700,7 +3712,7 @@ struct Allocator {
             mark.assign(S.pods.size(), 0);
         }
         if (ready_ok.size() != S.jobs.size()) reset_ready_cache();
-        if (vic_mode != (preempt ? 1 : 0) || pod_queue.size() != S.pods.size()) compile_victims(preempt);
+        if (vic_mode != (preempt ? 1 : 0) || S.pod_queue.size() != S.pods.size()) compile_victims(preempt);
         for (auto& tier : vic_tiers) {
             for (int code : tier) {
                 cand.clear();
@@ -3713,7 +3725,7 @@ struct Allocator {
                             ready_ok[jb] = 1;
                             ready_val[jb] = c;
                         }
-                        const int mn = pod_min[e];
+                        const int mn = S.pod_min[e];
                         if (mn <= ready_val[jb] - 1 || mn == 1) cand.push_back(e);
                     }
                 } else if (code == 2) {  // conformance.go:37-56
@@ -3734,7 +3746,7 @@ struct Allocator {
                 } else if (code == 4) {  // proportion.go:159-183
                     const uint32_t ea = ++epoch;
                     for (int e : evictees) {
-                        const int qi = pod_queue[e];
+                        const int qi = S.pod_queue[e];
                         const HQueue& q = S.queues[qi];
                         if (alloc_stamp[qi] != ea) { alloc_stamp[qi] = ea; alloc_val[qi] = q.allocated; }
                         F3 rq;
@@ -3853,7 +3865,7 @@ struct Allocator {
                     const int pq = S.jobs[pj].queue, ptj = S.pods[pt].job;
                     if (preempt_one(st, pt, [&](int t) {
                             const HPod& p = S.pods[t];
-                            return run_copy[t] && p.job >= 0 && pod_queue[t] == pq && ptj != p.job;
+                            return run_copy[t] && p.job >= 0 && S.pod_queue[t] == pq && ptj != p.job;
                         }))
                         assigned = true;
                     if (job_ready(S.jobs[pj])) {
@@ -3928,7 +3940,7 @@ struct Allocator {
             for (int n : order) {
                 cands.clear();
                 for (int t : S.node_tasks[n])
-                    if (run_copy[t] && pod_queue[t] >= 0 && pod_queue[t] != jq) cands.push_back(t);
+                    if (run_copy[t] && S.pod_queue[t] >= 0 && S.pod_queue[t] != jq) cands.push_back(t);
                 victims_of(false, pt, cands, victims);
                 if (victims.empty()) continue;
                 R3 all, resreq = pr.ireq, got;
@@ -4400,6 +4412,7 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // Succeeded / Failed (isTerminated: the task stays in its job, off its node).
 // New pods, node and PodGroup changes: kbhip_session_carry_snapshot.
 static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0) {
+    S.model_gen++;  // per-pod caches of the host model (Session::pod_queue) are rebuilt
     // every node's row is recomputed on the host (a shard's host model holds
     // all of them); this device's rows [lo, lo + Nl) are compared and uploaded
     const int N = (int)S.h_alloc.size(), Nl = S.nc.n, lo = S.nc.base, P = (int)S.pods.size();
@@ -4731,6 +4744,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     mark("maps");
     ov_quiesce(S);
     HIPCHK(hipStreamSynchronize(S.stream));
+    S.model_gen++;  // jobs are renumbered: per-pod caches of the host model are rebuilt
     if (!carry_fast_ok(S, s, v, old_pod, old_node)) {
         reopen_in_place(ks, s);
         return;
