@@ -73,7 +73,7 @@ def main():
             if a in ("reclaim", "preempt"):
                 n_rank += st1["sweeps"] - st0["sweeps"]  # one node-ranking sweep per reclaim / preempt task
                 launches[a] = {k: st1[k] - st0[k] for k in ("evict_rank_s", "evict_walk_s", "evict_visits",
-                                                            "evict_cands")}
+                                                            "evict_cands", "evict_setup_s")}
             else:  # batched pops (one launch places a chunk) vs per-task sweeps
                 bp = st1["batched_pops"] - st0["batched_pops"]
                 launches[a] = {"batched_pops": bp, "per_task_sweeps": st1["sweeps"] - st0["sweeps"] - bp}

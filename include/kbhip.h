@@ -120,6 +120,8 @@ typedef struct kbhip_stats {
     int64_t evict_cands;     /* ... candidates handed to those calls */
     int64_t fit_syncs;       /* allocate: FitDelta histograms recounted after a pop (a job left not Ready) */
     double alloc_setup_s;    /* allocate: host time before the first pop (plugin open, job and queue heaps) */
+    double evict_setup_s;    /* reclaim / preempt: host time before the first node ranking (plugin open, node
+                                task lists, victim codes, job heaps); part of evict_walk_s */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

@@ -3470,26 +3470,71 @@ struct Allocator {
         j.priority = p.priority;
     }
     void build_node_tasks() {  // NodeInfo.Tasks of every node from the host model
-        // one pass over the pod records (≈ 160 MB at C5): the (node, pod) pairs, each pod's
-        // running-copy byte; then the lists, sized first (one allocation per node, kept across actions)
+        // two passes over the pod records (≈ 110 MB at C5) by pod ranges in parallel: each
+        // pod's running-copy byte and per range the tasks per node; then each node's list
+        // sized and the ranges' pods written at their offsets (pod order within a node kept)
         const int N = S.nc.n, P = (int)S.pods.size();
-        vector<int32_t> cnt(N, 0);
-        vector<std::pair<int32_t, int32_t>> on;
-        on.reserve(P);
+        const int nth = P < (1 << 16) ? 1 : 8;
+        vector<vector<int32_t>> cnt(nth, vector<int32_t>(N, 0));
         run_copy.assign(P, 0);
-        for (int i = 0; i < P; ++i) {
-            const HPod& p = S.pods[i];
-            run_copy[i] = (p.status == Running && !p.node_rel) ? 1 : 0;
-            if (!on_node_of(p) || p.status == Pending) continue;
-            cnt[p.node]++;
-            on.emplace_back(p.node, i);
-        }
+        auto range = [&](int r, int& b, int& e) { b = (int)((int64_t)P * r / nth); e = (int)((int64_t)P * (r + 1) / nth); };
+        run_ranges(nth, [&](int r) {
+            int b, e;
+            range(r, b, e);
+            int32_t* c = cnt[r].data();
+            for (int i = b; i < e; ++i) {
+                const HPod& p = S.pods[i];
+                run_copy[i] = (p.status == Running && !p.node_rel) ? 1 : 0;
+                if (on_node_of(p) && p.status != Pending) c[p.node]++;
+            }
+        });
         S.node_tasks.resize(N);
         for (int n = 0; n < N; ++n) {
-            S.node_tasks[n].clear();
-            S.node_tasks[n].reserve(cnt[n]);
+            int32_t base = 0;
+            for (int r = 0; r < nth; ++r) { const int32_t k = cnt[r][n]; cnt[r][n] = base; base += k; }
+            S.node_tasks[n].resize(base);
         }
-        for (auto& x : on) S.node_tasks[x.first].push_back(x.second);
+        run_ranges(nth, [&](int r) {
+            int b, e;
+            range(r, b, e);
+            int32_t* c = cnt[r].data();
+            for (int i = b; i < e; ++i) {
+                const HPod& p = S.pods[i];
+                if (on_node_of(p) && p.status != Pending) S.node_tasks[p.node][c[p.node]++] = i;
+            }
+        });
+    }
+    // fn(0..nth-1), fn(0) on this thread
+    template <typename Fn>
+    static void run_ranges(int nth, Fn fn) {
+        vector<std::thread> th;
+        for (int r = 1; r < nth; ++r) th.emplace_back(fn, r);
+        fn(0);
+        for (auto& x : th) x.join();
+    }
+    // The eviction actions' job scan (reclaim.go:60-90 / preempt.go:58-85 build their
+    // preemptor lists from every job's Pending tasks): per job its Pending tasks in
+    // TaskOrderFn order, and gang's readyTaskNum (gang.go:212-222) of every job, kept exact
+    // from here on by set_status; job ranges in parallel
+    void scan_jobs(vector<vector<int>>& pend) {
+        const int J = (int)S.jobs.size();
+        pend.assign(J, {});
+        reset_ready_cache();
+        const int nth = S.pods.size() < (1u << 16) ? 1 : 8;
+        run_ranges(nth, [&](int r) {
+            for (int jb = (int)((int64_t)J * r / nth); jb < (int)((int64_t)J * (r + 1) / nth); ++jb) {
+                int c = 0;
+                for (int t : S.jobs[jb].tasks) {
+                    const int st = S.pods[t].status;
+                    c += gang_ready_status(st);
+                    if (st == Pending) pend[jb].push_back(t);
+                }
+                ready_val[jb] = c;
+                ready_ok[jb] = 1;
+                if (pend[jb].size() > 1)
+                    std::sort(pend[jb].begin(), pend[jb].end(), [this](int a, int b) { return task_less(a, b); });
+            }
+        });
     }
     bool node_copy_running(int pi) const { return S.pods[pi].status == Running && !S.pods[pi].node_rel; }
     // node_copy_running per pod as a byte (the candidate filters read it for every task of every
@@ -3783,7 +3828,12 @@ struct Allocator {
         if (pr.cls < 0) throw Error(KBHIP_EUNSUPPORTED, "preemptor without a task class");
         vector<int> order, cands, victims;
         rank_nodes(pr.cls, true, order);
-        for (int n : order) {
+        const int no = (int)order.size();
+        for (int i = 0; i < std::min(no, kPrefetchAhead); ++i) prefetch_pods(order[i]);
+        for (int oi = 0; oi < no; ++oi) {
+            const int n = order[oi];
+            if (oi + kPrefetchAhead < no) prefetch_pods(order[oi + kPrefetchAhead]);
+            if (oi + 1 < no) prefetch_jobs(order[oi + 1]);
             cands.clear();
             for (int t : S.node_tasks[n]) if (keep(t)) cands.push_back(t);
             victims_of(true, pi, cands, victims);
@@ -3807,19 +3857,57 @@ struct Allocator {
         }
         return false;
     }
-    // pending tasks of a job in TaskOrderFn order (a strict total order: heap pops = sorted order)
-    vector<int> pending_sorted(const HJob& j) {
-        vector<int> v;
-        for (int t : j.tasks) if (S.pods[t].status == Pending) v.push_back(t);
-        std::sort(v.begin(), v.end(), [this](int a, int b) { return task_less(a, b); });
-        return v;
+    // The walks read the records of every task on each visited node (run copy, queue,
+    // MinAvailable, job, request) and evict most candidates (C5: ≈ 2.4 M candidates and
+    // ≈ 720 k evictions per reclaim, pods scattered over 160 MB of records): the next
+    // nodes' records are prefetched while one node is visited (the order is known), their
+    // jobs one visit ahead (the job index is in the pod record fetched before).
+    static constexpr int kPrefetchAhead = 3;
+    void prefetch_pods(int n) {
+        for (int t : S.node_tasks[n]) {
+            const char* pp = reinterpret_cast<const char*>(&S.pods[t]);
+            for (size_t o = 0; o < sizeof(HPod); o += 64) __builtin_prefetch(pp + o);
+            __builtin_prefetch(pp + sizeof(HPod) - 1);
+            __builtin_prefetch(&run_copy[t]);
+            __builtin_prefetch(&S.pod_queue[t]);
+            __builtin_prefetch(&S.pod_min[t]);
+        }
     }
+    void prefetch_jobs(int n) {
+        for (int t : S.node_tasks[n]) {
+            const int jb = S.pods[t].job;
+            if (jb < 0) continue;
+            const char* jp = reinterpret_cast<const char*>(&S.jobs[jb]);
+            for (size_t o = 0; o < sizeof(HJob); o += 64) __builtin_prefetch(jp + o);
+            __builtin_prefetch(jp + sizeof(HJob) - 1);
+            __builtin_prefetch(&ready_val[jb]);
+        }
+    }
+#ifdef KBHIP_WALK_PROF  // diagnostic build: reclaim walk split (gather / victims / evictions), stderr
+    uint64_t wp_acc[3] = {0, 0, 0}, wp_last = 0;
+    int wp_ph = -1;
+    void wp_mark(int ph) {
+        const uint64_t t = __builtin_ia32_rdtsc();
+        if (wp_ph >= 0) wp_acc[wp_ph] += t - wp_last;
+        wp_last = t;
+        wp_ph = ph;
+    }
+#define WP_MARK(ph) wp_mark(ph)
+#define WP_REPORT(name) (fprintf(stderr, "walkprof %s gather %.3g victims %.3g evict %.3g Gcycles\n", name, \
+                                 wp_acc[0] * 1e-9, wp_acc[1] * 1e-9, wp_acc[2] * 1e-9), wp_ph = -1)
+#else
+#define WP_MARK(ph) ((void)0)
+#define WP_REPORT(name) ((void)0)
+#endif
     // host wall time of an eviction action minus its node rankings (stats.evict_walk_s)
     struct WalkTimer {
         Session& S;
         std::chrono::steady_clock::time_point t0;
         double rank0;
         explicit WalkTimer(Session& s) : S(s), t0(std::chrono::steady_clock::now()), rank0(s.stats.evict_rank_s) {}
+        void setup_done() {
+            S.stats.evict_setup_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
         ~WalkTimer() {
             S.stats.evict_walk_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() -
                                     (S.stats.evict_rank_s - rank0);
@@ -3839,10 +3927,12 @@ struct Allocator {
         std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;  // job -> (tasks, cursor)
         vector<int> under;
         vector<char> seen(S.queues.size(), 0);
+        vector<vector<int>> pends;
+        scan_jobs(pends);
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
             seen[j.queue] = 1;
-            vector<int> pend = pending_sorted(j);
+            vector<int>& pend = pends[jb];
             if (pend.empty()) continue;
             auto it = preemptors.find(j.queue);
             if (it == preemptors.end()) it = preemptors.emplace(j.queue, GoHeap<decltype(jl)>(jl)).first;
@@ -3850,6 +3940,7 @@ struct Allocator {
             under.push_back(jb);
             ptasks[jb] = {std::move(pend), 0};
         }
+        wt.setup_done();
         Stmt st;
         for (int qi = 0; qi < (int)S.queues.size(); ++qi) {  // map `queues`, pinned to queue order
             if (!seen[qi]) continue;
@@ -3912,16 +4003,19 @@ struct Allocator {
         vector<char> qseen(S.queues.size(), 0);
         std::map<int, GoHeap<decltype(jl)>> preemptors;
         std::unordered_map<int, std::pair<vector<int>, size_t>> ptasks;
+        vector<vector<int>> pends;
+        scan_jobs(pends);
         for (int jb = 0; jb < (int)S.jobs.size(); ++jb) {
             HJob& j = S.jobs[jb];
             if (!qseen[j.queue]) { qseen[j.queue] = 1; queues.push(j.queue); }
-            vector<int> pend = pending_sorted(j);
+            vector<int>& pend = pends[jb];
             if (pend.empty()) continue;
             auto it = preemptors.find(j.queue);
             if (it == preemptors.end()) it = preemptors.emplace(j.queue, GoHeap<decltype(jl)>(jl)).first;
             it->second.push(jb);
             ptasks[jb] = {std::move(pend), 0};
         }
+        wt.setup_done();
         vector<int> order, cands, victims;
         while (!queues.empty()) {
             const int qi = queues.pop();
@@ -3937,11 +4031,19 @@ struct Allocator {
             const int jq = S.jobs[jb].queue;
             bool assigned = false;
             rank_nodes(pr.cls, false, order);
-            for (int n : order) {
+            const int no = (int)order.size();
+            for (int i = 0; i < std::min(no, kPrefetchAhead); ++i) prefetch_pods(order[i]);
+            for (int oi = 0; oi < no; ++oi) {
+                const int n = order[oi];
+                WP_MARK(0);
+                if (oi + kPrefetchAhead < no) prefetch_pods(order[oi + kPrefetchAhead]);
+                if (oi + 1 < no) prefetch_jobs(order[oi + 1]);
                 cands.clear();
                 for (int t : S.node_tasks[n])
                     if (run_copy[t] && S.pod_queue[t] >= 0 && S.pod_queue[t] != jq) cands.push_back(t);
+                WP_MARK(1);
                 victims_of(false, pt, cands, victims);
+                WP_MARK(2);
                 if (victims.empty()) continue;
                 R3 all, resreq = pr.ireq, got;
                 for (int v : victims) { all.c += S.pods[v].req.c; all.m += S.pods[v].req.m; all.g += S.pods[v].req.g; }
@@ -3964,6 +4066,8 @@ struct Allocator {
             }
             if (assigned) queues.push(qi);
         }
+        WP_MARK(0);
+        WP_REPORT("reclaim");
         flush_evictions();
         HIPCHK(hipStreamSynchronize(S.stream));
     }

@@ -2,6 +2,10 @@
 # from another revision of kbhip_session.cpp), alternating.
 set -o pipefail
 mkdir -p gpurun_out/r04ab
+if [ -n "$AB_TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest $AB_TESTS -x -q --timeout 300 --timeout-method thread > gpurun_out/r04ab/tests.log 2>&1 || { tail -30 gpurun_out/r04ab/tests.log; exit 1; }
+  tail -3 gpurun_out/r04ab/tests.log
+fi
 for R in 1 2 3; do
   for V in a b; do
     if [ $V = b ]; then export KBHIP_LIB=kube-batch-1_amd/_build/libkbhip_b.so; else unset KBHIP_LIB; fi
