@@ -195,6 +195,24 @@ hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t
     return hipGetLastError();
 }
 
+// Carry-over's node rows (kbhip_session_carry_snapshot): every element that differs
+// from the read-back device rows, packed on the host, written in one launch
+// (instead of one copy per run of differing rows).
+__global__ __launch_bounds__(kBlock) void k_row_patch(const RowPatch* e, int n) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const RowPatch p = e[i];
+    if (p.size == 8) *reinterpret_cast<uint64_t*>(p.addr) = p.val;
+    else if (p.size == 4) *reinterpret_cast<uint32_t*>(p.addr) = (uint32_t)p.val;
+    else *reinterpret_cast<uint8_t*>(p.addr) = (uint8_t)p.val;
+}
+
+hipError_t launch_row_patch(const RowPatch* e, int n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_row_patch, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, st, e, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_rank_nodes(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
                              int by_score, uint64_t* keys, uint32_t* count, hipStream_t st) {
     int grid = (nc.n + kBlock - 1) / kBlock;

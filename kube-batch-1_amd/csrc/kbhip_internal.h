@@ -84,6 +84,12 @@ hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_
 // Count-table deltas (pod (anti-)affinity): idx >= 0 aff_cnt, < 0 aff_scalar[-1 - idx]; distinct indices.
 hipError_t launch_tab_add(const DevTables& t, const int32_t* idx, const int32_t* delta, int n, hipStream_t st);
 hipError_t launch_rel_add(const NodeCols& nc, const int32_t* node, const int64_t* d, int n, hipStream_t st);
+// carry's node-row patch: entry i writes the low size bytes (8, 4 or 1) of val at device address addr
+struct RowPatch {
+    uint64_t addr, val;
+    int32_t size, pad;
+};
+hipError_t launch_row_patch(const RowPatch* e, int n, hipStream_t st);
 hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
                           int64_t rg, hipStream_t st);
 

@@ -4833,13 +4833,28 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     require_no_tickets(S);
     const PodView v(s);
     const int P = v.P, Pold = (int)S.pods.size(), N = (int)s.rows("n_name"), Nold = (int)S.h_alloc.size();
-    {  // the maps: indices in range, each old pod / node at most once
-        vector<char> seen(std::max(Pold, Nold), 0);
-        for (int i = 0; i < P; ++i) {
-            const int o = old_pod[i];
-            if (o < -1 || o >= Pold || (o >= 0 && seen[o]++)) throw Error(KBHIP_EINVAL, "bad old_pod map");
+    {  // the maps: indices in range, each old pod / node at most once (the pod map by ranges in parallel)
+        const size_t ns = (size_t)std::max(Pold, Nold);
+        {
+            std::unique_ptr<std::atomic<uint8_t>[]> seen_p(new std::atomic<uint8_t>[ns]());
+            std::atomic<bool> bad{false};
+            const int nth = P < (1 << 16) ? 1 : 8;
+            auto chk = [&](int t) {
+                for (int i = (int)((int64_t)P * t / nth); i < (int)((int64_t)P * (t + 1) / nth); ++i) {
+                    const int o = old_pod[i];
+                    if (o < -1 || o >= Pold || (o >= 0 && seen_p[o].fetch_or(1, std::memory_order_relaxed))) {
+                        bad = true;
+                        return;
+                    }
+                }
+            };
+            vector<std::thread> th;
+            for (int t = 1; t < nth; ++t) th.emplace_back(chk, t);
+            chk(0);
+            for (auto& x : th) x.join();
+            if (bad) throw Error(KBHIP_EINVAL, "bad old_pod map");
         }
-        std::fill(seen.begin(), seen.end(), 0);
+        vector<char> seen(ns, 0);
         for (int n = 0; n < N; ++n) {
             const int o = old_node[n];
             if (o < -1 || o >= Nold || (o >= 0 && seen[o]++)) throw Error(KBHIP_EINVAL, "bad old_node map");
@@ -4876,6 +4891,39 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         }
     }
     mark("checks");
+    // the device node rows, read back into pinned memory while the host model is rebuilt
+    // (compared with the new rows at the upload: only rows that differ are written)
+    const int Nl = S.nc.n;
+    struct ColRef { void* d; size_t elem, off; };
+    vector<ColRef> dcols;
+    size_t stage_bytes = 0;
+    auto add_col = [&](void* d, size_t elem) {
+        dcols.push_back({d, elem, stage_bytes});
+        stage_bytes += ((size_t)Nl * elem + 255) & ~(size_t)255;
+    };
+    int64_t* dcol[13] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem, S.nc.rel_gpu,
+                         S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu, S.nc.acpu, S.nc.amem, S.nc.nzc, S.nc.nzm};
+    for (int k = 0; k < 13; ++k) add_col(dcol[k], sizeof(int64_t));
+    add_col(S.nc.pods, sizeof(int32_t));
+    add_col(S.nc.maxtasks, sizeof(int32_t));
+    add_col(S.nc.flags, sizeof(uint8_t));
+    for (int w = 0; w < S.nc.port_words; ++w) add_col(S.nc.ports + (size_t)w * S.nc.npad, sizeof(uint64_t));
+    struct Stage {  // pooled pinned buffer, returned on every exit (after the stream has drained)
+        uint8_t* p = nullptr;
+        size_t cap = 0;
+        int dev = 0;
+        hipStream_t st = nullptr;
+        ~Stage() {
+            if (!p) return;
+            (void)hipStreamSynchronize(st);
+            MemPool::get().give(MemPool::kPinned, p, cap, dev);
+        }
+    } stage;
+    stage.dev = S.device;
+    stage.st = S.stream;
+    stage.p = (uint8_t*)MemPool::get().take(MemPool::kPinned, std::max<size_t>(stage_bytes, 256), &stage.cap);
+    for (auto& c : dcols)
+        HIPCHK(hipMemcpyAsync(stage.p + c.off, c.d, (size_t)Nl * c.elem, hipMemcpyDeviceToHost, S.stream));
     // ---------------- nodes: allocatable, pods, unschedulable (labels / taints unchanged) ----------------
     auto acpu = s.vec<int64_t>("n_alloc_cpu"), amem = s.vec<int64_t>("n_alloc_mem"), agpu = s.vec<int64_t>("n_alloc_gpu"),
          apods = s.vec<int64_t>("n_alloc_pods");
@@ -4892,6 +4940,95 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         auto it = node_idx.find(nm);
         return it == node_idx.end() ? -1 : it->second;
     };
+    // ---------------- queues & jobs (as at open) ----------------
+    auto qn = s.vec<int32_t>("q_name"), qw = s.vec<int32_t>("q_weight");
+    auto qts = s.vec<int64_t>("q_ts");
+    std::map<string, int> qidx;
+    vector<HQueue> queues(qn.size());
+    for (size_t i = 0; i < qn.size(); ++i) {
+        queues[i].name = s.s(qn[i]);
+        queues[i].weight = qw[i];
+        queues[i].ts = qts.empty() ? 0 : qts[i];
+        qidx[queues[i].name] = (int)i;
+    }
+    {
+        int r = 0;
+        std::map<string, int> rank;
+        for (auto& kv : qidx) rank[kv.first] = r++;
+        for (auto& q : queues) q.rank = rank[q.name];
+    }
+    auto jns = s.vec<int32_t>("j_ns"), jname = s.vec<int32_t>("j_name"), jq = s.vec<int32_t>("j_queue"),
+         jmin = s.vec<int32_t>("j_min"), jpri = s.vec<int32_t>("j_pg_priority");
+    auto jts = s.vec<int64_t>("j_ts");
+    struct Src { string uid; int row, pod; };
+    vector<Src> srcs;
+    const int JN = (int)jns.size();
+    const int jth = JN < (1 << 13) ? 1 : 8;
+    srcs.resize(JN);
+    auto par_j = [&](auto&& fn) {
+        vector<std::thread> th;
+        for (int t = 1; t < jth; ++t) th.emplace_back(fn, t);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    par_j([&](int t) {  // job UIDs (namespace/name) by job ranges
+        for (int j = (int)((int64_t)JN * t / jth); j < (int)((int64_t)JN * (t + 1) / jth); ++j)
+            srcs[j] = {s.s(jns[j]) + "/" + s.s(jname[j]), j, -1};
+    });
+    for (int i = 0; i < P; ++i) {
+        if (v.pjob[i] >= JN) throw Error(KBHIP_EINVAL, "pod job index out of range");
+        if (v.pjob[i] < 0) srcs.push_back({s.s(v.puid[i]), -1, i});  // shadow PodGroup
+    }
+    {
+        const int ns = (int)srcs.size();
+        std::atomic<bool> sorted{true};
+        if (jth == 1 || ns != JN) {
+            sorted = std::is_sorted(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+        } else {
+            par_j([&](int t) {  // UID order checked by ranges
+                for (int j = std::max(1, (int)((int64_t)ns * t / jth)); j < (int)((int64_t)ns * (t + 1) / jth); ++j)
+                    if (srcs[j].uid < srcs[j - 1].uid) { sorted = false; return; }
+            });
+        }
+        if (!sorted)
+            std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
+    }
+    mark("jobs:srcs");
+    vector<HJob> jobs;
+    vector<string> job_uid;
+    jobs.reserve(srcs.size());
+    job_uid.reserve(srcs.size());
+    vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
+    const auto default_q = qidx.find("default");
+    std::unordered_map<int32_t, int> qslot_of;  // queue name (interned string offset) -> queue slot
+    for (auto& src : srcs) {
+        int qslot = -1;
+        if (src.row >= 0) {
+            auto qc = qslot_of.find(jq[src.row]);
+            if (qc == qslot_of.end()) {
+                auto qit = qidx.find(s.s(jq[src.row]));
+                qc = qslot_of.emplace(jq[src.row], qit == qidx.end() ? -1 : qit->second).first;
+            }
+            qslot = qc->second;
+        } else {
+            qslot = default_q == qidx.end() ? -1 : default_q->second;
+        }
+        int slot = -1;
+        if (qslot >= 0) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
+            HJob j;
+            j.queue = qslot;
+            j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
+            j.ts = src.row >= 0 ? jts[src.row] : 0;
+            j.priority = j.pg_priority = src.row >= 0 ? jpri[src.row] : 0;
+            j.shadow = src.row < 0;
+            slot = (int)jobs.size();
+            jobs.push_back(std::move(j));
+            job_uid.push_back(std::move(src.uid));
+        }
+        if (src.row >= 0) row_slot[src.row] = slot;
+        else shadow_slot[src.pod] = slot;
+    }
+    mark("jobs:slots");
     // ---------------- pods ----------------
     vector<HPod> pods;  // the pooled array (its pages already mapped): every element is assigned below
     spare_pods().take_keep(pods);
@@ -4904,6 +5041,10 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     auto tlk = s.span<int32_t>("tl_key"), tlo = s.span<int32_t>("tl_op"), tlv = s.span<int32_t>("tl_val"),
          tle = s.span<int32_t>("tl_effect");
     vector<int> new_classes;  // classes this carry appended
+    // the pod pass's ranges; per range the tasks per job (the job task lists' offsets below)
+    const int jth_p = P < (1 << 15) ? 1 : 8;
+    const int per_p = (P + jth_p - 1) / jth_p;
+    vector<vector<int32_t>> jcnt(jth_p, vector<int32_t>(jobs.size(), 0));
     {
         // node names of new bound pods and of pods whose node changed are looked up in a map
         // built up front (read-only in the parallel pass below)
@@ -4912,7 +5053,8 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         if (need_map) find_node("");
         std::atomic<int> bad_pod{-1};
         vector<int32_t> pcount(P, 0);
-        auto pass = [&](int lo, int hi) {  // the pods' records (kept or decoded), status and node
+        auto pass = [&](int t, int lo, int hi) {  // the pods' records (kept or decoded), status, node, job
+            int32_t* jc = jcnt[t].data();
             for (int i = lo; i < hi; ++i) {
                 HPod& p = pods[i];
                 const int o = old_pod[i];
@@ -4922,6 +5064,8 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
                     p = HPod{};
                     v.spec(i, p);
                 }
+                p.job = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];  // session job slot
+                if (p.job >= 0) jc[p.job]++;
                 p.uid_rank = i;
                 p.status = v.status(i);
                 p.node = -1;
@@ -4948,15 +5092,14 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
                 pcount[i] = o >= 0 ? S.pod_port_off[o + 1] - S.pod_port_off[o] : 0;
             }
         };
-        constexpr int kThreads = 8;
         auto run = [&]() {
-            if (P < (1 << 15)) {
-                pass(0, P);
+            for (auto& c : jcnt) std::fill(c.begin(), c.end(), 0);
+            if (jth_p == 1) {
+                pass(0, 0, P);
             } else {
-                const int per = (P + kThreads - 1) / kThreads;
                 vector<std::thread> th;
-                for (int t = 1; t < kThreads; ++t) th.emplace_back(pass, t * per, std::min(P, (t + 1) * per));
-                pass(0, std::min(P, per));
+                for (int t = 1; t < jth_p; ++t) th.emplace_back(pass, t, t * per_p, std::min(P, (t + 1) * per_p));
+                pass(0, 0, std::min(P, per_p));
                 for (auto& x : th) x.join();
             }
         };
@@ -4971,104 +5114,32 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
             throw Error(KBHIP_EINVAL, "pod " + s.s(v.puid[i]) + " is bound to node " + s.s(v.pnode[i]) +
                                           " which is not in the snapshot");
         }
-        for (int i = 0; i < P; ++i) {  // namespace ids of new pods (the kept dictionary grows in order)
+        for (int i = 0; i < P; ++i)  // namespace ids of new pods (the kept dictionary grows in order)
             if (old_pod[i] < 0) pods[i].ns = S.keep.nss.get(s.s(pns[i]));
-            port_off[i + 1] = port_off[i] + pcount[i];
+        if (!S.pod_port_ids.empty()) {  // kept pods' host ports (none held: every offset stays 0)
+            for (int i = 0; i < P; ++i) port_off[i + 1] = port_off[i] + pcount[i];
+            port_ids.resize(port_off[P]);
+            for (int i = 0; i < P; ++i)
+                if (pcount[i])
+                    std::copy(S.pod_port_ids.begin() + S.pod_port_off[old_pod[i]],
+                              S.pod_port_ids.begin() + S.pod_port_off[old_pod[i] + 1], port_ids.begin() + port_off[i]);
         }
-        port_ids.resize(port_off[P]);
-        for (int i = 0; i < P; ++i)
-            if (pcount[i])
-                std::copy(S.pod_port_ids.begin() + S.pod_port_off[old_pod[i]],
-                          S.pod_port_ids.begin() + S.pod_port_off[old_pod[i] + 1], port_ids.begin() + port_off[i]);
     }
     mark("pods");
-    // ---------------- queues & jobs (as at open) ----------------
-    auto qn = s.vec<int32_t>("q_name"), qw = s.vec<int32_t>("q_weight");
-    auto qts = s.vec<int64_t>("q_ts");
-    std::map<string, int> qidx;
-    vector<HQueue> queues(qn.size());
-    for (size_t i = 0; i < qn.size(); ++i) {
-        queues[i].name = s.s(qn[i]);
-        queues[i].weight = qw[i];
-        queues[i].ts = qts.empty() ? 0 : qts[i];
-        qidx[queues[i].name] = (int)i;
-    }
-    {
-        int r = 0;
-        std::map<string, int> rank;
-        for (auto& kv : qidx) rank[kv.first] = r++;
-        for (auto& q : queues) q.rank = rank[q.name];
-    }
-    auto jns = s.vec<int32_t>("j_ns"), jname = s.vec<int32_t>("j_name"), jq = s.vec<int32_t>("j_queue"),
-         jmin = s.vec<int32_t>("j_min"), jpri = s.vec<int32_t>("j_pg_priority");
-    auto jts = s.vec<int64_t>("j_ts");
-    struct Src { string uid; int row, pod; };
-    vector<Src> srcs;
-    srcs.reserve(jns.size() + 64);
-    for (size_t j = 0; j < jns.size(); ++j) srcs.push_back({s.s(jns[j]) + "/" + s.s(jname[j]), (int)j, -1});
-    for (int i = 0; i < P; ++i) {
-        if (v.pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
-        if (v.pjob[i] < 0) srcs.push_back({s.s(v.puid[i]), -1, i});  // shadow PodGroup
-    }
-    if (!std::is_sorted(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; }))
-        std::stable_sort(srcs.begin(), srcs.end(), [](const Src& a, const Src& b) { return a.uid < b.uid; });
-    mark("jobs:srcs");
-    vector<HJob> jobs;
-    vector<string> job_uid;
-    vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
-    const auto default_q = qidx.find("default");
-    std::unordered_map<int32_t, int> qslot_of;  // queue name (interned string offset) -> queue slot
-    for (auto& src : srcs) {
-        int qslot = -1;
-        if (src.row >= 0) {
-            auto qc = qslot_of.find(jq[src.row]);
-            if (qc == qslot_of.end()) {
-                auto qit = qidx.find(s.s(jq[src.row]));
-                qc = qslot_of.emplace(jq[src.row], qit == qidx.end() ? -1 : qit->second).first;
-            }
-            qslot = qc->second;
-        } else {
-            qslot = default_q == qidx.end() ? -1 : default_q->second;
-        }
-        int slot = -1;
-        if (qslot >= 0) {  // Snapshot drops jobs whose queue does not exist (cache.go:556-560)
-            HJob j;
-            j.queue = qslot;
-            j.min_avail = src.row >= 0 ? jmin[src.row] : 1;
-            j.ts = src.row >= 0 ? jts[src.row] : 0;
-            j.priority = j.pg_priority = src.row >= 0 ? jpri[src.row] : 0;
-            j.shadow = src.row < 0;
-            slot = (int)jobs.size();
-            jobs.push_back(std::move(j));
-            job_uid.push_back(src.uid);
-        }
-        if (src.row >= 0) row_slot[src.row] = slot;
-        else shadow_slot[src.pod] = slot;
-    }
-    mark("jobs:slots");
     {
         // job task lists in pod order, filled by kThreads pod ranges: per-range counts per job
         // give every range its first position in each job's list
-        constexpr int kThreads = 8;
+        // (each pod's job slot and the per-range counts: the pod pass above)
         const int J = (int)jobs.size();
-        const int nth = P < (1 << 15) ? 1 : kThreads;
-        const int per = (P + nth - 1) / nth;
-        vector<vector<int32_t>> cnt(nth, vector<int32_t>(J, 0));
+        const int nth = jth_p;
+        const int per = per_p;
+        vector<vector<int32_t>>& cnt = jcnt;
         auto par = [&](auto&& fn) {
             vector<std::thread> th;
             for (int t = 1; t < nth; ++t) th.emplace_back(fn, t);
             fn(0);
             for (auto& x : th) x.join();
         };
-        par([&](int t) {
-            const int lo = t * per, hi = std::min(P, lo + per);
-            int32_t* c = cnt[t].data();
-            for (int i = lo; i < hi; ++i) {
-                const int slot = v.pjob[i] >= 0 ? row_slot[v.pjob[i]] : shadow_slot[i];
-                pods[i].job = slot;
-                if (slot >= 0) c[slot]++;
-            }
-        });
         for (int j = 0; j < J; ++j) {  // per job: the ranges' offsets, the list's size
             int32_t off = 0;
             for (int t = 0; t < nth; ++t) {
@@ -5119,10 +5190,26 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         }
         return true;
     };
-    for (int i = 0; i < P; ++i) {
+    vector<int> need_cls;  // pending pods of a job without a class (new pods), in pod order
+    {
+        const int nth = P < (1 << 15) ? 1 : 8;
+        vector<vector<int>> part(nth);
+        auto scan = [&](int t) {
+            const int lo = (int)((int64_t)P * t / nth), hi = (int)((int64_t)P * (t + 1) / nth);
+            for (int i = lo; i < hi; ++i) {
+                HPod& p = pods[i];
+                if (p.status != Pending || p.job < 0) { if (old_pod[i] < 0) p.cls = -1; continue; }
+                if (p.cls < 0) part[t].push_back(i);  // (else kept: the pod's spec did not change)
+            }
+        };
+        vector<std::thread> th;
+        for (int t = 1; t < nth; ++t) th.emplace_back(scan, t);
+        scan(0);
+        for (auto& x : th) x.join();
+        for (auto& q : part) need_cls.insert(need_cls.end(), q.begin(), q.end());
+    }
+    for (int i : need_cls) {
         HPod& p = pods[i];
-        if (p.status != Pending || p.job < 0) { if (old_pod[i] < 0) p.cls = -1; continue; }
-        if (p.cls >= 0) continue;  // kept: the pod's spec did not change
         if (prev_new >= 0 && same_spec(prev_new, i)) {  // (string offsets compared: the table is interned)
             p.cls = pods[prev_new].cls;
             prev_new = i;
@@ -5168,7 +5255,6 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     }
     mark("classes");
     // ---------------- node rows from the pods (cache addTask -> NodeInfo.AddTask) ----------------
-    const int Nl = S.nc.n;
     vector<int64_t> col[13];
     for (auto& c : col) c.assign(N, 0);
     vector<int32_t> podcnt(N, 0), maxc(N, 0);
@@ -5186,12 +5272,33 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         // per node the additions keep pod order, as the serial pass would)
         constexpr int kThreads = 8;
         const int nth = P < (1 << 15) ? 1 : kThreads;
+        // pods on a node, bucketed by (pod range, node range) in one parallel pass; then each
+        // thread adds its node range's pods, pod ranges in order (per node: pod order)
+        vector<int> nb(nth + 1);
+        for (int t = 0; t <= nth; ++t) nb[t] = (int)((int64_t)N * t / nth);
+        vector<vector<vector<int32_t>>> bucket(nth, vector<vector<int32_t>>(nth));
+        auto fill = [&](int t) {
+            const int lo = (int)((int64_t)P * t / nth), hi = (int)((int64_t)P * (t + 1) / nth);
+            for (int i = lo; i < hi; ++i) {
+                const HPod& p = pods[i];
+                if (!on_node_of(p)) continue;
+                int r = (int)((int64_t)p.node * nth / N);
+                while (r > 0 && p.node < nb[r]) --r;
+                while (r + 1 < nth && p.node >= nb[r + 1]) ++r;
+                bucket[t][r].push_back(i);
+            }
+        };
+        {
+            vector<std::thread> th;
+            for (int t = 1; t < nth; ++t) th.emplace_back(fill, t);
+            fill(0);
+            for (auto& x : th) x.join();
+        }
         auto rows = [&](int t) {
-            const int nlo = (int)((int64_t)N * t / nth), nhi = (int)((int64_t)N * (t + 1) / nth);
-            for (int i = 0; i < P; ++i) {
+            for (int b = 0; b < nth; ++b)
+            for (int i : bucket[b][t]) {
                 const HPod& p = pods[i];
                 const int n = p.node;
-                if (n < nlo || n >= nhi || !on_node_of(p)) continue;
                 if (p.backfill) { col[6][n] += p.req.c; col[7][n] += p.req.m; col[8][n] += p.req.g; }
                 if (p.status == Releasing) { col[3][n] += p.req.c; col[4][n] += p.req.m; col[5][n] += p.req.g; }
                 col[0][n] -= p.req.c; col[1][n] -= p.req.m; col[2][n] -= p.req.g;
@@ -5215,29 +5322,40 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     mark("rows");
     // ---------------- device: the node rows that differ, the grown class tables ----------------
     int64_t uploaded = 0;
+    HIPCHK(hipStreamSynchronize(S.stream));  // the read-back of the device rows
+    size_t ci = 0;
+    vector<RowPatch> patches;  // the differing elements, written by one k_row_patch launch
     auto sync_col = [&](void* dptr, const void* want, size_t elem) {
-        vector<uint8_t> have((size_t)Nl * elem);
-        HIPCHK(hipMemcpy(have.data(), dptr, have.size(), hipMemcpyDeviceToHost));
+        if (ci >= dcols.size() || dcols[ci].d != dptr || dcols[ci].elem != elem)
+            throw Error(KBHIP_EDEVICE, "carry: device row read-back out of order");
+        const uint8_t* hv = stage.p + dcols[ci++].off;
         const uint8_t* w = (const uint8_t*)want;
-        int n = 0;
-        while (n < Nl) {
-            if (std::memcmp(have.data() + (size_t)n * elem, w + (size_t)n * elem, elem) == 0) { ++n; continue; }
-            int e = n + 1;
-            while (e < Nl && std::memcmp(have.data() + (size_t)e * elem, w + (size_t)e * elem, elem) != 0) ++e;
-            HIPCHK(hipMemcpyAsync((uint8_t*)dptr + (size_t)n * elem, w + (size_t)n * elem, (size_t)(e - n) * elem,
-                                  hipMemcpyHostToDevice, S.stream));
-            uploaded += (int64_t)(e - n) * (int64_t)elem;
-            n = e;
-        }
+        auto scan = [&](auto zero) {  // typed compares (a memcmp call per element costs more than the rows)
+            using T = decltype(zero);
+            const T* a = reinterpret_cast<const T*>(hv);
+            const T* b = reinterpret_cast<const T*>(w);
+            for (int n = 0; n < Nl; ++n) {
+                if (a[n] == b[n]) continue;
+                patches.push_back({(uint64_t)(uintptr_t)((T*)dptr + n), (uint64_t)b[n], (int32_t)sizeof(T), 0});
+                uploaded += (int64_t)sizeof(T);
+            }
+        };
+        if (elem == 8) scan(uint64_t{0});
+        else if (elem == 4) scan(uint32_t{0});
+        else scan(uint8_t{0});
     };
-    int64_t* dcol[13] = {S.nc.idle_cpu, S.nc.idle_mem, S.nc.idle_gpu, S.nc.rel_cpu, S.nc.rel_mem, S.nc.rel_gpu,
-                         S.nc.bf_cpu, S.nc.bf_mem, S.nc.bf_gpu, S.nc.acpu, S.nc.amem, S.nc.nzc, S.nc.nzm};
     for (int k = 0; k < 13; ++k) sync_col(dcol[k], col[k].data(), sizeof(int64_t));
     sync_col(S.nc.pods, podcnt.data(), sizeof(int32_t));
     sync_col(S.nc.maxtasks, maxc.data(), sizeof(int32_t));
     sync_col(S.nc.flags, flg.data(), sizeof(uint8_t));
     for (int w = 0; w < S.nc.port_words; ++w)
         sync_col(S.nc.ports + (size_t)w * S.nc.npad, pcol.data() + (size_t)w * S.nc.npad, sizeof(uint64_t));
+    DevBuf d_patch;
+    if (!patches.empty()) {
+        RowPatch* dp = d_patch.alloc<RowPatch>(patches.size());
+        HIPCHK(hipMemcpyAsync(dp, patches.data(), patches.size() * sizeof(RowPatch), hipMemcpyHostToDevice, S.stream));
+        HIPCHK(launch_row_patch(dp, (int)patches.size(), S.stream));
+    }
     if (!new_classes.empty()) {
         S.class_kf.resize(S.classes.size());
         S.class_srange.resize(S.classes.size());
