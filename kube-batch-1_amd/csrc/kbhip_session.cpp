@@ -1158,11 +1158,30 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
         if (pjob[i] >= (int)jns.size()) throw Error(KBHIP_EINVAL, "pod job index out of range");
         if (pjob[i] < 0) srcs.push_back({s.str(puid[i]), nullptr, -1, i});  // shadow PodGroup
     }
-    if (!std::is_sorted(srcs.begin(), srcs.end(), src_less)) std::stable_sort(srcs.begin(), srcs.end(), src_less);
+    const int jth = srcs.size() < (1u << 14) ? 1 : 8;
+    auto par_j = [&](auto&& fn) {
+        vector<std::thread> th;
+        for (int t = 1; t < jth; ++t) th.emplace_back(fn, t);
+        fn(0);
+        for (auto& x : th) x.join();
+    };
+    {
+        const size_t ns = srcs.size();
+        std::atomic<bool> sorted{true};
+        par_j([&](int t) {  // UID order checked by ranges
+            for (size_t k = std::max<size_t>(1, ns * t / jth); k < ns * (t + 1) / jth; ++k)
+                if (src_less(srcs[k], srcs[k - 1])) { sorted = false; return; }
+        });
+        if (!sorted) std::stable_sort(srcs.begin(), srcs.end(), src_less);
+    }
     vector<int> row_slot(jns.size(), -1), shadow_slot(P, -1);
     std::unordered_map<int32_t, int> q_by_off;  // strtab offset of a job's queue name -> queue (-1: none)
     const auto default_q = qidx.find("default");
-    for (auto& src : srcs) {
+    vector<int32_t> uid_src;  // job slot -> its source (the UID strings are built after, in parallel)
+    S.jobs.reserve(srcs.size());
+    uid_src.reserve(srcs.size());
+    for (size_t si = 0; si < srcs.size(); ++si) {
+        const Src& src = srcs[si];
         std::map<string, int>::const_iterator qit;
         int qslot = -1;
         if (src.row >= 0) {
@@ -1185,10 +1204,20 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
             j.shadow = src.row < 0;
             slot = (int)S.jobs.size();
             S.jobs.push_back(j);
-            S.job_uid.push_back(src.b ? string(src.a) + "/" + src.b : string(src.a));
+            uid_src.push_back((int32_t)si);
         }
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
+    }
+    {
+        const size_t nj = uid_src.size();
+        S.job_uid.resize(nj);
+        par_j([&](int t) {
+            for (size_t k = nj * t / jth; k < nj * (t + 1) / jth; ++k) {
+                const Src& src = srcs[uid_src[k]];
+                S.job_uid[k] = src.b ? string(src.a) + "/" + src.b : string(src.a);
+            }
+        });
     }
     mark("jobs:slots");
     // Pass B (pod order): namespace and host-port dictionaries, node accumulation,
