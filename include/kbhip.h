@@ -122,6 +122,9 @@ typedef struct kbhip_stats {
     double alloc_setup_s;    /* allocate: host time before the first pop (plugin open, job and queue heaps) */
     double evict_setup_s;    /* reclaim / preempt: host time before the first node ranking (plugin open, node
                                 task lists, victim codes, job heaps); part of evict_walk_s */
+    int64_t engine_pops;     /* batched pops served by the persistent pop engine (option "engine") */
+    int64_t engine_launches; /* launches of the engine's resident grid (one per run of engine pops) */
+    int64_t engine_workers;  /* its worker blocks (0: the engine was not used) */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

@@ -231,6 +231,13 @@ __device__ __forceinline__ T sweep_key(uint64_t k64, const PopArgs& a) {
                ((uint32_t)(a.kidxmax - key_idx(k64)) << 1) | (uint32_t)(k64 & 1);
     }
 }
+// The node index of a selection key.
+template <typename KT>
+__device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
+    if constexpr (sizeof(KT) == 8) return key_idx(k);
+    else return a.kidxmax - (int)((k >> 1) & (uint32_t)a.kidxmax);
+}
+
 template <typename T>
 __device__ __forceinline__ uint64_t key64_of(T k, const PopArgs& a) {
     if constexpr (sizeof(T) == 8) {
@@ -465,18 +472,27 @@ __device__ __forceinline__ int hash_slot(int n) { return (int)(((uint32_t)n * 26
 // Rows of the nodes a placement may use, gathered before it starts (LDS):
 // the overlapped pop loads them while it waits for the previous pop, so the
 // placement reads no node row from memory.  Slot lookup by node index.
-// Slots: 0..63 the sweep's list, 64..127 pop seq-1's candidates, 128..191
-// pop seq-2's (overlap depth 2).
-constexpr int kRcSlots = 192, kRcHash = 512;
-__device__ __forceinline__ int rc_slot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 23); }
-struct RowCache {
-    Row row[kRcSlots];
-    uint64_t pw[kRcSlots][4];
-    int32_t na[kRcSlots];
-    int32_t s1[kRcSlots];  // score after one more commit (depth-1 key; INT32_MIN: infeasible)
-    int32_t hkey[kRcHash];
-    int32_t hslot[kRcHash];
+// RowCache (k_pop_batch_ov, k_shard_place): slots 0..63 the sweep's list,
+// 64..127 pop seq-1's candidates, 128..191 pop seq-2's (overlap depth 2).
+// The persistent engine (kbhip_engine.hip) keeps four pops' candidates.
+template <int S, int HB>  // S slots, 2^HB hash entries
+struct RowCacheT {
+    static constexpr int kSlots = S, kHashN = 1 << HB;
+    Row row[S];
+    uint64_t pw[S][4];
+    int32_t na[S];
+    int32_t s1[S];  // score after one more commit (depth-1 key; INT32_MIN: infeasible)
+    int32_t hkey[1 << HB];
+    int32_t hslot[1 << HB];
 };
+constexpr int kRcSlots = 192, kRcHash = 512;
+using RowCache = RowCacheT<kRcSlots, 9>;
+template <typename RC>
+__device__ __forceinline__ int rc_slot(int n) {
+    constexpr int hb = RC::kHashN == 512 ? 9 : RC::kHashN == 1024 ? 10 : 8;
+    static_assert((1 << hb) == RC::kHashN, "row-cache hash size");
+    return (int)(((uint32_t)n * 2654435761u) >> (32 - hb));
+}
 // Score of candidate n after one more commit of class c (Allocate unless its
 // key is a Pipeline), INT32_MIN when that key is infeasible: the placement's
 // fast-path test (place_parallel), computed where the row is loaded.
@@ -492,14 +508,16 @@ __device__ __forceinline__ int32_t depth1_score(const Conf& cf, const NodeCols& 
     const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
     return k1 ? key_score(k1) : INT32_MIN;
 }
-__device__ __forceinline__ void rc_insert(RowCache* rc, int n, int slot) {  // n distinct
-    int h = rc_slot(n);
-    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (kRcHash - 1);
+template <typename RC>
+__device__ __forceinline__ void rc_insert(RC* rc, int n, int slot) {  // n distinct
+    int h = rc_slot<RC>(n);
+    while (atomicCAS(&rc->hkey[h], -1, n) != -1) h = (h + 1) & (RC::kHashN - 1);
     rc->hslot[h] = slot;
 }
-__device__ __forceinline__ int rc_find(const RowCache* rc, int n) {
-    int h = rc_slot(n);
-    for (int i = 0; i < kRcHash; ++i, h = (h + 1) & (kRcHash - 1)) {
+template <typename RC>
+__device__ __forceinline__ int rc_find(const RC* rc, int n) {
+    int h = rc_slot<RC>(n);
+    for (int i = 0; i < RC::kHashN; ++i, h = (h + 1) & (RC::kHashN - 1)) {
         const int k = rc->hkey[h];
         if (k == n) return rc->hslot[h];
         if (k == -1) return -1;
@@ -526,19 +544,41 @@ __device__ __forceinline__ uint32_t fit_sum(uint32_t v) {  // count b in lanes b
     return v + __shfl_xor(v, 32, 64);
 }
 
-template <typename ET, bool SC1 = false>
-__device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
-                               uint32_t seq = 0, const RowCache* rc = nullptr, const int32_t* fit_in = nullptr,
-                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
-                               uint64_t (*row_msg)[64] = nullptr) {
-    // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
-    // (a node-array shard writes back only its own; one GPU: all of them).
-    // t0 (a cut): the candidates are exact down to the selection key t0 only
-    // — a node outside them may beat an entry below it — so the launch places
-    // the entries at or above it and leaves the rest of the chunk to the host
-    // (stop 0 with done < m; done 0 when none).
-    // Node indices in keys and entries are global.
+// What a parallel-levels placement decided, per lane of wave 0: lane j holds
+// candidate j (its node, row before the chunk, port words and node-affinity
+// weight) and position j of the placement order (entry L, its candidate lane
+// lf and commit kind); cc = commits of candidate j, ap_l = its first Pipeline
+// depth; done / stop for the chunk.
+template <typename ET>
+struct PlaceDec {
+    int n;
+    Row base;
+    uint64_t pw[4], pwc[4];
+    int32_t na_n;
+    ET L;
+    bool inm;
+    int lf, kind, cc, ap_l;
+    int done, stop;
+};
+// Candidate j's row after the chunk's commits (Allocate^a Pipeline^p, a = min(cc, first Pipeline depth)).
+template <typename ET>
+__device__ __forceinline__ Row place_row(const TaskClass& c, const PlaceDec<ET>& D) {
+    if (D.cc <= 0) return D.base;
+    const int na = D.cc < D.ap_l ? D.cc : D.ap_l;
+    return apply_commits(D.base, c, na, D.cc - na);
+}
+
+// The parallel-levels decision (every wave calls; true on wave 0, which holds
+// the result — the other waves return false after their last barrier).
+// t0 (a cut): the candidates are exact down to the selection key t0 only
+// — a node outside them may beat an entry below it — so the launch places
+// the entries at or above it and leaves the rest of the chunk to the host
+// (stop 0 with done < m; done 0 when none).
+// Node indices in keys and entries are global.
+template <typename ET, bool SC1, typename RC>
+__device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                             const PopArgs& a, uint64_t (*wl64)[64], uint32_t seq, const RC* rc,
+                                             uint64_t t0, PlaceDec<ET>& D) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -553,6 +593,7 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
     const uint64_t K = wl64[0][lane];
     ET (*wl)[64] = (ET (*)[64])wl64;      // sort / merge lists of entries (same LDS)
     const int n = K ? key_idx(K) : -1;
+    D.n = n;
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
     int32_t na_n = 0;
@@ -621,7 +662,7 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
     int lf = 0, kind = 0, cc = 0, ap_l = 64;
     bool inm = false;
     if (fast) {
-        if (wave != 0) return;
+        if (wave != 0) return false;
         STAMP(gridDim.x * 4 + 13);
         inm = lane < m;
         L = inm ? depth_entry<ET>(key_score(K), n, 0, a) : (ET)0;
@@ -697,7 +738,7 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
         if (!s_more) break;
         alive = s_last[lane] != 0;  // rewritten by wave kW-1 only after the next round's first barrier
     }
-    if (wave != 0) return;
+    if (wave != 0) return false;
     STAMP(gridDim.x * 4 + 2);
     // commit kind of each position: its node's candidate lane, the entry's depth
     inm = lane < m && L != 0;
@@ -745,38 +786,79 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
     if constexpr (SC1) {
         if (lane == 0) { TL(seq, 7); TL_VAL(seq, 9, fast ? 1 : 2); TL_VAL(seq, 10, (uint64_t)done); }
     }
-    if (fit_in && stop == 1) {  // a task found no node: the walk's FitDelta histogram at that task
-        // fit_in: every node at the state this pop started from; the candidates
-        // then carry the commits made before the failing task
-        uint32_t fb_base = 0, fb_post = 0;
-        if (n >= 0) {
-            fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
-            const int ap = ap_l;
-            const int na = cc < ap ? cc : ap;
-            const Row r = apply_commits(base, c, na, cc - na);
-            int32_t sc;
-            bool passed;
-            (void)dyn_key(cf, c, t, nc, r, cc > 0 ? pwc : pw, n, true, na_n, &sc, &passed);
-            fb_post = fit_bits(c, r, passed);
-        }
-        const uint32_t sweep = fit_sum(fit_raw);
-        int32_t tot[4];
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-            tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
-                     __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
-        if (lane == 0) {
-            __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
+    D.base = base;
+    for (int w = 0; w < 4; ++w) { D.pw[w] = pw[w]; D.pwc[w] = pwc[w]; }
+    D.na_n = na_n;
+    D.L = L;
+    D.inm = inm;
+    D.lf = lf;
+    D.kind = kind;
+    D.cc = cc;
+    D.ap_l = ap_l;
+    D.done = done;
+    D.stop = stop;
+    return true;
+}
+
+// The walk FitDelta histogram of a task that found no node (D.stop == 1):
+// fit_in = the counts of the candidates the sweep left out (at the state the
+// pop started from), fit_raw = the sweep's counts (fit_sum layout); the
+// candidates then carry the commits made before the failing task.  Two
+// granules beside the placements (wave 0).
+template <typename ET>
+__device__ __forceinline__ void place_fit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                          const PopArgs& a, PopOut* out, const PlaceDec<ET>& D, const int32_t* fit_in,
+                                          uint32_t fit_raw) {
+    const int lane = threadIdx.x & 63;
+    uint32_t fb_base = 0, fb_post = 0;
+    if (D.n >= 0) {
+        fb_base = fit_bits(c, D.base, true);  // candidates had a key: in the walk
+        const Row r = place_row(c, D);
+        int32_t sc;
+        bool passed;
+        (void)dyn_key(cf, c, t, nc, r, D.cc > 0 ? D.pwc : D.pw, D.n, true, D.na_n, &sc, &passed);
+        fb_post = fit_bits(c, r, passed);
     }
+    const uint32_t sweep = fit_sum(fit_raw);
+    int32_t tot[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                 __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+    if (lane == 0) {
+        __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The result granules of the chunk (wave 0; pinned host memory, one 8-byte store each).
+template <typename ET>
+__device__ __forceinline__ void place_granules(const PopArgs& a, PopOut* out, const PlaceDec<ET>& D) {
+    const int lane = threadIdx.x & 63;
+    if (lane < D.done || (D.done == 0 && lane == 0))
+        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, D.stop, D.done, lane < D.done ? D.kind : 0,
+                                                       (lane < D.done && D.inm) ? entry_node(D.L, a) : -1),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename ET, bool SC1 = false, typename RC = RowCache>
+__device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                               const PopArgs& a, PopOut* out, uint64_t (*wl64)[64], uint32_t* done_flag = nullptr,
+                               uint32_t seq = 0, const RC* rc = nullptr, const int32_t* fit_in = nullptr,
+                               uint32_t fit_raw = 0, int wb_base = 0, int wb_n = 0x7fffffff, uint64_t t0 = 0,
+                               uint64_t (*row_msg)[64] = nullptr) {
+    // wb_base / wb_n: node rows [wb_base, wb_base + wb_n) are this device's
+    // (a node-array shard writes back only its own; one GPU: all of them).
+    PlaceDec<ET> D;
+    if (!place_decide<ET, SC1>(cf, nc, t, c, a, wl64, seq, rc, t0, D)) return;
+    const int lane = threadIdx.x & 63;
+    if (fit_in && D.stop == 1) place_fit(cf, nc, t, c, a, out, D, fit_in, fit_raw);
+    const int n = D.n, cc = D.cc;
     const int ln = n - wb_base;  // local row of the written-back node
-    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {  // Allocate^a Pipeline^p: a = min(cc, first Pipeline depth)
-        const int ap = ap_l;
-        const int na = cc < ap ? cc : ap;
-        const Row r = apply_commits(base, c, na, cc - na);
+    if (n >= 0 && cc > 0 && ln >= 0 && ln < wb_n) {
+        const Row r = place_row(c, D);
         if constexpr (SC1) {
             st_sc1(&nc.idle_cpu[ln], r.idle_cpu); st_sc1(&nc.idle_mem[ln], r.idle_mem); st_sc1(&nc.idle_gpu[ln], r.idle_gpu);
             st_sc1(&nc.rel_cpu[ln], r.rel_cpu); st_sc1(&nc.rel_mem[ln], r.rel_mem); st_sc1(&nc.rel_gpu[ln], r.rel_gpu);
@@ -784,7 +866,7 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
             st_sc1(&nc.nzc[ln], r.nzc);
             st_sc1(&nc.nzm[ln], r.nzm);
             if (c.has_ports)
-                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) st_sc1(&nc.ports[port_at(c, nc, w, ln)], pwc[w]);
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) st_sc1(&nc.ports[port_at(c, nc, w, ln)], D.pwc[w]);
         } else {
             nc.idle_cpu[ln] = r.idle_cpu; nc.idle_mem[ln] = r.idle_mem; nc.idle_gpu[ln] = r.idle_gpu;
             nc.rel_cpu[ln] = r.rel_cpu; nc.rel_mem[ln] = r.rel_mem; nc.rel_gpu[ln] = r.rel_gpu;
@@ -792,17 +874,13 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
             nc.nzc[ln] = r.nzc;
             nc.nzm[ln] = r.nzm;
             if (c.has_ports)
-                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, ln)] = pwc[w];
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) nc.ports[port_at(c, nc, w, ln)] = D.pwc[w];
         }
     }
     if constexpr (SC1) {  // the only storing wave drained, then the row message, then the flag (sc1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (row_msg) {  // every candidate's row after this pop (self-tagged halves, PopLink::rows)
-            Row rw = base;
-            if (cc > 0) {
-                const int na = cc < ap_l ? cc : ap_l;
-                rw = apply_commits(base, c, na, cc - na);
-            }
+            const Row rw = place_row(c, D);
             uint32_t w[kRowWords];
             row_words(rw, w);
 #pragma unroll
@@ -810,13 +888,9 @@ __device__ __forceinline__ void place_parallel(const Conf& cf, const NodeCols& n
         }
         if (lane == 0) { st_sc1(done_flag, seq); TL(seq, 8); }
     }
-    if (lane < done || (done == 0 && lane == 0))
-        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, stop, done, lane < done ? kind : 0,
-                                                       (lane < done && inm) ? entry_node(L, a) : -1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    place_granules(a, out, D);
     STAMP(gridDim.x * 4 + 3);
 }
-
 
 // ---------------------------------------------------------------------------
 // Placement of a session with Backfilled nodes (placement 6; one wave, task

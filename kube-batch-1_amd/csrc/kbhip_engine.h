@@ -1,0 +1,62 @@
+// kbhip_engine.h — the persistent pop engine (kbhip_engine.hip): memory
+// layout shared by the host driver (kbhip_session.cpp) and the kernel.
+//
+// One resident grid serves a run of batched job pops (allocate.go:110-185 for
+// a gang's chunk of one task class) without a kernel launch
+// per pop:
+//   * worker blocks own node ranges: per pop they evaluate their nodes
+//     (PredicateFn + NodeOrderFn -> selection key, kbhip_eval.h) and publish
+//     their top-128 keys;
+//   * merger blocks (one per group of workers) merge their group's lists;
+//   * the placer block merges the group lists, re-evaluates the previous two
+//     pops' candidates from its own LDS rows, places the chunk (parallel
+//     levels, kbhip_batch.h) and writes the rows back;
+//   * the dispatcher block copies pop descriptors from the host's pinned ring
+//     into a device ring.
+// Pop p's workers read the node rows as pop p-3 left them; the candidates of
+// pops p-2 (left out by the workers) and p-1 (dropped by the placer from the
+// merged top-128) are the only rows that can have changed since, and the
+// placer holds both pops' rows.  So the placer sees every node's exact key.
+#pragma once
+#include <stdint.h>
+
+namespace kbhip {
+
+constexpr int kEngRing = 8;       // device descriptor ring
+constexpr int kEngHostRing = 16;  // host descriptor ring (pinned)
+constexpr int kEngSlots = 4;      // list / candidate slots (pop % 4)
+constexpr int kEngMaxGroups = 8;  // merger blocks
+constexpr int kEngListWords = 136;  // a list: 128 tagged keys + 4 tagged counts (+ pad), 17 lines
+constexpr int kEngMaxNpb = 8192;  // nodes per worker block
+constexpr int kEngWorkersMax = 512;
+
+// Descriptor words (each {seq << 32 | value}, self-tagged: a reader takes a
+// descriptor once all eight tags read its sequence number).
+enum : int { kDwCls = 0, kDwFlags, kDwMinAvail, kDwReady, kDwEpochSlot, kDwKbase, kDwKshift, kDwKidxmax };
+// kDwFlags: m | gang << 8 | ent32 << 9 | op << 12
+enum : uint32_t { kEngOpPop = 0, kEngOpExit = 1 };
+
+// Device control block (hipMalloc'ed, zeroed at each launch).
+struct EngCtl {
+    uint32_t done;  // the last pop whose node write-back is visible (sc1)
+    uint32_t pad0[31];
+    uint32_t err;   // first error (kEngErr*), 0: none; every wait gives up once it is set
+    uint32_t pad1[31];
+    uint64_t desc[kEngRing][8];     // descriptors, slot seq % kEngRing
+    uint64_t cands[kEngSlots][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}
+};
+enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2 };
+
+// Kernel arguments beyond the session's tables.
+struct EngArgs {
+    EngCtl* ctl;
+    uint64_t* blists;          // [kEngSlots][nw][kEngListWords] worker lists (+ 2 count words)
+    uint64_t* glists;          // [kEngSlots][ng][kEngListWords] group lists (+ 4 count words)
+    const uint64_t* hring;     // [kEngHostRing][8] pinned host descriptors (device view)
+    uint64_t* hexit;           // pinned host word: {exit seq | idle << 40 | 1 << 41} when the engine ends
+    void* out;                 // result slots (PopOut, pinned host memory, device view)
+    uint32_t first;            // the first pop of this launch (earlier pops are written back)
+    int nw, npb, ng;           // workers, nodes per worker, merger groups
+};
+
+}  // namespace kbhip

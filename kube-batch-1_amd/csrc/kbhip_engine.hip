@@ -1,0 +1,628 @@
+// kbhip_engine.hip — the persistent pop engine: one
+// resident grid places a run of batched job pops (allocate.go:110-185, one
+// gang chunk of one task class per pop) with no kernel launch per pop.
+// Roles by block (kbhip_engine.h):
+//   [0, nw)        workers: node range [b * npb, (b + 1) * npb)
+//   [nw, nw + ng)  mergers: group g = workers b with b % ng == g
+//   nw + ng        placer
+//   nw + ng + 1    dispatcher (one wave)
+// Hand-offs are self-tagged 8-byte granules {seq << 32 | value} written with
+// sc1 stores and polled with sc1 loads (MI355X_MICROARCH.md, R2), or sc1 row
+// stores drained before the sc1 `done` flag (valid forms, table row 1).
+// Every wait is bounded (s_memrealtime) and gives up once ctl->err is set.
+#include <hip/hip_runtime.h>
+
+#define KBHIP_STAMPS_OFF  // phase stamps belong to k_pop_batch (kbhip_kernels.hip)
+#include "kbhip_batch.h"
+#include "kbhip_engine.h"
+
+namespace kbhip {
+
+constexpr uint64_t kEngWaitTicks = 200000000ull;  // 2 s at 100 MHz: a pipeline wait that long is a fault
+constexpr uint64_t kEngIdleTicks = 100000000ull;  // 1 s without a descriptor: the dispatcher ends the run
+constexpr uint64_t kEngDescTicks = 400000000ull;  // a block waiting for its next descriptor
+
+__device__ __forceinline__ uint64_t eng_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// A bounded wait: call tick() once per unsuccessful poll; false = give up
+// (timed out: the error is recorded; or another block recorded one).
+struct EngWait {
+    EngCtl* ctl;
+    uint64_t limit;
+    uint64_t t0 = 0;
+    uint32_t it = 0;
+    __device__ EngWait(EngCtl* c, uint64_t l) : ctl(c), limit(l) {}
+    __device__ __forceinline__ bool tick(uint32_t code = kEngErrWait) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((++it & 63) != 0) return true;
+        const uint64_t now = eng_now();
+        if (!t0) t0 = now;
+        if (ld_sc1(&ctl->err) != 0) return false;
+        if (now - t0 > limit) {
+            __hip_atomic_store(&ctl->err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        return true;
+    }
+};
+
+// The pop's descriptor as a block sees it (from the device ring).
+struct EngDesc {
+    uint32_t op, cls, m, gang, ent32, min_avail, ready, epoch, slot;
+    int32_t kbase, kshift, kidxmax;
+};
+__device__ __forceinline__ EngDesc eng_decode(const uint32_t* w) {
+    EngDesc d;
+    d.cls = w[kDwCls];
+    d.m = w[kDwFlags] & 0xff;
+    d.gang = (w[kDwFlags] >> 8) & 1;
+    d.ent32 = (w[kDwFlags] >> 9) & 1;
+    d.op = (w[kDwFlags] >> 12) & 0xf;
+    d.min_avail = w[kDwMinAvail];
+    d.ready = w[kDwReady];
+    d.epoch = w[kDwEpochSlot] & 0xffff;
+    d.slot = w[kDwEpochSlot] >> 16;
+    d.kbase = (int32_t)w[kDwKbase];
+    d.kshift = (int32_t)w[kDwKshift];
+    d.kidxmax = (int32_t)w[kDwKidxmax];
+    return d;
+}
+__device__ __forceinline__ PopArgs eng_args(const EngDesc& d) {
+    PopArgs a{};
+    a.cls = (int32_t)d.cls;
+    a.n_tasks = (int32_t)d.m;
+    a.gang_mode = (int32_t)d.gang;
+    a.min_avail = (int32_t)d.min_avail;
+    a.ready_count = (int32_t)d.ready;
+    a.epoch = d.epoch;
+    a.placement = 2;
+    a.kbase = d.kbase;
+    a.kshift = d.kshift;
+    a.kidxmax = d.kidxmax;
+    a.ent32 = (int32_t)d.ent32;
+    a.fit_set = 0;
+    return a;
+}
+
+// Wave 0: wait for descriptor p in the device ring, leave its words in w[8] (LDS).
+__device__ __forceinline__ bool eng_wait_desc(EngCtl* ctl, uint32_t p, uint32_t* w) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t* src = &ctl->desc[p % kEngRing][lane & 7];
+    EngWait wt(ctl, kEngDescTicks);
+    for (;;) {
+        const uint64_t x = ld_sc1(src);
+        if (__ballot(lane < 8 && (uint32_t)(x >> 32) != p) == 0) {
+            if (lane < 8) w[lane] = (uint32_t)x;
+            return true;
+        }
+        if (!wt.tick(kEngErrDesc)) return false;
+    }
+}
+
+// Wave 0: wait until ctl->done reaches `want`.
+__device__ __forceinline__ bool eng_wait_done(EngCtl* ctl, uint32_t want) {
+    EngWait wt(ctl, kEngWaitTicks);
+    for (;;) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&ctl->done));
+        if ((int32_t)(v - want) >= 0) return true;
+        if (!wt.tick()) return false;
+    }
+}
+
+// Wave 0: candidate `lane` of pop q (-1: none), waiting for the granules.
+__device__ __forceinline__ bool eng_wait_cands(EngCtl* ctl, uint32_t q, int* node) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t* src = &ctl->cands[q % kEngSlots][lane];
+    EngWait wt(ctl, kEngWaitTicks);
+    for (;;) {
+        const uint64_t x = ld_sc1(src);
+        if (__ballot((uint32_t)(x >> 32) != q) == 0) {
+            *node = (int)(uint32_t)x;
+            return true;
+        }
+        if (!wt.tick()) return false;
+    }
+}
+
+// Top 128 of the 8 waves' descending 128-lists (a0: ranks 0..63, a1: 64..127);
+// the result in w0[0] / w1[0] (every wave calls).
+template <typename T>
+__device__ __forceinline__ void block_merge128_all(T (*w0)[64], T (*w1)[64], T a0, T a1, int wave, int lane) {
+    w0[wave][lane] = a0;
+    w1[wave][lane] = a1;
+    __syncthreads();
+#pragma unroll
+    for (int s = kPopThreads / 128; s >= 1; s >>= 1) {
+        if (wave < s) {
+            T x0 = w0[wave][lane], x1 = w1[wave][lane];
+            wave_merge128_desc(x0, x1, w0[wave + s][lane], w1[wave + s][lane]);
+            w0[wave][lane] = x0;
+            w1[wave][lane] = x1;
+        }
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+    x += __shfl_xor(x, 1, 64);
+    x += __shfl_xor(x, 2, 64);
+    x += __shfl_xor(x, 4, 64);
+    x += __shfl_xor(x, 8, 64);
+    x += __shfl_xor(x, 16, 64);
+    return x + __shfl_xor(x, 32, 64);
+}
+
+// The evaluation of a worker's node: the mutable row columns through sc1
+// (the placer writes them write-through from another CU), the static ones
+// plain; all loads issued before the predicates' early exits (eval_node).
+__device__ __forceinline__ uint64_t eng_eval(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                             const NodeCols& nc, int n, uint32_t* fb) {
+    const uint8_t fl = nc.flags[n];
+    const Row r = load_row_sc1(nc, n);
+    const bool st = static_pred_f(cf, c, t, nc, n, fl);
+    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+    const uint64_t pw[4] = {0, 0, 0, 0};  // engine classes carry no host ports
+    int32_t s;
+    bool passed;
+    const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
+    *fb = fit_bits(c, r, passed);
+    return k;
+}
+
+// ---------------------------------------------------------------------------
+// LDS of the roles (one union: the kernel's footprint is the largest role's)
+// ---------------------------------------------------------------------------
+struct EngWorkerLds {
+    uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
+    uint32_t skip[kEngMaxNpb / 32];
+    uint8_t fb[kEngMaxNpb];
+    uint32_t desc[8];
+    uint32_t fitb[4];
+    int ok;
+};
+struct EngMergerLds {
+    uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
+    uint32_t desc[8];
+    int ok;
+};
+constexpr int kEngRc = 4 * 64;  // the placer's rows: four pops' candidates, slot = 64 * (pop % 4) + lane
+using EngRowCache = RowCacheT<kEngRc, 10>;
+struct EngPlacerLds {
+    EngRowCache rc;
+    uint8_t flags[kEngRc];
+    int32_t xn[4][64];           // candidates of pop q in ring q % 4 (-1: none)
+    uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
+    uint64_t wl64[kPopThreads / 64][64];
+    uint32_t s64[64];            // the merged list without pop p-1's candidates
+    uint32_t e[2][64];           // re-evaluated keys of pops p-1 / p-2's candidates
+    uint8_t fbp[2][64];
+    uint8_t x2use[64];
+    int32_t fitin[4];
+    uint32_t desc[8];
+    int ok;
+};
+union EngLds {
+    EngWorkerLds w;
+    EngMergerLds m;
+    EngPlacerLds p;
+};
+
+// ---------------------------------------------------------------------------
+// worker
+// ---------------------------------------------------------------------------
+__device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                           EngWorkerLds& L, int b) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    const int lo = b * A.npb;
+    const int cnt = nc.n - lo < A.npb ? (nc.n - lo > 0 ? nc.n - lo : 0) : A.npb;
+    if (threadIdx.x == 0) L.ok = 1;
+    for (uint32_t p = A.first;; ++p) {
+        // 1. the pop's descriptor; the node rows as pop p-3 left them; pop p-2's candidates
+        for (int i = threadIdx.x; i < (cnt + 31) / 32; i += kPopThreads) L.skip[i] = 0;
+        __syncthreads();  // the previous pop done (wave 0 cleared L.ok if it failed)
+        if (!L.ok) return;
+        if (threadIdx.x < 4) L.fitb[threadIdx.x] = 0;
+        if (wave == 0) {
+            bool ok = eng_wait_desc(ctl, p, L.desc);
+            const EngDesc d0 = eng_decode(L.desc);  // (LDS written by this wave, in order)
+            if (ok && d0.op == kEngOpPop) {
+                if (p >= A.first + 3) ok = eng_wait_done(ctl, p - 3);
+                if (ok && p >= A.first + 2) {
+                    int node = -1;
+                    ok = eng_wait_cands(ctl, p - 2, &node);
+                    const int o = node - lo;
+                    if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
+                }
+            }
+            if (lane == 0) L.ok = ok;
+        }
+        __syncthreads();
+        if (!L.ok) return;
+        const EngDesc d = eng_decode(L.desc);
+        if (d.op != kEngOpPop) return;
+        const PopArgs a = eng_args(d);
+        const TaskClass& c = t.classes[__builtin_amdgcn_readfirstlane((int)d.cls)];
+        // 2. evaluate, one node per thread and chunk; each wave keeps its top 128
+        uint32_t a0 = 0, a1 = 0;
+        for (int base = 0; base < cnt; base += kPopThreads) {
+            const int o = base + (int)threadIdx.x;
+            uint32_t k = 0, fb = 0;
+            if (o < cnt && !((L.skip[o >> 5] >> (o & 31)) & 1u)) k = sweep_key<uint32_t>(eng_eval(cf, c, t, nc, lo + o, &fb), a);
+            if (o < cnt) L.fb[o] = (uint8_t)fb;
+            fit_block_add(L.fitb, fb);
+            const uint32_t ks = wave_sort_desc(k);
+            if (base == 0) a0 = ks;
+            else wave_merge128_desc(a0, a1, ks, 0u);
+        }
+        block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
+        // 3. publish the block's top 128 (wave 0), then its FitDelta counts
+        // without pop p-1's candidates (their rows may be in flight: the
+        // placer counts them on their final rows)
+        if (wave == 0) {
+            uint64_t* dst = A.blists + ((size_t)(p % kEngSlots) * A.nw + b) * kEngListWords;
+            st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
+            st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
+            bool ok = true;
+            if (p >= A.first + 1) {
+                int node = -1;
+                ok = eng_wait_cands(ctl, p - 1, &node);
+                const int o = node - lo;
+                const uint32_t fb = (ok && node >= 0 && o >= 0 && o < cnt) ? L.fb[o] : 0u;  // 0 if skipped
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = __popcll(__ballot((fb >> q) & 1u));
+                    if (lane == q && k) atomicSub(&L.fitb[q], (uint32_t)k);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+                __builtin_amdgcn_wave_barrier();
+            }
+            if (!ok && lane == 0) L.ok = 0;  // (the error is recorded: every block gives up)
+            if (ok && lane < 2) {
+                const uint32_t v = (L.fitb[2 * lane] & 0xffff) | (L.fitb[2 * lane + 1] << 16);
+                st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | v);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// merger of group g
+// ---------------------------------------------------------------------------
+__device__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    const int cg = (A.nw - g + A.ng - 1) / A.ng;  // workers of the group: g, g + ng, ...
+    if (threadIdx.x == 0) L.ok = 1;
+    for (uint32_t p = A.first;; ++p) {
+        __syncthreads();  // the previous pop done (wave 0 cleared L.ok if it failed)
+        if (!L.ok) return;
+        if (wave == 0) {
+            const bool ok = eng_wait_desc(ctl, p, L.desc);
+            if (lane == 0) L.ok = ok;
+        }
+        __syncthreads();
+        if (!L.ok) return;
+        if (eng_decode(L.desc).op != kEngOpPop) return;
+        const uint64_t* src0 = A.blists + (size_t)(p % kEngSlots) * A.nw * kEngListWords;
+        // wave w merges the group's lists w, w + 8, ... (4 in flight)
+        uint32_t a0 = 0, a1 = 0;
+        bool ok = true;
+        for (int i0 = wave; i0 < cg && ok; i0 += 4 * (kPopThreads / 64)) {
+            constexpr int kQ = 4;
+            uint64_t v0[kQ], v1[kQ];
+            const uint64_t* s[kQ];
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                const int i = i0 + q * (kPopThreads / 64);
+                s[q] = i < cg ? src0 + (size_t)(g + i * A.ng) * kEngListWords : nullptr;
+                v0[q] = s[q] ? ld_sc1(&s[q][lane]) : ((uint64_t)p << 32);
+                v1[q] = s[q] ? ld_sc1(&s[q][64 + lane]) : ((uint64_t)p << 32);
+            }
+            EngWait wt(ctl, kEngWaitTicks);
+            for (;;) {
+                bool miss = false;
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) {
+                    if (__ballot((uint32_t)(v0[q] >> 32) != p || (uint32_t)(v1[q] >> 32) != p) == 0) continue;
+                    miss = true;
+                    v0[q] = ld_sc1(&s[q][lane]);
+                    v1[q] = ld_sc1(&s[q][64 + lane]);
+                }
+                if (!miss) break;
+                if (!wt.tick()) { ok = false; break; }
+            }
+            if (ok)
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) wave_merge128_desc(a0, a1, (uint32_t)v0[q], (uint32_t)v1[q]);
+        }
+        if (!ok) L.ok = 0;
+        block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
+        if (!L.ok) return;
+        if (wave == 0) {
+            uint64_t* dst = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords;
+            st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
+            st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
+            // the group's FitDelta counts: lane i reads worker g + i * ng's two count words
+            uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+            for (int i0 = 0; i0 < cg && ok; i0 += 64) {
+                const int i = i0 + lane;
+                const uint64_t* s = i < cg ? src0 + (size_t)(g + i * A.ng) * kEngListWords + 128 : nullptr;
+                uint64_t x0 = s ? ld_sc1(&s[0]) : ((uint64_t)p << 32), x1 = s ? ld_sc1(&s[1]) : ((uint64_t)p << 32);
+                EngWait wt(ctl, kEngWaitTicks);
+                while (__ballot((uint32_t)(x0 >> 32) != p || (uint32_t)(x1 >> 32) != p) != 0) {
+                    if (!wt.tick()) { ok = false; break; }
+                    if (s) { x0 = ld_sc1(&s[0]); x1 = ld_sc1(&s[1]); }
+                }
+                const uint32_t y0 = (uint32_t)x0, y1 = (uint32_t)x1;  // two 16-bit counts per word
+                t0 += wave_sum_u32(y0 & 0xffff);
+                t1 += wave_sum_u32(y0 >> 16);
+                t2 += wave_sum_u32(y1 & 0xffff);
+                t3 += wave_sum_u32(y1 >> 16);
+            }
+            if (!ok && lane == 0) L.ok = 0;
+            if (ok && lane < 4)
+                st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | (lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? t2 : t3));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// placer
+// ---------------------------------------------------------------------------
+// The placer's wave 0 after the decision: the FitDelta histogram of a task
+// that found no node (the sweep's counts from the group count words), the
+// chunk's rows into the cache (ring r0) and, write-through, into the node
+// columns, drained before `done`; then the result granules.
+template <typename ET>
+__device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                           const PopArgs& a, const EngArgs& A, EngPlacerLds& L, uint32_t p, int r0,
+                                           PopOut* out, const PlaceDec<ET>& D) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    if (D.stop == 1) {
+        uint32_t fr = 0;  // group g's count b in lane 4g + b (fit_sum layout)
+        const int g = lane >> 2;
+        if (g < A.ng) {
+            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords + 128 + (lane & 3);
+            uint64_t x = ld_sc1(s);
+            EngWait wt(ctl, kEngWaitTicks);
+            while (__ballot((uint32_t)(x >> 32) != p) != 0) {
+                if (!wt.tick()) break;
+                x = ld_sc1(s);
+            }
+            fr = (uint32_t)x;
+        }
+        place_fit(cf, nc, t, c, a, out, D, L.fitin, fr);
+    }
+    const int n = D.n;
+    if (n >= 0 && D.cc > 0) {
+        const Row r = place_row(c, D);
+        L.rc.row[64 * r0 + lane] = r;
+        st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
+        st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
+        st_sc1(&nc.pods[n], r.pods);
+        st_sc1(&nc.nzc[n], r.nzc);
+        st_sc1(&nc.nzm[n], r.nzm);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back, then `done`
+    if (lane == 0) st_sc1(&ctl->done, p);
+    place_granules(a, out, D);
+}
+
+__device__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                           EngPlacerLds& L) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    EngRowCache& rc = L.rc;
+    for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
+    if (threadIdx.x == 0) L.ok = 1;
+    for (uint32_t p = A.first;; ++p) {
+        const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r0 = (int)(p % 4);  // rings of p-1, p-2, p
+        // P0: descriptor; the hash of pops p-1 / p-2's candidates (node -> latest row slot)
+        for (int h = threadIdx.x; h < EngRowCache::kHashN; h += kPopThreads) rc.hkey[h] = -1;
+        __syncthreads();
+        if (!L.ok) return;
+        if (wave == 0) {
+            const bool ok = eng_wait_desc(ctl, p, L.desc);
+            if (lane == 0) L.ok = ok;
+            const int n1 = L.xn[r1][lane];
+            if (n1 >= 0) rc_insert(&rc, n1, 64 * r1 + lane);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int n2 = L.xn[r2][lane];
+            const bool use2 = n2 >= 0 && rc_find(&rc, n2) < 0;  // a node of both: pop p-1's row is the latest
+            L.x2use[lane] = use2;
+            if (use2) rc_insert(&rc, n2, 64 * r2 + lane);
+        }
+        __syncthreads();
+        if (!L.ok) return;
+        const EngDesc d = eng_decode(L.desc);
+        if (d.op != kEngOpPop) return;
+        const PopArgs a = eng_args(d);
+        const TaskClass& c = t.classes[__builtin_amdgcn_readfirstlane((int)d.cls)];
+        // P1: the group lists (wave g polls group g), merged to the top 128
+        uint32_t a0 = 0, a1 = 0;
+        bool ok = true;
+        if (wave < A.ng) {
+            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + wave) * kEngListWords;
+            uint64_t v0 = ld_sc1(&s[lane]), v1 = ld_sc1(&s[64 + lane]);
+            EngWait wt(ctl, kEngWaitTicks);
+            while (__ballot((uint32_t)(v0 >> 32) != p || (uint32_t)(v1 >> 32) != p) != 0) {
+                if (!wt.tick()) { ok = false; break; }
+                v0 = ld_sc1(&s[lane]);
+                v1 = ld_sc1(&s[64 + lane]);
+            }
+            a0 = (uint32_t)v0;
+            a1 = (uint32_t)v1;
+            if (!ok && lane == 0) L.ok = 0;
+        }
+        block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
+        if (!L.ok) return;
+        // P2: wave 0 drops pop p-1's candidates from the merged list (their
+        // keys are stale; at most 64 of 128: the first 64 left are exact);
+        // waves 1 / 2 re-evaluate pops p-1 / p-2's candidates on their rows
+        if (wave == 0) {
+            L.s64[lane] = 0;
+            const uint32_t k0 = L.wl[0][lane], k1 = L.wl2[0][lane];
+            auto kept = [&](uint32_t k) {
+                if (!k) return false;
+                const int sl = rc_find(&rc, key_node(k, a));
+                return !(sl >= 64 * r1 && sl < 64 * r1 + 64);
+            };
+            const bool c0 = kept(k0), c1 = kept(k1);
+            const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+            const int q0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0));
+            const int q1 = __popcll(m0) +
+                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0));
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            if (c0) L.s64[q0] = k0;
+            if (c1 && q1 < 64) L.s64[q1] = k1;
+        } else if (wave == 1 || wave == 2) {
+            const int q = wave - 1;
+            const int ring = q == 0 ? r1 : r2;
+            const int node = L.xn[ring][lane];
+            const bool use = node >= 0 && (q == 0 || L.x2use[lane]);
+            uint32_t e = 0, fb = 0;
+            if (use) {
+                const int sl = 64 * ring + lane;
+                const Row r = rc.row[sl];
+                const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
+                const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
+                const uint64_t pw[4] = {0, 0, 0, 0};
+                int32_t sc;
+                bool passed;
+                const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
+                rc.na[sl] = na;
+                rc.s1[sl] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, na, k0) : INT32_MIN;
+                e = sweep_key<uint32_t>(k0, a);
+                fb = fit_bits(c, r, passed);
+            }
+            L.e[q][lane] = e;
+            L.fbp[q][lane] = (uint8_t)fb;
+        }
+        __syncthreads();
+        // P3: wave 0: the final list, pop p's candidates published, their rows into ring p % 4
+        if (wave == 0) {
+            uint32_t top = wave_merge_desc(L.s64[lane], wave_sort_desc(L.e[0][lane]));
+            top = wave_merge_desc(top, wave_sort_desc(L.e[1][lane]));
+            const uint32_t fbp = (uint32_t)L.fbp[0][lane] | ((uint32_t)L.fbp[1][lane] << 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int k = __popcll(__ballot((fbp >> q) & 1u)) + __popcll(__ballot((fbp >> (q + 4)) & 1u));
+                if (lane == q) L.fitin[q] = k;
+            }
+            const int n = top ? key_node(top, a) : -1;
+            st_sc1(&ctl->cands[p % kEngSlots][lane], ((uint64_t)p << 32) | (uint32_t)n);
+            const int dst = 64 * r0 + lane;
+            if (n >= 0) {
+                const int src = rc_find(&rc, n);
+                if (src >= 0) {
+                    rc.row[dst] = rc.row[src];
+                    L.flags[dst] = L.flags[src];
+                    rc.na[dst] = rc.na[src];
+                    rc.s1[dst] = rc.s1[src];
+                } else {
+                    const Row r = load_row_sc1(nc, n);
+                    const uint8_t fl = nc.flags[n];
+                    const int32_t na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+                    const uint64_t pw[4] = {0, 0, 0, 0};
+                    rc.row[dst] = r;
+                    L.flags[dst] = fl;
+                    rc.na[dst] = na;
+                    rc.s1[dst] = depth1_score(cf, nc, t, c, r, pw, n, na, key64_of(top, a));
+                }
+                for (int w = 0; w < 4; ++w) rc.pw[dst][w] = 0;
+            }
+            L.xn[r0][lane] = n;
+            L.wl64[0][lane] = key64_of(top, a);
+        }
+        __syncthreads();
+        for (int h = threadIdx.x; h < EngRowCache::kHashN; h += kPopThreads) rc.hkey[h] = -1;
+        __syncthreads();
+        if (wave == 0) {
+            const int n = L.xn[r0][lane];
+            if (n >= 0) rc_insert(&rc, n, 64 * r0 + lane);
+        }
+        __syncthreads();
+        // P4: the placement (parallel levels; rows from the cache); wave 0 then
+        // reports, updates the cached rows and writes them back
+        PopOut* out = (PopOut*)((char*)A.out + (size_t)d.slot * sizeof(PopOut));
+        // (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
+        // sends the others to the launched kernels; one instantiation keeps the
+        // kernel's registers within one 512-thread block per CU)
+        PlaceDec<uint32_t> D;
+        if (place_decide<uint32_t, true>(cf, nc, t, c, a, L.wl64, p, &rc, 0, D))
+            eng_finish(cf, nc, t, c, a, A, L, p, r0, out, D);
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dispatcher: host ring -> device ring (one wave)
+// ---------------------------------------------------------------------------
+__device__ void eng_dispatch(const EngArgs& A) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    uint32_t s = A.first;
+    bool idle = false;
+    for (;; ++s) {
+        // the device ring slot of pop s - kEngRing is free once the placer finished pop s - 5
+        if (s >= A.first + 5 && !eng_wait_done(ctl, s - 5)) break;
+        const uint64_t* src = A.hring + (size_t)(s % kEngHostRing) * 8 + (lane & 7);
+        uint64_t x = 0;
+        uint64_t t0 = 0;
+        bool got = false;
+        for (uint32_t it = 0;; ++it) {
+            x = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__ballot(lane < 8 && (uint32_t)(x >> 32) != s) == 0) { got = true; break; }
+            if ((it & 15) == 15) {
+                const uint64_t now = eng_now();
+                if (!t0) t0 = now;
+                if (ld_sc1(&ctl->err) != 0) break;
+                if (now - t0 > kEngIdleTicks) { idle = true; break; }
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        uint32_t op = kEngOpExit;
+        if (got) op = ((uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, kDwFlags) >> 12) & 0xf;
+        else if (ld_sc1(&ctl->err) != 0) break;
+        // forward (an idle end becomes an exit descriptor at s)
+        uint64_t v = x;
+        if (!got) v = lane == kDwFlags ? (((uint64_t)s << 32) | ((uint64_t)kEngOpExit << 12)) : ((uint64_t)s << 32);
+        if (lane < 8) st_sc1(&ctl->desc[s % kEngRing][lane], v);
+        if (op != kEngOpPop) break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+        __hip_atomic_store(A.hexit, (uint64_t)s | ((uint64_t)(idle ? 1 : 0) << 40) | (1ull << 41), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kPopThreads) void k_engine(Conf cf, NodeCols nc, DevTables t, EngArgs A) {
+    __shared__ EngLds lds;
+    const int b = blockIdx.x;
+    if (b < A.nw) {
+        eng_worker(cf, nc, t, A, lds.w, b);
+    } else if (b < A.nw + A.ng) {
+        eng_merger(A, lds.m, b - A.nw);
+    } else if (b == A.nw + A.ng) {
+        eng_placer(cf, nc, t, A, lds.p);
+    } else if (threadIdx.x < 64) {
+        eng_dispatch(A);
+    }
+}
+
+int engine_grid(const EngArgs& A) { return A.nw + A.ng + 2; }
+
+hipError_t launch_engine(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A, hipStream_t st) {
+    hipLaunchKernelGGL(k_engine, dim3(engine_grid(A)), dim3(kPopThreads), 0, st, cf, nc, t, A);
+    return hipGetLastError();
+}
+
+hipError_t engine_occupancy(int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_engine, kPopThreads, 0);
+}
+
+}  // namespace kbhip

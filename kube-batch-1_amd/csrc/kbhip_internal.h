@@ -211,6 +211,12 @@ struct SweepReq {
 };
 hipError_t launch_sweep_multi(const SweepReq* reqs, int n, int k, hipStream_t st, int* launches);
 size_t pop_out_bytes();
+// The persistent pop engine (kbhip_engine.hip, kbhip_engine.h): one resident
+// grid of engine_grid(A) blocks serving batched pops from a descriptor ring.
+struct EngArgs;
+hipError_t launch_engine(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A, hipStream_t st);
+hipError_t engine_occupancy(int* blocks_per_cu);
+int engine_grid(const EngArgs& A);
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);
 #endif

@@ -346,21 +346,14 @@ struct PopDescs {
 };
 static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed the kernel argument space");
 
-// The node index of a selection key.
-template <typename KT>
-__device__ __forceinline__ int key_node(KT k, const PopArgs& a) {
-    if constexpr (sizeof(KT) == 8) return key_idx(k);
-    else return a.kidxmax - (int)((k >> 1) & (uint32_t)a.kidxmax);
-}
-
 // Placement 7 with per-domain candidates (TaskClass::dd_space, kbhip_session.cpp
 // dedup_space): of the block's nodes of one domain of the space only the one
-// with the largest key stays (keys are unique: they carry the node index);
-// nodes without the topology key stay as they are.  The block's list then
-// holds at most one node per domain, so the pop's 64 candidates reach across
-// up to 64 domains instead of stopping at the first few domains' best nodes.
-// Every block also adds its domain maxima to the session's dd_max table, from
-// which the final merger takes the best node of every domain (dedup_final).
+// with the largest key can win (keys are unique: they carry the node index).
+// Every block adds its domain maxima to the session's dd_max table, from which
+// the final merger takes the best node of every domain (dedup_final), and
+// sends only its nodes without the topology key through the merge tree.  So
+// the pop's 64 candidates reach across up to 64 domains instead of stopping at
+// the first few domains' best nodes.
 template <typename KT, int R>
 __device__ __forceinline__ void dedup_domains(const NodeCols& nc, const DevTables& t, int space, int ndom, int bid,
                                               KT (&keys)[R]) {
@@ -378,9 +371,14 @@ __device__ __forceinline__ void dedup_domains(const NodeCols& nc, const DevTable
         }
     }
     __syncthreads();
+    // Every node with the topology key leaves the block's list: dd_max holds the
+    // exact best key of each domain over all blocks, so the merge tree carries
+    // only nodes without the key and yields their exact top 64 (a keyed node
+    // kept here could push keyless ones out of a merged list and the final
+    // merger would then miss them).
 #pragma unroll
     for (int r = 0; r < R; ++r)
-        if (d[r] >= 0 && dmax[d[r]] != keys[r]) keys[r] = 0;
+        if (d[r] >= 0) keys[r] = 0;
     for (int i = threadIdx.x; i < ndom; i += kPopThreads) {  // (drained before the block arrives)
         const KT v = dmax[i];
         if (v) atomicMax((unsigned long long*)&t.dd_max[i], (unsigned long long)v);
@@ -388,10 +386,10 @@ __device__ __forceinline__ void dedup_domains(const NodeCols& nc, const DevTable
 }
 
 // The final merger of a placement-7 pop with per-domain candidates (wave 0):
-// the merged list keeps its nodes without the topology key; every domain
-// contributes its best node from dd_max (all blocks added theirs before they
-// arrived), which is reset for the next launch.  The top 64 of those: at most
-// one node per domain.
+// the merged list is the exact top 64 of the nodes without the topology key
+// (dedup_domains left the others out); every domain contributes its best node
+// from dd_max (all blocks added theirs before they arrived), which is reset
+// for the next launch.  The top 64 of those: at most one node per domain.
 template <typename KT>
 __device__ __forceinline__ KT dedup_final(const NodeCols& nc, const DevTables& t, const TaskClass& c, const PopArgs& a,
                                           KT k) {
@@ -556,8 +554,8 @@ __device__ __forceinline__ void pop_batch_body(const Conf& cf, const NodeCols& n
     } else {  // PL == 2: parallel levels, every wave takes part
         static_assert(PL == 2, "batched placements: 2, 3, 6, 7");
         STAMP(nb_ * 4 + 1);
-        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
-        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, nullptr, s_fitin, fit_raw);
+        if (a.ent32) place_parallel<uint32_t>(cf, nc, t, c, a, out, wl, nullptr, 0, (const RowCache*)nullptr, s_fitin, fit_raw);
+        else place_parallel<uint64_t>(cf, nc, t, c, a, out, wl, nullptr, 0, (const RowCache*)nullptr, s_fitin, fit_raw);
     }
 }
 

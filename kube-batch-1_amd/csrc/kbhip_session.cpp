@@ -40,6 +40,7 @@
 #include "../../include/kbhip.h"
 #include "../../include/kbsnap.h"
 #include "kbhip_affinity.h"
+#include "kbhip_engine.h"
 #include "kbhip_eval.h"
 #include "kbhip_internal.h"
 
@@ -453,6 +454,7 @@ struct BatchLaunch {
     bool fit = false;  // placement 2: the kernel reports the FitDelta histogram of a task that found no node
     bool bf = false;   // placement 6 (Backfilled nodes): may end before its first task (n_done 0)
     bool aff = false;  // placement 7 (pod-affinity class): may end before its first task (n_done 0)
+    bool engine = false;  // served by the persistent pop engine (no launch of its own)
 };
 
 // A job pop submitted through the asynchronous per-pop ABI
@@ -560,6 +562,25 @@ struct Session {
     PopLink* d_link = nullptr;
     uint32_t ov_seq = 0;        // sequence number of the last overlapped pop launched
     uint32_t msg_from = 1;      // PopLink row messages of pops from this one on are current (none drained since)
+    // persistent pop engine (option "engine", kbhip_engine.hip): the batched pops of
+    // eligible classes go to one resident kernel on `stream` through a pinned descriptor ring
+#ifdef KBHIP_STAMPS
+    bool engine = false;        // stamps are written by k_pop_batch only
+#else
+    bool engine = true;
+#endif
+    bool eng_running = false;   // its kernel was launched and has not been seen to end
+    uint32_t eng_seq = 0;       // the last descriptor written (pop or exit)
+    uint32_t eng_first = 1;     // the first pop of the next launch
+    int eng_nw = 0, eng_npb = 0, eng_ng = 0;  // worker blocks (0: not sized yet, -1: the engine cannot run here)
+    int eng_nw_opt = 0;         // option "engine_workers" (0: as many as stay resident)
+    DevBuf b_eng;               // EngCtl + the worker and group lists
+    EngCtl* d_eng_ctl = nullptr;
+    uint64_t* d_eng_bl = nullptr;
+    uint64_t* d_eng_gl = nullptr;
+    uint64_t* h_eng = nullptr;  // pinned, mapped: [kEngHostRing][8] descriptor words, then the exit word
+    uint64_t* dv_eng = nullptr; // ... as the device sees it
+    size_t h_eng_cap = 0;
     int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
     bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
     DevBuf b_fit4;
@@ -645,6 +666,14 @@ struct Session {
     // Device side of the teardown: drain the streams, then hand streams, pinned
     // and device buffers back to the pool.  Idempotent.
     void release_device() {
+        if (eng_running && h_eng) {  // the engine's exit descriptor, then the stream drains below
+            const uint32_t sq = ++eng_seq;
+            for (int i = 0; i < 8; ++i)
+                __atomic_store_n(&h_eng[(sq % kEngHostRing) * 8 + i],
+                                 ((uint64_t)sq << 32) | (i == kDwFlags ? (uint64_t)kEngOpExit << 12 : 0),
+                                 __ATOMIC_RELEASE);
+            eng_running = false;
+        }
         for (int k = 1; k <= kMaxDep; ++k)
             if (ov_streams[k]) (void)hipStreamSynchronize(ov_streams[k]);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -673,6 +702,11 @@ struct Session {
             for (auto& e : pr)
                 if (e) { (void)hipEventDestroy(e); e = nullptr; }
         if (h_out) MemPool::get().give(MemPool::kPinnedMapped, h_out, h_out_cap, device);
+        if (h_eng) MemPool::get().give(MemPool::kPinnedMapped, h_eng, h_eng_cap, device);
+        h_eng = nullptr;
+        dv_eng = nullptr;
+        b_eng.release();
+        eng_nw = 0;
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
         h_rank = nullptr;
         h_out = nullptr;
@@ -2115,8 +2149,161 @@ static void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_
     S.stats.sweep_batch_sum += r.batch;
 }
 
+// ---------------------------------------------------------------------------
+// persistent pop engine (kbhip_engine.hip).  Eligible batched
+// pops are written as descriptors into a pinned ring; one resident kernel on
+// the session stream serves them in order and reports through the usual
+// result slots.  It runs until an exit descriptor (eng_stop: before any other
+// device work, from ov_drain) or until it has been idle for a second (then
+// eng_poll restarts it for descriptors written meanwhile).
+// ---------------------------------------------------------------------------
+static void eng_size(Session& S) {
+    S.eng_nw = -1;
+    const int N = S.nc.n;
+    if (S.encode_only || S.world != 1 || N < 1) return;
+    int cus = 0, bpc = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, S.device));
+    HIPCHK(engine_occupancy(&bpc));
+    const int resident = cus * bpc;  // every block of the grid must be resident at once
+    int nw = std::min(kEngWorkersMax, resident - kEngMaxGroups - 2);
+    if (S.eng_nw_opt > 0) nw = std::min(nw, S.eng_nw_opt);
+    nw = std::min(nw, std::max(1, (N + 63) / 64));  // at least 64 nodes per worker
+    if (nw < 1) return;
+    const int npb = (N + nw - 1) / nw;
+    if (npb > kEngMaxNpb) return;
+    const int ng = std::min(kEngMaxGroups, nw);
+    const size_t lists = (size_t)kEngSlots * (nw + ng) * kEngListWords;
+    const size_t words = sizeof(EngCtl) / 8 + lists;
+    char* d = (char*)S.b_eng.alloc<uint64_t>(words);
+    S.d_eng_ctl = (EngCtl*)d;
+    S.d_eng_bl = (uint64_t*)(d + sizeof(EngCtl));
+    S.d_eng_gl = S.d_eng_bl + (size_t)kEngSlots * nw * kEngListWords;
+    HIPCHK(hipMemsetAsync(d, 0, words * 8, S.stream));  // every tag 0: no pop has that sequence number
+    if (!S.h_eng) {
+        S.h_eng = (uint64_t*)MemPool::get().take(MemPool::kPinnedMapped, (kEngHostRing * 8 + 8) * sizeof(uint64_t),
+                                                 &S.h_eng_cap);
+        std::memset(S.h_eng, 0, (kEngHostRing * 8 + 8) * sizeof(uint64_t));
+        void* dv = nullptr;
+        HIPCHK(hipHostGetDevicePointer(&dv, S.h_eng, 0));
+        S.dv_eng = (uint64_t*)dv;
+        S.eng_seq = 0;
+        S.eng_first = 1;
+    }
+    S.eng_nw = nw;
+    S.eng_npb = npb;
+    S.eng_ng = ng;
+    S.stats.engine_workers = nw;
+}
+
+// A batched pop the engine can serve: one GPU, no Backfilled nodes, a class
+// without pod affinity, host ports or the backfill annotation, 32-bit keys
+// and placement entries (the engine's single placement instantiation).
+static bool eng_eligible(Session& S, int cls, const KeyFormat& kf) {
+    if (!S.engine || S.world != 1 || S.any_bf || S.rank_group || S.encode_only) return false;
+    const TaskClass& c = S.classes[cls];
+    if (c.aff || c.has_ports || c.backfill || !kf.use32 || !kf.ent32) return false;
+    if (S.eng_nw == 0) eng_size(S);
+    return S.eng_nw > 0;
+}
+
+static uint64_t* eng_exit_word(Session& S) { return S.h_eng + kEngHostRing * 8; }
+
+static void eng_write(Session& S, uint32_t seq, const uint32_t* w) {
+    uint64_t* slot = S.h_eng + (size_t)(seq % kEngHostRing) * 8;
+    for (int i = 0; i < 8; ++i) __atomic_store_n(&slot[i], ((uint64_t)seq << 32) | w[i], __ATOMIC_RELEASE);
+}
+
+static void eng_start(Session& S) {
+    HIPCHK(hipMemsetAsync(S.d_eng_ctl, 0, sizeof(EngCtl), S.stream));  // done 0, no error, ring tags 0
+    __atomic_store_n(eng_exit_word(S), (uint64_t)0, __ATOMIC_RELEASE);
+    EngArgs A{};
+    A.ctl = S.d_eng_ctl;
+    A.blists = S.d_eng_bl;
+    A.glists = S.d_eng_gl;
+    A.hring = S.dv_eng;
+    A.hexit = S.dv_eng + kEngHostRing * 8;
+    A.out = S.d_out;
+    A.first = S.eng_first;
+    A.nw = S.eng_nw;
+    A.npb = S.eng_npb;
+    A.ng = S.eng_ng;
+    HIPCHK(launch_engine(S.conf, S.nc, S.tab, A, S.stream));
+    S.eng_running = true;
+    S.stats.engine_launches++;
+}
+
+// The engine's kernel ended (its exit word, after a stream sync): check its
+// error word; the next launch starts at the first pop it did not serve.
+static void eng_ended(Session& S) {
+    HIPCHK(hipStreamSynchronize(S.stream));
+    S.eng_running = false;
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, &S.d_eng_ctl->err, sizeof(err), hipMemcpyDeviceToHost));
+    const uint64_t x = __atomic_load_n(eng_exit_word(S), __ATOMIC_ACQUIRE);
+    if (err || !(x & (1ull << 41))) throw Error(KBHIP_EDEVICE, "the pop engine stopped on a fault (error " +
+                                                                    std::to_string(err) + ")");
+    S.eng_first = (uint32_t)(x & 0xffffffffu);
+    const bool idle = (x >> 40) & 1;
+    if (!idle) S.eng_first += 1;  // an exit descriptor took that sequence number
+    S.msg_from = S.ov_seq + 1;    // the overlapped path's row messages are stale now
+    S.chain_fence = true;
+}
+
+// While waiting for an engine pop: a kernel that ended idle before it read
+// descriptors written meanwhile is restarted.  true: it was.
+static bool eng_poll(Session& S) {
+    if (!S.eng_running) return false;
+    const uint64_t x = __atomic_load_n(eng_exit_word(S), __ATOMIC_ACQUIRE);
+    if (!(x & (1ull << 41))) return false;
+    eng_ended(S);
+    if ((int32_t)(S.eng_seq - S.eng_first) >= 0) eng_start(S);  // descriptors it never served
+    return true;
+}
+
+static void eng_submit(Session& S, BatchLaunch& L, int cls, int m, int gang_mode, int min_avail, int ready_count,
+                       const KeyFormat& kf) {
+    if (S.eng_running) eng_poll(S);
+    uint32_t w[8];
+    w[kDwCls] = (uint32_t)cls;
+    w[kDwFlags] = (uint32_t)m | ((uint32_t)(gang_mode ? 1 : 0) << 8) | (1u << 9) | (kEngOpPop << 12);
+    w[kDwMinAvail] = (uint32_t)min_avail;
+    w[kDwReady] = (uint32_t)ready_count;
+    w[kDwEpochSlot] = (L.epoch & 0xffff) | ((uint32_t)L.slot << 16);
+    w[kDwKbase] = (uint32_t)kf.base;
+    w[kDwKshift] = (uint32_t)kf.shift;
+    w[kDwKidxmax] = (uint32_t)kf.idxmax;
+    eng_write(S, ++S.eng_seq, w);
+    if (!S.eng_running) {
+        if (S.ov_pending) {  // overlapped pops of the launched path may still run on the other stream
+            for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
+            S.ov_pending = false;
+        }
+        eng_start(S);
+    }
+    S.stats.engine_pops++;
+    L.engine = true;
+    L.st = S.stream;
+}
+
+// Stop the engine: an exit descriptor behind every pop written, then the
+// kernel's end.  The pops ahead of it complete first (their results stay in
+// the result slots for collect_batched).
+static void eng_stop(Session& S) {
+    if (!S.eng_running) return;
+    const uint32_t sq = ++S.eng_seq;
+    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    w[kDwFlags] = kEngOpExit << 12;
+    eng_write(S, sq, w);
+    for (;;) {
+        eng_ended(S);
+        if ((int32_t)(S.eng_first - sq) > 0) return;  // it reached the exit descriptor
+        eng_start(S);  // it ended idle before that: serve the rest
+    }
+}
+
 // Wait until no overlapped pop can still run.
 static void ov_drain(Session& S) {
+    eng_stop(S);
     S.msg_from = S.ov_seq + 1;  // device work outside the chain may follow: earlier row messages go stale
     S.chain_fence = true;       // ... on the session stream: the next chained pop is ordered after it
     if (!S.ov_pending) return;
@@ -2247,6 +2434,16 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     L.slot = take_slot(S, &L.epoch);
     L.cls = cls;
     L.m = m;
+    const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
+    if (eng_eligible(S, cls, kf)) {  // the persistent engine: a descriptor, no launch
+        auto te0 = std::chrono::steady_clock::now();
+        eng_submit(S, L, cls, m, gang_mode, min_avail, ready_count, kf);
+        L.fit = true;
+        S.sweep_launches++;
+        S.host_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - te0).count();
+        return L;
+    }
+    eng_stop(S);  // any other device work is ordered behind the engine's exit
     L.timed = S.time_every > 0 && (S.sweep_launches % S.time_every) == 0;
     S.sweep_launches++;
     hipEvent_t* ev = nullptr;
@@ -2296,7 +2493,6 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
     auto tl0 = std::chrono::steady_clock::now();
     if (L.timed) HIPCHK(hipEventRecord(ev[0], L.st));
     void* out = (char*)S.d_out + L.slot * sizeof(PopOutHost);
-    const KeyFormat kf = S.keys32 ? S.class_kf[cls] : KeyFormat{};
     if (shov) {  // overlapped shard pops: both kernels on stream seq % 2, chained to pop seq-1 on the device
         MboxArgs mb{};
         for (int p = 0; p < S.world; ++p) mb.dst[p] = S.mbox_peer[p];
@@ -2399,7 +2595,14 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
             while (got < n_done && tag(load(got)) == L.epoch) ++got;
             if (got == n_done) break;
         }
-        if (spin == (1L << 22)) HIPCHK(hipStreamSynchronize(L.st));  // long waits: runtime
+        if (L.engine && (spin & 0x3fff) == 0x3fff && eng_poll(S)) spin = 0;  // restarted after an idle end
+        if (spin == (1L << 22)) {  // long waits: the runtime (errors), or the engine's end
+            if (L.engine) {
+                if (S.eng_running) eng_stop(S);
+            } else {
+                HIPCHK(hipStreamSynchronize(L.st));
+            }
+        }
         if (spin > (1L << 22) + 1000) throw Error(KBHIP_EDEVICE, "batched pop produced no result");
         __builtin_ia32_pause();
     }
@@ -5549,6 +5752,20 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             s->s.speculate = (int)value;
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
+        else if (std::strcmp(key, "engine") == 0 || std::strcmp(key, "engine_workers") == 0) {
+            kbhip::Session& S = s->s;
+            if (!S.encode_only) {
+                HIPCHK(hipSetDevice(S.device));
+                kbhip::ov_quiesce(S);  // the running engine (if any) ends first
+            }
+            if (key[6] == 0) {
+                S.engine = value != 0;
+            } else {
+                if (value < 0 || value > kbhip::kEngWorkersMax) throw kbhip::Error(KBHIP_EINVAL, "engine_workers out of range");
+                S.eng_nw_opt = (int)value;
+                S.eng_nw = 0;  // sized again at the next engine pop
+            }
+        }
         else if (std::strcmp(key, "overlap") == 0) {
             if (value < 0 || value > kbhip::kMaxDep) throw kbhip::Error(KBHIP_EINVAL, "overlap must be 0, 1 or 2");
             if (!s->s.encode_only) {

@@ -142,3 +142,44 @@ def test_per_domain_candidates_pipelined(engine, oracle_mod, kbgen_mod, tmp_path
     p = c.write(str(tmp_path / "p.kbs"))
     st, st0 = _check(engine, oracle_mod, p)
     assert st["batched_pops"] >= st0["batched_pops"]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_per_domain_candidates_keyless_nodes(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Per-domain candidates over many sweep blocks with nodes that lack the
+    topology key: big nodes carry one of 24 zones (each block's
+    list holds a node per zone, enough to fill a merged top-64 with keyed
+    nodes), a third of the nodes — smaller, lower scores — have no zone label,
+    so a zone-anti-affine gang of up to 64 pods must spill onto them once the
+    zones are used.  Records equal the hoisted restatement's and the per-task
+    path's."""
+    rng = np.random.default_rng(9100 + seed)
+    c = kbgen_mod.Cluster()
+    c.add_queue("q0", 1)
+    zones = [f"z{i:02d}" for i in range(24)]
+    for i in range(3000 + 500 * seed):
+        name = f"n{i:05d}"
+        if rng.random() < 0.35:  # keyless: no zone label
+            c.add_node(name, 8000, 16 * GI, 0, 110, labels={"kubernetes.io/hostname": name})
+        else:
+            c.add_node(name, 64000, 256 * GI, 0, 110,
+                       labels={"zone": zones[int(rng.integers(24))], "kubernetes.io/hostname": name})
+    uid = 0
+    for j in range(24):
+        jn = f"j{j:03d}"
+        size = int(rng.integers(30, 65))
+        aff = {"anti": {"required": [{"selector": {"ml": {"job": jn}}, "topology_key": "zone"}]}} \
+            if j % 3 != 2 else None
+        c.add_job("ns", jn, "q0", min_member=int(rng.integers(size // 2, size + 1)), ts=j)
+        req = kbgen_mod.res(cpu=int(rng.choice([500, 1000])), mem=int(rng.choice([1, 2])) * GI)
+        for k in range(size):
+            c.add_pod("ns", f"{jn}-{k}", uid=f"p{uid:05d}", group=jn, ts=j, labels={"job": jn},
+                      containers=[dict(req)], affinity=aff)
+            uid += 1
+    p = c.write(str(tmp_path / "k.kbs"))
+    exp = oracle_mod.fast_allocate(p, threads=8).as_list()
+    got, ns, st, close = _run(engine, p)
+    assert [(a, b, 4 if k == 1 else 8) for a, b, k in got] == exp
+    ref, ns0, st0, close0 = _run(engine, p, aff_batch=0)
+    assert ref == got and np.array_equal(ns0, ns) and close0 == close
+    assert st["batched_pops"] > 0
