@@ -71,6 +71,10 @@ def parse():
     ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2),
                     help="1: batched pops alternate over two streams, a pop's sweep beside the previous pop's "
                          "placement (device-side chaining); 0 = one pop kernel at a time")
+    ap.add_argument("--engine", type=int, default=1, choices=(0, 1),
+                    help="1: batched pops go to the persistent pop engine (one resident kernel, DESIGN.md §4.10); "
+                         "0 = one launched kernel per pop")
+    ap.add_argument("--engine-workers", type=int, default=0, help="engine worker blocks (0: as many as stay resident)")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
                     help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
                          "each shard sweeps its node range to its top-64, one RCCL all-gather, identical placement "
@@ -208,12 +212,15 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2, keep_log=False):
+def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2, keep_log=False, engine=1,
+                engine_workers=0):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
     s.set_option("overlap", overlap)
     s.set_option("speculate", speculate)
+    s.set_option("engine", engine)
+    s.set_option("engine_workers", engine_workers)
     t1 = time.perf_counter()
     pod, node, kind = s.allocate(cap=1 << 21)
     t2 = time.perf_counter()
@@ -294,14 +301,16 @@ def main():
     device = local
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
-        run_session(buf, device, 0, shard, args.overlap, args.speculate)
+        run_session(buf, device, 0, shard, args.overlap, args.speculate, engine=args.engine,
+                    engine_workers=args.engine_workers)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
     dev_s, dev_pops = 0.0, 0
     for i in range(args.steps):
         dt, n, st = run_session(buf, device, args.time_every, shard, args.overlap,
-                                args.speculate, keep_log=(i == 0 and rank == 0))
+                                args.speculate, keep_log=(i == 0 and rank == 0), engine=args.engine,
+                                engine_workers=args.engine_workers)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
@@ -327,8 +336,9 @@ def main():
     # the hot kernel's mean duration: HIP events around every batched pop launch on the stream it runs on
     # (overlapped pops: the duration includes the wait for the previous pop's write-back, as rocprof's does)
     launch_us = (sweeps_ms / max(sweeps_n, 1)) * 1e3 if sweeps_n else 0.0
+    engine_on = st_last["engine_pops"] > 0
     kernel = "k_pop_batch (shard sweep, placement 3)" if shard else (
-        "k_pop_batch_ov" if args.overlap else "k_pop_batch")
+        "k_engine (persistent pop engine)" if engine_on else "k_pop_batch_ov" if args.overlap else "k_pop_batch")
     period_us = dev_s / dev_pops * 1e6 if dev_pops else 0.0
     # the kernel's busy period per launch: allocate's device span (HIP events on the engine streams) / launches
     achieved = nodes_per_launch * B_NODE / (period_us * 1e-6) / 1e9 if period_us > 0 else 0.0
@@ -353,6 +363,8 @@ def main():
                    "sweeps_per_session": st_last["sweeps"], "batched_pops": st_last["batched_pops"],
                    "open_s": st_last["open_s"], "allocate_s": st_last["allocate_s"],
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
+                   "engine_pops": st_last["engine_pops"], "engine_launches": st_last["engine_launches"],
+                   "engine_workers": st_last["engine_workers"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
                    "unassigned_pops": st_last["unassigned_pops"], "collectives": st_last["collectives"],

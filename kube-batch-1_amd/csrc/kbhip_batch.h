@@ -575,10 +575,11 @@ __device__ __forceinline__ Row place_row(const TaskClass& c, const PlaceDec<ET>&
 // the entries at or above it and leaves the rest of the chunk to the host
 // (stop 0 with done < m; done 0 when none).
 // Node indices in keys and entries are global.
+// rc_slots (LDS, optional): candidate j's row is in row-cache slot rc_slots[j] (no lookup).
 template <typename ET, bool SC1, typename RC>
 __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                              const PopArgs& a, uint64_t (*wl64)[64], uint32_t seq, const RC* rc,
-                                             uint64_t t0, PlaceDec<ET>& D) {
+                                             uint64_t t0, PlaceDec<ET>& D, const int32_t* rc_slots = nullptr) {
     constexpr int kW = kPopThreads / 64;  // depths per round
     __shared__ int32_t s_sc[kW][64];      // this round's scores, by depth slot
     __shared__ uint8_t s_kind[64][64];    // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
@@ -597,7 +598,7 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
     Row base{};
     uint64_t pw[4] = {0, 0, 0, 0};
     int32_t na_n = 0;
-    const int rslot = (rc && n >= 0) ? rc_find(rc, n) : -1;
+    const int rslot = (rc && n >= 0) ? (rc_slots ? rc_slots[lane] : rc_find(rc, n)) : -1;
     if (rslot >= 0) {
         base = rc->row[rslot];
         for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
@@ -806,10 +807,9 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
 // candidates then carry the commits made before the failing task.  Two
 // granules beside the placements (wave 0).
 template <typename ET>
-__device__ __forceinline__ void place_fit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                                          const PopArgs& a, PopOut* out, const PlaceDec<ET>& D, const int32_t* fit_in,
-                                          uint32_t fit_raw) {
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void place_fit_vals(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                               const TaskClass& c, const PopArgs& a, const PlaceDec<ET>& D,
+                                               const int32_t* fit_in, uint32_t fit_raw, uint64_t* g0, uint64_t* g1) {
     uint32_t fb_base = 0, fb_post = 0;
     if (D.n >= 0) {
         fb_base = fit_bits(c, D.base, true);  // candidates had a key: in the walk
@@ -825,22 +825,34 @@ __device__ __forceinline__ void place_fit(const Conf& cf, const NodeCols& nc, co
     for (int b = 0; b < 4; ++b)
         tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
                  __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
-    if (lane == 0) {
-        __hip_atomic_store(&out->fit[0], make_fit_granule(a.epoch, tot[0], tot[1]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&out->fit[1], make_fit_granule(a.epoch, tot[2], tot[3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    *g0 = make_fit_granule(a.epoch, tot[0], tot[1]);
+    *g1 = make_fit_granule(a.epoch, tot[2], tot[3]);
+}
+template <typename ET>
+__device__ __forceinline__ void place_fit(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                          const PopArgs& a, PopOut* out, const PlaceDec<ET>& D, const int32_t* fit_in,
+                                          uint32_t fit_raw) {
+    uint64_t g0, g1;
+    place_fit_vals(cf, nc, t, c, a, D, fit_in, fit_raw, &g0, &g1);
+    if ((threadIdx.x & 63) == 0) {
+        __hip_atomic_store(&out->fit[0], g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&out->fit[1], g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
+// The result granule of position `lane` (0: none to write).
+template <typename ET>
+__device__ __forceinline__ uint64_t place_granule_val(const PopArgs& a, const PlaceDec<ET>& D) {
+    const int lane = threadIdx.x & 63;
+    if (!(lane < D.done || (D.done == 0 && lane == 0))) return 0;
+    return make_granule(a.epoch, D.stop, D.done, lane < D.done ? D.kind : 0,
+                        (lane < D.done && D.inm) ? entry_node(D.L, a) : -1);
+}
 // The result granules of the chunk (wave 0; pinned host memory, one 8-byte store each).
 template <typename ET>
 __device__ __forceinline__ void place_granules(const PopArgs& a, PopOut* out, const PlaceDec<ET>& D) {
-    const int lane = threadIdx.x & 63;
-    if (lane < D.done || (D.done == 0 && lane == 0))
-        __hip_atomic_store(&out->g[lane], make_granule(a.epoch, D.stop, D.done, lane < D.done ? D.kind : 0,
-                                                       (lane < D.done && D.inm) ? entry_node(D.L, a) : -1),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t g = place_granule_val(a, D);
+    if (g) __hip_atomic_store(&out->g[threadIdx.x & 63], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename ET, bool SC1 = false, typename RC = RowCache>

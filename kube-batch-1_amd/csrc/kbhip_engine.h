@@ -8,9 +8,11 @@
 //     (PredicateFn + NodeOrderFn -> selection key, kbhip_eval.h) and publish
 //     their top-128 keys;
 //   * merger blocks (one per group of workers) merge their group's lists;
-//   * the placer block merges the group lists, re-evaluates the previous two
-//     pops' candidates from its own LDS rows, places the chunk (parallel
-//     levels, kbhip_batch.h) and writes the rows back;
+//   * the final merger merges the group lists and gathers the rows of the
+//     top 128 into a package (EngPkg);
+//   * the placer block loads the package, drops the previous pop's candidates,
+//     re-evaluates the previous two pops' candidates from its own LDS rows,
+//     places the chunk (parallel levels, kbhip_batch.h) and writes the rows back;
 //   * the dispatcher block copies pop descriptors from the host's pinned ring
 //     into a device ring.
 // Pop p's workers read the node rows as pop p-3 left them; the candidates of
@@ -29,6 +31,20 @@ constexpr int kEngMaxGroups = 8;  // merger blocks
 constexpr int kEngListWords = 136;  // a list: 128 tagged keys + 4 tagged counts (+ pad), 17 lines
 constexpr int kEngMaxNpb = 8192;  // nodes per worker block
 constexpr int kEngWorkersMax = 512;
+
+// The final merger's package for pop p (slot p % kEngSlots): the pop's
+// descriptor and task class, and the top 128 keys of the group lists with
+// every entry's node row and its node-affinity weight and depth-1 score for
+// the pop's class, field-major (word f of entry e at w[f][e]): 0 key, 1..28
+// the Row (kbhip_eval.h, as 32-bit words), 29 flags, 30 na, 31 s1.  Every
+// word is a self-tagged granule {p << 32 | value} (one sc1 store each): the
+// placer takes the package once every tag reads p.
+constexpr int kEngPkgN = 128, kEngPkgFields = 32, kEngPkgHdr = 64;
+enum : int { kPkKey = 0, kPkRow = 1, kPkFlags = 29, kPkNa = 30, kPkS1 = 31 };
+struct EngPkg {
+    uint64_t hdr[kEngPkgHdr];  // 0..7 the descriptor words, 8.. the TaskClass words
+    uint64_t w[kEngPkgFields][kEngPkgN];
+};
 
 // Descriptor words (each {seq << 32 | value}, self-tagged: a reader takes a
 // descriptor once all eight tags read its sequence number).
@@ -52,11 +68,15 @@ struct EngArgs {
     EngCtl* ctl;
     uint64_t* blists;          // [kEngSlots][nw][kEngListWords] worker lists (+ 2 count words)
     uint64_t* glists;          // [kEngSlots][ng][kEngListWords] group lists (+ 4 count words)
+    EngPkg* pkg;               // [kEngSlots] the final merger's packages
     const uint64_t* hring;     // [kEngHostRing][8] pinned host descriptors (device view)
     uint64_t* hexit;           // pinned host word: {exit seq | idle << 40 | 1 << 41} when the engine ends
     void* out;                 // result slots (PopOut, pinned host memory, device view)
     uint32_t first;            // the first pop of this launch (earlier pops are written back)
     int nw, npb, ng;           // workers, nodes per worker, merger groups
+    uint64_t* tl;              // diagnostic event timeline (option "engine_timeline"), or null
 };
+// Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
+constexpr int kEngTlSlots = 8192, kEngTlEvents = 32;
 
 }  // namespace kbhip

@@ -4,8 +4,9 @@
 // Roles by block (kbhip_engine.h):
 //   [0, nw)        workers: node range [b * npb, (b + 1) * npb)
 //   [nw, nw + ng)  mergers: group g = workers b with b % ng == g
-//   nw + ng        placer
-//   nw + ng + 1    dispatcher (one wave)
+//   nw + ng        final merger (the package of the group lists' top 128)
+//   nw + ng + 1    placer
+//   nw + ng + 2    dispatcher (one wave)
 // Hand-offs are self-tagged 8-byte granules {seq << 32 | value} written with
 // sc1 stores and polled with sc1 loads (MI355X_MICROARCH.md, R2), or sc1 row
 // stores drained before the sc1 `done` flag (valid forms, table row 1).
@@ -23,6 +24,14 @@ constexpr uint64_t kEngIdleTicks = 100000000ull;  // 1 s without a descriptor: t
 constexpr uint64_t kEngDescTicks = 400000000ull;  // a block waiting for its next descriptor
 
 __device__ __forceinline__ uint64_t eng_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+// Diagnostic timeline: lane 0 of the calling wave stamps event ev of pop p
+// (null buffer: nothing; the check is a scalar branch on a kernel argument).
+#define ETL(A, p, ev)                                                                                    \
+    do {                                                                                                 \
+        if ((A).tl && (threadIdx.x & 63) == 0)                                                           \
+            (A).tl[(size_t)((p) % kEngTlSlots) * kEngTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 
 // A bounded wait: call tick() once per unsuccessful poll; false = give up
 // (timed out: the error is recorded; or another block recorded one).
@@ -45,6 +54,20 @@ struct EngWait {
         return true;
     }
 };
+
+// Every dword of v through readfirstlane: a wave-uniform value held in scalar
+// registers (a TaskClass read from LDS or global memory: otherwise every
+// field access in the evaluation functions is a dependent memory round trip).
+template <typename T>
+__device__ __forceinline__ T eng_uniform(const T& v) {
+    static_assert(sizeof(T) % 4 == 0, "dwords");
+    T r;
+    const uint32_t* s = (const uint32_t*)&v;
+    uint32_t* d = (uint32_t*)&r;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[i]);
+    return r;
+}
 
 // The pop's descriptor as a block sees it (from the device ring).
 struct EngDesc {
@@ -183,23 +206,33 @@ struct EngWorkerLds {
 struct EngMergerLds {
     uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
     uint32_t desc[8];
+    TaskClass cls;  // the final merger: the pop's class (na, depth-1 scores)
     int ok;
 };
-constexpr int kEngRc = 4 * 64;  // the placer's rows: four pops' candidates, slot = 64 * (pop % 4) + lane
+// The placer's rows: four pops' candidates (slot 64 * (pop % 4) + lane) and
+// two packages' 128 entries (pop q's in slots kEngStage + 128 * (q % 2) + e).
+constexpr int kEngStage = 4 * 64, kEngRc = kEngStage + 2 * kEngPkgN;
 using EngRowCache = RowCacheT<kEngRc, 10>;
 struct EngPlacerLds {
     EngRowCache rc;
     uint8_t flags[kEngRc];
     int32_t xn[4][64];           // candidates of pop q in ring q % 4 (-1: none)
-    uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
     uint64_t wl64[kPopThreads / 64][64];
+    uint32_t pkey[2][kEngPkgN];  // pop q's package keys (q % 2)
     uint32_t s64[64];            // the merged list without pop p-1's candidates
-    uint32_t e[2][64];           // re-evaluated keys of pops p-1 / p-2's candidates
+    uint32_t e[2][64];           // re-evaluated keys of pops p-1 / p-2's candidates (sorted)
+    int32_t s1a[2][64], s1p[2][64];  // ... their depth-1 scores after an Allocate / a Pipeline
     uint8_t fbp[2][64];
     uint8_t x2use[64];
+    int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
-    uint32_t desc[8];
+    uint32_t desc[2][8];         // pop q's descriptor (q % 2)
+    TaskClass cls[2];            // pop q's task class (q % 2)
+    uint64_t gran[64];           // the pop's result granules (0: none), stored to the host by wave 5
+    uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
+    int gran_seq;                // the pop whose granules are in gran / gfit
+    int s1_ready[2];             // P2: depth-1 score waves done (per candidate set; 2 = both kinds)
 };
 union EngLds {
     EngWorkerLds w;
@@ -210,7 +243,7 @@ union EngLds {
 // ---------------------------------------------------------------------------
 // worker
 // ---------------------------------------------------------------------------
-__device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+__device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                            EngWorkerLds& L, int b) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
@@ -223,11 +256,14 @@ __device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& 
         __syncthreads();  // the previous pop done (wave 0 cleared L.ok if it failed)
         if (!L.ok) return;
         if (threadIdx.x < 4) L.fitb[threadIdx.x] = 0;
+        const int tb = b == 0 ? 10 : -1;  // timeline: worker 0
         if (wave == 0) {
             bool ok = eng_wait_desc(ctl, p, L.desc);
+            if (tb >= 0) ETL(A, p, tb);
             const EngDesc d0 = eng_decode(L.desc);  // (LDS written by this wave, in order)
             if (ok && d0.op == kEngOpPop) {
                 if (p >= A.first + 3) ok = eng_wait_done(ctl, p - 3);
+                if (tb >= 0) ETL(A, p, tb + 1);
                 if (ok && p >= A.first + 2) {
                     int node = -1;
                     ok = eng_wait_cands(ctl, p - 2, &node);
@@ -255,6 +291,7 @@ __device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& 
             if (base == 0) a0 = ks;
             else wave_merge128_desc(a0, a1, ks, 0u);
         }
+        if (tb >= 0 && wave == 0) ETL(A, p, tb + 2);
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
         // 3. publish the block's top 128 (wave 0), then its FitDelta counts
         // without pop p-1's candidates (their rows may be in flight: the
@@ -263,6 +300,7 @@ __device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& 
             uint64_t* dst = A.blists + ((size_t)(p % kEngSlots) * A.nw + b) * kEngListWords;
             st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
             st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
+            if (tb >= 0) ETL(A, p, tb + 3);
             bool ok = true;
             if (p >= A.first + 1) {
                 int node = -1;
@@ -282,6 +320,7 @@ __device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& 
                 const uint32_t v = (L.fitb[2 * lane] & 0xffff) | (L.fitb[2 * lane + 1] << 16);
                 st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | v);
             }
+            if (tb >= 0) ETL(A, p, tb + 4);
         }
     }
 }
@@ -289,7 +328,7 @@ __device__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& 
 // ---------------------------------------------------------------------------
 // merger of group g
 // ---------------------------------------------------------------------------
-__device__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
+__device__ __forceinline__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     const int cg = (A.nw - g + A.ng - 1) / A.ng;  // workers of the group: g, g + ng, ...
@@ -300,6 +339,7 @@ __device__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
         if (wave == 0) {
             const bool ok = eng_wait_desc(ctl, p, L.desc);
             if (lane == 0) L.ok = ok;
+            if (g == 0) ETL(A, p, 24);
         }
         __syncthreads();
         if (!L.ok) return;
@@ -337,12 +377,14 @@ __device__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
                 for (int q = 0; q < kQ; ++q) wave_merge128_desc(a0, a1, (uint32_t)v0[q], (uint32_t)v1[q]);
         }
         if (!ok) L.ok = 0;
+        if (g == 0 && wave == 0) ETL(A, p, 25);
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
         if (!L.ok) return;
         if (wave == 0) {
             uint64_t* dst = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords;
             st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
             st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
+            if (g == 0) ETL(A, p, 26);
             // the group's FitDelta counts: lane i reads worker g + i * ng's two count words
             uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             for (int i0 = 0; i0 < cg && ok; i0 += 64) {
@@ -363,85 +405,41 @@ __device__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
             if (!ok && lane == 0) L.ok = 0;
             if (ok && lane < 4)
                 st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | (lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? t2 : t3));
+            if (g == 0) ETL(A, p, 27);
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// placer
+// final merger: the group lists' top 128 with their rows -> the package
 // ---------------------------------------------------------------------------
-// The placer's wave 0 after the decision: the FitDelta histogram of a task
-// that found no node (the sweep's counts from the group count words), the
-// chunk's rows into the cache (ring r0) and, write-through, into the node
-// columns, drained before `done`; then the result granules.
-template <typename ET>
-__device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                                           const PopArgs& a, const EngArgs& A, EngPlacerLds& L, uint32_t p, int r0,
-                                           PopOut* out, const PlaceDec<ET>& D) {
-    const int lane = threadIdx.x & 63;
-    EngCtl* ctl = A.ctl;
-    if (D.stop == 1) {
-        uint32_t fr = 0;  // group g's count b in lane 4g + b (fit_sum layout)
-        const int g = lane >> 2;
-        if (g < A.ng) {
-            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords + 128 + (lane & 3);
-            uint64_t x = ld_sc1(s);
-            EngWait wt(ctl, kEngWaitTicks);
-            while (__ballot((uint32_t)(x >> 32) != p) != 0) {
-                if (!wt.tick()) break;
-                x = ld_sc1(s);
-            }
-            fr = (uint32_t)x;
-        }
-        place_fit(cf, nc, t, c, a, out, D, L.fitin, fr);
-    }
-    const int n = D.n;
-    if (n >= 0 && D.cc > 0) {
-        const Row r = place_row(c, D);
-        L.rc.row[64 * r0 + lane] = r;
-        st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
-        st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
-        st_sc1(&nc.pods[n], r.pods);
-        st_sc1(&nc.nzc[n], r.nzc);
-        st_sc1(&nc.nzm[n], r.nzm);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the write-back, then `done`
-    if (lane == 0) st_sc1(&ctl->done, p);
-    place_granules(a, out, D);
-}
-
-__device__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
-                           EngPlacerLds& L) {
+// The nodes of pop p's lists are not pop p-2's candidates (the workers left
+// those out); pop p-1's may be among them with stale keys and rows (the placer
+// drops them); every other node was last written by pop p-3 or earlier, whose
+// write-back the workers saw drained before they evaluated pop p.
+__device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                          EngMergerLds& L) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
-    EngRowCache& rc = L.rc;
-    for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
     if (threadIdx.x == 0) L.ok = 1;
     for (uint32_t p = A.first;; ++p) {
-        const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r0 = (int)(p % 4);  // rings of p-1, p-2, p
-        // P0: descriptor; the hash of pops p-1 / p-2's candidates (node -> latest row slot)
-        for (int h = threadIdx.x; h < EngRowCache::kHashN; h += kPopThreads) rc.hkey[h] = -1;
         __syncthreads();
         if (!L.ok) return;
         if (wave == 0) {
             const bool ok = eng_wait_desc(ctl, p, L.desc);
+            const EngDesc d0 = eng_decode(L.desc);
+            if (ok && d0.op == kEngOpPop && lane < (int)(sizeof(TaskClass) / 4))
+                ((uint32_t*)&L.cls)[lane] =
+                    ((const uint32_t*)&t.classes[__builtin_amdgcn_readfirstlane((int)d0.cls)])[lane];
             if (lane == 0) L.ok = ok;
-            const int n1 = L.xn[r1][lane];
-            if (n1 >= 0) rc_insert(&rc, n1, 64 * r1 + lane);
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-            const int n2 = L.xn[r2][lane];
-            const bool use2 = n2 >= 0 && rc_find(&rc, n2) < 0;  // a node of both: pop p-1's row is the latest
-            L.x2use[lane] = use2;
-            if (use2) rc_insert(&rc, n2, 64 * r2 + lane);
+            ETL(A, p, 20);
         }
         __syncthreads();
         if (!L.ok) return;
         const EngDesc d = eng_decode(L.desc);
         if (d.op != kEngOpPop) return;
         const PopArgs a = eng_args(d);
-        const TaskClass& c = t.classes[__builtin_amdgcn_readfirstlane((int)d.cls)];
-        // P1: the group lists (wave g polls group g), merged to the top 128
+        const TaskClass& c = L.cls;
         uint32_t a0 = 0, a1 = 0;
         bool ok = true;
         if (wave < A.ng) {
@@ -459,12 +457,219 @@ __device__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& 
         }
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
         if (!L.ok) return;
-        // P2: wave 0 drops pop p-1's candidates from the merged list (their
-        // keys are stale; at most 64 of 128: the first 64 left are exact);
-        // waves 1 / 2 re-evaluate pops p-1 / p-2's candidates on their rows
+        if (wave == 0) ETL(A, p, 21);
+        EngPkg* pk = A.pkg + (p % kEngSlots);
+        const uint64_t tag = (uint64_t)p << 32;
+        if (wave < 2) {  // entry e = 64 * wave + lane: its key, row, flags, node-affinity weight, depth-1 score
+            const int e = 64 * wave + lane;
+            const uint32_t k = wave == 0 ? L.wl[0][lane] : L.wl2[0][lane];
+            const int n = k ? key_node(k, a) : -1;
+            uint32_t v[kEngPkgFields];
+#pragma unroll
+            for (int f = 0; f < kEngPkgFields; ++f) v[f] = 0;
+            v[kPkKey] = k;
+            if (n >= 0) {
+                const Row r = load_row_sc1(nc, n);
+                const uint8_t fl = nc.flags[n];
+                const int32_t na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+                const uint64_t pw[4] = {0, 0, 0, 0};
+                const uint32_t* rw = (const uint32_t*)&r;
+#pragma unroll
+                for (int f = 0; f < (int)(sizeof(Row) / 4); ++f) v[kPkRow + f] = rw[f];
+                v[kPkFlags] = fl;
+                v[kPkNa] = (uint32_t)na;
+                v[kPkS1] = (uint32_t)depth1_score(cf, nc, t, c, r, pw, n, na, key64_of(k, a));
+            }
+#pragma unroll
+            for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
+        } else if (wave == 2) {  // the header: descriptor and class words
+            uint32_t v = 0;
+            if (lane < 8) v = L.desc[lane];
+            else if (lane < 8 + (int)(sizeof(TaskClass) / 4)) v = ((const uint32_t*)&L.cls)[lane - 8];
+            st_sc1(&pk->hdr[lane], tag | v);
+        }
+        if (wave == 0) ETL(A, p, 22);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// placer
+// ---------------------------------------------------------------------------
+static_assert(sizeof(Row) == 4 * (kPkFlags - kPkRow), "the package carries a Row as 28 32-bit words");
+static_assert(sizeof(TaskClass) / 4 + 8 <= kEngPkgHdr, "the package header carries the descriptor and class");
+
+// The placer's wave 0 after the decision: the FitDelta histogram of a task
+// that found no node (the sweep's counts from the group count words), the
+// result granules into LDS for wave 5 (which stores them to the host: the
+// system-scope stores' completion never holds up a wait of this wave), the
+// chunk's rows into the cache (ring r0) and, write-through, into the node
+// columns.  The row stores are left in flight: the next pop drains them
+// before it publishes its candidates, and only then raises `done` for this
+// pop (*pend).
+template <typename ET>
+__device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                           const PopArgs& a, const EngArgs& A, EngPlacerLds& L, uint32_t p, int r0,
+                                           const PlaceDec<ET>& D, uint32_t* pend) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    uint64_t g0 = 0, g1 = 0;
+    if (D.stop == 1) {
+        uint32_t fr = 0;  // group g's count b in lane 4g + b (fit_sum layout)
+        const int g = lane >> 2;
+        if (g < A.ng) {
+            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords + 128 + (lane & 3);
+            uint64_t x = ld_sc1(s);
+            EngWait wt(ctl, kEngWaitTicks);
+            while (__ballot((uint32_t)(x >> 32) != p) != 0) {
+                if (!wt.tick()) break;
+                x = ld_sc1(s);
+            }
+            fr = (uint32_t)x;
+        }
+        place_fit_vals(cf, nc, t, c, a, D, L.fitin, fr, &g0, &g1);
+    }
+    L.gran[lane] = place_granule_val(a, D);
+    if (lane == 0) { L.gfit[0] = g0; L.gfit[1] = g1; }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the granules are in LDS before the flag
+    if (lane == 0) __hip_atomic_store(&L.gran_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int n = D.n;
+    if (n >= 0) {  // every candidate's row after the chunk into ring r0 (the next two pops re-evaluate them)
+        const int src = L.srcslot[lane];
+        L.rc.row[64 * r0 + lane] = place_row(c, D);
+        L.flags[64 * r0 + lane] = L.flags[src];
+    }
+    if (n >= 0 && D.cc > 0) {
+        const Row r = place_row(c, D);
+        st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
+        st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
+        st_sc1(&nc.pods[n], r.pods);
+        st_sc1(&nc.nzc[n], r.nzc);
+        st_sc1(&nc.nzm[n], r.nzm);
+    }
+    ETL(A, p, 7);
+    *pend = p;
+}
+
+// Wave 0: drain this wave's stores (the write-back of pop *pend), then raise `done`.
+__device__ __forceinline__ void eng_publish_done(EngCtl* ctl, uint32_t* pend) {
+    if (!*pend) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if ((threadIdx.x & 63) == 0) st_sc1(&ctl->done, *pend);
+    *pend = 0;
+}
+
+// Pop q's front, by waves: 2 the hash of pops q-1 / q-2's candidates (node
+// -> latest row slot); 3, 4, 6, 7 its package — fields 8k .. 8k + 7 of the 128
+// entries each, wave 3 also the descriptor and class — into LDS, polled
+// until every granule carries q (one round trip when it is ready).  Run for
+// pop p + 1 by the waves pop p's placement leaves idle (and for the first pop
+// up front).  An exit descriptor has no package: its descriptor comes from
+// the device ring.
+__device__ __forceinline__ void eng_front(const EngArgs& A, EngPlacerLds& L, uint32_t q, int wave) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    EngRowCache& rc = L.rc;
+    if (wave == 2) {
+        const int r1 = (int)((q + 3) % 4), r2 = (int)((q + 2) % 4);
+        for (int h = lane; h < EngRowCache::kHashN; h += 64) rc.hkey[h] = -1;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int n1 = L.xn[r1][lane];
+        if (n1 >= 0) rc_insert(&rc, n1, 64 * r1 + lane);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int n2 = L.xn[r2][lane];
+        const bool use2 = n2 >= 0 && rc_find(&rc, n2) < 0;  // a node of both: pop q-1's row is the latest
+        L.x2use[lane] = use2;
+        if (use2) rc_insert(&rc, n2, 64 * r2 + lane);
+        return;
+    }
+    if (!(wave == 3 || wave == 4 || wave == 6 || wave == 7)) return;
+    const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block
+    const EngPkg* pk = A.pkg + (q % kEngSlots);
+    uint64_t v[16];
+    uint64_t h = (uint64_t)q << 32;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+    if (k == 0) h = ld_sc1(&pk->hdr[lane]);
+    bool got = false;
+    EngWait wt(ctl, kEngDescTicks);  // (a package waits as long as its pop's descriptor may)
+    for (;;) {
+        bool miss = (uint32_t)(h >> 32) != q;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) miss |= (uint32_t)(v[i] >> 32) != q;
+        if (__ballot(miss) == 0) { got = true; break; }
+        const uint64_t dw = ld_sc1(&ctl->desc[q % kEngRing][kDwFlags]);
+        if ((uint32_t)(dw >> 32) == q && (((uint32_t)dw >> 12) & 0xf) != kEngOpPop) break;  // an exit
+        if (!wt.tick()) break;
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if ((uint32_t)(v[i] >> 32) != q) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+        if (k == 0 && (uint32_t)(h >> 32) != q) h = ld_sc1(&pk->hdr[lane]);
+    }
+    if (got) {
+        const int base = kEngStage + kEngPkgN * (int)(q % 2);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int f = 8 * k + (i >> 1), e = lane + 64 * (i & 1), sl = base + e;
+            const uint32_t x = (uint32_t)v[i];
+            if (f == kPkKey) L.pkey[q % 2][e] = x;
+            else if (f < kPkFlags) ((uint32_t*)&rc.row[sl])[f - kPkRow] = x;
+            else if (f == kPkFlags) L.flags[sl] = (uint8_t)x;
+            else if (f == kPkNa) rc.na[sl] = (int32_t)x;
+            else rc.s1[sl] = (int32_t)x;
+        }
+        if (k == 0) {
+            for (int w = 0; w < 4; ++w) { rc.pw[base + lane][w] = 0; rc.pw[base + 64 + lane][w] = 0; }
+            if (lane < 8) L.desc[q % 2][lane] = (uint32_t)h;
+            else if (lane < 8 + (int)(sizeof(TaskClass) / 4)) ((uint32_t*)&L.cls[q % 2])[lane - 8] = (uint32_t)h;
+        }
+    } else if (k == 0) {  // the exit descriptor, or an error
+        const bool ok = eng_wait_desc(ctl, q, L.desc[q % 2]);
+        if (!ok && lane == 0) L.ok = 0;
+    }
+}
+
+// The placer, per pop p (its front — descriptor, class, candidate hash,
+// package — was prepared during pop p-1's placement):
+//   P2  wave 0 drops pop p-1's candidates from the package list (stale keys: at most 64
+//       of 128, the first 64 left are exact); waves 1-4 re-evaluate pops p-1 / p-2's
+//       candidates on the rows this block left them with (keys, depth-1 scores);
+//   P3  the final top 64, pop p-1's `done` (its write-back drained), pop p's candidates
+//       published, their rows into ring p % 4;
+//   P4  the placement (place_decide, parallel levels, rows in ring order); wave 0 then
+//       the results and rows, wave 5 stores the results to the host, the other waves
+//       prepare pop p+1's front.
+__device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                                           EngPlacerLds& L) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    EngRowCache& rc = L.rc;
+    for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
+    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready[0] = L.s1_ready[1] = 0; }
+    __syncthreads();
+    eng_front(A, L, A.first, wave);
+    uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
+    for (uint32_t p = A.first;; ++p) {
+        const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r0 = (int)(p % 4);  // rings of p-1, p-2, p
+        const int stage = kEngStage + kEngPkgN * (int)(p % 2);
+        __syncthreads();
+        if (!L.ok) return;
+        const EngDesc d = eng_decode(L.desc[p % 2]);
+        if (d.op != kEngOpPop) {
+            if (wave == 0) eng_publish_done(ctl, &pend);
+            return;
+        }
+        const PopArgs a = eng_args(d);
+        const TaskClass& c = L.cls[p % 2];
+        if (wave == 0) {
+            ETL(A, p, 0);
+            if (lane == 0 && A.tl) A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 31] = p;
+        }
+        // P2
         if (wave == 0) {
             L.s64[lane] = 0;
-            const uint32_t k0 = L.wl[0][lane], k1 = L.wl2[0][lane];
+            const uint32_t k0 = L.pkey[p % 2][lane], k1 = L.pkey[p % 2][64 + lane];
             auto kept = [&](uint32_t k) {
                 if (!k) return false;
                 const int sl = rc_find(&rc, key_node(k, a));
@@ -479,34 +684,70 @@ __device__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& 
             __builtin_amdgcn_wave_barrier();
             if (c0) L.s64[q0] = k0;
             if (c1 && q1 < 64) L.s64[q1] = k1;
-        } else if (wave == 1 || wave == 2) {
-            const int q = wave - 1;
+            // the kept nodes' rows: their package entries
+            if (c0) rc_insert(&rc, key_node(k0, a), stage + lane);
+            if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
+            ETL(A, p, 1);
+        } else if (wave != 2) {  // pops p-1 (q 0) / p-2 (q 1)'s candidates on this block's rows:
+            // waves 1 / 3 their keys (sorted) and FitDelta bits, waves 5 / 4 and 6 / 7 their
+            // depth-1 scores after an Allocate / a Pipeline; the key wave then keeps the one its
+            // key's kind calls for
+            const int q = (wave == 1 || wave == 5 || wave == 6) ? 0 : 1;
+            const int role = (wave == 1 || wave == 3) ? 0 : (wave == 5 || wave == 4) ? 1 : 2;
             const int ring = q == 0 ? r1 : r2;
             const int node = L.xn[ring][lane];
             const bool use = node >= 0 && (q == 0 || L.x2use[lane]);
-            uint32_t e = 0, fb = 0;
-            if (use) {
-                const int sl = 64 * ring + lane;
-                const Row r = rc.row[sl];
-                const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
-                const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
-                const uint64_t pw[4] = {0, 0, 0, 0};
-                int32_t sc;
-                bool passed;
-                const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
-                rc.na[sl] = na;
-                rc.s1[sl] = k0 ? depth1_score(cf, nc, t, c, r, pw, node, na, k0) : INT32_MIN;
-                e = sweep_key<uint32_t>(k0, a);
-                fb = fit_bits(c, r, passed);
+            const int sl = 64 * ring + lane;
+            const uint64_t pw[4] = {0, 0, 0, 0};
+            if (role == 0) {
+                uint32_t e = 0, fb = 0;
+                int kind = 0;
+                if (use) {
+                    const Row r = rc.row[sl];
+                    const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
+                    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
+                    int32_t sc;
+                    bool passed;
+                    const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
+                    rc.na[sl] = na;
+                    e = sweep_key<uint32_t>(k0, a);
+                    fb = fit_bits(c, r, passed);
+                    kind = k0 ? key_kind(k0) : 0;
+                }
+                if (wave == 1) ETL(A, p, 2);
+                L.e[q][lane] = wave_sort_desc(e);
+                if (wave == 1) ETL(A, p, 9);
+                L.fbp[q][lane] = (uint8_t)fb;
+                // the depth-1 score the placement reads (its key's kind decides the commit)
+                while (__hip_atomic_load(&L.s1_ready[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
+                    __builtin_amdgcn_s_sleep(1);
+                if (use) rc.s1[sl] = kind == 0 ? INT32_MIN : kind == 2 ? L.s1p[q][lane] : L.s1a[q][lane];
+            } else {
+                int32_t s1 = INT32_MIN;
+                if (use) {
+                    const Row r = rc.row[sl];
+                    const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
+                    const int alloc = role == 1 ? 1 : 0;
+                    const Row r1 = apply_commits(r, c, alloc, 1 - alloc);
+                    int32_t sc;
+                    bool passed;
+                    const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
+                    s1 = k1 ? key_score(k1) : INT32_MIN;
+                }
+                if (role == 1) L.s1a[q][lane] = s1;
+                else L.s1p[q][lane] = s1;
+                if (wave == 5) ETL(A, p, 19);
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the scores are in LDS before the count
+                if (lane == 0) __hip_atomic_fetch_add(&L.s1_ready[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-            L.e[q][lane] = e;
-            L.fbp[q][lane] = (uint8_t)fb;
         }
         __syncthreads();
-        // P3: wave 0: the final list, pop p's candidates published, their rows into ring p % 4
+        if (wave == 0) ETL(A, p, 3);
+        // P3
         if (wave == 0) {
-            uint32_t top = wave_merge_desc(L.s64[lane], wave_sort_desc(L.e[0][lane]));
-            top = wave_merge_desc(top, wave_sort_desc(L.e[1][lane]));
+            if (lane < 2) L.s1_ready[lane] = 0;
+            uint32_t top = wave_merge_desc(L.s64[lane], L.e[0][lane]);
+            top = wave_merge_desc(top, L.e[1][lane]);
             const uint32_t fbp = (uint32_t)L.fbp[0][lane] | ((uint32_t)L.fbp[1][lane] << 4);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -514,55 +755,55 @@ __device__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& 
                 if (lane == q) L.fitin[q] = k;
             }
             const int n = top ? key_node(top, a) : -1;
+            eng_publish_done(ctl, &pend);  // pop p-1's write-back (every node a worker may read next)
             st_sc1(&ctl->cands[p % kEngSlots][lane], ((uint64_t)p << 32) | (uint32_t)n);
-            const int dst = 64 * r0 + lane;
-            if (n >= 0) {
-                const int src = rc_find(&rc, n);
-                if (src >= 0) {
-                    rc.row[dst] = rc.row[src];
-                    L.flags[dst] = L.flags[src];
-                    rc.na[dst] = rc.na[src];
-                    rc.s1[dst] = rc.s1[src];
-                } else {
-                    const Row r = load_row_sc1(nc, n);
-                    const uint8_t fl = nc.flags[n];
-                    const int32_t na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
-                    const uint64_t pw[4] = {0, 0, 0, 0};
-                    rc.row[dst] = r;
-                    L.flags[dst] = fl;
-                    rc.na[dst] = na;
-                    rc.s1[dst] = depth1_score(cf, nc, t, c, r, pw, n, na, key64_of(top, a));
-                }
-                for (int w = 0; w < 4; ++w) rc.pw[dst][w] = 0;
+            int src = n >= 0 ? rc_find(&rc, n) : -1;  // a previous pop's candidate, or a package entry
+            if (n >= 0 && src < 0) {  // (every node of the list is one of those: kept for safety)
+                src = 64 * r0 + lane;
+                const Row r = load_row_sc1(nc, n);
+                const int32_t na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+                const uint64_t pw[4] = {0, 0, 0, 0};
+                rc.row[src] = r;
+                L.flags[src] = nc.flags[n];
+                rc.na[src] = na;
+                rc.s1[src] = depth1_score(cf, nc, t, c, r, pw, n, na, key64_of(top, a));
+                for (int w = 0; w < 4; ++w) rc.pw[src][w] = 0;
             }
+            L.srcslot[lane] = src;
             L.xn[r0][lane] = n;
             L.wl64[0][lane] = key64_of(top, a);
+            ETL(A, p, 4);
         }
         __syncthreads();
-        for (int h = threadIdx.x; h < EngRowCache::kHashN; h += kPopThreads) rc.hkey[h] = -1;
-        __syncthreads();
-        if (wave == 0) {
-            const int n = L.xn[r0][lane];
-            if (n >= 0) rc_insert(&rc, n, 64 * r0 + lane);
-        }
-        __syncthreads();
-        // P4: the placement (parallel levels; rows from the cache); wave 0 then
-        // reports, updates the cached rows and writes them back
-        PopOut* out = (PopOut*)((char*)A.out + (size_t)d.slot * sizeof(PopOut));
-        // (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
+        if (wave == 0) ETL(A, p, 5);
+        // P4 (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
         // sends the others to the launched kernels; one instantiation keeps the
         // kernel's registers within one 512-thread block per CU)
         PlaceDec<uint32_t> D;
-        if (place_decide<uint32_t, true>(cf, nc, t, c, a, L.wl64, p, &rc, 0, D))
-            eng_finish(cf, nc, t, c, a, A, L, p, r0, out, D);
-        __syncthreads();
+        if (place_decide<uint32_t, true>(cf, nc, t, c, a, L.wl64, p, &rc, 0, D, L.srcslot)) {
+            ETL(A, p, 6);
+            if (lane == 0 && A.tl) A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 30] = (uint64_t)D.done | ((uint64_t)D.stop << 8);
+            eng_finish(cf, nc, t, c, a, A, L, p, r0, D, &pend);
+        } else if (wave == 5) {  // the results to the host
+            while (__hip_atomic_load(&L.gran_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)p)
+                __builtin_amdgcn_s_sleep(1);
+            PopOut* out = (PopOut*)((char*)A.out + (size_t)d.slot * sizeof(PopOut));
+            const uint64_t g = L.gran[lane];
+            if (lane < 2 && L.gfit[lane]) __hip_atomic_store(&out->fit[lane], L.gfit[lane], __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_SYSTEM);
+            if (g) __hip_atomic_store(&out->g[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            ETL(A, p, 8);
+        } else {
+            eng_front(A, L, p + 1, wave);
+            if (wave == 3) ETL(A, p, 15);
+        }
     }
 }
 
 // ---------------------------------------------------------------------------
 // dispatcher: host ring -> device ring (one wave)
 // ---------------------------------------------------------------------------
-__device__ void eng_dispatch(const EngArgs& A) {
+__device__ __forceinline__ void eng_dispatch(const EngArgs& A) {
     const int lane = threadIdx.x & 63;
     EngCtl* ctl = A.ctl;
     uint32_t s = A.first;
@@ -592,6 +833,7 @@ __device__ void eng_dispatch(const EngArgs& A) {
         uint64_t v = x;
         if (!got) v = lane == kDwFlags ? (((uint64_t)s << 32) | ((uint64_t)kEngOpExit << 12)) : ((uint64_t)s << 32);
         if (lane < 8) st_sc1(&ctl->desc[s % kEngRing][lane], v);
+        ETL(A, s, 28);
         if (op != kEngOpPop) break;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -608,13 +850,15 @@ __global__ __launch_bounds__(kPopThreads) void k_engine(Conf cf, NodeCols nc, De
     } else if (b < A.nw + A.ng) {
         eng_merger(A, lds.m, b - A.nw);
     } else if (b == A.nw + A.ng) {
+        eng_final(cf, nc, t, A, lds.m);
+    } else if (b == A.nw + A.ng + 1) {
         eng_placer(cf, nc, t, A, lds.p);
     } else if (threadIdx.x < 64) {
         eng_dispatch(A);
     }
 }
 
-int engine_grid(const EngArgs& A) { return A.nw + A.ng + 2; }
+int engine_grid(const EngArgs& A) { return A.nw + A.ng + 3; }
 
 hipError_t launch_engine(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A, hipStream_t st) {
     hipLaunchKernelGGL(k_engine, dim3(engine_grid(A)), dim3(kPopThreads), 0, st, cf, nc, t, A);

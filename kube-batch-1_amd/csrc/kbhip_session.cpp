@@ -576,11 +576,14 @@ struct Session {
     int eng_nw_opt = 0;         // option "engine_workers" (0: as many as stay resident)
     DevBuf b_eng;               // EngCtl + the worker and group lists
     EngCtl* d_eng_ctl = nullptr;
+    EngPkg* d_eng_pkg = nullptr;
     uint64_t* d_eng_bl = nullptr;
     uint64_t* d_eng_gl = nullptr;
     uint64_t* h_eng = nullptr;  // pinned, mapped: [kEngHostRing][8] descriptor words, then the exit word
     uint64_t* dv_eng = nullptr; // ... as the device sees it
     size_t h_eng_cap = 0;
+    DevBuf b_eng_tl;            // option "engine_timeline": the engine's event stamps (kEngTlSlots pops)
+    uint64_t* d_eng_tl = nullptr;
     int32_t last_fit[4] = {0, 0, 0, 0};  // FitDelta histogram of the last pop's failing task
     bool last_fit_ok = false;            // ... computed in-kernel (else: fit_sync)
     DevBuf b_fit4;
@@ -659,6 +662,7 @@ struct Session {
     vector<uint8_t> h_shard;                   // host staging of the host all-gather
     // encode-only sessions (kbhip_debug_encode): host copies of the compiled tables
     bool encode_only = false;
+    string broken;  // non-empty: a carry failed part way; every call but close fails with this message
     vector<int32_t> h_dom, h_aff_cnt, h_aff_scalar, h_aff_items;
     int n_spaces = 0;
     size_t n_aff_cnt = 0, n_aff_scalar = 0;  // table sizes (device sessions read them back for tests)
@@ -706,6 +710,8 @@ struct Session {
         h_eng = nullptr;
         dv_eng = nullptr;
         b_eng.release();
+        b_eng_tl.release();
+        d_eng_tl = nullptr;
         eng_nw = 0;
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
         h_rank = nullptr;
@@ -2165,7 +2171,7 @@ static void eng_size(Session& S) {
     HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, S.device));
     HIPCHK(engine_occupancy(&bpc));
     const int resident = cus * bpc;  // every block of the grid must be resident at once
-    int nw = std::min(kEngWorkersMax, resident - kEngMaxGroups - 2);
+    int nw = std::min(kEngWorkersMax, resident - kEngMaxGroups - 3);  // + final merger, placer, dispatcher
     if (S.eng_nw_opt > 0) nw = std::min(nw, S.eng_nw_opt);
     nw = std::min(nw, std::max(1, (N + 63) / 64));  // at least 64 nodes per worker
     if (nw < 1) return;
@@ -2173,10 +2179,12 @@ static void eng_size(Session& S) {
     if (npb > kEngMaxNpb) return;
     const int ng = std::min(kEngMaxGroups, nw);
     const size_t lists = (size_t)kEngSlots * (nw + ng) * kEngListWords;
-    const size_t words = sizeof(EngCtl) / 8 + lists;
+    static_assert(sizeof(EngCtl) % 256 == 0 && sizeof(EngPkg) % 256 == 0, "engine buffers stay line-aligned");
+    const size_t words = (sizeof(EngCtl) + kEngSlots * sizeof(EngPkg)) / 8 + lists;
     char* d = (char*)S.b_eng.alloc<uint64_t>(words);
     S.d_eng_ctl = (EngCtl*)d;
-    S.d_eng_bl = (uint64_t*)(d + sizeof(EngCtl));
+    S.d_eng_pkg = (EngPkg*)(d + sizeof(EngCtl));
+    S.d_eng_bl = (uint64_t*)(d + sizeof(EngCtl) + kEngSlots * sizeof(EngPkg));
     S.d_eng_gl = S.d_eng_bl + (size_t)kEngSlots * nw * kEngListWords;
     HIPCHK(hipMemsetAsync(d, 0, words * 8, S.stream));  // every tag 0: no pop has that sequence number
     if (!S.h_eng) {
@@ -2220,6 +2228,7 @@ static void eng_start(Session& S) {
     A.ctl = S.d_eng_ctl;
     A.blists = S.d_eng_bl;
     A.glists = S.d_eng_gl;
+    A.pkg = S.d_eng_pkg;
     A.hring = S.dv_eng;
     A.hexit = S.dv_eng + kEngHostRing * 8;
     A.out = S.d_out;
@@ -2227,6 +2236,7 @@ static void eng_start(Session& S) {
     A.nw = S.eng_nw;
     A.npb = S.eng_npb;
     A.ng = S.eng_ng;
+    A.tl = S.d_eng_tl;
     HIPCHK(launch_engine(S.conf, S.nc, S.tab, A, S.stream));
     S.eng_running = true;
     S.stats.engine_launches++;
@@ -4544,6 +4554,7 @@ using namespace kbhip;
 // communicator is connected taints it (aborted at close, never pooled).
 #define ABI_GUARD_S(sp, ...)                                 \
     try {                                                    \
+        check_usable(sp);                                    \
         __VA_ARGS__                                          \
     } catch (kbhip::Error & e) {                             \
         kbhip::g_err = e.what();                             \
@@ -4566,6 +4577,9 @@ struct kb_session {
 };
 static void taint_comm(kb_session* s) {
     if (s && s->s.comm) s->s.comm_bad = true;
+}
+static void check_usable(kb_session* s) {
+    if (s && !s->s.broken.empty()) throw kbhip::Error(KBHIP_EINVAL, s->s.broken);
 }
 
 const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
@@ -5284,6 +5298,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         for (int i = 0; i < P && !need_map; ++i) need_map = old_pod[i] < 0 && v.has_node(i);
         if (need_map) find_node("");
         std::atomic<int> bad_pod{-1};
+        std::atomic<bool> spec_changed{false};
         vector<int32_t> pcount(P, 0);
         auto pass = [&](int t, int lo, int hi) {  // the pods' records (kept or decoded), status, node, job
             int32_t* jc = jcnt[t].data();
@@ -5292,6 +5307,14 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
                 const int o = old_pod[i];
                 if (o >= 0) {
                     p = S.pods[o];  // spec-derived fields and session ids (namespace, class) kept
+                    // ... once the cheap spec fields agree: an updated pod the caller mapped by UID
+                    // (updatePod rebuilds its TaskInfo, event_handlers.go:167-184) must not keep a
+                    // stale priority, backfill flag or request (its class): the session re-opens
+                    R3 rq{};
+                    for (int k = v.pco[i]; k < v.pco[i + 1]; ++k) { rq.c += v.ccpu[k]; rq.m += v.cmem[k]; rq.g += v.cgpu[k]; }
+                    if (p.priority != v.ppri[i] || p.ts != v.pts[i] || p.backfill != (!v.pbf.empty() && v.pbf[i]) ||
+                        rq.c != p.req.c || rq.m != p.req.m || rq.g != p.req.g)
+                        spec_changed.store(true, std::memory_order_relaxed);
                 } else {
                     p = HPod{};
                     v.spec(i, p);
@@ -5346,6 +5369,11 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
             throw Error(KBHIP_EINVAL, "pod " + s.s(v.puid[i]) + " is bound to node " + s.s(v.pnode[i]) +
                                           " which is not in the snapshot");
         }
+        if (spec_changed) {  // nothing of the session has changed yet
+            spare_pods().give(pods);
+            reopen_in_place(ks, s);
+            return;
+        }
         for (int i = 0; i < P; ++i)  // namespace ids of new pods (the kept dictionary grows in order)
             if (old_pod[i] < 0) pods[i].ns = S.keep.nss.get(s.s(pns[i]));
         if (!S.pod_port_ids.empty()) {  // kept pods' host ports (none held: every offset stays 0)
@@ -5358,6 +5386,16 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
         }
     }
     mark("pods");
+    // From here the session's own state changes (classes, masks, node rows, then pods and jobs):
+    // a failure part way leaves it unusable (every later call but close fails, kbhip.h)
+    struct BreakOnThrow {
+        Session& S;
+        int pending = std::uncaught_exceptions();
+        ~BreakOnThrow() {
+            if (std::uncaught_exceptions() > pending)
+                S.broken = "kbhip_session_carry_snapshot failed part way: close the session";
+        }
+    } break_on_throw{S};
     {
         // job task lists in pod order, filled by kThreads pod ranges: per-range counts per job
         // give every range its first position in each job's list
@@ -5752,7 +5790,8 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             s->s.speculate = (int)value;
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
-        else if (std::strcmp(key, "engine") == 0 || std::strcmp(key, "engine_workers") == 0) {
+        else if (std::strcmp(key, "engine") == 0 || std::strcmp(key, "engine_workers") == 0 ||
+                 std::strcmp(key, "engine_timeline") == 0) {
             kbhip::Session& S = s->s;
             if (!S.encode_only) {
                 HIPCHK(hipSetDevice(S.device));
@@ -5760,6 +5799,12 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
             if (key[6] == 0) {
                 S.engine = value != 0;
+            } else if (std::strcmp(key, "engine_timeline") == 0) {  // diagnostic: the engine's event stamps
+                const size_t words = (size_t)kbhip::kEngTlSlots * kbhip::kEngTlEvents;
+                if (value && !S.d_eng_tl && !S.encode_only) {
+                    S.d_eng_tl = S.b_eng_tl.alloc<uint64_t>(words);
+                    HIPCHK(hipMemset(S.d_eng_tl, 0, words * 8));
+                }
             } else {
                 if (value < 0 || value > kbhip::kEngWorkersMax) throw kbhip::Error(KBHIP_EINVAL, "engine_workers out of range");
                 S.eng_nw_opt = (int)value;
@@ -6032,6 +6077,13 @@ int64_t kbhip_debug_table(kb_session* s, const char* name, void* out, int64_t ca
             return bytes;
         } else if (n == "dbg_pods") {
             v = S.dbg_pods;
+        } else if (n == "engine_tl") {  // u64 words: kEngTlSlots x kEngTlEvents (option "engine_timeline")
+            if (!S.d_eng_tl) throw kbhip::Error(KBHIP_EINVAL, "set option engine_timeline first");
+            const int64_t bytes = (int64_t)kbhip::kEngTlSlots * kbhip::kEngTlEvents * 8;
+            HIPCHK(hipSetDevice(S.device));
+            kbhip::ov_quiesce(s->s);
+            if (out && cap_bytes >= bytes) HIPCHK(hipMemcpy(out, S.d_eng_tl, (size_t)bytes, hipMemcpyDeviceToHost));
+            return bytes;
         } else if (n == "pod_status" || n == "pod_node") {  // the host model: TaskStatus code / node per pod
             v.resize(S.pods.size());
             for (size_t i = 0; i < S.pods.size(); ++i) v[i] = n == "pod_status" ? S.pods[i].status : S.pods[i].node;

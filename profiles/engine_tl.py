@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""Event timeline of the persistent pop engine (diagnostic; option
+"engine_timeline", kbhip_engine.hip ETL stamps, 100 MHz): one C4 session,
+then per-phase medians over the last kEngTlSlots pops.  Prints one JSON line.
+
+Placer events: 0 iteration start, 1 descriptor, 2 package loaded, 3 drop +
+patch done, 4 list published + rows, 5 placement start, 6 decided, 7 rows
+written (stores issued), 8 granules stored (wave 5).  Final merger: 20
+descriptor, 21 lists merged, 22 package flag.  Workers (blocks 0 and nw/2: 10.. / 16..): descriptor, done(p-3),
+evaluated, list published, counts published.  Merger 0: 24 descriptor, 25
+lists in, 26 group list published, 27 counts.  28: dispatcher forwarded."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+import kbgen  # noqa: E402
+import kbhip  # noqa: E402
+
+SLOTS, EV = 8192, 32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--pending", type=int, default=800_000)
+    ap.add_argument("--workers", type=int, default=0)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    path = f"/tmp/kbhip_bench/c4_{a.nodes}_{a.pending}_{kbgen.BASE_SEED + 4}.kbs"
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        kbgen.gen_c4(path, n_nodes=a.nodes, n_pending=a.pending)
+    buf = open(path, "rb").read()
+    with kbhip.Session(buf) as s:  # warm
+        s.allocate()
+    with kbhip.Session(buf) as s:
+        s.set_option("engine_workers", a.workers)
+        s.set_option("engine_timeline", 1)
+        s.allocate()
+        st = s.stats()
+        raw = np.zeros(SLOTS * EV, np.uint64)
+        n = kbhip.lib().kbhip_debug_table(s._h, b"engine_tl", raw.ctypes.data, raw.nbytes)
+        assert n == raw.nbytes
+    t = raw.reshape(SLOTS, EV).astype(np.int64)
+    pops = t[:, 31]
+    order = np.argsort(pops)
+    t = t[order]
+    pops = pops[order]
+    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 19, 24, 25, 26, 28]] > 0,
+                                 axis=1)
+    t = t[keep]
+    pops = t[:, 31]
+    cont = np.diff(pops) == 1
+    us = lambda x: float(np.median(x)) / 100.0  # 100 MHz ticks -> us
+    res = {"pops": int(len(t)), "stats": {k: st[k] for k in ("engine_pops", "engine_launches", "engine_workers",
+                                                             "alloc_device_s", "batched_pops", "host_wait_s")}}
+    per = {}
+    per["period"] = us(np.diff(t[:, 0])[cont])
+    per["placer 0->3 drop+patch"] = us(t[:, 3] - t[:, 0])
+    per["placer 3->4 final list + rows"] = us(t[:, 4] - t[:, 3])
+    per["placer 4->5 barrier"] = us(t[:, 5] - t[:, 4])
+    per["placer 5->6 decided"] = us(t[:, 6] - t[:, 5])
+    per["placer 6->7 rows written"] = us(t[:, 7] - t[:, 6])
+    per["placer 6->8 granules (wave 5)"] = us(t[:, 8] - t[:, 6])
+    per["placer 5->15 front of next (wave 3, package)"] = us(t[:, 15] - t[:, 5])
+    per["P2 wave0 drop (0->1)"] = us(t[:, 1] - t[:, 0])
+    per["P2 wave1 key dyn_key (0->2)"] = us(t[:, 2] - t[:, 0])
+    per["P2 wave1 sort (2->9)"] = us(t[:, 9] - t[:, 2])
+    per["P2 wave5 s1 dyn_key (0->19)"] = us(t[:, 19] - t[:, 0])
+    per["placer 7 -> next 0"] = us((t[1:, 0] - t[:-1, 7])[cont])
+    # when do the lists of pop p arrive, relative to the placer's start of pop p
+    fin = np.all(t[:, [20, 21, 22]] > 0, axis=1)
+    if fin.any():
+        per["final: package flag (22) - placer start (0)"] = us((t[:, 22] - t[:, 0])[fin])
+        per["final: desc(20)->merged(21)"] = us((t[:, 21] - t[:, 20])[fin])
+        per["final: merged(21)->flag(22)"] = us((t[:, 22] - t[:, 21])[fin])
+    per["merger0 published (26) - placer start (0)"] = us(t[:, 26] - t[:, 0])
+    per["merger0 lists in (25) - placer start (0)"] = us(t[:, 25] - t[:, 0])
+    per["worker0 published (13) - placer start (0)"] = us(t[:, 13] - t[:, 0])
+    per["worker0 desc(10)->done(11)"] = us(t[:, 11] - t[:, 10])
+    per["worker0 done(11)->eval(12)"] = us(t[:, 12] - t[:, 11])
+    per["worker0 eval(12)->pub(13)"] = us(t[:, 13] - t[:, 12])
+    per["worker0 pub(13)->counts(14)"] = us(t[:, 14] - t[:, 13])
+    per["worker0 counts(14) -> next desc(10)"] = us((t[1:, 10] - t[:-1, 14])[cont])
+    per["worker0 desc(p) - placer done(p-3)"] = us((t[3:, 10] - t[:-3, 7])[np.diff(pops, 3) == 3])
+    per["worker0 done-seen(11,p) - placer done(7,p-3)"] = us((t[3:, 11] - t[:-3, 7])[np.diff(pops, 3) == 3])
+    per["merger0 desc(24)->lists in(25)"] = us(t[:, 25] - t[:, 24])
+    per["merger0 lists in(25)->pub(26)"] = us(t[:, 26] - t[:, 25])
+    per["merger0 pub(26)->counts(27)"] = us(t[:, 27] - t[:, 26])
+    per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
+    res["median_us"] = {k: round(v, 3) for k, v in per.items()}
+    stop = (t[:, 30] >> 8) & 0xff
+    res["stop_hist"] = {int(k): int(v) for k, v in zip(*np.unique(stop, return_counts=True))}
+    dec = (t[:, 6] - t[:, 5]) / 100.0
+    res["decide_us_quantiles"] = [round(float(np.quantile(dec, q)), 2) for q in (0.1, 0.25, 0.5, 0.75, 0.9, 0.99)]
+    print(json.dumps(res))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -170,3 +170,37 @@ def test_carry_snapshot_rejects_bad_maps(engine, kbgen_mod, tmp_path):
             with pytest.raises(engine.KbhipError):
                 s.carry_snapshot(p, op, on)
         assert s.carry_snapshot(p, np.arange(P, dtype=np.int32), np.arange(N, dtype=np.int32)) >= 0
+
+
+@pytest.mark.parametrize("field", ["priority", "request", "backfill"])
+def test_carry_snapshot_updated_pod_mapped(engine, kbgen_mod, tmp_path, field):
+    """A pending pod updated between the sessions (updatePod rebuilds its
+    TaskInfo, event_handlers.go:167-184) but mapped by UID: the carry must not
+    keep its old priority, request or backfill flag — the next
+    session schedules exactly like one opened fresh on the new snapshot."""
+    c = kbgen_mod.gen_random(9601, n_nodes=10, n_jobs=10, max_tasks=6, features=NO_POD_AFFINITY)
+    if "default" not in {q.name for q in c.queues}:
+        c.add_queue("default")
+    p1 = c.write(str(tmp_path / "s1.kbs"))
+    old_pods = sorted(c.pods, key=lambda q: q.uid)
+    old_nodes = sorted(n.name for n in c.nodes)
+    with engine.Session(p1) as s:
+        s.allocate()
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+        c2 = snapshot_after_session(clone(c), status, node)
+        pending = [q for q in sorted(c2.pods, key=lambda q: q.uid) if q.node is None and q.phase == "Pending"]
+        assert pending
+        for q in pending[:3]:
+            if field == "priority":
+                q.priority += 100
+            elif field == "request":
+                q.containers = [dict(q.containers[0], cpu=int(q.containers[0].get("cpu", 100)) + 1000)]
+            else:
+                q.backfill = not q.backfill
+        op, on = index_maps(old_pods, old_nodes, c2)
+        p2 = c2.write(str(tmp_path / "s2.kbs"))
+        s.carry_snapshot(p2, op, on)
+        got = s.allocate()
+    with engine.Session(p2) as f:
+        exp = f.allocate()
+    assert all(np.array_equal(a, b) for a, b in zip(got, exp))
