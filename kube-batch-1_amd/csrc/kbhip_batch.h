@@ -178,6 +178,24 @@ __device__ __forceinline__ void wave_merge128_desc(T& a0, T& a1, T b0, T b1) {
     a0 = bitonic_clean_desc(c0 > c1 ? c0 : c1);
     a1 = bitonic_clean_desc(c0 > c1 ? c1 : c0);
 }
+// Top 256 of two descending 256-lists (a[k] holds ranks 64k .. 64k + 63):
+// c[i] = max(a[i], b[255 - i]) is bitonic; half-cleaners at distances 128
+// and 64 (between registers), then each register is cleaned.
+template <typename T>
+__device__ __forceinline__ void wave_merge256_desc(T* a, const T* b) {
+    T c[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const T r = reverse_lanes(b[3 - k]);
+        c[k] = a[k] > r ? a[k] : r;
+    }
+    const T x0 = c[0] > c[2] ? c[0] : c[2], x2 = c[0] > c[2] ? c[2] : c[0];
+    const T x1 = c[1] > c[3] ? c[1] : c[3], x3 = c[1] > c[3] ? c[3] : c[1];
+    a[0] = bitonic_clean_desc(x0 > x1 ? x0 : x1);
+    a[1] = bitonic_clean_desc(x0 > x1 ? x1 : x0);
+    a[2] = bitonic_clean_desc(x2 > x3 ? x2 : x3);
+    a[3] = bitonic_clean_desc(x2 > x3 ? x3 : x2);
+}
 
 // Results land in pinned host memory as self-tagged 8-byte granules, one per
 // consumed task, each written by ONE 8-byte store (no fence needed: the host
@@ -568,6 +586,66 @@ __device__ __forceinline__ Row place_row(const TaskClass& c, const PlaceDec<ET>&
     return apply_commits(D.base, c, na, D.cc - na);
 }
 
+// The end of a placement decision (wave 0): the stop rule over the placement
+// order (allocate.go:187-195, gang.go:63-66), the commits per candidate, the
+// decision into D.  Position p holds entry L of candidate lane lf with commit
+// kind `kind`; fast: position p is candidate p (else cnt[64], zeroed, counts).
+template <typename ET, bool SC1>
+__device__ __forceinline__ bool place_tail(const PopArgs& a, uint64_t t0, bool fast, ET L, bool inm, int lf, int kind,
+                                           int ap_l, int32_t* cnt, const Row& base, const uint64_t* pw,
+                                           const uint64_t* pwc, int32_t na_n, int n, uint32_t seq, PlaceDec<ET>& D) {
+    const int lane = threadIdx.x & 63;
+    const int m = a.n_tasks;
+    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int ready_p = a.ready_count + __popcll(amask & upto);
+    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
+    int cap = m;  // positions decided exactly (a prefix: the entries are sorted)
+    if (t0) {
+        const int32_t s0 = key_score(t0);
+        const int i0 = key_idx(t0);
+        const int32_t rm = inm ? entry_rm<ET>(L, a) : 0;
+        const bool ex = inm && (rm > s0 || (rm == s0 && entry_node(L, a) <= i0));
+        cap = __popcll(__ballot(ex && lane < m));
+    }
+    int done, stop;
+    const int p0 = smask ? __ffsll((unsigned long long)smask) - 1 : 64;
+    if (p0 < cap) {
+        done = p0 + 1;
+        stop = __builtin_amdgcn_readlane((int)inm, p0) ? 2 : 1;
+    } else {
+        done = cap;  // cap == m: every task placed, the pop goes on (stop 0)
+        stop = 0;
+    }
+    STAMP(gridDim.x * 4 + 8);
+    int cc;
+    if (fast) {  // position p is candidate p, once
+        cc = lane < done ? 1 : 0;
+    } else {
+        if (lane < done && inm) atomicAdd(&cnt[lf], 1);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
+        __builtin_amdgcn_wave_barrier();
+        cc = cnt[lane];
+    }
+    STAMP(gridDim.x * 4 + 9);
+    if constexpr (SC1) {
+        if (lane == 0) { TL(seq, 7); TL_VAL(seq, 9, fast ? 1 : 2); TL_VAL(seq, 10, (uint64_t)done); }
+    }
+    D.n = n;
+    D.base = base;
+    for (int w = 0; w < 4; ++w) { D.pw[w] = pw[w]; D.pwc[w] = pwc[w]; }
+    D.na_n = na_n;
+    D.L = L;
+    D.inm = inm;
+    D.lf = lf;
+    D.kind = kind;
+    D.cc = cc;
+    D.ap_l = ap_l;
+    D.done = done;
+    D.stop = stop;
+    return true;
+}
+
 // The parallel-levels decision (every wave calls; true on wave 0, which holds
 // the result — the other waves return false after their last barrier).
 // t0 (a cut): the candidates are exact down to the selection key t0 only
@@ -576,7 +654,9 @@ __device__ __forceinline__ Row place_row(const TaskClass& c, const PlaceDec<ET>&
 // (stop 0 with done < m; done 0 when none).
 // Node indices in keys and entries are global.
 // rc_slots (LDS, optional): candidate j's row is in row-cache slot rc_slots[j] (no lookup).
-template <typename ET, bool SC1, typename RC>
+// CACHED (the persistent engine): every candidate's row is in the cache and
+// read from there where it is used (not held in registers); no host ports.
+template <typename ET, bool SC1, typename RC, bool CACHED = false>
 __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                              const PopArgs& a, uint64_t (*wl64)[64], uint32_t seq, const RC* rc,
                                              uint64_t t0, PlaceDec<ET>& D, const int32_t* rc_slots = nullptr) {
@@ -599,7 +679,9 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
     uint64_t pw[4] = {0, 0, 0, 0};
     int32_t na_n = 0;
     const int rslot = (rc && n >= 0) ? (rc_slots ? rc_slots[lane] : rc_find(rc, n)) : -1;
-    if (rslot >= 0) {
+    if constexpr (CACHED) {
+        if (rslot >= 0) na_n = rc->na[rslot];
+    } else if (rslot >= 0) {
         base = rc->row[rslot];
         for (int w = 0; w < 4; ++w) pw[w] = rc->pw[rslot][w];
         na_n = rc->na[rslot];
@@ -609,9 +691,14 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
             for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = load_port_t<SC1>(nc, c.pw_lo + w, n);
         if (cf.score_mult) na_n = na_weight(c, t, nc, n);
     }
+    auto base_row = [&]() -> Row {
+        if constexpr (CACHED) return rslot >= 0 ? rc->row[rslot] : Row{};
+        else return base;
+    };
     STAMP(gridDim.x * 4 + 11);
     uint64_t pwc[4];
-    for (int w = 0; w < 4; ++w) pwc[w] = pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
+    for (int w = 0; w < 4; ++w)
+        pwc[w] = CACHED ? 0 : pw[w] | ((c.has_ports && w < port_win(c, nc)) ? t.masks[c.pown_off + w] : 0);
     const int m = a.n_tasks;
     // Fast path (no second commit reaches the chunk): T0 = the m-th depth-0
     // entry.  A second entry of any candidate is its running minimum after one
@@ -635,7 +722,7 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
                     s1d = rc->s1[rslot];
                 } else {
                     const int na = ap0 == 0 ? 0 : 1;
-                    const Row r1 = apply_commits(base, c, na, 1 - na);
+                    const Row r1 = apply_commits(base_row(), c, na, 1 - na);
                     int32_t s1;
                     bool passed1;
                     const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pwc, n, true, na_n, &s1, &passed1);
@@ -660,7 +747,7 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
         if (threadIdx.x == 0) TL(seq, 15);
     }
     ET L = 0;            // wave 0: merged top-64 entries so far (lane p = entry p)
-    int lf = 0, kind = 0, cc = 0, ap_l = 64;
+    int lf = 0, kind = 0, ap_l = 64;
     bool inm = false;
     if (fast) {
         if (wave != 0) return false;
@@ -681,7 +768,7 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
     auto eval_at = [&](int d, int ap, int32_t* sc) -> int {  // kind of commit d+1's key (0: infeasible)
         if (d == 0) { *sc = key_score(K); return key_kind(K); }
         const int na = d < ap ? d : ap;
-        const Row r = apply_commits(base, c, na, d - na);
+        const Row r = apply_commits(base_row(), c, na, d - na);
         int32_t s;
         bool passed;
         const uint64_t k = dyn_key(cf, c, t, nc, r, pwc, n, true, na_n, &s, &passed);
@@ -752,53 +839,162 @@ __device__ __forceinline__ bool place_decide(const Conf& cf, const NodeCols& nc,
     kind = inm ? s_kind[entry_depth(L)][lf] : 0;
     ap_l = s_apos[lane];
     }  // slow path
-    // stop rule over the placement order (allocate.go:187-195, gang.go:63-66)
-    const uint64_t amask = __ballot(inm && kind == 1);  // Pipelined is not an AllocatedStatus
-    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-    const int ready_p = a.ready_count + __popcll(amask & upto);
-    const uint64_t smask = __ballot(lane < m && (!inm || !a.gang_mode || ready_p >= a.min_avail));
-    int cap = m;  // positions decided exactly (a prefix: the entries are sorted)
-    if (t0) {
-        const int32_t s0 = key_score(t0);
-        const int i0 = key_idx(t0);
-        const int32_t rm = inm ? entry_rm<ET>(L, a) : 0;
-        const bool ex = inm && (rm > s0 || (rm == s0 && entry_node(L, a) <= i0));
-        cap = __popcll(__ballot(ex && lane < m));
+    return place_tail<ET, SC1>(a, t0, fast, L, inm, lf, kind, ap_l, s_cnt, base_row(), pw, pwc, na_n, n, seq, D);
+}
+
+// The decision on wave 0 alone, with no block barrier (the other waves go on
+// with other work): the fast path, or the levels on one wave.  Only the
+// candidates whose second entry reaches the chunk (set R, see the fast path
+// in place_decide) can place more than once; their deeper entries are
+// computed in rounds, lane = (member r, one of Dd = 64 / |members| depths,
+// rounded to powers of two, following the member's deepest so far), merged
+// into the placement order L; a member stays for the next round while its
+// deepest entry still reaches the m-th position.  The same entries, commit
+// kinds and order as the levels over all waves.  every_member (a test mode):
+// every feasible candidate in R, no fast path.  Every candidate's row is in
+// the row cache (slot rc_slots[j]); no cut (t0 = 0); no host ports (false:
+// nothing decided).
+template <typename ET, bool SC1, typename RC>
+__device__ __forceinline__ bool place_decide_wave(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                                  const TaskClass& c, const PopArgs& a, const uint64_t* K0,
+                                                  uint32_t seq, const RC* rc, const int32_t* rc_slots,
+                                                  bool every_member, PlaceDec<ET>& D) {
+    __shared__ uint8_t q_kind[64][64];  // [depth][candidate]: 1 Allocate, 2 Pipeline, 0 infeasible
+    __shared__ int32_t q_rl[64];        // this round's members, in list order
+    __shared__ int32_t q_cnt[64], q_apos[64], q_rm[64], q_dl[64];
+    __shared__ uint8_t q_alive[64];
+    __shared__ int32_t q_hkey[kHash], q_hlane[kHash];
+    const int lane = threadIdx.x & 63;
+    if (c.has_ports) return false;  // (host-port words: the levels over all waves)
+    const uint64_t K = K0[lane];
+    const int n = K ? key_idx(K) : -1;
+    const int rslot = n >= 0 ? rc_slots[lane] : -1;
+    const int32_t s1d = rslot >= 0 ? rc->s1[rslot] : INT32_MIN;
+    const uint64_t pw[4] = {0, 0, 0, 0};
+    auto tail = [&](bool fast, ET L, bool inm, int lf, int kind, int ap_l) {
+        Row base{};  // (loaded here: not live across the evaluation)
+        int32_t na_n = 0;
+        if (rslot >= 0) {
+            base = rc->row[rslot];
+            na_n = rc->na[rslot];
+        }
+        return place_tail<ET, SC1>(a, 0, fast, L, inm, lf, kind, ap_l, q_cnt, base, pw, pw, na_n, n, seq, D);
+    };
+    const int m = a.n_tasks;
+    const uint64_t Km = m >= 1 && m <= 64 ? readlane64(K, m - 1) : 0;
+    bool reach = false;  // (with fewer than m feasible candidates every second entry counts)
+    if (K && (lane < m || !Km || every_member) && s1d != INT32_MIN) {
+        if (!Km || every_member) {
+            reach = true;
+        } else {
+            const int32_t s0 = key_score(K), sm = key_score(Km);
+            const int32_t rm = s1d < s0 ? s1d : s0;
+            reach = rm > sm || (rm == sm && n < key_idx(Km));
+        }
     }
-    int done, stop;
-    const int p0 = smask ? __ffsll((unsigned long long)smask) - 1 : 64;
-    if (p0 < cap) {
-        done = p0 + 1;
-        stop = __builtin_amdgcn_readlane((int)inm, p0) ? 2 : 1;
-    } else {
-        done = cap;  // cap == m: every task placed, the pop goes on (stop 0)
-        stop = 0;
+    uint64_t alive = __ballot(reach);
+    const int ap_own = K && key_kind(K) == 2 ? 0 : 64;
+    if (Km && !alive && !every_member) {  // the first m candidates once each, in list order
+        const bool inm = lane < m;
+        const ET L = inm ? depth_entry<ET>(key_score(K), n, 0, a) : (ET)0;
+        return tail(true, L, inm, lane, inm ? key_kind(K) : 0, ap_own);
     }
-    STAMP(gridDim.x * 4 + 8);
-    if (fast) {  // position p is candidate p, once
-        cc = lane < done ? 1 : 0;
-    } else {
-        if (lane < done && inm) atomicAdd(&s_cnt[lf], 1);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds of this wave
+    q_cnt[lane] = 0;
+    q_apos[lane] = ap_own;
+    q_rm[lane] = K ? key_score(K) : 0;
+    q_dl[lane] = 0;
+    q_kind[0][lane] = K ? (uint8_t)key_kind(K) : (uint8_t)0;
+    for (int h = lane; h < kHash; h += 64) q_hkey[h] = -1;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (n >= 0) {  // node -> candidate lane (candidate nodes are distinct)
+        int h = hash_slot(n);
+        while (atomicCAS(&q_hkey[h], -1, n) != -1) h = (h + 1) & (kHash - 1);
+        q_hlane[h] = lane;
+    }
+    ET L = K ? depth_entry<ET>(key_score(K), n, 0, a) : (ET)0;  // the depth-0 entries (list order)
+    while (alive) {
+        const int k = __popcll(alive);
+        const int lk = k <= 1 ? 0 : k <= 2 ? 1 : k <= 4 ? 2 : k <= 8 ? 3 : k <= 16 ? 4 : k <= 32 ? 5 : 6;
+        const int Dd = 64 >> lk;  // depths per member this round
+        if ((alive >> lane) & 1)
+            q_rl[__builtin_amdgcn_mbcnt_hi((uint32_t)(alive >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)alive, 0))] = lane;
+        q_alive[lane] = 0;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        cc = s_cnt[lane];
+        const int seg = lane >> (6 - lk), off = lane & (Dd - 1);
+        int j = seg < k ? q_rl[seg] : -1;
+        const int dl = j >= 0 ? q_dl[j] : 0;
+        const int d = dl + 1 + off;
+        const int lastoff = (Dd < 63 - dl ? Dd : 63 - dl) - 1;  // the member's deepest lane (depth 63 at most)
+        if (off > lastoff) j = -1;
+        Row bj{};
+        int32_t naj = 0, rm0 = 0;
+        int nj = -1, apj = 64;
+        if (j >= 0) {
+            const int sl = rc_slots[j];
+            nj = key_idx(K0[j]);
+            bj = rc->row[sl];
+            naj = rc->na[sl];
+            rm0 = q_rm[j];
+            apj = q_apos[j];
+        }
+        auto eval_at = [&](int dd, int ap, int32_t* sc) -> int {  // kind of commit dd+1's key (0: infeasible)
+            const int na = dd < ap ? dd : ap;
+            const Row r = apply_commits(bj, c, na, dd - na);
+            int32_t s = 0;
+            bool passed;
+            const uint64_t kk = dyn_key(cf, c, t, nc, r, pw, nj, true, naj, &s, &passed);
+            *sc = kk ? key_score(kk) : 0;
+            return kk ? key_kind(kk) : 0;
+        };
+        int32_t sc = 0;
+        int kd = j >= 0 ? eval_at(d, apj, &sc) : 0;
+        // the member's first Pipeline depth; the depths behind it, assumed Allocates: again
+        int ap = (j >= 0 && kd == 2) ? d : 64;
+        for (int o = 1; o < Dd; o <<= 1) {
+            const int x = __shfl_xor(ap, o, 64);
+            ap = x < ap ? x : ap;
+        }
+        ap = apj < ap ? apj : ap;
+        const bool redo = j >= 0 && apj == 64 && d > ap;
+        if (__ballot(redo) != 0 && redo) kd = eval_at(d, ap, &sc);
+        // entries: running minimum through depth d; the chain ends at the first infeasible depth
+        bool ok = j >= 0 && kd != 0;
+        int32_t rm = sc;
+        for (int o = 1; o < Dd; o <<= 1) {
+            const int32_t x = __shfl_up(rm, o, 64);
+            const int y = __shfl_up((int)ok, o, 64);
+            if (off >= o) {
+                rm = x < rm ? x : rm;
+                ok = ok && y;
+            }
+        }
+        rm = rm0 < rm ? rm0 : rm;
+        const ET e = ok ? depth_entry<ET>(rm, nj, d, a) : (ET)0;
+        if (j >= 0) q_kind[d][j] = (uint8_t)kd;
+        L = wave_merge_desc(L, wave_sort_desc(e));
+        const ET T = readlane_t(L, m - 1);  // the m-th entry (0: fewer entries than tasks)
+        if (j >= 0 && off == lastoff) {
+            q_rm[j] = rm;
+            q_dl[j] = d;
+            q_apos[j] = ap;
+            q_alive[j] = (e != 0 && e >= T && d < 63) ? 1 : 0;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        alive = __ballot(q_alive[lane] != 0);
     }
-    STAMP(gridDim.x * 4 + 9);
-    if constexpr (SC1) {
-        if (lane == 0) { TL(seq, 7); TL_VAL(seq, 9, fast ? 1 : 2); TL_VAL(seq, 10, (uint64_t)done); }
+    const bool inm = lane < m && L != 0;
+    int lf = 0;
+    if (inm) {
+        const int ni = entry_node(L, a);
+        int h = hash_slot(ni);
+        while (q_hkey[h] != ni) h = (h + 1) & (kHash - 1);
+        lf = q_hlane[h];
     }
-    D.base = base;
-    for (int w = 0; w < 4; ++w) { D.pw[w] = pw[w]; D.pwc[w] = pwc[w]; }
-    D.na_n = na_n;
-    D.L = L;
-    D.inm = inm;
-    D.lf = lf;
-    D.kind = kind;
-    D.cc = cc;
-    D.ap_l = ap_l;
-    D.done = done;
-    D.stop = stop;
-    return true;
+    const int kind = inm ? q_kind[entry_depth(L)][lf] : 0;
+    return tail(false, L, inm, lf, kind, q_apos[lane]);
 }
 
 // The walk FitDelta histogram of a task that found no node (D.stop == 1):

@@ -61,7 +61,7 @@ struct EngCtl {
     uint64_t desc[kEngRing][8];     // descriptors, slot seq % kEngRing
     uint64_t cands[kEngSlots][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}
 };
-enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2 };
+enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3 };
 
 // Kernel arguments beyond the session's tables.
 struct EngArgs {
@@ -75,6 +75,7 @@ struct EngArgs {
     uint32_t first;            // the first pop of this launch (earlier pops are written back)
     int nw, npb, ng;           // workers, nodes per worker, merger groups
     uint64_t* tl;              // diagnostic event timeline (option "engine_timeline"), or null
+    int quick;                 // 0 (a test mode): no fast path, every feasible candidate through the levels rounds
 };
 // Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
 constexpr int kEngTlSlots = 8192, kEngTlEvents = 32;

@@ -55,18 +55,13 @@ struct EngWait {
     }
 };
 
-// Every dword of v through readfirstlane: a wave-uniform value held in scalar
-// registers (a TaskClass read from LDS or global memory: otherwise every
-// field access in the evaluation functions is a dependent memory round trip).
-template <typename T>
-__device__ __forceinline__ T eng_uniform(const T& v) {
-    static_assert(sizeof(T) % 4 == 0, "dwords");
-    T r;
-    const uint32_t* s = (const uint32_t*)&v;
-    uint32_t* d = (uint32_t*)&r;
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[i]);
-    return r;
+// The lane index through an opaque move: addresses derived from it are
+// computed where they are used instead of being hoisted out of the role
+// loops and held (or spilled) for the kernel's lifetime.
+__device__ __forceinline__ int eng_lane() {
+    int l;
+    asm volatile("v_and_b32 %0, 63, %1" : "=v"(l) : "v"((int)threadIdx.x));
+    return l;
 }
 
 // The pop's descriptor as a block sees it (from the device ring).
@@ -166,6 +161,27 @@ __device__ __forceinline__ void block_merge128_all(T (*w0)[64], T (*w1)[64], T a
     }
 }
 
+// Top 256 of the 8 waves' descending 256-lists (a[k]: ranks 64k .. 64k + 63);
+// the result in wl[k][0] (every wave calls).
+__device__ __forceinline__ void block_merge256_all(uint32_t (*wl)[kPopThreads / 64][64], const uint32_t* a, int wave,
+                                                   int lane) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wl[k][wave][lane] = a[k];
+    __syncthreads();
+#pragma unroll
+    for (int s = kPopThreads / 128; s >= 1; s >>= 1) {
+        if (wave < s) {
+            uint32_t x[4], y[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { x[k] = wl[k][wave][lane]; y[k] = wl[k][wave + s][lane]; }
+            wave_merge256_desc(x, y);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) wl[k][wave][lane] = x[k];
+        }
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
     x += __shfl_xor(x, 1, 64);
     x += __shfl_xor(x, 2, 64);
@@ -196,11 +212,12 @@ __device__ __forceinline__ uint64_t eng_eval(const Conf& cf, const TaskClass& c,
 // LDS of the roles (one union: the kernel's footprint is the largest role's)
 // ---------------------------------------------------------------------------
 struct EngWorkerLds {
-    uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
-    uint32_t skip[kEngMaxNpb / 32];
-    uint8_t fb[kEngMaxNpb];
+    uint32_t wl[4][kPopThreads / 64][64];  // per-wave top-256 lists (register k of wave w in wl[k][w])
+    uint32_t out[128];                     // the published top 128 (late exclusion)
+    uint32_t skip[kEngMaxNpb / 32];        // pop p-3's (then also p-2's) candidates among this block's nodes
+    uint8_t fb[2][kEngMaxNpb];             // FitDelta bits of pops p (p % 2) and p-1
     uint32_t desc[8];
-    uint32_t fitb[4];
+    uint32_t fitb[2][4];                   // FitDelta counts of pops p (p % 2) and p-1
     int ok;
 };
 struct EngMergerLds {
@@ -220,10 +237,14 @@ struct EngPlacerLds {
     uint64_t wl64[kPopThreads / 64][64];
     uint32_t pkey[2][kEngPkgN];  // pop q's package keys (q % 2)
     uint32_t s64[64];            // the merged list without pop p-1's candidates
-    uint32_t e[2][64];           // re-evaluated keys of pops p-1 / p-2's candidates (sorted)
-    int32_t s1a[2][64], s1p[2][64];  // ... their depth-1 scores after an Allocate / a Pipeline
-    uint8_t fbp[2][64];
-    uint8_t x2use[64];
+    uint32_t e[3][64];           // re-evaluated keys of pops p-1 / p-2 / p-3's candidates (sorted)
+    int32_t s1a[64], s1p[64];    // pop p-1's candidates: depth-1 scores after an Allocate / a Pipeline
+    uint8_t fbp[3][64];          // FitDelta bits of the three sets
+    // the front's evaluation of pops p-2 / p-3's candidates (set 0 / 1, by ring lane)
+    uint32_t fe[2][64];
+    uint8_t fkind[2][64], ffb[2][64];
+    int32_t fna[2][64], fs1a[2][64], fs1p[2][64];
+    uint8_t x2use[64], x3use[64];  // pop p-2's candidate not p-1's; pop p-3's neither
     int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
     uint32_t desc[2][8];         // pop q's descriptor (q % 2)
@@ -232,7 +253,7 @@ struct EngPlacerLds {
     uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
     int gran_seq;                // the pop whose granules are in gran / gfit
-    int s1_ready[2];             // P2: depth-1 score waves done (per candidate set; 2 = both kinds)
+    int s1_ready;                // P2: depth-1 score waves done (2 = both kinds)
 };
 union EngLds {
     EngWorkerLds w;
@@ -243,6 +264,40 @@ union EngLds {
 // ---------------------------------------------------------------------------
 // worker
 // ---------------------------------------------------------------------------
+// Pop p's FitDelta counts leave out pops p-3 (not evaluated), p-2 and p-1's
+// candidates (the placer counts those on their final rows): pop p-1's
+// candidates are known one pop later, so pop p publishes pop p-1's counts.
+// Wave 0: subtract the bits of this block's nodes among pop q's candidates
+// (node, one per lane) from counts set `set` (zeroing them: a node of two
+// such pops leaves the counts once).
+__device__ __forceinline__ void eng_fit_drop(EngWorkerLds& L, int set, int node, int lo, int cnt) {
+    const int lane = threadIdx.x & 63;
+    const int o = node - lo;
+    const bool own = node >= 0 && o >= 0 && o < cnt;
+    uint32_t fb = 0;
+    if (own) {
+        fb = L.fb[set][o];
+        L.fb[set][o] = 0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int k = __popcll(__ballot((fb >> q) & 1u));
+        if (lane == q && k) atomicSub(&L.fitb[set][q], (uint32_t)k);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+// Wave 0: publish pop q's FitDelta counts (two 16-bit counts per word).
+__device__ __forceinline__ void eng_fit_publish(const EngArgs& A, EngWorkerLds& L, uint32_t q, int b) {
+    const int lane = threadIdx.x & 63;
+    uint64_t* dst = A.blists + ((size_t)(q % kEngSlots) * A.nw + b) * kEngListWords;
+    const int set = (int)(q % 2);
+    if (lane < 2) {
+        const uint32_t v = (L.fitb[set][2 * lane] & 0xffff) | (L.fitb[set][2 * lane + 1] << 16);
+        st_sc1(&dst[128 + lane], ((uint64_t)q << 32) | v);
+    }
+}
+
 __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                            EngWorkerLds& L, int b) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -251,24 +306,32 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
     const int cnt = nc.n - lo < A.npb ? (nc.n - lo > 0 ? nc.n - lo : 0) : A.npb;
     if (threadIdx.x == 0) L.ok = 1;
     for (uint32_t p = A.first;; ++p) {
-        // 1. the pop's descriptor; the node rows as pop p-3 left them; pop p-2's candidates
+        const int set = (int)(p % 2), pset = 1 - set;
+        // 1. the pop's descriptor; the node rows as pop p-4 left them; pop p-3's candidates
         for (int i = threadIdx.x; i < (cnt + 31) / 32; i += kPopThreads) L.skip[i] = 0;
         __syncthreads();  // the previous pop done (wave 0 cleared L.ok if it failed)
         if (!L.ok) return;
-        if (threadIdx.x < 4) L.fitb[threadIdx.x] = 0;
+        if (threadIdx.x < 4) L.fitb[set][threadIdx.x] = 0;
         const int tb = b == 0 ? 10 : -1;  // timeline: worker 0
         if (wave == 0) {
             bool ok = eng_wait_desc(ctl, p, L.desc);
             if (tb >= 0) ETL(A, p, tb);
             const EngDesc d0 = eng_decode(L.desc);  // (LDS written by this wave, in order)
             if (ok && d0.op == kEngOpPop) {
-                if (p >= A.first + 3) ok = eng_wait_done(ctl, p - 3);
+                if (p >= A.first + 4) ok = eng_wait_done(ctl, p - 4);
                 if (tb >= 0) ETL(A, p, tb + 1);
-                if (ok && p >= A.first + 2) {
+                if (ok && p >= A.first + 3) {
                     int node = -1;
-                    ok = eng_wait_cands(ctl, p - 2, &node);
+                    ok = eng_wait_cands(ctl, p - 3, &node);
                     const int o = node - lo;
                     if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
+                }
+            } else if (ok && p >= A.first + 1) {  // the run ends: the last pop's counts
+                int node = -1;
+                if (p >= A.first + 2) ok = eng_wait_cands(ctl, p - 2, &node);
+                if (ok) {
+                    eng_fit_drop(L, pset, node, lo, cnt);
+                    eng_fit_publish(A, L, p - 1, b);
                 }
             }
             if (lane == 0) L.ok = ok;
@@ -279,47 +342,68 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
         if (d.op != kEngOpPop) return;
         const PopArgs a = eng_args(d);
         const TaskClass& c = t.classes[__builtin_amdgcn_readfirstlane((int)d.cls)];
-        // 2. evaluate, one node per thread and chunk; each wave keeps its top 128
-        uint32_t a0 = 0, a1 = 0;
+        // 2. evaluate, one node per thread and chunk; each wave keeps its top 256
+        uint32_t al[4] = {0, 0, 0, 0};
         for (int base = 0; base < cnt; base += kPopThreads) {
             const int o = base + (int)threadIdx.x;
             uint32_t k = 0, fb = 0;
             if (o < cnt && !((L.skip[o >> 5] >> (o & 31)) & 1u)) k = sweep_key<uint32_t>(eng_eval(cf, c, t, nc, lo + o, &fb), a);
-            if (o < cnt) L.fb[o] = (uint8_t)fb;
-            fit_block_add(L.fitb, fb);
+            if (o < cnt) L.fb[set][o] = (uint8_t)fb;
+            fit_block_add(L.fitb[set], fb);
             const uint32_t ks = wave_sort_desc(k);
-            if (base == 0) a0 = ks;
-            else wave_merge128_desc(a0, a1, ks, 0u);
+            if (base == 0) {
+                al[0] = ks;
+            } else {
+                const uint32_t bl[4] = {ks, 0u, 0u, 0u};
+                wave_merge256_desc(al, bl);
+            }
         }
         if (tb >= 0 && wave == 0) ETL(A, p, tb + 2);
-        block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
-        // 3. publish the block's top 128 (wave 0), then its FitDelta counts
-        // without pop p-1's candidates (their rows may be in flight: the
-        // placer counts them on their final rows)
+        block_merge256_all(L.wl, al, wave, lane);
+        // 3. pop p-2's candidates (their rows may be in flight; the placer
+        // evaluates them): out of the list — the top 256 keeps at least 192
+        // others, so its first 128 remaining are the top 128 without them —
+        // and out of pop p's counts; publish (wave 0).  Then out of pop p-1's
+        // counts, which are complete now.
         if (wave == 0) {
-            uint64_t* dst = A.blists + ((size_t)(p % kEngSlots) * A.nw + b) * kEngListWords;
-            st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
-            st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
-            if (tb >= 0) ETL(A, p, tb + 3);
             bool ok = true;
-            if (p >= A.first + 1) {
-                int node = -1;
-                ok = eng_wait_cands(ctl, p - 1, &node);
+            int node = -1;
+            if (p >= A.first + 2) {
+                ok = eng_wait_cands(ctl, p - 2, &node);
                 const int o = node - lo;
-                const uint32_t fb = (ok && node >= 0 && o >= 0 && o < cnt) ? L.fb[o] : 0u;  // 0 if skipped
+                if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
+                if (ok) eng_fit_drop(L, set, node, lo, cnt);
+            }
+            int run = 0;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int k = __popcll(__ballot((fb >> q) & 1u));
-                    if (lane == q && k) atomicSub(&L.fitb[q], (uint32_t)k);
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t v = L.wl[k][0][lane];
+                bool keep = v != 0;
+                if (keep) {
+                    const int o = key_node(v, a) - lo;
+                    keep = !((L.skip[o >> 5] >> (o & 31)) & 1u);
                 }
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-                __builtin_amdgcn_wave_barrier();
+                const uint64_t m = __ballot(keep);
+                const int pos = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (keep && pos < 128) L.out[pos] = v;
+                run += __popcll(m);
+            }
+            if (lane >= run) L.out[lane] = 0;
+            if (64 + lane >= run) L.out[64 + lane] = 0;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            if (ok) {
+                uint64_t* dst = A.blists + ((size_t)(p % kEngSlots) * A.nw + b) * kEngListWords;
+                st_sc1(&dst[lane], ((uint64_t)p << 32) | L.out[lane]);
+                st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.out[64 + lane]);
+            }
+            if (tb >= 0) ETL(A, p, tb + 3);
+            if (ok && p >= A.first + 1) {
+                eng_fit_drop(L, pset, node, lo, cnt);
+                eng_fit_publish(A, L, p - 1, b);
             }
             if (!ok && lane == 0) L.ok = 0;  // (the error is recorded: every block gives up)
-            if (ok && lane < 2) {
-                const uint32_t v = (L.fitb[2 * lane] & 0xffff) | (L.fitb[2 * lane + 1] << 16);
-                st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | v);
-            }
             if (tb >= 0) ETL(A, p, tb + 4);
         }
     }
@@ -558,19 +642,95 @@ __device__ __forceinline__ void eng_publish_done(EngCtl* ctl, uint32_t* pend) {
     *pend = 0;
 }
 
-// Pop q's front, by waves: 2 the hash of pops q-1 / q-2's candidates (node
-// -> latest row slot); 3, 4, 6, 7 its package — fields 8k .. 8k + 7 of the 128
-// entries each, wave 3 also the descriptor and class — into LDS, polled
-// until every granule carries q (one round trip when it is ready).  Run for
-// pop p + 1 by the waves pop p's placement leaves idle (and for the first pop
-// up front).  An exit descriptor has no package: its descriptor comes from
-// the device ring.
-__device__ __forceinline__ void eng_front(const EngArgs& A, EngPlacerLds& L, uint32_t q, int wave) {
+// Wave 5: pop p's result granules (from LDS, eng_finish) to the host's pinned slot.
+__device__ __forceinline__ void eng_host_out(const EngArgs& A, EngPlacerLds& L, uint32_t p, uint32_t slot) {
+    const int lane = threadIdx.x & 63;
+    while (__hip_atomic_load(&L.gran_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)p) {
+        if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    PopOut* out = (PopOut*)((char*)A.out + (size_t)slot * sizeof(PopOut));
+    const uint64_t g = L.gran[lane];
+    if (lane < 2 && L.gfit[lane])
+        __hip_atomic_store(&out->fit[lane], L.gfit[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (g) __hip_atomic_store(&out->g[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ETL(A, p, 8);
+}
+
+// Pop q's older candidates, evaluated during pop q-1's placement by waves it
+// leaves idle (their rows are final): set 0 = pop q-2's candidates (ring
+// (q + 2) % 4), set 1 = pop q-3's (ring (q + 1) % 4); role 0 the key (static
+// predicates, node-affinity weight, FitDelta bits, kind), 1 / 2 the depth-1
+// score after an Allocate / a Pipeline.  Into the front arrays (fe, ...):
+// pop q-1's placement still reads the row cache's na / s1 of these slots;
+// pop q's P2 moves the ones that count (x2use / x3use) there.
+__device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                               const EngArgs& A, EngPlacerLds& L, uint32_t q, int set, int role) {
+    const int lane = eng_lane();
+    EngCtl* ctl = A.ctl;
+    const uint64_t* src = &ctl->desc[q % kEngRing][lane & 7];  // (the dispatcher forwards descriptors ahead)
+    uint64_t x = 0;
+    EngWait wt(ctl, kEngDescTicks);
+    for (;;) {
+        x = ld_sc1(src);
+        if (__ballot(lane < 8 && (uint32_t)(x >> 32) != q) == 0) break;
+        if (!wt.tick(kEngErrDesc)) return;
+    }
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, i);
+    const EngDesc d = eng_decode(w);
+    if (d.op != kEngOpPop) return;
+    const PopArgs a = eng_args(d);
+    const TaskClass& c = t.classes[d.cls];
+    const int ring = set == 0 ? (int)((q + 2) % 4) : (int)((q + 1) % 4);
+    const int node = L.xn[ring][lane];
+    const int sl = 64 * ring + lane;
+    const uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t sc;
+    bool passed;
+    if (role == 0) {
+        uint32_t e = 0, fb = 0, kind = 0;
+        int32_t na = 0;
+        if (node >= 0) {
+            const Row r = L.rc.row[sl];
+            const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
+            na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
+            const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
+            e = sweep_key<uint32_t>(k0, a);
+            fb = fit_bits(c, r, passed);
+            kind = k0 ? key_kind(k0) : 0;
+        }
+        L.fe[set][lane] = e;
+        L.ffb[set][lane] = (uint8_t)fb;
+        L.fkind[set][lane] = (uint8_t)kind;
+        L.fna[set][lane] = na;
+    } else if (node >= 0) {
+        const Row r = L.rc.row[sl];
+        const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
+        const int alloc = role == 1 ? 1 : 0;
+        const Row r1 = apply_commits(r, c, alloc, 1 - alloc);
+        const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
+        (role == 1 ? L.fs1a : L.fs1p)[set][lane] = k1 ? key_score(k1) : INT32_MIN;
+    }
+}
+
+// Pop q's front, by waves: 2 the hash of pops q-1 / q-2 / q-3's candidates
+// (node -> latest row slot), 1, 2, 3, 5, 6, 7 the evaluation of pops q-2 /
+// q-3's candidates (eng_front_eval; wave 0's SIMD left to the placement),
+// then 3, 4, 6, 7 its package — fields
+// 8k .. 8k + 7 of the 128 entries each, wave 3 also the descriptor and class —
+// into LDS, polled until every granule carries q (one round trip when it is
+// ready).  Run for pop p + 1 by the waves pop p's placement leaves idle (and
+// for the first pop up front).  An exit descriptor has no package: its
+// descriptor comes from the device ring.
+__device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                                          EngPlacerLds& L, uint32_t q, int wave) {
     const int lane = threadIdx.x & 63;
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     if (wave == 2) {
-        const int r1 = (int)((q + 3) % 4), r2 = (int)((q + 2) % 4);
+        const int r1 = (int)((q + 3) % 4), r2 = (int)((q + 2) % 4), r3 = (int)((q + 1) % 4);
         for (int h = lane; h < EngRowCache::kHashN; h += 64) rc.hkey[h] = -1;
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
@@ -582,9 +742,18 @@ __device__ __forceinline__ void eng_front(const EngArgs& A, EngPlacerLds& L, uin
         const bool use2 = n2 >= 0 && rc_find(&rc, n2) < 0;  // a node of both: pop q-1's row is the latest
         L.x2use[lane] = use2;
         if (use2) rc_insert(&rc, n2, 64 * r2 + lane);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int n3 = L.xn[r3][lane];
+        const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
+        L.x3use[lane] = use3;
+        if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
+        eng_front_eval(cf, nc, t, A, L, q, 1, 2);
         return;
     }
+    if (wave == 1 || wave == 5) { eng_front_eval(cf, nc, t, A, L, q, 0, wave == 1 ? 0 : 1); return; }
     if (!(wave == 3 || wave == 4 || wave == 6 || wave == 7)) return;
+    if (wave != 4) eng_front_eval(cf, nc, t, A, L, q, wave == 6 ? 0 : 1, wave == 7 ? 0 : wave == 3 ? 1 : 2);
     const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block
     const EngPkg* pk = A.pkg + (q % kEngSlots);
     uint64_t v[16];
@@ -631,27 +800,32 @@ __device__ __forceinline__ void eng_front(const EngArgs& A, EngPlacerLds& L, uin
 }
 
 // The placer, per pop p (its front — descriptor, class, candidate hash,
-// package — was prepared during pop p-1's placement):
+// package, pops p-2 / p-3's candidates evaluated — was prepared during pop
+// p-1's placement):
 //   P2  wave 0 drops pop p-1's candidates from the package list (stale keys: at most 64
-//       of 128, the first 64 left are exact); waves 1-4 re-evaluate pops p-1 / p-2's
-//       candidates on the rows this block left them with (keys, depth-1 scores);
+//       of 128, the first 64 left are exact); waves 1-3 re-evaluate pop p-1's candidates
+//       on the rows this block left them with (keys, depth-1 scores); waves 5 / 6 move
+//       the front's results for pops p-2 / p-3's candidates that count into place;
 //   P3  the final top 64, pop p-1's `done` (its write-back drained), pop p's candidates
 //       published, their rows into ring p % 4;
 //   P4  the placement (place_decide, parallel levels, rows in ring order); wave 0 then
 //       the results and rows, wave 5 stores the results to the host, the other waves
 //       prepare pop p+1's front.
+// The workers of pop p leave out pops p-3 / p-2's candidates and may hold stale
+// keys of pop p-1's: every node of the three sets is re-evaluated here.
 __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                                            EngPlacerLds& L) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
-    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready[0] = L.s1_ready[1] = 0; }
+    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready = 0; }
     __syncthreads();
-    eng_front(A, L, A.first, wave);
+    eng_front(cf, nc, t, A, L, A.first, wave);
     uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
     for (uint32_t p = A.first;; ++p) {
-        const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r0 = (int)(p % 4);  // rings of p-1, p-2, p
+        // rings of p-1, p-2, p-3, p
+        const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r3 = (int)((p + 1) % 4), r0 = (int)(p % 4);
         const int stage = kEngStage + kEngPkgN * (int)(p % 2);
         __syncthreads();
         if (!L.ok) return;
@@ -688,21 +862,16 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             if (c0) rc_insert(&rc, key_node(k0, a), stage + lane);
             if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
             ETL(A, p, 1);
-        } else if (wave != 2) {  // pops p-1 (q 0) / p-2 (q 1)'s candidates on this block's rows:
-            // waves 1 / 3 their keys (sorted) and FitDelta bits, waves 5 / 4 and 6 / 7 their
-            // depth-1 scores after an Allocate / a Pipeline; the key wave then keeps the one its
-            // key's kind calls for
-            const int q = (wave == 1 || wave == 5 || wave == 6) ? 0 : 1;
-            const int role = (wave == 1 || wave == 3) ? 0 : (wave == 5 || wave == 4) ? 1 : 2;
-            const int ring = q == 0 ? r1 : r2;
-            const int node = L.xn[ring][lane];
-            const bool use = node >= 0 && (q == 0 || L.x2use[lane]);
-            const int sl = 64 * ring + lane;
+        } else if (wave <= 3) {  // pop p-1's candidates: wave 1 their keys (sorted) and FitDelta
+            // bits, waves 2 / 3 their depth-1 scores after an Allocate / a Pipeline; the key
+            // wave then keeps the one its key's kind calls for
+            const int node = L.xn[r1][lane];
+            const int sl = 64 * r1 + lane;
             const uint64_t pw[4] = {0, 0, 0, 0};
-            if (role == 0) {
+            if (wave == 1) {
                 uint32_t e = 0, fb = 0;
                 int kind = 0;
-                if (use) {
+                if (node >= 0) {
                     const Row r = rc.row[sl];
                     const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
                     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
@@ -714,44 +883,59 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                     fb = fit_bits(c, r, passed);
                     kind = k0 ? key_kind(k0) : 0;
                 }
-                if (wave == 1) ETL(A, p, 2);
-                L.e[q][lane] = wave_sort_desc(e);
-                if (wave == 1) ETL(A, p, 9);
-                L.fbp[q][lane] = (uint8_t)fb;
-                // the depth-1 score the placement reads (its key's kind decides the commit)
-                while (__hip_atomic_load(&L.s1_ready[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
+                ETL(A, p, 2);
+                L.e[0][lane] = wave_sort_desc(e);
+                ETL(A, p, 9);
+                L.fbp[0][lane] = (uint8_t)fb;
+                while (__hip_atomic_load(&L.s1_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
                     __builtin_amdgcn_s_sleep(1);
-                if (use) rc.s1[sl] = kind == 0 ? INT32_MIN : kind == 2 ? L.s1p[q][lane] : L.s1a[q][lane];
+                if (node >= 0) rc.s1[sl] = kind == 0 ? INT32_MIN : kind == 2 ? L.s1p[lane] : L.s1a[lane];
             } else {
                 int32_t s1 = INT32_MIN;
-                if (use) {
+                if (node >= 0) {
                     const Row r = rc.row[sl];
                     const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
-                    const int alloc = role == 1 ? 1 : 0;
-                    const Row r1 = apply_commits(r, c, alloc, 1 - alloc);
+                    const int alloc = wave == 2 ? 1 : 0;
+                    const Row r1r = apply_commits(r, c, alloc, 1 - alloc);
                     int32_t sc;
                     bool passed;
-                    const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
+                    const uint64_t k1 = dyn_key(cf, c, t, nc, r1r, pw, node, true, na, &sc, &passed);
                     s1 = k1 ? key_score(k1) : INT32_MIN;
                 }
-                if (role == 1) L.s1a[q][lane] = s1;
-                else L.s1p[q][lane] = s1;
-                if (wave == 5) ETL(A, p, 19);
+                if (wave == 2) L.s1a[lane] = s1;
+                else L.s1p[lane] = s1;
+                if (wave == 2) ETL(A, p, 19);
                 __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the scores are in LDS before the count
-                if (lane == 0) __hip_atomic_fetch_add(&L.s1_ready[q], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (lane == 0) __hip_atomic_fetch_add(&L.s1_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (wave == 5 || wave == 6) {  // pops p-2 / p-3's candidates that count (the front's results)
+            const int set = wave - 5;
+            const int ring = set == 0 ? r2 : r3;
+            const int node = L.xn[ring][lane];
+            const bool use = node >= 0 && (set == 0 ? L.x2use[lane] : L.x3use[lane]);
+            L.e[1 + set][lane] = wave_sort_desc(use ? L.fe[set][lane] : 0u);
+            L.fbp[1 + set][lane] = use ? L.ffb[set][lane] : (uint8_t)0;
+            if (use) {
+                const int sl = 64 * ring + lane;
+                const int kind = L.fkind[set][lane];
+                rc.na[sl] = L.fna[set][lane];
+                rc.s1[sl] = kind == 0 ? INT32_MIN : kind == 2 ? L.fs1p[set][lane] : L.fs1a[set][lane];
             }
         }
         __syncthreads();
         if (wave == 0) ETL(A, p, 3);
         // P3
         if (wave == 0) {
-            if (lane < 2) L.s1_ready[lane] = 0;
+            if (lane == 0) L.s1_ready = 0;
             uint32_t top = wave_merge_desc(L.s64[lane], L.e[0][lane]);
             top = wave_merge_desc(top, L.e[1][lane]);
-            const uint32_t fbp = (uint32_t)L.fbp[0][lane] | ((uint32_t)L.fbp[1][lane] << 4);
+            top = wave_merge_desc(top, L.e[2][lane]);
+            const uint32_t fbp = (uint32_t)L.fbp[0][lane] | ((uint32_t)L.fbp[1][lane] << 4) |
+                                 ((uint32_t)L.fbp[2][lane] << 8);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int k = __popcll(__ballot((fbp >> q) & 1u)) + __popcll(__ballot((fbp >> (q + 4)) & 1u));
+                const int k = __popcll(__ballot((fbp >> q) & 1u)) + __popcll(__ballot((fbp >> (q + 4)) & 1u)) +
+                              __popcll(__ballot((fbp >> (q + 8)) & 1u));
                 if (lane == q) L.fitin[q] = k;
             }
             const int n = top ? key_node(top, a) : -1;
@@ -777,25 +961,24 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         __syncthreads();
         if (wave == 0) ETL(A, p, 5);
         // P4 (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
-        // sends the others to the launched kernels; one instantiation keeps the
-        // kernel's registers within one 512-thread block per CU)
-        PlaceDec<uint32_t> D;
-        if (place_decide<uint32_t, true>(cf, nc, t, c, a, L.wl64, p, &rc, 0, D, L.srcslot)) {
-            ETL(A, p, 6);
-            if (lane == 0 && A.tl) A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 30] = (uint64_t)D.done | ((uint64_t)D.stop << 8);
-            eng_finish(cf, nc, t, c, a, A, L, p, r0, D, &pend);
-        } else if (wave == 5) {  // the results to the host
-            while (__hip_atomic_load(&L.gran_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)p)
-                __builtin_amdgcn_s_sleep(1);
-            PopOut* out = (PopOut*)((char*)A.out + (size_t)d.slot * sizeof(PopOut));
-            const uint64_t g = L.gran[lane];
-            if (lane < 2 && L.gfit[lane]) __hip_atomic_store(&out->fit[lane], L.gfit[lane], __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_SYSTEM);
-            if (g) __hip_atomic_store(&out->g[lane], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            ETL(A, p, 8);
+        // sends the others to the launched kernels).  Wave 0 decides alone
+        // (place_decide_wave) and writes the results and rows, while the other
+        // waves prepare pop p+1's front and wave 5 then stores the results.
+        if (wave == 0) {
+            PlaceDec<uint32_t> D;
+            if (place_decide_wave<uint32_t, true>(cf, nc, t, c, a, L.wl64[0], p, &rc, L.srcslot, !A.quick, D)) {
+                ETL(A, p, 6);
+                if (lane == 0 && A.tl)
+                    A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 30] = (uint64_t)D.done | ((uint64_t)D.stop << 8);
+                eng_finish(cf, nc, t, c, a, A, L, p, r0, D, &pend);
+            } else if (lane == 0) {  // (a class with host ports: never sent to the engine, eng_eligible)
+                __hip_atomic_store(&ctl->err, (uint32_t)kEngErrClass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&L.ok, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
         } else {
-            eng_front(A, L, p + 1, wave);
+            eng_front(cf, nc, t, A, L, p + 1, wave);
             if (wave == 3) ETL(A, p, 15);
+            if (wave == 5) eng_host_out(A, L, p, d.slot);
         }
     }
 }

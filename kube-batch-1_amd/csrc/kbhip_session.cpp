@@ -574,6 +574,7 @@ struct Session {
     uint32_t eng_first = 1;     // the first pop of the next launch
     int eng_nw = 0, eng_npb = 0, eng_ng = 0;  // worker blocks (0: not sized yet, -1: the engine cannot run here)
     int eng_nw_opt = 0;         // option "engine_workers" (0: as many as stay resident)
+    bool eng_quick = true;      // option "engine_quick" = 0 (test mode): place_decide_wave without its fast path
     DevBuf b_eng;               // EngCtl + the worker and group lists
     EngCtl* d_eng_ctl = nullptr;
     EngPkg* d_eng_pkg = nullptr;
@@ -2237,6 +2238,7 @@ static void eng_start(Session& S) {
     A.npb = S.eng_npb;
     A.ng = S.eng_ng;
     A.tl = S.d_eng_tl;
+    A.quick = S.eng_quick ? 1 : 0;
     HIPCHK(launch_engine(S.conf, S.nc, S.tab, A, S.stream));
     S.eng_running = true;
     S.stats.engine_launches++;
@@ -5791,7 +5793,7 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
         else if (std::strcmp(key, "engine") == 0 || std::strcmp(key, "engine_workers") == 0 ||
-                 std::strcmp(key, "engine_timeline") == 0) {
+                 std::strcmp(key, "engine_timeline") == 0 || std::strcmp(key, "engine_quick") == 0) {
             kbhip::Session& S = s->s;
             if (!S.encode_only) {
                 HIPCHK(hipSetDevice(S.device));
@@ -5799,6 +5801,8 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
             if (key[6] == 0) {
                 S.engine = value != 0;
+            } else if (std::strcmp(key, "engine_quick") == 0) {  // 0 (test mode): no fast path, every candidate in the levels
+                S.eng_quick = value != 0;
             } else if (std::strcmp(key, "engine_timeline") == 0) {  // diagnostic: the engine's event stamps
                 const size_t words = (size_t)kbhip::kEngTlSlots * kbhip::kEngTlEvents;
                 if (value && !S.d_eng_tl && !S.encode_only) {

@@ -66,6 +66,36 @@ def test_engine_worker_shapes(engine, oracle_mod, kbgen_mod, tmp_path, workers):
     assert np.array_equal(ns0, ns) and close0 == close
 
 
+@pytest.mark.parametrize("seed", range(8))
+def test_engine_levels_only(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """engine_quick = 0: every decision by the levels over all the placer's
+    waves (place_decide), not the single-wave path (place_decide_quick) —
+    both must give the restatement's placements."""
+    c = kbgen_mod.gen_random(5300 + seed, n_nodes=3 + seed % 5, n_jobs=6, max_tasks=12,
+                             features=("labels", "running", "selector", "taints"), tiers=TIERS[seed % 4])
+    p = str(tmp_path / "l.kbs")
+    c.write(p)
+    exp, ons = oracle_mod.ref_allocate(p, with_nodes=True)
+    got, ns, st, close = _run(engine, p, engine_quick=0)
+    assert got == exp.as_list()
+    assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
+    assert close == oracle_mod.ref_gang_close(p)
+    assert st["engine_pops"] > 0
+    got1, ns1, _, close1 = _run(engine, p)
+    assert got1 == got and np.array_equal(ns1, ns) and close1 == close
+
+
+def test_engine_c2_levels_only(engine, oracle_mod, kbgen_mod, tmp_path):
+    """C2's generator at 2k nodes x 12k pods, levels only vs the default."""
+    p = str(tmp_path / "c2l.kbs")
+    kbgen_mod.gen_c2(p, n_nodes=2000, n_pending=12000, seed=9350)
+    exp = oracle_mod.fast_allocate(p, threads=8).as_list()
+    got, ns, st, _ = _run(engine, p, engine_quick=0)
+    assert got == exp and st["engine_pops"] > 50
+    got1, ns1, _, _ = _run(engine, p)
+    assert got1 == exp and np.array_equal(ns1, ns)
+
+
 def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path):
     """A crowded cluster: many pops end on a task with no node, so the gang
     close messages carry the FitDelta histograms the engine counts (workers'
