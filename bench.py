@@ -19,14 +19,15 @@ every rank runs the same placement (strong scaling).  --mode replicas: N
 independent sessions.
 
 Also reported:
-* roofline of the fused pop kernel (k_pop_batch_ov: sweep + top-64 + placement):
-  algorithmic bytes = nodes x 113 B per launch / the
-  kernel's device busy period per launch (allocate's device span, HIP events
-  on the engine streams, / launches: consecutive launches overlap, so their
-  own spans — also reported, `span_us` — add up to more than the step);
-  beside it the standalone predicate + score sweep (`sweep`: the product
-  kernel k_rank_nodes behind kbhip_sweep_scores, one launch per task over all
-  nodes, each launch timed with HIP events on its stream);
+* roofline of the batched pop path: with the persistent pop engine (default,
+  --engine 1: k_engine, one resident kernel serving every eligible pop from a
+  descriptor ring) or the fused pop kernel (--engine 0: k_pop_batch_ov, sweep
+  + top-64 + placement per launch): algorithmic bytes = nodes x 113 B
+   per pop / the device busy period per pop (allocate's
+  device span, HIP events on the session streams, / batched pops); beside it
+  the standalone predicate + score sweep (`sweep`: the product kernel
+  k_score_sweep behind kbhip_sweep_scores, one launch over all nodes, timed
+  with HIP events around back-to-back launches);
 * cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
   cores, timed on a stratified sample of the same session: pop windows early,
   mid and late in the session, the pops between them fast-forwarded from the
@@ -66,7 +67,7 @@ def parse():
     ap.add_argument("--time-every", type=int, default=50,
                     help="HIP-event time every k-th batched pop launch on its own stream (the roofline's kernel "
                          "duration; 0 = off)")
-    ap.add_argument("--speculate", type=int, default=2, choices=(0, 1, 2, 3),
+    ap.add_argument("--speculate", type=int, default=4, choices=range(7),
                     help="predicted job pops queued ahead of the running one")
     ap.add_argument("--overlap", type=int, default=1, choices=(0, 1, 2),
                     help="1: batched pops alternate over two streams, a pop's sweep beside the previous pop's "
@@ -212,7 +213,7 @@ def open_sharded(buf, device, rank, world, dist):
     return s
 
 
-def run_session(buf, device, time_every, shard=None, overlap=1, speculate=2, keep_log=False, engine=1,
+def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, keep_log=False, engine=1,
                 engine_workers=0):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)

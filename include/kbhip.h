@@ -328,10 +328,14 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "keys32" = 1 (default) uses 32-bit selection keys in the batched sweep
  * when the class's score range and the node count fit (same order as the
  * 64-bit key), 0 = always 64-bit;
- * "speculate" = 2 (default) lets kbhip_allocate queue up to that many
- * predicted next job pops behind the running one (0..3; each used only if it
+ * "speculate" = 4 (default) lets kbhip_allocate queue up to that many
+ * predicted next job pops behind the running one (0..6; each used only if it
  * is exactly the next pop, retracted on device otherwise: placements are
  * unchanged), 0 = one pop at a time;
+ * "engine" = 1 (default) serves eligible batched pops with the persistent pop
+ * engine (one resident kernel, a descriptor ring), 0 = launched kernels;
+ * "engine_workers" = n caps its worker blocks (0: as many as stay resident);
+ * "engine_groups" = g its merger blocks (-1: automatic, 0: none);
  * "overlap" = k rotates batched pops over k + 1 streams so that a pop's sweep
  * runs beside the previous k pops' placements, chained on the device (1, the
  * default, or 2); 0 = one stream, one pop kernel at a time;

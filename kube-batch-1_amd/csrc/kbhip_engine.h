@@ -78,6 +78,6 @@ struct EngArgs {
     int quick;                 // 0 (a test mode): no fast path, every feasible candidate through the levels rounds
 };
 // Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
-constexpr int kEngTlSlots = 8192, kEngTlEvents = 32;
+constexpr int kEngTlSlots = 32768, kEngTlEvents = 32;
 
 }  // namespace kbhip

@@ -305,6 +305,7 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
     const int lo = b * A.npb;
     const int cnt = nc.n - lo < A.npb ? (nc.n - lo > 0 ? nc.n - lo : 0) : A.npb;
     if (threadIdx.x == 0) L.ok = 1;
+    uint32_t cpub = A.first - 1;  // wave 0: the last pop whose FitDelta counts are published
     for (uint32_t p = A.first;; ++p) {
         const int set = (int)(p % 2), pset = 1 - set;
         // 1. the pop's descriptor; the node rows as pop p-4 left them; pop p-3's candidates
@@ -314,7 +315,36 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
         if (threadIdx.x < 4) L.fitb[set][threadIdx.x] = 0;
         const int tb = b == 0 ? 10 : -1;  // timeline: worker 0
         if (wave == 0) {
-            bool ok = eng_wait_desc(ctl, p, L.desc);
+            // pop p's descriptor; meanwhile pop p-1's counts once pop p-2's candidates are
+            // known (a placement whose task found no node reads them: they must not wait
+            // for a descriptor the host sends only after that placement's results)
+            bool ok = true;
+            {
+                const uint64_t* src = &ctl->desc[p % kEngRing][lane & 7];
+                EngWait wt(ctl, kEngDescTicks);
+                for (;;) {
+                    const uint64_t x = ld_sc1(src);
+                    if (__ballot(lane < 8 && (uint32_t)(x >> 32) != p) == 0) {
+                        if (lane < 8) L.desc[lane] = (uint32_t)x;
+                        break;
+                    }
+                    if (cpub + 1 < p) {
+                        int node = -1;
+                        bool have = true;
+                        if (p >= A.first + 2) {
+                            const uint64_t cw = ld_sc1(&ctl->cands[(p - 2) % kEngSlots][lane]);
+                            have = __ballot((uint32_t)(cw >> 32) != p - 2) == 0;
+                            node = (int)(uint32_t)cw;
+                        }
+                        if (have) {
+                            eng_fit_drop(L, pset, node, lo, cnt);
+                            eng_fit_publish(A, L, p - 1, b);
+                            cpub = p - 1;
+                        }
+                    }
+                    if (!wt.tick(kEngErrDesc)) { ok = false; break; }
+                }
+            }
             if (tb >= 0) ETL(A, p, tb);
             const EngDesc d0 = eng_decode(L.desc);  // (LDS written by this wave, in order)
             if (ok && d0.op == kEngOpPop) {
@@ -326,12 +356,13 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                     const int o = node - lo;
                     if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
                 }
-            } else if (ok && p >= A.first + 1) {  // the run ends: the last pop's counts
+            } else if (ok && cpub + 1 < p) {  // the run ends: the last pop's counts
                 int node = -1;
                 if (p >= A.first + 2) ok = eng_wait_cands(ctl, p - 2, &node);
                 if (ok) {
                     eng_fit_drop(L, pset, node, lo, cnt);
                     eng_fit_publish(A, L, p - 1, b);
+                    cpub = p - 1;
                 }
             }
             if (lane == 0) L.ok = ok;
@@ -368,8 +399,10 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
         if (wave == 0) {
             bool ok = true;
             int node = -1;
+            if (tb >= 0) ETL(A, p, 16);
             if (p >= A.first + 2) {
                 ok = eng_wait_cands(ctl, p - 2, &node);
+                if (tb >= 0) ETL(A, p, 17);
                 const int o = node - lo;
                 if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
                 if (ok) eng_fit_drop(L, set, node, lo, cnt);
@@ -399,14 +432,53 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                 st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.out[64 + lane]);
             }
             if (tb >= 0) ETL(A, p, tb + 3);
-            if (ok && p >= A.first + 1) {
+            if (ok && cpub + 1 < p) {
                 eng_fit_drop(L, pset, node, lo, cnt);
                 eng_fit_publish(A, L, p - 1, b);
+                cpub = p - 1;
             }
             if (!ok && lane == 0) L.ok = 0;  // (the error is recorded: every block gives up)
             if (tb >= 0) ETL(A, p, tb + 4);
         }
     }
+}
+
+// The top 128 of pop p's worker lists g, g + stride, ... (cnt of them), in
+// (a0: ranks 0..63, a1: 64..127) of each wave: wave w merges lists w, w + 8, ...
+// (4 in flight); block_merge128_all then merges the waves'.  false: a wait gave up.
+__device__ __forceinline__ bool eng_merge_lists(EngCtl* ctl, const uint64_t* src0, int g, int stride, int cnt,
+                                                uint32_t p, uint32_t* a0, uint32_t* a1) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    bool ok = true;
+    for (int i0 = wave; i0 < cnt && ok; i0 += 4 * (kPopThreads / 64)) {
+        constexpr int kQ = 4;
+        uint64_t v0[kQ], v1[kQ];
+        const uint64_t* s[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int i = i0 + q * (kPopThreads / 64);
+            s[q] = i < cnt ? src0 + (size_t)(g + i * stride) * kEngListWords : nullptr;
+            v0[q] = s[q] ? ld_sc1(&s[q][lane]) : ((uint64_t)p << 32);
+            v1[q] = s[q] ? ld_sc1(&s[q][64 + lane]) : ((uint64_t)p << 32);
+        }
+        EngWait wt(ctl, kEngWaitTicks);
+        for (;;) {
+            bool miss = false;
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) {
+                if (__ballot((uint32_t)(v0[q] >> 32) != p || (uint32_t)(v1[q] >> 32) != p) == 0) continue;
+                miss = true;
+                v0[q] = ld_sc1(&s[q][lane]);
+                v1[q] = ld_sc1(&s[q][64 + lane]);
+            }
+            if (!miss) break;
+            if (!wt.tick()) { ok = false; break; }
+        }
+        if (ok)
+#pragma unroll
+            for (int q = 0; q < kQ; ++q) wave_merge128_desc(*a0, *a1, (uint32_t)v0[q], (uint32_t)v1[q]);
+    }
+    return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -429,37 +501,8 @@ __device__ __forceinline__ void eng_merger(const EngArgs& A, EngMergerLds& L, in
         if (!L.ok) return;
         if (eng_decode(L.desc).op != kEngOpPop) return;
         const uint64_t* src0 = A.blists + (size_t)(p % kEngSlots) * A.nw * kEngListWords;
-        // wave w merges the group's lists w, w + 8, ... (4 in flight)
         uint32_t a0 = 0, a1 = 0;
-        bool ok = true;
-        for (int i0 = wave; i0 < cg && ok; i0 += 4 * (kPopThreads / 64)) {
-            constexpr int kQ = 4;
-            uint64_t v0[kQ], v1[kQ];
-            const uint64_t* s[kQ];
-#pragma unroll
-            for (int q = 0; q < kQ; ++q) {
-                const int i = i0 + q * (kPopThreads / 64);
-                s[q] = i < cg ? src0 + (size_t)(g + i * A.ng) * kEngListWords : nullptr;
-                v0[q] = s[q] ? ld_sc1(&s[q][lane]) : ((uint64_t)p << 32);
-                v1[q] = s[q] ? ld_sc1(&s[q][64 + lane]) : ((uint64_t)p << 32);
-            }
-            EngWait wt(ctl, kEngWaitTicks);
-            for (;;) {
-                bool miss = false;
-#pragma unroll
-                for (int q = 0; q < kQ; ++q) {
-                    if (__ballot((uint32_t)(v0[q] >> 32) != p || (uint32_t)(v1[q] >> 32) != p) == 0) continue;
-                    miss = true;
-                    v0[q] = ld_sc1(&s[q][lane]);
-                    v1[q] = ld_sc1(&s[q][64 + lane]);
-                }
-                if (!miss) break;
-                if (!wt.tick()) { ok = false; break; }
-            }
-            if (ok)
-#pragma unroll
-                for (int q = 0; q < kQ; ++q) wave_merge128_desc(a0, a1, (uint32_t)v0[q], (uint32_t)v1[q]);
-        }
+        bool ok = eng_merge_lists(ctl, src0, g, A.ng, cg, p, &a0, &a1);
         if (!ok) L.ok = 0;
         if (g == 0 && wave == 0) ETL(A, p, 25);
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
@@ -526,7 +569,10 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
         const TaskClass& c = L.cls;
         uint32_t a0 = 0, a1 = 0;
         bool ok = true;
-        if (wave < A.ng) {
+        if (A.ng == 0) {  // no merger level: the worker lists
+            ok = eng_merge_lists(ctl, A.blists + (size_t)(p % kEngSlots) * A.nw * kEngListWords, 0, 1, A.nw, p, &a0,
+                                 &a1);
+        } else if (wave < A.ng) {
             const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + wave) * kEngListWords;
             uint64_t v0 = ld_sc1(&s[lane]), v1 = ld_sc1(&s[64 + lane]);
             EngWait wt(ctl, kEngWaitTicks);
@@ -537,8 +583,8 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
             }
             a0 = (uint32_t)v0;
             a1 = (uint32_t)v1;
-            if (!ok && lane == 0) L.ok = 0;
         }
+        if (!ok) L.ok = 0;
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
         if (!L.ok) return;
         if (wave == 0) ETL(A, p, 21);
@@ -600,7 +646,26 @@ __device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, c
     if (D.stop == 1) {
         uint32_t fr = 0;  // group g's count b in lane 4g + b (fit_sum layout)
         const int g = lane >> 2;
-        if (g < A.ng) {
+        if (A.ng == 0) {  // the worker count words: two 16-bit counts each, count b in lane b
+            uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+            for (int i0 = 0; i0 < A.nw; i0 += 64) {
+                const int i = i0 + lane;
+                const uint64_t* s =
+                    i < A.nw ? A.blists + ((size_t)(p % kEngSlots) * A.nw + i) * kEngListWords + 128 : nullptr;
+                uint64_t x0 = s ? ld_sc1(&s[0]) : ((uint64_t)p << 32), x1 = s ? ld_sc1(&s[1]) : ((uint64_t)p << 32);
+                EngWait wt(ctl, kEngWaitTicks);
+                while (__ballot((uint32_t)(x0 >> 32) != p || (uint32_t)(x1 >> 32) != p) != 0) {
+                    if (!wt.tick()) break;
+                    if (s) { x0 = ld_sc1(&s[0]); x1 = ld_sc1(&s[1]); }
+                }
+                const uint32_t y0 = (uint32_t)x0, y1 = (uint32_t)x1;
+                t0 += wave_sum_u32(y0 & 0xffff);
+                t1 += wave_sum_u32(y0 >> 16);
+                t2 += wave_sum_u32(y1 & 0xffff);
+                t3 += wave_sum_u32(y1 >> 16);
+            }
+            fr = lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? t2 : lane == 3 ? t3 : 0u;
+        } else if (g < A.ng) {
             const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + g) * kEngListWords + 128 + (lane & 3);
             uint64_t x = ld_sc1(s);
             EngWait wt(ctl, kEngWaitTicks);
@@ -962,8 +1027,8 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         if (wave == 0) ETL(A, p, 5);
         // P4 (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
         // sends the others to the launched kernels).  Wave 0 decides alone
-        // (place_decide_wave) and writes the results and rows, while the other
-        // waves prepare pop p+1's front and wave 5 then stores the results.
+        // (place_decide_wave) and writes the results and rows, while wave 5
+        // stores the results to the host and the others prepare pop p+1's front.
         if (wave == 0) {
             PlaceDec<uint32_t> D;
             if (place_decide_wave<uint32_t, true>(cf, nc, t, c, a, L.wl64[0], p, &rc, L.srcslot, !A.quick, D)) {
@@ -976,9 +1041,11 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 __hip_atomic_store(&L.ok, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         } else {
+            // (wave 5's results first: its front waits for pop p+1's descriptor, which
+            // the host may send only after it has seen them)
+            if (wave == 5) eng_host_out(A, L, p, d.slot);
             eng_front(cf, nc, t, A, L, p + 1, wave);
             if (wave == 3) ETL(A, p, 15);
-            if (wave == 5) eng_host_out(A, L, p, d.slot);
         }
     }
 }

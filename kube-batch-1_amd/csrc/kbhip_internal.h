@@ -129,6 +129,7 @@ constexpr int kMaxGroups = 32;  // >= kGroups of kbhip_kernels.hip
 // per block and per group, 80 words (5 lines) apart.
 constexpr int kCandStride = 80;
 constexpr int kMaxDep = 2;     // previous pops an overlapped pop runs beside (streams - 1)
+constexpr int kMaxSpeculate = 6;  // predicted batched pops queued behind the running one (option "speculate")
 constexpr int kLinkSlots = 4;  // > kMaxDep: a slot is rewritten only after its readers finished
 // rows[e % kLinkSlots][f][i] = {e << 32 | half f of candidate i's row after
 // pop e} — kRowWords 32-bit halves of Row's dynamic and static fields (not

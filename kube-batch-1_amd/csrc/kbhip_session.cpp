@@ -574,6 +574,7 @@ struct Session {
     uint32_t eng_first = 1;     // the first pop of the next launch
     int eng_nw = 0, eng_npb = 0, eng_ng = 0;  // worker blocks (0: not sized yet, -1: the engine cannot run here)
     int eng_nw_opt = 0;         // option "engine_workers" (0: as many as stay resident)
+    int eng_ng_opt = -1;        // option "engine_groups": merger blocks (0: the final merger reads the worker lists; -1: auto)
     bool eng_quick = true;      // option "engine_quick" = 0 (test mode): place_decide_wave without its fast path
     DevBuf b_eng;               // EngCtl + the worker and group lists
     EngCtl* d_eng_ctl = nullptr;
@@ -596,6 +597,7 @@ struct Session {
     PopOutHost* h_out = nullptr;  // pinned, mapped: written by the device; 2 result slots
     void* d_out = nullptr;
     static constexpr int kSlots = 8;  // result slots: up to 1 + speculate batched pops in flight
+    static_assert(1 + kMaxSpeculate < kSlots, "a result slot per batched pop in flight");
     uint32_t slot_epoch[kSlots] = {};  // granule tags per result slot
     int next_slot = 0;                // slot of the next batched launch (round robin)
     // HIP-event pairs around batched pop launches (option "time_every"): a ring, each
@@ -609,7 +611,7 @@ struct Session {
 #ifdef KBHIP_STAMPS
     int speculate = 0;                // stamps are read per launch: no overlapped launches
 #else
-    int speculate = 2;                // predicted pops queued ahead of the running one (0..3)
+    int speculate = 4;                // predicted pops queued ahead of the running one (0..kMaxSpeculate)
 #endif
     int32_t res_node_buf[kMaxChunk], res_kind_buf[kMaxChunk];
     std::deque<PopTicket> tickets;    // asynchronous per-pop ABI: outstanding pops, oldest first
@@ -2178,7 +2180,7 @@ static void eng_size(Session& S) {
     if (nw < 1) return;
     const int npb = (N + nw - 1) / nw;
     if (npb > kEngMaxNpb) return;
-    const int ng = std::min(kEngMaxGroups, nw);
+    const int ng = S.eng_ng_opt >= 0 ? std::min(S.eng_ng_opt, nw) : std::min(kEngMaxGroups, nw);
     const size_t lists = (size_t)kEngSlots * (nw + ng) * kEngListWords;
     static_assert(sizeof(EngCtl) % 256 == 0 && sizeof(EngPkg) % 256 == 0, "engine buffers stay line-aligned");
     const size_t words = (sizeof(EngCtl) + kEngSlots * sizeof(EngPkg)) / 8 + lists;
@@ -3455,31 +3457,41 @@ struct Allocator {
             if (S.prop_on) prop_update(Q);
             return pstop;
         };
+        constexpr int kPredictSkip = 64;
         struct Pred {
             int q = -1, jb = -1, cls = -1, m = 0, n = 0, ready = 0;
             size_t cur = 0;
         };
         // The loop's next pop after pop (q, jb) stopped with pstop (heaps
         // changed through the journal); false when it is not a batched pop.
+        // The loop's steps that place nothing (an overused queue or one without
+        // jobs is dropped, a job without pending tasks is dropped and its queue
+        // pushed back) are followed, up to kPredictSkip of them.
         auto next_pop = [&](int q, int jb, int pstop, Pred* P) -> bool {
             if (pstop == KBHIP_STOP_READY) jobs_map.at(q).push(jb);
             queues.push(q);
-            const int q2 = queues.pop();
-            if (overused(q2)) return false;
-            auto jit2 = jobs_map.find(q2);
-            if (jit2 == jobs_map.end() || jit2->second.empty()) return false;
-            const int jb2 = jit2->second.pop();
-            HJob& j2 = S.jobs[jb2];
-            build_pending(j2);
-            const size_t cur2 = j2.cursor;
-            if (cur2 >= j2.pending.size()) return false;  // an empty pop next
-            const int cls2 = S.pods[j2.pending[cur2]].cls;
-            const size_t rem = j2.pending.size() - cur2;
-            int m2 = 0;
-            while ((size_t)m2 < rem && m2 < kMaxChunk && S.pods[j2.pending[cur2 + m2]].cls == cls2) ++m2;
-            if (!batchable(S, cls2)) return false;
-            *P = Pred{q2, jb2, cls2, m2, (int)rem, j2.cnt_alloc, cur2};
-            return true;
+            for (int skip = 0; skip <= kPredictSkip && !queues.empty(); ++skip) {
+                const int q2 = queues.pop();
+                if (overused(q2)) continue;
+                auto jit2 = jobs_map.find(q2);
+                if (jit2 == jobs_map.end() || jit2->second.empty()) continue;
+                const int jb2 = jit2->second.pop();
+                HJob& j2 = S.jobs[jb2];
+                build_pending(j2);
+                const size_t cur2 = j2.cursor;
+                if (cur2 >= j2.pending.size()) {  // an empty pop
+                    queues.push(q2);
+                    continue;
+                }
+                const int cls2 = S.pods[j2.pending[cur2]].cls;
+                const size_t rem = j2.pending.size() - cur2;
+                int m2 = 0;
+                while ((size_t)m2 < rem && m2 < kMaxChunk && S.pods[j2.pending[cur2 + m2]].cls == cls2) ++m2;
+                if (!batchable(S, cls2)) return false;
+                *P = Pred{q2, jb2, cls2, m2, (int)rem, j2.cnt_alloc, cur2};
+                return true;
+            }
+            return false;
         };
         auto launch_pred = [&](const Pred& p) {
             Spec sp;
@@ -3491,10 +3503,10 @@ struct Allocator {
         };
         // Keep up to S.speculate predicted pops queued behind pop (q, jb).
         auto speculate = [&](int q, int jb, int m, int n) {
-            Pred p[3];
+            Pred p[kMaxSpeculate];
             int got = 0;
             journal.on = true;
-            for (int cq = q, cjb = jb, cm = m, cn = n; got < S.speculate && got < 3;) {
+            for (int cq = q, cjb = jb, cm = m, cn = n; got < S.speculate && got < kMaxSpeculate;) {
                 const int ps = apply_outcome(cq, cjb, cm, cn);
                 if (ps < 0 || !next_pop(cq, cjb, ps, &p[got])) break;
                 cq = p[got].q;
@@ -5788,12 +5800,13 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             kbhip::set_sweep_variant((int)value);
         }
         else if (std::strcmp(key, "speculate") == 0) {
-            if (value < 0 || value > 3) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0..3");
+            if (value < 0 || value > kbhip::kMaxSpeculate) throw kbhip::Error(KBHIP_EINVAL, "speculate must be 0..6");
             s->s.speculate = (int)value;
         }
         else if (std::strcmp(key, "keys32") == 0) s->s.keys32 = value != 0;
         else if (std::strcmp(key, "engine") == 0 || std::strcmp(key, "engine_workers") == 0 ||
-                 std::strcmp(key, "engine_timeline") == 0 || std::strcmp(key, "engine_quick") == 0) {
+                 std::strcmp(key, "engine_timeline") == 0 || std::strcmp(key, "engine_quick") == 0 ||
+                 std::strcmp(key, "engine_groups") == 0) {
             kbhip::Session& S = s->s;
             if (!S.encode_only) {
                 HIPCHK(hipSetDevice(S.device));
@@ -5801,6 +5814,10 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
             }
             if (key[6] == 0) {
                 S.engine = value != 0;
+            } else if (std::strcmp(key, "engine_groups") == 0) {
+                if (value < -1 || value > kbhip::kEngMaxGroups) throw kbhip::Error(KBHIP_EINVAL, "engine_groups out of range");
+                S.eng_ng_opt = (int)value;
+                S.eng_nw = 0;  // sized again at the next engine pop
             } else if (std::strcmp(key, "engine_quick") == 0) {  // 0 (test mode): no fast path, every candidate in the levels
                 S.eng_quick = value != 0;
             } else if (std::strcmp(key, "engine_timeline") == 0) {  // diagnostic: the engine's event stamps

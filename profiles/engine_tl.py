@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 import kbgen  # noqa: E402
 import kbhip  # noqa: E402
 
-SLOTS, EV = 8192, 32
+SLOTS, EV = 32768, 32
 
 
 def main():
@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--pending", type=int, default=800_000)
     ap.add_argument("--workers", type=int, default=0)
+    ap.add_argument("--groups", type=int, default=-1)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     path = f"/tmp/kbhip_bench/c4_{a.nodes}_{a.pending}_{kbgen.BASE_SEED + 4}.kbs"
@@ -40,6 +41,7 @@ def main():
         s.allocate()
     with kbhip.Session(buf) as s:
         s.set_option("engine_workers", a.workers)
+        s.set_option("engine_groups", a.groups)
         s.set_option("engine_timeline", 1)
         s.allocate()
         st = s.stats()
@@ -51,13 +53,12 @@ def main():
     order = np.argsort(pops)
     t = t[order]
     pops = pops[order]
-    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 19, 24, 25, 26, 28]] > 0,
-                                 axis=1)
+    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 19, 28]] > 0, axis=1)
     t = t[keep]
     pops = t[:, 31]
     cont = np.diff(pops) == 1
     us = lambda x: float(np.median(x)) / 100.0  # 100 MHz ticks -> us
-    res = {"pops": int(len(t)), "stats": {k: st[k] for k in ("engine_pops", "engine_launches", "engine_workers",
+    res = {"pops": int(len(t)), "workers": a.workers, "groups": a.groups, "all_stats": {k: (v if isinstance(v, (int, float)) else str(v)) for k, v in st.items()}, "stats": {k: st[k] for k in ("engine_pops", "engine_launches", "engine_workers",
                                                              "alloc_device_s", "batched_pops", "host_wait_s")}}
     per = {}
     per["period"] = us(np.diff(t[:, 0])[cont])
@@ -79,23 +80,44 @@ def main():
         per["final: package flag (22) - placer start (0)"] = us((t[:, 22] - t[:, 0])[fin])
         per["final: desc(20)->merged(21)"] = us((t[:, 21] - t[:, 20])[fin])
         per["final: merged(21)->flag(22)"] = us((t[:, 22] - t[:, 21])[fin])
-    per["merger0 published (26) - placer start (0)"] = us(t[:, 26] - t[:, 0])
-    per["merger0 lists in (25) - placer start (0)"] = us(t[:, 25] - t[:, 0])
+    mg = np.all(t[:, [24, 25, 26]] > 0, axis=1)
+    if mg.any():
+        per["merger0 published (26) - placer start (0)"] = us((t[:, 26] - t[:, 0])[mg])
+        per["merger0 lists in (25) - placer start (0)"] = us((t[:, 25] - t[:, 0])[mg])
+        per["merger0 desc(24)->lists in(25)"] = us((t[:, 25] - t[:, 24])[mg])
+        per["merger0 lists in(25)->pub(26)"] = us((t[:, 26] - t[:, 25])[mg])
+        per["merger0 pub(26)->counts(27)"] = us((t[:, 27] - t[:, 26])[mg])
     per["worker0 published (13) - placer start (0)"] = us(t[:, 13] - t[:, 0])
     per["worker0 desc(10)->done(11)"] = us(t[:, 11] - t[:, 10])
     per["worker0 done(11)->eval(12)"] = us(t[:, 12] - t[:, 11])
     per["worker0 eval(12)->pub(13)"] = us(t[:, 13] - t[:, 12])
+    w2 = np.all(t[:, [16, 17]] > 0, axis=1)
+    if w2.any():
+        per["worker0 eval(12)->merged256(16)"] = us((t[:, 16] - t[:, 12])[w2])
+        per["worker0 merged256(16)->cands p-2 seen(17)"] = us((t[:, 17] - t[:, 16])[w2])
+        per["worker0 cands seen(17)->pub(13)"] = us((t[:, 13] - t[:, 17])[w2])
+        per["worker0 cands p-2 seen(17,p) - placer P3(4,p-2)"] = us(
+            (t[2:, 17] - t[:-2, 4])[((pops[2:] - pops[:-2]) == 2) & w2[2:]])
     per["worker0 pub(13)->counts(14)"] = us(t[:, 14] - t[:, 13])
     per["worker0 counts(14) -> next desc(10)"] = us((t[1:, 10] - t[:-1, 14])[cont])
-    per["worker0 desc(p) - placer done(p-3)"] = us((t[3:, 10] - t[:-3, 7])[np.diff(pops, 3) == 3])
-    per["worker0 done-seen(11,p) - placer done(7,p-3)"] = us((t[3:, 11] - t[:-3, 7])[np.diff(pops, 3) == 3])
-    per["merger0 desc(24)->lists in(25)"] = us(t[:, 25] - t[:, 24])
-    per["merger0 lists in(25)->pub(26)"] = us(t[:, 26] - t[:, 25])
-    per["merger0 pub(26)->counts(27)"] = us(t[:, 27] - t[:, 26])
+    per["worker0 published (13, p) - placer P3 (4, p-2)"] = us((t[2:, 13] - t[:-2, 4])[(pops[2:] - pops[:-2]) == 2])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     res["median_us"] = {k: round(v, 3) for k, v in per.items()}
     stop = (t[:, 30] >> 8) & 0xff
     res["stop_hist"] = {int(k): int(v) for k, v in zip(*np.unique(stop, return_counts=True))}
+    # the whole session: placer starts of every pop (pop -> start), and where the time between them goes
+    t0all = t[:, 0]
+    span = (t0all[-1] - t0all[0]) / 100.0
+    dif = np.diff(t0all) / 100.0
+    big = np.argsort(dif)[-12:][::-1]
+    res["session"] = {"pops_seen": int(len(t0all)), "span_us": round(span, 1), "mean_us": round(span / max(1, len(t0all) - 1), 3),
+                      "largest_gaps": [(int(pops[i]), round(float(dif[i]), 1)) for i in big],
+                      "gaps_over_20us_total": round(float(dif[dif > 20].sum()), 1), "n_over_20": int((dif > 20).sum())}
+    per_all = np.diff(t[:, 0])[cont] / 100.0
+    res["period_us"] = {"mean": round(float(per_all.mean()), 3),
+                        "quantiles_10_50_90_99": [round(float(np.quantile(per_all, q)), 2) for q in (0.1, 0.5, 0.9, 0.99)],
+                        "gaps_over_20us": int((per_all > 20).sum()), "gap_time_over_20us": round(float(per_all[per_all > 20].sum()), 1)}
+    # placer waiting at the loop top for the package / descriptor (front done late): 7 -> next 0
     dec = (t[:, 6] - t[:, 5]) / 100.0
     res["decide_us_quantiles"] = [round(float(np.quantile(dec, q)), 2) for q in (0.1, 0.25, 0.5, 0.75, 0.9, 0.99)]
     print(json.dumps(res))

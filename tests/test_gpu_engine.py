@@ -96,11 +96,14 @@ def test_engine_c2_levels_only(engine, oracle_mod, kbgen_mod, tmp_path):
     assert got1 == exp and np.array_equal(ns1, ns)
 
 
-def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path):
+@pytest.mark.parametrize("speculate", [2, 0])
+def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path, speculate):
     """A crowded cluster: many pops end on a task with no node, so the gang
     close messages carry the FitDelta histograms the engine counts (workers'
     counts without the previous pops' candidates, the placer's re-evaluated
-    ones) — equal to the faithful restatement's."""
+    ones) — equal to the faithful restatement's.  speculate 0: the host sends
+    the next descriptor only after such a pop's results (the counts it reads
+    must not wait for it)."""
     GI = 1 << 30
     rng = np.random.default_rng(9400)
     c = kbgen_mod.Cluster()
@@ -121,7 +124,9 @@ def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path):
     p = c.write(str(tmp_path / "u.kbs"))
     exp = oracle_mod.ref_allocate(p).as_list()
     exp_close = oracle_mod.ref_gang_close(p)
-    got, ns, st, close = _run(engine, p)
+    t0 = time.time()
+    got, ns, st, close = _run(engine, p, speculate=speculate)
+    assert time.time() - t0 < 20
     assert got == exp
     assert close == exp_close and len(close) > 5
     assert st["unassigned_pops"] > 5 and st["engine_pops"] > 20
