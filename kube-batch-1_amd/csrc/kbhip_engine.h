@@ -32,22 +32,23 @@ constexpr int kEngListWords = 136;  // a list: 128 tagged keys + 4 tagged counts
 constexpr int kEngMaxNpb = 8192;  // nodes per worker block
 constexpr int kEngWorkersMax = 512;
 
-// The final merger's package for pop p (slot p % kEngSlots): the pop's
-// descriptor and task class, and the top 128 keys of the group lists with
-// every entry's node row and its node-affinity weight and depth-1 score for
-// the pop's class, field-major (word f of entry e at w[f][e]): 0 key, 1..28
-// the Row (kbhip_eval.h, as 32-bit words), 29 flags, 30 na, 31 s1.  Every
-// word is a self-tagged granule {p << 32 | value} (one sc1 store each): the
-// placer takes the package once every tag reads p.
-constexpr int kEngPkgN = 128, kEngPkgFields = 32, kEngPkgHdr = 64;
+// The final merger's package for pop p (slot p % kEngSlots): the top 128
+// keys of the group lists with every entry's node row and its node-affinity
+// weight and depth-1 score for the pop's class, field-major (word f of entry
+// e at w[f][e]): 0 key, 1..28 the Row (kbhip_eval.h, as 32-bit words), 29
+// flags, 30 na, 31 s1.  Every word is a self-tagged granule {p << 32 | value}
+// (one sc1 store each): the placer takes the package once every tag reads p.
+constexpr int kEngPkgN = 128, kEngPkgFields = 32;
 enum : int { kPkKey = 0, kPkRow = 1, kPkFlags = 29, kPkNa = 30, kPkS1 = 31 };
 struct EngPkg {
-    uint64_t hdr[kEngPkgHdr];  // 0..7 the descriptor words, 8.. the TaskClass words
     uint64_t w[kEngPkgFields][kEngPkgN];
 };
 
 // Descriptor words (each {seq << 32 | value}, self-tagged: a reader takes a
-// descriptor once all eight tags read its sequence number).
+// descriptor once all kEngDescWords tags read its sequence number): the pop's
+// arguments, then the words of its TaskClass from kEngDescClass on (every
+// block that reads the descriptor has the class in the same round trip).
+constexpr int kEngDescWords = 64, kEngDescClass = 8;
 enum : int { kDwCls = 0, kDwFlags, kDwMinAvail, kDwReady, kDwEpochSlot, kDwKbase, kDwKshift, kDwKidxmax };
 // kDwFlags: m | gang << 8 | ent32 << 9 | op << 12
 enum : uint32_t { kEngOpPop = 0, kEngOpExit = 1 };
@@ -58,7 +59,7 @@ struct EngCtl {
     uint32_t pad0[31];
     uint32_t err;   // first error (kEngErr*), 0: none; every wait gives up once it is set
     uint32_t pad1[31];
-    uint64_t desc[kEngRing][8];     // descriptors, slot seq % kEngRing
+    uint64_t desc[kEngRing][kEngDescWords];  // descriptors, slot seq % kEngRing
     uint64_t cands[kEngSlots][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}
 };
 enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3 };
@@ -69,7 +70,7 @@ struct EngArgs {
     uint64_t* blists;          // [kEngSlots][nw][kEngListWords] worker lists (+ 2 count words)
     uint64_t* glists;          // [kEngSlots][ng][kEngListWords] group lists (+ 4 count words)
     EngPkg* pkg;               // [kEngSlots] the final merger's packages
-    const uint64_t* hring;     // [kEngHostRing][8] pinned host descriptors (device view)
+    const uint64_t* hring;     // [kEngHostRing][kEngDescWords] pinned host descriptors (device view)
     uint64_t* hexit;           // pinned host word: {exit seq | idle << 40 | 1 << 41} when the engine ends
     void* out;                 // result slots (PopOut, pinned host memory, device view)
     uint32_t first;            // the first pop of this launch (earlier pops are written back)

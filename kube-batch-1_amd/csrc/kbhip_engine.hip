@@ -64,6 +64,34 @@ __device__ __forceinline__ int eng_lane() {
     return l;
 }
 
+// A wave-uniform copy of v through readfirstlane (scalar registers): the
+// evaluation functions read the task class field by field, from LDS one
+// dependent access after another otherwise.
+template <typename T>
+__device__ __forceinline__ T eng_uniform(const T& v) {
+    static_assert(sizeof(T) % 4 == 0, "dwords");
+    T r;
+    const uint32_t* s = (const uint32_t*)&v;
+    uint32_t* d = (uint32_t*)&r;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); ++i) d[i] = (uint32_t)__builtin_amdgcn_readfirstlane((int)s[i]);
+    return r;
+}
+
+// A descriptor's TaskClass (words kEngDescClass.. of w, LDS; or of x, one
+// descriptor word per lane) in scalar registers.
+__device__ __forceinline__ TaskClass eng_class(const uint32_t* w) {
+    return eng_uniform(*(const TaskClass*)(w + kEngDescClass));
+}
+__device__ __forceinline__ TaskClass eng_class_x(uint32_t x) {
+    TaskClass c;
+    uint32_t* d = (uint32_t*)&c;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(TaskClass) / 4); ++i)
+        d[i] = (uint32_t)__builtin_amdgcn_readlane((int)x, kEngDescClass + i);
+    return c;
+}
+
 // The pop's descriptor as a block sees it (from the device ring).
 struct EngDesc {
     uint32_t op, cls, m, gang, ent32, min_avail, ready, epoch, slot;
@@ -102,15 +130,16 @@ __device__ __forceinline__ PopArgs eng_args(const EngDesc& d) {
     return a;
 }
 
-// Wave 0: wait for descriptor p in the device ring, leave its words in w[8] (LDS).
+// Wave 0: wait for descriptor p in the device ring, leave its words in
+// w[kEngDescWords] (LDS).
 __device__ __forceinline__ bool eng_wait_desc(EngCtl* ctl, uint32_t p, uint32_t* w) {
     const int lane = threadIdx.x & 63;
-    const uint64_t* src = &ctl->desc[p % kEngRing][lane & 7];
+    const uint64_t* src = &ctl->desc[p % kEngRing][lane];
     EngWait wt(ctl, kEngDescTicks);
     for (;;) {
         const uint64_t x = ld_sc1(src);
-        if (__ballot(lane < 8 && (uint32_t)(x >> 32) != p) == 0) {
-            if (lane < 8) w[lane] = (uint32_t)x;
+        if (__ballot((uint32_t)(x >> 32) != p) == 0) {
+            w[lane] = (uint32_t)x;
             return true;
         }
         if (!wt.tick(kEngErrDesc)) return false;
@@ -127,10 +156,56 @@ __device__ __forceinline__ bool eng_wait_done(EngCtl* ctl, uint32_t want) {
     }
 }
 
+// Until the tag (high half) of the granule *w reads q: kPollDepth sc1 loads of
+// it in flight, one issued per check, so that the wave sees the store about
+// a round trip / kPollDepth after it lands rather than up to two round trips
+// (every lane loads the same word: one request).  false: gave up (EngWait).
+constexpr int kPollDepth = 8;
+__device__ __forceinline__ bool eng_poll_tag(EngCtl* ctl, const uint64_t* w, uint32_t q, uint64_t limit) {
+    uint64_t v[kPollDepth];
+#pragma unroll
+    for (int i = 0; i < kPollDepth; ++i) {
+        v[i] = ld_sc1(w);
+        __builtin_amdgcn_s_sleep(1);
+    }
+    EngWait wt(ctl, limit);
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < kPollDepth; ++i) {
+            if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v[i] >> 32)) == q) return true;
+            v[i] = ld_sc1(w);
+            if (!wt.tick()) return false;
+        }
+    }
+}
+
+// The same for one granule per lane (w: this lane's, null: none): until every
+// lane's tag has read q (tags only grow while a slot is in use).
+__device__ __forceinline__ bool eng_poll_tags(EngCtl* ctl, const uint64_t* w, uint32_t q, uint64_t limit) {
+    uint64_t v[kPollDepth];
+#pragma unroll
+    for (int i = 0; i < kPollDepth; ++i) {
+        v[i] = w ? ld_sc1(w) : ((uint64_t)q << 32);
+        __builtin_amdgcn_s_sleep(1);
+    }
+    bool seen = false;
+    EngWait wt(ctl, limit);
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < kPollDepth; ++i) {
+            seen = seen || (uint32_t)(v[i] >> 32) == q;
+            if (__ballot(!seen) == 0) return true;
+            v[i] = (w && !seen) ? ld_sc1(w) : ((uint64_t)q << 32);
+            if (!wt.tick()) return false;
+        }
+    }
+}
+
 // Wave 0: candidate `lane` of pop q (-1: none), waiting for the granules.
 __device__ __forceinline__ bool eng_wait_cands(EngCtl* ctl, uint32_t q, int* node) {
     const int lane = threadIdx.x & 63;
     const uint64_t* src = &ctl->cands[q % kEngSlots][lane];
+    if (!eng_poll_tag(ctl, &ctl->cands[q % kEngSlots][0], q, kEngWaitTicks)) return false;
     EngWait wt(ctl, kEngWaitTicks);
     for (;;) {
         const uint64_t x = ld_sc1(src);
@@ -216,14 +291,13 @@ struct EngWorkerLds {
     uint32_t out[128];                     // the published top 128 (late exclusion)
     uint32_t skip[kEngMaxNpb / 32];        // pop p-3's (then also p-2's) candidates among this block's nodes
     uint8_t fb[2][kEngMaxNpb];             // FitDelta bits of pops p (p % 2) and p-1
-    uint32_t desc[8];
+    alignas(16) uint32_t desc[kEngDescWords];
     uint32_t fitb[2][4];                   // FitDelta counts of pops p (p % 2) and p-1
     int ok;
 };
 struct EngMergerLds {
     uint32_t wl[kPopThreads / 64][64], wl2[kPopThreads / 64][64];
-    uint32_t desc[8];
-    TaskClass cls;  // the final merger: the pop's class (na, depth-1 scores)
+    alignas(16) uint32_t desc[kEngDescWords];
     int ok;
 };
 // The placer's rows: four pops' candidates (slot 64 * (pop % 4) + lane) and
@@ -247,8 +321,9 @@ struct EngPlacerLds {
     uint8_t x2use[64], x3use[64];  // pop p-2's candidate not p-1's; pop p-3's neither
     int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
-    uint32_t desc[2][8];         // pop q's descriptor (q % 2)
-    TaskClass cls[2];            // pop q's task class (q % 2)
+    alignas(16) uint32_t desc[2][kEngDescWords];  // pop q's descriptor and class (q % 2)
+    alignas(16) uint32_t ndesc[kEngDescWords];    // pop ndesc_seq's, prefetched during P2 (a front reads it)
+    int ndesc_seq;
     uint64_t gran[64];           // the pop's result granules (0: none), stored to the host by wave 5
     uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
@@ -320,12 +395,12 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
             // for a descriptor the host sends only after that placement's results)
             bool ok = true;
             {
-                const uint64_t* src = &ctl->desc[p % kEngRing][lane & 7];
+                const uint64_t* src = &ctl->desc[p % kEngRing][lane];
                 EngWait wt(ctl, kEngDescTicks);
                 for (;;) {
                     const uint64_t x = ld_sc1(src);
-                    if (__ballot(lane < 8 && (uint32_t)(x >> 32) != p) == 0) {
-                        if (lane < 8) L.desc[lane] = (uint32_t)x;
+                    if (__ballot((uint32_t)(x >> 32) != p) == 0) {
+                        L.desc[lane] = (uint32_t)x;
                         break;
                     }
                     if (cpub + 1 < p) {
@@ -372,7 +447,7 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
         const EngDesc d = eng_decode(L.desc);
         if (d.op != kEngOpPop) return;
         const PopArgs a = eng_args(d);
-        const TaskClass& c = t.classes[__builtin_amdgcn_readfirstlane((int)d.cls)];
+        const TaskClass c = eng_class(L.desc);
         // 2. evaluate, one node per thread and chunk; each wave keeps its top 256
         uint32_t al[4] = {0, 0, 0, 0};
         for (int base = 0; base < cnt; base += kPopThreads) {
@@ -400,16 +475,19 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
             bool ok = true;
             int node = -1;
             if (tb >= 0) ETL(A, p, 16);
+            bool any_own = false;
             if (p >= A.first + 2) {
                 ok = eng_wait_cands(ctl, p - 2, &node);
                 if (tb >= 0) ETL(A, p, 17);
                 const int o = node - lo;
-                if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
-                if (ok) eng_fit_drop(L, set, node, lo, cnt);
+                const bool own = ok && node >= 0 && o >= 0 && o < cnt;
+                if (own) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
+                any_own = __ballot(own) != 0;
+                if (ok && any_own) eng_fit_drop(L, set, node, lo, cnt);
             }
             int run = 0;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int k = 0; k < (any_own ? 4 : 0); ++k) {
                 const uint32_t v = L.wl[k][0][lane];
                 bool keep = v != 0;
                 if (keep) {
@@ -422,16 +500,22 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                 if (keep && pos < 128) L.out[pos] = v;
                 run += __popcll(m);
             }
-            if (lane >= run) L.out[lane] = 0;
-            if (64 + lane >= run) L.out[64 + lane] = 0;
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
+            uint32_t o0 = L.wl[0][0][lane], o1 = L.wl[1][0][lane];  // (none of them: the first 128)
+            if (any_own) {
+                if (lane >= run) L.out[lane] = 0;
+                if (64 + lane >= run) L.out[64 + lane] = 0;
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+                o0 = L.out[lane];
+                o1 = L.out[64 + lane];
+            }
             if (ok) {
                 uint64_t* dst = A.blists + ((size_t)(p % kEngSlots) * A.nw + b) * kEngListWords;
-                st_sc1(&dst[lane], ((uint64_t)p << 32) | L.out[lane]);
-                st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.out[64 + lane]);
+                st_sc1(&dst[lane], ((uint64_t)p << 32) | o0);
+                st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | o1);
             }
             if (tb >= 0) ETL(A, p, tb + 3);
+            if (b == A.nw - 1) ETL(A, p, 18);
             if (ok && cpub + 1 < p) {
                 eng_fit_drop(L, pset, node, lo, cnt);
                 eng_fit_publish(A, L, p - 1, b);
@@ -465,13 +549,19 @@ __device__ __forceinline__ bool eng_merge_lists(EngCtl* ctl, const uint64_t* src
         for (;;) {
             bool miss = false;
 #pragma unroll
+            for (int q = 0; q < kQ; ++q) miss |= __ballot((uint32_t)(v0[q] >> 32) != p || (uint32_t)(v1[q] >> 32) != p) != 0;
+            if (!miss) break;
+            // not all there: wait on the lists' last granules (lanes 2q, 2q + 1: list q's; few
+            // bytes, several loads in flight), then reload what is missing
+            const int li = lane >> 1;
+            const uint64_t* sl = li == 0 ? s[0] : li == 1 ? s[1] : li == 2 ? s[2] : li == 3 ? s[3] : nullptr;
+            if (!eng_poll_tags(ctl, sl ? &sl[(lane & 1) ? 127 : 63] : nullptr, p, kEngWaitTicks)) { ok = false; break; }
+#pragma unroll
             for (int q = 0; q < kQ; ++q) {
                 if (__ballot((uint32_t)(v0[q] >> 32) != p || (uint32_t)(v1[q] >> 32) != p) == 0) continue;
-                miss = true;
                 v0[q] = ld_sc1(&s[q][lane]);
                 v1[q] = ld_sc1(&s[q][64 + lane]);
             }
-            if (!miss) break;
             if (!wt.tick()) { ok = false; break; }
         }
         if (ok)
@@ -484,16 +574,65 @@ __device__ __forceinline__ bool eng_merge_lists(EngCtl* ctl, const uint64_t* src
 // ---------------------------------------------------------------------------
 // merger of group g
 // ---------------------------------------------------------------------------
+// Wave 0 of merger g: pop q's group FitDelta counts — lane i reads worker
+// g + i * ng's two count words — summed and published.  block: wait for every
+// worker's words; else one attempt (false: some not there yet).
+__device__ __forceinline__ bool eng_group_counts(const EngArgs& A, int g, int cg, uint32_t q, bool block, bool* ok) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    const uint64_t* src0 = A.blists + (size_t)(q % kEngSlots) * A.nw * kEngListWords;
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+    for (int i0 = 0; i0 < cg; i0 += 64) {
+        const int i = i0 + lane;
+        const uint64_t* s = i < cg ? src0 + (size_t)(g + i * A.ng) * kEngListWords + 128 : nullptr;
+        uint64_t x0 = s ? ld_sc1(&s[0]) : ((uint64_t)q << 32), x1 = s ? ld_sc1(&s[1]) : ((uint64_t)q << 32);
+        EngWait wt(ctl, kEngWaitTicks);
+        while (__ballot((uint32_t)(x0 >> 32) != q || (uint32_t)(x1 >> 32) != q) != 0) {
+            if (!block) return false;
+            if (!wt.tick()) { *ok = false; return false; }
+            if (s) { x0 = ld_sc1(&s[0]); x1 = ld_sc1(&s[1]); }
+        }
+        const uint32_t y0 = (uint32_t)x0, y1 = (uint32_t)x1;  // two 16-bit counts per word
+        t0 += wave_sum_u32(y0 & 0xffff);
+        t1 += wave_sum_u32(y0 >> 16);
+        t2 += wave_sum_u32(y1 & 0xffff);
+        t3 += wave_sum_u32(y1 >> 16);
+    }
+    uint64_t* dst = A.glists + ((size_t)(q % kEngSlots) * A.ng + g) * kEngListWords;
+    if (lane < 4) st_sc1(&dst[128 + lane], ((uint64_t)q << 32) | (lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? t2 : t3));
+    return true;
+}
+
+// Pop p's group list; pop p-1's group counts (complete once the workers know
+// pop p-2's candidates: published during the descriptor wait if they come
+// first — a placement whose task found no node reads them, and the host may
+// send pop p's descriptor only after its results — else after the list).
 __device__ __forceinline__ void eng_merger(const EngArgs& A, EngMergerLds& L, int g) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     const int cg = (A.nw - g + A.ng - 1) / A.ng;  // workers of the group: g, g + ng, ...
     if (threadIdx.x == 0) L.ok = 1;
+    uint32_t cpub = A.first - 1;  // wave 0: the last pop whose group counts are published
     for (uint32_t p = A.first;; ++p) {
         __syncthreads();  // the previous pop done (wave 0 cleared L.ok if it failed)
         if (!L.ok) return;
         if (wave == 0) {
-            const bool ok = eng_wait_desc(ctl, p, L.desc);
+            bool ok = true;
+            const uint64_t* src = &ctl->desc[p % kEngRing][lane];
+            EngWait wt(ctl, kEngDescTicks);
+            for (;;) {
+                const uint64_t x = ld_sc1(src);
+                if (__ballot((uint32_t)(x >> 32) != p) == 0) {
+                    L.desc[lane] = (uint32_t)x;
+                    break;
+                }
+                if (cpub + 1 < p && eng_group_counts(A, g, cg, p - 1, false, &ok)) cpub = p - 1;
+                if (!wt.tick(kEngErrDesc)) { ok = false; break; }
+            }
+            if (ok && eng_decode(L.desc).op != kEngOpPop && cpub + 1 < p) {  // the run ends
+                eng_group_counts(A, g, cg, p - 1, true, &ok);
+                cpub = p - 1;
+            }
             if (lane == 0) L.ok = ok;
             if (g == 0) ETL(A, p, 24);
         }
@@ -512,26 +651,12 @@ __device__ __forceinline__ void eng_merger(const EngArgs& A, EngMergerLds& L, in
             st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
             st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
             if (g == 0) ETL(A, p, 26);
-            // the group's FitDelta counts: lane i reads worker g + i * ng's two count words
-            uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
-            for (int i0 = 0; i0 < cg && ok; i0 += 64) {
-                const int i = i0 + lane;
-                const uint64_t* s = i < cg ? src0 + (size_t)(g + i * A.ng) * kEngListWords + 128 : nullptr;
-                uint64_t x0 = s ? ld_sc1(&s[0]) : ((uint64_t)p << 32), x1 = s ? ld_sc1(&s[1]) : ((uint64_t)p << 32);
-                EngWait wt(ctl, kEngWaitTicks);
-                while (__ballot((uint32_t)(x0 >> 32) != p || (uint32_t)(x1 >> 32) != p) != 0) {
-                    if (!wt.tick()) { ok = false; break; }
-                    if (s) { x0 = ld_sc1(&s[0]); x1 = ld_sc1(&s[1]); }
-                }
-                const uint32_t y0 = (uint32_t)x0, y1 = (uint32_t)x1;  // two 16-bit counts per word
-                t0 += wave_sum_u32(y0 & 0xffff);
-                t1 += wave_sum_u32(y0 >> 16);
-                t2 += wave_sum_u32(y1 & 0xffff);
-                t3 += wave_sum_u32(y1 >> 16);
+            if (g == A.ng - 1) ETL(A, p, 23);
+            if (cpub + 1 < p) {
+                eng_group_counts(A, g, cg, p - 1, true, &ok);
+                cpub = p - 1;
             }
             if (!ok && lane == 0) L.ok = 0;
-            if (ok && lane < 4)
-                st_sc1(&dst[128 + lane], ((uint64_t)p << 32) | (lane == 0 ? t0 : lane == 1 ? t1 : lane == 2 ? t2 : t3));
             if (g == 0) ETL(A, p, 27);
         }
     }
@@ -554,10 +679,6 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
         if (!L.ok) return;
         if (wave == 0) {
             const bool ok = eng_wait_desc(ctl, p, L.desc);
-            const EngDesc d0 = eng_decode(L.desc);
-            if (ok && d0.op == kEngOpPop && lane < (int)(sizeof(TaskClass) / 4))
-                ((uint32_t*)&L.cls)[lane] =
-                    ((const uint32_t*)&t.classes[__builtin_amdgcn_readfirstlane((int)d0.cls)])[lane];
             if (lane == 0) L.ok = ok;
             ETL(A, p, 20);
         }
@@ -566,23 +687,15 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
         const EngDesc d = eng_decode(L.desc);
         if (d.op != kEngOpPop) return;
         const PopArgs a = eng_args(d);
-        const TaskClass& c = L.cls;
+        const TaskClass c = eng_class(L.desc);
         uint32_t a0 = 0, a1 = 0;
         bool ok = true;
         if (A.ng == 0) {  // no merger level: the worker lists
             ok = eng_merge_lists(ctl, A.blists + (size_t)(p % kEngSlots) * A.nw * kEngListWords, 0, 1, A.nw, p, &a0,
                                  &a1);
-        } else if (wave < A.ng) {
-            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + wave) * kEngListWords;
-            uint64_t v0 = ld_sc1(&s[lane]), v1 = ld_sc1(&s[64 + lane]);
-            EngWait wt(ctl, kEngWaitTicks);
-            while (__ballot((uint32_t)(v0 >> 32) != p || (uint32_t)(v1 >> 32) != p) != 0) {
-                if (!wt.tick()) { ok = false; break; }
-                v0 = ld_sc1(&s[lane]);
-                v1 = ld_sc1(&s[64 + lane]);
-            }
-            a0 = (uint32_t)v0;
-            a1 = (uint32_t)v1;
+        } else {
+            ok = eng_merge_lists(ctl, A.glists + (size_t)(p % kEngSlots) * A.ng * kEngListWords, 0, 1, A.ng, p, &a0,
+                                 &a1);
         }
         if (!ok) L.ok = 0;
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
@@ -612,11 +725,6 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
             }
 #pragma unroll
             for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
-        } else if (wave == 2) {  // the header: descriptor and class words
-            uint32_t v = 0;
-            if (lane < 8) v = L.desc[lane];
-            else if (lane < 8 + (int)(sizeof(TaskClass) / 4)) v = ((const uint32_t*)&L.cls)[lane - 8];
-            st_sc1(&pk->hdr[lane], tag | v);
         }
         if (wave == 0) ETL(A, p, 22);
     }
@@ -626,7 +734,7 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
 // placer
 // ---------------------------------------------------------------------------
 static_assert(sizeof(Row) == 4 * (kPkFlags - kPkRow), "the package carries a Row as 28 32-bit words");
-static_assert(sizeof(TaskClass) / 4 + 8 <= kEngPkgHdr, "the package header carries the descriptor and class");
+static_assert(kEngDescClass + sizeof(TaskClass) / 4 <= kEngDescWords, "a descriptor carries its class");
 
 // The placer's wave 0 after the decision: the FitDelta histogram of a task
 // that found no node (the sweep's counts from the group count words), the
@@ -730,24 +838,14 @@ __device__ __forceinline__ void eng_host_out(const EngArgs& A, EngPlacerLds& L, 
 // pop q-1's placement still reads the row cache's na / s1 of these slots;
 // pop q's P2 moves the ones that count (x2use / x3use) there.
 __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& nc, const DevTables& t,
-                                               const EngArgs& A, EngPlacerLds& L, uint32_t q, int set, int role) {
+                                               EngPlacerLds& L, uint32_t q, uint32_t dw, int set, int role) {
     const int lane = eng_lane();
-    EngCtl* ctl = A.ctl;
-    const uint64_t* src = &ctl->desc[q % kEngRing][lane & 7];  // (the dispatcher forwards descriptors ahead)
-    uint64_t x = 0;
-    EngWait wt(ctl, kEngDescTicks);
-    for (;;) {
-        x = ld_sc1(src);
-        if (__ballot(lane < 8 && (uint32_t)(x >> 32) != q) == 0) break;
-        if (!wt.tick(kEngErrDesc)) return;
-    }
     uint32_t w[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, i);
+    for (int i = 0; i < 8; ++i) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)dw, i);
     const EngDesc d = eng_decode(w);
-    if (d.op != kEngOpPop) return;
     const PopArgs a = eng_args(d);
-    const TaskClass& c = t.classes[d.cls];
+    const TaskClass c = eng_class_x(dw);
     const int ring = set == 0 ? (int)((q + 2) % 4) : (int)((q + 1) % 4);
     const int node = L.xn[ring][lane];
     const int sl = 64 * ring + lane;
@@ -794,6 +892,36 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
     const int lane = threadIdx.x & 63;
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
+    if (wave == 0) return;
+    const bool loads = wave == 3 || wave == 4 || wave == 6 || wave == 7;
+    const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block of a loading wave
+    const EngPkg* pk = A.pkg + (q % kEngSlots);
+    // the package's loads first (in flight during the rest; reloaded below if early)
+    uint64_t v[16];
+    if (loads)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+    // pop q's descriptor and class (prefetched during P2, else from the ring); wave 3
+    // leaves them in L.desc.  An exit has no package.
+    uint32_t dw;
+    if (__hip_atomic_load(&L.ndesc_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q) {
+        dw = L.ndesc[lane];
+    } else {
+        const uint64_t* src = &ctl->desc[q % kEngRing][lane];
+        EngWait wt(ctl, kEngDescTicks);
+        uint64_t x = 0;
+        for (;;) {
+            x = ld_sc1(src);
+            if (__ballot((uint32_t)(x >> 32) != q) == 0) break;
+            if (!wt.tick(kEngErrDesc)) {
+                if (wave == 3 && lane == 0) L.ok = 0;
+                return;
+            }
+        }
+        dw = (uint32_t)x;
+    }
+    if (wave == 3) L.desc[q % 2][lane] = dw;
+    if (((uint32_t)__builtin_amdgcn_readlane((int)dw, kDwFlags) >> 12 & 0xf) != kEngOpPop) return;
     if (wave == 2) {
         const int r1 = (int)((q + 3) % 4), r2 = (int)((q + 2) % 4), r3 = (int)((q + 1) % 4);
         for (int h = lane; h < EngRowCache::kHashN; h += 64) rc.hkey[h] = -1;
@@ -813,33 +941,25 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
         L.x3use[lane] = use3;
         if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
-        eng_front_eval(cf, nc, t, A, L, q, 1, 2);
+        eng_front_eval(cf, nc, t, L, q, dw, 1, 2);
         return;
     }
-    if (wave == 1 || wave == 5) { eng_front_eval(cf, nc, t, A, L, q, 0, wave == 1 ? 0 : 1); return; }
-    if (!(wave == 3 || wave == 4 || wave == 6 || wave == 7)) return;
-    if (wave != 4) eng_front_eval(cf, nc, t, A, L, q, wave == 6 ? 0 : 1, wave == 7 ? 0 : wave == 3 ? 1 : 2);
-    const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block
-    const EngPkg* pk = A.pkg + (q % kEngSlots);
-    uint64_t v[16];
-    uint64_t h = (uint64_t)q << 32;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
-    if (k == 0) h = ld_sc1(&pk->hdr[lane]);
+    if (wave == 1 || wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 0, wave == 1 ? 0 : 1); return; }
+    if (wave != 4) eng_front_eval(cf, nc, t, L, q, dw, wave == 6 ? 0 : 1, wave == 7 ? 0 : wave == 3 ? 1 : 2);
     bool got = false;
-    EngWait wt(ctl, kEngDescTicks);  // (a package waits as long as its pop's descriptor may)
+    EngWait wt(ctl, kEngWaitTicks);
     for (;;) {
-        bool miss = (uint32_t)(h >> 32) != q;
+        bool miss = false;
 #pragma unroll
         for (int i = 0; i < 16; ++i) miss |= (uint32_t)(v[i] >> 32) != q;
         if (__ballot(miss) == 0) { got = true; break; }
-        const uint64_t dw = ld_sc1(&ctl->desc[q % kEngRing][kDwFlags]);
-        if ((uint32_t)(dw >> 32) == q && (((uint32_t)dw >> 12) & 0xf) != kEngOpPop) break;  // an exit
+        // the last granules of this wave's fields (each half written by one of the final
+        // merger's waves), polled with loads in flight; then one reload
+        if (!eng_poll_tags(ctl, lane < 2 ? &pk->w[8 * k + 7][lane ? 127 : 63] : nullptr, q, kEngWaitTicks)) break;
         if (!wt.tick()) break;
 #pragma unroll
         for (int i = 0; i < 16; ++i)
             if ((uint32_t)(v[i] >> 32) != q) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
-        if (k == 0 && (uint32_t)(h >> 32) != q) h = ld_sc1(&pk->hdr[lane]);
     }
     if (got) {
         const int base = kEngStage + kEngPkgN * (int)(q % 2);
@@ -853,14 +973,10 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
             else if (f == kPkNa) rc.na[sl] = (int32_t)x;
             else rc.s1[sl] = (int32_t)x;
         }
-        if (k == 0) {
+        if (k == 0)
             for (int w = 0; w < 4; ++w) { rc.pw[base + lane][w] = 0; rc.pw[base + 64 + lane][w] = 0; }
-            if (lane < 8) L.desc[q % 2][lane] = (uint32_t)h;
-            else if (lane < 8 + (int)(sizeof(TaskClass) / 4)) ((uint32_t*)&L.cls[q % 2])[lane - 8] = (uint32_t)h;
-        }
-    } else if (k == 0) {  // the exit descriptor, or an error
-        const bool ok = eng_wait_desc(ctl, q, L.desc[q % 2]);
-        if (!ok && lane == 0) L.ok = 0;
+    } else if (k == 0 && lane == 0) {  // a wait gave up (the error is recorded)
+        L.ok = 0;
     }
 }
 
@@ -884,7 +1000,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
-    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready = 0; }
+    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready = 0; L.ndesc_seq = 0; }
     __syncthreads();
     eng_front(cf, nc, t, A, L, A.first, wave);
     uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
@@ -900,7 +1016,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             return;
         }
         const PopArgs a = eng_args(d);
-        const TaskClass& c = L.cls[p % 2];
+        const TaskClass& c = *(const TaskClass*)&L.desc[p % 2][kEngDescClass];
         if (wave == 0) {
             ETL(A, p, 0);
             if (lane == 0 && A.tl) A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 31] = p;
@@ -930,6 +1046,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         } else if (wave <= 3) {  // pop p-1's candidates: wave 1 their keys (sorted) and FitDelta
             // bits, waves 2 / 3 their depth-1 scores after an Allocate / a Pipeline; the key
             // wave then keeps the one its key's kind calls for
+            const TaskClass c = eng_class(L.desc[p % 2]);
             const int node = L.xn[r1][lane];
             const int sl = 64 * r1 + lane;
             const uint64_t pw[4] = {0, 0, 0, 0};
@@ -972,6 +1089,13 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 if (wave == 2) ETL(A, p, 19);
                 __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the scores are in LDS before the count
                 if (lane == 0) __hip_atomic_fetch_add(&L.s1_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (wave == 4) {  // pop p+1's descriptor, if the dispatcher has it (one attempt)
+            const uint64_t x = ld_sc1(&ctl->desc[(p + 1) % kEngRing][lane]);
+            if (__ballot((uint32_t)(x >> 32) != p + 1) == 0) {
+                L.ndesc[lane] = (uint32_t)x;
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                if (lane == 0) __hip_atomic_store(&L.ndesc_seq, (int)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         } else if (wave == 5 || wave == 6) {  // pops p-2 / p-3's candidates that count (the front's results)
             const int set = wave - 5;
@@ -1061,13 +1185,13 @@ __device__ __forceinline__ void eng_dispatch(const EngArgs& A) {
     for (;; ++s) {
         // the device ring slot of pop s - kEngRing is free once the placer finished pop s - 5
         if (s >= A.first + 5 && !eng_wait_done(ctl, s - 5)) break;
-        const uint64_t* src = A.hring + (size_t)(s % kEngHostRing) * 8 + (lane & 7);
+        const uint64_t* src = A.hring + (size_t)(s % kEngHostRing) * kEngDescWords + lane;
         uint64_t x = 0;
         uint64_t t0 = 0;
         bool got = false;
         for (uint32_t it = 0;; ++it) {
             x = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (__ballot(lane < 8 && (uint32_t)(x >> 32) != s) == 0) { got = true; break; }
+            if (__ballot((uint32_t)(x >> 32) != s) == 0) { got = true; break; }
             if ((it & 15) == 15) {
                 const uint64_t now = eng_now();
                 if (!t0) t0 = now;
@@ -1082,7 +1206,7 @@ __device__ __forceinline__ void eng_dispatch(const EngArgs& A) {
         // forward (an idle end becomes an exit descriptor at s)
         uint64_t v = x;
         if (!got) v = lane == kDwFlags ? (((uint64_t)s << 32) | ((uint64_t)kEngOpExit << 12)) : ((uint64_t)s << 32);
-        if (lane < 8) st_sc1(&ctl->desc[s % kEngRing][lane], v);
+        st_sc1(&ctl->desc[s % kEngRing][lane], v);
         ETL(A, s, 28);
         if (op != kEngOpPop) break;
     }

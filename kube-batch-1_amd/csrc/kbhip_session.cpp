@@ -581,7 +581,7 @@ struct Session {
     EngPkg* d_eng_pkg = nullptr;
     uint64_t* d_eng_bl = nullptr;
     uint64_t* d_eng_gl = nullptr;
-    uint64_t* h_eng = nullptr;  // pinned, mapped: [kEngHostRing][8] descriptor words, then the exit word
+    uint64_t* h_eng = nullptr;  // pinned, mapped: [kEngHostRing][kEngDescWords] descriptor words, then the exit word
     uint64_t* dv_eng = nullptr; // ... as the device sees it
     size_t h_eng_cap = 0;
     DevBuf b_eng_tl;            // option "engine_timeline": the engine's event stamps (kEngTlSlots pops)
@@ -675,8 +675,8 @@ struct Session {
     void release_device() {
         if (eng_running && h_eng) {  // the engine's exit descriptor, then the stream drains below
             const uint32_t sq = ++eng_seq;
-            for (int i = 0; i < 8; ++i)
-                __atomic_store_n(&h_eng[(sq % kEngHostRing) * 8 + i],
+            for (int i = 0; i < kEngDescWords; ++i)
+                __atomic_store_n(&h_eng[(sq % kEngHostRing) * kEngDescWords + i],
                                  ((uint64_t)sq << 32) | (i == kDwFlags ? (uint64_t)kEngOpExit << 12 : 0),
                                  __ATOMIC_RELEASE);
             eng_running = false;
@@ -2191,9 +2191,9 @@ static void eng_size(Session& S) {
     S.d_eng_gl = S.d_eng_bl + (size_t)kEngSlots * nw * kEngListWords;
     HIPCHK(hipMemsetAsync(d, 0, words * 8, S.stream));  // every tag 0: no pop has that sequence number
     if (!S.h_eng) {
-        S.h_eng = (uint64_t*)MemPool::get().take(MemPool::kPinnedMapped, (kEngHostRing * 8 + 8) * sizeof(uint64_t),
+        S.h_eng = (uint64_t*)MemPool::get().take(MemPool::kPinnedMapped, (kEngHostRing * kEngDescWords + 8) * sizeof(uint64_t),
                                                  &S.h_eng_cap);
-        std::memset(S.h_eng, 0, (kEngHostRing * 8 + 8) * sizeof(uint64_t));
+        std::memset(S.h_eng, 0, (kEngHostRing * kEngDescWords + 8) * sizeof(uint64_t));
         void* dv = nullptr;
         HIPCHK(hipHostGetDevicePointer(&dv, S.h_eng, 0));
         S.dv_eng = (uint64_t*)dv;
@@ -2217,11 +2217,11 @@ static bool eng_eligible(Session& S, int cls, const KeyFormat& kf) {
     return S.eng_nw > 0;
 }
 
-static uint64_t* eng_exit_word(Session& S) { return S.h_eng + kEngHostRing * 8; }
+static uint64_t* eng_exit_word(Session& S) { return S.h_eng + kEngHostRing * kEngDescWords; }
 
 static void eng_write(Session& S, uint32_t seq, const uint32_t* w) {
-    uint64_t* slot = S.h_eng + (size_t)(seq % kEngHostRing) * 8;
-    for (int i = 0; i < 8; ++i) __atomic_store_n(&slot[i], ((uint64_t)seq << 32) | w[i], __ATOMIC_RELEASE);
+    uint64_t* slot = S.h_eng + (size_t)(seq % kEngHostRing) * kEngDescWords;
+    for (int i = 0; i < kEngDescWords; ++i) __atomic_store_n(&slot[i], ((uint64_t)seq << 32) | w[i], __ATOMIC_RELEASE);
 }
 
 static void eng_start(Session& S) {
@@ -2233,7 +2233,7 @@ static void eng_start(Session& S) {
     A.glists = S.d_eng_gl;
     A.pkg = S.d_eng_pkg;
     A.hring = S.dv_eng;
-    A.hexit = S.dv_eng + kEngHostRing * 8;
+    A.hexit = S.dv_eng + kEngHostRing * kEngDescWords;
     A.out = S.d_out;
     A.first = S.eng_first;
     A.nw = S.eng_nw;
@@ -2277,7 +2277,9 @@ static bool eng_poll(Session& S) {
 static void eng_submit(Session& S, BatchLaunch& L, int cls, int m, int gang_mode, int min_avail, int ready_count,
                        const KeyFormat& kf) {
     if (S.eng_running) eng_poll(S);
-    uint32_t w[8];
+    uint32_t w[kEngDescWords] = {};
+    static_assert(kEngDescClass + sizeof(TaskClass) / 4 <= kEngDescWords, "the descriptor carries the class");
+    std::memcpy(w + kEngDescClass, &S.classes[cls], sizeof(TaskClass));
     w[kDwCls] = (uint32_t)cls;
     w[kDwFlags] = (uint32_t)m | ((uint32_t)(gang_mode ? 1 : 0) << 8) | (1u << 9) | (kEngOpPop << 12);
     w[kDwMinAvail] = (uint32_t)min_avail;
@@ -2305,7 +2307,7 @@ static void eng_submit(Session& S, BatchLaunch& L, int cls, int m, int gang_mode
 static void eng_stop(Session& S) {
     if (!S.eng_running) return;
     const uint32_t sq = ++S.eng_seq;
-    uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t w[kEngDescWords] = {};
     w[kDwFlags] = kEngOpExit << 12;
     eng_write(S, sq, w);
     for (;;) {

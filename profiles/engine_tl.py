@@ -80,6 +80,13 @@ def main():
         per["final: package flag (22) - placer start (0)"] = us((t[:, 22] - t[:, 0])[fin])
         per["final: desc(20)->merged(21)"] = us((t[:, 21] - t[:, 20])[fin])
         per["final: merged(21)->flag(22)"] = us((t[:, 22] - t[:, 21])[fin])
+    lw = t[:, 18] > 0
+    if lw.any():
+        per["last worker published (18) - worker0 published (13)"] = us((t[:, 18] - t[:, 13])[lw])
+        per["last worker published (18) - placer start (0)"] = us((t[:, 18] - t[:, 0])[lw])
+    lm = t[:, 23] > 0
+    if lm.any():
+        per["last merger published (23) - placer start (0)"] = us((t[:, 23] - t[:, 0])[lm])
     mg = np.all(t[:, [24, 25, 26]] > 0, axis=1)
     if mg.any():
         per["merger0 published (26) - placer start (0)"] = us((t[:, 26] - t[:, 0])[mg])
