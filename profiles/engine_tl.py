@@ -53,7 +53,7 @@ def main():
     order = np.argsort(pops)
     t = t[order]
     pops = pops[order]
-    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 19, 28]] > 0, axis=1)
+    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 19, 28]] > 0, axis=1)
     t = t[keep]
     pops = t[:, 31]
     cont = np.diff(pops) == 1
@@ -80,6 +80,11 @@ def main():
         per["final: package flag (22) - placer start (0)"] = us((t[:, 22] - t[:, 0])[fin])
         per["final: desc(20)->merged(21)"] = us((t[:, 21] - t[:, 20])[fin])
         per["final: merged(21)->flag(22)"] = us((t[:, 22] - t[:, 21])[fin])
+        f29 = fin & (t[:, 29] > 0)
+        if f29.any():
+            per["final: merged(21)->cands p-2 seen(29)"] = us((t[:, 29] - t[:, 21])[f29])
+            per["final: cands p-2 seen(29,p) - placer P3(4,p-2)"] = us(
+                (t[2:, 29] - t[:-2, 4])[((pops[2:] - pops[:-2]) == 2) & f29[2:]])
     lw = t[:, 18] > 0
     if lw.any():
         per["last worker published (18) - worker0 published (13)"] = us((t[:, 18] - t[:, 13])[lw])
@@ -98,6 +103,7 @@ def main():
     per["worker0 desc(10)->done(11)"] = us(t[:, 11] - t[:, 10])
     per["worker0 done(11)->eval(12)"] = us(t[:, 12] - t[:, 11])
     per["worker0 eval(12)->pub(13)"] = us(t[:, 13] - t[:, 12])
+    per["worker0 pub(13) -> next desc(10)"] = us((t[1:, 10] - t[:-1, 13])[cont])
     w2 = np.all(t[:, [16, 17]] > 0, axis=1)
     if w2.any():
         per["worker0 eval(12)->merged256(16)"] = us((t[:, 16] - t[:, 12])[w2])
@@ -105,8 +111,6 @@ def main():
         per["worker0 cands seen(17)->pub(13)"] = us((t[:, 13] - t[:, 17])[w2])
         per["worker0 cands p-2 seen(17,p) - placer P3(4,p-2)"] = us(
             (t[2:, 17] - t[:-2, 4])[((pops[2:] - pops[:-2]) == 2) & w2[2:]])
-    per["worker0 pub(13)->counts(14)"] = us(t[:, 14] - t[:, 13])
-    per["worker0 counts(14) -> next desc(10)"] = us((t[1:, 10] - t[:-1, 14])[cont])
     per["worker0 published (13, p) - placer P3 (4, p-2)"] = us((t[2:, 13] - t[:-2, 4])[(pops[2:] - pops[:-2]) == 2])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     res["median_us"] = {k: round(v, 3) for k, v in per.items()}
