@@ -160,8 +160,9 @@ def snapshot_path(args):
     return p
 
 
-def pmc_traffic():
-    """HBM bytes per k_pop_batch launch from the newest committed rocprofv3 PMC
+def pmc_traffic(engine=False):
+    """HBM bytes per k_pop_batch launch (engine: per pop of k_engine, whose one
+    dispatch serves a session's pops) from the newest committed rocprofv3 PMC
     summary (profiles/<tag>_summary.json: FETCH_SIZE x 2, the gfx950 correction
     of MI355X_MICROARCH.md).  PMC counters cannot be read inside a timed run,
     so this comes from the profiling pass of profiles/run_profile.sh."""
@@ -171,7 +172,9 @@ def pmc_traffic():
         with open(p) as f:
             d = json.load(f)
         for name, k in d.get("kernels", {}).items():
-            if name.startswith("kbhip::k_pop_batch") and "hbm_bytes_per_launch_corrected" in k:
+            if engine and name.startswith("kbhip::k_engine") and "hbm_bytes_per_pop_corrected" in k:
+                best = (k["hbm_bytes_per_pop_corrected"], os.path.basename(p))
+            elif not engine and name.startswith("kbhip::k_pop_batch") and "hbm_bytes_per_launch_corrected" in k:
                 best = (k["hbm_bytes_per_launch_corrected"], os.path.basename(p))
     return best
 
@@ -245,11 +248,21 @@ def sweep_roofline(buf, device, pods, n_tasks=512):
         ids = np.ascontiguousarray(pods[::step][:n_tasks], np.int32)
         s.time_sweeps(ids[:16])  # warm
         mean_us = s.time_sweeps(ids)
+        s.set_option("time_sweeps_cold", 1)
+        cold_ids = ids[:64]
+        cold_us = s.time_sweeps(cold_ids)
         nodes = s.stats()["nodes"]
     achieved = nodes * B_NODE / (mean_us * 1e-6) / 1e9 if mean_us > 0 else 0.0
+    cold_achieved = nodes * B_NODE / (cold_us * 1e-6) / 1e9 if cold_us > 0 else 0.0
     return {"kernel": "k_score_sweep (kbhip_sweep_scores)", "launches": int(len(ids)), "mean_us": mean_us,
             "bytes_per_launch": nodes * B_NODE, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
-            "timing": "HIP events around the back-to-back launches (kbhip_time_sweeps), / launches",
+            "timing": "HIP events around the back-to-back launches (kbhip_time_sweeps), / launches: the node "
+                      "columns (11.3 MB) stay in the 256 MB Infinity Cache between launches",
+            "cold": {"launches": int(len(cold_ids)), "mean_us": cold_us, "achieved": cold_achieved,
+                     "frac": cold_achieved / HBM_PEAK_GBS,
+                     "timing": "HIP events around each launch alone (option time_sweeps_cold): a 512 MB write "
+                               "before every launch evicts L2 and the Infinity Cache, so the columns come from HBM; "
+                               "the span includes the launch's dispatch and drain"},
             "note": "reads 113 B/node (SURVEY §8(d)); writes an 8-byte key per node (not counted)"}
 
 
@@ -331,7 +344,7 @@ def main():
             dist.destroy_process_group()
         return
     nodes = st_last["nodes"]
-    traffic = None if shard else pmc_traffic()
+    traffic = None if shard else pmc_traffic(st_last["engine_pops"] > 0)
     sweep = None if shard else sweep_roofline(buf, device, log0[0])
     nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
     # the hot kernel's mean duration: HIP events around every batched pop launch on the stream it runs on
@@ -378,19 +391,25 @@ def main():
         "roofline": {"kernel": kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,
-                     "traffic_source": f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per launch)"
-                     if traffic else None,
+                     "traffic_source": (f"profiles/{traffic[1]} (rocprofv3 FETCH_SIZE x2, bytes per "
+                                        f"{'pop' if engine_on else 'launch'})") if traffic else None,
                      "busy_period_us": period_us,
-                     "timing": "busy period = allocate's device span (HIP events on the engine streams around the "
-                               "allocate action, summed over the timed sessions) / batched pop launches: the launches "
-                               "overlap, so this is the device time each one adds; the sum over launches = the span",
-                     "span_us": launch_us, "span_frac": span_achieved / HBM_PEAK_GBS,
-                     "span_timing": f"each launch's own start-to-end span (HIP events around every "
-                                    f"{args.time_every}-th launch on its stream, {sweeps_n} launches): it includes the "
-                                    f"wait for the previous pop, so consecutive spans overlap",
+                     "timing": ("busy period = allocate's device span (HIP events on the session stream around the "
+                                "allocate action, summed over the timed sessions) / batched pops: the engine's one "
+                                "dispatch per session serves them all, each pop's nodes evaluated once")
+                     if engine_on else
+                     ("busy period = allocate's device span (HIP events on the engine streams around the "
+                      "allocate action, summed over the timed sessions) / batched pop launches: the launches "
+                      "overlap, so this is the device time each one adds; the sum over launches = the span"),
                      "bytes_per_launch": nodes_per_launch * B_NODE,
                      "sweep": sweep},
     }
+    if not engine_on:
+        out["roofline"]["span_us"] = launch_us
+        out["roofline"]["span_frac"] = span_achieved / HBM_PEAK_GBS
+        out["roofline"]["span_timing"] = (f"each launch's own start-to-end span (HIP events around every "
+                                          f"{args.time_every}-th launch on its stream, {sweeps_n} launches): it "
+                                          f"includes the wait for the previous pop, so consecutive spans overlap")
     if args.cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(path, args.cpu_seconds, log0)
         out["cpu_baseline"]["gpu_p50_session_ms"] = out["p50_session_ms"]

@@ -1,0 +1,42 @@
+#!/bin/bash
+# r05 measurement pass (each GPU step under its own limit, chained so that a
+# failure ends the script): the GPU suite (optional), the C4 bench line, the
+# engine timeline, rocprofv3 kernel stats of the bench, a FETCH_SIZE pass and
+# an SQ-counter pass (separate runs: counters never share a run with tracing
+# domains), then the cold standalone sweep: its kernel stats and FETCH_SIZE.
+# usage: bash profiles/r05_measure.sh TAG [tests=1]
+set -o pipefail
+TAG=${1:-r05}
+TESTS=${2:-1}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+if [ "$TESTS" = 1 ]; then
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+      > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+  tail -1 gpurun_out/${TAG}_pytest.log
+fi
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_bench.json \
+    2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+cat gpurun_out/${TAG}_bench.json
+timeout -k 10 200 python -u profiles/engine_tl.py --out gpurun_out/${TAG}_engine_tl.json > /dev/null 2>&1 || exit 1
+OUT=gpurun_out/prof_${TAG}
+mkdir -p $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
+    python3 bench.py --steps 2 --warmup 0 --cpu-baseline 0 > $OUT/bench_trace.json 2> $OUT/trace.err || exit 1
+timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --time-every 0 > $OUT/bench_pmc.json 2> $OUT/pmc.err || exit 1
+timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+    SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d $OUT/sq -o run --output-format csv -- \
+    python3 bench.py --steps 1 --warmup 0 --cpu-baseline 0 --time-every 0 > $OUT/bench_sq.json 2> $OUT/sq.err || exit 1
+python3 profiles/summarize.py $OUT ${TAG} gpurun_out > $OUT/summary.log 2>&1 || exit 1
+rm -rf $OUT/trace $OUT/pmc $OUT/sq
+# the cold standalone sweep
+C=gpurun_out/prof_${TAG}_cold
+mkdir -p $C
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $C/trace -o run --output-format csv -- \
+    python3 profiles/sweep_cold.py 64 > $C/probe_trace.json 2> $C/trace.err || exit 1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $C/pmc -o run --output-format csv -- \
+    python3 profiles/sweep_cold.py 64 > $C/probe_pmc.json 2> $C/pmc.err || exit 1
+python3 profiles/summarize.py $C ${TAG}_cold gpurun_out > $C/summary.log 2>&1 || exit 1
+rm -rf $C/trace $C/pmc
+echo done

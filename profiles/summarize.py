@@ -68,11 +68,23 @@ def main(src, tag, dest=None):
                 a = acc[short(row["Kernel_Name"])]
                 a[0] += float(row["Counter_Value"])
                 a[1] += 1
+        pops = None  # the persistent engine: one dispatch serves a session's pops (the PMC pass's bench line)
+        bj = os.path.join(src, "bench_pmc.json")
+        if os.path.exists(bj):
+            try:
+                with open(bj) as f:
+                    line = [ln for ln in f.read().splitlines() if ln.startswith("{")][-1]
+                pops = json.loads(line)["config"].get("engine_pops") or None
+            except (IndexError, ValueError, KeyError):
+                pops = None
         for k, (tot, n) in acc.items():
             d = out["kernels"].setdefault(k, {})
             d["fetch_size_kb_per_launch"] = tot / n
             d["hbm_bytes_per_launch_corrected"] = 2.0 * tot / n * 1024.0
             d["pmc_launches"] = n
+            if k.startswith("kbhip::k_engine") and pops:
+                d["engine_pops"] = pops
+                d["hbm_bytes_per_pop_corrected"] = 2.0 * tot * 1024.0 / pops
     sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
     if os.path.exists(sq_csv):  # occupancy / stall counters, per launch, with the kernel's resources
         acc = defaultdict(lambda: defaultdict(float))
