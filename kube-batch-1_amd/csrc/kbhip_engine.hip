@@ -693,9 +693,36 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
         if (A.ng == 0) {  // no merger level: the worker lists
             ok = eng_merge_lists(ctl, A.blists + (size_t)(p % kEngSlots) * A.nw * kEngListWords, 0, 1, A.nw, p, &a0,
                                  &a1);
-        } else {
-            ok = eng_merge_lists(ctl, A.glists + (size_t)(p % kEngSlots) * A.ng * kEngListWords, 0, 1, A.ng, p, &a0,
-                                 &a1);
+        } else if (wave < A.ng) {
+            // group list `wave`, polled whole with kFinalDepth loads in flight (one block: a few
+            // tens of GB/s), so that it is in registers about a round trip after it lands
+            constexpr int kFinalDepth = 4;
+            const uint64_t* s = A.glists + ((size_t)(p % kEngSlots) * A.ng + wave) * kEngListWords;
+            uint64_t v0[kFinalDepth], v1[kFinalDepth];
+#pragma unroll
+            for (int i = 0; i < kFinalDepth; ++i) {
+                v0[i] = ld_sc1(&s[lane]);
+                v1[i] = ld_sc1(&s[64 + lane]);
+                __builtin_amdgcn_s_sleep(2);
+            }
+            bool got = false;
+            EngWait wt(ctl, kEngWaitTicks);
+            while (!got) {
+#pragma unroll
+                for (int i = 0; i < kFinalDepth; ++i) {
+                    if (__ballot((uint32_t)(v0[i] >> 32) != p || (uint32_t)(v1[i] >> 32) != p) == 0) {
+                        a0 = (uint32_t)v0[i];
+                        a1 = (uint32_t)v1[i];
+                        got = true;
+                        break;
+                    }
+                    v0[i] = ld_sc1(&s[lane]);
+                    v1[i] = ld_sc1(&s[64 + lane]);
+                    if (!wt.tick()) break;
+                }
+                if (!got && ld_sc1(&ctl->err) != 0) break;
+            }
+            ok = got;
         }
         if (!ok) L.ok = 0;
         block_merge128_all(L.wl, L.wl2, a0, a1, wave, lane);
@@ -946,6 +973,12 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
     }
     if (wave == 1 || wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 0, wave == 1 ? 0 : 1); return; }
     if (wave != 4) eng_front_eval(cf, nc, t, L, q, dw, wave == 6 ? 0 : 1, wave == 7 ? 0 : wave == 3 ? 1 : 2);
+    // two generations of the package's loads in flight, checked in turn (the package is
+    // read whole each time: four waves of one block, a few tens of GB/s), so that it is
+    // in registers about a round trip after it lands
+    uint64_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
     bool got = false;
     EngWait wt(ctl, kEngWaitTicks);
     for (;;) {
@@ -953,13 +986,20 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
 #pragma unroll
         for (int i = 0; i < 16; ++i) miss |= (uint32_t)(v[i] >> 32) != q;
         if (__ballot(miss) == 0) { got = true; break; }
-        // the last granules of this wave's fields (each half written by one of the final
-        // merger's waves), polled with loads in flight; then one reload
-        if (!eng_poll_tags(ctl, lane < 2 ? &pk->w[8 * k + 7][lane ? 127 : 63] : nullptr, q, kEngWaitTicks)) break;
-        if (!wt.tick()) break;
 #pragma unroll
-        for (int i = 0; i < 16; ++i)
-            if ((uint32_t)(v[i] >> 32) != q) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+        for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+        miss = false;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) miss |= (uint32_t)(w[i] >> 32) != q;
+        if (__ballot(miss) == 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) v[i] = w[i];
+            got = true;
+            break;
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+        if (!wt.tick()) break;
     }
     if (got) {
         const int base = kEngStage + kEngPkgN * (int)(q % 2);
