@@ -312,12 +312,12 @@ struct EngPlacerLds {
     uint32_t pkey[2][kEngPkgN];  // pop q's package keys (q % 2)
     uint32_t s64[64];            // the merged list without pop p-1's candidates
     uint32_t e[3][64];           // re-evaluated keys of pops p-1 / p-2 / p-3's candidates (sorted)
-    int32_t s1a[64], s1p[64];    // pop p-1's candidates: depth-1 scores after an Allocate / a Pipeline
     uint8_t fbp[3][64];          // FitDelta bits of the three sets
     // the front's evaluation of pops p-2 / p-3's candidates (set 0 / 1, by ring lane)
-    uint32_t fe[2][64];
-    uint8_t fkind[2][64], ffb[2][64];
-    int32_t fna[2][64], fs1a[2][64], fs1p[2][64];
+    uint32_t fe[3][64];
+    uint8_t fkind[3][64], ffb[3][64];
+    int32_t fna[3][64], fs1a[3][64], fs1p[3][64];
+    int rows_seq;                // the last pop whose candidates' rows are in their ring (eng_finish)
     uint8_t x2use[64], x3use[64];  // pop p-2's candidate not p-1's; pop p-3's neither
     int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
@@ -328,7 +328,6 @@ struct EngPlacerLds {
     uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
     int gran_seq;                // the pop whose granules are in gran / gfit
-    int s1_ready;                // P2: depth-1 score waves done (2 = both kinds)
 };
 union EngLds {
     EngWorkerLds w;
@@ -817,11 +816,13 @@ __device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, c
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the granules are in LDS before the flag
     if (lane == 0) __hip_atomic_store(&L.gran_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int n = D.n;
-    if (n >= 0) {  // every candidate's row after the chunk into ring r0 (the next two pops re-evaluate them)
+    if (n >= 0) {  // every candidate's row after the chunk into ring r0 (the next three pops re-evaluate them)
         const int src = L.srcslot[lane];
         L.rc.row[64 * r0 + lane] = place_row(c, D);
         L.flags[64 * r0 + lane] = L.flags[src];
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the rows are in LDS before the flag (the front reads them)
+    if (lane == 0) __hip_atomic_store(&L.rows_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (n >= 0 && D.cc > 0) {
         const Row r = place_row(c, D);
         st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
@@ -857,13 +858,13 @@ __device__ __forceinline__ void eng_host_out(const EngArgs& A, EngPlacerLds& L, 
     ETL(A, p, 8);
 }
 
-// Pop q's older candidates, evaluated during pop q-1's placement by waves it
-// leaves idle (their rows are final): set 0 = pop q-2's candidates (ring
-// (q + 2) % 4), set 1 = pop q-3's (ring (q + 1) % 4); role 0 the key (static
-// predicates, node-affinity weight, FitDelta bits, kind), 1 / 2 the depth-1
-// score after an Allocate / a Pipeline.  Into the front arrays (fe, ...):
-// pop q-1's placement still reads the row cache's na / s1 of these slots;
-// pop q's P2 moves the ones that count (x2use / x3use) there.
+// Pop q's previous candidates, evaluated during pop q-1's placement by waves
+// it leaves idle: set s = pop q-1-s's candidates (ring (q + 3 - s) % 4; set 0's
+// rows once pop q-1's decision has written them, L.rows_seq); role 0 the key
+// (static predicates, node-affinity weight, FitDelta bits, kind), 1 / 2 the
+// depth-1 score after an Allocate / a Pipeline.  Into the front arrays (fe,
+// ...): pop q-1's placement still reads the row cache's na / s1 of the older
+// slots; pop q's P2 moves the ones that count there.
 __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& nc, const DevTables& t,
                                                EngPlacerLds& L, uint32_t q, uint32_t dw, int set, int role) {
     const int lane = eng_lane();
@@ -873,7 +874,12 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
     const EngDesc d = eng_decode(w);
     const PopArgs a = eng_args(d);
     const TaskClass c = eng_class_x(dw);
-    const int ring = set == 0 ? (int)((q + 2) % 4) : (int)((q + 1) % 4);
+    const int ring = (int)((q + 3 - set) % 4);
+    if (set == 0)  // pop q-1's rows: written by its decision's wave (eng_finish)
+        while (__hip_atomic_load(&L.rows_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)(q - 1)) {
+            if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+            __builtin_amdgcn_s_sleep(1);
+        }
     const int node = L.xn[ring][lane];
     const int sl = 64 * ring + lane;
     const uint64_t pw[4] = {0, 0, 0, 0};
@@ -895,13 +901,18 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
         L.ffb[set][lane] = (uint8_t)fb;
         L.fkind[set][lane] = (uint8_t)kind;
         L.fna[set][lane] = na;
-    } else if (node >= 0) {
+        // the depth-1 score after a Pipeline, for the (rare) keys whose commit is one
+        if (__ballot(kind == 2) != 0 && kind == 2) {
+            const Row r1 = apply_commits(L.rc.row[sl], c, 0, 1);
+            const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
+            L.fs1p[set][lane] = k1 ? key_score(k1) : INT32_MIN;
+        }
+    } else if (node >= 0) {  // the depth-1 score after an Allocate
         const Row r = L.rc.row[sl];
         const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
-        const int alloc = role == 1 ? 1 : 0;
-        const Row r1 = apply_commits(r, c, alloc, 1 - alloc);
+        const Row r1 = apply_commits(r, c, 1, 0);
         const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
-        (role == 1 ? L.fs1a : L.fs1p)[set][lane] = k1 ? key_score(k1) : INT32_MIN;
+        L.fs1a[set][lane] = k1 ? key_score(k1) : INT32_MIN;
     }
 }
 
@@ -968,11 +979,16 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
         L.x3use[lane] = use3;
         if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
-        eng_front_eval(cf, nc, t, L, q, dw, 1, 2);
         return;
     }
-    if (wave == 1 || wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 0, wave == 1 ? 0 : 1); return; }
-    if (wave != 4) eng_front_eval(cf, nc, t, L, q, dw, wave == 6 ? 0 : 1, wave == 7 ? 0 : wave == 3 ? 1 : 2);
+    // one evaluation per wave (set, role: 0 the key, 1 the depth-1 score after an Allocate);
+    // waves w and w + 4 share a SIMD's issue slots; set 0 waits for pop q-1's rows
+    if (wave == 1) { eng_front_eval(cf, nc, t, L, q, dw, 0, 0); return; }
+    if (wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 1, 1); return; }
+    if (wave == 3) eng_front_eval(cf, nc, t, L, q, dw, 2, 1);
+    else if (wave == 4) eng_front_eval(cf, nc, t, L, q, dw, 0, 1);
+    else if (wave == 6) eng_front_eval(cf, nc, t, L, q, dw, 1, 0);
+    else eng_front_eval(cf, nc, t, L, q, dw, 2, 0);
     // two generations of the package's loads in flight, checked in turn (the package is
     // read whole each time: four waves of one block, a few tens of GB/s), so that it is
     // in registers about a round trip after it lands
@@ -1021,17 +1037,16 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
 }
 
 // The placer, per pop p (its front — descriptor, class, candidate hash,
-// package, pops p-2 / p-3's candidates evaluated — was prepared during pop
-// p-1's placement):
+// package, pops p-1 / p-2 / p-3's candidates evaluated — was prepared during
+// pop p-1's placement):
 //   P2  wave 0 drops pop p-1's candidates from the package list (stale keys: at most 64
-//       of 128, the first 64 left are exact); waves 1-3 re-evaluate pop p-1's candidates
-//       on the rows this block left them with (keys, depth-1 scores); waves 5 / 6 move
-//       the front's results for pops p-2 / p-3's candidates that count into place;
+//       of 128, the first 64 left are exact); waves 1, 5, 6 move the front's results for
+//       pops p-1 / p-2 / p-3's candidates that count into place; wave 4 prefetches pop
+//       p+1's descriptor;
 //   P3  the final top 64, pop p-1's `done` (its write-back drained), pop p's candidates
 //       published, their rows into ring p % 4;
-//   P4  the placement (place_decide, parallel levels, rows in ring order); wave 0 then
-//       the results and rows, wave 5 stores the results to the host, the other waves
-//       prepare pop p+1's front.
+//   P4  the placement (place_decide_wave, one wave); wave 0 then the results and rows,
+//       wave 5 stores the results to the host, the other waves prepare pop p+1's front.
 // The workers of pop p leave out pops p-3 / p-2's candidates and may hold stale
 // keys of pop p-1's: every node of the three sets is re-evaluated here.
 __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
@@ -1040,7 +1055,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
-    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.s1_ready = 0; L.ndesc_seq = 0; }
+    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1; }
     __syncthreads();
     eng_front(cf, nc, t, A, L, A.first, wave);
     uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
@@ -1083,53 +1098,6 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             if (c0) rc_insert(&rc, key_node(k0, a), stage + lane);
             if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
             ETL(A, p, 1);
-        } else if (wave <= 3) {  // pop p-1's candidates: wave 1 their keys (sorted) and FitDelta
-            // bits, waves 2 / 3 their depth-1 scores after an Allocate / a Pipeline; the key
-            // wave then keeps the one its key's kind calls for
-            const TaskClass c = eng_class(L.desc[p % 2]);
-            const int node = L.xn[r1][lane];
-            const int sl = 64 * r1 + lane;
-            const uint64_t pw[4] = {0, 0, 0, 0};
-            if (wave == 1) {
-                uint32_t e = 0, fb = 0;
-                int kind = 0;
-                if (node >= 0) {
-                    const Row r = rc.row[sl];
-                    const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
-                    const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
-                    int32_t sc;
-                    bool passed;
-                    const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
-                    rc.na[sl] = na;
-                    e = sweep_key<uint32_t>(k0, a);
-                    fb = fit_bits(c, r, passed);
-                    kind = k0 ? key_kind(k0) : 0;
-                }
-                ETL(A, p, 2);
-                L.e[0][lane] = wave_sort_desc(e);
-                ETL(A, p, 9);
-                L.fbp[0][lane] = (uint8_t)fb;
-                while (__hip_atomic_load(&L.s1_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 2)
-                    __builtin_amdgcn_s_sleep(1);
-                if (node >= 0) rc.s1[sl] = kind == 0 ? INT32_MIN : kind == 2 ? L.s1p[lane] : L.s1a[lane];
-            } else {
-                int32_t s1 = INT32_MIN;
-                if (node >= 0) {
-                    const Row r = rc.row[sl];
-                    const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
-                    const int alloc = wave == 2 ? 1 : 0;
-                    const Row r1r = apply_commits(r, c, alloc, 1 - alloc);
-                    int32_t sc;
-                    bool passed;
-                    const uint64_t k1 = dyn_key(cf, c, t, nc, r1r, pw, node, true, na, &sc, &passed);
-                    s1 = k1 ? key_score(k1) : INT32_MIN;
-                }
-                if (wave == 2) L.s1a[lane] = s1;
-                else L.s1p[lane] = s1;
-                if (wave == 2) ETL(A, p, 19);
-                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the scores are in LDS before the count
-                if (lane == 0) __hip_atomic_fetch_add(&L.s1_ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
         } else if (wave == 4) {  // pop p+1's descriptor, if the dispatcher has it (one attempt)
             const uint64_t x = ld_sc1(&ctl->desc[(p + 1) % kEngRing][lane]);
             if (__ballot((uint32_t)(x >> 32) != p + 1) == 0) {
@@ -1137,13 +1105,17 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 if (lane == 0) __hip_atomic_store(&L.ndesc_seq, (int)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        } else if (wave == 5 || wave == 6) {  // pops p-2 / p-3's candidates that count (the front's results)
-            const int set = wave - 5;
-            const int ring = set == 0 ? r2 : r3;
+        } else if (wave == 1 || wave == 5 || wave == 6) {  // pops p-1 / p-2 / p-3's candidates that count
+            // (the front's evaluation): sorted keys, FitDelta bits, node-affinity weights and
+            // depth-1 scores (the one their key's kind calls for) into the row cache
+            const int set = wave == 1 ? 0 : wave - 4;
+            const int ring = set == 0 ? r1 : set == 1 ? r2 : r3;
             const int node = L.xn[ring][lane];
-            const bool use = node >= 0 && (set == 0 ? L.x2use[lane] : L.x3use[lane]);
-            L.e[1 + set][lane] = wave_sort_desc(use ? L.fe[set][lane] : 0u);
-            L.fbp[1 + set][lane] = use ? L.ffb[set][lane] : (uint8_t)0;
+            const bool use = node >= 0 && (set == 0 || (set == 1 ? L.x2use[lane] : L.x3use[lane]));
+            if (wave == 1) ETL(A, p, 2);
+            L.e[set][lane] = wave_sort_desc(use ? L.fe[set][lane] : 0u);
+            if (wave == 1) ETL(A, p, 9);
+            L.fbp[set][lane] = use ? L.ffb[set][lane] : (uint8_t)0;
             if (use) {
                 const int sl = 64 * ring + lane;
                 const int kind = L.fkind[set][lane];
@@ -1155,7 +1127,6 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         if (wave == 0) ETL(A, p, 3);
         // P3
         if (wave == 0) {
-            if (lane == 0) L.s1_ready = 0;
             uint32_t top = wave_merge_desc(L.s64[lane], L.e[0][lane]);
             top = wave_merge_desc(top, L.e[1][lane]);
             top = wave_merge_desc(top, L.e[2][lane]);

@@ -53,7 +53,7 @@ def main():
     order = np.argsort(pops)
     t = t[order]
     pops = pops[order]
-    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 19, 28]] > 0, axis=1)
+    keep = (pops > 100) & np.all(t[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 28]] > 0, axis=1)
     t = t[keep]
     pops = t[:, 31]
     cont = np.diff(pops) == 1
@@ -70,9 +70,8 @@ def main():
     per["placer 6->8 granules (wave 5)"] = us(t[:, 8] - t[:, 6])
     per["placer 5->15 front of next (wave 3, package)"] = us(t[:, 15] - t[:, 5])
     per["P2 wave0 drop (0->1)"] = us(t[:, 1] - t[:, 0])
-    per["P2 wave1 key dyn_key (0->2)"] = us(t[:, 2] - t[:, 0])
+    per["P2 wave1 start (0->2)"] = us(t[:, 2] - t[:, 0])
     per["P2 wave1 sort (2->9)"] = us(t[:, 9] - t[:, 2])
-    per["P2 wave5 s1 dyn_key (0->19)"] = us(t[:, 19] - t[:, 0])
     per["placer 7 -> next 0"] = us((t[1:, 0] - t[:-1, 7])[cont])
     # when do the lists of pop p arrive, relative to the placer's start of pop p
     fin = np.all(t[:, [20, 21, 22]] > 0, axis=1)
