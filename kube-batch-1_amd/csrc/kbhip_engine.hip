@@ -473,11 +473,9 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
         if (wave == 0) {
             bool ok = true;
             int node = -1;
-            if (tb >= 0) ETL(A, p, 16);
             bool any_own = false;
             if (p >= A.first + 2) {
                 ok = eng_wait_cands(ctl, p - 2, &node);
-                if (tb >= 0) ETL(A, p, 17);
                 const int o = node - lo;
                 const bool own = ok && node >= 0 && o >= 0 && o < cnt;
                 if (own) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
@@ -521,7 +519,6 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                 cpub = p - 1;
             }
             if (!ok && lane == 0) L.ok = 0;  // (the error is recorded: every block gives up)
-            if (tb >= 0) ETL(A, p, tb + 4);
         }
     }
 }
@@ -650,7 +647,6 @@ __device__ __forceinline__ void eng_merger(const EngArgs& A, EngMergerLds& L, in
             st_sc1(&dst[lane], ((uint64_t)p << 32) | L.wl[0][lane]);
             st_sc1(&dst[64 + lane], ((uint64_t)p << 32) | L.wl2[0][lane]);
             if (g == 0) ETL(A, p, 26);
-            if (g == A.ng - 1) ETL(A, p, 23);
             if (cpub + 1 < p) {
                 eng_group_counts(A, g, cg, p - 1, true, &ok);
                 cpub = p - 1;
@@ -979,6 +975,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
         L.x3use[lane] = use3;
         if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
+        eng_front_eval(cf, nc, t, L, q, dw, 0, 1);
         return;
     }
     // one evaluation per wave (set, role: 0 the key, 1 the depth-1 score after an Allocate);
@@ -986,9 +983,8 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
     if (wave == 1) { eng_front_eval(cf, nc, t, L, q, dw, 0, 0); return; }
     if (wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 1, 1); return; }
     if (wave == 3) eng_front_eval(cf, nc, t, L, q, dw, 2, 1);
-    else if (wave == 4) eng_front_eval(cf, nc, t, L, q, dw, 0, 1);
     else if (wave == 6) eng_front_eval(cf, nc, t, L, q, dw, 1, 0);
-    else eng_front_eval(cf, nc, t, L, q, dw, 2, 0);
+    else if (wave == 7) eng_front_eval(cf, nc, t, L, q, dw, 2, 0);  // (wave 4: wave 0's SIMD, loads only)
     // two generations of the package's loads in flight, checked in turn (the package is
     // read whole each time: four waves of one block, a few tens of GB/s), so that it is
     // in registers about a round trip after it lands
@@ -1181,6 +1177,12 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             if (wave == 5) eng_host_out(A, L, p, d.slot);
             eng_front(cf, nc, t, A, L, p + 1, wave);
             if (wave == 3) ETL(A, p, 15);
+            if (wave == 1) ETL(A, p, 19);
+            if (wave == 5) ETL(A, p, 29);
+            if (wave == 7) ETL(A, p, 16);
+            if (wave == 6) ETL(A, p, 17);
+            if (wave == 4) ETL(A, p, 14);
+            if (wave == 2) ETL(A, p, 23);
         }
     }
 }

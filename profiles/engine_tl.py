@@ -69,6 +69,11 @@ def main():
     per["placer 6->7 rows written"] = us(t[:, 7] - t[:, 6])
     per["placer 6->8 granules (wave 5)"] = us(t[:, 8] - t[:, 6])
     per["placer 5->15 front of next (wave 3, package)"] = us(t[:, 15] - t[:, 5])
+    for ev, name in ((19, "wave 1 (pop p-1 cands key)"), (29, "wave 5 (host out + eval)"), (16, "wave 7 (eval + package)"),
+                     (17, "wave 6 (eval + package)"), (14, "wave 4 (eval + package)"), (23, "wave 2 (hash)")):
+        ok = t[:, ev] > 0
+        if ok.any():
+            per[f"placer 5->{ev} front {name}"] = us((t[:, ev] - t[:, 5])[ok])
     per["P2 wave0 drop (0->1)"] = us(t[:, 1] - t[:, 0])
     per["P2 wave1 start (0->2)"] = us(t[:, 2] - t[:, 0])
     per["P2 wave1 sort (2->9)"] = us(t[:, 9] - t[:, 2])
@@ -88,9 +93,6 @@ def main():
     if lw.any():
         per["last worker published (18) - worker0 published (13)"] = us((t[:, 18] - t[:, 13])[lw])
         per["last worker published (18) - placer start (0)"] = us((t[:, 18] - t[:, 0])[lw])
-    lm = t[:, 23] > 0
-    if lm.any():
-        per["last merger published (23) - placer start (0)"] = us((t[:, 23] - t[:, 0])[lm])
     mg = np.all(t[:, [24, 25, 26]] > 0, axis=1)
     if mg.any():
         per["merger0 published (26) - placer start (0)"] = us((t[:, 26] - t[:, 0])[mg])
@@ -103,13 +105,6 @@ def main():
     per["worker0 done(11)->eval(12)"] = us(t[:, 12] - t[:, 11])
     per["worker0 eval(12)->pub(13)"] = us(t[:, 13] - t[:, 12])
     per["worker0 pub(13) -> next desc(10)"] = us((t[1:, 10] - t[:-1, 13])[cont])
-    w2 = np.all(t[:, [16, 17]] > 0, axis=1)
-    if w2.any():
-        per["worker0 eval(12)->merged256(16)"] = us((t[:, 16] - t[:, 12])[w2])
-        per["worker0 merged256(16)->cands p-2 seen(17)"] = us((t[:, 17] - t[:, 16])[w2])
-        per["worker0 cands seen(17)->pub(13)"] = us((t[:, 13] - t[:, 17])[w2])
-        per["worker0 cands p-2 seen(17,p) - placer P3(4,p-2)"] = us(
-            (t[2:, 17] - t[:-2, 4])[((pops[2:] - pops[:-2]) == 2) & w2[2:]])
     per["worker0 published (13, p) - placer P3 (4, p-2)"] = us((t[2:, 13] - t[:-2, 4])[(pops[2:] - pops[:-2]) == 2])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     res["median_us"] = {k: round(v, 3) for k, v in per.items()}
