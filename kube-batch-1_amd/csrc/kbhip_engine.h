@@ -31,6 +31,7 @@ constexpr int kEngMaxGroups = 8;  // merger blocks
 constexpr int kEngListWords = 136;  // a list: 128 tagged keys + 4 tagged counts (+ pad), 17 lines
 constexpr int kEngMaxNpb = 8192;  // nodes per worker block
 constexpr int kEngWorkersMax = 512;
+constexpr int kEngCandCopies = 8;  // the candidate granules' copies (the workers' polls spread over them)
 
 // The final merger's package for pop p (slot p % kEngSlots): the top 128
 // keys of the group lists with every entry's node row and its node-affinity
@@ -60,7 +61,7 @@ struct EngCtl {
     uint32_t err;   // first error (kEngErr*), 0: none; every wait gives up once it is set
     uint32_t pad1[31];
     uint64_t desc[kEngRing][kEngDescWords];  // descriptors, slot seq % kEngRing
-    uint64_t cands[kEngSlots][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}
+    uint64_t cands[kEngSlots][kEngCandCopies][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}, in copies
 };
 enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3 };
 

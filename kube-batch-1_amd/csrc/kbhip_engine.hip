@@ -201,11 +201,12 @@ __device__ __forceinline__ bool eng_poll_tags(EngCtl* ctl, const uint64_t* w, ui
     }
 }
 
-// Wave 0: candidate `lane` of pop q (-1: none), waiting for the granules.
-__device__ __forceinline__ bool eng_wait_cands(EngCtl* ctl, uint32_t q, int* node) {
+// Wave 0: candidate `lane` of pop q (-1: none), waiting for the granules of
+// copy `copy` (the placer stores kEngCandCopies: a few tens of pollers each).
+__device__ __forceinline__ bool eng_wait_cands(EngCtl* ctl, uint32_t q, int* node, int copy) {
     const int lane = threadIdx.x & 63;
-    const uint64_t* src = &ctl->cands[q % kEngSlots][lane];
-    if (!eng_poll_tag(ctl, &ctl->cands[q % kEngSlots][0], q, kEngWaitTicks)) return false;
+    const uint64_t* src = &ctl->cands[q % kEngSlots][copy % kEngCandCopies][lane];
+    if (!eng_poll_tag(ctl, &ctl->cands[q % kEngSlots][copy % kEngCandCopies][0], q, kEngWaitTicks)) return false;
     EngWait wt(ctl, kEngWaitTicks);
     for (;;) {
         const uint64_t x = ld_sc1(src);
@@ -406,7 +407,7 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                         int node = -1;
                         bool have = true;
                         if (p >= A.first + 2) {
-                            const uint64_t cw = ld_sc1(&ctl->cands[(p - 2) % kEngSlots][lane]);
+                            const uint64_t cw = ld_sc1(&ctl->cands[(p - 2) % kEngSlots][b % kEngCandCopies][lane]);
                             have = __ballot((uint32_t)(cw >> 32) != p - 2) == 0;
                             node = (int)(uint32_t)cw;
                         }
@@ -426,13 +427,13 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
                 if (tb >= 0) ETL(A, p, tb + 1);
                 if (ok && p >= A.first + 3) {
                     int node = -1;
-                    ok = eng_wait_cands(ctl, p - 3, &node);
+                    ok = eng_wait_cands(ctl, p - 3, &node, b);
                     const int o = node - lo;
                     if (ok && node >= 0 && o >= 0 && o < cnt) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
                 }
             } else if (ok && cpub + 1 < p) {  // the run ends: the last pop's counts
                 int node = -1;
-                if (p >= A.first + 2) ok = eng_wait_cands(ctl, p - 2, &node);
+                if (p >= A.first + 2) ok = eng_wait_cands(ctl, p - 2, &node, b);
                 if (ok) {
                     eng_fit_drop(L, pset, node, lo, cnt);
                     eng_fit_publish(A, L, p - 1, b);
@@ -475,7 +476,7 @@ __device__ __forceinline__ void eng_worker(const Conf& cf, const NodeCols& nc, c
             int node = -1;
             bool any_own = false;
             if (p >= A.first + 2) {
-                ok = eng_wait_cands(ctl, p - 2, &node);
+                ok = eng_wait_cands(ctl, p - 2, &node, b);
                 const int o = node - lo;
                 const bool own = ok && node >= 0 && o >= 0 && o < cnt;
                 if (own) atomicOr(&L.skip[o >> 5], 1u << (o & 31));
@@ -1136,7 +1137,9 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             }
             const int n = top ? key_node(top, a) : -1;
             eng_publish_done(ctl, &pend);  // pop p-1's write-back (every node a worker may read next)
-            st_sc1(&ctl->cands[p % kEngSlots][lane], ((uint64_t)p << 32) | (uint32_t)n);
+#pragma unroll
+            for (int cp = 0; cp < kEngCandCopies; ++cp)
+                st_sc1(&ctl->cands[p % kEngSlots][cp][lane], ((uint64_t)p << 32) | (uint32_t)n);
             int src = n >= 0 ? rc_find(&rc, n) : -1;  // a previous pop's candidate, or a package entry
             if (n >= 0 && src < 0) {  // (every node of the list is one of those: kept for safety)
                 src = 64 * r0 + lane;
