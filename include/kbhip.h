@@ -408,6 +408,15 @@ int kbhip_shard_connect_host(kb_session* s, kbhip_allreduce_fn fn, void* ctx);
  * of kbhip_shard_connect_rccl / kbhip_shard_connect_host.  Mailboxes and
  * mappings are kept per process and reused by later sessions. */
 int kbhip_shard_connect_mailbox(kb_session* s, kbhip_allgather_fn fn, void* ctx);
+/* Ranks that are threads of one process on one device (a rehearsal; one
+ * process per GPU is the deployment): a rank's placement kernel spins on the
+ * other ranks' flags, so their chained kernels must never share a hardware
+ * queue.  kbhip_shard_connect_mailbox returns KBHIP_EUNSUPPORTED (every rank
+ * of the group, after the all-gather) unless all ranks' streams fit in the
+ * process's queues (GPU_MAX_HW_QUEUES, default 4).  This query gives the
+ * same verdict without a device: 1 when ranks_on_device ranks fit in
+ * hw_queues queues (hw_queues <= 0: the environment's), else 0. */
+int kbhip_shard_mailbox_fits(int32_t ranks_on_device, int32_t hw_queues);
 int kbhip_shard_connect_host_gather(kb_session* s, kbhip_allgather_fn fn, void* ctx);
 
 /* Test support (not part of the placement path): encode a snapshot without a

@@ -29,7 +29,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_shard_connect_rccl", "kbhip_shard_connect_host", "kbhip_debug_replay",
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
-           "kbhip_session_carry_events", "kbhip_shard_connect_mailbox", "kbhip_place_job_submit",
+           "kbhip_session_carry_events", "kbhip_shard_connect_mailbox", "kbhip_shard_mailbox_fits", "kbhip_place_job_submit",
            "kbhip_place_job_wait", "kbhip_place_job_cancel", "kbhip_time_sweeps",
            "kbhip_session_carry_snapshot")
 
@@ -110,6 +110,8 @@ def lib() -> ctypes.CDLL:
         L.kbhip_shard_connect_host.argtypes = [vp, ALLREDUCE_FN, vp]
         L.kbhip_shard_connect_host_gather.argtypes = [vp, ALLGATHER_FN, vp]
         L.kbhip_shard_connect_mailbox.argtypes = [vp, ALLGATHER_FN, vp]
+        L.kbhip_shard_mailbox_fits.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        L.kbhip_shard_mailbox_fits.restype = ctypes.c_int
         L.kbhip_read_nodes.argtypes = [vp, vp, i64]
         L.kbhip_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
         L.kbhip_set_option.argtypes = [vp, ctypes.c_char_p, i64]

@@ -280,3 +280,56 @@ def test_rccl_communicator_dropped_after_failure(engine, oracle_mod, kbgen_mod, 
         s.close()
         assert [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)] == exp
     assert reused == [0, 1]
+
+
+def test_mailbox_queue_rule(engine_lib):
+    """kbhip_shard_mailbox_fits: the rule kbhip_shard_connect_mailbox applies to
+    rank threads of one process sharing a device (each session has 3 streams;
+    one process per GPU always fits)."""
+    fits = engine_lib.kbhip_shard_mailbox_fits
+    assert fits(1, 1) == 1 and fits(1, 4) == 1  # one rank per process and device
+    assert fits(2, 4) == 0  # the r04 rank-thread rehearsal under the default 4 queues
+    assert fits(2, 6) == 1 and fits(2, 5) == 0
+    assert fits(8, 24) == 1 and fits(8, 16) == 0
+
+
+@pytest.mark.gpu
+def test_mailbox_refuses_shared_hw_queues(engine, kbgen_mod, tmp_path):
+    """Two shard ranks as threads of this process on one GPU, with the default
+    hardware queues: kbhip_shard_connect_mailbox refuses on both ranks
+    (KBHIP_EUNSUPPORTED, after the handle all-gather) instead of letting their
+    mailbox kernels share a queue and wait on each other."""
+    import threading
+    kb = engine
+    q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    if kb.lib().kbhip_shard_mailbox_fits(2, q):
+        pytest.skip(f"GPU_MAX_HW_QUEUES={q} fits two in-process ranks")
+    c = kbgen_mod.gen_c3(n_nodes=90, n_pending=200)
+    p = str(tmp_path / "c.kbs")
+    c.write(p)
+    buf = open(p, "rb").read()
+    bar, slots, errs = threading.Barrier(2), [None, None], [None, None]
+
+    def gather(rank):
+        def g(send, recv):
+            slots[rank] = bytes(send)
+            bar.wait()
+            recv[:] = np.frombuffer(b"".join(slots), np.uint8)
+            bar.wait()
+        return g
+
+    def run(rank):
+        s = kb.ShardedSession(buf, 0, rank, 2)
+        try:
+            s.connect_mailbox(gather(rank))
+        except kb.KbhipError as e:
+            errs[rank] = str(e)
+        finally:
+            s.close()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert all(e is not None and "error -3" in e and "hardware queues" in e for e in errs), errs
