@@ -325,6 +325,9 @@ struct EngPlacerLds {
     alignas(16) uint32_t desc[2][kEngDescWords];  // pop q's descriptor and class (q % 2)
     alignas(16) uint32_t ndesc[kEngDescWords];    // pop ndesc_seq's, prefetched during P2 (a front reads it)
     int ndesc_seq;
+    int hash_seq;                // the pop whose front hashed its previous candidates (wave 2)
+    int drop_seq;                // the pop whose package the front already cut to L.s64 (wave 3)
+    int sort_seq[3];             // the pop whose front sorted set s's keys into L.e / L.fbp
     uint64_t gran[64];           // the pop's result granules (0: none), stored to the host by wave 5
     uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
@@ -855,6 +858,36 @@ __device__ __forceinline__ void eng_host_out(const EngArgs& A, EngPlacerLds& L, 
     ETL(A, p, 8);
 }
 
+// One wave: pop q's package keys without pop q-1's candidates (stale: the
+// workers evaluated them before pop q-1 placed; at most 64 of 128, so the
+// first 64 left are exact) into L.s64, the kept entries' rows hashed into the
+// row cache.  Needs the front's hash of pops q-1..q-3's candidates.
+__device__ __forceinline__ void eng_drop_stale(EngPlacerLds& L, const PopArgs& a, uint32_t q) {
+    const int lane = threadIdx.x & 63;
+    EngRowCache& rc = L.rc;
+    const int r1 = (int)((q + 3) % 4);
+    const int stage = kEngStage + kEngPkgN * (int)(q % 2);
+    L.s64[lane] = 0;
+    const uint32_t k0 = L.pkey[q % 2][lane], k1 = L.pkey[q % 2][64 + lane];
+    auto kept = [&](uint32_t k) {
+        if (!k) return false;
+        const int sl = rc_find(&rc, key_node(k, a));
+        return !(sl >= 64 * r1 && sl < 64 * r1 + 64);
+    };
+    const bool c0 = kept(k0), c1 = kept(k1);
+    const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
+    const int q0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0));
+    const int q1 = __popcll(m0) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0));
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    if (c0) L.s64[q0] = k0;
+    if (c1 && q1 < 64) L.s64[q1] = k1;
+    // the kept nodes' rows: their package entries
+    if (c0) rc_insert(&rc, key_node(k0, a), stage + lane);
+    if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
+}
+
 // Pop q's previous candidates, evaluated during pop q-1's placement by waves
 // it leaves idle: set s = pop q-1-s's candidates (ring (q + 3 - s) % 4; set 0's
 // rows once pop q-1's decision has written them, L.rows_seq); role 0 the key
@@ -903,6 +936,20 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
             const Row r1 = apply_commits(L.rc.row[sl], c, 0, 1);
             const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
             L.fs1p[set][lane] = k1 ? key_score(k1) : INT32_MIN;
+        }
+        // the set's keys that count (sets 1, 2: not a later set's node, from wave 2's hash)
+        // sorted for pop q's P3, and their FitDelta bits; else the placer's P2 does it
+        bool hashed = set == 0;
+        for (int i = 0; i < 4096 && !hashed; ++i) {
+            hashed = __hip_atomic_load(&L.hash_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q;
+            if (!hashed) __builtin_amdgcn_s_sleep(1);
+        }
+        if (hashed) {
+            const bool use = node >= 0 && (set == 0 || (set == 1 ? L.x2use[lane] : L.x3use[lane]));
+            L.e[set][lane] = wave_sort_desc(use ? e : 0u);
+            L.fbp[set][lane] = use ? (uint8_t)fb : (uint8_t)0;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) __hip_atomic_store(&L.sort_seq[set], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     } else if (node >= 0) {  // the depth-1 score after an Allocate
         const Row r = L.rc.row[sl];
@@ -976,6 +1023,8 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
         L.x3use[lane] = use3;
         if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the hash is in LDS before the flag
+        if (lane == 0) __hip_atomic_store(&L.hash_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         eng_front_eval(cf, nc, t, L, q, dw, 0, 1);
         return;
     }
@@ -1026,8 +1075,24 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
             else if (f == kPkNa) rc.na[sl] = (int32_t)x;
             else rc.s1[sl] = (int32_t)x;
         }
-        if (k == 0)
+        if (k == 0) {
             for (int w = 0; w < 4; ++w) { rc.pw[base + lane][w] = 0; rc.pw[base + 64 + lane][w] = 0; }
+            // pop q-1's candidates out of the package (its keys, written above by this wave),
+            // once wave 2 has hashed the rings; else the placer's P2 does it
+            bool hashed = false;
+            for (int i = 0; i < 4096 && !hashed; ++i) {
+                hashed = __hip_atomic_load(&L.hash_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q;
+                if (!hashed) __builtin_amdgcn_s_sleep(1);
+            }
+            if (hashed) {
+                uint32_t w8[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) w8[i] = (uint32_t)__builtin_amdgcn_readlane((int)dw, i);
+                eng_drop_stale(L, eng_args(eng_decode(w8)), q);
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                if (lane == 0) __hip_atomic_store(&L.drop_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
     } else if (k == 0 && lane == 0) {  // a wait gave up (the error is recorded)
         L.ok = 0;
     }
@@ -1052,14 +1117,17 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     for (int i = threadIdx.x; i < 4 * 64; i += kPopThreads) L.xn[i >> 6][i & 63] = -1;
-    if (threadIdx.x == 0) { L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1; }
+    if (threadIdx.x == 0) {
+        L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1;
+        L.hash_seq = L.drop_seq = (int)A.first - 1;
+        L.sort_seq[0] = L.sort_seq[1] = L.sort_seq[2] = (int)A.first - 1;
+    }
     __syncthreads();
     eng_front(cf, nc, t, A, L, A.first, wave);
     uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
     for (uint32_t p = A.first;; ++p) {
         // rings of p-1, p-2, p-3, p
         const int r1 = (int)((p + 3) % 4), r2 = (int)((p + 2) % 4), r3 = (int)((p + 1) % 4), r0 = (int)(p % 4);
-        const int stage = kEngStage + kEngPkgN * (int)(p % 2);
         __syncthreads();
         if (!L.ok) return;
         const EngDesc d = eng_decode(L.desc[p % 2]);
@@ -1075,25 +1143,8 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         }
         // P2
         if (wave == 0) {
-            L.s64[lane] = 0;
-            const uint32_t k0 = L.pkey[p % 2][lane], k1 = L.pkey[p % 2][64 + lane];
-            auto kept = [&](uint32_t k) {
-                if (!k) return false;
-                const int sl = rc_find(&rc, key_node(k, a));
-                return !(sl >= 64 * r1 && sl < 64 * r1 + 64);
-            };
-            const bool c0 = kept(k0), c1 = kept(k1);
-            const uint64_t m0 = __ballot(c0), m1 = __ballot(c1);
-            const int q0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0));
-            const int q1 = __popcll(m0) +
-                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0));
-            __builtin_amdgcn_s_waitcnt(0xc07f);
-            __builtin_amdgcn_wave_barrier();
-            if (c0) L.s64[q0] = k0;
-            if (c1 && q1 < 64) L.s64[q1] = k1;
-            // the kept nodes' rows: their package entries
-            if (c0) rc_insert(&rc, key_node(k0, a), stage + lane);
-            if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
+            if (__hip_atomic_load(&L.drop_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)p)
+                eng_drop_stale(L, a, p);
             ETL(A, p, 1);
         } else if (wave == 4) {  // pop p+1's descriptor, if the dispatcher has it (one attempt)
             const uint64_t x = ld_sc1(&ctl->desc[(p + 1) % kEngRing][lane]);
@@ -1110,9 +1161,11 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             const int node = L.xn[ring][lane];
             const bool use = node >= 0 && (set == 0 || (set == 1 ? L.x2use[lane] : L.x3use[lane]));
             if (wave == 1) ETL(A, p, 2);
-            L.e[set][lane] = wave_sort_desc(use ? L.fe[set][lane] : 0u);
+            if (__hip_atomic_load(&L.sort_seq[set], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)p) {
+                L.e[set][lane] = wave_sort_desc(use ? L.fe[set][lane] : 0u);
+                L.fbp[set][lane] = use ? L.ffb[set][lane] : (uint8_t)0;
+            }
             if (wave == 1) ETL(A, p, 9);
-            L.fbp[set][lane] = use ? L.ffb[set][lane] : (uint8_t)0;
             if (use) {
                 const int sl = 64 * ring + lane;
                 const int kind = L.fkind[set][lane];
