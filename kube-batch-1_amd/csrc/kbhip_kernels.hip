@@ -1407,355 +1407,5 @@ hipError_t launch_pop_batch(const Conf& cf, const NodeCols& nc, const DevTables&
 }
 
 #endif
-#if KBHIP_PART <= 1
-// ---------------------------------------------------------------------------
-// Node-array shards, batched pops: after the all-gather of
-// every shard's ShardMsg, each shard runs this identical placement on the
-// merged list — the global top-64, since every shard's list holds its own
-// top-64 — and writes back the rows it owns.  One workgroup.
-// ---------------------------------------------------------------------------
-constexpr int kShardHash = 2048;  // node -> (rank, slot) of the gathered candidates (<= 16 ranks x 64)
-constexpr long kMboxSpin = 1L << 23;  // mailbox poll bound (seconds): a lost rank ends the pop with an error
-// link (overlapped shard pops, k_shard_sweep_ov): the merged list's nodes are
-// published as pop `seq`'s candidates right after the merge, and the rows this
-// shard writes back go out through sc1 before link->done = seq.
-__global__ __launch_bounds__(kPopThreads) void k_shard_place(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                             const ShardMsg* msgs, int world, PopOut* out,
-                                                             const uint64_t* flags, uint32_t seq, PopLink* link) {
-    __shared__ uint64_t wl[kPopThreads / 64][64];
-    __shared__ RowCache rc;
-    __shared__ int32_t s_hk[kShardHash];
-    __shared__ int16_t s_hv[kShardHash];
-    __shared__ int32_t s_fitin[4];
-    __shared__ int s_ok;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const TaskClass c = t.classes[a.cls];
-    for (int i = threadIdx.x; i < kShardHash; i += kPopThreads) s_hk[i] = -1;
-    for (int i = threadIdx.x; i < kRcHash; i += kPopThreads) rc.hkey[i] = -1;
-    if (wave == 0) {  // mailbox: every shard's message of pop `seq` has arrived (lane r polls rank r's flag)
-        bool ok = true;
-        if (flags && lane < world) {
-            long spin = 0;
-            while (ld_sys(&flags[lane * 16]) != (uint64_t)seq) {
-                if (++spin >= kMboxSpin) { ok = false; break; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        const bool all = __ballot(!ok) == 0;
-        if (lane == 0) s_ok = all;
-    }
-    __syncthreads();
-    if (!s_ok) {  // n_done 0 on a shard pop: the host reports a lost exchange
-        if (threadIdx.x == 0) {
-            if (link) st_sc1(&link->done, seq);
-            __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        return;
-    }
-    if (threadIdx.x < 4) {
-        uint32_t f = 0;
-        bool broken = false;
-        for (int r = 0; r < world; ++r) {
-            const uint64_t w = ld_sys((const uint64_t*)msgs[r].fit + (threadIdx.x >> 1));
-            f += (uint32_t)(w >> (32 * (threadIdx.x & 1)));
-            broken = broken || (threadIdx.x == 0 && (uint32_t)w == 0xffffffffu);  // a shard's chain broke
-        }
-        s_fitin[threadIdx.x] = (int32_t)f;
-        if (broken) s_ok = 0;
-    }
-    __syncthreads();
-    if (!s_ok) {
-        if (threadIdx.x == 0) {
-            if (link) st_sc1(&link->done, seq);  // keep the chain going: the host sees n_done 0
-            __hip_atomic_store(&out->g[0], make_granule(a.epoch, 0, 0, 0, -1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        return;
-    }
-    // every gathered candidate into the node -> entry table; lists merged by waves
-    uint64_t acc = 0;
-    for (int r = wave; r < world; r += kPopThreads / 64) {
-        struct { uint64_t key; int32_t node, na; } e;  // the candidate's first 16 bytes
-        const uint64_t w1 = ld_sys((const uint64_t*)&msgs[r].c[lane] + 1);
-        e.key = ld_sys((const uint64_t*)&msgs[r].c[lane]);
-        e.node = (int32_t)(uint32_t)w1;
-        if (e.node >= 0) {
-            int h = (int)(((uint32_t)e.node * 2654435761u) >> 21);
-            while (atomicCAS(&s_hk[h], -1, e.node) != -1) h = (h + 1) & (kShardHash - 1);
-            s_hv[h] = (int16_t)(r * 64 + lane);
-        }
-        acc = wave_merge_desc(acc, e.key);
-    }
-    wl[wave][lane] = acc;
-    __syncthreads();
-    block_tree_merge(wl, wave, lane);  // wl[0]: the global top-64 keys
-    if (wave == 0) {  // their rows into the row cache (slot = lane)
-        const uint64_t K = wl[0][lane];
-        if (link)  // this pop's candidates (global nodes): the next pop's sweep leaves those of its shard out
-            st_sc1(&link->touched[seq % kLinkSlots][lane], ((uint64_t)seq << 32) | (uint32_t)(K ? key_idx(K) : -1));
-        if (K) {
-            const int g = key_idx(K);
-            int h = (int)(((uint32_t)g * 2654435761u) >> 21);
-            while (s_hk[h] != g) h = (h + 1) & (kShardHash - 1);
-            const int src = s_hv[h];
-            const ShardCand e = load_words_sys(&msgs[src >> 6].c[src & 63]);
-            rc.row[lane] = e.row;
-            for (int w = 0; w < 4; ++w) rc.pw[lane][w] = e.pw[w];
-            rc.na[lane] = e.na;
-            rc.s1[lane] = depth1_score(cf, nc, t, c, e.row, e.pw, g - nc.base, e.na, K);  // (the score only)
-            rc_insert(&rc, g, lane);
-        }
-    }
-    __syncthreads();
-    NodeCols ncg = nc;  // keys / entries carry global node indices
-    ncg.base = 0;
-    if (link) {  // write-back through sc1, drained, then link->done = seq
-        if (a.ent32)
-            place_parallel<uint32_t, true>(cf, ncg, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, 0u, nc.base, nc.n);
-        else
-            place_parallel<uint64_t, true>(cf, ncg, t, c, a, out, wl, &link->done, seq, &rc, s_fitin, 0u, nc.base, nc.n);
-    } else if (a.ent32) {
-        place_parallel<uint32_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
-    } else {
-        place_parallel<uint64_t>(cf, ncg, t, c, a, out, wl, nullptr, 0, &rc, s_fitin, 0u, nc.base, nc.n);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Overlapped shard pops (option "overlap" on a node-array shard with peer
-// mailboxes): pop e's sweep of this shard runs beside pop e-1's k_shard_place.
-// Every row pop e-1 writes belongs to one of its 64 candidates, which every
-// rank knows identically after the exchange and k_shard_place publishes
-// (link->touched) right after its merge; this sweep leaves those of its shard
-// out, merges its blocks' lists, then — once pop e-1's write-back is done
-// (link->done, this device) — evaluates them on their final rows, merges
-// them in (the shard's exact top 64) and sends the message.  Pops alternate
-// over two streams; each pop's k_shard_place follows its sweep on its stream.
-// prev_chained: pop seq-1 was such a pop (its candidates are in the link).
-// ---------------------------------------------------------------------------
-template <int R, typename KT>
-__global__ __launch_bounds__(kPopThreads) void k_shard_sweep_ov(Conf cf, NodeCols nc, DevTables t, PopArgs a,
-                                                                TaskClass cl, uint64_t* cand64, uint32_t* arrive,
-                                                                PopLink* link, uint32_t seq, int prev_chained,
-                                                                MboxArgs mb) {
-    __shared__ KT wlk[kPopThreads / 64][64];
-    __shared__ uint32_t s_skip[R * kPopThreads / 32];  // this block's nodes among pop seq-1's candidates
-    __shared__ int32_t s_tn[64];
-    __shared__ int role, s_ok;
-    __shared__ uint32_t s_fitb[4];
-    KT* cand = (KT*)cand64;
-    uint32_t* fitc = fit_counters(arrive, a.fit_set);
-    fit_zero_other(arrive, a.fit_set);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const TaskClass& c = cl;
-    const int base = blockIdx.x * R * kPopThreads;  // first local row of the block
-    uint64_t tv = 0;
-    if (wave == 0 && prev_chained) tv = ld_sc1(&link->touched[(seq - 1) % kLinkSlots][lane]);
-    for (int i = threadIdx.x; i < R * kPopThreads / 32; i += kPopThreads) s_skip[i] = 0;
-    if (threadIdx.x < 4) s_fitb[threadIdx.x] = 0;
-    KT keys[R];
-    uint32_t fbs[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int n = base + r * kPopThreads + threadIdx.x;
-        keys[r] = 0;
-        fbs[r] = 0;
-        if (n < nc.n) {
-            int32_t s;
-            bool passed;
-            keys[r] = sweep_key<KT>(eval_node(cf, c, t, nc, n, &s, &passed, &fbs[r]), a);
-        }
-    }
-    __syncthreads();  // s_skip zeroed
-    if (wave == 0) {  // pop seq-1's candidates (global nodes), those of this block marked
-        bool ok = true;
-        int tn = -1;
-        if (prev_chained) {
-            const uint64_t* src = &link->touched[(seq - 1) % kLinkSlots][lane];
-            long spin = 0;
-            while (__ballot((uint32_t)(tv >> 32) != seq - 1) != 0) {
-                if (++spin >= kLinkSpin) { ok = false; break; }
-                __builtin_amdgcn_s_sleep(1);
-                tv = ld_sc1(src);
-            }
-            tn = ok ? (int)(uint32_t)tv : -1;
-            const int ln = tn - nc.base - base;
-            if (tn >= 0 && ln >= 0 && ln < R * kPopThreads) atomicOr(&s_skip[ln >> 5], 1u << (ln & 31));
-        }
-        s_tn[lane] = tn;
-        if (lane == 0) s_ok = ok;
-    }
-    __syncthreads();
-    KT best = 0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int o = r * kPopThreads + threadIdx.x;
-        const bool skip = (s_skip[o >> 5] >> (o & 31)) & 1u;  // rows in flight: evaluated by the patch
-        fit_block_add(s_fitb, skip ? 0u : fbs[r]);
-        const KT k = wave_sort_desc(skip ? (KT)0 : keys[r]);
-        best = r == 0 ? k : wave_merge_desc(best, k);
-    }
-    wlk[wave][lane] = best;
-    __syncthreads();
-    block_tree_merge(wlk, wave, lane);
-    // merge tree: the last block of each group merges its group, the last group merger the groups
-    const int nb = gridDim.x;
-    const int g = blockIdx.x % kGroups;
-    const int g_count = (nb - g + kGroups - 1) / kGroups;
-    const int n_groups = nb < kGroups ? nb : kGroups;
-    KT* gcand = cand + (int64_t)nb * 64;
-    if (wave == 0) {
-        if (lane < 4 && s_fitb[lane])
-            __hip_atomic_fetch_add(&fitc[g * kCtrStride + lane], s_fitb[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        put_list(cand + (int64_t)blockIdx.x * 64, wlk[0][lane]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) role = atomicAdd(&arrive[g * kCtrStride], 1u) == (unsigned)(g_count - 1);
-    __syncthreads();
-    if (!role) return;
-    {
-        KT acc = 0;
-        for (int i = wave; i < g_count; i += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(cand + (int64_t)(g + i * kGroups) * 64));
-        wlk[wave][lane] = acc;
-        __syncthreads();
-        block_tree_merge(wlk, wave, lane);
-        if (wave == 0) {
-            put_list(gcand + (int64_t)g * 64, wlk[0][lane]);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) role = atomicAdd(&arrive[kGroups * kCtrStride], 1u) == (unsigned)(n_groups - 1);
-        __syncthreads();
-        if (!role) return;
-    }
-    {
-        KT acc = 0;
-        for (int gi = wave; gi < n_groups; gi += kPopThreads / 64) acc = wave_merge_desc(acc, get_list(gcand + (int64_t)gi * 64));
-        wlk[wave][lane] = acc;
-    }
-    __syncthreads();
-    block_tree_merge(wlk, wave, lane);
-    if (wave == 0 && lane <= kGroups)
-        __hip_atomic_store(&arrive[lane * kCtrStride], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __shared__ uint64_t s_k64[64];
-    __shared__ int s_bad;
-    uint32_t fit_raw = 0;
-    if (wave == 0) {
-        fit_raw = fit_load(fitc, n_groups);  // every block's counts (each added before it arrived)
-        bool okp = s_ok;
-        KT top = wlk[0][lane];
-        if (prev_chained) {  // the patch: pop seq-1's candidates of this shard on their final rows
-            okp = okp && poll_done(&link->done, seq - 1);
-            const int gn = s_tn[lane];
-            const int ln = gn - nc.base;
-            KT e = 0;
-            uint32_t pfb = 0;
-            if (okp && gn >= 0 && ln >= 0 && ln < nc.n) {
-                uint32_t fb = 0;
-                e = sweep_key<KT>(eval_node_sc1(cf, c, t, nc, ln, &fb), a);
-                pfb = fb;
-            }
-            top = wave_merge_desc(top, wave_sort_desc(e));
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const uint32_t cnt = (uint32_t)__popcll(__ballot((pfb >> b) & 1u));
-                if (lane == b) fit_raw += cnt;  // fit_sum adds lanes b, b + 4, ...
-            }
-        }
-        s_k64[lane] = okp ? key64_of(top, a) : 0;
-        if (lane == 0) s_bad = !okp;
-    }
-    __syncthreads();
-    shard_emit<true>(cf, nc, t, c, wave == 0 ? s_k64[lane] : 0, fit_raw, nullptr, mb, s_bad != 0);
-}
-
-hipError_t launch_shard_place(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, int n_tasks,
-                              int gang_mode, int min_avail, int ready_count, uint32_t epoch, const KeyFormat& kf,
-                              const ShardMsg* msgs, int world, void* out_dev, hipStream_t st, const uint64_t* flags,
-                              uint32_t seq, PopLink* link) {
-    if (world < 1 || world * 64 > kShardHash / 2) return hipErrorInvalidValue;
-    if (link && !flags) return hipErrorInvalidValue;  // the overlapped chain runs over the mailboxes
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0, 0};
-    hipLaunchKernelGGL(k_shard_place, dim3(1), dim3(kPopThreads), 0, st, cf, nc, t, a, msgs, world, (PopOut*)out_dev,
-                       flags, seq, link);
-    return hipGetLastError();
-}
-
-template <typename KT>
-static void launch_shard_sweep_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
-                                    const PopArgs& a, const TaskClass& cl, uint64_t* cand, uint32_t* arrive,
-                                    PopLink* link, uint32_t seq, int prev_chained, const MboxArgs& mb,
-                                    hipStream_t st) {
-#define KBHIP_SOV(RR)                                                                                               \
-    hipLaunchKernelGGL((k_shard_sweep_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cl, cand, arrive, \
-                       link, seq, prev_chained, mb)
-    switch (R) {
-        case 1: KBHIP_SOV(1); break;
-        case 2: KBHIP_SOV(2); break;
-        case 4: KBHIP_SOV(4); break;
-        case 8: KBHIP_SOV(8); break;
-        default: KBHIP_SOV(16); break;
-    }
-#undef KBHIP_SOV
-}
-
-hipError_t launch_shard_sweep_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, const TaskClass& cl,
-                                 int n_tasks, int gang_mode, int min_avail, int ready_count, uint32_t epoch,
-                                 uint64_t* cand, uint32_t* arrive, const KeyFormat& kf, int fit_set, PopLink* link,
-                                 int prev_chained, const MboxArgs& mb, hipStream_t st) {
-    if (!link || mb.world < 1 || mb.seq < 1) return hipErrorInvalidValue;
-    int R;
-    const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 3, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
-    if (kf.use32) launch_shard_sweep_ov_t<uint32_t>(R, nb, cf, nc, t, a, cl, cand, arrive, link, mb.seq, prev_chained, mb, st);
-    else launch_shard_sweep_ov_t<uint64_t>(R, nb, cf, nc, t, a, cl, cand, arrive, link, mb.seq, prev_chained, mb, st);
-    return hipGetLastError();
-}
-
-template <typename KT>
-static void launch_pop_batch_ov_t(int R, int nb, const Conf& cf, const NodeCols& nc, const DevTables& t,
-                                  const PopArgs& a, const TaskClass& cl, uint64_t* cand, uint32_t* arrive, PopOut* o,
-                                  PopLink* link, uint32_t seq, int dep, uint32_t msg_from, hipStream_t st) {
-#define KBHIP_OV(RR)                                                                                              \
-    hipLaunchKernelGGL((k_pop_batch_ov<RR, KT>), dim3(nb), dim3(kPopThreads), 0, st, cf, nc, t, a, cl, cand, arrive, \
-                       o, link, seq, dep, msg_from)
-    switch (R) {
-        case 1: KBHIP_OV(1); break;
-        case 2: KBHIP_OV(2); break;
-        case 4: KBHIP_OV(4); break;
-        case 8: KBHIP_OV(8); break;
-        default: KBHIP_OV(16); break;
-    }
-#undef KBHIP_OV
-}
-
-hipError_t launch_pop_batch_ov(const Conf& cf, const NodeCols& nc, const DevTables& t, int cls, const TaskClass& cl,
-                               int n_tasks, int gang_mode, int min_avail, int ready_count, uint32_t epoch,
-                               uint64_t* cand, uint32_t* arrive, void* out_dev, hipStream_t st, const KeyFormat& kf,
-                               PopLink* link, uint32_t seq, int fit_set, int dep, uint32_t msg_from) {
-    if (seq < 1 || dep < 1 || dep > kMaxDep) return hipErrorInvalidValue;
-    int R;
-    const int nb = pop_blocks(nc.n, &R);
-    PopArgs a{cls, n_tasks, gang_mode, min_avail, ready_count, epoch, 2, kf.base, kf.shift, kf.idxmax,
-              kf.use32 && kf.ent32 ? 1 : 0, fit_set};
-    PopOut* o = (PopOut*)out_dev;
-    if (kf.use32) launch_pop_batch_ov_t<uint32_t>(R, nb, cf, nc, t, a, cl, cand, arrive, o, link, seq, dep, msg_from, st);
-    else launch_pop_batch_ov_t<uint64_t>(R, nb, cf, nc, t, a, cl, cand, arrive, o, link, seq, dep, msg_from, st);
-    return hipGetLastError();
-}
-
-size_t pop_out_bytes() { return sizeof(PopOut); }
-
-#ifdef KBHIP_STAMPS
-hipError_t set_stamp_buffer(uint64_t* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &p, sizeof(p)); }
-#endif
-#ifdef KBHIP_TIMELINE
-hipError_t set_timeline_buffer(uint64_t* p) { return hipMemcpyToSymbol(HIP_SYMBOL(g_tl), &p, sizeof(p)); }
-#endif
-
-#endif
+#include "kernels/shard.inc"  // node-array shard kernels, launchers (KBHIP_PART <= 1)
 }  // namespace kbhip
