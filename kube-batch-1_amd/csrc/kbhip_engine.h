@@ -15,10 +15,15 @@
 //     places the chunk (parallel levels, kbhip_batch.h) and writes the rows back;
 //   * the dispatcher block copies pop descriptors from the host's pinned ring
 //     into a device ring.
-// Pop p's workers read the node rows as pop p-3 left them; the candidates of
-// pops p-2 (left out by the workers) and p-1 (dropped by the placer from the
-// merged top-128) are the only rows that can have changed since, and the
-// placer holds both pops' rows.  So the placer sees every node's exact key.
+// Pop p's workers read the node rows as pop p-4 left them (its write-back is
+// drained before `done` reaches p-4) and leave out the candidates of pops p-3
+// and p-2; pop p-1's candidates may sit in the merged top-128 with stale keys
+// and the placer drops them.  Those three sets are the only rows that can have
+// changed since pop p-4, and the placer holds the rows of all three (four rings
+// of 64 rows) and re-evaluates them.  So the placer sees every node's exact key.
+// List mode keeps the same contract: the owner of pop p's class keys every
+// node on its rows as of pop p-4 or later (each applied after that pop's
+// `done`), leaves out pops p-3 and p-2's candidates, and packages the top 128.
 #pragma once
 #include <stdint.h>
 
@@ -54,6 +59,17 @@ enum : int { kDwCls = 0, kDwFlags, kDwMinAvail, kDwReady, kDwEpochSlot, kDwKbase
 // kDwFlags: m | gang << 8 | ent32 << 9 | op << 12
 enum : uint32_t { kEngOpPop = 0, kEngOpExit = 1 };
 
+// List mode: one owner block per task class keeps every
+// node's selection key for its class in LDS, updated from the rows each pop
+// touches; the owner of pop p's class writes pop p's package.  Owners read
+// the pops' candidates and classes from a log of kEngLog pops (the placer does
+// not overwrite an entry some owner has not applied yet: own_ap).
+constexpr int kEngLog = 64;
+constexpr int kEngOwnMax = 256;
+constexpr int kOwnSeg = 1792, kOwnSegs = 64, kOwnMaxN = kOwnSeg * kOwnSegs;  // nodes per owner (LDS key bytes: 112 KiB)
+static_assert(kOwnSeg % 256 == 0, "a segment is whole scan steps (64 lanes x 4 nodes)");
+constexpr int kOwnLv = 128;  // key levels (score - kbase + 1) an owner's byte holds: 1 .. kOwnLv - 1
+
 // Device control block (hipMalloc'ed, zeroed at each launch).
 struct EngCtl {
     uint32_t done;  // the last pop whose node write-back is visible (sc1)
@@ -62,6 +78,9 @@ struct EngCtl {
     uint32_t pad1[31];
     uint64_t desc[kEngRing][kEngDescWords];  // descriptors, slot seq % kEngRing
     uint64_t cands[kEngSlots][kEngCandCopies][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}, in copies
+    uint64_t tlog[kEngLog][64];  // list mode: pop p's candidates {p << 32 | node}, slot p % kEngLog
+    uint64_t tcls[kEngLog];      // ... and its class {p << 32 | cls}
+    uint32_t own_ap[kEngOwnMax]; // owner o: the last pop whose rows it applied (written by owner o only)
 };
 enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3 };
 
@@ -78,6 +97,12 @@ struct EngArgs {
     int nw, npb, ng;           // workers, nodes per worker, merger groups
     uint64_t* tl;              // diagnostic event timeline (option "engine_timeline"), or null
     int quick;                 // 0 (a test mode): no fast path, every feasible candidate through the levels rounds
+    // list mode (nown > 0): blocks [0, nown) own a class each; then the placer and the dispatcher
+    int nown;
+    const int32_t* own_cls;    // [nown] owner o's class
+    const int32_t* own_kbase;  // [nown] its key base (KeyFormat::base)
+    uint8_t* own_fb;           // [nown][npad] each node's FitDelta bits for the owner's class (owner-private)
+    int kshift, kidxmax;       // the session's 32-bit key format (KeyFormat::shift / idxmax)
 };
 // Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
 constexpr int kEngTlSlots = 32768, kEngTlEvents = 32;

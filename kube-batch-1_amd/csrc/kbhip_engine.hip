@@ -270,10 +270,8 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
 // The evaluation of a worker's node: the mutable row columns through sc1
 // (the placer writes them write-through from another CU), the static ones
 // plain; all loads issued before the predicates' early exits (eval_node).
-__device__ __forceinline__ uint64_t eng_eval(const Conf& cf, const TaskClass& c, const DevTables& t,
-                                             const NodeCols& nc, int n, uint32_t* fb) {
-    const uint8_t fl = nc.flags[n];
-    const Row r = load_row_sc1(nc, n);
+__device__ __forceinline__ uint64_t eng_eval_row(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                                 const NodeCols& nc, int n, const Row& r, uint8_t fl, uint32_t* fb) {
     const bool st = static_pred_f(cf, c, t, nc, n, fl);
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const uint64_t pw[4] = {0, 0, 0, 0};  // engine classes carry no host ports
@@ -282,6 +280,12 @@ __device__ __forceinline__ uint64_t eng_eval(const Conf& cf, const TaskClass& c,
     const uint64_t k = dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);
     *fb = fit_bits(c, r, passed);
     return k;
+}
+__device__ __forceinline__ uint64_t eng_eval(const Conf& cf, const TaskClass& c, const DevTables& t,
+                                             const NodeCols& nc, int n, uint32_t* fb) {
+    const uint8_t fl = nc.flags[n];
+    const Row r = load_row_sc1(nc, n);
+    return eng_eval_row(cf, c, t, nc, n, r, fl, fb);
 }
 
 // ---------------------------------------------------------------------------
@@ -332,12 +336,40 @@ struct EngPlacerLds {
     uint64_t gfit[2];            // ... and its FitDelta granules (stop 1)
     int ok;
     int gran_seq;                // the pop whose granules are in gran / gfit
+    uint32_t apmin;              // list mode: every owner has applied this pop (as last read)
+};
+// A class owner (list mode): its class's key byte for every node, the node
+// counts per level (and per segment of kOwnSeg nodes and level: the package
+// scan reads only the segments that hold its entries), the FitDelta counts.
+constexpr int kOwnHash = 1024;
+struct EngOwnerLds {
+    uint8_t sv[kOwnMaxN];             // node n: level << 1 | pipelined (0: not a candidate of the class)
+    uint32_t seg[kOwnLv / 2][kOwnSegs];  // nodes per (level, segment): level l in half l & 1 of word [l / 2]
+                                         // (a segment holds at most kOwnSeg < 2^16 nodes)
+    uint32_t lvl[kOwnLv];             // nodes per level
+    uint32_t fit[4];                  // FitDelta counts over every node (fit_bits)
+    int32_t hkey[kOwnHash];           // node set (an apply batch's nodes; a package's left-out nodes)
+    int32_t hval[kOwnHash];
+    uint32_t keys[kEngPkgN];          // the package's entries (unsorted until the sort)
+    uint32_t nkeys;
+    int32_t act[kOwnSegs];            // the segments the package scan reads ...
+    int32_t take[kOwnSegs];           // ... and how many level-L nodes it takes from each
+    int32_t nact, thr;                // their number; the threshold level L
+    int32_t xfit[4];                  // FitDelta bits of the left-out nodes
+    alignas(16) uint32_t desc[kEngDescWords];
+    int32_t next, dp, ok;             // wave 0's findings: own pop / exit / none, next descriptor to look at
+    uint32_t dn;                      // `done` as wave 0 last read it
 };
 union EngLds {
     EngWorkerLds w;
     EngMergerLds m;
     EngPlacerLds p;
 };
+union EngLdsList {
+    EngOwnerLds o;
+    EngPlacerLds p;
+};
+static_assert(sizeof(EngLdsList) <= 160 * 1024, "one block per CU");
 
 // ---------------------------------------------------------------------------
 // worker
@@ -757,6 +789,486 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
 }
 
 // ---------------------------------------------------------------------------
+// class owner (list mode)
+// ---------------------------------------------------------------------------
+// A node's key for the owner's class as one byte: level << 1 | pipelined,
+// level = score - kbase + 1 in [1, kOwnLv - 1] (the host admits only classes
+// whose score range fits); 0 = not a candidate.  The 32-bit selection key
+// (PopArgs) follows from the byte and the node index: the byte order is the
+// key order among nodes of one level, and the index breaks ties.
+__device__ __forceinline__ uint32_t own_val(uint64_t k64, int32_t kbase) {
+    if (!k64) return 0;
+    return ((uint32_t)(key_score(k64) - kbase + 1) << 1) | (uint32_t)(k64 & 1);
+}
+__device__ __forceinline__ uint32_t own_key(uint32_t v, int g, const EngArgs& A) {
+    return ((v >> 1) << A.kshift) | ((uint32_t)(A.kidxmax - g) << 1) | (v & 1);
+}
+// Level counts of node n with byte v (d = 1 or ~0u: add or remove).
+__device__ __forceinline__ void own_count(EngOwnerLds& L, int n, uint32_t v, uint32_t d) {
+    if (!v) return;
+    const uint32_t lv = v >> 1;
+    atomicAdd(&L.lvl[lv], d);
+    atomicAdd(&L.seg[lv >> 1][n / kOwnSeg], d << (16 * (lv & 1)));
+}
+__device__ __forceinline__ uint32_t own_segcnt(const EngOwnerLds& L, int lv, int sg) {
+    return (L.seg[lv >> 1][sg] >> (16 * (lv & 1))) & 0xffffu;
+}
+// Per wave: FitDelta counts from old to new bits of the lanes with `on`.
+__device__ __forceinline__ void own_fit_delta(EngOwnerLds& L, bool on, uint32_t ofb, uint32_t nfb) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t o = (ofb >> b) & 1u, n = (nfb >> b) & 1u;
+        const int up = __popcll(__ballot(on && n && !o)), dn = __popcll(__ballot(on && o && !n));
+        if (lane == b && up != dn) atomicAdd(&L.fit[b], (uint32_t)(up - dn));
+    }
+}
+// The node set (open addressing over kOwnHash slots; every user clears the
+// slots it filled before the next use).
+__device__ __forceinline__ int own_hslot(int n) { return (int)(((uint32_t)n * 2654435761u) >> 22); }
+__device__ __forceinline__ int own_hinsert(EngOwnerLds& L, int n, bool* fresh) {
+    static_assert(kOwnHash == 1024, "own_hslot takes 10 bits");
+    int h = own_hslot(n);
+    for (;;) {
+        const int old = atomicCAS(&L.hkey[h], -1, n);
+        if (old == -1 || old == n) {
+            *fresh = old == -1;
+            return h;
+        }
+        h = (h + 1) & (kOwnHash - 1);
+    }
+}
+__device__ __forceinline__ int own_hfind(const EngOwnerLds& L, int n) {
+    int h = own_hslot(n);
+    for (int i = 0; i < kOwnHash; ++i, h = (h + 1) & (kOwnHash - 1)) {
+        const int k = L.hkey[h];
+        if (k == n) return h;
+        if (k == -1) return -1;
+    }
+    return -1;
+}
+
+// Wave 0: pop q's logged candidate `lane` (-1: none); false: the wait gave up.
+__device__ __forceinline__ bool own_log_node(EngCtl* ctl, uint32_t q, int* node) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t* src = &ctl->tlog[q % kEngLog][lane];
+    EngWait wt(ctl, kEngWaitTicks);
+    for (;;) {
+        const uint64_t x = ld_sc1(src);
+        if (__ballot((uint32_t)(x >> 32) != q) == 0) {
+            *node = (int)(uint32_t)x;
+            return true;
+        }
+        if (!wt.tick()) return false;
+    }
+}
+
+// Wave 0: from descriptor dp on, the next pop of class cls (L.next = its
+// sequence number, its words in L.desc), the run's end (L.next = -2) or
+// neither yet (-1); L.dp = the first descriptor not looked at.  The ring's
+// slots are read together; a slot already reused by a later descriptor
+// belongs to a pop that ran — its class comes from the log (it is not this
+// owner's: that pop's package was this owner's to write).
+__device__ __forceinline__ bool own_scan_desc(const EngArgs& A, EngOwnerLds& L, int cls, uint32_t dp) {
+    const int lane = threadIdx.x & 63;
+    EngCtl* ctl = A.ctl;
+    uint64_t x[kEngRing];
+#pragma unroll
+    for (int i = 0; i < kEngRing; ++i) x[i] = ld_sc1(&ctl->desc[(dp + i) % kEngRing][lane]);
+    int next = -1;
+#pragma unroll
+    for (int i = 0; i < kEngRing; ++i) {
+        const uint32_t q = dp;
+        const uint32_t tg = (uint32_t)(x[i] >> 32);
+        if (__ballot(tg != q) == 0) {
+            const uint32_t w = (uint32_t)x[i];
+            const uint32_t flags = (uint32_t)__builtin_amdgcn_readlane((int)w, kDwFlags);
+            if (((flags >> 12) & 0xf) != kEngOpPop) { next = -2; break; }
+            if (__builtin_amdgcn_readlane((int)w, kDwCls) == cls) {
+                L.desc[lane] = w;
+                next = (int)q;
+                break;
+            }
+            ++dp;
+            continue;
+        }
+        if (__ballot((int32_t)(tg - q) > 0) == 0) break;  // not there yet
+        // reused: pop q ran; its class from the log
+        const uint64_t* src = &ctl->tcls[q % kEngLog];
+        EngWait wt(ctl, kEngWaitTicks);
+        uint64_t y;
+        for (;;) {
+            y = ld_sc1(src);
+            if ((uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(y >> 32)) == q) break;
+            if (!wt.tick()) return false;
+        }
+        if ((int)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)y) == cls) {  // cannot happen
+            if (lane == 0) __hip_atomic_store(&ctl->err, (uint32_t)kEngErrDesc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        ++dp;
+    }
+    if (lane == 0) {
+        L.next = next;
+        L.dp = (int)dp;
+    }
+    return true;
+}
+
+// Every wave: apply pops a0 .. a0 + nb - 1 (nb <= 8, each `done`): wave w
+// reads pop a0 + w's candidates' rows and re-keys them; a node of several of
+// these pops is applied once (every copy was read after the last one's
+// `done`).  A row read while a later pop writes it is torn or newer: that node
+// is a candidate of the later pop, applied again after its `done`, and left
+// out of every package until then.
+__device__ __forceinline__ bool own_apply(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                          const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, int32_t kbase, uint32_t a0,
+                                          int nb) {
+    const int wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    int node = -1;
+    bool ok = true;
+    if (wave < nb) ok = own_log_node(ctl, a0 + (uint32_t)wave, &node);
+    if (!ok && (threadIdx.x & 63) == 0) L.ok = 0;
+    Row r{};
+    uint8_t fl = 0;
+    uint32_t ofb = 0;
+    int hs = -1;
+    bool fresh = false;
+    if (node >= 0) {
+        fl = nc.flags[node];
+        r = load_row_sc1(nc, node);
+        ofb = ld_sc1(&fbh[node]);
+        hs = own_hinsert(L, node, &fresh);
+    }
+    uint32_t nfb = 0;
+    const uint32_t nv = node >= 0 ? own_val(eng_eval_row(cf, c, t, nc, node, r, fl, &nfb), kbase) : 0u;
+    __syncthreads();
+    if (node >= 0) atomicMax(&L.hval[hs], wave);  // the latest pop's copy is applied
+    __syncthreads();
+    const bool win = node >= 0 && L.hval[hs] == wave;
+    if (win) {
+        const uint32_t ov = L.sv[node];
+        L.sv[node] = (uint8_t)nv;
+        own_count(L, node, ov, ~0u);
+        own_count(L, node, nv, 1u);
+        st_sc1(&fbh[node], (uint8_t)nfb);
+    }
+    own_fit_delta(L, win, ofb, nfb);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bits are stored before a later batch reads them
+    __syncthreads();
+    if (node >= 0) { L.hkey[hs] = -1; L.hval[hs] = -1; }
+    return L.ok != 0;
+}
+
+// Every wave: pop p's package (its descriptor in L.desc) — the top 128 keys of
+// the class over every node but pops p-3 and p-2's candidates, with their rows
+// (the layout of eng_final) — and, once pop p-1's candidates are logged, pop
+// p's FitDelta counts over every node but the three sets (the placer counts
+// those on their final rows).
+__device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                            const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, uint32_t p) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    const EngDesc d = eng_decode(L.desc);
+    const PopArgs a = eng_args(d);
+    ETL(A, p, 10);
+    // 1. pops p-3 (wave 0) and p-2 (wave 1)'s candidates out of the counts and the scan
+    int xn = -1;
+    bool ok = true;
+    if (wave < 2) {
+        const uint32_t q = p - 3 + (uint32_t)wave;
+        if ((int32_t)(q - A.first) >= 0) ok = own_log_node(ctl, q, &xn);
+        if (!ok && lane == 0) L.ok = 0;
+    }
+    if (wave == 1) ETL(A, p, 11);
+    if (threadIdx.x < 4) L.xfit[threadIdx.x] = 0;
+    bool xf = false;
+    int xs = -1;
+    uint32_t xfb = 0;
+    if (xn >= 0) {
+        xs = own_hinsert(L, xn, &xf);
+        xfb = ld_sc1(&fbh[xn]);
+    }
+    __syncthreads();
+    uint32_t xv = 0;
+    if (xf) {
+        xv = L.sv[xn];
+        L.sv[xn] = 0;
+        own_count(L, xn, xv, ~0u);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const int k = __popcll(__ballot(xf && ((xfb >> b) & 1u)));
+        if (lane == 0 && k) atomicAdd((uint32_t*)&L.xfit[b], (uint32_t)k);
+    }
+    __syncthreads();
+    // 2. wave 0: the threshold level thr (fewer than 128 nodes above it, at least 128 at or
+    // above; or level 1 when fewer than 128 are left) and the segments holding the entries
+    if (wave == 0) {
+        static_assert(kOwnLv == 128, "two levels per lane");
+        const uint32_t c0 = lane ? L.lvl[2 * lane] : 0u, c1 = L.lvl[2 * lane + 1];  // levels 2 lane, 2 lane + 1
+        uint32_t s = c0 + c1;  // nodes at levels >= 2 lane
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_down((int)s, dd, 64);
+            if (lane + dd < 64) s += u;
+        }
+        const uint32_t s1 = s - c0;  // nodes at levels >= 2 lane + 1
+        const int bl = s1 >= (uint32_t)kEngPkgN ? 2 * lane + 1 : (lane && s >= (uint32_t)kEngPkgN) ? 2 * lane : 0;
+        int thr = bl;
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) thr = max(thr, __shfl_xor(thr, dd, 64));
+        if (thr == 0) thr = 1;  // fewer than 128 nodes: all of them
+        const int tl = thr >> 1;
+        // nodes above thr, at thr
+        const uint32_t s_tl = (uint32_t)__shfl((int)s, tl, 64), s1_tl = (uint32_t)__shfl((int)s1, tl, 64);
+        const uint32_t above = (thr & 1) ? s1_tl - (uint32_t)__shfl((int)c1, tl, 64) : s1_tl;
+        const uint32_t at = (thr & 1) ? (uint32_t)__shfl((int)c1, tl, 64) : s_tl - s1_tl;
+        const int need = (int)min((uint32_t)kEngPkgN - min(above, (uint32_t)kEngPkgN), at);
+        const uint64_t nz = __ballot(c0 + c1 != 0);
+        const int top = nz ? 2 * (63 - __builtin_clzll(nz)) + 1 : 0;
+        uint32_t hi = 0;  // (lane = segment)
+        for (int lv = thr + 1; lv <= top; ++lv) hi += own_segcnt(L, lv, lane);
+        const uint32_t eq = own_segcnt(L, thr, lane);
+        uint32_t inc = eq;  // inclusive prefix over segments
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_up((int)inc, dd, 64);
+            if (lane >= dd) inc += u;
+        }
+        const int tk = max(0, min(need - (int)(inc - eq), (int)eq));
+        const bool act = hi > 0 || tk > 0;
+        const uint64_t am = __ballot(act);
+        const int pos = __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0));
+        if (act) {
+            L.act[pos] = lane;
+            L.take[pos] = tk;
+        }
+        if (lane == 0) {
+            L.nact = __popcll(am);
+            L.thr = thr;
+            L.nkeys = 0;
+        }
+    }
+    __syncthreads();
+    // 3. the entries: wave w scans active segments w, w + 8, ... in index order (every node
+    // above thr, the first take[] nodes at thr)
+    {
+        const int thr = L.thr, nact = L.nact;
+        for (int i = wave; i < nact; i += kPopThreads / 64) {
+            const int sg = L.act[i], tk = L.take[i];
+            const uint32_t* w32 = (const uint32_t*)&L.sv[sg * kOwnSeg];
+            int run = 0;  // nodes at thr before this step (index order)
+#pragma unroll 2
+            for (int j = 0; j < kOwnSeg / 256; ++j) {
+                const uint32_t wv = w32[j * 64 + lane];
+                const int n0 = sg * kOwnSeg + (j * 64 + lane) * 4;
+                int below = 0, tot = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t v = (wv >> (8 * b)) & 0xffu;
+                    const uint64_t bm = __ballot(v != 0 && (int)(v >> 1) == thr);
+                    below += __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
+                    tot += __popcll(bm);
+                }
+                int k_in = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t v = (wv >> (8 * b)) & 0xffu;
+                    bool take = false;
+                    if (v && (int)(v >> 1) > thr) {
+                        take = true;
+                    } else if (v && (int)(v >> 1) == thr) {
+                        take = run + below + k_in < tk;
+                        ++k_in;
+                    }
+                    if (take) {
+                        const uint32_t at = atomicAdd(&L.nkeys, 1u);
+                        if (at < (uint32_t)kEngPkgN) L.keys[at] = own_key(v, n0 + b + nc.base, A);
+                    }
+                }
+                run += tot;
+            }
+        }
+    }
+    __syncthreads();
+    // 4. the left-out nodes back; wave 0 sorts the entries (two sorted 64-lists, merged)
+    if (xf) {
+        L.sv[xn] = (uint8_t)xv;
+        own_count(L, xn, xv, 1u);
+    }
+    if (wave == 0) {
+        const uint32_t nk = L.nkeys;
+        uint32_t a0 = (uint32_t)lane < nk ? L.keys[lane] : 0u, a1 = (uint32_t)(64 + lane) < nk ? L.keys[64 + lane] : 0u;
+        a0 = wave_sort_desc(a0);
+        a1 = wave_sort_desc(a1);
+        const uint32_t r = reverse_lanes(a1);
+        const uint32_t hi = a0 > r ? a0 : r, lo = a0 > r ? r : a0;
+        a0 = bitonic_clean_desc(hi);
+        a1 = bitonic_clean_desc(lo);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        L.keys[lane] = a0;
+        L.keys[64 + lane] = a1;
+        ETL(A, p, 12);
+    }
+    __syncthreads();
+    // 5. the package (waves 0, 1: entry 64 * wave + lane; eng_final's layout)
+    EngPkg* pk = A.pkg + (p % kEngSlots);
+    const uint64_t tag = (uint64_t)p << 32;
+    if (wave < 2) {
+        const int e = 64 * wave + lane;
+        const uint32_t k = L.keys[e];
+        const int n = k ? key_node(k, a) - nc.base : -1;
+        uint32_t v[kEngPkgFields];
+#pragma unroll
+        for (int f = 0; f < kEngPkgFields; ++f) v[f] = 0;
+        v[kPkKey] = k;
+        if (n >= 0) {
+            const Row r = load_row_sc1(nc, n);
+            const uint8_t fl = nc.flags[n];
+            const int32_t na = cf.score_mult ? na_weight(c, t, nc, n) : 0;
+            const uint64_t pw[4] = {0, 0, 0, 0};
+            const uint32_t* rw = (const uint32_t*)&r;
+#pragma unroll
+            for (int f = 0; f < (int)(sizeof(Row) / 4); ++f) v[kPkRow + f] = rw[f];
+            v[kPkFlags] = fl;
+            v[kPkNa] = (uint32_t)na;
+            v[kPkS1] = (uint32_t)depth1_score(cf, nc, t, c, r, pw, n, na, key64_of(k, a));
+        }
+#pragma unroll
+        for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
+        if (wave == 0) ETL(A, p, 13);
+    }
+    // 6. wave 2: pop p's FitDelta counts once pop p-1's candidates are logged
+    if (wave == 2 && L.ok) {
+        int n1 = -1;
+        if ((int32_t)(p - 1 - A.first) >= 0) ok = own_log_node(ctl, p - 1, &n1);
+        const bool in = ok && n1 >= 0 && own_hfind(L, n1) < 0;  // not a left-out node (counted there)
+        const uint32_t fb1 = in ? ld_sc1(&fbh[n1]) : 0u;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t k = (uint32_t)__popcll(__ballot(in && ((fb1 >> b) & 1u)));
+            if (lane == b) cnt = L.fit[b] - (uint32_t)L.xfit[b] - k;
+        }
+        if (ok && lane < 4) st_sc1(&A.blists[(size_t)(p % kEngSlots) * kEngListWords + 128 + lane], tag | cnt);
+        if (!ok && lane == 0) L.ok = 0;
+        ETL(A, p, 18);
+    }
+    __syncthreads();
+    if (xn >= 0) { L.hkey[xs] = -1; L.hval[xs] = -1; }
+    return L.ok != 0;
+}
+
+__device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
+                                          EngOwnerLds& L, int o) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    EngCtl* ctl = A.ctl;
+    const int cls = A.own_cls[o];
+    const int32_t kbase = A.own_kbase[o];
+    const TaskClass& c = t.classes[cls];  // (read field by field where used: scalar loads)
+    uint8_t* fbh = A.own_fb + (size_t)o * nc.npad;
+    const int N = nc.n;
+    // every node's key for the class (rows written by pops of this run meanwhile are read
+    // again when those pops are applied)
+    for (int i = threadIdx.x; i < kOwnLv / 2 * kOwnSegs; i += kPopThreads) (&L.seg[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kOwnHash; i += kPopThreads) { L.hkey[i] = -1; L.hval[i] = -1; }
+    for (int i = threadIdx.x; i < kOwnLv; i += kPopThreads) L.lvl[i] = 0;
+    if (threadIdx.x < 4) L.fit[threadIdx.x] = 0;
+    if (threadIdx.x == 0) L.ok = 1;
+    __syncthreads();
+    const int nend = ((N + kOwnSeg - 1) / kOwnSeg) * kOwnSeg;
+    for (int n0 = 0; n0 < nend; n0 += 2 * kPopThreads) {
+        uint32_t v[2] = {0, 0}, fb[2] = {0, 0};
+        uint64_t k[2] = {0, 0};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // two nodes per thread in flight
+            const int n = n0 + u * kPopThreads + (int)threadIdx.x;
+            if (n < N) k[u] = eng_eval(cf, c, t, nc, n, &fb[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int n = n0 + u * kPopThreads + (int)threadIdx.x;
+            v[u] = own_val(k[u], kbase);
+            if (n < nend) L.sv[n] = (uint8_t)v[u];
+            if (n < N) fbh[n] = (uint8_t)fb[u];
+            fit_block_add(L.fit, fb[u]);
+            // level counts, aggregated per wave (a wave's 64 nodes share a segment)
+            uint64_t act = __ballot(v[u] != 0);
+            while (act) {
+                const int l0 = __builtin_ctzll(act);
+                const uint32_t lv = (uint32_t)__shfl((int)v[u], l0, 64) >> 1;
+                const uint64_t m = __ballot(v[u] != 0 && (v[u] >> 1) == lv);
+                if (lane == l0) {
+                    atomicAdd(&L.lvl[lv], (uint32_t)__popcll(m));
+                    atomicAdd(&L.seg[lv >> 1][n / kOwnSeg], (uint32_t)__popcll(m) << (16 * (lv & 1)));
+                }
+                act &= ~m;
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t ap = A.first - 1;  // the last pop whose rows are applied
+    uint32_t dp = A.first;      // the next descriptor to look at
+    uint64_t t0 = 0;            // wave 0: since when nothing has changed
+    int seen = -1;              // wave 0 (timeline): the last own pop seen
+    for (;;) {
+        if (wave == 0) {
+            bool ok = own_scan_desc(A, L, cls, dp);
+            if (lane == 0) {
+                L.dn = ld_sc1(&ctl->done);
+                if (!ok) L.ok = 0;
+            }
+        }
+        __syncthreads();
+        if (!L.ok) return;
+        const int next = L.next;
+        const uint32_t dn = L.dn;
+        const bool moved = (uint32_t)L.dp != dp;
+        if (next >= 0 && next != seen && wave == 0) {  // timeline: this owner's pop seen
+            ETL(A, (uint32_t)next, 20);
+            seen = next;
+        }
+        dp = (uint32_t)L.dp;
+        if (next == -2) {  // the run's end: no package of this owner is pending
+            if (threadIdx.x == 0) st_sc1(&ctl->own_ap[o], ap + (1u << 30));
+            return;
+        }
+        // apply the pops that are done, up to pop next - 4 (or up to the last one looked at)
+        const uint32_t want = next >= 0 ? (uint32_t)next - 4 : dp - 1;
+        const uint32_t bound = (int32_t)(dn - want) < 0 ? dn : want;
+        if ((int32_t)(bound - ap) > 0) {
+            const int nb = min((int)(bound - ap), kPopThreads / 64);
+            if (!own_apply(cf, nc, t, c, A, L, fbh, kbase, ap + 1, nb)) return;
+            ap += (uint32_t)nb;
+            if (threadIdx.x == 0) st_sc1(&ctl->own_ap[o], ap);
+            t0 = 0;
+            continue;
+        }
+        if (next >= 0 && (int32_t)(ap - ((uint32_t)next - 4)) >= 0) {
+            if (!own_package(cf, nc, t, c, A, L, fbh, (uint32_t)next)) return;
+            dp = (uint32_t)next + 1;
+            t0 = 0;
+            continue;
+        }
+        if (wave == 0 && !moved) {  // nothing new: a bounded wait
+            __builtin_amdgcn_s_sleep(2);
+            const uint64_t now = eng_now();
+            if (!t0) t0 = now;
+            if (lane == 0 && (ld_sc1(&ctl->err) != 0 || now - t0 > kEngDescTicks)) {
+                if (ld_sc1(&ctl->err) == 0)
+                    __hip_atomic_store(&ctl->err, (uint32_t)kEngErrDesc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                L.ok = 0;
+            }
+        }
+        if (moved) t0 = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // placer
 // ---------------------------------------------------------------------------
 static_assert(sizeof(Row) == 4 * (kPkFlags - kPkRow), "the package carries a Row as 28 32-bit words");
@@ -770,7 +1282,7 @@ static_assert(kEngDescClass + sizeof(TaskClass) / 4 <= kEngDescWords, "a descrip
 // columns.  The row stores are left in flight: the next pop drains them
 // before it publishes its candidates, and only then raises `done` for this
 // pop (*pend).
-template <typename ET>
+template <bool LIST, typename ET>
 __device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                            const PopArgs& a, const EngArgs& A, EngPlacerLds& L, uint32_t p, int r0,
                                            const PlaceDec<ET>& D, uint32_t* pend) {
@@ -780,7 +1292,16 @@ __device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, c
     if (D.stop == 1) {
         uint32_t fr = 0;  // group g's count b in lane 4g + b (fit_sum layout)
         const int g = lane >> 2;
-        if (A.ng == 0) {  // the worker count words: two 16-bit counts each, count b in lane b
+        if constexpr (LIST) {  // list mode: the class owner's four count words (count b in lane b)
+            const uint64_t* s = A.blists + (size_t)(p % kEngSlots) * kEngListWords + 128 + (lane & 3);
+            uint64_t x = lane < 4 ? ld_sc1(s) : ((uint64_t)p << 32);
+            EngWait wt(ctl, kEngWaitTicks);
+            while (__ballot((uint32_t)(x >> 32) != p) != 0) {
+                if (!wt.tick()) break;
+                if (lane < 4) x = ld_sc1(s);
+            }
+            fr = lane < 4 ? (uint32_t)x : 0u;
+        } else if (A.ng == 0) {  // the worker count words: two 16-bit counts each, count b in lane b
             uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
             for (int i0 = 0; i0 < A.nw; i0 += 64) {
                 const int i = i0 + lane;
@@ -841,6 +1362,29 @@ __device__ __forceinline__ void eng_publish_done(EngCtl* ctl, uint32_t* pend) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if ((threadIdx.x & 63) == 0) st_sc1(&ctl->done, *pend);
     *pend = 0;
+}
+
+// Wave 0 (list mode): until every owner has applied pop `want` (L.apmin: the
+// owners' minimum as last read).  false: the wait gave up.
+__device__ __forceinline__ bool eng_own_apmin(const EngArgs& A, EngPlacerLds& L, uint32_t want) {
+    const int lane = threadIdx.x & 63;
+    EngWait wt(A.ctl, kEngWaitTicks);
+    for (;;) {
+        uint32_t m = 0xffffffffu;  // the minimum of (ap - want) as signed distances, biased
+        for (int o = lane; o < A.nown; o += 64) {
+            const uint32_t d = ld_sc1(&A.ctl->own_ap[o]) - want + 0x80000000u;
+            m = d < m ? d : m;
+        }
+#pragma unroll
+        for (int dd = 1; dd < 64; dd <<= 1) {
+            const uint32_t u = (uint32_t)__shfl_xor((int)m, dd, 64);
+            m = u < m ? u : m;
+        }
+        const uint32_t mn = m - 0x80000000u + want;  // the owners' minimum
+        if (lane == 0) L.apmin = mn;
+        if ((int32_t)(mn - want) >= 0) return true;
+        if (!wt.tick()) return false;
+    }
 }
 
 // Wave 5: pop p's result granules (from LDS, eng_finish) to the host's pinned slot.
@@ -1111,6 +1655,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
 //       wave 5 stores the results to the host, the other waves prepare pop p+1's front.
 // The workers of pop p leave out pops p-3 / p-2's candidates and may hold stale
 // keys of pop p-1's: every node of the three sets is re-evaluated here.
+template <bool LIST>
 __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                                            EngPlacerLds& L) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1121,6 +1666,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1;
         L.hash_seq = L.drop_seq = (int)A.first - 1;
         L.sort_seq[0] = L.sort_seq[1] = L.sort_seq[2] = (int)A.first - 1;
+        L.apmin = A.first - 1;
     }
     __syncthreads();
     eng_front(cf, nc, t, A, L, A.first, wave);
@@ -1190,9 +1736,18 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             }
             const int n = top ? key_node(top, a) : -1;
             eng_publish_done(ctl, &pend);  // pop p-1's write-back (every node a worker may read next)
+            if constexpr (LIST) {
+                // list mode: the log entry of pop p, once every owner has applied pop p - kEngLog
+                if ((int32_t)(L.apmin - (p - kEngLog)) < 0 && !eng_own_apmin(A, L, p - kEngLog)) {
+                    if (lane == 0) __hip_atomic_store(&L.ok, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                st_sc1(&ctl->tlog[p % kEngLog][lane], ((uint64_t)p << 32) | (uint32_t)n);
+                if (lane == 0) st_sc1(&ctl->tcls[p % kEngLog], ((uint64_t)p << 32) | (uint32_t)a.cls);
+            } else {
 #pragma unroll
-            for (int cp = 0; cp < kEngCandCopies; ++cp)
-                st_sc1(&ctl->cands[p % kEngSlots][cp][lane], ((uint64_t)p << 32) | (uint32_t)n);
+                for (int cp = 0; cp < kEngCandCopies; ++cp)
+                    st_sc1(&ctl->cands[p % kEngSlots][cp][lane], ((uint64_t)p << 32) | (uint32_t)n);
+            }
             int src = n >= 0 ? rc_find(&rc, n) : -1;  // a previous pop's candidate, or a package entry
             if (n >= 0 && src < 0) {  // (every node of the list is one of those: kept for safety)
                 src = 64 * r0 + lane;
@@ -1222,7 +1777,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 ETL(A, p, 6);
                 if (lane == 0 && A.tl)
                     A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 30] = (uint64_t)D.done | ((uint64_t)D.stop << 8);
-                eng_finish(cf, nc, t, c, a, A, L, p, r0, D, &pend);
+                eng_finish<LIST>(cf, nc, t, c, a, A, L, p, r0, D, &pend);
             } else if (lane == 0) {  // (a class with host ports: never sent to the engine, eng_eligible)
                 __hip_atomic_store(&ctl->err, (uint32_t)kEngErrClass, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __hip_atomic_store(&L.ok, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1295,20 +1850,35 @@ __global__ __launch_bounds__(kPopThreads) void k_engine(Conf cf, NodeCols nc, De
     } else if (b == A.nw + A.ng) {
         eng_final(cf, nc, t, A, lds.m);
     } else if (b == A.nw + A.ng + 1) {
-        eng_placer(cf, nc, t, A, lds.p);
+        eng_placer<false>(cf, nc, t, A, lds.p);
     } else if (threadIdx.x < 64) {
         eng_dispatch(A);
     }
 }
 
-int engine_grid(const EngArgs& A) { return A.nw + A.ng + 3; }
+// List mode: class owners, the placer, the dispatcher.  A
+// kernel of its own, so that the owners' registers do not weigh on the sweep
+// engine's placer.
+__global__ __launch_bounds__(kPopThreads) void k_engine_lists(Conf cf, NodeCols nc, DevTables t, EngArgs A) {
+    __shared__ EngLdsList lds;
+    const int b = blockIdx.x;
+    if (b < A.nown) eng_owner(cf, nc, t, A, lds.o, b);
+    else if (b == A.nown) eng_placer<true>(cf, nc, t, A, lds.p);
+    else if (threadIdx.x < 64) eng_dispatch(A);
+}
+
+int engine_grid(const EngArgs& A) { return A.nown > 0 ? A.nown + 2 : A.nw + A.ng + 3; }
 
 hipError_t launch_engine(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A, hipStream_t st) {
-    hipLaunchKernelGGL(k_engine, dim3(engine_grid(A)), dim3(kPopThreads), 0, st, cf, nc, t, A);
+    if (A.nown > 0)
+        hipLaunchKernelGGL(k_engine_lists, dim3(engine_grid(A)), dim3(kPopThreads), 0, st, cf, nc, t, A);
+    else
+        hipLaunchKernelGGL(k_engine, dim3(engine_grid(A)), dim3(kPopThreads), 0, st, cf, nc, t, A);
     return hipGetLastError();
 }
 
-hipError_t engine_occupancy(int* blocks_per_cu) {
+hipError_t engine_occupancy(int* blocks_per_cu, bool lists) {
+    if (lists) return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_engine_lists, kPopThreads, 0);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_engine, kPopThreads, 0);
 }
 

@@ -216,7 +216,7 @@ size_t pop_out_bytes();
 // grid of engine_grid(A) blocks serving batched pops from a descriptor ring.
 struct EngArgs;
 hipError_t launch_engine(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A, hipStream_t st);
-hipError_t engine_occupancy(int* blocks_per_cu);
+hipError_t engine_occupancy(int* blocks_per_cu, bool lists = false);  // lists: the list-mode kernel
 int engine_grid(const EngArgs& A);
 #ifdef KBHIP_STAMPS
 hipError_t set_stamp_buffer(uint64_t* p);

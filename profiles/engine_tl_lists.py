@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Event timeline of the persistent pop engine in list mode (diagnostic;
+option "engine_timeline", kbhip_engine.hip ETL stamps, 100 MHz): one C4
+session, then per-phase medians.  Prints one JSON line.
+
+Placer events as in engine_tl.py (0 iteration start .. 8 granules stored, 15
+the next pop's package in LDS).  The owner of pop p's class:
+20 pop p seen among the descriptors, 10 package start (rows applied up to pop
+p-4), 11 pop p-2's candidates seen, 12 entries sorted, 13 package stored, 18
+FitDelta counts stored.  28: dispatcher forwarded."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+import kbgen  # noqa: E402
+import kbhip  # noqa: E402
+
+SLOTS, EV = 32768, 32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--pending", type=int, default=800_000)
+    ap.add_argument("--lists", type=int, default=1)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    path = f"/tmp/kbhip_bench/c4_{a.nodes}_{a.pending}_{kbgen.BASE_SEED + 4}.kbs"
+    if not os.path.exists(path):
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        kbgen.gen_c4(path, n_nodes=a.nodes, n_pending=a.pending)
+    buf = open(path, "rb").read()
+    with kbhip.Session(buf) as s:  # warm
+        s.set_option("engine_lists", a.lists)
+        s.allocate()
+    with kbhip.Session(buf) as s:
+        s.set_option("engine_lists", a.lists)
+        s.set_option("engine_timeline", 1)
+        s.allocate()
+        st = s.stats()
+        raw = np.zeros(SLOTS * EV, np.uint64)
+        n = kbhip.lib().kbhip_debug_table(s._h, b"engine_tl", raw.ctypes.data, raw.nbytes)
+        assert n == raw.nbytes
+    t = raw.reshape(SLOTS, EV).astype(np.int64)
+    pops = t[:, 31]
+    order = np.argsort(pops)
+    t, pops = t[order], pops[order]
+    keep = (pops > 100) & np.all(t[:, [0, 1, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 20, 28]] > 0, axis=1)
+    t = t[keep]
+    pops = t[:, 31]
+    cont = np.diff(pops) == 1
+    us = lambda x: round(float(np.median(x)) / 100.0, 3)  # 100 MHz ticks -> us
+    prev = lambda k: (pops[k:] - pops[:-k]) == k
+    per = {}
+    per["period"] = us(np.diff(t[:, 0])[cont])
+    per["placer 0->3 P2"] = us(t[:, 3] - t[:, 0])
+    per["placer 3->4 P3"] = us(t[:, 4] - t[:, 3])
+    per["placer 5->6 decided"] = us(t[:, 6] - t[:, 5])
+    per["placer 6->7 rows written"] = us(t[:, 7] - t[:, 6])
+    per["placer 7 -> next 0"] = us((t[1:, 0] - t[:-1, 7])[cont])
+    per["placer 5->15 next package in LDS"] = us(t[:, 15] - t[:, 5])
+    per["owner seen(20) - placer start(0)"] = us(t[:, 20] - t[:, 0])
+    per["owner seen(20) -> start(10)"] = us(t[:, 10] - t[:, 20])
+    per["owner start(10) - placer start(0)"] = us(t[:, 10] - t[:, 0])
+    per["owner start(10) -> p-2 cands(11)"] = us(t[:, 11] - t[:, 10])
+    per["owner p-2 cands(11) -> sorted(12)"] = us(t[:, 12] - t[:, 11])
+    per["owner sorted(12) -> stored(13)"] = us(t[:, 13] - t[:, 12])
+    per["owner stored(13) - placer start(0)"] = us(t[:, 13] - t[:, 0])
+    per["owner p-2 cands seen(11,p) - placer P3(4,p-2)"] = us((t[2:, 11] - t[:-2, 4])[prev(2)])
+    per["owner start(10,p) - placer P3(4,p-3) (done p-4)"] = us((t[3:, 10] - t[:-3, 4])[prev(3)])
+    per["owner stored(13,p) - placer 15(p-1) package in LDS"] = us((t[1:, 13] - t[:-1, 15])[cont])
+    per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
+    per_all = np.diff(t[:, 0])[cont] / 100.0
+    res = {"pops": int(len(t)), "lists": a.lists,
+           "stats": {k: st[k] for k in ("engine_pops", "engine_launches", "engine_workers", "engine_owners",
+                                        "alloc_device_s", "batched_pops", "host_wait_s")},
+           "median_us": per,
+           "period_us": {"mean": round(float(per_all.mean()), 3),
+                         "quantiles_10_50_90_99": [round(float(np.quantile(per_all, q)), 2) for q in (0.1, 0.5, 0.9, 0.99)]}}
+    print(json.dumps(res))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

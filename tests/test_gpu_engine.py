@@ -32,21 +32,25 @@ def _run(lib, path, **opts):
     return [(int(p), int(n), 4 if k == 1 else 8) for p, n, k in zip(pod, node, kind)], ns, st, close
 
 
+@pytest.mark.parametrize("lists", [1, 0])
 @pytest.mark.parametrize("seed", range(32))
-def test_engine_random_snapshots(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+def test_engine_random_snapshots(engine, oracle_mod, kbgen_mod, tmp_path, seed, lists):
     """Feature-rich small snapshots: engine pops (resource / selector / taint
     classes) between launched ones (host ports, backfill annotation), against
-    the faithful restatement and the launched path."""
+    the faithful restatement and the launched path; list mode (class owners,
+    DESIGN.md §4.11) and sweep mode."""
     c = kbgen_mod.gen_random(5100 + seed, n_nodes=4 + seed % 13, n_jobs=4 + seed % 9, max_tasks=1 + seed % 9,
                              features=NO_POD_AFFINITY, tiers=TIERS[seed % 4], n_queues=1 + seed % 3)
     p = str(tmp_path / "r.kbs")
     c.write(p)
     exp, ons = oracle_mod.ref_allocate(p, with_nodes=True)
     exp_close = oracle_mod.ref_gang_close(p)
-    got, ns, st, close = _run(engine, p)
+    got, ns, st, close = _run(engine, p, engine_lists=lists)
     assert got == exp.as_list()
     assert np.array_equal(ns.astype(np.float64), ons[:ns.shape[0]])
     assert close == exp_close
+    if st["engine_pops"]:
+        assert (st["engine_owners"] > 0) == bool(lists)
     ref, ns0, st0, close0 = _run(engine, p, engine=0)
     assert ref == got and np.array_equal(ns0, ns) and close0 == close
     assert st0["engine_pops"] == 0
@@ -59,7 +63,7 @@ def test_engine_worker_shapes(engine, oracle_mod, kbgen_mod, tmp_path, workers):
     p = str(tmp_path / "c2w.kbs")
     kbgen_mod.gen_c2(p, n_nodes=3000, n_pending=20000, seed=9300 + workers)
     exp = oracle_mod.fast_allocate(p, threads=8).as_list()
-    got, ns, st, close = _run(engine, p, engine_workers=workers)
+    got, ns, st, close = _run(engine, p, engine_workers=workers, engine_lists=0)
     assert got == exp
     assert st["engine_workers"] == workers and st["engine_pops"] == st["batched_pops"] > 100
     ref, ns0, _, close0 = _run(engine, p, engine=0)
@@ -96,8 +100,9 @@ def test_engine_c2_levels_only(engine, oracle_mod, kbgen_mod, tmp_path):
     assert got1 == exp and np.array_equal(ns1, ns)
 
 
+@pytest.mark.parametrize("lists", [1, 0])
 @pytest.mark.parametrize("speculate", [2, 0])
-def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path, speculate):
+def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path, speculate, lists):
     """A crowded cluster: many pops end on a task with no node, so the gang
     close messages carry the FitDelta histograms the engine counts (workers'
     counts without the previous pops' candidates, the placer's re-evaluated
@@ -125,21 +130,23 @@ def test_engine_unplaceable_gangs(engine, oracle_mod, kbgen_mod, tmp_path, specu
     exp = oracle_mod.ref_allocate(p).as_list()
     exp_close = oracle_mod.ref_gang_close(p)
     t0 = time.time()
-    got, ns, st, close = _run(engine, p, speculate=speculate)
+    got, ns, st, close = _run(engine, p, speculate=speculate, engine_lists=lists)
     assert time.time() - t0 < 20
     assert got == exp
     assert close == exp_close and len(close) > 5
     assert st["unassigned_pops"] > 5 and st["engine_pops"] > 20
 
 
-def test_engine_c4_scaled(engine, oracle_mod, kbgen_mod, tmp_path):
+@pytest.mark.parametrize("lists", [1, 0])
+def test_engine_c4_scaled(engine, oracle_mod, kbgen_mod, tmp_path, lists):
     """C4's shape at 20k nodes x 120k pods through the engine (every pop)."""
     p = str(tmp_path / "c4s.kbs")
     kbgen_mod.gen_c4(p, n_nodes=20000, n_pending=120000)
     exp = oracle_mod.fast_allocate(p, threads=16).as_list()
-    got, _, st, _ = _run(engine, p)
+    got, _, st, _ = _run(engine, p, engine_lists=lists)
     assert got == exp
     assert st["engine_pops"] == st["batched_pops"] and st["engine_launches"] <= 3
+    assert (st["engine_owners"] > 0) == bool(lists)
 
 
 def test_engine_idle_restart(engine, oracle_mod, kbgen_mod, tmp_path):
