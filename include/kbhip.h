@@ -126,6 +126,8 @@ typedef struct kbhip_stats {
     int64_t engine_launches; /* launches of the engine's resident grid (one per run of engine pops) */
     int64_t engine_workers;  /* its worker blocks (0: the engine was not used) */
     int64_t engine_owners;   /* list mode (option "engine_lists"): its class-owner blocks (0: sweep mode) */
+    int64_t engine_not_resident; /* engine grids that could not become resident (other kernels held CUs)
+                                    and were started again */
 } kbhip_stats;
 
 /* Library / device probe: returns the number of usable gfx950 devices (>= 0),

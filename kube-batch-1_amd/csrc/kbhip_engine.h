@@ -76,13 +76,18 @@ struct EngCtl {
     uint32_t pad0[31];
     uint32_t err;   // first error (kEngErr*), 0: none; every wait gives up once it is set
     uint32_t pad1[31];
+    uint32_t arrive;  // blocks that have started (the grid runs only once every block is resident)
+    uint32_t pad2[63];
     uint64_t desc[kEngRing][kEngDescWords];  // descriptors, slot seq % kEngRing
     uint64_t cands[kEngSlots][kEngCandCopies][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}, in copies
     uint64_t tlog[kEngLog][64];  // list mode: pop p's candidates {p << 32 | node}, slot p % kEngLog
     uint64_t tcls[kEngLog];      // ... and its class {p << 32 | cls}
     uint32_t own_ap[kEngOwnMax]; // owner o: the last pop whose rows it applied (written by owner o only)
 };
-enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3 };
+enum : uint32_t { kEngErrWait = 1, kEngErrDesc = 2, kEngErrClass = 3, kEngErrResident = 4 };
+// kEngErrResident: not every block of the grid became resident within kEngArriveTicks (other
+// kernels hold CUs — another session's, or another process's); the grid ends at once, serving
+// nothing, and the host starts it again (not a fault).  The exit word then carries bit 42.
 
 // Kernel arguments beyond the session's tables.
 struct EngArgs {
@@ -91,7 +96,8 @@ struct EngArgs {
     uint64_t* glists;          // [kEngSlots][ng][kEngListWords] group lists (+ 4 count words)
     EngPkg* pkg;               // [kEngSlots] the final merger's packages
     const uint64_t* hring;     // [kEngHostRing][kEngDescWords] pinned host descriptors (device view)
-    uint64_t* hexit;           // pinned host word: {exit seq | idle << 40 | 1 << 41} when the engine ends
+    uint64_t* hexit;           // pinned host word: {exit seq | idle << 40 | 1 << 41 | not resident << 42} at the end
+    uint32_t idle_ticks;       // the dispatcher ends the run after this long without a descriptor (100 MHz)
     void* out;                 // result slots (PopOut, pinned host memory, device view)
     uint32_t first;            // the first pop of this launch (earlier pops are written back)
     int nw, npb, ng;           // workers, nodes per worker, merger groups
@@ -104,7 +110,8 @@ struct EngArgs {
     uint8_t* own_fb;           // [nown][npad] each node's FitDelta bits for the owner's class (owner-private)
     int kshift, kidxmax;       // the session's 32-bit key format (KeyFormat::shift / idxmax)
 };
+constexpr uint32_t kEngIdleTicks = 10000000u;  // 100 ms without a descriptor: the run ends (100 MHz ticks)
 // Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
-constexpr int kEngTlSlots = 32768, kEngTlEvents = 32;
+constexpr int kEngTlSlots = 32768, kEngTlEvents = 48;
 
 }  // namespace kbhip

@@ -20,7 +20,7 @@
 namespace kbhip {
 
 constexpr uint64_t kEngWaitTicks = 200000000ull;  // 2 s at 100 MHz: a pipeline wait that long is a fault
-constexpr uint64_t kEngIdleTicks = 100000000ull;  // 1 s without a descriptor: the dispatcher ends the run
+constexpr uint64_t kEngArriveTicks = 500000ull;  // 5 ms for every block of the grid to start (co-residency)
 constexpr uint64_t kEngDescTicks = 400000000ull;  // a block waiting for its next descriptor
 
 __device__ __forceinline__ uint64_t eng_now() { return __builtin_amdgcn_s_memrealtime(); }
@@ -323,6 +323,7 @@ struct EngPlacerLds {
     uint8_t fkind[3][64], ffb[3][64];
     int32_t fna[3][64], fs1a[3][64], fs1p[3][64];
     int rows_seq;                // the last pop whose candidates' rows are in their ring (eng_finish)
+    int xn_seq;                  // the last pop whose candidates are in their ring of L.xn (P3)
     uint8_t x2use[64], x3use[64];  // pop p-2's candidate not p-1's; pop p-3's neither
     int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
@@ -342,18 +343,29 @@ struct EngPlacerLds {
 // counts per level (and per segment of kOwnSeg nodes and level: the package
 // scan reads only the segments that hold its entries), the FitDelta counts.
 constexpr int kOwnHash = 1024;
+constexpr int kOwnPre = 192;  // a package's entries before pop p-2's candidates (<= 64) leave: >= 128 stay
+constexpr int kOwnSub = 128;  // the package scan's blocks: two per wave step (32 lanes x 4 nodes each)
+static_assert(kOwnSeg % kOwnSub == 0 && kOwnSeg / kOwnSub <= 64, "a segment's blocks fit one wave's lanes");
 struct EngOwnerLds {
-    uint8_t sv[kOwnMaxN];             // node n: level << 1 | pipelined (0: not a candidate of the class)
+    alignas(16) uint8_t sv[kOwnMaxN]; // node n: level << 1 | pipelined (0: not a candidate of the class)
     uint32_t seg[kOwnLv / 2][kOwnSegs];  // nodes per (level, segment): level l in half l & 1 of word [l / 2]
                                          // (a segment holds at most kOwnSeg < 2^16 nodes)
     uint32_t lvl[kOwnLv];             // nodes per level
     uint32_t fit[4];                  // FitDelta counts over every node (fit_bits)
     int32_t hkey[kOwnHash];           // node set (an apply batch's nodes; a package's left-out nodes)
     int32_t hval[kOwnHash];
-    uint32_t keys[kEngPkgN];          // the package's entries (unsorted until the sort)
+    union {
+        uint32_t keys[256];           // a package's entries: the top kOwnPre without pop p-3's candidates
+        int32_t lognode[8][64];       // the next apply batch's candidates as read with `done` (-2: not yet)
+    };
+    int32_t slot_entry[kEngPkgN];     // package slot -> its entry (-1: none)
+    uint32_t wcnt[4];                 // kept entries per wave (the package's compaction)
     uint32_t nkeys;
+    uint32_t smax[kOwnMaxN / kOwnSub];  // per block of kOwnSub nodes: at least its highest level (raised by
+                                        // every re-key, made exact by every package scan that reads the block)
     int32_t act[kOwnSegs];            // the segments the package scan reads ...
-    int32_t take[kOwnSegs];           // ... and how many level-L nodes it takes from each
+    int32_t take[kOwnSegs];           // ... how many level-thr nodes it takes from each ...
+    int32_t hic[kOwnSegs];            // ... and how many nodes above thr each holds
     int32_t nact, thr;                // their number; the threshold level L
     int32_t xfit[4];                  // FitDelta bits of the left-out nodes
     alignas(16) uint32_t desc[kEngDescWords];
@@ -920,16 +932,22 @@ __device__ __forceinline__ bool own_scan_desc(const EngArgs& A, EngOwnerLds& L, 
 // these pops is applied once (every copy was read after the last one's
 // `done`).  A row read while a later pop writes it is torn or newer: that node
 // is a candidate of the later pop, applied again after its `done`, and left
-// out of every package until then.
+// out of every package until then.  The candidates come from
+// L.lognode (read with `done`, the log entries then published) or the log.
+// The FitDelta bits are stored without a wait: every later reader of them runs
+// after a barrier that the storing waves reach drained (own_drain).
 __device__ __forceinline__ bool own_apply(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                           const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, int32_t kbase, uint32_t a0,
                                           int nb) {
-    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     int node = -1;
     bool ok = true;
-    if (wave < nb) ok = own_log_node(ctl, a0 + (uint32_t)wave, &node);
-    if (!ok && (threadIdx.x & 63) == 0) L.ok = 0;
+    if (wave < nb) {
+        node = L.lognode[wave][lane];
+        if (__ballot(node == -2) != 0) ok = own_log_node(ctl, a0 + (uint32_t)wave, &node);
+    }
+    if (!ok && lane == 0) L.ok = 0;
     Row r{};
     uint8_t fl = 0;
     uint32_t ofb = 0;
@@ -955,17 +973,33 @@ __device__ __forceinline__ bool own_apply(const Conf& cf, const NodeCols& nc, co
         st_sc1(&fbh[node], (uint8_t)nfb);
     }
     own_fit_delta(L, win, ofb, nfb);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the bits are stored before a later batch reads them
     __syncthreads();
+    if (win) {  // the exact level bound of the node's block (every byte written above)
+        const uint4* bw = (const uint4*)&L.sv[(node / kOwnSub) * kOwnSub];
+        uint32_t mx = 0;
+#pragma unroll
+        for (int k = 0; k < kOwnSub / 16; ++k) {
+            const uint4 q = bw[k];
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                mx = max(mx, max(max((q.x >> (8 * b + 1)) & 0x7fu, (q.y >> (8 * b + 1)) & 0x7fu),
+                                 max((q.z >> (8 * b + 1)) & 0x7fu, (q.w >> (8 * b + 1)) & 0x7fu)));
+        }
+        L.smax[node / kOwnSub] = mx;
+    }
     if (node >= 0) { L.hkey[hs] = -1; L.hval[hs] = -1; }
     return L.ok != 0;
 }
+// This wave's stores done (the FitDelta bits of an apply) before the next barrier.
+__device__ __forceinline__ void own_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Every wave: pop p's package (its descriptor in L.desc) — the top 128 keys of
 // the class over every node but pops p-3 and p-2's candidates, with their rows
 // (the layout of eng_final) — and, once pop p-1's candidates are logged, pop
 // p's FitDelta counts over every node but the three sets (the placer counts
-// those on their final rows).
+// those on their final rows).  Everything but the last step runs before pop
+// p-2's candidates are known: the top kOwnPre without pop p-3's, sorted; then
+// pop p-2's leave the list (at most 64) and the first 128 left are packaged.
 __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                             const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, uint32_t p) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -973,40 +1007,32 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
     const EngDesc d = eng_decode(L.desc);
     const PopArgs a = eng_args(d);
     ETL(A, p, 10);
-    // 1. pops p-3 (wave 0) and p-2 (wave 1)'s candidates out of the counts and the scan
-    int xn = -1;
+    // 1. pop p-3's candidates (wave 0) out of the counts and the scan
+    int x3 = -1;
     bool ok = true;
-    if (wave < 2) {
-        const uint32_t q = p - 3 + (uint32_t)wave;
-        if ((int32_t)(q - A.first) >= 0) ok = own_log_node(ctl, q, &xn);
+    if (wave == 0) {
+        if ((int32_t)(p - 3 - A.first) >= 0) ok = own_log_node(ctl, p - 3, &x3);
         if (!ok && lane == 0) L.ok = 0;
     }
-    if (wave == 1) ETL(A, p, 11);
     if (threadIdx.x < 4) L.xfit[threadIdx.x] = 0;
-    bool xf = false;
-    int xs = -1;
-    uint32_t xfb = 0;
-    if (xn >= 0) {
-        xs = own_hinsert(L, xn, &xf);
-        xfb = ld_sc1(&fbh[xn]);
+    bool xf3 = false;
+    int xs3 = -1;
+    if (x3 >= 0) xs3 = own_hinsert(L, x3, &xf3);
+    const uint32_t xfb3 = xf3 ? ld_sc1(&fbh[x3]) : 0u;  // (used at the end: in flight meanwhile)
+    __syncthreads();
+    if (wave == 0) ETL(A, p, 21);
+    uint32_t xv3 = 0;
+    if (xf3) {
+        xv3 = L.sv[x3];
+        L.sv[x3] = 0;
+        own_count(L, x3, xv3, ~0u);
     }
     __syncthreads();
-    uint32_t xv = 0;
-    if (xf) {
-        xv = L.sv[xn];
-        L.sv[xn] = 0;
-        own_count(L, xn, xv, ~0u);
-    }
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int k = __popcll(__ballot(xf && ((xfb >> b) & 1u)));
-        if (lane == 0 && k) atomicAdd((uint32_t*)&L.xfit[b], (uint32_t)k);
-    }
-    __syncthreads();
-    // 2. wave 0: the threshold level thr (fewer than 128 nodes above it, at least 128 at or
-    // above; or level 1 when fewer than 128 are left) and the segments holding the entries
+    // 2. wave 0: the threshold level thr (fewer than kOwnPre nodes above it, at least kOwnPre
+    // at or above; or level 1 when fewer are left) and the segments holding the entries
     if (wave == 0) {
         static_assert(kOwnLv == 128, "two levels per lane");
+        const uint32_t K = (uint32_t)kOwnPre;
         const uint32_t c0 = lane ? L.lvl[2 * lane] : 0u, c1 = L.lvl[2 * lane + 1];  // levels 2 lane, 2 lane + 1
         uint32_t s = c0 + c1;  // nodes at levels >= 2 lane
 #pragma unroll
@@ -1015,21 +1041,24 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
             if (lane + dd < 64) s += u;
         }
         const uint32_t s1 = s - c0;  // nodes at levels >= 2 lane + 1
-        const int bl = s1 >= (uint32_t)kEngPkgN ? 2 * lane + 1 : (lane && s >= (uint32_t)kEngPkgN) ? 2 * lane : 0;
+        const int bl = s1 >= K ? 2 * lane + 1 : (lane && s >= K) ? 2 * lane : 0;
         int thr = bl;
 #pragma unroll
         for (int dd = 1; dd < 64; dd <<= 1) thr = max(thr, __shfl_xor(thr, dd, 64));
-        if (thr == 0) thr = 1;  // fewer than 128 nodes: all of them
+        if (thr == 0) thr = 1;  // fewer than K nodes: all of them
         const int tl = thr >> 1;
-        // nodes above thr, at thr
         const uint32_t s_tl = (uint32_t)__shfl((int)s, tl, 64), s1_tl = (uint32_t)__shfl((int)s1, tl, 64);
-        const uint32_t above = (thr & 1) ? s1_tl - (uint32_t)__shfl((int)c1, tl, 64) : s1_tl;
-        const uint32_t at = (thr & 1) ? (uint32_t)__shfl((int)c1, tl, 64) : s_tl - s1_tl;
-        const int need = (int)min((uint32_t)kEngPkgN - min(above, (uint32_t)kEngPkgN), at);
+        const uint32_t c1_tl = (uint32_t)__shfl((int)c1, tl, 64);
+        const uint32_t above = (thr & 1) ? s1_tl - c1_tl : s1_tl;  // nodes above thr
+        const uint32_t at = (thr & 1) ? c1_tl : s_tl - s1_tl;       // nodes at thr
+        const int need = (int)min(K - min(above, K), at);
         const uint64_t nz = __ballot(c0 + c1 != 0);
         const int top = nz ? 2 * (63 - __builtin_clzll(nz)) + 1 : 0;
-        uint32_t hi = 0;  // (lane = segment)
-        for (int lv = thr + 1; lv <= top; ++lv) hi += own_segcnt(L, lv, lane);
+        uint32_t hi = 0;  // (lane = segment) nodes above thr: level pairs, the words' halves
+        for (int lp = (thr + 1) >> 1; lp <= (top >> 1); ++lp) {
+            const uint32_t w = L.seg[lp][lane];
+            hi += (2 * lp > thr ? (w & 0xffffu) : 0u) + (w >> 16);
+        }
         const uint32_t eq = own_segcnt(L, thr, lane);
         uint32_t inc = eq;  // inclusive prefix over segments
 #pragma unroll
@@ -1044,82 +1073,161 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         if (act) {
             L.act[pos] = lane;
             L.take[pos] = tk;
+            L.hic[pos] = (int)hi;
         }
         if (lane == 0) {
             L.nact = __popcll(am);
             L.thr = thr;
             L.nkeys = 0;
         }
+        ETL(A, p, 24);
+        if (A.tl && lane == 0) A.tl[(size_t)(p % kEngTlSlots) * kEngTlEvents + 25] = (uint64_t)__popcll(am) | ((uint64_t)thr << 8);
     }
     __syncthreads();
-    // 3. the entries: wave w scans active segments w, w + 8, ... in index order (every node
-    // above thr, the first take[] nodes at thr)
+    // 3. the entries: wave w scans active segments w, w + 8, ... — only the blocks of
+    // kOwnSub nodes whose level bound reaches thr, two per step in index order, until
+    // the segment's nodes above thr and its first take[] nodes at thr are found
     {
         const int thr = L.thr, nact = L.nact;
+        constexpr int nsub = kOwnSeg / kOwnSub;
+        const int g = lane >> 5, w = lane & 31;  // block g of the step, word w of the block
         for (int i = wave; i < nact; i += kPopThreads / 64) {
-            const int sg = L.act[i], tk = L.take[i];
-            const uint32_t* w32 = (const uint32_t*)&L.sv[sg * kOwnSeg];
-            int run = 0;  // nodes at thr before this step (index order)
-#pragma unroll 2
-            for (int j = 0; j < kOwnSeg / 256; ++j) {
-                const uint32_t wv = w32[j * 64 + lane];
-                const int n0 = sg * kOwnSeg + (j * 64 + lane) * 4;
-                int below = 0, tot = 0;
+            const int sg = L.act[i], tk = L.take[i], hs = L.hic[i];
+            const int sb0 = sg * nsub;
+            uint64_t cm = __ballot(lane < nsub && (int)L.smax[sb0 + min(lane, nsub - 1)] >= thr);
+            int found = 0, run = 0;  // nodes above thr found, nodes at thr seen (index order)
+            while (cm && (found < hs || run < tk)) {
+                const int b0 = __builtin_ctzll(cm);
+                const uint64_t cm1 = cm & (cm - 1);
+                const int b1 = cm1 ? __builtin_ctzll(cm1) : -1;
+                cm = cm1 ? (cm1 & (cm1 - 1)) : 0;
+                const int sb = g == 0 ? b0 : b1;
+                const uint32_t wv = sb >= 0 ? ((const uint32_t*)L.sv)[(sb0 + sb) * (kOwnSub / 4) + w] : 0u;
+                const int n0 = (sb0 + sb) * kOwnSub + 4 * w;
+                int below = 0, tot = 0, nh = 0;
+                uint32_t mx = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     const uint32_t v = (wv >> (8 * b)) & 0xffu;
                     const uint64_t bm = __ballot(v != 0 && (int)(v >> 1) == thr);
                     below += __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
                     tot += __popcll(bm);
+                    nh += __popcll(__ballot((int)(v >> 1) > thr));
+                    mx = max(mx, v >> 1);
                 }
+                // the entries of this step: positions from one LDS add per step
+                bool tb[4];
                 int k_in = 0;
 #pragma unroll
                 for (int b = 0; b < 4; ++b) {
                     const uint32_t v = (wv >> (8 * b)) & 0xffu;
-                    bool take = false;
+                    tb[b] = false;
                     if (v && (int)(v >> 1) > thr) {
-                        take = true;
+                        tb[b] = true;
                     } else if (v && (int)(v >> 1) == thr) {
-                        take = run + below + k_in < tk;
+                        tb[b] = run + below + k_in < tk;
                         ++k_in;
                     }
-                    if (take) {
-                        const uint32_t at = atomicAdd(&L.nkeys, 1u);
-                        if (at < (uint32_t)kEngPkgN) L.keys[at] = own_key(v, n0 + b + nc.base, A);
-                    }
                 }
+                uint64_t tm[4];
+                int ntot = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    tm[b] = __ballot(tb[b]);
+                    ntot += __popcll(tm[b]);
+                }
+                uint32_t base = 0;
+                if (ntot) {
+                    if (lane == 0) base = atomicAdd(&L.nkeys, (uint32_t)ntot);
+                    base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+                }
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const uint32_t at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(tm[b] >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)tm[b], 0));
+                    if (tb[b] && at < (uint32_t)kOwnPre)
+                        L.keys[at] = own_key((wv >> (8 * b)) & 0xffu, n0 + b + nc.base, A);
+                    base += (uint32_t)__popcll(tm[b]);
+                }
+                // the blocks read are exact now (the left-out nodes are raised back below)
+#pragma unroll
+                for (int dd = 1; dd < 32; dd <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, dd, 64));
+                if (w == 0 && sb >= 0) L.smax[sb0 + sb] = mx;
                 run += tot;
+                found += nh;
             }
         }
     }
     __syncthreads();
-    // 4. the left-out nodes back; wave 0 sorts the entries (two sorted 64-lists, merged)
-    if (xf) {
-        L.sv[xn] = (uint8_t)xv;
-        own_count(L, xn, xv, 1u);
+    if (wave == 0) ETL(A, p, 26);
+    // 4. pop p-3's nodes back; wave 0 sorts the entries (four sorted 64-lists, merged)
+    if (xf3) {
+        L.sv[x3] = (uint8_t)xv3;
+        own_count(L, x3, xv3, 1u);
+        if (xv3) atomicMax(&L.smax[x3 / kOwnSub], xv3 >> 1);
     }
     if (wave == 0) {
-        const uint32_t nk = L.nkeys;
-        uint32_t a0 = (uint32_t)lane < nk ? L.keys[lane] : 0u, a1 = (uint32_t)(64 + lane) < nk ? L.keys[64 + lane] : 0u;
-        a0 = wave_sort_desc(a0);
-        a1 = wave_sort_desc(a1);
-        const uint32_t r = reverse_lanes(a1);
-        const uint32_t hi = a0 > r ? a0 : r, lo = a0 > r ? r : a0;
-        a0 = bitonic_clean_desc(hi);
-        a1 = bitonic_clean_desc(lo);
+        static_assert(kOwnPre <= 256, "four registers");
+        const uint32_t nk = min(L.nkeys, (uint32_t)kOwnPre);
+        uint32_t r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = (uint32_t)(64 * k + lane) < nk ? L.keys[64 * k + lane] : 0u;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = wave_sort_desc(r[k]);
+        uint32_t m[4], n[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // (r0, r1) and (r2, r3) into sorted 128-lists
+            const uint32_t rv = reverse_lanes(r[2 * h + 1]);
+            const uint32_t hi = r[2 * h] > rv ? r[2 * h] : rv, lo = r[2 * h] > rv ? rv : r[2 * h];
+            (h ? n : m)[0] = bitonic_clean_desc(hi);
+            (h ? n : m)[1] = bitonic_clean_desc(lo);
+        }
+        m[2] = m[3] = n[2] = n[3] = 0u;
+        wave_merge256_desc(m, n);  // all of the two 128-lists, sorted
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        L.keys[lane] = a0;
-        L.keys[64 + lane] = a1;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) L.keys[64 * k + lane] = m[k];
         ETL(A, p, 12);
     }
+    // 5. pop p-2's candidates (wave 1): out of the sorted entries; the first 128 left are the package
+    int x2 = -1;
+    if (wave == 1) {
+        if ((int32_t)(p - 2 - A.first) >= 0) ok = own_log_node(ctl, p - 2, &x2);
+        if (!ok && lane == 0) L.ok = 0;
+        ETL(A, p, 11);
+    }
+    bool xf2 = false;
+    int xs2 = -1;
+    if (x2 >= 0) xs2 = own_hinsert(L, x2, &xf2);  // (a node of both pops: counted once, with pop p-3's)
+    const uint32_t xfb2 = xf2 ? ld_sc1(&fbh[x2]) : 0u;
     __syncthreads();
-    // 5. the package (waves 0, 1: entry 64 * wave + lane; eng_final's layout)
+    bool keep = false;
+    uint64_t km = 0;
+    if (wave < 3) {
+        const uint32_t k = L.keys[64 * wave + lane];
+        keep = k && own_hfind(L, key_node(k, a) - nc.base) < 0;  // (pop p-3's nodes are not entries)
+        km = __ballot(keep);
+        if (lane == 0) L.wcnt[wave] = (uint32_t)__popcll(km);
+    }
+    __syncthreads();
+    if (wave < 3) {
+        uint32_t base = 0;
+        for (int w = 0; w < wave; ++w) base += L.wcnt[w];
+        const uint32_t tot = L.wcnt[0] + L.wcnt[1] + L.wcnt[2];
+        const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0));
+        if (keep && pos < (uint32_t)kEngPkgN) L.slot_entry[pos] = 64 * wave + lane;
+        if (wave < 2 && (uint32_t)(64 * wave + lane) >= tot) L.slot_entry[64 * wave + lane] = -1;
+    }
+    __syncthreads();
+    // 6. the package (waves 0, 1: slot 64 * wave + lane; eng_final's layout); then their
+    // left-out nodes' FitDelta bits
     EngPkg* pk = A.pkg + (p % kEngSlots);
     const uint64_t tag = (uint64_t)p << 32;
     if (wave < 2) {
         const int e = 64 * wave + lane;
-        const uint32_t k = L.keys[e];
+        const int src = L.slot_entry[e];
+        const uint32_t k = src >= 0 ? L.keys[src] : 0u;
         const int n = k ? key_node(k, a) - nc.base : -1;
         uint32_t v[kEngPkgFields];
 #pragma unroll
@@ -1140,8 +1248,16 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
 #pragma unroll
         for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
         if (wave == 0) ETL(A, p, 13);
+        const uint32_t xfb = wave == 0 ? xfb3 : xfb2;
+        const bool xf = wave == 0 ? xf3 : xf2;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int kx = __popcll(__ballot(xf && ((xfb >> b) & 1u)));
+            if (lane == 0 && kx) atomicAdd((uint32_t*)&L.xfit[b], (uint32_t)kx);
+        }
     }
-    // 6. wave 2: pop p's FitDelta counts once pop p-1's candidates are logged
+    __syncthreads();
+    // 7. wave 2: pop p's FitDelta counts once pop p-1's candidates are logged
     if (wave == 2 && L.ok) {
         int n1 = -1;
         if ((int32_t)(p - 1 - A.first) >= 0) ok = own_log_node(ctl, p - 1, &n1);
@@ -1158,7 +1274,8 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         ETL(A, p, 18);
     }
     __syncthreads();
-    if (xn >= 0) { L.hkey[xs] = -1; L.hval[xs] = -1; }
+    if (xs3 >= 0) { L.hkey[xs3] = -1; L.hval[xs3] = -1; }
+    if (xs2 >= 0) { L.hkey[xs2] = -1; L.hval[xs2] = -1; }
     return L.ok != 0;
 }
 
@@ -1175,6 +1292,7 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
     // again when those pops are applied)
     for (int i = threadIdx.x; i < kOwnLv / 2 * kOwnSegs; i += kPopThreads) (&L.seg[0][0])[i] = 0;
     for (int i = threadIdx.x; i < kOwnHash; i += kPopThreads) { L.hkey[i] = -1; L.hval[i] = -1; }
+    for (int i = threadIdx.x; i < kOwnMaxN / kOwnSub; i += kPopThreads) L.smax[i] = 0;
     for (int i = threadIdx.x; i < kOwnLv; i += kPopThreads) L.lvl[i] = 0;
     if (threadIdx.x < 4) L.fit[threadIdx.x] = 0;
     if (threadIdx.x == 0) L.ok = 1;
@@ -1193,6 +1311,12 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
             const int n = n0 + u * kPopThreads + (int)threadIdx.x;
             v[u] = own_val(k[u], kbase);
             if (n < nend) L.sv[n] = (uint8_t)v[u];
+            {  // the block's level bound (a wave's 64 nodes lie in one block)
+                uint32_t mx = v[u] >> 1;
+#pragma unroll
+                for (int dd = 1; dd < 64; dd <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, dd, 64));
+                if (lane == 0 && n < nend) atomicMax(&L.smax[n / kOwnSub], mx);
+            }
             if (n < N) fbh[n] = (uint8_t)fb[u];
             fit_block_add(L.fit, fb[u]);
             // level counts, aggregated per wave (a wave's 64 nodes share a segment)
@@ -1218,11 +1342,20 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
     for (;;) {
         if (wave == 0) {
             bool ok = own_scan_desc(A, L, cls, dp);
-            if (lane == 0) {
-                L.dn = ld_sc1(&ctl->done);
-                if (!ok) L.ok = 0;
+            if (!ok && lane == 0) L.ok = 0;
+        } else if (wave == 1) {  // `done`, then the log entries of the next pops (-2: not published yet)
+            const uint32_t dn = ld_sc1(&ctl->done);
+            uint64_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = ld_sc1(&ctl->tlog[(ap + 1 + k) % kEngLog][lane]);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool got = __ballot((uint32_t)(x[k] >> 32) != ap + 1 + k) == 0;
+                L.lognode[k][lane] = got ? (int)(uint32_t)x[k] : -2;
             }
+            if (lane == 0) L.dn = dn;
         }
+        own_drain();  // (an apply's FitDelta bits, before the barrier)
         __syncthreads();
         if (!L.ok) return;
         const int next = L.next;
@@ -1249,6 +1382,7 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
             continue;
         }
         if (next >= 0 && (int32_t)(ap - ((uint32_t)next - 4)) >= 0) {
+            own_drain();
             if (!own_package(cf, nc, t, c, A, L, fbh, (uint32_t)next)) return;
             dp = (uint32_t)next + 1;
             t0 = 0;
@@ -1440,7 +1574,8 @@ __device__ __forceinline__ void eng_drop_stale(EngPlacerLds& L, const PopArgs& a
 // ...): pop q-1's placement still reads the row cache's na / s1 of the older
 // slots; pop q's P2 moves the ones that count there.
 __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& nc, const DevTables& t,
-                                               EngPlacerLds& L, uint32_t q, uint32_t dw, int set, int role) {
+                                               const EngArgs& A, EngPlacerLds& L, uint32_t q, uint32_t dw, int set,
+                                               int role) {
     const int lane = eng_lane();
     uint32_t w[8];
 #pragma unroll
@@ -1454,6 +1589,7 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
             if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
             __builtin_amdgcn_s_sleep(1);
         }
+    if (role == 0) ETL(A, q - 1, 32 + 4 * set);  // timeline (pop q-1's slot): set s's key at events 32 + 4 s ..
     const int node = L.xn[ring][lane];
     const int sl = 64 * ring + lane;
     const uint64_t pw[4] = {0, 0, 0, 0};
@@ -1471,6 +1607,7 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
             fb = fit_bits(c, r, passed);
             kind = k0 ? key_kind(k0) : 0;
         }
+        ETL(A, q - 1, 33 + 4 * set);
         L.fe[set][lane] = e;
         L.ffb[set][lane] = (uint8_t)fb;
         L.fkind[set][lane] = (uint8_t)kind;
@@ -1488,12 +1625,14 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
             hashed = __hip_atomic_load(&L.hash_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q;
             if (!hashed) __builtin_amdgcn_s_sleep(1);
         }
+        ETL(A, q - 1, 34 + 4 * set);
         if (hashed) {
             const bool use = node >= 0 && (set == 0 || (set == 1 ? L.x2use[lane] : L.x3use[lane]));
             L.e[set][lane] = wave_sort_desc(use ? e : 0u);
             L.fbp[set][lane] = use ? (uint8_t)fb : (uint8_t)0;
             __builtin_amdgcn_s_waitcnt(0xc07f);
             if (lane == 0) __hip_atomic_store(&L.sort_seq[set], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            ETL(A, q - 1, 35 + 4 * set);
         }
     } else if (node >= 0) {  // the depth-1 score after an Allocate
         const Row r = L.rc.row[sl];
@@ -1550,6 +1689,11 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
     if (((uint32_t)__builtin_amdgcn_readlane((int)dw, kDwFlags) >> 12 & 0xf) != kEngOpPop) return;
     if (wave == 2) {
         const int r1 = (int)((q + 3) % 4), r2 = (int)((q + 2) % 4), r3 = (int)((q + 1) % 4);
+        // pop q-1's candidates (its P3); the hash is rebuilt only after that P3's look-ups
+        while (__hip_atomic_load(&L.xn_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)(q - 1)) {
+            if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+            __builtin_amdgcn_s_sleep(1);
+        }
         for (int h = lane; h < EngRowCache::kHashN; h += 64) rc.hkey[h] = -1;
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
@@ -1569,16 +1713,16 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the hash is in LDS before the flag
         if (lane == 0) __hip_atomic_store(&L.hash_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        eng_front_eval(cf, nc, t, L, q, dw, 0, 1);
+        eng_front_eval(cf, nc, t, A, L, q, dw, 0, 1);
         return;
     }
     // one evaluation per wave (set, role: 0 the key, 1 the depth-1 score after an Allocate);
     // waves w and w + 4 share a SIMD's issue slots; set 0 waits for pop q-1's rows
-    if (wave == 1) { eng_front_eval(cf, nc, t, L, q, dw, 0, 0); return; }
-    if (wave == 5) { eng_front_eval(cf, nc, t, L, q, dw, 1, 1); return; }
-    if (wave == 3) eng_front_eval(cf, nc, t, L, q, dw, 2, 1);
-    else if (wave == 6) eng_front_eval(cf, nc, t, L, q, dw, 1, 0);
-    else if (wave == 7) eng_front_eval(cf, nc, t, L, q, dw, 2, 0);  // (wave 4: wave 0's SIMD, loads only)
+    if (wave == 1) { eng_front_eval(cf, nc, t, A, L, q, dw, 0, 0); return; }
+    if (wave == 5) { eng_front_eval(cf, nc, t, A, L, q, dw, 1, 1); return; }
+    if (wave == 3) eng_front_eval(cf, nc, t, A, L, q, dw, 2, 1);
+    else if (wave == 6) eng_front_eval(cf, nc, t, A, L, q, dw, 1, 0);
+    else if (wave == 7) eng_front_eval(cf, nc, t, A, L, q, dw, 2, 0);  // (wave 4: wave 0's SIMD, loads only)
     // two generations of the package's loads in flight, checked in turn (the package is
     // read whole each time: four waves of one block, a few tens of GB/s), so that it is
     // in registers about a round trip after it lands
@@ -1665,6 +1809,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
     if (threadIdx.x == 0) {
         L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1;
         L.hash_seq = L.drop_seq = (int)A.first - 1;
+        L.xn_seq = (int)A.first - 1;
         L.sort_seq[0] = L.sort_seq[1] = L.sort_seq[2] = (int)A.first - 1;
         L.apmin = A.first - 1;
     }
@@ -1763,10 +1908,13 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             L.srcslot[lane] = src;
             L.xn[r0][lane] = n;
             L.wl64[0][lane] = key64_of(top, a);
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the candidates are in LDS before the flag
+            if (lane == 0) __hip_atomic_store(&L.xn_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             ETL(A, p, 4);
+            ETL(A, p, 5);
         }
-        __syncthreads();
-        if (wave == 0) ETL(A, p, 5);
+        // (no barrier: the other waves start pop p+1's front during P3 and take pop p's
+        // candidates once L.xn_seq reads p)
         // P4 (engine pops' classes have 32-bit entries, PopArgs::ent32: the host
         // sends the others to the launched kernels).  Wave 0 decides alone
         // (place_decide_wave) and writes the results and rows, while wave 5
@@ -1820,7 +1968,7 @@ __device__ __forceinline__ void eng_dispatch(const EngArgs& A) {
                 const uint64_t now = eng_now();
                 if (!t0) t0 = now;
                 if (ld_sc1(&ctl->err) != 0) break;
-                if (now - t0 > kEngIdleTicks) { idle = true; break; }
+                if (now - t0 > (uint64_t)A.idle_ticks) { idle = true; break; }
             }
             __builtin_amdgcn_s_sleep(2);
         }
@@ -1840,9 +1988,52 @@ __device__ __forceinline__ void eng_dispatch(const EngArgs& A) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Every block at its start: wait until every block of the grid has started (its
+// blocks spin on each other, so all of them must be resident at once).  One
+// counter decides for all: a block that waited kEngArriveTicks closes it
+// (bit 31) unless it has reached the grid size, and a closed counter never
+// does — so either every block runs or none serves a pop (kEngErrResident; the
+// dispatcher reports it, eng_not_resident).
+__device__ __forceinline__ bool eng_arrive(const EngArgs& A, int* flag) {
+    EngCtl* ctl = A.ctl;
+    if (threadIdx.x == 0) {
+        constexpr uint32_t kClosed = 0x80000000u;
+        const uint32_t old = __hip_atomic_fetch_add(&ctl->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = !(old & kClosed);
+        const uint64_t t0 = eng_now();
+        while (ok) {
+            uint32_t v = ld_sc1(&ctl->arrive);
+            if (v & kClosed) { ok = false; break; }
+            if (v == gridDim.x) break;
+            if (eng_now() - t0 > kEngArriveTicks &&
+                __hip_atomic_compare_exchange_strong(&ctl->arrive, &v, v | kClosed, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                __hip_atomic_store(&ctl->err, (uint32_t)kEngErrResident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+        *flag = ok;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
+// The dispatcher of a grid that did not become resident: the exit word (nothing served).
+__device__ __forceinline__ void eng_not_resident(const EngArgs& A) {
+    if (threadIdx.x == 0)
+        __hip_atomic_store(A.hexit, (uint64_t)A.first | (1ull << 41) | (1ull << 42), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kPopThreads) void k_engine(Conf cf, NodeCols nc, DevTables t, EngArgs A) {
     __shared__ EngLds lds;
+    __shared__ int arrived;
     const int b = blockIdx.x;
+    if (!eng_arrive(A, &arrived)) {
+        if (b == A.nw + A.ng + 2) eng_not_resident(A);
+        return;
+    }
     if (b < A.nw) {
         eng_worker(cf, nc, t, A, lds.w, b);
     } else if (b < A.nw + A.ng) {
@@ -1861,7 +2052,12 @@ __global__ __launch_bounds__(kPopThreads) void k_engine(Conf cf, NodeCols nc, De
 // engine's placer.
 __global__ __launch_bounds__(kPopThreads) void k_engine_lists(Conf cf, NodeCols nc, DevTables t, EngArgs A) {
     __shared__ EngLdsList lds;
+    __shared__ int arrived;
     const int b = blockIdx.x;
+    if (!eng_arrive(A, &arrived)) {
+        if (b == A.nown + 1) eng_not_resident(A);
+        return;
+    }
     if (b < A.nown) eng_owner(cf, nc, t, A, lds.o, b);
     else if (b == A.nown) eng_placer<true>(cf, nc, t, A, lds.p);
     else if (threadIdx.x < 64) eng_dispatch(A);

@@ -62,7 +62,8 @@ class Stats(ctypes.Structure):
                 ("evict_visits", ctypes.c_int64), ("evict_cands", ctypes.c_int64), ("fit_syncs", ctypes.c_int64),
                 ("alloc_setup_s", ctypes.c_double), ("evict_setup_s", ctypes.c_double),
                 ("engine_pops", ctypes.c_int64), ("engine_launches", ctypes.c_int64),
-                ("engine_workers", ctypes.c_int64), ("engine_owners", ctypes.c_int64)]
+                ("engine_workers", ctypes.c_int64), ("engine_owners", ctypes.c_int64),
+                ("engine_not_resident", ctypes.c_int64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 import kbgen  # noqa: E402
 import kbhip  # noqa: E402
 
-SLOTS, EV = 32768, 32
+SLOTS, EV = 32768, 48
 
 
 def main():
@@ -64,22 +64,43 @@ def main():
     per["placer 6->7 rows written"] = us(t[:, 7] - t[:, 6])
     per["placer 7 -> next 0"] = us((t[1:, 0] - t[:-1, 7])[cont])
     per["placer 5->15 next package in LDS"] = us(t[:, 15] - t[:, 5])
+    for ev, name in ((19, "wave 1 (pop p-1 cands key)"), (29, "wave 5 (host out + eval)"), (16, "wave 7 (eval + package)"),
+                     (17, "wave 6 (eval + package)"), (14, "wave 4 (eval + package)"), (23, "wave 2 (hash)")):
+        ok = t[:, ev] > 0
+        if ok.any():
+            per[f"placer 5->{ev} front {name}"] = us((t[:, ev] - t[:, 5])[ok])
+    per["P2 wave0 drop (0->1)"] = us(t[:, 1] - t[:, 0])
+    for st_, nm in ((0, "set 0 (pop p cands)"), (1, "set 1"), (2, "set 2")):
+        b = 32 + 4 * st_
+        ok = np.all(t[:, [b, b + 1, b + 2, b + 3]] > 0, axis=1)
+        if ok.any():
+            per[f"front {nm}: start(5)->rows ready"] = us((t[:, b] - t[:, 5])[ok])
+            per[f"front {nm}: eval"] = us((t[:, b + 1] - t[:, b])[ok])
+            per[f"front {nm}: ->hashed"] = us((t[:, b + 2] - t[:, b + 1])[ok])
+            per[f"front {nm}: sort"] = us((t[:, b + 3] - t[:, b + 2])[ok])
+            per[f"front {nm}: end - 5"] = us((t[:, b + 3] - t[:, 5])[ok])
     per["owner seen(20) - placer start(0)"] = us(t[:, 20] - t[:, 0])
     per["owner seen(20) -> start(10)"] = us(t[:, 10] - t[:, 20])
     per["owner start(10) - placer start(0)"] = us(t[:, 10] - t[:, 0])
-    per["owner start(10) -> p-2 cands(11)"] = us(t[:, 11] - t[:, 10])
-    per["owner p-2 cands(11) -> sorted(12)"] = us(t[:, 12] - t[:, 11])
-    per["owner sorted(12) -> stored(13)"] = us(t[:, 13] - t[:, 12])
-    per["owner stored(13) - placer start(0)"] = us(t[:, 13] - t[:, 0])
-    per["owner p-2 cands seen(11,p) - placer P3(4,p-2)"] = us((t[2:, 11] - t[:-2, 4])[prev(2)])
     per["owner start(10,p) - placer P3(4,p-3) (done p-4)"] = us((t[3:, 10] - t[:-3, 4])[prev(3)])
+    per["owner 10 -> 21 (p-3 cands, hash)"] = us(t[:, 21] - t[:, 10])
+    per["owner 21 -> 24 (threshold, wave 0)"] = us(t[:, 24] - t[:, 21])
+    per["owner 24 -> 26 (scan)"] = us(t[:, 26] - t[:, 24])
+    per["owner 26 -> 12 (sort)"] = us(t[:, 12] - t[:, 26])
+    per["owner sorted(12) - placer P3(4,p-2)"] = us((t[2:, 12] - t[:-2, 4])[prev(2)])
+    per["owner p-2 cands seen(11,p) - placer P3(4,p-2)"] = us((t[2:, 11] - t[:-2, 4])[prev(2)])
+    per["owner p-2 seen(11) -> stored(13)"] = us(t[:, 13] - t[:, 11])
+    per["owner stored(13) - placer start(0)"] = us(t[:, 13] - t[:, 0])
+    res_extra = {"active_segments_quantiles": [float(np.quantile(t[:, 25] & 0xff, q)) for q in (0.1, 0.5, 0.9)],
+                 "thr_quantiles": [float(np.quantile(t[:, 25] >> 8, q)) for q in (0.1, 0.5, 0.9)]}
+    per["owner stored(13,p) - placer 5(p-1) front start"] = us((t[1:, 13] - t[:-1, 5])[cont])
     per["owner stored(13,p) - placer 15(p-1) package in LDS"] = us((t[1:, 13] - t[:-1, 15])[cont])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     per_all = np.diff(t[:, 0])[cont] / 100.0
     res = {"pops": int(len(t)), "lists": a.lists,
            "stats": {k: st[k] for k in ("engine_pops", "engine_launches", "engine_workers", "engine_owners",
                                         "alloc_device_s", "batched_pops", "host_wait_s")},
-           "median_us": per,
+           "median_us": per, "extra": res_extra,
            "period_us": {"mean": round(float(per_all.mean()), 3),
                          "quantiles_10_50_90_99": [round(float(np.quantile(per_all, q)), 2) for q in (0.1, 0.5, 0.9, 0.99)]}}
     print(json.dumps(res))

@@ -169,3 +169,74 @@ def test_engine_idle_restart(engine, oracle_mod, kbgen_mod, tmp_path):
         st = s.stats()
     assert got == exp
     assert st["engine_launches"] >= 2
+
+
+def test_engine_two_sessions_threads(engine, oracle_mod, kbgen_mod, tmp_path):
+    """Two engine-eligible sessions allocating at once from two threads of one
+    process: one device, one engine at a time (the in-process claim,
+    eng_claim); the other session's pops take the launched path meanwhile.
+    Both logs equal the hoisted restatement's, no KBHIP_EDEVICE, bounded
+    time."""
+    import threading
+    paths, exps = [], []
+    for i in range(2):
+        p = str(tmp_path / f"c2t{i}.kbs")
+        kbgen_mod.gen_c2(p, n_nodes=3000, n_pending=20000, seed=9600 + i)
+        paths.append(p)
+        exps.append(oracle_mod.fast_allocate(p, threads=8).as_list())
+    out = [None, None]
+    errs = []
+
+    def run(i):
+        try:
+            for _ in range(3):  # several sessions each, so that the two overlap
+                out[i] = _run(engine, paths[i])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(repr(e))
+    t0 = time.time()
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th)
+    assert not errs, errs
+    assert time.time() - t0 < 120
+    for i in range(2):
+        assert out[i][0] == exps[i]
+    assert out[0][2]["engine_pops"] + out[1][2]["engine_pops"] > 0
+
+
+def _proc_allocate(path, q):
+    import kbhip
+    with kbhip.Session(path) as s:
+        pod, node, kind = s.allocate()
+        st = s.stats()
+    q.put(([(int(p), int(n), 4 if k == 1 else 8) for p, n, k in zip(pod, node, kind)],
+           int(st["engine_pops"]), int(st["engine_not_resident"])))
+
+
+def test_engine_two_processes(engine, oracle_mod, kbgen_mod, tmp_path):
+    """Two processes on one GPU, each with an engine-eligible session: a grid
+    that cannot become resident while the other holds the CUs ends serving
+    nothing and is started again (eng_arrive, kEngErrResident) — both logs
+    equal the restatement's."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    paths, exps = [], []
+    for i in range(2):
+        p = str(tmp_path / f"c2p{i}.kbs")
+        kbgen_mod.gen_c2(p, n_nodes=3000, n_pending=20000, seed=9700 + i)
+        paths.append(p)
+        exps.append(oracle_mod.fast_allocate(p, threads=8).as_list())
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_proc_allocate, args=(paths[i], q)) for i in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in ps:
+        p.join(30)
+        assert p.exitcode == 0
+    logs = sorted(r[0] for r in res)
+    assert logs == sorted(exps)
+    assert all(r[1] > 0 for r in res)
