@@ -76,6 +76,8 @@ def parse():
                     help="1: batched pops go to the persistent pop engine (one resident kernel, DESIGN.md §4.10); "
                          "0 = one launched kernel per pop")
     ap.add_argument("--engine-workers", type=int, default=0, help="engine worker blocks (0: as many as stay resident)")
+    ap.add_argument("--engine-lists", type=int, default=1, choices=(0, 1),
+                    help="1 = the engine's list mode when every class fits (class owners, DESIGN.md §4.11), 0 = sweep mode")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
                     help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
                          "each shard sweeps its node range to its top-64, one RCCL all-gather, identical placement "
@@ -217,7 +219,7 @@ def open_sharded(buf, device, rank, world, dist):
 
 
 def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, keep_log=False, engine=1,
-                engine_workers=0):
+                engine_workers=0, engine_lists=1):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
@@ -225,6 +227,7 @@ def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, kee
     s.set_option("speculate", speculate)
     s.set_option("engine", engine)
     s.set_option("engine_workers", engine_workers)
+    s.set_option("engine_lists", engine_lists)
     t1 = time.perf_counter()
     pod, node, kind = s.allocate(cap=1 << 21)
     t2 = time.perf_counter()
@@ -316,7 +319,7 @@ def main():
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
         run_session(buf, device, 0, shard, args.overlap, args.speculate, engine=args.engine,
-                    engine_workers=args.engine_workers)
+                    engine_workers=args.engine_workers, engine_lists=args.engine_lists)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
@@ -324,7 +327,7 @@ def main():
     for i in range(args.steps):
         dt, n, st = run_session(buf, device, args.time_every, shard, args.overlap,
                                 args.speculate, keep_log=(i == 0 and rank == 0), engine=args.engine,
-                                engine_workers=args.engine_workers)
+                                engine_workers=args.engine_workers, engine_lists=args.engine_lists)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
@@ -379,6 +382,7 @@ def main():
                    "overlap": args.overlap, "speculate": args.speculate, "alloc_device_s": st_last["alloc_device_s"],
                    "engine_pops": st_last["engine_pops"], "engine_launches": st_last["engine_launches"],
                    "engine_workers": st_last["engine_workers"],
+                   "engine_owners": st_last["engine_owners"],
                    "host_launch_s": st_last["host_launch_s"], "host_wait_s": st_last["host_wait_s"],
                    "spec_hits": st_last["spec_hits"], "spec_missed": st_last["spec_missed"],
                    "unassigned_pops": st_last["unassigned_pops"], "collectives": st_last["collectives"],

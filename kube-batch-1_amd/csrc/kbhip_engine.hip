@@ -324,6 +324,16 @@ struct EngPlacerLds {
     int32_t fna[3][64], fs1a[3][64], fs1p[3][64];
     int rows_seq;                // the last pop whose candidates' rows are in their ring (eng_finish)
     int xn_seq;                  // the last pop whose candidates are in their ring of L.xn (P3)
+    // set 0 of the next pop evaluated ahead of the decision: on each candidate's row before this
+    // pop (variant 0, in fe / ...) and after one Allocate of this pop's class (variant 1, below);
+    // the decision's commits per candidate (ccm: Allocates | Pipelines << 8) select one
+    int32_t ccm[64];
+    uint32_t v1e[64];
+    uint8_t v1fb[64], v1kind[64];
+    int32_t v1s1p[64], v1s1a[64];
+    int v1_seq[2];               // the pop whose variant-1 keys (0) / depth-1 scores (1) are in v1*
+    uint32_t pre64[64];          // the next pop's package list merged with its sets 1 and 2 (P3 adds set 0)
+    int pre_seq;
     uint8_t x2use[64], x3use[64];  // pop p-2's candidate not p-1's; pop p-3's neither
     int32_t srcslot[64];         // the final list's candidate j: its row's slot (a ring or a package entry)
     int32_t fitin[4];
@@ -938,13 +948,13 @@ __device__ __forceinline__ bool own_scan_desc(const EngArgs& A, EngOwnerLds& L, 
 // after a barrier that the storing waves reach drained (own_drain).
 __device__ __forceinline__ bool own_apply(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                                           const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, int32_t kbase, uint32_t a0,
-                                          int nb) {
+                                          int nb, bool prefetched = true) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     int node = -1;
     bool ok = true;
     if (wave < nb) {
-        node = L.lognode[wave][lane];
+        node = prefetched ? L.lognode[wave][lane] : -2;
         if (__ballot(node == -2) != 0) ok = own_log_node(ctl, a0 + (uint32_t)wave, &node);
     }
     if (!ok && lane == 0) L.ok = 0;
@@ -1001,7 +1011,8 @@ __device__ __forceinline__ void own_drain() { asm volatile("s_waitcnt vmcnt(0)" 
 // p-2's candidates are known: the top kOwnPre without pop p-3's, sorted; then
 // pop p-2's leave the list (at most 64) and the first 128 left are packaged.
 __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
-                                            const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, uint32_t p) {
+                                            const EngArgs& A, EngOwnerLds& L, uint8_t* fbh, int32_t kbase, uint32_t p,
+                                            uint32_t* ap) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     EngCtl* ctl = A.ctl;
     const EngDesc d = eng_decode(L.desc);
@@ -1018,7 +1029,6 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
     bool xf3 = false;
     int xs3 = -1;
     if (x3 >= 0) xs3 = own_hinsert(L, x3, &xf3);
-    const uint32_t xfb3 = xf3 ? ld_sc1(&fbh[x3]) : 0u;  // (used at the end: in flight meanwhile)
     __syncthreads();
     if (wave == 0) ETL(A, p, 21);
     uint32_t xv3 = 0;
@@ -1166,31 +1176,60 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         own_count(L, x3, xv3, 1u);
         if (xv3) atomicMax(&L.smax[x3 / kOwnSub], xv3 >> 1);
     }
+    uint32_t m[4];  // (wave 0) the sorted entries, ranks 64 k .. 64 k + 63 in m[k]
     if (wave == 0) {
-        static_assert(kOwnPre <= 256, "four registers");
+        static_assert(kOwnPre <= 192, "three registers and pop p-3's candidates");
         const uint32_t nk = min(L.nkeys, (uint32_t)kOwnPre);
         uint32_t r[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) r[k] = (uint32_t)(64 * k + lane) < nk ? L.keys[64 * k + lane] : 0u;
 #pragma unroll
         for (int k = 0; k < 4; ++k) r[k] = wave_sort_desc(r[k]);
-        uint32_t m[4], n[4];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {  // (r0, r1) and (r2, r3) into sorted 128-lists
-            const uint32_t rv = reverse_lanes(r[2 * h + 1]);
-            const uint32_t hi = r[2 * h] > rv ? r[2 * h] : rv, lo = r[2 * h] > rv ? rv : r[2 * h];
-            (h ? n : m)[0] = bitonic_clean_desc(hi);
-            (h ? n : m)[1] = bitonic_clean_desc(lo);
+        uint32_t n[4];  // (r0, r1) and (r2, r3) into sorted 128-lists
+        {
+            const uint32_t rv = reverse_lanes(r[1]);
+            m[0] = bitonic_clean_desc(r[0] > rv ? r[0] : rv);
+            m[1] = bitonic_clean_desc(r[0] > rv ? rv : r[0]);
+        }
+        {
+            const uint32_t rv = reverse_lanes(r[3]);
+            n[0] = bitonic_clean_desc(r[2] > rv ? r[2] : rv);
+            n[1] = bitonic_clean_desc(r[2] > rv ? rv : r[2]);
         }
         m[2] = m[3] = n[2] = n[3] = 0u;
-        wave_merge256_desc(m, n);  // all of the two 128-lists, sorted
+        wave_merge256_desc(m, n);  // all of the two 128-lists, sorted (at most 192)
+        ETL(A, p, 12);
+    }
+    __syncthreads();
+    if (xs3 >= 0) { L.hkey[xs3] = -1; L.hval[xs3] = -1; }
+    // 5. pop p-3's rows, once it is done: its candidates re-keyed (the apply), then merged
+    // into the entries with their new keys — the package covers them, the placer re-evaluates
+    // only pops p-2 and p-1's candidates (list mode)
+    if ((int32_t)(p - 3 - A.first) >= 0 && (int32_t)(*ap - (p - 3)) < 0) {
+        if (wave == 0) {
+            EngWait wt(ctl, kEngWaitTicks);
+            while ((int32_t)((uint32_t)__builtin_amdgcn_readfirstlane((int)ld_sc1(&ctl->done)) - (p - 3)) < 0)
+                if (!wt.tick()) { if (lane == 0) L.ok = 0; break; }
+        }
+        __syncthreads();
+        if (!L.ok) return false;
+        if (!own_apply(cf, nc, t, c, A, L, fbh, kbase, p - 3, 1, false)) return false;
+        *ap = p - 3;
+        own_drain();  // (its FitDelta bits, read below)
+        if (threadIdx.x == 0) st_sc1(&ctl->own_ap[blockIdx.x], *ap);
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t v = x3 >= 0 ? (uint32_t)L.sv[x3] : 0u;
+        const uint32_t k3 = wave_sort_desc(v ? own_key(v, x3 + nc.base, A) : 0u);
+        const uint32_t b[4] = {k3, 0u, 0u, 0u};
+        wave_merge256_desc(m, b);  // the entries and pop p-3's candidates, sorted (at most 256)
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int k = 0; k < 3; ++k) L.keys[64 * k + lane] = m[k];
-        ETL(A, p, 12);
+        for (int k = 0; k < 4; ++k) L.keys[64 * k + lane] = m[k];
     }
-    // 5. pop p-2's candidates (wave 1): out of the sorted entries; the first 128 left are the package
+    // 6. pop p-2's candidates (wave 1): out of the sorted entries; the first 128 left are the package
     int x2 = -1;
     if (wave == 1) {
         if ((int32_t)(p - 2 - A.first) >= 0) ok = own_log_node(ctl, p - 2, &x2);
@@ -1199,22 +1238,22 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
     }
     bool xf2 = false;
     int xs2 = -1;
-    if (x2 >= 0) xs2 = own_hinsert(L, x2, &xf2);  // (a node of both pops: counted once, with pop p-3's)
+    if (x2 >= 0) xs2 = own_hinsert(L, x2, &xf2);
     const uint32_t xfb2 = xf2 ? ld_sc1(&fbh[x2]) : 0u;
     __syncthreads();
     bool keep = false;
     uint64_t km = 0;
-    if (wave < 3) {
+    if (wave < 4) {
         const uint32_t k = L.keys[64 * wave + lane];
-        keep = k && own_hfind(L, key_node(k, a) - nc.base) < 0;  // (pop p-3's nodes are not entries)
+        keep = k && own_hfind(L, key_node(k, a) - nc.base) < 0;
         km = __ballot(keep);
         if (lane == 0) L.wcnt[wave] = (uint32_t)__popcll(km);
     }
     __syncthreads();
-    if (wave < 3) {
+    if (wave < 4) {
         uint32_t base = 0;
         for (int w = 0; w < wave; ++w) base += L.wcnt[w];
-        const uint32_t tot = L.wcnt[0] + L.wcnt[1] + L.wcnt[2];
+        const uint32_t tot = L.wcnt[0] + L.wcnt[1] + L.wcnt[2] + L.wcnt[3];
         const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0));
         if (keep && pos < (uint32_t)kEngPkgN) L.slot_entry[pos] = 64 * wave + lane;
         if (wave < 2 && (uint32_t)(64 * wave + lane) >= tot) L.slot_entry[64 * wave + lane] = -1;
@@ -1248,11 +1287,11 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
 #pragma unroll
         for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
         if (wave == 0) ETL(A, p, 13);
-        const uint32_t xfb = wave == 0 ? xfb3 : xfb2;
-        const bool xf = wave == 0 ? xf3 : xf2;
+    }
+    if (wave == 1) {  // pop p-2's candidates' FitDelta bits (left out of pop p's counts)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int kx = __popcll(__ballot(xf && ((xfb >> b) & 1u)));
+            const int kx = __popcll(__ballot(xf2 && ((xfb2 >> b) & 1u)));
             if (lane == 0 && kx) atomicAdd((uint32_t*)&L.xfit[b], (uint32_t)kx);
         }
     }
@@ -1274,7 +1313,6 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         ETL(A, p, 18);
     }
     __syncthreads();
-    if (xs3 >= 0) { L.hkey[xs3] = -1; L.hval[xs3] = -1; }
     if (xs2 >= 0) { L.hkey[xs2] = -1; L.hval[xs2] = -1; }
     return L.ok != 0;
 }
@@ -1383,7 +1421,7 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
         }
         if (next >= 0 && (int32_t)(ap - ((uint32_t)next - 4)) >= 0) {
             own_drain();
-            if (!own_package(cf, nc, t, c, A, L, fbh, (uint32_t)next)) return;
+            if (!own_package(cf, nc, t, c, A, L, fbh, kbase, (uint32_t)next, &ap)) return;
             dp = (uint32_t)next + 1;
             t0 = 0;
             continue;
@@ -1407,6 +1445,42 @@ __device__ __forceinline__ void eng_owner(const Conf& cf, const NodeCols& nc, co
 // ---------------------------------------------------------------------------
 static_assert(sizeof(Row) == 4 * (kPkFlags - kPkRow), "the package carries a Row as 28 32-bit words");
 static_assert(kEngDescClass + sizeof(TaskClass) / 4 <= kEngDescWords, "a descriptor carries its class");
+
+// Candidate j's row after the chunk's commits (place_row) from its row before
+// (`base`: the placer's row cache — the decision does not keep its copy live).
+template <typename ET>
+__device__ __forceinline__ Row eng_row_after(const TaskClass& c, const PlaceDec<ET>& D, const Row& base) {
+    // branch-free (no commits: zero of each): a Row chosen between two branches is copied
+    // through the stack, and its reload waits for every store in flight
+    const int cc = D.cc > 0 ? D.cc : 0;
+    const int na = cc < D.ap_l ? cc : D.ap_l;
+    return apply_commits(base, c, na, cc - na);
+}
+// place_fit_vals for engine classes (no host ports), the row before from the cache.
+template <typename ET>
+__device__ __forceinline__ void eng_fit_vals(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                             const TaskClass& c, const PopArgs& a, const PlaceDec<ET>& D,
+                                             const Row& base, const int32_t* fit_in, uint32_t fit_raw, uint64_t* g0,
+                                             uint64_t* g1) {
+    uint32_t fb_base = 0, fb_post = 0;
+    if (D.n >= 0) {
+        fb_base = fit_bits(c, base, true);  // candidates had a key: in the walk
+        const Row r = eng_row_after(c, D, base);
+        const uint64_t pw[4] = {0, 0, 0, 0};
+        int32_t sc;
+        bool passed;
+        (void)dyn_key(cf, c, t, nc, r, pw, D.n, true, D.na_n, &sc, &passed);
+        fb_post = fit_bits(c, r, passed);
+    }
+    const uint32_t sweep = fit_sum(fit_raw);
+    int32_t tot[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+        tot[b] = (int32_t)__builtin_amdgcn_readlane((int)sweep, b) + fit_in[b] +
+                 __popcll(__ballot((fb_post >> b) & 1u)) - __popcll(__ballot((fb_base >> b) & 1u));
+    *g0 = make_fit_granule(a.epoch, tot[0], tot[1]);
+    *g1 = make_fit_granule(a.epoch, tot[2], tot[3]);
+}
 
 // The placer's wave 0 after the decision: the FitDelta histogram of a task
 // that found no node (the sweep's counts from the group count words), the
@@ -1464,22 +1538,30 @@ __device__ __forceinline__ void eng_finish(const Conf& cf, const NodeCols& nc, c
             }
             fr = (uint32_t)x;
         }
-        place_fit_vals(cf, nc, t, c, a, D, L.fitin, fr, &g0, &g1);
+        eng_fit_vals(cf, nc, t, c, a, D, L.rc.row[L.srcslot[lane]], L.fitin, fr, &g0, &g1);
     }
+    ETL(A, p, 47);
     L.gran[lane] = place_granule_val(a, D);
     if (lane == 0) { L.gfit[0] = g0; L.gfit[1] = g1; }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the granules are in LDS before the flag
     if (lane == 0) __hip_atomic_store(&L.gran_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     const int n = D.n;
-    if (n >= 0) {  // every candidate's row after the chunk into ring r0 (the next three pops re-evaluate them)
+    {
+        const int cc = D.cc > 0 ? D.cc : 0;
+        const int na = cc < D.ap_l ? cc : D.ap_l;
+        L.ccm[lane] = n >= 0 ? (na | ((cc - na) << 8)) : 0;
+    }
+    if (n >= 0) {  // every candidate's row after the chunk into ring r0 (the next three pops re-evaluate them;
+                   // from its row before in the cache, not the decision's copy)
         const int src = L.srcslot[lane];
-        L.rc.row[64 * r0 + lane] = place_row(c, D);
+        L.rc.row[64 * r0 + lane] = eng_row_after(c, D, L.rc.row[src]);
         L.flags[64 * r0 + lane] = L.flags[src];
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the rows are in LDS before the flag (the front reads them)
     if (lane == 0) __hip_atomic_store(&L.rows_seq, (int)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    ETL(A, p, 27);
     if (n >= 0 && D.cc > 0) {
-        const Row r = place_row(c, D);
+        const Row r = L.rc.row[64 * r0 + lane];
         st_sc1(&nc.idle_cpu[n], r.idle_cpu); st_sc1(&nc.idle_mem[n], r.idle_mem); st_sc1(&nc.idle_gpu[n], r.idle_gpu);
         st_sc1(&nc.rel_cpu[n], r.rel_cpu); st_sc1(&nc.rel_mem[n], r.rel_mem); st_sc1(&nc.rel_gpu[n], r.rel_gpu);
         st_sc1(&nc.pods[n], r.pods);
@@ -1566,13 +1648,61 @@ __device__ __forceinline__ void eng_drop_stale(EngPlacerLds& L, const PopArgs& a
     if (c1 && q1 < 64) rc_insert(&rc, key_node(k1, a), stage + 64 + lane);
 }
 
+// Role 0 of one candidate on row r: its key, FitDelta bits, key kind, node-affinity
+// weight, and (kind 2) the depth-1 score after a Pipeline.
+struct FrontKey {
+    uint32_t e, fb, kind;
+    int32_t na, s1p;
+};
+__device__ __forceinline__ FrontKey front_key(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                              const TaskClass& c, const PopArgs& a, int node, const Row& r,
+                                              uint8_t fl) {
+    FrontKey k{0u, 0u, 0u, 0, INT32_MIN};
+    const uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t sc;
+    bool passed;
+    const bool st = static_pred_f(cf, c, t, nc, node, fl);
+    k.na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
+    const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, k.na, &sc, &passed);
+    k.e = sweep_key<uint32_t>(k0, a);
+    k.fb = fit_bits(c, r, passed);
+    k.kind = k0 ? key_kind(k0) : 0;
+    if (__ballot(k.kind == 2) != 0 && k.kind == 2) {  // (rare)
+        const uint64_t k1 = dyn_key(cf, c, t, nc, apply_commits(r, c, 0, 1), pw, node, true, k.na, &sc, &passed);
+        k.s1p = k1 ? key_score(k1) : INT32_MIN;
+    }
+    return k;
+}
+// Role 1: the depth-1 score after an Allocate on row r.
+__device__ __forceinline__ int32_t front_s1a(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                             const TaskClass& c, int node, const Row& r) {
+    const uint64_t pw[4] = {0, 0, 0, 0};
+    int32_t sc;
+    bool passed;
+    const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
+    const uint64_t k1 = dyn_key(cf, c, t, nc, apply_commits(r, c, 1, 0), pw, node, true, na, &sc, &passed);
+    return k1 ? key_score(k1) : INT32_MIN;
+}
+__device__ __forceinline__ bool front_wait(const EngPlacerLds& L, const int* seq, int want) {
+    while (__hip_atomic_load(seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != want) {
+        if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+
 // Pop q's previous candidates, evaluated during pop q-1's placement by waves
-// it leaves idle: set s = pop q-1-s's candidates (ring (q + 3 - s) % 4; set 0's
-// rows once pop q-1's decision has written them, L.rows_seq); role 0 the key
-// (static predicates, node-affinity weight, FitDelta bits, kind), 1 / 2 the
-// depth-1 score after an Allocate / a Pipeline.  Into the front arrays (fe,
-// ...): pop q-1's placement still reads the row cache's na / s1 of the older
-// slots; pop q's P2 moves the ones that count there.
+// it leaves idle: set s = pop q-1-s's candidates (ring (q + 3 - s) % 4); role 0
+// the key (static predicates, node-affinity weight, FitDelta bits, kind), 1 the
+// depth-1 score after an Allocate (after a Pipeline: with role 0, for the rare
+// keys of that kind).  Into the front arrays (fe, ...): pop q-1's placement
+// still reads the row cache's na / s1 of the older slots; pop q's P2 moves the
+// ones that count there.  Set 0's rows are pop q-1's results: its candidates are
+// evaluated ahead of that decision on their rows before it (variant 0, here)
+// and after one Allocate of its class (variant 1, eng_front_v1, another wave);
+// once the decision is in (L.rows_seq) each lane takes the variant of its
+// commits (L.ccm), or evaluates its final row (two or more commits, a Pipeline).
+template <bool LIST>
 __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& nc, const DevTables& t,
                                                const EngArgs& A, EngPlacerLds& L, uint32_t q, uint32_t dw, int set,
                                                int role) {
@@ -1584,63 +1714,134 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
     const PopArgs a = eng_args(d);
     const TaskClass c = eng_class_x(dw);
     const int ring = (int)((q + 3 - set) % 4);
-    if (set == 0)  // pop q-1's rows: written by its decision's wave (eng_finish)
-        while (__hip_atomic_load(&L.rows_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != (int)(q - 1)) {
-            if (!__hip_atomic_load(&L.ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
-            __builtin_amdgcn_s_sleep(1);
+    const int sl = 64 * ring + lane;
+    if (!LIST && set == 0) {  // sweep mode: pop q-1's candidates on their final rows (its decision)
+        if (!front_wait(L, &L.rows_seq, (int)(q - 1))) return;
+        const int node = L.xn[ring][lane];
+        if (role == 0) {
+            ETL(A, q - 1, 32);
+            FrontKey k{0u, 0u, 0u, 0, INT32_MIN};
+            if (node >= 0) k = front_key(cf, nc, t, c, a, node, L.rc.row[sl], L.flags[sl]);
+            ETL(A, q - 1, 33);
+            L.fe[0][lane] = k.e;
+            L.ffb[0][lane] = (uint8_t)k.fb;
+            L.fkind[0][lane] = (uint8_t)k.kind;
+            L.fna[0][lane] = k.na;
+            if (k.kind == 2) L.fs1p[0][lane] = k.s1p;
+            ETL(A, q - 1, 34);
+            L.e[0][lane] = wave_sort_desc(node >= 0 ? k.e : 0u);
+            L.fbp[0][lane] = node >= 0 ? (uint8_t)k.fb : (uint8_t)0;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) __hip_atomic_store(&L.sort_seq[0], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            ETL(A, q - 1, 35);
+        } else if (node >= 0) {
+            L.fs1a[0][lane] = front_s1a(cf, nc, t, c, node, L.rc.row[sl]);
         }
+        return;
+    }
+    if (set == 0) {  // list mode: pop q-1's candidates (its P3): their rows before it, both variants
+        if (!front_wait(L, &L.xn_seq, (int)(q - 1))) return;
+        const int node = L.xn[ring][lane];
+        const int src = node >= 0 ? L.srcslot[lane] : 0;
+        // (a row P3 had to load into this pop's own ring is overwritten by the decision: final row only)
+        const bool own_ring = src >= 64 * ring && src < 64 * ring + 64;
+        if (role == 0) {
+            FrontKey k{0u, 0u, 0u, 0, INT32_MIN};
+            if (node >= 0) k = front_key(cf, nc, t, c, a, node, L.rc.row[src], L.flags[src]);
+            if (!front_wait(L, &L.rows_seq, (int)(q - 1))) return;
+            ETL(A, q - 1, 32);
+            const int m = L.ccm[lane];
+            if (m == 1 && node >= 0 && !own_ring) {  // one Allocate: variant 1
+                if (!front_wait(L, &L.v1_seq[0], (int)q)) return;
+                k.e = L.v1e[lane]; k.fb = L.v1fb[lane]; k.kind = L.v1kind[lane]; k.s1p = L.v1s1p[lane];
+            }
+            const bool slow = node >= 0 && (m > 1 || own_ring);  // two or more commits, or a Pipeline: the final row
+            if (__ballot(slow) != 0 && slow) k = front_key(cf, nc, t, c, a, node, L.rc.row[sl], L.flags[sl]);
+            ETL(A, q - 1, 33);
+            L.fe[0][lane] = k.e;
+            L.ffb[0][lane] = (uint8_t)k.fb;
+            L.fkind[0][lane] = (uint8_t)k.kind;
+            L.fna[0][lane] = k.na;
+            if (k.kind == 2) L.fs1p[0][lane] = k.s1p;
+            ETL(A, q - 1, 34);
+            L.e[0][lane] = wave_sort_desc(node >= 0 ? k.e : 0u);
+            L.fbp[0][lane] = node >= 0 ? (uint8_t)k.fb : (uint8_t)0;
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) __hip_atomic_store(&L.sort_seq[0], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            ETL(A, q - 1, 35);
+        } else {
+            int32_t s1 = INT32_MIN;
+            if (node >= 0) s1 = front_s1a(cf, nc, t, c, node, L.rc.row[src]);
+            if (!front_wait(L, &L.rows_seq, (int)(q - 1))) return;
+            const int m = L.ccm[lane];
+            if (m == 1 && node >= 0 && !own_ring) {
+                if (!front_wait(L, &L.v1_seq[1], (int)q)) return;
+                s1 = L.v1s1a[lane];
+            }
+            const bool slow = node >= 0 && (m > 1 || own_ring);
+            if (__ballot(slow) != 0 && slow) s1 = front_s1a(cf, nc, t, c, node, L.rc.row[sl]);
+            if (node >= 0) L.fs1a[0][lane] = s1;
+        }
+        return;
+    }
     if (role == 0) ETL(A, q - 1, 32 + 4 * set);  // timeline (pop q-1's slot): set s's key at events 32 + 4 s ..
     const int node = L.xn[ring][lane];
-    const int sl = 64 * ring + lane;
-    const uint64_t pw[4] = {0, 0, 0, 0};
-    int32_t sc;
-    bool passed;
     if (role == 0) {
-        uint32_t e = 0, fb = 0, kind = 0;
-        int32_t na = 0;
-        if (node >= 0) {
-            const Row r = L.rc.row[sl];
-            const bool st = static_pred_f(cf, c, t, nc, node, L.flags[sl]);
-            na = (st && cf.score_mult) ? na_weight(c, t, nc, node) : 0;
-            const uint64_t k0 = dyn_key(cf, c, t, nc, r, pw, node, st, na, &sc, &passed);
-            e = sweep_key<uint32_t>(k0, a);
-            fb = fit_bits(c, r, passed);
-            kind = k0 ? key_kind(k0) : 0;
-        }
+        FrontKey k{0u, 0u, 0u, 0, INT32_MIN};
+        if (node >= 0) k = front_key(cf, nc, t, c, a, node, L.rc.row[sl], L.flags[sl]);
         ETL(A, q - 1, 33 + 4 * set);
-        L.fe[set][lane] = e;
-        L.ffb[set][lane] = (uint8_t)fb;
-        L.fkind[set][lane] = (uint8_t)kind;
-        L.fna[set][lane] = na;
-        // the depth-1 score after a Pipeline, for the (rare) keys whose commit is one
-        if (__ballot(kind == 2) != 0 && kind == 2) {
-            const Row r1 = apply_commits(L.rc.row[sl], c, 0, 1);
-            const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
-            L.fs1p[set][lane] = k1 ? key_score(k1) : INT32_MIN;
-        }
-        // the set's keys that count (sets 1, 2: not a later set's node, from wave 2's hash)
-        // sorted for pop q's P3, and their FitDelta bits; else the placer's P2 does it
-        bool hashed = set == 0;
+        L.fe[set][lane] = k.e;
+        L.ffb[set][lane] = (uint8_t)k.fb;
+        L.fkind[set][lane] = (uint8_t)k.kind;
+        L.fna[set][lane] = k.na;
+        if (k.kind == 2) L.fs1p[set][lane] = k.s1p;
+        // the set's keys that count (not a later set's node, from wave 2's hash) sorted for
+        // pop q's P3, and their FitDelta bits; else the placer's P2 does it
+        bool hashed = false;
         for (int i = 0; i < 4096 && !hashed; ++i) {
             hashed = __hip_atomic_load(&L.hash_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q;
             if (!hashed) __builtin_amdgcn_s_sleep(1);
         }
         ETL(A, q - 1, 34 + 4 * set);
         if (hashed) {
-            const bool use = node >= 0 && (set == 0 || (set == 1 ? L.x2use[lane] : L.x3use[lane]));
-            L.e[set][lane] = wave_sort_desc(use ? e : 0u);
-            L.fbp[set][lane] = use ? (uint8_t)fb : (uint8_t)0;
+            const bool use = node >= 0 && (set == 1 ? L.x2use[lane] : L.x3use[lane]);
+            L.e[set][lane] = wave_sort_desc(use ? k.e : 0u);
+            L.fbp[set][lane] = use ? (uint8_t)k.fb : (uint8_t)0;
             __builtin_amdgcn_s_waitcnt(0xc07f);
             if (lane == 0) __hip_atomic_store(&L.sort_seq[set], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             ETL(A, q - 1, 35 + 4 * set);
         }
-    } else if (node >= 0) {  // the depth-1 score after an Allocate
-        const Row r = L.rc.row[sl];
-        const int32_t na = cf.score_mult ? na_weight(c, t, nc, node) : 0;
-        const Row r1 = apply_commits(r, c, 1, 0);
-        const uint64_t k1 = dyn_key(cf, c, t, nc, r1, pw, node, true, na, &sc, &passed);
-        L.fs1a[set][lane] = k1 ? key_score(k1) : INT32_MIN;
+    } else if (node >= 0) {
+        L.fs1a[set][lane] = front_s1a(cf, nc, t, c, node, L.rc.row[sl]);
     }
+}
+
+// Variant 1 of set 0 (eng_front_eval): pop q-1's candidates after one Allocate of
+// its class, role 0 (key) or 1 (depth-1 score), into L.v1*; then L.v1_seq[role] = q.
+__device__ __forceinline__ void eng_front_v1(const Conf& cf, const NodeCols& nc, const DevTables& t,
+                                             EngPlacerLds& L, uint32_t q, uint32_t dw, int role) {
+    const int lane = eng_lane();
+    uint32_t w[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)dw, i);
+    const PopArgs a = eng_args(eng_decode(w));
+    const TaskClass c = eng_class_x(dw);
+    if (!front_wait(L, &L.xn_seq, (int)(q - 1))) return;
+    const TaskClass& cp = *(const TaskClass*)&L.desc[(q - 1) % 2][kEngDescClass];  // pop q-1's class
+    const int ring = (int)((q + 3) % 4);
+    const int node = L.xn[ring][lane];
+    if (node >= 0) {
+        const int src = L.srcslot[lane];
+        const Row r = apply_commits(L.rc.row[src], cp, 1, 0);
+        if (role == 0) {
+            const FrontKey k = front_key(cf, nc, t, c, a, node, r, L.flags[src]);
+            L.v1e[lane] = k.e; L.v1fb[lane] = (uint8_t)k.fb; L.v1kind[lane] = (uint8_t)k.kind; L.v1s1p[lane] = k.s1p;
+        } else {
+            L.v1s1a[lane] = front_s1a(cf, nc, t, c, node, r);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    if (lane == 0) __hip_atomic_store(&L.v1_seq[role], (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // Pop q's front, by waves: 2 the hash of pops q-1 / q-2 / q-3's candidates
@@ -1652,6 +1853,7 @@ __device__ __forceinline__ void eng_front_eval(const Conf& cf, const NodeCols& n
 // ready).  Run for pop p + 1 by the waves pop p's placement leaves idle (and
 // for the first pop up front).  An exit descriptor has no package: its
 // descriptor comes from the device ring.
+template <bool LIST>
 __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                                           EngPlacerLds& L, uint32_t q, int wave) {
     const int lane = threadIdx.x & 63;
@@ -1702,27 +1904,41 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         const int n2 = L.xn[r2][lane];
+        // list mode: the package holds pop q-2's candidates too (with stale keys) — a node of both
+        // pops is in both sets, pop q-1's row is the latest either way; the hash keeps that one
         const bool use2 = n2 >= 0 && rc_find(&rc, n2) < 0;  // a node of both: pop q-1's row is the latest
         L.x2use[lane] = use2;
         if (use2) rc_insert(&rc, n2, 64 * r2 + lane);
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_wave_barrier();
-        const int n3 = L.xn[r3][lane];
-        const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
-        L.x3use[lane] = use3;
-        if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
+        if (!LIST) {  // sweep mode: pop q-3's candidates too (list mode: the owner re-keyed them)
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            const int n3 = L.xn[r3][lane];
+            const bool use3 = n3 >= 0 && rc_find(&rc, n3) < 0;
+            L.x3use[lane] = use3;
+            if (use3) rc_insert(&rc, n3, 64 * r3 + lane);
+        }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the hash is in LDS before the flag
         if (lane == 0) __hip_atomic_store(&L.hash_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        eng_front_eval(cf, nc, t, A, L, q, dw, 0, 1);
+        eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 0, 1);
         return;
     }
-    // one evaluation per wave (set, role: 0 the key, 1 the depth-1 score after an Allocate);
-    // waves w and w + 4 share a SIMD's issue slots; set 0 waits for pop q-1's rows
-    if (wave == 1) { eng_front_eval(cf, nc, t, A, L, q, dw, 0, 0); return; }
-    if (wave == 5) { eng_front_eval(cf, nc, t, A, L, q, dw, 1, 1); return; }
-    if (wave == 3) eng_front_eval(cf, nc, t, A, L, q, dw, 2, 1);
-    else if (wave == 6) eng_front_eval(cf, nc, t, A, L, q, dw, 1, 0);
-    else if (wave == 7) eng_front_eval(cf, nc, t, A, L, q, dw, 2, 0);  // (wave 4: wave 0's SIMD, loads only)
+    // the evaluations (set, role: 0 the key, 1 the depth-1 score after an Allocate), a few
+    // per wave; waves w and w + 4 share a SIMD's issue slots.  List mode: two sets, set 0
+    // (pop q-1's candidates) evaluated beside pop q-1's decision (variants 0 and 1) and only
+    // chosen once it is in; sweep mode: three sets, set 0 after the decision.
+    if constexpr (LIST) {
+        if (wave == 1) { eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 0, 0); return; }
+        if (wave == 5) { eng_front_v1(cf, nc, t, L, q, dw, 1); return; }  // (after the host results)
+        if (wave == 3) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 1, 1);
+        else if (wave == 6) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 1, 0);
+        else if (wave == 7) eng_front_v1(cf, nc, t, L, q, dw, 0);  // (wave 4: wave 0's SIMD, loads only)
+    } else {
+        if (wave == 1) { eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 0, 0); return; }
+        if (wave == 5) { eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 1, 1); return; }
+        if (wave == 3) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 2, 1);
+        else if (wave == 6) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 1, 0);
+        else if (wave == 7) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 2, 0);
+    }
     // two generations of the package's loads in flight, checked in turn (the package is
     // read whole each time: four waves of one block, a few tens of GB/s), so that it is
     // in registers about a round trip after it lands
@@ -1779,6 +1995,20 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
                 eng_drop_stale(L, eng_args(eng_decode(w8)), q);
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 if (lane == 0) __hip_atomic_store(&L.drop_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                // the list merged with sets 1 and 2 once they are sorted (P3 then merges set 0 only)
+                bool both = false;
+                for (int i = 0; i < 4096 && !both; ++i) {
+                    both = __hip_atomic_load(&L.sort_seq[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q &&
+                           (LIST ||
+                            __hip_atomic_load(&L.sort_seq[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q);
+                    if (!both) __builtin_amdgcn_s_sleep(1);
+                }
+                if (both) {
+                    uint32_t top = wave_merge_desc(L.s64[lane], L.e[1][lane]);
+                    L.pre64[lane] = LIST ? top : wave_merge_desc(top, L.e[2][lane]);
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    if (lane == 0) __hip_atomic_store(&L.pre_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
             }
         }
     } else if (k == 0 && lane == 0) {  // a wait gave up (the error is recorded)
@@ -1810,11 +2040,12 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         L.ok = 1; L.gran_seq = 0; L.ndesc_seq = 0; L.rows_seq = (int)A.first - 1;
         L.hash_seq = L.drop_seq = (int)A.first - 1;
         L.xn_seq = (int)A.first - 1;
+        L.v1_seq[0] = L.v1_seq[1] = L.pre_seq = (int)A.first - 1;
         L.sort_seq[0] = L.sort_seq[1] = L.sort_seq[2] = (int)A.first - 1;
         L.apmin = A.first - 1;
     }
     __syncthreads();
-    eng_front(cf, nc, t, A, L, A.first, wave);
+    eng_front<LIST>(cf, nc, t, A, L, A.first, wave);
     uint32_t pend = 0;  // wave 0: the pop whose write-back is still in flight (0: none)
     for (uint32_t p = A.first;; ++p) {
         // rings of p-1, p-2, p-3, p
@@ -1844,7 +2075,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 if (lane == 0) __hip_atomic_store(&L.ndesc_seq, (int)(p + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        } else if (wave == 1 || wave == 5 || wave == 6) {  // pops p-1 / p-2 / p-3's candidates that count
+        } else if (wave == 1 || wave == 5 || (!LIST && wave == 6)) {  // pops p-1 / p-2 (/ p-3)'s candidates that count
             // (the front's evaluation): sorted keys, FitDelta bits, node-affinity weights and
             // depth-1 scores (the one their key's kind calls for) into the row cache
             const int set = wave == 1 ? 0 : wave - 4;
@@ -1868,11 +2099,17 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
         if (wave == 0) ETL(A, p, 3);
         // P3
         if (wave == 0) {
-            uint32_t top = wave_merge_desc(L.s64[lane], L.e[0][lane]);
-            top = wave_merge_desc(top, L.e[1][lane]);
-            top = wave_merge_desc(top, L.e[2][lane]);
+            uint32_t top;
+            if (__hip_atomic_load(&L.pre_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)p) {
+                top = wave_merge_desc(L.pre64[lane], L.e[0][lane]);  // (the front merged sets 1 (, 2))
+            } else {
+                top = wave_merge_desc(L.s64[lane], L.e[0][lane]);
+                top = wave_merge_desc(top, L.e[1][lane]);
+                if (!LIST) top = wave_merge_desc(top, L.e[2][lane]);
+            }
+            // (list mode: the owner counted pop p-3's candidates)
             const uint32_t fbp = (uint32_t)L.fbp[0][lane] | ((uint32_t)L.fbp[1][lane] << 4) |
-                                 ((uint32_t)L.fbp[2][lane] << 8);
+                                 (LIST ? 0u : ((uint32_t)L.fbp[2][lane] << 8));
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int k = __popcll(__ballot((fbp >> q) & 1u)) + __popcll(__ballot((fbp >> (q + 4)) & 1u)) +
@@ -1880,7 +2117,9 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 if (lane == q) L.fitin[q] = k;
             }
             const int n = top ? key_node(top, a) : -1;
+            ETL(A, p, 44);
             eng_publish_done(ctl, &pend);  // pop p-1's write-back (every node a worker may read next)
+            ETL(A, p, 45);
             if constexpr (LIST) {
                 // list mode: the log entry of pop p, once every owner has applied pop p - kEngLog
                 if ((int32_t)(L.apmin - (p - kEngLog)) < 0 && !eng_own_apmin(A, L, p - kEngLog)) {
@@ -1893,6 +2132,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
                 for (int cp = 0; cp < kEngCandCopies; ++cp)
                     st_sc1(&ctl->cands[p % kEngSlots][cp][lane], ((uint64_t)p << 32) | (uint32_t)n);
             }
+            ETL(A, p, 46);
             int src = n >= 0 ? rc_find(&rc, n) : -1;  // a previous pop's candidate, or a package entry
             if (n >= 0 && src < 0) {  // (every node of the list is one of those: kept for safety)
                 src = 64 * r0 + lane;
@@ -1934,7 +2174,7 @@ __device__ __forceinline__ void eng_placer(const Conf& cf, const NodeCols& nc, c
             // (wave 5's results first: its front waits for pop p+1's descriptor, which
             // the host may send only after it has seen them)
             if (wave == 5) eng_host_out(A, L, p, d.slot);
-            eng_front(cf, nc, t, A, L, p + 1, wave);
+            eng_front<LIST>(cf, nc, t, A, L, p + 1, wave);
             if (wave == 3) ETL(A, p, 15);
             if (wave == 1) ETL(A, p, 19);
             if (wave == 5) ETL(A, p, 29);

@@ -26,6 +26,7 @@
 #include <memory>
 #include <condition_variable>
 #include <mutex>
+#include <random>
 #include <tuple>
 #include <set>
 #include <stdexcept>

@@ -50,7 +50,8 @@ def main():
     pops = t[:, 31]
     order = np.argsort(pops)
     t, pops = t[order], pops[order]
-    keep = (pops > 100) & np.all(t[:, [0, 1, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 20, 28]] > 0, axis=1)
+    need = [0, 1, 3, 4, 5, 6, 7, 8, 15, 28] + ([10, 11, 12, 13, 20] if a.lists else [])
+    keep = (pops > 100) & np.all(t[:, need] > 0, axis=1)
     t = t[keep]
     pops = t[:, 31]
     cont = np.diff(pops) == 1
@@ -70,6 +71,13 @@ def main():
         if ok.any():
             per[f"placer 5->{ev} front {name}"] = us((t[:, ev] - t[:, 5])[ok])
     per["P2 wave0 drop (0->1)"] = us(t[:, 1] - t[:, 0])
+    per["P3: 3->44 merge"] = us(t[:, 44] - t[:, 3])
+    per["P3: 44->45 publish done (vmcnt)"] = us(t[:, 45] - t[:, 44])
+    per["P3: 45->46 cands / log stores"] = us(t[:, 46] - t[:, 45])
+    per["P3: 46->4 rc_find, srcslot"] = us(t[:, 4] - t[:, 46])
+    per["finish: 6->47 fit counts"] = us(t[:, 47] - t[:, 6])
+    per["finish: 47->27 rows_seq"] = us(t[:, 27] - t[:, 47])
+    per["finish: 27->7 write-back issued"] = us(t[:, 7] - t[:, 27])
     for st_, nm in ((0, "set 0 (pop p cands)"), (1, "set 1"), (2, "set 2")):
         b = 32 + 4 * st_
         ok = np.all(t[:, [b, b + 1, b + 2, b + 3]] > 0, axis=1)
@@ -79,22 +87,24 @@ def main():
             per[f"front {nm}: ->hashed"] = us((t[:, b + 2] - t[:, b + 1])[ok])
             per[f"front {nm}: sort"] = us((t[:, b + 3] - t[:, b + 2])[ok])
             per[f"front {nm}: end - 5"] = us((t[:, b + 3] - t[:, 5])[ok])
-    per["owner seen(20) - placer start(0)"] = us(t[:, 20] - t[:, 0])
-    per["owner seen(20) -> start(10)"] = us(t[:, 10] - t[:, 20])
-    per["owner start(10) - placer start(0)"] = us(t[:, 10] - t[:, 0])
-    per["owner start(10,p) - placer P3(4,p-3) (done p-4)"] = us((t[3:, 10] - t[:-3, 4])[prev(3)])
-    per["owner 10 -> 21 (p-3 cands, hash)"] = us(t[:, 21] - t[:, 10])
-    per["owner 21 -> 24 (threshold, wave 0)"] = us(t[:, 24] - t[:, 21])
-    per["owner 24 -> 26 (scan)"] = us(t[:, 26] - t[:, 24])
-    per["owner 26 -> 12 (sort)"] = us(t[:, 12] - t[:, 26])
-    per["owner sorted(12) - placer P3(4,p-2)"] = us((t[2:, 12] - t[:-2, 4])[prev(2)])
-    per["owner p-2 cands seen(11,p) - placer P3(4,p-2)"] = us((t[2:, 11] - t[:-2, 4])[prev(2)])
-    per["owner p-2 seen(11) -> stored(13)"] = us(t[:, 13] - t[:, 11])
-    per["owner stored(13) - placer start(0)"] = us(t[:, 13] - t[:, 0])
-    res_extra = {"active_segments_quantiles": [float(np.quantile(t[:, 25] & 0xff, q)) for q in (0.1, 0.5, 0.9)],
+    if a.lists:
+        per["owner seen(20) - placer start(0)"] = us(t[:, 20] - t[:, 0])
+        per["owner seen(20) -> start(10)"] = us(t[:, 10] - t[:, 20])
+        per["owner start(10) - placer start(0)"] = us(t[:, 10] - t[:, 0])
+        per["owner start(10,p) - placer P3(4,p-3) (done p-4)"] = us((t[3:, 10] - t[:-3, 4])[prev(3)])
+        per["owner 10 -> 21 (p-3 cands, hash)"] = us(t[:, 21] - t[:, 10])
+        per["owner 21 -> 24 (threshold, wave 0)"] = us(t[:, 24] - t[:, 21])
+        per["owner 24 -> 26 (scan)"] = us(t[:, 26] - t[:, 24])
+        per["owner 26 -> 12 (sort)"] = us(t[:, 12] - t[:, 26])
+        per["owner sorted(12) - placer P3(4,p-2)"] = us((t[2:, 12] - t[:-2, 4])[prev(2)])
+        per["owner p-2 cands seen(11,p) - placer P3(4,p-2)"] = us((t[2:, 11] - t[:-2, 4])[prev(2)])
+        per["owner p-2 seen(11) -> stored(13)"] = us(t[:, 13] - t[:, 11])
+        per["owner stored(13) - placer start(0)"] = us(t[:, 13] - t[:, 0])
+    res_extra = {} if not a.lists else {"active_segments_quantiles": [float(np.quantile(t[:, 25] & 0xff, q)) for q in (0.1, 0.5, 0.9)],
                  "thr_quantiles": [float(np.quantile(t[:, 25] >> 8, q)) for q in (0.1, 0.5, 0.9)]}
-    per["owner stored(13,p) - placer 5(p-1) front start"] = us((t[1:, 13] - t[:-1, 5])[cont])
-    per["owner stored(13,p) - placer 15(p-1) package in LDS"] = us((t[1:, 13] - t[:-1, 15])[cont])
+    if a.lists:
+        per["owner stored(13,p) - placer 5(p-1) front start"] = us((t[1:, 13] - t[:-1, 5])[cont])
+        per["owner stored(13,p) - placer 15(p-1) package in LDS"] = us((t[1:, 13] - t[:-1, 15])[cont])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     per_all = np.diff(t[:, 0])[cont] / 100.0
     res = {"pops": int(len(t)), "lists": a.lists,

@@ -289,12 +289,12 @@ def test_mailbox_queue_rule(engine_lib):
     fits = engine_lib.kbhip_shard_mailbox_fits
     assert fits(1, 1) == 1 and fits(1, 4) == 1  # one rank per process and device
     assert fits(2, 4) == 0  # the r04 rank-thread rehearsal under the default 4 queues
-    assert fits(2, 6) == 1 and fits(2, 5) == 0
-    assert fits(8, 24) == 1 and fits(8, 16) == 0
+    assert fits(2, 8) == 1 and fits(2, 7) == 0 and fits(2, 6) == 0  # two queues of headroom
+    assert fits(8, 26) == 1 and fits(8, 24) == 0
 
 
 @pytest.mark.gpu
-def test_mailbox_refuses_shared_hw_queues(engine, kbgen_mod, tmp_path):
+def test_mailbox_refuses_shared_hw_queues(engine, oracle_mod, kbgen_mod, tmp_path):
     """Two shard ranks as threads of this process on one GPU, with the default
     hardware queues: kbhip_shard_connect_mailbox refuses on both ranks
     (KBHIP_EUNSUPPORTED, after the handle all-gather) instead of letting their
@@ -318,12 +318,38 @@ def test_mailbox_refuses_shared_hw_queues(engine, kbgen_mod, tmp_path):
             bar.wait()
         return g
 
+    red = [None, None]
+
+    def reduce(rank):  # an in-process all-reduce over the two rank threads
+        def f(vals, op):
+            red[rank] = vals.copy()
+            bar.wait()
+            a, b = red[0], red[1]
+            if op == kb.RED_MAX_U64:
+                out = np.maximum(a, b)
+            elif op == kb.RED_MIN_I64:
+                out = np.minimum(a.view(np.int64), b.view(np.int64)).view(vals.dtype)
+            elif op == kb.RED_SUM_I64:
+                out = (a.view(np.int64) + b.view(np.int64)).view(vals.dtype)
+            else:
+                out = np.maximum(a.view(np.int64), b.view(np.int64)).view(vals.dtype)
+            bar.wait()
+            vals[:] = out
+        return f
+
+    logs = [None, None]
+
     def run(rank):
         s = kb.ShardedSession(buf, 0, rank, 2)
         try:
-            s.connect_mailbox(gather(rank))
-        except kb.KbhipError as e:
-            errs[rank] = str(e)
+            try:
+                s.connect_mailbox(gather(rank))
+            except kb.KbhipError as e:
+                errs[rank] = str(e)
+            # the refusal left the session unconnected: the host exchange works after it
+            s.connect_host(reduce(rank), gather(rank))
+            pod, node, kind = s.allocate()
+            logs[rank] = [(int(a), int(b), 4 if k == 1 else 8) for a, b, k in zip(pod, node, kind)]
         finally:
             s.close()
 
@@ -333,3 +359,4 @@ def test_mailbox_refuses_shared_hw_queues(engine, kbgen_mod, tmp_path):
     for t in th:
         t.join(timeout=120)
     assert all(e is not None and "error -3" in e and "hardware queues" in e for e in errs), errs
+    assert logs[0] is not None and logs[0] == logs[1] == oracle_mod.ref_allocate(p).as_list()
