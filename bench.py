@@ -76,7 +76,7 @@ def parse():
                     help="1: batched pops go to the persistent pop engine (one resident kernel, DESIGN.md §4.10); "
                          "0 = one launched kernel per pop")
     ap.add_argument("--engine-workers", type=int, default=0, help="engine worker blocks (0: as many as stay resident)")
-    ap.add_argument("--engine-lists", type=int, default=1, choices=(0, 1),
+    ap.add_argument("--engine-lists", type=int, default=0, choices=(0, 1),
                     help="1 = the engine's list mode when every class fits (class owners, DESIGN.md §4.11), 0 = sweep mode")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
                     help="N>1: one C4 session node-sharded over the GPUs (default; SURVEY.md §8e: per batched pop "
@@ -219,7 +219,7 @@ def open_sharded(buf, device, rank, world, dist):
 
 
 def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, keep_log=False, engine=1,
-                engine_workers=0, engine_lists=1):
+                engine_workers=0, engine_lists=0):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)

@@ -339,10 +339,10 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * engine (one resident kernel, a descriptor ring), 0 = launched kernels;
  * "engine_workers" = n caps its worker blocks (0: as many as stay resident);
  * "engine_groups" = g its merger blocks (-1: automatic, 0: none);
- * "engine_lists" = 1 (default) runs the engine in list mode when every
- * eligible class fits (one owner block per task class keeps the class's key
- * of every node, updated from the rows each pop touches),
- * 0 = sweep mode (worker blocks sweep every node per pop);
+ * "engine_lists" = 1 runs the engine in list mode when every eligible class
+ * fits (one owner block per task class keeps the class's key of every node,
+ * updated from the rows each pop touches), 0 (default) =
+ * sweep mode (worker blocks sweep every node per pop);
  * "overlap" = k rotates batched pops over k + 1 streams so that a pop's sweep
  * runs beside the previous k pops' placements, chained on the device (1, the
  * default, or 2); 0 = one stream, one pop kernel at a time;

@@ -730,9 +730,19 @@ def gen_c4(path: str, seed: int = BASE_SEED + 4, n_nodes: int = 100_000,
 
 
 def gen_c3(seed: int = BASE_SEED + 3, n_nodes: int = 20_000, n_pending: int = 50_000,
-           n_queues: int = 8) -> Cluster:
-    """C3: labels, taints/tolerations, selectors, zone anti-affinity, 8 queues."""
+           n_queues: int = 8, keyless: float = 0.0, pod_affinity: float = 0.0, ipa: float = 0.0) -> Cluster:
+    """C3: labels, taints/tolerations, selectors, zone anti-affinity, 8 queues.
+
+    Hardening options (0 = the C3 of the bench; they draw from a second
+    generator so the default stream is unchanged): ``keyless`` — the share of
+    nodes without the zone label (topology-keyless nodes: a pod-affinity term
+    by zone never matches there, predicates.go:1402-1458); ``pod_affinity`` —
+    the share of gangs with a required pod-affinity term by zone to their own
+    job (self-affine: the first pod goes anywhere, the rest follow it);
+    ``ipa`` — the share of gangs with preferred inter-pod affinity / anti-
+    affinity terms (interpod_affinity.go:119-240)."""
     rng = np.random.default_rng(seed)
+    rng2 = np.random.default_rng(seed + 7919)
     c = Cluster()
     zones = [f"z{i:02d}" for i in range(48)]
     itypes = ["it-a", "it-b", "it-c", "it-d"]
@@ -742,6 +752,8 @@ def gen_c3(seed: int = BASE_SEED + 3, n_nodes: int = 20_000, n_pending: int = 50
         labels = {"zone": zones[int(rng.integers(48))], "rack": f"r{i // 40:04d}",
                   "instance-type": itypes[int(rng.integers(4))],
                   "gen": str(int(rng.integers(1, 6))), "kubernetes.io/hostname": name}
+        if keyless and rng2.random() < keyless:
+            del labels["zone"]
         taints = [("dedicated", "gpu", "NoSchedule")] if rng.random() < 0.1 else []
         c.add_node(name, s[0], s[1], s[2], 110, labels=labels, taints=taints)
     for q in range(n_queues):
@@ -765,6 +777,18 @@ def gen_c3(seed: int = BASE_SEED + 3, n_nodes: int = 20_000, n_pending: int = 50
             aff = dict(aff or {})
             aff["node"] = {"preferred": [(10, {"expr": [("gen", "Gt", ["3"])]}),
                                          (5, {"expr": [("zone", "In", zones[:8])]})]}
+        if pod_affinity and rng2.random() < pod_affinity:
+            aff = dict(aff or {})
+            aff["pod"] = {"required": [{"selector": {"ml": {"job": jn}}, "topology_key": "zone"}]}
+        if ipa and rng2.random() < ipa:
+            aff = dict(aff or {})
+            other = f"jp{int(rng2.integers(max(1, j))):07d}"
+            aff["pod"] = dict(aff.get("pod") or {})
+            aff["pod"]["preferred"] = [(int(rng2.integers(1, 50)),
+                                        {"selector": {"ml": {"job": other}}, "topology_key": "zone"})]
+            aff["anti"] = dict(aff.get("anti") or {})
+            aff["anti"]["preferred"] = [(int(rng2.integers(1, 20)),
+                                         {"selector": {"ml": {"job": jn}}, "topology_key": "rack"})]
         for k in range(size):
             c.add_pod("default", f"{jn}-{k:03d}", uid=f"u{total + k:08d}", group=jn, priority=pri, ts=ts,
                       labels={"job": jn}, containers=[dict(r)], node_selector=dict(nsel),
@@ -778,9 +802,13 @@ def gen_random(seed: int, n_nodes: int = 8, n_jobs: int = 6, max_tasks: int = 5,
                features: Sequence[str] = ("labels", "taints", "ports", "affinity", "init",
                                           "running", "releasing", "backfill", "selector", "nodeaffinity",
                                           "podaffinity", "unsched", "bestEffort"),
-               tiers=None, n_queues: int = 2, best_effort_p: float = 0.1) -> Cluster:
-    """Small random cluster exercising every feature of the hot path (parity tests)."""
+               tiers=None, n_queues: int = 2, best_effort_p: float = 0.1, keyless: float = 0.0) -> Cluster:
+    """Small random cluster exercising every feature of the hot path (parity tests).
+
+    ``keyless``: the share of nodes without the zone label (a second generator:
+    the default stream is unchanged)."""
     rng = np.random.default_rng(seed)
+    rng2 = np.random.default_rng(seed + 7919)
     f = set(features)
     c = Cluster(tiers=tiers)
     zones = ["za", "zb", "zc"]
@@ -790,6 +818,8 @@ def gen_random(seed: int, n_nodes: int = 8, n_jobs: int = 6, max_tasks: int = 5,
         labels = {}
         if "labels" in f:
             labels = {"zone": zones[int(rng.integers(3))], "kubernetes.io/hostname": name}
+            if keyless and rng2.random() < keyless:
+                del labels["zone"]
             if rng.random() < 0.8:
                 labels["itype"] = itypes[int(rng.integers(2))]
             if rng.random() < 0.7:

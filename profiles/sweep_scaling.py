@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""The standalone predicate + score sweep (k_score_sweep, kbhip_sweep_scores'
+kernel: every node's PredicateFn + NodeOrderFn key for one task,
+preempt.go:270-287) against the node count N (VERDICT r05 "next" 5):
+C4-shaped clusters (its SKU mix and task classes, no running pods) of N nodes,
+`launches` tasks swept back to back (warm: the columns stay in the caches
+while they fit the 256 MB Infinity Cache, N x 113 B) and one at a time behind
+a 512 MB cache-evicting write (cold: every launch reads HBM).  Prints one JSON
+line per N with the HIP-event time per launch and the roofline fraction on the
+algorithmic bytes (N x 113 B).  Run one N per process under
+rocprofv3 --kernel-trace --stats for the kernel's own duration and under
+--pmc FETCH_SIZE for its HBM bytes (profiles/r06_sweep_scaling.sh)."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import kbgen  # noqa: E402
+import kbhip  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, nargs="+", default=[100_000, 400_000, 1_000_000, 4_000_000])
+    ap.add_argument("--pending", type=int, default=20_000)
+    ap.add_argument("--launches", type=int, default=256)
+    ap.add_argument("--cold", type=int, default=32)
+    ap.add_argument("--mode", choices=("both", "warm", "cold"), default="both")
+    ap.add_argument("--cache", default="/tmp/kbhip_bench")
+    a = ap.parse_args()
+    os.makedirs(a.cache, exist_ok=True)
+    for n in a.nodes:
+        path = os.path.join(a.cache, f"sweep_{n}_{a.pending}.kbs")
+        if not os.path.exists(path):
+            kbgen.gen_c4(path, n_nodes=n, n_pending=a.pending, running_per_node=0)
+        with open(path, "rb") as f:
+            buf = f.read()
+        rec = {"nodes": n, "bytes_per_launch": n * bench.B_NODE,
+               "fits_infinity_cache": n * bench.B_NODE < 256 << 20}
+        with kbhip.Session(buf) as s:
+            ids = np.arange(0, a.pending, max(1, a.pending // a.launches), dtype=np.int32)[: a.launches]
+            if a.mode in ("both", "warm"):
+                s.time_sweeps(ids[:16])  # warm up
+                us = s.time_sweeps(ids)
+                gbs = n * bench.B_NODE / (us * 1e-6) / 1e9
+                rec["warm"] = {"launches": int(len(ids)), "mean_us": us, "gbs": gbs, "frac": gbs / bench.HBM_PEAK_GBS}
+            if a.mode in ("both", "cold"):
+                s.set_option("time_sweeps_cold", 1)
+                us = s.time_sweeps(ids[: a.cold])
+                gbs = n * bench.B_NODE / (us * 1e-6) / 1e9
+                rec["cold"] = {"launches": int(a.cold), "mean_us": us, "gbs": gbs, "frac": gbs / bench.HBM_PEAK_GBS,
+                               "timing": "HIP events around each launch alone (dispatch and drain included)"}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
