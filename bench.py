@@ -26,8 +26,11 @@ Also reported:
    per pop / the device busy period per pop (allocate's
   device span, HIP events on the session streams, / batched pops); beside it
   the standalone predicate + score sweep (`sweep`: the product kernel
-  k_score_sweep behind kbhip_sweep_scores, one launch over all nodes, timed
-  with HIP events around back-to-back launches);
+  k_score_sweep behind kbhip_sweep_scores, one launch over all nodes; 41 B
+  read + 8 B written per node), warm (HIP events around back-to-back
+  launches) and cold (each launch alone behind a cache-evicting read), on the
+  C4 session and on a C4-shaped cluster of --sweep-nodes nodes (`at_scale`),
+  each beside the committed rocprofv3 counter bytes of that size;
 * cpu_baseline: the hoisted C++ restatement (oracle/kbfast.cpp) on the host
   cores, timed on a stratified sample of the same session: pop windows early,
   mid and late in the session, the pops between them fast-forwarded from the
@@ -51,6 +54,11 @@ import kbhip  # noqa: E402
 
 METRIC = "pod placements/sec + p50 session latency, 100k nodes × 1M pods"
 B_NODE = 113  # algorithmic bytes per node per sweep
+# the standalone predicate + score sweep (kbhip_sweep_scores): its keys depend on
+# 41 B of each node (flags, acpu / amem / nzc / nzm, pods, maxtasks: PredicateFn
+# + NodeOrderFn read no Idle / Releasing / Backfilled column) + the 8-byte key
+SWEEP_B_READ, SWEEP_B_WRITE = 41, 8
+SWEEP_B_NODE = SWEEP_B_READ + SWEEP_B_WRITE
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -63,6 +71,8 @@ def parse():
     ap.add_argument("--pending", type=int, default=800_000)
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the CPU restatement on rank 0")
+    ap.add_argument("--sweep-nodes", type=int, default=4_000_000,
+                    help="node count of the standalone sweep's at-scale line (roofline.sweep.at_scale; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU baseline sample length")
     ap.add_argument("--time-every", type=int, default=50,
                     help="HIP-event time every k-th batched pop launch on its own stream (the roofline's kernel "
@@ -240,33 +250,83 @@ def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, kee
     return t3 - t0, len(pod), st
 
 
-def sweep_roofline(buf, device, pods, n_tasks=512):
-    """The standalone predicate + score sweep at full size: kbhip_sweep_scores'
-    kernel (k_score_sweep: every node's PredicateFn + NodeOrderFn key,
-    preempt.go:270-287) for n_tasks pending tasks of the session, launched back
-    to back on the engine stream with one HIP-event pair around them
-    (kbhip_time_sweeps; outside the timed steps)."""
+def sweep_counters(nodes):
+    """The newest committed rocprofv3 summary of the standalone sweep at this
+    node count, cold (profiles/<tag>_<nodes>_cold_summary.json, written by
+    profiles/r06_sweep_scaling.sh): the kernel's own mean duration and its
+    FETCH_SIZE x 2 read bytes per launch (PMC cannot be read in a timed run)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{nodes}_cold_summary.json"))):
+        with open(p) as f:
+            d = json.load(f)
+        for name, k in d.get("kernels", {}).items():
+            if name.startswith("kbhip::k_score_sweep") and "hbm_bytes_per_launch_corrected" in k:
+                best = (k, os.path.basename(p))
+    if best is None:
+        return None
+    k, src = best
+    rd = k["hbm_bytes_per_launch_corrected"]
+    wr = k["write_size_kb_per_launch"] * 1024.0 if "write_size_kb_per_launch" in k else nodes * SWEEP_B_WRITE
+    gbs = (rd + wr) / (k["mean_us"] * 1e-6) / 1e9
+    return {"source": f"profiles/{src}", "kernel_mean_us": k["mean_us"], "read_bytes_per_launch": rd,
+            "write_bytes_per_launch": wr, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS,
+            "note": "over the kernel's own rocprofv3 duration, cold; read = FETCH_SIZE x 2 (the gfx950 "
+                    "correction: 41 B/node, what the kernel addresses), write = WRITE_SIZE (8.1 B/node: the keys)"}
+
+
+def sweep_line(s, nodes, ids, warm_n, cold_n):
+    s.set_option("time_sweeps_cold", 0)
+    s.time_sweeps(ids[:16])  # warm
+    mean_us = s.time_sweeps(ids[:warm_n])
+    s.set_option("time_sweeps_cold", 2)
+    cold_us = s.time_sweeps(ids[:cold_n])
+    s.set_option("time_sweeps_cold", 0)
+    b = nodes * SWEEP_B_NODE
+    warm = b / (mean_us * 1e-6) / 1e9 if mean_us > 0 else 0.0
+    cold = b / (cold_us * 1e-6) / 1e9 if cold_us > 0 else 0.0
+    return {"nodes": nodes, "bytes_per_launch": b, "launches": int(min(warm_n, len(ids))), "mean_us": mean_us,
+            "achieved": warm, "frac": warm / HBM_PEAK_GBS,
+            "cold": {"launches": int(min(cold_n, len(ids))), "mean_us": cold_us, "achieved": cold,
+                     "frac": cold / HBM_PEAK_GBS},
+            "counters": sweep_counters(nodes)}
+
+
+SWEEP_TIMING = ("warm: HIP events around back-to-back launches (kbhip_time_sweeps) / launches, the columns "
+                "staying in the 256 MB Infinity Cache; cold: HIP events around each launch alone behind a 512 MB "
+                "read that evicts L2 and the Infinity Cache (option time_sweeps_cold = 2), dispatch and drain "
+                "included; bytes = 41 B read (flags, acpu / amem / nzc / nzm, pods, maxtasks) + 8 B key written "
+                "per node")
+
+
+def sweep_roofline(buf, device, pods, cache, big_nodes, n_tasks=512):
+    """The standalone predicate + score sweep: kbhip_sweep_scores' kernel
+    (k_score_sweep: every node's PredicateFn + NodeOrderFn key,
+    preempt.go:270-287) for pending tasks of the session, on the C4 session
+    itself (100k nodes: bounded by the launch) and on a
+    C4-shaped cluster of big_nodes nodes (same SKU mix and task classes, no
+    running pods), where one launch is long enough to be bounded by HBM
+    (outside the timed steps)."""
     with kbhip.Session(buf, device=device) as s:
         step = max(1, len(pods) // n_tasks)
         ids = np.ascontiguousarray(pods[::step][:n_tasks], np.int32)
-        s.time_sweeps(ids[:16])  # warm
-        mean_us = s.time_sweeps(ids)
-        s.set_option("time_sweeps_cold", 1)
-        cold_ids = ids[:64]
-        cold_us = s.time_sweeps(cold_ids)
-        nodes = s.stats()["nodes"]
-    achieved = nodes * B_NODE / (mean_us * 1e-6) / 1e9 if mean_us > 0 else 0.0
-    cold_achieved = nodes * B_NODE / (cold_us * 1e-6) / 1e9 if cold_us > 0 else 0.0
-    return {"kernel": "k_score_sweep (kbhip_sweep_scores)", "launches": int(len(ids)), "mean_us": mean_us,
-            "bytes_per_launch": nodes * B_NODE, "achieved": achieved, "frac": achieved / HBM_PEAK_GBS,
-            "timing": "HIP events around the back-to-back launches (kbhip_time_sweeps), / launches: the node "
-                      "columns (11.3 MB) stay in the 256 MB Infinity Cache between launches",
-            "cold": {"launches": int(len(cold_ids)), "mean_us": cold_us, "achieved": cold_achieved,
-                     "frac": cold_achieved / HBM_PEAK_GBS,
-                     "timing": "HIP events around each launch alone (option time_sweeps_cold): a 512 MB write "
-                               "before every launch evicts L2 and the Infinity Cache, so the columns come from HBM; "
-                               "the span includes the launch's dispatch and drain"},
-            "note": "reads 113 B/node (SURVEY §8(d)); writes an 8-byte key per node (not counted)"}
+        out = sweep_line(s, s.stats()["nodes"], ids, n_tasks, 64)
+    out["kernel"] = "k_score_sweep (kbhip_sweep_scores)"
+    out["timing"] = SWEEP_TIMING
+    if big_nodes:
+        path = os.path.join(cache, f"sweep_{big_nodes}_20000.kbs")
+        if not os.path.exists(path):
+            os.makedirs(cache, exist_ok=True)
+            tmp = f"{path}.{os.getpid()}.tmp"
+            kbgen.gen_c4(tmp, n_nodes=big_nodes, n_pending=20_000, running_per_node=0)
+            os.replace(tmp, path)
+        with open(path, "rb") as f:
+            big = f.read()
+        with kbhip.Session(big, device=device) as s:
+            ids = np.arange(0, 20_000, 20_000 // 128, dtype=np.int32)[:128]
+            out["at_scale"] = sweep_line(s, big_nodes, ids, 128, 32)
+        del big
+    return out
 
 
 def cpu_baseline(path, target_s, log):
@@ -348,7 +408,7 @@ def main():
         return
     nodes = st_last["nodes"]
     traffic = None if shard else pmc_traffic(st_last["engine_pops"] > 0)
-    sweep = None if shard else sweep_roofline(buf, device, log0[0])
+    sweep = None if shard else sweep_roofline(buf, device, log0[0], args.cache, args.sweep_nodes)
     nodes_per_launch = (nodes + world - 1) // world if shard else nodes  # a shard sweeps its own range
     # the hot kernel's mean duration: HIP events around every batched pop launch on the stream it runs on
     # (overlapped pops: the duration includes the wait for the previous pop's write-back, as rocprof's does)

@@ -132,17 +132,6 @@ KBHIP_HD bool static_pred(const Conf& cf, const TaskClass& c, const DevTables& t
     return static_pred_f(cf, c, t, nc, n, cf.pred_on ? nc.flags[n] : (uint8_t)0);
 }
 
-// ((cap - req) * 10) / cap for 0 <= req <= cap, cap > 0: the quotient is in
-// [0, 10]; a double estimate plus one exact integer correction step.
-KBHIP_HD int64_t lr_score(int64_t req, int64_t cap) {  // least_requested.go:44-53
-    if (cap == 0 || req > cap) return 0;
-    const int64_t num = (cap - req) * 10;
-    int64_t q = (int64_t)((double)num / (double)cap);
-    if (q * cap > num) --q;
-    if ((q + 1) * cap <= num) ++q;
-    return q;
-}
-
 // Static part of the node-affinity priority: the summed weights of the
 // preferred terms the node matches (node_affinity.go:34-74).  Node labels do
 // not change in a session, so callers compute it once per node.
@@ -155,16 +144,31 @@ KBHIP_HD int32_t na_weight(const TaskClass& c, const DevTables& t, const NodeCol
     return na;
 }
 
+// least_requested.go:44-53: ((cap - req) * 10) / cap for 0 <= req <= cap,
+// cap > 0 (a quotient in [0, 10]), given f = the correctly rounded req / cap
+// (BRA's fraction, computed anyway): 10 - 10 f is within 1e-14 of the exact
+// quotient, so its truncation is off by at most one and the two exact
+// integer steps fix it — one IEEE division per resource instead of two.
+KBHIP_HD int64_t lr_score_f(int64_t req, int64_t cap, double f) {
+    if (cap == 0 || req > cap) return 0;
+    const int64_t num = (cap - req) * 10;
+    int64_t q = (int64_t)(10.0 - 10.0 * f);
+    q = q < 0 ? 0 : (q > 10 ? 10 : q);
+    if (q * cap > num) --q;
+    if ((q + 1) * cap <= num) ++q;
+    return q;
+}
+
 // Score of a feasible node (nodeorder.go:281-313): LR and BRA from the row,
 // na = na_weight(), ipa = the normalised inter-pod affinity score (0 for
 // classes without inter-pod terms).
 KBHIP_HD int32_t node_score(const Conf& cf, const TaskClass& c, const Row& r, int32_t na, int32_t ipa) {
     if (!cf.score_mult) return 0;
     const int64_t rc = c.nz_cpu + r.nzc, rm = c.nz_mem + r.nzm;
-    const int64_t lr = (lr_score(rc, r.acpu) + lr_score(rm, r.amem)) / 2;
     // balanced_resource_allocation.go:41-77, IEEE double, no contraction
     const double cpuF = r.acpu == 0 ? 1.0 : (double)rc / (double)r.acpu;
     const double memF = r.amem == 0 ? 1.0 : (double)rm / (double)r.amem;
+    const int64_t lr = (lr_score_f(rc, r.acpu, cpuF) + lr_score_f(rm, r.amem, memF)) / 2;
     int64_t bra = 0;
     if (!(cpuF >= 1.0 || memF >= 1.0)) {
         const double d = fabs(cpuF - memF);

@@ -14,8 +14,10 @@
 // zero for a node that fails; a stable counting sort over the class's small
 // score range orders them (launch_rank_sorted; classes whose score range
 // exceeds 256 values: four stable 8-bit counting passes over the score,
-// launch_rank_radix), and the host reads the passing prefix back.  Traffic per task: the per-task sweep's
-// B_node bytes per node + 8 B written per node + the sort's passes over 8 B keys.
+// launch_rank_radix), and the host reads the passing prefix back.  Traffic per task: the columns
+// PredicateFn + NodeOrderFn read — 41 B per node (flags, acpu / amem / nzc / nzm, pods, maxtasks;
+// no Idle / Releasing / Backfilled column: the compiler drops the fit loads, whose result the
+// sweep does not use) + 8 B written per node + the sort's passes over 8 B keys.
 #include <hip/hip_runtime.h>
 
 #include "kbhip_eval.h"
@@ -116,8 +118,91 @@ __global__ __launch_bounds__(TB) void k_score_sweep(Conf cf, NodeCols nc, DevTab
     if (threadIdx.x == 0 && s_cnt) atomicAdd(&counts[(blockIdx.x % kSweepGroups) * 32], s_cnt);
 }
 
+// The same sweep for a plain class over a grid of a few blocks per CU: each
+// thread walks nodes n, n + stride, ... and loads the next node's columns
+// before it evaluates the current one, so a wave's loads overlap its own
+// arithmetic (the one-node-per-thread grid issues every wave's loads, then
+// every wave's evaluation).  Only the columns the keys depend on are read:
+// flags, acpu / amem / nzc / nzm, pods, maxtasks (41 B per node; the fit
+// columns are not part of PredicateFn + NodeOrderFn) plus the class's port
+// words when it has host ports.
+struct SweepIn {
+    int64_t acpu, amem, nzc, nzm;
+    int32_t pods, maxtasks;
+    uint8_t fl;
+};
+__device__ __forceinline__ SweepIn sweep_in(const NodeCols& nc, int n) {
+    SweepIn v;
+    v.acpu = nc.acpu[n]; v.amem = nc.amem[n]; v.nzc = nc.nzc[n]; v.nzm = nc.nzm[n];
+    v.pods = nc.pods[n]; v.maxtasks = nc.maxtasks[n]; v.fl = nc.flags[n];
+    return v;
+}
+template <int TB>
+__global__ __launch_bounds__(TB) void k_score_sweep_gs(Conf cf, NodeCols nc, DevTables t, TaskClass c,
+                                                       uint64_t* keys, uint32_t* counts) {
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
+    const int stride = gridDim.x * TB;
+    int n = blockIdx.x * TB + threadIdx.x;
+    uint32_t cnt = 0;
+    SweepIn cur{};
+    if (n < nc.n) cur = sweep_in(nc, n);
+    for (; n < nc.n; n += stride) {
+        SweepIn nxt{};
+        if (n + stride < nc.n) nxt = sweep_in(nc, n + stride);
+        uint64_t pw[4] = {0, 0, 0, 0};
+        if (c.has_ports)
+            for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
+        Row r{};
+        r.acpu = cur.acpu; r.amem = cur.amem; r.nzc = cur.nzc; r.nzm = cur.nzm;
+        r.pods = cur.pods; r.maxtasks = cur.maxtasks;
+        const bool st = static_pred_f(cf, c, t, nc, n, cur.fl);
+        const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+        int32_t s = 0;
+        bool passed = false;
+        (void)dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);  // passed and s read no fit column
+        keys[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
+        cnt += passed;
+        cur = nxt;
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    __syncthreads();  // s_cnt zeroed
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_cnt) atomicAdd(&counts[(blockIdx.x % kSweepGroups) * 32], s_cnt);
+}
+
+static int cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+// Cache eviction by reading (kbhip_time_sweeps, option time_sweeps_cold = 2):
+// every 16-byte word of the buffer loaded, one word written only if the xor
+// hits a value it never takes (the loads stay live).
+__global__ __launch_bounds__(256) void k_evict_read(const uint4* p, size_t n16, uint32_t* sink) {
+    uint32_t x = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += (size_t)gridDim.x * 256) {
+        const uint4 v = p[i];
+        x ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (x == 0x9e3779b9u && sink) sink[0] = x;
+}
+hipError_t launch_evict_read(const void* buf, size_t bytes, hipStream_t st) {
+    hipLaunchKernelGGL(k_evict_read, dim3(cu_count() * 8), dim3(256), 0, st, (const uint4*)buf, bytes / 16,
+                       (uint32_t*)nullptr);
+    return hipGetLastError();
+}
+
 // variant (option "sweep_variant", a tuning knob): 0 = 256 threads x 1 node,
-// 1 = 512 x 1, 2 = 256 x 2, 3 = 256 x 4
+// 1 = 512 x 1, 2 = 256 x 2, 3 = 256 x 4; 4 / 5 / 6 = the prefetching grid
+// (k_score_sweep_gs) with 8 / 4 / 16 blocks of 256 per CU
 static int g_sweep_variant = 0;
 void set_sweep_variant(int v) { g_sweep_variant = v; }
 template <int TB, int NPT>
@@ -133,6 +218,13 @@ static void launch_sweep_t(const Conf& cf, const NodeCols& nc, const DevTables& 
 }
 hipError_t launch_score_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                               const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts, hipStream_t st) {
+    if (g_sweep_variant >= 4 && g_sweep_variant <= 6 && !c.aff && c.ipa_n == 0) {
+        const int per_cu = g_sweep_variant == 4 ? 8 : g_sweep_variant == 5 ? 4 : 16;
+        const int need = nc.n > 0 ? (nc.n + 255) / 256 : 1;
+        const int grid = need < cu_count() * per_cu ? need : cu_count() * per_cu;
+        hipLaunchKernelGGL((k_score_sweep_gs<256>), dim3(grid), dim3(256), 0, st, cf, nc, t, c, keys, counts);
+        return hipGetLastError();
+    }
     switch (g_sweep_variant) {
         case 1: launch_sweep_t<512, 1>(cf, nc, t, c, ctrl, keys, counts, st); break;
         case 2: launch_sweep_t<256, 2>(cf, nc, t, c, ctrl, keys, counts, st); break;

@@ -47,6 +47,7 @@ hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ct
 // pipeline, 2 unpipeline).
 // kbhip_sweep_scores' standalone sweep: keys per node, the passing count in
 // 8 counters (counts[32 g], g = 0..7; the caller zeroes and sums them).
+hipError_t launch_evict_read(const void* buf, size_t bytes, hipStream_t st);  // time_sweeps_cold = 2
 void set_sweep_variant(int v);  // option "sweep_variant" (process-wide tuning knob)
 hipError_t launch_score_sweep(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
                               const PopCtrl* ctrl, uint64_t* keys, uint32_t* counts, hipStream_t st);

@@ -85,6 +85,19 @@ def main(src, tag, dest=None):
             if k.startswith("kbhip::k_engine") and pops:
                 d["engine_pops"] = pops
                 d["hbm_bytes_per_pop_corrected"] = 2.0 * tot * 1024.0 / pops
+    w_csv = os.path.join(src, "pmcw", "run_counter_collection.csv")
+    if os.path.exists(w_csv):  # WRITE_SIZE (its own pass: FETCH_SIZE and WRITE_SIZE do not fit one)
+        acc = defaultdict(lambda: [0.0, 0])
+        with open(w_csv) as f:
+            for row in csv.DictReader(f):
+                if row["Counter_Name"] != "WRITE_SIZE":
+                    continue
+                a = acc[short(row["Kernel_Name"])]
+                a[0] += float(row["Counter_Value"])
+                a[1] += 1
+        for k, (tot, n) in acc.items():
+            d = out["kernels"].setdefault(k, {})
+            d["write_size_kb_per_launch"] = tot / n  # KB as reported; no gfx950 calibration for writes
     sq_csv = os.path.join(src, "sq", "run_counter_collection.csv")
     if os.path.exists(sq_csv):  # occupancy / stall counters, per launch, with the kernel's resources
         acc = defaultdict(lambda: defaultdict(float))

@@ -17,6 +17,19 @@ from test_gpu_parity import NO_POD_AFFINITY
 pytestmark = pytest.mark.gpu
 
 
+class _variant:
+    """sweep_variant is process-wide: set it for a block, back to 0 after."""
+
+    def __init__(self, s, v):
+        self.s, self.v = s, v
+
+    def __enter__(self):
+        self.s.set_option("sweep_variant", self.v)
+
+    def __exit__(self, *a):
+        self.s.set_option("sweep_variant", 0)
+
+
 def _pending(c_path, oracle_mod):
     import kbhip
     enc = kbhip.EncodedSnapshot(c_path)
@@ -25,8 +38,11 @@ def _pending(c_path, oracle_mod):
     return [int(i) for i in np.nonzero(cls >= 0)[0]]
 
 
+@pytest.mark.parametrize("variant", [0, 4, 6])
 @pytest.mark.parametrize("seed", range(16))
-def test_sweep_scores_vs_oracle(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+def test_sweep_scores_vs_oracle(engine, oracle_mod, kbgen_mod, tmp_path, seed, variant):
+    """variant: option sweep_variant (0 one node per thread, 4 / 6 the
+    prefetching grid of k_score_sweep_gs)."""
     feats = NO_POD_AFFINITY if seed % 2 else None
     kw = {} if feats is None else {"features": feats}
     c = kbgen_mod.gen_random(7100 + seed, n_nodes=5 + seed % 9, n_jobs=4 + seed % 5, max_tasks=1 + seed % 5, **kw)
@@ -36,7 +52,7 @@ def test_sweep_scores_vs_oracle(engine, oracle_mod, kbgen_mod, tmp_path, seed):
     pend = _pending(p, oracle_mod)
     assert pend
     for actions in ("", "allocate"):
-        with engine.Session(p) as s:
+        with engine.Session(p) as s, _variant(s, variant):
             todo = pend
             if actions:
                 s.allocate()
@@ -98,3 +114,21 @@ def test_first_fit_any_tasks(engine, kbgen_mod, tmp_path, seed):
             exp = int(ok[0]) if ok.size else -1
             got = int(s.first_fit([pod])[0])
             assert got == exp, pod
+
+
+@pytest.mark.parametrize("n_nodes", [70_000, 300_000])
+def test_sweep_variants_agree_large(engine, kbgen_mod, tmp_path, n_nodes):
+    """At sizes where the prefetching grid walks several nodes per thread (and
+    the last walk is ragged): every kernel shape writes the same keys and the
+    same passing count as the one-node-per-thread grid."""
+    p = str(tmp_path / "big.kbs")
+    kbgen_mod.gen_c4(p, n_nodes=n_nodes, n_pending=2000, running_per_node=1)
+    pend = _pending(p, None)
+    with engine.Session(p) as s:
+        for pod in pend[::397][:5]:
+            ref = s.sweep_scores(pod, n_nodes)
+            assert ref[0] > 0
+            for v in (1, 2, 3, 4, 5, 6):
+                with _variant(s, v):
+                    got = s.sweep_scores(pod, n_nodes)
+                assert got[0] == ref[0] and np.array_equal(got[1], ref[1]), (pod, v)
