@@ -36,9 +36,9 @@ def main():
     ap.add_argument("--cache", default=os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench"))
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1 = time the hoisted CPU restatement on one session")
     ap.add_argument("--group", type=int, default=1,
-                    help="1 = the concurrent sessions form a lockstep what-if group (option rank_group): their "
-                         "allocate pops and reclaim / preempt rankings go out as multi-session launches; "
-                         "0 = every session launches alone")
+                    help="1 = option rank_group on the concurrent sessions: their allocate pops, per-task chunks "
+                         "and reclaim / preempt rankings go out as multi-session launches, each request at once "
+                         "with whatever other sessions' requests are pending; 0 = every session launches alone")
     ap.add_argument("--concurrent", type=int, default=8,
                     help="what-if sessions in flight (host threads); their node rankings share launches")
     args = ap.parse_args()
@@ -135,7 +135,7 @@ def one_session(buf, group, barrier=None):
     t0 = time.perf_counter()
     s = kbhip.Session(buf, device=0)
     if group and GROUP[0]:
-        s.set_option("rank_group", 1)
+        s.set_option("rank_group", GROUP[0])
     if barrier is not None:
         barrier.wait()
     kinds = []
@@ -155,9 +155,9 @@ def one_session(buf, group, barrier=None):
 
 def concurrent(args, bufs):
     """S what-if sessions in flight from S host threads (the engine releases the
-    GIL); their reclaim / preempt node rankings and their allocate pops are
-    issued in lockstep as shared multi-session launches (option rank_group,
-    kbhip_session.cpp StepBatcher)."""
+    GIL); with --group their reclaim / preempt node rankings, allocate pops
+    and per-task chunks go out as shared multi-session launches (option
+    rank_group, session/03_pop.inc StepBatcher)."""
     from concurrent.futures import ThreadPoolExecutor
     # the sessions of one wave of `concurrent` start together (a barrier after
     # their opens), as a what-if sweep over one cluster state would

@@ -97,7 +97,7 @@ typedef struct kbhip_stats {
     double alloc_device_s;  /* HIP-event span of kbhip_allocate's device work (first launch to idle) */
     int64_t unassigned_pops; /* job pops that stopped on a task with no node (allocate.go:187-189) */
     int64_t collectives;     /* node-array shards: cross-shard all-gathers + all-reduces issued */
-    int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if lockstep group ("rank_group") */
+    int64_t rank_requests;   /* reclaim / preempt node rankings served by the what-if batcher ("rank_group") */
     int64_t rank_batch_sum;  /* sum over those of the sessions in the launch that served it */
     int64_t pop_requests;    /* batched allocate pops served by the what-if batcher ("rank_group") */
     int64_t pop_batch_sum;   /* sum over those of the sessions in the launch that served it */
@@ -223,6 +223,18 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys);
  * (their sweep needs a min / max prepass per task). */
 int kbhip_time_sweeps(kb_session* s, const int32_t* task_ids, int32_t n, double* out_mean_us);
 
+/* Measurement entry (config C5): the preempt node ranking
+ * (PredicateFn + NodeOrderFn sweep + stable counting sort) of n what-if
+ * sessions on one device as ONE multi-session launch chain (blockIdx.y =
+ * session, each on its own node columns), session i for its pending task
+ * task_ids[i]; launched reps times (evict 0: back to back; 2: each behind a
+ * 512 MB cache-evicting read), descriptors copied to device memory (mapped 0)
+ * or read in place from pinned mapped host memory (1).  *out_us = device
+ * microseconds per chain (HIP events).  Classes of the one-pass counting sort
+ * only (score range < 256, no inter-pod terms), else KBHIP_EUNSUPPORTED. */
+int kbhip_time_rank_multi(kb_session* const* sessions, int32_t n, const int32_t* task_ids, int32_t reps,
+                          int32_t evict, int32_t mapped, double* out_us);
+
 /* Run the reclaim action (actions/reclaim/reclaim.go:41-196) / the preempt
  * action (actions/preempt/preempt.go:43-353) on the session's current state.
  * Output records in decision order: (pod, node, KBHIP_EVICTED) for every
@@ -317,12 +329,12 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * "rank_radix" = 1 orders reclaim / preempt walks with the wide-range radix
  * passes (four 8-bit counting passes over the score) instead of the one-pass
  * counting sort (tests);
- * "rank_group" = 1 makes this session one of a lockstep group of what-if
- * sessions run from concurrent host threads: while inside allocate /
- * backfill / reclaim / preempt, their allocate pops of placements 6 / 7, their
- * per-task chunks and their reclaim / preempt node rankings are issued in
- * steps, once every member has a request in, as shared multi-session launches
- * (blockIdx.y = session; kbhip_stats
+ * "rank_group" = 1 makes this session one of a group of what-if sessions
+ * run from concurrent host threads: their allocate pops of placements 6 / 7,
+ * their per-task chunks and their reclaim / preempt node rankings are issued
+ * as shared multi-session launches (blockIdx.y = session): each request is
+ * issued at once together with whatever other sessions' requests are pending
+ * (no session waits for another; kbhip_stats
  * rank_batch_sum / rank_requests, pop_batch_sum / pop_requests and
  * sweep_batch_sum / sweep_requests (per-task chunks: allocate's general path
  * and backfill first-fits, k_sweep_argmax_multi) = requests

@@ -399,18 +399,33 @@ hipError_t launch_rank_radix(const uint64_t* keys, int n, const uint32_t* count,
 // ---------------------------------------------------------------------------
 constexpr int kRankBuckets = 256;
 // blk / nblk: this block's node range and the number of blocks of the ranking
-__device__ __forceinline__ void rank_bucket(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
-                                            int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
-                                            uint32_t* count, int blk, int nblk) {
+__device__ __forceinline__ void rank_bucket(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                                            const PopCtrl* ctrl, int by_score, int shi, int nb, uint64_t* keys,
+                                            uint32_t* hist, uint32_t* count, int blk, int nblk) {
     __shared__ uint32_t s_h[kRankBuckets];
-    for (int i = threadIdx.x; i < nb; i += kBlock) s_h[i] = 0;
-    __syncthreads();
-    const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[0]);
-    const TaskClass c = t.classes[cls];
     const int n = blk * kBlock + threadIdx.x;
+    // a plain class's columns (SweepIn) are loaded first: their latency runs
+    // under the histogram's zeroing and the predicates' table reads
+    const bool plain = by_score && !c.aff && c.ipa_n == 0;
+    SweepIn pre{};
+    if (plain && n < nc.n) pre = sweep_in(nc, n);
+    for (int i = threadIdx.x; i < nb; i += kBlock) s_h[i] = 0;
     uint64_t k = 0;
     if (n < nc.n) {
-        if (by_score) {
+        if (plain) {
+            uint64_t pw[4] = {0, 0, 0, 0};
+            if (c.has_ports)
+                for (int w = 0; w < 4; ++w) if (w < port_win(c, nc)) pw[w] = nc.ports[port_at(c, nc, w, n)];
+            Row r{};
+            r.acpu = pre.acpu; r.amem = pre.amem; r.nzc = pre.nzc; r.nzm = pre.nzm;
+            r.pods = pre.pods; r.maxtasks = pre.maxtasks;
+            const bool st = static_pred_f(cf, c, t, nc, n, pre.fl);
+            const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
+            int32_t s = 0;
+            bool passed = false;
+            (void)dyn_key(cf, c, t, nc, r, pw, n, st, na, &s, &passed);  // passed and s read no fit column
+            k = passed ? pack_key(s, n + nc.base, 0) : 0;
+        } else if (by_score) {
             int32_t s = 0;
             bool passed = false;
             (void)eval_node_aff(cf, c, t, nc, n, ctrl->ipa_lo[0], ctrl->ipa_hi[0], ctrl->fallback, &s, &passed);
@@ -424,7 +439,19 @@ __device__ __forceinline__ void rank_bucket(const Conf& cf, const NodeCols& nc, 
             k = 0;
         }
         keys[n] = k;
-        if (k) atomicAdd(&s_h[b], 1u);
+    }
+    __syncthreads();  // s_h zeroed
+    // the histogram: one LDS add per distinct bucket of the wave (a class's
+    // nodes fall into few score buckets: one add per node serialised up to
+    // 64 adds on one LDS word)
+    {
+        const int bb = k ? (by_score ? shi - key_score(k) : 0) : -1;
+        for (uint64_t todo = __ballot(bb >= 0); todo;) {
+            const int bv = __builtin_amdgcn_readlane(bb, __ffsll((unsigned long long)todo) - 1);
+            const uint64_t m = __ballot(bb == bv);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&s_h[bv], (uint32_t)__popcll(m));
+            todo &= ~m;
+        }
     }
     __syncthreads();
     uint32_t tot = 0;
@@ -483,10 +510,10 @@ __device__ __forceinline__ void rank_scatter(const NodeCols& nc, const uint64_t*
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, DevTables t, const PopCtrl* ctrl,
-                                                        int by_score, int shi, int nb, uint64_t* keys, uint32_t* hist,
-                                                        uint32_t* count) {
-    rank_bucket(cf, nc, t, ctrl, by_score, shi, nb, keys, hist, count, blockIdx.x, gridDim.x);
+__global__ __launch_bounds__(kBlock) void k_rank_bucket(Conf cf, NodeCols nc, DevTables t, TaskClass c,
+                                                        const PopCtrl* ctrl, int by_score, int shi, int nb,
+                                                        uint64_t* keys, uint32_t* hist, uint32_t* count) {
+    rank_bucket(cf, nc, t, c, ctrl, by_score, shi, nb, keys, hist, count, blockIdx.x, gridDim.x);
 }
 __global__ __launch_bounds__(1024) void k_rank_scan(uint32_t* v, int n) { rank_scan(v, n); }
 __global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, const uint64_t* keys, const uint32_t* offs,
@@ -495,15 +522,15 @@ __global__ __launch_bounds__(kBlock) void k_rank_scatter(const NodeCols nc, cons
     rank_scatter(nc, keys, offs, by_score, shi, sorted, blockIdx.x, gridDim.x);
 }
 
-hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
-                              int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
-                              uint32_t* count, hipStream_t st) {
+hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                              const PopCtrl* ctrl, int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist,
+                              uint64_t* sorted, uint32_t* count, hipStream_t st) {
     const int nb = by_score ? shi - slo + 1 : 1;
     if (nb < 1 || nb > kRankBuckets) return hipErrorInvalidValue;
     const int nblk = (nc.n + kBlock - 1) / kBlock;
     if (nblk < 1) return hipSuccess;
-    hipLaunchKernelGGL(k_rank_bucket, dim3(nblk), dim3(kBlock), 0, st, cf, nc, t, ctrl, by_score, shi, nb, keys, hist,
-                       count);
+    hipLaunchKernelGGL(k_rank_bucket, dim3(nblk), dim3(kBlock), 0, st, cf, nc, t, c, ctrl, by_score, shi, nb, keys,
+                       hist, count);
     hipLaunchKernelGGL(k_rank_scan, dim3(1), dim3(1024), 0, st, hist, nb * nblk);
     hipLaunchKernelGGL(k_rank_scatter, dim3(nblk), dim3(kBlock), 0, st, nc, (const uint64_t*)keys,
                        (const uint32_t*)hist, by_score, shi, nb, sorted);
@@ -519,7 +546,7 @@ hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTable
 __global__ __launch_bounds__(kBlock) void k_rank_bucket_multi(const RankDesc* d) {
     const RankDesc& q = d[blockIdx.y];
     if ((int)blockIdx.x >= q.nblk) return;  // uniform
-    rank_bucket(q.cf, q.nc, q.t, q.ctrl, q.by_score, q.shi, q.nb, q.keys, q.hist, q.count, blockIdx.x, q.nblk);
+    rank_bucket(q.cf, q.nc, q.t, q.c, q.ctrl, q.by_score, q.shi, q.nb, q.keys, q.hist, q.count, blockIdx.x, q.nblk);
 }
 __global__ __launch_bounds__(1024) void k_rank_scan_multi(const RankDesc* d) {
     const RankDesc& q = d[blockIdx.x];
@@ -531,12 +558,13 @@ __global__ __launch_bounds__(kBlock) void k_rank_scatter_multi(const RankDesc* d
     rank_scatter(q.nc, q.keys, q.hist, q.by_score, q.shi, q.sorted, blockIdx.x, q.nblk);
 }
 
-hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
-                          int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
-                          uint32_t* count) {
+hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                          const PopCtrl* ctrl, int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist,
+                          uint64_t* sorted, uint32_t* count) {
     const int nb = by_score ? shi - slo + 1 : 1;
     if (nb < 1 || nb > kRankBuckets) return hipErrorInvalidValue;
-    *q = RankDesc{cf, nc, t, ctrl, by_score ? 1 : 0, shi, nb, (nc.n + kBlock - 1) / kBlock, keys, hist, sorted, count};
+    *q = RankDesc{cf, nc, t, c, ctrl, by_score ? 1 : 0, shi, nb, (nc.n + kBlock - 1) / kBlock, keys, hist, sorted,
+                  count};
     return hipSuccess;
 }
 

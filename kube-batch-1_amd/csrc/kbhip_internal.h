@@ -62,15 +62,16 @@ hipError_t launch_rank_radix(const uint64_t* keys, int n, const uint32_t* count,
 // score range [slo, shi] of at most 256 values; hipErrorInvalidValue beyond):
 // keys, sorted (descending key order), *count += passing nodes; hist holds
 // rank_hist_words(n) words of scratch.
-hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
-                              int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
-                              uint32_t* count, hipStream_t st);
+hipError_t launch_rank_sorted(const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                              const PopCtrl* ctrl, int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist,
+                              uint64_t* sorted, uint32_t* count, hipStream_t st);
 size_t rank_hist_words(int n_nodes);
 // One session's ranking request in a batched launch (what-if sessions).
 struct RankDesc {
     Conf cf;
     NodeCols nc;
     DevTables t;
+    TaskClass c;  // the request's class (ctrl->cls[0]), here so a block needs no load chain to it
     const PopCtrl* ctrl;
     int by_score, shi, nb, nblk;
     uint64_t* keys;
@@ -78,9 +79,9 @@ struct RankDesc {
     uint64_t* sorted;
     uint32_t* count;
 };
-hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const PopCtrl* ctrl,
-                          int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist, uint64_t* sorted,
-                          uint32_t* count);
+hipError_t fill_rank_desc(RankDesc* q, const Conf& cf, const NodeCols& nc, const DevTables& t, const TaskClass& c,
+                          const PopCtrl* ctrl, int by_score, int slo, int shi, uint64_t* keys, uint32_t* hist,
+                          uint64_t* sorted, uint32_t* count);
 hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_nblk, hipStream_t st);
 // Count-table deltas (pod (anti-)affinity): idx >= 0 aff_cnt, < 0 aff_scalar[-1 - idx]; distinct indices.
 hipError_t launch_tab_add(const DevTables& t, const int32_t* idx, const int32_t* delta, int n, hipStream_t st);

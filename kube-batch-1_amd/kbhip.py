@@ -30,7 +30,7 @@ EXPORTS = ("kbhip_device_count", "kbhip_session_open", "kbhip_session_open_file"
            "kbhip_gang_unschedulable", "kbhip_reclaim", "kbhip_preempt", "kbhip_session_carry",
            "kbhip_first_fit", "kbhip_sweep_scores", "kbhip_shard_connect_host_gather",
            "kbhip_session_carry_events", "kbhip_shard_connect_mailbox", "kbhip_shard_mailbox_fits", "kbhip_place_job_submit",
-           "kbhip_place_job_wait", "kbhip_place_job_cancel", "kbhip_time_sweeps",
+           "kbhip_place_job_wait", "kbhip_place_job_cancel", "kbhip_time_sweeps", "kbhip_time_rank_multi",
            "kbhip_session_carry_snapshot")
 
 RED_MAX_U64, RED_MIN_I64, RED_MAX_I64, RED_SUM_I64 = 0, 1, 2, 3
@@ -99,6 +99,7 @@ def lib() -> ctypes.CDLL:
         L.kbhip_first_fit.argtypes = [vp, vp, i32, vp]
         L.kbhip_sweep_scores.argtypes = [vp, i32, vp]
         L.kbhip_time_sweeps.argtypes = [vp, vp, i32, vp]
+        L.kbhip_time_rank_multi.argtypes = [vp, i32, vp, i32, i32, i32, vp]
         L.kbhip_reclaim.argtypes = [vp, vp, vp, vp, i64]
         L.kbhip_session_carry.argtypes = [vp, vp]
         L.kbhip_session_carry_events.argtypes = [vp, vp, vp, i64, vp]
@@ -417,6 +418,19 @@ class EncodedSnapshot:
 
     def __exit__(self, *a):
         self.close()
+
+
+def time_rank_multi(sessions, task_ids, reps: int = 16, evict: int = 0, mapped: int = 0) -> float:
+    """kbhip_time_rank_multi: device microseconds of one multi-session preempt
+    ranking launch chain over the given sessions (session i for its pending
+    task task_ids[i])."""
+    hs = (ctypes.c_void_p * len(sessions))(*[s._h for s in sessions])
+    ids = np.ascontiguousarray(task_ids, dtype=np.int32)
+    if ids.size != len(sessions):
+        raise ValueError("one task id per session")
+    out = np.zeros(1, np.float64)
+    _check(lib().kbhip_time_rank_multi(hs, len(sessions), _p(ids), reps, evict, mapped, _p(out)))
+    return float(out[0])
 
 
 def shard_range(n_nodes: int, rank: int, world: int) -> Tuple[int, int]:
