@@ -157,7 +157,7 @@ def concurrent(args, bufs):
     """S what-if sessions in flight from S host threads (the engine releases the
     GIL); with --group their reclaim / preempt node rankings, allocate pops
     and per-task chunks go out as shared multi-session launches (option
-    rank_group, session/03_pop.inc StepBatcher)."""
+    rank_group, session/session.h StepBatcher)."""
     from concurrent.futures import ThreadPoolExecutor
     # the sessions of one wave of `concurrent` start together (a barrier after
     # their opens), as a what-if sweep over one cluster state would

@@ -54,7 +54,7 @@ struct AffProgram {
 
 struct AffPod {  // what the model needs to know about each pod
     int ns = -1;              // namespace id (index into ns_names)
-    int status = 0;           // St code of kbhip_session.cpp
+    int status = 0;           // St code of session/session.h
     bool session_job = false; // belongs to a job of the session
     bool target = false;      // AllocatedStatuses task of a session job, on a node
     bool pending = false;     // pending task of a session job (gets a program)

@@ -1,5 +1,5 @@
 // kbhip_engine.h — the persistent pop engine (kbhip_engine.hip): memory
-// layout shared by the host driver (kbhip_session.cpp) and the kernel.
+// layout shared by the host driver (session/03_pop.cpp) and the kernels.
 //
 // One resident grid serves a run of batched job pops (allocate.go:110-185 for
 // a gang's chunk of one task class) without a kernel launch

@@ -256,7 +256,7 @@ __global__ __launch_bounds__(64) void k_node_op(NodeCols nc, DevTables t, int op
 }
 
 // Count-table changes queued on the host (evictions / unevicts of predicate
-// targets, kbhip_session.cpp flush_tables): idx >= 0 -> aff_cnt[idx],
+// targets, session/03_pop.cpp flush_tables): idx >= 0 -> aff_cnt[idx],
 // idx < 0 -> aff_scalar[-1 - idx]; the indices are distinct.
 __global__ __launch_bounds__(kBlock) void k_tab_add(DevTables t, const int32_t* idx, const int32_t* delta, int n) {
     const int i = blockIdx.x * kBlock + threadIdx.x;

@@ -346,7 +346,7 @@ struct PopDescs {
 };
 static_assert(sizeof(PopDescs) <= 4000, "multi-session pop descriptors exceed the kernel argument space");
 
-// Placement 7 with per-domain candidates (TaskClass::dd_space, kbhip_session.cpp
+// Placement 7 with per-domain candidates (TaskClass::dd_space, session/session.h
 // dedup_space): of the block's nodes of one domain of the space only the one
 // with the largest key can win (keys are unique: they carry the node index).
 // Every block adds its domain maxima to the session's dd_max table, from which

@@ -1,6 +1,7 @@
-// kbhip_session.cpp, part 2 of 7 (02_open.inc): snapshot encoder and session open: KBS1 decode, host model, device columns and tables.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 02: session open (KBS1 decode, dictionary encoding, task classes, upload to HBM)
+#include "session.h"
+
+namespace kbhip {
 
 // ---------------------------------------------------------------------------
 // encoder
@@ -35,7 +36,7 @@ struct Encoder {
 
 };
 
-static void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
+void fail_unsupported(const string& m) { throw Error(KBHIP_EUNSUPPORTED, m); }
 
 // Host-port ids of pod i: run i of the session's port CSR, compared by value.
 struct PortRun {
@@ -57,7 +58,7 @@ struct PortRuns {
 // of a batched-path class is mult x (w_lr lr + w_bra bra + w_na na) with
 // lr, bra in [0, 10] and na between the sums of its negative / positive
 // preferred-term weights; it fits when (range + 1) < 2^(31 - index bits).
-static void class_key_format(const Session& S, const TaskClass& c, const vector<Term>& terms, int N, KeyFormat* kf_out,
+void class_key_format(const Session& S, const TaskClass& c, const vector<Term>& terms, int N, KeyFormat* kf_out,
                              std::pair<int64_t, int64_t>* range_out) {
     int ibits = 1;  // keys carry global node indices (shards too)
     while (ibits < 30 && ((int64_t)1 << ibits) < (int64_t)N) ++ibits;
@@ -103,7 +104,7 @@ static uint64_t fnv(uint64_t h, const void* p, size_t n) {
     return h;
 }
 static uint64_t fnv_str(uint64_t h, const char* z) { return fnv(h, z, std::strlen(z) + 1); }
-static uint64_t conf_digest(const kbs::Snapshot& s) {
+uint64_t conf_digest(const kbs::Snapshot& s) {
     uint64_t h = 1469598103934665603ULL;
     for (const char* n : {"conf_plugin_name", "conf_arg_key", "conf_arg_val", "conf_actions"})
         for (int32_t o : s.vec<int32_t>(n)) h = fnv_str(h, s.str(o));
@@ -114,7 +115,7 @@ static uint64_t conf_digest(const kbs::Snapshot& s) {
     }
     return h;
 }
-static uint64_t node_spec_digest(const kbs::Snapshot& s) {
+uint64_t node_spec_digest(const kbs::Snapshot& s) {
     uint64_t h = 1469598103934665603ULL;
     const size_t N = s.rows("n_name");
     auto loff = s.offs("n_label_off", N), toff = s.offs("n_taint_off", N);
@@ -133,8 +134,8 @@ static uint64_t node_spec_digest(const kbs::Snapshot& s) {
     return h;
 }
 
-static void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
-                         int world = 1) {
+void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only, int rank,
+                         int world) {
     if (world < 1 || world > 16 || rank < 0 || rank >= world) throw Error(KBHIP_EINVAL, "bad shard rank / world (1..16)");
     S.rank = rank;
     S.world = world;
@@ -1188,3 +1189,4 @@ static void open_session(Session& S, const kbs::Snapshot& s, int device, bool en
     S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+}  // namespace kbhip

@@ -1,6 +1,7 @@
-// kbhip_session.cpp, part 3 of 7 (03_pop.inc): device pops: shard exchange, what-if batching, the persistent engine's host driver, batched launches and their results, the per-task path, the asynchronous per-pop ABI.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 03: the per-pop device driver (batched pops, the persistent engine, tickets)
+#include "session.h"
+
+namespace kbhip {
 
 // ---------------------------------------------------------------------------
 // cross-shard exchange of n 8-byte values in device memory:
@@ -9,7 +10,7 @@
 // ---------------------------------------------------------------------------
 // KBHIP_TRACE_SHARD=1: every collective of a shard session on stderr (diagnostic)
 static const bool g_trace_shard = std::getenv("KBHIP_TRACE_SHARD") != nullptr;
-static void exchange(Session& S, void* dev, int op, int n = 1) {
+void exchange(Session& S, void* dev, int op, int n) {
     if (S.world == 1) return;
     S.stats.collectives++;
     if (g_trace_shard)
@@ -32,7 +33,7 @@ static void exchange(Session& S, void* dev, int op, int n = 1) {
 }
 
 // The FitDelta counts of one task summed over the shards (in place; one GPU: nothing).
-static void fit_allreduce(Session& S, int32_t* fit4) {
+void fit_allreduce(Session& S, int32_t* fit4) {
     if (S.world == 1) return;
     int64_t* d = (int64_t*)S.d_fit4 + 2;  // after the device counters (int32[4])
     int64_t h[4] = {fit4[0], fit4[1], fit4[2], fit4[3]};
@@ -72,7 +73,7 @@ static void shard_gather(Session& S) {
 // [cross-shard max of the key + commit].
 // defer_visits: the walk's GetAccessibleResource mutation as a grid-wide second
 // kernel (worth it whenever some node may carry Backfilled resources).
-static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
+void sweep_task(Session& S, int i, int cls, bool defer_visits) {
     if (S.classes[cls].ipa_n > 0) {
         HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
         exchange(S, &S.d_ctrl->ipa_lo[i], KBHIP_RED_MIN_I64);
@@ -86,238 +87,6 @@ static void sweep_task(Session& S, int i, int cls, bool defer_visits = false) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// ---------------------------------------------------------------------------
-// What-if sessions batched per launch:
-// sessions opened with option "rank_group", each driven by its own host
-// thread, send their device requests — the allocate pops of sessions with
-// Backfilled nodes or of pod-affinity classes (placements 6 / 7: one pop in
-// flight per session), per-task chunks, and the reclaim / preempt node
-// rankings — to this batcher, which serves every request pending in a lane as
-// ONE multi-session launch per kind and device (k_pop_batch_multi, task k of
-// every chunk in k_sweep_argmax_multi, the k_rank_*_multi sorts; blockIdx.y =
-// session).  Pops are ordered by events after each session's earlier device
-// work and before its later work; their results are the sessions' own
-// granules.  Rankings complete before their requesters resume.  Combining:
-// a request is issued at once with whatever else is pending in its lane;
-// while a step is being launched new requests collect, and the first of
-// their requesters to find the lane free issues them all — no session waits
-// for another's host work.  (r03-r05 issued lockstep steps, once every member
-// inside an action of the kind had a request in: 7.0-7.4 sessions/s at 16 in
-// flight against 9.5-11.3 ungrouped and 9.6 combining, profiles/r06c_*;
-// removed.)
-// ---------------------------------------------------------------------------
-struct StepBatcher {
-    static StepBatcher& get() {
-        static StepBatcher b;
-        return b;
-    }
-    // kSweep requests (per-task chunks) go in the pop lane: the same sessions
-    // (sessions inside allocate or backfill) send either
-    enum Kind { kPop = 0, kRank = 1, kSweep = 2 };
-    static int lane_of(int kind) { return kind == kRank ? 1 : 0; }
-    struct Req {
-        int kind = kPop;
-        int device = 0;
-        PopReq pop{};
-        SweepReq sweep{};
-        hipEvent_t before = nullptr;  // pop: recorded on the requester's stream (its earlier work)
-        hipEvent_t after = nullptr;   // pop: recorded after the launch that served it
-        RankDesc rank{};
-        hipStream_t st = nullptr;     // rank: the requester's stream
-        std::atomic<bool> done{false};
-        hipError_t err = hipSuccess;
-        int batch = 0;                // requests of its kind in the launch that served it
-        std::chrono::steady_clock::time_point t0;  // when it was submitted (linger)
-    };
-    std::mutex mu;
-    std::condition_variable cv;  // a step is out: requests done, the lane free
-    // One lane per request lane kind: pops and chunks in one, rankings in the
-    // other (a ranking waits for its launch; pops and chunks do not).
-    struct Lane {
-        vector<Req*> pending;
-        bool busy = false;
-    };
-    Lane lane[2];
-    int64_t steps = 0;
-    // Test knob (option "group_linger_us", process-wide; 0 = off): a lane waits
-    // until every grouped session has a request in it, or its oldest request
-    // is that old, so that concurrent sessions' requests meet deterministically.
-    std::atomic<int64_t> linger_us{0};
-    std::atomic<int> sessions{0};  // live sessions with rank_group set
-    static constexpr int kStreams = 4;
-    struct Dev {
-        hipStream_t sts[kStreams] = {};  // pop / chunk steps, round robin (a session has one request in
-        int rr = 0;                      // flight, so consecutive steps need no order between them)
-        hipStream_t st = nullptr;        // this step's
-        vector<hipEvent_t> ring;
-        size_t next = 0;
-        RankDesc* h_desc = nullptr;  // pinned: the step's ranking descriptors, copied to d_desc
-        RankDesc* d_desc = nullptr;  // device memory (kernels reading descriptors from mapped host memory
-                                     // measured 1.6x slower at 64 sessions: profiles/r06m_c5_multi.jsonl)
-        size_t cap_bytes = 0, n_cap = 0;
-    };
-    std::map<int, Dev> dev;
-
-    // The requester issues at once if the lane is free, else it sleeps until
-    // the current step is out and then one of the waiting requesters issues
-    // what has collected.  (Spinning requesters — r03-r05 — took the host
-    // cores the other sessions' host work needed: 16 sessions in flight are
-    // host-bound.)
-    void submit(Req& r) {
-        const int l = lane_of(r.kind);
-        r.t0 = std::chrono::steady_clock::now();
-        std::unique_lock<std::mutex> lk(mu);
-        lane[l].pending.push_back(&r);
-        while (!r.done.load(std::memory_order_acquire)) {
-            if (ready(l)) {
-                issue(lk, l);
-                continue;
-            }
-            if (linger_us.load(std::memory_order_relaxed) > 0) cv.wait_for(lk, std::chrono::microseconds(100));
-            else cv.wait(lk);
-        }
-    }
-
-  private:
-    bool ready(int l) const {
-        const Lane& L = lane[l];
-        if (L.busy || L.pending.empty()) return false;
-        const int64_t lg = linger_us.load(std::memory_order_relaxed);
-        if (lg <= 0 || (int)L.pending.size() >= sessions.load(std::memory_order_relaxed)) return true;
-        return std::chrono::steady_clock::now() - L.pending.front()->t0 >= std::chrono::microseconds(lg);
-    }
-    // One step of one lane: every pending request of that lane (the lock is
-    // released while launching).
-    void issue(std::unique_lock<std::mutex>& lk, int l) {
-        Lane& L = lane[l];
-        L.busy = true;
-        vector<Req*> batch;
-        batch.swap(L.pending);
-        ++steps;
-        // each device's streams and events, created under the lock (both lanes may issue at once)
-        hipError_t e0 = hipSuccess;
-        for (Req* q : batch)
-            if (e0 == hipSuccess && (e0 = hipSetDevice(q->device)) == hipSuccess) (void)device(q->device, &e0);
-        lk.unlock();
-        std::map<int, vector<Req*>> by;  // device -> requests
-        for (Req* q : batch) by[q->device].push_back(q);
-        for (auto& kv : by) {
-            if (e0 != hipSuccess) {
-                for (Req* q : kv.second) q->err = e0;
-                continue;
-            }
-            if (l == 1) {
-                const hipError_t e = launch_ranks(kv.first, kv.second);
-                for (Req* q : kv.second) { q->err = e; q->batch = (int)kv.second.size(); }
-                continue;
-            }
-            vector<Req*> pops, sweeps;
-            for (Req* q : kv.second) (q->kind == kSweep ? sweeps : pops).push_back(q);
-            int pl = 0, sl = 0, sw_tasks = 0;
-            hipError_t e = hipSetDevice(kv.first);
-            if (e == hipSuccess) {
-                Dev& D = device(kv.first, &e);
-                if (e == hipSuccess) D.st = D.sts[D.rr++ % kStreams];  // this step's stream
-            }
-            if (e == hipSuccess && !pops.empty()) e = launch_pops(kv.first, pops, &pl);
-            if (e == hipSuccess && !sweeps.empty()) e = launch_sweeps(kv.first, sweeps, &sl, &sw_tasks);
-            if (e == hipSuccess) e = record_after(kv.first, kv.second);
-            for (Req* q : pops) q->batch = (int)((pops.size() + std::max(pl, 1) - 1) / std::max(pl, 1));
-            for (Req* q : sweeps) q->batch = (int)((sw_tasks + std::max(sl, 1) - 1) / std::max(sl, 1));
-            for (Req* q : kv.second) q->err = e;
-        }
-        lk.lock();
-        L.busy = false;
-        // q may go away after this; requests that came in meanwhile are issued by their requesters
-        for (Req* q : batch) q->done.store(true, std::memory_order_release);
-        cv.notify_all();
-    }
-    Dev& device(int d, hipError_t* e) {
-        Dev& D = dev[d];
-        *e = hipSuccess;
-        if (!D.st) {
-            for (auto& s : D.sts)
-                if ((*e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return D;
-            D.st = D.sts[0];
-            D.ring.assign(64, nullptr);
-            for (auto& ev : D.ring)
-                if ((*e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return D;
-        }
-        return D;
-    }
-    hipError_t launch_pops(int d, const vector<Req*>& b, int* launches) {
-        hipError_t e = hipSetDevice(d);
-        if (e != hipSuccess) return e;
-        Dev& D = device(d, &e);
-        if (e != hipSuccess) return e;
-        vector<PopReq> qs;
-        for (Req* q : b) {
-            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
-            qs.push_back(q->pop);
-        }
-        int nl = 0;
-        if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), D.st, &nl)) != hipSuccess) return e;
-        *launches = std::max(nl, 1);
-        return hipSuccess;
-    }
-    // Task k of every chunk for k = 0, 1, ...: each session's tasks in order on
-    // the one stream, the sessions side by side (*tasks: session-tasks swept).
-    hipError_t launch_sweeps(int d, const vector<Req*>& b, int* launches, int* tasks) {
-        hipError_t e = hipSetDevice(d);
-        if (e != hipSuccess) return e;
-        Dev& D = device(d, &e);
-        if (e != hipSuccess) return e;
-        vector<SweepReq> qs;
-        int max_m = 0;
-        for (Req* q : b) {
-            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
-            qs.push_back(q->sweep);
-            max_m = std::max(max_m, q->sweep.m);
-            *tasks += q->sweep.m;
-        }
-        for (int k = 0; k < max_m; ++k)
-            if ((e = launch_sweep_multi(qs.data(), (int)qs.size(), k, D.st, launches)) != hipSuccess) return e;
-        return hipSuccess;
-    }
-    // Every request of the step follows its launches on the requester's stream.
-    hipError_t record_after(int d, const vector<Req*>& b) {
-        hipError_t e = hipSetDevice(d);
-        if (e != hipSuccess) return e;
-        Dev& D = device(d, &e);
-        if (e != hipSuccess) return e;
-        hipEvent_t ev = D.ring[D.next++ % D.ring.size()];
-        if ((e = hipEventRecord(ev, D.st)) != hipSuccess) return e;
-        for (Req* q : b) q->after = ev;
-        return hipSuccess;
-    }
-    hipError_t launch_ranks(int d, const vector<Req*>& b) {
-        hipError_t e = hipSetDevice(d);
-        if (e != hipSuccess) return e;
-        Dev& D = device(d, &e);
-        if (e != hipSuccess) return e;
-        if (b.size() > D.n_cap) {
-            if (D.h_desc) MemPool::get().give(MemPool::kPinned, D.h_desc, D.cap_bytes, d);
-            if (D.d_desc && (e = hipFree(D.d_desc)) != hipSuccess) return e;
-            D.h_desc = nullptr;
-            D.d_desc = nullptr;
-            D.n_cap = std::max<size_t>(64, b.size());
-            D.h_desc = (RankDesc*)MemPool::get().take(MemPool::kPinned, D.n_cap * sizeof(RankDesc), &D.cap_bytes);
-            if ((e = hipMalloc((void**)&D.d_desc, D.n_cap * sizeof(RankDesc))) != hipSuccess) return e;
-        }
-        int max_nblk = 1;
-        for (size_t i = 0; i < b.size(); ++i) {
-            D.h_desc[i] = b[i]->rank;
-            max_nblk = std::max(max_nblk, b[i]->rank.nblk);
-        }
-        hipStream_t st = b[0]->st;  // a stream of this device; every requester's inputs are in place
-        if ((e = hipMemcpyAsync(D.d_desc, D.h_desc, b.size() * sizeof(RankDesc), hipMemcpyHostToDevice, st)) !=
-            hipSuccess)
-            return e;
-        if ((e = launch_rank_sorted_multi(D.d_desc, (int)b.size(), max_nblk, st)) != hipSuccess) return e;
-        return hipStreamSynchronize(st);  // (h_desc is reused by the next step)
-    }
-};
 
 // The sweeps of a per-task chunk (tasks 0 .. m-1 of the control block): one
 // k_sweep_argmax launch per task, or, for a what-if session of the batched
@@ -325,7 +94,7 @@ struct StepBatcher {
 // sessions' pending chunks (k_sweep_argmax_multi: task k of every chunk in one launch).
 // Classes with inter-pod priority terms (their k_ipa_minmax prepass) and
 // debug-key sessions keep the per-task launches.
-static void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task = false) {
+void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task) {
     S.stats.pertask_sweeps += m;
     bool group = S.rank_group && S.world == 1 && !S.d_dbg && !per_task;
     for (int i = 0; i < m && group; ++i) group = S.classes[cls[i]].ipa_n == 0;
@@ -638,14 +407,14 @@ static void ov_drain(Session& S) {
 
 // Wait until no batched pop can still run (before device work that is not a
 // batched pop, which the overlap chain does not order).
-static void ov_quiesce(Session& S) { ov_drain(S); }
+void ov_quiesce(Session& S) { ov_drain(S); }
 
 // The device-side form of ov_quiesce for a non-overlapped batched pop on the
 // session stream (placement 7): that stream waits for the end of every
 // overlap stream's work, without the host waiting.  Row messages of earlier
 // pops go stale as after a drain (the pop writes rows outside their
 // candidate lists); the overlapped pops after it wait for it (ev_nonov).
-static void ov_fence(Session& S) {
+void ov_fence(Session& S) {
     S.msg_from = S.ov_seq + 1;
     if (!S.ov_pending) return;
     for (int k = 1; k <= S.overlap; ++k) {
@@ -668,11 +437,11 @@ static void ev_harvest(Session& S, int k) {
     S.timed_n++;
     S.ev_used[k] = false;
 }
-static void ev_harvest_all(Session& S) {
+void ev_harvest_all(Session& S) {
     for (int k = 0; k < Session::kEvRing; ++k) ev_harvest(S, k);
 }
 
-static bool batchable(const Session& S, int cls) {
+bool batchable(const Session& S, int cls) {
     const TaskClass& c = S.classes[cls];
     // Backfilled nodes (some Idle grows on each walk visit): placement 6, one GPU only
     const bool bf_ok = !S.any_bf || (S.world == 1 && S.bf_batch);
@@ -683,7 +452,7 @@ static bool batchable(const Session& S, int cls) {
 }
 
 // The next result slot (pinned, mapped PopOutHost) and its granules' tag.
-static int take_slot(Session& S, uint32_t* epoch) {
+int take_slot(Session& S, uint32_t* epoch) {
     const int slot = S.next_slot;
     S.next_slot = (S.next_slot + 1) % Session::kSlots;
     uint32_t& ep = S.slot_epoch[slot];
@@ -697,7 +466,7 @@ static int take_slot(Session& S, uint32_t* epoch) {
 
 // The per-task path's chunk: control block set up on the device (k_ctrl_init,
 // no copy), results as tagged granules in result slot `slot`.
-static void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_avail, int gang, int mode, int slot,
+void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_avail, int gang, int mode, int slot,
                        uint32_t epoch) {
     CtrlInit ci{};
     ci.ready_count = ready;
@@ -716,7 +485,7 @@ static void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_ava
 // Poll the per-task granules of a chunk (written by commit_task): results up
 // to the task whose granule carries the chunk's stop; fit4 (optional) gets
 // that task's walk FitDelta counts when it found no node.
-static void collect_tasks(Session& S, int slot, uint32_t epoch, int m, int* n_done, int* stop, int32_t* node,
+void collect_tasks(Session& S, int slot, uint32_t epoch, int m, int* n_done, int* stop, int32_t* node,
                           int32_t* kind, int32_t* fit4) {
     const PopOutHost& o = S.h_out[slot];
     auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
@@ -753,7 +522,7 @@ static void collect_tasks(Session& S, int slot, uint32_t epoch, int m, int* n_do
     }
 }
 
-static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
+BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count) {
     BatchLaunch L;
     L.slot = take_slot(S, &L.epoch);
     L.cls = cls;
@@ -902,7 +671,7 @@ static BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int
 
 // Wait for a batched launch's self-tagged result granules (each one 8-byte
 // store on the device) and decode them.
-static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, int* stop_out, int32_t* res_node,
+void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, int* stop_out, int32_t* res_node,
                             int32_t* res_kind) {
     const PopOutHost& o = S.h_out[L.slot];
     auto tag = [](uint64_t g) { return (uint32_t)(g >> 48); };
@@ -1009,7 +778,7 @@ static void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, i
 // A session-placed pod (its Spec.NodeName is still "") arrives on / leaves
 // node n: the inter-pod priority's fallback node is the lowest such node
 // (nodeorder.go:78-93).
-static void sess_placed(Session& S, int n, int d) {
+void sess_placed(Session& S, int n, int d) {
     if (S.sess_cnt.empty()) S.sess_cnt.assign(S.n_total, 0);  // global node indices (shards too)
     S.sess_cnt[n] += d;
     if (d > 0 && (S.fallback < 0 || n < S.fallback)) S.fallback = n;
@@ -1023,7 +792,7 @@ static void sess_placed(Session& S, int n, int d) {
 // Count-table changes of a predicate target leaving / re-entering the target
 // set (eviction / unevict, AffinityModel::target_updates), queued on the host
 // and applied before the next device read of the tables (flush_tables).
-static void queue_target(Session& S, int pi, int sign) {
+void queue_target(Session& S, int pi, int sign) {
     if (!S.aff || !S.aff->active) return;
     const HPod& p = S.pods[pi];
     if (p.node < 0) return;
@@ -1039,7 +808,7 @@ static void queue_target(Session& S, int pi, int sign) {
         }
     }
 }
-static void flush_tables(Session& S) {
+void flush_tables(Session& S) {
     if (S.tab_delta.empty()) return;
     vector<int32_t> idx, val;
     for (auto& kv : S.tab_delta)
@@ -1056,7 +825,7 @@ static void flush_tables(Session& S) {
 
 // Host mirror of the device commits of consumed tasks (NodeInfo.Used, the
 // fallback node of nodeorder.go:78-93) + the caller's output arrays.
-static void apply_results(Session& S, const int32_t* ids, int n, const int32_t* res_node, const int32_t* res_kind,
+void apply_results(Session& S, const int32_t* ids, int n, const int32_t* res_node, const int32_t* res_kind,
                           int32_t* out_node, uint8_t* out_kind) {
     for (int i = 0; i < n; ++i) {
         out_node[i] = res_node[i];
@@ -1079,8 +848,7 @@ static void check_task_ids(const Session& S, const int32_t* ids, int n) {
             throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
 }
 
-constexpr uint8_t kBfBackoff = 4;  // pops of a class sent to the general path after a placement-6 miss
-static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
+int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
                      int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop) {
     int done = 0, stop = KBHIP_STOP_ALL;
     check_task_ids(S, ids, n);
@@ -1195,7 +963,7 @@ static int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int m
 static constexpr int kMaxLaunchedTickets = 4;  // < Session::kSlots result slots in flight
 static constexpr size_t kMaxTickets = 64;
 
-static void require_no_tickets(const Session& S) {
+void require_no_tickets(const Session& S) {
     if (!S.tickets.empty())
         throw Error(KBHIP_EINVAL, "submitted job pops are outstanding (kbhip_place_job_wait / _cancel them first)");
 }
@@ -1252,7 +1020,7 @@ static void retract_tickets(Session& S, size_t from) {
     if (S.overlap > 0) HIPCHK(hipStreamSynchronize(S.stream));  // overlapped pops are not ordered after it
 }
 
-static int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail,
+int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail,
                                 int ready_count) {
     check_task_ids(S, ids, n);
     if (S.tickets.size() >= kMaxTickets) throw Error(KBHIP_EINVAL, "too many outstanding job pops");
@@ -1275,7 +1043,7 @@ static int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_
     return id;
 }
 
-static int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
                           int32_t* out_stop) {
     if (S.tickets.empty() || S.tickets.front().id != ticket)
         throw Error(KBHIP_EINVAL, "kbhip_place_job_wait must name the oldest outstanding ticket");
@@ -1324,7 +1092,7 @@ static int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t
     return 0;
 }
 
-static int place_job_cancel(Session& S, int64_t ticket) {
+int place_job_cancel(Session& S, int64_t ticket) {
     size_t from = 0;
     while (from < S.tickets.size() && S.tickets[from].id < ticket) ++from;
     if (from == S.tickets.size() || S.tickets[from].id != ticket)
@@ -1336,3 +1104,4 @@ static int place_job_cancel(Session& S, int64_t ticket) {
     return k;
 }
 
+}  // namespace kbhip

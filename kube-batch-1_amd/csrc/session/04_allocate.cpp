@@ -1,6 +1,7 @@
-// kbhip_session.cpp, part 4 of 7 (04_allocate.inc): the allocate action's host loop (allocate.go:41-195) with speculative pop pipelining.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 04: the allocate / reclaim / preempt actions and the ordering plugins (C++ mirror)
+#include "session.h"
+
+namespace kbhip {
 
 // ---------------------------------------------------------------------------
 // allocate action with the Go framework's ordering (host mirror)
@@ -107,7 +108,7 @@ struct JobQueue {
 
 // The node-ranking buffers of a session (keys, sorted keys, histogram,
 // counters, the host copy), allocated on its first ranking.
-static void rank_buffers(Session& S) {
+void rank_buffers(Session& S) {
     if (S.b_rank_sorted.p) return;
     const int N = S.nc.n;
     S.b_rank_keys.alloc<uint64_t>(N);
@@ -1331,3 +1332,75 @@ struct Allocator {
     }
 };
 
+
+// The actions other files run (05_actions.cpp, 06_carry.cpp): the allocate
+// action, reclaim / preempt, and the first-fit node loop of given tasks.
+void allocate_run(Session& S) {
+    Allocator a(S);
+    a.run();
+}
+void evict_run(Session& S, bool preempt) {
+    Allocator a(S);
+    if (preempt) a.preempt_action();
+    else a.reclaim_action();
+}
+
+// ---------------------------------------------------------------------------
+// backfill action (actions/backfill/backfill.go:40-70): every Pending task of
+// every job whose InitResreq is empty is allocated on the first node (lowest
+// index) passing the predicates.  Pinned order:
+// jobs by UID, tasks by UID, nodes by index.  Per-task first-fit sweeps of the
+// general kernel (mode 1), 64 tasks per control-block round trip.
+// ---------------------------------------------------------------------------
+// first_fit: the inner loop of backfill.go:51-65 for the given tasks, in
+// order: each goes to the lowest-index node passing PredicateFn and is
+// committed with Session.Allocate (session.go:237-297); out_node[i] = that
+// node or -1.  Tasks must be Pending tasks of the session (task class >= 0).
+void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) {
+    vector<int> cand(ids, ids + n);
+    for (int t : cand)
+        if (t < 0 || t >= (int)S.pods.size() || S.pods[t].cls < 0 || S.pods[t].status != Pending)
+            throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
+    std::fill(out_node, out_node + n, -1);
+    ov_quiesce(S);
+    Allocator A(S);
+    A.compile_orders();
+    A.open_plugins();
+    for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
+        const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
+        int cls[kMaxChunk];
+        for (int i = 0; i < m; ++i) cls[i] = S.pods[cand[off + i]].cls;
+        uint32_t epoch = 0;
+        const int slot = take_slot(S, &epoch);
+        ctrl_setup(S, m, cls, 0, 0, 0, 1, slot, epoch);
+        sweep_chunk(S, m, cls, false);
+        int n_done = 0, stop = -1;
+        collect_tasks(S, slot, epoch, m, &n_done, &stop, S.res_node_buf, S.res_kind_buf, nullptr);
+        S.stats.sweeps += m;
+        S.stats.tasks += m;
+        if (n_done != m || stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
+        for (int i = 0; i < m; ++i) {
+            const int node = S.res_node_buf[i];
+            out_node[off + i] = node;
+            if (node < 0) continue;
+            const int pi = cand[off + i];
+            HPod& p = S.pods[pi];
+            HJob& job = S.jobs[p.job];
+            p.status = Allocated;  // Session.Allocate(task, node, false) (session.go:237-297)
+            p.node = node;
+            job.cnt_alloc++;
+            job.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
+            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
+            sess_placed(S, node, +1);
+            A.on_allocate(pi);  // drf / proportion AllocateFunc
+            S.stats.placed++;
+            S.log.emplace_back(pi, node, KBHIP_ALLOCATED);
+            if (A.job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-321)
+                for (int t : job.tasks)
+                    if (S.pods[t].status == Allocated) { S.pods[t].status = Binding; job.priority = S.pods[t].priority; }
+            if (S.classes[cls[i]].backfill) S.any_bf = 1;  // IsBackfill commit (commit_task)
+        }
+    }
+}
+
+}  // namespace kbhip

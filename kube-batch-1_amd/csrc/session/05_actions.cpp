@@ -1,66 +1,10 @@
-// kbhip_session.cpp, part 5 of 7 (05_actions.inc): backfill, sweeps for tests and benches, FitError texts; the C ABI's session entry points.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 05: backfill, the standalone sweeps and the C-ABI entry points of the actions
+#include "session.h"
 
-// ---------------------------------------------------------------------------
-// backfill action (actions/backfill/backfill.go:40-70): every Pending task of
-// every job whose InitResreq is empty is allocated on the first node (lowest
-// index) passing the predicates.  Pinned order:
-// jobs by UID, tasks by UID, nodes by index.  Per-task first-fit sweeps of the
-// general kernel (mode 1), 64 tasks per control-block round trip.
-// ---------------------------------------------------------------------------
-// first_fit: the inner loop of backfill.go:51-65 for the given tasks, in
-// order: each goes to the lowest-index node passing PredicateFn and is
-// committed with Session.Allocate (session.go:237-297); out_node[i] = that
-// node or -1.  Tasks must be Pending tasks of the session (task class >= 0).
-static void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node) {
-    vector<int> cand(ids, ids + n);
-    for (int t : cand)
-        if (t < 0 || t >= (int)S.pods.size() || S.pods[t].cls < 0 || S.pods[t].status != Pending)
-            throw Error(KBHIP_EINVAL, "task id is not a pending task of the session");
-    std::fill(out_node, out_node + n, -1);
-    ov_quiesce(S);
-    Allocator A(S);
-    A.compile_orders();
-    A.open_plugins();
-    for (size_t off = 0; off < cand.size(); off += kMaxChunk) {
-        const int m = (int)std::min<size_t>(kMaxChunk, cand.size() - off);
-        int cls[kMaxChunk];
-        for (int i = 0; i < m; ++i) cls[i] = S.pods[cand[off + i]].cls;
-        uint32_t epoch = 0;
-        const int slot = take_slot(S, &epoch);
-        ctrl_setup(S, m, cls, 0, 0, 0, 1, slot, epoch);
-        sweep_chunk(S, m, cls, false);
-        int n_done = 0, stop = -1;
-        collect_tasks(S, slot, epoch, m, &n_done, &stop, S.res_node_buf, S.res_kind_buf, nullptr);
-        S.stats.sweeps += m;
-        S.stats.tasks += m;
-        if (n_done != m || stop != 0) throw Error(KBHIP_EDEVICE, "backfill chunk did not complete");
-        for (int i = 0; i < m; ++i) {
-            const int node = S.res_node_buf[i];
-            out_node[off + i] = node;
-            if (node < 0) continue;
-            const int pi = cand[off + i];
-            HPod& p = S.pods[pi];
-            HJob& job = S.jobs[p.job];
-            p.status = Allocated;  // Session.Allocate(task, node, false) (session.go:237-297)
-            p.node = node;
-            job.cnt_alloc++;
-            job.priority = p.priority;  // UpdateTaskStatus -> AddTaskInfo (job_info.go:242)
-            S.used[node].c += p.req.c; S.used[node].m += p.req.m; S.used[node].g += p.req.g;
-            sess_placed(S, node, +1);
-            A.on_allocate(pi);  // drf / proportion AllocateFunc
-            S.stats.placed++;
-            S.log.emplace_back(pi, node, KBHIP_ALLOCATED);
-            if (A.job_ready(job))  // dispatch: Allocated -> Binding (session.go:286-321)
-                for (int t : job.tasks)
-                    if (S.pods[t].status == Allocated) { S.pods[t].status = Binding; job.priority = S.pods[t].priority; }
-            if (S.classes[cls[i]].backfill) S.any_bf = 1;  // IsBackfill commit (commit_task)
-        }
-    }
-}
+namespace kbhip {
 
-static void backfill_run(Session& S) {
+
+void backfill_run(Session& S) {
     vector<int32_t> cand;
     for (auto& j : S.jobs)
         for (int t : j.tasks) {
@@ -78,7 +22,7 @@ static void backfill_run(Session& S) {
 // PredicateFn and has a NodeOrderFn score, 0 otherwise; sorting the keys
 // descending gives util.SelectBestNode's order.  Reads the session state,
 // changes nothing.  Returns the number of passing nodes.
-static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
+int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
     if (pod < 0 || pod >= (int)S.pods.size() || S.pods[pod].cls < 0)
         throw Error(KBHIP_EINVAL, "task id has no task class (not a pending task of the session)");
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "sweep_scores on a node-sharded session");
@@ -124,7 +68,7 @@ static int sweep_scores(Session& S, int pod, uint64_t* out_keys) {
 // (option "time_sweeps_cold": one at a time behind a cache-evicting write)
 // (no copies in between), one HIP-event pair around the whole sequence: the
 // device time per sweep launch, boundaries between launches included.
-static double time_sweeps(Session& S, const int32_t* ids, int n) {
+double time_sweeps(Session& S, const int32_t* ids, int n) {
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "time_sweeps on a node-sharded session");
     for (int i = 0; i < n; ++i)
         if (ids[i] < 0 || ids[i] >= (int)S.pods.size() || S.pods[ids[i]].cls < 0)
@@ -204,7 +148,7 @@ static double time_sweeps(Session& S, const int32_t* ids, int n) {
 // read (evict 2) on session 0's stream, HIP events around each; returns the
 // microseconds per chain.  The descriptors are copied to device memory first
 // (mapped = 0) or read by the kernels from pinned mapped host memory (1).
-static double time_rank_multi(Session* const* ss, int n, const int32_t* ids, int reps, int evict, int mapped) {
+double time_rank_multi(Session* const* ss, int n, const int32_t* ids, int reps, int evict, int mapped) {
     if (n < 1 || reps < 1) throw Error(KBHIP_EINVAL, "time_rank_multi: n and reps must be positive");
     if (evict != 0 && evict != 2) throw Error(KBHIP_EINVAL, "time_rank_multi: evict must be 0 or 2");
     Session& S0 = *ss[0];
@@ -277,7 +221,7 @@ static double time_rank_multi(Session* const* ss, int n, const int32_t* ids, int
 }
 
 // JobInfo.FitError (job_info.go:343-372) from the histogram of the job's last walk.
-static string fit_error(const HJob& j) {
+string fit_error(const HJob& j) {
     if (j.fit[0] == 0) return "0 nodes are available";
     vector<string> rs;  // "%v insufficient %v", sort.Strings
     const std::pair<const char*, int32_t> rz[3] = {{"cpu", j.fit[1]}, {"memory", j.fit[2]}, {"GPU", j.fit[3]}};
@@ -293,7 +237,7 @@ static string fit_error(const HJob& j) {
 // "<job uid>\t<message>\n" per job in UID order; empty without gang.  A job
 // with an IsBackfill task gets the PodGroupBackfilled condition instead, which
 // has no message (gang.go:189-199): "<job uid>\tBackfilled\n".
-static string gang_close_text(const Session& S) {
+string gang_close_text(const Session& S) {
     if (!S.gang_close) return "";
     string out;
     for (size_t i = 0; i < S.jobs.size(); ++i) {
@@ -316,7 +260,7 @@ static string gang_close_text(const Session& S) {
     return out;
 }
 
-static int device_count() {
+int device_count() {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) {
@@ -332,244 +276,8 @@ static int device_count() {
     return ok;
 }
 
-}  // namespace kbhip
 
-using namespace kbhip;
 
-#define ABI_GUARD(...)                                       \
-    try {                                                    \
-        __VA_ARGS__                                          \
-    } catch (kbhip::Error & e) {                             \
-        kbhip::g_err = e.what();                             \
-        return e.code;                                       \
-    } catch (std::exception & e) {                           \
-        kbhip::g_err = e.what();                             \
-        return KBHIP_EINVAL;                                 \
-    } catch (...) {                                          \
-        kbhip::g_err = "unknown error";                      \
-        return KBHIP_EINVAL;                                 \
-    }
-// The same for calls on a session: a failure while the session's RCCL
-// communicator is connected taints it (aborted at close, never pooled).
-#define ABI_GUARD_S(sp, ...)                                 \
-    try {                                                    \
-        check_usable(sp);                                    \
-        __VA_ARGS__                                          \
-    } catch (kbhip::Error & e) {                             \
-        kbhip::g_err = e.what();                             \
-        taint_comm(sp);                                      \
-        return e.code;                                       \
-    } catch (std::exception & e) {                           \
-        kbhip::g_err = e.what();                             \
-        taint_comm(sp);                                      \
-        return KBHIP_EINVAL;                                 \
-    } catch (...) {                                          \
-        kbhip::g_err = "unknown error";                      \
-        taint_comm(sp);                                      \
-        return KBHIP_EINVAL;                                 \
-    }
-
-extern "C" {
-
-struct kb_session {
-    kb_session() { kbhip::g_live_sessions.fetch_add(1, std::memory_order_relaxed); }
-    ~kb_session() {
-        kbhip::g_live_sessions.fetch_sub(1, std::memory_order_relaxed);
-        set_grouped(false);
-    }
-    void set_grouped(bool g) {  // the StepBatcher's count of live grouped sessions
-        if (g != grouped) kbhip::StepBatcher::get().sessions.fetch_add(g ? 1 : -1, std::memory_order_relaxed);
-        grouped = g;
-    }
-    bool grouped = false;
-    kb_session(const kb_session&) = delete;
-    kb_session& operator=(const kb_session&) = delete;
-    kbhip::Session s;
-};
-static void taint_comm(kb_session* s) {
-    if (s && s->s.comm) s->s.comm_bad = true;
-}
-static void check_usable(kb_session* s) {
-    if (s && !s->s.broken.empty()) throw kbhip::Error(KBHIP_EINVAL, s->s.broken);
-}
-
-const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
-
-int kbhip_device_count(void) { ABI_GUARD(return kbhip::device_count();) }
-
-// Arguments of the actions that return a record log: a device session and,
-// when cap > 0, three output arrays of at least cap entries.
-static void check_log_args(kb_session* s, const int32_t* out_pod, const int32_t* out_node, const uint8_t* out_kind,
-                           int64_t cap) {
-    if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
-    if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-    if (cap < 0 || (cap > 0 && (!out_pod || !out_node || !out_kind)))
-        throw kbhip::Error(KBHIP_EINVAL, "null output array with cap > 0");
-}
-
-static int open_common(const kbs::Snapshot& snap, int device, kb_session** out) {
-    int nd = kbhip::device_count();
-    if (nd <= 0) throw kbhip::Error(KBHIP_ENODEV, "no gfx950 HIP device available");
-    if (device < 0 || device >= nd) throw kbhip::Error(KBHIP_EINVAL, "device index out of range");
-    std::unique_ptr<kb_session> s(new kb_session());
-    kbhip::open_session(s->s, snap, device);
-    *out = s.release();
-    return KBHIP_OK;
-}
-
-int kbhip_session_open(const void* bytes, size_t len, int device, kb_session** out) {
-    ABI_GUARD({
-        if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        kbs::Snapshot snap;
-        snap.view_bytes(bytes, len);  // the caller's buffer outlives the call; nothing keeps a view after it
-        return open_common(snap, device, out);
-    })
-}
-
-int kbhip_session_open_file(const char* path, int device, kb_session** out) {
-    ABI_GUARD({
-        if (!path || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        kbs::Snapshot snap(path);
-        return open_common(snap, device, out);
-    })
-}
-
-int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode, int32_t min_available,
-                    int32_t ready_count, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
-                    int32_t* out_stop_reason) {
-    ABI_GUARD_S(s, {
-        if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
-            throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        // results come back through the pinned result granules; device work still in flight (an
-        // overlapped pop's write-back) is ordered before the next pop by the device chain, and
-        // before anything else by ov_quiesce in the entry point that runs it
-        return kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
-                                out_n_done, out_stop_reason);
-    })
-}
-
-int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
-                               int32_t min_available, int32_t ready_count) {
-    ABI_GUARD_S(s, {
-        if (!s || (!task_ids && n_tasks) || n_tasks < 0) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-        // a shard's launch would block inside the exchange, and a retraction needs every rank to cancel
-        // identically: node-sharded sessions use the synchronous kbhip_place_job
-        if (s->s.world > 1)
-            throw kbhip::Error(KBHIP_EUNSUPPORTED, "kbhip_place_job_submit on a node-sharded session (use kbhip_place_job)");
-        HIPCHK(hipSetDevice(s->s.device));
-        return kbhip::place_job_submit(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count);
-    })
-}
-
-int kbhip_place_job_wait(kb_session* s, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
-                         int32_t* out_stop_reason) {
-    ABI_GUARD_S(s, {
-        if (!s || !out_node || !out_kind || !out_n_done || !out_stop_reason)
-            throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        HIPCHK(hipSetDevice(s->s.device));
-        return kbhip::place_job_wait(s->s, ticket, out_node, out_kind, out_n_done, out_stop_reason);
-    })
-}
-
-int kbhip_place_job_cancel(kb_session* s, int64_t ticket) {
-    ABI_GUARD_S(s, {
-        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        HIPCHK(hipSetDevice(s->s.device));
-        return kbhip::place_job_cancel(s->s, ticket);
-    })
-}
-
-int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
-    ABI_GUARD_S(s, {
-        check_log_args(s, out_pod, out_node, out_kind, cap);
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        s->s.log.clear();
-        kbhip::Allocator a(s->s);
-        a.run();
-        const int64_t n = (int64_t)s->s.log.size();
-        for (int64_t i = 0; i < n && i < cap; ++i) {
-            out_pod[i] = std::get<0>(s->s.log[i]);
-            out_node[i] = std::get<1>(s->s.log[i]);
-            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
-        }
-        return (int)n;
-    })
-}
-
-int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
-    ABI_GUARD_S(s, {
-        check_log_args(s, out_pod, out_node, out_kind, cap);
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        kbhip::ov_quiesce(s->s);
-        s->s.log.clear();
-        kbhip::backfill_run(s->s);
-        const int64_t n = (int64_t)s->s.log.size();
-        for (int64_t i = 0; i < n && i < cap; ++i) {
-            out_pod[i] = std::get<0>(s->s.log[i]);
-            out_node[i] = std::get<1>(s->s.log[i]);
-            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
-        }
-        return (int)n;
-    })
-}
-
-int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node) {
-    ABI_GUARD_S(s, {
-        if (!s || n < 0 || (n > 0 && (!task_ids || !out_node))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        s->s.log.clear();
-        kbhip::first_fit(s->s, task_ids, n, out_node);
-        int placed = 0;
-        for (int i = 0; i < n; ++i) placed += out_node[i] >= 0;
-        return placed;
-    })
-}
-
-int kbhip_time_sweeps(kb_session* s, const int32_t* task_ids, int32_t n, double* out_mean_us) {
-    ABI_GUARD_S(s, {
-        if (!s || (!task_ids && n) || n < 0 || !out_mean_us) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        *out_mean_us = kbhip::time_sweeps(s->s, task_ids, n);
-        return KBHIP_OK;
-    })
-}
-
-int kbhip_time_rank_multi(kb_session* const* sessions, int32_t n, const int32_t* task_ids, int32_t reps,
-                          int32_t evict, int32_t mapped, double* out_us) {
-    ABI_GUARD({
-        if (!sessions || !task_ids || n < 1 || n > 4096 || !out_us) throw kbhip::Error(KBHIP_EINVAL, "null argument");
-        vector<kbhip::Session*> ss(n);
-        for (int i = 0; i < n; ++i) {
-            if (!sessions[i]) throw kbhip::Error(KBHIP_EINVAL, "null session");
-            check_usable(sessions[i]);
-            kbhip::require_no_tickets(sessions[i]->s);
-            ss[i] = &sessions[i]->s;
-        }
-        HIPCHK(hipSetDevice(ss[0]->device));
-        *out_us = kbhip::time_rank_multi(ss.data(), n, task_ids, reps, evict, mapped);
-        return KBHIP_OK;
-    })
-}
-
-int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
-    ABI_GUARD_S(s, {
-        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
-        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
-        kbhip::require_no_tickets(s->s);
-        HIPCHK(hipSetDevice(s->s.device));
-        return kbhip::sweep_scores(s->s, task_id, out_keys);
-    })
-}
 // kbhip_session_carry: the next scheduling session's
 // start state from this one's end state, without a new snapshot — what the
 // scheduler cache holds after the session's binds and evictions reached it
@@ -589,7 +297,7 @@ int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
 // only its node drops it (detached); no job is deleted — and updatePod to
 // Succeeded / Failed (isTerminated: the task stays in its job, off its node).
 // New pods, node and PodGroup changes: kbhip_session_carry_snapshot.
-static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0) {
+void session_carry(Session& S, const int32_t* ev_pod, const uint8_t* ev, int64_t n_ev) {
     S.model_gen++;  // per-pod caches of the host model (Session::pod_queue) are rebuilt
     // every node's row is recomputed on the host (a shard's host model holds
     // all of them); this device's rows [lo, lo + Nl) are compared and uploaded
@@ -759,3 +467,182 @@ static void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uin
     S.last_fit_ok = false;
 }
 
+}  // namespace kbhip
+
+using namespace kbhip;
+
+extern "C" {
+
+const char* kbhip_last_error(void) { return kbhip::g_err.c_str(); }
+
+
+int kbhip_device_count(void) { ABI_GUARD(return kbhip::device_count();) }
+
+// Arguments of the actions that return a record log: a device session and,
+// when cap > 0, three output arrays of at least cap entries.
+
+static int open_common(const kbs::Snapshot& snap, int device, kb_session** out) {
+    int nd = kbhip::device_count();
+    if (nd <= 0) throw kbhip::Error(KBHIP_ENODEV, "no gfx950 HIP device available");
+    if (device < 0 || device >= nd) throw kbhip::Error(KBHIP_EINVAL, "device index out of range");
+    std::unique_ptr<kb_session> s(new kb_session());
+    kbhip::open_session(s->s, snap, device);
+    *out = s.release();
+    return KBHIP_OK;
+}
+
+int kbhip_session_open(const void* bytes, size_t len, int device, kb_session** out) {
+    ABI_GUARD({
+        if (!bytes || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbs::Snapshot snap;
+        snap.view_bytes(bytes, len);  // the caller's buffer outlives the call; nothing keeps a view after it
+        return open_common(snap, device, out);
+    })
+}
+
+int kbhip_session_open_file(const char* path, int device, kb_session** out) {
+    ABI_GUARD({
+        if (!path || !out) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        kbs::Snapshot snap(path);
+        return open_common(snap, device, out);
+    })
+}
+
+int kbhip_place_job(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode, int32_t min_available,
+                    int32_t ready_count, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                    int32_t* out_stop_reason) {
+    ABI_GUARD_S(s, {
+        if (!s || (!task_ids && n_tasks) || !out_node || !out_kind || !out_n_done || !out_stop_reason)
+            throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        // results come back through the pinned result granules; device work still in flight (an
+        // overlapped pop's write-back) is ordered before the next pop by the device chain, and
+        // before anything else by ov_quiesce in the entry point that runs it
+        return kbhip::place_job(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count, out_node, out_kind,
+                                out_n_done, out_stop_reason);
+    })
+}
+
+int64_t kbhip_place_job_submit(kb_session* s, const int32_t* task_ids, int32_t n_tasks, int32_t gang_mode,
+                               int32_t min_available, int32_t ready_count) {
+    ABI_GUARD_S(s, {
+        if (!s || (!task_ids && n_tasks) || n_tasks < 0) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        // a shard's launch would block inside the exchange, and a retraction needs every rank to cancel
+        // identically: node-sharded sessions use the synchronous kbhip_place_job
+        if (s->s.world > 1)
+            throw kbhip::Error(KBHIP_EUNSUPPORTED, "kbhip_place_job_submit on a node-sharded session (use kbhip_place_job)");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_submit(s->s, task_ids, n_tasks, gang_mode, min_available, ready_count);
+    })
+}
+
+int kbhip_place_job_wait(kb_session* s, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                         int32_t* out_stop_reason) {
+    ABI_GUARD_S(s, {
+        if (!s || !out_node || !out_kind || !out_n_done || !out_stop_reason)
+            throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_wait(s->s, ticket, out_node, out_kind, out_n_done, out_stop_reason);
+    })
+}
+
+int kbhip_place_job_cancel(kb_session* s, int64_t ticket) {
+    ABI_GUARD_S(s, {
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::place_job_cancel(s->s, ticket);
+    })
+}
+
+int kbhip_allocate(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    ABI_GUARD_S(s, {
+        check_log_args(s, out_pod, out_node, out_kind, cap);
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        s->s.log.clear();
+        kbhip::allocate_run(s->s);
+        const int64_t n = (int64_t)s->s.log.size();
+        for (int64_t i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(s->s.log[i]);
+            out_node[i] = std::get<1>(s->s.log[i]);
+            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
+        }
+        return (int)n;
+    })
+}
+
+int kbhip_backfill(kb_session* s, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind, int64_t cap) {
+    ABI_GUARD_S(s, {
+        check_log_args(s, out_pod, out_node, out_kind, cap);
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        kbhip::ov_quiesce(s->s);
+        s->s.log.clear();
+        kbhip::backfill_run(s->s);
+        const int64_t n = (int64_t)s->s.log.size();
+        for (int64_t i = 0; i < n && i < cap; ++i) {
+            out_pod[i] = std::get<0>(s->s.log[i]);
+            out_node[i] = std::get<1>(s->s.log[i]);
+            out_kind[i] = (uint8_t)std::get<2>(s->s.log[i]);
+        }
+        return (int)n;
+    })
+}
+
+int kbhip_first_fit(kb_session* s, const int32_t* task_ids, int32_t n, int32_t* out_node) {
+    ABI_GUARD_S(s, {
+        if (!s || n < 0 || (n > 0 && (!task_ids || !out_node))) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        s->s.log.clear();
+        kbhip::first_fit(s->s, task_ids, n, out_node);
+        int placed = 0;
+        for (int i = 0; i < n; ++i) placed += out_node[i] >= 0;
+        return placed;
+    })
+}
+
+int kbhip_time_sweeps(kb_session* s, const int32_t* task_ids, int32_t n, double* out_mean_us) {
+    ABI_GUARD_S(s, {
+        if (!s || (!task_ids && n) || n < 0 || !out_mean_us) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        *out_mean_us = kbhip::time_sweeps(s->s, task_ids, n);
+        return KBHIP_OK;
+    })
+}
+
+int kbhip_time_rank_multi(kb_session* const* sessions, int32_t n, const int32_t* task_ids, int32_t reps,
+                          int32_t evict, int32_t mapped, double* out_us) {
+    ABI_GUARD({
+        if (!sessions || !task_ids || n < 1 || n > 4096 || !out_us) throw kbhip::Error(KBHIP_EINVAL, "null argument");
+        vector<kbhip::Session*> ss(n);
+        for (int i = 0; i < n; ++i) {
+            if (!sessions[i]) throw kbhip::Error(KBHIP_EINVAL, "null session");
+            check_usable(sessions[i]);
+            kbhip::require_no_tickets(sessions[i]->s);
+            ss[i] = &sessions[i]->s;
+        }
+        HIPCHK(hipSetDevice(ss[0]->device));
+        *out_us = kbhip::time_rank_multi(ss.data(), n, task_ids, reps, evict, mapped);
+        return KBHIP_OK;
+    })
+}
+
+
+int kbhip_sweep_scores(kb_session* s, int32_t task_id, uint64_t* out_keys) {
+    ABI_GUARD_S(s, {
+        if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+        if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+        kbhip::require_no_tickets(s->s);
+        HIPCHK(hipSetDevice(s->s.device));
+        return kbhip::sweep_scores(s->s, task_id, out_keys);
+    })
+}
+
+}  // extern "C"

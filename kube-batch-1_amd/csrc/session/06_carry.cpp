@@ -1,6 +1,7 @@
-// kbhip_session.cpp, part 6 of 7 (06_carry.inc): session carry-over from the scheduler cache's next snapshot.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 06: session carry-over from the scheduler cache
+#include "session.h"
+
+namespace kbhip {
 
 // ---------------------------------------------------------------------------
 // kbhip_session_carry_snapshot: the next session from the
@@ -119,7 +120,7 @@ struct PodView {
     }
 };
 
-static void reopen_in_place(kb_session* ks, const kbs::Snapshot& s) {
+void reopen_in_place(kb_session* ks, const kbs::Snapshot& s) {
     Session& S = ks->s;
     const SavedOptions o = save_options(S);
     const int dev = S.device;
@@ -148,7 +149,7 @@ static bool carry_fast_ok(const Session& S, const kbs::Snapshot& s, const PodVie
     return true;
 }
 
-static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t* old_pod, const int32_t* old_node) {
+void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t* old_pod, const int32_t* old_node) {
     Session& S = ks->s;
     if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "kbhip_session_carry_snapshot on a node-sharded session");
     static const bool prof = std::getenv("KBHIP_OPEN_PROFILE") != nullptr;  // per-phase host times (diagnostic)
@@ -743,7 +744,7 @@ static void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t
     mark("swap");
 }
 
-static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
+int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
                         int64_t cap) {
     ABI_GUARD_S(s, {
         check_log_args(s, out_pod, out_node, out_kind, cap);
@@ -751,9 +752,7 @@ static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* 
         HIPCHK(hipSetDevice(s->s.device));
         kbhip::ov_quiesce(s->s);
         s->s.log.clear();
-        kbhip::Allocator a(s->s);
-        if (preempt) a.preempt_action();
-        else a.reclaim_action();
+        kbhip::evict_run(s->s, preempt);
         HIPCHK(hipStreamSynchronize(s->s.stream));
         const int64_t n = (int64_t)s->s.log.size();
         for (int64_t i = 0; i < n && i < cap; ++i) {
@@ -764,3 +763,5 @@ static int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* 
         return (int)n;
     })
 }
+
+}  // namespace kbhip

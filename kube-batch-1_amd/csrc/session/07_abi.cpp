@@ -1,7 +1,9 @@
-// kbhip_session.cpp, part 7 of 7 (07_abi.inc): the remaining C ABI entry points (carry, reclaim / preempt, reads, options, stats).
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// kbhip session, part 07: the remaining C-ABI entry points (carry, options, shards, debug, close)
+#include "session.h"
 
+using namespace kbhip;
+
+extern "C" {
 int kbhip_session_carry(kb_session* s, int64_t* out_uploaded_bytes) {
     ABI_GUARD_S(s, {
         if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");

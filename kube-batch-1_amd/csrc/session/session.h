@@ -1,10 +1,65 @@
-// kbhip_session.cpp, part 1 of 7 (01_types.inc): session types: host model (pods, jobs, queues), pools (RCCL communicators, pinned and device memory), BatchLaunch, Session.
-// Not a separate translation unit: kbhip_session.cpp includes the parts in
-// order (one unit: the file-local helpers and the Session type stay shared).
+// session.h — the host side of libkbhip.so, shared header of its parts
+// (session/*.cpp, each its own translation unit): the host model and device
+// buffers of a session (Session), the pools, the what-if batcher, the C-ABI
+// handle, and the functions the parts call across files.
+//
+// The parts: 02_open (session open: KBS1 decode, dictionary encoding, task
+// classes, upload of the node SoA to HBM), 03_pop (the per-pop device driver:
+// batched pops, the persistent engine, tickets), 04_allocate (a C++ mirror of
+// the Go framework's ordering plugins running the allocate / reclaim /
+// preempt actions), 05_actions (backfill, the standalone sweeps, the actions'
+// C-ABI entry points), 06_carry (session carry-over), 07_abi (the remaining
+// C-ABI entry points).
+//
+// Reference map (pkg/scheduler unless noted):
+//   session open      cache/cache.go:515-583 (Snapshot), framework/session.go:66-122,
+//                     api/node_info.go:62-145 (NodeInfo.AddTask), api/job_info.go:239-326
+//   ordering          util/priority_queue.go + Go container/heap, framework/session_plugins.go:
+//                     244-329 (Job/Queue/TaskOrderFn), plugins/{priority,gang,drf,proportion}
+//   allocate loop     actions/allocate/allocate.go:41-201
+//   placement         the HIP kernels (kbhip_kernels.hip)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <exception>
+#include <map>
+#include <memory>
+#include <condition_variable>
+#include <mutex>
+#include <random>
+#include <tuple>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include <unistd.h>
+
+#include "../../../include/kbhip.h"
+#include "../../../include/kbsnap.h"
+#include "../kbhip_affinity.h"
+#include "../kbhip_engine.h"
+#include "../kbhip_eval.h"
+#include "../kbhip_internal.h"
+
+using std::string;
+using std::vector;
 
 namespace kbhip {
 
-static thread_local string g_err;
+inline thread_local string g_err;
 
 struct Error : std::runtime_error {
     int code;
@@ -20,7 +75,7 @@ struct Error : std::runtime_error {
 enum St { Pending = 1, AOB = 2, Allocated = 4, Pipelined = 8, Binding = 16, Bound = 32, Running = 64,
           Releasing = 128, Succeeded = 256, Failed = 512, Unknown = 1024,
           Gone = 2048 };  // Gone: deleted from the cache between sessions (kbhip_session_carry_events)
-static inline bool allocated_status(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
+inline bool allocated_status(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
 
 struct Dict {
     std::unordered_map<string, int> ids;
@@ -34,7 +89,7 @@ struct Dict {
     }
 };
 
-static bool parse_int64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
+inline bool parse_int64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
     if (s.empty()) return false;
     size_t i = 0;
     bool neg = false;
@@ -66,15 +121,15 @@ struct F3 {  // float64 Resource of the ordering plugins
     }
     bool empty() const { return c < (double)kMinCPU && m < (double)kMinMem && g < (double)kMinGPU; }
 };
-static double share(double l, double r) { return r == 0 ? (l == 0 ? 0 : 1) : l / r; }  // helpers.go:35-48
+inline double share(double l, double r) { return r == 0 ? (l == 0 ? 0 : 1) : l / r; }  // helpers.go:35-48
 
 // Host worker threads for the session's parallel passes over pods / jobs: a
 // process-wide budget — the machine's hardware threads, at most 16
 // (KBHIP_HOST_THREADS overrides, 1..64) — shared by the sessions alive in the
 // process (what-if sessions run 16 at a time from their own host threads: 16
 // passes of 16 threads each oversubscribed the box's cores).
-static std::atomic<int> g_live_sessions{0};
-static int host_threads() {
+inline std::atomic<int> g_live_sessions{0};
+inline int host_threads() {
     static const int budget = [] {
         if (const char* e = std::getenv("KBHIP_HOST_THREADS")) {
             const int v = std::atoi(e);
@@ -87,7 +142,7 @@ static int host_threads() {
 }
 // The hardware queues HIP gives this process per device (GPU_MAX_HW_QUEUES, the
 // runtime's default 4).  Streams beyond them share queues.
-static int hw_queues() {
+inline int hw_queues() {
     const char* e = std::getenv("GPU_MAX_HW_QUEUES");
     const int v = e ? std::atoi(e) : 0;
     return v > 0 ? v : 4;
@@ -100,7 +155,7 @@ static int hw_queues() {
 // in the queues with room for two more (the null stream of the runtime's own
 // copies, a StepBatcher or pooled stream), refuse (one process per GPU, k = 1,
 // always fits).  Returns the reason, or "" when the group is safe.
-static std::string mailbox_queue_check(int k, int queues) {
+inline std::string mailbox_queue_check(int k, int queues) {
     const int per = 1 + kMaxDep;
     if (k <= 1 || k * per + 2 <= queues) return "";
     return "kbhip_shard_connect_mailbox: " + std::to_string(k) + " shard ranks of this process share one device; their " +
@@ -113,7 +168,7 @@ static std::string mailbox_queue_check(int k, int queues) {
 // A token of this process, unique across hosts and containers (process ids and
 // device ordinals repeat between containers): the mailbox records tell ranks
 // of this process from others by it.
-static uint64_t process_token() {
+inline uint64_t process_token() {
     static const uint64_t tok = [] {
         std::random_device rd;
         uint64_t v = ((uint64_t)rd() << 32) ^ rd();
@@ -142,7 +197,7 @@ struct HPod {
 };
 // The pod is in its node's task list (NodeInfo.Tasks): bound, not terminated
 // (cache addTask, event_handlers.go:63-79), not taken off by a deletePod.
-static inline bool on_node_of(const HPod& p) {
+inline bool on_node_of(const HPod& p) {
     return p.node >= 0 && !p.detached && p.status != Succeeded && p.status != Failed;
 }
 // Placement 7's per-domain candidates (kbhip_batch.h place_aff): the sweep may
@@ -152,7 +207,7 @@ static inline bool on_node_of(const HPod& p) {
 // its own domain (a self-matching anti-affinity term): a node beaten by one
 // of its domain fails exactly when that one does, or ranks below it.  -1:
 // the class keeps plain candidates.  space_ndom: domains per space.
-static int32_t dedup_space(const AffProgram& pg, const vector<int>& space_ndom) {
+inline int32_t dedup_space(const AffProgram& pg, const vector<int>& space_ndom) {
     if (pg.pa_space >= 0 || !pg.ipa.empty() || pg.pred_err) return -1;
     int32_t sp = pg.paa_space;
     vector<int32_t> offs;
@@ -217,7 +272,7 @@ struct CommPool {
         return p;
     }
 };
-static ncclComm_t comm_acquire(const string& id, int rank, int world, int device) {
+inline ncclComm_t comm_acquire(const string& id, int rank, int world, int device) {
     CommPool& P = CommPool::get();
     std::lock_guard<std::mutex> lk(P.mu);
     for (size_t i = 0; i < P.v.size(); ++i) {
@@ -235,12 +290,12 @@ static ncclComm_t comm_acquire(const string& id, int rank, int world, int device
     }
     return nullptr;
 }
-static void comm_add(const string& id, int rank, int world, int device, ncclComm_t c) {
+inline void comm_add(const string& id, int rank, int world, int device, ncclComm_t c) {
     CommPool& P = CommPool::get();
     std::lock_guard<std::mutex> lk(P.mu);
     P.v.push_back({id, rank, world, device, c, true});
 }
-static void comm_release(ncclComm_t c) {
+inline void comm_release(ncclComm_t c) {
     CommPool& P = CommPool::get();
     std::lock_guard<std::mutex> lk(P.mu);
     for (auto& e : P.v)
@@ -249,7 +304,7 @@ static void comm_release(ncclComm_t c) {
 // A communicator whose session failed part-way (an ABI call returned an error
 // while it was connected: the ranks' collective sequences may no longer
 // match) or that reports an asynchronous error is aborted and leaves the pool.
-static void comm_drop(ncclComm_t c) {
+inline void comm_drop(ncclComm_t c) {
     {
         CommPool& P = CommPool::get();
         std::lock_guard<std::mutex> lk(P.mu);
@@ -264,7 +319,7 @@ static void comm_drop(ncclComm_t c) {
 }
 // A unique id serves one ncclCommInitRank bootstrap (its root listens once):
 // after its communicator was aborted, the ranks connect with a new id.
-static bool comm_id_aborted(const string& id) {
+inline bool comm_id_aborted(const string& id) {
     CommPool& P = CommPool::get();
     std::lock_guard<std::mutex> lk(P.mu);
     return P.aborted.count(id) != 0;
@@ -758,10 +813,10 @@ struct Session {
 #endif
     }
     ~Session();
-    void eng_unclaim();  // (03_pop.inc: the engine arbiter)
+    void eng_unclaim();  // (03_pop.cpp: the engine arbiter)
 };
 
-Session::~Session() {
+inline Session::~Session() {
     release_device();
     spare_pods().give(pods);
 }
@@ -769,11 +824,366 @@ Session::~Session() {
 // Table upload: HBM on the session stream, or a host copy for encode-only
 // sessions (kbhip_debug_encode / kbhip_debug_replay).
 template <typename T>
-static T* upload(Session& S, DevBuf& b, const vector<T>& v) {
+inline T* upload(Session& S, DevBuf& b, const vector<T>& v) {
     T* d = b.alloc<T>(v.size(), S.encode_only);
     if (v.empty()) return d;
     if (S.encode_only) std::memcpy(d, v.data(), v.size() * sizeof(T));
     else HIPCHK(hipMemcpyAsync(d, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, S.stream));
     return d;
 }
+
+// ---------------------------------------------------------------------------
+// What-if sessions batched per launch:
+// sessions opened with option "rank_group", each driven by its own host
+// thread, send their device requests — the allocate pops of sessions with
+// Backfilled nodes or of pod-affinity classes (placements 6 / 7: one pop in
+// flight per session), per-task chunks, and the reclaim / preempt node
+// rankings — to this batcher, which serves every request pending in a lane as
+// ONE multi-session launch per kind and device (k_pop_batch_multi, task k of
+// every chunk in k_sweep_argmax_multi, the k_rank_*_multi sorts; blockIdx.y =
+// session).  Pops are ordered by events after each session's earlier device
+// work and before its later work; their results are the sessions' own
+// granules.  Rankings complete before their requesters resume.  Combining:
+// a request is issued at once with whatever else is pending in its lane;
+// while a step is being launched new requests collect, and the first of
+// their requesters to find the lane free issues them all — no session waits
+// for another's host work.  (r03-r05 issued lockstep steps, once every member
+// inside an action of the kind had a request in: 7.0-7.4 sessions/s at 16 in
+// flight against 9.5-11.3 ungrouped and 9.6 combining, profiles/r06c_*;
+// removed.)
+// ---------------------------------------------------------------------------
+struct StepBatcher {
+    static StepBatcher& get() {
+        static StepBatcher b;
+        return b;
+    }
+    // kSweep requests (per-task chunks) go in the pop lane: the same sessions
+    // (sessions inside allocate or backfill) send either
+    enum Kind { kPop = 0, kRank = 1, kSweep = 2 };
+    static int lane_of(int kind) { return kind == kRank ? 1 : 0; }
+    struct Req {
+        int kind = kPop;
+        int device = 0;
+        PopReq pop{};
+        SweepReq sweep{};
+        hipEvent_t before = nullptr;  // pop: recorded on the requester's stream (its earlier work)
+        hipEvent_t after = nullptr;   // pop: recorded after the launch that served it
+        RankDesc rank{};
+        hipStream_t st = nullptr;     // rank: the requester's stream
+        std::atomic<bool> done{false};
+        hipError_t err = hipSuccess;
+        int batch = 0;                // requests of its kind in the launch that served it
+        std::chrono::steady_clock::time_point t0;  // when it was submitted (linger)
+    };
+    std::mutex mu;
+    std::condition_variable cv;  // a step is out: requests done, the lane free
+    // One lane per request lane kind: pops and chunks in one, rankings in the
+    // other (a ranking waits for its launch; pops and chunks do not).
+    struct Lane {
+        vector<Req*> pending;
+        bool busy = false;
+    };
+    Lane lane[2];
+    int64_t steps = 0;
+    // Test knob (option "group_linger_us", process-wide; 0 = off): a lane waits
+    // until every grouped session has a request in it, or its oldest request
+    // is that old, so that concurrent sessions' requests meet deterministically.
+    std::atomic<int64_t> linger_us{0};
+    std::atomic<int> sessions{0};  // live sessions with rank_group set
+    static constexpr int kStreams = 4;
+    struct Dev {
+        hipStream_t sts[kStreams] = {};  // pop / chunk steps, round robin (a session has one request in
+        int rr = 0;                      // flight, so consecutive steps need no order between them)
+        hipStream_t st = nullptr;        // this step's
+        vector<hipEvent_t> ring;
+        size_t next = 0;
+        RankDesc* h_desc = nullptr;  // pinned: the step's ranking descriptors, copied to d_desc
+        RankDesc* d_desc = nullptr;  // device memory (kernels reading descriptors from mapped host memory
+                                     // measured 1.6x slower at 64 sessions: profiles/r06m_c5_multi.jsonl)
+        size_t cap_bytes = 0, n_cap = 0;
+    };
+    std::map<int, Dev> dev;
+
+    // The requester issues at once if the lane is free, else it sleeps until
+    // the current step is out and then one of the waiting requesters issues
+    // what has collected.  (Spinning requesters — r03-r05 — took the host
+    // cores the other sessions' host work needed: 16 sessions in flight are
+    // host-bound.)
+    void submit(Req& r) {
+        const int l = lane_of(r.kind);
+        r.t0 = std::chrono::steady_clock::now();
+        std::unique_lock<std::mutex> lk(mu);
+        lane[l].pending.push_back(&r);
+        while (!r.done.load(std::memory_order_acquire)) {
+            if (ready(l)) {
+                issue(lk, l);
+                continue;
+            }
+            if (linger_us.load(std::memory_order_relaxed) > 0) cv.wait_for(lk, std::chrono::microseconds(100));
+            else cv.wait(lk);
+        }
+    }
+
+  private:
+    bool ready(int l) const {
+        const Lane& L = lane[l];
+        if (L.busy || L.pending.empty()) return false;
+        const int64_t lg = linger_us.load(std::memory_order_relaxed);
+        if (lg <= 0 || (int)L.pending.size() >= sessions.load(std::memory_order_relaxed)) return true;
+        return std::chrono::steady_clock::now() - L.pending.front()->t0 >= std::chrono::microseconds(lg);
+    }
+    // One step of one lane: every pending request of that lane (the lock is
+    // released while launching).
+    void issue(std::unique_lock<std::mutex>& lk, int l) {
+        Lane& L = lane[l];
+        L.busy = true;
+        vector<Req*> batch;
+        batch.swap(L.pending);
+        ++steps;
+        // each device's streams and events, created under the lock (both lanes may issue at once)
+        hipError_t e0 = hipSuccess;
+        for (Req* q : batch)
+            if (e0 == hipSuccess && (e0 = hipSetDevice(q->device)) == hipSuccess) (void)device(q->device, &e0);
+        lk.unlock();
+        std::map<int, vector<Req*>> by;  // device -> requests
+        for (Req* q : batch) by[q->device].push_back(q);
+        for (auto& kv : by) {
+            if (e0 != hipSuccess) {
+                for (Req* q : kv.second) q->err = e0;
+                continue;
+            }
+            if (l == 1) {
+                const hipError_t e = launch_ranks(kv.first, kv.second);
+                for (Req* q : kv.second) { q->err = e; q->batch = (int)kv.second.size(); }
+                continue;
+            }
+            vector<Req*> pops, sweeps;
+            for (Req* q : kv.second) (q->kind == kSweep ? sweeps : pops).push_back(q);
+            int pl = 0, sl = 0, sw_tasks = 0;
+            hipError_t e = hipSetDevice(kv.first);
+            if (e == hipSuccess) {
+                Dev& D = device(kv.first, &e);
+                if (e == hipSuccess) D.st = D.sts[D.rr++ % kStreams];  // this step's stream
+            }
+            if (e == hipSuccess && !pops.empty()) e = launch_pops(kv.first, pops, &pl);
+            if (e == hipSuccess && !sweeps.empty()) e = launch_sweeps(kv.first, sweeps, &sl, &sw_tasks);
+            if (e == hipSuccess) e = record_after(kv.first, kv.second);
+            for (Req* q : pops) q->batch = (int)((pops.size() + std::max(pl, 1) - 1) / std::max(pl, 1));
+            for (Req* q : sweeps) q->batch = (int)((sw_tasks + std::max(sl, 1) - 1) / std::max(sl, 1));
+            for (Req* q : kv.second) q->err = e;
+        }
+        lk.lock();
+        L.busy = false;
+        // q may go away after this; requests that came in meanwhile are issued by their requesters
+        for (Req* q : batch) q->done.store(true, std::memory_order_release);
+        cv.notify_all();
+    }
+    Dev& device(int d, hipError_t* e) {
+        Dev& D = dev[d];
+        *e = hipSuccess;
+        if (!D.st) {
+            for (auto& s : D.sts)
+                if ((*e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return D;
+            D.st = D.sts[0];
+            D.ring.assign(64, nullptr);
+            for (auto& ev : D.ring)
+                if ((*e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return D;
+        }
+        return D;
+    }
+    hipError_t launch_pops(int d, const vector<Req*>& b, int* launches) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        vector<PopReq> qs;
+        for (Req* q : b) {
+            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
+            qs.push_back(q->pop);
+        }
+        int nl = 0;
+        if ((e = launch_pop_batch_multi(qs.data(), (int)qs.size(), D.st, &nl)) != hipSuccess) return e;
+        *launches = std::max(nl, 1);
+        return hipSuccess;
+    }
+    // Task k of every chunk for k = 0, 1, ...: each session's tasks in order on
+    // the one stream, the sessions side by side (*tasks: session-tasks swept).
+    hipError_t launch_sweeps(int d, const vector<Req*>& b, int* launches, int* tasks) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        vector<SweepReq> qs;
+        int max_m = 0;
+        for (Req* q : b) {
+            if ((e = hipStreamWaitEvent(D.st, q->before, 0)) != hipSuccess) return e;
+            qs.push_back(q->sweep);
+            max_m = std::max(max_m, q->sweep.m);
+            *tasks += q->sweep.m;
+        }
+        for (int k = 0; k < max_m; ++k)
+            if ((e = launch_sweep_multi(qs.data(), (int)qs.size(), k, D.st, launches)) != hipSuccess) return e;
+        return hipSuccess;
+    }
+    // Every request of the step follows its launches on the requester's stream.
+    hipError_t record_after(int d, const vector<Req*>& b) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        hipEvent_t ev = D.ring[D.next++ % D.ring.size()];
+        if ((e = hipEventRecord(ev, D.st)) != hipSuccess) return e;
+        for (Req* q : b) q->after = ev;
+        return hipSuccess;
+    }
+    hipError_t launch_ranks(int d, const vector<Req*>& b) {
+        hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) return e;
+        Dev& D = device(d, &e);
+        if (e != hipSuccess) return e;
+        if (b.size() > D.n_cap) {
+            if (D.h_desc) MemPool::get().give(MemPool::kPinned, D.h_desc, D.cap_bytes, d);
+            if (D.d_desc && (e = hipFree(D.d_desc)) != hipSuccess) return e;
+            D.h_desc = nullptr;
+            D.d_desc = nullptr;
+            D.n_cap = std::max<size_t>(64, b.size());
+            D.h_desc = (RankDesc*)MemPool::get().take(MemPool::kPinned, D.n_cap * sizeof(RankDesc), &D.cap_bytes);
+            if ((e = hipMalloc((void**)&D.d_desc, D.n_cap * sizeof(RankDesc))) != hipSuccess) return e;
+        }
+        int max_nblk = 1;
+        for (size_t i = 0; i < b.size(); ++i) {
+            D.h_desc[i] = b[i]->rank;
+            max_nblk = std::max(max_nblk, b[i]->rank.nblk);
+        }
+        hipStream_t st = b[0]->st;  // a stream of this device; every requester's inputs are in place
+        if ((e = hipMemcpyAsync(D.d_desc, D.h_desc, b.size() * sizeof(RankDesc), hipMemcpyHostToDevice, st)) !=
+            hipSuccess)
+            return e;
+        if ((e = launch_rank_sorted_multi(D.d_desc, (int)b.size(), max_nblk, st)) != hipSuccess) return e;
+        return hipStreamSynchronize(st);  // (h_desc is reused by the next step)
+    }
+};
+
+constexpr uint8_t kBfBackoff = 4;  // pops of a class sent to the general path after a placement-6 miss
+
+// ---------------------------------------------------------------------------
+// Functions defined in one part and called from others
+// ---------------------------------------------------------------------------
+void class_key_format(const Session& S, const TaskClass& c, const vector<Term>& terms, int N, KeyFormat* kf_out,
+                             std::pair<int64_t, int64_t>* range_out);
+uint64_t conf_digest(const kbs::Snapshot& s);
+uint64_t node_spec_digest(const kbs::Snapshot& s);
+void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only = false, int rank = 0,
+                         int world = 1);
+void fail_unsupported(const string& m);
+void apply_results(Session& S, const int32_t* ids, int n, const int32_t* res_node, const int32_t* res_kind,
+                          int32_t* out_node, uint8_t* out_kind);
+bool batchable(const Session& S, int cls);
+void collect_batched(Session& S, const BatchLaunch& L, int* n_done_out, int* stop_out, int32_t* res_node,
+                            int32_t* res_kind);
+void collect_tasks(Session& S, int slot, uint32_t epoch, int m, int* n_done, int* stop, int32_t* node,
+                          int32_t* kind, int32_t* fit4);
+void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_avail, int gang, int mode, int slot,
+                       uint32_t epoch);
+void ev_harvest_all(Session& S);
+void exchange(Session& S, void* dev, int op, int n = 1);
+void fit_allreduce(Session& S, int32_t* fit4);
+void flush_tables(Session& S);
+BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count);
+void ov_quiesce(Session& S);
+void ov_fence(Session& S);
+int place_job(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail, int ready_count,
+                     int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done, int32_t* out_stop);
+int place_job_cancel(Session& S, int64_t ticket);
+int64_t place_job_submit(Session& S, const int32_t* ids, int n, int gang_mode, int min_avail,
+                                int ready_count);
+int place_job_wait(Session& S, int64_t ticket, int32_t* out_node, uint8_t* out_kind, int32_t* out_n_done,
+                          int32_t* out_stop);
+void queue_target(Session& S, int pi, int sign);
+void require_no_tickets(const Session& S);
+void sess_placed(Session& S, int n, int d);
+void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task = false);
+int take_slot(Session& S, uint32_t* epoch);
+void sweep_task(Session& S, int i, int cls, bool defer_visits = false);
+void rank_buffers(Session& S);
+void backfill_run(Session& S);
+int sweep_scores(Session& S, int pod, uint64_t* out_keys);
+double time_sweeps(Session& S, const int32_t* ids, int n);
+double time_rank_multi(Session* const* ss, int n, const int32_t* ids, int reps, int evict, int mapped);
+string fit_error(const HJob& j);
+string gang_close_text(const Session& S);
+int device_count();
+void session_carry(Session& S, const int32_t* ev_pod = nullptr, const uint8_t* ev = nullptr, int64_t n_ev = 0);
+void carry_snapshot(kb_session* ks, const kbs::Snapshot& s, const int32_t* old_pod, const int32_t* old_node);
+int evict_action(kb_session* s, bool preempt, int32_t* out_pod, int32_t* out_node, uint8_t* out_kind,
+                        int64_t cap);
+void reopen_in_place(kb_session* ks, const kbs::Snapshot& s);
+void allocate_run(Session& S);
+void evict_run(Session& S, bool preempt);
+void first_fit(Session& S, const int32_t* ids, int n, int32_t* out_node);
+
+}  // namespace kbhip
+
+struct kb_session {
+    kb_session() { kbhip::g_live_sessions.fetch_add(1, std::memory_order_relaxed); }
+    ~kb_session() {
+        kbhip::g_live_sessions.fetch_sub(1, std::memory_order_relaxed);
+        set_grouped(false);
+    }
+    void set_grouped(bool g) {  // the StepBatcher's count of live grouped sessions
+        if (g != grouped) kbhip::StepBatcher::get().sessions.fetch_add(g ? 1 : -1, std::memory_order_relaxed);
+        grouped = g;
+    }
+    bool grouped = false;
+    kb_session(const kb_session&) = delete;
+    kb_session& operator=(const kb_session&) = delete;
+    kbhip::Session s;
+};
+inline void taint_comm(kb_session* s) {
+    if (s && s->s.comm) s->s.comm_bad = true;
+}
+inline void check_usable(kb_session* s) {
+    if (s && !s->s.broken.empty()) throw kbhip::Error(KBHIP_EINVAL, s->s.broken);
+}
+
+inline void check_log_args(kb_session* s, const int32_t* out_pod, const int32_t* out_node, const uint8_t* out_kind,
+                           int64_t cap) {
+    if (!s) throw kbhip::Error(KBHIP_EINVAL, "null session");
+    if (s->s.encode_only) throw kbhip::Error(KBHIP_EINVAL, "encode-only session has no device state");
+    if (cap < 0 || (cap > 0 && (!out_pod || !out_node || !out_kind)))
+        throw kbhip::Error(KBHIP_EINVAL, "null output array with cap > 0");
+}
+
+#define ABI_GUARD(...)                                       \
+    try {                                                    \
+        __VA_ARGS__                                          \
+    } catch (kbhip::Error & e) {                             \
+        kbhip::g_err = e.what();                             \
+        return e.code;                                       \
+    } catch (std::exception & e) {                           \
+        kbhip::g_err = e.what();                             \
+        return KBHIP_EINVAL;                                 \
+    } catch (...) {                                          \
+        kbhip::g_err = "unknown error";                      \
+        return KBHIP_EINVAL;                                 \
+    }
+// The same for calls on a session: a failure while the session's RCCL
+// communicator is connected taints it (aborted at close, never pooled).
+#define ABI_GUARD_S(sp, ...)                                 \
+    try {                                                    \
+        check_usable(sp);                                    \
+        __VA_ARGS__                                          \
+    } catch (kbhip::Error & e) {                             \
+        kbhip::g_err = e.what();                             \
+        taint_comm(sp);                                      \
+        return e.code;                                       \
+    } catch (std::exception & e) {                           \
+        kbhip::g_err = e.what();                             \
+        taint_comm(sp);                                      \
+        return KBHIP_EINVAL;                                 \
+    } catch (...) {                                          \
+        kbhip::g_err = "unknown error";                      \
+        taint_comm(sp);                                      \
+        return KBHIP_EINVAL;                                 \
+    }
 
