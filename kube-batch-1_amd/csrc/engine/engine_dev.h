@@ -24,6 +24,18 @@ __device__ __forceinline__ uint64_t eng_now() { return __builtin_amdgcn_s_memrea
             (A).tl[(size_t)((p) % kEngTlSlots) * kEngTlEvents + (ev)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 
+// Polling shape (tuning builds, profiles/r06_poll.sh): sc1 loads in flight per
+// granule poll, and the s_sleep between polls (64-cycle units; 0 = none).
+#ifndef KBHIP_POLL_DEPTH
+#define KBHIP_POLL_DEPTH 8
+#endif
+#ifndef KBHIP_POLL_SLEEP
+#define KBHIP_POLL_SLEEP 1
+#endif
+__device__ __forceinline__ void eng_pause() {
+    if constexpr (KBHIP_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(KBHIP_POLL_SLEEP);
+}
+
 // A bounded wait: call tick() once per unsuccessful poll; false = give up
 // (timed out: the error is recorded; or another block recorded one).
 struct EngWait {
@@ -33,7 +45,7 @@ struct EngWait {
     uint32_t it = 0;
     __device__ EngWait(EngCtl* c, uint64_t l) : ctl(c), limit(l) {}
     __device__ __forceinline__ bool tick(uint32_t code = kEngErrWait) {
-        __builtin_amdgcn_s_sleep(1);
+        eng_pause();
         if ((++it & 63) != 0) return true;
         const uint64_t now = eng_now();
         if (!t0) t0 = now;
@@ -151,13 +163,13 @@ __device__ __forceinline__ bool eng_wait_done(EngCtl* ctl, uint32_t want) {
 // it in flight, one issued per check, so that the wave sees the store about
 // a round trip / kPollDepth after it lands rather than up to two round trips
 // (every lane loads the same word: one request).  false: gave up (EngWait).
-constexpr int kPollDepth = 8;
+constexpr int kPollDepth = KBHIP_POLL_DEPTH;
 __device__ __forceinline__ bool eng_poll_tag(EngCtl* ctl, const uint64_t* w, uint32_t q, uint64_t limit) {
     uint64_t v[kPollDepth];
 #pragma unroll
     for (int i = 0; i < kPollDepth; ++i) {
         v[i] = ld_sc1(w);
-        __builtin_amdgcn_s_sleep(1);
+        eng_pause();
     }
     EngWait wt(ctl, limit);
     for (;;) {
@@ -177,7 +189,7 @@ __device__ __forceinline__ bool eng_poll_tags(EngCtl* ctl, const uint64_t* w, ui
 #pragma unroll
     for (int i = 0; i < kPollDepth; ++i) {
         v[i] = w ? ld_sc1(w) : ((uint64_t)q << 32);
-        __builtin_amdgcn_s_sleep(1);
+        eng_pause();
     }
     bool seen = false;
     EngWait wt(ctl, limit);

@@ -204,3 +204,39 @@ def test_carry_snapshot_updated_pod_mapped(engine, kbgen_mod, tmp_path, field):
     with engine.Session(p2) as f:
         exp = f.allocate()
     assert all(np.array_equal(a, b) for a, b in zip(got, exp))
+
+
+@pytest.mark.parametrize("variant", ["keyless", "podaff"])
+def test_carry_snapshot_c3_affinity_arrivals(engine, oracle_mod, kbgen_mod, tmp_path, variant):
+    """C3-shaped carry at 2k nodes: zone anti-affinity,
+    topology-keyless nodes, required pod affinity (podaff); after allocate the
+    cache model's next snapshot brings arrivals with hostname anti-affinity
+    (the affinity shape of the events above, so the session re-opens in
+    place), deletions, completions, node and PodGroup updates.  The carried
+    session's allocate equals the hoisted restatement's on that snapshot (the
+    faithful one, pinned against it on small instances, would take about half
+    an hour at this size) and a session opened fresh on it."""
+    opts = dict(keyless=0.2) if variant == "keyless" else dict(keyless=0.1, pod_affinity=0.15)
+    c = kbgen_mod.gen_c3(seed=9700, n_nodes=2000, n_pending=3000, **opts)
+    if "default" not in {q.name for q in c.queues}:
+        c.add_queue("default")
+    p1 = c.write(str(tmp_path / "c3a.kbs"))
+    old_pods = sorted(c.pods, key=lambda q: q.uid)
+    old_nodes = sorted(n.name for n in c.nodes)
+    rng = np.random.default_rng(9701)
+    with engine.Session(p1) as s:
+        s.allocate()
+        status, node = s.table("pod_status").copy(), s.table("pod_node").copy()
+        c2 = snapshot_after_session(clone(c), status, node)
+        M = CacheModel(c2)
+        _events(M, rng, 2, 97, {q.uid: int(status[i]) for i, q in enumerate(old_pods)})
+        op, on = index_maps(old_pods, old_nodes, c2)
+        p2 = c2.write(str(tmp_path / "c3b.kbs"))
+        s.carry_snapshot(p2, op, on)
+        pod, nd, kind = s.allocate()
+    got = [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)]
+    assert len(got) > 500
+    assert got == oracle_mod.fast_allocate(p2, threads=8).as_list()
+    with engine.Session(p2) as s:
+        pod, nd, kind = s.allocate()
+    assert got == [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)]
