@@ -26,11 +26,15 @@ __device__ __forceinline__ uint64_t eng_now() { return __builtin_amdgcn_s_memrea
 
 // Polling shape (tuning builds, profiles/r06_poll.sh): sc1 loads in flight per
 // granule poll, and the s_sleep between polls (64-cycle units; 0 = none).
+// Measured at C4 (profiles/r06p_*, r06q_*: device period per pop): 8 loads in
+// flight / sleep 1 (r05) 8.25-8.28 us, 2 / 0 8.05-8.08, 1 / 1 7.98-8.02,
+// 1 / 2 8.00, 1 / 8 8.15: the pollers' own loads slowed the hand-offs they
+// wait for (every poll is a request to the line's home L2 channel).
 #ifndef KBHIP_POLL_DEPTH
-#define KBHIP_POLL_DEPTH 8
+#define KBHIP_POLL_DEPTH 1
 #endif
 #ifndef KBHIP_POLL_SLEEP
-#define KBHIP_POLL_SLEEP 1
+#define KBHIP_POLL_SLEEP 2
 #endif
 __device__ __forceinline__ void eng_pause() {
     if constexpr (KBHIP_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(KBHIP_POLL_SLEEP);
@@ -160,9 +164,8 @@ __device__ __forceinline__ bool eng_wait_done(EngCtl* ctl, uint32_t want) {
 }
 
 // Until the tag (high half) of the granule *w reads q: kPollDepth sc1 loads of
-// it in flight, one issued per check, so that the wave sees the store about
-// a round trip / kPollDepth after it lands rather than up to two round trips
-// (every lane loads the same word: one request).  false: gave up (EngWait).
+// it in flight, one issued per check (every lane loads the same word: one
+// request).  false: gave up (EngWait).
 constexpr int kPollDepth = KBHIP_POLL_DEPTH;
 __device__ __forceinline__ bool eng_poll_tag(EngCtl* ctl, const uint64_t* w, uint32_t q, uint64_t limit) {
     uint64_t v[kPollDepth];
