@@ -1189,4 +1189,31 @@ void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_on
     S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Option "cu_split" (rehearsals of the node-sharded path on one GPU, DESIGN.md
+// §6): the session's streams are replaced by streams restricted to CUs
+// [part * C / parts, (part + 1) * C / parts) of the device's C, so that W
+// ranks sharing one GPU each get their own share of the chip as W GPUs would.
+void cu_split(Session& S, int part, int parts) {
+    if (parts < 1 || part < 0 || part >= parts) throw Error(KBHIP_EINVAL, "cu_split: part must be in [0, parts)");
+    if (S.encode_only || !S.stream) throw Error(KBHIP_EINVAL, "cu_split: the session has no streams");
+    ov_quiesce(S);
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, S.device));
+    if (cus < parts) throw Error(KBHIP_EINVAL, "cu_split: more parts than CUs");
+    vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int c = part * cus / parts; c < (part + 1) * cus / parts; ++c) mask[c / 32] |= 1u << (c % 32);
+    HIPCHK(hipDeviceSynchronize());
+    hipStream_t fresh[kMaxDep + 1] = {};
+    for (int k = 0; k <= kMaxDep; ++k)
+        HIPCHK(hipExtStreamCreateWithCUMask(&fresh[k], (uint32_t)mask.size(), mask.data()));
+    for (int k = 0; k <= kMaxDep; ++k) {
+        hipStream_t old = k == 0 ? S.stream : S.ov_streams[k];
+        if (S.cu_masked) (void)hipStreamDestroy(old);
+        else MemPool::get().give_stream(old, S.device);
+        if (k == 0) S.stream = fresh[0];
+        S.ov_streams[k] = fresh[k];
+    }
+    S.cu_masked = true;
+}
+
 }  // namespace kbhip

@@ -104,6 +104,11 @@ int kbhip_set_option(kb_session* s, const char* key, int64_t value) {
         kbhip::require_no_tickets(s->s);  // options change how queued pops would run
         if (std::strcmp(key, "batched") == 0) s->s.batched = value != 0;
         else if (std::strcmp(key, "time_every") == 0) s->s.time_every = value;
+        else if (std::strcmp(key, "cu_split") == 0) {  // value = part * 256 + parts (rehearsals)
+            kbhip::require_no_tickets(s->s);
+            HIPCHK(hipSetDevice(s->s.device));
+            kbhip::cu_split(s->s, (int)(value >> 8), (int)(value & 0xff));
+        }
         else if (std::strcmp(key, "sweep_variant") == 0) {  // kbhip_sweep_scores' kernel shape (tuning)
             if (value < 0 || value > 6) throw kbhip::Error(KBHIP_EINVAL, "sweep_variant must be 0..6");
             kbhip::set_sweep_variant((int)value);

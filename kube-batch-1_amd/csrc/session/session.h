@@ -733,6 +733,7 @@ struct Session {
     Mailbox* mbox_peer[kMaxWorld] = {};        // and every rank's as mapped here (own included)
     uint32_t mbox_seq = 0;                     // sequence number of the last batched pop sent
     uint32_t sh_chained_seq = 0;               // the last overlapped shard pop (k_shard_sweep_ov), 0: none
+    bool cu_masked = false;  // option "cu_split": the streams run on a share of the CUs (rehearsals)
     bool shard_overlap = false;                // option "shard_overlap": overlapped shard pops (with "overlap" > 0;
                                                // off: measured slower in the one-chip rehearsal)
     bool chain_fence = false;                  // device work ran on the session stream after the last drain
@@ -795,8 +796,14 @@ struct Session {
         if (h_rank) MemPool::get().give(MemPool::kPinned, h_rank, h_rank_cap, device);
         h_rank = nullptr;
         h_out = nullptr;
-        for (int k = 1; k <= kMaxDep; ++k) MemPool::get().give_stream(ov_streams[k], device);
-        MemPool::get().give_stream(stream, device);
+        if (cu_masked) {  // streams of option "cu_split" are this session's own
+            for (int k = 1; k <= kMaxDep; ++k)
+                if (ov_streams[k]) (void)hipStreamDestroy(ov_streams[k]);
+            if (stream) (void)hipStreamDestroy(stream);
+        } else {
+            for (int k = 1; k <= kMaxDep; ++k) MemPool::get().give_stream(ov_streams[k], device);
+            MemPool::get().give_stream(stream, device);
+        }
         for (auto& st : ov_streams) st = nullptr;
         stream = nullptr;
         for (auto& b : b_cols) b.release();
@@ -1069,6 +1076,7 @@ constexpr uint8_t kBfBackoff = 4;  // pops of a class sent to the general path a
 // ---------------------------------------------------------------------------
 // Functions defined in one part and called from others
 // ---------------------------------------------------------------------------
+void cu_split(Session& S, int part, int parts);
 void class_key_format(const Session& S, const TaskClass& c, const vector<Term>& terms, int N, KeyFormat* kf_out,
                              std::pair<int64_t, int64_t>* range_out);
 uint64_t conf_digest(const kbs::Snapshot& s);

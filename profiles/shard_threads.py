@@ -7,9 +7,12 @@ time-slicing between processes — what W GPUs over xGMI see, minus the link
 latency, with the W sweeps sharing one chip.  Every rank's placement log is
 checked against the C4 digest (tests/golden/fullsize.json).
 
-usage (on the box, repo root): python3 profiles/shard_threads.py <tag> [W] [sessions] [shard_overlap]
+usage (on the box, repo root): python3 profiles/shard_threads.py <tag> [W] [sessions] [shard_overlap] [cu_split]
 (shard_overlap 1, the default: a shard's sweep of pop e beside pop e-1's
-placement; 0: sweep, exchange and placement one after another)
+placement; 0: sweep, exchange and placement one after another; cu_split 1:
+rank r's streams run on CUs [r C / W, (r + 1) C / W) only — option
+"cu_split" — so that each rank has its own share of the chip, as W GPUs
+would, instead of all ranks' kernels spreading over every CU)
 """
 import hashlib
 import json
@@ -72,6 +75,7 @@ def main():
     w = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     sessions = int(sys.argv[3]) if len(sys.argv) > 3 else 3
     shov = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+    cus = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     cache = os.environ.get("KBHIP_BENCH_CACHE", "/tmp/kbhip_bench")
     os.makedirs(cache, exist_ok=True)
     path = os.path.join(cache, f"c4_100000_800000_{kbgen.BASE_SEED + 4}.kbs")
@@ -87,6 +91,8 @@ def main():
         def run(rank):
             t0 = time.perf_counter()
             s = kbhip.ShardedSession(buf, 0, rank, w)
+            if cus:
+                s.set_option("cu_split", rank * 256 + w)
             s.connect_host(red.fn(rank))
             s.connect_mailbox(gat.fn(rank))
             s.set_option("shard_overlap", shov)
@@ -111,7 +117,7 @@ def main():
         print(json.dumps({"session": it, "ranks": res}), file=sys.stderr, flush=True)
     out = {"what": f"C4 (100k nodes x 1M pods) node-sharded over {w} rank threads of one process on one MI355X, "
                    "peer-mailbox exchange (kbhip_shard_connect_mailbox)",
-           "ranks": w, "sessions": sessions, "shard_overlap": shov,
+           "ranks": w, "sessions": sessions, "shard_overlap": shov, "cu_split": cus,
            "all_digests_ok": all(r["digest_ok"] for res in rows for r in res),
            "p50_session_ms": statistics.median(max(r["session_s"] for r in res) for res in rows) * 1e3,
            "p50_allocate_ms": statistics.median(max(r["allocate_s"] for r in res) for res in rows) * 1e3,
@@ -121,7 +127,7 @@ def main():
            "one_exchange_per_pop": all(r["collectives"] == r["pops"] for res in rows for r in res),
            "last": rows[-1]}
     os.makedirs("gpurun_out", exist_ok=True)
-    with open(f"gpurun_out/{tag}_shard_threads_w{w}_ov{shov}.json", "w") as f:
+    with open(f"gpurun_out/{tag}_shard_threads_w{w}_ov{shov}_cu{cus}.json", "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
 

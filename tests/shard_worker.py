@@ -31,6 +31,9 @@ def main():
     with kbhip.ShardedSession(path, 0, rank, world) as s:
         mark("session open")
         exchange = os.environ.get("KBHIP_TEST_EXCHANGE", "host")
+        if exchange.endswith("_cu"):  # this rank's streams on its own share of the CUs (option cu_split)
+            exchange = exchange[:-3]
+            s.set_option("cu_split", rank * 256 + world)
         s.connect_host(kbhip.torch_exchange(), kbhip.torch_gather() if batched and exchange == "host" else None)
         if batched and exchange in ("mailbox", "mailbox_serial"):  # batched pops through the peer mailboxes
             s.connect_mailbox(kbhip.torch_gather())

@@ -111,12 +111,13 @@ def test_sharded_close_messages_gpu(engine, oracle_mod, kbgen_mod, tmp_path, see
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("exchange", ["host", "mailbox", "mailbox_serial"])
+@pytest.mark.parametrize("exchange", ["host", "mailbox", "mailbox_serial", "mailbox_cu"])
 @pytest.mark.parametrize("seed", range(8))
 def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed, exchange):
     """Batched-path features only (no pod affinity / backfill): every pop is
     one exchange — a host all-gather, or the peer mailboxes (kernels only;
-    a shard's sweep of the next pop beside the placement, or serial)."""
+    a shard's sweep of the next pop beside the placement, or serial; _cu:
+    each rank's streams on its own share of the CUs, option cu_split)."""
     from test_gpu_parity import NO_POD_AFFINITY
     feats = tuple(f for f in NO_POD_AFFINITY if f != "backfill")
     c = kbgen_mod.gen_random(2400 + seed, n_nodes=10 + seed * 7, n_jobs=8, max_tasks=8, features=feats,
