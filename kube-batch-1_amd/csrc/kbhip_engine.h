@@ -36,7 +36,10 @@ constexpr int kEngMaxGroups = 8;  // merger blocks
 constexpr int kEngListWords = 136;  // a list: 128 tagged keys + 4 tagged counts (+ pad), 17 lines
 constexpr int kEngMaxNpb = 8192;  // nodes per worker block
 constexpr int kEngWorkersMax = 512;
-constexpr int kEngCandCopies = 8;  // the candidate granules' copies (the workers' polls spread over them)
+#ifndef KBHIP_CAND_COPIES
+#define KBHIP_CAND_COPIES 8  // (tuning builds: host and device must agree, so the whole library)
+#endif
+constexpr int kEngCandCopies = KBHIP_CAND_COPIES;  // the candidate granules' copies (the workers' polls spread over them)
 
 // The final merger's package for pop p (slot p % kEngSlots): the top 128
 // keys of the group lists with every entry's node row and its node-affinity
