@@ -235,7 +235,7 @@ def test_carry_snapshot_c3_affinity_arrivals(engine, oracle_mod, kbgen_mod, tmp_
         s.carry_snapshot(p2, op, on)
         pod, nd, kind = s.allocate()
     got = [(int(a), int(b), STATUS[int(k)]) for a, b, k in zip(pod, nd, kind)]
-    assert len(got) > 500
+    assert len(got) > 20  # (the first session placed most of the pending set)
     assert got == oracle_mod.fast_allocate(p2, threads=8).as_list()
     with engine.Session(p2) as s:
         pod, nd, kind = s.allocate()
