@@ -25,1401 +25,11 @@
  * pods bound to nodes that are not in the snapshot (the reference's
  * predicates plugin would dereference a nil node, predicates.go:124-125).
  */
-#include <algorithm>
-#include <cmath>
-#include <cstdint>
-#include <cstring>
-#include <deque>
-#include <functional>
-#include <map>
-#include <memory>
-#include <set>
-#include <stdexcept>
-#include <string>
-#include <vector>
+#include "kbref.h"
 
-#include "../include/kbsnap.h"
+#include <functional>
 
 namespace ref {
-
-using std::map;
-using std::string;
-using std::vector;
-
-/* ------------------------------------------------------------------------ */
-/* k8s object model subset                                                   */
-/* ------------------------------------------------------------------------ */
-enum Op { OpIn = 0, OpNotIn = 1, OpExists = 2, OpDoesNotExist = 3, OpGt = 4, OpLt = 5, OpEquals = 6,
-          OpInvalid = 15 };
-
-struct Requirement {  // labels.Requirement (apimachinery/pkg/labels/selector.go)
-    string key;
-    int op;
-    vector<string> values;
-};
-
-struct LabelSelector {  // metav1.LabelSelector
-    map<string, string> ml;
-    vector<Requirement> me;
-};
-
-struct NodeSelectorTerm {
-    vector<Requirement> expr, fields;
-};
-
-struct PodAffinityTerm {
-    std::shared_ptr<LabelSelector> sel;  // nil-able
-    vector<string> namespaces;
-    string topologyKey;
-};
-
-struct WeightedPodAffinityTerm {
-    int32_t weight;
-    PodAffinityTerm term;
-};
-
-struct Affinity {
-    bool hasNA = false, hasNAReq = false, hasPA = false, hasPAA = false;
-    vector<NodeSelectorTerm> naReq;
-    vector<std::pair<int32_t, NodeSelectorTerm>> naPref;
-    vector<PodAffinityTerm> paReq, paaReq;
-    vector<WeightedPodAffinityTerm> paPref, paaPref;
-};
-
-struct ContainerPort {
-    string ip, proto;
-    int32_t port;
-};
-
-struct Container {
-    int64_t cpu = 0, mem = 0, gpu = 0;
-    int has = 0;  // KBS_HAS_* : key present in Requests
-    vector<ContainerPort> ports;
-};
-
-struct Toleration {
-    string key, op, value, effect;
-};
-
-struct Taint {
-    string key, value, effect;
-};
-
-struct Pod {
-    int index = 0;
-    string uid, name, ns;
-    map<string, string> labels;
-    string nodeName;  // Spec.NodeName
-    int phase = KBS_PENDING;
-    bool deleting = false;
-    bool detached = false;  // p_detached (kbsnap.h): in its job, off its node's task list
-    int32_t priority = 0;
-    int64_t ts = 0;
-    bool backfill = false;
-    string priorityClassName;  // Spec.PriorityClassName (conformance.go:40-45)
-    vector<Container> containers, initContainers;
-    map<string, string> nodeSelector;
-    vector<Toleration> tolerations;
-    std::shared_ptr<Affinity> affinity;
-    int job = -1;  // snapshot job row
-};
-
-struct KNode {  // v1.Node
-    int index = 0;
-    string name;
-    map<string, string> labels;
-    vector<Taint> taints;
-    bool unschedulable = false;
-    int64_t a_cpu, a_mem, a_gpu, a_pods, c_cpu, c_mem, c_gpu, c_pods;
-};
-
-/* ------------------------------------------------------------------------ */
-/* kube-batch api (pkg/scheduler/api)                                        */
-/* ------------------------------------------------------------------------ */
-static const double minMilliCPU = 10, minMilliGPU = 10, minMemory = 10 * 1024 * 1024;  // resource_info.go:54-56
-
-struct Resource {  // resource_info.go:26-33
-    double MilliCPU = 0, Memory = 0, MilliGPU = 0;
-    int MaxTaskNum = 0;
-    Resource& Add(const Resource& r) { MilliCPU += r.MilliCPU; Memory += r.Memory; MilliGPU += r.MilliGPU; return *this; }
-    Resource& Sub(const Resource& r) { MilliCPU -= r.MilliCPU; Memory -= r.Memory; MilliGPU -= r.MilliGPU; return *this; }
-    Resource& Multi(double ratio) { MilliCPU *= ratio; Memory *= ratio; MilliGPU *= ratio; return *this; }
-    bool IsEmpty() const { return MilliCPU < minMilliCPU && Memory < minMemory && MilliGPU < minMilliGPU; }  // :75-77
-    bool Less(const Resource& rr) const {  // :156-158 — strict in every dimension
-        return MilliCPU < rr.MilliCPU && Memory < rr.Memory && MilliGPU < rr.MilliGPU;
-    }
-    bool LessEqual(const Resource& rr) const {  // :164-168
-        return (MilliCPU < rr.MilliCPU || std::fabs(rr.MilliCPU - MilliCPU) < minMilliCPU) &&
-               (Memory < rr.Memory || std::fabs(rr.Memory - Memory) < minMemory) &&
-               (MilliGPU < rr.MilliGPU || std::fabs(rr.MilliGPU - MilliGPU) < minMilliGPU);
-    }
-    void SetMaxResource(const Resource& rr) {  // :114-128
-        if (rr.MilliCPU > MilliCPU) MilliCPU = rr.MilliCPU;
-        if (rr.Memory > Memory) Memory = rr.Memory;
-        if (rr.MilliGPU > MilliGPU) MilliGPU = rr.MilliGPU;
-    }
-    double Get(int rn) const { return rn == 0 ? MilliCPU : rn == 1 ? Memory : MilliGPU; }
-};
-
-static Resource MinRes(const Resource& l, const Resource& r) {  // api/helpers/helpers.go:25-33
-    Resource res;
-    res.MilliCPU = std::fmin(l.MilliCPU, r.MilliCPU);
-    res.MilliGPU = std::fmin(l.MilliGPU, r.MilliGPU);
-    res.Memory = std::fmin(l.Memory, r.Memory);
-    return res;
-}
-
-static double Share(double l, double r) {  // helpers.go:35-48
-    if (r == 0) return l == 0 ? 0 : 1;
-    return l / r;
-}
-
-enum TaskStatus {  // types.go:22-61
-    Pending = 1 << 0, AllocatedOverBackfill = 1 << 1, Allocated = 1 << 2, Pipelined = 1 << 3,
-    Binding = 1 << 4, Bound = 1 << 5, Running = 1 << 6, Releasing = 1 << 7, Succeeded = 1 << 8,
-    Failed = 1 << 9, Unknown = 1 << 10
-};
-static const int AllocatedStatusesList[] = {Bound, Binding, Running, Allocated};  // types.go:82-84
-static bool AllocatedStatus(int s) { return s == Bound || s == Binding || s == Running || s == Allocated; }
-
-enum JobReadiness { Ready = 1, AlmostReady = 2, NotReady = 4 };
-
-static int getTaskStatus(const Pod& p) {  // helpers.go:35-61
-    switch (p.phase) {
-        case KBS_RUNNING: return p.deleting ? Releasing : Running;
-        case KBS_PENDING:
-            if (p.deleting) return Releasing;
-            if (p.nodeName.empty()) return Pending;
-            return Bound;
-        case KBS_UNKNOWN: return Unknown;
-        case KBS_SUCCEEDED: return Succeeded;
-        case KBS_FAILED: return Failed;
-    }
-    return Unknown;
-}
-
-static Resource ContainerRes(const Container& c) {  // NewResource(container.Resources.Requests)
-    Resource r;
-    r.MilliCPU = (double)c.cpu;
-    r.Memory = (double)c.mem;
-    r.MilliGPU = (double)c.gpu;
-    return r;
-}
-
-static Resource GetPodResourceWithoutInitContainers(const Pod& p) {  // pod_info.go:64-71
-    Resource r;
-    for (auto& c : p.containers) r.Add(ContainerRes(c));
-    return r;
-}
-static Resource GetPodResourceRequest(const Pod& p) {  // pod_info.go:51-60
-    Resource r = GetPodResourceWithoutInitContainers(p);
-    for (auto& c : p.initContainers) r.SetMaxResource(ContainerRes(c));
-    return r;
-}
-
-struct TaskInfo {  // job_info.go:36-58
-    int pod = -1;  // index of pod (also the pinned map-iteration key)
-    string uid;
-    int job = -1;  // session job slot (-1 = not in a session job)
-    string jobUID;
-    string name, ns;
-    Resource Resreq, InitResreq;
-    string NodeName;
-    int Status = Pending;
-    int32_t Priority = 1;
-    Pod* P = nullptr;
-    bool IsBackfill = false;
-};
-
-struct NodeInfo {  // node_info.go:27-45
-    string Name;
-    KNode* Node = nullptr;
-    Resource Releasing, Idle, Used, Backfilled, Allocatable, Capability;
-    map<int, TaskInfo> Tasks;  // keyed by pod index: pinned map order
-
-    void init(KNode* n) {  // NewNodeInfo(node) :62-75
-        Name = n->name;
-        Node = n;
-        Idle.MilliCPU = (double)n->a_cpu; Idle.Memory = (double)n->a_mem; Idle.MilliGPU = (double)n->a_gpu;
-        Idle.MaxTaskNum = (int)n->a_pods;
-        Allocatable = Idle;
-        Capability.MilliCPU = (double)n->c_cpu; Capability.Memory = (double)n->c_mem;
-        Capability.MilliGPU = (double)n->c_gpu; Capability.MaxTaskNum = (int)n->c_pods;
-    }
-    bool AddTask(const TaskInfo& task) {  // :113-145
-        if (Tasks.count(task.pod)) return false;
-        TaskInfo ti = task;  // task.Clone()
-        if (Node) {
-            if (task.IsBackfill) Backfilled.Add(task.Resreq);
-            switch (ti.Status) {
-                case ::ref::Releasing: Releasing.Add(ti.Resreq); Idle.Sub(ti.Resreq); break;
-                case ::ref::Pipelined: Releasing.Sub(ti.Resreq); break;
-                default: Idle.Sub(ti.Resreq);
-            }
-            Used.Add(ti.Resreq);
-        }
-        Tasks[task.pod] = ti;
-        return true;
-    }
-    bool RemoveTask(const TaskInfo& ti) {  // :147-177
-        auto it = Tasks.find(ti.pod);
-        if (it == Tasks.end()) return false;
-        const TaskInfo& task = it->second;
-        if (Node) {
-            if (task.IsBackfill) Backfilled.Sub(task.Resreq);
-            switch (task.Status) {
-                case ::ref::Releasing: Releasing.Sub(task.Resreq); Idle.Add(task.Resreq); break;
-                case ::ref::Pipelined: Releasing.Add(task.Resreq); break;
-                default: Idle.Add(task.Resreq);
-            }
-            Used.Sub(task.Resreq);
-        }
-        Tasks.erase(it);
-        return true;
-    }
-    bool UpdateTask(const TaskInfo& ti) {  // :179-185
-        if (!RemoveTask(ti)) return false;
-        return AddTask(ti);
-    }
-    vector<Pod*> Pods() const {  // :201-207
-        vector<Pod*> v;
-        for (auto& kv : Tasks) v.push_back(kv.second.P);
-        return v;
-    }
-    Resource GetAccessibleResource() {  // :209-211 — mutates Idle (Appendix A.1)
-        Idle.Add(Backfilled);
-        return Idle;
-    }
-};
-
-struct JobInfo {  // job_info.go:140-167
-    string UID, Name, Namespace, Queue;
-    int32_t Priority = 0;
-    int32_t MinAvailable = 0;
-    map<int, map<int, TaskInfo*>> TaskStatusIndex;  // status -> pod index -> task
-    map<int, TaskInfo*> Tasks;
-    Resource Allocated, TotalRequest;
-    int64_t CreationTimestamp = 0;
-    map<string, Resource> NodesFitDelta;
-    int slot = 0;
-
-    void addTaskIndex(TaskInfo* ti) { TaskStatusIndex[ti->Status][ti->pod] = ti; }
-    void AddTaskInfo(TaskInfo* ti) {  // :239-249
-        Tasks[ti->pod] = ti;
-        addTaskIndex(ti);
-        Priority = ti->P->priority;
-        TotalRequest.Add(ti->Resreq);
-        if (AllocatedStatus(ti->Status)) Allocated.Add(ti->Resreq);
-    }
-    void deleteTaskIndex(TaskInfo* ti) {
-        auto it = TaskStatusIndex.find(ti->Status);
-        if (it != TaskStatusIndex.end()) {
-            it->second.erase(ti->pod);
-            if (it->second.empty()) TaskStatusIndex.erase(it);
-        }
-    }
-    void DeleteTaskInfo(TaskInfo* ti) {  // :276-292
-        auto it = Tasks.find(ti->pod);
-        if (it == Tasks.end()) return;
-        TaskInfo* task = it->second;
-        TotalRequest.Sub(task->Resreq);
-        if (AllocatedStatus(task->Status)) Allocated.Sub(task->Resreq);
-        Tasks.erase(it);
-        deleteTaskIndex(task);
-    }
-    void UpdateTaskStatus(TaskInfo* task, int status) {  // :251-264
-        DeleteTaskInfo(task);
-        task->Status = status;
-        AddTaskInfo(task);
-    }
-    int count(int status) const {
-        auto it = TaskStatusIndex.find(status);
-        return it == TaskStatusIndex.end() ? 0 : (int)it->second.size();
-    }
-    int GetReadiness() const {  // :374-388
-        int allocated = 0;
-        for (int s : AllocatedStatusesList) allocated += count(s);
-        if (allocated >= MinAvailable) return Ready;
-        if (allocated + count(AllocatedOverBackfill) >= MinAvailable) return AlmostReady;
-        return NotReady;
-    }
-};
-
-struct QueueInfo {
-    string UID, Name;
-    int32_t Weight = 1;
-    int64_t ts = 0;
-    int slot = 0;
-};
-
-/* ------------------------------------------------------------------------ */
-/* Go container/heap + util.PriorityQueue (util/priority_queue.go)           */
-/* ------------------------------------------------------------------------ */
-template <typename T>
-struct PriorityQueue {
-    vector<T*> items;
-    std::function<bool(T*, T*)> lessFn;
-    bool Less(int i, int j) { return lessFn(items[i], items[j]); }
-    void Swap(int i, int j) { std::swap(items[i], items[j]); }
-    void up(int j) {
-        for (;;) {
-            int i = (j - 1) / 2;  // parent
-            if (i == j || !Less(j, i)) break;
-            Swap(i, j);
-            j = i;
-        }
-    }
-    bool down(int i0, int n) {
-        int i = i0;
-        for (;;) {
-            int j1 = 2 * i + 1;
-            if (j1 >= n || j1 < 0) break;
-            int j = j1;
-            int j2 = j1 + 1;
-            if (j2 < n && Less(j2, j1)) j = j2;
-            if (!Less(j, i)) break;
-            Swap(i, j);
-            i = j;
-        }
-        return i > i0;
-    }
-    void Push(T* x) {
-        items.push_back(x);
-        up((int)items.size() - 1);
-    }
-    T* Pop() {
-        if (items.empty()) return nullptr;
-        int n = (int)items.size() - 1;
-        Swap(0, n);
-        down(0, n);
-        T* it = items.back();
-        items.pop_back();
-        return it;
-    }
-    bool Empty() const { return items.empty(); }
-    int Len() const { return (int)items.size(); }
-};
-
-/* ------------------------------------------------------------------------ */
-/* labels / selectors (apimachinery/pkg/labels/selector.go)                  */
-/* ------------------------------------------------------------------------ */
-static bool parseInt64(const string& s, int64_t* out) {  // strconv.ParseInt(s, 10, 64)
-    if (s.empty()) return false;
-    size_t i = 0;
-    bool neg = false;
-    if (s[0] == '+' || s[0] == '-') {
-        neg = s[0] == '-';
-        i = 1;
-        if (s.size() == 1) return false;
-    }
-    unsigned long long v = 0;
-    const unsigned long long lim = neg ? 9223372036854775808ULL : 9223372036854775807ULL;
-    for (; i < s.size(); ++i) {
-        char ch = s[i];
-        if (ch < '0' || ch > '9') return false;
-        unsigned d = (unsigned)(ch - '0');
-        if (v > (lim - d) / 10) return false;
-        v = v * 10 + d;
-    }
-    *out = neg ? (int64_t)(0 - v) : (int64_t)v;
-    return true;
-}
-
-typedef map<string, string> Labels;
-
-static bool hasValue(const Requirement& r, const string& v) {
-    for (auto& s : r.values) if (s == v) return true;
-    return false;
-}
-
-static bool RequirementMatches(const Requirement& r, const Labels& ls) {  // selector.go:192-236
-    auto it = ls.find(r.key);
-    bool has = it != ls.end();
-    switch (r.op) {
-        case OpIn:
-        case OpEquals:
-            if (!has) return false;
-            return hasValue(r, it->second);
-        case OpNotIn:
-            if (!has) return true;
-            return !hasValue(r, it->second);
-        case OpExists: return has;
-        case OpDoesNotExist: return !has;
-        case OpGt:
-        case OpLt: {
-            if (!has) return false;
-            int64_t lv, rv = 0;
-            if (!parseInt64(it->second, &lv)) return false;
-            if (r.values.size() != 1) return false;
-            for (auto& s : r.values) if (!parseInt64(s, &rv)) return false;
-            return (r.op == OpGt && lv > rv) || (r.op == OpLt && lv < rv);
-        }
-    }
-    return false;
-}
-
-/* labels.NewRequirement validation (selector.go:134-170), without the
- * key/value syntax checks (documented limitation). */
-static bool ValidRequirement(const Requirement& r) {
-    switch (r.op) {
-        case OpIn:
-        case OpNotIn: return !r.values.empty();
-        case OpEquals: return r.values.size() == 1;
-        case OpExists:
-        case OpDoesNotExist: return r.values.empty();
-        case OpGt:
-        case OpLt: {
-            if (r.values.size() != 1) return false;
-            int64_t v;
-            return parseInt64(r.values[0], &v);
-        }
-    }
-    return false;
-}
-
-/* A compiled selector: kind 0 = internal (AND of reqs), 1 = Nothing. */
-struct Selector {
-    bool nothing = false;
-    vector<Requirement> reqs;
-    bool Matches(const Labels& ls) const {
-        if (nothing) return false;
-        for (auto& r : reqs) if (!RequirementMatches(r, ls)) return false;
-        return true;
-    }
-};
-
-/* metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:31-67) */
-static bool LabelSelectorAsSelector(const LabelSelector* ps, Selector* out) {
-    *out = Selector();
-    if (!ps) { out->nothing = true; return true; }
-    if (ps->ml.size() + ps->me.size() == 0) return true;  // Everything
-    for (auto& kv : ps->ml) {
-        Requirement r{kv.first, OpEquals, {kv.second}};
-        if (!ValidRequirement(r)) return false;
-        out->reqs.push_back(r);
-    }
-    for (auto& e : ps->me) {
-        if (e.op != OpIn && e.op != OpNotIn && e.op != OpExists && e.op != OpDoesNotExist) return false;
-        if (!ValidRequirement(e)) return false;
-        out->reqs.push_back(e);
-    }
-    // internalSelector.Add sorts by key; irrelevant for Matches (AND).
-    return true;
-}
-
-/* v1helper.NodeSelectorRequirementsAsSelector (helper/helpers.go:222-252) */
-static bool NodeSelectorRequirementsAsSelector(const vector<Requirement>& nsm, Selector* out) {
-    *out = Selector();
-    if (nsm.empty()) { out->nothing = true; return true; }
-    for (auto& e : nsm) {
-        if (e.op > OpLt) return false;
-        if (!ValidRequirement(e)) return false;
-        out->reqs.push_back(e);
-    }
-    return true;
-}
-
-/* NodeSelectorRequirementsAsFieldSelector (helper/helpers.go:255-283) + Matches
- * against fields.Set{metadata.name: node.Name} (algorithm/types.go:30-32). */
-static bool FieldSelectorMatches(const vector<Requirement>& nsm, const string& nodeName, bool* err) {
-    *err = false;
-    if (nsm.empty()) return false;  // fields.Nothing()
-    for (auto& e : nsm) {
-        if ((e.op != OpIn && e.op != OpNotIn) || e.values.size() != 1) { *err = true; return false; }
-    }
-    for (auto& e : nsm) {
-        string fv = e.key == "metadata.name" ? nodeName : string();
-        bool eq = fv == e.values[0];
-        if (e.op == OpIn && !eq) return false;
-        if (e.op == OpNotIn && eq) return false;
-    }
-    return true;
-}
-
-/* v1helper.MatchNodeSelectorTerms (helper/helpers.go:302-333) */
-static bool MatchNodeSelectorTerms(const vector<NodeSelectorTerm>& terms, const KNode& node) {
-    for (auto& req : terms) {
-        if (req.expr.empty() && req.fields.empty()) continue;
-        if (!req.expr.empty()) {
-            Selector sel;
-            if (!NodeSelectorRequirementsAsSelector(req.expr, &sel) || !sel.Matches(node.labels)) continue;
-        }
-        if (!req.fields.empty()) {
-            bool err;
-            if (!FieldSelectorMatches(req.fields, node.name, &err) || err) continue;
-        }
-        return true;
-    }
-    return false;
-}
-
-/* predicates.podMatchesNodeSelectorAndAffinityTerms (predicates.go:807-850) */
-static bool podMatchesNodeSelectorAndAffinityTerms(const Pod& pod, const KNode& node) {
-    if (!pod.nodeSelector.empty()) {
-        // labels.SelectorFromSet (selector.go:849-862): Equals requirements
-        for (auto& kv : pod.nodeSelector) {
-            auto it = node.labels.find(kv.first);
-            if (it == node.labels.end() || it->second != kv.second) return false;
-        }
-    }
-    bool nodeAffinityMatches = true;
-    if (pod.affinity && pod.affinity->hasNA) {
-        if (!pod.affinity->hasNAReq) return true;
-        nodeAffinityMatches = nodeAffinityMatches && MatchNodeSelectorTerms(pod.affinity->naReq, node);
-    }
-    return nodeAffinityMatches;
-}
-
-/* Toleration.ToleratesTaint (vendor/k8s.io/api/core/v1/toleration.go:37-56) */
-static bool ToleratesTaint(const Toleration& t, const Taint& taint) {
-    if (!t.effect.empty() && t.effect != taint.effect) return false;
-    if (!t.key.empty() && t.key != taint.key) return false;
-    if (t.op.empty() || t.op == "Equal") return t.value == taint.value;
-    if (t.op == "Exists") return true;
-    return false;
-}
-
-/* ------------------------------------------------------------------------ */
-/* vendored k8s scheduler cache NodeInfo (pkg/scheduler/cache/node_info.go)  */
-/* ------------------------------------------------------------------------ */
-struct PP {
-    string proto;
-    int32_t port;
-    bool operator<(const PP& o) const { return proto != o.proto ? proto < o.proto : port < o.port; }
-};
-typedef map<string, std::set<PP>> HostPortInfo;  // host_ports.go:50-51
-
-static void sanitize(string* ip, string* proto) {
-    if (ip->empty()) *ip = "0.0.0.0";
-    if (proto->empty()) *proto = "TCP";
-}
-static void HPAdd(HostPortInfo& h, string ip, string proto, int32_t port) {  // :53-72
-    if (port <= 0) return;
-    sanitize(&ip, &proto);
-    h[ip].insert(PP{proto, port});
-}
-static bool HPCheckConflict(const HostPortInfo& h, string ip, string proto, int32_t port) {  // :96-125
-    if (port <= 0) return false;
-    sanitize(&ip, &proto);
-    PP pp{proto, port};
-    if (ip == "0.0.0.0") {
-        for (auto& kv : h) if (kv.second.count(pp)) return true;
-        return false;
-    }
-    for (const string& key : {string("0.0.0.0"), ip}) {
-        auto it = h.find(key);
-        if (it != h.end() && it->second.count(pp)) return true;
-    }
-    return false;
-}
-
-static void GetNonzeroRequests(const Container& c, int64_t* cpu, int64_t* mem) {  // util/non_zero.go:37-52
-    *cpu = (c.has & KBS_HAS_CPU) ? c.cpu : 100;
-    *mem = (c.has & KBS_HAS_MEM) ? c.mem : 200LL * 1024 * 1024;
-}
-
-struct K8sNodeInfo {
-    KNode* node = nullptr;
-    vector<Pod*> pods, podsWithAffinity;
-    int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
-    HostPortInfo usedPorts;
-    int64_t alloc_cpu = 0, alloc_mem = 0;
-
-    static bool hasPodAffinityConstraints(const Pod* p) {
-        return p->affinity && (p->affinity->hasPA || p->affinity->hasPAA);
-    }
-    void AddPod(Pod* p) {  // :498-521
-        for (auto& c : p->containers) {
-            req_cpu += c.cpu;
-            req_mem += c.mem;
-            int64_t a, b;
-            GetNonzeroRequests(c, &a, &b);
-            nz_cpu += a;
-            nz_mem += b;
-        }
-        pods.push_back(p);
-        if (hasPodAffinityConstraints(p)) podsWithAffinity.push_back(p);
-        for (auto& c : p->containers)
-            for (auto& pt : c.ports) HPAdd(usedPorts, pt.ip, pt.proto, pt.port);
-    }
-    void SetNode(KNode* n) {  // :608-631
-        node = n;
-        alloc_cpu = n->a_cpu;
-        alloc_mem = n->a_mem;
-    }
-    bool Filter(const Pod* p) const {  // :692-702
-        if (p->nodeName != node->name) return true;
-        for (auto* q : pods) if (q->name == p->name && q->ns == p->ns) return true;
-        return false;
-    }
-};
-
-static K8sNodeInfo BuildK8sNodeInfo(const NodeInfo& ni) {  // cache.NewNodeInfo(node.Pods()...) + SetNode
-    K8sNodeInfo k;
-    for (auto* p : ni.Pods()) k.AddPod(p);
-    k.SetNode(ni.Node);
-    return k;
-}
-
-/* ------------------------------------------------------------------------ */
-/* framework.Session + plugins                                               */
-/* ------------------------------------------------------------------------ */
-struct PluginOption {
-    string name;
-    int flags = 0;
-    map<string, string> args;
-};
-typedef vector<vector<PluginOption>> Tiers;
-
-struct Session;
-typedef std::function<int(void*, void*)> CompareFn;
-typedef std::function<bool(TaskInfo*, NodeInfo*, string*)> PredicateFn;  // returns ok
-typedef std::function<bool(TaskInfo*, NodeInfo*, int*)> NodeOrderFn;      // returns ok
-typedef std::function<int(JobInfo*)> JobReadyFn;
-typedef std::function<bool(QueueInfo*)> OverusedFn;
-
-struct EventHandler {  // framework/event.go:27-30
-    std::function<void(TaskInfo*)> AllocateFunc;
-    std::function<void(TaskInfo*)> DeallocateFunc;
-};
-typedef std::function<vector<TaskInfo*>(TaskInfo*, const vector<TaskInfo*>&)> EvictableFn;  // api/types.go
-
-struct Session {
-    vector<JobInfo*> Jobs;          // pinned order (by job UID)
-    map<string, JobInfo*> JobByUID;
-    vector<NodeInfo*> Nodes;        // pinned order (by node name)
-    map<string, NodeInfo*> NodeByName;
-    vector<QueueInfo*> Queues;      // pinned order (by queue name)
-    map<string, QueueInfo*> QueueByUID;
-    Tiers tiers;
-    map<string, CompareFn> jobOrderFns, queueOrderFns, taskOrderFns;
-    map<string, PredicateFn> predicateFns;
-    map<string, NodeOrderFn> nodeOrderFns;
-    map<string, JobReadyFn> jobReadyFns;
-    map<string, OverusedFn> overusedFns;
-    vector<EventHandler> eventHandlers;
-    map<string, EvictableFn> preemptableFns, reclaimableFns;
-    std::deque<TaskInfo> clones;  // task.Clone() results (preempt.go:298-300, reclaim.go:138): the job keeps them after an eviction
-    // observer: placement log
-    vector<std::tuple<int, int, int>> log;  // (pod, node index, status)
-    map<string, int> nodeIndex;
-
-    bool JobOrderFn(JobInfo* l, JobInfo* r) {  // session_plugins.go:244-268
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_JOBORDER) continue;
-                auto it = jobOrderFns.find(p.name);
-                if (it == jobOrderFns.end()) continue;
-                int j = it->second(l, r);
-                if (j != 0) return j < 0;
-            }
-        if (l->CreationTimestamp == r->CreationTimestamp) return l->UID < r->UID;
-        return l->CreationTimestamp < r->CreationTimestamp;
-    }
-    bool QueueOrderFn(QueueInfo* l, QueueInfo* r) {  // :270-295
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_QUEUEORDER) continue;
-                auto it = queueOrderFns.find(p.name);
-                if (it == queueOrderFns.end()) continue;
-                int j = it->second(l, r);
-                if (j != 0) return j < 0;
-            }
-        if (l->ts == r->ts) return l->UID < r->UID;
-        return l->ts < r->ts;
-    }
-    bool TaskOrderFn(TaskInfo* l, TaskInfo* r) {  // :297-329
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_TASKORDER) continue;
-                auto it = taskOrderFns.find(p.name);
-                if (it == taskOrderFns.end()) continue;
-                int j = it->second(l, r);
-                if (j != 0) return j < 0;
-            }
-        if (l->P->ts == r->P->ts) return l->uid < r->uid;
-        return l->P->ts < r->P->ts;
-    }
-    bool PredicateFn_(TaskInfo* t, NodeInfo* n) {  // :331-348
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_PREDICATE) continue;
-                auto it = predicateFns.find(p.name);
-                if (it == predicateFns.end()) continue;
-                string err;
-                if (!it->second(t, n, &err)) return false;
-            }
-        return true;
-    }
-    bool NodeOrderFn_(TaskInfo* t, NodeInfo* n, int* score) {  // :350-370
-        int priorityScore = 0;
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_NODEORDER) continue;
-                auto it = nodeOrderFns.find(p.name);
-                if (it == nodeOrderFns.end()) continue;
-                int s = 0;
-                if (!it->second(t, n, &s)) { *score = 0; return false; }
-                priorityScore += s;
-            }
-        *score = priorityScore;
-        return true;
-    }
-    bool JobReady(JobInfo* job) {  // :167-186 — `break` leaves the plugin loop only,
-        int status = Ready;          // so the last tier with an enabled JobReadyFn decides
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                if (p.flags & KBS_DIS_JOBREADY) continue;
-                auto it = jobReadyFns.find(p.name);
-                if (it == jobReadyFns.end()) continue;
-                status = it->second(job);
-                break;
-            }
-        return status == Ready;
-    }
-    bool Overused(QueueInfo* q) {  // :150-164
-        for (auto& tier : tiers)
-            for (auto& p : tier) {
-                auto it = overusedFns.find(p.name);
-                if (it == overusedFns.end()) continue;
-                if (it->second(q)) return true;
-            }
-        return false;
-    }
-
-    // Session.Reclaimable / Preemptable (session_plugins.go:67-148): per tier,
-    // the intersection (in victim order) of the enabled plugins' candidates;
-    // the first tier whose result is non-nil decides.  A nil result (no plugin
-    // yet, or a plugin that returned nothing) lets the next tier decide.
-    vector<TaskInfo*> evictable(map<string, EvictableFn>& fns, int disFlag, TaskInfo* evictor,
-                                const vector<TaskInfo*>& evictees) {
-        vector<TaskInfo*> victims;
-        bool init = false, isNil = true;
-        for (auto& tier : tiers) {
-            for (auto& p : tier) {
-                if (p.flags & disFlag) continue;
-                auto it = fns.find(p.name);
-                if (it == fns.end()) continue;
-                vector<TaskInfo*> candidates = it->second(evictor, evictees);
-                if (!init) {
-                    victims = candidates;
-                    isNil = candidates.empty();  // the plugins build their slices by append: empty == nil
-                    init = true;
-                } else {
-                    vector<TaskInfo*> inter;
-                    for (auto* v : victims)
-                        for (auto* c : candidates)
-                            if (v->uid == c->uid) inter.push_back(v);
-                    victims = inter;
-                    isNil = inter.empty();  // `var intersection []*TaskInfo` stays nil when nothing matches
-                }
-            }
-            if (!isNil) return victims;
-        }
-        return victims;
-    }
-    vector<TaskInfo*> Reclaimable(TaskInfo* t, const vector<TaskInfo*>& es) {
-        return evictable(reclaimableFns, KBS_DIS_RECLAIMABLE, t, es);
-    }
-    vector<TaskInfo*> Preemptable(TaskInfo* t, const vector<TaskInfo*>& es) {
-        return evictable(preemptableFns, KBS_DIS_PREEMPTABLE, t, es);
-    }
-    // The session-side half of an eviction (session.go:331-356, statement.go:35-67):
-    // job status -> Releasing, node copy updated, Deallocate handlers.
-    void evictInSession(TaskInfo* reclaimee) {
-        auto jit = JobByUID.find(reclaimee->jobUID);
-        if (jit != JobByUID.end()) jit->second->UpdateTaskStatus(reclaimee, Releasing);
-        auto nit = NodeByName.find(reclaimee->NodeName);
-        if (nit != NodeByName.end()) nit->second->UpdateTask(*reclaimee);
-        for (auto& eh : eventHandlers) if (eh.DeallocateFunc) eh.DeallocateFunc(reclaimee);
-    }
-    void logEvict(TaskInfo* t) { log.emplace_back(t->pod, nodeIndex[t->NodeName], Releasing); }  // cache.Evict
-    void Evict(TaskInfo* reclaimee) {  // session.go:323-359 (the fake cache's Evict never fails)
-        logEvict(reclaimee);
-        evictInSession(reclaimee);
-    }
-    void Pipeline(TaskInfo* task, NodeInfo* node) {  // session.go:199-235
-        auto jit = JobByUID.find(task->jobUID);
-        if (jit != JobByUID.end()) jit->second->UpdateTaskStatus(task, Pipelined);
-        task->NodeName = node->Name;
-        node->AddTask(*task);
-        for (auto& eh : eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(task);
-        log.emplace_back(task->pod, nodeIndex[node->Name], Pipelined);
-    }
-    bool Allocate(TaskInfo* task, NodeInfo* node, bool usingBackfillTaskRes) {  // :237-297
-        auto jit = JobByUID.find(task->jobUID);
-        if (jit == JobByUID.end()) return false;
-        JobInfo* job = jit->second;
-        job->UpdateTaskStatus(task, usingBackfillTaskRes ? AllocatedOverBackfill : Allocated);
-        task->NodeName = node->Name;
-        if (!node->AddTask(*task)) return false;
-        for (auto& eh : eventHandlers) if (eh.AllocateFunc) eh.AllocateFunc(task);
-        log.emplace_back(task->pod, nodeIndex[node->Name], task->Status);
-        if (JobReady(job)) {
-            // dispatch every Allocated task (session.go:299-321): status -> Binding
-            auto it = job->TaskStatusIndex.find(Allocated);
-            if (it != job->TaskStatusIndex.end()) {
-                vector<TaskInfo*> ts;
-                for (auto& kv : it->second) ts.push_back(kv.second);
-                for (auto* t : ts) job->UpdateTaskStatus(t, Binding);
-            }
-        }
-        return true;
-    }
-};
-
-/* ---- priority plugin (plugins/priority/priority.go:38-79) ---------------- */
-static void priorityOpen(Session& ssn, const PluginOption&) {
-    ssn.taskOrderFns["priority"] = [](void* l, void* r) {
-        auto* lv = (TaskInfo*)l;
-        auto* rv = (TaskInfo*)r;
-        if (lv->Priority == rv->Priority) return 0;
-        if (lv->Priority > rv->Priority) return -1;
-        return 1;
-    };
-    ssn.jobOrderFns["priority"] = [](void* l, void* r) {
-        auto* lv = (JobInfo*)l;
-        auto* rv = (JobInfo*)r;
-        if (lv->Priority > rv->Priority) return -1;
-        if (lv->Priority < rv->Priority) return 1;
-        return 0;
-    };
-}
-
-/* ---- gang plugin (plugins/gang/gang.go:82-164) --------------------------- */
-static void gangOpen(Session& ssn, const PluginOption&) {
-    ssn.jobOrderFns["gang"] = [](void* l, void* r) {
-        bool lReady = ((JobInfo*)l)->GetReadiness() == Ready;
-        bool rReady = ((JobInfo*)r)->GetReadiness() == Ready;
-        if (lReady && rReady) return 0;
-        if (lReady) return 1;
-        if (rReady) return -1;
-        return 0;
-    };
-    ssn.jobReadyFns["gang"] = [](JobInfo* j) { return j->GetReadiness(); };
-    // preemptableFn (gang.go:107-129), registered as both Reclaimable and Preemptable
-    Session* sp = &ssn;
-    EvictableFn pf = [sp](TaskInfo*, const vector<TaskInfo*>& preemptees) {
-        vector<TaskInfo*> victims;
-        for (auto* preemptee : preemptees) {
-            JobInfo* job = sp->JobByUID[preemptee->jobUID];
-            int ready = 0;  // readyTaskNum (gang.go:212-222)
-            for (auto& kv : job->TaskStatusIndex)
-                if (AllocatedStatus(kv.first) || kv.first == Succeeded || kv.first == Pipelined)
-                    ready += (int)kv.second.size();
-            if (job->MinAvailable <= ready - 1 || job->MinAvailable == 1) victims.push_back(preemptee);
-        }
-        return victims;
-    };
-    ssn.reclaimableFns["gang"] = pf;
-    ssn.preemptableFns["gang"] = pf;
-}
-
-/* ---- conformance plugin (plugins/conformance/conformance.go:37-61) ------- */
-static void conformanceOpen(Session& ssn, const PluginOption&) {
-    EvictableFn ef = [](TaskInfo*, const vector<TaskInfo*>& evictees) {
-        vector<TaskInfo*> victims;
-        for (auto* e : evictees) {
-            const string& cls = e->P->priorityClassName;
-            if (cls == "system-cluster-critical" || cls == "system-node-critical" || e->ns == "kube-system") continue;
-            victims.push_back(e);
-        }
-        return victims;
-    };
-    ssn.preemptableFns["conformance"] = ef;
-    ssn.reclaimableFns["conformance"] = ef;
-}
-
-/* ---- drf plugin (plugins/drf/drf.go:59-170) ------------------------------ */
-struct DrfState {
-    Resource total;
-    map<string, Resource> allocated;
-    map<string, double> share;
-};
-static double drfShare(const Resource& alloc, const Resource& total) {  // :160-170
-    double res = 0;
-    for (int rn = 0; rn < 3; ++rn) {
-        double s = Share(alloc.Get(rn), total.Get(rn));
-        if (s > res) res = s;
-    }
-    return res;
-}
-static void drfOpen(Session& ssn, const PluginOption&, std::shared_ptr<DrfState> st) {
-    for (auto* n : ssn.Nodes) st->total.Add(n->Allocatable);
-    for (auto* job : ssn.Jobs) {
-        Resource a;
-        for (auto& kv : job->TaskStatusIndex)
-            if (AllocatedStatus(kv.first))
-                for (auto& t : kv.second) a.Add(t.second->Resreq);
-        st->allocated[job->UID] = a;
-        st->share[job->UID] = drfShare(a, st->total);
-    }
-    // preemptableFn (drf.go:84-109)
-    ssn.preemptableFns["drf"] = [st](TaskInfo* preemptor, const vector<TaskInfo*>& preemptees) {
-        vector<TaskInfo*> victims;
-        Resource lalloc = st->allocated[preemptor->jobUID];
-        lalloc.Add(preemptor->Resreq);
-        double ls = drfShare(lalloc, st->total);
-        map<string, Resource> allocations;
-        for (auto* preemptee : preemptees) {
-            if (!allocations.count(preemptee->jobUID)) allocations[preemptee->jobUID] = st->allocated[preemptee->jobUID];
-            Resource& ralloc = allocations[preemptee->jobUID].Sub(preemptee->Resreq);
-            double rs = drfShare(ralloc, st->total);
-            if (ls < rs || std::fabs(ls - rs) <= 0.000001) victims.push_back(preemptee);  // shareDelta (drf.go:29)
-        }
-        return victims;
-    };
-    ssn.jobOrderFns["drf"] = [st](void* l, void* r) {
-        double ls = st->share[((JobInfo*)l)->UID], rs = st->share[((JobInfo*)r)->UID];
-        if (ls == rs) return 0;
-        if (ls < rs) return -1;
-        return 1;
-    };
-    EventHandler eh;
-    eh.AllocateFunc = [st](TaskInfo* t) {
-        Resource& a = st->allocated[t->jobUID];
-        a.Add(t->Resreq);
-        st->share[t->jobUID] = drfShare(a, st->total);
-    };
-    eh.DeallocateFunc = [st](TaskInfo* t) {  // drf.go:144-151
-        Resource& a = st->allocated[t->jobUID];
-        a.Sub(t->Resreq);
-        st->share[t->jobUID] = drfShare(a, st->total);
-    };
-    ssn.eventHandlers.push_back(eh);
-}
-
-/* ---- proportion plugin (plugins/proportion/proportion.go:57-241) --------- */
-struct QueueAttr {
-    string queueID, name;
-    int32_t weight = 0;
-    double share = 0;
-    Resource deserved, allocated, request;
-};
-struct PropState {
-    Resource total;
-    map<string, QueueAttr> opts;
-    vector<string> order;  // pinned iteration order of queueOpts (by queue index)
-};
-static void propUpdateShare(QueueAttr& a) {  // :229-241
-    double res = 0;
-    for (int rn = 0; rn < 3; ++rn) {
-        double s = Share(a.allocated.Get(rn), a.deserved.Get(rn));
-        if (s > res) res = s;
-    }
-    a.share = res;
-}
-static void propOpen(Session& ssn, const PluginOption&, std::shared_ptr<PropState> st) {
-    for (auto* n : ssn.Nodes) st->total.Add(n->Allocatable);
-    for (auto* job : ssn.Jobs) {
-        if (!st->opts.count(job->Queue)) {
-            QueueInfo* q = ssn.QueueByUID[job->Queue];
-            QueueAttr a;
-            a.queueID = q->UID;
-            a.name = q->Name;
-            a.weight = q->Weight;
-            st->opts[job->Queue] = a;
-        }
-        QueueAttr& a = st->opts[job->Queue];
-        for (auto& kv : job->TaskStatusIndex) {
-            if (AllocatedStatus(kv.first)) {
-                for (auto& t : kv.second) { a.allocated.Add(t.second->Resreq); a.request.Add(t.second->Resreq); }
-            } else if (kv.first == Pending) {
-                for (auto& t : kv.second) a.request.Add(t.second->Resreq);
-            }
-        }
-    }
-    for (auto* q : ssn.Queues) if (st->opts.count(q->UID)) st->order.push_back(q->UID);
-    Resource remaining = st->total;
-    std::set<string> meet;
-    for (;;) {
-        int32_t totalWeight = 0;
-        for (auto& id : st->order) if (!meet.count(id)) totalWeight += st->opts[id].weight;
-        if (totalWeight == 0) break;
-        Resource deserved;
-        for (auto& id : st->order) {
-            QueueAttr& a = st->opts[id];
-            if (meet.count(id)) continue;
-            Resource r = remaining;
-            a.deserved.Add(r.Multi((double)a.weight / (double)totalWeight));
-            if (!a.deserved.LessEqual(a.request)) {
-                a.deserved = MinRes(a.deserved, a.request);
-                meet.insert(id);
-            }
-            propUpdateShare(a);
-            deserved.Add(a.deserved);
-        }
-        remaining.Sub(deserved);
-        if (remaining.IsEmpty()) break;
-    }
-    ssn.queueOrderFns["proportion"] = [st](void* l, void* r) {
-        double ls = st->opts[((QueueInfo*)l)->UID].share, rs = st->opts[((QueueInfo*)r)->UID].share;
-        if (ls == rs) return 0;
-        if (ls < rs) return -1;
-        return 1;
-    };
-    // reclaimableFn (proportion.go:159-183)
-    ssn.reclaimableFns["proportion"] = [st, &ssn](TaskInfo*, const vector<TaskInfo*>& reclaimees) {
-        vector<TaskInfo*> victims;
-        map<string, Resource> allocations;
-        for (auto* reclaimee : reclaimees) {
-            JobInfo* job = ssn.JobByUID[reclaimee->jobUID];
-            QueueAttr& attr = st->opts[job->Queue];
-            if (!allocations.count(job->Queue)) allocations[job->Queue] = attr.allocated;
-            Resource& allocated = allocations[job->Queue];
-            if (allocated.Less(reclaimee->Resreq)) continue;
-            allocated.Sub(reclaimee->Resreq);
-            if (attr.deserved.LessEqual(allocated)) victims.push_back(reclaimee);
-        }
-        return victims;
-    };
-    ssn.overusedFns["proportion"] = [st](QueueInfo* q) {
-        QueueAttr& a = st->opts[q->UID];
-        return a.deserved.LessEqual(a.allocated);
-    };
-    Session* sp = &ssn;
-    EventHandler eh;
-    eh.AllocateFunc = [st, sp](TaskInfo* t) {
-        JobInfo* job = sp->JobByUID[t->jobUID];
-        QueueAttr& a = st->opts[job->Queue];
-        a.allocated.Add(t->Resreq);
-        propUpdateShare(a);
-    };
-    eh.DeallocateFunc = [st, sp](TaskInfo* t) {  // proportion.go:211-219
-        JobInfo* job = sp->JobByUID[t->jobUID];
-        QueueAttr& a = st->opts[job->Queue];
-        a.allocated.Sub(t->Resreq);
-        propUpdateShare(a);
-    };
-    ssn.eventHandlers.push_back(eh);
-}
-
-/* ---- predicates plugin (plugins/predicates/predicates.go:114-204) -------- */
-
-// podLister.FilteredList (predicates.go:72-91): allocated-status tasks of all
-// session jobs, copied with Spec.NodeName = task.NodeName.
-struct ListedPod {
-    Pod* pod;
-    string nodeName;  // overridden Spec.NodeName
-};
-static vector<ListedPod> predFilteredList(Session& ssn, const K8sNodeInfo& ni) {
-    vector<ListedPod> out;
-    for (auto* job : ssn.Jobs)
-        for (auto& kv : job->TaskStatusIndex) {
-            if (!AllocatedStatus(kv.first)) continue;
-            for (auto& t : kv.second) {
-                TaskInfo* task = t.second;
-                if (ni.Filter(task->P)) out.push_back({task->P, task->NodeName});
-            }
-        }
-    return out;
-}
-
-// priorityutil.GetNamespacesFromPodAffinityTerm / PodMatchesTermsNamespaceAndSelector
-static std::set<string> termNamespaces(const Pod& definer, const PodAffinityTerm& t) {
-    std::set<string> s;
-    if (t.namespaces.empty()) s.insert(definer.ns);
-    else s.insert(t.namespaces.begin(), t.namespaces.end());
-    return s;
-}
-static bool podMatchesTermsNamespaceAndSelector(const Pod& pod, const std::set<string>& nss, const Selector& sel) {
-    if (!nss.count(pod.ns)) return false;
-    return sel.Matches(pod.labels);
-}
-
-// priorityutil.NodesHaveSameTopologyKey (util/topologies.go:53-75)
-static bool NodesHaveSameTopologyKey(const KNode* a, const KNode* b, const string& key) {
-    if (key.empty()) return false;
-    auto ia = a->labels.find(key), ib = b->labels.find(key);
-    if (ia != a->labels.end() && ib != b->labels.end()) return ia->second == ib->second;
-    return false;
-}
-
-struct PredErr {};
-
-// predicates cachedNodeInfo.GetNodeInfo (predicates.go:97-104): no fallback
-static KNode* predGetNode(Session& ssn, const string& name) {
-    auto it = ssn.NodeByName.find(name);
-    if (it == ssn.NodeByName.end()) throw PredErr();
-    return it->second->Node;
-}
-
-// podMatchesPodAffinityTerms (predicates.go:1189-1215): returns {match, propsMatch}; throws on error
-static std::pair<bool, bool> podMatchesPodAffinityTerms(Session& ssn, const Pod& pod, const ListedPod& target,
-                                                        const K8sNodeInfo& ni,
-                                                        const vector<PodAffinityTerm>& terms) {
-    if (terms.empty()) throw PredErr();
-    // getAffinityTermProperties + podMatchesAllAffinityTermProperties
-    for (auto& term : terms) {
-        Selector sel;
-        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) throw PredErr();
-    }
-    for (auto& term : terms) {
-        Selector sel;
-        LabelSelectorAsSelector(term.sel.get(), &sel);
-        if (!podMatchesTermsNamespaceAndSelector(*target.pod, termNamespaces(pod, term), sel))
-            return {false, false};
-    }
-    KNode* targetNode = predGetNode(ssn, target.nodeName);
-    for (auto& term : terms) {
-        if (term.topologyKey.empty()) throw PredErr();
-        if (!NodesHaveSameTopologyKey(ni.node, targetNode, term.topologyKey)) return {false, true};
-    }
-    return {true, true};
-}
-
-static bool targetPodMatchesAffinityOfPod(const Pod& pod, const Pod& target) {  // metadata.go:498-509
-    if (!pod.affinity || !pod.affinity->hasPA) return false;
-    const auto& terms = pod.affinity->paReq;
-    if (terms.empty()) return false;  // podMatchesAllAffinityTermProperties: no properties -> false
-    for (auto& term : terms) {
-        Selector sel;
-        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) return false;
-        if (!podMatchesTermsNamespaceAndSelector(target, termNamespaces(pod, term), sel)) return false;
-    }
-    return true;
-}
-
-// InterPodAffinityMatches slow path (predicates.go:1155-1184, 1293-1334, 1402-1458)
-static bool InterPodAffinityMatches(Session& ssn, const Pod& pod, const K8sNodeInfo& ni) {
-    try {
-        // satisfiesExistingPodsAntiAffinity
-        vector<ListedPod> filtered = predFilteredList(ssn, ni);
-        std::set<std::pair<string, string>> forbidden;
-        for (auto& ep : filtered) {
-            KNode* epNode = predGetNode(ssn, ep.nodeName);
-            const Pod& existing = *ep.pod;
-            if (!existing.affinity || !existing.affinity->hasPAA) continue;
-            for (auto& term : existing.affinity->paaReq) {
-                Selector sel;
-                if (!LabelSelectorAsSelector(term.sel.get(), &sel)) throw PredErr();
-                if (podMatchesTermsNamespaceAndSelector(pod, termNamespaces(existing, term), sel)) {
-                    auto it = epNode->labels.find(term.topologyKey);
-                    if (it != epNode->labels.end()) forbidden.insert({term.topologyKey, it->second});
-                }
-            }
-        }
-        for (auto& kv : ni.node->labels)
-            if (forbidden.count({kv.first, kv.second})) return false;
-
-        if (!pod.affinity || (!pod.affinity->hasPA && !pod.affinity->hasPAA)) return true;
-        // satisfiesPodsAffinityAntiAffinity, meta == nil branch
-        const vector<PodAffinityTerm> empty;
-        const auto& affinityTerms = pod.affinity->hasPA ? pod.affinity->paReq : empty;
-        const auto& antiAffinityTerms = pod.affinity->hasPAA ? pod.affinity->paaReq : empty;
-        bool matchFound = false, termsSelectorMatchFound = false;
-        for (auto& target : filtered) {
-            if (!matchFound && !affinityTerms.empty()) {
-                auto r = podMatchesPodAffinityTerms(ssn, pod, target, ni, affinityTerms);
-                if (r.second) termsSelectorMatchFound = true;
-                if (r.first) matchFound = true;
-            }
-            if (!antiAffinityTerms.empty()) {
-                try {
-                    auto r = podMatchesPodAffinityTerms(ssn, pod, target, ni, antiAffinityTerms);
-                    if (r.first) return false;
-                } catch (PredErr&) {
-                    return false;
-                }
-            }
-        }
-        if (!matchFound && !affinityTerms.empty()) {
-            if (termsSelectorMatchFound) return false;
-            if (!targetPodMatchesAffinityOfPod(pod, pod)) return false;
-        }
-        return true;
-    } catch (PredErr&) {
-        return false;
-    }
-}
-
-static void predicatesOpen(Session& ssn, const PluginOption&) {
-    Session* sp = &ssn;
-    ssn.predicateFns["predicates"] = [sp](TaskInfo* task, NodeInfo* node, string* err) {
-        K8sNodeInfo ni = BuildK8sNodeInfo(*node);
-        if (node->Allocatable.MaxTaskNum <= (int)ni.pods.size()) { *err = "maxtasks"; return false; }
-        const Pod& pod = *task->P;
-        if (!podMatchesNodeSelectorAndAffinityTerms(pod, *node->Node)) { *err = "selector"; return false; }
-        // PodFitsHostPorts (predicates.go:1031-1052)
-        for (auto& c : pod.containers)
-            for (auto& pt : c.ports)
-                if (HPCheckConflict(ni.usedPorts, pt.ip, pt.proto, pt.port)) { *err = "ports"; return false; }
-        // CheckNodeUnschedulable (predicates.go:107-112)
-        if (node->Node->unschedulable) { *err = "unschedulable"; return false; }
-        // PodToleratesNodeTaints (predicates.go:1489-1499, helper/helpers.go:425-440)
-        for (auto& taint : node->Node->taints) {
-            if (taint.effect != "NoSchedule" && taint.effect != "NoExecute") continue;
-            bool tol = false;
-            for (auto& t : pod.tolerations) if (ToleratesTaint(t, taint)) { tol = true; break; }
-            if (!tol) { *err = "taints"; return false; }
-        }
-        if (!InterPodAffinityMatches(*sp, pod, ni)) { *err = "podaffinity"; return false; }
-        return true;
-    };
-}
-
-/* ---- nodeorder plugin (plugins/nodeorder/nodeorder.go:177-319) ----------- */
-struct Weights {
-    int leastReq = 1, nodeAffinity = 1, podAffinity = 1, balanced = 1;
-};
-static bool atoi_go(const string& s, int* out) {  // strconv.Atoi
-    int64_t v;
-    if (!parseInt64(s, &v)) return false;
-    if (v < INT32_MIN || v > INT32_MAX) { /* Go int is 64-bit; keep within int */ }
-    *out = (int)v;
-    return true;
-}
-static Weights calculateWeight(const map<string, string>& args) {  // :177-249
-    Weights w;
-    auto get = [&](const char* k, int* dst) {
-        auto it = args.find(k);
-        if (it != args.end() && !it->second.empty()) {
-            int v;
-            if (atoi_go(it->second, &v)) *dst = v;
-        }
-    };
-    get("nodeaffinity.weight", &w.nodeAffinity);
-    get("podaffinity.weight", &w.podAffinity);
-    get("leastrequested.weight", &w.leastReq);
-    get("balancedresource.weight", &w.balanced);
-    return w;
-}
-
-static int64_t leastRequestedScore(int64_t requested, int64_t capacity) {  // least_requested.go:44-53
-    if (capacity == 0) return 0;
-    if (requested > capacity) return 0;
-    return ((capacity - requested) * 10) / capacity;
-}
-static double fractionOfCapacity(int64_t requested, int64_t capacity) {  // balanced_resource_allocation.go:72-77
-    if (capacity == 0) return 1;
-    return (double)requested / (double)capacity;
-}
-
-static void podNonZero(const Pod& p, int64_t* cpu, int64_t* mem) {  // resource_allocation.go:94-103
-    *cpu = 0;
-    *mem = 0;
-    for (auto& c : p.containers) {
-        int64_t a, b;
-        GetNonzeroRequests(c, &a, &b);
-        *cpu += a;
-        *mem += b;
-    }
-}
-
-// nodeorder cachedNodeInfo.GetNodeInfo with the empty-NodeName fallback (:78-93)
-static KNode* noGetNode(Session& ssn, const string& name, bool* ok) {
-    *ok = true;
-    auto it = ssn.NodeByName.find(name);
-    if (it != ssn.NodeByName.end()) return it->second->Node;
-    for (auto* n : ssn.Nodes)
-        for (auto* p : n->Pods())
-            if (p->nodeName.empty()) return n->Node;
-    *ok = false;
-    return nullptr;
-}
-
-// CalculateInterPodAffinityPriority (interpod_affinity.go:119-240); returns false on error
-static bool interPodAffinityScores(Session& ssn, const Pod& pod, map<string, int>* out) {
-    const Affinity* aff = pod.affinity.get();
-    bool hasAff = aff && aff->hasPA;
-    bool hasAnti = aff && aff->hasPAA;
-    map<string, double> counts;
-    bool err = false;
-    auto processTerm = [&](const PodAffinityTerm& term, const Pod& definer, const Pod& toCheck,
-                           const KNode* fixed, double weight) {
-        Selector sel;
-        if (!LabelSelectorAsSelector(term.sel.get(), &sel)) { err = true; return; }
-        if (podMatchesTermsNamespaceAndSelector(toCheck, termNamespaces(definer, term), sel)) {
-            for (auto* n : ssn.Nodes)
-                if (NodesHaveSameTopologyKey(n->Node, fixed, term.topologyKey)) counts[n->Name] += weight;
-        }
-    };
-    auto processTerms = [&](const vector<WeightedPodAffinityTerm>& terms, const Pod& definer, const Pod& toCheck,
-                            const KNode* fixed, int mult) {
-        for (auto& t : terms) processTerm(t.term, definer, toCheck, fixed, (double)(t.weight * mult));
-    };
-    auto processPod = [&](const Pod& existing) {
-        bool ok;
-        KNode* epNode = noGetNode(ssn, existing.nodeName, &ok);
-        if (!ok) { err = true; return; }
-        const Affinity* ea = existing.affinity.get();
-        bool eAff = ea && ea->hasPA, eAnti = ea && ea->hasPAA;
-        if (hasAff) processTerms(aff->paPref, pod, existing, epNode, 1);
-        if (hasAnti) processTerms(aff->paaPref, pod, existing, epNode, -1);
-        if (eAff) {
-            for (auto& term : ea->paReq) processTerm(term, existing, pod, epNode, 1.0);  // hardPodAffinityWeight
-            processTerms(ea->paPref, existing, pod, epNode, 1);
-        }
-        if (eAnti) processTerms(ea->paaPref, existing, pod, epNode, -1);
-    };
-    for (auto* n : ssn.Nodes) {  // processNode over all nodes (16-way in the reference; sums are exact)
-        K8sNodeInfo ni = BuildK8sNodeInfo(*n);
-        const vector<Pod*>& pods = (hasAff || hasAnti) ? ni.pods : ni.podsWithAffinity;
-        for (auto* p : pods) processPod(*p);
-    }
-    if (err) return false;
-    double maxCount = 0, minCount = 0;
-    for (auto* n : ssn.Nodes) {
-        double c = counts[n->Name];
-        if (c > maxCount) maxCount = c;
-        if (c < minCount) minCount = c;
-    }
-    for (auto* n : ssn.Nodes) {
-        double f = 0;
-        if (maxCount - minCount > 0) f = 10.0 * ((counts[n->Name] - minCount) / (maxCount - minCount));
-        (*out)[n->Name] = (int)f;
-    }
-    return true;
-}
-
-static void nodeorderOpen(Session& ssn, const PluginOption& opt) {
-    Session* sp = &ssn;
-    map<string, string> args = opt.args;
-    ssn.nodeOrderFns["nodeorder"] = [sp, args](TaskInfo* task, NodeInfo* node, int* out) {
-        Weights weight = calculateWeight(args);
-        Session& s = *sp;
-        // generateNodeMapAndSlice(ssn.Nodes) is rebuilt inside the IPA below
-        K8sNodeInfo ni = BuildK8sNodeInfo(*node);
-        const Pod& pod = *task->P;
-        int score = 0;
-        int64_t rc, rm;
-        podNonZero(pod, &rc, &rm);
-        rc += ni.nz_cpu;
-        rm += ni.nz_mem;
-        // LeastRequestedPriorityMap
-        int64_t lr = (leastRequestedScore(rc, ni.alloc_cpu) + leastRequestedScore(rm, ni.alloc_mem)) / 2;
-        score += (int)lr * weight.leastReq;
-        // BalancedResourceAllocationMap
-        double cpuF = fractionOfCapacity(rc, ni.alloc_cpu), memF = fractionOfCapacity(rm, ni.alloc_mem);
-        int64_t bra;
-        if (cpuF >= 1 || memF >= 1) bra = 0;
-        else {
-            double diff = std::fabs(cpuF - memF);
-            volatile double t = 1 - diff;  // no contraction: Go rounds each op
-            bra = (int64_t)(t * 10.0);
-        }
-        score += (int)bra * weight.balanced;
-        // CalculateNodeAffinityPriorityMap
-        int32_t count = 0;
-        if (pod.affinity && pod.affinity->hasNA) {
-            for (auto& pt : pod.affinity->naPref) {
-                if (pt.first == 0) continue;
-                Selector sel;
-                if (!NodeSelectorRequirementsAsSelector(pt.second.expr, &sel)) { *out = 0; return false; }
-                if (sel.Matches(node->Node->labels)) count += pt.first;
-            }
-        }
-        score += (int)count * weight.nodeAffinity;
-        // CalculateInterPodAffinityPriority over all nodes, then lookup
-        map<string, int> ipa;
-        if (!interPodAffinityScores(s, pod, &ipa)) { *out = 0; return false; }
-        auto it = ipa.find(node->Name);
-        int hostScore = it == ipa.end() ? 0 : it->second;
-        score += hostScore * weight.podAffinity;
-        *out = score;
-        return true;
-    };
-}
 
 /* ------------------------------------------------------------------------ */
 /* Cache + Snapshot (pkg/scheduler/cache) and allocate action                */
