@@ -314,7 +314,7 @@ struct EngMergerLds {
 // The placer's rows: four pops' candidates (slot 64 * (pop % 4) + lane) and
 // two packages' 128 entries (pop q's in slots kEngStage + 128 * (q % 2) + e).
 constexpr int kEngStage = 4 * 64, kEngRc = kEngStage + 2 * kEngPkgN;
-using EngRowCache = RowCacheT<kEngRc, 10>;
+using EngRowCache = RowCacheT<kEngRc, 11>;  // (2048 hash slots for 512 rows: short probe chains)
 struct EngPlacerLds {
     EngRowCache rc;
     uint8_t flags[kEngRc];

@@ -485,6 +485,7 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         }
 #pragma unroll
         for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before the flag below
         if (wave == 0) ETL(A, p, 13);
     }
     if (wave == 1) {  // pop p-2's candidates' FitDelta bits (left out of pop p's counts)
@@ -495,6 +496,7 @@ __device__ __forceinline__ bool own_package(const Conf& cf, const NodeCols& nc, 
         }
     }
     __syncthreads();
+    if (threadIdx.x == 0) st_sc1(&A.ctl->pkg_ready[p % kEngSlots][0], tag | 1u);  // the package has landed
     // 7. wave 2: pop p's FitDelta counts once pop p-1's candidates are logged
     if (wave == 2 && L.ok) {
         int n1 = -1;

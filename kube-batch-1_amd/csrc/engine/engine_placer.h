@@ -423,6 +423,26 @@ __device__ __forceinline__ void eng_front_v1(const Conf& cf, const NodeCols& nc,
 // ready).  Run for pop p + 1 by the waves pop p's placement leaves idle (and
 // for the first pop up front).  An exit descriptor has no package: its
 // descriptor comes from the device ring.
+// Field block K of a package (8 of its 32 fields, 128 entries: 16 granules per
+// lane) from registers into the placer's LDS: keys, the row words, flags,
+// node-affinity weights, depth-1 scores.
+template <int K>
+__device__ __forceinline__ void front_pkg_store(EngPlacerLds& L, const uint64_t (&v)[16], int base, uint32_t q,
+                                                int lane) {
+    EngRowCache& rc = L.rc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        constexpr int kF0 = 8 * K;
+        const int f = kF0 + (i >> 1), e = lane + 64 * (i & 1), sl = base + e;
+        const uint32_t x = (uint32_t)v[i];
+        if (f == kPkKey) L.pkey[q % 2][e] = x;
+        else if (f < kPkFlags) ((uint32_t*)&rc.row[sl])[f - kPkRow] = x;
+        else if (f == kPkFlags) L.flags[sl] = (uint8_t)x;
+        else if (f == kPkNa) rc.na[sl] = (int32_t)x;
+        else rc.s1[sl] = (int32_t)x;
+    }
+}
+
 template <bool LIST>
 __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, const DevTables& t, const EngArgs& A,
                                           EngPlacerLds& L, uint32_t q, int wave) {
@@ -430,14 +450,9 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
     EngCtl* ctl = A.ctl;
     EngRowCache& rc = L.rc;
     if (wave == 0) return;
-    const bool loads = wave == 3 || wave == 4 || wave == 6 || wave == 7;
-    const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block of a loading wave
+    const int k = wave == 3 ? 0 : wave == 4 ? 1 : wave - 4;  // field block of a loading wave (3, 4, 6, 7)
     const EngPkg* pk = A.pkg + (q % kEngSlots);
-    // the package's loads first (in flight during the rest; reloaded below if early)
     uint64_t v[16];
-    if (loads)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
     // pop q's descriptor and class (prefetched during P2, else from the ring); wave 3
     // leaves them in L.desc.  An exit has no package.
     uint32_t dw;
@@ -489,6 +504,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the hash is in LDS before the flag
         if (lane == 0) __hip_atomic_store(&L.hash_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ETL(A, q - 1, 63);
         eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 0, 1);
         return;
     }
@@ -509,46 +525,38 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
         else if (wave == 6) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 1, 0);
         else if (wave == 7) eng_front_eval<LIST>(cf, nc, t, A, L, q, dw, 2, 0);
     }
-    // two generations of the package's loads in flight, checked in turn (the package is
-    // read whole each time: four waves of one block, a few tens of GB/s), so that it is
-    // in registers about a round trip after it lands
-    uint64_t w[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+    ETL(A, q - 1, 56 + k);  // (timeline: the loading wave's evaluation done)
+    // the package's flag (one granule: its writer drained every store before it), then
+    // this wave's field block in one round trip (r05: the whole block re-read until every
+    // tag matched — a fifth of the front's time at C4, profiles/r06t*_tl_sweep.json)
     bool got = false;
+    if (!eng_poll_tag(ctl, &ctl->pkg_ready[q % kEngSlots][0], q, kEngWaitTicks)) {
+        if (k == 0 && lane == 0) L.ok = 0;
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
     EngWait wt(ctl, kEngWaitTicks);
-    for (;;) {
+    for (;;) {  // (every tag is q after the flag; the check stays as a guard)
         bool miss = false;
 #pragma unroll
         for (int i = 0; i < 16; ++i) miss |= (uint32_t)(v[i] >> 32) != q;
         if (__ballot(miss) == 0) { got = true; break; }
 #pragma unroll
-        for (int i = 0; i < 16; ++i) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
-        miss = false;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) miss |= (uint32_t)(w[i] >> 32) != q;
-        if (__ballot(miss) == 0) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) v[i] = w[i];
-            got = true;
-            break;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
+        for (int i = 0; i < 16; ++i)
+            if ((uint32_t)(v[i] >> 32) != q) v[i] = ld_sc1(&pk->w[8 * k + (i >> 1)][lane + 64 * (i & 1)]);
         if (!wt.tick()) break;
     }
     if (got) {
+        ETL(A, q - 1, 48 + k);  // (timeline: this wave's package fields in registers)
         const int base = kEngStage + kEngPkgN * (int)(q % 2);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int f = 8 * k + (i >> 1), e = lane + 64 * (i & 1), sl = base + e;
-            const uint32_t x = (uint32_t)v[i];
-            if (f == kPkKey) L.pkey[q % 2][e] = x;
-            else if (f < kPkFlags) ((uint32_t*)&rc.row[sl])[f - kPkRow] = x;
-            else if (f == kPkFlags) L.flags[sl] = (uint8_t)x;
-            else if (f == kPkNa) rc.na[sl] = (int32_t)x;
-            else rc.s1[sl] = (int32_t)x;
+        switch (k) {  // (the field block as a constant: every store's target resolved at compile time)
+            case 0: front_pkg_store<0>(L, v, base, q, lane); break;
+            case 1: front_pkg_store<1>(L, v, base, q, lane); break;
+            case 2: front_pkg_store<2>(L, v, base, q, lane); break;
+            default: front_pkg_store<3>(L, v, base, q, lane); break;
         }
+        ETL(A, q - 1, 52 + k);  // (timeline: ... and in LDS)
         if (k == 0) {
             for (int w = 0; w < 4; ++w) { rc.pw[base + lane][w] = 0; rc.pw[base + 64 + lane][w] = 0; }
             // pop q-1's candidates out of the package (its keys, written above by this wave),
@@ -558,6 +566,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
                 hashed = __hip_atomic_load(&L.hash_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == (int)q;
                 if (!hashed) __builtin_amdgcn_s_sleep(1);
             }
+            ETL(A, q - 1, 62);
             if (hashed) {
                 uint32_t w8[8];
 #pragma unroll
@@ -565,6 +574,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
                 eng_drop_stale(L, eng_args(eng_decode(w8)), q);
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 if (lane == 0) __hip_atomic_store(&L.drop_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ETL(A, q - 1, 60);
                 // the list merged with sets 1 and 2 once they are sorted (P3 then merges set 0 only)
                 bool both = false;
                 for (int i = 0; i < 4096 && !both; ++i) {
@@ -578,6 +588,7 @@ __device__ __forceinline__ void eng_front(const Conf& cf, const NodeCols& nc, co
                     L.pre64[lane] = LIST ? top : wave_merge_desc(top, L.e[2][lane]);
                     __builtin_amdgcn_s_waitcnt(0xc07f);
                     if (lane == 0) __hip_atomic_store(&L.pre_seq, (int)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    ETL(A, q - 1, 61);
                 }
             }
         }

@@ -422,8 +422,13 @@ __device__ __forceinline__ void eng_final(const Conf& cf, const NodeCols& nc, co
             }
 #pragma unroll
             for (int f = 0; f < kEngPkgFields; ++f) st_sc1(&pk->w[f][e], tag | v[f]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before the flag below
         }
         if (wave == 0) ETL(A, p, 22);
+        __syncthreads();
+        // one flag for the whole package: the placer polls it with one load instead of
+        // re-reading its blocks until every granule's tag is p
+        if (threadIdx.x == 0) st_sc1(&ctl->pkg_ready[p % kEngSlots][0], tag | 1u);
     }
 }
 

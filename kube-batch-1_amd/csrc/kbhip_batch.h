@@ -507,7 +507,7 @@ constexpr int kRcSlots = 192, kRcHash = 512;
 using RowCache = RowCacheT<kRcSlots, 9>;
 template <typename RC>
 __device__ __forceinline__ int rc_slot(int n) {
-    constexpr int hb = RC::kHashN == 512 ? 9 : RC::kHashN == 1024 ? 10 : 8;
+    constexpr int hb = RC::kHashN == 512 ? 9 : RC::kHashN == 1024 ? 10 : RC::kHashN == 2048 ? 11 : 8;
     static_assert((1 << hb) == RC::kHashN, "row-cache hash size");
     return (int)(((uint32_t)n * 2654435761u) >> (32 - hb));
 }

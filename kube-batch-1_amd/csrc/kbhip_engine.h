@@ -83,6 +83,7 @@ struct EngCtl {
     uint32_t pad2[63];
     uint64_t desc[kEngRing][kEngDescWords];  // descriptors, slot seq % kEngRing
     uint64_t cands[kEngSlots][kEngCandCopies][64];  // pop p's candidates {p << 32 | node (or 0xffffffff)}, in copies
+    uint64_t pkg_ready[kEngSlots][16];  // {p << 32 | 1} once package p % kEngSlots has landed (a line each)
     uint64_t tlog[kEngLog][64];  // list mode: pop p's candidates {p << 32 | node}, slot p % kEngLog
     uint64_t tcls[kEngLog];      // ... and its class {p << 32 | cls}
     uint32_t own_ap[kEngOwnMax]; // owner o: the last pop whose rows it applied (written by owner o only)
@@ -115,6 +116,6 @@ struct EngArgs {
 };
 constexpr uint32_t kEngIdleTicks = 10000000u;  // 100 ms without a descriptor: the run ends (100 MHz ticks)
 // Event timeline (s_memrealtime, 100 MHz): kEngTlEvents words per pop, pop p in slot p % kEngTlSlots.
-constexpr int kEngTlSlots = 32768, kEngTlEvents = 48;
+constexpr int kEngTlSlots = 32768, kEngTlEvents = 64;
 
 }  // namespace kbhip

@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 import kbgen  # noqa: E402
 import kbhip  # noqa: E402
 
-SLOTS, EV = 32768, 48
+SLOTS, EV = 32768, 64
 
 
 def main():

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "kube-batch-1_amd"))
 import kbgen  # noqa: E402
 import kbhip  # noqa: E402
 
-SLOTS, EV = 32768, 48
+SLOTS, EV = 32768, 64
 
 
 def main():
@@ -105,6 +105,16 @@ def main():
     if a.lists:
         per["owner stored(13,p) - placer 5(p-1) front start"] = us((t[1:, 13] - t[:-1, 5])[cont])
         per["owner stored(13,p) - placer 15(p-1) package in LDS"] = us((t[1:, 13] - t[:-1, 15])[cont])
+    for k, wv in enumerate((3, 4, 6, 7)):  # the package-loading waves of the front (r06 events)
+        for ev, nm in ((56 + k, "eval done"), (48 + k, "package in registers"), (52 + k, "package in LDS")):
+            ok = t[:, ev] > 0
+            if ok.any():
+                per[f"front wave {wv}: {nm} - 5"] = us((t[:, ev] - t[:, 5])[ok])
+    for ev, nm in ((63, "wave 2: hash built"), (62, "wave 3: hash seen"), (60, "wave 3: stale dropped"),
+                   (61, "wave 3: pre-merged")):
+        ok = t[:, ev] > 0
+        if ok.any():
+            per[f"front {nm} - 5"] = us((t[:, ev] - t[:, 5])[ok])
     per["dispatch(28) - placer start(0)"] = us(t[:, 28] - t[:, 0])
     per_all = np.diff(t[:, 0])[cont] / 100.0
     res = {"pops": int(len(t)), "lists": a.lists,
