@@ -263,7 +263,8 @@ struct Allocator {
         }
         if (S.prop_on) {  // proportion.go:65-142
             // each queue's sums in job and task order (floating point: the order is kept), queues
-            // split over the threads
+            // split over the threads — or, when prop_sums_exact finds every addend and every
+            // total a non-negative integer below 2^53, job ranges in parallel
             const int NQ = (int)S.queues.size();
             const int nth = S.pods.size() < (1u << 16) ? 1 : std::min(NQ, host_threads());
             auto prop = [&](int t) {
@@ -278,10 +279,12 @@ struct Allocator {
                     }
                 }
             };
-            vector<std::thread> th;
-            for (int t = 1; t < nth; ++t) th.emplace_back(prop, t);
-            if (nth > 0) prop(0);
-            for (auto& x : th) x.join();
+            if (!(S.pods.size() >= (1u << 16) && prop_sums_exact())) {
+                vector<std::thread> th;
+                for (int t = 1; t < nth; ++t) th.emplace_back(prop, t);
+                if (nth > 0) prop(0);
+                for (auto& x : th) x.join();
+            }
             vector<int> order;
             for (size_t i = 0; i < S.queues.size(); ++i) if (S.queues[i].has_attr) order.push_back((int)i);
             F3 remaining = S.total;
@@ -312,6 +315,61 @@ struct Allocator {
             }
         }
     }
+    // proportion's queue sums (proportion.go:88-103) over job ranges in parallel. A float64 sum
+    // of non-negative integers whose total stays below 2^53 is exact in any order (every
+    // partial sum is an integer no larger than the total), so it equals the in-order sum; the
+    // queues are written only when every addend, start value and total meets that.
+    bool prop_sums_exact() {
+        constexpr int64_t kLim = int64_t(1) << 53;
+        const int NQ = (int)S.queues.size(), J = (int)S.jobs.size();
+        const int nth = std::max(1, std::min(host_threads(), J / 256));
+        vector<vector<int64_t>> acc(nth, vector<int64_t>(6 * (size_t)NQ, 0));
+        vector<vector<uint8_t>> has(nth, vector<uint8_t>(NQ, 0));
+        vector<uint8_t> ok(nth, 1);
+        run_ranges(nth, [&](int t) {
+            int64_t* a = acc[t].data();
+            auto put = [&](int64_t* s, const R3& r) {
+                if ((uint64_t)r.c >= (uint64_t)kLim || (uint64_t)r.m >= (uint64_t)kLim ||
+                    (uint64_t)r.g >= (uint64_t)kLim)
+                    return false;  // negative or too large
+                s[0] += r.c; s[1] += r.m; s[2] += r.g;
+                return s[0] < kLim && s[1] < kLim && s[2] < kLim;
+            };
+            for (int jb = (int)((int64_t)J * t / nth); jb < (int)((int64_t)J * (t + 1) / nth); ++jb) {
+                const HJob& j = S.jobs[jb];
+                has[t][j.queue] = 1;
+                int64_t* qa = a + 6 * (size_t)j.queue;
+                for (int k : j.tasks) {
+                    const HPod& p = S.pods[k];
+                    bool good = true;
+                    if (allocated_status(p.status)) good = put(qa, p.req) && put(qa + 3, p.req);
+                    else if (p.status == Pending) good = put(qa + 3, p.req);
+                    if (!good) { ok[t] = 0; return; }
+                }
+            }
+        });
+        for (int t = 0; t < nth; ++t) if (!ok[t]) return false;
+        vector<double> out(6 * (size_t)NQ);
+        for (int q = 0; q < NQ; ++q) {
+            const HQueue& Q = S.queues[q];
+            const double x0[6] = {Q.allocated.c, Q.allocated.m, Q.allocated.g, Q.request.c, Q.request.m, Q.request.g};
+            for (int k = 0; k < 6; ++k) {
+                if (!(x0[k] >= 0 && x0[k] < (double)kLim && x0[k] == std::floor(x0[k]))) return false;
+                int64_t s = (int64_t)x0[k];
+                for (int t = 0; t < nth; ++t) s += acc[t][6 * (size_t)q + k];  // each < 2^53: no overflow
+                if (s >= kLim) return false;
+                out[6 * (size_t)q + k] = (double)s;
+            }
+        }
+        for (int q = 0; q < NQ; ++q) {
+            HQueue& Q = S.queues[q];
+            const double* o = &out[6 * (size_t)q];
+            Q.allocated.c = o[0]; Q.allocated.m = o[1]; Q.allocated.g = o[2];
+            Q.request.c = o[3]; Q.request.m = o[4]; Q.request.g = o[5];
+            for (int t = 0; t < nth; ++t) if (has[t][q]) Q.has_attr = true;
+        }
+        return true;
+    }
     bool overused(int qi) const {  // proportion.go:186-197
         if (!S.prop_on) return false;
         return S.queues[qi].deserved.less_equal(S.queues[qi].allocated);
@@ -341,6 +399,28 @@ struct Allocator {
         auto jl = [this](int a, int b) { return job_less(a, b); };
         GoHeap<decltype(ql)> queues(ql);
         std::map<int, JobQueue<decltype(jl)>> jobs_map;
+        // allocate.go:91-104: a job has work if it holds a pending task that is not BestEffort
+        // (its task lists scanned over job ranges in parallel; the pushes below stay in order)
+        const int NJ = (int)S.jobs.size();
+        vector<uint8_t> has_work(NJ, 0);
+        const int nth_w = NJ < (1 << 14) ? 1 : host_threads();
+        run_ranges(nth_w, [&, NJ, nth_w](int r) {
+            const int nth = nth_w;
+            for (int j = (int)((int64_t)NJ * r / nth); j < (int)((int64_t)NJ * (r + 1) / nth); ++j) {
+                const HJob& job = S.jobs[j];
+                bool work = false;
+                if (job.pending_built) work = job.cursor < job.pending.size();
+                else if (job.maybe_pending)
+                    for (int t : job.tasks) {
+                        const HPod& p = S.pods[t];
+                        if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) {
+                            work = true;
+                            break;
+                        }
+                    }
+                has_work[j] = work;
+            }
+        });
         for (size_t j = 0; j < S.jobs.size(); ++j) {
             const HJob& job = S.jobs[j];
             int q = job.queue;
@@ -350,17 +430,7 @@ struct Allocator {
             queues.push(q);
             auto it = jobs_map.find(q);
             if (it == jobs_map.end()) it = jobs_map.emplace(q, JobQueue<decltype(jl)>(jl)).first;
-            bool work = false;  // allocate.go:91-104: a pending task that is not BestEffort
-            if (job.pending_built) work = job.cursor < job.pending.size();
-            else if (job.maybe_pending)
-                for (int t : job.tasks) {
-                    const HPod& p = S.pods[t];
-                    if (p.status == Pending && !(p.req.c < kMinCPU && p.req.m < kMinMem && p.req.g < kMinGPU)) {
-                        work = true;
-                        break;
-                    }
-                }
-            if (work) {
+            if (has_work[j]) {
                 it->second.push((int)j);
             } else {
                 it->second.idle.push_back((int)j);
