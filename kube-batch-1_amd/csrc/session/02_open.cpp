@@ -115,23 +115,36 @@ uint64_t conf_digest(const kbs::Snapshot& s) {
     }
     return h;
 }
+// (over kDigestParts fixed node ranges hashed in parallel, their digests then
+// hashed in range order: the value depends on the snapshot only)
 uint64_t node_spec_digest(const kbs::Snapshot& s) {
-    uint64_t h = 1469598103934665603ULL;
+    constexpr int kDigestParts = 16;
     const size_t N = s.rows("n_name");
     auto loff = s.offs("n_label_off", N), toff = s.offs("n_taint_off", N);
     auto lk = s.span<int32_t>("nl_key"), lv = s.span<int32_t>("nl_val");
     auto tk = s.span<int32_t>("nt_key"), tv = s.span<int32_t>("nt_val"), te = s.span<int32_t>("nt_effect");
-    for (size_t i = 0; i < N; ++i) {
-        for (int k = loff[i]; k < loff[i + 1]; ++k) { h = fnv_str(h, s.str(lk[k])); h = fnv_str(h, s.str(lv[k])); }
-        h = fnv(h, "|", 1);
-        for (int k = toff[i]; k < toff[i + 1]; ++k) {
-            h = fnv_str(h, s.str(tk[k]));
-            h = fnv_str(h, s.str(tv[k]));
-            h = fnv_str(h, s.str(te[k]));
+    uint64_t part[kDigestParts];
+    auto range = [&](int r) {
+        uint64_t h = 1469598103934665603ULL;
+        for (size_t i = N * r / kDigestParts; i < N * (r + 1) / kDigestParts; ++i) {
+            for (int k = loff[i]; k < loff[i + 1]; ++k) { h = fnv_str(h, s.str(lk[k])); h = fnv_str(h, s.str(lv[k])); }
+            h = fnv(h, "|", 1);
+            for (int k = toff[i]; k < toff[i + 1]; ++k) {
+                h = fnv_str(h, s.str(tk[k]));
+                h = fnv_str(h, s.str(tv[k]));
+                h = fnv_str(h, s.str(te[k]));
+            }
+            h = fnv(h, "#", 1);
         }
-        h = fnv(h, "#", 1);
-    }
-    return h;
+        part[r] = h;
+    };
+    const int nth = N < (1u << 13) ? 1 : std::min(kDigestParts, host_threads());
+    vector<std::thread> th;
+    for (int t = 1; t < nth; ++t)
+        th.emplace_back([&, t] { for (int r = t; r < kDigestParts; r += nth) range(r); });
+    for (int r = 0; r < kDigestParts; r += nth) range(r);
+    for (auto& x : th) x.join();
+    return fnv(1469598103934665603ULL, part, sizeof(part));
 }
 
 void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_only, int rank,
@@ -1185,6 +1198,7 @@ void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_on
     }
     // ---------------- ordering plugins OnSessionOpen ----------------
     for (int i = 0; i < N; ++i) S.total.add(R3{acpu[i], amem[i], agpu[i]});  // drf.go:61-63, proportion.go:59-61
+    mark("keep");
     S.stats.nodes = N;
     S.stats.open_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
