@@ -125,6 +125,12 @@ void sweep_chunk(Session& S, int m, const int* cls, bool defer, bool per_task) {
 // device work, from ov_drain) or until it has been idle for a second (then
 // eng_poll restarts it for descriptors written meanwhile).
 // ---------------------------------------------------------------------------
+// Restart hysteresis (eng_eligible / eng_stop): a run that an engine-ineligible
+// pop ended after fewer than kEngShortRun pops sets the backoff to 8 or doubles
+// it (at most kEngBackoffMax); a run of 4 * kEngShortRun pops or more clears it.
+static constexpr int kEngShortRun = 16;
+static constexpr int kEngBackoffMax = 64;
+
 // A class the engine can serve (with a session that can run it, eng_eligible):
 // no pod affinity, host ports or backfill annotation, 32-bit keys and entries.
 static bool eng_class_ok(const Session& S, int cls, const KeyFormat& kf) {
@@ -222,17 +228,26 @@ static void eng_stop(Session& S);
 static bool eng_claim(Session& S);
 
 // A batched pop the engine can serve: one GPU, no Backfilled nodes, an
-// eligible class (eng_class_ok) — in list mode one with an owner.
+// eligible class (eng_class_ok) — in list mode one with an owner.  A stopped
+// engine starts again after more than S.eng_backoff such pops in a row (the
+// ones before take the launched path: same results, no launch + exit of the
+// persistent grid for a run of a few pops).
 static bool eng_eligible(Session& S, int cls, const KeyFormat& kf) {
     if (!S.engine || S.world != 1 || S.any_bf || S.rank_group || S.encode_only) return false;
-    if (!eng_class_ok(S, cls, kf)) return false;
+    if (!eng_class_ok(S, cls, kf)) {
+        S.eng_streak = 0;
+        S.eng_stop_cls = S.eng_running;  // the stop that follows (launch_batched) ends the run for this pop
+        return false;
+    }
     if (S.eng_nw != 0 && S.eng_ncls != S.classes.size()) {  // a carry added classes: size again (owners)
         eng_stop(S);
         S.eng_nw = 0;
     }
     if (S.eng_nw == 0) eng_size(S);
     if (!(S.eng_nw > 0 && (S.eng_nown == 0 || S.eng_own_of[cls] >= 0))) return false;
-    return S.eng_running || eng_claim(S);  // another session's engine on this device: the launched path
+    if (S.eng_running) return true;
+    if (++S.eng_streak <= S.eng_backoff) return false;
+    return eng_claim(S);  // another session's engine on this device: the launched path
 }
 
 static uint64_t* eng_exit_word(Session& S) { return S.h_eng + kEngHostRing * kEngDescWords; }
@@ -368,6 +383,7 @@ static void eng_submit(Session& S, BatchLaunch& L, int cls, int m, int gang_mode
             for (int k = 1; k <= kMaxDep; ++k) HIPCHK(hipStreamSynchronize(S.ov_streams[k]));
             S.ov_pending = false;
         }
+        S.eng_run_pops0 = S.stats.engine_pops;
         eng_start(S);
     }
     S.stats.engine_pops++;
@@ -388,6 +404,14 @@ static void eng_stop(Session& S) {
         eng_ended(S);
         if ((int32_t)(S.eng_first - sq) > 0) {  // it reached the exit descriptor
             eng_release(S);
+            // the restart hysteresis: runs ended by an engine-ineligible pop (other stops leave it)
+            const int64_t served = S.stats.engine_pops - S.eng_run_pops0;
+            if (S.eng_stop_cls && served < kEngShortRun)
+                S.eng_backoff = std::min(kEngBackoffMax, std::max(8, 2 * S.eng_backoff));
+            else if (served >= 4 * kEngShortRun)
+                S.eng_backoff = 0;
+            S.eng_stop_cls = false;
+            S.eng_streak = 0;
             return;
         }
         eng_start(S);  // it ended idle (or was not resident) before that: serve the rest

@@ -637,6 +637,12 @@ struct Session {
 #endif
     bool eng_running = false;   // its kernel was launched and has not been seen to end
     bool eng_claimed = false;   // this session holds its device's engine claim (eng_claim)
+    // restart hysteresis (eng_eligible): a run stopped after few pops (C3: affinity pops between
+    // short runs of engine-eligible ones) raises eng_backoff, the eligible pops in a row the
+    // launched path takes before the engine starts again; a long run clears it
+    int eng_backoff = 0, eng_streak = 0;
+    bool eng_stop_cls = false;  // the pending eng_stop is for an engine-ineligible batched pop
+    int64_t eng_run_pops0 = 0;  // stats.engine_pops when the current run started
     uint32_t eng_seq = 0;       // the last descriptor written (pop or exit)
     uint32_t eng_first = 1;     // the first pop of the next launch
     int eng_nw = 0, eng_npb = 0, eng_ng = 0;  // worker blocks (0: not sized yet, -1: the engine cannot run here)

@@ -3,7 +3,7 @@
 session's allocate with the engine's path counters — batched pops, the
 sequential placements (6: Backfilled nodes, 7: pod anti-affinity classes) and
 how they ended, per-task sweeps, unassigned pops, FitDelta recounts — plus
-open / allocate times.  Prints one JSON line; run under rocprofv3
+open / allocate times (--engine0: the persistent engine off).  Prints one JSON line; run under rocprofv3
 --kernel-trace --stats for the kernel split."""
 import json
 import os
@@ -19,6 +19,7 @@ import kbhip  # noqa: E402
 
 def main():
     c5 = "--c5" in sys.argv
+    engine = 0 if "--engine0" in sys.argv else 1
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     reps = int(args[0]) if args else 3
     p = "/tmp/kbhip_bench/c5_50000_2000_0.kbs" if c5 else "/tmp/kbhip_bench/c3.kbs"
@@ -35,6 +36,7 @@ def main():
     for _ in range(reps):
         t0 = time.perf_counter()
         s = kbhip.Session(buf)
+        s.set_option("engine", engine)
         t1 = time.perf_counter()
         if c5:
             s.reclaim()  # the shipped actions' order: allocate runs after reclaim (not timed)
@@ -48,8 +50,8 @@ def main():
         allocs.append(t2 - t1)
     keys = ("pops", "tasks", "placed", "sweeps", "batched_pops", "pertask_sweeps", "seq_launches", "seq_cut",
             "seq_none", "unassigned_pops", "spec_hits", "spec_missed", "fit_syncs", "alloc_setup_s", "alloc_device_s", "host_launch_s",
-            "host_wait_s")
-    print(json.dumps({"config": "C5 allocate" if c5 else "C3", "placements": int(len(pod)), "open_ms": statistics.median(opens) * 1e3,
+            "host_wait_s", "engine_pops", "engine_launches")
+    print(json.dumps({"config": "C5 allocate" if c5 else "C3", "engine": engine, "placements": int(len(pod)), "open_ms": statistics.median(opens) * 1e3,
                       "allocate_ms": statistics.median(allocs) * 1e3, **{k: st[k] for k in keys}}))
 
 
