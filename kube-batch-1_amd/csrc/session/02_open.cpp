@@ -482,6 +482,9 @@ void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_on
     std::unordered_map<int32_t, int> q_by_off;  // strtab offset of a job's queue name -> queue (-1: none)
     const auto default_q = qidx.find("default");
     vector<int32_t> uid_src;  // job slot -> its source (the UID strings are built after, in parallel)
+    spare_jobs().take_keep(S.jobs);  // a predecessor's records: reset below, their task lists' buffers kept
+    const size_t reuse = S.jobs.size();
+    size_t nslot = 0;
     S.jobs.reserve(srcs.size());
     uid_src.reserve(srcs.size());
     for (size_t si = 0; si < srcs.size(); ++si) {
@@ -506,20 +509,33 @@ void open_session(Session& S, const kbs::Snapshot& s, int device, bool encode_on
             j.ts = src.row >= 0 ? jts[src.row] : 0;
             j.priority = j.pg_priority = src.row >= 0 ? jpri[src.row] : 0;
             j.shadow = src.row < 0;
-            slot = (int)S.jobs.size();
-            S.jobs.push_back(j);
+            slot = (int)nslot++;
+            if ((size_t)slot < reuse) {  // keep the old record's task-list buffers (emptied)
+                HJob& d = S.jobs[slot];
+                j.tasks.swap(d.tasks);
+                j.pending.swap(d.pending);
+                j.tasks.clear();
+                j.pending.clear();
+                d = std::move(j);
+            } else {
+                S.jobs.push_back(std::move(j));
+            }
             uid_src.push_back((int32_t)si);
         }
         if (src.row >= 0) row_slot[src.row] = slot;
         else shadow_slot[src.pod] = slot;
     }
+    S.jobs.resize(nslot);
     {
         const size_t nj = uid_src.size();
+        spare_uids().take_keep(S.job_uid);  // assigned in place: the strings' buffers are reused
         S.job_uid.resize(nj);
         par_j([&](int t) {
             for (size_t k = nj * t / jth; k < nj * (t + 1) / jth; ++k) {
                 const Src& src = srcs[uid_src[k]];
-                S.job_uid[k] = src.b ? string(src.a) + "/" + src.b : string(src.a);
+                string& u = S.job_uid[k];
+                u.assign(src.a);
+                if (src.b) { u += '/'; u += src.b; }
             }
         });
     }

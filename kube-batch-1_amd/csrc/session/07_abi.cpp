@@ -551,10 +551,12 @@ int kbhip_session_close(kb_session* s) {
             (void)hipSetDevice(s->s.device);
             s->s.release_device();
         }
+        const auto t1 = std::chrono::steady_clock::now();
         delete s;  // the host model: freeing it on another thread measured slower (contention with the next open)
         if (prof)
-            std::fprintf(stderr, "[close] total      %8.2f ms\n",
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
+            std::fprintf(stderr, "[close] total      %8.2f ms (device %.2f ms)\n",
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3,
+                         std::chrono::duration<double>(t1 - t0).count() * 1e3);
         return KBHIP_OK;
     })
 }

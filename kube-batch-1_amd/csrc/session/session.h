@@ -503,6 +503,19 @@ inline SpareVec<HPod>& spare_pods() {
     static SpareVec<HPod> sp;
     return sp;
 }
+// The job records and job UIDs likewise: their elements own heap buffers (a
+// job's task list, a UID string — ≈ 400 k of them at C5, whose frees were
+// most of a session's close); a session reuses its predecessor's elements and
+// their capacity.  (The node task lists of the eviction actions are not
+// reused: reclaim's walk over reused, scattered lists measured slower.)
+inline SpareVec<HJob>& spare_jobs() {
+    static SpareVec<HJob> sp;
+    return sp;
+}
+inline SpareVec<string>& spare_uids() {
+    static SpareVec<string> sp;
+    return sp;
+}
 
 // ---------------------------------------------------------------------------
 // batched pop launches: one k_pop_batch per job-pop chunk of one class.  Two
@@ -832,6 +845,8 @@ struct Session {
 inline Session::~Session() {
     release_device();
     spare_pods().give(pods);
+    spare_jobs().give(jobs);
+    spare_uids().give(job_uid);
 }
 
 // Table upload: HBM on the session stream, or a host copy for encode-only
