@@ -179,22 +179,24 @@ struct Allocator {
             return;
         }
         vector<K> k(v.size());
-        for (size_t i = 0; i < v.size(); ++i) {
-            const HJob& J = S.jobs[v[i]];
-            K& x = k[i];
-            for (int c = 0; c < nd; ++c) {
-                const int code = job_order[c];
-                if (code == 1) x.d[c] = (uint64_t)((int64_t)INT32_MAX - (int64_t)J.priority);
-                else if (code == 2) x.d[c] = readiness(J) == 1 ? 1 : 0;
-                else {
-                    uint64_t b = 0;
-                    if (J.drf_share != 0) std::memcpy(&b, &J.drf_share, 8);
-                    x.d[c] = b;
+        auto keys = [&](size_t lo, size_t hi) {
+            for (size_t i = lo; i < hi; ++i) {
+                const HJob& J = S.jobs[v[i]];
+                K& x = k[i];
+                for (int c = 0; c < nd; ++c) {
+                    const int code = job_order[c];
+                    if (code == 1) x.d[c] = (uint64_t)((int64_t)INT32_MAX - (int64_t)J.priority);
+                    else if (code == 2) x.d[c] = readiness(J) == 1 ? 1 : 0;
+                    else {
+                        uint64_t b = 0;
+                        if (J.drf_share != 0) std::memcpy(&b, &J.drf_share, 8);
+                        x.d[c] = b;
+                    }
                 }
+                x.ts = J.ts;
+                x.j = v[i];
             }
-            x.ts = J.ts;
-            x.j = v[i];
-        }
+        };
         auto lt = [nd](const K& a, const K& b) {
             for (int c = 0; c < nd; ++c)
                 if (a.d[c] != b.d[c]) return a.d[c] < b.d[c];
@@ -202,21 +204,30 @@ struct Allocator {
             return a.j < b.j;
         };
         const size_t n = k.size();
-        if (n < (1u << 15)) {
+        if (n < (1u << 14)) {
+            keys(0, n);
             std::sort(k.begin(), k.end(), lt);
-        } else {  // C5: ~180 k running jobs without pending tasks: 8 sorted runs in parallel, merged
+        } else {  // C4 / C5: 10 k - 180 k jobs without pending tasks: 8 runs keyed and sorted in parallel,
+                  // merged pairwise (each level's merges in parallel)
             constexpr int kRuns = 8;
             vector<size_t> cut(kRuns + 1);
             for (int r = 0; r <= kRuns; ++r) cut[r] = n * r / kRuns;
-            vector<std::thread> th;
-            for (int r = 1; r < kRuns; ++r)
-                th.emplace_back([&, r]() { std::sort(k.begin() + cut[r], k.begin() + cut[r + 1], lt); });
-            std::sort(k.begin(), k.begin() + cut[1], lt);
-            for (auto& x : th) x.join();
+            auto par = [](int cnt, auto&& fn) {
+                vector<std::thread> th;
+                for (int r = 1; r < cnt; ++r) th.emplace_back(fn, r);
+                fn(0);
+                for (auto& x : th) x.join();
+            };
+            par(kRuns, [&](int r) {
+                keys(cut[r], cut[r + 1]);
+                std::sort(k.begin() + cut[r], k.begin() + cut[r + 1], lt);
+            });
             for (int w = 1; w < kRuns; w *= 2)  // the keys are distinct (job index last): a strict order
-                for (int r = 0; r + w < kRuns; r += 2 * w)
+                par(kRuns / (2 * w), [&, w](int i) {
+                    const int r = 2 * w * i;
                     std::inplace_merge(k.begin() + cut[r], k.begin() + cut[r + w],
                                        k.begin() + cut[std::min(r + 2 * w, kRuns)], lt);
+                });
         }
         for (size_t i = 0; i < v.size(); ++i) v[i] = k[i].j;
     }
