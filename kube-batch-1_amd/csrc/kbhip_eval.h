@@ -353,7 +353,10 @@ KBHIP_HD uint64_t eval_first_fit(const Conf& cf, const TaskClass& c, const DevTa
 // Written branch-free on purpose: the if / else-if / else form (one increment
 // per branch, two tables) is miscompiled by the ROCm 7.2 gfx950 backend when
 // it runs in a single lane — the UPD_SCALAR_ANY branch reused a stale table
-// pointer register ("toolchain note").
+// pointer register ("toolchain note").  A node without the
+// space's key (domain -1) adds 0 at the table's first entry: the index stays
+// inside the table (u[2] + -1 was one word before it — outside the buffer for
+// the first table, a fault at full-size C3 with keyless nodes).
 KBHIP_HD void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols& nc, int g, int kind) {
     for (int i = 0; i < c.upd_n; ++i) {
         const int32_t* u = t.aff_items + c.upd_off + 3 * i;
@@ -362,7 +365,7 @@ KBHIP_HD void commit_aff(const TaskClass& c, const DevTables& t, const NodeCols&
         const int d = to_cnt ? dom_g(nc, u[1], g) : 0;
         const bool apply = (typ == 2 || kind == 1) && d >= 0;
         int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
-        tab[u[2] + d] += apply ? 1 : 0;
+        tab[u[2] + (d < 0 ? 0 : d)] += apply ? 1 : 0;  // (a keyless node: +0 at the table's first entry)
     }
 }
 
@@ -376,7 +379,7 @@ KBHIP_HD void uncommit_aff(const TaskClass& c, const DevTables& t, const NodeCol
         const int d = to_cnt ? dom_g(nc, u[1], g) : 0;
         const bool apply = (typ == 2 || kind == 1) && d >= 0;
         int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
-        tab[u[2] + d] -= apply ? 1 : 0;
+        tab[u[2] + (d < 0 ? 0 : d)] -= apply ? 1 : 0;
     }
 }
 

@@ -14,7 +14,10 @@ placement logs, so the fixture pins them by digest:
   oracle/kbref.cpp on smaller snapshots, tests/test_oracle.py);
 * head — the first 64 placements verbatim (readable diffs on a mismatch).
 
-Usage: python tests/golden/make_fullsize.py [c3] [c4]   (C4 takes ~8 min on 8 cores)
+c3aff is C3 with keyless nodes (10 %), required pod affinity (15 % of gangs)
+and preferred inter-pod affinity / anti-affinity terms (15 %).
+
+Usage: python tests/golden/make_fullsize.py [c3] [c3aff] [c4]   (C4 takes ~8 min on 8 cores)
 """
 import hashlib
 import json
@@ -30,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 
 OUT = os.path.join(HERE, "fullsize.json")
+C3AFF = dict(keyless=0.1, pod_affinity=0.15, ipa=0.15)
 
 
 def log_digest(pod, node, status):
@@ -43,6 +47,8 @@ def snapshot(cfg, path):
         kbgen.gen_c4(path)
     elif cfg == "c3":
         kbgen.gen_c3().write(path)
+    elif cfg == "c3aff":  # C3 with keyless nodes, required pod affinity and preferred inter-pod terms
+        kbgen.gen_c3(**C3AFF).write(path)
     else:
         raise ValueError(cfg)
     with open(path, "rb") as f:

@@ -1,4 +1,5 @@
-"""Full-size parity of the headline configs (BASELINE.json C4, and C3).
+"""Full-size parity of the headline configs (BASELINE.json C4, and C3 with a
+required-affinity / inter-pod-priority variant).
 
 The engine's placement log on the exact bench snapshot must equal the CPU
 oracle's, bit for bit.  The oracle's logs are pinned as digests in
@@ -54,3 +55,15 @@ def test_c3_full_size_parity(engine, kbgen_mod, tmp_path):
     with open(p, "rb") as f:
         assert hashlib.sha256(f.read()).hexdigest() == GOLD["c3"]["snap_sha256"]
     _check(engine, p, GOLD["c3"])
+
+
+@pytest.mark.skipif("c3aff" not in GOLD, reason="no C3 affinity digest")
+def test_c3_affinity_ipa_full_size_parity(engine, kbgen_mod, tmp_path):
+    """C3 at full size with keyless nodes, required pod affinity and preferred
+    inter-pod affinity / anti-affinity terms beside its zone anti-affinity
+    (make_fullsize.py C3AFF; predicates.go:1402-1458, interpod_affinity.go:119-240)."""
+    p = str(tmp_path / "c3aff.kbs")
+    kbgen_mod.gen_c3(keyless=0.1, pod_affinity=0.15, ipa=0.15).write(p)
+    with open(p, "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == GOLD["c3aff"]["snap_sha256"]
+    _check(engine, p, GOLD["c3aff"])
