@@ -243,8 +243,12 @@ int kbhip_time_rank_multi(kb_session* const* sessions, int32_t n, const int32_t*
  * (pod, node, KBHIP_PIPELINED) for every pipelined preemptor (reclaim: each
  * ssn.Pipeline; preempt: those of a committed Statement).  Discarded
  * statements leave no record (and, like the reference, leave the victims'
- * node copies Releasing).  Returns the record count.  KBHIP_EUNSUPPORTED on
- * node-sharded sessions.
+ * node copies Releasing).  Returns the record count.  On node-sharded
+ * sessions every rank calls it collectively and returns the same records:
+ * each rank ranks its own nodes, the sorted lists are all-gathered
+ * (kbhip_shard_connect_host_gather or kbhip_shard_connect_rccl is required,
+ * else KBHIP_EINVAL) and merged, and evictions / pipelines change the rows of
+ * the owning rank only.
  * Replaces the reference's reclaimAction.Execute / preemptAction.Execute.
  * If an action fails part-way (negative return) the session's host model may
  * hold a partial action: close it and open a new one. */

@@ -239,19 +239,21 @@ hipError_t launch_score_sweep(const Conf& cf, const NodeCols& nc, const DevTable
 //                    (node_info.go:147-185; Idle / Used / Backfilled net unchanged)
 //   op 1 pipeline    NodeInfo.AddTask Pipelined (commit_node, kind 2)
 //   op 2 unpipeline  NodeInfo.RemoveTask of the Pipelined copy (uncommit_node, kind 2)
-__global__ __launch_bounds__(64) void k_node_op(NodeCols nc, DevTables t, int op, int n, int cls, int64_t rc,
+// n: this shard's row of global node g, or -1 (another shard's node: the
+// replicated count tables only).
+__global__ __launch_bounds__(64) void k_node_op(NodeCols nc, DevTables t, int op, int n, int g, int cls, int64_t rc,
                                                 int64_t rm, int64_t rg) {
     if (threadIdx.x != 0) return;
     if (op == 0) {
-        nc.rel_cpu[n] += rc; nc.rel_mem[n] += rm; nc.rel_gpu[n] += rg;
+        if (n >= 0) { nc.rel_cpu[n] += rc; nc.rel_mem[n] += rm; nc.rel_gpu[n] += rg; }
     } else if (op == 1) {
         const TaskClass c = t.classes[cls];
-        commit_node(c, t, nc, n, 2);
-        if (c.aff) commit_aff(c, t, nc, n + nc.base, 2);  // a session-placed pod (inter-pod priority)
+        if (n >= 0) commit_node(c, t, nc, n, 2);
+        if (c.aff) commit_aff(c, t, nc, g, 2);  // a session-placed pod (inter-pod priority)
     } else {
         const TaskClass c = t.classes[cls];
-        uncommit_node(c, t, nc, n, 2);
-        if (c.aff) uncommit_aff(c, t, nc, n + nc.base, 2);
+        if (n >= 0) uncommit_node(c, t, nc, n, 2);
+        if (c.aff) uncommit_aff(c, t, nc, g, 2);
     }
 }
 
@@ -577,9 +579,10 @@ hipError_t launch_rank_sorted_multi(const RankDesc* d_desc, int n_desc, int max_
 }
 size_t rank_hist_words(int n_nodes) { return (size_t)kRankBuckets * ((n_nodes + kBlock - 1) / kBlock + 1); }
 
-hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
-                          int64_t rg, hipStream_t st) {
-    hipLaunchKernelGGL(k_node_op, dim3(1), dim3(64), 0, st, nc, t, op, n, cls, rc, rm, rg);
+hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int g, int cls, int64_t rc,
+                          int64_t rm, int64_t rg, hipStream_t st) {
+    if (n >= nc.n || g < 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_node_op, dim3(1), dim3(64), 0, st, nc, t, op, n, g, cls, rc, rm, rg);
     return hipGetLastError();
 }
 

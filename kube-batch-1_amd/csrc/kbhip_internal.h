@@ -92,8 +92,10 @@ struct RowPatch {
     int32_t size, pad;
 };
 hipError_t launch_row_patch(const RowPatch* e, int n, hipStream_t st);
-hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int cls, int64_t rc, int64_t rm,
-                          int64_t rg, hipStream_t st);
+// op 0 Releasing += (rc, rm, rg), 1 a pipelined pod committed, 2 uncommitted, on this shard's row n of
+// global node g (n = -1: another shard's node — the replicated count tables only)
+hipError_t launch_node_op(const NodeCols& nc, const DevTables& t, int op, int n, int g, int cls, int64_t rc,
+                          int64_t rm, int64_t rg, hipStream_t st);
 
 // Selection-key format of a batched launch: 32-bit keys when the class's
 // score range and the node count fit (kbhip_kernels.hip, PopArgs).

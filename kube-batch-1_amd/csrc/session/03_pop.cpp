@@ -44,6 +44,26 @@ void fit_allreduce(Session& S, int32_t* fit4) {
     for (int q = 0; q < 4; ++q) fit4[q] = (int32_t)h[q];
 }
 
+// All-gather of `bytes` host bytes per rank into recv, in rank order (the
+// eviction actions' node rankings on shards): the host callback, or RCCL
+// through a device staging buffer on the session stream.
+void gather_host(Session& S, const void* send, void* recv, size_t bytes) {
+    S.stats.collectives++;
+    if (g_trace_shard)
+        std::fprintf(stderr, "[shard %d] #%lld all-gather %zu bytes\n", S.rank, (long long)S.stats.collectives, bytes);
+    if (S.xgfn) {
+        if (S.xgfn(S.xgctx, send, recv, (int64_t)bytes) != 0) throw Error(KBHIP_EDEVICE, "shard all-gather callback failed");
+        return;
+    }
+    if (!S.comm) throw Error(KBHIP_EINVAL, "sharded session has no all-gather (kbhip_shard_connect_*)");
+    uint8_t* d = S.b_gather.alloc<uint8_t>(bytes * (S.world + 1));
+    HIPCHK(hipMemcpyAsync(d + bytes * S.world, send, bytes, hipMemcpyHostToDevice, S.stream));
+    const ncclResult_t r = ncclAllGather(d + bytes * S.world, d, bytes, ncclUint8, S.comm, S.stream);
+    if (r != ncclSuccess) throw Error(KBHIP_EDEVICE, string("ncclAllGather: ") + ncclGetErrorString(r));
+    HIPCHK(hipMemcpyAsync(recv, d, bytes * S.world, hipMemcpyDeviceToHost, S.stream));
+    HIPCHK(hipStreamSynchronize(S.stream));
+}
+
 // The all-gather of a batched pop on a node-array shard: every rank's
 // ShardMsg into d_shard_recv in rank order.  RCCL on the session stream (no
 // host synchronisation), or the host callback around two copies.

@@ -794,8 +794,19 @@ struct Allocator {
         return a.c - b.c < kMinCPU && a.m - b.m < kMinMem && a.g - b.g < kMinGPU;
     }
     static bool less_strict(const R3& a, const R3& b) { return a.c < b.c && a.m < b.m && a.g < b.g; }
+    // Node-sharded sessions: the host model — victims, statements, records — is
+    // replicated on every rank; each rank ranks its own node range and the sorted lists are
+    // all-gathered and merged (the keys carry the global node index, so the merge is the
+    // one-GPU order); evictions and pipelines change the device rows of the owning shard only,
+    // the pod-affinity count tables on every shard.
     void check_evict_supported() {
-        if (S.world != 1) throw Error(KBHIP_EUNSUPPORTED, "reclaim / preempt on a node-sharded session");
+        if (S.world != 1 && !S.xgfn && !S.comm)
+            throw Error(KBHIP_EINVAL, "reclaim / preempt on a node-sharded session need an all-gather "
+                                      "(kbhip_shard_connect_host with a gather, or kbhip_shard_connect_rccl)");
+    }
+    int local_node(int g) const {  // this shard's row of global node g, or -1
+        const int l = g - S.nc.base;
+        return l >= 0 && l < S.nc.n ? l : -1;
     }
     void on_deallocate(int pi) {  // event handlers drf.go:144-151, proportion.go:211-219
         const HPod& p = S.pods[pi];
@@ -823,7 +834,7 @@ struct Allocator {
         // two passes over the pod records (≈ 110 MB at C5) by pod ranges in parallel: each
         // pod's running-copy byte and per range the tasks per node; then each node's list
         // sized and the ranges' pods written at their offsets (pod order within a node kept)
-        const int N = S.nc.n, P = (int)S.pods.size();
+        const int N = S.n_total, P = (int)S.pods.size();  // (every node: the host model is global on shards)
         const int nth = P < (1 << 16) ? 1 : host_threads();
         vector<vector<int32_t>> cnt(nth, vector<int32_t>(N, 0));
         run_copy.assign(P, 0);
@@ -906,13 +917,15 @@ struct Allocator {
         auto sr = S.class_srange[cls];
         if (by_score && S.classes[cls].ipa_n > 0) {  // inter-pod priority: normalisation prepass, wider range
             HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, 0, S.stream));
+            exchange(S, &S.d_ctrl->ipa_lo[0], KBHIP_RED_MIN_I64);  // (shards: over every node)
+            exchange(S, &S.d_ctrl->ipa_hi[0], KBHIP_RED_MAX_I64);
             const int64_t w = 10 * (int64_t)S.conf.w_pa * S.conf.score_mult;
             sr.first += std::min<int64_t>(0, w);
             sr.second += std::max<int64_t>(0, w);
         }
         const bool counting = !S.force_radix && sr.second - sr.first < 256 && sr.first >= INT32_MIN &&
                               sr.second <= INT32_MAX;
-        if (counting && S.rank_group) {  // one launch with the concurrent what-if sessions' rankings
+        if (counting && S.rank_group && S.world == 1) {  // one launch with the concurrent what-if sessions' rankings
             StepBatcher::Req r;
             r.kind = StepBatcher::kRank;
             HIPCHK(fill_rank_desc(&r.rank, S.conf, S.nc, S.tab, S.classes[cls], S.d_ctrl, by_score ? 1 : 0, (int)sr.first,
@@ -950,14 +963,45 @@ struct Allocator {
                                   (size_t)(cnt - first) * sizeof(uint64_t), hipMemcpyDeviceToHost, S.stream));
             HIPCHK(hipStreamSynchronize(S.stream));
         }
-        out.resize(cnt);
-        for (int i = 0; i < cnt; ++i) out[i] = key_idx(S.h_rank[1 + i]);
+        if (S.world > 1) {
+            merge_shard_ranks(cnt, out);
+        } else {
+            out.resize(cnt);
+            for (int i = 0; i < cnt; ++i) out[i] = key_idx(S.h_rank[1 + i]);
+        }
         S.stats.sweeps++;
         S.stats.tasks++;
     }
-    void dev_op(int op, int pi) {
+    // Node-sharded ranking: every shard's sorted passing keys (descending; global node index
+    // inside) all-gathered as fixed-size records [count, keys...], merged into the order one
+    // GPU's sort of every node gives (the keys are distinct).
+    void merge_shard_ranks(int cnt, vector<int>& out) {
+        const size_t rec = (size_t)(S.n_total + S.world - 1) / S.world + 1;  // >= every shard's rows + 1
+        vector<uint64_t> send(rec, 0), recv(rec * S.world);
+        send[0] = (uint64_t)cnt;
+        std::memcpy(send.data() + 1, S.h_rank + 1, (size_t)cnt * sizeof(uint64_t));
+        gather_host(S, send.data(), recv.data(), rec * sizeof(uint64_t));
+        vector<size_t> at(S.world), end(S.world);
+        size_t total = 0;
+        for (int r = 0; r < S.world; ++r) {
+            const uint64_t c = recv[rec * r];
+            if (c >= rec) throw Error(KBHIP_EDEVICE, "shard ranking: a rank's count exceeds its record");
+            at[r] = rec * r + 1;
+            end[r] = at[r] + c;
+            total += c;
+        }
+        out.resize(total);
+        for (size_t i = 0; i < total; ++i) {
+            int best = -1;
+            for (int r = 0; r < S.world; ++r)
+                if (at[r] < end[r] && (best < 0 || recv[at[r]] > recv[at[best]])) best = r;
+            out[i] = key_idx(recv[at[best]++]);
+        }
+    }
+    void dev_op(int op, int pi) {  // the row on the owning shard, the count tables on every shard
         const HPod& p = S.pods[pi];
-        HIPCHK(launch_node_op(S.nc, S.tab, op, p.node, p.cls, p.req.c, p.req.m, p.req.g, S.stream));
+        HIPCHK(launch_node_op(S.nc, S.tab, op, local_node(p.node), p.node, p.cls, p.req.c, p.req.m, p.req.g,
+                              S.stream));
     }
     // the session half of an eviction (session.go:331-356 / statement.go:35-67)
     void evict_in_session(int v) {
@@ -966,25 +1010,32 @@ struct Allocator {
         // node.UpdateTask: Releasing += Resreq.  No node ranking reads Releasing, so
         // evictions are summed per node and applied in one launch (flush_evictions)
         const HPod& p = S.pods[v];
-        if (S.rel_delta.empty()) { S.rel_delta.assign(S.nc.n, R3{}); S.rel_flag.assign(S.nc.n, 0); }
+        if (S.rel_delta.empty()) { S.rel_delta.assign(S.n_total, R3{}); S.rel_flag.assign(S.n_total, 0); }
         if (!S.rel_flag[p.node]) { S.rel_flag[p.node] = 1; S.rel_touched.push_back(p.node); }
         R3& d = S.rel_delta[p.node];
         d.c += p.req.c; d.m += p.req.m; d.g += p.req.g;
         on_deallocate(v);
     }
     void flush_evictions() {
-        const int n = (int)S.rel_touched.size();
-        if (!n) return;
-        vector<int32_t> nodes(n);
-        vector<int64_t> d(3 * (size_t)n);
-        for (int i = 0; i < n; ++i) {
+        const int nt = (int)S.rel_touched.size();
+        if (!nt) return;
+        vector<int32_t> nodes;
+        vector<int64_t> d;
+        nodes.reserve(nt);
+        d.reserve(3 * (size_t)nt);
+        for (int i = 0; i < nt; ++i) {
             const int v = S.rel_touched[i];
-            nodes[i] = v;
-            d[3 * i] = S.rel_delta[v].c; d[3 * i + 1] = S.rel_delta[v].m; d[3 * i + 2] = S.rel_delta[v].g;
+            const int l = local_node(v);  // (shards: the owning rank's rows only)
+            if (l >= 0) {
+                nodes.push_back(l);
+                d.push_back(S.rel_delta[v].c); d.push_back(S.rel_delta[v].m); d.push_back(S.rel_delta[v].g);
+            }
             S.rel_delta[v] = R3{};
             S.rel_flag[v] = 0;
         }
         S.rel_touched.clear();
+        const int n = (int)nodes.size();
+        if (!n) { flush_tables(S); return; }
         int32_t* dn = S.b_rel_nodes.alloc<int32_t>(n);
         int64_t* dd = S.b_rel_d.alloc<int64_t>(3 * (size_t)n);
         HIPCHK(hipMemcpyAsync(dn, nodes.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, S.stream));

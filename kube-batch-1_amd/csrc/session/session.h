@@ -745,6 +745,7 @@ struct Session {
     kbhip_allgather_fn xgfn = nullptr;         // host all-gather (batched pops of a shard session)
     void* xgctx = nullptr;
     DevBuf b_shard_send, b_shard_recv;         // this shard's ShardMsg / all of them (rank order)
+    DevBuf b_gather;                           // gather_host's staging (RCCL)
     ShardMsg* d_shard_send = nullptr;
     ShardMsg* d_shard_recv = nullptr;
     Mailbox* mbox_own = nullptr;               // peer mailboxes (kbhip_shard_connect_mailbox): this rank's,
@@ -1116,6 +1117,7 @@ void ctrl_setup(Session& S, int m, const int* cls, int ready, int min_avail, int
                        uint32_t epoch);
 void ev_harvest_all(Session& S);
 void exchange(Session& S, void* dev, int op, int n = 1);
+void gather_host(Session& S, const void* send, void* recv, size_t bytes);
 void fit_allreduce(Session& S, int32_t* fit4);
 void flush_tables(Session& S);
 BatchLaunch launch_batched(Session& S, int cls, int m, int gang_mode, int min_avail, int ready_count);

@@ -80,7 +80,7 @@ def _shard_case(oracle_mod, tmp_path, c, world, actions="allocate", batched=1, e
     for r in range(world):
         lo, hi = kbhip.shard_range(n_nodes, r, world)
         assert res[r]["info"] == [r, world, lo, hi]
-        got = [(a, b, 4 if k == 1 else 8) for a, b, k in res[r]["log"]]
+        got = [(a, b, {1: 4, 2: 8, 3: 128}[k]) for a, b, k in res[r]["log"]]  # (3: evicted, Releasing)
         assert got == exp, f"rank {r}"
         if exp_close is not None:
             assert res[r]["close"] == exp_close, f"rank {r}"
@@ -125,6 +125,39 @@ def test_sharded_batched_random_gpu(engine, oracle_mod, kbgen_mod, tmp_path, see
                                                                            "nodeorder"]])
     res = _shard_case(oracle_mod, tmp_path, c, 2 + seed % 3, exchange=exchange)
     assert all(r["batched_pops"] > 0 for r in res)
+
+
+EVICT_ACTIONS = ["reclaim", "preempt", "reclaim, allocate, backfill, preempt", "allocate, preempt"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_sharded_evict_gpu(engine, oracle_mod, kbgen_mod, tmp_path, seed):
+    """Reclaim and preempt on node-array shards (reclaim.go:41-196,
+    preempt.go:43-353): each rank ranks its own nodes, the sorted lists are
+    all-gathered and merged, the replicated host model walks them; every
+    rank's records equal the faithful restatement's.  Odd seeds add pod
+    (anti-)affinity and inter-pod priority terms (replicated count tables,
+    the inter-pod min / max reduced over the shards)."""
+    feats = ("selector", "taints", "init", "bestEffort") + (("podaffinity",) if seed % 2 else ())
+    c = kbgen_mod.gen_preempt(3100 + seed, n_nodes=6 + seed * 2, n_queues=1 + seed % 3, n_run_jobs=6 + seed % 5,
+                              n_pend_jobs=3 + seed % 3, max_tasks=2 + seed % 4, features=feats)
+    _shard_case(oracle_mod, tmp_path, c, 2 + seed % 2, actions=EVICT_ACTIONS[seed % len(EVICT_ACTIONS)])
+
+
+@pytest.mark.gpu
+def test_sharded_c5_scaled_gpu(engine, oracle_mod, kbgen_mod, tmp_path):
+    """C5's what-if action sequence on 2 shards at a size the faithful
+    restatement finishes in seconds."""
+    p = str(tmp_path / "c5s.kbs")
+    kbgen_mod.gen_c5(p, seed=kbgen_mod.BASE_SEED + 5, n_nodes=90, n_pending=80, best_effort=8)
+    acts = "reclaim, allocate, backfill, preempt"
+    exp = oracle_mod.ref_allocate(p, actions=acts).as_list()
+    assert any(k == 128 for _, _, k in exp)
+    res = _run_ranks("shard_worker.py", 2, tmp_path, lambda r, init, out: [p, str(r), "2", init, out, acts, "1"],
+                     timeout=240)
+    for r in range(2):
+        assert [(a, b, {1: 4, 2: 8, 3: 128}[k]) for a, b, k in res[r]["log"]] == exp, f"rank {r}"
 
 
 @pytest.mark.gpu
