@@ -314,12 +314,13 @@ KBHIP_HD int64_t ipa_count(const TaskClass& c, const DevTables& t, const NodeCol
 // inter-pod score normalised by the prepass's [lo, hi] (interpod_affinity.go:228-237).
 KBHIP_HD uint64_t eval_node_aff(const Conf& cf, const TaskClass& c, const DevTables& t,
                                                   const NodeCols& nc, int n, int64_t lo, int64_t hi, int F,
-                                                  int32_t* score_out, bool* passed, uint32_t* fit = nullptr) {
+                                                  int32_t* score_out, bool* passed, uint32_t* fit = nullptr,
+                                                  const int64_t* ipa_pre = nullptr) {
     bool st = static_pred(cf, c, t, nc, n);
     if (st && c.aff && cf.pred_on) st = aff_pred(c, t, nc, n);
     int32_t ipa = 0;
-    if (st && c.ipa_n && hi - lo > 0)
-        ipa = (int32_t)(10.0 * ((double)(ipa_count(c, t, nc, n, F) - lo) / (double)(hi - lo)));
+    if (st && c.ipa_n && hi - lo > 0)  // ipa_pre: the raw counts k_ipa_minmax just computed on this state
+        ipa = (int32_t)(10.0 * ((double)((ipa_pre ? ipa_pre[n] : ipa_count(c, t, nc, n, F)) - lo) / (double)(hi - lo)));
     const int32_t na = (st && cf.score_mult) ? na_weight(c, t, nc, n) : 0;
     const Row r = load_row(nc, n);
     uint64_t pw[4] = {0, 0, 0, 0};

@@ -32,14 +32,17 @@ hipError_t launch_ctrl_init(PopCtrl* ctrl, const CtrlInit& ci, hipStream_t st);
 // sessions reduce ctrl->slot[task_i] across shards and then launch_commit_task.
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
                                uint64_t* walk, hipStream_t st, bool commit_here = true, uint64_t* dbg = nullptr,
-                               bool defer_visits = false);
+                               bool defer_visits = false, const int64_t* ipa_pre = nullptr);
 // defer_visits (one GPU): the GetAccessibleResource mutation of the walk runs as a
 // second, grid-wide kernel (k_visit_mutate) instead of in the committing block.
 hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const uint64_t* walk,
                               hipStream_t st);
 // Inter-pod affinity priority prepass: min / max of the raw count over all
-// nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi.
-hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st);
+// nodes for task task_i (interpod_affinity.go:214-226) -> ctrl->ipa_lo/hi;
+// counts (optional, npad entries): each node's raw count, which the sweep that
+// follows on the same state then reads (launch_sweep_argmax's ipa_pre).
+hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st,
+                             int64_t* counts = nullptr);
 
 // Reclaim / preempt (kbhip_evict.hip): per-node order keys of the task of
 // ctrl->cls[0] (by_score 1: predicates + score, preempt; 0: predicates only,

@@ -38,7 +38,8 @@ namespace kbhip {
 
 
 #if KBHIP_PART <= 1  // everything but the batched-pop launchers of parts 2 / 3
-__global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t, PopCtrl* ctrl, int task_i) {
+__global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t, PopCtrl* ctrl, int task_i,
+                                                       int64_t* counts) {
     __shared__ int64_t rlo[kBlock / 64], rhi[kBlock / 64];
     if (ctrl->stop >= 0) return;
     const int cls = __builtin_amdgcn_readfirstlane(ctrl->cls[task_i]);
@@ -47,6 +48,7 @@ __global__ __launch_bounds__(kBlock) void k_ipa_minmax(NodeCols nc, DevTables t,
     int64_t lo = 0, hi = 0;  // maxCount / minCount start at 0 (interpod_affinity.go:214-226)
     for (int n = blockIdx.x * kBlock + threadIdx.x; n < nc.n; n += gridDim.x * kBlock) {
         const int64_t v = ipa_count(c, t, nc, n, F);
+        if (counts) counts[n] = v;  // (the sweep that follows reads them instead of counting again)
         lo = v < lo ? v : lo;
         hi = v > hi ? v : hi;
     }
@@ -131,7 +133,9 @@ __device__ void task_granule(PopCtrl* ctrl, int task_i, int kind, int node) {
 __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, const TaskClass& c,
                             bool first_fit, bool track, const uint64_t* walk, bool defer_visits = false) {
     __shared__ uint64_t win;
+    __shared__ int s_aff_g, s_aff_kind;  // the pod-affinity count tables' commit (global node, kind; -1: none)
     if (threadIdx.x == 0) {
+        s_aff_g = -1;
         const uint64_t k = __hip_atomic_load(&ctrl->slot[task_i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         win = k;
         const int g = k ? key_idx(k) : -1;            // global node index
@@ -142,7 +146,8 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
             ctrl->res_kind[task_i] = k ? 1 : 0;
             if (k) {
                 if (own) commit_node(c, t, nc, n, 1);
-                if (c.aff) commit_aff(c, t, nc, g, 1);
+                s_aff_g = g;
+                s_aff_kind = 1;
                 if (ctrl->fallback < 0 || g < ctrl->fallback) ctrl->fallback = g;
                 if (c.backfill) ctrl->any_bf = 1;
             }
@@ -165,7 +170,8 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
                 }
                 commit_node(c, t, nc, n, kind);
             }
-            if (c.aff) commit_aff(c, t, nc, g, kind);
+            s_aff_g = g;
+            s_aff_kind = kind;
             if (ctrl->fallback < 0 || g < ctrl->fallback) ctrl->fallback = g;
             if (c.backfill) ctrl->any_bf = 1;
             after_assign(ctrl, task_i, kind);
@@ -173,6 +179,17 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
         }
     }
     __syncthreads();
+    // commit_aff with one update per lane (was one lane looping over the class's updates, each a
+    // dependent chain of loads and a read-modify-write); atomic: two updates may share an entry
+    if (c.aff && s_aff_g >= 0 && (int)threadIdx.x < c.upd_n) {
+        const int32_t* it = t.aff_items + c.upd_off + 3 * threadIdx.x;
+        const bool to_cnt = it[0] == 0;
+        const int d = to_cnt ? dom_g(nc, it[1], s_aff_g) : 0;
+        const bool apply = (it[0] == 2 || s_aff_kind == 1) && d >= 0;
+        int32_t* tab = to_cnt ? t.aff_cnt : t.aff_scalar;
+        __hip_atomic_fetch_add(tab + it[2] + (d >= 0 ? d : 0), apply ? 1 : 0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (defer_visits) {  // k_visit_mutate does the loop below over the whole grid
         if (threadIdx.x == 0) ctrl->pad = track ? 1 : 0;
         return;
@@ -197,7 +214,7 @@ __device__ void commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* ctr
 // gridDim.x, or one session's blocks of a multi-session grid)
 __device__ __forceinline__ void sweep_body(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl,
                                            int task_i, uint64_t* walk, int commit_here, uint64_t* dbg, int bx,
-                                           int nbx) {
+                                           int nbx, const int64_t* ipa_pre = nullptr) {
     __shared__ uint64_t red[kBlock / 64];
     __shared__ int last;
     __shared__ int32_t s_fit[4];
@@ -216,7 +233,7 @@ __device__ __forceinline__ void sweep_body(const Conf& cf, const NodeCols& nc, c
         bool passed = false;
         uint32_t fb = 0;
         const uint64_t k = first_fit ? eval_first_fit(cf, c, t, nc, n)
-                                     : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed, &fb);
+                                     : eval_node_aff(cf, c, t, nc, n, ilo, ihi, F, &s, &passed, &fb, ipa_pre);
         for (int b = 0; b < 4; ++b) fc[b] += (fb >> b) & 1;
         if (track) walk[n] = passed ? pack_key(s, n + nc.base, 0) : 0;
         if (dbg) {  // kbhip_set_option("debug_keys")
@@ -254,8 +271,9 @@ __device__ __forceinline__ void sweep_body(const Conf& cf, const NodeCols& nc, c
     commit_task(nc, t, ctrl, task_i, c, first_fit, track, walk, (commit_here & 2) != 0);
 }
 __global__ __launch_bounds__(kBlock) void k_sweep_argmax(Conf cf, NodeCols nc, DevTables t, PopCtrl* ctrl,
-                                                         int task_i, uint64_t* walk, int commit_here, uint64_t* dbg) {
-    sweep_body(cf, nc, t, ctrl, task_i, walk, commit_here, dbg, blockIdx.x, gridDim.x);
+                                                         int task_i, uint64_t* walk, int commit_here, uint64_t* dbg,
+                                                         const int64_t* ipa_pre) {
+    sweep_body(cf, nc, t, ctrl, task_i, walk, commit_here, dbg, blockIdx.x, gridDim.x, ipa_pre);
 }
 
 // The GetAccessibleResource mutation of task task_i's walk (node_info.go:209-211,
@@ -1091,12 +1109,14 @@ __global__ __launch_bounds__(kPopThreads) void k_pop_batch_ov(Conf cf, NodeCols 
 // launchers (host)
 // ---------------------------------------------------------------------------
 hipError_t launch_sweep_argmax(const Conf& cf, const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i,
-                               uint64_t* walk, hipStream_t st, bool commit_here, uint64_t* dbg, bool defer_visits) {
+                               uint64_t* walk, hipStream_t st, bool commit_here, uint64_t* dbg, bool defer_visits,
+                               const int64_t* ipa_pre) {
     int grid = (nc.n + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
     const int mode = commit_here ? (defer_visits ? 3 : 1) : 0;
-    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk, mode, dbg);
+    hipLaunchKernelGGL(k_sweep_argmax, dim3(grid), dim3(kBlock), 0, st, cf, nc, t, ctrl, task_i, walk, mode, dbg,
+                       ipa_pre);
     if (commit_here && defer_visits)
         hipLaunchKernelGGL(k_visit_mutate, dim3(grid), dim3(kBlock), 0, st, nc, (const PopCtrl*)ctrl, task_i,
                            (const uint64_t*)walk);
@@ -1280,11 +1300,12 @@ hipError_t launch_commit_task(const NodeCols& nc, const DevTables& t, PopCtrl* c
     return hipGetLastError();
 }
 
-hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st) {
+hipError_t launch_ipa_minmax(const NodeCols& nc, const DevTables& t, PopCtrl* ctrl, int task_i, hipStream_t st,
+                             int64_t* counts) {
     int grid = (nc.n + kBlock - 1) / kBlock;
     if (grid > 2048) grid = 2048;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(k_ipa_minmax, dim3(grid), dim3(kBlock), 0, st, nc, t, ctrl, task_i);
+    hipLaunchKernelGGL(k_ipa_minmax, dim3(grid), dim3(kBlock), 0, st, nc, t, ctrl, task_i, counts);
     return hipGetLastError();
 }
 

@@ -94,13 +94,16 @@ static void shard_gather(Session& S) {
 // defer_visits: the walk's GetAccessibleResource mutation as a grid-wide second
 // kernel (worth it whenever some node may carry Backfilled resources).
 void sweep_task(Session& S, int i, int cls, bool defer_visits) {
+    int64_t* ipa = nullptr;
     if (S.classes[cls].ipa_n > 0) {
-        HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream));
+        if (!S.d_ipa) S.d_ipa = S.b_ipa.alloc<int64_t>((size_t)S.nc.npad);
+        ipa = S.d_ipa;
+        HIPCHK(launch_ipa_minmax(S.nc, S.tab, S.d_ctrl, i, S.stream, ipa));
         exchange(S, &S.d_ctrl->ipa_lo[i], KBHIP_RED_MIN_I64);
         exchange(S, &S.d_ctrl->ipa_hi[i], KBHIP_RED_MAX_I64);
     }
     HIPCHK(launch_sweep_argmax(S.conf, S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream, S.world == 1, S.d_dbg,
-                               defer_visits && S.world == 1));
+                               defer_visits && S.world == 1, ipa));
     if (S.world > 1) {
         exchange(S, &S.d_ctrl->slot[i], KBHIP_RED_MAX_U64);
         HIPCHK(launch_commit_task(S.nc, S.tab, S.d_ctrl, i, S.d_walk, S.stream));

@@ -746,6 +746,8 @@ struct Session {
     void* xgctx = nullptr;
     DevBuf b_shard_send, b_shard_recv;         // this shard's ShardMsg / all of them (rank order)
     DevBuf b_gather;                           // gather_host's staging (RCCL)
+    DevBuf b_ipa;                              // the per-task path's raw inter-pod counts (k_ipa_minmax -> sweep)
+    int64_t* d_ipa = nullptr;
     ShardMsg* d_shard_send = nullptr;
     ShardMsg* d_shard_recv = nullptr;
     Mailbox* mbox_own = nullptr;               // peer mailboxes (kbhip_shard_connect_mailbox): this rank's,
