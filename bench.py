@@ -86,6 +86,8 @@ def parse():
                     help="1: batched pops go to the persistent pop engine (one resident kernel, DESIGN.md §4.10); "
                          "0 = one launched kernel per pop")
     ap.add_argument("--engine-workers", type=int, default=0, help="engine worker blocks (0: as many as stay resident)")
+    ap.add_argument("--engine-groups", type=int, default=-1,
+                    help="engine merger blocks (-1: the library's default, 8)")
     ap.add_argument("--engine-lists", type=int, default=0, choices=(0, 1),
                     help="1 = the engine's list mode when every class fits (class owners, DESIGN.md §4.11), 0 = sweep mode")
     ap.add_argument("--mode", choices=("replicas", "shard"), default="shard",
@@ -229,7 +231,7 @@ def open_sharded(buf, device, rank, world, dist):
 
 
 def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, keep_log=False, engine=1,
-                engine_workers=0, engine_lists=0):
+                engine_workers=0, engine_lists=0, engine_groups=-1):
     t0 = time.perf_counter()
     s = open_sharded(buf, device, *shard) if shard else kbhip.Session(buf, device=device)
     s.set_option("time_every", time_every)
@@ -237,6 +239,8 @@ def run_session(buf, device, time_every, shard=None, overlap=1, speculate=4, kee
     s.set_option("speculate", speculate)
     s.set_option("engine", engine)
     s.set_option("engine_workers", engine_workers)
+    if engine_groups >= 0:
+        s.set_option("engine_groups", engine_groups)
     s.set_option("engine_lists", engine_lists)
     t1 = time.perf_counter()
     pod, node, kind = s.allocate(cap=1 << 21)
@@ -379,7 +383,8 @@ def main():
     shard = (rank, world, dist) if (args.mode == "shard" and world > 1) else None
     for _ in range(args.warmup):
         run_session(buf, device, 0, shard, args.overlap, args.speculate, engine=args.engine,
-                    engine_workers=args.engine_workers, engine_lists=args.engine_lists)
+                    engine_workers=args.engine_workers, engine_lists=args.engine_lists,
+                    engine_groups=args.engine_groups)
     barrier(dist, local)
     t0 = time.perf_counter()
     lat, placed, sweeps_ms, sweeps_n, st_last = [], 0, 0.0, 0, None
@@ -387,7 +392,8 @@ def main():
     for i in range(args.steps):
         dt, n, st = run_session(buf, device, args.time_every, shard, args.overlap,
                                 args.speculate, keep_log=(i == 0 and rank == 0), engine=args.engine,
-                                engine_workers=args.engine_workers, engine_lists=args.engine_lists)
+                                engine_workers=args.engine_workers, engine_lists=args.engine_lists,
+                                engine_groups=args.engine_groups)
         lat.append(dt)
         placed += n
         sweeps_ms += st["device_s"] * 1e3
