@@ -367,7 +367,19 @@ int kbhip_get_stats(kb_session* s, kbhip_stats* out);
  * pop's candidates out and re-evaluating them once its write-back is done;
  * 0 (default) = sweep, exchange and placement one after another;
  * "debug_keys" = 1 records every per-task sweep's per-node keys (tests,
- * read back with kbhip_debug_table "dbg_keys" / "dbg_pods"). */
+ * read back with kbhip_debug_table "dbg_keys" / "dbg_pods").
+ * Measurement and rehearsal options (not part of a scheduler's use):
+ * "sweep_variant" = 0..6 the kernel shape of kbhip_sweep_scores (process-wide;
+ * 0 default, 4..6 grid-stride forms);
+ * "time_sweeps_cold" = 0 warm, 1 write-evict, 2 read-evict the caches before
+ * each launch kbhip_time_sweeps times;
+ * "group_linger_us" = t (process-wide, tests) keeps a what-if batch open for
+ * up to t µs for more sessions' requests;
+ * "cu_split" = part * 256 + parts runs this session's streams on CUs
+ * [part * C / parts, (part + 1) * C / parts) of the device's C (one-GPU
+ * rehearsals of node-array shards).  "time_sweeps_cold" and
+ * "cu_split" are not kept across the re-open of
+ * kbhip_session_carry_snapshot's slow path. */
 int kbhip_set_option(kb_session* s, const char* key, int64_t value);
 
 /* The gang plugin's OnSessionClose after kbhip_allocate (plugins/gang/gang.go:
